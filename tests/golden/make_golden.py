@@ -1,0 +1,387 @@
+"""Generate golden vectors by running the REFERENCE (qingxu-thu/INSR-PDE) on the CPU.
+
+Run in the build container only (needs /root/reference, which does not exist on
+the GPU box):   python tests/golden/make_golden.py
+
+What it does, and nothing else:
+* imports the reference's own `base` package and the advection / fluid /
+  elasticity model classes from /root/reference.  Four third-party modules the
+  reference imports at module top but never calls on these paths are absent
+  from the image (pytorch3d.ops -- vortex kNN, base/networks.py:4; tensorboardX
+  -- logging, base/baseModel.py:5; meshio -- mesh files, elasticity/model.py:13;
+  open3d -- .ply output, elasticity/visualize.py:5); they get empty placeholder
+  modules so the import succeeds.  No reference function is replaced.
+* forces the CPU (the reference hard-codes cuda:0, base/baseModel.py:25) and
+  drops ReduceLROnPlateau's removed `verbose` kwarg (torch 2.10).
+* builds reference MLPs from fixed torch seeds, evaluates the reference diff
+  ops on fixed samples, and runs the reference phase bodies (pulled out of the
+  `_training_loop` closure) + the reference `_update_network` (backward + Adam)
+  on fixed samples.
+* writes the inputs and outputs to tests/golden/*.npz (fixtures = data only).
+"""
+import os
+import sys
+import types
+
+import numpy as np
+import torch
+
+REF = "/root/reference"
+OUT = os.path.dirname(os.path.abspath(__file__))
+
+
+def _placeholder_modules():
+    class _Unused:
+        def __init__(self, *a, **k):
+            pass
+
+        def __getattr__(self, name):
+            return lambda *a, **k: None
+
+    p3d = types.ModuleType("pytorch3d")
+    p3d_ops = types.ModuleType("pytorch3d.ops")
+    p3d_ops.knn_points = p3d_ops.knn_gather = None
+    p3d.ops = p3d_ops
+    tbx = types.ModuleType("tensorboardX")
+    tbx.SummaryWriter = _Unused
+    sys.modules.update({"pytorch3d": p3d, "pytorch3d.ops": p3d_ops, "tensorboardX": tbx,
+                        "meshio": types.ModuleType("meshio"), "open3d": types.ModuleType("open3d")})
+
+
+def load_reference():
+    _placeholder_modules()
+    import matplotlib
+    matplotlib.use("Agg")
+    sys.path.insert(0, REF)
+    import base  # noqa: E402  (reference package)
+    import base.baseModel as bm
+
+    orig_init = bm.BaseModel.__init__
+
+    def cpu_init(self, cfg):
+        orig_init(self, cfg)
+        self.device = torch.device("cpu")
+
+    bm.BaseModel.__init__ = cpu_init
+    orig_plateau = torch.optim.lr_scheduler.ReduceLROnPlateau
+
+    class Plateau(orig_plateau):
+        def __init__(self, *a, verbose=None, **k):
+            super().__init__(*a, **k)
+
+    torch.optim.lr_scheduler.ReduceLROnPlateau = Plateau
+    torch.Tensor.cuda = lambda self, *a, **k: self
+    torch.nn.Module.cuda = lambda self, *a, **k: self
+    return base
+
+
+def raw_phase(cls, name):
+    """Unwrap the BaseModel._training_loop closure to the phase body."""
+    loop = getattr(cls, name)
+    for cell in loop.__closure__:
+        if callable(cell.cell_contents) and getattr(cell.cell_contents, "__name__", "") == name:
+            return cell.cell_contents
+    raise KeyError(name)
+
+
+class Cfg(types.SimpleNamespace):
+    pass
+
+
+def base_cfg(**kw):
+    c = Cfg(exp_dir="/tmp/golden_exp", log_dir="/tmp/golden_exp/log", model_dir="/tmp/golden_exp/model",
+            dt=0.05, max_n_iters=3, sample_resolution=32, vis_resolution=8, lr=1e-4, network="siren",
+            num_hidden_layers=3, hidden_features=64, nonlinearity="sine", vis_frequency=10**9,
+            early_stop=False, init_cond=None)
+    for k, v in kw.items():
+        setattr(c, k, v)
+    return c
+
+
+def flat(net):
+    return torch.cat([p.detach().reshape(-1) for p in net.parameters()]).numpy().copy()
+
+
+def flat_grad(net):
+    return torch.cat([(p.grad if p.grad is not None else torch.zeros_like(p)).reshape(-1)
+                      for p in net.parameters()]).detach().numpy().copy()
+
+
+def set_flat(net, vec):
+    off = 0
+    with torch.no_grad():
+        for p in net.parameters():
+            n = p.numel()
+            p.copy_(torch.from_numpy(vec[off:off + n]).view_as(p))
+            off += n
+
+
+def seeded_net(base, d_in, d_out, L, W, seed):
+    torch.manual_seed(seed)
+    return base.MLP(d_in, d_out, L, W, nonlinearity="sine")
+
+
+# ---------------------------------------------------------------------------
+def gen_networks_and_ops(base):
+    """Init bit-pattern + every diff op + param-grads of a fixed functional."""
+    cases = {"advect": (1, 1, 3, 64), "fluid_vel": (2, 2, 4, 128), "fluid_pres": (2, 1, 4, 128),
+             "el2d": (2, 2, 5, 128), "el3d": (3, 3, 5, 256)}
+    out = {}
+    for i, (name, (din, dout, L, W)) in enumerate(cases.items()):
+        seed = 100 + i
+        net = seeded_net(base, din, dout, L, W, seed)
+        out[f"{name}/seed"] = np.array(seed)
+        out[f"{name}/shape"] = np.array([din, dout, L, W])
+        stride = 61 if W == 256 else 1  # el3d: strided subsample keeps the fixture small
+        out[f"{name}/param_stride"] = np.array(stride)
+        out[f"{name}/params"] = flat(net)[::stride]
+        g = torch.Generator().manual_seed(1000 + i)
+        n_pts = 64 if W == 256 else 256
+        x = (torch.rand(n_pts, din, generator=g) * 2 - 1).requires_grad_(True)
+        out[f"{name}/x"] = x.detach().numpy().copy()
+        y = net(x)
+        out[f"{name}/y"] = y.detach().numpy().copy()
+        ops = {}
+        if W < 256:
+            ops["gradient"] = base.gradient(y, x)
+            if dout == din:
+                ops["divergence"] = base.divergence(y, x)
+            ops["laplace"] = base.laplace(y, x)
+        jac, st = base.jacobian(y, x)
+        ops["jacobian"] = jac
+        out[f"{name}/jacobian_status"] = np.array(st)
+        if W <= 128 and din <= 2:
+            # reference hessian wants (meta_batch, obs, ch) / (meta_batch, obs, dim)
+            x3 = x.detach()[None].clone().requires_grad_(True)
+            hes, st = base.hessian(net(x3), x3)
+            ops["hessian"] = hes
+            out[f"{name}/hessian_status"] = np.array(st)
+        for op, val in ops.items():
+            out[f"{name}/{op}"] = val.detach().numpy().copy()
+            r = torch.randn(val.shape, generator=g)
+            out[f"{name}/{op}_R"] = r.numpy().copy()
+            net.zero_grad(set_to_none=True)
+            (val * r).sum().backward(retain_graph=True)
+            out[f"{name}/{op}_pgrad"] = flat_grad(net)[::stride]
+        # trainable value functional
+        r = torch.randn(y.shape, generator=g)
+        out[f"{name}/value_R"] = r.numpy().copy()
+        net.zero_grad(set_to_none=True)
+        (net(x) * r).sum().backward()
+        out[f"{name}/value_pgrad"] = flat_grad(net)[::stride]
+    return out
+
+
+# ---------------------------------------------------------------------------
+def run_phase(model, cls, phase, n_iters, samples_fn, patches):
+    """Reset the optimiser, then n_iters x (phase body + _update_network)."""
+    body = raw_phase(cls, phase)
+    model._reset_optimizer()
+    rec = []
+    for it in range(n_iters):
+        for mod, attr, fn in patches(it):
+            setattr(mod, attr, fn)
+        model._sample_in_training = samples_fn(it)
+        loss_dict = body(model)
+        model._update_network(loss_dict)
+        rec.append({k: float(v.detach()) for k, v in loss_dict.items()})
+    return rec
+
+
+def gen_fluid(base):
+    import fluid.model as fm
+    from fluid.model import Fluid2DModel
+    cfg = base_cfg(num_hidden_layers=4, hidden_features=128, sample_resolution=32, dt=0.05,
+                   init_cond="taylorgreen")
+    torch.manual_seed(7)
+    model = Fluid2DModel(cfg)
+    out = {}
+    # distinct, seeded weights for current / prev / pressure
+    for name, net, seed in (("vel", model.velocity_field, 11), ("vel_prev", model.velocity_field_prev, 12),
+                            ("pres", model.pressure_field, 13)):
+        set_flat(net, flat(seeded_net(base, 2, net.net[-1].out_features, 4, 128, seed)))
+        out[f"fluid/{name}/params0"] = flat(net)
+    N = cfg.sample_resolution ** 2
+    nb = N // 100
+    g = torch.Generator().manual_seed(2024)
+    iters = 2
+    xs = [(torch.rand(N, 2, generator=g) * 2 - 1) for _ in range(iters)]
+    bxs = [base.sample_boundary2D_separate(nb, "horizontal") for _ in range(iters)]
+    bys = [base.sample_boundary2D_separate(nb, "vertical") for _ in range(iters)]
+    for it in range(iters):
+        out[f"fluid/x{it}"] = xs[it].numpy()
+        out[f"fluid/bcx{it}"] = bxs[it].numpy()
+        out[f"fluid/bcy{it}"] = bys[it].numpy()
+
+    def samples_fn(it):
+        return lambda: xs[it].clone().requires_grad_(True)
+
+    def patches(it):
+        seq = iter([bxs[it], bys[it]])
+        return [(fm, "sample_boundary2D_separate", lambda n, side, device=None, **k: next(seq).clone())]
+
+    state0 = {n: flat(getattr(model, a)) for n, a in
+              (("vel", "velocity_field"), ("vel_prev", "velocity_field_prev"), ("pres", "pressure_field"))}
+    for phase in ("_advect_velocity", "_solve_pressure", "_projection"):
+        for n, a in (("vel", "velocity_field"), ("vel_prev", "velocity_field_prev"), ("pres", "pressure_field")):
+            set_flat(getattr(model, a), state0[n])
+        # single iteration: loss + grads
+        body = raw_phase(Fluid2DModel, phase)
+        model._reset_optimizer()
+        for mod, attr, fn in patches(0):
+            setattr(mod, attr, fn)
+        model._sample_in_training = samples_fn(0)
+        ld = body(model)
+        for k, v in ld.items():
+            out[f"fluid/{phase}/loss_{k}"] = np.array(float(v.detach()))
+        loss = sum(ld.values())
+        model.optimizer.zero_grad()
+        loss.backward()
+        out[f"fluid/{phase}/grad_vel"] = flat_grad(model.velocity_field)
+        out[f"fluid/{phase}/grad_pres"] = flat_grad(model.pressure_field)
+        # full iterations through the reference update
+        for n, a in (("vel", "velocity_field"), ("vel_prev", "velocity_field_prev"), ("pres", "pressure_field")):
+            set_flat(getattr(model, a), state0[n])
+        rec = run_phase(model, Fluid2DModel, phase, iters, samples_fn, patches)
+        out[f"fluid/{phase}/loss_trace"] = np.array([[r[k] for k in sorted(r)] for r in rec])
+        out[f"fluid/{phase}/vel_after"] = flat(model.velocity_field)
+        out[f"fluid/{phase}/pres_after"] = flat(model.pressure_field)
+    return out
+
+
+def gen_advect(base):
+    import advection.model as am
+    from advection.model import Advection1DModel
+    cfg = base_cfg(num_hidden_layers=3, hidden_features=64, sample_resolution=512, dt=0.05, vel=0.25,
+                   length=4.0, init_cond="example1")
+    model = Advection1DModel(cfg)
+    out = {}
+    for name, net, seed in (("field", model.field, 21), ("field_prev", model.field_prev, 22)):
+        set_flat(net, flat(seeded_net(base, 1, 1, 3, 64, seed)))
+        out[f"advect/{name}/params0"] = flat(net)
+    g = torch.Generator().manual_seed(77)
+    iters = 2
+    xs = [(torch.rand(cfg.sample_resolution, 1, generator=g) * 2 - 1) * cfg.length / 2 for _ in range(iters)]
+    nb = max(cfg.sample_resolution // 100, 10)
+    bs = [base.sample_boundary(nb, 1) * cfg.length / 2 for _ in range(iters)]
+    for it in range(iters):
+        out[f"advect/x{it}"] = xs[it].numpy()
+        out[f"advect/bc{it}"] = bs[it].numpy()
+
+    def samples_fn(it):
+        return lambda: xs[it].clone().requires_grad_(True)
+
+    def patches(it):
+        # reference multiplies the band by length/2 itself (advection/model.py:86)
+        return [(am, "sample_boundary", lambda n, sdim, device=None, **k: bs[it] / (cfg.length / 2))]
+
+    s0 = {"field": flat(model.field), "field_prev": flat(model.field_prev)}
+    body = raw_phase(Advection1DModel, "_advect")
+    model._reset_optimizer()
+    for mod, attr, fn in patches(0):
+        setattr(mod, attr, fn)
+    model._sample_in_training = samples_fn(0)
+    ld = body(model)
+    for k, v in ld.items():
+        out[f"advect/_advect/loss_{k}"] = np.array(float(v.detach()))
+    model.optimizer.zero_grad()
+    sum(ld.values()).backward()
+    out["advect/_advect/grad_field"] = flat_grad(model.field)
+    set_flat(model.field, s0["field"])
+    rec = run_phase(model, Advection1DModel, "_advect", iters, samples_fn, patches)
+    out["advect/_advect/loss_trace"] = np.array([[r[k] for k in sorted(r)] for r in rec])
+    out["advect/_advect/field_after"] = flat(model.field)
+    return out
+
+
+def gen_elasticity(base):
+    from elasticity.model import ElasticityModel
+    cfg = base_cfg(num_hidden_layers=5, hidden_features=128, sample_resolution=16, dt=0.1, lr=1e-4, dim=2,
+                   energy=["arap", "constraint", "constraint_right", "volume", "kinematics", "external",
+                           "collision"],
+                   sample_pattern=["random", "uniform"], ratio_constraint=1e4, ratio_volume=1e3, ratio_arap=1.0,
+                   ratio_collide=1e2, ratio_kinematics=1.0, use_mesh=False, mesh_path="",
+                   external_force_timesteps=5, external_force_x=0.0, external_force_y=-1.0,
+                   external_force_z=0.0, constraint_right_offset_x=2.0, constraint_right_offset_y=0.0,
+                   constraint_right_offset_z=0.0, plane_height=-0.9, collide_circle_x=0.0,
+                   collide_circle_y=-2.0, collide_circle_z=0.0, collide_circle_radius=1.0)
+    model = ElasticityModel(cfg)
+    model.timestep = 1
+    out = {}
+    for name, net, seed in (("f", model.deformation_field, 31), ("f_prev", model.deformation_field_prev, 32),
+                            ("f_pp", model.deformation_field_prev_prev, 33)):
+        set_flat(net, flat(seeded_net(base, 2, 2, 5, 128, seed)))
+        out[f"el2d/{name}/params0"] = flat(net)
+    g = torch.Generator().manual_seed(55)
+    R = cfg.sample_resolution
+    iters = 2
+    xs, fl, fr = [], [], []
+    for it in range(iters):
+        rnd = torch.rand(R * R, 2, generator=g) * 2 - 1
+        xs.append(torch.cat([rnd, base.sample_uniform(R, 2)], 0))
+        fl.append(torch.cat([torch.cat([-torch.ones(R, 1), torch.rand(R, 1, generator=g) * 2 - 1], 1),
+                             torch.cat([-torch.ones(R, 1), base.sample_uniform(R, 1)], 1)], 0))
+        fr.append(torch.cat([torch.cat([torch.ones(R, 1), torch.rand(R, 1, generator=g) * 2 - 1], 1),
+                             torch.cat([torch.ones(R, 1), base.sample_uniform(R, 1)], 1)], 0))
+        out[f"el2d/x{it}"] = xs[it].numpy()
+        out[f"el2d/fixed_l{it}"] = fl[it].numpy()
+        out[f"el2d/fixed_r{it}"] = fr[it].numpy()
+
+    def samples_fn(it):
+        return lambda res: xs[it].clone().requires_grad_(True)
+
+    def patches(it):
+        return [(model, "_sample_fixed_in_training",
+                 lambda res: (fl[it].clone().requires_grad_(True), fr[it].clone().requires_grad_(True)))]
+
+    s0 = flat(model.deformation_field)
+    body = raw_phase(ElasticityModel, "_solve_deformation")
+    model._reset_optimizer()
+    for mod, attr, fn in patches(0):
+        setattr(mod, attr, fn)
+    model._sample_in_training = samples_fn(0)
+    ld = body(model)
+    out["el2d/_solve_deformation/loss_main"] = np.array(float(ld["main"].detach()))
+    model.optimizer.zero_grad()
+    ld["main"].backward()
+    out["el2d/_solve_deformation/grad_f"] = flat_grad(model.deformation_field)
+    set_flat(model.deformation_field, s0)
+    rec = run_phase(model, ElasticityModel, "_solve_deformation", iters, samples_fn, patches)
+    out["el2d/_solve_deformation/loss_trace"] = np.array([[r[k] for k in sorted(r)] for r in rec])
+    out["el2d/_solve_deformation/f_after"] = flat(model.deformation_field)
+    out["el2d/cfg_energy"] = np.array(cfg.energy)
+    return out
+
+
+def gen_samplers(base):
+    torch.manual_seed(5)
+    out = {"sampling/uniform_8_2": base.sample_uniform(8, 2).numpy(),
+           "sampling/uniform_5_1": base.sample_uniform(5, 1).numpy(),
+           "sampling/uniform_4_3": base.sample_uniform(4, 3).numpy()}
+    torch.manual_seed(6)
+    out["sampling/random_seed6_100x2"] = base.sample_random(100, 2).numpy()
+    torch.manual_seed(8)
+    out["sampling/bnd2d_h_seed8_20"] = base.sample_boundary2D_separate(20, "horizontal").numpy()
+    torch.manual_seed(9)
+    out["sampling/bnd1d_seed9_20"] = base.sample_boundary(20, 1).numpy()
+    return out
+
+
+def main():
+    torch.set_num_threads(8)
+    base = load_reference()
+    data = {}
+    data.update(gen_samplers(base))
+    data.update(gen_networks_and_ops(base))
+    np.savez_compressed(os.path.join(OUT, "ref_ops.npz"), **data)
+    phases = {}
+    phases.update(gen_advect(base))
+    phases.update(gen_fluid(base))
+    phases.update(gen_elasticity(base))
+    np.savez_compressed(os.path.join(OUT, "ref_phases.npz"), **phases)
+    for f in ("ref_ops.npz", "ref_phases.npz"):
+        print(f, os.path.getsize(os.path.join(OUT, f)) / 1e6, "MB")
+
+
+if __name__ == "__main__":
+    main()
