@@ -1,0 +1,133 @@
+/*
+ * insr_siren.h -- C ABI of libinsr_hip.so, the MI355X (gfx950) hot path of the
+ * INSR-PDE per-timestep training loop.
+ *
+ * The reference (qingxu-thu/INSR-PDE) is pure Python over PyTorch; its "FFI" for
+ * this path is the torch dispatcher.  Each entry point below replaces the group
+ * of aten kernels the reference's Python launches for one operator:
+ *
+ *   insr_siren_jet_fwd   MLP.forward (base/networks.py:67-71) + the create_graph
+ *                        autograd passes of gradient / divergence / jacobian /
+ *                        laplace (base/diff_ops.py:33-82), as ONE forward Taylor
+ *                        jet (value, d tangents, Laplacian stream).
+ *   insr_siren_jet_bwd   loss.backward() through those graphs down to the
+ *                        parameters (base/baseModel.py:77) -- the 2nd/3rd-order
+ *                        reverse pass -- as per-block partial gradients.
+ *   insr_reduce_partials deterministic sum of the per-block partials into the
+ *                        network's flat .grad buffer (autograd's AccumulateGrad).
+ *   insr_adam_prepare /  torch.optim.Adam.step() + ReduceLROnPlateau.step()
+ *   insr_adam_step       (base/baseModel.py:55-62,79-81) over one flat buffer,
+ *                        with lr / step / plateau state kept on the device.
+ *
+ * Conventions
+ *   - Every pointer is a device pointer owned by the caller (torch tensors);
+ *     the library never allocates or frees.  Sizes come from the *_bytes /
+ *     *_count queries.
+ *   - Every call is asynchronous on the caller's hipStream_t (passed as void*);
+ *     no host synchronisation, so calls are hipGraph-capturable.
+ *   - Return 0 on success, a negative INSR_E* code for a bad argument, or a
+ *     positive hipError_t from the launch.  Nothing throws across the ABI.
+ *   - Parameters are ONE flat fp32 buffer in torch state_dict order:
+ *       net.0.weight (W x d_in), net.0.bias (W),
+ *       net.2.weight (W x W), net.2.bias (W), ... (L hidden layers),
+ *       net.{2L+2}.weight (d_out x W), net.{2L+2}.bias (d_out)
+ *     i.e. nn.Linear's (out, in) row-major weights, exactly as the reference
+ *     stores them (base/networks.py:50-60), so state_dicts load unchanged.
+ */
+#ifndef INSR_SIREN_H
+#define INSR_SIREN_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* jet modes: which derivative streams ride along with the value */
+#define INSR_MODE_VALUE 0 /* y                                  (1 stream)        */
+#define INSR_MODE_GRAD  1 /* y, dy/dx_i  (Jacobian rows)         (1 + d_in streams) */
+#define INSR_MODE_LAP   2 /* y, dy/dx_i, sum_i d2y/dx_i^2        (2 + d_in streams) */
+
+#define INSR_EINVAL   (-1) /* unsupported shape / mode / null pointer */
+#define INSR_EWIDTH   (-2) /* hidden width not in the compiled set      */
+
+/* Library version (major*10000 + minor*100 + patch). */
+int insr_version(void);
+
+/* Number of fp32 parameters of an SIREN(d_in -> W x (L+1) -> d_out). */
+long insr_siren_param_count(int d_in, int d_out, int num_hidden, int width);
+
+/* 1 if (d_in, d_out, width, mode) is served by a compiled kernel, else 0. */
+int insr_siren_supported(int d_in, int d_out, int num_hidden, int width, int mode);
+
+/* Bytes of the activation buffer the forward saves for the backward. */
+long insr_jet_act_bytes(long n_points, int d_in, int num_hidden, int width, int mode);
+
+/* Bytes of the per-block partial-gradient buffer the backward writes. */
+long insr_jet_partial_bytes(long n_points, int d_in, int d_out, int num_hidden, int width);
+
+/*
+ * Forward jet over n_points collocation points.
+ *   x    (n, d_in)                      sample coordinates
+ *   y    (n, d_out)                     network value
+ *   dy   (n, d_out, d_in)  [GRAD, LAP]  Jacobian d y_o / d x_i (else may be NULL)
+ *   lap  (n, d_out)        [LAP]        sum_i d2 y_o / dx_i^2   (else may be NULL)
+ *   act  insr_jet_act_bytes            saved pre-activation streams for
+ *                                       insr_siren_jet_bwd; NULL = inference only.
+ * Replaces: base/networks.py:67-71 and base/diff_ops.py:33-82.
+ */
+int insr_siren_jet_fwd(const float* x, long n_points, int d_in, int d_out, int num_hidden,
+                       int width, int mode, const float* params, float* y, float* dy, float* lap,
+                       float* act, void* stream);
+
+/*
+ * Backward of the jet to the parameters.  Adjoints (any may be NULL = zero):
+ *   gy (n, d_out), gdy (n, d_out, d_in), glap (n, d_out).
+ *   partial  insr_jet_partial_bytes scratch (one fp32 gradient per block).
+ *   grad     flat fp32 gradient (insr_siren_param_count); accumulate != 0 adds
+ *            into it (autograd accumulation), 0 overwrites.
+ * The gradient w.r.t. x is not produced (the reference never reads it).
+ * Replaces: the autograd backward of loss.backward() (base/baseModel.py:77).
+ */
+int insr_siren_jet_bwd(const float* x, long n_points, int d_in, int d_out, int num_hidden,
+                       int width, int mode, const float* params, const float* act,
+                       const float* gy, const float* gdy, const float* glap, float* partial,
+                       float* grad, int accumulate, void* stream);
+
+/* grad[i] = (accumulate ? grad[i] : 0) + sum_b partial[b * count + i], fixed order. */
+int insr_reduce_partials(const float* partial, int n_blocks, long count, float* grad,
+                         int accumulate, void* stream);
+
+/*
+ * Device-resident optimiser state (INSR_OPT_NFLOATS floats, caller-allocated):
+ *   [0] lr  [1] step t  [2] plateau best  [3] plateau num_bad
+ *   [4] step_size = lr / (1 - b1^t)        [5] sqrt(1 - b2^t)
+ *   [6] plateau factor  [7] plateau min_lr
+ * Keeping these on the device lets one training iteration be replayed from a
+ * hipGraph with no host round trip (the reference syncs twice per iteration,
+ * base/baseModel.py:81,116).
+ */
+#define INSR_OPT_LR 0
+#define INSR_OPT_STEP 1
+#define INSR_OPT_BEST 2
+#define INSR_OPT_BAD 3
+#define INSR_OPT_STEPSIZE 4
+#define INSR_OPT_BC2SQRT 5
+#define INSR_OPT_FACTOR 6
+#define INSR_OPT_MINLR 7
+#define INSR_OPT_NFLOATS 8
+
+/* t += 1; refresh step_size and sqrt(1-b2^t) (torch.optim.Adam bias correction). */
+int insr_adam_prepare(float* opt_state, float beta1, float beta2, void* stream);
+
+/* One ReduceLROnPlateau.step(*loss) (mode min, rel threshold 1e-4, cooldown 0,
+ * eps 1e-8), base/baseModel.py:61-62,80-81. */
+int insr_plateau_step(float* opt_state, const float* loss, int patience, void* stream);
+
+/* p -= step_size * m / (sqrt(v)/bc2sqrt + eps) after m,v moments (torch order). */
+int insr_adam_step(float* params, const float* grads, float* exp_avg, float* exp_avg_sq,
+                   long count, const float* opt_state, float beta1, float beta2, float eps,
+                   void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* INSR_SIREN_H */

@@ -1,0 +1,15 @@
+"""insr-pde_amd `base`: drop-in for the reference's base package (base/__init__.py:1-4).
+
+    from base import BaseModel, gradient, divergence, laplace, jacobian, \
+        sample_random, sample_uniform, sample_boundary, sample_boundary2D_separate, get_network
+
+The hot path runs on libinsr_hip.so (gfx950); see DESIGN.md.
+"""
+from .baseModel import BaseModel
+from .diff_ops import *  # noqa: F401,F403
+from .sampling import *  # noqa: F401,F403
+from .networks import *  # noqa: F401,F403
+from .networks import MLP, Sine, get_network  # noqa: F401
+from .optim import DevicePlateau, FusedAdam  # noqa: F401
+from ._jet import UnsupportedPattern  # noqa: F401
+from ._native import NativeUnavailable, NativeError  # noqa: F401

@@ -1,0 +1,205 @@
+"""Autograd bridge between the `base` API and the HIP jet kernels.
+
+`siren_value(mlp, x)` is MLP.forward.  Its output carries provenance
+(`_insr_src = (mlp, x)`), so that
+
+    gradient(y, x) / divergence(y, x) / jacobian(y, x) / laplace(y, x)
+
+on that output run ONE forward Taylor jet (value + d tangents [+ Laplacian
+stream]) in HIP instead of the reference's create_graph autograd passes
+(base/diff_ops.py:33-82), and `loss.backward()` runs the matching HIP reverse
+jet straight into the network's flat gradient buffer.
+
+Recognised shapes of `y` (everything the reference models use):
+  * y = mlp(x)                          (advection, fluid)
+  * y = mlp(x) + x   /  x + mlp(x)      (elasticity/model.py:137, q = f(x) + x)
+  * y = gradient(mlp(x), x)  inside divergence  (-> Laplacian stream)
+Anything else raises UnsupportedPattern (there is no silent fallback).
+"""
+import weakref
+
+import torch
+from torch.autograd.function import once_differentiable
+
+from . import _native as nat
+
+MODE_NAMES = {nat.MODE_VALUE: "value", nat.MODE_GRAD: "grad", nat.MODE_LAP: "lap"}
+
+
+class UnsupportedPattern(RuntimeError):
+    pass
+
+
+def _flatten_x(x, din):
+    if x.shape[-1] != din:
+        raise ValueError(f"expected last dim {din}, got {tuple(x.shape)}")
+    lead = x.shape[:-1]
+    x2 = x.reshape(-1, din)
+    if x2.dtype != torch.float32:
+        raise TypeError("the HIP path computes in fp32; got " + str(x2.dtype))
+    if not x2.is_cuda:
+        raise nat.NativeUnavailable("insr-pde_amd runs on the GPU only (got a CPU tensor); "
+                                    "move the network and samples to cuda")
+    return x2.contiguous(), lead
+
+
+def _needs_save(mlp):
+    return torch.is_grad_enabled() and any(p.requires_grad for p in mlp.parameters())
+
+
+class _SirenJet(torch.autograd.Function):
+    """Forward jet (one kernel) + reverse jet (one kernel + partial reduction)."""
+
+    @staticmethod
+    def forward(ctx, x2, mode, mlp, save, *params):
+        lib = nat.lib()
+        n, din = x2.shape
+        L, W, dout = mlp.num_hidden_layers, mlp.hidden_features, mlp.out_features
+        flat = mlp.flat_params()
+        dev = x2.device
+        y = torch.empty(n, dout, device=dev, dtype=torch.float32)
+        dy = torch.empty(n, dout, din, device=dev, dtype=torch.float32) if mode != nat.MODE_VALUE else None
+        lap = torch.empty(n, dout, device=dev, dtype=torch.float32) if mode == nat.MODE_LAP else None
+        act = None
+        if save:
+            nbytes = lib.insr_jet_act_bytes(n, din, L, W, mode)
+            act = torch.empty(max(nbytes // 4, 1), device=dev, dtype=torch.float32)
+        rc = lib.insr_siren_jet_fwd(nat.ptr(x2), n, din, dout, L, W, mode, nat.ptr(flat), nat.ptr(y), nat.ptr(dy),
+                                    nat.ptr(lap), nat.ptr(act), nat.stream_of(dev))
+        nat.check(rc, "insr_siren_jet_fwd")
+        ctx.mode, ctx.mlp, ctx.save = mode, mlp, save
+        ctx.x2, ctx.act = x2, act
+        outs = [y]
+        if dy is not None:
+            outs.append(dy)
+        if lap is not None:
+            outs.append(lap)
+        return tuple(outs)
+
+    @staticmethod
+    @once_differentiable
+    def backward(ctx, *grads):
+        mlp, mode = ctx.mlp, ctx.mode
+        none = (None,) * (4 + len(list(mlp.parameters())))
+        if not ctx.save or not any(p.requires_grad for p in mlp.parameters()):
+            return none
+        gy = grads[0]
+        gdy = grads[1] if mode != nat.MODE_VALUE else None
+        glap = grads[2] if mode == nat.MODE_LAP else None
+        x2, act = ctx.x2, ctx.act
+        n, din = x2.shape
+        L, W, dout = mlp.num_hidden_layers, mlp.hidden_features, mlp.out_features
+        lib = nat.lib()
+        part = torch.empty(max(lib.insr_jet_partial_bytes(n, din, dout, L, W) // 4, 1), device=x2.device,
+                           dtype=torch.float32)
+        gflat, accumulate = mlp.grad_for_backward()
+        c = lambda t: None if t is None else t.contiguous()  # noqa: E731
+        gy, gdy, glap = c(gy), c(gdy), c(glap)
+        rc = lib.insr_siren_jet_bwd(nat.ptr(x2), n, din, dout, L, W, mode, nat.ptr(mlp.flat_params()), nat.ptr(act),
+                                    nat.ptr(gy), nat.ptr(gdy), nat.ptr(glap), nat.ptr(part), nat.ptr(gflat), accumulate,
+                                    nat.stream_of(x2.device))
+        nat.check(rc, "insr_siren_jet_bwd")
+        return none
+
+
+def run_jet(mlp, x, mode):
+    """Run the fused jet of `mlp` at `x`.  Returns (y, dy, lap) with leading dims of x;
+    dy is (..., d_out, d_in), lap (..., d_out); missing streams are None."""
+    mlp.ensure_packed()
+    din = mlp.in_features
+    lib = nat.lib()
+    if not lib.insr_siren_supported(din, mlp.out_features, mlp.num_hidden_layers, mlp.hidden_features, mode):
+        raise UnsupportedPattern(
+            f"no HIP kernel for SIREN(in={din}, out={mlp.out_features}, width={mlp.hidden_features}) "
+            f"in {MODE_NAMES[mode]} mode")
+    x2, lead = _flatten_x(x, din)
+    params = tuple(mlp.parameters())
+    outs = _SirenJet.apply(x2, mode, mlp, _needs_save(mlp), *params)
+    if x.dim() == 2:  # no view node: keeps y.grad_fn == our node (identity-stable, see match())
+        y = outs[0]
+        dy = outs[1] if mode != nat.MODE_VALUE else None
+        lap = outs[2] if mode == nat.MODE_LAP else None
+        return y, dy, lap
+    y = outs[0].view(*lead, mlp.out_features)
+    dy = outs[1].view(*lead, mlp.out_features, din) if mode != nat.MODE_VALUE else None
+    lap = outs[2].view(*lead, mlp.out_features) if mode == nat.MODE_LAP else None
+    return y, dy, lap
+
+
+# value tensors by the id of their autograd node (validated on lookup: no stale ids)
+_VALUES = {}
+
+
+def _register_value(y):
+    node = y.grad_fn
+    if node is None:
+        return
+    if len(_VALUES) > 4096:
+        for k in [k for k, r in _VALUES.items() if r() is None]:
+            del _VALUES[k]
+    _VALUES[id(node)] = weakref.ref(y)
+
+
+def _value_of_node(node):
+    r = _VALUES.get(id(node))
+    y = r() if r is not None else None
+    if y is not None and y.grad_fn is node:
+        return y
+    return None
+
+
+def siren_value(mlp, x):
+    y, _, _ = run_jet(mlp, x, nat.MODE_VALUE)
+    y._insr_src = (mlp, x)
+    y._insr_jets = {}
+    _register_value(y)
+    return y
+
+
+# --------------------------------------------------------------------------
+# provenance matching
+# --------------------------------------------------------------------------
+def _grad_edge_node(t):
+    if t.grad_fn is not None:
+        return t.grad_fn
+    if t.requires_grad:
+        return torch.autograd.graph.get_gradient_edge(t).node
+    return None
+
+
+def match(y, x):
+    """Return (mlp, value_tensor, affine) if y is a recognised function of x, else None.
+
+    affine=True means y = mlp(x) + x (the identity is added to the Jacobian).
+    """
+    src = getattr(y, "_insr_src", None)
+    if src is not None:
+        return (src[0], y, False) if src[1] is x else None
+    fn = y.grad_fn
+    if fn is None or type(fn).__name__ != "AddBackward0" or getattr(fn, "_saved_alpha", 1) != 1:
+        return None
+    nodes = [nf[0] for nf in fn.next_functions]
+    if len(nodes) != 2:
+        return None
+    xnode = _grad_edge_node(x)
+    if xnode is None:
+        return None
+    for a, b in ((0, 1), (1, 0)):
+        if nodes[b] is xnode and nodes[a] is not None:
+            v = _value_of_node(nodes[a])
+            if v is not None and v._insr_src[1] is x and v.shape == x.shape:
+                return v._insr_src[0], v, True
+    return None
+
+
+def jet_of(mlp, value, x, mode):
+    """Derivative jets are cached on the value tensor; a LAP jet also serves GRAD."""
+    cache = getattr(value, "_insr_jets", None)
+    if cache is not None:
+        for m in ((nat.MODE_LAP,) if mode == nat.MODE_LAP else (nat.MODE_GRAD, nat.MODE_LAP)):
+            if m in cache:
+                return cache[m]
+    res = run_jet(mlp, x, mode)
+    if cache is not None:
+        cache[mode] = res
+    return res

@@ -1,0 +1,97 @@
+"""The inner optimisation loop of one phase (base/baseModel.py:96-135 semantics).
+
+  reset optimiser -> for i < max_n_iters: loss_dict = phase(); update();
+                     log losses; optional vis; early stop when lr <= 1.1e-8
+
+Differences, all controlled by cfg attributes:
+  insr_sync_every (int, default 1) -- losses/lr are read on the host every k
+      iterations (the reference reads them every iteration, which costs two
+      device->host syncs per iteration).  Early stop is checked at those reads.
+  insr_graph (bool, default False) -- iteration 0 runs eagerly (warm-up,
+      allocator settle); iteration 1 is captured into a hipGraph and every
+      later iteration is one graph replay.  If capture fails (e.g. a phase
+      with data-dependent shapes or host syncs) the loop stays eager.
+"""
+import torch
+
+try:
+    from tqdm import tqdm
+except Exception:  # pragma: no cover
+    tqdm = None
+
+
+class PhaseLoop:
+    def __init__(self, model, func, tag, args, kwargs):
+        self.m, self.func, self.tag = model, func, tag
+        self.args, self.kwargs = args, kwargs
+        cfg = model.cfg
+        self.sync_every = max(1, int(getattr(cfg, "insr_sync_every", 1)))
+        self.use_graph = bool(getattr(cfg, "insr_graph", False))
+        self.vis_every = int(getattr(cfg, "vis_frequency", 1000))
+        self.early_stop = bool(getattr(cfg, "early_stop", True))
+        self.show = bool(getattr(cfg, "insr_progress", True)) and tqdm is not None
+        self.graph = None
+        self.static = None
+
+    def _body(self):
+        loss_dict = self.func(self.m, *self.args, **self.kwargs)
+        synced = self.m._update_network(loss_dict)
+        return synced if isinstance(synced, dict) else loss_dict
+
+    def _capture(self):
+        m = self.m
+        side = torch.cuda.Stream(device=m.device)
+        side.wait_stream(torch.cuda.current_stream(m.device))
+        g = torch.cuda.CUDAGraph()
+        try:
+            with torch.cuda.stream(side):
+                with torch.cuda.graph(g, stream=side):
+                    out = self._body()
+            torch.cuda.current_stream(m.device).wait_stream(side)
+        except Exception as e:  # not capturable: stay eager
+            torch.cuda.synchronize(m.device)
+            self.use_graph = False
+            self.capture_error = repr(e)
+            return None
+        self.graph, self.static = g, {k: v.detach() for k, v in out.items()}
+        return self.static
+
+    def step(self, i):
+        """Run iteration i; returns the device loss dict of that iteration."""
+        if self.use_graph and i >= 1:
+            if self.graph is None:
+                if self._capture() is None:
+                    return self._body()
+            self.graph.replay()
+            return self.static
+        return self._body()
+
+    def run(self):
+        m = self.m
+        m._reset_optimizer()
+        m.train_step = 0
+        pbar = tqdm(range(m.max_n_iters), desc=f"{self.tag}[{m.timestep}]", disable=not self.show) \
+            if tqdm is not None else range(m.max_n_iters)
+        min_loss, accum = float("inf"), 0
+        for i in pbar:
+            loss_dict = self.step(i)
+            m.train_step += 1
+            last = (i == m.max_n_iters - 1)
+            if (i + 1) % self.sync_every == 0 or last or i == 0:
+                vals = {k: float(v) for k, v in loss_dict.items()}
+                if m.tb is not None:
+                    m.tb.add_scalars(self.tag, vals, global_step=i)
+                if tqdm is not None and hasattr(pbar, "set_postfix"):
+                    pbar.set_postfix(vals)
+                if vals["main"] < min_loss:
+                    min_loss, accum = vals["main"], 0
+                else:
+                    accum += 1
+                if self.early_stop and m.optimizer.param_groups[0]['lr'] <= m.min_lr:
+                    if tqdm is not None:
+                        tqdm.write(f"early stopping at iteration {i}")
+                    break
+            if (i == 0 or (i + 1) % self.vis_every == 0) and hasattr(m, f"_vis{self.tag}"):
+                getattr(m, f"_vis{self.tag}")()
+        self.graph = None
+        self.static = None

@@ -1,0 +1,85 @@
+"""ctypes binding of libinsr_hip.so (C ABI declared in include/insr_siren.h).
+
+The library is the product: there is no CPU or eager-torch fallback behind it.
+If it is missing or was not built, every hot-path call raises NativeUnavailable.
+torch is imported first so the library binds to the HIP runtime torch already
+loaded (both carry SONAME libamdhip64.so.7).
+"""
+import ctypes
+import os
+
+import torch  # noqa: F401  (must precede the CDLL load: shared HIP runtime)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("INSR_HIP_LIB", os.path.join(os.path.dirname(_HERE), "lib", "libinsr_hip.so"))
+
+MODE_VALUE, MODE_GRAD, MODE_LAP = 0, 1, 2
+OPT_LR, OPT_STEP, OPT_BEST, OPT_BAD, OPT_STEPSIZE, OPT_BC2SQRT, OPT_FACTOR, OPT_MINLR = range(8)
+OPT_NFLOATS = 8
+
+_P = ctypes.c_void_p
+_I = ctypes.c_int
+_L = ctypes.c_long
+_F = ctypes.c_float
+
+# name -> (restype, argtypes); mirrors include/insr_siren.h one to one
+SIGNATURES = {
+    "insr_version": (_I, []),
+    "insr_siren_param_count": (_L, [_I, _I, _I, _I]),
+    "insr_siren_supported": (_I, [_I, _I, _I, _I, _I]),
+    "insr_jet_act_bytes": (_L, [_L, _I, _I, _I, _I]),
+    "insr_jet_partial_bytes": (_L, [_L, _I, _I, _I, _I]),
+    "insr_siren_jet_fwd": (_I, [_P, _L, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P]),
+    "insr_siren_jet_bwd": (_I, [_P, _L, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _I, _P]),
+    "insr_reduce_partials": (_I, [_P, _I, _L, _P, _I, _P]),
+    "insr_adam_prepare": (_I, [_P, _F, _F, _P]),
+    "insr_plateau_step": (_I, [_P, _P, _I, _P]),
+    "insr_adam_step": (_I, [_P, _P, _P, _P, _L, _P, _F, _F, _F, _P]),
+}
+
+
+class NativeUnavailable(RuntimeError):
+    pass
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+_lib = None
+_load_error = None
+
+
+def load(path=None):
+    """Load (once) and return the CDLL with typed signatures."""
+    global _lib, _load_error
+    if _lib is not None:
+        return _lib
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        _load_error = f"{p} not found: run `python -c 'import __graft_entry__ as g; g.build()'`"
+        raise NativeUnavailable(_load_error)
+    lib = ctypes.CDLL(p)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def lib():
+    return _lib if _lib is not None else load()
+
+
+def ptr(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def stream_of(device):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def check(rc, what):
+    if rc != 0:
+        raise NativeError(f"{what} failed with code {rc}")

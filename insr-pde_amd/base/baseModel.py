@@ -1,0 +1,223 @@
+"""Training-loop framework, drop-in for base/baseModel.py:10-162 of the reference.
+
+Same abstract members (_trainable_networks, _sample_in_training, initialize,
+step), decorators (_timestepping, _training_loop), helpers (_update_network,
+_reset_optimizer, _create_network, _set_require_grads, _create_tb,
+save_ckpt, load_ckpt) and attributes (device, dt, max_n_iters,
+sample_resolution, vis_resolution, timestep, train_step, optimizer,
+scheduler, tb).  Model files written for the reference run unchanged.
+
+MI355X-specific behaviour (all opt-in through cfg attributes, defaults keep
+the reference's semantics except where noted):
+  * the optimiser is base.optim.FusedAdam (flat buffers, device-resident lr /
+    step / plateau state) -- same update rule as torch.optim.Adam;
+  * cfg.insr_sync_every (default 1): the loop reads the loss values (tqdm /
+    tensorboard / early stop) every k iterations instead of every iteration;
+  * cfg.insr_graph (default False): after one eager iteration the phase body +
+    update is captured into a hipGraph (torch.cuda.CUDAGraph) and replayed;
+    falls back to eager if the phase is not capturable;
+  * data parallel: when torch.distributed is initialised, _update_network
+    all-reduces the flat gradients (RCCL) before the Adam step and the losses
+    before the plateau step (mean or sum per `_dp_loss_reduction`).
+"""
+import os
+import shutil
+from abc import ABC, abstractmethod
+
+import torch
+
+from .networks import get_network
+from .optim import DevicePlateau, FusedAdam
+
+try:  # tensorboardX is optional (not installed on the MI355X image)
+    from tensorboardX import SummaryWriter
+except Exception:  # pragma: no cover - depends on the environment
+    SummaryWriter = None
+
+try:
+    from tqdm import tqdm
+except Exception:  # pragma: no cover
+    tqdm = None
+
+
+class _NullWriter:
+    def __init__(self, *a, **k):
+        pass
+
+    def add_scalars(self, *a, **k):
+        pass
+
+    def add_scalar(self, *a, **k):
+        pass
+
+    def add_figure(self, *a, **k):
+        pass
+
+    def close(self):
+        pass
+
+
+def _local_device():
+    rank = int(os.environ.get("LOCAL_RANK", "0"))
+    return torch.device("cuda", rank)
+
+
+class BaseModel(ABC):
+    _dp_loss_reduction = 'mean'  # how per-rank losses combine under data parallelism
+
+    def __init__(self, cfg):
+        self.cfg = cfg
+        self.exp_dir = cfg.exp_dir
+        self.dt = cfg.dt
+        self.max_n_iters = cfg.max_n_iters
+        self.sample_resolution = cfg.sample_resolution
+        self.vis_resolution = cfg.vis_resolution
+        self.timestep = -1
+
+        self.tb = None
+        self.min_lr = 1.1e-8
+        self.early_stop_plateau = 500
+        self.train_step = 0
+        self.optimizer = None
+        self.scheduler = None
+
+        self.device = _local_device()
+
+    def _create_network(self, input_dim, output_dim):
+        return get_network(self.cfg, input_dim, output_dim).to(self.device)
+
+    @property
+    @abstractmethod
+    def _trainable_networks(self):
+        """return a dict of trainable networks"""
+        raise NotImplementedError
+
+    @abstractmethod
+    def _sample_in_training(self):
+        """sampling points in each training step"""
+        raise NotImplementedError
+
+    @abstractmethod
+    def initialize(self):
+        """fit network to initial condition (timestep = 0). NOTE: warp with _timestepping."""
+        raise NotImplementedError
+
+    @abstractmethod
+    def step(self):
+        """step the system by one time step (timestep >= 1). NOTE: warp with _timestepping."""
+        raise NotImplementedError
+
+    def write_output(self, output_folder):
+        """write visulized/discrete output"""
+        pass
+
+    # ------------------------------------------------------------------ optimiser
+    def _reset_optimizer(self, use_scheduler=True, gamma=0.1, patience=500, min_lr=1e-8):
+        """Adam (one group per trainable network) + ReduceLROnPlateau (base/baseModel.py:55-62)."""
+        groups = [{"params": list(net.parameters()), "lr": self.cfg.lr, "module": net}
+                  for net in self._trainable_networks.values()]
+        self.optimizer = FusedAdam(groups)
+        self.scheduler = DevicePlateau(self.optimizer, factor=gamma, patience=patience,
+                                       min_lr=min_lr) if use_scheduler else None
+
+    def _create_tb(self, name, overwrite=True):
+        """create tensorboard log (a no-op writer when tensorboardX is absent)"""
+        self.log_path = os.path.join(self.cfg.log_dir, name)
+        if os.path.exists(self.log_path) and overwrite:
+            shutil.rmtree(self.log_path, ignore_errors=True)
+        if self.tb is not None:
+            self.tb.close()
+        self.tb = SummaryWriter(self.log_path) if SummaryWriter is not None else _NullWriter()
+
+    def _dp_world(self):
+        d = torch.distributed
+        return d.get_world_size() if (d.is_available() and d.is_initialized()) else 1
+
+    def _dp_sync(self, loss_dict):
+        """All-reduce gradients (+ losses) across ranks: one RCCL call per tensor group."""
+        world = self._dp_world()
+        if world == 1:
+            return loss_dict
+        d = torch.distributed
+        grads = [net.flat_grad_buffer() for net in self._trainable_networks.values()]
+        flat = torch.cat(grads) if len(grads) > 1 else grads[0]
+        keys = list(loss_dict.keys())
+        losses = torch.stack([torch.as_tensor(loss_dict[k], device=flat.device).detach().float().reshape(())
+                              for k in keys])
+        buf = torch.cat([flat, losses])
+        d.all_reduce(buf, op=d.ReduceOp.SUM)
+        if self._dp_loss_reduction == 'mean':
+            buf.div_(world)
+        if len(grads) > 1:
+            off = 0
+            for g in grads:
+                g.copy_(buf[off:off + g.numel()])
+                off += g.numel()
+        else:
+            grads[0].copy_(buf[:grads[0].numel()])
+        red = buf[flat.numel():]
+        return {k: red[i] for i, k in enumerate(keys)}
+
+    def _update_network(self, loss_dict):
+        """update network by back propagation (base/baseModel.py:73-81)"""
+        loss = sum(loss_dict.values())
+        self.optimizer.zero_grad()
+        loss.backward()
+        synced = self._dp_sync(loss_dict)
+        self.optimizer.step()
+        if self.scheduler is not None:
+            self.scheduler.step(synced['main'])
+        return synced
+
+    def _set_require_grads(self, model, require_grad):
+        for p in model.parameters():
+            p.requires_grad_(require_grad)
+
+    # ------------------------------------------------------------------ decorators
+    @classmethod
+    def _timestepping(cls, func):
+        def warp(self):
+            self.timestep += 1
+            self._create_tb(f"t{self.timestep:03d}")
+            func(self)
+            self.save_ckpt()
+        return warp
+
+    @classmethod
+    def _training_loop(cls, func):
+        """Wrap a phase body (returns a loss dict with key 'main') in the inner
+        optimisation loop (base/baseModel.py:96-135)."""
+        tag = func.__name__
+
+        def loop(self, *args, **kwargs):
+            from ._loop import PhaseLoop
+            PhaseLoop(self, func, tag, args, kwargs).run()
+        loop.__name__ = tag
+        loop._insr_phase = func
+        return loop
+
+    # ------------------------------------------------------------------ checkpoints
+    def save_ckpt(self, name=None):
+        """save checkpoint for future restore (keys as base/baseModel.py:137-150)"""
+        if name is None:
+            save_path = os.path.join(self.cfg.model_dir, f"ckpt_step_t{self.timestep:03d}.pth")
+        else:
+            save_path = os.path.join(self.cfg.model_dir, f"ckpt_{name}.pth")
+        save_dict = {}
+        for key, net in self._trainable_networks.items():
+            save_dict[f'net_{key}'] = {k: v.detach().cpu() for k, v in net.state_dict().items()}
+        save_dict['timestep'] = self.timestep
+        if getattr(self, '_dp_rank0', True):
+            os.makedirs(os.path.dirname(save_path), exist_ok=True)
+            torch.save(save_dict, save_path)
+
+    def load_ckpt(self, name):
+        """load saved checkpoint (base/baseModel.py:152-162)"""
+        if type(name) is int:
+            load_path = os.path.join(self.cfg.model_dir, f"ckpt_step_t{name:03d}.pth")
+        else:
+            load_path = os.path.join(self.cfg.model_dir, f"ckpt_{name}.pth")
+        checkpoint = torch.load(load_path, map_location=self.device, weights_only=True)
+        for key, net in self._trainable_networks.items():
+            net.load_state_dict(checkpoint[f'net_{key}'])
+        self.timestep = checkpoint['timestep']

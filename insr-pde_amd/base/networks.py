@@ -1,0 +1,210 @@
+"""SIREN field network, drop-in for base/networks.py:12-93 of the reference.
+
+`get_network(cfg, in, out)` / `MLP(...)` keep the reference's module tree
+(`.net` = Sequential[Linear, Sine, (Linear, Sine) x L, Linear]), its init RNG
+order (so a torch seed gives the reference's weights bit for bit), and its
+state_dict keys (net.0.weight ... net.{2L+2}.bias), so checkpoints and
+`load_state_dict` interoperate with the reference unchanged.
+
+What differs is storage and execution:
+  * all parameters are views into ONE flat fp32 buffer in state_dict order --
+    the layout the HIP kernels and the fused Adam consume directly (see
+    include/insr_siren.h); `.grad` tensors are views into one flat gradient;
+  * `forward` runs the fused HIP jet kernel (value stream) instead of the
+    aten addmm/sin chain, and tags its output with its provenance so the
+    diff ops (base/diff_ops.py) can dispatch derivative jets.
+"""
+import math
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+from . import _jet
+
+OMEGA = 30.0
+
+
+def get_network(cfg, in_features, out_features):
+    """base/networks.py:12-17: only the 'siren' network exists."""
+    if cfg.network == 'siren':
+        return MLP(in_features, out_features, cfg.num_hidden_layers, cfg.hidden_features,
+                   nonlinearity=cfg.nonlinearity)
+    raise NotImplementedError(cfg.network)
+
+
+class Sine(nn.Module):
+    """sin(30 x) (base/networks.py:21-27).  Only used when `.net` is called directly;
+    MLP.forward never runs it (the HIP kernel fuses it)."""
+
+    def forward(self, input):
+        return torch.sin(OMEGA * input)
+
+
+def _sine_init(m):
+    # base/networks.py:80-85
+    with torch.no_grad():
+        if hasattr(m, 'weight'):
+            fan_in = m.weight.size(-1)
+            b = np.sqrt(6 / fan_in) / OMEGA
+            m.weight.uniform_(-b, b)
+
+
+def _first_layer_sine_init(m):
+    # base/networks.py:88-93
+    with torch.no_grad():
+        if hasattr(m, 'weight'):
+            fan_in = m.weight.size(-1)
+            m.weight.uniform_(-1 / fan_in, 1 / fan_in)
+
+
+class MLP(nn.Module):
+    """SIREN MLP with flat parameter storage and a HIP forward (base/networks.py:30-71)."""
+
+    def __init__(self, in_features, out_features, num_hidden_layers, hidden_features,
+                 outermost_linear=True, nonlinearity='relu', weight_init=None):
+        super().__init__()
+        if nonlinearity != 'sine' or not outermost_linear:
+            # the reference also offers relu/elu nets; INSR-PDE only ever builds SIRENs
+            raise NotImplementedError("insr-pde_amd implements the SIREN ('sine', outermost linear) network")
+        self.in_features, self.out_features = in_features, out_features
+        self.num_hidden_layers, self.hidden_features = num_hidden_layers, hidden_features
+        layers = [nn.Linear(in_features, hidden_features), Sine()]
+        for _ in range(num_hidden_layers):
+            layers += [nn.Linear(hidden_features, hidden_features), Sine()]
+        layers.append(nn.Linear(hidden_features, out_features))
+        self.net = nn.Sequential(*layers)
+        self.weight_init = weight_init if weight_init is not None else _sine_init
+        self.net.apply(self.weight_init)
+        self.net[0].apply(_first_layer_sine_init)
+        self.first_layer_init = None
+        self._flat = None
+        self._flat_grad = None
+        self._repack()
+
+    # ---- flat storage ------------------------------------------------------
+    @property
+    def param_count(self):
+        return sum(p.numel() for p in self.parameters())
+
+    def flat_params(self):
+        return self._flat
+
+    def _repack(self):
+        """Move every parameter into one contiguous buffer (Parameter identity kept)."""
+        params = list(self.parameters())
+        if not params:
+            return
+        dev, dt = params[0].device, params[0].dtype
+        flat = torch.empty(sum(p.numel() for p in params), device=dev, dtype=dt)
+        grads_present = any(p.grad is not None for p in params)
+        gflat = torch.zeros_like(flat) if grads_present else None
+        off = 0
+        for p in params:
+            n = p.numel()
+            view = flat[off:off + n].view_as(p)
+            view.copy_(p.data)
+            p.data = view
+            if gflat is not None:
+                gv = gflat[off:off + n].view_as(p)
+                if p.grad is not None:
+                    gv.copy_(p.grad)
+                p.grad = gv
+            off += n
+        self._flat = flat
+        self._flat_grad = gflat
+
+    def _apply(self, fn, *args, **kwargs):
+        out = super()._apply(fn, *args, **kwargs)
+        self._repack()
+        return out
+
+    def _is_packed(self):
+        params = list(self.parameters())
+        if self._flat is None or not params:
+            return False
+        base = self._flat.data_ptr()
+        off = 0
+        for p in params:
+            if p.data_ptr() != base + off * p.element_size() or not p.is_contiguous():
+                return False
+            off += p.numel()
+        return off == self._flat.numel()
+
+    def ensure_packed(self):
+        if not self._is_packed():
+            self._repack()
+
+    # ---- flat gradient ---------------------------------------------------------
+    # state 'stale': zero_grad() ran; the buffer holds garbage and the first
+    # backward overwrites it (no memset launch).  'live': it holds the sum of
+    # the backward passes since then.
+    def _attach_grad_views(self, fold_foreign):
+        params = list(self.parameters())
+        g = self._flat_grad
+        if g is None or g.device != self._flat.device or g.numel() != self._flat.numel():
+            g = torch.zeros_like(self._flat)
+            self._flat_grad = g
+        off, folded = 0, False
+        for p in params:
+            n = p.numel()
+            if p.grad is None or p.grad.data_ptr() != g.data_ptr() + off * 4:
+                view = g[off:off + n].view_as(p)
+                if fold_foreign and p.grad is not None:
+                    view.copy_(p.grad)
+                    folded = True
+                elif fold_foreign:
+                    view.zero_()
+                    folded = True
+                p.grad = view
+            off += n
+        return g, folded
+
+    def mark_grad_stale(self, set_to_none=True):
+        self.ensure_packed()
+        if set_to_none:
+            for p in self.parameters():
+                p.grad = None
+        else:
+            g, _ = self._attach_grad_views(fold_foreign=False)
+            g.zero_()
+        self._grad_state = 'stale'
+
+    def grad_for_backward(self):
+        """(flat grad buffer, accumulate flag) for the next HIP backward."""
+        self.ensure_packed()
+        if getattr(self, '_grad_state', 'stale') == 'stale' and all(p.grad is None for p in self.parameters()):
+            g, _ = self._attach_grad_views(fold_foreign=False)
+            self._grad_state = 'live'
+            return g, 0
+        if getattr(self, '_grad_state', 'stale') == 'stale':
+            # set_to_none=False zeroing already happened; or foreign grads: fold them
+            g, _ = self._attach_grad_views(fold_foreign=True)
+            self._grad_state = 'live'
+            return g, 1
+        g, _ = self._attach_grad_views(fold_foreign=True)
+        return g, 1
+
+    def grad_touched(self):
+        return getattr(self, '_grad_state', 'stale') == 'live' or any(p.grad is not None for p in self.parameters())
+
+    def flat_grad_buffer(self):
+        """Flat gradient with every parameter's .grad attached to it (None grads -> 0)."""
+        self.ensure_packed()
+        if self._flat_grad is None or any(p.grad is None for p in self.parameters()):
+            g, _ = self._attach_grad_views(fold_foreign=True)
+            self._grad_state = 'live'
+            return g
+        g, _ = self._attach_grad_views(fold_foreign=True)
+        return g
+
+    # ---- forward -------------------------------------------------------------
+    def forward(self, coords, weights=None):
+        out = _jet.siren_value(self, coords)
+        if weights is not None:
+            out = out * weights
+        return out
+
+    def extra_repr(self):
+        return (f"in={self.in_features}, out={self.out_features}, hidden_layers={self.num_hidden_layers}, "
+                f"width={self.hidden_features}, backend=hip")
