@@ -1,0 +1,218 @@
+"""Headline benchmark: collocation-points/sec/timestep (incl. grad/Lap residual + Adam).
+
+Workload (BASELINE.json configs[1]): fluid2Dtlgn -- SIREN 4x128
+velocity (2->2) + pressure (2->1) networks, 128^2 = 16384 uniform-random interior
+collocation points per phase iteration, Taylor-Green weights/dt as the reference.
+One "step" = one inner iteration of EACH of the three phases of a fluid timestep
+(_advect_velocity, _solve_pressure, _projection): fresh samples, fused HIP jets,
+residual, HIP reverse jets, RCCL gradient all-reduce (N>1), fused Adam + plateau.
+Each phase iteration is replayed from a hipGraph captured during warm-up.
+
+    value = (points per phase-iteration, all ranks) x 3 phases x K / max_rank(time)
+
+Also reported: a roofline object for the dominant kernel (HIP events on its launch
+stream, eager re-run of the same step after the timed region) and a CPU baseline
+(the oracle restatement of the reference's torch graph, timed on this host).
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--scaling strong|weak]
+       (N > 1: launched by torch.distributed.run, one rank per GPU, RCCL).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "insr-pde_amd")]
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md chip table: dense fp32 matrix peak (spec)
+HBM_PEAK_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="fluid2Dtlgn")
+    ap.add_argument("--scaling", choices=["strong", "weak"], default="weak")
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the CPU-baseline sample")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-roofline", action="store_true")
+    return ap.parse_args()
+
+
+def setup_dist(args):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    return world, rank, local
+
+
+def build_model(args, world):
+    import base
+    from pde.config import baseline_config
+    from pde.fluid import Fluid2DModel
+    base._native.load()
+    N = 128 * 128
+    # strong: the global 16384 points are split over ranks; weak: every rank keeps 16384
+    sr = 128 if args.scaling == "strong" else int(round((N * world) ** 0.5))
+    cfg = baseline_config(args.config, sample_resolution=sr, insr_graph=not args.no_graph, insr_sync_every=10 ** 9,
+                          insr_progress=False, early_stop=False, proj_dir="/tmp/insr_bench", max_n_iters=10 ** 9)
+    torch.manual_seed(1234)
+    model = Fluid2DModel(cfg)
+    model.timestep = 1
+    model.init_cond_func = None
+    return model, cfg
+
+
+def phase_loops(model):
+    from base._loop import PhaseLoop
+    from pde.fluid import Fluid2DModel
+    loops = []
+    for name in ("_advect_velocity", "_solve_pressure", "_projection"):
+        pl = PhaseLoop(model, getattr(Fluid2DModel, name)._insr_phase, name, (), {})
+        pl.start()
+        loops.append(pl)
+    return loops
+
+
+def run_steps(loops, i0, k):
+    out = None
+    for i in range(i0, i0 + k):
+        for pl in loops:
+            out = pl.step(i)
+    return out
+
+
+def sync_all(world):
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+        torch.cuda.synchronize()
+
+
+def roofline(model, loops, n_local, P_pres):
+    """Eager re-run of one step with HIP events around every jet launch."""
+    from base import _jet
+    for pl in loops:  # eager path, same kernels and shapes as the captured graphs
+        pl.use_graph = False
+    _jet.TIMING["events"].clear()
+    _jet.TIMING["on"] = True
+    reps = 5
+    for _ in range(reps):
+        run_steps(loops, 10 ** 6, 1)
+    torch.cuda.synchronize()
+    _jet.TIMING["on"] = False
+    agg = {}
+    for key, e0, e1 in _jet.TIMING["events"]:
+        agg.setdefault(key, []).append(e0.elapsed_time(e1))
+    _jet.TIMING["events"].clear()
+    per_step = {k: sum(v) / reps for k, v in agg.items()}
+    dom = max(per_step, key=per_step.get)
+    kind, mode, n, W = dom
+    ms = sum(agg[dom]) / len(agg[dom])
+    # algorithmic flops per launch: 2P per point per stream per GEMM pass
+    P = P_pres if mode == "lap" else 2 * 128 + 4 * 128 * 128 + 128 * 2  # MACs/point/stream: pressure | velocity
+    streams = {"value": 1, "grad": 3, "lap": 4}[mode]
+    passes = 1 if kind == "fwd" else 2
+    flops = n * streams * passes * 2 * P
+    achieved = flops / (ms * 1e-3) / 1e12
+    table = {f"{k[0]}:{k[1]}:n{k[2]}": round(v, 4) for k, v in sorted(per_step.items(), key=lambda t: -t[1])}
+    return {"bound": "mfma", "achieved": round(achieved, 2), "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": None,
+            "kernel": f"jet_{kind}_kernel<{mode}> n={n} W={W}", "avg_ms": round(ms, 4),
+            "algorithmic_gflop_per_launch": round(flops / 1e9, 3), "per_step_ms_by_launch": table}
+
+
+def cpu_baseline(seconds):
+    """The oracle (torch-CPU restatement of the reference graph) on this host's cores."""
+    from oracle import siren_oracle as O
+    cores = len(os.sched_getaffinity(0))
+    torch.set_num_threads(cores)
+    torch.manual_seed(0)
+    vel, vel_prev, pres = O.OracleSiren(2, 2, 4, 128), O.OracleSiren(2, 2, 4, 128), O.OracleSiren(2, 1, 4, 128)
+    for p in vel_prev.parameters():
+        p.requires_grad_(False)
+    opts = [O.OracleAdam(list(vel.parameters()) + list(pres.parameters()), lr=1e-4) for _ in range(3)]
+    N, nb = 16384, 16384 // 100
+
+    def X():
+        return (torch.rand(N, 2) * 2 - 1).requires_grad_(True)
+
+    def B(side):
+        return O.sample_boundary2d_side(nb, side).requires_grad_(True)
+
+    def one_step():
+        O.update_step([vel, pres], O.fluid_advect_loss(vel, vel_prev, X(), B("horizontal"), B("vertical"), 0.05),
+                      opts[0])
+        O.update_step([vel, pres], O.fluid_pressure_loss(vel, pres, X(), B("horizontal"), B("vertical")), opts[1])
+        O.update_step([vel, pres], O.fluid_projection_loss(vel, vel_prev, pres, X(), B("horizontal"),
+                                                           B("vertical")), opts[2])
+
+    one_step()  # warm-up
+    t0 = time.perf_counter()
+    one_step()
+    t1 = time.perf_counter() - t0
+    reps = max(1, int(seconds / max(t1, 1e-3)) - 1)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        one_step()
+    dt = (time.perf_counter() - t0) / reps
+    return {"value": round(3 * N / dt, 1), "unit": "collocation-points/s", "cores": cores, "kind": "port",
+            "sample": f"oracle/siren_oracle.py fluid2Dtlgn: {reps} timed timestep-iterations (3 phases x 16384 pts, "
+                      f"torch CPU autograd + Adam), {torch.get_num_threads()} threads, {dt * 1e3:.1f} ms/iter"}
+
+
+def main():
+    args = parse()
+    world, rank, local = setup_dist(args)
+    model, cfg = build_model(args, world)
+    n_local = model._n_interior()
+    loops = phase_loops(model)
+    for i in range(args.warmup):  # iteration 0 eager, iteration 1 captured (warm-up)
+        run_steps(loops, i, 1)
+    sync_all(world)
+    t0 = time.perf_counter()
+    run_steps(loops, args.warmup, args.steps)
+    sync_all(world)
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t)
+    total_points = n_local * world * 3 * args.steps
+    value = total_points / elapsed
+    result = {
+        "metric": "collocation-points/sec/timestep (incl. ∇/Δ residual + Adam) at 1/2/4/8 GPUs",
+        "value": round(value, 1), "unit": "collocation-points/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
+        "scaling": args.scaling, "vs_baseline": None, "dtype": "fp32", "data": "synthetic (uniform-random "
+        "collocation points, seeded SIREN init; no dataset exists for this path)",
+        "config": {"workload": "fluid2Dtlgn", "model": "SIREN 4x128 velocity(2->2) + pressure(2->1)",
+                   "points_per_phase_iter": n_local * world, "phases": 3, "global_batch": n_local * world,
+                   "seq_len": None, "parallelism": f"dp{world}", "graph": not args.no_graph},
+    }
+    if rank == 0 and not args.no_roofline:
+        P_pres = 2 * 128 + 4 * 128 * 128 + 128 * 1  # d_in W + L W^2 + W d_out
+        result["roofline"] = roofline(model, loops, n_local, P_pres)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+        result["speedup_vs_cpu_baseline"] = round(value / result["cpu_baseline"]["value"], 1)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -81,16 +81,19 @@ int insr_siren_jet_fwd(const float* x, long n_points, int d_in, int d_out, int n
 /*
  * Backward of the jet to the parameters.  Adjoints (any may be NULL = zero):
  *   gy (n, d_out), gdy (n, d_out, d_in), glap (n, d_out).
- *   partial  insr_jet_partial_bytes scratch (one fp32 gradient per block).
- *   grad     flat fp32 gradient (insr_siren_param_count); accumulate != 0 adds
- *            into it (autograd accumulation), 0 overwrites.
+ *   partial  insr_jet_partial_bytes: one fp32 parameter-gradient per block of
+ *            64 points (insr_jet_partial_blocks(n) rows x param_count).
+ * Sum the rows with insr_reduce_partials into the network's flat .grad.
  * The gradient w.r.t. x is not produced (the reference never reads it).
  * Replaces: the autograd backward of loss.backward() (base/baseModel.py:77).
  */
 int insr_siren_jet_bwd(const float* x, long n_points, int d_in, int d_out, int num_hidden,
                        int width, int mode, const float* params, const float* act,
                        const float* gy, const float* gdy, const float* glap, float* partial,
-                       float* grad, int accumulate, void* stream);
+                       void* stream);
+
+/* Number of partial-gradient rows insr_siren_jet_bwd writes for n points. */
+int insr_jet_partial_blocks(long n_points);
 
 /* grad[i] = (accumulate ? grad[i] : 0) + sum_b partial[b * count + i], fixed order. */
 int insr_reduce_partials(const float* partial, int n_blocks, long count, float* grad,

@@ -47,6 +47,29 @@ def _needs_save(mlp):
     return torch.is_grad_enabled() and any(p.requires_grad for p in mlp.parameters())
 
 
+# Optional per-launch HIP-event timing (bench.py's roofline leg).  When enabled,
+# every jet launch is bracketed by torch.cuda.Event records on the launch stream.
+TIMING = {"on": False, "events": []}
+
+
+class _timed:
+    def __init__(self, kind, mode, n, W):
+        self.key = (kind, MODE_NAMES[mode], n, W)
+
+    def __enter__(self):
+        if TIMING["on"]:
+            self.e0 = torch.cuda.Event(enable_timing=True)
+            self.e0.record()
+        return self
+
+    def __exit__(self, *exc):
+        if TIMING["on"]:
+            e1 = torch.cuda.Event(enable_timing=True)
+            e1.record()
+            TIMING["events"].append((self.key, self.e0, e1))
+        return False
+
+
 class _SirenJet(torch.autograd.Function):
     """Forward jet (one kernel) + reverse jet (one kernel + partial reduction)."""
 
@@ -64,8 +87,9 @@ class _SirenJet(torch.autograd.Function):
         if save:
             nbytes = lib.insr_jet_act_bytes(n, din, L, W, mode)
             act = torch.empty(max(nbytes // 4, 1), device=dev, dtype=torch.float32)
-        rc = lib.insr_siren_jet_fwd(nat.ptr(x2), n, din, dout, L, W, mode, nat.ptr(flat), nat.ptr(y), nat.ptr(dy),
-                                    nat.ptr(lap), nat.ptr(act), nat.stream_of(dev))
+        with _timed("fwd", mode, n, W):
+            rc = lib.insr_siren_jet_fwd(nat.ptr(x2), n, din, dout, L, W, mode, nat.ptr(flat), nat.ptr(y),
+                                        nat.ptr(dy), nat.ptr(lap), nat.ptr(act), nat.stream_of(dev))
         nat.check(rc, "insr_siren_jet_fwd")
         ctx.mode, ctx.mlp, ctx.save = mode, mlp, save
         ctx.x2, ctx.act = x2, act
@@ -95,10 +119,15 @@ class _SirenJet(torch.autograd.Function):
         gflat, accumulate = mlp.grad_for_backward()
         c = lambda t: None if t is None else t.contiguous()  # noqa: E731
         gy, gdy, glap = c(gy), c(gdy), c(glap)
-        rc = lib.insr_siren_jet_bwd(nat.ptr(x2), n, din, dout, L, W, mode, nat.ptr(mlp.flat_params()), nat.ptr(act),
-                                    nat.ptr(gy), nat.ptr(gdy), nat.ptr(glap), nat.ptr(part), nat.ptr(gflat), accumulate,
-                                    nat.stream_of(x2.device))
+        st = nat.stream_of(x2.device)
+        with _timed("bwd", mode, n, W):
+            rc = lib.insr_siren_jet_bwd(nat.ptr(x2), n, din, dout, L, W, mode, nat.ptr(mlp.flat_params()),
+                                        nat.ptr(act), nat.ptr(gy), nat.ptr(gdy), nat.ptr(glap), nat.ptr(part), st)
         nat.check(rc, "insr_siren_jet_bwd")
+        with _timed("reduce", mode, n, W):
+            rc = lib.insr_reduce_partials(nat.ptr(part), lib.insr_jet_partial_blocks(n), gflat.numel(),
+                                          nat.ptr(gflat), accumulate, st)
+        nat.check(rc, "insr_reduce_partials")
         return none
 
 

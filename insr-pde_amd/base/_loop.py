@@ -33,7 +33,14 @@ class PhaseLoop:
         self.graph = None
         self.static = None
 
+    def start(self):
+        """Fresh optimiser + scheduler for this phase (base/baseModel.py:106)."""
+        self.m._reset_optimizer()
+        self.opt, self.sched = self.m.optimizer, self.m.scheduler
+        self.graph, self.static = None, None
+
     def _body(self):
+        self.m.optimizer, self.m.scheduler = self.opt, self.sched
         loss_dict = self.func(self.m, *self.args, **self.kwargs)
         synced = self.m._update_network(loss_dict)
         return synced if isinstance(synced, dict) else loss_dict
@@ -68,7 +75,7 @@ class PhaseLoop:
 
     def run(self):
         m = self.m
-        m._reset_optimizer()
+        self.start()
         m.train_step = 0
         pbar = tqdm(range(m.max_n_iters), desc=f"{self.tag}[{m.timestep}]", disable=not self.show) \
             if tqdm is not None else range(m.max_n_iters)

@@ -30,7 +30,8 @@ SIGNATURES = {
     "insr_jet_act_bytes": (_L, [_L, _I, _I, _I, _I]),
     "insr_jet_partial_bytes": (_L, [_L, _I, _I, _I, _I]),
     "insr_siren_jet_fwd": (_I, [_P, _L, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P]),
-    "insr_siren_jet_bwd": (_I, [_P, _L, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _I, _P]),
+    "insr_siren_jet_bwd": (_I, [_P, _L, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P]),
+    "insr_jet_partial_blocks": (_I, [_L]),
     "insr_reduce_partials": (_I, [_P, _I, _L, _P, _I, _P]),
     "insr_adam_prepare": (_I, [_P, _F, _F, _P]),
     "insr_plateau_step": (_I, [_P, _P, _I, _P]),

@@ -750,21 +750,17 @@ int insr_siren_jet_fwd(const float* x, long n, int din, int dout, int L, int W, 
 
 int insr_siren_jet_bwd(const float* x, long n, int din, int dout, int L, int W, int mode, const float* params,
                        const float* act, const float* gy, const float* gdy, const float* glap, float* partial,
-                       float* grad, int accumulate, void* stream) {
+                       void* stream) {
   if (!shape_ok(din, dout, L, W, mode) || n < 0 || n > 0x7fffffffL) return INSR_EINVAL;
+  if (n == 0) return 0;
+  if (!x || !params || !act || !partial) return INSR_EINVAL;
   const long P = insr_siren_param_count(din, dout, L, W);
-  if (n == 0) {
-    if (!accumulate && grad) return (int)hipMemsetAsync(grad, 0, P * sizeof(float), (hipStream_t)stream);
-    return 0;
-  }
-  if (!x || !params || !act || !partial || !grad) return INSR_EINVAL;
   const int S = streams_for(din, mode);
-  int rc = dispatch_bwd(nt_for(W), S, mode == INSR_MODE_LAP, x, (int)n, din, dout, L, params, act, gy, gdy, glap,
-                        partial, P, (hipStream_t)stream);
-  if (rc) return rc;
-  const int nb = (int)((n + kPts - 1) / kPts);
-  return insr_reduce_partials(partial, nb, P, grad, accumulate, stream);
+  return dispatch_bwd(nt_for(W), S, mode == INSR_MODE_LAP, x, (int)n, din, dout, L, params, act, gy, gdy, glap,
+                      partial, P, (hipStream_t)stream);
 }
+
+int insr_jet_partial_blocks(long n) { return n <= 0 ? 0 : (int)((n + kPts - 1) / kPts); }
 
 int insr_reduce_partials(const float* partial, int nb, long count, float* grad, int accumulate, void* stream) {
   if (!partial || !grad || nb < 0 || count < 0) return INSR_EINVAL;

@@ -1,0 +1,74 @@
+"""1-D advection u_t + v u_x = 0 with the midpoint rule in time (the reference's
+Advection1DModel, advection/model.py:10-111), on the insr-pde_amd `base` API."""
+import os
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+from base import BaseModel, gradient, sample_boundary, sample_random, sample_uniform
+
+from .examples import get_examples
+
+
+class Advection1DModel(BaseModel):
+    """advection equation with constant velocity"""
+
+    def __init__(self, cfg):
+        super().__init__(cfg)
+        self.vel = cfg.vel
+        self.length = cfg.length
+        self.field = self._create_network(1, 1)
+        self.field_prev = self._create_network(1, 1)
+        self._set_require_grads(self.field_prev, False)
+
+    @property
+    def _trainable_networks(self):
+        return {"field": self.field}
+
+    def _n_interior(self):
+        return max(1, self.sample_resolution // self._dp_world())
+
+    def _sample_in_training(self):
+        half = self.length / 2
+        return sample_random(self._n_interior(), 1, device=self.device).requires_grad_(True) * half
+
+    def sample_field(self, resolution, return_samples=False):
+        grid = sample_uniform(resolution, 1, device=self.device) * self.length / 2
+        u = self.field(grid).squeeze(-1)
+        return (u, grid.squeeze(-1)) if return_samples else u
+
+    @BaseModel._timestepping
+    def initialize(self):
+        if not hasattr(self, "init_cond_func"):
+            self.init_cond_func = get_examples(self.cfg.init_cond)
+        self._initialize()
+
+    @BaseModel._training_loop
+    def _initialize(self):
+        x = self._sample_in_training()
+        return {'main': F.mse_loss(self.field(x), self.init_cond_func(x))}
+
+    @BaseModel._timestepping
+    def step(self):
+        self.field_prev.load_state_dict(self.field.state_dict())
+        self._advect()
+
+    @BaseModel._training_loop
+    def _advect(self):
+        x = self._sample_in_training()
+        u0 = self.field_prev(x)
+        u = self.field(x)
+        # midpoint rule: (u - u0)/dt + v (u_x + u0_x)/2 = 0
+        ux = gradient(u, x)
+        with torch.no_grad():
+            u0x = gradient(u0, x)
+        residual = (u - u0) / self.dt + self.vel * (ux + u0x) / 2.
+        n_bc = max(self._n_interior() // 100, 10)
+        xb = sample_boundary(n_bc, 1, device=self.device) * self.length / 2
+        return {'main': torch.mean(residual ** 2), 'bc': torch.mean(self.field(xb) ** 2) * 1.}
+
+    def write_output(self, output_folder):
+        u, grid = self.sample_field(self.vis_resolution, return_samples=True)
+        os.makedirs(output_folder, exist_ok=True)
+        np.savez(os.path.join(output_folder, f"t{self.timestep:03d}.npz"), u.detach().cpu().numpy())

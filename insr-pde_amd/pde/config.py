@@ -1,0 +1,68 @@
+"""Experiment configuration with the reference's flag names and defaults
+(config.py:86-168), as a plain namespace (no argparse side effects, no prompts)."""
+import os
+import types
+
+BASIC = dict(proj_dir="checkpoints", tag="run", gpu_ids=0)
+NETWORK = dict(network="siren", num_hidden_layers=3, hidden_features=64, nonlinearity="sine")
+TRAINING = dict(ckpt=None, vis_frequency=1000, max_n_iters=20000, lr=1e-4, sample_resolution=128,
+                vis_resolution=500, early_stop=True)
+TIMESTEP = dict(init_cond=None, dt=0.05, n_timesteps=30, fps=10)
+PDE = {
+    "advection": dict(length=4.0, vel=0.25),
+    "fluid": dict(),
+    "elasticity": dict(dim=2, sample_pattern=["random", "uniform"],
+                       energy=["arap", "kinematics", "external", "constraint"],
+                       ratio_constraint=1e3, ratio_volume=1e1, ratio_arap=1e0, ratio_collide=1e0,
+                       ratio_kinematics=1e0, use_mesh=False, mesh_path="./elasticity/data/woody.obj",
+                       external_force_timesteps=5, external_force_x=0.0, external_force_y=0.0,
+                       external_force_z=0.0, constraint_right_offset_x=1e0, constraint_right_offset_y=0.0,
+                       constraint_right_offset_z=0.0, plane_height=-2.0, collide_circle_x=0.0,
+                       collide_circle_y=-2e0, collide_circle_z=0.0, collide_circle_radius=1.0),
+}
+# insr-pde_amd execution knobs (see base/_loop.py)
+EXEC = dict(insr_sync_every=1, insr_graph=False, insr_progress=True)
+
+
+def make_config(pde, **overrides):
+    if pde not in PDE:
+        raise ValueError(pde)
+    d = {}
+    for part in (BASIC, NETWORK, TRAINING, TIMESTEP, PDE[pde], EXEC):
+        d.update(part)
+    d.update(overrides)
+    d["pde"] = pde
+    c = types.SimpleNamespace(**d)
+    c.exp_dir = os.path.join(c.proj_dir, c.tag)
+    c.log_dir = os.path.join(c.exp_dir, "log")
+    c.model_dir = os.path.join(c.exp_dir, "model")
+    return c
+
+
+# The BASELINE.json configurations; "SIREN LxW" = num_hidden_layers x hidden_features.
+BASELINE_CONFIGS = {
+    "advect1D": ("advection", dict(num_hidden_layers=3, hidden_features=64, sample_resolution=4096,
+                                   init_cond="example1", dt=0.05)),
+    "fluid2Dtlgn": ("fluid", dict(num_hidden_layers=4, hidden_features=128, sample_resolution=128,
+                                  init_cond="taylorgreen", dt=0.05)),
+    "elasticity2Dstretch": ("elasticity", dict(num_hidden_layers=5, hidden_features=128, sample_resolution=100,
+                                               dim=2, lr=1e-4, energy=["arap", "constraint", "constraint_right",
+                                                                       "volume"],
+                                               ratio_volume=1e3, ratio_arap=1e0, ratio_constraint=1e4,
+                                               constraint_right_offset_x=2.0)),
+    "elasticity3Dbunny": ("elasticity", dict(num_hidden_layers=5, hidden_features=256, sample_resolution=64,
+                                             dim=3, dt=0.1, sample_pattern=["random"],
+                                             energy=["arap", "kinematics", "collision", "external", "volume"],
+                                             ratio_volume=1e3, ratio_arap=1e2, ratio_collide=1e6,
+                                             ratio_kinematics=1e0, external_force_z=-1e2,
+                                             external_force_timesteps=5, plane_height=-2.0)),
+    "fluid2DtlgnM": ("fluid", dict(num_hidden_layers=4, hidden_features=128, sample_resolution=256,
+                                   init_cond="taylorgreen_multi", dt=0.05)),
+}
+
+
+def baseline_config(name, **overrides):
+    pde, kw = BASELINE_CONFIGS[name]
+    kw = dict(kw)
+    kw.update(overrides)
+    return make_config(pde, **kw)

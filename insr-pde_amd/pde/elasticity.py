@@ -1,0 +1,179 @@
+"""Elastodynamics by energy minimisation on a deformation field q = x + f(x)
+(the reference's ElasticityModel, elasticity/model.py:15-250, losses from
+elasticity/losses.py:6-39), on the insr-pde_amd `base` API.
+
+Energy terms (all SUMS over collocation points, as in the reference):
+  arap        r_a  sum (sigma_i - 1)^2         sigma = singular values of dq/dx
+  volume      r_v  sum (prod sigma_i - 1)^2
+  kinematics  r_k  sum |qdot - qdot_prev|^2     qdot = (q - q_prev)/dt
+  external    -dt  sum qdot . f_ext             (first T_ext timesteps)
+  constraint(_right[_compress]) r_c sum |f(x_fixed) - target|^2
+  collision(_sphere)  -dt sum qdot . penalty force on penetrating points
+
+Only the synthetic box geometry (use_mesh=False) is supported; the tet-mesh
+sampler is SURVEY.md §8(f) row 3 (next).
+"""
+import torch
+
+from base import BaseModel, sample_random, sample_uniform
+from base.diff_ops import jacobian_nosync
+
+from . import singular_values
+
+
+class ElasticityModel(BaseModel):
+    _dp_loss_reduction = 'sum'
+
+    def __init__(self, cfg):
+        super().__init__(cfg)
+        self.dim = cfg.dim
+        self.deformation_field = self._create_network(self.dim, self.dim)
+        self.deformation_field_prev = self._create_network(self.dim, self.dim)
+        self.deformation_field_prev_prev = self._create_network(self.dim, self.dim)
+        self._set_require_grads(self.deformation_field_prev, False)
+        self._set_require_grads(self.deformation_field_prev_prev, False)
+        with torch.no_grad():
+            self.deformation_field_prev.load_state_dict(self.deformation_field.state_dict())
+            self.deformation_field_prev_prev.load_state_dict(self.deformation_field.state_dict())
+        self._init_params(cfg)
+
+    def _init_params(self, cfg):
+        d, dev = self.dim, self.device
+        self.energy = list(cfg.energy)
+        self.use_mesh = bool(getattr(cfg, "use_mesh", False))
+        if self.use_mesh:
+            raise NotImplementedError("mesh-based sampling (bunny/spot scripts) is not built yet")
+        self.sample_pattern = list(cfg.sample_pattern)
+        self.ratio_arap, self.ratio_volume = cfg.ratio_arap, cfg.ratio_volume
+        self.ratio_kinematics, self.ratio_constraint = cfg.ratio_kinematics, cfg.ratio_constraint
+        self.ratio_collide = cfg.ratio_collide
+        self.external_force_timesteps = cfg.external_force_timesteps
+        self.plane_height = cfg.plane_height
+        self.circle_radius = cfg.collide_circle_radius
+        vec = lambda *v: torch.tensor(v[:d], dtype=torch.float32, device=dev)  # noqa: E731
+        self.external_force = vec(cfg.external_force_x, cfg.external_force_y, cfg.external_force_z)
+        self.constraint_offset_right = vec(cfg.constraint_right_offset_x, cfg.constraint_right_offset_y,
+                                           cfg.constraint_right_offset_z)
+        self.circle_center = vec(cfg.collide_circle_x, cfg.collide_circle_y, cfg.collide_circle_z)
+        self.sample_resolution_init = {2: 500, 3: 100}[d]
+
+    @property
+    def _trainable_networks(self):
+        return {'deformation': self.deformation_field}
+
+    # ---- sampling ------------------------------------------------------------
+    def _sample_in_training(self, resolution):
+        d, parts = self.dim, []
+        for s in self.sample_pattern:
+            if s == 'random':
+                parts.append(sample_random(resolution ** d, d, device=self.device).requires_grad_(True))
+            elif s == 'uniform':
+                parts.append(sample_uniform(resolution, d, device=self.device).requires_grad_(True))
+            else:
+                raise NotImplementedError(s)
+        x = torch.cat(parts, dim=0)
+        return self._dp_shard(x)
+
+    def _sample_fixed_in_training(self, resolution):
+        """Points on the x = -1 face (left) and x = +1 face (right)."""
+        d, left, right = self.dim, [], []
+        for s in self.sample_pattern:
+            if s == 'random':
+                faces = [sample_random(resolution, d - 1, device=self.device) for _ in range(2)]
+            elif s == 'uniform':
+                g = sample_uniform(resolution, d - 1, device=self.device)
+                faces = [g, g]
+            else:
+                raise NotImplementedError(s)
+            one = torch.ones(faces[0].shape[0], 1, device=self.device)
+            left.append(torch.cat([-one, faces[0]], 1).requires_grad_(True))
+            right.append(torch.cat([one, faces[1]], 1).requires_grad_(True))
+        return self._dp_shard(torch.cat(left, 0)), self._dp_shard(torch.cat(right, 0))
+
+    def _dp_shard(self, x):
+        world = self._dp_world()
+        if world == 1:
+            return x
+        r = torch.distributed.get_rank()
+        n = x.shape[0]
+        return x[r * n // world:(r + 1) * n // world]
+
+    # ---- timestepping ----------------------------------------------------------
+    @BaseModel._timestepping
+    def initialize(self):
+        self._initialize()
+        self.deformation_field_prev_prev.load_state_dict(self.deformation_field.state_dict())
+        self.deformation_field_prev.load_state_dict(self.deformation_field.state_dict())
+
+    @BaseModel._training_loop
+    def _initialize(self):
+        x = self._sample_in_training(self.sample_resolution_init)
+        return {'main': torch.mean(self.deformation_field(x) ** 2)}
+
+    @BaseModel._timestepping
+    def step(self):
+        self.deformation_field_prev_prev.load_state_dict(self.deformation_field_prev.state_dict())
+        self.deformation_field_prev.load_state_dict(self.deformation_field.state_dict())
+        self._solve_deformation()
+
+    @BaseModel._training_loop
+    def _solve_deformation(self):
+        x = self._sample_in_training(self.sample_resolution)
+        fixed_l, fixed_r = self._sample_fixed_in_training(self.sample_resolution)
+        return {'main': self.energy_of(x, fixed_l, fixed_r)}
+
+    def energy_of(self, x, fixed_l, fixed_r):
+        dt = self.dt
+        with torch.no_grad():
+            q_prev = self.deformation_field_prev(x) + x
+            q_pp = self.deformation_field_prev_prev(x) + x
+        q = self.deformation_field(x) + x
+        qdot = (q - q_prev) / dt
+        total = 0
+        sig = None
+        for term in self.energy:
+            if term in ('arap', 'volume') and sig is None:
+                J, _ = jacobian_nosync(q, x)  # status unused (as in the reference): no host sync
+                sig = singular_values(J)
+            if term == 'arap':
+                total = total + self.ratio_arap * torch.sum((sig - 1.0) ** 2)
+            elif term == 'volume':
+                total = total + self.ratio_volume * torch.sum((torch.prod(sig, dim=1) - 1) ** 2)
+            elif term == 'kinematics':
+                qdot_prev = (q_prev - q_pp) / dt
+                total = total + self.ratio_kinematics * torch.sum((qdot - qdot_prev) ** 2)
+            elif term == 'external':
+                if self.timestep <= self.external_force_timesteps:
+                    total = total - dt * torch.sum(qdot * self.external_force)
+            elif term == 'constraint':
+                total = total + self.ratio_constraint * torch.sum(self.deformation_field(fixed_l) ** 2)
+            elif term in ('constraint_right', 'constraint_right_compress'):
+                sign = 1.0 if term == 'constraint_right' else -1.0
+                tgt = sign * self.constraint_offset_right
+                total = total + self.ratio_constraint * torch.sum((self.deformation_field(fixed_r) - tgt) ** 2)
+            elif term == 'collision':
+                total = total + self._plane_penalty(q, qdot)
+            elif term == 'collision_sphere':
+                total = total + self._sphere_penalty(q, qdot)
+            else:
+                raise NotImplementedError(term)
+        return total
+
+    def _plane_penalty(self, q, qdot):
+        """elasticity/losses.py:10-20, written mask-free (no host sync): force only
+        on points below the plane; the reference's empty-set case gives 0 too."""
+        depth = torch.clamp(self.plane_height - q[:, -1], min=0.0)
+        hit = (q[:, -1] < self.plane_height).to(q.dtype)
+        return -self.dt * torch.sum(qdot[:, -1] * self.ratio_collide * depth * hit)
+
+    def _sphere_penalty(self, q, qdot):
+        """elasticity/losses.py:22-39, mask-free.  In 3-D the reference broadcasts
+        dist[:, None, None] * dir (K,1,1)x(K,3) -> (K,K,3), i.e. the energy becomes
+        (sum_i dist_i) * (sum_j qdot_j . dir_j); that is reproduced as is."""
+        vec = q - self.circle_center
+        dist = torch.sqrt(torch.sum(vec ** 2, dim=1))
+        hit = (dist < self.circle_radius).to(q.dtype)
+        direc = vec / dist[:, None]
+        if q.shape[1] == 2:
+            return -self.dt * torch.sum(qdot * (self.ratio_collide * dist[:, None] * direc) * hit[:, None])
+        return -self.dt * self.ratio_collide * torch.sum(dist * hit) * torch.sum(qdot * direc * hit[:, None])

@@ -1,0 +1,121 @@
+"""2-D inviscid Navier-Stokes on [-1, 1]^2 by operator splitting (the reference's
+Fluid2DModel, fluid/model.py:11-151), written against the insr-pde_amd `base` API.
+
+One timestep = three inner optimisation phases:
+  _advect_velocity  semi-Lagrangian: u(x) ~ u_prev(clamp(x - u_prev(x) dt))  (:72-101)
+  _solve_pressure   Poisson: lap p = div u, Neumann grad p . n = 0          (:103-125)
+  _projection       u ~ u_prev - grad p, no-slip-normal boundary            (:127-151)
+
+Under data parallelism each rank draws N / world collocation points (and its
+share of the boundary bands); the HIP jets and the RCCL gradient all-reduce
+in BaseModel._update_network make the step equal to one on the global batch.
+"""
+import os
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+from base import BaseModel, divergence, gradient, laplace, sample_boundary2D_separate, sample_random, sample_uniform
+
+from .examples import get_examples
+
+
+class Fluid2DModel(BaseModel):
+    """inviscid Navier-Stokes equation. 2D fluid. [-1, 1]^2."""
+
+    def __init__(self, cfg):
+        super().__init__(cfg)
+        self.velocity_field = self._create_network(2, 2)
+        self.velocity_field_prev = self._create_network(2, 2)
+        self.pressure_field = self._create_network(2, 1)
+        self._set_require_grads(self.velocity_field_prev, False)
+
+    @property
+    def _trainable_networks(self):
+        return {'velocity': self.velocity_field, 'pressure': self.pressure_field}
+
+    # ---- sampling ------------------------------------------------------------
+    def _n_interior(self):
+        return max(1, self.sample_resolution ** 2 // self._dp_world())
+
+    def _sample_in_training(self):
+        return sample_random(self._n_interior(), 2, device=self.device).requires_grad_(True)
+
+    def _boundary_pair(self, n_interior):
+        nb = n_interior // 100
+        bx = sample_boundary2D_separate(nb, side='horizontal', device=self.device).requires_grad_(True)
+        by = sample_boundary2D_separate(nb, side='vertical', device=self.device).requires_grad_(True)
+        return bx, by
+
+    def sample_field(self, resolution, return_samples=False):
+        grid = sample_uniform(resolution, 2, device=self.device, flatten=False).requires_grad_(True)
+        u = self.velocity_field(grid)
+        return (u, grid) if return_samples else u
+
+    # ---- timestepping ----------------------------------------------------------
+    @BaseModel._timestepping
+    def initialize(self):
+        if not hasattr(self, "init_cond_func"):
+            self.init_cond_func = get_examples(self.cfg.init_cond)
+        self._initialize()
+
+    @BaseModel._training_loop
+    def _initialize(self):
+        x = self._sample_in_training()
+        return {'main': F.mse_loss(self.velocity_field(x), self.init_cond_func(x))}
+
+    @BaseModel._timestepping
+    def step(self):
+        self.velocity_field_prev.load_state_dict(self.velocity_field.state_dict())
+        self._advect_velocity()
+        self._solve_pressure()
+        self.velocity_field_prev.load_state_dict(self.velocity_field.state_dict())
+        self._projection()
+
+    def _wall_loss(self, n_interior):
+        """u_x = 0 on the x-faces, u_y = 0 on the y-faces (mean squares)."""
+        bx, by = self._boundary_pair(n_interior)
+        ux = self.velocity_field(bx)[..., 0]
+        uy = self.velocity_field(by)[..., 1]
+        return (torch.mean(ux ** 2) + torch.mean(uy ** 2)) * 1.0
+
+    @BaseModel._training_loop
+    def _advect_velocity(self):
+        x = self._sample_in_training()
+        with torch.no_grad():
+            u_prev = self.velocity_field_prev(x).detach()
+        u = self.velocity_field(x)
+        foot = torch.clamp(x - u_prev * self.cfg.dt, min=-1.0, max=1.0)
+        with torch.no_grad():
+            u_target = self.velocity_field_prev(foot).detach()
+        return {'main': torch.mean((u - u_target) ** 2), 'bc': self._wall_loss(x.shape[0])}
+
+    @BaseModel._training_loop
+    def _solve_pressure(self):
+        x = self._sample_in_training()
+        with torch.no_grad():  # the reference detaches div u: no reverse jet, no saved streams
+            div_u = divergence(self.velocity_field(x), x)
+        lap_p = laplace(self.pressure_field(x), x)
+        main = torch.mean((div_u - lap_p) ** 2)  # rho = 1
+        bx, by = self._boundary_pair(x.shape[0])
+        dpx = gradient(self.pressure_field(bx), bx)[..., 0]
+        dpy = gradient(self.pressure_field(by), by)[..., 1]
+        return {'main': main, 'bc': torch.mean(dpx ** 2) + torch.mean(dpy ** 2)}
+
+    @BaseModel._training_loop
+    def _projection(self):
+        x = self._sample_in_training()
+        with torch.no_grad():
+            u_prev = self.velocity_field_prev(x).detach()
+        with torch.no_grad():  # detached in the reference as well
+            grad_p = gradient(self.pressure_field(x), x)
+        u = self.velocity_field(x)
+        return {'main': torch.mean((u - (u_prev - grad_p)) ** 2), 'bc': self._wall_loss(x.shape[0])}
+
+    # ---- output (host side; figures are out of scope) ------------------------
+    def write_output(self, output_folder):
+        u, grid = self.sample_field(self.vis_resolution, return_samples=True)
+        u_np = u.detach().cpu().numpy()
+        os.makedirs(output_folder, exist_ok=True)
+        np.save(os.path.join(output_folder, f"t{self.timestep:03d}_velocity.npy"), u_np)

@@ -1,0 +1,58 @@
+"""C ABI checks that need no GPU: the library loads, exports every symbol that
+include/insr_siren.h declares, and the pure-host queries answer correctly."""
+import os
+import re
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "insr_siren.h")
+
+
+def declared_symbols():
+    txt = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:int|long)\s+(insr_\w+)\s*\(", txt, flags=re.M)))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    import __graft_entry__ as ge
+    ge.build()
+    import base
+    return base._native.load(ge.LIB)
+
+
+def test_header_matches_binding():
+    from base import _native as nat
+    assert declared_symbols() == sorted(nat.SIGNATURES)
+
+
+def test_exports_every_declared_symbol(lib):
+    import ctypes
+    for name in declared_symbols():
+        assert isinstance(getattr(lib, name), ctypes._CFuncPtr), name
+
+
+def test_host_queries(lib):
+    assert lib.insr_version() >= 100
+    # SURVEY.md §8 parameter counts, verified against the reference MLP
+    assert lib.insr_siren_param_count(1, 1, 3, 64) == 12673
+    assert lib.insr_siren_param_count(2, 2, 4, 128) == 66690
+    assert lib.insr_siren_param_count(2, 1, 4, 128) == 66561
+    assert lib.insr_siren_param_count(2, 2, 5, 128) == 83202
+    assert lib.insr_siren_param_count(3, 3, 5, 256) == 330755
+    assert lib.insr_siren_supported(2, 1, 4, 128, 2) == 1
+    assert lib.insr_siren_supported(3, 1, 4, 128, 2) == 0   # Laplacian jet: d_in <= 2
+    assert lib.insr_siren_supported(2, 1, 4, 100, 0) == 0   # width not compiled
+    # saved activations: (L+1) layers x 16 W floats per 16-point tile x S streams
+    assert lib.insr_jet_act_bytes(64, 2, 4, 128, 2) == 5 * 4 * 16 * 128 * 4 * 4
+    assert lib.insr_jet_partial_bytes(65, 2, 1, 4, 128) == 2 * 66561 * 4
+    assert lib.insr_jet_partial_blocks(65) == 2 and lib.insr_jet_partial_blocks(0) == 0
+
+
+def test_invalid_arguments_rejected_without_launch(lib):
+    # bad shapes are refused before anything touches the device
+    assert lib.insr_siren_jet_fwd(None, 10, 0, 1, 4, 128, 0, None, None, None, None, None, None) == -1
+    assert lib.insr_siren_jet_fwd(None, 10, 2, 1, 4, 100, 0, None, None, None, None, None, None) == -1
+    assert lib.insr_siren_jet_fwd(None, 0, 2, 1, 4, 128, 0, None, None, None, None, None, None) == 0
+    assert lib.insr_adam_step(None, None, None, None, 10, None, 0.9, 0.999, 1e-8, None) == -1

@@ -1,0 +1,222 @@
+"""Phase-level parity: the HIP path against vectors recorded from the REFERENCE itself
+(tests/golden/ref_phases.npz, made by tests/golden/make_golden.py on identical weights
+and samples).  Covers the loss dict of every phase body, the parameter gradients after
+loss.backward(), and two full optimiser iterations (Adam + plateau) per phase.
+
+Tolerances: losses 1e-5 relative; gradients 1e-5 normwise per network.  After Adam,
+parameter *updates* are compared on entries whose reference gradient is well away from
+zero (|g| > 1e-3 max|g|): Adam's first step is ~lr*sign(g), so entries with |g| at the
+fp32 noise floor may legitimately flip sign.
+"""
+import os
+import types
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden", "ref_phases.npz")
+TOL = 1e-5
+
+
+@pytest.fixture(scope="module")
+def ph():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return dict(np.load(GOLD))
+
+
+def nerr(a, b):
+    a = torch.as_tensor(np.asarray(a, np.float64))
+    b = torch.as_tensor(np.asarray(b, np.float64))
+    return float((a - b).abs().max() / b.abs().max().clamp_min(1e-30))
+
+
+def set_flat(net, vec):
+    with torch.no_grad():
+        net.flat_params().copy_(torch.from_numpy(np.asarray(vec, np.float32)).cuda())
+
+
+def flat_grad(net):
+    return net.flat_grad_buffer().detach().cpu().numpy() if net.grad_touched() else np.zeros(net.param_count)
+
+
+def flat(net):
+    return net.flat_params().detach().cpu().numpy()
+
+
+def check_update(after_hip, before, after_ref, g_ref):
+    d_hip, d_ref = after_hip - before, after_ref - before
+    mask = np.abs(g_ref) > 1e-3 * np.abs(g_ref).max()
+    assert mask.sum() > 0.5 * mask.size
+    assert nerr(d_hip[mask], d_ref[mask]) < 1e-3
+    # everything else moved by at most ~2 lr per step (sign flips at the noise floor)
+    assert np.abs(d_hip - d_ref).max() <= 2 * 2 * 1e-4 * 1.01
+
+
+def _cfg(pde, **kw):
+    from pde.config import make_config
+    kw.setdefault("insr_progress", False)
+    kw.setdefault("early_stop", False)
+    kw.setdefault("max_n_iters", 2)
+    kw.setdefault("lr", 1e-4)
+    return make_config(pde, proj_dir="/tmp/insr_test", **kw)
+
+
+def test_fluid_phases(ph):
+    from pde.fluid import Fluid2DModel
+    cfg = _cfg("fluid", num_hidden_layers=4, hidden_features=128, sample_resolution=32, dt=0.05)
+    model = Fluid2DModel(cfg)
+    T = lambda k: torch.from_numpy(ph[k]).cuda()  # noqa: E731
+    nets = {"vel": model.velocity_field, "vel_prev": model.velocity_field_prev, "pres": model.pressure_field}
+
+    def reset():
+        for k, n in nets.items():
+            set_flat(n, ph[f"fluid/{k}/params0"])
+
+    def patch(it):
+        model._sample_in_training = lambda: T(f"fluid/x{it}").clone().requires_grad_(True)
+        model._boundary_pair = lambda n: (T(f"fluid/bcx{it}").clone().requires_grad_(True),
+                                          T(f"fluid/bcy{it}").clone().requires_grad_(True))
+
+    for phase in ("_advect_velocity", "_solve_pressure", "_projection"):
+        body = getattr(Fluid2DModel, phase)._insr_phase
+        reset()
+        patch(0)
+        model._reset_optimizer()
+        ld = body(model)
+        for k, v in ld.items():
+            ref = float(ph[f"fluid/{phase}/loss_{k}"])
+            assert abs(float(v) - ref) <= TOL * abs(ref) + 1e-12, (phase, k, float(v), ref)
+        model.optimizer.zero_grad()
+        sum(ld.values()).backward()
+        assert nerr(flat_grad(model.velocity_field), ph[f"fluid/{phase}/grad_vel"]) < TOL, phase
+        gp = ph[f"fluid/{phase}/grad_pres"]
+        if np.abs(gp).max() > 0:
+            assert nerr(flat_grad(model.pressure_field), gp) < TOL, phase
+        else:
+            assert not model.pressure_field.grad_touched()
+        # two reference iterations: phase + _update_network (Adam + plateau)
+        reset()
+        model._reset_optimizer()
+        trace = []
+        for it in range(2):
+            patch(it)
+            ld = body(model)
+            model._update_network(ld)
+            trace.append([float(ld[k]) for k in sorted(ld)])
+        assert nerr(np.array(trace), ph[f"fluid/{phase}/loss_trace"]) < TOL
+        check_update(flat(model.velocity_field), ph["fluid/vel/params0"], ph[f"fluid/{phase}/vel_after"],
+                     ph[f"fluid/{phase}/grad_vel"])
+        if np.abs(gp).max() > 0:
+            check_update(flat(model.pressure_field), ph["fluid/pres/params0"], ph[f"fluid/{phase}/pres_after"], gp)
+        else:
+            assert np.array_equal(flat(model.pressure_field), ph["fluid/pres/params0"])
+
+
+def test_advect_phase(ph):
+    import pde.advection as adv
+    cfg = _cfg("advection", num_hidden_layers=3, hidden_features=64, sample_resolution=512, dt=0.05, vel=0.25,
+               length=4.0)
+    model = adv.Advection1DModel(cfg)
+    set_flat(model.field, ph["advect/field/params0"])
+    set_flat(model.field_prev, ph["advect/field_prev/params0"])
+    T = lambda k: torch.from_numpy(ph[k]).cuda()  # noqa: E731
+    orig = adv.sample_boundary
+
+    def patch(it):
+        model._sample_in_training = lambda: T(f"advect/x{it}").clone().requires_grad_(True)
+        adv.sample_boundary = lambda n, sdim, device=None, **k: T(f"advect/bc{it}") / 2.0
+
+    try:
+        body = adv.Advection1DModel._advect._insr_phase
+        patch(0)
+        model._reset_optimizer()
+        ld = body(model)
+        for k, v in ld.items():
+            ref = float(ph[f"advect/_advect/loss_{k}"])
+            assert abs(float(v) - ref) <= TOL * abs(ref) + 1e-12, (k, float(v), ref)
+        model.optimizer.zero_grad()
+        sum(ld.values()).backward()
+        assert nerr(flat_grad(model.field), ph["advect/_advect/grad_field"]) < TOL
+        set_flat(model.field, ph["advect/field/params0"])
+        model._reset_optimizer()
+        trace = []
+        for it in range(2):
+            patch(it)
+            ld = body(model)
+            model._update_network(ld)
+            trace.append([float(ld[k]) for k in sorted(ld)])
+        assert nerr(np.array(trace), ph["advect/_advect/loss_trace"]) < TOL
+        check_update(flat(model.field), ph["advect/field/params0"], ph["advect/_advect/field_after"],
+                     ph["advect/_advect/grad_field"])
+    finally:
+        adv.sample_boundary = orig
+
+
+def test_elasticity_phase(ph):
+    from pde.elasticity import ElasticityModel
+    energy = [str(e) for e in ph["el2d/cfg_energy"]]
+    cfg = _cfg("elasticity", num_hidden_layers=5, hidden_features=128, sample_resolution=16, dt=0.1, dim=2,
+               energy=energy, ratio_constraint=1e4, ratio_volume=1e3, ratio_arap=1.0, ratio_collide=1e2,
+               ratio_kinematics=1.0, external_force_timesteps=5, external_force_y=-1.0,
+               constraint_right_offset_x=2.0, plane_height=-0.9)
+    model = ElasticityModel(cfg)
+    model.timestep = 1
+    for k, n in (("f", model.deformation_field), ("f_prev", model.deformation_field_prev),
+                 ("f_pp", model.deformation_field_prev_prev)):
+        set_flat(n, ph[f"el2d/{k}/params0"])
+    T = lambda k: torch.from_numpy(ph[k]).cuda()  # noqa: E731
+
+    def patch(it):
+        model._sample_in_training = lambda res: T(f"el2d/x{it}").clone().requires_grad_(True)
+        model._sample_fixed_in_training = lambda res: (T(f"el2d/fixed_l{it}").clone().requires_grad_(True),
+                                                       T(f"el2d/fixed_r{it}").clone().requires_grad_(True))
+
+    body = ElasticityModel._solve_deformation._insr_phase
+    patch(0)
+    model._reset_optimizer()
+    ld = body(model)
+    ref = float(ph["el2d/_solve_deformation/loss_main"])
+    assert abs(float(ld["main"]) - ref) <= TOL * abs(ref)
+    model.optimizer.zero_grad()
+    ld["main"].backward()
+    assert nerr(flat_grad(model.deformation_field), ph["el2d/_solve_deformation/grad_f"]) < TOL
+    set_flat(model.deformation_field, ph["el2d/f/params0"])
+    model._reset_optimizer()
+    trace = []
+    for it in range(2):
+        patch(it)
+        ld = body(model)
+        model._update_network(ld)
+        trace.append([float(ld[k]) for k in sorted(ld)])
+    assert nerr(np.array(trace), ph["el2d/_solve_deformation/loss_trace"]) < TOL
+    check_update(flat(model.deformation_field), ph["el2d/f/params0"], ph["el2d/_solve_deformation/f_after"],
+                 ph["el2d/_solve_deformation/grad_f"])
+
+
+def test_training_loop_graph_matches_eager(ph):
+    """insr_graph=True (hipGraph replay) gives the same trajectory as eager execution."""
+    from pde.fluid import Fluid2DModel
+    res = {}
+    for graph in (False, True):
+        torch.manual_seed(0)
+        cfg = _cfg("fluid", num_hidden_layers=4, hidden_features=128, sample_resolution=32, max_n_iters=6,
+                   insr_graph=graph, insr_sync_every=3)
+        model = Fluid2DModel(cfg)
+        set_flat(model.velocity_field, ph["fluid/vel/params0"])
+        set_flat(model.velocity_field_prev, ph["fluid/vel_prev/params0"])
+        set_flat(model.pressure_field, ph["fluid/pres/params0"])
+        xs = [torch.from_numpy(ph["fluid/x0"]).cuda(), torch.from_numpy(ph["fluid/x1"]).cuda()]
+        static_x = xs[0].clone()
+        static_bx = torch.from_numpy(ph["fluid/bcx0"]).cuda()
+        static_by = torch.from_numpy(ph["fluid/bcy0"]).cuda()
+        model._sample_in_training = lambda: static_x.clone().requires_grad_(True)
+        model._boundary_pair = lambda n: (static_bx.clone().requires_grad_(True), static_by.clone().requires_grad_(True))
+        model.timestep = 1
+        model._solve_pressure()
+        res[graph] = (flat(model.pressure_field), float(model.optimizer.state[0]),
+                      float(model.optimizer.state[1]))
+    assert res[True][2] == res[False][2] == 6.0
+    assert nerr(res[True][0], res[False][0]) < 1e-6

@@ -1,0 +1,26 @@
+#!/bin/bash
+# One GPU-box session: parity tests -> bench -> rocprofv3 kernel stats.
+# Stops at the first GPU fault / abort / segfault / timeout (exit 124,134,137,139 or >128).
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+OUT=gpurun_out/${SESSION:-s}
+mkdir -p "$OUT"
+fatal() { [ "$1" -ge 124 ] && { echo "FATAL step exit $1 -- stopping" | tee -a "$OUT/status.log"; exit "$1"; }; return 0; }
+step() {  # name timeout cmd...
+  local name=$1 to=$2; shift 2
+  echo "== $name: $*" >> "$OUT/status.log"
+  timeout -k 10 "$to" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "   $name exit $rc" >> "$OUT/status.log"
+  fatal $rc
+  return 0
+}
+for s in ${STEPS:-tests bench prof}; do
+  case $s in
+    tests) step tests 500 python -m pytest tests -q -m gpu -x ;;
+    smoke) step smoke 200 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) step bench 400 python bench.py --steps ${BSTEPS:-20} --warmup 3 ;;
+    prof)  export TMPDIR=/tmp; step prof 400 rocprofv3 --kernel-trace --stats -d "$PWD/$OUT/prof" -o run --output-format csv -- python bench.py --steps 10 --warmup 3 --no-cpu-baseline ;;
+  esac
+done
+echo done >> "$OUT/status.log"
