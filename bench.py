@@ -33,6 +33,13 @@ FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md chip table: dense fp32 matr
 HBM_PEAK_GBS = 8000.0
 
 
+T0 = time.time()
+
+
+def log(msg):
+    print(f"[bench {time.time() - T0:7.2f}s] {msg}", file=sys.stderr, flush=True)
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -117,7 +124,8 @@ def roofline(model, loops, n_local, P_pres):
         agg.setdefault(key, []).append(e0.elapsed_time(e1))
     _jet.TIMING["events"].clear()
     per_step = {k: sum(v) / reps for k, v in agg.items()}
-    dom = max(per_step, key=per_step.get)
+    # dominant kernel = the longest launch over the interior batch (the bc bands are 1% of points)
+    dom = max((k for k in per_step if k[2] == n_local and k[0] != "reduce"), key=lambda k: sum(agg[k]) / len(agg[k]))
     kind, mode, n, W = dom
     ms = sum(agg[dom]) / len(agg[dom])
     # algorithmic flops per launch: 2P per point per stream per GEMM pass
@@ -136,7 +144,8 @@ def roofline(model, loops, n_local, P_pres):
 def cpu_baseline(seconds):
     """The oracle (torch-CPU restatement of the reference graph) on this host's cores."""
     from oracle import siren_oracle as O
-    cores = len(os.sched_getaffinity(0))
+    # the box exports OMP_NUM_THREADS = its CPU share; affinity may list the whole host
+    cores = min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "1024")))
     torch.set_num_threads(cores)
     torch.manual_seed(0)
     vel, vel_prev, pres = O.OracleSiren(2, 2, 4, 128), O.OracleSiren(2, 2, 4, 128), O.OracleSiren(2, 1, 4, 128)
@@ -175,11 +184,16 @@ def cpu_baseline(seconds):
 def main():
     args = parse()
     world, rank, local = setup_dist(args)
+    log(f"world={world} rank={rank}")
     model, cfg = build_model(args, world)
     n_local = model._n_interior()
     loops = phase_loops(model)
+    log(f"model built, {n_local} points per rank per phase")
     for i in range(args.warmup):  # iteration 0 eager, iteration 1 captured (warm-up)
         run_steps(loops, i, 1)
+        torch.cuda.synchronize()
+        log(f"warmup step {i} done" + "".join(f" [{pl.tag}: capture failed {pl.capture_error}]"
+                                              for pl in loops if getattr(pl, "capture_error", None)))
     sync_all(world)
     t0 = time.perf_counter()
     run_steps(loops, args.warmup, args.steps)
@@ -189,6 +203,7 @@ def main():
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t)
+    log(f"timed {args.steps} steps: {elapsed * 1e3:.2f} ms")
     total_points = n_local * world * 3 * args.steps
     value = total_points / elapsed
     result = {
@@ -204,8 +219,10 @@ def main():
     if rank == 0 and not args.no_roofline:
         P_pres = 2 * 128 + 4 * 128 * 128 + 128 * 1  # d_in W + L W^2 + W d_out
         result["roofline"] = roofline(model, loops, n_local, P_pres)
+        log("roofline done")
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+        log("cpu baseline done")
         result["speedup_vs_cpu_baseline"] = round(value / result["cpu_baseline"]["value"], 1)
     if rank == 0:
         print(json.dumps(result), flush=True)

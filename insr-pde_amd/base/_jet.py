@@ -16,8 +16,6 @@ Recognised shapes of `y` (everything the reference models use):
   * y = gradient(mlp(x), x)  inside divergence  (-> Laplacian stream)
 Anything else raises UnsupportedPattern (there is no silent fallback).
 """
-import weakref
-
 import torch
 from torch.autograd.function import once_differentiable
 
@@ -155,33 +153,16 @@ def run_jet(mlp, x, mode):
     return y, dy, lap
 
 
-# value tensors by the id of their autograd node (validated on lookup: no stale ids)
-_VALUES = {}
-
-
-def _register_value(y):
-    node = y.grad_fn
-    if node is None:
-        return
-    if len(_VALUES) > 4096:
-        for k in [k for k, r in _VALUES.items() if r() is None]:
-            del _VALUES[k]
-    _VALUES[id(node)] = weakref.ref(y)
-
-
-def _value_of_node(node):
-    r = _VALUES.get(id(node))
-    y = r() if r is not None else None
-    if y is not None and y.grad_fn is node:
-        return y
-    return None
-
-
 def siren_value(mlp, x):
+    """MLP.forward.  Provenance lives on the tensor AND on its autograd node, because
+    in `q = mlp(x) + x` the value tensor itself is a dropped temporary; only the node
+    survives inside q's graph."""
     y, _, _ = run_jet(mlp, x, nat.MODE_VALUE)
-    y._insr_src = (mlp, x)
-    y._insr_jets = {}
-    _register_value(y)
+    jets = {}
+    y._insr_src, y._insr_jets = (mlp, x), jets
+    node = y.grad_fn
+    if node is not None:
+        node._insr_src, node._insr_jets = (mlp, x), jets
     return y
 
 
@@ -197,8 +178,9 @@ def _grad_edge_node(t):
 
 
 def match(y, x):
-    """Return (mlp, value_tensor, affine) if y is a recognised function of x, else None.
+    """Return (mlp, holder, affine) if y is a recognised function of x, else None.
 
+    holder carries the jet cache (the value tensor or its autograd node);
     affine=True means y = mlp(x) + x (the identity is added to the Jacobian).
     """
     src = getattr(y, "_insr_src", None)
@@ -215,15 +197,15 @@ def match(y, x):
         return None
     for a, b in ((0, 1), (1, 0)):
         if nodes[b] is xnode and nodes[a] is not None:
-            v = _value_of_node(nodes[a])
-            if v is not None and v._insr_src[1] is x and v.shape == x.shape:
-                return v._insr_src[0], v, True
+            src = getattr(nodes[a], "_insr_src", None)
+            if src is not None and src[1] is x and src[0].out_features == x.shape[-1]:
+                return src[0], nodes[a], True
     return None
 
 
-def jet_of(mlp, value, x, mode):
-    """Derivative jets are cached on the value tensor; a LAP jet also serves GRAD."""
-    cache = getattr(value, "_insr_jets", None)
+def jet_of(mlp, holder, x, mode):
+    """Derivative jets are cached on the value tensor / node; a LAP jet also serves GRAD."""
+    cache = getattr(holder, "_insr_jets", None)
     if cache is not None:
         for m in ((nat.MODE_LAP,) if mode == nat.MODE_LAP else (nat.MODE_GRAD, nat.MODE_LAP)):
             if m in cache:

@@ -91,12 +91,16 @@ def test_fluid_phases(ph):
             assert abs(float(v) - ref) <= TOL * abs(ref) + 1e-12, (phase, k, float(v), ref)
         model.optimizer.zero_grad()
         sum(ld.values()).backward()
-        assert nerr(flat_grad(model.velocity_field), ph[f"fluid/{phase}/grad_vel"]) < TOL, phase
+        gv = ph[f"fluid/{phase}/grad_vel"]
+        if np.abs(gv).max() > 0:
+            assert nerr(flat_grad(model.velocity_field), gv) < TOL, phase
         gp = ph[f"fluid/{phase}/grad_pres"]
         if np.abs(gp).max() > 0:
             assert nerr(flat_grad(model.pressure_field), gp) < TOL, phase
         else:
             assert not model.pressure_field.grad_touched()
+        if np.abs(ph[f"fluid/{phase}/grad_vel"]).max() == 0:
+            assert not model.velocity_field.grad_touched()
         # two reference iterations: phase + _update_network (Adam + plateau)
         reset()
         model._reset_optimizer()
@@ -107,12 +111,12 @@ def test_fluid_phases(ph):
             model._update_network(ld)
             trace.append([float(ld[k]) for k in sorted(ld)])
         assert nerr(np.array(trace), ph[f"fluid/{phase}/loss_trace"]) < TOL
-        check_update(flat(model.velocity_field), ph["fluid/vel/params0"], ph[f"fluid/{phase}/vel_after"],
-                     ph[f"fluid/{phase}/grad_vel"])
-        if np.abs(gp).max() > 0:
-            check_update(flat(model.pressure_field), ph["fluid/pres/params0"], ph[f"fluid/{phase}/pres_after"], gp)
-        else:
-            assert np.array_equal(flat(model.pressure_field), ph["fluid/pres/params0"])
+        for key, net, g_ref in (("vel", model.velocity_field, ph[f"fluid/{phase}/grad_vel"]),
+                                ("pres", model.pressure_field, gp)):
+            if np.abs(g_ref).max() > 0:
+                check_update(flat(net), ph[f"fluid/{key}/params0"], ph[f"fluid/{phase}/{key}_after"], g_ref)
+            else:  # no gradient reaches this network in this phase: torch skips it, so do we
+                assert np.array_equal(flat(net), ph[f"fluid/{key}/params0"])
 
 
 def test_advect_phase(ph):
