@@ -118,14 +118,23 @@ int insr_reduce_partials(const float* partial, int n_blocks, long count, float* 
 #define INSR_OPT_MINLR 7
 #define INSR_OPT_NFLOATS 8
 
-/* t += 1; refresh step_size and sqrt(1-b2^t) (torch.optim.Adam bias correction). */
+/* t += 1; refresh step_size and sqrt(1-b2^t) (explicit-prepare convention). */
 int insr_adam_prepare(float* opt_state, float beta1, float beta2, void* stream);
 
 /* One ReduceLROnPlateau.step(*loss) (mode min, rel threshold 1e-4, cooldown 0,
- * eps 1e-8), base/baseModel.py:61-62,80-81. */
-int insr_plateau_step(float* opt_state, const float* loss, int patience, void* stream);
+ * eps 1e-8), base/baseModel.py:61-62,80-81.  advance_step != 0 also does t += 1
+ * (the fused-Adam convention: the update of iteration t used st[STEP] + 1).
+ * loss == NULL with advance_step != 0 only advances t. */
+int insr_plateau_step(float* opt_state, const float* loss, int patience, int advance_step, void* stream);
 
-/* p -= step_size * m / (sqrt(v)/bc2sqrt + eps) after m,v moments (torch order). */
+/* Adam over up to INSR_ADAM_MAX_TENSORS flat buffers in ONE launch (torch op order).
+ * Bias corrections use t = opt_state[STEP] + step_offset. */
+#define INSR_ADAM_MAX_TENSORS 8
+int insr_adam_step_multi(int count, float* const* params, const float* const* grads, float* const* exp_avg,
+                         float* const* exp_avg_sq, const long* sizes, const float* opt_state, float beta1,
+                         float beta2, float eps, int step_offset, void* stream);
+
+/* Single-buffer Adam, explicit-prepare convention (t = opt_state[STEP]). */
 int insr_adam_step(float* params, const float* grads, float* exp_avg, float* exp_avg_sq,
                    long count, const float* opt_state, float beta1, float beta2, float eps,
                    void* stream);

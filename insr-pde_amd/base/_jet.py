@@ -89,6 +89,7 @@ class _SirenJet(torch.autograd.Function):
             rc = lib.insr_siren_jet_fwd(nat.ptr(x2), n, din, dout, L, W, mode, nat.ptr(flat), nat.ptr(y),
                                         nat.ptr(dy), nat.ptr(lap), nat.ptr(act), nat.stream_of(dev))
         nat.check(rc, "insr_siren_jet_fwd")
+        ctx.set_materialize_grads(False)  # unused outputs -> None -> NULL adjoint (no zero-fill launch)
         ctx.mode, ctx.mlp, ctx.save = mode, mlp, save
         ctx.x2, ctx.act = x2, act
         outs = [y]
@@ -108,6 +109,8 @@ class _SirenJet(torch.autograd.Function):
         gy = grads[0]
         gdy = grads[1] if mode != nat.MODE_VALUE else None
         glap = grads[2] if mode == nat.MODE_LAP else None
+        if gy is None and gdy is None and glap is None:
+            return none
         x2, act = ctx.x2, ctx.act
         n, din = x2.shape
         L, W, dout = mlp.num_hidden_layers, mlp.hidden_features, mlp.out_features
@@ -115,7 +118,7 @@ class _SirenJet(torch.autograd.Function):
         part = torch.empty(max(lib.insr_jet_partial_bytes(n, din, dout, L, W) // 4, 1), device=x2.device,
                            dtype=torch.float32)
         gflat, accumulate = mlp.grad_for_backward()
-        c = lambda t: None if t is None else t.contiguous()  # noqa: E731
+        c = lambda t: None if t is None else (t if t.is_contiguous() else t.contiguous())  # noqa: E731
         gy, gdy, glap = c(gy), c(gdy), c(glap)
         st = nat.stream_of(x2.device)
         with _timed("bwd", mode, n, W):

@@ -16,6 +16,7 @@ LIB_PATH = os.environ.get("INSR_HIP_LIB", os.path.join(os.path.dirname(_HERE), "
 MODE_VALUE, MODE_GRAD, MODE_LAP = 0, 1, 2
 OPT_LR, OPT_STEP, OPT_BEST, OPT_BAD, OPT_STEPSIZE, OPT_BC2SQRT, OPT_FACTOR, OPT_MINLR = range(8)
 OPT_NFLOATS = 8
+ADAM_MAX_TENSORS = 8
 
 _P = ctypes.c_void_p
 _I = ctypes.c_int
@@ -34,7 +35,8 @@ SIGNATURES = {
     "insr_jet_partial_blocks": (_I, [_L]),
     "insr_reduce_partials": (_I, [_P, _I, _L, _P, _I, _P]),
     "insr_adam_prepare": (_I, [_P, _F, _F, _P]),
-    "insr_plateau_step": (_I, [_P, _P, _I, _P]),
+    "insr_plateau_step": (_I, [_P, _P, _I, _I, _P]),
+    "insr_adam_step_multi": (_I, [_I, _P, _P, _P, _P, _P, _P, _F, _F, _F, _I, _P]),
     "insr_adam_step": (_I, [_P, _P, _P, _P, _L, _P, _F, _F, _F, _P]),
 }
 

@@ -40,7 +40,8 @@ def gradient(y, x, grad_outputs=None):
     mlp, value, affine = _resolve(y, x, "gradient")
     _, J, _ = _jet.jet_of(mlp, value, x, nat.MODE_GRAD)  # (..., dout, din)
     if grad_outputs is None:
-        g = J.sum(dim=-2)
+        # scalar net: a view (no launch, and its backward is a view too)
+        g = J.squeeze(-2) if J.shape[-2] == 1 else J.sum(dim=-2)
         if affine:
             g = g + 1.0
     else:
@@ -61,11 +62,16 @@ def divergence(y, x):
         if not unit:
             raise _jet.UnsupportedPattern("divergence of a weighted gradient is not fused")
         _, _, lap = _jet.jet_of(mlp, value, x, nat.MODE_LAP)
-        return lap.sum(dim=-1, keepdim=True)
+        return lap if lap.shape[-1] == 1 else lap.sum(dim=-1, keepdim=True)
     mlp, value, affine = r
     _, J, _ = _jet.jet_of(mlp, value, x, nat.MODE_GRAD)
     k = min(J.shape[-2], J.shape[-1])
-    div = torch.diagonal(J[..., :k, :k], dim1=-2, dim2=-1).sum(dim=-1, keepdim=True)
+    if k == 1:
+        div = J[..., 0, :1]
+    elif k == 2:  # one fused add instead of diagonal + reduction
+        div = J[..., 0, 0:1] + J[..., 1, 1:2]
+    else:
+        div = torch.diagonal(J[..., :k, :k], dim1=-2, dim2=-1).sum(dim=-1, keepdim=True)
     if affine:
         div = div + float(k)
     return div
@@ -77,9 +83,10 @@ def laplace(y, x, normalize=False, eps=0., return_grad=False):
         raise _jet.UnsupportedPattern("laplace(normalize=True) is not on the INSR-PDE path")
     mlp, value, affine = _resolve(y, x, "laplace")
     _, J, lap = _jet.jet_of(mlp, value, x, nat.MODE_LAP)
-    div = lap.sum(dim=-1, keepdim=True)  # the identity part of f(x)+x has zero Laplacian
+    # the identity part of f(x)+x has zero Laplacian; a scalar net needs no reduction launch
+    div = lap if lap.shape[-1] == 1 else lap.sum(dim=-1, keepdim=True)
     if return_grad:
-        g = J.sum(dim=-2)
+        g = J.squeeze(-2) if J.shape[-2] == 1 else J.sum(dim=-2)
         if affine:
             g = g + 1.0
         return div, g

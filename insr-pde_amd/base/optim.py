@@ -6,8 +6,9 @@ network, lr = cfg.lr) and ReduceLROnPlateau(factor=0.1, patience=500,
 min_lr=1e-8).  lr, step count and plateau state live in one small device
 tensor, so an iteration needs no host round trip (hipGraph-replayable):
 
-    prepare (t += 1, bias corrections)  -> one Adam launch per network's flat
-    buffer -> plateau step on the device-resident loss.
+    ONE multi-tensor Adam launch over every network's flat buffer (bias
+    corrections computed in-kernel from t + 1) -> ONE plateau launch that also
+    advances t.
 
 Reading `param_groups[i]['lr']` synchronises (as the reference's early-stop
 check does, base/baseModel.py:132).
@@ -69,6 +70,7 @@ class FusedAdam:
         self.state[nat.OPT_BEST] = math.inf
         self.state[nat.OPT_FACTOR] = 0.1
         self.state[nat.OPT_MINLR] = 0.0
+        self._pending_advance = False
 
     @property
     def lr(self):
@@ -84,24 +86,38 @@ class FusedAdam:
                 else:
                     p.grad.zero_()
 
+    def _advance_pending(self):
+        """t += 1 for a step() whose scheduler step never came (no scheduler / repeat step)."""
+        if self._pending_advance:
+            nat.check(nat.lib().insr_plateau_step(nat.ptr(self.state), None, 0, 1, nat.stream_of(self.device)),
+                      "insr_plateau_step(advance)")
+            self._pending_advance = False
+
     @torch.no_grad()
     def step(self):
+        """One Adam update of every buffer whose grad exists, in ONE launch.
+        Uses t = state[STEP] + 1; the step counter itself is advanced by the
+        scheduler's plateau launch that follows (or lazily, without one)."""
+        import ctypes
         lib = nat.lib()
+        self._advance_pending()
+        bufs = []
+        for mlp, m, v in self._nets:
+            if mlp.grad_touched():  # torch skips params whose .grad is None
+                bufs.append((mlp.flat_params(), mlp.flat_grad_buffer(), m, v))
+        for p, m, v in self._loose:
+            if p.grad is not None:
+                bufs.append((p.data, p.grad if p.grad.is_contiguous() else p.grad.contiguous(), m, v))
         b1, b2 = self.betas
         st = nat.stream_of(self.device)
-        nat.check(lib.insr_adam_prepare(nat.ptr(self.state), b1, b2, st), "insr_adam_prepare")
-        for mlp, m, v in self._nets:
-            if not mlp.grad_touched():
-                continue  # torch skips params whose .grad is None
-            flat, g = mlp.flat_params(), mlp.flat_grad_buffer()
-            nat.check(lib.insr_adam_step(nat.ptr(flat), nat.ptr(g), nat.ptr(m), nat.ptr(v), flat.numel(),
-                                         nat.ptr(self.state), b1, b2, self.eps, st), "insr_adam_step")
-        for p, m, v in self._loose:
-            if p.grad is None:
-                continue
-            g = p.grad.contiguous()
-            nat.check(lib.insr_adam_step(nat.ptr(p.data), nat.ptr(g), nat.ptr(m), nat.ptr(v), p.numel(),
-                                         nat.ptr(self.state), b1, b2, self.eps, st), "insr_adam_step")
+        for i in range(0, len(bufs), nat.ADAM_MAX_TENSORS):
+            chunk = bufs[i:i + nat.ADAM_MAX_TENSORS]
+            k = len(chunk)
+            arr = lambda j: (ctypes.c_void_p * k)(*[c[j].data_ptr() for c in chunk])  # noqa: E731
+            sizes = (ctypes.c_long * k)(*[c[0].numel() for c in chunk])
+            nat.check(lib.insr_adam_step_multi(k, arr(0), arr(1), arr(2), arr(3), sizes, nat.ptr(self.state), b1, b2,
+                                               self.eps, 1, st), "insr_adam_step_multi")
+        self._pending_advance = True
 
 
 class DevicePlateau:
@@ -123,5 +139,8 @@ class DevicePlateau:
         else:
             self._scratch.fill_(float(metrics))
             m = self._scratch
-        nat.check(nat.lib().insr_plateau_step(nat.ptr(self.optimizer.state), nat.ptr(m), self.patience,
-                                              nat.stream_of(self.optimizer.device)), "insr_plateau_step")
+        opt = self.optimizer
+        adv = 1 if opt._pending_advance else 0
+        nat.check(nat.lib().insr_plateau_step(nat.ptr(opt.state), nat.ptr(m), self.patience, adv,
+                                              nat.stream_of(opt.device)), "insr_plateau_step")
+        opt._pending_advance = False

@@ -83,17 +83,58 @@ __device__ __forceinline__ float sum16(float v) {
 }
 
 // ---------------------------------------------------------------------------
+// sin / cos of w*z.  Straight-line Cody-Waite reduction by pi/2 (3-part constant,
+// valid for |x| <= 8192) + minimax polynomials on [-pi/4, pi/4]: ~1 ulp, ~20 VALU
+// ops for the pair, no branches, so the compiler can interleave it with MFMAs.
+// A wave with any |x| > 8192 takes the libm (ocml) path instead (uniform branch).
+// ---------------------------------------------------------------------------
+constexpr float kFastArgMax = 8192.0f;
+
+__device__ __forceinline__ void sincos_fast(float x, float& s, float& c) {
+  const float n = rintf(x * 0.636619772367581343f);
+  float r = fmaf(-n, 1.5703125f, x);
+  r = fmaf(-n, 4.837512969970703125e-4f, r);
+  r = fmaf(-n, 7.54978995489188216e-8f, r);
+  const float z = r * r;
+  const float ps = fmaf(r * z, fmaf(z, fmaf(z, -1.9515295891e-4f, 8.3321608736e-3f), -1.6666654611e-1f), r);
+  const float pc = fmaf(z * z, fmaf(z, fmaf(z, 2.443315711809948e-5f, -1.388731625493765e-3f),
+                                    4.166664568298827e-2f), fmaf(-0.5f, z, 1.0f));
+  const int q = (int)n;
+  const float a = (q & 1) ? pc : ps;   // |sin|
+  const float b = (q & 1) ? ps : pc;   // |cos|
+  s = (q & 2) ? -a : a;
+  c = ((q + 1) & 2) ? -b : b;
+}
+
+__device__ __forceinline__ float sin_fast(float x) {
+  float s, c;
+  sincos_fast(x, s, c);
+  return s;
+}
+
+// true if any lane of the wave holds an argument outside the fast range
+__device__ __forceinline__ bool wave_any_big(float amax) {
+  return __any(amax > kFastArgMax);
+}
+
+// ---------------------------------------------------------------------------
 // forward jet
 // ---------------------------------------------------------------------------
-template <int NT, int S, bool LAP>
-__device__ __forceinline__ void sine_jet(floatx4 (&a)[NT][S]) {
+template <int NT, int S, bool LAP, bool FAST>
+__device__ __forceinline__ void sine_jet_impl(floatx4 (&a)[NT][S]) {
   constexpr int NTAN = LAP ? S - 2 : S - 1;
 #pragma unroll
   for (int rt = 0; rt < NT; ++rt) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
+      const float arg = OMEGA * a[rt][0][r];
       float sn, cs;
-      sincosf(OMEGA * a[rt][0][r], &sn, &cs);
+      if constexpr (S == 1) {  // value-only jet: sin is all we need
+        if constexpr (FAST) sn = sin_fast(arg); else sn = sinf(arg);
+        a[rt][0][r] = sn;
+        continue;
+      }
+      if constexpr (FAST) sincos_fast(arg, sn, cs); else sincosf(arg, &sn, &cs);
       const float wc = OMEGA * cs;
       if constexpr (LAP) {
         float t2 = 0.f;
@@ -106,6 +147,19 @@ __device__ __forceinline__ void sine_jet(floatx4 (&a)[NT][S]) {
       a[rt][0][r] = sn;
     }
   }
+}
+
+template <int NT, int S, bool LAP>
+__device__ __forceinline__ void sine_jet(floatx4 (&a)[NT][S]) {
+  float amax = 0.f;
+#pragma unroll
+  for (int rt = 0; rt < NT; ++rt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) amax = fmaxf(amax, fabsf(OMEGA * a[rt][0][r]));
+  if (wave_any_big(amax))
+    sine_jet_impl<NT, S, LAP, false>(a);
+  else
+    sine_jet_impl<NT, S, LAP, true>(a);
 }
 
 template <int NT, int S>
@@ -256,13 +310,24 @@ __device__ __forceinline__ void sine_rev(floatx4 (&hb)[S], const floatx4 (&zs)[S
 template <int NT>
 __device__ __forceinline__ void load_z_sincos(const float* base, int S, int lane, floatx4 (&sn)[NT],
                                               floatx4 (&cs)[NT]) {
+  floatx4 z[NT];
+  float amax = 0.f;
 #pragma unroll
   for (int rt = 0; rt < NT; ++rt) {
-    const floatx4 z = *reinterpret_cast<const floatx4*>(base + (rt * 64 + lane) * 4);
+    z[rt] = *reinterpret_cast<const floatx4*>(base + (rt * 64 + lane) * 4);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) amax = fmaxf(amax, fabsf(OMEGA * z[rt][r]));
+  }
+  const bool big = wave_any_big(amax);
+#pragma unroll
+  for (int rt = 0; rt < NT; ++rt) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       float a, b;
-      sincosf(OMEGA * z[r], &a, &b);
+      if (big)
+        sincosf(OMEGA * z[rt][r], &a, &b);
+      else
+        sincos_fast(OMEGA * z[rt][r], a, b);
       sn[rt][r] = a;
       cs[rt][r] = b;
     }
@@ -562,18 +627,19 @@ __global__ __launch_bounds__(64 * kRedWaves) void reduce_partials_kernel(const f
 }
 
 __global__ void adam_prepare_kernel(float* st, float b1, float b2) {
+  // legacy explicit prepare: t += 1 and refresh the bias-corrected scalars
   if (threadIdx.x == 0 && blockIdx.x == 0) {
     const double t = (double)st[INSR_OPT_STEP] + 1.0;
     st[INSR_OPT_STEP] = (float)t;
-    const double bc1 = 1.0 - pow((double)b1, t);
-    const double bc2 = 1.0 - pow((double)b2, t);
-    st[INSR_OPT_STEPSIZE] = (float)((double)st[INSR_OPT_LR] / bc1);
-    st[INSR_OPT_BC2SQRT] = (float)sqrt(bc2);
+    st[INSR_OPT_STEPSIZE] = (float)((double)st[INSR_OPT_LR] / (1.0 - pow((double)b1, t)));
+    st[INSR_OPT_BC2SQRT] = (float)sqrt(1.0 - pow((double)b2, t));
   }
 }
 
-__global__ void plateau_kernel(float* st, const float* loss, int patience) {
+__global__ void plateau_kernel(float* st, const float* loss, int patience, int advance_step) {
   if (threadIdx.x == 0 && blockIdx.x == 0) {
+    if (advance_step) st[INSR_OPT_STEP] = st[INSR_OPT_STEP] + 1.f;
+    if (!loss) return;  // advance-only (optimiser without a scheduler)
     const float cur = *loss;
     float best = st[INSR_OPT_BEST];
     float bad = st[INSR_OPT_BAD];
@@ -596,21 +662,46 @@ __global__ void plateau_kernel(float* st, const float* loss, int patience) {
   }
 }
 
-__global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
-                            float* __restrict__ v, long n, const float* __restrict__ st, float b1, float b2,
-                            float eps) {
-  const float step_size = st[INSR_OPT_STEPSIZE];
-  const float bc2s = st[INSR_OPT_BC2SQRT];
+struct AdamList {
+  float* p[INSR_ADAM_MAX_TENSORS];
+  const float* g[INSR_ADAM_MAX_TENSORS];
+  float* m[INSR_ADAM_MAX_TENSORS];
+  float* v[INSR_ADAM_MAX_TENSORS];
+  long n[INSR_ADAM_MAX_TENSORS];
+  long start[INSR_ADAM_MAX_TENSORS + 1];  // prefix sums of n
+  int count;
+};
+
+// One launch over up to INSR_ADAM_MAX_TENSORS flat buffers.  The step t used is
+// st[STEP] + step_offset (the plateau kernel advances st[STEP] after the update,
+// so the bias corrections need no separate prepare launch); torch's op order:
+//   m.lerp_(g, 1-b1); v.mul_(b2).addcmul_(g, g, 1-b2);
+//   p.addcdiv_(m, sqrt(v)/sqrt(1-b2^t) + eps, -lr/(1-b1^t))
+__global__ void adam_multi_kernel(AdamList L, const float* __restrict__ st, float b1, float b2, float eps,
+                                  int step_offset) {
+  __shared__ float sc[2];
+  if (threadIdx.x == 0) {
+    const double t = (double)st[INSR_OPT_STEP] + (double)step_offset;
+    sc[0] = (float)((double)st[INSR_OPT_LR] / (1.0 - pow((double)b1, t)));
+    sc[1] = (float)sqrt(1.0 - pow((double)b2, t));
+  }
+  __syncthreads();
+  const float step_size = sc[0], bc2s = sc[1];
   const float w1 = (float)(1.0 - (double)b1);
   const float w2 = (float)(1.0 - (double)b2);
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
-    const float gi = g[i];
-    const float mi = m[i] + w1 * (gi - m[i]);          // lerp_(g, 1-b1)
-    const float vi = v[i] * b2 + w2 * gi * gi;          // mul_(b2).addcmul_(g, g, 1-b2)
-    m[i] = mi;
-    v[i] = vi;
+  const long total = L.start[L.count];
+  for (long gi = (long)blockIdx.x * blockDim.x + threadIdx.x; gi < total; gi += (long)gridDim.x * blockDim.x) {
+    int k = 0;
+    while (k + 1 < L.count && gi >= L.start[k + 1]) ++k;
+    const long i = gi - L.start[k];
+    const float g = L.g[k][i];
+    const float m0 = L.m[k][i];
+    const float mi = m0 + w1 * (g - m0);
+    const float vi = L.v[k][i] * b2 + w2 * g * g;
+    L.m[k][i] = mi;
+    L.v[k][i] = vi;
     const float denom = sqrtf(vi) / bc2s + eps;
-    p[i] = p[i] - step_size * (mi / denom);             // addcdiv_(m, denom, -step_size)
+    L.p[k][i] = L.p[k][i] - step_size * (mi / denom);
   }
 }
 
@@ -777,21 +868,42 @@ int insr_adam_prepare(float* st, float b1, float b2, void* stream) {
   return (int)hipGetLastError();
 }
 
-int insr_plateau_step(float* st, const float* loss, int patience, void* stream) {
-  if (!st || !loss) return INSR_EINVAL;
-  hipLaunchKernelGGL(plateau_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, st, loss, patience);
+int insr_plateau_step(float* st, const float* loss, int patience, int advance_step, void* stream) {
+  if (!st || (!loss && !advance_step)) return INSR_EINVAL;
+  hipLaunchKernelGGL(plateau_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, st, loss, patience, advance_step);
+  return (int)hipGetLastError();
+}
+
+int insr_adam_step_multi(int count, float* const* params, const float* const* grads, float* const* exp_avg,
+                         float* const* exp_avg_sq, const long* sizes, const float* st, float b1, float b2,
+                         float eps, int step_offset, void* stream) {
+  if (count < 1 || count > INSR_ADAM_MAX_TENSORS || !st) return INSR_EINVAL;
+  AdamList L;
+  L.count = count;
+  L.start[0] = 0;
+  for (int k = 0; k < count; ++k) {
+    if (!params[k] || !grads[k] || !exp_avg[k] || !exp_avg_sq[k] || sizes[k] < 0) return INSR_EINVAL;
+    L.p[k] = params[k];
+    L.g[k] = grads[k];
+    L.m[k] = exp_avg[k];
+    L.v[k] = exp_avg_sq[k];
+    L.n[k] = sizes[k];
+    L.start[k + 1] = L.start[k] + sizes[k];
+  }
+  const long total = L.start[count];
+  if (total == 0) return 0;
+  long blocks = (total + 255) / 256;
+  if (blocks > 1024) blocks = 1024;
+  hipLaunchKernelGGL(adam_multi_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, L, st, b1, b2,
+                     eps, step_offset);
   return (int)hipGetLastError();
 }
 
 int insr_adam_step(float* p, const float* g, float* m, float* v, long n, const float* st, float b1, float b2,
                    float eps, void* stream) {
-  if (!p || !g || !m || !v || !st || n < 0) return INSR_EINVAL;
-  if (n == 0) return 0;
-  long blocks = (n + 255) / 256;
-  if (blocks > 2048) blocks = 2048;
-  hipLaunchKernelGGL(adam_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, p, g, m, v, n, st, b1,
-                     b2, eps);
-  return (int)hipGetLastError();
+  // single buffer, explicit-prepare convention (t = st[STEP])
+  long sz = n;
+  return insr_adam_step_multi(1, &p, &g, &m, &v, &sz, st, b1, b2, eps, 0, stream);
 }
 
 }  // extern "C"

@@ -137,12 +137,23 @@ def test_affine_jacobian_and_accumulation(base):
 
 
 def test_empty_and_tiny_batches(base):
+    """Single points make "normwise" pointwise, where even the reference's own fp32
+    Laplacian deviates from fp64 by up to ~1e-2 (cancellation in w^2 s sum t_i^2).
+    So here the judge is fp64: the HIP error must stay within the reference-fp32
+    error band (3x its error, or 1e-5 of the value, whichever is larger)."""
     ref, net = pair(base, "fluid_pres", seed=2)
+    ref64 = O.OracleSiren(2, 1, 4, 128).double()
+    ref64.load_state_dict({k: v.double() for k, v in ref.state_dict().items()})
     for n in (1, 15, 17, 65):
-        x = torch.rand(n, 2) * 2 - 1
+        x = torch.rand(n, 2, generator=torch.Generator().manual_seed(n)) * 2 - 1
         xr = x.clone().requires_grad_(True)
+        x64 = x.double().requires_grad_(True)
         xg = x.cuda().requires_grad_(True)
-        assert nerr(base.laplace(net(xg), xg), O.op_laplace(ref(xr), xr)) < TOL
+        l64 = O.op_laplace(ref64(x64), x64).detach()
+        e_ref = (O.op_laplace(ref(xr), xr).detach().double() - l64).abs()
+        e_hip = (base.laplace(net(xg), xg).detach().cpu().double() - l64).abs()
+        bound = torch.maximum(3 * e_ref, 1e-5 * l64.abs().max().expand_as(l64))
+        assert bool((e_hip <= bound).all()), (n, e_hip.max().item(), e_ref.max().item())
     y = net(torch.zeros(0, 2, device="cuda"))
     assert y.shape == (0, 1)
 
