@@ -62,7 +62,7 @@ int insr_siren_supported(int d_in, int d_out, int num_hidden, int width, int mod
 long insr_jet_act_bytes(long n_points, int d_in, int num_hidden, int width, int mode);
 
 /* Bytes of the per-block partial-gradient buffer the backward writes. */
-long insr_jet_partial_bytes(long n_points, int d_in, int d_out, int num_hidden, int width);
+long insr_jet_partial_bytes(long n_points, int d_in, int d_out, int num_hidden, int width, int mode);
 
 /*
  * Forward jet over n_points collocation points.
@@ -81,8 +81,8 @@ int insr_siren_jet_fwd(const float* x, long n_points, int d_in, int d_out, int n
 /*
  * Backward of the jet to the parameters.  Adjoints (any may be NULL = zero):
  *   gy (n, d_out), gdy (n, d_out, d_in), glap (n, d_out).
- *   partial  insr_jet_partial_bytes: one fp32 parameter-gradient per block of
- *            64 points (insr_jet_partial_blocks(n) rows x param_count).
+ *   partial  insr_jet_partial_bytes: one fp32 parameter-gradient row per block
+ *            (insr_jet_partial_blocks(n, d_in, mode) rows x param_count).
  * Sum the rows with insr_reduce_partials into the network's flat .grad.
  * The gradient w.r.t. x is not produced (the reference never reads it).
  * Replaces: the autograd backward of loss.backward() (base/baseModel.py:77).
@@ -92,8 +92,24 @@ int insr_siren_jet_bwd(const float* x, long n_points, int d_in, int d_out, int n
                        const float* gy, const float* gdy, const float* glap, float* partial,
                        void* stream);
 
-/* Number of partial-gradient rows insr_siren_jet_bwd writes for n points. */
-int insr_jet_partial_blocks(long n_points);
+/* Number of partial-gradient rows insr_siren_jet_bwd writes for n points
+ * (one per 64-point block, or per 16-point tile when the tile-split backward
+ * is selected for this size and mode). */
+int insr_jet_partial_blocks(long n_points, int d_in, int mode);
+
+/* Largest batch (points) served by the tile-split backward of derivative jets
+ * (4 waves per 16-point tile); larger batches use the wave-tile kernels.  The
+ * forward and value-jet thresholds are separate (env INSR_SPLIT_MAX_N_FWD,
+ * INSR_SPLIT_MAX_N_BWD, INSR_SPLIT_MAX_N_BWD_VALUE). */
+int insr_jet_split_threshold(void);
+
+/* Set all three thresholds to n_points (0 = always wave-tile).  Returns the old
+ * backward threshold.  Process-wide tuning/testing knob, not thread-safe. */
+int insr_jet_set_split_threshold(int n_points);
+
+/* All three thresholds: forward, derivative-jet backward, value-jet backward. */
+void insr_jet_get_split_thresholds(int* fwd, int* bwd, int* bwd_value);
+void insr_jet_set_split_thresholds(int fwd, int bwd, int bwd_value);
 
 /* grad[i] = (accumulate ? grad[i] : 0) + sum_b partial[b * count + i], fixed order. */
 int insr_reduce_partials(const float* partial, int n_blocks, long count, float* grad,

@@ -115,7 +115,7 @@ class _SirenJet(torch.autograd.Function):
         n, din = x2.shape
         L, W, dout = mlp.num_hidden_layers, mlp.hidden_features, mlp.out_features
         lib = nat.lib()
-        part = torch.empty(max(lib.insr_jet_partial_bytes(n, din, dout, L, W) // 4, 1), device=x2.device,
+        part = torch.empty(max(lib.insr_jet_partial_bytes(n, din, dout, L, W, mode) // 4, 1), device=x2.device,
                            dtype=torch.float32)
         gflat, accumulate = mlp.grad_for_backward()
         c = lambda t: None if t is None else (t if t.is_contiguous() else t.contiguous())  # noqa: E731
@@ -126,7 +126,7 @@ class _SirenJet(torch.autograd.Function):
                                         nat.ptr(act), nat.ptr(gy), nat.ptr(gdy), nat.ptr(glap), nat.ptr(part), st)
         nat.check(rc, "insr_siren_jet_bwd")
         with _timed("reduce", mode, n, W):
-            rc = lib.insr_reduce_partials(nat.ptr(part), lib.insr_jet_partial_blocks(n), gflat.numel(),
+            rc = lib.insr_reduce_partials(nat.ptr(part), lib.insr_jet_partial_blocks(n, din, mode), gflat.numel(),
                                           nat.ptr(gflat), accumulate, st)
         nat.check(rc, "insr_reduce_partials")
         return none

@@ -29,10 +29,14 @@ SIGNATURES = {
     "insr_siren_param_count": (_L, [_I, _I, _I, _I]),
     "insr_siren_supported": (_I, [_I, _I, _I, _I, _I]),
     "insr_jet_act_bytes": (_L, [_L, _I, _I, _I, _I]),
-    "insr_jet_partial_bytes": (_L, [_L, _I, _I, _I, _I]),
+    "insr_jet_partial_bytes": (_L, [_L, _I, _I, _I, _I, _I]),
     "insr_siren_jet_fwd": (_I, [_P, _L, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P]),
     "insr_siren_jet_bwd": (_I, [_P, _L, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P]),
-    "insr_jet_partial_blocks": (_I, [_L]),
+    "insr_jet_partial_blocks": (_I, [_L, _I, _I]),
+    "insr_jet_split_threshold": (_I, []),
+    "insr_jet_set_split_threshold": (_I, [_I]),
+    "insr_jet_get_split_thresholds": (None, [_P, _P, _P]),
+    "insr_jet_set_split_thresholds": (None, [_I, _I, _I]),
     "insr_reduce_partials": (_I, [_P, _I, _L, _P, _I, _P]),
     "insr_adam_prepare": (_I, [_P, _F, _F, _P]),
     "insr_plateau_step": (_I, [_P, _P, _I, _I, _P]),
@@ -73,6 +77,16 @@ def load(path=None):
 
 def lib():
     return _lib if _lib is not None else load()
+
+
+def get_split_thresholds():
+    v = [ctypes.c_int(), ctypes.c_int(), ctypes.c_int()]
+    lib().insr_jet_get_split_thresholds(*[ctypes.byref(a) for a in v])
+    return tuple(a.value for a in v)
+
+
+def set_split_thresholds(fwd, bwd, bwd_value):
+    lib().insr_jet_set_split_thresholds(int(fwd), int(bwd), int(bwd_value))
 
 
 def ptr(t):

@@ -1,0 +1,282 @@
+// jet_common.hpp -- shared device helpers of the gfx950 SIREN jet kernels.
+//
+// Replaces, for the INSR-PDE per-iteration training loop, the aten graph that
+// the reference builds with torch.autograd (create_graph=True):
+//   MLP.forward ............................ base/networks.py:25-27,67-71
+//   gradient / divergence / jacobian ....... base/diff_ops.py:44-82
+//   laplace = divergence(gradient) ......... base/diff_ops.py:33-41
+//   loss.backward() to the parameters ..... base/baseModel.py:73-78
+//
+// Math.  Linear layer k: z = W_k h + b_k.  Sine layer: h = sin(w z), w = 30.
+// A forward Taylor jet carries, per point and neuron, S streams:
+//   value z, tangents t_i = dz/dx_i (i < d), optionally q = sum_i d2z/dx_i^2.
+// Linear layers act on every stream with the same W (bias on the value only),
+// so a layer is ONE GEMM over (streams x points).  The sine couples streams
+// per (point, neuron), lane-locally:
+//   h = s,  dh_i = w c t_i,  ddh = w c q - w^2 s sum_i t_i^2       (s,c = sin,cos(w z))
+// and its reverse (adjoints hb, dhb_i, ddhb -> zb, tb_i, qb):
+//   zb  = w c hb - w^2 s sum_i t_i dhb_i - ddhb (w^2 s q + w^3 c sum_i t_i^2)
+//   tb_i = w c dhb_i - 2 w^2 s t_i ddhb,   qb = w c ddhb
+// Weight gradients: dW_k = sum_{streams,points} zb_stream (x) h_prev_stream.
+//
+// Layout on the chip ("transposed" orientation, MFMA v_mfma_f32_16x16x4_f32,
+// exact fp32 = the fp32 matrix rate, no xf32 on gfx950):
+//   * a wave owns 16 points = the 16 MFMA columns; neurons are MFMA rows.
+//   * activations of all W neurons x S streams live in VGPRs as floatx4
+//     h[rt][s] (rows 16rt+4g+r, column = point lane&15), which is exactly the
+//     MFMA C/D layout AND the B-operand layout of the next layer, so layers
+//     chain in registers with no LDS round trip.
+//   * weights are the A operand, staged once per layer per block into LDS
+//     (row stride W+8 floats: conflict-free ds_read_b128).
+//   * the forward saves pre-activation streams to HBM in the MFMA-native
+//     layout (each store = one contiguous 1 KiB wave write).
+//   * the backward rebuilds sin/cos from the saved z, runs the sine reverse
+//     lane-locally, and computes dW as an MFMA GEMM over the block's 64
+//     points (operands transposed through LDS), writing one partial gradient
+//     per block; insr_reduce_partials sums them in a fixed order.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/insr_siren.h"
+
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+#define OMEGA 30.0f
+#define OMEGA2 900.0f
+#define OMEGA3 27000.0f
+
+namespace insr {
+
+
+constexpr int kThreads = 256;  // 4 waves
+constexpr int kWaves = 4;
+constexpr int kPts = 64;       // points per block (16 per wave)
+constexpr int kLdp = kPts + 8; // padded row of the point-major LDS planes
+
+__device__ __forceinline__ floatx4 mfma4(float a, float b, floatx4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+__host__ __device__ inline long hidden_off(int din, int W, int j) {
+  // offset of net.{2j}.weight for hidden linear j >= 1
+  return (long)W * din + W + (long)(j - 1) * ((long)W * W + W);
+}
+__host__ __device__ inline long out_off(int din, int W, int L) {
+  return (long)W * din + W + (long)L * ((long)W * W + W);
+}
+
+// wave-tile base of layer `layer` in the saved-activation buffer
+__device__ __forceinline__ float* act_base(float* act, int layer, int ntiles, int tile, int S, int NT) {
+  return act + ((long)layer * ntiles + tile) * (long)(S * NT) * 256;
+}
+__device__ __forceinline__ const float* act_base(const float* act, int layer, int ntiles, int tile, int S,
+                                                 int NT) {
+  return act + ((long)layer * ntiles + tile) * (long)(S * NT) * 256;
+}
+
+// sum over the 16 point-lanes that share lane>>4
+__device__ __forceinline__ float sum16(float v) {
+  v += __shfl_xor(v, 1);
+  v += __shfl_xor(v, 2);
+  v += __shfl_xor(v, 4);
+  v += __shfl_xor(v, 8);
+  return v;
+}
+
+// ---------------------------------------------------------------------------
+// sin / cos of w*z.  Straight-line Cody-Waite reduction by pi/2 (3-part constant,
+// valid for |x| <= 8192) + minimax polynomials on [-pi/4, pi/4]: ~1 ulp, ~20 VALU
+// ops for the pair, no branches, so the compiler can interleave it with MFMAs.
+// A wave with any |x| > 8192 takes the libm (ocml) path instead (uniform branch).
+// ---------------------------------------------------------------------------
+constexpr float kFastArgMax = 8192.0f;
+
+__device__ __forceinline__ void sincos_fast(float x, float& s, float& c) {
+  const float n = rintf(x * 0.636619772367581343f);
+  float r = fmaf(-n, 1.5703125f, x);
+  r = fmaf(-n, 4.837512969970703125e-4f, r);
+  r = fmaf(-n, 7.54978995489188216e-8f, r);
+  const float z = r * r;
+  const float ps = fmaf(r * z, fmaf(z, fmaf(z, -1.9515295891e-4f, 8.3321608736e-3f), -1.6666654611e-1f), r);
+  const float pc = fmaf(z * z, fmaf(z, fmaf(z, 2.443315711809948e-5f, -1.388731625493765e-3f),
+                                    4.166664568298827e-2f), fmaf(-0.5f, z, 1.0f));
+  const int q = (int)n;
+  const float a = (q & 1) ? pc : ps;   // |sin|
+  const float b = (q & 1) ? ps : pc;   // |cos|
+  s = (q & 2) ? -a : a;
+  c = ((q + 1) & 2) ? -b : b;
+}
+
+__device__ __forceinline__ float sin_fast(float x) {
+  float s, c;
+  sincos_fast(x, s, c);
+  return s;
+}
+
+// true if any lane of the wave holds an argument outside the fast range
+__device__ __forceinline__ bool wave_any_big(float amax) {
+  return __any(amax > kFastArgMax);
+}
+
+
+template <int NT, int S, bool LAP, bool FAST>
+__device__ __forceinline__ void sine_jet_impl(floatx4 (&a)[NT][S]) {
+  constexpr int NTAN = LAP ? S - 2 : S - 1;
+#pragma unroll
+  for (int rt = 0; rt < NT; ++rt) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float arg = OMEGA * a[rt][0][r];
+      float sn, cs;
+      if constexpr (S == 1) {  // value-only jet: sin is all we need
+        if constexpr (FAST) sn = sin_fast(arg); else sn = sinf(arg);
+        a[rt][0][r] = sn;
+        continue;
+      }
+      if constexpr (FAST) sincos_fast(arg, sn, cs); else sincosf(arg, &sn, &cs);
+      const float wc = OMEGA * cs;
+      if constexpr (LAP) {
+        float t2 = 0.f;
+#pragma unroll
+        for (int i = 0; i < NTAN; ++i) t2 = fmaf(a[rt][1 + i][r], a[rt][1 + i][r], t2);
+        a[rt][S - 1][r] = wc * a[rt][S - 1][r] - OMEGA2 * sn * t2;
+      }
+#pragma unroll
+      for (int i = 0; i < NTAN; ++i) a[rt][1 + i][r] *= wc;
+      a[rt][0][r] = sn;
+    }
+  }
+}
+
+template <int NT, int S, bool LAP>
+__device__ __forceinline__ void sine_jet(floatx4 (&a)[NT][S]) {
+  float amax = 0.f;
+#pragma unroll
+  for (int rt = 0; rt < NT; ++rt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) amax = fmaxf(amax, fabsf(OMEGA * a[rt][0][r]));
+  if (wave_any_big(amax))
+    sine_jet_impl<NT, S, LAP, false>(a);
+  else
+    sine_jet_impl<NT, S, LAP, true>(a);
+}
+
+template <int NT, int S>
+__device__ __forceinline__ void save_streams(float* base, const floatx4 (&a)[NT][S], int lane) {
+#pragma unroll
+  for (int s = 0; s < S; ++s)
+#pragma unroll
+    for (int rt = 0; rt < NT; ++rt)
+      *reinterpret_cast<floatx4*>(base + ((s * NT + rt) * 64 + lane) * 4) = a[rt][s];
+}
+
+// Sine reverse for one row-tile.  hb: adjoints of h-streams in, zb out (in place).
+template <int S, bool LAP>
+__device__ __forceinline__ void sine_rev(floatx4 (&hb)[S], const floatx4 (&zs)[S], const floatx4& sn,
+                                         const floatx4& cs) {
+  constexpr int NTAN = LAP ? S - 2 : S - 1;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const float wc = OMEGA * cs[r], ws = OMEGA2 * sn[r];
+    float dot = 0.f;
+#pragma unroll
+    for (int i = 0; i < NTAN; ++i) dot = fmaf(zs[1 + i][r], hb[1 + i][r], dot);
+    float zb = wc * hb[0][r] - ws * dot;
+    if constexpr (LAP) {
+      const float qh = hb[S - 1][r];
+      float t2 = 0.f;
+#pragma unroll
+      for (int i = 0; i < NTAN; ++i) t2 = fmaf(zs[1 + i][r], zs[1 + i][r], t2);
+      zb -= qh * (ws * zs[S - 1][r] + OMEGA3 * cs[r] * t2);
+#pragma unroll
+      for (int i = 0; i < NTAN; ++i) hb[1 + i][r] = wc * hb[1 + i][r] - 2.f * ws * zs[1 + i][r] * qh;
+      hb[S - 1][r] = wc * qh;
+    } else {
+#pragma unroll
+      for (int i = 0; i < NTAN; ++i) hb[1 + i][r] *= wc;
+    }
+    hb[0][r] = zb;
+  }
+}
+
+template <int NT>
+__device__ __forceinline__ void load_z_sincos(const float* base, int S, int lane, floatx4 (&sn)[NT],
+                                              floatx4 (&cs)[NT]) {
+  floatx4 z[NT];
+  float amax = 0.f;
+#pragma unroll
+  for (int rt = 0; rt < NT; ++rt) {
+    z[rt] = *reinterpret_cast<const floatx4*>(base + (rt * 64 + lane) * 4);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) amax = fmaxf(amax, fabsf(OMEGA * z[rt][r]));
+  }
+  const bool big = wave_any_big(amax);
+#pragma unroll
+  for (int rt = 0; rt < NT; ++rt) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float a, b;
+      if (big)
+        sincosf(OMEGA * z[rt][r], &a, &b);
+      else
+        sincos_fast(OMEGA * z[rt][r], a, b);
+      sn[rt][r] = a;
+      cs[rt][r] = b;
+    }
+  }
+}
+
+// h-stream s of a sine layer (for the weight gradient of the layer above),
+// rebuilt from saved z-streams + cached sin/cos.
+template <int NT, int S, bool LAP>
+__device__ __forceinline__ floatx4 h_stream(const float* base, int s, int rt, int lane, const floatx4& sn,
+                                            const floatx4& cs) {
+  constexpr int NTAN = LAP ? S - 2 : S - 1;
+  if (s == 0) return sn;
+  const floatx4 zs = *reinterpret_cast<const floatx4*>(base + ((s * NT + rt) * 64 + lane) * 4);
+  floatx4 out;
+  if (LAP && s == S - 1) {
+    floatx4 t2 = floatx4{0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < NTAN; ++i) {
+      const floatx4 t = *reinterpret_cast<const floatx4*>(base + (((1 + i) * NT + rt) * 64 + lane) * 4);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) t2[r] = fmaf(t[r], t[r], t2[r]);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) out[r] = OMEGA * cs[r] * zs[r] - OMEGA2 * sn[r] * t2[r];
+  } else {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) out[r] = OMEGA * cs[r] * zs[r];
+  }
+  return out;
+}
+
+
+// ---------------------------------------------------------------------------
+// launchers (defined in jet_wave.hip / jet_split.hip)
+// ---------------------------------------------------------------------------
+int dispatch_fwd_wave(int NT, int S, bool LAP, const float* x, int N, int din, int dout, int L, const float* prm,
+                      float* y, float* dy, float* lap, float* act, hipStream_t st);
+int dispatch_bwd_wave(int NT, int S, bool LAP, const float* x, int N, int din, int dout, int L, const float* prm,
+                      const float* act, const float* gy, const float* gdy, const float* glap, float* part, long P,
+                      hipStream_t st);
+int dispatch_fwd_split(int NT, int S, bool LAP, const float* x, int N, int din, int dout, int L, const float* prm,
+                       float* y, float* dy, float* lap, float* act, hipStream_t st);
+int dispatch_bwd_split(int NT, int S, bool LAP, const float* x, int N, int din, int dout, int L, const float* prm,
+                       const float* act, const float* gy, const float* gdy, const float* glap, float* part, long P,
+                       hipStream_t st);
+
+// (S, LAP) combinations: value (1), grad d=1..3 (2..4), lap d=1,2 (3,4)
+#define INSR_DISPATCH(NTV, FN, ...)                \
+  switch (S * 2 + (LAP ? 1 : 0)) {                 \
+    case 2: return FN<NTV, 1, false>(__VA_ARGS__); \
+    case 4: return FN<NTV, 2, false>(__VA_ARGS__); \
+    case 6: return FN<NTV, 3, false>(__VA_ARGS__); \
+    case 8: return FN<NTV, 4, false>(__VA_ARGS__); \
+    case 7: return FN<NTV, 3, true>(__VA_ARGS__);  \
+    case 9: return FN<NTV, 4, true>(__VA_ARGS__);  \
+    default: return INSR_EINVAL;                   \
+  }
+
+}  // namespace insr

@@ -11,7 +11,7 @@ HEADER = os.path.join(ROOT, "include", "insr_siren.h")
 
 def declared_symbols():
     txt = open(HEADER).read()
-    return sorted(set(re.findall(r"^\s*(?:int|long)\s+(insr_\w+)\s*\(", txt, flags=re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int|long|void)\s+(insr_\w+)\s*\(", txt, flags=re.M)))
 
 
 @pytest.fixture(scope="module")
@@ -46,8 +46,17 @@ def test_host_queries(lib):
     assert lib.insr_siren_supported(2, 1, 4, 100, 0) == 0   # width not compiled
     # saved activations: (L+1) layers x 16 W floats per 16-point tile x S streams
     assert lib.insr_jet_act_bytes(64, 2, 4, 128, 2) == 5 * 4 * 16 * 128 * 4 * 4
-    assert lib.insr_jet_partial_bytes(65, 2, 1, 4, 128) == 2 * 66561 * 4
-    assert lib.insr_jet_partial_blocks(65) == 2 and lib.insr_jet_partial_blocks(0) == 0
+    from base import _native as nat
+    saved = nat.get_split_thresholds()
+    old = lib.insr_jet_set_split_threshold(0)          # wave-tile kernels: one row per 64 points
+    assert lib.insr_jet_partial_bytes(65, 2, 1, 4, 128, 2) == 2 * 66561 * 4
+    assert lib.insr_jet_partial_blocks(65, 2, 2) == 2 and lib.insr_jet_partial_blocks(0, 2, 2) == 0
+    lib.insr_jet_set_split_threshold(1 << 20)           # tile-split kernels: one row per 16 points
+    assert lib.insr_jet_partial_blocks(65, 2, 2) == 5
+    lib.insr_jet_set_split_threshold(old)
+    assert lib.insr_jet_split_threshold() == old
+    nat.set_split_thresholds(*saved)
+    assert nat.get_split_thresholds() == saved
 
 
 def test_invalid_arguments_rejected_without_launch(lib):

@@ -26,13 +26,26 @@ NETS = {  # name: (d_in, d_out, L, W)
 }
 
 
-@pytest.fixture(scope="module")
-def base():
+BIG = 1 << 30
+VARIANTS = {  # (fwd, bwd, bwd_value) split thresholds
+    "wave": (0, 0, 0),                 # one wave per 16-point tile, both directions
+    "split": (BIG, BIG, BIG),          # 4 waves per 16-point tile, both directions
+    "split_fwd_wave_bwd": (BIG, 0, 0),  # mixed: the saved-activation layout is shared
+    "wave_fwd_split_bwd": (0, BIG, BIG),
+}
+
+
+@pytest.fixture(scope="module", params=list(VARIANTS))
+def base(request):
+    """Every test runs for each kernel-variant combination."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     import base as B
     B._native.load()
-    return B
+    old = B._native.get_split_thresholds()
+    B._native.set_split_thresholds(*VARIANTS[request.param])
+    yield B
+    B._native.set_split_thresholds(*old)
 
 
 def nerr(a, b):

@@ -20,6 +20,7 @@ for s in ${STEPS:-tests bench prof}; do
     tests) step tests 500 python -m pytest tests -q -m gpu -x ;;
     smoke) step smoke 200 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 400 python bench.py --steps ${BSTEPS:-20} --warmup 3 ;;
+    kbench) step kbench 300 python tools/kbench.py --sizes ${KSIZES:-324,2048,8192,16384} ;;
     eager) step eager 150 python bench.py --steps 5 --warmup 2 --no-graph --no-cpu-baseline ;;
     graph) step graph 150 python bench.py --steps 5 --warmup 3 --no-cpu-baseline --no-roofline ;;
     prof)  export TMPDIR=/tmp; step prof 400 rocprofv3 --kernel-trace --stats -d "$PWD/$OUT/prof" -o run --output-format csv -- python bench.py --steps 10 --warmup 3 --no-cpu-baseline ;;

@@ -1,0 +1,101 @@
+"""Kernel micro-benchmark: fwd / bwd jet kernels back-to-back on one stream
+(HIP events around R launches, no host gaps), for both kernel variants.
+
+    python tools/kbench.py [--nets fluid_pres,fluid_vel] [--sizes 324,4096,16384]
+"""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "insr-pde_amd")]
+
+import torch  # noqa: E402
+
+NETS = {"fluid_pres": (2, 1, 4, 128), "fluid_vel": (2, 2, 4, 128), "advect": (1, 1, 3, 64),
+        "el2d": (2, 2, 5, 128)}
+MODES = {"value": 0, "grad": 1, "lap": 2}
+
+
+def P_macs(din, dout, L, W):
+    return din * W + L * W * W + W * dout
+
+
+def time_it(fn, reps):
+    fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps * 1e3  # us
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--nets", default="fluid_pres,fluid_vel")
+    ap.add_argument("--sizes", default="324,2048,8192,16384,65536")
+    ap.add_argument("--modes", default="value,grad,lap")
+    ap.add_argument("--reps", type=int, default=20)
+    args = ap.parse_args()
+    import base
+    from base import _native as nat
+    lib = nat.load()
+    out = []
+    for name in args.nets.split(","):
+        din, dout, L, W = NETS[name]
+        torch.manual_seed(0)
+        net = base.MLP(din, dout, L, W, nonlinearity="sine").cuda()
+        flat = net.flat_params()
+        P = net.param_count
+        for mname in args.modes.split(","):
+            mode = MODES[mname]
+            if mode == 2 and din > 2:
+                continue
+            S = {0: 1, 1: 1 + din, 2: 2 + din}[mode]
+            for n in [int(v) for v in args.sizes.split(",")]:
+                x = (torch.rand(n, din, device="cuda") * 2 - 1).contiguous()
+                y = torch.empty(n, dout, device="cuda")
+                dy = torch.empty(n, dout, din, device="cuda")
+                lap = torch.empty(n, dout, device="cuda")
+                gy, gdy, glap = torch.randn_like(y), torch.randn_like(dy), torch.randn_like(lap)
+                act = torch.empty(lib.insr_jet_act_bytes(n, din, L, W, mode) // 4, device="cuda")
+                g = torch.zeros(P, device="cuda")
+                st = nat.stream_of(x.device)
+                for variant, thr in (("wave", 0), ("split", 1 << 30)):
+                    lib.insr_jet_set_split_threshold(thr)
+                    part = torch.empty(max(lib.insr_jet_partial_bytes(n, din, dout, L, W, mode) // 4, 1), device="cuda")
+                    nb = lib.insr_jet_partial_blocks(n, din, mode)
+
+                    def fwd():
+                        nat.check(lib.insr_siren_jet_fwd(nat.ptr(x), n, din, dout, L, W, mode, nat.ptr(flat),
+                                                         nat.ptr(y), nat.ptr(dy), nat.ptr(lap), nat.ptr(act), st),
+                                  "fwd")
+
+                    def bwd():
+                        nat.check(lib.insr_siren_jet_bwd(nat.ptr(x), n, din, dout, L, W, mode, nat.ptr(flat),
+                                                         nat.ptr(act), nat.ptr(gy), nat.ptr(gdy), nat.ptr(glap),
+                                                         nat.ptr(part), st), "bwd")
+
+                    def red():
+                        nat.check(lib.insr_reduce_partials(nat.ptr(part), nb, P, nat.ptr(g), 0, st), "reduce")
+
+                    tf = time_it(fwd, args.reps)
+                    fwd()
+                    tb = time_it(bwd, args.reps)
+                    tr = time_it(red, args.reps)
+                    macs = P_macs(din, dout, L, W)
+                    rec = {"net": name, "mode": mname, "n": n, "variant": variant, "fwd_us": round(tf, 2),
+                           "bwd_us": round(tb, 2), "reduce_us": round(tr, 2),
+                           "fwd_tflops": round(n * S * 2 * macs / tf / 1e6, 2),
+                           "bwd_tflops": round(n * S * 4 * macs / tb / 1e6, 2)}
+                    out.append(rec)
+                    print(json.dumps(rec), flush=True)
+
+
+
+if __name__ == "__main__":
+    main()
