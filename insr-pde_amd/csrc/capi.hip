@@ -25,8 +25,10 @@ int nt_for(int width) {
 // wave-tile kernels (one wave per 16 points).  Both write/read the same saved-
 // activation layout, so forward and backward choose independently.  Defaults from
 // tools/kbench.py on MI355X (W=128): the split forward wins at every size
-// measured; the split backward wins up to 16384 points for derivative jets but its
-// one-partial-row-per-16-points reduction loses beyond 8192 for value jets.
+// measured (324..65536 points); the split backward wins at every size for
+// derivative jets even counting its 4x larger partial reduction (65536 points, LAP:
+// 1187+270 us vs 1793+68 us), but loses beyond 8192 points for value jets (16384:
+// 111+69 us vs 144+17 us).
 // Env overrides: INSR_SPLIT_MAX_N_FWD / _BWD / _BWD_VALUE (points).
 static int g_thr[3] = {-1, -1, -1};  // fwd, bwd (S > 1), bwd value
 
@@ -37,8 +39,8 @@ static int env_or(const char* name, int dflt) {
 
 int split_max_n() {
   if (g_thr[0] < 0) {
-    g_thr[0] = env_or("INSR_SPLIT_MAX_N_FWD", 32768);
-    g_thr[1] = env_or("INSR_SPLIT_MAX_N_BWD", 16384);
+    g_thr[0] = env_or("INSR_SPLIT_MAX_N_FWD", 1 << 30);
+    g_thr[1] = env_or("INSR_SPLIT_MAX_N_BWD", 1 << 30);
     g_thr[2] = env_or("INSR_SPLIT_MAX_N_BWD_VALUE", 8192);
   }
   return g_thr[1];
