@@ -51,6 +51,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--backend", default="nccl", help="nccl (= RCCL) or gloo (functional rehearsal)")
     return ap.parse_args()
 
 
@@ -58,9 +59,15 @@ def setup_dist(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
+    ndev = torch.cuda.device_count()
+    dev = local % max(ndev, 1)  # >1 rank per GPU only for functional rehearsal (--backend gloo)
+    os.environ["LOCAL_RANK"] = str(dev)
+    torch.cuda.set_device(dev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        else:
+            dist.init_process_group(args.backend)
     return world, rank, local
 
 

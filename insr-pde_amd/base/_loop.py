@@ -11,6 +11,9 @@ Differences, all controlled by cfg attributes:
       allocator settle); iteration 1 is captured into a hipGraph and every
       later iteration is one graph replay.  If capture fails (e.g. a phase
       with data-dependent shapes or host syncs) the loop stays eager.
+      Under data parallelism the iteration is two graphs -- [phase + backward]
+      and [Adam + plateau] -- with the single RCCL all-reduce of gradients and
+      losses issued eagerly between them (no collective inside a capture).
 """
 import torch
 
@@ -30,14 +33,15 @@ class PhaseLoop:
         self.vis_every = int(getattr(cfg, "vis_frequency", 1000))
         self.early_stop = bool(getattr(cfg, "early_stop", True))
         self.show = bool(getattr(cfg, "insr_progress", True)) and tqdm is not None
-        self.graph = None
+        self.graph = self.graph2 = None
         self.static = None
+        self.static_main = None
 
     def start(self):
         """Fresh optimiser + scheduler for this phase (base/baseModel.py:106)."""
         self.m._reset_optimizer()
         self.opt, self.sched = self.m.optimizer, self.m.scheduler
-        self.graph, self.static = None, None
+        self.graph, self.graph2, self.static = None, None, None
 
     def _body(self):
         self.m.optimizer, self.m.scheduler = self.opt, self.sched
@@ -45,33 +49,72 @@ class PhaseLoop:
         synced = self.m._update_network(loss_dict)
         return synced if isinstance(synced, dict) else loss_dict
 
-    def _capture(self):
+    # ---- data-parallel split: [phase + backward] graph | eager RCCL all-reduce | [Adam + plateau] graph
+    def _stage1(self):
+        m = self.m
+        m.optimizer, m.scheduler = self.opt, self.sched
+        loss_dict = self.func(m, *self.args, **self.kwargs)
+        loss = sum(loss_dict.values())
+        m.optimizer.zero_grad()
+        loss.backward()
+        return loss_dict
+
+    def _stage2(self):
+        m = self.m
+        m.optimizer.step()
+        if m.scheduler is not None:
+            m.scheduler.step(self.static_main)
+
+    def _dp_step_eager(self):
+        ld = self._stage1()
+        synced = self.m._dp_sync(ld)
+        self.static_main = synced['main'].detach().reshape(1).clone()
+        self._stage2()
+        return synced
+
+    def _capture_graph(self, fn):
         m = self.m
         side = torch.cuda.Stream(device=m.device)
         side.wait_stream(torch.cuda.current_stream(m.device))
         g = torch.cuda.CUDAGraph()
+        with torch.cuda.stream(side):
+            with torch.cuda.graph(g, stream=side):
+                out = fn()
+        torch.cuda.current_stream(m.device).wait_stream(side)
+        return g, out
+
+    def _capture(self):
         try:
-            with torch.cuda.stream(side):
-                with torch.cuda.graph(g, stream=side):
-                    out = self._body()
-            torch.cuda.current_stream(m.device).wait_stream(side)
+            if self.m._dp_world() > 1:
+                g1, out = self._capture_graph(self._stage1)
+                g2, _ = self._capture_graph(self._stage2)
+                self.graph, self.graph2 = g1, g2
+            else:
+                self.graph, out = self._capture_graph(self._body)
+                self.graph2 = None
         except Exception as e:  # not capturable: stay eager
-            torch.cuda.synchronize(m.device)
+            torch.cuda.synchronize(self.m.device)
             self.use_graph = False
             self.capture_error = repr(e)
+            self.graph = self.graph2 = None
             return None
-        self.graph, self.static = g, {k: v.detach() for k, v in out.items()}
+        self.static = {k: v.detach() for k, v in out.items()}
         return self.static
 
     def step(self, i):
         """Run iteration i; returns the device loss dict of that iteration."""
+        dp = self.m._dp_world() > 1
         if self.use_graph and i >= 1:
-            if self.graph is None:
-                if self._capture() is None:
-                    return self._body()
+            if self.graph is None and self._capture() is None:
+                return self._dp_step_eager() if dp else self._body()
             self.graph.replay()
-            return self.static
-        return self._body()
+            if self.graph2 is None:
+                return self.static
+            synced = self.m._dp_sync(self.static)  # one RCCL all-reduce, eager
+            self.static_main.copy_(synced['main'].detach().reshape(1))
+            self.graph2.replay()
+            return synced
+        return self._dp_step_eager() if dp else self._body()
 
     def run(self):
         m = self.m
@@ -100,5 +143,5 @@ class PhaseLoop:
                     break
             if (i == 0 or (i + 1) % self.vis_every == 0) and hasattr(m, f"_vis{self.tag}"):
                 getattr(m, f"_vis{self.tag}")()
-        self.graph = None
+        self.graph = self.graph2 = None
         self.static = None
