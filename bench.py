@@ -78,9 +78,10 @@ def build_model(args, world):
     base._native.load()
     N = 128 * 128
     # strong: the global 16384 points are split over ranks; weak: every rank keeps 16384
-    sr = 128 if args.scaling == "strong" else int(round((N * world) ** 0.5))
-    cfg = baseline_config(args.config, sample_resolution=sr, insr_graph=not args.no_graph, insr_sync_every=10 ** 9,
-                          insr_progress=False, early_stop=False, proj_dir="/tmp/insr_bench", max_n_iters=10 ** 9)
+    per_rank = N // world if args.scaling == "strong" else N
+    cfg = baseline_config(args.config, sample_resolution=128, insr_points_per_rank=per_rank,
+                          insr_graph=not args.no_graph, insr_sync_every=10 ** 9, insr_progress=False,
+                          early_stop=False, proj_dir="/tmp/insr_bench", max_n_iters=10 ** 9)
     torch.manual_seed(1234)
     model = Fluid2DModel(cfg)
     model.timestep = 1
@@ -223,9 +224,11 @@ def main():
                    "points_per_phase_iter": n_local * world, "phases": 3, "global_batch": n_local * world,
                    "seq_len": None, "parallelism": f"dp{world}", "graph": not args.no_graph},
     }
-    if rank == 0 and not args.no_roofline:
+    if not args.no_roofline:  # every rank runs the eager steps (they contain the all-reduce)
         P_pres = 2 * 128 + 4 * 128 * 128 + 128 * 1  # d_in W + L W^2 + W d_out
-        result["roofline"] = roofline(model, loops, n_local, P_pres)
+        roof = roofline(model, loops, n_local, P_pres)
+        if rank == 0:
+            result["roofline"] = roof
         log("roofline done")
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args.cpu_seconds)

@@ -27,7 +27,8 @@ class Advection1DModel(BaseModel):
         return {"field": self.field}
 
     def _n_interior(self):
-        return max(1, self.sample_resolution // self._dp_world())
+        fixed = getattr(self.cfg, "insr_points_per_rank", None)
+        return int(fixed) if fixed else max(1, self.sample_resolution // self._dp_world())
 
     def _sample_in_training(self):
         half = self.length / 2

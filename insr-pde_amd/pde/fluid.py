@@ -37,7 +37,10 @@ class Fluid2DModel(BaseModel):
 
     # ---- sampling ------------------------------------------------------------
     def _n_interior(self):
-        return max(1, self.sample_resolution ** 2 // self._dp_world())
+        """Points per rank: sample_resolution^2 split over ranks (strong scaling), or
+        cfg.insr_points_per_rank when set (weak scaling)."""
+        fixed = getattr(self.cfg, "insr_points_per_rank", None)
+        return int(fixed) if fixed else max(1, self.sample_resolution ** 2 // self._dp_world())
 
     def _sample_in_training(self):
         return sample_random(self._n_interior(), 2, device=self.device).requires_grad_(True)
