@@ -82,7 +82,7 @@ int insr_siren_jet_fwd(const float* x, long n_points, int d_in, int d_out, int n
  * Backward of the jet to the parameters.  Adjoints (any may be NULL = zero):
  *   gy (n, d_out), gdy (n, d_out, d_in), glap (n, d_out).
  *   partial  insr_jet_partial_bytes: one fp32 parameter-gradient row per block
- *            (insr_jet_partial_blocks(n, d_in, mode) rows x param_count).
+ *            (insr_jet_partial_blocks(n, d_in, width, mode) rows x param_count).
  * Sum the rows with insr_reduce_partials into the network's flat .grad.
  * The gradient w.r.t. x is not produced (the reference never reads it).
  * Replaces: the autograd backward of loss.backward() (base/baseModel.py:77).
@@ -92,15 +92,16 @@ int insr_siren_jet_bwd(const float* x, long n_points, int d_in, int d_out, int n
                        const float* gy, const float* gdy, const float* glap, float* partial,
                        void* stream);
 
-/* Number of partial-gradient rows insr_siren_jet_bwd writes for n points
- * (one per 64-point block, or per 16-point tile when the tile-split backward
- * is selected for this size and mode). */
-int insr_jet_partial_blocks(long n_points, int d_in, int mode);
+/* Number of partial-gradient rows insr_siren_jet_bwd writes for n points: one
+ * per 64-point wave-tile block, or one per T-tile (16T-point) tile-split block,
+ * whichever the backward selects for this size, width and mode. */
+int insr_jet_partial_blocks(long n_points, int d_in, int width, int mode);
 
 /* Largest batch (points) served by the tile-split backward of derivative jets
- * (4 waves per 16-point tile); larger batches use the wave-tile kernels.  The
- * forward and value-jet thresholds are separate (env INSR_SPLIT_MAX_N_FWD,
- * INSR_SPLIT_MAX_N_BWD, INSR_SPLIT_MAX_N_BWD_VALUE). */
+ * (the neurons of a layer split over the waves of a block); larger batches use
+ * the wave-tile kernels (width <= 128 only).  The forward and value-jet thresholds
+ * are separate (env INSR_SPLIT_MAX_N_FWD, INSR_SPLIT_MAX_N_BWD,
+ * INSR_SPLIT_MAX_N_BWD_VALUE). */
 int insr_jet_split_threshold(void);
 
 /* Set all three thresholds to n_points (0 = always wave-tile).  Returns the old
@@ -110,6 +111,16 @@ int insr_jet_set_split_threshold(int n_points);
 /* All three thresholds: forward, derivative-jet backward, value-jet backward. */
 void insr_jet_get_split_thresholds(int* fwd, int* bwd, int* bwd_value);
 void insr_jet_set_split_thresholds(int fwd, int bwd, int bwd_value);
+
+/* Tiles per tile-split block (1, 2 or 4) the forward (backward != 0: the
+ * backward) uses for this batch, or 0 if it uses the wave-tile kernel. */
+int insr_jet_split_tiles(long n_points, int d_in, int width, int mode, int backward);
+
+/* Tile-count policy: force T for forward / backward (0 = auto: the largest T
+ * whose LDS fits, lowered while the grid has fewer than min_blocks blocks).
+ * Env: INSR_SPLIT_TILES_FWD, INSR_SPLIT_TILES_BWD, INSR_SPLIT_MIN_BLOCKS. */
+void insr_jet_set_split_tiles(int fwd_tiles, int bwd_tiles, int min_blocks);
+void insr_jet_get_split_tiles(int* fwd_tiles, int* bwd_tiles, int* min_blocks);
 
 /* grad[i] = (accumulate ? grad[i] : 0) + sum_b partial[b * count + i], fixed order. */
 int insr_reduce_partials(const float* partial, int n_blocks, long count, float* grad,

@@ -126,7 +126,7 @@ class _SirenJet(torch.autograd.Function):
                                         nat.ptr(act), nat.ptr(gy), nat.ptr(gdy), nat.ptr(glap), nat.ptr(part), st)
         nat.check(rc, "insr_siren_jet_bwd")
         with _timed("reduce", mode, n, W):
-            rc = lib.insr_reduce_partials(nat.ptr(part), lib.insr_jet_partial_blocks(n, din, mode), gflat.numel(),
+            rc = lib.insr_reduce_partials(nat.ptr(part), lib.insr_jet_partial_blocks(n, din, W, mode), gflat.numel(),
                                           nat.ptr(gflat), accumulate, st)
         nat.check(rc, "insr_reduce_partials")
         return none

@@ -32,11 +32,14 @@ SIGNATURES = {
     "insr_jet_partial_bytes": (_L, [_L, _I, _I, _I, _I, _I]),
     "insr_siren_jet_fwd": (_I, [_P, _L, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P]),
     "insr_siren_jet_bwd": (_I, [_P, _L, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P]),
-    "insr_jet_partial_blocks": (_I, [_L, _I, _I]),
+    "insr_jet_partial_blocks": (_I, [_L, _I, _I, _I]),
     "insr_jet_split_threshold": (_I, []),
     "insr_jet_set_split_threshold": (_I, [_I]),
     "insr_jet_get_split_thresholds": (None, [_P, _P, _P]),
     "insr_jet_set_split_thresholds": (None, [_I, _I, _I]),
+    "insr_jet_split_tiles": (_I, [_L, _I, _I, _I, _I]),
+    "insr_jet_set_split_tiles": (None, [_I, _I, _I]),
+    "insr_jet_get_split_tiles": (None, [_P, _P, _P]),
     "insr_reduce_partials": (_I, [_P, _I, _L, _P, _I, _P]),
     "insr_adam_prepare": (_I, [_P, _F, _F, _P]),
     "insr_plateau_step": (_I, [_P, _P, _I, _I, _P]),
@@ -87,6 +90,16 @@ def get_split_thresholds():
 
 def set_split_thresholds(fwd, bwd, bwd_value):
     lib().insr_jet_set_split_thresholds(int(fwd), int(bwd), int(bwd_value))
+
+
+def get_split_tiles():
+    v = [ctypes.c_int(), ctypes.c_int(), ctypes.c_int()]
+    lib().insr_jet_get_split_tiles(*[ctypes.byref(a) for a in v])
+    return tuple(a.value for a in v)
+
+
+def set_split_tiles(fwd_tiles, bwd_tiles, min_blocks):
+    lib().insr_jet_set_split_tiles(int(fwd_tiles), int(bwd_tiles), int(min_blocks))
 
 
 def ptr(t):

@@ -17,19 +17,17 @@ int nt_for(int width) {
   if (width == 32) return 2;
   if (width == 64) return 4;
   if (width == 128) return 8;
+  if (width == 256) return 16;  // tile-split kernels only
   return -1;
 }
 
-// Kernel-variant choice.  Batches up to these sizes use the tile-split kernels (a
-// 16-point tile per 4-wave block, neurons split over the waves); larger ones the
-// wave-tile kernels (one wave per 16 points).  Both write/read the same saved-
-// activation layout, so forward and backward choose independently.  Defaults from
-// tools/kbench.py on MI355X (W=128): the split forward wins at every size
-// measured (324..65536 points); the split backward wins at every size for
-// derivative jets even counting its 4x larger partial reduction (65536 points, LAP:
-// 1187+270 us vs 1793+68 us), but loses beyond 8192 points for value jets (16384:
-// 111+69 us vs 144+17 us).
-// Env overrides: INSR_SPLIT_MAX_N_FWD / _BWD / _BWD_VALUE (points).
+// Kernel-variant choice.  Batches up to these sizes use the tile-split kernels
+// (jet_split.hpp: the neurons of a layer split over the waves of a block, T
+// 16-point tiles per block); larger ones the wave-tile kernels (jet_wave.hip: one
+// wave per 16 points, all neurons in its registers).  Both write/read the same
+// saved-activation layout, so forward and backward choose independently.  Width
+// 256 is served by the tile-split kernels only (its wave-tile state would not fit
+// the register file).  Env overrides: INSR_SPLIT_MAX_N_FWD / _BWD / _BWD_VALUE.
 static int g_thr[3] = {-1, -1, -1};  // fwd, bwd (S > 1), bwd value
 
 static int env_or(const char* name, int dflt) {
@@ -41,19 +39,49 @@ int split_max_n() {
   if (g_thr[0] < 0) {
     g_thr[0] = env_or("INSR_SPLIT_MAX_N_FWD", 1 << 30);
     g_thr[1] = env_or("INSR_SPLIT_MAX_N_BWD", 1 << 30);
-    g_thr[2] = env_or("INSR_SPLIT_MAX_N_BWD_VALUE", 8192);
+    g_thr[2] = env_or("INSR_SPLIT_MAX_N_BWD_VALUE", 1 << 30);
   }
   return g_thr[1];
 }
 
-bool use_split_fwd(long n) {
+bool use_split_fwd(long n, int NT) {
   split_max_n();
-  return n <= g_thr[0];
+  return NT > 8 || n <= g_thr[0];
 }
 
-bool use_split_bwd(long n, int S) {
+bool use_split_bwd(long n, int S, int NT) {
   split_max_n();
-  return n <= (S == 1 ? g_thr[2] : g_thr[1]);
+  return NT > 8 || n <= (S == 1 ? g_thr[2] : g_thr[1]);
+}
+
+// Tiles per tile-split block.  The largest T in {1, 2, 4} whose LDS fits a CU,
+// lowered while the grid would have fewer than `min_blocks` blocks (small batches
+// want many short blocks, large ones fewer blocks that share W fetches, barriers
+// and partial rows).  Env/API overrides: INSR_SPLIT_TILES_FWD / _BWD (force T,
+// 0 = auto), INSR_SPLIT_MIN_BLOCKS.
+static int g_tiles[3] = {-1, -1, -1};  // forced fwd T, forced bwd T, min blocks
+
+static void tiles_init() {
+  if (g_tiles[0] < 0) {
+    g_tiles[0] = env_or("INSR_SPLIT_TILES_FWD", 0);
+    g_tiles[1] = env_or("INSR_SPLIT_TILES_BWD", 0);
+    g_tiles[2] = env_or("INSR_SPLIT_MIN_BLOCKS", 512);
+  }
+}
+
+int split_tiles(int bwd, int NT, int S, long n) {
+  tiles_init();
+  const size_t plane = (size_t)S * 16 * (16 * NT + 8) * sizeof(float) * (bwd ? 2 : 1);
+  int T = NT > 8 ? 1 : 4;  // width 256: one tile (register budget of 8 waves x 2 row tiles)
+  while (T > 1 && (size_t)T * plane > 163840) T >>= 1;
+  const int forced = g_tiles[bwd ? 1 : 0];
+  if (forced > 0) {
+    while (T > forced) T >>= 1;
+    return T;
+  }
+  const long tiles = (n + 15) / 16;
+  while (T > 1 && (tiles + T - 1) / T < g_tiles[2]) T >>= 1;
+  return T;
 }
 
 constexpr int kRedWaves = 8;
@@ -184,7 +212,7 @@ using namespace insr;
 
 extern "C" {
 
-int insr_version(void) { return 100; }
+int insr_version(void) { return 200; }
 
 long insr_siren_param_count(int din, int dout, int L, int W) {
   return (long)W * din + W + (long)L * ((long)W * W + W) + (long)dout * W + dout;
@@ -200,7 +228,9 @@ long insr_jet_act_bytes(long n, int din, int L, int W, int mode) {
 }
 
 long insr_jet_partial_bytes(long n, int din, int dout, int L, int W, int mode) {
-  return (long)insr_jet_partial_blocks(n, din, mode) * insr_siren_param_count(din, dout, L, W) * (long)sizeof(float);
+  const int nb = insr_jet_partial_blocks(n, din, W, mode);
+  if (nb < 0) return nb;
+  return (long)nb * insr_siren_param_count(din, dout, L, W) * (long)sizeof(float);
 }
 
 int insr_siren_jet_fwd(const float* x, long n, int din, int dout, int L, int W, int mode, const float* params,
@@ -212,9 +242,9 @@ int insr_siren_jet_fwd(const float* x, long n, int din, int dout, int L, int W, 
   if (mode == INSR_MODE_LAP && !lap) return INSR_EINVAL;
   const int S = streams_for(din, mode);
   const int NT = nt_for(W);
-  if (use_split_fwd(n))
-    return dispatch_fwd_split(NT, S, mode == INSR_MODE_LAP, x, (int)n, din, dout, L, params, y, dy, lap, act,
-                              (hipStream_t)stream);
+  if (use_split_fwd(n, NT))
+    return dispatch_fwd_split(NT, S, mode == INSR_MODE_LAP, split_tiles(0, NT, S, n), x, (int)n, din, dout, L,
+                              params, y, dy, lap, act, (hipStream_t)stream);
   return dispatch_fwd_wave(NT, S, mode == INSR_MODE_LAP, x, (int)n, din, dout, L, params, y, dy, lap, act,
                            (hipStream_t)stream);
 }
@@ -228,16 +258,41 @@ int insr_siren_jet_bwd(const float* x, long n, int din, int dout, int L, int W, 
   const long P = insr_siren_param_count(din, dout, L, W);
   const int S = streams_for(din, mode);
   const int NT = nt_for(W);
-  if (use_split_bwd(n, S))
-    return dispatch_bwd_split(NT, S, mode == INSR_MODE_LAP, x, (int)n, din, dout, L, params, act, gy, gdy, glap,
-                              partial, P, (hipStream_t)stream);
+  if (use_split_bwd(n, S, NT))
+    return dispatch_bwd_split(NT, S, mode == INSR_MODE_LAP, split_tiles(1, NT, S, n), x, (int)n, din, dout, L,
+                              params, act, gy, gdy, glap, partial, P, (hipStream_t)stream);
   return dispatch_bwd_wave(NT, S, mode == INSR_MODE_LAP, x, (int)n, din, dout, L, params, act, gy, gdy, glap,
                            partial, P, (hipStream_t)stream);
 }
 
-int insr_jet_partial_blocks(long n, int din, int mode) {
-  if (n <= 0) return 0;
-  return use_split_bwd(n, streams_for(din, mode)) ? (int)((n + 15) / 16) : (int)((n + kPts - 1) / kPts);
+int insr_jet_partial_blocks(long n, int din, int W, int mode) {
+  const int S = streams_for(din, mode), NT = nt_for(W);
+  if (S < 0 || NT < 0 || n < 0) return INSR_EINVAL;
+  if (n == 0) return 0;
+  if (!use_split_bwd(n, S, NT)) return (int)((n + kPts - 1) / kPts);
+  const int T = split_tiles(1, NT, S, n);
+  return (int)(((n + 15) / 16 + T - 1) / T);
+}
+
+int insr_jet_split_tiles(long n, int din, int W, int mode, int backward) {
+  const int S = streams_for(din, mode), NT = nt_for(W);
+  if (S < 0 || NT < 0 || n < 0) return INSR_EINVAL;
+  const bool split = backward ? use_split_bwd(n, S, NT) : use_split_fwd(n, NT);
+  return split ? split_tiles(backward ? 1 : 0, NT, S, n) : 0;
+}
+
+void insr_jet_set_split_tiles(int fwd_tiles, int bwd_tiles, int min_blocks) {
+  tiles_init();
+  g_tiles[0] = fwd_tiles < 0 ? 0 : fwd_tiles;
+  g_tiles[1] = bwd_tiles < 0 ? 0 : bwd_tiles;
+  g_tiles[2] = min_blocks < 1 ? 1 : min_blocks;
+}
+
+void insr_jet_get_split_tiles(int* fwd_tiles, int* bwd_tiles, int* min_blocks) {
+  tiles_init();
+  if (fwd_tiles) *fwd_tiles = g_tiles[0];
+  if (bwd_tiles) *bwd_tiles = g_tiles[1];
+  if (min_blocks) *min_blocks = g_tiles[2];
 }
 
 int insr_jet_split_threshold(void) { return split_max_n(); }

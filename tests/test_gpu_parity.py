@@ -23,15 +23,19 @@ NETS = {  # name: (d_in, d_out, L, W)
     "el2d": (2, 2, 5, 128),
     "small32": (2, 3, 2, 32),
     "el3d_w64": (3, 3, 3, 64),
+    "el3d": (3, 3, 5, 256),          # elasticity3D bunny: width 256
+    "w256_lap": (2, 1, 2, 256),      # width 256 with the 4-stream Laplacian jet
 }
 
 
 BIG = 1 << 30
-VARIANTS = {  # (fwd, bwd, bwd_value) split thresholds
-    "wave": (0, 0, 0),                 # one wave per 16-point tile, both directions
-    "split": (BIG, BIG, BIG),          # 4 waves per 16-point tile, both directions
-    "split_fwd_wave_bwd": (BIG, 0, 0),  # mixed: the saved-activation layout is shared
-    "wave_fwd_split_bwd": (0, BIG, BIG),
+VARIANTS = {  # (fwd, bwd, bwd_value) split thresholds, (fwd, bwd) forced tiles per split block
+    "wave": ((0, 0, 0), (0, 0)),                  # one wave per 16-point tile, both directions
+    "split": ((BIG, BIG, BIG), (1, 1)),           # neurons split over a block's waves, 1 tile/block
+    "split_t2": ((BIG, BIG, BIG), (2, 2)),        # 2 tiles per block (ragged last block)
+    "split_t4": ((BIG, BIG, BIG), (4, 4)),        # 4 tiles per block (capped by LDS)
+    "split_fwd_wave_bwd": ((BIG, 0, 0), (4, 0)),  # mixed: the saved-activation layout is shared
+    "wave_fwd_split_bwd": ((0, BIG, BIG), (0, 2)),
 }
 
 
@@ -42,10 +46,13 @@ def base(request):
         pytest.skip("no GPU")
     import base as B
     B._native.load()
-    old = B._native.get_split_thresholds()
-    B._native.set_split_thresholds(*VARIANTS[request.param])
+    old, old_tiles = B._native.get_split_thresholds(), B._native.get_split_tiles()
+    thr, tiles = VARIANTS[request.param]
+    B._native.set_split_thresholds(*thr)
+    B._native.set_split_tiles(tiles[0], tiles[1], old_tiles[2])
     yield B
     B._native.set_split_thresholds(*old)
+    B._native.set_split_tiles(*old_tiles)
 
 
 def nerr(a, b):
@@ -179,3 +186,30 @@ def test_no_grad_jets_skip_saving(base):
     assert not y.requires_grad
     d = base.divergence(net(x), x).detach()
     assert torch.isfinite(d).all()
+
+
+@pytest.mark.parametrize("op", ["value", "laplace", "divergence"])
+def test_large_batch_default_policy(base, op):
+    """Batches large enough for the automatic multi-tile choice (T = 2 / 4)."""
+    old_tiles = base._native.get_split_tiles()
+    base._native.set_split_tiles(0, 0, old_tiles[2])
+    try:
+        name = "fluid_pres" if op != "divergence" else "fluid_vel"
+        din = NETS[name][0]
+        ref, net = pair(base, name, seed=6)
+        n = 20000
+        x = torch.rand(n, din, generator=torch.Generator().manual_seed(13)) * 2 - 1
+        xr = x.clone().requires_grad_(True)
+        xg = x.cuda().requires_grad_(True)
+        if op == "value":
+            v_ref, v = ref(xr), net(xg)
+        else:
+            v_ref, v = ORACLE_OPS[op](ref(xr), xr), _ops(base, net(xg), xg)[op]()
+        assert nerr(v, v_ref) < TOL
+        R = torch.randn(v_ref.shape, generator=torch.Generator().manual_seed(14))
+        (v_ref * R).sum().backward()
+        (v * R.cuda()).sum().backward()
+        for k, e in param_errs(ref, net):
+            assert e < TOL, (op, k, e)
+    finally:
+        base._native.set_split_tiles(*old_tiles)

@@ -14,7 +14,15 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "insr-pde_amd")]
 import torch  # noqa: E402
 
 NETS = {"fluid_pres": (2, 1, 4, 128), "fluid_vel": (2, 2, 4, 128), "advect": (1, 1, 3, 64),
-        "el2d": (2, 2, 5, 128)}
+        "el2d": (2, 2, 5, 128), "el3d": (3, 3, 5, 256)}
+BIG = 1 << 30
+VARIANTS = {  # label: ((fwd, bwd, bwd_value) thresholds, (fwd, bwd) forced tiles)
+    "wave": ((0, 0, 0), (0, 0)),
+    "split1": ((BIG, BIG, BIG), (1, 1)),
+    "split2": ((BIG, BIG, BIG), (2, 2)),
+    "split4": ((BIG, BIG, BIG), (4, 4)),
+    "auto": ((BIG, BIG, BIG), (0, 0)),
+}
 MODES = {"value": 0, "grad": 1, "lap": 2}
 
 
@@ -40,6 +48,7 @@ def main():
     ap.add_argument("--sizes", default="324,2048,8192,16384,65536")
     ap.add_argument("--modes", default="value,grad,lap")
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--variants", default=",".join(VARIANTS))
     args = ap.parse_args()
     import base
     from base import _native as nat
@@ -65,10 +74,16 @@ def main():
                 act = torch.empty(lib.insr_jet_act_bytes(n, din, L, W, mode) // 4, device="cuda")
                 g = torch.zeros(P, device="cuda")
                 st = nat.stream_of(x.device)
-                for variant, thr in (("wave", 0), ("split", 1 << 30)):
-                    lib.insr_jet_set_split_threshold(thr)
+                for variant in args.variants.split(","):
+                    thr, tiles = VARIANTS[variant]
+                    if W > 128 and variant == "wave":
+                        continue
+                    nat.set_split_thresholds(*thr)
+                    nat.set_split_tiles(tiles[0], tiles[1], 512)
                     part = torch.empty(max(lib.insr_jet_partial_bytes(n, din, dout, L, W, mode) // 4, 1), device="cuda")
-                    nb = lib.insr_jet_partial_blocks(n, din, mode)
+                    nb = lib.insr_jet_partial_blocks(n, din, W, mode)
+                    tf_, tb_ = (lib.insr_jet_split_tiles(n, din, W, mode, 0),
+                                lib.insr_jet_split_tiles(n, din, W, mode, 1))
 
                     def fwd():
                         nat.check(lib.insr_siren_jet_fwd(nat.ptr(x), n, din, dout, L, W, mode, nat.ptr(flat),
@@ -88,7 +103,8 @@ def main():
                     tb = time_it(bwd, args.reps)
                     tr = time_it(red, args.reps)
                     macs = P_macs(din, dout, L, W)
-                    rec = {"net": name, "mode": mname, "n": n, "variant": variant, "fwd_us": round(tf, 2),
+                    rec = {"net": name, "mode": mname, "n": n, "variant": variant, "T": [tf_, tb_], "nb": nb,
+                           "fwd_us": round(tf, 2),
                            "bwd_us": round(tb, 2), "reduce_us": round(tr, 2),
                            "fwd_tflops": round(n * S * 2 * macs / tf / 1e6, 2),
                            "bwd_tflops": round(n * S * 4 * macs / tb / 1e6, 2)}
