@@ -156,16 +156,64 @@ def run_jet(mlp, x, mode):
     return y, dy, lap
 
 
+# --------------------------------------------------------------------------
+# jet-mode hints: inside a training loop the phase body makes the same calls every
+# iteration, so when the value of call #k of a network was later differentiated
+# (gradient / divergence / jacobian / laplace), iteration i+1 runs that call's
+# forward directly as the derivative jet: the value is the jet's value stream
+# (bit-identical to the value-only kernel), the diff op is served from the cache,
+# and one reverse jet handles every adjoint -- no wasted value-only forward and
+# backward.  A wrong hint costs time, never correctness: the cache is keyed by the
+# exact value tensor / node, and a miss computes the requested jet as usual.
+# --------------------------------------------------------------------------
+class _HintScope:
+    hints = None     # {(id(mlp), ordinal): mode} of the active loop, or None
+    counts = None    # {id(mlp): calls so far in this iteration}
+
+
+class call_scope:
+    """`with call_scope(owner):` around one iteration of a phase body; hints live on
+    `owner` (the PhaseLoop), so they persist across its iterations only."""
+
+    def __init__(self, owner):
+        if not hasattr(owner, "_insr_jet_hints"):
+            owner._insr_jet_hints = {}
+        self.hints = owner._insr_jet_hints
+
+    def __enter__(self):
+        self.saved = (_HintScope.hints, _HintScope.counts)
+        _HintScope.hints, _HintScope.counts = self.hints, {}
+        return self
+
+    def __exit__(self, *exc):
+        _HintScope.hints, _HintScope.counts = self.saved
+        return False
+
+
+def _supported(mlp, mode):
+    return bool(nat.lib().insr_siren_supported(mlp.in_features, mlp.out_features, mlp.num_hidden_layers,
+                                               mlp.hidden_features, mode))
+
+
 def siren_value(mlp, x):
     """MLP.forward.  Provenance lives on the tensor AND on its autograd node, because
     in `q = mlp(x) + x` the value tensor itself is a dropped temporary; only the node
     survives inside q's graph."""
-    y, _, _ = run_jet(mlp, x, nat.MODE_VALUE)
-    jets = {}
-    y._insr_src, y._insr_jets = (mlp, x), jets
+    key, mode = None, nat.MODE_VALUE
+    if _HintScope.hints is not None:
+        ordinal = _HintScope.counts.get(id(mlp), 0)
+        _HintScope.counts[id(mlp)] = ordinal + 1
+        key = (id(mlp), ordinal)
+        mode = _HintScope.hints.get(key, nat.MODE_VALUE)
+        if mode != nat.MODE_VALUE and not (x.requires_grad and _supported(mlp, mode)):
+            mode = nat.MODE_VALUE
+    res = run_jet(mlp, x, mode)
+    y = res[0]
+    jets = {} if mode == nat.MODE_VALUE else {mode: res}
+    y._insr_src, y._insr_jets, y._insr_key = (mlp, x), jets, key
     node = y.grad_fn
     if node is not None:
-        node._insr_src, node._insr_jets = (mlp, x), jets
+        node._insr_src, node._insr_jets, node._insr_key = (mlp, x), jets, key
     return y
 
 
@@ -207,12 +255,16 @@ def match(y, x):
 
 
 def jet_of(mlp, holder, x, mode):
-    """Derivative jets are cached on the value tensor / node; a LAP jet also serves GRAD."""
+    """Derivative jets are cached on the value tensor / node; a LAP jet also serves GRAD.
+    A miss inside a hint scope records the mode for this call site's next iteration."""
     cache = getattr(holder, "_insr_jets", None)
     if cache is not None:
         for m in ((nat.MODE_LAP,) if mode == nat.MODE_LAP else (nat.MODE_GRAD, nat.MODE_LAP)):
             if m in cache:
                 return cache[m]
+    key = getattr(holder, "_insr_key", None)
+    if key is not None and _HintScope.hints is not None:
+        _HintScope.hints[key] = max(_HintScope.hints.get(key, nat.MODE_VALUE), mode)
     res = run_jet(mlp, x, mode)
     if cache is not None:
         cache[mode] = res

@@ -17,6 +17,8 @@ Differences, all controlled by cfg attributes:
 """
 import torch
 
+from . import _jet
+
 try:
     from tqdm import tqdm
 except Exception:  # pragma: no cover
@@ -45,7 +47,8 @@ class PhaseLoop:
 
     def _body(self):
         self.m.optimizer, self.m.scheduler = self.opt, self.sched
-        loss_dict = self.func(self.m, *self.args, **self.kwargs)
+        with _jet.call_scope(self):
+            loss_dict = self.func(self.m, *self.args, **self.kwargs)
         synced = self.m._update_network(loss_dict)
         return synced if isinstance(synced, dict) else loss_dict
 
@@ -53,7 +56,8 @@ class PhaseLoop:
     def _stage1(self):
         m = self.m
         m.optimizer, m.scheduler = self.opt, self.sched
-        loss_dict = self.func(m, *self.args, **self.kwargs)
+        with _jet.call_scope(self):
+            loss_dict = self.func(m, *self.args, **self.kwargs)
         loss = sum(loss_dict.values())
         m.optimizer.zero_grad()
         loss.backward()

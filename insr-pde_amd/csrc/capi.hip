@@ -65,7 +65,7 @@ static void tiles_init() {
   if (g_tiles[0] < 0) {
     g_tiles[0] = env_or("INSR_SPLIT_TILES_FWD", 0);
     g_tiles[1] = env_or("INSR_SPLIT_TILES_BWD", 0);
-    g_tiles[2] = env_or("INSR_SPLIT_MIN_BLOCKS", 512);
+    g_tiles[2] = env_or("INSR_SPLIT_MIN_BLOCKS", 256);
   }
 }
 

@@ -55,6 +55,9 @@ def check_update(after_hip, before, after_ref, g_ref):
     assert np.abs(d_hip - d_ref).max() <= 2 * 2 * 1e-4 * 1.01
 
 
+from base import _jet  # noqa: E402
+
+
 def _cfg(pde, **kw):
     from pde.config import make_config
     kw.setdefault("insr_progress", False)
@@ -105,12 +108,16 @@ def test_fluid_phases(ph):
         reset()
         model._reset_optimizer()
         trace = []
+        owner = types.SimpleNamespace()  # jet-mode hints: iteration 1 replays iteration 0's diff ops
         for it in range(2):
             patch(it)
-            ld = body(model)
+            with _jet.call_scope(owner):
+                ld = body(model)
             model._update_network(ld)
             trace.append([float(ld[k]) for k in sorted(ld)])
         assert nerr(np.array(trace), ph[f"fluid/{phase}/loss_trace"]) < TOL
+        if phase != "_advect_velocity":  # divergence / laplace / gradient of network values
+            assert owner._insr_jet_hints, phase
         for key, net, g_ref in (("vel", model.velocity_field, ph[f"fluid/{phase}/grad_vel"]),
                                 ("pres", model.pressure_field, gp)):
             if np.abs(g_ref).max() > 0:
@@ -147,9 +154,11 @@ def test_advect_phase(ph):
         set_flat(model.field, ph["advect/field/params0"])
         model._reset_optimizer()
         trace = []
+        owner = types.SimpleNamespace()  # jet-mode hints: iteration 1 replays iteration 0's diff ops
         for it in range(2):
             patch(it)
-            ld = body(model)
+            with _jet.call_scope(owner):
+                ld = body(model)
             model._update_network(ld)
             trace.append([float(ld[k]) for k in sorted(ld)])
         assert nerr(np.array(trace), ph["advect/_advect/loss_trace"]) < TOL
@@ -190,9 +199,11 @@ def test_elasticity_phase(ph):
     set_flat(model.deformation_field, ph["el2d/f/params0"])
     model._reset_optimizer()
     trace = []
+    owner = types.SimpleNamespace()  # jet-mode hints: iteration 1 replays iteration 0's diff ops
     for it in range(2):
         patch(it)
-        ld = body(model)
+        with _jet.call_scope(owner):
+            ld = body(model)
         model._update_network(ld)
         trace.append([float(ld[k]) for k in sorted(ld)])
     assert nerr(np.array(trace), ph["el2d/_solve_deformation/loss_trace"]) < TOL
