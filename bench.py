@@ -143,10 +143,44 @@ def roofline(model, loops, n_local, P_pres):
     flops = n * streams * passes * 2 * P
     achieved = flops / (ms * 1e-3) / 1e12
     table = {f"{k[0]}:{k[1]}:n{k[2]}": round(v, 4) for k, v in sorted(per_step.items(), key=lambda t: -t[1])}
+    din = 2
+    kname, grid = kernel_identity(kind, mode, n, din, W)
+    traffic, tsrc = pmc_traffic(kname, grid)
     return {"bound": "mfma", "achieved": round(achieved, 2), "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-            "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": None,
-            "kernel": f"jet_{kind}_kernel<{mode}> n={n} W={W}", "avg_ms": round(ms, 4),
+            "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": traffic,
+            "traffic_unit": "bytes/launch (HBM: corrected FETCH_SIZE + WRITE_SIZE)", "traffic_source": tsrc,
+            "kernel": f"{kname} grid={grid} (n={n}, W={W}, {mode} jet {kind})", "avg_ms": round(ms, 4),
             "algorithmic_gflop_per_launch": round(flops / 1e9, 3), "per_step_ms_by_launch": table}
+
+
+def kernel_identity(kind, mode, n, din, W):
+    """The rocprof name and grid (threads) of the jet kernel the library picks for this launch."""
+    from base import _native as nat
+    lib = nat.lib()
+    m = {"value": nat.MODE_VALUE, "grad": nat.MODE_GRAD, "lap": nat.MODE_LAP}[mode]
+    S = {"value": 1, "grad": 1 + din, "lap": 2 + din}[mode]
+    NT = W // 16
+    lap = "true" if mode == "lap" else "false"
+    T = lib.insr_jet_split_tiles(n, din, W, m, 1 if kind == "bwd" else 0)
+    if T > 0:
+        nb = ((n + 15) // 16 + T - 1) // T
+        return f"insr::jet_{kind}_split<{NT}, {S}, {lap}, {T}>", nb * 64 * min(NT, 8)
+    return f"insr::jet_{kind}_wave<{NT}, {S}, {lap}>", ((n + 63) // 64) * 256
+
+
+def pmc_traffic(kname, grid):
+    """HBM bytes per launch of this kernel from the committed rocprofv3 --pmc summary
+    (profiles/pmc_traffic.json, written by tools/pmc_summary.py from separate
+    FETCH_SIZE / WRITE_SIZE passes of this benchmark); None if not profiled."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        tab = json.load(open(path))
+    except (OSError, ValueError):
+        return None, None
+    e = tab.get(f"{kname}|grid={grid}")
+    if not e or "fetch_bytes" not in e or "write_bytes" not in e:
+        return None, None
+    return e["fetch_bytes"] + e["write_bytes"], tab.get("_source")
 
 
 def cpu_baseline(seconds):
