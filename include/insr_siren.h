@@ -166,6 +166,34 @@ int insr_adam_step(float* params, const float* grads, float* exp_avg, float* exp
                    long count, const float* opt_state, float beta1, float beta2, float eps,
                    void* stream);
 
+/*
+ * Fused squared-residual losses (the reductions that close every phase's PDE
+ * residual: fluid/model.py:96-101,121-125,147-151, the wall terms :90-94,129-133,
+ * advection/model.py:78-91).  One launch forward, one backward.
+ *   INSR_LOSS_COMBO  out = scale * sum_{i<n} r_i^2,
+ *                    r = alpha (a + beta b) + gamma (c + delta d), evaluated in that
+ *                    order; b, c, d may be NULL (= 0; d needs c); all contiguous, n elements
+ *   INSR_LOSS_BANDS  out = scale * (sum_{r<n} y[r][0]^2 + sum_{r<n} y[n+r][1]^2)
+ *                    (a = y, (2n, m) row-major, m >= 2; b = c = d = NULL)
+ * The forward reduction is deterministic: fixed per-block order, partials summed
+ * by the last block in block order.  `work` (insr_sq_loss_work_floats() floats) and
+ * `ticket` (one zero-initialised unsigned int, reset by the kernel) are a workspace
+ * that launches sharing it must not use concurrently (one stream); only touched when
+ * n is large enough for more than one block.
+ * Backward: g = 2 scale gout r;  ga = alpha g, gb = alpha beta g, gc = gamma g,
+ * gd = gamma delta g (bands: ga = the full (2n, m) gradient, zeros outside the
+ * selected columns); any output may be NULL (bands: ga required).
+ */
+#define INSR_LOSS_COMBO 0
+#define INSR_LOSS_BANDS 1
+long insr_sq_loss_work_floats(void);
+int insr_sq_loss_fwd(int kind, const float* a, const float* b, const float* c, const float* d, long n, int m,
+                     float alpha, float beta, float gamma, float delta, float scale, float* out, float* work,
+                     unsigned int* ticket, void* stream);
+int insr_sq_loss_bwd(int kind, const float* a, const float* b, const float* c, const float* d, long n, int m,
+                     float alpha, float beta, float gamma, float delta, float scale, const float* gout, float* ga,
+                     float* gb, float* gc, float* gd, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -58,9 +58,8 @@ class PhaseLoop:
         m.optimizer, m.scheduler = self.opt, self.sched
         with _jet.call_scope(self):
             loss_dict = self.func(m, *self.args, **self.kwargs)
-        loss = sum(loss_dict.values())
         m.optimizer.zero_grad()
-        loss.backward()
+        m._backward(loss_dict)
         return loss_dict
 
     def _stage2(self):

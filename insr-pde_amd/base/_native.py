@@ -14,6 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("INSR_HIP_LIB", os.path.join(os.path.dirname(_HERE), "lib", "libinsr_hip.so"))
 
 MODE_VALUE, MODE_GRAD, MODE_LAP = 0, 1, 2
+LOSS_COMBO, LOSS_BANDS = 0, 1
 OPT_LR, OPT_STEP, OPT_BEST, OPT_BAD, OPT_STEPSIZE, OPT_BC2SQRT, OPT_FACTOR, OPT_MINLR = range(8)
 OPT_NFLOATS = 8
 ADAM_MAX_TENSORS = 8
@@ -38,6 +39,9 @@ SIGNATURES = {
     "insr_jet_get_split_thresholds": (None, [_P, _P, _P]),
     "insr_jet_set_split_thresholds": (None, [_I, _I, _I]),
     "insr_jet_split_tiles": (_I, [_L, _I, _I, _I, _I]),
+    "insr_sq_loss_work_floats": (_L, []),
+    "insr_sq_loss_fwd": (_I, [_I, _P, _P, _P, _P, _L, _I, _F, _F, _F, _F, _F, _P, _P, _P, _P]),
+    "insr_sq_loss_bwd": (_I, [_I, _P, _P, _P, _P, _L, _I, _F, _F, _F, _F, _F, _P, _P, _P, _P, _P, _P]),
     "insr_jet_set_split_tiles": (None, [_I, _I, _I]),
     "insr_jet_get_split_tiles": (None, [_P, _P, _P]),
     "insr_reduce_partials": (_I, [_P, _I, _L, _P, _I, _P]),

@@ -159,15 +159,28 @@ class BaseModel(ABC):
         return {k: red[i] for i, k in enumerate(keys)}
 
     def _update_network(self, loss_dict):
-        """update network by back propagation (base/baseModel.py:73-81)"""
-        loss = sum(loss_dict.values())
+        """update network by back propagation (base/baseModel.py:73-81).  backward of
+        sum(loss_dict.values()) is run as backward of every term with a persistent unit
+        seed: the same gradients without the add and ones-fill launches."""
         self.optimizer.zero_grad()
-        loss.backward()
+        self._backward(loss_dict)
         synced = self._dp_sync(loss_dict)
         self.optimizer.step()
         if self.scheduler is not None:
             self.scheduler.step(synced['main'])
         return synced
+
+    def _backward(self, loss_dict):
+        terms = [v for v in loss_dict.values() if v.requires_grad]
+        if terms:
+            torch.autograd.backward(terms, grad_tensors=[self._unit_seed(v) for v in terms])
+
+    def _unit_seed(self, v):
+        seeds = self.__dict__.setdefault("_insr_seeds", {})
+        key = (v.device, v.dtype, tuple(v.shape))
+        if key not in seeds:
+            seeds[key] = torch.ones(v.shape, device=v.device, dtype=v.dtype)
+        return seeds[key]
 
     def _set_require_grads(self, model, require_grad):
         for p in model.parameters():

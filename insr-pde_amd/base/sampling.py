@@ -11,7 +11,8 @@ import torch
 
 _AFFINE = {}  # (N, side-key, epsilon, device) -> (scale, shift) constant tensors
 
-__all__ = ["sample_uniform", "sample_random", "sample_boundary", "sample_boundary2D_separate"]
+__all__ = ["sample_uniform", "sample_random", "sample_boundary", "sample_boundary2D_separate",
+           "sample_boundary2D_pair"]
 
 
 def sample_uniform(resolution, sdim=1, device="cpu", flatten=True):
@@ -76,4 +77,15 @@ def sample_boundary2D_separate(N, side, epsilon=1e-4, device='cpu'):
         raise RuntimeError
     if torch.device(device).type == "cuda":
         return _fused_bands(N // 2, faces, (side, epsilon), device)
+    return torch.cat([_band(N // 2, f, device) for f in faces], dim=0)
+
+
+def sample_boundary2D_pair(N, epsilon=1e-4, device='cpu'):
+    """torch.cat([sample_boundary2D_separate(N, 'horizontal'), sample_boundary2D_separate(N,
+    'vertical')]) -- the x-face bands then the y-face bands, N//2 points per face -- as
+    one draw (the fluid wall terms use both band pairs together, fluid/model.py:90-94)."""
+    full, lo, hi = (-1, 1), (-1 - epsilon, -1 + epsilon), (1 - epsilon, 1 + epsilon)
+    faces = [(lo, full), (hi, full), (full, lo), (full, hi)]
+    if torch.device(device).type == "cuda":
+        return _fused_bands(N // 2, faces, ("pair", epsilon), device)
     return torch.cat([_band(N // 2, f, device) for f in faces], dim=0)

@@ -1,0 +1,156 @@
+// residual.hip -- fused squared-residual losses of the model phases.
+//
+// The reference writes every PDE residual loss as a chain of aten ops, e.g.
+//   torch.mean((u - u_target) ** 2)                       fluid/model.py:96-101
+//   torch.mean((div_u - lap_p) ** 2)                       fluid/model.py:121-125
+//   torch.mean((u - (u_prev - grad_p)) ** 2)               fluid/model.py:147-151
+//   mean(u[:nb, 0] ** 2) + mean(u[nb:, 1] ** 2)  (walls)   fluid/model.py:90-94,129-133
+// i.e. 3-5 launches forward and as many backward (sub, pow, mean, slice/select
+// backward zero-fills, ...).  On the GPU each of those is a ~3 us launch over a few
+// hundred KB, so they cost more than they compute.  Here a loss is ONE launch
+// forward (a deterministic two-level reduction: fixed per-block order, partials
+// combined by the last block in block order) and ONE launch backward (the
+// residual is recomputed, every input gradient written in the same pass).
+#include "jet_common.hpp"
+
+namespace insr {
+
+constexpr int kLossThreads = 512;
+constexpr int kLossMaxBlocks = 256;
+constexpr long kLossPerBlock = 8192;  // elements per block before the grid grows
+
+struct LossIn {
+  const float* a;
+  const float* b;
+  const float* c;
+  const float* d;
+  float alpha, beta, gamma, delta;
+};
+
+// r = alpha (a + beta b) + gamma (c + delta d), evaluated in exactly that order
+// (the reference's rounding for (u - u0)/dt + v (ux + u0x)/2 and u - (u_prev - grad_p))
+__device__ __forceinline__ float combo_residual(const LossIn& in, long i) {
+  float p = in.a[i];
+  if (in.b) p = p + in.beta * in.b[i];
+  p = in.alpha * p;
+  if (in.c) {
+    float q = in.c[i];
+    if (in.d) q = q + in.delta * in.d[i];
+    p = p + in.gamma * q;
+  }
+  return p;
+}
+
+__device__ __forceinline__ float loss_term(int kind, const LossIn& in, long n, int m, long i) {
+  if (kind == INSR_LOSS_COMBO) {
+    const float r = combo_residual(in, i);
+    return r * r;
+  }
+  const float* a = in.a;
+  // INSR_LOSS_BANDS: element i < 2n is row i; band 0 (rows < n) uses column 0, band 1 column 1
+  const float v = a[i * m + (i < n ? 0 : 1)];
+  return v * v;
+}
+
+__global__ __launch_bounds__(kLossThreads) void sq_loss_fwd_kernel(int kind, LossIn in, long n, int m, float scale,
+                                                                   float* __restrict__ out, float* work,
+                                                                   unsigned int* ticket) {
+  __shared__ float red[kLossThreads / 64];
+  const long count = kind == INSR_LOSS_COMBO ? n : 2 * n;
+  float acc = 0.f;
+  for (long i = (long)blockIdx.x * kLossThreads + threadIdx.x; i < count; i += (long)gridDim.x * kLossThreads)
+    acc += loss_term(kind, in, n, m, i);
+  // wave reduction (fixed butterfly order), then the block's waves in order
+  for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane == 0) red[w] = acc;
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  float part = 0.f;
+  for (int k = 0; k < kLossThreads / 64; ++k) part += red[k];
+  if (gridDim.x == 1) {
+    out[0] = scale * part;
+    return;
+  }
+  __hip_atomic_store(work + blockIdx.x, part, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __threadfence();  // release the partial (agent scope: the L2s are per XCD)
+  const unsigned int done = atomicAdd(ticket, 1u);
+  if (done == gridDim.x - 1) {  // last block: combine the partials in block order
+    __threadfence();  // acquire every block's partial
+    float tot = 0.f;
+    for (unsigned int k = 0; k < gridDim.x; ++k) tot += __hip_atomic_load(work + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    out[0] = scale * tot;
+    *ticket = 0u;  // ready for the next launch on this stream (and graph replays)
+  }
+}
+
+__global__ __launch_bounds__(256) void sq_loss_bwd_kernel(int kind, LossIn in, long n, int m, float scale,
+                                                          const float* __restrict__ gout, float* __restrict__ ga,
+                                                          float* __restrict__ gb, float* __restrict__ gc,
+                                                          float* __restrict__ gd) {
+  const float g2 = 2.f * scale * gout[0];
+  if (kind == INSR_LOSS_COMBO) {
+    const float ca = in.alpha, cb = in.alpha * in.beta, cc = in.gamma, cd = in.gamma * in.delta;
+    for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+      const float g = g2 * combo_residual(in, i);
+      if (ga) ga[i] = ca * g;
+      if (gb) gb[i] = cb * g;
+      if (gc) gc[i] = cc * g;
+      if (gd) gd[i] = cd * g;
+    }
+    return;
+  }
+  // bands: the full (2n, m) gradient, zero outside the selected columns
+  const long total = 2 * n * m;
+  for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < total; e += (long)gridDim.x * 256) {
+    const long row = e / m;
+    const int col = (int)(e - row * m);
+    const int sel = row < n ? 0 : 1;
+    ga[e] = col == sel ? g2 * in.a[e] : 0.f;
+  }
+}
+
+}  // namespace insr
+
+using namespace insr;
+
+extern "C" {
+
+long insr_sq_loss_work_floats(void) { return kLossMaxBlocks; }
+
+int insr_sq_loss_fwd(int kind, const float* a, const float* b, const float* c, const float* d, long n, int m,
+                     float alpha, float beta, float gamma, float delta, float scale, float* out, float* work,
+                     unsigned int* ticket, void* stream) {
+  if (!a || !out || n < 0) return INSR_EINVAL;
+  if (kind == INSR_LOSS_BANDS && (m < 2 || b || c || d)) return INSR_EINVAL;
+  if (kind != INSR_LOSS_COMBO && kind != INSR_LOSS_BANDS) return INSR_EINVAL;
+  if (d && !c) return INSR_EINVAL;
+  const long count = kind == INSR_LOSS_COMBO ? n : 2 * n;
+  long nb = (count + kLossPerBlock - 1) / kLossPerBlock;
+  if (nb < 1) nb = 1;
+  if (nb > kLossMaxBlocks) nb = kLossMaxBlocks;
+  if (nb > 1 && (!work || !ticket)) return INSR_EINVAL;
+  const LossIn in{a, b, c, d, alpha, beta, gamma, delta};
+  hipLaunchKernelGGL(sq_loss_fwd_kernel, dim3((unsigned)nb), dim3(kLossThreads), 0, (hipStream_t)stream, kind, in, n,
+                     m, scale, out, work, ticket);
+  return (int)hipGetLastError();
+}
+
+int insr_sq_loss_bwd(int kind, const float* a, const float* b, const float* c, const float* d, long n, int m,
+                     float alpha, float beta, float gamma, float delta, float scale, const float* gout, float* ga,
+                     float* gb, float* gc, float* gd, void* stream) {
+  if (!a || !gout || n < 0) return INSR_EINVAL;
+  if (kind == INSR_LOSS_BANDS && (m < 2 || !ga || b || c || d || gb || gc || gd)) return INSR_EINVAL;
+  if (kind != INSR_LOSS_COMBO && kind != INSR_LOSS_BANDS) return INSR_EINVAL;
+  if (d && !c) return INSR_EINVAL;
+  const long total = kind == INSR_LOSS_COMBO ? n : 2 * n * m;
+  if (total == 0) return 0;
+  long nb = (total + 255) / 256;
+  if (nb > 2048) nb = 2048;
+  const LossIn in{a, b, c, d, alpha, beta, gamma, delta};
+  hipLaunchKernelGGL(sq_loss_bwd_kernel, dim3((unsigned)nb), dim3(256), 0, (hipStream_t)stream, kind, in, n, m, scale,
+                     gout, ga, gb, gc, gd);
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

@@ -14,9 +14,9 @@ import os
 
 import numpy as np
 import torch
-import torch.nn.functional as F
 
-from base import BaseModel, divergence, gradient, laplace, sample_boundary2D_separate, sample_random, sample_uniform
+from base import (BaseModel, divergence, fused_mse, gradient, laplace, sample_boundary2D_pair,
+                  sample_boundary2D_separate, sample_random, sample_uniform, wall_mse)
 
 from .examples import get_examples
 
@@ -51,6 +51,17 @@ class Fluid2DModel(BaseModel):
         by = sample_boundary2D_separate(nb, side='vertical', device=self.device).requires_grad_(True)
         return bx, by
 
+    def _boundary_bands(self, n_interior):
+        """Both band pairs as one (2 nb, 2) tensor [x-face bands; y-face bands] and nb.
+        One sampler draw and one jet launch for both (a band is ~1% of the points, so
+        these launches are latency-bound).  An instance-level `_boundary_pair` hook
+        (tests pass recorded samples) takes precedence."""
+        if "_boundary_pair" in self.__dict__:
+            bx, by = self._boundary_pair(n_interior)
+            return torch.cat([bx, by]), bx.shape[0]
+        bxy = sample_boundary2D_pair(n_interior // 100, device=self.device).requires_grad_(True)
+        return bxy, bxy.shape[0] // 2
+
     def sample_field(self, resolution, return_samples=False):
         grid = sample_uniform(resolution, 2, device=self.device, flatten=False).requires_grad_(True)
         u = self.velocity_field(grid)
@@ -66,7 +77,7 @@ class Fluid2DModel(BaseModel):
     @BaseModel._training_loop
     def _initialize(self):
         x = self._sample_in_training()
-        return {'main': F.mse_loss(self.velocity_field(x), self.init_cond_func(x))}
+        return {'main': fused_mse(self.velocity_field(x), self.init_cond_func(x))}
 
     @BaseModel._timestepping
     def step(self):
@@ -77,14 +88,10 @@ class Fluid2DModel(BaseModel):
         self._projection()
 
     def _wall_loss(self, n_interior):
-        """u_x = 0 on the x-faces, u_y = 0 on the y-faces (mean squares).  Both
-        bands go through ONE jet launch (a band is ~1% of the points: these
-        launches are latency-bound, so two of them cost twice one)."""
-        bx, by = self._boundary_pair(n_interior)
-        nb = bx.shape[0]
-        u = self.velocity_field(torch.cat([bx, by]))
-        ux, uy = u[:nb, 0], u[nb:, 1]
-        return (torch.mean(ux ** 2) + torch.mean(uy ** 2)) * 1.0
+        """u_x = 0 on the x-faces, u_y = 0 on the y-faces: mean(u_x^2) + mean(u_y^2)
+        (fluid/model.py:90-94) as one jet launch and one fused loss launch."""
+        bxy, nb = self._boundary_bands(n_interior)
+        return wall_mse(self.velocity_field(bxy), nb)
 
     @BaseModel._training_loop
     def _advect_velocity(self):
@@ -92,10 +99,10 @@ class Fluid2DModel(BaseModel):
         with torch.no_grad():
             u_prev = self.velocity_field_prev(x).detach()
         u = self.velocity_field(x)
-        foot = torch.clamp(x - u_prev * self.cfg.dt, min=-1.0, max=1.0)
         with torch.no_grad():
-            u_target = self.velocity_field_prev(foot).detach()
-        return {'main': torch.mean((u - u_target) ** 2), 'bc': self._wall_loss(x.shape[0])}
+            foot = torch.add(x, u_prev, alpha=-self.cfg.dt).clamp_(-1.0, 1.0)
+            u_target = self.velocity_field_prev(foot)
+        return {'main': fused_mse(u, u_target), 'bc': self._wall_loss(x.shape[0])}
 
     @BaseModel._training_loop
     def _solve_pressure(self):
@@ -103,12 +110,10 @@ class Fluid2DModel(BaseModel):
         with torch.no_grad():  # the reference detaches div u: no reverse jet, no saved streams
             div_u = divergence(self.velocity_field(x), x)
         lap_p = laplace(self.pressure_field(x), x)
-        main = torch.mean((div_u - lap_p) ** 2)  # rho = 1
-        bx, by = self._boundary_pair(x.shape[0])
-        nb, bxy = bx.shape[0], torch.cat([bx, by])  # one jet launch for both bands
+        main = fused_mse(div_u, lap_p)  # mean((div u - lap p)^2), rho = 1
+        bxy, nb = self._boundary_bands(x.shape[0])  # one jet launch for both bands
         gp = gradient(self.pressure_field(bxy), bxy)
-        dpx, dpy = gp[:nb, 0], gp[nb:, 1]
-        return {'main': main, 'bc': torch.mean(dpx ** 2) + torch.mean(dpy ** 2)}
+        return {'main': main, 'bc': wall_mse(gp, nb)}  # mean(dp/dx^2) + mean(dp/dy^2)
 
     @BaseModel._training_loop
     def _projection(self):
@@ -118,7 +123,8 @@ class Fluid2DModel(BaseModel):
         with torch.no_grad():  # detached in the reference as well
             grad_p = gradient(self.pressure_field(x), x)
         u = self.velocity_field(x)
-        return {'main': torch.mean((u - (u_prev - grad_p)) ** 2), 'bc': self._wall_loss(x.shape[0])}
+        # mean((u - (u_prev - grad_p))^2): r = 1*(u + 0) + (-1)*(u_prev + (-1)*grad_p)
+        return {'main': fused_mse(u, None, u_prev, grad_p, gamma=-1.0, delta=-1.0), 'bc': self._wall_loss(x.shape[0])}
 
     # ---- output (host side; figures are out of scope) ------------------------
     def write_output(self, output_folder):

@@ -1,0 +1,95 @@
+"""Fused residual losses (base.losses, residual.hip) vs the plain torch fp32 expressions
+the reference writes (fluid/model.py:90-151, advection/model.py:78-91).
+
+Tolerance: the fused forward sums in a different (deterministic) order than
+torch.mean, so losses agree to 1e-6 relative; gradients are elementwise formulas of
+the same residual and agree to 1e-6 relative normwise."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def B():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import base
+    base._native.load()
+    return base
+
+
+def rel(a, b):
+    return float((a.double() - b.double()).abs().max() / b.double().abs().max().clamp_min(1e-30))
+
+
+CASES = [  # (alpha, beta, gamma, delta, which of b, c, d present)
+    (1.0, -1.0, 1.0, 1.0, "b"),        # mean((u - target)^2)
+    (1.0, -1.0, 1.0, 1.0, ""),         # mean(u^2)
+    (1.0, 0.0, -1.0, -1.0, "cd"),      # u - (u_prev - grad_p)
+    (20.0, -1.0, 0.125, 1.0, "bcd"),   # (u - u0)/dt + v (ux + u0x)/2
+]
+
+
+@pytest.mark.parametrize("n", [1, 1000, 40000, 300000])
+@pytest.mark.parametrize("case", range(len(CASES)))
+def test_fused_mse_matches_torch(B, n, case):
+    alpha, beta, gamma, delta, which = CASES[case]
+    g = torch.Generator(device="cuda").manual_seed(n + case)
+    t = {k: torch.randn(n, 2, device="cuda", generator=g).requires_grad_(True) for k in "abcd"}
+    a = t["a"]
+    b, c, d = (t[k] if k in which else None for k in "bcd")
+
+    def ref():
+        p = a + beta * b if b is not None else a
+        p = alpha * p
+        if c is not None:
+            q = c + delta * d if d is not None else c
+            p = p + gamma * q
+        return torch.mean(p ** 2)
+
+    lr = ref()
+    gr = torch.autograd.grad(lr, [x for x in (a, b, c, d) if x is not None])
+    for _ in range(2):  # twice: the multi-block ticket must reset itself
+        lf = B.fused_mse(a, b, c, d, alpha=alpha, beta=beta, gamma=gamma, delta=delta)
+        assert rel(lf.detach(), lr.detach()) < 1e-6
+    gf = torch.autograd.grad(lf, [x for x in (a, b, c, d) if x is not None])
+    for x, y in zip(gf, gr):
+        assert rel(x, y) < 1e-6
+
+
+@pytest.mark.parametrize("nb", [1, 162, 654, 50000])
+def test_wall_mse_matches_torch(B, nb):
+    y = torch.randn(2 * nb, 3, device="cuda", generator=torch.Generator(device="cuda").manual_seed(nb))
+    y.requires_grad_(True)
+    lr = torch.mean(y[:nb, 0] ** 2) + torch.mean(y[nb:, 1] ** 2)
+    (gr,) = torch.autograd.grad(lr, y)
+    lf = B.wall_mse(y, nb)
+    assert rel(lf.detach(), lr.detach()) < 1e-6
+    (gf,) = torch.autograd.grad(lf, y)
+    assert rel(gf, gr) < 1e-6 and bool((gf[:nb, 1:] == 0).all()) and bool((gf[nb:, 0] == 0).all())
+
+
+def test_fused_mse_in_graph_replay(B):
+    """The ticketed multi-block reduction inside a captured hipGraph, replayed."""
+    x = torch.randn(200000, device="cuda")
+    y = torch.randn(200000, device="cuda")
+    B.fused_mse(x, y)  # workspace allocated outside the capture
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        B.fused_mse(x, y)
+        gr = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(gr, stream=s):
+            out = B.fused_mse(x, y)
+    torch.cuda.current_stream().wait_stream(s)
+    for k in range(3):
+        x.mul_(1.5)
+        gr.replay()
+        torch.cuda.synchronize()
+        assert rel(out, torch.mean((x - y) ** 2)) < 1e-6, k
+
+
+def test_losses_reject_cpu(B):
+    with pytest.raises(B.NativeUnavailable):
+        B.fused_mse(torch.ones(3))
