@@ -175,11 +175,10 @@ int insr_adam_step(float* params, const float* grads, float* exp_avg, float* exp
  *                    order; b, c, d may be NULL (= 0; d needs c); all contiguous, n elements
  *   INSR_LOSS_BANDS  out = scale * (sum_{r<n} y[r][0]^2 + sum_{r<n} y[n+r][1]^2)
  *                    (a = y, (2n, m) row-major, m >= 2; b = c = d = NULL)
- * The forward reduction is deterministic: fixed per-block order, partials summed
- * by the last block in block order.  `work` (insr_sq_loss_work_floats() floats) and
- * `ticket` (one zero-initialised unsigned int, reset by the kernel) are a workspace
- * that launches sharing it must not use concurrently (one stream); only touched when
- * n is large enough for more than one block.
+ * The forward reduction is deterministic (fixed order).  Up to 2^17 terms it is one
+ * launch; beyond, per-block partials go to `work` (insr_sq_loss_work_floats()
+ * floats, not shared by concurrent launches) and a second one-block launch combines
+ * them in block order.
  * Backward: g = 2 scale gout r;  ga = alpha g, gb = alpha beta g, gc = gamma g,
  * gd = gamma delta g (bands: ga = the full (2n, m) gradient, zeros outside the
  * selected columns); any output may be NULL (bands: ga required).
@@ -189,7 +188,7 @@ int insr_adam_step(float* params, const float* grads, float* exp_avg, float* exp
 long insr_sq_loss_work_floats(void);
 int insr_sq_loss_fwd(int kind, const float* a, const float* b, const float* c, const float* d, long n, int m,
                      float alpha, float beta, float gamma, float delta, float scale, float* out, float* work,
-                     unsigned int* ticket, void* stream);
+                     void* stream);
 int insr_sq_loss_bwd(int kind, const float* a, const float* b, const float* c, const float* d, long n, int m,
                      float alpha, float beta, float gamma, float delta, float scale, const float* gout, float* ga,
                      float* gb, float* gc, float* gd, void* stream);

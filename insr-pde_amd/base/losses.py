@@ -16,21 +16,18 @@ import torch
 
 from . import _native as nat
 
-_WORK = {}  # device index -> (partials, ticket): workspace of the multi-block reduction
+_WORK = {}  # device index -> partials buffer of the (large-n) two-launch reduction
 
 
 def _workspace(dev):
-    """One workspace per device: loss launches are ordered on the caller's stream, and
-    the ticket is reset by the kernel itself (so graph replays need no memset).  It is
-    created on the first (eager) call -- phase loops always run iteration 0 eagerly
-    before capturing -- and lives outside any graph pool."""
+    """One partials buffer per device (loss launches are ordered on the caller's
+    stream).  Created on the first eager call -- phase loops always run iteration 0
+    eagerly before capturing -- so it lives outside any graph pool."""
     key = dev.index
     if key not in _WORK:
         if torch.cuda.is_current_stream_capturing():
             raise RuntimeError("fused loss workspace must be created before graph capture (run one eager call)")
-        n = nat.lib().insr_sq_loss_work_floats()
-        _WORK[key] = (torch.zeros(n, device=dev, dtype=torch.float32),
-                      torch.zeros(1, device=dev, dtype=torch.int32))
+        _WORK[key] = torch.empty(nat.lib().insr_sq_loss_work_floats(), device=dev, dtype=torch.float32)
     return _WORK[key]
 
 
@@ -47,10 +44,10 @@ class _SqLoss(torch.autograd.Function):
     def forward(ctx, kind, n, m, coef, scale, a, b, c, d):
         lib = nat.lib()
         dev = a.device
-        work, ticket = _workspace(dev)
+        work = _workspace(dev)
         out = torch.empty((), device=dev, dtype=torch.float32)
         rc = lib.insr_sq_loss_fwd(kind, nat.ptr(a), nat.ptr(b), nat.ptr(c), nat.ptr(d), n, m, *coef, scale,
-                                  nat.ptr(out), nat.ptr(work), nat.ptr(ticket), nat.stream_of(dev))
+                                  nat.ptr(out), nat.ptr(work), nat.stream_of(dev))
         nat.check(rc, "insr_sq_loss_fwd")
         ctx.save_for_backward(a, b, c, d)
         ctx.args = (kind, n, m, coef, scale)

@@ -89,6 +89,22 @@ __global__ __launch_bounds__(SplitGeo<NT>::THREADS) void jet_fwd_split(
       }
     }
   }
+  // Next layer's W rows are prefetched into registers one layer ahead (RPW == 1:
+  // 2 x NT floatx4), so the L2/HBM latency of the A operand hides behind the
+  // current layer's MFMAs, sine and barriers.
+  constexpr bool kPrefetch = RPW == 1;
+  floatx4 wn[kPrefetch ? NT : 1];
+  floatx4 bnx = floatx4{0.f, 0.f, 0.f, 0.f};
+  auto load_rows = [&](int jj) {
+    const float* Wj = prm + hidden_off(din, W, jj);
+#pragma unroll
+    for (int kt = 0; kt < (kPrefetch ? NT : 1); ++kt)
+      wn[kt] = *reinterpret_cast<const floatx4*>(Wj + (long)(16 * rt0 + c) * W + 16 * kt + 4 * g);
+    bnx = *reinterpret_cast<const floatx4*>(Wj + (long)W * W + 16 * rt0 + 4 * g);
+  };
+  if constexpr (kPrefetch) {
+    if (L >= 1) load_rows(1);
+  }
   for (int j = 0; j <= L; ++j) {
     if (j > 0) {
       // hidden layer j: B operands (layer j-1 activations) from LDS, A = W rows in registers
@@ -98,10 +114,18 @@ __global__ __launch_bounds__(SplitGeo<NT>::THREADS) void jet_fwd_split(
       for (int i = 0; i < RPW; ++i) {
         const int rt = rt0 + i;
         floatx4 wr[NT];
+        floatx4 bias;
+        if constexpr (kPrefetch) {
 #pragma unroll
-        for (int kt = 0; kt < NT; ++kt)
-          wr[kt] = *reinterpret_cast<const floatx4*>(Wj + (long)(16 * rt + c) * W + 16 * kt + 4 * g);
-        const floatx4 bias = *reinterpret_cast<const floatx4*>(bj + 16 * rt + 4 * g);
+          for (int kt = 0; kt < NT; ++kt) wr[kt] = wn[kt];
+          bias = bnx;
+          if (j < L) load_rows(j + 1);
+        } else {
+#pragma unroll
+          for (int kt = 0; kt < NT; ++kt)
+            wr[kt] = *reinterpret_cast<const floatx4*>(Wj + (long)(16 * rt + c) * W + 16 * kt + 4 * g);
+          bias = *reinterpret_cast<const floatx4*>(bj + 16 * rt + 4 * g);
+        }
 #pragma unroll
         for (int t = 0; t < T; ++t) {
           a[t][i][0] = bias;
@@ -321,7 +345,20 @@ __global__ __launch_bounds__(SplitGeo<NT>::THREADS) void jet_bwd_split(
   }
 
   // ---- sine layers j = L .. 0 ----
+  // Small register states hoist the propagation's W^T operand loads to the top of
+  // the layer, so their latency overlaps the sine reverse, the LDS exchange and dW.
+  constexpr bool kHoistWT = RPW == 1 && T * S <= 4;
+  float wt[kHoistWT ? NT : 1][4];
   for (int j = L; j >= 0; --j) {
+    if constexpr (kHoistWT) {
+      if (j > 0) {
+        const float* Wj = prm + hidden_off(din, W, j);
+#pragma unroll
+        for (int kt = 0; kt < NT; ++kt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) wt[kt][r] = Wj[(long)(16 * kt + 4 * g + r) * W + 16 * rt0 + c];
+      }
+    }
 #pragma unroll
     for (int t = 0; t < T; ++t) {
       const float* basej = act_base(act, j, ntiles, tile0 + t, S, NT);
@@ -430,7 +467,12 @@ __global__ __launch_bounds__(SplitGeo<NT>::THREADS) void jet_bwd_split(
 #pragma unroll
         for (int i = 0; i < RPW; ++i)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) wa[i][r] = Wj[(long)(16 * kt + 4 * g + r) * W + 16 * (rt0 + i) + c];
+          for (int r = 0; r < 4; ++r) {
+            if constexpr (kHoistWT)
+              wa[i][r] = wt[kt][r];
+            else
+              wa[i][r] = Wj[(long)(16 * kt + 4 * g + r) * W + 16 * (rt0 + i) + c];
+          }
 #pragma unroll
         for (int t = 0; t < T; ++t)
 #pragma unroll

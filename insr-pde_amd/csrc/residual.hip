@@ -8,16 +8,17 @@
 // i.e. 3-5 launches forward and as many backward (sub, pow, mean, slice/select
 // backward zero-fills, ...).  On the GPU each of those is a ~3 us launch over a few
 // hundred KB, so they cost more than they compute.  Here a loss is ONE launch
-// forward (a deterministic two-level reduction: fixed per-block order, partials
-// combined by the last block in block order) and ONE launch backward (the
-// residual is recomputed, every input gradient written in the same pass).
+// forward (a deterministic reduction in a fixed order) and ONE launch backward (the
+// residual is recomputed, every input gradient written in the same pass).  Losses
+// over more than 2^17 terms use a second one-block launch to combine the per-block
+// partials in block order (deterministic, and no cross-XCD fences).
 #include "jet_common.hpp"
 
 namespace insr {
 
 constexpr int kLossThreads = 512;
 constexpr int kLossMaxBlocks = 256;
-constexpr long kLossPerBlock = 8192;  // elements per block before the grid grows
+constexpr long kLossPerBlock = 1L << 17;  // elements per block before the grid grows
 
 struct LossIn {
   const float* a;
@@ -53,8 +54,8 @@ __device__ __forceinline__ float loss_term(int kind, const LossIn& in, long n, i
 }
 
 __global__ __launch_bounds__(kLossThreads) void sq_loss_fwd_kernel(int kind, LossIn in, long n, int m, float scale,
-                                                                   float* __restrict__ out, float* work,
-                                                                   unsigned int* ticket) {
+                                                                   float* __restrict__ out) {
+  // grid == 1: out[0] = scale * sum;  grid > 1: out[block] = partial sum (combined by sq_loss_combine_kernel)
   __shared__ float red[kLossThreads / 64];
   const long count = kind == INSR_LOSS_COMBO ? n : 2 * n;
   float acc = 0.f;
@@ -68,20 +69,15 @@ __global__ __launch_bounds__(kLossThreads) void sq_loss_fwd_kernel(int kind, Los
   if (threadIdx.x != 0) return;
   float part = 0.f;
   for (int k = 0; k < kLossThreads / 64; ++k) part += red[k];
-  if (gridDim.x == 1) {
-    out[0] = scale * part;
-    return;
-  }
-  __hip_atomic_store(work + blockIdx.x, part, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __threadfence();  // release the partial (agent scope: the L2s are per XCD)
-  const unsigned int done = atomicAdd(ticket, 1u);
-  if (done == gridDim.x - 1) {  // last block: combine the partials in block order
-    __threadfence();  // acquire every block's partial
-    float tot = 0.f;
-    for (unsigned int k = 0; k < gridDim.x; ++k) tot += __hip_atomic_load(work + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    out[0] = scale * tot;
-    *ticket = 0u;  // ready for the next launch on this stream (and graph replays)
-  }
+  out[blockIdx.x] = gridDim.x == 1 ? scale * part : part;
+}
+
+__global__ __launch_bounds__(64) void sq_loss_combine_kernel(const float* __restrict__ part, int nb, float scale,
+                                                             float* __restrict__ out) {
+  float acc = 0.f;
+  for (int k = threadIdx.x; k < nb; k += 64) acc += part[k];
+  for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off);
+  if (threadIdx.x == 0) out[0] = scale * acc;
 }
 
 __global__ __launch_bounds__(256) void sq_loss_bwd_kernel(int kind, LossIn in, long n, int m, float scale,
@@ -120,7 +116,7 @@ long insr_sq_loss_work_floats(void) { return kLossMaxBlocks; }
 
 int insr_sq_loss_fwd(int kind, const float* a, const float* b, const float* c, const float* d, long n, int m,
                      float alpha, float beta, float gamma, float delta, float scale, float* out, float* work,
-                     unsigned int* ticket, void* stream) {
+                     void* stream) {
   if (!a || !out || n < 0) return INSR_EINVAL;
   if (kind == INSR_LOSS_BANDS && (m < 2 || b || c || d)) return INSR_EINVAL;
   if (kind != INSR_LOSS_COMBO && kind != INSR_LOSS_BANDS) return INSR_EINVAL;
@@ -129,10 +125,12 @@ int insr_sq_loss_fwd(int kind, const float* a, const float* b, const float* c, c
   long nb = (count + kLossPerBlock - 1) / kLossPerBlock;
   if (nb < 1) nb = 1;
   if (nb > kLossMaxBlocks) nb = kLossMaxBlocks;
-  if (nb > 1 && (!work || !ticket)) return INSR_EINVAL;
+  if (nb > 1 && !work) return INSR_EINVAL;
   const LossIn in{a, b, c, d, alpha, beta, gamma, delta};
-  hipLaunchKernelGGL(sq_loss_fwd_kernel, dim3((unsigned)nb), dim3(kLossThreads), 0, (hipStream_t)stream, kind, in, n,
-                     m, scale, out, work, ticket);
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(sq_loss_fwd_kernel, dim3((unsigned)nb), dim3(kLossThreads), 0, st, kind, in, n, m, scale,
+                     nb > 1 ? work : out);
+  if (nb > 1) hipLaunchKernelGGL(sq_loss_combine_kernel, dim3(1), dim3(64), 0, st, work, (int)nb, scale, out);
   return (int)hipGetLastError();
 }
 

@@ -1,9 +1,10 @@
 """Fused residual losses (base.losses, residual.hip) vs the plain torch fp32 expressions
 the reference writes (fluid/model.py:90-151, advection/model.py:78-91).
 
-Tolerance: the fused forward sums in a different (deterministic) order than
-torch.mean, so losses agree to 1e-6 relative; gradients are elementwise formulas of
-the same residual and agree to 1e-6 relative normwise."""
+Tolerance: the fused forward sums in its own (deterministic) order, so losses are
+judged against the fp64 value of the same expression at 1e-5 relative (fp32
+summation of up to 6e5 squares); gradients are elementwise formulas of the same
+residual and agree with torch fp32 to 1e-6 relative normwise."""
 import pytest
 import torch
 
@@ -31,7 +32,7 @@ CASES = [  # (alpha, beta, gamma, delta, which of b, c, d present)
 ]
 
 
-@pytest.mark.parametrize("n", [1, 1000, 40000, 300000])
+@pytest.mark.parametrize("n", [1, 1000, 40000, 300000])  # x2 columns: 300000 -> 5 blocks
 @pytest.mark.parametrize("case", range(len(CASES)))
 def test_fused_mse_matches_torch(B, n, case):
     alpha, beta, gamma, delta, which = CASES[case]
@@ -50,9 +51,12 @@ def test_fused_mse_matches_torch(B, n, case):
 
     lr = ref()
     gr = torch.autograd.grad(lr, [x for x in (a, b, c, d) if x is not None])
-    for _ in range(2):  # twice: the multi-block ticket must reset itself
+    a, b, c, d = (None if x is None else x.detach().double().requires_grad_(False) for x in (a, b, c, d))
+    l64 = ref()
+    a, b, c, d = (t[k] if (k == "a" or k in which) else None for k in "abcd")
+    for _ in range(2):  # twice: the multi-block path reuses its partials buffer
         lf = B.fused_mse(a, b, c, d, alpha=alpha, beta=beta, gamma=gamma, delta=delta)
-        assert rel(lf.detach(), lr.detach()) < 1e-6
+        assert rel(lf.detach(), l64) < 1e-5
     gf = torch.autograd.grad(lf, [x for x in (a, b, c, d) if x is not None])
     for x, y in zip(gf, gr):
         assert rel(x, y) < 1e-6
@@ -65,15 +69,16 @@ def test_wall_mse_matches_torch(B, nb):
     lr = torch.mean(y[:nb, 0] ** 2) + torch.mean(y[nb:, 1] ** 2)
     (gr,) = torch.autograd.grad(lr, y)
     lf = B.wall_mse(y, nb)
-    assert rel(lf.detach(), lr.detach()) < 1e-6
+    y64 = y.detach().double()
+    assert rel(lf.detach(), torch.mean(y64[:nb, 0] ** 2) + torch.mean(y64[nb:, 1] ** 2)) < 1e-5
     (gf,) = torch.autograd.grad(lf, y)
     assert rel(gf, gr) < 1e-6 and bool((gf[:nb, 1:] == 0).all()) and bool((gf[nb:, 0] == 0).all())
 
 
 def test_fused_mse_in_graph_replay(B):
-    """The ticketed multi-block reduction inside a captured hipGraph, replayed."""
-    x = torch.randn(200000, device="cuda")
-    y = torch.randn(200000, device="cuda")
+    """The two-launch (multi-block) reduction inside a captured hipGraph, replayed."""
+    x = torch.randn(400000, device="cuda")
+    y = torch.randn(400000, device="cuda")
     B.fused_mse(x, y)  # workspace allocated outside the capture
     s = torch.cuda.Stream()
     s.wait_stream(torch.cuda.current_stream())
@@ -87,7 +92,7 @@ def test_fused_mse_in_graph_replay(B):
         x.mul_(1.5)
         gr.replay()
         torch.cuda.synchronize()
-        assert rel(out, torch.mean((x - y) ** 2)) < 1e-6, k
+        assert rel(out, torch.mean((x.double() - y.double()) ** 2)) < 1e-5, k
 
 
 def test_losses_reject_cpu(B):
