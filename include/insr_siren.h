@@ -175,7 +175,7 @@ int insr_adam_step(float* params, const float* grads, float* exp_avg, float* exp
  *                    order; b, c, d may be NULL (= 0; d needs c); all contiguous, n elements
  *   INSR_LOSS_BANDS  out = scale * (sum_{r<n} y[r][0]^2 + sum_{r<n} y[n+r][1]^2)
  *                    (a = y, (2n, m) row-major, m >= 2; b = c = d = NULL)
- * The forward reduction is deterministic (fixed order).  Up to 2^17 terms it is one
+ * The forward reduction is deterministic (fixed order).  Up to 4096 terms it is one
  * launch; beyond, per-block partials go to `work` (insr_sq_loss_work_floats()
  * floats, not shared by concurrent launches) and a second one-block launch combines
  * them in block order.

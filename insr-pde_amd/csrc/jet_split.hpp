@@ -40,9 +40,14 @@ template <int NT, int S, int T>
 constexpr size_t fwd_split_lds_bytes() {
   return (size_t)T * S * SplitGeo<NT>::PLANE * sizeof(float);
 }
+// backward: zb planes point-major with row W+8 (conflict-free ds_read_b128 rows for
+// the propagation), h planes point-major with row W+4 (they are only read as b32
+// columns and written as b128 rows: both conflict-free at +4)
+template <int NT>
+constexpr int kLdhH = 16 * NT + 4;
 template <int NT, int S, int T>
 constexpr size_t bwd_split_lds_bytes() {
-  return (size_t)2 * T * S * SplitGeo<NT>::PLANE * sizeof(float);
+  return (size_t)T * S * (SplitGeo<NT>::PLANE + 16 * kLdhH<NT>) * sizeof(float);
 }
 
 template <int NT, int S, bool LAP, int T>
@@ -89,22 +94,6 @@ __global__ __launch_bounds__(SplitGeo<NT>::THREADS) void jet_fwd_split(
       }
     }
   }
-  // Next layer's W rows are prefetched into registers one layer ahead (RPW == 1:
-  // 2 x NT floatx4), so the L2/HBM latency of the A operand hides behind the
-  // current layer's MFMAs, sine and barriers.
-  constexpr bool kPrefetch = RPW == 1;
-  floatx4 wn[kPrefetch ? NT : 1];
-  floatx4 bnx = floatx4{0.f, 0.f, 0.f, 0.f};
-  auto load_rows = [&](int jj) {
-    const float* Wj = prm + hidden_off(din, W, jj);
-#pragma unroll
-    for (int kt = 0; kt < (kPrefetch ? NT : 1); ++kt)
-      wn[kt] = *reinterpret_cast<const floatx4*>(Wj + (long)(16 * rt0 + c) * W + 16 * kt + 4 * g);
-    bnx = *reinterpret_cast<const floatx4*>(Wj + (long)W * W + 16 * rt0 + 4 * g);
-  };
-  if constexpr (kPrefetch) {
-    if (L >= 1) load_rows(1);
-  }
   for (int j = 0; j <= L; ++j) {
     if (j > 0) {
       // hidden layer j: B operands (layer j-1 activations) from LDS, A = W rows in registers
@@ -114,35 +103,44 @@ __global__ __launch_bounds__(SplitGeo<NT>::THREADS) void jet_fwd_split(
       for (int i = 0; i < RPW; ++i) {
         const int rt = rt0 + i;
         floatx4 wr[NT];
-        floatx4 bias;
-        if constexpr (kPrefetch) {
 #pragma unroll
-          for (int kt = 0; kt < NT; ++kt) wr[kt] = wn[kt];
-          bias = bnx;
-          if (j < L) load_rows(j + 1);
-        } else {
-#pragma unroll
-          for (int kt = 0; kt < NT; ++kt)
-            wr[kt] = *reinterpret_cast<const floatx4*>(Wj + (long)(16 * rt + c) * W + 16 * kt + 4 * g);
-          bias = *reinterpret_cast<const floatx4*>(bj + 16 * rt + 4 * g);
-        }
+        for (int kt = 0; kt < NT; ++kt)
+          wr[kt] = *reinterpret_cast<const floatx4*>(Wj + (long)(16 * rt + c) * W + 16 * kt + 4 * g);
+        const floatx4 bias = *reinterpret_cast<const floatx4*>(bj + 16 * rt + 4 * g);
 #pragma unroll
         for (int t = 0; t < T; ++t) {
           a[t][i][0] = bias;
 #pragma unroll
           for (int s = 1; s < S; ++s) a[t][i][s] = floatx4{0.f, 0.f, 0.f, 0.f};
         }
+        // consecutive MFMAs go to independent accumulators (the f32 16x16x4 MFMA has a
+        // 40-cycle dependent latency vs a 32-cycle issue); each accumulator's k-order is
+        // unchanged, so results are bit-identical to the plain loop
 #pragma unroll
-        for (int kt = 0; kt < NT; ++kt)
+        for (int kt = 0; kt < NT; ++kt) {
+          if constexpr (S >= 2) {
 #pragma unroll
-          for (int t = 0; t < T; ++t)
+            for (int t = 0; t < T; ++t) {
+              floatx4 hv[S];
 #pragma unroll
-            for (int s = 0; s < S; ++s) {
-              const floatx4 hv =
-                  *reinterpret_cast<const floatx4*>(lds + (t * S + s) * PLANE + c * LDH + 16 * kt + 4 * g);
+              for (int s = 0; s < S; ++s)
+                hv[s] = *reinterpret_cast<const floatx4*>(lds + (t * S + s) * PLANE + c * LDH + 16 * kt + 4 * g);
 #pragma unroll
-              for (int r = 0; r < 4; ++r) a[t][i][s] = mfma4(wr[kt][r], hv[r], a[t][i][s]);
+              for (int r = 0; r < 4; ++r)
+#pragma unroll
+                for (int s = 0; s < S; ++s) a[t][i][s] = mfma4(wr[kt][r], hv[s][r], a[t][i][s]);
             }
+          } else {
+            floatx4 hv[T];
+#pragma unroll
+            for (int t = 0; t < T; ++t)
+              hv[t] = *reinterpret_cast<const floatx4*>(lds + t * PLANE + c * LDH + 16 * kt + 4 * g);
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+#pragma unroll
+              for (int t = 0; t < T; ++t) a[t][i][0] = mfma4(wr[kt][r], hv[t][r], a[t][i][0]);
+          }
+        }
       }
       __syncthreads();  // every wave has read layer j-1
     }
@@ -236,8 +234,9 @@ __global__ __launch_bounds__(SplitGeo<NT>::THREADS) void jet_bwd_split(
   extern __shared__ __attribute__((aligned(16))) float lds[];
   // both planes point-major [t][s][16 points][LDH]: zbp is read as b128 rows (the
   // propagation B operand) and as 4 b32 columns (the dW A operand); hpp as columns
-  float* zbp = lds;                  // zb of layer j
-  float* hpp = lds + T * S * PLANE;  // h of layer j-1
+  constexpr int LDHH = kLdhH<NT>, PLANEH = 16 * LDHH;
+  float* zbp = lds;                  // zb of layer j      [t][s][p][LDH]
+  float* hpp = lds + T * S * PLANE;  // h of layer j-1     [t][s][p][LDHH]
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
   const int ntiles = ((N + 63) / 64) * 4;
   const int tile0 = blockIdx.x * T;
@@ -411,9 +410,9 @@ __global__ __launch_bounds__(SplitGeo<NT>::THREADS) void jet_bwd_split(
       for (int i = 0; i < RPW; ++i)
 #pragma unroll
         for (int s = 0; s < S; ++s) {
-          const int off = (t * S + s) * PLANE + c * LDH + 16 * (rt0 + i) + 4 * g;
-          *reinterpret_cast<floatx4*>(zbp + off) = hb[t][i][s];
-          *reinterpret_cast<floatx4*>(hpp + off) =
+          const int col = 16 * (rt0 + i) + 4 * g;
+          *reinterpret_cast<floatx4*>(zbp + (t * S + s) * PLANE + c * LDH + col) = hb[t][i][s];
+          *reinterpret_cast<floatx4*>(hpp + (t * S + s) * PLANEH + c * LDHH + col) =
               h_stream<NT, S, LAP>(basep, s, rt0 + i, lane, snp[t][i], csp[t][i]);
         }
     }
@@ -434,15 +433,16 @@ __global__ __launch_bounds__(SplitGeo<NT>::THREADS) void jet_bwd_split(
 #pragma unroll
             for (int s = 0; s < S; ++s) {
               const float* zb_ts = zbp + (t * S + s) * PLANE;
-              const float* hp_ts = hpp + (t * S + s) * PLANE;
+              const float* hp_ts = hpp + (t * S + s) * PLANEH;
               floatx4 a4;
 #pragma unroll
               for (int r = 0; r < 4; ++r) a4[r] = zb_ts[(4 * g + r) * LDH + 16 * rt + c];
+              // r outer: CTC independent accumulators between dependent MFMAs
 #pragma unroll
-              for (int ct = 0; ct < CTC; ++ct)
+              for (int r = 0; r < 4; ++r)
 #pragma unroll
-                for (int r = 0; r < 4; ++r)
-                  dacc[ct] = mfma4(a4[r], hp_ts[(4 * g + r) * LDH + 16 * (ct0 + ct) + c], dacc[ct]);
+                for (int ct = 0; ct < CTC; ++ct)
+                  dacc[ct] = mfma4(a4[r], hp_ts[(4 * g + r) * LDHH + 16 * (ct0 + ct) + c], dacc[ct]);
             }
 #pragma unroll
           for (int ct = 0; ct < CTC; ++ct)
@@ -473,17 +473,32 @@ __global__ __launch_bounds__(SplitGeo<NT>::THREADS) void jet_bwd_split(
             else
               wa[i][r] = Wj[(long)(16 * kt + 4 * g + r) * W + 16 * (rt0 + i) + c];
           }
+        if constexpr (S >= 2) {  // r outer over S (x RPW) independent accumulators
 #pragma unroll
-        for (int t = 0; t < T; ++t)
+          for (int t = 0; t < T; ++t) {
+            floatx4 b4[S];
 #pragma unroll
-          for (int s = 0; s < S; ++s) {
-            const floatx4 b4 =
-                *reinterpret_cast<const floatx4*>(zbp + (t * S + s) * PLANE + c * LDH + 16 * kt + 4 * g);
+            for (int s = 0; s < S; ++s)
+              b4[s] = *reinterpret_cast<const floatx4*>(zbp + (t * S + s) * PLANE + c * LDH + 16 * kt + 4 * g);
 #pragma unroll
-            for (int i = 0; i < RPW; ++i)
+            for (int r = 0; r < 4; ++r)
 #pragma unroll
-              for (int r = 0; r < 4; ++r) nh[t][i][s] = mfma4(wa[i][r], b4[r], nh[t][i][s]);
+              for (int s = 0; s < S; ++s)
+#pragma unroll
+                for (int i = 0; i < RPW; ++i) nh[t][i][s] = mfma4(wa[i][r], b4[s][r], nh[t][i][s]);
           }
+        } else {  // value jets: r outer over the T tiles
+          floatx4 b4[T];
+#pragma unroll
+          for (int t = 0; t < T; ++t)
+            b4[t] = *reinterpret_cast<const floatx4*>(zbp + t * PLANE + c * LDH + 16 * kt + 4 * g);
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int t = 0; t < T; ++t)
+#pragma unroll
+              for (int i = 0; i < RPW; ++i) nh[t][i][0] = mfma4(wa[i][r], b4[t][r], nh[t][i][0]);
+        }
       }
 #pragma unroll
       for (int t = 0; t < T; ++t)

@@ -10,7 +10,7 @@
 // hundred KB, so they cost more than they compute.  Here a loss is ONE launch
 // forward (a deterministic reduction in a fixed order) and ONE launch backward (the
 // residual is recomputed, every input gradient written in the same pass).  Losses
-// over more than 2^17 terms use a second one-block launch to combine the per-block
+// over more than 4096 terms use a second one-block launch to combine the per-block
 // partials in block order (deterministic, and no cross-XCD fences).
 #include "jet_common.hpp"
 
@@ -18,7 +18,7 @@ namespace insr {
 
 constexpr int kLossThreads = 512;
 constexpr int kLossMaxBlocks = 256;
-constexpr long kLossPerBlock = 1L << 17;  // elements per block before the grid grows
+constexpr long kLossPerBlock = 4096;  // elements per block (8 per thread) before the grid grows
 
 struct LossIn {
   const float* a;
@@ -59,6 +59,7 @@ __global__ __launch_bounds__(kLossThreads) void sq_loss_fwd_kernel(int kind, Los
   __shared__ float red[kLossThreads / 64];
   const long count = kind == INSR_LOSS_COMBO ? n : 2 * n;
   float acc = 0.f;
+#pragma unroll 4
   for (long i = (long)blockIdx.x * kLossThreads + threadIdx.x; i < count; i += (long)gridDim.x * kLossThreads)
     acc += loss_term(kind, in, n, m, i);
   // wave reduction (fixed butterfly order), then the block's waves in order
