@@ -254,6 +254,25 @@ __device__ __forceinline__ floatx4 h_stream(const float* base, int s, int rt, in
 
 
 // ---------------------------------------------------------------------------
+// Diagnostic phase stamps (build with -DINSR_STAMPS, tools/diag_stamps.py): s_memtime
+// at phase boundaries for every wave of two blocks, [blk][wave][layer][phase].
+// ---------------------------------------------------------------------------
+#ifdef INSR_STAMPS
+constexpr int kStampSlots = 2 * 16 * 8 * 8;
+static __device__ unsigned long long g_insr_stamps[kStampSlots];
+#define INSR_STAMP(layer, k)                                                                      \
+  do {                                                                                            \
+    const int sb_ = blockIdx.x == 0 ? 0 : (blockIdx.x == gridDim.x / 2 ? 1 : -1);               \
+    if (sb_ >= 0 && (threadIdx.x & 63) == 0 && (layer) < 8)                                        \
+      g_insr_stamps[((sb_ * 16 + (threadIdx.x >> 6)) * 8 + (layer)) * 8 + (k)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#else
+#define INSR_STAMP(layer, k) \
+  do {                       \
+  } while (0)
+#endif
+
+// ---------------------------------------------------------------------------
 // launchers (defined in jet_wave.hip / jet_split_fwd.hip / jet_split_bwd.hip)
 // ---------------------------------------------------------------------------
 int dispatch_fwd_wave(int NT, int S, bool LAP, const float* x, int N, int din, int dout, int L, const float* prm,

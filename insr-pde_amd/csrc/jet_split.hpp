@@ -349,6 +349,7 @@ __global__ __launch_bounds__(SplitGeo<NT>::THREADS) void jet_bwd_split(
   constexpr bool kHoistWT = RPW == 1 && T * S <= 4;
   float wt[kHoistWT ? NT : 1][4];
   for (int j = L; j >= 0; --j) {
+    INSR_STAMP(L - j, 0);
     if constexpr (kHoistWT) {
       if (j > 0) {
         const float* Wj = prm + hidden_off(din, W, j);
@@ -382,6 +383,7 @@ __global__ __launch_bounds__(SplitGeo<NT>::THREADS) void jet_bwd_split(
         v = sum16(v);
         if (c == 0) mypart[boff + 16 * (rt0 + i) + 4 * g + r] = v;
       }
+    INSR_STAMP(L - j, 1);
     if (j == 0) {
 #pragma unroll
       for (int i = 0; i < RPW; ++i)
@@ -402,7 +404,9 @@ __global__ __launch_bounds__(SplitGeo<NT>::THREADS) void jet_bwd_split(
     // sin/cos of z_{j-1}: h_{j-1} now, and the sine reverse of the next iteration
     floatx4 snp[T][RPW], csp[T][RPW];
     load_sc(j - 1, snp, csp);
+    INSR_STAMP(L - j, 2);
     __syncthreads();  // the previous layer's LDS readers are done
+    INSR_STAMP(L - j, 3);
 #pragma unroll
     for (int t = 0; t < T; ++t) {
       const float* basep = act_base(act, j - 1, ntiles, tile0 + t, S, NT);
@@ -416,7 +420,9 @@ __global__ __launch_bounds__(SplitGeo<NT>::THREADS) void jet_bwd_split(
               h_stream<NT, S, LAP>(basep, s, rt0 + i, lane, snp[t][i], csp[t][i]);
         }
     }
+    INSR_STAMP(L - j, 4);
     __syncthreads();
+    INSR_STAMP(L - j, 5);
     {  // dW_j, this wave's rows: K = 16T points x S streams (k = point 4g + r)
       float* dW = mypart + hidden_off(din, W, j);
       constexpr int CTC = NT < 8 ? NT : 8;  // column tiles per accumulator pass
@@ -451,6 +457,7 @@ __global__ __launch_bounds__(SplitGeo<NT>::THREADS) void jet_bwd_split(
         }
       }
     }
+    INSR_STAMP(L - j, 6);
     {  // propagate: hb_{j-1}[m] (this wave's rows) = sum_n W_j[n][m] zb[n]; A = W^T from L2
       const float* Wj = prm + hidden_off(din, W, j);
       floatx4 nh[T][RPW][S];
@@ -510,6 +517,7 @@ __global__ __launch_bounds__(SplitGeo<NT>::THREADS) void jet_bwd_split(
           for (int s = 0; s < S; ++s) hb[t][i][s] = nh[t][i][s];
         }
     }
+    INSR_STAMP(L - j, 7);
   }
 }
 

@@ -27,3 +27,16 @@ int dispatch_bwd_split(int NT, int S, bool LAP, int T, const float* x, int N, in
 }
 
 }  // namespace insr
+
+#ifdef INSR_STAMPS
+// diagnostic build only (make diag): read / clear the phase stamps of the backward
+extern "C" int insr_diag_stamps(unsigned long long* host, int n) {
+  if (n > insr::kStampSlots) n = insr::kStampSlots;
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(insr::g_insr_stamps), n * sizeof(unsigned long long), 0,
+                                  hipMemcpyDeviceToHost);
+}
+extern "C" int insr_diag_clear(void) {
+  static unsigned long long zero[insr::kStampSlots];
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(insr::g_insr_stamps), zero, sizeof(zero), 0, hipMemcpyHostToDevice);
+}
+#endif
