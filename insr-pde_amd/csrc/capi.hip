@@ -71,8 +71,10 @@ static void tiles_init() {
 
 int split_tiles(int bwd, int NT, int S, long n) {
   tiles_init();
-  const size_t plane = (size_t)S * 16 * ((16 * NT + 8) + (bwd ? 16 * NT + 4 : 0)) * sizeof(float);
-  int T = NT > 8 ? 1 : 4;  // width 256: one tile (register budget of 8 waves x 2 row tiles)
+  const size_t plane = (size_t)S * 16 * ((16 * NT + 8) + (bwd ? 16 * NT : 0)) * sizeof(float);
+  // width 256: one tile (register budget of 8 waves x 2 row tiles); backward T = 4 only
+  // for value jets (register budget of the derivative streams)
+  int T = NT > 8 ? 1 : ((bwd && S > 1) ? 2 : 4);
   while (T > 1 && (size_t)T * plane > 163840) T >>= 1;
   const int forced = g_tiles[bwd ? 1 : 0];
   if (forced > 0) {

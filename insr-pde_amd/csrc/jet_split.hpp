@@ -41,13 +41,14 @@ constexpr size_t fwd_split_lds_bytes() {
   return (size_t)T * S * SplitGeo<NT>::PLANE * sizeof(float);
 }
 // backward: zb planes point-major with row W+8 (conflict-free ds_read_b128 rows for
-// the propagation), h planes point-major with row W+4 (they are only read as b32
-// columns and written as b128 rows: both conflict-free at +4)
-template <int NT>
-constexpr int kLdhH = 16 * NT + 4;
+// the propagation B operand, 4 b32 column reads for the dW A operand); h planes
+// NEURON-major [m][16 points] so the dW B operand (4 consecutive points of one
+// neuron) is one ds_read_b128.  The 16-B slot of (m, p) is XOR-swizzled by
+// ((m>>1) ^ (m>>2)) & 3: conflict-free b128 reads, 2-way b32 writes, no padding.
+__device__ __forceinline__ int hT_index(int m, int p) { return m * 16 + ((((p >> 2) ^ (m >> 1) ^ (m >> 2)) & 3) << 2) + (p & 3); }
 template <int NT, int S, int T>
 constexpr size_t bwd_split_lds_bytes() {
-  return (size_t)T * S * (SplitGeo<NT>::PLANE + 16 * kLdhH<NT>) * sizeof(float);
+  return (size_t)T * S * (SplitGeo<NT>::PLANE + 16 * 16 * NT) * sizeof(float);
 }
 
 template <int NT, int S, bool LAP, int T>
@@ -234,9 +235,9 @@ __global__ __launch_bounds__(SplitGeo<NT>::THREADS) void jet_bwd_split(
   extern __shared__ __attribute__((aligned(16))) float lds[];
   // both planes point-major [t][s][16 points][LDH]: zbp is read as b128 rows (the
   // propagation B operand) and as 4 b32 columns (the dW A operand); hpp as columns
-  constexpr int LDHH = kLdhH<NT>, PLANEH = 16 * LDHH;
+  constexpr int PLANEH = 16 * W;
   float* zbp = lds;                  // zb of layer j      [t][s][p][LDH]
-  float* hpp = lds + T * S * PLANE;  // h of layer j-1     [t][s][p][LDHH]
+  float* hpp = lds + T * S * PLANE;  // h of layer j-1     [t][s][m][16] (hT_index)
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
   const int ntiles = ((N + 63) / 64) * 4;
   const int tile0 = blockIdx.x * T;
@@ -416,8 +417,10 @@ __global__ __launch_bounds__(SplitGeo<NT>::THREADS) void jet_bwd_split(
         for (int s = 0; s < S; ++s) {
           const int col = 16 * (rt0 + i) + 4 * g;
           *reinterpret_cast<floatx4*>(zbp + (t * S + s) * PLANE + c * LDH + col) = hb[t][i][s];
-          *reinterpret_cast<floatx4*>(hpp + (t * S + s) * PLANEH + c * LDHH + col) =
-              h_stream<NT, S, LAP>(basep, s, rt0 + i, lane, snp[t][i], csp[t][i]);
+          const floatx4 hs = h_stream<NT, S, LAP>(basep, s, rt0 + i, lane, snp[t][i], csp[t][i]);
+          float* hp_ts = hpp + (t * S + s) * PLANEH;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) hp_ts[hT_index(col + r, c)] = hs[r];
         }
     }
     INSR_STAMP(L - j, 4);
@@ -425,7 +428,7 @@ __global__ __launch_bounds__(SplitGeo<NT>::THREADS) void jet_bwd_split(
     INSR_STAMP(L - j, 5);
     {  // dW_j, this wave's rows: K = 16T points x S streams (k = point 4g + r)
       float* dW = mypart + hidden_off(din, W, j);
-      constexpr int CTC = NT < 8 ? NT : 8;  // column tiles per accumulator pass
+      constexpr int CTC = NT < 4 ? NT : 4;  // column tiles per accumulator pass (register budget)
 #pragma unroll 1
       for (int i = 0; i < RPW; ++i) {
         const int rt = rt0 + i;
@@ -440,15 +443,17 @@ __global__ __launch_bounds__(SplitGeo<NT>::THREADS) void jet_bwd_split(
             for (int s = 0; s < S; ++s) {
               const float* zb_ts = zbp + (t * S + s) * PLANE;
               const float* hp_ts = hpp + (t * S + s) * PLANEH;
-              floatx4 a4;
+              floatx4 a4, hv[CTC];
 #pragma unroll
               for (int r = 0; r < 4; ++r) a4[r] = zb_ts[(4 * g + r) * LDH + 16 * rt + c];
+#pragma unroll
+              for (int ct = 0; ct < CTC; ++ct)  // h(points 4g..4g+3, neuron 16ct + c)
+                hv[ct] = *reinterpret_cast<const floatx4*>(hp_ts + hT_index(16 * (ct0 + ct) + c, 4 * g));
               // r outer: CTC independent accumulators between dependent MFMAs
 #pragma unroll
               for (int r = 0; r < 4; ++r)
 #pragma unroll
-                for (int ct = 0; ct < CTC; ++ct)
-                  dacc[ct] = mfma4(a4[r], hp_ts[(4 * g + r) * LDHH + 16 * (ct0 + ct) + c], dacc[ct]);
+                for (int ct = 0; ct < CTC; ++ct) dacc[ct] = mfma4(a4[r], hv[ct][r], dacc[ct]);
             }
 #pragma unroll
           for (int ct = 0; ct < CTC; ++ct)
