@@ -120,6 +120,11 @@ int insr_jet_split_tiles(long n_points, int d_in, int width, int mode, int backw
  * whose LDS fits, lowered while the grid has fewer than min_blocks blocks).
  * Env: INSR_SPLIT_TILES_FWD, INSR_SPLIT_TILES_BWD, INSR_SPLIT_MIN_BLOCKS. */
 void insr_jet_set_split_tiles(int fwd_tiles, int bwd_tiles, int min_blocks);
+
+/* Software-pipelined tile-split backward (two tile halves half a layer apart, so one
+ * half's MFMA phase overlaps the other's VALU phase) for T >= 2 at width <= 128:
+ * 1 = on (default; env INSR_BWD_PIPE), 0 = plain.  Returns the previous setting. */
+int insr_jet_set_bwd_pipe(int enable);
 void insr_jet_get_split_tiles(int* fwd_tiles, int* bwd_tiles, int* min_blocks);
 
 /* grad[i] = (accumulate ? grad[i] : 0) + sum_b partial[b * count + i], fixed order. */

@@ -252,6 +252,31 @@ __device__ __forceinline__ floatx4 h_stream(const float* base, int s, int rt, in
   return out;
 }
 
+// As h_stream, and stores the loaded z-stream s (>= 1) into zkeep[s] for the caller's
+// next sine reverse (the Laplacian stream reads the tangents from zkeep, which the
+// caller fills in stream order 1..S-1 before stream S-1).
+template <int NT, int S, bool LAP>
+__device__ __forceinline__ floatx4 h_from_z(const float* base, int s, int rt, int lane, const floatx4& sn,
+                                            const floatx4& cs, floatx4 (&zkeep)[S]) {
+  constexpr int NTAN = LAP ? S - 2 : S - 1;
+  if (s == 0) return sn;
+  const floatx4 zs = *reinterpret_cast<const floatx4*>(base + ((s * NT + rt) * 64 + lane) * 4);
+  zkeep[s] = zs;
+  floatx4 out;
+  if (LAP && s == S - 1) {
+    floatx4 t2 = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < NTAN; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) t2[r] = fmaf(zkeep[1 + i][r], zkeep[1 + i][r], t2[r]);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) out[r] = OMEGA * cs[r] * zs[r] - OMEGA2 * sn[r] * t2[r];
+  } else {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) out[r] = OMEGA * cs[r] * zs[r];
+  }
+  return out;
+}
 
 // ---------------------------------------------------------------------------
 // Diagnostic phase stamps (build with -DINSR_STAMPS, tools/diag_stamps.py): s_memtime

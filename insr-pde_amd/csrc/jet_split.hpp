@@ -349,6 +349,21 @@ __global__ __launch_bounds__(SplitGeo<NT>::THREADS) void jet_bwd_split(
   // the layer, so their latency overlaps the sine reverse, the LDS exchange and dW.
   constexpr bool kHoistWT = RPW == 1 && T * S <= 4;
   float wt[kHoistWT ? NT : 1][4];
+  // z-streams s >= 1 of the layer the next sine reverse needs: loaded once (with the h
+  // planes of the layer above) and kept in registers when the state is small enough
+  constexpr bool kKeepZ = S > 1 && T * (S - 1) * RPW <= 3;
+  floatx4 zk[kKeepZ ? T : 1][kKeepZ ? RPW : 1][kKeepZ ? S : 1];
+  if constexpr (kKeepZ) {
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+      const float* baseL = act_base(act, L, ntiles, tile0 + t, S, NT);
+#pragma unroll
+      for (int i = 0; i < RPW; ++i)
+#pragma unroll
+        for (int s = 1; s < S; ++s)
+          zk[t][i][s] = *reinterpret_cast<const floatx4*>(baseL + ((s * NT + rt0 + i) * 64 + lane) * 4);
+    }
+  }
   for (int j = L; j >= 0; --j) {
     INSR_STAMP(L - j, 0);
     if constexpr (kHoistWT) {
@@ -367,9 +382,13 @@ __global__ __launch_bounds__(SplitGeo<NT>::THREADS) void jet_bwd_split(
       for (int i = 0; i < RPW; ++i) {
         floatx4 zs[S];
 #pragma unroll
-        for (int s = 0; s < S; ++s)
-          zs[s] = (s == 0) ? floatx4{0.f, 0.f, 0.f, 0.f}
-                           : *reinterpret_cast<const floatx4*>(basej + ((s * NT + rt0 + i) * 64 + lane) * 4);
+        for (int s = 0; s < S; ++s) {
+          if constexpr (kKeepZ)
+            zs[s] = (s == 0) ? floatx4{0.f, 0.f, 0.f, 0.f} : zk[t][i][s];
+          else
+            zs[s] = (s == 0) ? floatx4{0.f, 0.f, 0.f, 0.f}
+                             : *reinterpret_cast<const floatx4*>(basej + ((s * NT + rt0 + i) * 64 + lane) * 4);
+        }
         sine_rev<S, LAP>(hb[t][i], zs, sn[t][i], cs[t][i]);
       }
     }
@@ -417,7 +436,12 @@ __global__ __launch_bounds__(SplitGeo<NT>::THREADS) void jet_bwd_split(
         for (int s = 0; s < S; ++s) {
           const int col = 16 * (rt0 + i) + 4 * g;
           *reinterpret_cast<floatx4*>(zbp + (t * S + s) * PLANE + c * LDH + col) = hb[t][i][s];
-          const floatx4 hs = h_stream<NT, S, LAP>(basep, s, rt0 + i, lane, snp[t][i], csp[t][i]);
+          floatx4 hs;
+          if constexpr (kKeepZ) {
+            hs = h_from_z<NT, S, LAP>(basep, s, rt0 + i, lane, snp[t][i], csp[t][i], zk[t][i]);
+          } else {
+            hs = h_stream<NT, S, LAP>(basep, s, rt0 + i, lane, snp[t][i], csp[t][i]);
+          }
           float* hp_ts = hpp + (t * S + s) * PLANEH;
 #pragma unroll
           for (int r = 0; r < 4; ++r) hp_ts[hT_index(col + r, c)] = hs[r];

@@ -22,6 +22,7 @@ VARIANTS = {  # label: ((fwd, bwd, bwd_value) thresholds, (fwd, bwd) forced tile
     "split2": ((BIG, BIG, BIG), (2, 2)),
     "split4": ((BIG, BIG, BIG), (4, 4)),
     "auto": ((BIG, BIG, BIG), (0, 0)),
+    "auto_nopipe": ((BIG, BIG, BIG), (0, 0)),
 }
 MODES = {"value": 0, "grad": 1, "lap": 2}
 
@@ -79,7 +80,8 @@ def main():
                     if W > 128 and variant == "wave":
                         continue
                     nat.set_split_thresholds(*thr)
-                    nat.set_split_tiles(tiles[0], tiles[1], 512)
+                    nat.set_split_tiles(tiles[0], tiles[1], 256)
+                    lib.insr_jet_set_bwd_pipe(0 if variant.endswith("nopipe") else 1)
                     part = torch.empty(max(lib.insr_jet_partial_bytes(n, din, dout, L, W, mode) // 4, 1), device="cuda")
                     nb = lib.insr_jet_partial_blocks(n, din, W, mode)
                     tf_, tb_ = (lib.insr_jet_split_tiles(n, din, W, mode, 0),
