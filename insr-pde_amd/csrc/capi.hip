@@ -71,7 +71,7 @@ static void tiles_init() {
 
 static int g_pipe = -1;
 int bwd_pipe_enabled() {
-  if (g_pipe < 0) g_pipe = env_or("INSR_BWD_PIPE", 1) ? 1 : 0;
+  if (g_pipe < 0) g_pipe = env_or("INSR_BWD_PIPE", 0);
   return g_pipe;
 }
 
@@ -298,7 +298,7 @@ void insr_jet_set_split_tiles(int fwd_tiles, int bwd_tiles, int min_blocks) {
 
 int insr_jet_set_bwd_pipe(int enable) {
   const int old = bwd_pipe_enabled();
-  g_pipe = enable ? 1 : 0;
+  g_pipe = enable < 0 ? 0 : enable;
   return old;
 }
 

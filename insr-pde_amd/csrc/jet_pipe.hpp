@@ -28,7 +28,7 @@ template <int NT, int S, bool LAP, int T>
 __global__ __launch_bounds__(SplitGeo<NT>::THREADS) void jet_bwd_pipe(
     const float* __restrict__ x, int N, int din, int dout, int L, const float* __restrict__ prm,
     const float* __restrict__ act, const float* __restrict__ gy, const float* __restrict__ gdy,
-    const float* __restrict__ glap, float* __restrict__ part, long P) {
+    const float* __restrict__ glap, float* __restrict__ part, long P, int order) {
   static_assert(NT <= 8 && T % 2 == 0, "pipelined backward: one row tile per wave, an even tile count");
   using G = SplitGeo<NT>;
   constexpr int W = G::W, LDH = G::LDH, PLANE = G::PLANE, PLANEH = 16 * W;
@@ -296,11 +296,8 @@ __global__ __launch_bounds__(SplitGeo<NT>::THREADS) void jet_bwd_pipe(
   // (w and w+4) take them in opposite orders, so while one issues the MFMA chain the
   // other runs its VALU work; a scheduling barrier keeps each wave's two parts apart
   // (their register states never coexist).
-#ifdef INSR_PIPE_MFIRST
-  const bool m_first = true;
-#else
-  const bool m_first = (wave & 4) == 0;
-#endif
+  // order 1: waves w, w+4 opposite; 2: waves 2k, 2k+1 opposite; 3: every wave M first
+  const bool m_first = order == 3 ? true : (order == 2 ? (wave & 1) == 0 : (wave & 4) == 0);
   auto half_step = [&](auto HM, auto HV, auto LASTC, int jm, int jv) __attribute__((always_inline)) {
     if (m_first) {
       M(HM, jm);
@@ -329,7 +326,8 @@ __global__ __launch_bounds__(SplitGeo<NT>::THREADS) void jet_bwd_pipe(
 
 template <int NT, int S, bool LAP, int T>
 int launch_bwd_pipe_t(const float* x, int N, int din, int dout, int L, const float* prm, const float* act,
-                      const float* gy, const float* gdy, const float* glap, float* part, long P, hipStream_t st) {
+                      const float* gy, const float* gdy, const float* glap, float* part, long P, hipStream_t st,
+                      int order) {
   constexpr size_t lds = bwd_split_lds_bytes<NT, S, T>();
   if constexpr (lds > kLdsMax || NT > 8 || T % 2 != 0) {
     return INSR_EINVAL;
@@ -344,7 +342,7 @@ int launch_bwd_pipe_t(const float* x, int N, int din, int dout, int L, const flo
       attr_set = true;
     }
     hipLaunchKernelGGL((jet_bwd_pipe<NT, S, LAP, T>), dim3(nb), dim3(SplitGeo<NT>::THREADS), lds, st, x, N, din,
-                       dout, L, prm, act, gy, gdy, glap, part, P);
+                       dout, L, prm, act, gy, gdy, glap, part, P, order);
     return (int)hipGetLastError();
   }
 }

@@ -30,13 +30,14 @@ NETS = {  # name: (d_in, d_out, L, W)
 
 BIG = 1 << 30
 VARIANTS = {  # (fwd, bwd, bwd_value) split thresholds, (fwd, bwd) forced tiles per split block, pipelined bwd
-    "wave": ((0, 0, 0), (0, 0), 1),                  # one wave per 16-point tile, both directions
-    "split": ((BIG, BIG, BIG), (1, 1), 1),           # neurons split over a block's waves, 1 tile/block
-    "split_t2": ((BIG, BIG, BIG), (2, 2), 1),        # 2 tiles per block (ragged last block), pipelined bwd
-    "split_t2_plain": ((BIG, BIG, BIG), (2, 2), 0),  # 2 tiles per block, non-pipelined bwd
-    "split_t4": ((BIG, BIG, BIG), (4, 4), 1),        # 4 tiles per block (capped by LDS / registers)
-    "split_fwd_wave_bwd": ((BIG, 0, 0), (4, 0), 1),  # mixed: the saved-activation layout is shared
-    "wave_fwd_split_bwd": ((0, BIG, BIG), (0, 2), 1),
+    "wave": ((0, 0, 0), (0, 0), 0),                  # one wave per 16-point tile, both directions
+    "split": ((BIG, BIG, BIG), (1, 1), 0),           # neurons split over a block's waves, 1 tile/block
+    "split_t2": ((BIG, BIG, BIG), (2, 2), 0),        # 2 tiles per block (ragged last block)
+    "split_t2_pipe": ((BIG, BIG, BIG), (2, 2), 1),   # 2 tiles per block, pipelined bwd (experiment)
+    "split_t4": ((BIG, BIG, BIG), (4, 4), 0),        # 4 tiles per block (capped by LDS / registers)
+    "split_t4_pipe": ((BIG, BIG, BIG), (4, 4), 2),
+    "split_fwd_wave_bwd": ((BIG, 0, 0), (4, 0), 0),  # mixed: the saved-activation layout is shared
+    "wave_fwd_split_bwd": ((0, BIG, BIG), (0, 2), 0),
 }
 
 
