@@ -121,13 +121,6 @@ int insr_jet_split_tiles(long n_points, int d_in, int width, int mode, int backw
  * Env: INSR_SPLIT_TILES_FWD, INSR_SPLIT_TILES_BWD, INSR_SPLIT_MIN_BLOCKS. */
 void insr_jet_set_split_tiles(int fwd_tiles, int bwd_tiles, int min_blocks);
 
-/* Software-pipelined tile-split backward (two tile halves half a layer apart, so one
- * half's MFMA phase can overlap the other's VALU phase) for T >= 2 at width <= 128.
- * 0 = off (default; env INSR_BWD_PIPE), 1..3 = on with a wave ordering (1: waves w
- * and w+4 take the halves in opposite order, 2: waves 2k and 2k+1, 3: none).  An
- * experiment kept for measurement: slower than the plain kernel on MI355X so far.
- * Returns the previous setting. */
-int insr_jet_set_bwd_pipe(int order);
 void insr_jet_get_split_tiles(int* fwd_tiles, int* bwd_tiles, int* min_blocks);
 
 /* grad[i] = (accumulate ? grad[i] : 0) + sum_b partial[b * count + i], fixed order. */

@@ -44,7 +44,6 @@ SIGNATURES = {
     "insr_sq_loss_bwd": (_I, [_I, _P, _P, _P, _P, _L, _I, _F, _F, _F, _F, _F, _P, _P, _P, _P, _P, _P]),
     "insr_jet_set_split_tiles": (None, [_I, _I, _I]),
     "insr_jet_get_split_tiles": (None, [_P, _P, _P]),
-    "insr_jet_set_bwd_pipe": (_I, [_I]),
     "insr_reduce_partials": (_I, [_P, _I, _L, _P, _I, _P]),
     "insr_adam_prepare": (_I, [_P, _F, _F, _P]),
     "insr_plateau_step": (_I, [_P, _P, _I, _I, _P]),

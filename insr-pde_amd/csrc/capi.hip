@@ -69,12 +69,6 @@ static void tiles_init() {
   }
 }
 
-static int g_pipe = -1;
-int bwd_pipe_enabled() {
-  if (g_pipe < 0) g_pipe = env_or("INSR_BWD_PIPE", 0);
-  return g_pipe;
-}
-
 int split_tiles(int bwd, int NT, int S, long n) {
   tiles_init();
   const size_t plane = (size_t)S * 16 * ((16 * NT + 8) + (bwd ? 16 * NT : 0)) * sizeof(float);
@@ -294,12 +288,6 @@ void insr_jet_set_split_tiles(int fwd_tiles, int bwd_tiles, int min_blocks) {
   g_tiles[0] = fwd_tiles < 0 ? 0 : fwd_tiles;
   g_tiles[1] = bwd_tiles < 0 ? 0 : bwd_tiles;
   g_tiles[2] = min_blocks < 1 ? 1 : min_blocks;
-}
-
-int insr_jet_set_bwd_pipe(int enable) {
-  const int old = bwd_pipe_enabled();
-  g_pipe = enable < 0 ? 0 : enable;
-  return old;
 }
 
 void insr_jet_get_split_tiles(int* fwd_tiles, int* bwd_tiles, int* min_blocks) {

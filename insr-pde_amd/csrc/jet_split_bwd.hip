@@ -1,25 +1,15 @@
 // jet_split_bwd.hip -- instantiations + dispatch of the tile-split backward (jet_split.hpp).
-#include "jet_pipe.hpp"
+#include "jet_split.hpp"
 
 namespace insr {
-
-// Pipelined variant (jet_pipe.hpp) for T >= 2 at widths <= 128 when enabled
-// (env INSR_BWD_PIPE=<order>, or insr_jet_set_bwd_pipe(order); default off).
-int bwd_pipe_enabled();
 
 template <int NT, int S, bool LAP>
 int launch_bwd_split(int T, const float* x, int N, int din, int dout, int L, const float* prm, const float* act,
                      const float* gy, const float* gdy, const float* glap, float* part, long P, hipStream_t st) {
-  const int order = bwd_pipe_enabled();
-  const bool pipe = NT <= 8 && order > 0;
   switch (T) {
     case 1: return launch_bwd_split_t<NT, S, LAP, 1>(x, N, din, dout, L, prm, act, gy, gdy, glap, part, P, st);
-    case 2:
-      if (pipe) return launch_bwd_pipe_t<NT, S, LAP, 2>(x, N, din, dout, L, prm, act, gy, gdy, glap, part, P, st, order);
-      return launch_bwd_split_t<NT, S, LAP, 2>(x, N, din, dout, L, prm, act, gy, gdy, glap, part, P, st);
-    case 4:
-      if (pipe) return launch_bwd_pipe_t<NT, S, LAP, 4>(x, N, din, dout, L, prm, act, gy, gdy, glap, part, P, st, order);
-      return launch_bwd_split_t<NT, S, LAP, 4>(x, N, din, dout, L, prm, act, gy, gdy, glap, part, P, st);
+    case 2: return launch_bwd_split_t<NT, S, LAP, 2>(x, N, din, dout, L, prm, act, gy, gdy, glap, part, P, st);
+    case 4: return launch_bwd_split_t<NT, S, LAP, 4>(x, N, din, dout, L, prm, act, gy, gdy, glap, part, P, st);
     default: return INSR_EINVAL;
   }
 }

@@ -29,15 +29,13 @@ NETS = {  # name: (d_in, d_out, L, W)
 
 
 BIG = 1 << 30
-VARIANTS = {  # (fwd, bwd, bwd_value) split thresholds, (fwd, bwd) forced tiles per split block, pipelined bwd
-    "wave": ((0, 0, 0), (0, 0), 0),                  # one wave per 16-point tile, both directions
-    "split": ((BIG, BIG, BIG), (1, 1), 0),           # neurons split over a block's waves, 1 tile/block
-    "split_t2": ((BIG, BIG, BIG), (2, 2), 0),        # 2 tiles per block (ragged last block)
-    "split_t2_pipe": ((BIG, BIG, BIG), (2, 2), 1),   # 2 tiles per block, pipelined bwd (experiment)
-    "split_t4": ((BIG, BIG, BIG), (4, 4), 0),        # 4 tiles per block (capped by LDS / registers)
-    "split_t4_pipe": ((BIG, BIG, BIG), (4, 4), 2),
-    "split_fwd_wave_bwd": ((BIG, 0, 0), (4, 0), 0),  # mixed: the saved-activation layout is shared
-    "wave_fwd_split_bwd": ((0, BIG, BIG), (0, 2), 0),
+VARIANTS = {  # (fwd, bwd, bwd_value) split thresholds, (fwd, bwd) forced tiles per split block
+    "wave": ((0, 0, 0), (0, 0)),                  # one wave per 16-point tile, both directions
+    "split": ((BIG, BIG, BIG), (1, 1)),           # neurons split over a block's waves, 1 tile/block
+    "split_t2": ((BIG, BIG, BIG), (2, 2)),        # 2 tiles per block (ragged last block)
+    "split_t4": ((BIG, BIG, BIG), (4, 4)),        # 4 tiles per block (capped by LDS / registers)
+    "split_fwd_wave_bwd": ((BIG, 0, 0), (4, 0)),  # mixed: the saved-activation layout is shared
+    "wave_fwd_split_bwd": ((0, BIG, BIG), (0, 2)),
 }
 
 
@@ -49,14 +47,12 @@ def base(request):
     import base as B
     B._native.load()
     old, old_tiles = B._native.get_split_thresholds(), B._native.get_split_tiles()
-    thr, tiles, pipe = VARIANTS[request.param]
+    thr, tiles = VARIANTS[request.param]
     B._native.set_split_thresholds(*thr)
     B._native.set_split_tiles(tiles[0], tiles[1], old_tiles[2])
-    old_pipe = B._native.lib().insr_jet_set_bwd_pipe(pipe)
     yield B
     B._native.set_split_thresholds(*old)
     B._native.set_split_tiles(*old_tiles)
-    B._native.lib().insr_jet_set_bwd_pipe(old_pipe)
 
 
 def nerr(a, b):

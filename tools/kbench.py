@@ -22,9 +22,6 @@ VARIANTS = {  # label: ((fwd, bwd, bwd_value) thresholds, (fwd, bwd) forced tile
     "split2": ((BIG, BIG, BIG), (2, 2)),
     "split4": ((BIG, BIG, BIG), (4, 4)),
     "auto": ((BIG, BIG, BIG), (0, 0)),
-    "auto_p1": ((BIG, BIG, BIG), (0, 0)),
-    "auto_p2": ((BIG, BIG, BIG), (0, 0)),
-    "auto_p3": ((BIG, BIG, BIG), (0, 0)),
 }
 MODES = {"value": 0, "grad": 1, "lap": 2}
 
@@ -51,7 +48,7 @@ def main():
     ap.add_argument("--sizes", default="324,2048,8192,16384,65536")
     ap.add_argument("--modes", default="value,grad,lap")
     ap.add_argument("--reps", type=int, default=20)
-    ap.add_argument("--variants", default="wave,split1,split2,split4,auto")
+    ap.add_argument("--variants", default=",".join(VARIANTS))
     args = ap.parse_args()
     import base
     from base import _native as nat
@@ -83,7 +80,6 @@ def main():
                         continue
                     nat.set_split_thresholds(*thr)
                     nat.set_split_tiles(tiles[0], tiles[1], 256)
-                    lib.insr_jet_set_bwd_pipe(int(variant[-1]) if variant.startswith("auto_p") else 0)
                     part = torch.empty(max(lib.insr_jet_partial_bytes(n, din, dout, L, W, mode) // 4, 1), device="cuda")
                     nb = lib.insr_jet_partial_blocks(n, din, W, mode)
                     tf_, tb_ = (lib.insr_jet_split_tiles(n, din, W, mode, 0),
