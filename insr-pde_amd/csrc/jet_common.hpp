@@ -75,12 +75,21 @@ __device__ __forceinline__ const float* act_base(const float* act, int layer, in
   return act + ((long)layer * ntiles + tile) * (long)(S * NT) * 256;
 }
 
-// sum over the 16 point-lanes that share lane>>4
+// v + (v of the lane DPP control CTRL selects), in the VALU (no LDS crossbar)
+template <int CTRL>
+__device__ __forceinline__ float add_dpp(float v) {
+  const int o = __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false);
+  return v + __builtin_bit_cast(float, o);
+}
+
+// sum over the 16 point-lanes that share lane>>4 (one DPP row), every lane gets it:
+// pairs (quad_perm 1,0,3,2), quads (quad_perm 2,3,0,1), halves (row_half_mirror),
+// row (row_mirror) -- fixed order, no ds_bpermute round trips
 __device__ __forceinline__ float sum16(float v) {
-  v += __shfl_xor(v, 1);
-  v += __shfl_xor(v, 2);
-  v += __shfl_xor(v, 4);
-  v += __shfl_xor(v, 8);
+  v = add_dpp<0xB1>(v);
+  v = add_dpp<0x4E>(v);
+  v = add_dpp<0x141>(v);
+  v = add_dpp<0x140>(v);
   return v;
 }
 

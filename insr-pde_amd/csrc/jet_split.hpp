@@ -106,7 +106,7 @@ __global__ __launch_bounds__(SplitGeo<NT>::THREADS) void jet_fwd_split(
         floatx4 wr[NT];
 #pragma unroll
         for (int kt = 0; kt < NT; ++kt)
-          wr[kt] = *reinterpret_cast<const floatx4*>(Wj + (long)(16 * rt + c) * W + 16 * kt + 4 * g);
+          wr[kt] = *reinterpret_cast<const floatx4*>(Wj + ((16 * rt + c) * W + 16 * kt + 4 * g));
         const floatx4 bias = *reinterpret_cast<const floatx4*>(bj + 16 * rt + 4 * g);
 #pragma unroll
         for (int t = 0; t < T; ++t) {
@@ -182,7 +182,7 @@ __global__ __launch_bounds__(SplitGeo<NT>::THREADS) void jet_fwd_split(
       for (int s = 0; s < S; ++s) sv[t][s] = 0.f;
 #pragma unroll
     for (int i = 0; i < RPW; ++i) {
-      const floatx4 w4 = *reinterpret_cast<const floatx4*>(Wo + (long)o * W + 16 * (rt0 + i) + 4 * g);
+      const floatx4 w4 = *reinterpret_cast<const floatx4*>(Wo + (o * W + 16 * (rt0 + i) + 4 * g));
 #pragma unroll
       for (int t = 0; t < T; ++t)
 #pragma unroll
@@ -314,7 +314,7 @@ __global__ __launch_bounds__(SplitGeo<NT>::THREADS) void jet_bwd_split(
 #pragma unroll
     for (int i = 0; i < RPW; ++i) {
       const int rt = rt0 + i;
-      const floatx4 w4 = *reinterpret_cast<const floatx4*>(Wo + (long)o * W + 16 * rt + 4 * g);
+      const floatx4 w4 = *reinterpret_cast<const floatx4*>(Wo + (o * W + 16 * rt + 4 * g));
       floatx4 acc4 = floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int t = 0; t < T; ++t) {
@@ -372,7 +372,7 @@ __global__ __launch_bounds__(SplitGeo<NT>::THREADS) void jet_bwd_split(
 #pragma unroll
         for (int kt = 0; kt < NT; ++kt)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) wt[kt][r] = Wj[(long)(16 * kt + 4 * g + r) * W + 16 * rt0 + c];
+          for (int r = 0; r < 4; ++r) wt[kt][r] = Wj[(16 * kt + 4 * g + r) * W + 16 * rt0 + c];
       }
     }
 #pragma unroll
@@ -482,7 +482,7 @@ __global__ __launch_bounds__(SplitGeo<NT>::THREADS) void jet_bwd_split(
 #pragma unroll
           for (int ct = 0; ct < CTC; ++ct)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) dW[(long)(16 * rt + 4 * g + r) * W + 16 * (ct0 + ct) + c] = dacc[ct][r];
+            for (int r = 0; r < 4; ++r) dW[(16 * rt + 4 * g + r) * W + 16 * (ct0 + ct) + c] = dacc[ct][r];
         }
       }
     }
@@ -507,7 +507,7 @@ __global__ __launch_bounds__(SplitGeo<NT>::THREADS) void jet_bwd_split(
             if constexpr (kHoistWT)
               wa[i][r] = wt[kt][r];
             else
-              wa[i][r] = Wj[(long)(16 * kt + 4 * g + r) * W + 16 * (rt0 + i) + c];
+              wa[i][r] = Wj[(16 * kt + 4 * g + r) * W + 16 * (rt0 + i) + c];
           }
         if constexpr (S >= 2) {  // r outer over S (x RPW) independent accumulators
 #pragma unroll
