@@ -194,6 +194,21 @@ int insr_sq_loss_bwd(int kind, const float* a, const float* b, const float* c, c
                      float alpha, float beta, float gamma, float delta, float scale, const float* gout, float* ga,
                      float* gb, float* gc, float* gd, void* stream);
 
+/*
+ * Singular-value energies of the elasticity model (elasticity/model.py:143-163):
+ *   out = sum_points [ ratio_arap sum_i (s_i - 1)^2 + ratio_volume (prod_i s_i - 1)^2 ],
+ * s = singular values of each d x d block of J (n blocks, row-major, d = 2 or 3).
+ * Forward: deterministic reduction (more than 1024 points: partials in `work`,
+ * insr_svd_energy_work_floats() floats, combined by a second one-block launch).
+ * Backward: gJ = gout[0] * U diag(dE/ds) V^T per block (torch.svd's gradient),
+ * the SVD recomputed in registers (2x2 closed form, 3x3 one-sided Jacobi).
+ */
+long insr_svd_energy_work_floats(void);
+int insr_svd_energy_fwd(const float* J, long n, int d, float ratio_arap, float ratio_volume, float* out,
+                        float* work, void* stream);
+int insr_svd_energy_bwd(const float* J, long n, int d, float ratio_arap, float ratio_volume, const float* gout,
+                        float* gJ, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -40,6 +40,9 @@ SIGNATURES = {
     "insr_jet_set_split_thresholds": (None, [_I, _I, _I]),
     "insr_jet_split_tiles": (_I, [_L, _I, _I, _I, _I]),
     "insr_sq_loss_work_floats": (_L, []),
+    "insr_svd_energy_work_floats": (_L, []),
+    "insr_svd_energy_fwd": (_I, [_P, _L, _I, _F, _F, _P, _P, _P]),
+    "insr_svd_energy_bwd": (_I, [_P, _L, _I, _F, _F, _P, _P, _P]),
     "insr_sq_loss_fwd": (_I, [_I, _P, _P, _P, _P, _L, _I, _F, _F, _F, _F, _F, _P, _P, _P]),
     "insr_sq_loss_bwd": (_I, [_I, _P, _P, _P, _P, _L, _I, _F, _F, _F, _F, _F, _P, _P, _P, _P, _P, _P]),
     "insr_jet_set_split_tiles": (None, [_I, _I, _I]),

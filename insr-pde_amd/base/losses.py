@@ -89,3 +89,47 @@ def wall_mse(y, n):
         raise ValueError(f"wall_mse: expected (2*{n}, m>=2), got {tuple(y.shape)}")
     y = _prep(y)
     return _SqLoss.apply(nat.LOSS_BANDS, n, y.shape[1], (0.0, 0.0, 0.0, 0.0), 1.0 / max(n, 1), y, None, None, None)
+
+
+_SVD_WORK = {}  # device index -> partials buffer of the SVD-energy reduction
+
+
+class _SvdEnergy(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, J, ratio_arap, ratio_volume):
+        lib = nat.lib()
+        dev = J.device
+        if dev.index not in _SVD_WORK:
+            if torch.cuda.is_current_stream_capturing():
+                raise RuntimeError("SVD-energy workspace must be created before graph capture (run one eager call)")
+            _SVD_WORK[dev.index] = torch.empty(lib.insr_svd_energy_work_floats(), device=dev, dtype=torch.float32)
+        out = torch.empty((), device=dev, dtype=torch.float32)
+        n, d = J.shape[0], J.shape[-1]
+        rc = lib.insr_svd_energy_fwd(nat.ptr(J), n, d, float(ratio_arap), float(ratio_volume), nat.ptr(out),
+                                     nat.ptr(_SVD_WORK[dev.index]), nat.stream_of(dev))
+        nat.check(rc, "insr_svd_energy_fwd")
+        ctx.save_for_backward(J)
+        ctx.ratios = (float(ratio_arap), float(ratio_volume))
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        (J,) = ctx.saved_tensors
+        if not ctx.needs_input_grad[0]:
+            return None, None, None
+        gJ = torch.empty_like(J)
+        g = gout.reshape(1) if gout.is_contiguous() else gout.contiguous().reshape(1)
+        rc = nat.lib().insr_svd_energy_bwd(nat.ptr(J), J.shape[0], J.shape[-1], *ctx.ratios, nat.ptr(g), nat.ptr(gJ),
+                                           nat.stream_of(J.device))
+        nat.check(rc, "insr_svd_energy_bwd")
+        return gJ, None, None
+
+
+def svd_energy(J, ratio_arap=1.0, ratio_volume=0.0):
+    """sum over points of ratio_arap * sum_i (s_i - 1)^2 + ratio_volume * (prod_i s_i - 1)^2,
+    s = singular values of each J[n] (d x d, d = 2 or 3) -- the ARAP and volume terms of
+    elasticity/model.py:143-163 in one launch (torch.svd's gradient U diag(dE/ds) V^T in
+    one backward launch)."""
+    if J.dim() != 3 or J.shape[-1] != J.shape[-2] or J.shape[-1] not in (2, 3):
+        raise ValueError(f"svd_energy: expected (N, d, d) with d in (2, 3), got {tuple(J.shape)}")
+    return _SvdEnergy.apply(_prep(J), ratio_arap, ratio_volume)

@@ -15,10 +15,9 @@ sampler is SURVEY.md §8(f) row 3 (next).
 """
 import torch
 
-from base import BaseModel, sample_random, sample_uniform
+from base import BaseModel, sample_random, sample_uniform, svd_energy
 from base.diff_ops import jacobian_nosync
 
-from . import singular_values
 
 
 class ElasticityModel(BaseModel):
@@ -130,15 +129,14 @@ class ElasticityModel(BaseModel):
         q = self.deformation_field(x) + x
         qdot = (q - q_prev) / dt
         total = 0
-        sig = None
+        if 'arap' in self.energy or 'volume' in self.energy:
+            # both singular-value terms in one fused HIP launch each way (torch.svd + ~12 ops in the reference)
+            J, _ = jacobian_nosync(q, x)  # status unused (as in the reference): no host sync
+            total = svd_energy(J, self.ratio_arap if 'arap' in self.energy else 0.0,
+                               self.ratio_volume if 'volume' in self.energy else 0.0)
         for term in self.energy:
-            if term in ('arap', 'volume') and sig is None:
-                J, _ = jacobian_nosync(q, x)  # status unused (as in the reference): no host sync
-                sig = singular_values(J)
-            if term == 'arap':
-                total = total + self.ratio_arap * torch.sum((sig - 1.0) ** 2)
-            elif term == 'volume':
-                total = total + self.ratio_volume * torch.sum((torch.prod(sig, dim=1) - 1) ** 2)
+            if term in ('arap', 'volume'):
+                continue
             elif term == 'kinematics':
                 qdot_prev = (q_prev - q_pp) / dt
                 total = total + self.ratio_kinematics * torch.sum((qdot - qdot_prev) ** 2)

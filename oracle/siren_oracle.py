@@ -349,7 +349,10 @@ def collision_sphere(q, qdot, dt, ratio, center, radius):
     hit = dist < radius
     if int(hit.sum()) == 0:
         return 0
-    force = ratio * dist[hit][:, None] * direc[hit]
+    if q.shape[1] == 2:
+        force = ratio * dist[hit][:, None] * direc[hit]
+    else:  # losses.py:35: dist[:, None, None] * dir broadcasts to (K, K, 3), as in the reference
+        force = ratio * dist[hit][:, None, None] * direc[hit]
     return -dt * torch.sum(qdot[hit] * force)
 
 

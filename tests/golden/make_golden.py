@@ -353,6 +353,58 @@ def gen_elasticity(base):
     return out
 
 
+def gen_elasticity3d(base):
+    """3-D phase (the elasticity3Dbunny energy set on the box geometry, plus the sphere
+    collider): singular values of 3x3 blocks, plane/sphere collisions, external force,
+    kinematics.  A small 3 -> 3, 2 x 64 net keeps the fixture small; the 5 x 256 width is
+    covered by the el3d operator vectors above."""
+    from elasticity.model import ElasticityModel
+    cfg = base_cfg(num_hidden_layers=2, hidden_features=64, sample_resolution=6, dt=0.1, lr=1e-4, dim=3,
+                   energy=["arap", "kinematics", "external", "volume", "collision", "collision_sphere"],
+                   sample_pattern=["random", "uniform"], ratio_constraint=1e4, ratio_volume=1e3, ratio_arap=1e2,
+                   ratio_collide=1e3, ratio_kinematics=1.0, use_mesh=False, mesh_path="",
+                   external_force_timesteps=5, external_force_x=0.0, external_force_y=0.0,
+                   external_force_z=-1e2, constraint_right_offset_x=0.0, constraint_right_offset_y=0.0,
+                   constraint_right_offset_z=0.0, plane_height=-0.5, collide_circle_x=0.0,
+                   collide_circle_y=-1.6, collide_circle_z=0.0, collide_circle_radius=1.0)
+    model = ElasticityModel(cfg)
+    model.timestep = 1
+    out = {}
+    for name, net, seed in (("f", model.deformation_field, 41), ("f_prev", model.deformation_field_prev, 42),
+                            ("f_pp", model.deformation_field_prev_prev, 43)):
+        set_flat(net, flat(seeded_net(base, 3, 3, 2, 64, seed)))
+        out[f"el3d/{name}/params0"] = flat(net)
+    g = torch.Generator().manual_seed(66)
+    R = cfg.sample_resolution
+    iters = 2
+    xs = []
+    for it in range(iters):
+        xs.append(torch.cat([torch.rand(R ** 3, 3, generator=g) * 2 - 1, base.sample_uniform(R, 3)], 0))
+        out[f"el3d/x{it}"] = xs[it].numpy()
+
+    def samples_fn(it):
+        return lambda res: xs[it].clone().requires_grad_(True)
+
+    def patches(it):
+        return []
+
+    s0 = flat(model.deformation_field)
+    body = raw_phase(ElasticityModel, "_solve_deformation")
+    model._reset_optimizer()
+    model._sample_in_training = samples_fn(0)
+    ld = body(model)
+    out["el3d/_solve_deformation/loss_main"] = np.array(float(ld["main"].detach()))
+    model.optimizer.zero_grad()
+    ld["main"].backward()
+    out["el3d/_solve_deformation/grad_f"] = flat_grad(model.deformation_field)
+    set_flat(model.deformation_field, s0)
+    rec = run_phase(model, ElasticityModel, "_solve_deformation", iters, samples_fn, patches)
+    out["el3d/_solve_deformation/loss_trace"] = np.array([[r[k] for k in sorted(r)] for r in rec])
+    out["el3d/_solve_deformation/f_after"] = flat(model.deformation_field)
+    out["el3d/cfg_energy"] = np.array(cfg.energy)
+    return out
+
+
 def gen_samplers(base):
     torch.manual_seed(5)
     out = {"sampling/uniform_8_2": base.sample_uniform(8, 2).numpy(),
@@ -370,6 +422,10 @@ def gen_samplers(base):
 def main():
     torch.set_num_threads(8)
     base = load_reference()
+    if "--el3d" in sys.argv:  # the 3-D elasticity phase vectors alone (ref_phases_el3d.npz)
+        np.savez_compressed(os.path.join(OUT, "ref_phases_el3d.npz"), **gen_elasticity3d(base))
+        print("ref_phases_el3d.npz", os.path.getsize(os.path.join(OUT, "ref_phases_el3d.npz")) / 1e6, "MB")
+        return
     data = {}
     data.update(gen_samplers(base))
     data.update(gen_networks_and_ops(base))

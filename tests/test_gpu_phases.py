@@ -211,6 +211,51 @@ def test_elasticity_phase(ph):
                  ph["el2d/_solve_deformation/grad_f"])
 
 
+def test_elasticity3d_phase(ph):
+    """3-D energies (3x3 singular values via the fused HIP SVD kernel, plane and sphere
+    collisions, external force, kinematics) against the reference's 3-D phase."""
+    from pde.elasticity import ElasticityModel
+    g3 = dict(np.load(GOLD.replace("ref_phases.npz", "ref_phases_el3d.npz")))
+    energy = [str(e) for e in g3["el3d/cfg_energy"]]
+    cfg = _cfg("elasticity", num_hidden_layers=2, hidden_features=64, sample_resolution=6, dt=0.1, dim=3,
+               energy=energy, ratio_constraint=1e4, ratio_volume=1e3, ratio_arap=1e2, ratio_collide=1e3,
+               ratio_kinematics=1.0, external_force_timesteps=5, external_force_x=0.0, external_force_y=0.0,
+               external_force_z=-1e2, constraint_right_offset_x=0.0, plane_height=-0.5, collide_circle_x=0.0,
+               collide_circle_y=-1.6, collide_circle_z=0.0, collide_circle_radius=1.0)
+    model = ElasticityModel(cfg)
+    model.timestep = 1
+    for k, n in (("f", model.deformation_field), ("f_prev", model.deformation_field_prev),
+                 ("f_pp", model.deformation_field_prev_prev)):
+        set_flat(n, g3[f"el3d/{k}/params0"])
+    T = lambda k: torch.from_numpy(g3[k]).cuda()  # noqa: E731
+
+    def patch(it):
+        model._sample_in_training = lambda res: T(f"el3d/x{it}").clone().requires_grad_(True)
+
+    body = ElasticityModel._solve_deformation._insr_phase
+    patch(0)
+    model._reset_optimizer()
+    ld = body(model)
+    ref = float(g3["el3d/_solve_deformation/loss_main"])
+    assert abs(float(ld["main"]) - ref) <= TOL * abs(ref), (float(ld["main"]), ref)
+    model.optimizer.zero_grad()
+    ld["main"].backward()
+    assert nerr(flat_grad(model.deformation_field), g3["el3d/_solve_deformation/grad_f"]) < TOL
+    set_flat(model.deformation_field, g3["el3d/f/params0"])
+    model._reset_optimizer()
+    trace = []
+    owner = types.SimpleNamespace()
+    for it in range(2):
+        patch(it)
+        with _jet.call_scope(owner):
+            ld = body(model)
+        model._update_network(ld)
+        trace.append([float(ld[k]) for k in sorted(ld)])
+    assert nerr(np.array(trace), g3["el3d/_solve_deformation/loss_trace"]) < TOL
+    check_update(flat(model.deformation_field), g3["el3d/f/params0"], g3["el3d/_solve_deformation/f_after"],
+                 g3["el3d/_solve_deformation/grad_f"])
+
+
 def test_training_loop_graph_matches_eager(ph):
     """insr_graph=True (hipGraph replay) gives the same trajectory as eager execution."""
     from pde.fluid import Fluid2DModel

@@ -198,6 +198,28 @@ def test_elasticity_phase(phases):
     assert nrm(trace, ph["el2d/_solve_deformation/loss_trace"]) < 1e-5
 
 
+def test_elasticity3d_phase():
+    """The 3-D energy set (3x3 singular values, plane + sphere collisions incl. the
+    reference's (K, K, 3) sphere-force broadcast, external force, kinematics)."""
+    ph = dict(np.load(os.path.join(GOLD, "ref_phases_el3d.npz")))
+    specs = {"f": (3, 3, 2, 64), "f_prev": (3, 3, 2, 64), "f_pp": (3, 3, 2, 64)}
+    cfg = dict(dt=0.1, energy=[str(e) for e in ph["el3d/cfg_energy"]], ratio_arap=1e2, ratio_volume=1e3,
+               ratio_kinematics=1.0, ratio_constraint=1e4, ratio_collide=1e3, plane_height=-0.5,
+               external_force=[0.0, 0.0, -1e2], constraint_offset_right=[0.0, 0.0, 0.0],
+               circle_center=[0.0, -1.6, 0.0], circle_radius=1.0, external_force_timesteps=5)
+    X = lambda it: torch.from_numpy(ph[f"el3d/x{it}"]).clone().requires_grad_(True)  # noqa: E731
+    nets = _nets(ph, "el3d", specs)
+    ld = O.elasticity_loss(nets["f"], nets["f_prev"], nets["f_pp"], X(0), None, None, cfg, timestep=1)
+    ref = float(ph["el3d/_solve_deformation/loss_main"])
+    assert abs(float(ld["main"]) - ref) <= 1e-5 * abs(ref)
+    ld["main"].backward()
+    assert nrm(O.flat_grads(nets["f"]), ph["el3d/_solve_deformation/grad_f"]) < 1e-5
+    nets = _nets(ph, "el3d", specs)
+    trace = _run(nets, ["f"], lambda it: O.elasticity_loss(nets["f"], nets["f_prev"], nets["f_pp"], X(it), None,
+                                                           None, cfg, timestep=1), 2)
+    assert nrm(trace, ph["el3d/_solve_deformation/loss_trace"]) < 1e-5
+
+
 def test_plateau_matches_torch():
     p = torch.nn.Parameter(torch.zeros(1))
     opt = torch.optim.SGD([p], lr=1e-4)
