@@ -162,9 +162,10 @@ def kernel_identity(kind, mode, n, din, W):
     NT = W // 16
     lap = "true" if mode == "lap" else "false"
     T = lib.insr_jet_split_tiles(n, din, W, m, 1 if kind == "bwd" else 0)
+    x6 = nat.get_precision()[1 if kind == "bwd" else 0] == nat.PREC_BF16X6 and (kind == "fwd" or NT <= 8)
     if T > 0:
         nb = ((n + 15) // 16 + T - 1) // T
-        return f"insr::jet_{kind}_split<{NT}, {S}, {lap}, {T}>", nb * 64 * min(NT, 8)
+        return f"insr::jet_{kind}_{'x6' if x6 else 'split'}<{NT}, {S}, {lap}, {T}>", nb * 64 * min(NT, 8)
     return f"insr::jet_{kind}_wave<{NT}, {S}, {lap}>", ((n + 63) // 64) * 256
 
 

@@ -123,6 +123,22 @@ void insr_jet_set_split_tiles(int fwd_tiles, int bwd_tiles, int min_blocks);
 
 void insr_jet_get_split_tiles(int* fwd_tiles, int* bwd_tiles, int* min_blocks);
 
+/*
+ * Matrix-core precision of the tile-split kernels (process-wide, per direction):
+ *   INSR_PREC_F32     v_mfma_f32_16x16x4_f32: exact fp32 products, the fp32 matrix rate.
+ *   INSR_PREC_BF16X6  every fp32 operand split in three bf16 terms, six
+ *                     v_mfma_f32_16x16x32_bf16 products per K chunk, fp32 accumulation:
+ *                     fp32-level accuracy (dropped terms <= 2^-26 |a||b|) at 2.67x
+ *                     the fp32 matrix throughput.
+ * Env: INSR_JET_PREC_FWD, INSR_JET_PREC_BWD.  The saved-activation and partial
+ * layouts do not depend on it: a forward of one precision pairs with a backward of
+ * the other.
+ */
+#define INSR_PREC_F32    0
+#define INSR_PREC_BF16X6 1
+void insr_jet_set_precision(int fwd, int bwd);
+void insr_jet_get_precision(int* fwd, int* bwd);
+
 /* grad[i] = (accumulate ? grad[i] : 0) + sum_b partial[b * count + i], fixed order. */
 int insr_reduce_partials(const float* partial, int n_blocks, long count, float* grad,
                          int accumulate, void* stream);

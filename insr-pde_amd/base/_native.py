@@ -14,6 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("INSR_HIP_LIB", os.path.join(os.path.dirname(_HERE), "lib", "libinsr_hip.so"))
 
 MODE_VALUE, MODE_GRAD, MODE_LAP = 0, 1, 2
+PREC_F32, PREC_BF16X6 = 0, 1
 LOSS_COMBO, LOSS_BANDS = 0, 1
 OPT_LR, OPT_STEP, OPT_BEST, OPT_BAD, OPT_STEPSIZE, OPT_BC2SQRT, OPT_FACTOR, OPT_MINLR = range(8)
 OPT_NFLOATS = 8
@@ -46,6 +47,8 @@ SIGNATURES = {
     "insr_sq_loss_fwd": (_I, [_I, _P, _P, _P, _P, _L, _I, _F, _F, _F, _F, _F, _P, _P, _P]),
     "insr_sq_loss_bwd": (_I, [_I, _P, _P, _P, _P, _L, _I, _F, _F, _F, _F, _F, _P, _P, _P, _P, _P, _P]),
     "insr_jet_set_split_tiles": (None, [_I, _I, _I]),
+    "insr_jet_set_precision": (None, [_I, _I]),
+    "insr_jet_get_precision": (None, [_P, _P]),
     "insr_jet_get_split_tiles": (None, [_P, _P, _P]),
     "insr_reduce_partials": (_I, [_P, _I, _L, _P, _I, _P]),
     "insr_adam_prepare": (_I, [_P, _F, _F, _P]),
@@ -107,6 +110,16 @@ def get_split_tiles():
 
 def set_split_tiles(fwd_tiles, bwd_tiles, min_blocks):
     lib().insr_jet_set_split_tiles(int(fwd_tiles), int(bwd_tiles), int(min_blocks))
+
+
+def get_precision():
+    v = [ctypes.c_int(), ctypes.c_int()]
+    lib().insr_jet_get_precision(*[ctypes.byref(a) for a in v])
+    return tuple(a.value for a in v)
+
+
+def set_precision(fwd, bwd):
+    lib().insr_jet_set_precision(int(fwd), int(bwd))
 
 
 def ptr(t):

@@ -69,9 +69,35 @@ static void tiles_init() {
   }
 }
 
+// Matrix-core precision of the tile-split kernels: INSR_PREC_F32 (v_mfma_f32_16x16x4_f32)
+// or INSR_PREC_BF16X6 (jet_x6.hpp: fp32-accurate split-bf16 products).  Env overrides
+// INSR_JET_PREC_FWD / INSR_JET_PREC_BWD.
+static int g_prec[2] = {-1, -1};  // fwd, bwd
+
+static void prec_init() {
+  if (g_prec[0] < 0) {
+    // default: split-bf16 matrix cores (same accuracy as fp32 MFMA, measured faster:
+    // tools/prec_errors.py, tools/kbench.py, profiles/r01/kbench_x6.jsonl)
+    g_prec[0] = env_or("INSR_JET_PREC_FWD", INSR_PREC_BF16X6);
+    g_prec[1] = env_or("INSR_JET_PREC_BWD", INSR_PREC_BF16X6);
+  }
+}
+
+bool use_x6(int bwd, int NT) {
+  prec_init();
+  // width 256 has no x6 backward (jet_x6_bwd.hip): fp32 tile-split there
+  return g_prec[bwd ? 1 : 0] == INSR_PREC_BF16X6 && (!bwd || NT <= 8);
+}
+
 int split_tiles(int bwd, int NT, int S, long n) {
   tiles_init();
-  const size_t plane = (size_t)S * 16 * ((16 * NT + 8) + (bwd ? 16 * NT : 0)) * sizeof(float);
+  const bool x6 = use_x6(bwd, NT);
+  // LDS per tile: fp32 planes [S][16][W+8] (+ backward h planes [S][16][W]); x6 forward:
+  // three bf16 planes [S][3][16][W+8]; x6 backward: one stream group of bf16 Z + H planes
+  // (the kernel picks the group size that fits, jet_x6.hpp x6_bwd_sg)
+  const size_t plane = x6 && !bwd ? (size_t)S * 3 * 16 * (16 * NT + 8) * 2
+                       : x6       ? (size_t)(3 * 16 * (16 * NT + 8) + 32 + 3 * 16 * 16 * NT) * 2
+                                  : (size_t)S * 16 * ((16 * NT + 8) + (bwd ? 16 * NT : 0)) * sizeof(float);
   // width 256: one tile (register budget of 8 waves x 2 row tiles); backward T = 4 only
   // for value jets (register budget of the derivative streams)
   int T = NT > 8 ? 1 : ((bwd && S > 1) ? 2 : 4);
@@ -244,6 +270,9 @@ int insr_siren_jet_fwd(const float* x, long n, int din, int dout, int L, int W, 
   if (mode == INSR_MODE_LAP && !lap) return INSR_EINVAL;
   const int S = streams_for(din, mode);
   const int NT = nt_for(W);
+  if (use_split_fwd(n, NT) && use_x6(0, NT))
+    return dispatch_fwd_x6(NT, S, mode == INSR_MODE_LAP, split_tiles(0, NT, S, n), x, (int)n, din, dout, L, params,
+                           y, dy, lap, act, (hipStream_t)stream);
   if (use_split_fwd(n, NT))
     return dispatch_fwd_split(NT, S, mode == INSR_MODE_LAP, split_tiles(0, NT, S, n), x, (int)n, din, dout, L,
                               params, y, dy, lap, act, (hipStream_t)stream);
@@ -260,6 +289,9 @@ int insr_siren_jet_bwd(const float* x, long n, int din, int dout, int L, int W, 
   const long P = insr_siren_param_count(din, dout, L, W);
   const int S = streams_for(din, mode);
   const int NT = nt_for(W);
+  if (use_split_bwd(n, S, NT) && use_x6(1, NT))
+    return dispatch_bwd_x6(NT, S, mode == INSR_MODE_LAP, split_tiles(1, NT, S, n), x, (int)n, din, dout, L, params,
+                           act, gy, gdy, glap, partial, P, (hipStream_t)stream);
   if (use_split_bwd(n, S, NT))
     return dispatch_bwd_split(NT, S, mode == INSR_MODE_LAP, split_tiles(1, NT, S, n), x, (int)n, din, dout, L,
                               params, act, gy, gdy, glap, partial, P, (hipStream_t)stream);
@@ -295,6 +327,18 @@ void insr_jet_get_split_tiles(int* fwd_tiles, int* bwd_tiles, int* min_blocks) {
   if (fwd_tiles) *fwd_tiles = g_tiles[0];
   if (bwd_tiles) *bwd_tiles = g_tiles[1];
   if (min_blocks) *min_blocks = g_tiles[2];
+}
+
+void insr_jet_set_precision(int fwd, int bwd) {
+  prec_init();
+  g_prec[0] = fwd == INSR_PREC_BF16X6 ? INSR_PREC_BF16X6 : INSR_PREC_F32;
+  g_prec[1] = bwd == INSR_PREC_BF16X6 ? INSR_PREC_BF16X6 : INSR_PREC_F32;
+}
+
+void insr_jet_get_precision(int* fwd, int* bwd) {
+  prec_init();
+  if (fwd) *fwd = g_prec[0];
+  if (bwd) *bwd = g_prec[1];
 }
 
 int insr_jet_split_threshold(void) { return split_max_n(); }

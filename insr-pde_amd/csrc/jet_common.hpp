@@ -319,6 +319,11 @@ int dispatch_fwd_split(int NT, int S, bool LAP, int T, const float* x, int N, in
 int dispatch_bwd_split(int NT, int S, bool LAP, int T, const float* x, int N, int din, int dout, int L,
                        const float* prm, const float* act, const float* gy, const float* gdy, const float* glap,
                        float* part, long P, hipStream_t st);
+int dispatch_fwd_x6(int NT, int S, bool LAP, int T, const float* x, int N, int din, int dout, int L,
+                    const float* prm, float* y, float* dy, float* lap, float* act, hipStream_t st);
+int dispatch_bwd_x6(int NT, int S, bool LAP, int T, const float* x, int N, int din, int dout, int L,
+                    const float* prm, const float* act, const float* gy, const float* gdy, const float* glap,
+                    float* part, long P, hipStream_t st);
 
 // (S, LAP) combinations: value (1), grad d=1..3 (2..4), lap d=1,2 (3,4)
 #define INSR_DISPATCH(NTV, FN, ...)                \

@@ -1,0 +1,776 @@
+// jet_x6.hpp -- tile-split SIREN jet kernels on the bf16 matrix cores with
+// fp32-level accuracy ("bf16x6": every fp32 GEMM operand split in three bf16
+// terms, six MFMA products per product pair).
+//
+// gfx950 has no xf32 path: the fp32 MFMA (v_mfma_f32_16x16x4_f32) runs at 1/16 of
+// the bf16 rate.  An fp32 value a is split exactly enough into
+//     a = a_h + a_m + a_l,   a_h = bf16(a), a_m = bf16(a - a_h), a_l = bf16(a - a_h - a_m)
+// (8 + 8 + 8 significant bits, representation error <= 2^-26 |a|), and
+//     a.b ~= a_m b_m + a_h b_l + a_l b_h + a_h b_m + a_m b_h + a_h b_h
+// drops only terms <= 2^-26 |a||b| (a_m b_l, a_l b_m, a_l b_l).  Each bf16
+// product is exact in fp32 and the MFMA accumulates in fp32, so a K-long dot
+// product carries the error of an fp32 GEMM (K roundings of 2^-24) plus ~2^-25
+// per term -- the same order as the reference's own fp32 addmm chain.  Six
+// v_mfma_f32_16x16x32_bf16 (16 cycles each, K = 32) replace eight
+// v_mfma_f32_16x16x4_f32 (32 cycles each) per 32-deep K chunk: 2.67x the matrix
+// throughput of the exact-fp32 kernels in jet_split.hpp.
+//
+// Geometry and HBM layouts are those of jet_split.hpp (same saved-activation
+// layout, same partial-gradient rows), so an x6 forward pairs with either
+// backward.  What changes:
+//   * the activations a block exchanges through LDS are stored pre-split, as
+//     three bf16 planes [t][s][q = h,m,l][16 points][W + 8]; a B fragment
+//     (8 consecutive neurons of one point) is one ds_read_b128 per plane;
+//   * every wave splits its own weight rows (the A operand) at load.
+// The K index of a 16x16x32 fragment is k = 8 (lane >> 4) + j, j = 0..7
+// (A[row lane & 15][k], B[k][col lane & 15]); outputs keep the 16x16 C layout
+// (rows 4 (lane >> 4) + r), which is what the sine jet and the saved layout use.
+#pragma once
+#include "jet_split.hpp"
+
+namespace insr {
+
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
+
+// (a, b) -> packed bf16 pair, round to nearest even (v_cvt_pk_bf16_f32); a in the low half
+__device__ __forceinline__ unsigned pk_bf16(float a, float b) {
+  const bf16x2v v = {(__bf16)a, (__bf16)b};
+  return __builtin_bit_cast(unsigned, v);
+}
+__device__ __forceinline__ float bf_lo(unsigned p) { return __builtin_bit_cast(float, p << 16); }
+__device__ __forceinline__ float bf_hi(unsigned p) { return __builtin_bit_cast(float, p & 0xffff0000u); }
+
+// three-term split of the pair (a, b): a = lo16(h) + lo16(m) + lo16(l), b likewise in the high halves
+__device__ __forceinline__ void split3(float a, float b, unsigned& h, unsigned& m, unsigned& l) {
+  h = pk_bf16(a, b);
+  float ra = a - bf_lo(h), rb = b - bf_hi(h);
+  m = pk_bf16(ra, rb);
+  ra -= bf_lo(m);
+  rb -= bf_hi(m);
+  l = pk_bf16(ra, rb);
+}
+
+struct Frag3 {
+  u32x4 h, m, l;
+};
+
+// 8 fp32 (k = j, j = 0..7: v0[0..3], v1[0..3]) -> one A/B fragment in three planes
+__device__ __forceinline__ Frag3 split_frag(const floatx4& v0, const floatx4& v1) {
+  unsigned h[4], m[4], l[4];
+  split3(v0[0], v0[1], h[0], m[0], l[0]);
+  split3(v0[2], v0[3], h[1], m[1], l[1]);
+  split3(v1[0], v1[1], h[2], m[2], l[2]);
+  split3(v1[2], v1[3], h[3], m[3], l[3]);
+  Frag3 f;
+  f.h = u32x4{h[0], h[1], h[2], h[3]};
+  f.m = u32x4{m[0], m[1], m[2], m[3]};
+  f.l = u32x4{l[0], l[1], l[2], l[3]};
+  return f;
+}
+
+__device__ __forceinline__ floatx4 mfma_bf(const u32x4& a, const u32x4& b, floatx4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c,
+                                                 0, 0, 0);
+}
+
+// c += A B over one 32-deep K chunk at fp32-level accuracy (small terms first)
+__device__ __forceinline__ floatx4 mfma_x6(const Frag3& a, const Frag3& b, floatx4 c) {
+  c = mfma_bf(a.m, b.m, c);
+  c = mfma_bf(a.h, b.l, c);
+  c = mfma_bf(a.l, b.h, c);
+  c = mfma_bf(a.h, b.m, c);
+  c = mfma_bf(a.m, b.h, c);
+  c = mfma_bf(a.h, b.h, c);
+  return c;
+}
+
+#ifndef X6_MAX_WAVES
+#define X6_MAX_WAVES 8
+#endif
+template <int NT>
+struct X6Geo {
+  static constexpr int W = 16 * NT;
+  static constexpr int WV = NT < X6_MAX_WAVES ? NT : X6_MAX_WAVES;  // waves per block
+  static constexpr int RPW = NT / WV;         // row tiles per wave
+  static constexpr int KC = NT / 2;           // 32-deep K chunks of a hidden layer
+  static constexpr int LDB = W + 8;           // point row of a bf16 plane (elements): conflict-free b128 reads
+  static constexpr int PLANE = 16 * LDB;      // one (tile, stream, term) plane, bf16 elements
+  static constexpr int THREADS = 64 * WV;
+};
+
+template <int NT, int S, int T>
+constexpr size_t fwd_x6_lds_bytes() {
+  using G = X6Geo<NT>;
+  const size_t planes = (size_t)T * S * 3 * G::PLANE * 2;
+  const size_t red = (size_t)G::WV * T * S * 3 * 16 * sizeof(float);  // output-layer combine
+  return planes > red ? planes : red;
+}
+
+// hidden-layer A fragments of this wave's row tile rt: W[16 rt + c][32 kc + 8 g + j]
+template <int NT>
+__device__ __forceinline__ Frag3 load_w_frag(const float* __restrict__ Wj, int rt, int kc, int g, int c) {
+  constexpr int W = 16 * NT;
+  const float* p = Wj + (16 * rt + c) * W + 32 * kc + 8 * g;
+  const floatx4 v0 = *reinterpret_cast<const floatx4*>(p);
+  const floatx4 v1 = *reinterpret_cast<const floatx4*>(p + 4);
+  return split_frag(v0, v1);
+}
+
+template <int NT, int S, bool LAP, int T>
+__global__ __launch_bounds__(X6Geo<NT>::THREADS) void jet_fwd_x6(
+    const float* __restrict__ x, int N, int din, int dout, int L, const float* __restrict__ prm,
+    float* __restrict__ y, float* __restrict__ dy, float* __restrict__ lap, float* __restrict__ act) {
+  using G = X6Geo<NT>;
+  constexpr int W = G::W, RPW = G::RPW, LDB = G::LDB, WV = G::WV, PLANE = G::PLANE, KC = G::KC;
+  constexpr int NTAN = LAP ? S - 2 : S - 1;
+  extern __shared__ __attribute__((aligned(16))) float lds_f[];
+  unsigned short* lds = reinterpret_cast<unsigned short*>(lds_f);
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
+  const int ntiles = ((N + 63) / 64) * 4;
+  const int tile0 = blockIdx.x * T;
+  const int rt0 = wave * RPW;
+
+  float xv[T][3];
+#pragma unroll
+  for (int t = 0; t < T; ++t) {
+    const int p = (tile0 + t) * 16 + c;
+    for (int k = 0; k < 3; ++k) xv[t][k] = (p < N && k < din) ? x[(long)p * din + k] : 0.f;
+  }
+
+  floatx4 a[T][RPW][S];
+  {  // layer 0 (K = d_in: VALU, exact fp32)
+    const float* W0 = prm;
+    const float* b0 = prm + (long)W * din;
+#pragma unroll
+    for (int i = 0; i < RPW; ++i) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int n = 16 * (rt0 + i) + 4 * g + r;
+        const float bn = b0[n];
+        float w0[3] = {0.f, 0.f, 0.f};
+        for (int k = 0; k < din; ++k) w0[k] = W0[n * din + k];
+#pragma unroll
+        for (int t = 0; t < T; ++t) {
+          float z = bn;
+          for (int k = 0; k < din; ++k) z = fmaf(w0[k], xv[t][k], z);
+          a[t][i][0][r] = z;
+#pragma unroll
+          for (int k = 0; k < NTAN; ++k) a[t][i][1 + k][r] = w0[k];
+          if constexpr (LAP) a[t][i][S - 1][r] = 0.f;
+        }
+      }
+    }
+  }
+  for (int j = 0; j <= L; ++j) {
+    if (j > 0) {
+      const float* Wj = prm + hidden_off(din, W, j);
+      const float* bj = Wj + (long)W * W;
+#pragma unroll
+      for (int i = 0; i < RPW; ++i) {
+        const int rt = rt0 + i;
+        Frag3 wf[KC];
+#pragma unroll
+        for (int kc = 0; kc < KC; ++kc) wf[kc] = load_w_frag<NT>(Wj, rt, kc, g, c);
+        const floatx4 bias = *reinterpret_cast<const floatx4*>(bj + 16 * rt + 4 * g);
+#pragma unroll
+        for (int t = 0; t < T; ++t) {
+          a[t][i][0] = bias;
+#pragma unroll
+          for (int s = 1; s < S; ++s) a[t][i][s] = floatx4{0.f, 0.f, 0.f, 0.f};
+        }
+#pragma unroll
+        for (int kc = 0; kc < KC; ++kc) {
+#pragma unroll
+          for (int t = 0; t < T; ++t)
+#pragma unroll
+            for (int s = 0; s < S; ++s) {
+              const unsigned short* pb = lds + (t * S + s) * 3 * PLANE + c * LDB + 32 * kc + 8 * g;
+              Frag3 hf;
+              hf.h = *reinterpret_cast<const u32x4*>(pb);
+              hf.m = *reinterpret_cast<const u32x4*>(pb + PLANE);
+              hf.l = *reinterpret_cast<const u32x4*>(pb + 2 * PLANE);
+              a[t][i][s] = mfma_x6(wf[kc], hf, a[t][i][s]);
+            }
+        }
+      }
+      __syncthreads();  // every wave has read layer j-1
+    }
+    if (act) {
+#pragma unroll
+      for (int t = 0; t < T; ++t) {
+        float* base = act_base(act, j, ntiles, tile0 + t, S, NT);
+#pragma unroll
+        for (int i = 0; i < RPW; ++i)
+#pragma unroll
+          for (int s = 0; s < S; ++s)
+            *reinterpret_cast<floatx4*>(base + ((s * NT + rt0 + i) * 64 + lane) * 4) = a[t][i][s];
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < T; ++t) sine_jet<RPW, S, LAP>(a[t]);
+    if (j < L) {
+#pragma unroll
+      for (int t = 0; t < T; ++t)
+#pragma unroll
+        for (int i = 0; i < RPW; ++i)
+#pragma unroll
+          for (int s = 0; s < S; ++s) {
+            unsigned h0, m0, l0, h1, m1, l1;
+            split3(a[t][i][s][0], a[t][i][s][1], h0, m0, l0);
+            split3(a[t][i][s][2], a[t][i][s][3], h1, m1, l1);
+            unsigned short* pw = lds + (t * S + s) * 3 * PLANE + c * LDB + 16 * (rt0 + i) + 4 * g;
+            *reinterpret_cast<u32x2*>(pw) = u32x2{h0, h1};
+            *reinterpret_cast<u32x2*>(pw + PLANE) = u32x2{m0, m1};
+            *reinterpret_cast<u32x2*>(pw + 2 * PLANE) = u32x2{l0, l1};
+          }
+      __syncthreads();
+    }
+  }
+  // output layer (exact fp32 VALU): each wave sums its own neurons, waves combine through LDS
+  float* red = lds_f;  // [WV][T][S][3][16]
+  const float* Wo = prm + out_off(din, W, L);
+  const float* bo = Wo + (long)dout * W;
+  for (int o = 0; o < dout; ++o) {
+    float sv[T][S];
+#pragma unroll
+    for (int t = 0; t < T; ++t)
+#pragma unroll
+      for (int s = 0; s < S; ++s) sv[t][s] = 0.f;
+#pragma unroll
+    for (int i = 0; i < RPW; ++i) {
+      const floatx4 w4 = *reinterpret_cast<const floatx4*>(Wo + (o * W + 16 * (rt0 + i) + 4 * g));
+#pragma unroll
+      for (int t = 0; t < T; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+          for (int s = 0; s < S; ++s) sv[t][s] = fmaf(w4[r], a[t][i][s][r], sv[t][s]);
+    }
+#pragma unroll
+    for (int t = 0; t < T; ++t)
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        float v = sv[t][s];
+        v += __shfl_xor(v, 16);
+        v += __shfl_xor(v, 32);
+        if (g == 0) red[(((wave * T + t) * S + s) * 3 + o) * 16 + c] = v;
+      }
+  }
+  __syncthreads();
+  if (wave == 0 && g < T) {  // lane group g finishes tile g
+    const int t = g;
+    const int p = (tile0 + t) * 16 + c;
+    if (p < N) {
+      for (int o = 0; o < dout; ++o) {
+        float tot[S];
+#pragma unroll
+        for (int s = 0; s < S; ++s) {
+          tot[s] = 0.f;
+#pragma unroll
+          for (int w = 0; w < WV; ++w) tot[s] += red[(((w * T + t) * S + s) * 3 + o) * 16 + c];
+        }
+        y[(long)p * dout + o] = tot[0] + bo[o];
+        if (dy)
+          for (int k = 0; k < NTAN; ++k) dy[((long)p * dout + o) * din + k] = tot[1 + k];
+        if constexpr (LAP) {
+          if (lap) lap[(long)p * dout + o] = tot[S - 1];
+        }
+      }
+    }
+  }
+}
+
+template <int NT, int S, bool LAP, int T>
+int launch_fwd_x6_t(const float* x, int N, int din, int dout, int L, const float* prm, float* y, float* dy,
+                    float* lap, float* act, hipStream_t st) {
+  constexpr size_t lds = fwd_x6_lds_bytes<NT, S, T>();
+  if constexpr (lds > kLdsMax) {
+    return INSR_EINVAL;
+  } else {
+    const int nb = ((N + 15) / 16 + T - 1) / T;
+    static bool attr_set = false;
+    if (!attr_set) {
+      (void)hipFuncSetAttribute((const void*)jet_fwd_x6<NT, S, LAP, T>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)lds);
+      attr_set = true;
+    }
+    hipLaunchKernelGGL((jet_fwd_x6<NT, S, LAP, T>), dim3(nb), dim3(X6Geo<NT>::THREADS), lds, st, x, N, din, dout, L,
+                       prm, y, dy, lap, act);
+    return (int)hipGetLastError();
+  }
+}
+
+}  // namespace insr
+
+namespace insr {
+
+// ---------------------------------------------------------------------------
+// backward.  Per layer j (after the lane-local sine reverse, zb in registers):
+//   for each stream group (SG streams of all T tiles -- the LDS holds one group):
+//     write zb  -> Z planes, point-major  [set][q][16 p][W + 8]   (b64 per plane)
+//           h_{j-1} (rebuilt from the saved z + sin/cos)
+//              -> H planes, neuron-major [set][q][W][16 p]        (b16 per plane)
+//     dW_j (this wave's rows n, all columns m):  K = (set, point) in 32-deep chunks of
+//           two 16-point sets; A = zb[n][p] (column reads of Z), B = h[m][p] (one b128
+//           per plane of H); accumulates over the groups in registers
+//     propagation of the group's streams:  hb_{j-1}[m] = sum_n W[n][m] zb[n];
+//           A = W^T rows m of this wave (strided L2 loads, split once per layer),
+//           B = Z rows (one b128 per plane)
+// ---------------------------------------------------------------------------
+// LDS images are pre-split bf16 planes (the producer splits each value once):
+// Z [set][q][16 p][W + 8], H [set][q][W][16 p]; the dW A operand comes from u16 column
+// reads of Z.  (Measured alternative, fp32 planes split by every reader: 1.4-2x slower --
+// the reader-side split is 8x redundant VALU work across the block's waves.)
+// h-stream s of a sine layer from the derivative z-streams held in registers
+// (zd[s - 1] = stream s >= 1) + sin/cos
+template <int S, bool LAP>
+__device__ __forceinline__ floatx4 h_from_regs(int s, const floatx4 (&zd)[S - 1], const floatx4& sn,
+                                               const floatx4& cs) {
+  constexpr int NTAN = LAP ? S - 2 : S - 1;
+  if (s == 0) return sn;
+  floatx4 out;
+  if (LAP && s == S - 1) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float t2 = 0.f;
+#pragma unroll
+      for (int i = 0; i < NTAN; ++i) t2 = fmaf(zd[i][r], zd[i][r], t2);
+      out[r] = OMEGA * cs[r] * zd[s - 1][r] - OMEGA2 * sn[r] * t2;
+    }
+  } else {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) out[r] = OMEGA * cs[r] * zd[s - 1][r];
+  }
+  return out;
+}
+
+// Scheduling fence between the unrolled fragment iterations of the backward: keeps the
+// compiler from hoisting every iteration's LDS reads to the top (register spills);
+// the MFMAs of one iteration still cover the next iteration's reads of the other wave.
+#ifndef X6_NO_FENCE
+#define X6_SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
+#else
+#define X6_SCHED_FENCE() \
+  do {                   \
+  } while (0)
+#endif
+
+template <int NT>
+struct X6BwdGeo {
+  using G = X6Geo<NT>;
+  static constexpr int W = G::W;
+  static constexpr int ZROW = G::LDB;                  // elements of a Z point row
+  static constexpr int ZPLANE = 16 * ZROW;
+  static constexpr int ZSET = 3 * ZPLANE + 32;         // +16 dwords: the four lane groups of a
+                                                       // column read hit disjoint banks
+  static constexpr int HPLANE = W * 16;
+  static constexpr int HSET = 3 * HPLANE;
+  static constexpr size_t SET_BYTES = (size_t)(ZSET + HSET) * 2;
+};
+
+// streams per LDS group: all S if T tiles of them fit, else S/2, else 1
+template <int NT, int S, int T>
+constexpr int x6_bwd_sg() {
+  constexpr size_t set = X6BwdGeo<NT>::SET_BYTES;
+  if ((size_t)T * S * set <= kLdsMax) return S;
+  if (S % 2 == 0 && (size_t)T * (S / 2) * set <= kLdsMax) return S / 2;
+  return 1;
+}
+
+template <int NT, int S, int T>
+constexpr size_t bwd_x6_lds_bytes() {
+  return (size_t)T * x6_bwd_sg<NT, S, T>() * X6BwdGeo<NT>::SET_BYTES;
+}
+
+template <int NT, int S, bool LAP, int T>
+__global__ __launch_bounds__(X6Geo<NT>::THREADS) void jet_bwd_x6(
+    const float* __restrict__ x, int N, int din, int dout, int L, const float* __restrict__ prm,
+    const float* __restrict__ act, const float* __restrict__ gy, const float* __restrict__ gdy,
+    const float* __restrict__ glap, float* __restrict__ part, long P) {
+  using G = X6Geo<NT>;
+  using BG = X6BwdGeo<NT>;
+  constexpr int W = G::W, RPW = G::RPW, KC = G::KC;
+  constexpr int LDB = BG::ZROW, ZPLANE = BG::ZPLANE, ZSET = BG::ZSET, HPLANE = BG::HPLANE, HSET = BG::HSET;
+  constexpr int NTAN = LAP ? S - 2 : S - 1;
+  constexpr int SG = x6_bwd_sg<NT, S, T>();
+  constexpr int NG = S / SG;            // stream groups per layer
+  constexpr int NSET = T * SG;          // 16-point sets per group
+  constexpr int NCH = (NSET + 1) / 2;   // 32-deep K chunks of the weight gradient
+  static_assert(S % SG == 0, "stream groups");
+  static_assert(NG == 1 || RPW * NT <= 16, "dW accumulators across groups");
+  extern __shared__ __attribute__((aligned(16))) float lds_f[];
+  unsigned short* Z = reinterpret_cast<unsigned short*>(lds_f);
+  unsigned short* H = Z + NSET * ZSET;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
+  const int ntiles = ((N + 63) / 64) * 4;
+  const int tile0 = blockIdx.x * T;
+  const int rt0 = wave * RPW;
+  float* mypart = part + (long)blockIdx.x * P;
+
+  // adjoint of output o, stream s, at this lane's point of tile t (0 outside / for NULL);
+  // read where used: the backward's register budget is tight
+  auto adjoint = [&](int t, int s, int o) -> float {
+    const int p = (tile0 + t) * 16 + c;
+    if (p >= N) return 0.f;
+    if (s == 0) return gy ? gy[(long)p * dout + o] : 0.f;
+    if (LAP && s == S - 1) return glap ? glap[(long)p * dout + o] : 0.f;
+    return gdy ? gdy[((long)p * dout + o) * din + (s - 1)] : 0.f;
+  };
+
+  auto load_sc = [&](int layer, floatx4(&s_)[T][RPW], floatx4(&c_)[T][RPW]) {
+    floatx4 z[T][RPW];
+    float amax = 0.f;
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+      const float* base = act_base(act, layer, ntiles, tile0 + t, S, NT);
+#pragma unroll
+      for (int i = 0; i < RPW; ++i) {
+        z[t][i] = *reinterpret_cast<const floatx4*>(base + ((rt0 + i) * 64 + lane) * 4);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) amax = fmaxf(amax, fabsf(OMEGA * z[t][i][r]));
+      }
+    }
+    const bool big = wave_any_big(amax);
+#pragma unroll
+    for (int t = 0; t < T; ++t)
+#pragma unroll
+      for (int i = 0; i < RPW; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float sv, cv;
+          if (big)
+            sincosf(OMEGA * z[t][i][r], &sv, &cv);
+          else
+            sincos_fast(OMEGA * z[t][i][r], sv, cv);
+          s_[t][i][r] = sv;
+          c_[t][i][r] = cv;
+        }
+  };
+
+  // ---- output layer (exact fp32 VALU) ----
+  floatx4 sn[T][RPW], cs[T][RPW];
+  load_sc(L, sn, cs);
+  const float* Wo = prm + out_off(din, W, L);
+  const long wo_off = out_off(din, W, L);
+  floatx4 hb[T][RPW][S];
+#pragma unroll
+  for (int t = 0; t < T; ++t)
+#pragma unroll
+    for (int i = 0; i < RPW; ++i)
+#pragma unroll
+      for (int s = 0; s < S; ++s) hb[t][i][s] = floatx4{0.f, 0.f, 0.f, 0.f};
+  for (int o = 0; o < dout; ++o) {
+    float ga[T][S];
+#pragma unroll
+    for (int t = 0; t < T; ++t)
+#pragma unroll
+      for (int s = 0; s < S; ++s) ga[t][s] = adjoint(t, s, o);
+#pragma unroll
+    for (int i = 0; i < RPW; ++i) {
+      const int rt = rt0 + i;
+      const floatx4 w4 = *reinterpret_cast<const floatx4*>(Wo + (o * W + 16 * rt + 4 * g));
+      floatx4 acc4 = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int t = 0; t < T; ++t) {
+        const float* baseL = act_base(act, L, ntiles, tile0 + t, S, NT);
+#pragma unroll
+        for (int s = 0; s < S; ++s) {
+          const floatx4 hs = h_stream<NT, S, LAP>(baseL, s, rt, lane, sn[t][i], cs[t][i]);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            acc4[r] = fmaf(ga[t][s], hs[r], acc4[r]);
+            hb[t][i][s][r] = fmaf(w4[r], ga[t][s], hb[t][i][s][r]);
+          }
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float v = sum16(acc4[r]);
+        if (c == 0) mypart[wo_off + (long)o * W + 16 * rt + 4 * g + r] = v;
+      }
+    }
+    if (wave == 0) {  // db_out[o]: every point counted once (lane group g == 0)
+      float v = 0.f;
+#pragma unroll
+      for (int t = 0; t < T; ++t) v += (g == 0) ? ga[t][0] : 0.f;
+      v = sum16(v);
+      if (lane == 0) mypart[wo_off + (long)dout * W + o] = v;
+    }
+  }
+
+  // ---- sine layers j = L .. 0 ----
+  // KZ: the derivative z-streams of layer j-1 are loaded once (early, before the first
+  // barrier of layer j) and serve both h_{j-1} and the sine reverse of layer j-1
+#ifndef X6_KZ_MAX
+#define X6_KZ_MAX 3  // measured: keeping more z-streams costs spills (LAP/GRAD at T = 2)
+#endif
+  constexpr bool KZ = S > 1 && T * RPW * (S - 1) <= X6_KZ_MAX;
+  constexpr int ZK = KZ ? S - 1 : 1;  // streams 1 .. S-1 (zk[..][s - 1])
+  floatx4 zk[KZ ? T : 1][KZ ? RPW : 1][ZK];
+  auto load_zk = [&](int layer) {
+    if constexpr (KZ) {
+#pragma unroll
+      for (int t = 0; t < T; ++t) {
+        const float* base = act_base(act, layer, ntiles, tile0 + t, S, NT);
+#pragma unroll
+        for (int i = 0; i < RPW; ++i)
+#pragma unroll
+          for (int s = 1; s < S; ++s)
+            zk[t][i][s - 1] = *reinterpret_cast<const floatx4*>(base + ((s * NT + rt0 + i) * 64 + lane) * 4);
+      }
+    }
+  };
+  load_zk(L);
+  for (int j = L; j >= 0; --j) {
+    INSR_STAMP(L - j, 0);
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+      const float* basej = act_base(act, j, ntiles, tile0 + t, S, NT);
+#pragma unroll
+      for (int i = 0; i < RPW; ++i) {
+        if constexpr (KZ) {
+          floatx4 zs[S];
+          zs[0] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int s = 1; s < S; ++s) zs[s] = zk[t][i][s - 1];
+          sine_rev<S, LAP>(hb[t][i], zs, sn[t][i], cs[t][i]);
+        } else {
+          floatx4 zs[S];
+#pragma unroll
+          for (int s = 0; s < S; ++s)
+            zs[s] = (s == 0) ? floatx4{0.f, 0.f, 0.f, 0.f}
+                             : *reinterpret_cast<const floatx4*>(basej + ((s * NT + rt0 + i) * 64 + lane) * 4);
+          sine_rev<S, LAP>(hb[t][i], zs, sn[t][i], cs[t][i]);
+        }
+      }
+    }
+    const long boff = (j == 0) ? (long)W * din : hidden_off(din, W, j) + (long)W * W;
+#pragma unroll
+    for (int i = 0; i < RPW; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float v = 0.f;
+#pragma unroll
+        for (int t = 0; t < T; ++t) v += hb[t][i][0][r];
+        v = sum16(v);
+        if (c == 0) mypart[boff + 16 * (rt0 + i) + 4 * g + r] = v;
+      }
+    if (j == 0) {
+#pragma unroll
+      for (int i = 0; i < RPW; ++i)
+        for (int k = 0; k < din; ++k)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float v = 0.f;
+#pragma unroll
+            for (int t = 0; t < T; ++t) {
+              const int p = (tile0 + t) * 16 + c;
+              const float xk = p < N ? x[(long)p * din + k] : 0.f;
+              v = fmaf(hb[t][i][0][r], xk, v);
+              if (k < NTAN) v += hb[t][i][1 + k][r];
+            }
+            v = sum16(v);
+            if (c == 0) mypart[(long)(16 * (rt0 + i) + 4 * g + r) * din + k] = v;
+          }
+      break;
+    }
+    INSR_STAMP(L - j, 1);
+    const float* Wj = prm + hidden_off(din, W, j);
+    // A operand of the propagation: W^T rows m = 16 rt + c, k = n = 32 kc + 8 g + jj
+    // (strided L2 loads issued here).  One group: split once; several groups: the raw
+    // values stay live and each group splits them again (fewer registers across groups)
+    floatx4 wraw[RPW][KC][2];
+    Frag3 wt[RPW][KC];
+#pragma unroll
+    for (int i = 0; i < RPW; ++i)
+#pragma unroll
+      for (int kc = 0; kc < KC; ++kc) {
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          wraw[i][kc][0][jj] = Wj[(32 * kc + 8 * g + jj) * W + 16 * (rt0 + i) + c];
+          wraw[i][kc][1][jj] = Wj[(32 * kc + 8 * g + 4 + jj) * W + 16 * (rt0 + i) + c];
+        }
+        if constexpr (NG == 1) wt[i][kc] = split_frag(wraw[i][kc][0], wraw[i][kc][1]);
+      }
+    floatx4 snp[T][RPW], csp[T][RPW];
+    load_sc(j - 1, snp, csp);
+    load_zk(j - 1);
+    floatx4 dacc[RPW][NT];
+#pragma unroll
+    for (int i = 0; i < RPW; ++i)
+#pragma unroll
+      for (int ct = 0; ct < NT; ++ct) dacc[i][ct] = floatx4{0.f, 0.f, 0.f, 0.f};
+    floatx4 nh[T][RPW][S];
+#pragma unroll
+    for (int gi = 0; gi < NG; ++gi) {
+      const int s0 = gi * SG;
+      INSR_STAMP(L - j, 2);
+      __syncthreads();  // the previous group's / layer's LDS readers are done
+      INSR_STAMP(L - j, 3);
+#pragma unroll
+      for (int t = 0; t < T; ++t) {
+        const float* basep = act_base(act, j - 1, ntiles, tile0 + t, S, NT);
+#pragma unroll
+        for (int i = 0; i < RPW; ++i)
+#pragma unroll
+          for (int sl = 0; sl < SG; ++sl) {
+            const int s = s0 + sl;
+            const int u = t * SG + sl;
+            const int col = 16 * (rt0 + i) + 4 * g;
+            unsigned h0, m0, l0, h1, m1, l1;
+            split3(hb[t][i][s][0], hb[t][i][s][1], h0, m0, l0);
+            split3(hb[t][i][s][2], hb[t][i][s][3], h1, m1, l1);
+            unsigned short* pz = Z + u * ZSET + c * LDB + col;
+            *reinterpret_cast<u32x2*>(pz) = u32x2{h0, h1};
+            *reinterpret_cast<u32x2*>(pz + ZPLANE) = u32x2{m0, m1};
+            *reinterpret_cast<u32x2*>(pz + 2 * ZPLANE) = u32x2{l0, l1};
+            floatx4 hs;
+            if constexpr (KZ) {
+              hs = h_from_regs<S, LAP>(s, zk[t][i], snp[t][i], csp[t][i]);
+            } else {
+              hs = h_stream<NT, S, LAP>(basep, s, rt0 + i, lane, snp[t][i], csp[t][i]);
+            }
+            split3(hs[0], hs[1], h0, m0, l0);
+            split3(hs[2], hs[3], h1, m1, l1);
+            unsigned short* ph = H + u * HSET + col * 16 + c;  // rows m = col + r, point c
+            ph[0] = (unsigned short)h0;
+            ph[16] = (unsigned short)(h0 >> 16);
+            ph[32] = (unsigned short)h1;
+            ph[48] = (unsigned short)(h1 >> 16);
+            ph[HPLANE] = (unsigned short)m0;
+            ph[HPLANE + 16] = (unsigned short)(m0 >> 16);
+            ph[HPLANE + 32] = (unsigned short)m1;
+            ph[HPLANE + 48] = (unsigned short)(m1 >> 16);
+            ph[2 * HPLANE] = (unsigned short)l0;
+            ph[2 * HPLANE + 16] = (unsigned short)(l0 >> 16);
+            ph[2 * HPLANE + 32] = (unsigned short)l1;
+            ph[2 * HPLANE + 48] = (unsigned short)(l1 >> 16);
+          }
+      }
+      INSR_STAMP(L - j, 4);
+      __syncthreads();
+      INSR_STAMP(L - j, 5);
+      // dW_j rows n = 16 rt + c (A), columns m (B); K = sets x 16 points
+#pragma unroll
+      for (int ch = 0; ch < NCH; ++ch) {
+        const int u = 2 * ch + (g >> 1);
+        const bool live = u < NSET;
+        const int p0 = 8 * (g & 1);
+#pragma unroll
+        for (int i = 0; i < RPW; ++i) {
+          Frag3 af;
+          {
+            const unsigned short* pa = Z + (live ? u : 0) * ZSET + p0 * LDB + 16 * (rt0 + i) + c;
+            unsigned hh[4], mm[4], ll[4];
+#pragma unroll
+            for (int d = 0; d < 4; ++d) {
+              const unsigned short* q0 = pa + (2 * d) * LDB;
+              const unsigned short* q1 = pa + (2 * d + 1) * LDB;
+              hh[d] = live ? ((unsigned)q0[0] | ((unsigned)q1[0] << 16)) : 0u;
+              mm[d] = live ? ((unsigned)q0[ZPLANE] | ((unsigned)q1[ZPLANE] << 16)) : 0u;
+              ll[d] = live ? ((unsigned)q0[2 * ZPLANE] | ((unsigned)q1[2 * ZPLANE] << 16)) : 0u;
+            }
+            af.h = u32x4{hh[0], hh[1], hh[2], hh[3]};
+            af.m = u32x4{mm[0], mm[1], mm[2], mm[3]};
+            af.l = u32x4{ll[0], ll[1], ll[2], ll[3]};
+          }
+#pragma unroll
+          for (int ct = 0; ct < NT; ++ct) {
+            Frag3 bf;
+            {
+              const unsigned short* pb = H + (live ? u : 0) * HSET + (16 * ct + c) * 16 + p0;
+              bf.h = *reinterpret_cast<const u32x4*>(pb);
+              bf.m = *reinterpret_cast<const u32x4*>(pb + HPLANE);
+              bf.l = *reinterpret_cast<const u32x4*>(pb + 2 * HPLANE);
+            }
+            dacc[i][ct] = mfma_x6(af, bf, dacc[i][ct]);
+            X6_SCHED_FENCE();
+          }
+        }
+      }
+      if constexpr (NG == 1) {  // dW_j rows of this wave: store now (frees the accumulators)
+        float* dW = mypart + hidden_off(din, W, j);
+#pragma unroll
+        for (int i = 0; i < RPW; ++i)
+#pragma unroll
+          for (int ct = 0; ct < NT; ++ct)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) dW[(16 * (rt0 + i) + 4 * g + r) * W + 16 * ct + c] = dacc[i][ct][r];
+      }
+      INSR_STAMP(L - j, 6);
+      if constexpr (NG > 1) {
+#pragma unroll
+        for (int i = 0; i < RPW; ++i)
+#pragma unroll
+          for (int kc = 0; kc < KC; ++kc) wt[i][kc] = split_frag(wraw[i][kc][0], wraw[i][kc][1]);
+      }
+      // propagation of this group's streams
+#pragma unroll
+      for (int t = 0; t < T; ++t)
+#pragma unroll
+        for (int sl = 0; sl < SG; ++sl) {
+          const int s = s0 + sl;
+          const int u = t * SG + sl;
+#pragma unroll
+          for (int i = 0; i < RPW; ++i) nh[t][i][s] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int kc = 0; kc < KC; ++kc) {
+            Frag3 bf;
+            {
+              const unsigned short* pb = Z + u * ZSET + c * LDB + 32 * kc + 8 * g;
+              bf.h = *reinterpret_cast<const u32x4*>(pb);
+              bf.m = *reinterpret_cast<const u32x4*>(pb + ZPLANE);
+              bf.l = *reinterpret_cast<const u32x4*>(pb + 2 * ZPLANE);
+            }
+#pragma unroll
+            for (int i = 0; i < RPW; ++i) nh[t][i][s] = mfma_x6(wt[i][kc], bf, nh[t][i][s]);
+            X6_SCHED_FENCE();
+          }
+        }
+    }
+    INSR_STAMP(L - j, 7);
+    if constexpr (NG > 1) {  // dW_j rows of this wave
+      float* dW = mypart + hidden_off(din, W, j);
+#pragma unroll
+      for (int i = 0; i < RPW; ++i)
+#pragma unroll
+        for (int ct = 0; ct < NT; ++ct)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) dW[(16 * (rt0 + i) + 4 * g + r) * W + 16 * ct + c] = dacc[i][ct][r];
+    }
+#pragma unroll
+    for (int t = 0; t < T; ++t)
+#pragma unroll
+      for (int i = 0; i < RPW; ++i) {
+        sn[t][i] = snp[t][i];
+        cs[t][i] = csp[t][i];
+#pragma unroll
+        for (int s = 0; s < S; ++s) hb[t][i][s] = nh[t][i][s];
+      }
+  }
+}
+
+template <int NT, int S, bool LAP, int T>
+int launch_bwd_x6_t(const float* x, int N, int din, int dout, int L, const float* prm, const float* act,
+                    const float* gy, const float* gdy, const float* glap, float* part, long P, hipStream_t st) {
+  constexpr size_t lds = bwd_x6_lds_bytes<NT, S, T>();
+  if constexpr (lds > kLdsMax || NT > 8) {
+    return INSR_EINVAL;
+  } else {
+    const int nb = ((N + 15) / 16 + T - 1) / T;
+    static bool attr_set = false;
+    if (!attr_set) {
+      (void)hipFuncSetAttribute((const void*)jet_bwd_x6<NT, S, LAP, T>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      attr_set = true;
+    }
+    hipLaunchKernelGGL((jet_bwd_x6<NT, S, LAP, T>), dim3(nb), dim3(X6Geo<NT>::THREADS), lds, st, x, N, din, dout,
+                       L, prm, act, gy, gdy, glap, part, P);
+    return (int)hipGetLastError();
+  }
+}
+
+}  // namespace insr

@@ -21,7 +21,8 @@ def B():
 
 
 def rel(a, b):
-    return float((a.double() - b.double()).abs().max() / b.double().abs().max().clamp_min(1e-30))
+    a, b = a.detach().double().cpu(), b.detach().double().cpu()
+    return float((a - b).abs().max() / b.abs().max().clamp_min(1e-30))
 
 
 CASES = [  # (alpha, beta, gamma, delta, which of b, c, d present)

@@ -29,13 +29,20 @@ NETS = {  # name: (d_in, d_out, L, W)
 
 
 BIG = 1 << 30
-VARIANTS = {  # (fwd, bwd, bwd_value) split thresholds, (fwd, bwd) forced tiles per split block
-    "wave": ((0, 0, 0), (0, 0)),                  # one wave per 16-point tile, both directions
-    "split": ((BIG, BIG, BIG), (1, 1)),           # neurons split over a block's waves, 1 tile/block
-    "split_t2": ((BIG, BIG, BIG), (2, 2)),        # 2 tiles per block (ragged last block)
-    "split_t4": ((BIG, BIG, BIG), (4, 4)),        # 4 tiles per block (capped by LDS / registers)
-    "split_fwd_wave_bwd": ((BIG, 0, 0), (4, 0)),  # mixed: the saved-activation layout is shared
-    "wave_fwd_split_bwd": ((0, BIG, BIG), (0, 2)),
+F32, X6 = 0, 1  # matrix-core precision of the tile-split kernels (insr_jet_set_precision)
+VARIANTS = {  # (fwd, bwd, bwd_value) split thresholds, (fwd, bwd) forced tiles per split block, (fwd, bwd) precision
+    "wave": ((0, 0, 0), (0, 0), (F32, F32)),                  # one wave per 16-point tile, both directions
+    "split": ((BIG, BIG, BIG), (1, 1), (F32, F32)),           # neurons split over a block's waves, 1 tile/block
+    "split_t2": ((BIG, BIG, BIG), (2, 2), (F32, F32)),        # 2 tiles per block (ragged last block)
+    "split_t4": ((BIG, BIG, BIG), (4, 4), (F32, F32)),        # 4 tiles per block (capped by LDS / registers)
+    "split_fwd_wave_bwd": ((BIG, 0, 0), (4, 0), (F32, F32)),  # mixed: the saved-activation layout is shared
+    "wave_fwd_split_bwd": ((0, BIG, BIG), (0, 2), (F32, F32)),
+    "x6": ((BIG, BIG, BIG), (1, 1), (X6, X6)),                # split-bf16 (6-product) matrix cores
+    "x6_t2": ((BIG, BIG, BIG), (2, 2), (X6, X6)),
+    "x6_t4": ((BIG, BIG, BIG), (4, 4), (X6, X6)),
+    "x6_fwd_f32_bwd": ((BIG, BIG, BIG), (4, 2), (X6, F32)),   # precisions mix: same saved layout
+    "f32_fwd_x6_bwd": ((BIG, BIG, BIG), (2, 4), (F32, X6)),
+    "x6_fwd_wave_bwd": ((BIG, 0, 0), (2, 0), (X6, F32)),
 }
 
 
@@ -47,12 +54,15 @@ def base(request):
     import base as B
     B._native.load()
     old, old_tiles = B._native.get_split_thresholds(), B._native.get_split_tiles()
-    thr, tiles = VARIANTS[request.param]
+    old_prec = B._native.get_precision()
+    thr, tiles, prec = VARIANTS[request.param]
     B._native.set_split_thresholds(*thr)
     B._native.set_split_tiles(tiles[0], tiles[1], old_tiles[2])
+    B._native.set_precision(*prec)
     yield B
     B._native.set_split_thresholds(*old)
     B._native.set_split_tiles(*old_tiles)
+    B._native.set_precision(*old_prec)
 
 
 def nerr(a, b):

@@ -18,6 +18,8 @@ import torch  # noqa: E402
 
 NETS = {"fluid_pres": (2, 1, 4, 128), "fluid_vel": (2, 2, 4, 128), "el3d": (3, 3, 5, 256)}
 PH = ["sine_rev+bias", "sincos(z_j-1)", "barrier1", "lds_write", "barrier2", "dW", "propagate"]
+# x6 backward (jet_x6.hpp): stamps of the LAST stream group of a layer
+PH_X6 = ["sine_rev+bias", "W^T frags+sincos(+prev groups)", "barrier1", "lds_write", "barrier2", "dW", "propagate"]
 
 
 def main():
@@ -25,11 +27,15 @@ def main():
     ap.add_argument("--net", default="fluid_pres")
     ap.add_argument("--mode", default="lap")
     ap.add_argument("--n", type=int, default=16384)
+    ap.add_argument("--prec", type=int, default=0, help="1: split-bf16 (x6) kernels")
     args = ap.parse_args()
     import base
     from base import _native as nat
     lib = nat.load(os.path.join(ROOT, "insr-pde_amd", "lib", "libinsr_hip_diag.so"))
     lib.insr_diag_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    lib.insr_diag_stamps_x6.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    nat.set_precision(args.prec, args.prec)
+    ph = PH_X6 if args.prec else PH
     din, dout, L, W = NETS[args.net]
     mode = {"value": 0, "grad": 1, "lap": 2}[args.mode]
     n = args.n
@@ -50,9 +56,9 @@ def main():
                                          nat.ptr(gy), nat.ptr(gdy), nat.ptr(glap), nat.ptr(part), st), "bwd")
     torch.cuda.synchronize()
     buf = (ctypes.c_ulonglong * (2 * 16 * 8 * 8))()
-    lib.insr_diag_stamps(buf, len(buf))
+    (lib.insr_diag_stamps_x6 if args.prec else lib.insr_diag_stamps)(buf, len(buf))
     T = lib.insr_jet_split_tiles(n, din, W, mode, 1)
-    print(f"{args.net} {args.mode} n={n} T={T}")
+    print(f"{args.net} {args.mode} n={n} T={T} prec={args.prec}")
     for blk in (0, 1):
         rows = []
         for wave in range(8):
@@ -66,7 +72,7 @@ def main():
         med = [sorted(r[k] for r in rows)[len(rows) // 2] for k in range(7)]
         tot = sum(med)
         print(f" block {'0' if blk == 0 else 'mid'}: layer total {tot} cyc; " +
-              ", ".join(f"{PH[k]} {med[k]} ({100 * med[k] / max(tot, 1):.0f}%)" for k in range(7)))
+              ", ".join(f"{ph[k]} {med[k]} ({100 * med[k] / max(tot, 1):.0f}%)" for k in range(7)))
 
 
 if __name__ == "__main__":

@@ -16,12 +16,16 @@ import torch  # noqa: E402
 NETS = {"fluid_pres": (2, 1, 4, 128), "fluid_vel": (2, 2, 4, 128), "advect": (1, 1, 3, 64),
         "el2d": (2, 2, 5, 128), "el3d": (3, 3, 5, 256)}
 BIG = 1 << 30
-VARIANTS = {  # label: ((fwd, bwd, bwd_value) thresholds, (fwd, bwd) forced tiles)
-    "wave": ((0, 0, 0), (0, 0)),
-    "split1": ((BIG, BIG, BIG), (1, 1)),
-    "split2": ((BIG, BIG, BIG), (2, 2)),
-    "split4": ((BIG, BIG, BIG), (4, 4)),
-    "auto": ((BIG, BIG, BIG), (0, 0)),
+VARIANTS = {  # label: ((fwd, bwd, bwd_value) thresholds, (fwd, bwd) forced tiles, (fwd, bwd) precision)
+    "wave": ((0, 0, 0), (0, 0), (0, 0)),
+    "split1": ((BIG, BIG, BIG), (1, 1), (0, 0)),
+    "split2": ((BIG, BIG, BIG), (2, 2), (0, 0)),
+    "split4": ((BIG, BIG, BIG), (4, 4), (0, 0)),
+    "auto": ((BIG, BIG, BIG), (0, 0), (0, 0)),
+    "x6": ((BIG, BIG, BIG), (0, 0), (1, 1)),
+    "x6_1": ((BIG, BIG, BIG), (1, 1), (1, 1)),
+    "x6_2": ((BIG, BIG, BIG), (2, 2), (1, 1)),
+    "x6_4": ((BIG, BIG, BIG), (4, 4), (1, 1)),
 }
 MODES = {"value": 0, "grad": 1, "lap": 2}
 
@@ -75,11 +79,12 @@ def main():
                 g = torch.zeros(P, device="cuda")
                 st = nat.stream_of(x.device)
                 for variant in args.variants.split(","):
-                    thr, tiles = VARIANTS[variant]
+                    thr, tiles, prec = VARIANTS[variant]
                     if W > 128 and variant == "wave":
                         continue
                     nat.set_split_thresholds(*thr)
                     nat.set_split_tiles(tiles[0], tiles[1], 256)
+                    nat.set_precision(*prec)
                     part = torch.empty(max(lib.insr_jet_partial_bytes(n, din, dout, L, W, mode) // 4, 1), device="cuda")
                     nb = lib.insr_jet_partial_blocks(n, din, W, mode)
                     tf_, tb_ = (lib.insr_jet_split_tiles(n, din, W, mode, 0),
