@@ -10,11 +10,16 @@ Each phase iteration is replayed from a hipGraph captured during warm-up.
 
     value = (points per phase-iteration, all ranks) x 3 phases x K / max_rank(time)
 
+Other BASELINE.json workloads (--config): fluid2DtlgnM (256^2 points), advect1D (one
+_advect phase, 4096 points), elasticity2Dstretch (one _solve_deformation phase, 20000
+points), elasticity3Dbunny (SIREN 5x256, 64^3 points); a step is one iteration of every
+phase of that model's timestep.
+
 Also reported: a roofline object for the dominant kernel (HIP events on its launch
 stream, eager re-run of the same step after the timed region) and a CPU baseline
 (the oracle restatement of the reference's torch graph, timed on this host).
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--scaling strong|weak]
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--scaling strong|weak] [--config NAME]
        (N > 1: launched by torch.distributed.run, one rank per GPU, RCCL).
 """
 import argparse
@@ -45,7 +50,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="fluid2Dtlgn")
+    ap.add_argument("--config", default="fluid2Dtlgn", choices=sorted(WORKLOADS),
+                    help="BASELINE.json workload (default: configs[1], the headline)")
     ap.add_argument("--scaling", choices=["strong", "weak"], default="weak")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the CPU-baseline sample")
@@ -71,30 +77,69 @@ def setup_dist(args):
     return world, rank, local
 
 
-def build_model(args, world):
+# BASELINE.json configs: model class, phases of one step, interior points
+# per phase iteration (global, before any sharding).  configs[1] fluid2Dtlgn is the default
+# (headline) workload; the others are measured with --config.
+WORKLOADS = {
+    "fluid2Dtlgn": dict(pde="fluid", phases=("_advect_velocity", "_solve_pressure", "_projection"), res=128,
+                        model="SIREN 4x128 velocity(2->2) + pressure(2->1)"),
+    "fluid2DtlgnM": dict(pde="fluid", phases=("_advect_velocity", "_solve_pressure", "_projection"), res=256,
+                         model="SIREN 4x128 velocity(2->2) + pressure(2->1), taylorgreen_multi"),
+    "advect1D": dict(pde="advection", phases=("_advect",), res=4096, model="SIREN 3x64 field(1->1)"),
+    "elasticity2Dstretch": dict(pde="elasticity", phases=("_solve_deformation",), res=100,
+                                model="SIREN 5x128 deformation(2->2), arap+constraint+constraint_right+volume"),
+    "elasticity3Dbunny": dict(pde="elasticity", phases=("_solve_deformation",), res=64,
+                              model="SIREN 5x256 deformation(3->3), arap+kinematics+collision+external+volume "
+                                    "(synthetic box volume)"),
+}
+
+
+def interior_points(cfg, wl):
+    """Global interior collocation points of one phase iteration."""
+    if wl["pde"] == "fluid":
+        return cfg.sample_resolution ** 2
+    if wl["pde"] == "advection":
+        return cfg.sample_resolution
+    d = cfg.dim
+    return sum(cfg.sample_resolution ** d for _ in cfg.sample_pattern)
+
+
+def build_model(args, world, rank):
     import base
     from pde.config import baseline_config
-    from pde.fluid import Fluid2DModel
     base._native.load()
-    N = 128 * 128
-    # strong: the global 16384 points are split over ranks; weak: every rank keeps 16384
-    per_rank = N // world if args.scaling == "strong" else N
-    cfg = baseline_config(args.config, sample_resolution=128, insr_points_per_rank=per_rank,
-                          insr_graph=not args.no_graph, insr_sync_every=10 ** 9, insr_progress=False,
-                          early_stop=False, proj_dir="/tmp/insr_bench", max_n_iters=10 ** 9)
-    torch.manual_seed(1234)
-    model = Fluid2DModel(cfg)
+    wl = WORKLOADS[args.config]
+    res = wl["res"]
+    cfg = baseline_config(args.config, sample_resolution=res, insr_graph=not args.no_graph,
+                          insr_sync_every=10 ** 9, insr_progress=False, early_stop=False,
+                          proj_dir="/tmp/insr_bench", max_n_iters=10 ** 9)
+    n_global = interior_points(cfg, wl)
+    if wl["pde"] in ("fluid", "advection"):
+        # strong: the global batch is split over ranks; weak: every rank keeps the full batch
+        cfg.insr_points_per_rank = n_global // world if args.scaling == "strong" else n_global
+    else:
+        # elasticity draws the global batch and keeps its rank's slice (strong); weak: no slicing
+        cfg.insr_dp_weak = args.scaling == "weak"
+    torch.manual_seed(1234)  # identical weights on every rank
+    if wl["pde"] == "fluid":
+        from pde.fluid import Fluid2DModel as M
+    elif wl["pde"] == "advection":
+        from pde.advection import Advection1DModel as M
+    else:
+        from pde.elasticity import ElasticityModel as M
+    model = M(cfg)
     model.timestep = 1
     model.init_cond_func = None
-    return model, cfg
+    torch.cuda.manual_seed(1234 + 7919 * rank)  # independent collocation points per rank
+    per_rank = n_global // world if args.scaling == "strong" else n_global
+    return model, cfg, wl, per_rank
 
 
-def phase_loops(model):
+def phase_loops(model, wl):
     from base._loop import PhaseLoop
-    from pde.fluid import Fluid2DModel
     loops = []
-    for name in ("_advect_velocity", "_solve_pressure", "_projection"):
-        pl = PhaseLoop(model, getattr(Fluid2DModel, name)._insr_phase, name, (), {})
+    for name in wl["phases"]:
+        pl = PhaseLoop(model, getattr(type(model), name)._insr_phase, name, (), {})
         pl.start()
         loops.append(pl)
     return loops
@@ -115,8 +160,13 @@ def sync_all(world):
         torch.cuda.synchronize()
 
 
-def roofline(model, loops, n_local, P_pres):
-    """Eager re-run of one step with HIP events around every jet launch."""
+def macs_per_point(din, dout, L, W):
+    """P = d_in W + L W^2 + W d_out multiply-accumulates per point per stream."""
+    return din * W + L * W * W + W * dout
+
+
+def roofline(loops, n_local):
+    """Eager re-run of one step with HIP events around every jet launch (on its launch stream)."""
     from base import _jet
     for pl in loops:  # eager path, same kernels and shapes as the captured graphs
         pl.use_graph = False
@@ -132,25 +182,33 @@ def roofline(model, loops, n_local, P_pres):
         agg.setdefault(key, []).append(e0.elapsed_time(e1))
     _jet.TIMING["events"].clear()
     per_step = {k: sum(v) / reps for k, v in agg.items()}
-    # dominant kernel = the longest launch over the interior batch (the bc bands are 1% of points)
+    # dominant kernel = the longest launch over the interior batch (boundary bands are ~1% of points)
     dom = max((k for k in per_step if k[2] == n_local and k[0] != "reduce"), key=lambda k: sum(agg[k]) / len(agg[k]))
-    kind, mode, n, W = dom
+    kind, mode, n, W, (din, dout, L) = dom
     ms = sum(agg[dom]) / len(agg[dom])
     # algorithmic flops per launch: 2P per point per stream per GEMM pass
-    P = P_pres if mode == "lap" else 2 * 128 + 4 * 128 * 128 + 128 * 2  # MACs/point/stream: pressure | velocity
-    streams = {"value": 1, "grad": 3, "lap": 4}[mode]
+    P = macs_per_point(din, dout, L, W)
+    streams = {"value": 1, "grad": 1 + din, "lap": 2 + din}[mode]
     passes = 1 if kind == "fwd" else 2
     flops = n * streams * passes * 2 * P
     achieved = flops / (ms * 1e-3) / 1e12
-    table = {f"{k[0]}:{k[1]}:n{k[2]}": round(v, 4) for k, v in sorted(per_step.items(), key=lambda t: -t[1])}
-    din = 2
-    kname, grid = kernel_identity(kind, mode, n, din, W)
+    table = {}
+    for k, v in sorted(per_step.items(), key=lambda t: -t[1]):
+        name = f"{k[0]}:{k[1]}:n{k[2]}:{k[4][0]}-{k[3]}x{k[4][2]}-{k[4][1]}"
+        table[name] = round(table.get(name, 0.0) + v, 4)
+    kname, grid, x6 = kernel_identity(kind, mode, n, din, W)
     traffic, tsrc = pmc_traffic(kname, grid)
-    return {"bound": "mfma", "achieved": round(achieved, 2), "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-            "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": traffic,
-            "traffic_unit": "bytes/launch (HBM: corrected FETCH_SIZE + WRITE_SIZE)", "traffic_source": tsrc,
-            "kernel": f"{kname} grid={grid} (n={n}, W={W}, {mode} jet {kind})", "avg_ms": round(ms, 4),
-            "algorithmic_gflop_per_launch": round(flops / 1e9, 3), "per_step_ms_by_launch": table}
+    out = {"bound": "mfma", "achieved": round(achieved, 2), "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+           "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": traffic,
+           "traffic_unit": "bytes/launch (HBM: corrected FETCH_SIZE + WRITE_SIZE)", "traffic_source": tsrc,
+           "kernel": f"{kname} grid={grid} (n={n}, {din}->{dout} {L}x{W}, {mode} jet {kind})", "avg_ms": round(ms, 4),
+           "algorithmic_gflop_per_launch": round(flops / 1e9, 3), "per_step_ms_by_launch": table}
+    if x6:
+        # the kernel runs split-bf16 products: 6 x v_mfma_f32_16x16x32_bf16 (16 cyc) per 16x16x32 fp32 MAC
+        # block = 85.3 fp32-equivalent MAC/clk/SIMD vs 32 for v_mfma_f32_16x16x4_f32 (MI355X_MICROARCH.md)
+        out["x6_ceiling"] = round(FP32_MFMA_PEAK_TFLOPS * (16 * 16 * 32 / 96.0) / 32.0, 1)
+        out["frac_of_x6_ceiling"] = round(achieved / out["x6_ceiling"], 4)
+    return out
 
 
 def kernel_identity(kind, mode, n, din, W):
@@ -165,8 +223,8 @@ def kernel_identity(kind, mode, n, din, W):
     x6 = nat.get_precision()[1 if kind == "bwd" else 0] == nat.PREC_BF16X6 and (kind == "fwd" or NT <= 8)
     if T > 0:
         nb = ((n + 15) // 16 + T - 1) // T
-        return f"insr::jet_{kind}_{'x6' if x6 else 'split'}<{NT}, {S}, {lap}, {T}>", nb * 64 * min(NT, 8)
-    return f"insr::jet_{kind}_wave<{NT}, {S}, {lap}>", ((n + 63) // 64) * 256
+        return f"insr::jet_{kind}_{'x6' if x6 else 'split'}<{NT}, {S}, {lap}, {T}>", nb * 64 * min(NT, 8), x6
+    return f"insr::jet_{kind}_wave<{NT}, {S}, {lap}>", ((n + 63) // 64) * 256, False
 
 
 def pmc_traffic(kname, grid):
@@ -184,31 +242,87 @@ def pmc_traffic(kname, grid):
     return e["fetch_bytes"] + e["write_bytes"], tab.get("_source")
 
 
-def cpu_baseline(seconds):
-    """The oracle (torch-CPU restatement of the reference graph) on this host's cores."""
+def cpu_baseline(config, seconds):
+    """The oracle (torch-CPU restatement of the reference graph) on this host's cores, over a
+    bounded sample of the same workload (same nets, same phases; elasticity3Dbunny on a
+    16384-point slice of its 262144-point batch: the per-point cost is size-independent)."""
     from oracle import siren_oracle as O
+    from pde.config import baseline_config
     # the box exports OMP_NUM_THREADS = its CPU share; affinity may list the whole host
     cores = min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "1024")))
     torch.set_num_threads(cores)
     torch.manual_seed(0)
-    vel, vel_prev, pres = O.OracleSiren(2, 2, 4, 128), O.OracleSiren(2, 2, 4, 128), O.OracleSiren(2, 1, 4, 128)
-    for p in vel_prev.parameters():
-        p.requires_grad_(False)
-    opts = [O.OracleAdam(list(vel.parameters()) + list(pres.parameters()), lr=1e-4) for _ in range(3)]
-    N, nb = 16384, 16384 // 100
+    wl = WORKLOADS[config]
+    cfg = baseline_config(config, sample_resolution=wl["res"])
+    L, W = cfg.num_hidden_layers, cfg.hidden_features
 
-    def X():
-        return (torch.rand(N, 2) * 2 - 1).requires_grad_(True)
+    def adam(nets):
+        return O.OracleAdam([p for n in nets for p in n.parameters() if p.requires_grad], lr=1e-4)
 
-    def B(side):
-        return O.sample_boundary2d_side(nb, side).requires_grad_(True)
+    if wl["pde"] == "fluid":
+        vel, vel_prev, pres = O.OracleSiren(2, 2, L, W), O.OracleSiren(2, 2, L, W), O.OracleSiren(2, 1, L, W)
+        for p in vel_prev.parameters():
+            p.requires_grad_(False)
+        opts = [adam([vel, pres]) for _ in range(3)]
+        N = cfg.sample_resolution ** 2
+        nb = N // 100
 
-    def one_step():
-        O.update_step([vel, pres], O.fluid_advect_loss(vel, vel_prev, X(), B("horizontal"), B("vertical"), 0.05),
-                      opts[0])
-        O.update_step([vel, pres], O.fluid_pressure_loss(vel, pres, X(), B("horizontal"), B("vertical")), opts[1])
-        O.update_step([vel, pres], O.fluid_projection_loss(vel, vel_prev, pres, X(), B("horizontal"),
-                                                           B("vertical")), opts[2])
+        def X():
+            return (torch.rand(N, 2) * 2 - 1).requires_grad_(True)
+
+        def B(side):
+            return O.sample_boundary2d_side(nb, side).requires_grad_(True)
+
+        def one_step():
+            O.update_step([vel, pres], O.fluid_advect_loss(vel, vel_prev, X(), B("horizontal"), B("vertical"),
+                                                           cfg.dt), opts[0])
+            O.update_step([vel, pres], O.fluid_pressure_loss(vel, pres, X(), B("horizontal"), B("vertical")),
+                          opts[1])
+            O.update_step([vel, pres], O.fluid_projection_loss(vel, vel_prev, pres, X(), B("horizontal"),
+                                                               B("vertical")), opts[2])
+        pts, what = 3 * N, f"3 phases x {N} pts"
+    elif wl["pde"] == "advection":
+        f, f_prev = O.OracleSiren(1, 1, L, W), O.OracleSiren(1, 1, L, W)
+        for p in f_prev.parameters():
+            p.requires_grad_(False)
+        opt = adam([f])
+        N = cfg.sample_resolution
+        half = cfg.length / 2
+
+        def one_step():
+            x = ((torch.rand(N, 1) * 2 - 1) * half).requires_grad_(True)
+            bc = O.sample_boundary1d(max(N // 100, 10)) * half
+            O.update_step([f], O.advect1d_loss(f, f_prev, x, bc, cfg.dt, cfg.vel), opt)
+        pts, what = N, f"1 phase x {N} pts"
+    else:
+        d = cfg.dim
+        f, fp, fpp = O.OracleSiren(d, d, L, W), O.OracleSiren(d, d, L, W), O.OracleSiren(d, d, L, W)
+        for n in (fp, fpp):
+            for p in n.parameters():
+                p.requires_grad_(False)
+        opt = adam([f])
+        vec = lambda *v: list(v[:d])  # noqa: E731
+        ecfg = dict(dt=cfg.dt, energy=list(cfg.energy), ratio_arap=cfg.ratio_arap, ratio_volume=cfg.ratio_volume,
+                    ratio_kinematics=cfg.ratio_kinematics, ratio_constraint=cfg.ratio_constraint,
+                    ratio_collide=cfg.ratio_collide, plane_height=cfg.plane_height,
+                    external_force=vec(cfg.external_force_x, cfg.external_force_y, cfg.external_force_z),
+                    constraint_offset_right=vec(cfg.constraint_right_offset_x, cfg.constraint_right_offset_y,
+                                                cfg.constraint_right_offset_z),
+                    circle_center=vec(cfg.collide_circle_x, cfg.collide_circle_y, cfg.collide_circle_z),
+                    circle_radius=cfg.collide_circle_radius, external_force_timesteps=cfg.external_force_timesteps)
+        full = interior_points(cfg, wl)
+        N = full if full <= 32768 else 16384
+        R = cfg.sample_resolution
+
+        def one_step():
+            parts = []
+            for sp in cfg.sample_pattern:
+                parts.append(torch.rand(R ** d, d) * 2 - 1 if sp == "random" else O.sample_uniform(R, d))
+            x = torch.cat(parts)[:N].clone().requires_grad_(True)
+            fixed = [torch.cat([torch.full((R, 1), s), torch.rand(R, d - 1) * 2 - 1], 1) for s in (-1.0, 1.0)]
+            O.update_step([f], O.elasticity_loss(f, fp, fpp, x, fixed[0], fixed[1], ecfg), opt)
+        pts = N
+        what = f"1 phase x {N} pts" + (f" (slice of the {full}-point batch)" if N < full else "")
 
     one_step()  # warm-up
     t0 = time.perf_counter()
@@ -219,18 +333,18 @@ def cpu_baseline(seconds):
     for _ in range(reps):
         one_step()
     dt = (time.perf_counter() - t0) / reps
-    return {"value": round(3 * N / dt, 1), "unit": "collocation-points/s", "cores": cores, "kind": "port",
-            "sample": f"oracle/siren_oracle.py fluid2Dtlgn: {reps} timed timestep-iterations (3 phases x 16384 pts, "
-                      f"torch CPU autograd + Adam), {torch.get_num_threads()} threads, {dt * 1e3:.1f} ms/iter"}
+    return {"value": round(pts / dt, 1), "unit": "collocation-points/s", "cores": cores, "kind": "port",
+            "sample": f"oracle/siren_oracle.py {config}: {reps} timed iterations ({what}, torch CPU autograd + "
+                      f"Adam), {torch.get_num_threads()} threads, {dt * 1e3:.1f} ms/iter"}
 
 
 def main():
     args = parse()
     world, rank, local = setup_dist(args)
     log(f"world={world} rank={rank}")
-    model, cfg = build_model(args, world)
-    n_local = model._n_interior()
-    loops = phase_loops(model)
+    model, cfg, wl, n_local = build_model(args, world, rank)
+    nph = len(wl["phases"])
+    loops = phase_loops(model, wl)
     log(f"model built, {n_local} points per rank per phase")
     for i in range(args.warmup):  # iteration 0 eager, iteration 1 captured (warm-up)
         run_steps(loops, i, 1)
@@ -247,7 +361,9 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t)
     log(f"timed {args.steps} steps: {elapsed * 1e3:.2f} ms")
-    total_points = n_local * world * 3 * args.steps
+    # points all ranks processed: strong = the global batch, weak = world x the per-rank batch
+    n_all = interior_points(cfg, wl) if args.scaling == "strong" else n_local * world
+    total_points = n_all * nph * args.steps
     value = total_points / elapsed
     result = {
         "metric": "collocation-points/sec/timestep (incl. ∇/Δ residual + Adam) at 1/2/4/8 GPUs",
@@ -255,18 +371,17 @@ def main():
         "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
         "scaling": args.scaling, "vs_baseline": None, "dtype": "fp32", "data": "synthetic (uniform-random "
         "collocation points, seeded SIREN init; no dataset exists for this path)",
-        "config": {"workload": "fluid2Dtlgn", "model": "SIREN 4x128 velocity(2->2) + pressure(2->1)",
-                   "points_per_phase_iter": n_local * world, "phases": 3, "global_batch": n_local * world,
+        "config": {"workload": args.config, "model": wl["model"],
+                   "points_per_phase_iter": n_all, "phases": nph, "global_batch": n_all,
                    "seq_len": None, "parallelism": f"dp{world}", "graph": not args.no_graph},
     }
     if not args.no_roofline:  # every rank runs the eager steps (they contain the all-reduce)
-        P_pres = 2 * 128 + 4 * 128 * 128 + 128 * 1  # d_in W + L W^2 + W d_out
-        roof = roofline(model, loops, n_local, P_pres)
+        roof = roofline(loops, n_local)
         if rank == 0:
             result["roofline"] = roof
         log("roofline done")
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+        result["cpu_baseline"] = cpu_baseline(args.config, args.cpu_seconds)
         log("cpu baseline done")
         result["speedup_vs_cpu_baseline"] = round(value / result["cpu_baseline"]["value"], 1)
     if rank == 0:

@@ -51,8 +51,9 @@ TIMING = {"on": False, "events": []}
 
 
 class _timed:
-    def __init__(self, kind, mode, n, W):
-        self.key = (kind, MODE_NAMES[mode], n, W)
+    def __init__(self, kind, mode, n, W, shape=None):
+        # (kind, mode, points, width, (d_in, d_out, hidden layers))
+        self.key = (kind, MODE_NAMES[mode], n, W, shape)
 
     def __enter__(self):
         if TIMING["on"]:
@@ -85,7 +86,7 @@ class _SirenJet(torch.autograd.Function):
         if save:
             nbytes = lib.insr_jet_act_bytes(n, din, L, W, mode)
             act = torch.empty(max(nbytes // 4, 1), device=dev, dtype=torch.float32)
-        with _timed("fwd", mode, n, W):
+        with _timed("fwd", mode, n, W, (din, dout, L)):
             rc = lib.insr_siren_jet_fwd(nat.ptr(x2), n, din, dout, L, W, mode, nat.ptr(flat), nat.ptr(y),
                                         nat.ptr(dy), nat.ptr(lap), nat.ptr(act), nat.stream_of(dev))
         nat.check(rc, "insr_siren_jet_fwd")
@@ -121,11 +122,11 @@ class _SirenJet(torch.autograd.Function):
         c = lambda t: None if t is None else (t if t.is_contiguous() else t.contiguous())  # noqa: E731
         gy, gdy, glap = c(gy), c(gdy), c(glap)
         st = nat.stream_of(x2.device)
-        with _timed("bwd", mode, n, W):
+        with _timed("bwd", mode, n, W, (din, dout, L)):
             rc = lib.insr_siren_jet_bwd(nat.ptr(x2), n, din, dout, L, W, mode, nat.ptr(mlp.flat_params()),
                                         nat.ptr(act), nat.ptr(gy), nat.ptr(gdy), nat.ptr(glap), nat.ptr(part), st)
         nat.check(rc, "insr_siren_jet_bwd")
-        with _timed("reduce", mode, n, W):
+        with _timed("reduce", mode, n, W, (din, dout, L)):
             rc = lib.insr_reduce_partials(nat.ptr(part), lib.insr_jet_partial_blocks(n, din, W, mode), gflat.numel(),
                                           nat.ptr(gflat), accumulate, st)
         nat.check(rc, "insr_reduce_partials")

@@ -90,8 +90,11 @@ class ElasticityModel(BaseModel):
         return self._dp_shard(torch.cat(left, 0)), self._dp_shard(torch.cat(right, 0))
 
     def _dp_shard(self, x):
+        """Rank r keeps rows [r n / world, (r + 1) n / world) of the global draw (strong
+        scaling).  cfg.insr_dp_weak: every rank keeps its whole draw (weak scaling; ranks
+        seed their device RNG differently, so the draws are independent)."""
         world = self._dp_world()
-        if world == 1:
+        if world == 1 or getattr(self.cfg, "insr_dp_weak", False):
             return x
         r = torch.distributed.get_rank()
         n = x.shape[0]
