@@ -182,8 +182,9 @@ def roofline(loops, n_local):
         agg.setdefault(key, []).append(e0.elapsed_time(e1))
     _jet.TIMING["events"].clear()
     per_step = {k: sum(v) / reps for k, v in agg.items()}
-    # dominant kernel = the longest launch over the interior batch (boundary bands are ~1% of points)
-    dom = max((k for k in per_step if k[2] == n_local and k[0] != "reduce"), key=lambda k: sum(agg[k]) / len(agg[k]))
+    # dominant kernel = the longest launch over the interior batch (boundary bands are ~1% of points;
+    # a merged launch carries the interior plus its boundary / fixed points: n >= n_local)
+    dom = max((k for k in per_step if k[2] >= n_local and k[0] != "reduce"), key=lambda k: sum(agg[k]) / len(agg[k]))
     kind, mode, n, W, (din, dout, L) = dom
     ms = sum(agg[dom]) / len(agg[dom])
     # algorithmic flops per launch: 2P per point per stream per GEMM pass

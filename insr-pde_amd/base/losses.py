@@ -12,6 +12,8 @@ They close the PDE residuals of the model phases (fluid/model.py:96-101,121-125,
 reference spells as 3-5 aten launches forward and as many backward.  Gradients flow
 to every input that requires them.  GPU only (the product path has no CPU fallback).
 """
+import ctypes
+
 import torch
 
 from . import _native as nat
@@ -39,56 +41,90 @@ def _prep(t):
     return t if t.is_contiguous() else t.contiguous()
 
 
+def _at(t, off):
+    """Device pointer to element `off` of t (None stays None)."""
+    if t is None:
+        return None
+    return ctypes.c_void_p(t.data_ptr() + 4 * int(off))
+
+
+def _grad_like(t, n_used):
+    """Gradient buffer of an input of which the loss reads n_used elements: elements the
+    loss does not read (the other rows of a merged jet launch) get zero gradient."""
+    return torch.empty_like(t) if t.numel() == n_used else torch.zeros_like(t)
+
+
 class _SqLoss(torch.autograd.Function):
+    # offs: element offset of the loss range in each of a, b, c, d (n terms for COMBO,
+    # the 2n x m band rows for BANDS)
     @staticmethod
-    def forward(ctx, kind, n, m, coef, scale, a, b, c, d):
+    def forward(ctx, kind, n, m, coef, scale, offs, a, b, c, d):
         lib = nat.lib()
         dev = a.device
         work = _workspace(dev)
         out = torch.empty((), device=dev, dtype=torch.float32)
-        rc = lib.insr_sq_loss_fwd(kind, nat.ptr(a), nat.ptr(b), nat.ptr(c), nat.ptr(d), n, m, *coef, scale,
-                                  nat.ptr(out), nat.ptr(work), nat.stream_of(dev))
+        rc = lib.insr_sq_loss_fwd(kind, _at(a, offs[0]), _at(b, offs[1]), _at(c, offs[2]), _at(d, offs[3]), n, m,
+                                  *coef, scale, nat.ptr(out), nat.ptr(work), nat.stream_of(dev))
         nat.check(rc, "insr_sq_loss_fwd")
         ctx.save_for_backward(a, b, c, d)
-        ctx.args = (kind, n, m, coef, scale)
+        ctx.args = (kind, n, m, coef, scale, offs)
         return out
 
     @staticmethod
     def backward(ctx, gout):
         a, b, c, d = ctx.saved_tensors
-        kind, n, m, coef, scale = ctx.args
-        need = ctx.needs_input_grad[5:9]
+        kind, n, m, coef, scale, offs = ctx.args
+        need = ctx.needs_input_grad[6:10]
         if not any(need):
-            return (None,) * 9
-        grads = [torch.empty_like(t) if (t is not None and nd) else None for t, nd in zip((a, b, c, d), need)]
+            return (None,) * 10
+        used = n if kind == nat.LOSS_COMBO else 2 * n * m
+        grads = [_grad_like(t, used) if (t is not None and nd) else None for t, nd in zip((a, b, c, d), need)]
         g = gout.reshape(1) if gout.is_contiguous() else gout.contiguous().reshape(1)
-        rc = nat.lib().insr_sq_loss_bwd(kind, nat.ptr(a), nat.ptr(b), nat.ptr(c), nat.ptr(d), n, m, *coef, scale,
-                                        nat.ptr(g), *[nat.ptr(t) for t in grads], nat.stream_of(a.device))
+        rc = nat.lib().insr_sq_loss_bwd(kind, _at(a, offs[0]), _at(b, offs[1]), _at(c, offs[2]), _at(d, offs[3]),
+                                        n, m, *coef, scale, nat.ptr(g),
+                                        *[_at(t, o) for t, o in zip(grads, offs)], nat.stream_of(a.device))
         nat.check(rc, "insr_sq_loss_bwd")
-        return (None, None, None, None, None, *grads)
+        return (None, None, None, None, None, None, *grads)
 
 
-def fused_mse(a, b=None, c=None, d=None, alpha=1.0, beta=-1.0, gamma=1.0, delta=1.0):
+def fused_mse(a, b=None, c=None, d=None, alpha=1.0, beta=-1.0, gamma=1.0, delta=1.0, count=None, a_row0=0,
+              reduction="mean"):
     """mean((alpha*(a + beta*b) + gamma*(c + delta*d))**2) over all elements; b, c, d are
-    None or the shape of a (d needs c).  fused_mse(u, target) == F.mse_loss(u, target)."""
-    for t in (b, c, d):
-        if t is not None and t.shape != a.shape:
-            raise ValueError(f"fused_mse: shape mismatch {tuple(t.shape)} vs {tuple(a.shape)}")
+    None or the shape of a (d needs c).  fused_mse(u, target) == F.mse_loss(u, target).
+
+    Merged jet launches (interior + boundary points of one network in one launch):
+    count = number of terms; every tensor is read from its first element except `a`,
+    which starts at row a_row0; elements outside the range get zero gradient.
+    reduction="sum" returns the sum instead of the mean."""
+    if count is None:
+        for t in (b, c, d):
+            if t is not None and t.shape != a.shape:
+                raise ValueError(f"fused_mse: shape mismatch {tuple(t.shape)} vs {tuple(a.shape)}")
+        count, a_off = a.numel(), 0
+    else:
+        row = a.numel() // max(a.shape[0], 1) if a.dim() > 0 else 1
+        a_off = int(a_row0) * row
+        if a_off + count > a.numel() or any(t is not None and t.numel() < count for t in (b, c, d)):
+            raise ValueError(f"fused_mse: count {count} (a from element {a_off}) exceeds an input")
     if d is not None and c is None:
         raise ValueError("fused_mse: d needs c")
+    if reduction not in ("mean", "sum"):
+        raise ValueError(reduction)
     a, b, c, d = _prep(a), _prep(b), _prep(c), _prep(d)
-    n = a.numel()
     coef = (float(alpha), float(beta), float(gamma), float(delta))
-    return _SqLoss.apply(nat.LOSS_COMBO, n, 1, coef, 1.0 / max(n, 1), a, b, c, d)
+    scale = 1.0 / max(count, 1) if reduction == "mean" else 1.0
+    return _SqLoss.apply(nat.LOSS_COMBO, int(count), 1, coef, scale, (a_off, 0, 0, 0), a, b, c, d)
 
 
-def wall_mse(y, n):
-    """mean(y[:n, 0]**2) + mean(y[n:2n, 1]**2) for y of shape (2n, m), m >= 2 (the
-    normal-component wall terms of both boundary bands in one launch)."""
-    if y.dim() != 2 or y.shape[0] != 2 * n or y.shape[1] < 2:
-        raise ValueError(f"wall_mse: expected (2*{n}, m>=2), got {tuple(y.shape)}")
+def wall_mse(y, n, row0=0):
+    """mean(y[r:r+n, 0]**2) + mean(y[r+n:r+2n, 1]**2), r = row0, for y of shape (R, m),
+    m >= 2, R >= r + 2n (the normal-component wall terms of both boundary bands in one
+    launch; the other rows -- a merged launch's interior points -- get zero gradient)."""
+    if y.dim() != 2 or y.shape[0] < row0 + 2 * n or y.shape[1] < 2 or (row0 == 0 and y.shape[0] != 2 * n):
+        raise ValueError(f"wall_mse: expected ({row0} + 2*{n} rows, m>=2), got {tuple(y.shape)}")
     y = _prep(y)
-    return _SqLoss.apply(nat.LOSS_BANDS, n, y.shape[1], (0.0, 0.0, 0.0, 0.0), 1.0 / max(n, 1), y, None, None, None)
+    return _SqLoss.apply(nat.LOSS_BANDS, n, y.shape[1], (0.0, 0.0, 0.0, 0.0), 1.0 / max(n, 1),
+                         (int(row0) * y.shape[1], 0, 0, 0), y, None, None, None)
 
 
 _SVD_WORK = {}  # device index -> partials buffer of the SVD-energy reduction
@@ -96,7 +132,7 @@ _SVD_WORK = {}  # device index -> partials buffer of the SVD-energy reduction
 
 class _SvdEnergy(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, J, ratio_arap, ratio_volume):
+    def forward(ctx, J, ratio_arap, ratio_volume, n):
         lib = nat.lib()
         dev = J.device
         if dev.index not in _SVD_WORK:
@@ -104,32 +140,37 @@ class _SvdEnergy(torch.autograd.Function):
                 raise RuntimeError("SVD-energy workspace must be created before graph capture (run one eager call)")
             _SVD_WORK[dev.index] = torch.empty(lib.insr_svd_energy_work_floats(), device=dev, dtype=torch.float32)
         out = torch.empty((), device=dev, dtype=torch.float32)
-        n, d = J.shape[0], J.shape[-1]
+        d = J.shape[-1]
         rc = lib.insr_svd_energy_fwd(nat.ptr(J), n, d, float(ratio_arap), float(ratio_volume), nat.ptr(out),
                                      nat.ptr(_SVD_WORK[dev.index]), nat.stream_of(dev))
         nat.check(rc, "insr_svd_energy_fwd")
         ctx.save_for_backward(J)
-        ctx.ratios = (float(ratio_arap), float(ratio_volume))
+        ctx.args = (float(ratio_arap), float(ratio_volume), n)
         return out
 
     @staticmethod
     def backward(ctx, gout):
         (J,) = ctx.saved_tensors
         if not ctx.needs_input_grad[0]:
-            return None, None, None
-        gJ = torch.empty_like(J)
+            return None, None, None, None
+        ra, rv, n = ctx.args
+        gJ = torch.empty_like(J) if n == J.shape[0] else torch.zeros_like(J)
         g = gout.reshape(1) if gout.is_contiguous() else gout.contiguous().reshape(1)
-        rc = nat.lib().insr_svd_energy_bwd(nat.ptr(J), J.shape[0], J.shape[-1], *ctx.ratios, nat.ptr(g), nat.ptr(gJ),
+        rc = nat.lib().insr_svd_energy_bwd(nat.ptr(J), n, J.shape[-1], ra, rv, nat.ptr(g), nat.ptr(gJ),
                                            nat.stream_of(J.device))
         nat.check(rc, "insr_svd_energy_bwd")
-        return gJ, None, None
+        return gJ, None, None, None
 
 
-def svd_energy(J, ratio_arap=1.0, ratio_volume=0.0):
+def svd_energy(J, ratio_arap=1.0, ratio_volume=0.0, count=None):
     """sum over points of ratio_arap * sum_i (s_i - 1)^2 + ratio_volume * (prod_i s_i - 1)^2,
     s = singular values of each J[n] (d x d, d = 2 or 3) -- the ARAP and volume terms of
     elasticity/model.py:143-163 in one launch (torch.svd's gradient U diag(dE/ds) V^T in
-    one backward launch)."""
+    one backward launch).  count: only the first `count` blocks (the interior rows of a
+    merged jet launch; the other blocks get zero gradient)."""
     if J.dim() != 3 or J.shape[-1] != J.shape[-2] or J.shape[-1] not in (2, 3):
         raise ValueError(f"svd_energy: expected (N, d, d) with d in (2, 3), got {tuple(J.shape)}")
-    return _SvdEnergy.apply(_prep(J), ratio_arap, ratio_volume)
+    n = J.shape[0] if count is None else int(count)
+    if n > J.shape[0] or n < 0:
+        raise ValueError(f"svd_energy: count {n} > {J.shape[0]} blocks")
+    return _SvdEnergy.apply(_prep(J), ratio_arap, ratio_volume, n)

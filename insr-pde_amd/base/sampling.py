@@ -12,7 +12,7 @@ import torch
 _AFFINE = {}  # (N, side-key, epsilon, device) -> (scale, shift) constant tensors
 
 __all__ = ["sample_uniform", "sample_random", "sample_boundary", "sample_boundary2D_separate",
-           "sample_boundary2D_pair"]
+           "sample_boundary2D_pair", "merge_samples"]
 
 
 def sample_uniform(resolution, sdim=1, device="cpu", flatten=True):
@@ -89,3 +89,11 @@ def sample_boundary2D_pair(N, epsilon=1e-4, device='cpu'):
     if torch.device(device).type == "cuda":
         return _fused_bands(N // 2, faces, ("pair", epsilon), device)
     return torch.cat([_band(N // 2, f, device) for f in faces], dim=0)
+
+
+def merge_samples(*parts):
+    """One leaf sample tensor holding several point sets of ONE network (interior points,
+    boundary bands, fixed points): the model evaluates the network once, so the HIP path
+    runs one jet launch each way instead of one per set -- a band of a few hundred points
+    would otherwise be a latency-bound launch of its own.  Row order = argument order."""
+    return torch.cat([p.detach() for p in parts]).requires_grad_(True)

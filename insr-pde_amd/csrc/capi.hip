@@ -98,9 +98,10 @@ int split_tiles(int bwd, int NT, int S, long n) {
   const size_t plane = x6 && !bwd ? (size_t)S * 3 * 16 * (16 * NT + 8) * 2
                        : x6       ? (size_t)(3 * 16 * (16 * NT + 8) + 32 + 3 * 16 * 16 * NT) * 2
                                   : (size_t)S * 16 * ((16 * NT + 8) + (bwd ? 16 * NT : 0)) * sizeof(float);
-  // width 256: one tile (register budget of 8 waves x 2 row tiles); backward T = 4 only
-  // for value jets (register budget of the derivative streams)
-  int T = NT > 8 ? 1 : ((bwd && S > 1) ? 2 : 4);
+  // width 256: fp32 kernels one tile (register budget of 8 waves x 2 row tiles); the x6
+  // forward T x S <= 4 (its a[T][2][S] accumulators next to the 8 split W fragments);
+  // backward T = 4 only for value jets (register budget of the derivative streams)
+  int T = NT > 8 ? ((x6 && !bwd) ? (S == 1 ? 4 : (S == 2 ? 2 : 1)) : 1) : ((bwd && S > 1) ? 2 : 4);
   while (T > 1 && (size_t)T * plane > 163840) T >>= 1;
   const int forced = g_tiles[bwd ? 1 : 0];
   if (forced > 0) {

@@ -5,7 +5,7 @@ import os
 import numpy as np
 import torch
 
-from base import BaseModel, fused_mse, gradient, sample_boundary, sample_random, sample_uniform
+from base import BaseModel, fused_mse, gradient, merge_samples, sample_boundary, sample_random, sample_uniform
 
 from .examples import get_examples
 
@@ -56,18 +56,21 @@ class Advection1DModel(BaseModel):
 
     @BaseModel._training_loop
     def _advect(self):
+        """advection/model.py:68-91 (midpoint rule + Dirichlet band term)."""
         x = self._sample_in_training()
+        n = x.shape[0]
         u0 = self.field_prev(x)
-        u = self.field(x)
-        # midpoint rule: (u - u0)/dt + v (u_x + u0_x)/2 = 0
-        ux = gradient(u, x)
         with torch.no_grad():
             u0x = gradient(u0, x)
-        # mean(((u - u0)/dt + vel (ux + u0x)/2)^2) as one fused launch (each way)
+        # interior points and the boundary band through ONE jet launch of the field
         n_bc = max(self._n_interior() // 100, 10)
         xb = sample_boundary(n_bc, 1, device=self.device) * self.length / 2
-        main = fused_mse(u, u0, ux, u0x, alpha=1.0 / self.dt, beta=-1.0, gamma=self.vel / 2., delta=1.0)
-        return {'main': main, 'bc': fused_mse(self.field(xb))}
+        xa = merge_samples(x, xb)
+        ua = self.field(xa)
+        uxa = gradient(ua, xa)
+        # mean(((u - u0)/dt + vel (ux + u0x)/2)^2) over the interior rows, one fused launch each way
+        main = fused_mse(ua, u0, uxa, u0x, alpha=1.0 / self.dt, beta=-1.0, gamma=self.vel / 2., delta=1.0, count=n)
+        return {'main': main, 'bc': fused_mse(ua, count=xb.shape[0], a_row0=n)}
 
     def write_output(self, output_folder):
         u, grid = self.sample_field(self.vis_resolution, return_samples=True)

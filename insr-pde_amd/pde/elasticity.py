@@ -15,7 +15,7 @@ sampler is SURVEY.md §8(f) row 3 (next).
 """
 import torch
 
-from base import BaseModel, sample_random, sample_uniform, svd_energy
+from base import BaseModel, fused_mse, merge_samples, sample_random, sample_uniform, svd_energy
 from base.diff_ops import jacobian_nosync
 
 
@@ -125,18 +125,29 @@ class ElasticityModel(BaseModel):
         return {'main': self.energy_of(x, fixed_l, fixed_r)}
 
     def energy_of(self, x, fixed_l, fixed_r):
-        dt = self.dt
+        """elasticity/model.py:131-189.  The interior points and the fixed points the
+        constraint terms need go through ONE jet launch of the deformation field
+        (base.merge_samples); every term reads its rows of it."""
+        dt, n = self.dt, x.shape[0]
+        use_l = 'constraint' in self.energy
+        use_r = any(t in self.energy for t in ('constraint_right', 'constraint_right_compress'))
+        parts = [x] + ([fixed_l] if use_l else []) + ([fixed_r] if use_r else [])
+        xa = merge_samples(*parts) if len(parts) > 1 else x
+        row_l = n
+        row_r = n + (fixed_l.shape[0] if use_l else 0)
         with torch.no_grad():
             q_prev = self.deformation_field_prev(x) + x
             q_pp = self.deformation_field_prev_prev(x) + x
-        q = self.deformation_field(x) + x
+        fa = self.deformation_field(xa)
+        qa = fa + xa
+        q = qa if xa is x else qa[:n]
         qdot = (q - q_prev) / dt
         total = 0
         if 'arap' in self.energy or 'volume' in self.energy:
             # both singular-value terms in one fused HIP launch each way (torch.svd + ~12 ops in the reference)
-            J, _ = jacobian_nosync(q, x)  # status unused (as in the reference): no host sync
+            J, _ = jacobian_nosync(qa, xa)  # status unused (as in the reference): no host sync
             total = svd_energy(J, self.ratio_arap if 'arap' in self.energy else 0.0,
-                               self.ratio_volume if 'volume' in self.energy else 0.0)
+                               self.ratio_volume if 'volume' in self.energy else 0.0, count=n)
         for term in self.energy:
             if term in ('arap', 'volume'):
                 continue
@@ -146,12 +157,14 @@ class ElasticityModel(BaseModel):
             elif term == 'external':
                 if self.timestep <= self.external_force_timesteps:
                     total = total - dt * torch.sum(qdot * self.external_force)
-            elif term == 'constraint':
-                total = total + self.ratio_constraint * torch.sum(self.deformation_field(fixed_l) ** 2)
-            elif term in ('constraint_right', 'constraint_right_compress'):
+            elif term == 'constraint':  # r_c sum |f(x_fixed)|^2
+                total = total + self.ratio_constraint * fused_mse(fa, count=fixed_l.numel(), a_row0=row_l,
+                                                                  reduction="sum")
+            elif term in ('constraint_right', 'constraint_right_compress'):  # r_c sum |f(x_r) -/+ offset|^2
                 sign = 1.0 if term == 'constraint_right' else -1.0
-                tgt = sign * self.constraint_offset_right
-                total = total + self.ratio_constraint * torch.sum((self.deformation_field(fixed_r) - tgt) ** 2)
+                tgt = self._target_rows(sign, fixed_r.shape[0])
+                total = total + self.ratio_constraint * fused_mse(fa, tgt, count=fixed_r.numel(), a_row0=row_r,
+                                                                  reduction="sum")
             elif term == 'collision':
                 total = total + self._plane_penalty(q, qdot)
             elif term == 'collision_sphere':
@@ -159,6 +172,14 @@ class ElasticityModel(BaseModel):
             else:
                 raise NotImplementedError(term)
         return total
+
+    def _target_rows(self, sign, rows):
+        """sign * constraint_offset_right repeated over the fixed points (cached constant)."""
+        cache = self.__dict__.setdefault("_insr_targets", {})
+        key = (sign, rows)
+        if key not in cache:
+            cache[key] = (sign * self.constraint_offset_right).expand(rows, self.dim).contiguous()
+        return cache[key]
 
     def _plane_penalty(self, q, qdot):
         """elasticity/losses.py:10-20, written mask-free (no host sync): force only

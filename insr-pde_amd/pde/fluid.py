@@ -87,6 +87,11 @@ class Fluid2DModel(BaseModel):
         self.velocity_field_prev.load_state_dict(self.velocity_field.state_dict())
         self._projection()
 
+    # The wall terms evaluate the network on the boundary bands in their own jet launch.
+    # (Merging them into the interior launch -- base.merge_samples, as the advection and
+    # elasticity models do -- was measured neutral on the jets at 128^2 points: the 2%
+    # extra points push the 1024-tile interior launches into one more block round on 256
+    # CUs, and the merged losses add glue launches: 1.09 vs 1.01 ms per step.)
     def _wall_loss(self, n_interior):
         """u_x = 0 on the x-faces, u_y = 0 on the y-faces: mean(u_x^2) + mean(u_y^2)
         (fluid/model.py:90-94) as one jet launch and one fused loss launch."""

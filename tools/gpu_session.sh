@@ -17,7 +17,7 @@ step() {  # name timeout cmd...
 }
 for s in ${STEPS:-tests bench prof}; do
   case $s in
-    tests) step tests ${TTO:-500} python -m pytest tests -q -m gpu -x ${TESTSEL:-} ;;
+    tests) step tests ${TTO:-500} python -m pytest tests -q -m gpu -x ${TESTSEL:+-k "$TESTSEL"} ;;
     smoke) step smoke 200 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 400 python bench.py --steps ${BSTEPS:-20} --warmup 3 ;;
     configs) for c in ${CONFIGS:-advect1D elasticity2Dstretch elasticity3Dbunny fluid2DtlgnM}; do
