@@ -10,8 +10,9 @@ Energy terms (all SUMS over collocation points, as in the reference):
   constraint(_right[_compress]) r_c sum |f(x_fixed) - target|^2
   collision(_sphere)  -dt sum qdot . penalty force on penetrating points
 
-Only the synthetic box geometry (use_mesh=False) is supported; the tet-mesh
-sampler is SURVEY.md §8(f) row 3 (next).
+Geometry: the synthetic box [-1, 1]^d (use_mesh=False), or a tet / triangle mesh
+(use_mesh=True, cfg.mesh_path: MEDIT .mesh or .obj; pde/mesh.py): volume-weighted
+random points ('random') and the mesh vertices ('uniform'), as elasticity/model.py:198-207.
 """
 import torch
 
@@ -41,7 +42,7 @@ class ElasticityModel(BaseModel):
         self.energy = list(cfg.energy)
         self.use_mesh = bool(getattr(cfg, "use_mesh", False))
         if self.use_mesh:
-            raise NotImplementedError("mesh-based sampling (bunny/spot scripts) is not built yet")
+            self._init_mesh(cfg.mesh_path)
         self.sample_pattern = list(cfg.sample_pattern)
         self.ratio_arap, self.ratio_volume = cfg.ratio_arap, cfg.ratio_volume
         self.ratio_kinematics, self.ratio_constraint = cfg.ratio_kinematics, cfg.ratio_constraint
@@ -54,7 +55,16 @@ class ElasticityModel(BaseModel):
         self.constraint_offset_right = vec(cfg.constraint_right_offset_x, cfg.constraint_right_offset_y,
                                            cfg.constraint_right_offset_z)
         self.circle_center = vec(cfg.collide_circle_x, cfg.collide_circle_y, cfg.collide_circle_z)
-        self.sample_resolution_init = {2: 500, 3: 100}[d]
+        self.sample_resolution_init = self.sample_resolution if self.use_mesh else {2: 500, 3: 100}[d]
+
+    def _init_mesh(self, path):
+        """elasticity/model.py:75-93 (meshio + torchgp restated in pde/mesh.py)."""
+        from .mesh import MeshSampler, load_mesh
+        V, E, SF = load_mesh(path, self.dim, device=self.device)
+        self.mesh_V, self.mesh_F, self.mesh_SF = V, E, SF
+        self.mesh_sampler = MeshSampler(V.double().cpu(), E, device=self.device)
+        self.surface_sampler = MeshSampler(V.double().cpu(), SF, device=self.device) if self.dim == 3 else \
+            self.mesh_sampler
 
     @property
     def _trainable_networks(self):
@@ -63,6 +73,15 @@ class ElasticityModel(BaseModel):
     # ---- sampling ------------------------------------------------------------
     def _sample_in_training(self, resolution):
         d, parts = self.dim, []
+        if self.use_mesh:  # elasticity/model.py:200-207
+            for s in self.sample_pattern:
+                if s == 'random':
+                    parts.append(self.mesh_sampler.sample(resolution ** d)[:, :d])
+                elif s == 'uniform':
+                    parts.append(self.mesh_V[:, :d])
+                else:
+                    raise NotImplementedError(s)
+            return self._dp_shard(torch.cat(parts, dim=0).requires_grad_(True))
         for s in self.sample_pattern:
             if s == 'random':
                 parts.append(sample_random(resolution ** d, d, device=self.device).requires_grad_(True))
@@ -74,8 +93,12 @@ class ElasticityModel(BaseModel):
         return self._dp_shard(x)
 
     def _sample_fixed_in_training(self, resolution):
-        """Points on the x = -1 face (left) and x = +1 face (right)."""
+        """Points on the x = -1 face (left) and x = +1 face (right); none on a mesh (the
+        reference's mesh scenes use no positional constraint, elasticity/model.py:228)."""
         d, left, right = self.dim, [], []
+        if self.use_mesh:
+            empty = torch.zeros(0, d, device=self.device).requires_grad_(True)
+            return empty, empty
         for s in self.sample_pattern:
             if s == 'random':
                 faces = [sample_random(resolution, d - 1, device=self.device) for _ in range(2)]
