@@ -14,6 +14,9 @@ Geometry: the synthetic box [-1, 1]^d (use_mesh=False), or a tet / triangle mesh
 (use_mesh=True, cfg.mesh_path: MEDIT .mesh or .obj; pde/mesh.py): volume-weighted
 random points ('random') and the mesh vertices ('uniform'), as elasticity/model.py:198-207.
 """
+import os
+
+import numpy as np
 import torch
 
 from base import BaseModel, fused_mse, merge_samples, sample_random, sample_uniform, svd_energy
@@ -222,3 +225,41 @@ class ElasticityModel(BaseModel):
         if q.shape[1] == 2:
             return -self.dt * torch.sum(qdot * (self.ratio_collide * dist[:, None] * direc) * hit[:, None])
         return -self.dt * self.ratio_collide * torch.sum(dist * hit) * torch.sum(qdot * direc * hit[:, None])
+
+    # ---- output (host side; PNG figures are out of scope) ---------------------------
+    def sample_visualization(self, resolution):
+        """elasticity/model.py:255-270: the box grid + both fixed faces, or on a mesh the
+        surface samples + the mesh vertices."""
+        d, dev = self.dim, self.device
+        if self.use_mesh:
+            return torch.cat([self.surface_sampler.sample(resolution)[:, :d], self.mesh_V[:, :d]], dim=0)
+        pts = sample_uniform(resolution, d, device=dev)
+        face = sample_uniform(resolution, d - 1, device=dev)
+        one = torch.ones(face.shape[0], 1, device=dev)
+        return torch.cat([pts, torch.cat([-one, face], 1), torch.cat([one, face], 1)], dim=0)
+
+    def deformed_points(self, resolution=None):
+        """q = x + f(x) at the visualisation samples (elasticity/model.py:277-288)."""
+        if getattr(self, "_vis_samples", None) is None:
+            self._vis_samples = self.sample_visualization(resolution or self.vis_resolution)
+        x = self._vis_samples
+        with torch.no_grad():
+            return (self.deformation_field(x) + x).detach()
+
+    def write_output(self, output_folder):
+        """elasticity/model.py:311-317: t###_deformation.ply (ASCII point cloud, 2-D lifted to
+        z = 0, as write_pointcloud_to_file) and t###_deformation.npy."""
+        q = self.deformed_points().cpu().numpy().astype(np.float64)
+        os.makedirs(output_folder, exist_ok=True)
+        np.save(os.path.join(output_folder, f"t{self.timestep:03d}_deformation.npy"), q)
+        write_ply(os.path.join(output_folder, f"t{self.timestep:03d}_deformation.ply"), q)
+
+
+def write_ply(path, points):
+    """ASCII PLY point cloud (x y z per vertex; 2-D points get z = 0)."""
+    if points.shape[1] == 2:
+        points = np.hstack([points, np.zeros((points.shape[0], 1))])
+    with open(path, "w") as f:
+        f.write("ply\nformat ascii 1.0\nelement vertex %d\nproperty double x\nproperty double y\n"
+                "property double z\nend_header\n" % points.shape[0])
+        np.savetxt(f, points, fmt="%.9g")

@@ -15,7 +15,7 @@ import os
 import numpy as np
 import torch
 
-from base import (BaseModel, divergence, fused_mse, gradient, laplace, sample_boundary2D_pair,
+from base import (BaseModel, divergence, fused_mse, gradient, jacobian, laplace, sample_boundary2D_pair,
                   sample_boundary2D_separate, sample_random, sample_uniform, wall_mse)
 
 from .examples import get_examples
@@ -131,9 +131,24 @@ class Fluid2DModel(BaseModel):
         # mean((u - (u_prev - grad_p))^2): r = 1*(u + 0) + (-1)*(u_prev + (-1)*grad_p)
         return {'main': fused_mse(u, None, u_prev, grad_p, gamma=-1.0, delta=-1.0), 'bc': self._wall_loss(x.shape[0])}
 
-    # ---- output (host side; figures are out of scope) ------------------------
+    # ---- output (host side; PNG figures are out of scope) ---------------------
+    def field_quantities(self, resolution):
+        """The fields fluid/model.py:207-217 writes, on the (R, R) cell-centred grid:
+        velocity u (R, R, 2), speed |u| (R, R) and vorticity curl u = dv/dx - du/dy (R, R)
+        from ONE gradient jet of the velocity net (no autograd passes)."""
+        grid = sample_uniform(resolution, 2, device=self.device, flatten=False).requires_grad_(True)
+        with torch.no_grad():  # no parameter gradients: no saved streams
+            u = self.velocity_field(grid)
+            jac, _ = jacobian(u, grid)  # (R, R, 2, 2)
+        u_mag = torch.sqrt(torch.sum(u ** 2, dim=-1))
+        u_curl = jac[..., 1, 0] - jac[..., 0, 1]
+        return u.detach(), u_mag.detach(), u_curl.detach(), grid.detach()
+
     def write_output(self, output_folder):
-        u, grid = self.sample_field(self.vis_resolution, return_samples=True)
-        u_np = u.detach().cpu().numpy()
+        """fluid/model.py:207-232: t###.npy = the velocity grid (as the reference), plus the
+        speed and curl arrays its PNGs are drawn from (t###_mag.npy, t###_curl.npy)."""
+        u, mag, curl, _ = self.field_quantities(self.vis_resolution)
         os.makedirs(output_folder, exist_ok=True)
-        np.save(os.path.join(output_folder, f"t{self.timestep:03d}_velocity.npy"), u_np)
+        np.save(os.path.join(output_folder, f"t{self.timestep:03d}.npy"), u.cpu().numpy())
+        np.save(os.path.join(output_folder, f"t{self.timestep:03d}_mag.npy"), mag.cpu().numpy())
+        np.save(os.path.join(output_folder, f"t{self.timestep:03d}_curl.npy"), curl.cpu().numpy())
