@@ -220,6 +220,10 @@ def kernel_identity(kind, mode, n, din, W):
     S = {"value": 1, "grad": 1 + din, "lap": 2 + din}[mode]
     NT = W // 16
     lap = "true" if mode == "lap" else "false"
+    if kind == "bwd" and lib.insr_jet_bwd_is_wide(n, din, W, m) == 1:  # W = 256: two kernels + reductions
+        grid = ((n + 15) // 16) * 512
+        return (f"insr::jet_bwd_x6p<{S}, {lap}> + insr::dw_x6<{S}, {lap}> + reductions (wide path; time = all four)",
+                grid, True)
     T = lib.insr_jet_split_tiles(n, din, W, m, 1 if kind == "bwd" else 0)
     x6 = nat.get_precision()[1 if kind == "bwd" else 0] == nat.PREC_BF16X6 and (kind == "fwd" or NT <= 8)
     if T > 0:

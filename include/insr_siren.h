@@ -92,6 +92,25 @@ int insr_siren_jet_bwd(const float* x, long n_points, int d_in, int d_out, int n
                        const float* gy, const float* gdy, const float* glap, float* partial,
                        void* stream);
 
+/*
+ * Backward of the jet straight into the network's flat gradient:
+ *   grad = (accumulate ? grad : 0) + d(loss)/d(params)   (fixed summation order)
+ *   work  insr_jet_bwd_work_bytes(...) of scratch.
+ * Width <= 128 (and F32 backward precision): insr_siren_jet_bwd + insr_reduce_partials.
+ * Width 256 with the x6 backward precision: the wide path (jet_x6w.hip) -- a
+ * propagation-only reverse sweep storing the pre-activation adjoints, a split-K GEMM
+ * for the hidden-layer weight gradients (K = points x streams), compact partial rows
+ * for the first layer, the biases and the output layer, and their reductions.
+ * Replaces: loss.backward() into the parameters (base/baseModel.py:77).
+ */
+int insr_siren_jet_bwd_grad(const float* x, long n_points, int d_in, int d_out, int num_hidden,
+                            int width, int mode, const float* params, const float* act,
+                            const float* gy, const float* gdy, const float* glap, float* work,
+                            float* grad, int accumulate, void* stream);
+long insr_jet_bwd_work_bytes(long n_points, int d_in, int d_out, int num_hidden, int width, int mode);
+/* 1 if insr_siren_jet_bwd_grad takes the wide path for this batch / width / mode. */
+int insr_jet_bwd_is_wide(long n_points, int d_in, int width, int mode);
+
 /* Number of partial-gradient rows insr_siren_jet_bwd writes for n points: one
  * per 64-point wave-tile block, or one per T-tile (16T-point) tile-split block,
  * whichever the backward selects for this size, width and mode. */

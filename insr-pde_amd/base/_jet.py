@@ -116,12 +116,22 @@ class _SirenJet(torch.autograd.Function):
         n, din = x2.shape
         L, W, dout = mlp.num_hidden_layers, mlp.hidden_features, mlp.out_features
         lib = nat.lib()
-        part = torch.empty(max(lib.insr_jet_partial_bytes(n, din, dout, L, W, mode) // 4, 1), device=x2.device,
-                           dtype=torch.float32)
         gflat, accumulate = mlp.grad_for_backward()
         c = lambda t: None if t is None else (t if t.is_contiguous() else t.contiguous())  # noqa: E731
         gy, gdy, glap = c(gy), c(gdy), c(glap)
         st = nat.stream_of(x2.device)
+        if lib.insr_jet_bwd_is_wide(n, din, W, mode) == 1:
+            # W = 256: propagation kernel + split-K dW GEMM + reductions, straight into .grad
+            work = torch.empty(max(lib.insr_jet_bwd_work_bytes(n, din, dout, L, W, mode) // 4, 1), device=x2.device,
+                               dtype=torch.float32)
+            with _timed("bwd", mode, n, W, (din, dout, L)):
+                rc = lib.insr_siren_jet_bwd_grad(nat.ptr(x2), n, din, dout, L, W, mode, nat.ptr(mlp.flat_params()),
+                                                 nat.ptr(act), nat.ptr(gy), nat.ptr(gdy), nat.ptr(glap), nat.ptr(work),
+                                                 nat.ptr(gflat), accumulate, st)
+            nat.check(rc, "insr_siren_jet_bwd_grad")
+            return none
+        part = torch.empty(max(lib.insr_jet_partial_bytes(n, din, dout, L, W, mode) // 4, 1), device=x2.device,
+                           dtype=torch.float32)
         with _timed("bwd", mode, n, W, (din, dout, L)):
             rc = lib.insr_siren_jet_bwd(nat.ptr(x2), n, din, dout, L, W, mode, nat.ptr(mlp.flat_params()),
                                         nat.ptr(act), nat.ptr(gy), nat.ptr(gdy), nat.ptr(glap), nat.ptr(part), st)

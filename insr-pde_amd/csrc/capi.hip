@@ -89,6 +89,12 @@ bool use_x6(int bwd, int NT) {
   return g_prec[bwd ? 1 : 0] == INSR_PREC_BF16X6 && (!bwd || NT <= 8);
 }
 
+// W = 256 backward on the x6 precision: the two-kernel wide path (jet_x6w.hip)
+bool use_wide(long n, int S, int NT) {
+  prec_init();
+  return NT == 16 && g_prec[1] == INSR_PREC_BF16X6 && use_split_bwd(n, S, NT);
+}
+
 int split_tiles(int bwd, int NT, int S, long n) {
   tiles_init();
   const bool x6 = use_x6(bwd, NT);
@@ -298,6 +304,35 @@ int insr_siren_jet_bwd(const float* x, long n, int din, int dout, int L, int W, 
                               params, act, gy, gdy, glap, partial, P, (hipStream_t)stream);
   return dispatch_bwd_wave(NT, S, mode == INSR_MODE_LAP, x, (int)n, din, dout, L, params, act, gy, gdy, glap,
                            partial, P, (hipStream_t)stream);
+}
+
+long insr_jet_bwd_work_bytes(long n, int din, int dout, int L, int W, int mode) {
+  if (!shape_ok(din, dout, L, W, mode) || n < 0) return INSR_EINVAL;
+  const int S = streams_for(din, mode), NT = nt_for(W);
+  if (use_wide(n, S, NT)) return wide_work_floats(n, din, dout, L, W, S) * (long)sizeof(float);
+  return insr_jet_partial_bytes(n, din, dout, L, W, mode);
+}
+
+int insr_jet_bwd_is_wide(long n, int din, int W, int mode) {
+  const int S = streams_for(din, mode), NT = nt_for(W);
+  if (S < 0 || NT < 0 || n < 0) return INSR_EINVAL;
+  return use_wide(n, S, NT) ? 1 : 0;
+}
+
+int insr_siren_jet_bwd_grad(const float* x, long n, int din, int dout, int L, int W, int mode, const float* params,
+                            const float* act, const float* gy, const float* gdy, const float* glap, float* work,
+                            float* grad, int accumulate, void* stream) {
+  if (!shape_ok(din, dout, L, W, mode) || n < 0 || n > 0x7fffffffL) return INSR_EINVAL;
+  if (n == 0) return 0;
+  if (!x || !params || !act || !work || !grad) return INSR_EINVAL;
+  const int S = streams_for(din, mode), NT = nt_for(W);
+  if (use_wide(n, S, NT))
+    return dispatch_wide_bwd(S, mode == INSR_MODE_LAP, x, (int)n, din, dout, L, params, act, gy, gdy, glap, work, grad,
+                             accumulate, (hipStream_t)stream);
+  int rc = insr_siren_jet_bwd(x, n, din, dout, L, W, mode, params, act, gy, gdy, glap, work, stream);
+  if (rc) return rc;
+  return insr_reduce_partials(work, insr_jet_partial_blocks(n, din, W, mode), insr_siren_param_count(din, dout, L, W),
+                              grad, accumulate, stream);
 }
 
 int insr_jet_partial_blocks(long n, int din, int W, int mode) {

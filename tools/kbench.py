@@ -100,6 +100,15 @@ def main():
                                                          nat.ptr(act), nat.ptr(gy), nat.ptr(gdy), nat.ptr(glap),
                                                          nat.ptr(part), st), "bwd")
 
+                    work = torch.empty(max(lib.insr_jet_bwd_work_bytes(n, din, dout, L, W, mode) // 4, 1),
+                                       device="cuda")
+                    wide = lib.insr_jet_bwd_is_wide(n, din, W, mode)
+
+                    def bwdg():  # backward straight into .grad (the path the autograd bridge takes)
+                        nat.check(lib.insr_siren_jet_bwd_grad(nat.ptr(x), n, din, dout, L, W, mode, nat.ptr(flat),
+                                                              nat.ptr(act), nat.ptr(gy), nat.ptr(gdy), nat.ptr(glap),
+                                                              nat.ptr(work), nat.ptr(g), 0, st), "bwd_grad")
+
                     def red():
                         nat.check(lib.insr_reduce_partials(nat.ptr(part), nb, P, nat.ptr(g), 0, st), "reduce")
 
@@ -107,10 +116,12 @@ def main():
                     fwd()
                     tb = time_it(bwd, args.reps)
                     tr = time_it(red, args.reps)
+                    tg = time_it(bwdg, args.reps)
                     macs = P_macs(din, dout, L, W)
                     rec = {"net": name, "mode": mname, "n": n, "variant": variant, "T": [tf_, tb_], "nb": nb,
                            "fwd_us": round(tf, 2),
-                           "bwd_us": round(tb, 2), "reduce_us": round(tr, 2),
+                           "bwd_us": round(tb, 2), "reduce_us": round(tr, 2), "bwd_grad_us": round(tg, 2),
+                           "wide": wide, "bwd_grad_tflops": round(n * S * 4 * macs / tg / 1e6, 2),
                            "fwd_tflops": round(n * S * 2 * macs / tf / 1e6, 2),
                            "bwd_tflops": round(n * S * 4 * macs / tb / 1e6, 2)}
                     out.append(rec)
