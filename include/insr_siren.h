@@ -110,6 +110,9 @@ int insr_siren_jet_bwd_grad(const float* x, long n_points, int d_in, int d_out, 
 long insr_jet_bwd_work_bytes(long n_points, int d_in, int d_out, int num_hidden, int width, int mode);
 /* 1 if insr_siren_jet_bwd_grad takes the wide path for this batch / width / mode. */
 int insr_jet_bwd_is_wide(long n_points, int d_in, int width, int mode);
+/* Smallest width (128 or 256) that takes the wide path; returns the old value.
+ * Env INSR_WIDE_MIN_WIDTH.  Process-wide tuning/testing knob. */
+int insr_jet_set_wide_min_width(int width);
 
 /* Number of partial-gradient rows insr_siren_jet_bwd writes for n points: one
  * per 64-point wave-tile block, or one per T-tile (16T-point) tile-split block,

@@ -89,10 +89,18 @@ bool use_x6(int bwd, int NT) {
   return g_prec[bwd ? 1 : 0] == INSR_PREC_BF16X6 && (!bwd || NT <= 8);
 }
 
-// W = 256 backward on the x6 precision: the two-kernel wide path (jet_x6w.hip)
-bool use_wide(long n, int S, int NT) {
+// Backward on the x6 precision through the two-kernel path (jet_x6w.hip: propagation kernel +
+// split-K dW GEMM) for widths >= g_wide_min (default 256; env INSR_WIDE_MIN_WIDTH) and, at
+// width 128, for Laplacian jets of >= 32768 points.  Measured (profiles/r01/kbench_wide*.jsonl):
+// W = 256 el3D grad 20.7 -> 10.0 ms; W = 128 LAP 65536 points 949 -> 805 us, while W = 128
+// value / grad jets and LAP at 16384 points are as fast or faster fused.
+static int g_wide_min = -1;
+bool use_wide(long n, int S, int NT, bool lap) {
   prec_init();
-  return NT == 16 && g_prec[1] == INSR_PREC_BF16X6 && use_split_bwd(n, S, NT);
+  if (g_wide_min < 0) g_wide_min = env_or("INSR_WIDE_MIN_WIDTH", 256);
+  if (NT < 8 || g_prec[1] != INSR_PREC_BF16X6 || !use_split_bwd(n, S, NT)) return false;
+  if (16 * NT >= g_wide_min) return true;
+  return NT == 8 && lap && n >= 32768 && g_wide_min <= 256;  // Laplacian jets at width 128
 }
 
 int split_tiles(int bwd, int NT, int S, long n) {
@@ -306,17 +314,23 @@ int insr_siren_jet_bwd(const float* x, long n, int din, int dout, int L, int W, 
                            partial, P, (hipStream_t)stream);
 }
 
+int insr_jet_set_wide_min_width(int width) {
+  const int old = g_wide_min < 0 ? env_or("INSR_WIDE_MIN_WIDTH", 256) : g_wide_min;
+  g_wide_min = width;
+  return old;
+}
+
 long insr_jet_bwd_work_bytes(long n, int din, int dout, int L, int W, int mode) {
   if (!shape_ok(din, dout, L, W, mode) || n < 0) return INSR_EINVAL;
   const int S = streams_for(din, mode), NT = nt_for(W);
-  if (use_wide(n, S, NT)) return wide_work_floats(n, din, dout, L, W, S) * (long)sizeof(float);
+  if (use_wide(n, S, NT, mode == INSR_MODE_LAP)) return wide_work_floats(n, din, dout, L, W, S) * (long)sizeof(float);
   return insr_jet_partial_bytes(n, din, dout, L, W, mode);
 }
 
 int insr_jet_bwd_is_wide(long n, int din, int W, int mode) {
   const int S = streams_for(din, mode), NT = nt_for(W);
   if (S < 0 || NT < 0 || n < 0) return INSR_EINVAL;
-  return use_wide(n, S, NT) ? 1 : 0;
+  return use_wide(n, S, NT, mode == INSR_MODE_LAP) ? 1 : 0;
 }
 
 int insr_siren_jet_bwd_grad(const float* x, long n, int din, int dout, int L, int W, int mode, const float* params,
@@ -326,8 +340,8 @@ int insr_siren_jet_bwd_grad(const float* x, long n, int din, int dout, int L, in
   if (n == 0) return 0;
   if (!x || !params || !act || !work || !grad) return INSR_EINVAL;
   const int S = streams_for(din, mode), NT = nt_for(W);
-  if (use_wide(n, S, NT))
-    return dispatch_wide_bwd(S, mode == INSR_MODE_LAP, x, (int)n, din, dout, L, params, act, gy, gdy, glap, work, grad,
+  if (use_wide(n, S, NT, mode == INSR_MODE_LAP))
+    return dispatch_wide_bwd(NT, S, mode == INSR_MODE_LAP, x, (int)n, din, dout, L, params, act, gy, gdy, glap, work, grad,
                              accumulate, (hipStream_t)stream);
   int rc = insr_siren_jet_bwd(x, n, din, dout, L, W, mode, params, act, gy, gdy, glap, work, stream);
   if (rc) return rc;

@@ -324,8 +324,8 @@ int dispatch_fwd_x6(int NT, int S, bool LAP, int T, const float* x, int N, int d
 int dispatch_bwd_x6(int NT, int S, bool LAP, int T, const float* x, int N, int din, int dout, int L,
                     const float* prm, const float* act, const float* gy, const float* gdy, const float* glap,
                     float* part, long P, hipStream_t st);
-// wide-layer (W = 256) backward: propagation kernel + dW GEMM + reductions (jet_x6w.hip)
-int dispatch_wide_bwd(int S, bool LAP, const float* x, int N, int din, int dout, int L, const float* prm,
+// two-kernel backward (W = 128 / 256): propagation kernel + dW GEMM + reductions (jet_x6w.hip)
+int dispatch_wide_bwd(int NT, int S, bool LAP, const float* x, int N, int din, int dout, int L, const float* prm,
                       const float* act, const float* gy, const float* gdy, const float* glap, float* work, float* grad,
                       int accumulate, hipStream_t st);
 long wide_work_floats(long n, int din, int dout, int L, int W, int S);

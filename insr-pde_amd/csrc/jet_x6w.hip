@@ -23,7 +23,6 @@
 
 namespace insr {
 
-constexpr int kWideNT = 16, kWideW = 256;
 
 // compact partial row of the wide path: [W0 (W din) | b0 (W) | b_1 .. b_L (L W) | Wout (dout W) | bout]
 __host__ __device__ inline long small_count(int din, int dout, int L, int W) {
@@ -33,13 +32,13 @@ __host__ __device__ inline long small_count(int din, int dout, int L, int W) {
 // ---------------------------------------------------------------------------------------
 // kernel 1: propagation-only reverse sweep (one 16-point tile per block, 8 waves x 2 row tiles)
 // ---------------------------------------------------------------------------------------
-template <int S, bool LAP>
+template <int NT, int S, bool LAP>
 __global__ __launch_bounds__(512) void jet_bwd_x6p(const float* __restrict__ x, int N, int din, int dout, int L,
                                                    const float* __restrict__ prm, const float* __restrict__ act,
                                                    const float* __restrict__ gy, const float* __restrict__ gdy,
                                                    const float* __restrict__ glap, float* __restrict__ adj,
                                                    float* __restrict__ part, long Ps) {
-  constexpr int NT = kWideNT, W = kWideW, RPW = 2, KC = NT / 2;
+  constexpr int W = 16 * NT, RPW = NT / 8, KC = NT / 2;
   constexpr int LDB = W + 8, ZPLANE = 16 * LDB, ZSET = 3 * ZPLANE;
   constexpr int NTAN = LAP ? S - 2 : S - 1;
   extern __shared__ __attribute__((aligned(16))) float lds_f[];
@@ -235,9 +234,11 @@ __global__ __launch_bounds__(512) void jet_bwd_x6p(const float* __restrict__ x, 
 //   A = z̄ [q][n][k], B = h [q][m][k] (k minor, rows padded to 40: conflict-free b128 reads);
 //   the loaders pack two adjacent points per u32 (DPP lane swap) and split each value once.
 // ---------------------------------------------------------------------------------------
-constexpr int kDwKR = 40;                    // k row (32 + 8 pad) in bf16 elements
-constexpr int kDwPL = kWideW * kDwKR;        // one plane
-constexpr size_t kDwLds = (size_t)6 * kDwPL * 2;  // A + B, 3 planes each
+constexpr int kDwKR = 40;  // k row (32 + 8 pad) in bf16 elements
+template <int NT>
+constexpr int dw_plane() { return 16 * NT * kDwKR; }  // one plane (bf16 elements)
+template <int NT>
+constexpr size_t dw_lds() { return (size_t)6 * dw_plane<NT>() * 2; }  // A + B, 3 planes each
 
 __device__ __forceinline__ float swap1(float v) {  // value of lane ^ 1 (quad_perm 1,0,3,2)
   return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, false));
@@ -246,7 +247,9 @@ __device__ __forceinline__ float swap1(float v) {  // value of lane ^ 1 (quad_pe
 // write one granule (4 neurons 4g..4g+3 of row tile rt, point c) as point pairs into the
 // k-minor planes: even lanes write neurons r = 0, 1 of points (c, c + 1), odd lanes r = 2, 3
 // of points (c - 1, c)
+template <int NT>
 __device__ __forceinline__ void dw_put(unsigned short* P, const floatx4& v, int rt, int ul, int lane) {
+  constexpr int kDwPL = dw_plane<NT>();
   const int g = lane >> 4, c = lane & 15, odd = c & 1;
   const float r0 = swap1(odd ? v[0] : v[2]);
   const float r1 = swap1(odd ? v[1] : v[3]);
@@ -267,11 +270,12 @@ __device__ __forceinline__ void dw_put(unsigned short* P, const floatx4& v, int 
   q1[kDwPL] = l;
 }
 
-template <int S, bool LAP>
+template <int NT, int S, bool LAP>
 __global__ __launch_bounds__(512) void dw_x6(int N, const float* __restrict__ act, const float* __restrict__ adj,
                                              float* __restrict__ dpart, int KS) {
-  constexpr int NT = kWideNT, W = kWideW;
-  constexpr int NTAN = LAP ? S - 2 : S - 1;
+  constexpr int W = 16 * NT, RT = NT / 8;  // RT: dW row tiles per wave
+  constexpr int G = NT / 4;                   // granules per thread per chunk (2 units x NT row tiles / 8 waves)
+  constexpr int kDwPL = dw_plane<NT>();
   extern __shared__ __attribute__((aligned(16))) float lds_f[];
   unsigned short* A = reinterpret_cast<unsigned short*>(lds_f);
   unsigned short* B = A + 3 * kDwPL;
@@ -282,44 +286,44 @@ __global__ __launch_bounds__(512) void dw_x6(int N, const float* __restrict__ ac
   const int chunks = (units + 1) / 2;
   const int c0 = (int)((long)chunks * blockIdx.x / KS), c1 = (int)((long)chunks * (blockIdx.x + 1) / KS);
 
-  floatx4 dacc[2][NT];
+  floatx4 dacc[RT][NT];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < RT; ++i)
 #pragma unroll
     for (int ct = 0; ct < NT; ++ct) dacc[i][ct] = floatx4{0.f, 0.f, 0.f, 0.f};
 
   // raw operands of one chunk, per thread: 4 granules (unit ul = it >> 1, row tile
   // wave + 8 (it & 1)) of z̄_j, z_{j-1} (stream 0) and z_{j-1} (stream s).  The next chunk's
   // loads are issued before the MFMA phase of the current one (software pipeline).
-  floatx4 rzb[4], rz0[4], rzs[4];
+  floatx4 rzb[G], rz0[G], rzs[G];
   // branch-free: a granule past the end loads unit 0 (valid memory) and is zeroed in put(),
   // so the compiler keeps every load of the chunk in flight (no waitcnt inside fetch)
   auto fetch = [&](int ch) {
 #pragma unroll
-    for (int it = 0; it < 4; ++it) {
-      const int ul = it >> 1, rt = wave + 8 * (it & 1);
+    for (int it = 0; it < G; ++it) {
+      const int ul = it / RT, rt = wave + 8 * (it % RT);
       const int u = 2 * ch + ul;
       const int uu = (ch < c1 && u < units) ? u : 0;
       const int t = uu / S, s = uu - t * S;
       const float* ba = act_base(act, j - 1, ntiles, t, S, NT);
       rzb[it] = *reinterpret_cast<const floatx4*>(act_base(adj, j - 1, ntiles, t, S, NT) +
                                                   ((s * NT + rt) * 64 + lane) * 4);
-      if (S % 2 != 0 || it < 2) rz0[it] = *reinterpret_cast<const floatx4*>(ba + (rt * 64 + lane) * 4);
+      if (S % 2 != 0 || it < RT) rz0[it] = *reinterpret_cast<const floatx4*>(ba + (rt * 64 + lane) * 4);
       rzs[it] = *reinterpret_cast<const floatx4*>(ba + ((s * NT + rt) * 64 + lane) * 4);
     }
   };
-  floatx4 ssv[4], scv[4];
+  floatx4 ssv[G], scv[G];
   auto put = [&](int ch) {
 #pragma unroll
-    for (int it = 0; it < 4; ++it) {
-      const int ul = it >> 1, rt = wave + 8 * (it & 1);
+    for (int it = 0; it < G; ++it) {
+      const int ul = it / RT, rt = wave + 8 * (it % RT);
       const int u = 2 * ch + ul;
       const bool live = u < units;
       const int uu = live ? u : 0;
       const int t = uu / S, s = uu - t * S;
-      // even S: units 2ch, 2ch + 1 are streams of ONE tile, so granules it and it + 2 share z0
+      // even S: units 2ch, 2ch + 1 are streams of ONE tile, so granules it and it + RT share z0
       constexpr bool kShare = S % 2 == 0;
-      if (!kShare || it < 2) {
+      if (!kShare || it < RT) {
         float amax = 0.f;
 #pragma unroll
         for (int r = 0; r < 4; ++r) amax = fmaxf(amax, fabsf(OMEGA * rz0[it][r]));
@@ -331,11 +335,11 @@ __global__ __launch_bounds__(512) void dw_x6(int N, const float* __restrict__ ac
             sincosf(OMEGA * rz0[it][r], &a, &b);
           else
             sincos_fast(OMEGA * rz0[it][r], a, b);
-          ssv[it & (kShare ? 1 : 3)][r] = a;
-          scv[it & (kShare ? 1 : 3)][r] = b;
+          ssv[kShare ? it % RT : it][r] = a;
+          scv[kShare ? it % RT : it][r] = b;
         }
       }
-      const floatx4 sv = ssv[it & (kShare ? 1 : 3)], cv = scv[it & (kShare ? 1 : 3)];
+      const floatx4 sv = ssv[kShare ? it % RT : it], cv = scv[kShare ? it % RT : it];
       floatx4 hv;
       if (LAP && s == S - 1) {  // Laplacian stream: needs the tangents (read here)
         hv = h_stream<NT, S, LAP>(act_base(act, j - 1, ntiles, t, S, NT), s, rt, lane, sv, cv);
@@ -344,8 +348,8 @@ __global__ __launch_bounds__(512) void dw_x6(int N, const float* __restrict__ ac
         for (int r = 0; r < 4; ++r) hv[r] = s == 0 ? sv[r] : OMEGA * cv[r] * rzs[it][r];
       }
       const floatx4 zero = floatx4{0.f, 0.f, 0.f, 0.f};
-      dw_put(A, live ? rzb[it] : zero, rt, ul, lane);
-      dw_put(B, live ? hv : zero, rt, ul, lane);
+      dw_put<NT>(A, live ? rzb[it] : zero, rt, ul, lane);
+      dw_put<NT>(B, live ? hv : zero, rt, ul, lane);
     }
   };
 
@@ -355,10 +359,10 @@ __global__ __launch_bounds__(512) void dw_x6(int N, const float* __restrict__ ac
     put(ch);
     fetch(ch + 1);
     __syncthreads();
-    Frag3 af[2];
+    Frag3 af[RT];
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const unsigned short* pa = A + (16 * (2 * wave + i) + c) * kDwKR + 8 * g;
+    for (int i = 0; i < RT; ++i) {
+      const unsigned short* pa = A + (16 * (RT * wave + i) + c) * kDwKR + 8 * g;
       af[i].h = *reinterpret_cast<const u32x4*>(pa);
       af[i].m = *reinterpret_cast<const u32x4*>(pa + kDwPL);
       af[i].l = *reinterpret_cast<const u32x4*>(pa + 2 * kDwPL);
@@ -371,16 +375,16 @@ __global__ __launch_bounds__(512) void dw_x6(int N, const float* __restrict__ ac
       bf.m = *reinterpret_cast<const u32x4*>(pb + kDwPL);
       bf.l = *reinterpret_cast<const u32x4*>(pb + 2 * kDwPL);
 #pragma unroll
-      for (int i = 0; i < 2; ++i) dacc[i][ct] = mfma_x6(af[i], bf, dacc[i][ct]);
+      for (int i = 0; i < RT; ++i) dacc[i][ct] = mfma_x6(af[i], bf, dacc[i][ct]);
     }
   }
   float* out = dpart + ((long)(j - 1) * KS + blockIdx.x) * W * W;
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < RT; ++i)
 #pragma unroll
     for (int ct = 0; ct < NT; ++ct)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) out[(16 * (2 * wave + i) + 4 * g + r) * W + 16 * ct + c] = dacc[i][ct][r];
+      for (int r = 0; r < 4; ++r) out[(16 * (RT * wave + i) + 4 * g + r) * W + 16 * ct + c] = dacc[i][ct][r];
 }
 
 // ---------------------------------------------------------------------------------------
@@ -461,10 +465,10 @@ long wide_work_floats(long n, int din, int dout, int L, int W, int S) {
   return adj + small + dw + (long)kSmallRS * small_count(din, dout, L, W);
 }
 
-template <int S, bool LAP>
+template <int NT, int S, bool LAP>
 int wide_bwd_t(const float* x, int N, int din, int dout, int L, const float* prm, const float* act, const float* gy,
                const float* gdy, const float* glap, float* work, float* grad, int accumulate, hipStream_t st) {
-  constexpr int W = kWideW, NT = kWideNT;
+  constexpr int W = 16 * NT;
   const long ntiles = ((N + 63) / 64) * 4;
   const int tiles = (N + 15) / 16;
   const long Ps = small_count(din, dout, L, W);
@@ -475,16 +479,17 @@ int wide_bwd_t(const float* x, int N, int din, int dout, int L, const float* prm
   constexpr size_t lds_p = (size_t)S * 3 * 16 * (W + 8) * 2;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)jet_bwd_x6p<S, LAP>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)jet_bwd_x6p<NT, S, LAP>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)lds_p);
-    (void)hipFuncSetAttribute((const void*)dw_x6<S, LAP>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kDwLds);
+    (void)hipFuncSetAttribute((const void*)dw_x6<NT, S, LAP>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)dw_lds<NT>());
     attr = true;
   }
-  hipLaunchKernelGGL((jet_bwd_x6p<S, LAP>), dim3(tiles), dim3(512), lds_p, st, x, N, din, dout, L, prm, act, gy, gdy,
-                     glap, adj, small, Ps);
+  hipLaunchKernelGGL((jet_bwd_x6p<NT, S, LAP>), dim3(tiles), dim3(512), lds_p, st, x, N, din, dout, L, prm, act, gy,
+                     gdy, glap, adj, small, Ps);
   if (L > 0) {
     const int KS = wide_ks(N, S, L);
-    hipLaunchKernelGGL((dw_x6<S, LAP>), dim3(KS, L), dim3(512), kDwLds, st, N, act, adj, dpart, KS);
+    hipLaunchKernelGGL((dw_x6<NT, S, LAP>), dim3(KS, L), dim3(512), dw_lds<NT>(), st, N, act, adj, dpart, KS);
     hipLaunchKernelGGL(reduce_dw_kernel, dim3((unsigned)((W * W + 255) / 256), L), dim3(256), 0, st, dpart, KS, din, W,
                        grad, accumulate);
   }
@@ -495,18 +500,27 @@ int wide_bwd_t(const float* x, int N, int din, int dout, int L, const float* prm
   return (int)hipGetLastError();
 }
 
-int dispatch_wide_bwd(int S, bool LAP, const float* x, int N, int din, int dout, int L, const float* prm,
-                      const float* act, const float* gy, const float* gdy, const float* glap, float* work, float* grad,
-                      int accumulate, hipStream_t st) {
+template <int NT>
+int wide_bwd_nt(int S, bool LAP, const float* x, int N, int din, int dout, int L, const float* prm, const float* act,
+                const float* gy, const float* gdy, const float* glap, float* work, float* grad, int accumulate,
+                hipStream_t st) {
   switch (S * 2 + (LAP ? 1 : 0)) {
-    case 2: return wide_bwd_t<1, false>(x, N, din, dout, L, prm, act, gy, gdy, glap, work, grad, accumulate, st);
-    case 4: return wide_bwd_t<2, false>(x, N, din, dout, L, prm, act, gy, gdy, glap, work, grad, accumulate, st);
-    case 6: return wide_bwd_t<3, false>(x, N, din, dout, L, prm, act, gy, gdy, glap, work, grad, accumulate, st);
-    case 8: return wide_bwd_t<4, false>(x, N, din, dout, L, prm, act, gy, gdy, glap, work, grad, accumulate, st);
-    case 7: return wide_bwd_t<3, true>(x, N, din, dout, L, prm, act, gy, gdy, glap, work, grad, accumulate, st);
-    case 9: return wide_bwd_t<4, true>(x, N, din, dout, L, prm, act, gy, gdy, glap, work, grad, accumulate, st);
+    case 2: return wide_bwd_t<NT, 1, false>(x, N, din, dout, L, prm, act, gy, gdy, glap, work, grad, accumulate, st);
+    case 4: return wide_bwd_t<NT, 2, false>(x, N, din, dout, L, prm, act, gy, gdy, glap, work, grad, accumulate, st);
+    case 6: return wide_bwd_t<NT, 3, false>(x, N, din, dout, L, prm, act, gy, gdy, glap, work, grad, accumulate, st);
+    case 8: return wide_bwd_t<NT, 4, false>(x, N, din, dout, L, prm, act, gy, gdy, glap, work, grad, accumulate, st);
+    case 7: return wide_bwd_t<NT, 3, true>(x, N, din, dout, L, prm, act, gy, gdy, glap, work, grad, accumulate, st);
+    case 9: return wide_bwd_t<NT, 4, true>(x, N, din, dout, L, prm, act, gy, gdy, glap, work, grad, accumulate, st);
     default: return INSR_EINVAL;
   }
+}
+
+int dispatch_wide_bwd(int NT, int S, bool LAP, const float* x, int N, int din, int dout, int L, const float* prm,
+                      const float* act, const float* gy, const float* gdy, const float* glap, float* work, float* grad,
+                      int accumulate, hipStream_t st) {
+  if (NT == 16) return wide_bwd_nt<16>(S, LAP, x, N, din, dout, L, prm, act, gy, gdy, glap, work, grad, accumulate, st);
+  if (NT == 8) return wide_bwd_nt<8>(S, LAP, x, N, din, dout, L, prm, act, gy, gdy, glap, work, grad, accumulate, st);
+  return INSR_EWIDTH;
 }
 
 }  // namespace insr

@@ -43,6 +43,7 @@ VARIANTS = {  # (fwd, bwd, bwd_value) split thresholds, (fwd, bwd) forced tiles 
     "x6_fwd_f32_bwd": ((BIG, BIG, BIG), (4, 2), (X6, F32)),   # precisions mix: same saved layout
     "f32_fwd_x6_bwd": ((BIG, BIG, BIG), (2, 4), (F32, X6)),
     "x6_fwd_wave_bwd": ((BIG, 0, 0), (2, 0), (X6, F32)),
+    "x6_wide128": ((BIG, BIG, BIG), (0, 0), (X6, X6), 128),   # two-kernel backward (prop + dW GEMM) from W = 128
 }
 
 
@@ -55,14 +56,17 @@ def base(request):
     B._native.load()
     old, old_tiles = B._native.get_split_thresholds(), B._native.get_split_tiles()
     old_prec = B._native.get_precision()
-    thr, tiles, prec = VARIANTS[request.param]
+    thr, tiles, prec = VARIANTS[request.param][:3]
+    wide = VARIANTS[request.param][3] if len(VARIANTS[request.param]) > 3 else 256
     B._native.set_split_thresholds(*thr)
     B._native.set_split_tiles(tiles[0], tiles[1], old_tiles[2])
     B._native.set_precision(*prec)
+    old_wide = B._native.lib().insr_jet_set_wide_min_width(wide)
     yield B
     B._native.set_split_thresholds(*old)
     B._native.set_split_tiles(*old_tiles)
     B._native.set_precision(*old_prec)
+    B._native.lib().insr_jet_set_wide_min_width(old_wide)
 
 
 def nerr(a, b):

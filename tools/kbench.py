@@ -26,6 +26,7 @@ VARIANTS = {  # label: ((fwd, bwd, bwd_value) thresholds, (fwd, bwd) forced tile
     "x6_1": ((BIG, BIG, BIG), (1, 1), (1, 1)),
     "x6_2": ((BIG, BIG, BIG), (2, 2), (1, 1)),
     "x6_4": ((BIG, BIG, BIG), (4, 4), (1, 1)),
+    "x6w": ((BIG, BIG, BIG), (0, 0), (1, 1)),  # x6 with the two-kernel backward from width 128
 }
 MODES = {"value": 0, "grad": 1, "lap": 2}
 
@@ -85,6 +86,7 @@ def main():
                     nat.set_split_thresholds(*thr)
                     nat.set_split_tiles(tiles[0], tiles[1], 256)
                     nat.set_precision(*prec)
+                    lib.insr_jet_set_wide_min_width(128 if variant.endswith("w") else 256)
                     part = torch.empty(max(lib.insr_jet_partial_bytes(n, din, dout, L, W, mode) // 4, 1), device="cuda")
                     nb = lib.insr_jet_partial_blocks(n, din, W, mode)
                     tf_, tb_ = (lib.insr_jet_split_tiles(n, din, W, mode, 0),
