@@ -120,6 +120,8 @@ class _SirenJet(torch.autograd.Function):
         c = lambda t: None if t is None else (t if t.is_contiguous() else t.contiguous())  # noqa: E731
         gy, gdy, glap = c(gy), c(gdy), c(glap)
         st = nat.stream_of(x2.device)
+        cur = torch.cuda.current_stream(x2.device)
+        mlp.grad_write_begin(cur)  # order after a write of .grad made on another stream
         if lib.insr_jet_bwd_is_wide(n, din, W, mode) == 1:
             # W = 256: propagation kernel + split-K dW GEMM + reductions, straight into .grad
             work = torch.empty(max(lib.insr_jet_bwd_work_bytes(n, din, dout, L, W, mode) // 4, 1), device=x2.device,
@@ -129,6 +131,7 @@ class _SirenJet(torch.autograd.Function):
                                                  nat.ptr(act), nat.ptr(gy), nat.ptr(gdy), nat.ptr(glap), nat.ptr(work),
                                                  nat.ptr(gflat), accumulate, st)
             nat.check(rc, "insr_siren_jet_bwd_grad")
+            mlp.grad_write_end(cur)
             return none
         part = torch.empty(max(lib.insr_jet_partial_bytes(n, din, dout, L, W, mode) // 4, 1), device=x2.device,
                            dtype=torch.float32)
@@ -140,6 +143,7 @@ class _SirenJet(torch.autograd.Function):
             rc = lib.insr_reduce_partials(nat.ptr(part), lib.insr_jet_partial_blocks(n, din, W, mode), gflat.numel(),
                                           nat.ptr(gflat), accumulate, st)
         nat.check(rc, "insr_reduce_partials")
+        mlp.grad_write_end(cur)
         return none
 
 

@@ -99,6 +99,7 @@ class PhaseLoop:
             torch.cuda.synchronize(self.m.device)
             self.use_graph = False
             self.capture_error = repr(e)
+            self.m._insr_capture_error = self.capture_error  # visible after run() (tests, logs)
             self.graph = self.graph2 = None
             return None
         self.static = {k: v.detach() for k, v in out.items()}

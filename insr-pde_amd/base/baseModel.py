@@ -139,6 +139,11 @@ class BaseModel(ABC):
         if world == 1:
             return loss_dict
         d = torch.distributed
+        if torch.device(self.device).type == "cuda" and torch.cuda.is_available():
+            cur = torch.cuda.current_stream(self.device)
+            for net in self._trainable_networks.values():
+                if hasattr(net, "grad_read_sync"):
+                    net.grad_read_sync(cur)
         grads = [net.flat_grad_buffer() for net in self._trainable_networks.values()]
         flat = torch.cat(grads) if len(grads) > 1 else grads[0]
         keys = list(loss_dict.keys())
@@ -174,6 +179,14 @@ class BaseModel(ABC):
         terms = [v for v in loss_dict.values() if v.requires_grad]
         if terms:
             torch.autograd.backward(terms, grad_tensors=[self._unit_seed(v) for v in terms])
+            # join .grad writes a side-stream backward made (fluid boundary bands): the
+            # caller's stream -- and a hipGraph capture -- must see them
+            cur = torch.cuda.current_stream(self.device) if (torch.device(self.device).type == "cuda"
+                                                             and torch.cuda.is_available()) else None
+            if cur is not None:
+                for net in self._trainable_networks.values():
+                    if hasattr(net, "grad_read_sync"):
+                        net.grad_read_sync(cur)
 
     def _unit_seed(self, v):
         seeds = self.__dict__.setdefault("_insr_seeds", {})

@@ -61,7 +61,11 @@ class _SqLoss(torch.autograd.Function):
     def forward(ctx, kind, n, m, coef, scale, offs, a, b, c, d):
         lib = nat.lib()
         dev = a.device
-        work = _workspace(dev)
+        # the partials workspace is needed (and shared per device: one stream at a time) only
+        # by losses over more than kLossPerBlock = 4096 terms; the small boundary-band losses
+        # a model runs on its side stream never touch it
+        terms = n if kind == nat.LOSS_COMBO else 2 * n
+        work = _workspace(dev) if terms > 4096 else None
         out = torch.empty((), device=dev, dtype=torch.float32)
         rc = lib.insr_sq_loss_fwd(kind, _at(a, offs[0]), _at(b, offs[1]), _at(c, offs[2]), _at(d, offs[3]), n, m,
                                   *coef, scale, nat.ptr(out), nat.ptr(work), nat.stream_of(dev))
@@ -135,14 +139,15 @@ class _SvdEnergy(torch.autograd.Function):
     def forward(ctx, J, ratio_arap, ratio_volume, n):
         lib = nat.lib()
         dev = J.device
-        if dev.index not in _SVD_WORK:
+        key = dev.index
+        if key not in _SVD_WORK:
             if torch.cuda.is_current_stream_capturing():
                 raise RuntimeError("SVD-energy workspace must be created before graph capture (run one eager call)")
-            _SVD_WORK[dev.index] = torch.empty(lib.insr_svd_energy_work_floats(), device=dev, dtype=torch.float32)
+            _SVD_WORK[key] = torch.empty(lib.insr_svd_energy_work_floats(), device=dev, dtype=torch.float32)
         out = torch.empty((), device=dev, dtype=torch.float32)
         d = J.shape[-1]
         rc = lib.insr_svd_energy_fwd(nat.ptr(J), n, d, float(ratio_arap), float(ratio_volume), nat.ptr(out),
-                                     nat.ptr(_SVD_WORK[dev.index]), nat.stream_of(dev))
+                                     nat.ptr(_SVD_WORK[key]), nat.stream_of(dev))
         nat.check(rc, "insr_svd_energy_fwd")
         ctx.save_for_backward(J)
         ctx.args = (float(ratio_arap), float(ratio_volume), n)

@@ -169,6 +169,7 @@ class MLP(nn.Module):
             g, _ = self._attach_grad_views(fold_foreign=False)
             g.zero_()
         self._grad_state = 'stale'
+        self._grad_event_stream = None  # a new iteration: earlier writes are ordered already
 
     def grad_for_backward(self):
         """(flat grad buffer, accumulate flag) for the next HIP backward."""
@@ -184,6 +185,32 @@ class MLP(nn.Module):
             return g, 1
         g, _ = self._attach_grad_views(fold_foreign=True)
         return g, 1
+
+    # ---- cross-stream ordering of the flat-gradient writes ---------------------------
+    # A model may run some jets on a side stream (fluid boundary bands); autograd then runs
+    # their backward on that stream too.  The HIP backward writes the flat .grad directly
+    # (overwrite on the first write of an iteration, accumulate after), so the writers and
+    # the readers (Adam, the DP all-reduce) are chained with an event when they are on
+    # different streams.  Works under hipGraph capture (event record / wait = graph edges).
+    def grad_write_begin(self, stream):
+        """Before a write of .grad on `stream`: wait for this iteration's previous write if it
+        was made on another stream (iterations start ordered: zero_grad clears the chain, so
+        a graph capture never waits on an event recorded outside it)."""
+        ev = getattr(self, "_grad_event", None)
+        last = getattr(self, "_grad_event_stream", None)
+        if ev is not None and last is not None and last != stream:
+            stream.wait_event(ev)
+
+    def grad_write_end(self, stream):
+        ev = getattr(self, "_grad_event", None)
+        if ev is None:
+            ev = self._grad_event = torch.cuda.Event()
+        ev.record(stream)
+        self._grad_event_stream = stream
+
+    def grad_read_sync(self, stream):
+        """Make `stream` wait for the last gradient write when it happened on another stream."""
+        self.grad_write_begin(stream)
 
     def grad_touched(self):
         return getattr(self, '_grad_state', 'stale') == 'live' or any(p.grad is not None for p in self.parameters())

@@ -102,8 +102,10 @@ class FusedAdam:
         lib = nat.lib()
         self._advance_pending()
         bufs = []
+        cur = torch.cuda.current_stream(self.device)
         for mlp, m, v in self._nets:
             if mlp.grad_touched():  # torch skips params whose .grad is None
+                mlp.grad_read_sync(cur)  # a backward may have written .grad on a side stream
                 bufs.append((mlp.flat_params(), mlp.flat_grad_buffer(), m, v))
         for p, m, v in self._loose:
             if p.grad is not None:

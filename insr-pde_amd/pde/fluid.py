@@ -87,49 +87,85 @@ class Fluid2DModel(BaseModel):
         self.velocity_field_prev.load_state_dict(self.velocity_field.state_dict())
         self._projection()
 
-    # The wall terms evaluate the network on the boundary bands in their own jet launch.
-    # (Merging them into the interior launch -- base.merge_samples, as the advection and
-    # elasticity models do -- was measured neutral on the jets at 128^2 points: the 2%
-    # extra points push the 1024-tile interior launches into one more block round on 256
-    # CUs, and the merged losses add glue launches: 1.09 vs 1.01 ms per step.)
+    # The wall terms evaluate the network on the boundary bands (~1% of the points) in their
+    # own jet launches -- latency-bound chains of a few tiles.  They are issued FIRST; with
+    # cfg.insr_band_stream = True on a side stream forked from the phase's stream, to overlap
+    # the interior launches (autograd runs their backward on that stream as well; the
+    # networks order the .grad writes across streams with events; hipGraph capture works).
+    # Off by default: measured 1.031 vs 1.009 ms per step -- the interior jets hold every
+    # CU's registers / LDS, so the band blocks cannot co-reside and only add the join.
+    # (Merging the bands into the interior launch -- base.merge_samples, as the advection and
+    # elasticity models do -- was measured neutral at 128^2 points: the 2% extra points push
+    # the 1024-tile launches into one more block round on 256 CUs; 1.09 vs 1.01 ms per step.)
     def _wall_loss(self, n_interior):
         """u_x = 0 on the x-faces, u_y = 0 on the y-faces: mean(u_x^2) + mean(u_y^2)
         (fluid/model.py:90-94) as one jet launch and one fused loss launch."""
         bxy, nb = self._boundary_bands(n_interior)
         return wall_mse(self.velocity_field(bxy), nb)
 
+    def _pressure_wall_loss(self, n_interior):
+        """mean(dp/dx^2) + mean(dp/dy^2) on the bands (fluid/model.py:116-120)."""
+        bxy, nb = self._boundary_bands(n_interior)  # one jet launch for both bands
+        gp = gradient(self.pressure_field(bxy), bxy)
+        return wall_mse(gp, nb)
+
+    def _fork(self, fn, *args):
+        """Run fn(*args) on the model's side stream (forked from the current stream) when
+        cfg.insr_band_stream (default off); returns (result, join) -- call join() before
+        the result is combined with main-stream work."""
+        if not getattr(self.cfg, "insr_band_stream", False) or torch.device(self.device).type != "cuda":
+            return fn(*args), (lambda: None)
+        main = torch.cuda.current_stream(self.device)
+        side = self.__dict__.get("_insr_side")
+        if side is None:
+            side = self._insr_side = torch.cuda.Stream(device=self.device)
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            out = fn(*args)
+
+        def join():
+            main.wait_stream(side)
+            out.record_stream(main)
+        return out, join
+
     @BaseModel._training_loop
     def _advect_velocity(self):
         x = self._sample_in_training()
+        bc, join = self._fork(self._wall_loss, x.shape[0])
         with torch.no_grad():
             u_prev = self.velocity_field_prev(x).detach()
         u = self.velocity_field(x)
         with torch.no_grad():
             foot = torch.add(x, u_prev, alpha=-self.cfg.dt).clamp_(-1.0, 1.0)
             u_target = self.velocity_field_prev(foot)
-        return {'main': fused_mse(u, u_target), 'bc': self._wall_loss(x.shape[0])}
+        main = fused_mse(u, u_target)
+        join()
+        return {'main': main, 'bc': bc}
 
     @BaseModel._training_loop
     def _solve_pressure(self):
         x = self._sample_in_training()
+        bc, join = self._fork(self._pressure_wall_loss, x.shape[0])
         with torch.no_grad():  # the reference detaches div u: no reverse jet, no saved streams
             div_u = divergence(self.velocity_field(x), x)
         lap_p = laplace(self.pressure_field(x), x)
         main = fused_mse(div_u, lap_p)  # mean((div u - lap p)^2), rho = 1
-        bxy, nb = self._boundary_bands(x.shape[0])  # one jet launch for both bands
-        gp = gradient(self.pressure_field(bxy), bxy)
-        return {'main': main, 'bc': wall_mse(gp, nb)}  # mean(dp/dx^2) + mean(dp/dy^2)
+        join()
+        return {'main': main, 'bc': bc}
 
     @BaseModel._training_loop
     def _projection(self):
         x = self._sample_in_training()
+        bc, join = self._fork(self._wall_loss, x.shape[0])
         with torch.no_grad():
             u_prev = self.velocity_field_prev(x).detach()
         with torch.no_grad():  # detached in the reference as well
             grad_p = gradient(self.pressure_field(x), x)
         u = self.velocity_field(x)
         # mean((u - (u_prev - grad_p))^2): r = 1*(u + 0) + (-1)*(u_prev + (-1)*grad_p)
-        return {'main': fused_mse(u, None, u_prev, grad_p, gamma=-1.0, delta=-1.0), 'bc': self._wall_loss(x.shape[0])}
+        main = fused_mse(u, None, u_prev, grad_p, gamma=-1.0, delta=-1.0)
+        join()
+        return {'main': main, 'bc': bc}
 
     # ---- output (host side; PNG figures are out of scope) ---------------------
     def field_quantities(self, resolution):

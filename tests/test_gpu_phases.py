@@ -67,9 +67,11 @@ def _cfg(pde, **kw):
     return make_config(pde, proj_dir="/tmp/insr_test", **kw)
 
 
-def test_fluid_phases(ph):
+@pytest.mark.parametrize("band_stream", [False, True])
+def test_fluid_phases(ph, band_stream):
     from pde.fluid import Fluid2DModel
-    cfg = _cfg("fluid", num_hidden_layers=4, hidden_features=128, sample_resolution=32, dt=0.05)
+    cfg = _cfg("fluid", num_hidden_layers=4, hidden_features=128, sample_resolution=32, dt=0.05,
+               insr_band_stream=band_stream)
     model = Fluid2DModel(cfg)
     T = lambda k: torch.from_numpy(ph[k]).cuda()  # noqa: E731
     nets = {"vel": model.velocity_field, "vel_prev": model.velocity_field_prev, "pres": model.pressure_field}
@@ -256,14 +258,16 @@ def test_elasticity3d_phase(ph):
                  g3["el3d/_solve_deformation/grad_f"])
 
 
-def test_training_loop_graph_matches_eager(ph):
-    """insr_graph=True (hipGraph replay) gives the same trajectory as eager execution."""
+@pytest.mark.parametrize("band_stream", [False, True])
+def test_training_loop_graph_matches_eager(ph, band_stream):
+    """insr_graph=True (hipGraph replay) gives the same trajectory as eager execution (also
+    with the boundary-band jets on a side stream: the capture must join it)."""
     from pde.fluid import Fluid2DModel
     res = {}
     for graph in (False, True):
         torch.manual_seed(0)
         cfg = _cfg("fluid", num_hidden_layers=4, hidden_features=128, sample_resolution=32, max_n_iters=6,
-                   insr_graph=graph, insr_sync_every=3)
+                   insr_graph=graph, insr_sync_every=3, insr_band_stream=band_stream)
         model = Fluid2DModel(cfg)
         set_flat(model.velocity_field, ph["fluid/vel/params0"])
         set_flat(model.velocity_field_prev, ph["fluid/vel_prev/params0"])
@@ -276,6 +280,8 @@ def test_training_loop_graph_matches_eager(ph):
         model._boundary_pair = lambda n: (static_bx.clone().requires_grad_(True), static_by.clone().requires_grad_(True))
         model.timestep = 1
         model._solve_pressure()
+        if graph:  # the capture succeeded (a failed capture silently stays eager)
+            assert getattr(model, "_insr_capture_error", None) is None
         res[graph] = (flat(model.pressure_field), float(model.optimizer.state[0]),
                       float(model.optimizer.state[1]))
     assert res[True][2] == res[False][2] == 6.0
