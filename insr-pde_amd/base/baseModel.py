@@ -134,34 +134,46 @@ class BaseModel(ABC):
         return d.get_world_size() if (d.is_available() and d.is_initialized()) else 1
 
     def _dp_sync(self, loss_dict):
-        """All-reduce gradients (+ losses) across ranks: one RCCL call per tensor group."""
+        """All-reduce gradients and losses across ranks: ONE RCCL call per iteration over the
+        model's gradient arena -- every trainable network's flat .grad is a view into it (bound
+        on the first call), followed by one slot per loss -- so there is no concatenation and
+        no copy-back.  A network no gradient reached this iteration contributes zeros (one
+        memset) and stays untouched for Adam (torch skips params whose .grad is None)."""
         world = self._dp_world()
         if world == 1:
             return loss_dict
         d = torch.distributed
-        if torch.device(self.device).type == "cuda" and torch.cuda.is_available():
-            cur = torch.cuda.current_stream(self.device)
-            for net in self._trainable_networks.values():
+        nets = list(self._trainable_networks.values())
+        keys = list(loss_dict.keys())
+        dev = nets[0].flat_params().device
+        if torch.device(dev).type == "cuda" and torch.cuda.is_available():
+            cur = torch.cuda.current_stream(dev)
+            for net in nets:
                 if hasattr(net, "grad_read_sync"):
                     net.grad_read_sync(cur)
-        grads = [net.flat_grad_buffer() for net in self._trainable_networks.values()]
-        flat = torch.cat(grads) if len(grads) > 1 else grads[0]
-        keys = list(loss_dict.keys())
-        losses = torch.stack([torch.as_tensor(loss_dict[k], device=flat.device).detach().float().reshape(())
-                              for k in keys])
-        buf = torch.cat([flat, losses])
-        d.all_reduce(buf, op=d.ReduceOp.SUM)
-        if self._dp_loss_reduction == 'mean':
-            buf.div_(world)
-        if len(grads) > 1:
+        sizes = [net.param_count for net in nets]
+        total = sum(sizes)
+        arena = self.__dict__.get("_insr_dp_arena")
+        if arena is None or arena.numel() < total + len(keys) or arena.device != dev:
+            arena = torch.zeros(total + max(len(keys), 8), device=dev, dtype=torch.float32)
+            self._insr_dp_arena = arena
             off = 0
-            for g in grads:
-                g.copy_(buf[off:off + g.numel()])
-                off += g.numel()
-        else:
-            grads[0].copy_(buf[:grads[0].numel()])
-        red = buf[flat.numel():]
-        return {k: red[i] for i, k in enumerate(keys)}
+            for net, n in zip(nets, sizes):
+                net.bind_flat_grad(arena[off:off + n])
+                off += n
+        touched = [net.grad_touched() for net in nets]
+        off = 0
+        for net, n, t in zip(nets, sizes, touched):
+            if not t:
+                arena[off:off + n].zero_()
+            off += n
+        tail = arena[total:total + len(keys)]
+        torch.stack([torch.as_tensor(loss_dict[k], device=dev).detach().float().reshape(()) for k in keys], out=tail)
+        red = arena[:total + len(keys)]
+        d.all_reduce(red, op=d.ReduceOp.SUM)
+        if self._dp_loss_reduction == 'mean':
+            red.div_(world)
+        return {k: tail[i] for i, k in enumerate(keys)}
 
     def _update_network(self, loss_dict):
         """update network by back propagation (base/baseModel.py:73-81).  backward of

@@ -186,6 +186,21 @@ class MLP(nn.Module):
         g, _ = self._attach_grad_views(fold_foreign=True)
         return g, 1
 
+    def bind_flat_grad(self, buf):
+        """Make `buf` (a 1-D fp32 tensor of param_count elements, e.g. a slice of a model's
+        data-parallel gradient arena) this network's flat .grad storage; the current
+        gradient values move into it."""
+        self.ensure_packed()
+        if buf.numel() != self._flat.numel() or buf.dtype != self._flat.dtype or buf.device != self._flat.device:
+            raise ValueError("bind_flat_grad: buffer does not match the flat parameters")
+        live = any(p.grad is not None for p in self.parameters())
+        if live:
+            old, _ = self._attach_grad_views(fold_foreign=True)
+            buf.copy_(old)
+        self._flat_grad = buf
+        if live:
+            self._attach_grad_views(fold_foreign=False)
+
     # ---- cross-stream ordering of the flat-gradient writes ---------------------------
     # A model may run some jets on a side stream (fluid boundary bands); autograd then runs
     # their backward on that stream too.  The HIP backward writes the flat .grad directly
