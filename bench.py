@@ -55,6 +55,7 @@ def parse():
     ap.add_argument("--scaling", choices=["strong", "weak"], default="weak")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--band-stream", action="store_true", help="fluid: boundary-band jets on a side stream")
+    ap.add_argument("--nograd-stream", action="store_true", help="fluid: no-grad jets on a side stream")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
@@ -114,7 +115,7 @@ def build_model(args, world, rank):
     cfg = baseline_config(args.config, sample_resolution=res, insr_graph=not args.no_graph,
                           insr_sync_every=10 ** 9, insr_progress=False, early_stop=False,
                           proj_dir="/tmp/insr_bench", max_n_iters=10 ** 9,
-                          insr_band_stream=args.band_stream)
+                          insr_band_stream=args.band_stream, insr_nograd_stream=args.nograd_stream)
     n_global = interior_points(cfg, wl)
     if wl["pde"] in ("fluid", "advection"):
         # strong: the global batch is split over ranks; weak: every rank keeps the full batch

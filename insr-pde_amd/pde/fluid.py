@@ -109,11 +109,11 @@ class Fluid2DModel(BaseModel):
         gp = gradient(self.pressure_field(bxy), bxy)
         return wall_mse(gp, nb)
 
-    def _fork(self, fn, *args):
+    def _fork(self, flag, fn, *args):
         """Run fn(*args) on the model's side stream (forked from the current stream) when
-        cfg.insr_band_stream (default off); returns (result, join) -- call join() before
-        the result is combined with main-stream work."""
-        if not getattr(self.cfg, "insr_band_stream", False) or torch.device(self.device).type != "cuda":
+        cfg.<flag> is set; returns (result, join) -- call join() before the result (a tensor
+        or a tuple of tensors) meets main-stream work."""
+        if not getattr(self.cfg, flag, False) or torch.device(self.device).type != "cuda":
             return fn(*args), (lambda: None)
         main = torch.cuda.current_stream(self.device)
         side = self.__dict__.get("_insr_side")
@@ -125,46 +125,61 @@ class Fluid2DModel(BaseModel):
 
         def join():
             main.wait_stream(side)
-            out.record_stream(main)
+            for t in (out if isinstance(out, tuple) else (out,)):
+                t.record_stream(main)
         return out, join
+
+    # no-grad parts of the phases (frozen previous field, detached operators): with
+    # cfg.insr_nograd_stream they run on the side stream, concurrently with the trainable
+    # forward jet on the phase's stream (they have no backward, so no .grad ordering).
+    # Off by default: measured 46.3 vs 48.0 M pts/s (the concurrent jets contend for the
+    # same CUs; a value-jet block fills half a CU, but co-scheduling did not pay).
+    def _advect_target(self, x):
+        with torch.no_grad():
+            u_prev = self.velocity_field_prev(x).detach()
+            foot = torch.add(x, u_prev, alpha=-self.cfg.dt).clamp_(-1.0, 1.0)
+            return self.velocity_field_prev(foot)
+
+    def _velocity_divergence(self, x):
+        with torch.no_grad():  # the reference detaches div u: no reverse jet, no saved streams
+            return divergence(self.velocity_field(x), x)
+
+    def _projection_target(self, x):
+        with torch.no_grad():  # both detached in the reference as well
+            return self.velocity_field_prev(x).detach(), gradient(self.pressure_field(x), x)
 
     @BaseModel._training_loop
     def _advect_velocity(self):
         x = self._sample_in_training()
-        bc, join = self._fork(self._wall_loss, x.shape[0])
-        with torch.no_grad():
-            u_prev = self.velocity_field_prev(x).detach()
+        bc, join_bc = self._fork("insr_band_stream", self._wall_loss, x.shape[0])
+        u_target, join_t = self._fork("insr_nograd_stream", self._advect_target, x)
         u = self.velocity_field(x)
-        with torch.no_grad():
-            foot = torch.add(x, u_prev, alpha=-self.cfg.dt).clamp_(-1.0, 1.0)
-            u_target = self.velocity_field_prev(foot)
+        join_t()
         main = fused_mse(u, u_target)
-        join()
+        join_bc()
         return {'main': main, 'bc': bc}
 
     @BaseModel._training_loop
     def _solve_pressure(self):
         x = self._sample_in_training()
-        bc, join = self._fork(self._pressure_wall_loss, x.shape[0])
-        with torch.no_grad():  # the reference detaches div u: no reverse jet, no saved streams
-            div_u = divergence(self.velocity_field(x), x)
+        bc, join_bc = self._fork("insr_band_stream", self._pressure_wall_loss, x.shape[0])
+        div_u, join_d = self._fork("insr_nograd_stream", self._velocity_divergence, x)
         lap_p = laplace(self.pressure_field(x), x)
+        join_d()
         main = fused_mse(div_u, lap_p)  # mean((div u - lap p)^2), rho = 1
-        join()
+        join_bc()
         return {'main': main, 'bc': bc}
 
     @BaseModel._training_loop
     def _projection(self):
         x = self._sample_in_training()
-        bc, join = self._fork(self._wall_loss, x.shape[0])
-        with torch.no_grad():
-            u_prev = self.velocity_field_prev(x).detach()
-        with torch.no_grad():  # detached in the reference as well
-            grad_p = gradient(self.pressure_field(x), x)
+        bc, join_bc = self._fork("insr_band_stream", self._wall_loss, x.shape[0])
+        (u_prev, grad_p), join_t = self._fork("insr_nograd_stream", self._projection_target, x)
         u = self.velocity_field(x)
+        join_t()
         # mean((u - (u_prev - grad_p))^2): r = 1*(u + 0) + (-1)*(u_prev + (-1)*grad_p)
         main = fused_mse(u, None, u_prev, grad_p, gamma=-1.0, delta=-1.0)
-        join()
+        join_bc()
         return {'main': main, 'bc': bc}
 
     # ---- output (host side; PNG figures are out of scope) ---------------------

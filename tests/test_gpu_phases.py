@@ -71,7 +71,7 @@ def _cfg(pde, **kw):
 def test_fluid_phases(ph, band_stream):
     from pde.fluid import Fluid2DModel
     cfg = _cfg("fluid", num_hidden_layers=4, hidden_features=128, sample_resolution=32, dt=0.05,
-               insr_band_stream=band_stream)
+               insr_band_stream=band_stream, insr_nograd_stream=band_stream)
     model = Fluid2DModel(cfg)
     T = lambda k: torch.from_numpy(ph[k]).cuda()  # noqa: E731
     nets = {"vel": model.velocity_field, "vel_prev": model.velocity_field_prev, "pres": model.pressure_field}
@@ -267,7 +267,8 @@ def test_training_loop_graph_matches_eager(ph, band_stream):
     for graph in (False, True):
         torch.manual_seed(0)
         cfg = _cfg("fluid", num_hidden_layers=4, hidden_features=128, sample_resolution=32, max_n_iters=6,
-                   insr_graph=graph, insr_sync_every=3, insr_band_stream=band_stream)
+                   insr_graph=graph, insr_sync_every=3, insr_band_stream=band_stream,
+                   insr_nograd_stream=band_stream)
         model = Fluid2DModel(cfg)
         set_flat(model.velocity_field, ph["fluid/vel/params0"])
         set_flat(model.velocity_field_prev, ph["fluid/vel_prev/params0"])
