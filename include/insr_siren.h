@@ -48,6 +48,8 @@ extern "C" {
 
 #define INSR_EINVAL   (-1) /* unsupported shape / mode / null pointer */
 #define INSR_EWIDTH   (-2) /* hidden width not in the compiled set      */
+#define INSR_ENOCOMM  (-3) /* RCCL (librccl.so.1) could not be loaded   */
+#define INSR_ECOMM_BASE 1000 /* + ncclResult_t of a failed RCCL call     */
 
 /* Library version (major*10000 + minor*100 + patch). */
 int insr_version(void);
@@ -246,6 +248,23 @@ int insr_svd_energy_fwd(const float* J, long n, int d, float ratio_arap, float r
                         float* work, void* stream);
 int insr_svd_energy_bwd(const float* J, long n, int d, float ratio_arap, float ratio_volume, const float* gout,
                         float* gJ, void* stream);
+
+/*
+ * Data-parallel collective (one process per GPU): the single sum all-reduce per optimiser
+ * step of the flat gradients (+ loss scalars) -- what BaseModel._dp_sync does through
+ * torch.distributed (backend "nccl" = RCCL), for hosts without PyTorch.  RCCL is loaded at
+ * run time (the copy PyTorch already loaded, if any).
+ *   rank 0: insr_comm_unique_id(id) -> share the insr_comm_id_bytes() bytes -> every rank:
+ *   insr_comm_init(&comm, rank, world, id); per step insr_comm_allreduce_sum(comm, buf, n,
+ *   stream) (in place, asynchronous on `stream`); insr_comm_destroy(comm) at the end.
+ * Replaces: the gradient averaging a DDP port of base/baseModel.py:73-81 would add.
+ */
+int insr_comm_available(void);
+long insr_comm_id_bytes(void);
+int insr_comm_unique_id(void* id_out);
+int insr_comm_init(void** comm, int rank, int world, const void* id);
+int insr_comm_allreduce_sum(void* comm, float* buf, long count, void* stream);
+int insr_comm_destroy(void* comm);
 
 #ifdef __cplusplus
 }

@@ -39,6 +39,12 @@ SIGNATURES = {
     "insr_jet_bwd_work_bytes": (_L, [_L, _I, _I, _I, _I, _I]),
     "insr_jet_bwd_is_wide": (_I, [_L, _I, _I, _I]),
     "insr_jet_set_wide_min_width": (_I, [_I]),
+    "insr_comm_available": (_I, []),
+    "insr_comm_id_bytes": (_L, []),
+    "insr_comm_unique_id": (_I, [_P]),
+    "insr_comm_init": (_I, [_P, _I, _I, _P]),
+    "insr_comm_allreduce_sum": (_I, [_P, _P, _L, _P]),
+    "insr_comm_destroy": (_I, [_P]),
     "insr_jet_split_threshold": (_I, []),
     "insr_jet_set_split_threshold": (_I, [_I]),
     "insr_jet_get_split_thresholds": (None, [_P, _P, _P]),

@@ -82,3 +82,10 @@ def test_invalid_arguments_rejected_without_launch(lib):
     assert lib.insr_siren_jet_fwd(None, 10, 2, 1, 4, 100, 0, None, None, None, None, None, None) == -1
     assert lib.insr_siren_jet_fwd(None, 0, 2, 1, 4, 128, 0, None, None, None, None, None, None) == 0
     assert lib.insr_adam_step(None, None, None, None, 10, None, 0.9, 0.999, 1e-8, None) == -1
+
+
+def test_comm_library_resolves(lib):
+    # RCCL ships with the ROCm image (and with PyTorch-ROCm): the C-ABI collective can load it
+    assert lib.insr_comm_available() == 1
+    assert lib.insr_comm_id_bytes() == 128
+    assert lib.insr_comm_init(None, 0, 1, None) == -1  # INSR_EINVAL, no RCCL call made
