@@ -84,8 +84,9 @@ int insr_siren_jet_fwd(const float* x, long n_points, int d_in, int d_out, int n
  * Backward of the jet to the parameters.  Adjoints (any may be NULL = zero):
  *   gy (n, d_out), gdy (n, d_out, d_in), glap (n, d_out).
  *   partial  insr_jet_partial_bytes: one fp32 parameter-gradient row per block
- *            (insr_jet_partial_blocks(n, d_in, width, mode) rows x param_count).
- * Sum the rows with insr_reduce_partials into the network's flat .grad.
+ *            (insr_jet_partial_blocks(n, d_in, width, mode) rows of
+ *            insr_jet_partial_stride(...) floats; the first param_count are used).
+ * Sum the rows with insr_reduce_partials_strided into the network's flat .grad.
  * The gradient w.r.t. x is not produced (the reference never reads it).
  * Replaces: the autograd backward of loss.backward() (base/baseModel.py:77).
  */
@@ -166,6 +167,13 @@ void insr_jet_get_precision(int* fwd, int* bwd);
 /* grad[i] = (accumulate ? grad[i] : 0) + sum_b partial[b * count + i], fixed order. */
 int insr_reduce_partials(const float* partial, int n_blocks, long count, float* grad,
                          int accumulate, void* stream);
+/* Row stride (floats) of insr_siren_jet_bwd's partial rows: param_count rounded up to a
+ * multiple of 4 (16-B aligned rows; the padding is never read). */
+long insr_jet_partial_stride(int d_in, int d_out, int num_hidden, int width);
+/* grad[i] = (accumulate ? grad[i] : 0) + sum_b partial[b * stride + i], i < count, fixed
+ * order; 16-B loads when stride % 4 == 0 and partial is 16-B aligned. */
+int insr_reduce_partials_strided(const float* partial, int n_blocks, long count, long stride,
+                                 float* grad, int accumulate, void* stream);
 
 /*
  * Device-resident optimiser state (INSR_OPT_NFLOATS floats, caller-allocated):

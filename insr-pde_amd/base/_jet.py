@@ -140,9 +140,10 @@ class _SirenJet(torch.autograd.Function):
                                         nat.ptr(act), nat.ptr(gy), nat.ptr(gdy), nat.ptr(glap), nat.ptr(part), st)
         nat.check(rc, "insr_siren_jet_bwd")
         with _timed("reduce", mode, n, W, (din, dout, L)):
-            rc = lib.insr_reduce_partials(nat.ptr(part), lib.insr_jet_partial_blocks(n, din, W, mode), gflat.numel(),
-                                          nat.ptr(gflat), accumulate, st)
-        nat.check(rc, "insr_reduce_partials")
+            rc = lib.insr_reduce_partials_strided(nat.ptr(part), lib.insr_jet_partial_blocks(n, din, W, mode),
+                                                  gflat.numel(), lib.insr_jet_partial_stride(din, dout, L, W),
+                                                  nat.ptr(gflat), accumulate, st)
+        nat.check(rc, "insr_reduce_partials_strided")
         mlp.grad_write_end(cur)
         return none
 

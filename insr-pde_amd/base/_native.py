@@ -61,6 +61,8 @@ SIGNATURES = {
     "insr_jet_get_precision": (None, [_P, _P]),
     "insr_jet_get_split_tiles": (None, [_P, _P, _P]),
     "insr_reduce_partials": (_I, [_P, _I, _L, _P, _I, _P]),
+    "insr_reduce_partials_strided": (_I, [_P, _I, _L, _L, _P, _I, _P]),
+    "insr_jet_partial_stride": (_L, [_I, _I, _I, _I]),
     "insr_adam_prepare": (_I, [_P, _F, _F, _P]),
     "insr_plateau_step": (_I, [_P, _P, _I, _I, _P]),
     "insr_adam_step_multi": (_I, [_I, _P, _P, _P, _P, _P, _P, _F, _F, _F, _I, _P]),

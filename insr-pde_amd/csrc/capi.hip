@@ -118,10 +118,13 @@ int split_tiles(int bwd, int NT, int S, long n) {
   int T = NT > 8 ? ((x6 && !bwd) ? (S == 1 ? 4 : (S == 2 ? 2 : 1)) : 1) : ((bwd && S > 1) ? 2 : 4);
   while (T > 1 && (size_t)T * plane > 163840) T >>= 1;
   const int forced = g_tiles[bwd ? 1 : 0];
-  if (forced > 0) {
+  if (forced > 0) {  // the largest feasible T not above the forced one
     while (T > forced) T >>= 1;
     return T;
   }
+  // x6 forward of 4-stream jets (Laplacian, 3-d gradient) at W <= 128: T = 1 measured faster
+  // than the LDS-capped T = 2 (16384 points: 66.6 vs 71.5 us, kbench s32)
+  if (x6 && !bwd && S >= 4 && NT <= 8) T = 1;
   const long tiles = (n + 15) / 16;
   while (T > 1 && (tiles + T - 1) / T < g_tiles[2]) T >>= 1;
   return T;
@@ -158,6 +161,44 @@ __global__ __launch_bounds__(64 * kRedWaves) void reduce_partials_kernel(const f
 #pragma unroll
     for (int k = 0; k < kRedWaves; ++k) t += red[k][lane];
     grad[i] = s + t;
+  }
+}
+
+// Partial rows padded to a multiple of 4 floats (insr_jet_partial_stride): 16-B aligned
+// rows, so the reduction streams them with 16-B loads (1 KiB per wave-instruction) and
+// 8 rows in flight per thread.  Fixed summation order as reduce_partials_kernel.
+constexpr int kRed4Waves = 8, kRed4Unroll = 8;
+__global__ __launch_bounds__(64 * kRed4Waves) void reduce_partials4_kernel(const float* __restrict__ part, int nb,
+                                                                            long count, long stride,
+                                                                            float* __restrict__ grad, int accumulate) {
+  __shared__ floatx4 red[kRed4Waves][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const long q = (long)blockIdx.x * 64 + lane;  // column quad
+  floatx4 acc = floatx4{0.f, 0.f, 0.f, 0.f};
+  if (4 * q < count) {
+    const floatx4* col = reinterpret_cast<const floatx4*>(part) + q;
+    const long rs = stride / 4;
+    int b = w;
+    for (; b + (kRed4Unroll - 1) * kRed4Waves < nb; b += kRed4Unroll * kRed4Waves) {
+      floatx4 v[kRed4Unroll];
+#pragma unroll
+      for (int u = 0; u < kRed4Unroll; ++u) v[u] = col[(long)(b + u * kRed4Waves) * rs];
+#pragma unroll
+      for (int u = 0; u < kRed4Unroll; ++u) acc += v[u];
+    }
+    for (; b < nb; b += kRed4Waves) acc += col[(long)b * rs];
+  }
+  red[w][lane] = acc;
+  __syncthreads();
+  if (w == 0 && 4 * q < count) {
+    floatx4 t = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < kRed4Waves; ++k) t += red[k][lane];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const long i = 4 * q + r;
+      if (i < count) grad[i] = accumulate ? grad[i] + t[r] : t[r];
+    }
   }
 }
 
@@ -261,6 +302,10 @@ long insr_siren_param_count(int din, int dout, int L, int W) {
   return (long)W * din + W + (long)L * ((long)W * W + W) + (long)dout * W + dout;
 }
 
+long insr_jet_partial_stride(int din, int dout, int L, int W) {
+  return (insr_siren_param_count(din, dout, L, W) + 3) & ~3L;  // 16-B aligned rows
+}
+
 int insr_siren_supported(int din, int dout, int L, int W, int mode) { return shape_ok(din, dout, L, W, mode) ? 1 : 0; }
 
 long insr_jet_act_bytes(long n, int din, int L, int W, int mode) {
@@ -273,7 +318,7 @@ long insr_jet_act_bytes(long n, int din, int L, int W, int mode) {
 long insr_jet_partial_bytes(long n, int din, int dout, int L, int W, int mode) {
   const int nb = insr_jet_partial_blocks(n, din, W, mode);
   if (nb < 0) return nb;
-  return (long)nb * insr_siren_param_count(din, dout, L, W) * (long)sizeof(float);
+  return (long)nb * insr_jet_partial_stride(din, dout, L, W) * (long)sizeof(float);
 }
 
 int insr_siren_jet_fwd(const float* x, long n, int din, int dout, int L, int W, int mode, const float* params,
@@ -301,7 +346,7 @@ int insr_siren_jet_bwd(const float* x, long n, int din, int dout, int L, int W, 
   if (!shape_ok(din, dout, L, W, mode) || n < 0 || n > 0x7fffffffL) return INSR_EINVAL;
   if (n == 0) return 0;
   if (!x || !params || !act || !partial) return INSR_EINVAL;
-  const long P = insr_siren_param_count(din, dout, L, W);
+  const long P = insr_jet_partial_stride(din, dout, L, W);  // row stride of the partial rows
   const int S = streams_for(din, mode);
   const int NT = nt_for(W);
   if (use_split_bwd(n, S, NT) && use_x6(1, NT))
@@ -345,8 +390,9 @@ int insr_siren_jet_bwd_grad(const float* x, long n, int din, int dout, int L, in
                              accumulate, (hipStream_t)stream);
   int rc = insr_siren_jet_bwd(x, n, din, dout, L, W, mode, params, act, gy, gdy, glap, work, stream);
   if (rc) return rc;
-  return insr_reduce_partials(work, insr_jet_partial_blocks(n, din, W, mode), insr_siren_param_count(din, dout, L, W),
-                              grad, accumulate, stream);
+  return insr_reduce_partials_strided(work, insr_jet_partial_blocks(n, din, W, mode),
+                                      insr_siren_param_count(din, dout, L, W), insr_jet_partial_stride(din, dout, L, W),
+                                      grad, accumulate, stream);
 }
 
 int insr_jet_partial_blocks(long n, int din, int W, int mode) {
@@ -412,6 +458,20 @@ void insr_jet_set_split_thresholds(int fwd, int bwd, int bwd_value) {
   g_thr[0] = fwd < 0 ? 0 : fwd;
   g_thr[1] = bwd < 0 ? 0 : bwd;
   g_thr[2] = bwd_value < 0 ? 0 : bwd_value;
+}
+
+int insr_reduce_partials_strided(const float* partial, int nb, long count, long stride, float* grad, int accumulate,
+                                 void* stream) {
+  if (!partial || !grad || nb < 0 || count < 0 || stride < count) return INSR_EINVAL;
+  if (count == 0) return 0;
+  if (stride % 4 == 0 && ((uintptr_t)partial & 15) == 0) {
+    const long blocks = (count + 255) / 256;
+    hipLaunchKernelGGL(reduce_partials4_kernel, dim3((unsigned)blocks), dim3(64 * kRed4Waves), 0, (hipStream_t)stream,
+                       partial, nb, count, stride, grad, accumulate);
+    return (int)hipGetLastError();
+  }
+  if (stride != count) return INSR_EINVAL;
+  return insr_reduce_partials(partial, nb, count, grad, accumulate, stream);
 }
 
 int insr_reduce_partials(const float* partial, int nb, long count, float* grad, int accumulate, void* stream) {

@@ -50,7 +50,8 @@ def test_host_queries(lib):
     saved, saved_tiles = nat.get_split_thresholds(), nat.get_split_tiles()
     try:
         old = lib.insr_jet_set_split_threshold(0)          # wave-tile kernels: one row per 64 points
-        assert lib.insr_jet_partial_bytes(65, 2, 1, 4, 128, 2) == 2 * 66561 * 4
+        assert lib.insr_jet_partial_bytes(65, 2, 1, 4, 128, 2) == 2 * 66564 * 4  # rows padded to 4 floats
+        assert lib.insr_jet_partial_stride(2, 1, 4, 128) == 66564 and lib.insr_jet_partial_stride(2, 2, 4, 128) == 66692
         assert lib.insr_jet_partial_blocks(65, 2, 128, 2) == 2 and lib.insr_jet_partial_blocks(0, 2, 128, 2) == 0
         assert lib.insr_jet_split_tiles(65, 2, 128, 2, 1) == 0
         # width 256 has no wave-tile kernel: always tile-split, one tile per block

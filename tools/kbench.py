@@ -112,7 +112,9 @@ def main():
                                                               nat.ptr(work), nat.ptr(g), 0, st), "bwd_grad")
 
                     def red():
-                        nat.check(lib.insr_reduce_partials(nat.ptr(part), nb, P, nat.ptr(g), 0, st), "reduce")
+                        nat.check(lib.insr_reduce_partials_strided(nat.ptr(part), nb, P,
+                                                                   lib.insr_jet_partial_stride(din, dout, L, W),
+                                                                   nat.ptr(g), 0, st), "reduce")
 
                     tf = time_it(fwd, args.reps)
                     fwd()
