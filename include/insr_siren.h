@@ -171,7 +171,8 @@ int insr_reduce_partials(const float* partial, int n_blocks, long count, float* 
  * multiple of 4 (16-B aligned rows; the padding is never read). */
 long insr_jet_partial_stride(int d_in, int d_out, int num_hidden, int width);
 /* grad[i] = (accumulate ? grad[i] : 0) + sum_b partial[b * stride + i], i < count, fixed
- * order; 16-B loads when stride % 4 == 0 and partial is 16-B aligned. */
+ * order; 16-B loads when stride % 4 == 0 and partial is 16-B aligned.  Many rows are
+ * summed in two levels IN PLACE: `partial` is scratch (its rows are overwritten). */
 int insr_reduce_partials_strided(const float* partial, int n_blocks, long count, long stride,
                                  float* grad, int accumulate, void* stream);
 

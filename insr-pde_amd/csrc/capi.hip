@@ -202,6 +202,40 @@ __global__ __launch_bounds__(64 * kRed4Waves) void reduce_partials4_kernel(const
   }
 }
 
+// First level of a two-level reduction for many rows: block (x, y) sums rows
+// [y R, (y + 1) R) of its 256 columns and writes the sum into row y R (in place: those
+// rows are read only by this block, before the write); the second level is
+// reduce_partials4_kernel over the slice rows (row stride R * stride).
+__global__ __launch_bounds__(64 * kRed4Waves) void reduce_slices4_kernel(float* __restrict__ part, int nb, int R,
+                                                                          long count, long stride) {
+  __shared__ floatx4 red[kRed4Waves][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const long q = (long)blockIdx.x * 64 + lane;
+  const int b0 = blockIdx.y * R, b1 = min(nb, b0 + R);
+  floatx4 acc = floatx4{0.f, 0.f, 0.f, 0.f};
+  floatx4* col = reinterpret_cast<floatx4*>(part) + q;
+  const long rs = stride / 4;
+  if (4 * q < count) {
+    int b = b0 + w;
+    for (; b + (kRed4Unroll - 1) * kRed4Waves < b1; b += kRed4Unroll * kRed4Waves) {
+      floatx4 v[kRed4Unroll];
+#pragma unroll
+      for (int u = 0; u < kRed4Unroll; ++u) v[u] = col[(long)(b + u * kRed4Waves) * rs];
+#pragma unroll
+      for (int u = 0; u < kRed4Unroll; ++u) acc += v[u];
+    }
+    for (; b < b1; b += kRed4Waves) acc += col[(long)b * rs];
+  }
+  red[w][lane] = acc;
+  __syncthreads();
+  if (w == 0 && 4 * q < count && b0 < nb) {
+    floatx4 t = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < kRed4Waves; ++k) t += red[k][lane];
+    col[(long)b0 * rs] = t;  // 16-B store; the row's padding columns are never summed
+  }
+}
+
 __global__ void adam_prepare_kernel(float* st, float b1, float b2) {
   // legacy explicit prepare: t += 1 and refresh the bias-corrected scalars
   if (threadIdx.x == 0 && blockIdx.x == 0) {
@@ -466,6 +500,18 @@ int insr_reduce_partials_strided(const float* partial, int nb, long count, long 
   if (count == 0) return 0;
   if (stride % 4 == 0 && ((uintptr_t)partial & 15) == 0) {
     const long blocks = (count + 255) / 256;
+    // many rows: two levels, so ~4 blocks per CU stream rows instead of ~1 (and no grid
+    // that overshoots 256 CUs by a few blocks)
+    int slices = 1;
+    while (slices < 16 && nb / (2 * slices) >= 64 && blocks * slices < 1024) slices *= 2;
+    if (slices > 1) {
+      const int R = (nb + slices - 1) / slices;
+      hipLaunchKernelGGL(reduce_slices4_kernel, dim3((unsigned)blocks, slices), dim3(64 * kRed4Waves), 0,
+                         (hipStream_t)stream, const_cast<float*>(partial), nb, R, count, stride);
+      hipLaunchKernelGGL(reduce_partials4_kernel, dim3((unsigned)blocks), dim3(64 * kRed4Waves), 0,
+                         (hipStream_t)stream, partial, (nb + R - 1) / R, count, stride * R, grad, accumulate);
+      return (int)hipGetLastError();
+    }
     hipLaunchKernelGGL(reduce_partials4_kernel, dim3((unsigned)blocks), dim3(64 * kRed4Waves), 0, (hipStream_t)stream,
                        partial, nb, count, stride, grad, accumulate);
     return (int)hipGetLastError();
