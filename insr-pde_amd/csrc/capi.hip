@@ -1,6 +1,7 @@
 // capi.hip -- the C ABI of libinsr_hip.so (include/insr_siren.h): argument checks,
 // kernel-variant selection, the partial reducer and the device-resident optimiser.
 #include <cstdlib>
+#include <map>
 
 #include "jet_common.hpp"
 
@@ -103,7 +104,37 @@ bool use_wide(long n, int S, int NT, bool lap) {
   return NT == 8 && lap && n >= 32768 && g_wide_min <= 256;  // Laplacian jets at width 128
 }
 
-int split_tiles(int bwd, int NT, int S, long n) {
+static int cu_count() {
+  static int c = -1;
+  if (c < 0) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c <= 0) c = 256;
+  }
+  return c;
+}
+
+// resident blocks per CU of a tile-split kernel instantiation (launchers answer N < 0)
+static int occupancy(int bwd, bool x6, int NT, int S, bool lap, int T) {
+  static std::map<int, int> cache;
+  const int key = (((((bwd * 2 + (x6 ? 1 : 0)) * 32 + NT) * 8 + S) * 2 + (lap ? 1 : 0)) * 8) + T;
+  auto it = cache.find(key);
+  if (it != cache.end()) return it->second;
+  int r;
+  if (bwd)
+    r = x6 ? dispatch_bwd_x6(NT, S, lap, T, nullptr, -1, 0, 0, 0, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
+                             0, nullptr)
+           : dispatch_bwd_split(NT, S, lap, T, nullptr, -1, 0, 0, 0, nullptr, nullptr, nullptr, nullptr, nullptr,
+                                nullptr, 0, nullptr);
+  else
+    r = x6 ? dispatch_fwd_x6(NT, S, lap, T, nullptr, -1, 0, 0, 0, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr)
+           : dispatch_fwd_split(NT, S, lap, T, nullptr, -1, 0, 0, 0, nullptr, nullptr, nullptr, nullptr, nullptr,
+                                nullptr);
+  cache[key] = r;
+  return r;
+}
+
+int split_tiles(int bwd, int NT, int S, long n, bool lap) {
   tiles_init();
   const bool x6 = use_x6(bwd, NT);
   // LDS per tile: fp32 planes [S][16][W+8] (+ backward h planes [S][16][W]); x6 forward:
@@ -127,6 +158,25 @@ int split_tiles(int bwd, int NT, int S, long n) {
   if (x6 && !bwd && S >= 4 && NT <= 8) T = 1;
   const long tiles = (n + 15) / 16;
   while (T > 1 && (tiles + T - 1) / T < g_tiles[2]) T >>= 1;
+  // occupancy-aware: a T whose last round of blocks (resident blocks per CU x CUs) is
+  // nearly empty loses to a smaller T that packs the CUs, e.g. the x6 gradient forward at
+  // 20,000 points: T = 4 -> 313 one-per-CU blocks = 2 rounds (97 us) vs T = 1 -> 1250
+  // two-per-CU blocks (68 us; profiles/r01/kbench_tiles_s44.jsonl).  Cost = rounds x T.
+  if (T > 1) {
+    const int cus = cu_count();
+    auto cost = [&](int t) -> double {
+      const int o = occupancy(bwd, x6, NT, S, lap, t);
+      if (o <= 0) return 1e30;
+      const long nb = (tiles + t - 1) / t, per = (long)o * cus;
+      return (double)((nb + per - 1) / per) * t;
+    };
+    const double c0 = cost(T);
+    for (int t = T >> 1; t >= 1; t >>= 1)
+      if (c0 > 2.2 * cost(t)) {
+        T = t;
+        break;
+      }
+  }
   return T;
 }
 
@@ -365,10 +415,10 @@ int insr_siren_jet_fwd(const float* x, long n, int din, int dout, int L, int W, 
   const int S = streams_for(din, mode);
   const int NT = nt_for(W);
   if (use_split_fwd(n, NT) && use_x6(0, NT))
-    return dispatch_fwd_x6(NT, S, mode == INSR_MODE_LAP, split_tiles(0, NT, S, n), x, (int)n, din, dout, L, params,
+    return dispatch_fwd_x6(NT, S, mode == INSR_MODE_LAP, split_tiles(0, NT, S, n, mode == INSR_MODE_LAP), x, (int)n, din, dout, L, params,
                            y, dy, lap, act, (hipStream_t)stream);
   if (use_split_fwd(n, NT))
-    return dispatch_fwd_split(NT, S, mode == INSR_MODE_LAP, split_tiles(0, NT, S, n), x, (int)n, din, dout, L,
+    return dispatch_fwd_split(NT, S, mode == INSR_MODE_LAP, split_tiles(0, NT, S, n, mode == INSR_MODE_LAP), x, (int)n, din, dout, L,
                               params, y, dy, lap, act, (hipStream_t)stream);
   return dispatch_fwd_wave(NT, S, mode == INSR_MODE_LAP, x, (int)n, din, dout, L, params, y, dy, lap, act,
                            (hipStream_t)stream);
@@ -384,10 +434,10 @@ int insr_siren_jet_bwd(const float* x, long n, int din, int dout, int L, int W, 
   const int S = streams_for(din, mode);
   const int NT = nt_for(W);
   if (use_split_bwd(n, S, NT) && use_x6(1, NT))
-    return dispatch_bwd_x6(NT, S, mode == INSR_MODE_LAP, split_tiles(1, NT, S, n), x, (int)n, din, dout, L, params,
+    return dispatch_bwd_x6(NT, S, mode == INSR_MODE_LAP, split_tiles(1, NT, S, n, mode == INSR_MODE_LAP), x, (int)n, din, dout, L, params,
                            act, gy, gdy, glap, partial, P, (hipStream_t)stream);
   if (use_split_bwd(n, S, NT))
-    return dispatch_bwd_split(NT, S, mode == INSR_MODE_LAP, split_tiles(1, NT, S, n), x, (int)n, din, dout, L,
+    return dispatch_bwd_split(NT, S, mode == INSR_MODE_LAP, split_tiles(1, NT, S, n, mode == INSR_MODE_LAP), x, (int)n, din, dout, L,
                               params, act, gy, gdy, glap, partial, P, (hipStream_t)stream);
   return dispatch_bwd_wave(NT, S, mode == INSR_MODE_LAP, x, (int)n, din, dout, L, params, act, gy, gdy, glap,
                            partial, P, (hipStream_t)stream);
@@ -434,7 +484,7 @@ int insr_jet_partial_blocks(long n, int din, int W, int mode) {
   if (S < 0 || NT < 0 || n < 0) return INSR_EINVAL;
   if (n == 0) return 0;
   if (!use_split_bwd(n, S, NT)) return (int)((n + kPts - 1) / kPts);
-  const int T = split_tiles(1, NT, S, n);
+  const int T = split_tiles(1, NT, S, n, mode == INSR_MODE_LAP);
   return (int)(((n + 15) / 16 + T - 1) / T);
 }
 
@@ -442,7 +492,7 @@ int insr_jet_split_tiles(long n, int din, int W, int mode, int backward) {
   const int S = streams_for(din, mode), NT = nt_for(W);
   if (S < 0 || NT < 0 || n < 0) return INSR_EINVAL;
   const bool split = backward ? use_split_bwd(n, S, NT) : use_split_fwd(n, NT);
-  return split ? split_tiles(backward ? 1 : 0, NT, S, n) : 0;
+  return split ? split_tiles(backward ? 1 : 0, NT, S, n, mode == INSR_MODE_LAP) : 0;
 }
 
 void insr_jet_set_split_tiles(int fwd_tiles, int bwd_tiles, int min_blocks) {

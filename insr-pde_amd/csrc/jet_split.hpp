@@ -567,6 +567,11 @@ int launch_fwd_split_t(const float* x, int N, int din, int dout, int L, const fl
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       attr_set = true;
     }
+    if (N < 0) {  // occupancy query (split_tiles): resident blocks per CU
+      int occ = 0;
+      (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)jet_fwd_split<NT, S, LAP, T>, SplitGeo<NT>::THREADS, lds);
+      return occ;
+    }
     hipLaunchKernelGGL((jet_fwd_split<NT, S, LAP, T>), dim3(nb), dim3(SplitGeo<NT>::THREADS), lds, st, x, N, din,
                        dout, L, prm, y, dy, lap, act);
     return (int)hipGetLastError();
@@ -586,6 +591,11 @@ int launch_bwd_split_t(const float* x, int N, int din, int dout, int L, const fl
       (void)hipFuncSetAttribute((const void*)jet_bwd_split<NT, S, LAP, T>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       attr_set = true;
+    }
+    if (N < 0) {  // occupancy query (split_tiles): resident blocks per CU
+      int occ = 0;
+      (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)jet_bwd_split<NT, S, LAP, T>, SplitGeo<NT>::THREADS, lds);
+      return occ;
     }
     hipLaunchKernelGGL((jet_bwd_split<NT, S, LAP, T>), dim3(nb), dim3(SplitGeo<NT>::THREADS), lds, st, x, N, din,
                        dout, L, prm, act, gy, gdy, glap, part, P);

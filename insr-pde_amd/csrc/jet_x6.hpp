@@ -297,6 +297,11 @@ int launch_fwd_x6_t(const float* x, int N, int din, int dout, int L, const float
                                 (int)lds);
       attr_set = true;
     }
+    if (N < 0) {  // occupancy query (split_tiles): resident blocks per CU
+      int occ = 0;
+      (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)jet_fwd_x6<NT, S, LAP, T>, X6Geo<NT>::THREADS, lds);
+      return occ;
+    }
     hipLaunchKernelGGL((jet_fwd_x6<NT, S, LAP, T>), dim3(nb), dim3(X6Geo<NT>::THREADS), lds, st, x, N, din, dout, L,
                        prm, y, dy, lap, act);
     return (int)hipGetLastError();
@@ -766,6 +771,11 @@ int launch_bwd_x6_t(const float* x, int N, int din, int dout, int L, const float
       (void)hipFuncSetAttribute((const void*)jet_bwd_x6<NT, S, LAP, T>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       attr_set = true;
+    }
+    if (N < 0) {  // occupancy query (split_tiles): resident blocks per CU
+      int occ = 0;
+      (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)jet_bwd_x6<NT, S, LAP, T>, X6Geo<NT>::THREADS, lds);
+      return occ;
     }
     hipLaunchKernelGGL((jet_bwd_x6<NT, S, LAP, T>), dim3(nb), dim3(X6Geo<NT>::THREADS), lds, st, x, N, din, dout,
                        L, prm, act, gy, gdy, glap, part, P);
