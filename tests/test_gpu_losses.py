@@ -132,3 +132,54 @@ def test_svd_energy_matches_torch_svd(B, d, kind, n):
     if kind == "degenerate":  # exactly repeated values: only the well-defined (non-repeated) blocks
         G, G64 = G[2 * n // 3:], G64[2 * n // 3:]
     assert rel(G / 2.0, G64) < 1e-4
+
+
+# ---- merged launches: losses over row ranges of one network output (base.merge_samples) ----
+@pytest.mark.parametrize("n_in,n_bc", [(1000, 40), (16384, 324), (5000, 0)])
+def test_offset_losses_match_slices(B, n_in, n_bc):
+    """fused_mse(count, a_row0) / wall_mse(row0) / svd_energy(count) on a merged (interior +
+    boundary) tensor == the torch expressions on the slices, and the gradient of the merged
+    tensor is the slices' gradients with zeros elsewhere."""
+    g = torch.Generator(device="cuda").manual_seed(n_in + n_bc)
+    rows = n_in + 2 * n_bc
+    u = torch.randn(rows, 2, device="cuda", generator=g).requires_grad_(True)
+    t = torch.randn(n_in, 2, device="cuda", generator=g)
+    ur = u.detach().clone().requires_grad_(True)
+    main = B.fused_mse(u, t, count=t.numel())
+    parts = [main]
+    main_r = torch.mean((ur[:n_in] - t) ** 2)
+    parts_r = [main_r]
+    if n_bc:
+        bc = B.wall_mse(u, n_bc, row0=n_in)
+        tail = B.fused_mse(u, count=2 * n_bc * 2, a_row0=n_in, reduction="sum")
+        bc_r = torch.mean(ur[n_in:n_in + n_bc, 0] ** 2) + torch.mean(ur[n_in + n_bc:, 1] ** 2)
+        tail_r = torch.sum(ur[n_in:] ** 2)
+        parts += [bc, tail]
+        parts_r += [bc_r, tail_r]
+    for a, b in zip(parts, parts_r):
+        assert rel(a, b) < 1e-5
+    sum(parts).backward()
+    sum(parts_r).backward()
+    assert rel(u.grad, ur.grad) < 1e-6
+
+
+def test_svd_energy_count(B):
+    g = torch.Generator(device="cuda").manual_seed(3)
+    J = (torch.eye(2, device="cuda") + 0.3 * torch.randn(700, 2, 2, device="cuda", generator=g)).requires_grad_(True)
+    n = 500
+    e = B.svd_energy(J, 1.0, 10.0, count=n)
+    Jr = J.detach().double().clone().requires_grad_(True)
+    S = torch.linalg.svdvals(Jr[:n])
+    er = torch.sum((S - 1) ** 2) + 10.0 * torch.sum((S.prod(1) - 1) ** 2)
+    assert rel(e, er) < 1e-5
+    e.backward()
+    er.backward()
+    assert rel(J.grad, Jr.grad) < 1e-4 and float(J.grad[n:].abs().max()) == 0.0
+
+
+def test_merge_samples(B):
+    x = torch.rand(10, 2, device="cuda").requires_grad_(True)
+    b = torch.rand(4, 2, device="cuda")
+    m = B.merge_samples(x, b)
+    assert m.is_leaf and m.requires_grad and m.shape == (14, 2)
+    assert torch.equal(m[:10], x.detach()) and torch.equal(m[10:], b)
