@@ -57,14 +57,23 @@ def _worker(rank, world, port, reduction, q):
         g.copy_(torch.arange(g.numel(), dtype=torch.float32) * (rank + 1) + k)
     losses = {"main": torch.tensor(1.0 + rank), "bc": torch.tensor(10.0 * (rank + 1))}
     out = m._dp_sync(losses)
-    q.put((rank, m.a.flat_grad_buffer().clone(), m.b.flat_grad_buffer().clone(),
-           {k: float(v) for k, v in out.items()}, m.a.grad_touched()))
+    res = (rank, m.a.flat_grad_buffer().clone(), m.b.flat_grad_buffer().clone(),
+           {k: float(v) for k, v in out.items()}, m.a.grad_touched())
+    # second iteration: b receives no gradient (zero_grad, no backward reaches it) -> it is
+    # summed as zeros and stays untouched (Adam skips it, as torch skips .grad None)
+    m.b.mark_grad_stale(set_to_none=True)
+    ga = m.a.flat_grad_buffer()
+    ga.fill_(float(rank + 1))
+    m._dp_sync({"main": torch.tensor(0.0)})
+    res2 = (m.a.flat_grad_buffer().clone(), m.b.grad_touched(),
+            float(m._insr_dp_arena[m.a.param_count:m.a.param_count + m.b.param_count].abs().max()))
+    q.put(res + res2)
     dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("world", [2, 3])
 @pytest.mark.parametrize("reduction", ["mean", "sum"])
-def test_dp_sync_two_ranks(reduction):
-    world = 2
+def test_dp_sync_two_ranks(reduction, world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -76,12 +85,15 @@ def test_dp_sync_two_ranks(reduction):
         p.join(timeout=60)
         assert p.exitcode == 0
     scale = {"mean": 1.0 / world, "sum": 1.0}[reduction]
-    for rank, ga, gb, losses, touched in res:
+    rsum = sum(r + 1 for r in range(world))  # sum over ranks of (rank + 1)
+    for rank, ga, gb, losses, touched, ga2, b_touched2, b_arena_max in res:
+        assert torch.allclose(ga2, torch.full_like(ga2, rsum * scale))
+        assert not b_touched2 and b_arena_max == 0.0
         n_a = ga.numel()
-        expect_a = torch.arange(n_a, dtype=torch.float32) * (1 + 2) * scale
-        expect_b = (torch.arange(gb.numel(), dtype=torch.float32) * 3 + 2) * scale
+        expect_a = torch.arange(n_a, dtype=torch.float32) * rsum * scale
+        expect_b = (torch.arange(gb.numel(), dtype=torch.float32) * rsum + world) * scale
         assert torch.allclose(ga, expect_a) and torch.allclose(gb, expect_b)
-        assert abs(losses["main"] - (1.0 + 2.0) * scale) < 1e-6
-        assert abs(losses["bc"] - 30.0 * scale) < 1e-5
+        assert abs(losses["main"] - sum(1.0 + r for r in range(world)) * scale) < 1e-5
+        assert abs(losses["bc"] - 10.0 * rsum * scale) < 1e-4
         assert touched
     assert torch.equal(res[0][1], res[1][1])  # replicas identical -> identical Adam steps
