@@ -54,10 +54,11 @@ def main():
     ap.add_argument("--modes", default="value,grad,lap")
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--variants", default=",".join(VARIANTS))
+    ap.add_argument("--lib", default=None, help="alternative build of libinsr_hip.so (flag studies)")
     args = ap.parse_args()
     import base
     from base import _native as nat
-    lib = nat.load()
+    lib = nat.load(args.lib)
     out = []
     for name in args.nets.split(","):
         din, dout, L, W = NETS[name]
