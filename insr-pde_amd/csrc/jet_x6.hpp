@@ -363,7 +363,45 @@ __device__ __forceinline__ floatx4 h_from_regs(int s, const floatx4 (&zd)[S - 1]
   } while (0)
 #endif
 
-template <int NT>
+// 4x4 transpose across a lane quad (lanes c & ~3 .. c | 3 of one lane group g): in, lane c
+// holds v[r] = M[neuron 4g + r][point c]; out, lane c holds neuron 4g + (c & 3) at points
+// (c & ~3) + r.  Two DPP exchange stages (lane ^ 1, lane ^ 2); every lane must be active.
+__device__ __forceinline__ float dpp_xor1(float v) {  // quad_perm 1,0,3,2
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float dpp_xor2(float v) {  // quad_perm 2,3,0,1
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, false));
+}
+__device__ __forceinline__ floatx4 quad_transpose(const floatx4& v, int c) {
+  const bool o1 = c & 1, o2 = c & 2;
+  const float s0 = dpp_xor1(o1 ? v[0] : v[1]), s1 = dpp_xor1(o1 ? v[2] : v[3]);
+  const floatx4 a = {o1 ? s0 : v[0], o1 ? v[1] : s0, o1 ? s1 : v[2], o1 ? v[3] : s1};
+  const float t0 = dpp_xor2(o2 ? a[0] : a[2]), t1 = dpp_xor2(o2 ? a[1] : a[3]);
+  return floatx4{o2 ? t0 : a[0], o2 ? t1 : a[1], o2 ? a[2] : t0, o2 ? a[3] : t1};
+}
+
+// one value granule (4 neurons x 1 point per lane, C layout) -> neuron-major bf16 planes
+// [q][m][16 p] at row0 = first neuron of the lane group: quad transpose, then one b64
+// store of 4 consecutive points per plane (instead of 12 b16 stores)
+template <int PLANE>
+__device__ __forceinline__ void put_neuron_major(unsigned short* P, const floatx4& v, int row0, int c) {
+  const floatx4 tv = quad_transpose(v, c);
+  unsigned h0, m0, l0, h1, m1, l1;
+  split3(tv[0], tv[1], h0, m0, l0);
+  split3(tv[2], tv[3], h1, m1, l1);
+  unsigned short* p = P + (row0 + (c & 3)) * 16 + (c & ~3);
+  *reinterpret_cast<u32x2*>(p) = u32x2{h0, h1};
+  *reinterpret_cast<u32x2*>(p + PLANE) = u32x2{m0, m1};
+  *reinterpret_cast<u32x2*>(p + 2 * PLANE) = u32x2{l0, l1};
+}
+
+// ZT (opt-in, -DX6_ZT): a second, neuron-major image of z-bar ([q][n][16 p]) from which the
+// weight-gradient A operand is one b128 read per plane (instead of 24 u16 column reads of Z),
+// when it does not shrink the stream group.  Measured (profiles/r01/s51): the quad-transposed
+// H stores gain 1-5% on the GRAD / LAP backward at 16384 points; ZT on top costs 4-6% on the
+// LAP backward (extra spills, 50% more LDS traffic per group), gains ~3% only on 1-tile value
+// launches -- so it stays off.  -DX6_NO_HT restores the b16 H stores.
+template <int NT, bool ZT>
 struct X6BwdGeo {
   using G = X6Geo<NT>;
   static constexpr int W = G::W;
@@ -373,21 +411,36 @@ struct X6BwdGeo {
                                                        // column read hit disjoint banks
   static constexpr int HPLANE = W * 16;
   static constexpr int HSET = 3 * HPLANE;
-  static constexpr size_t SET_BYTES = (size_t)(ZSET + HSET) * 2;
+  static constexpr int ZTSET = ZT ? HSET : 0;
+  static constexpr size_t SET_BYTES = (size_t)(ZSET + HSET + ZTSET) * 2;
 };
 
 // streams per LDS group: all S if T tiles of them fit, else S/2, else 1
-template <int NT, int S, int T>
-constexpr int x6_bwd_sg() {
-  constexpr size_t set = X6BwdGeo<NT>::SET_BYTES;
+template <int NT, int S, int T, bool ZT>
+constexpr int x6_bwd_sg_z() {
+  constexpr size_t set = X6BwdGeo<NT, ZT>::SET_BYTES;
   if ((size_t)T * S * set <= kLdsMax) return S;
   if (S % 2 == 0 && (size_t)T * (S / 2) * set <= kLdsMax) return S / 2;
   return 1;
 }
 
 template <int NT, int S, int T>
+constexpr bool x6_bwd_zt() {
+#ifndef X6_ZT
+  return false;
+#else
+  return x6_bwd_sg_z<NT, S, T, true>() == x6_bwd_sg_z<NT, S, T, false>();
+#endif
+}
+
+template <int NT, int S, int T>
+constexpr int x6_bwd_sg() {
+  return x6_bwd_sg_z<NT, S, T, x6_bwd_zt<NT, S, T>()>();
+}
+
+template <int NT, int S, int T>
 constexpr size_t bwd_x6_lds_bytes() {
-  return (size_t)T * x6_bwd_sg<NT, S, T>() * X6BwdGeo<NT>::SET_BYTES;
+  return (size_t)T * x6_bwd_sg<NT, S, T>() * X6BwdGeo<NT, x6_bwd_zt<NT, S, T>()>::SET_BYTES;
 }
 
 template <int NT, int S, bool LAP, int T>
@@ -396,7 +449,8 @@ __global__ __launch_bounds__(X6Geo<NT>::THREADS) void jet_bwd_x6(
     const float* __restrict__ act, const float* __restrict__ gy, const float* __restrict__ gdy,
     const float* __restrict__ glap, float* __restrict__ part, long P) {
   using G = X6Geo<NT>;
-  using BG = X6BwdGeo<NT>;
+  constexpr bool ZTX = x6_bwd_zt<NT, S, T>();
+  using BG = X6BwdGeo<NT, ZTX>;
   constexpr int W = G::W, RPW = G::RPW, KC = G::KC;
   constexpr int LDB = BG::ZROW, ZPLANE = BG::ZPLANE, ZSET = BG::ZSET, HPLANE = BG::HPLANE, HSET = BG::HSET;
   constexpr int NTAN = LAP ? S - 2 : S - 1;
@@ -409,6 +463,7 @@ __global__ __launch_bounds__(X6Geo<NT>::THREADS) void jet_bwd_x6(
   extern __shared__ __attribute__((aligned(16))) float lds_f[];
   unsigned short* Z = reinterpret_cast<unsigned short*>(lds_f);
   unsigned short* H = Z + NSET * ZSET;
+  unsigned short* ZTp = H + NSET * HSET;  // [set][q][n][16 p] when ZTX
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
   const int ntiles = ((N + 63) / 64) * 4;
   const int tile0 = blockIdx.x * T;
@@ -632,12 +687,16 @@ __global__ __launch_bounds__(X6Geo<NT>::THREADS) void jet_bwd_x6(
             *reinterpret_cast<u32x2*>(pz) = u32x2{h0, h1};
             *reinterpret_cast<u32x2*>(pz + ZPLANE) = u32x2{m0, m1};
             *reinterpret_cast<u32x2*>(pz + 2 * ZPLANE) = u32x2{l0, l1};
+            if constexpr (ZTX) put_neuron_major<HPLANE>(ZTp + u * HSET, hb[t][i][s], col, c);
             floatx4 hs;
             if constexpr (KZ) {
               hs = h_from_regs<S, LAP>(s, zk[t][i], snp[t][i], csp[t][i]);
             } else {
               hs = h_stream<NT, S, LAP>(basep, s, rt0 + i, lane, snp[t][i], csp[t][i]);
             }
+#ifndef X6_NO_HT
+            put_neuron_major<HPLANE>(H + u * HSET, hs, col, c);
+#else
             split3(hs[0], hs[1], h0, m0, l0);
             split3(hs[2], hs[3], h1, m1, l1);
             unsigned short* ph = H + u * HSET + col * 16 + c;  // rows m = col + r, point c
@@ -653,6 +712,7 @@ __global__ __launch_bounds__(X6Geo<NT>::THREADS) void jet_bwd_x6(
             ph[2 * HPLANE + 16] = (unsigned short)(l0 >> 16);
             ph[2 * HPLANE + 32] = (unsigned short)l1;
             ph[2 * HPLANE + 48] = (unsigned short)(l1 >> 16);
+#endif
           }
       }
       INSR_STAMP(L - j, 4);
@@ -667,7 +727,13 @@ __global__ __launch_bounds__(X6Geo<NT>::THREADS) void jet_bwd_x6(
 #pragma unroll
         for (int i = 0; i < RPW; ++i) {
           Frag3 af;
-          {
+          if constexpr (ZTX) {
+            const unsigned short* pa = ZTp + (live ? u : 0) * HSET + (16 * (rt0 + i) + c) * 16 + p0;
+            const u32x4 zero4 = u32x4{0u, 0u, 0u, 0u};
+            af.h = live ? *reinterpret_cast<const u32x4*>(pa) : zero4;
+            af.m = live ? *reinterpret_cast<const u32x4*>(pa + HPLANE) : zero4;
+            af.l = live ? *reinterpret_cast<const u32x4*>(pa + 2 * HPLANE) : zero4;
+          } else {
             const unsigned short* pa = Z + (live ? u : 0) * ZSET + p0 * LDB + 16 * (rt0 + i) + c;
             unsigned hh[4], mm[4], ll[4];
 #pragma unroll

@@ -1,3 +1,5 @@
+# Machine-scheduler study (profiles/r01/flag_study).  Build the variants first:
+#   make -C insr-pde_amd/csrc OUT=../lib/libinsr_hip_<s>.so OBJDIR=/tmp/obj_<s> EXTRA="-mllvm -amdgpu-sched-strategy=<s>"
 set -e
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out/flags
