@@ -48,8 +48,8 @@ def log(msg):
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", default="fluid2Dtlgn", choices=sorted(WORKLOADS),
                     help="BASELINE.json workload (default: configs[1], the headline)")
     ap.add_argument("--scaling", choices=["strong", "weak"], default="weak")
@@ -187,7 +187,8 @@ def roofline(loops, n_local):
     per_step = {k: sum(v) / reps for k, v in agg.items()}
     # dominant kernel = the longest launch over the interior batch (boundary bands are ~1% of points;
     # a merged launch carries the interior plus its boundary / fixed points: n >= n_local)
-    dom = max((k for k in per_step if k[2] >= n_local and k[0] != "reduce"), key=lambda k: sum(agg[k]) / len(agg[k]))
+    # (fused multi-network forwards, kind "fwdK", are listed in the table but not candidates)
+    dom = max((k for k in per_step if k[2] >= n_local and k[0] in ("fwd", "bwd")), key=lambda k: sum(agg[k]) / len(agg[k]))
     kind, mode, n, W, (din, dout, L) = dom
     ms = sum(agg[dom]) / len(agg[dom])
     # algorithmic flops per launch: 2P per point per stream per GEMM pass

@@ -81,6 +81,32 @@ int insr_siren_jet_fwd(const float* x, long n_points, int d_in, int d_out, int n
                        float* act, void* stream);
 
 /*
+ * Several independent forward jets of ONE architecture and mode in one launch
+ * (horizontal fusion): each job is an insr_siren_jet_fwd call's own buffers
+ * (its network's params, its points). Results are those of insr_siren_jet_fwd
+ * per job, bit for bit, and each job's act feeds insr_siren_jet_bwd as usual.
+ * Used where a model phase evaluates two networks (or one network at two
+ * batches) with no dependency between them, e.g. the frozen and the trainable
+ * velocity fields at the same collocation points (fluid/model.py:97-98 and
+ * :143-147): a value jet of 16384 points is a latency-bound launch that holds
+ * one block per CU, so two side by side cost well under two launches.
+ * 1 <= n_jobs <= INSR_MAX_FWD_JOBS; jobs with n == 0 are allowed.
+ * Replaces: consecutive MLP.forward calls (base/networks.py:67-71).
+ */
+#define INSR_MAX_FWD_JOBS 4
+typedef struct InsrJetJob {
+  const float* x;       /* (n, d_in) */
+  const float* params;  /* flat parameters of this job's network */
+  float* y;             /* (n, d_out) */
+  float* dy;            /* (n, d_out, d_in) [GRAD, LAP] else NULL */
+  float* lap;           /* (n, d_out) [LAP] else NULL */
+  float* act;           /* insr_jet_act_bytes(n, ...) or NULL (no backward) */
+  long n;               /* points of this job */
+} InsrJetJob;
+int insr_siren_jet_fwd_multi(const InsrJetJob* jobs, int n_jobs, int d_in, int d_out,
+                             int num_hidden, int width, int mode, void* stream);
+
+/*
  * Backward of the jet to the parameters.  Adjoints (any may be NULL = zero):
  *   gy (n, d_out), gdy (n, d_out, d_in), glap (n, d_out).
  *   partial  insr_jet_partial_bytes: one fp32 parameter-gradient row per block

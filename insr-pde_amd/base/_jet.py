@@ -86,10 +86,13 @@ class _SirenJet(torch.autograd.Function):
         if save:
             nbytes = lib.insr_jet_act_bytes(n, din, L, W, mode)
             act = torch.empty(max(nbytes // 4, 1), device=dev, dtype=torch.float32)
-        with _timed("fwd", mode, n, W, (din, dout, L)):
-            rc = lib.insr_siren_jet_fwd(nat.ptr(x2), n, din, dout, L, W, mode, nat.ptr(flat), nat.ptr(y),
-                                        nat.ptr(dy), nat.ptr(lap), nat.ptr(act), nat.stream_of(dev))
-        nat.check(rc, "insr_siren_jet_fwd")
+        if _Fused.pending is not None:  # launched with the other jets of the scope, at its exit
+            _Fused.pending.append(((din, dout, L, W, mode, dev), (x2, flat, y, dy, lap, act, n)))
+        else:
+            with _timed("fwd", mode, n, W, (din, dout, L)):
+                rc = lib.insr_siren_jet_fwd(nat.ptr(x2), n, din, dout, L, W, mode, nat.ptr(flat), nat.ptr(y),
+                                            nat.ptr(dy), nat.ptr(lap), nat.ptr(act), nat.stream_of(dev))
+            nat.check(rc, "insr_siren_jet_fwd")
         ctx.set_materialize_grads(False)  # unused outputs -> None -> NULL adjoint (no zero-fill launch)
         ctx.mode, ctx.mlp, ctx.save = mode, mlp, save
         ctx.x2, ctx.act = x2, act
@@ -146,6 +149,53 @@ class _SirenJet(torch.autograd.Function):
         nat.check(rc, "insr_reduce_partials_strided")
         mlp.grad_write_end(cur)
         return none
+
+
+class _Fused:
+    pending = None  # list of (arch key, job) while a fused_forwards scope is open
+
+
+class fused_forwards:
+    """`with fused_forwards(): a = f(x); b = g(x)` -- the forward jets issued inside the
+    scope are launched together at its exit: jets of one architecture and mode go into ONE
+    insr_siren_jet_fwd_multi launch (horizontal fusion, up to MAX_FWD_JOBS per launch),
+    e.g. the frozen previous velocity field and the trainable one at the same collocation
+    points (fluid/model.py:97-98, :143-147).  Outputs, autograd nodes and saved streams are
+    those of separate calls, bit for bit.  The outputs hold no values until the scope
+    exits: read them only after it (the scope accepts network calls, nothing that consumes
+    their results).  Nested scopes join the outermost one."""
+
+    def __enter__(self):
+        self.outer = _Fused.pending is None
+        if self.outer:
+            _Fused.pending = []
+        return self
+
+    def __exit__(self, exc_type, *exc):
+        if not self.outer:
+            return False
+        jobs, _Fused.pending = _Fused.pending, None
+        if exc_type is None:
+            _launch_fused(jobs)
+        return False
+
+
+def _launch_fused(jobs):
+    groups = {}
+    for key, job in jobs:
+        groups.setdefault(key, []).append(job)
+    lib = nat.lib()
+    for (din, dout, L, W, mode, dev), js in groups.items():
+        for k in range(0, len(js), nat.MAX_FWD_JOBS):
+            chunk = js[k:k + nat.MAX_FWD_JOBS]
+            n = sum(j[6] for j in chunk)
+            arr = (nat.JetJob * len(chunk))(*[
+                nat.JetJob(x2.data_ptr(), flat.data_ptr(), y.data_ptr(), None if dy is None else dy.data_ptr(),
+                           None if lap is None else lap.data_ptr(), None if act is None else act.data_ptr(), nj)
+                for x2, flat, y, dy, lap, act, nj in chunk])
+            with _timed("fwd%d" % len(chunk) if len(chunk) > 1 else "fwd", mode, n, W, (din, dout, L)):
+                rc = lib.insr_siren_jet_fwd_multi(arr, len(chunk), din, dout, L, W, mode, nat.stream_of(dev))
+            nat.check(rc, "insr_siren_jet_fwd_multi")
 
 
 def run_jet(mlp, x, mode):

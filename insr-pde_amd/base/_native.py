@@ -33,6 +33,7 @@ SIGNATURES = {
     "insr_jet_act_bytes": (_L, [_L, _I, _I, _I, _I]),
     "insr_jet_partial_bytes": (_L, [_L, _I, _I, _I, _I, _I]),
     "insr_siren_jet_fwd": (_I, [_P, _L, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P]),
+    "insr_siren_jet_fwd_multi": (_I, [_P, _I, _I, _I, _I, _I, _I, _P]),
     "insr_siren_jet_bwd": (_I, [_P, _L, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P]),
     "insr_jet_partial_blocks": (_I, [_L, _I, _I, _I]),
     "insr_siren_jet_bwd_grad": (_I, [_P, _L, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _I, _P]),
@@ -68,6 +69,14 @@ SIGNATURES = {
     "insr_adam_step_multi": (_I, [_I, _P, _P, _P, _P, _P, _P, _F, _F, _F, _I, _P]),
     "insr_adam_step": (_I, [_P, _P, _P, _P, _L, _P, _F, _F, _F, _P]),
 }
+
+
+MAX_FWD_JOBS = 4  # INSR_MAX_FWD_JOBS
+
+
+class JetJob(ctypes.Structure):
+    """struct InsrJetJob (include/insr_siren.h): one forward jet of insr_siren_jet_fwd_multi."""
+    _fields_ = [("x", _P), ("params", _P), ("y", _P), ("dy", _P), ("lap", _P), ("act", _P), ("n", _L)]
 
 
 class NativeUnavailable(RuntimeError):

@@ -424,6 +424,44 @@ int insr_siren_jet_fwd(const float* x, long n, int din, int dout, int L, int W, 
                            (hipStream_t)stream);
 }
 
+int insr_siren_jet_fwd_multi(const InsrJetJob* jobs, int njobs, int din, int dout, int L, int W, int mode,
+                             void* stream) {
+  if (!jobs || njobs < 1 || njobs > INSR_MAX_FWD_JOBS || !shape_ok(din, dout, L, W, mode)) return INSR_EINVAL;
+  long total = 0;
+  int live = 0;
+  for (int k = 0; k < njobs; ++k) {
+    const InsrJetJob& j = jobs[k];
+    if (j.n < 0 || j.n > 0x7fffffffL) return INSR_EINVAL;
+    if (j.n == 0) continue;
+    if (!j.x || !j.params || !j.y) return INSR_EINVAL;
+    if (mode != INSR_MODE_VALUE && !j.dy) return INSR_EINVAL;
+    if (mode == INSR_MODE_LAP && !j.lap) return INSR_EINVAL;
+    total += j.n;
+    ++live;
+  }
+  if (total > 0x7fffffffL) return INSR_EINVAL;
+  if (live == 0) return 0;
+  const int S = streams_for(din, mode);
+  const int NT = nt_for(W);
+  // one fused launch where the x6 forward serves the combined batch; otherwise (another
+  // kernel family, a Laplacian jet, a single job) the jobs launch one after another
+  if (live > 1 && mode != INSR_MODE_LAP && use_split_fwd(total, NT) && use_x6(0, NT)) {
+    InsrJetJob pk[INSR_MAX_FWD_JOBS];
+    int m = 0;
+    for (int k = 0; k < njobs; ++k)
+      if (jobs[k].n > 0) pk[m++] = jobs[k];
+    return dispatch_fwd_x6_multi(NT, S, false, split_tiles(0, NT, S, total, false), pk, m, din, dout, L,
+                                 (hipStream_t)stream);
+  }
+  for (int k = 0; k < njobs; ++k) {
+    const InsrJetJob& j = jobs[k];
+    if (j.n == 0) continue;
+    const int rc = insr_siren_jet_fwd(j.x, j.n, din, dout, L, W, mode, j.params, j.y, j.dy, j.lap, j.act, stream);
+    if (rc) return rc;
+  }
+  return 0;
+}
+
 int insr_siren_jet_bwd(const float* x, long n, int din, int dout, int L, int W, int mode, const float* params,
                        const float* act, const float* gy, const float* gdy, const float* glap, float* partial,
                        void* stream) {

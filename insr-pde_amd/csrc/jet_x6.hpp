@@ -119,10 +119,13 @@ __device__ __forceinline__ Frag3 load_w_frag(const float* __restrict__ Wj, int r
   return split_frag(v0, v1);
 }
 
+// The forward of one block (tiles tile0 .. tile0 + T - 1 of one network's batch): the body
+// of jet_fwd_x6 and of jet_fwd_x6_multi (several networks / batches in one launch).
 template <int NT, int S, bool LAP, int T>
-__global__ __launch_bounds__(X6Geo<NT>::THREADS) void jet_fwd_x6(
-    const float* __restrict__ x, int N, int din, int dout, int L, const float* __restrict__ prm,
-    float* __restrict__ y, float* __restrict__ dy, float* __restrict__ lap, float* __restrict__ act) {
+__device__ __forceinline__ void fwd_x6_block(const float* __restrict__ x, int N, int din, int dout, int L,
+                                             const float* __restrict__ prm, float* __restrict__ y,
+                                             float* __restrict__ dy, float* __restrict__ lap,
+                                             float* __restrict__ act, const int tile0) {
   using G = X6Geo<NT>;
   constexpr int W = G::W, RPW = G::RPW, LDB = G::LDB, WV = G::WV, PLANE = G::PLANE, KC = G::KC;
   constexpr int NTAN = LAP ? S - 2 : S - 1;
@@ -130,7 +133,6 @@ __global__ __launch_bounds__(X6Geo<NT>::THREADS) void jet_fwd_x6(
   unsigned short* lds = reinterpret_cast<unsigned short*>(lds_f);
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
   const int ntiles = ((N + 63) / 64) * 4;
-  const int tile0 = blockIdx.x * T;
   const int rt0 = wave * RPW;
 
   float xv[T][3];
@@ -280,6 +282,67 @@ __global__ __launch_bounds__(X6Geo<NT>::THREADS) void jet_fwd_x6(
         }
       }
     }
+  }
+}
+
+template <int NT, int S, bool LAP, int T>
+__global__ __launch_bounds__(X6Geo<NT>::THREADS) void jet_fwd_x6(
+    const float* __restrict__ x, int N, int din, int dout, int L, const float* __restrict__ prm,
+    float* __restrict__ y, float* __restrict__ dy, float* __restrict__ lap, float* __restrict__ act) {
+  fwd_x6_block<NT, S, LAP, T>(x, N, din, dout, L, prm, y, dy, lap, act, blockIdx.x * T);
+}
+
+// Horizontal fusion: up to kFwdJobs independent forward jets of one architecture and jet
+// mode (different networks and/or batches, e.g. the frozen previous velocity field and the
+// trainable one at the same collocation points) in ONE launch.  A value jet of 16384 points
+// fills one 8-wave block per CU and is latency-bound (layer-serial chain); two such jets
+// side by side keep two blocks per CU in flight, so one launch costs well under two.
+// Blocks [first[k], first[k + 1]) belong to job k; the per-point arithmetic is that of
+// jet_fwd_x6 (same results bit for bit, any T).
+struct FwdJobsX6 {
+  InsrJetJob job[kFwdJobs];
+  int first[kFwdJobs + 1];
+  int njobs;
+};
+
+template <int NT, int S, bool LAP, int T>
+__global__ __launch_bounds__(X6Geo<NT>::THREADS) void jet_fwd_x6_multi(const FwdJobsX6 jobs, int din, int dout,
+                                                                       int L) {
+  const int b = blockIdx.x;
+  int k = 0;
+#pragma unroll
+  for (int q = 1; q < kFwdJobs; ++q) k += (q < jobs.njobs && b >= jobs.first[q]) ? 1 : 0;
+  const InsrJetJob& jb = jobs.job[k];
+  fwd_x6_block<NT, S, LAP, T>(jb.x, (int)jb.n, din, dout, L, jb.params, jb.y, jb.dy, jb.lap, jb.act,
+                              (b - jobs.first[k]) * T);
+}
+
+template <int NT, int S, bool LAP, int T>
+int launch_fwd_x6_multi_t(const InsrJetJob* jobs, int njobs, int din, int dout, int L, hipStream_t st) {
+  constexpr size_t lds = fwd_x6_lds_bytes<NT, S, T>();
+  if constexpr (lds > kLdsMax) {
+    return INSR_EINVAL;
+  } else {
+    if (njobs < 1 || njobs > kFwdJobs) return INSR_EINVAL;
+    static bool attr_set = false;
+    if (!attr_set) {
+      (void)hipFuncSetAttribute((const void*)jet_fwd_x6_multi<NT, S, LAP, T>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      attr_set = true;
+    }
+    FwdJobsX6 pk{};
+    int nb = 0;
+    for (int k = 0; k < njobs; ++k) {
+      pk.job[k] = jobs[k];
+      pk.first[k] = nb;
+      nb += (int)(((jobs[k].n + 15) / 16 + T - 1) / T);
+    }
+    pk.first[njobs] = nb;
+    pk.njobs = njobs;
+    if (nb == 0) return 0;
+    hipLaunchKernelGGL((jet_fwd_x6_multi<NT, S, LAP, T>), dim3(nb), dim3(X6Geo<NT>::THREADS), lds, st, pk, din,
+                       dout, L);
+    return (int)hipGetLastError();
   }
 }
 

@@ -15,8 +15,8 @@ import os
 import numpy as np
 import torch
 
-from base import (BaseModel, divergence, fused_mse, gradient, jacobian, laplace, sample_boundary2D_pair,
-                  sample_boundary2D_separate, sample_random, sample_uniform, wall_mse)
+from base import (BaseModel, divergence, fused_forwards, fused_mse, gradient, jacobian, laplace,
+                  sample_boundary2D_pair, sample_boundary2D_separate, sample_random, sample_uniform, wall_mse)
 
 from .examples import get_examples
 
@@ -148,10 +148,33 @@ class Fluid2DModel(BaseModel):
         with torch.no_grad():  # both detached in the reference as well
             return self.velocity_field_prev(x).detach(), gradient(self.pressure_field(x), x)
 
+    # Horizontal fusion (cfg.insr_fuse_forwards, default on; not with insr_nograd_stream):
+    # the frozen field's value jet and the trainable field's value jet at the same points
+    # are independent -- ONE insr_siren_jet_fwd_multi launch holds two blocks per CU
+    # instead of two latency-bound launches of one block per CU each.
+    def _fused_pair(self):
+        return getattr(self.cfg, "insr_fuse_forwards", True) and not getattr(self.cfg, "insr_nograd_stream", False)
+
+    def _prev_and_current(self, x):
+        """(u_prev(x) detached, u(x)) -- one fused forward launch."""
+        with fused_forwards():
+            with torch.no_grad():
+                u_prev = self.velocity_field_prev(x)
+            u = self.velocity_field(x)
+        return u_prev.detach(), u
+
     @BaseModel._training_loop
     def _advect_velocity(self):
         x = self._sample_in_training()
         bc, join_bc = self._fork("insr_band_stream", self._wall_loss, x.shape[0])
+        if self._fused_pair():
+            u_prev, u = self._prev_and_current(x)
+            with torch.no_grad():
+                foot = torch.add(x, u_prev, alpha=-self.cfg.dt).clamp_(-1.0, 1.0)
+                u_target = self.velocity_field_prev(foot)
+            main = fused_mse(u, u_target)
+            join_bc()
+            return {'main': main, 'bc': bc}
         u_target, join_t = self._fork("insr_nograd_stream", self._advect_target, x)
         u = self.velocity_field(x)
         join_t()
@@ -174,9 +197,14 @@ class Fluid2DModel(BaseModel):
     def _projection(self):
         x = self._sample_in_training()
         bc, join_bc = self._fork("insr_band_stream", self._wall_loss, x.shape[0])
-        (u_prev, grad_p), join_t = self._fork("insr_nograd_stream", self._projection_target, x)
-        u = self.velocity_field(x)
-        join_t()
+        if self._fused_pair():
+            u_prev, u = self._prev_and_current(x)
+            with torch.no_grad():
+                grad_p = gradient(self.pressure_field(x), x)
+        else:
+            (u_prev, grad_p), join_t = self._fork("insr_nograd_stream", self._projection_target, x)
+            u = self.velocity_field(x)
+            join_t()
         # mean((u - (u_prev - grad_p))^2): r = 1*(u + 0) + (-1)*(u_prev + (-1)*grad_p)
         main = fused_mse(u, None, u_prev, grad_p, gamma=-1.0, delta=-1.0)
         join_bc()
