@@ -446,12 +446,18 @@ int insr_siren_jet_fwd_multi(const InsrJetJob* jobs, int njobs, int din, int dou
   // one fused launch where the x6 forward serves the combined batch; otherwise (another
   // kernel family, a Laplacian jet, a single job) the jobs launch one after another
   if (live > 1 && mode != INSR_MODE_LAP && use_split_fwd(total, NT) && use_x6(0, NT)) {
+    // tiles per block from the combined batch; a job whose own batch would take fewer
+    // (a boundary band) runs 1-tile blocks, placed first in the grid
+    const int T = split_tiles(0, NT, S, total, false);
     InsrJetJob pk[INSR_MAX_FWD_JOBS];
+    int small[INSR_MAX_FWD_JOBS];
     int m = 0;
     for (int k = 0; k < njobs; ++k)
-      if (jobs[k].n > 0) pk[m++] = jobs[k];
-    return dispatch_fwd_x6_multi(NT, S, false, split_tiles(0, NT, S, total, false), pk, m, din, dout, L,
-                                 (hipStream_t)stream);
+      if (jobs[k].n > 0) {
+        small[m] = split_tiles(0, NT, S, jobs[k].n, false) < T ? 1 : 0;
+        pk[m++] = jobs[k];
+      }
+    return dispatch_fwd_x6_multi(NT, S, false, T, pk, small, m, din, dout, L, (hipStream_t)stream);
   }
   for (int k = 0; k < njobs; ++k) {
     const InsrJetJob& j = jobs[k];

@@ -322,8 +322,8 @@ int dispatch_bwd_split(int NT, int S, bool LAP, int T, const float* x, int N, in
 int dispatch_fwd_x6(int NT, int S, bool LAP, int T, const float* x, int N, int din, int dout, int L,
                     const float* prm, float* y, float* dy, float* lap, float* act, hipStream_t st);
 constexpr int kFwdJobs = INSR_MAX_FWD_JOBS;
-int dispatch_fwd_x6_multi(int NT, int S, bool LAP, int T, const InsrJetJob* jobs, int njobs, int din, int dout,
-                          int L, hipStream_t st);
+int dispatch_fwd_x6_multi(int NT, int S, bool LAP, int T, const InsrJetJob* jobs, const int* small, int njobs,
+                          int din, int dout, int L, hipStream_t st);
 int dispatch_bwd_x6(int NT, int S, bool LAP, int T, const float* x, int N, int din, int dout, int L,
                     const float* prm, const float* act, const float* gy, const float* gdy, const float* glap,
                     float* part, long P, hipStream_t st);

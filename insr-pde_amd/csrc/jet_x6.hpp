@@ -294,31 +294,52 @@ __global__ __launch_bounds__(X6Geo<NT>::THREADS) void jet_fwd_x6(
 
 // Horizontal fusion: up to kFwdJobs independent forward jets of one architecture and jet
 // mode (different networks and/or batches, e.g. the frozen previous velocity field and the
-// trainable one at the same collocation points) in ONE launch.  A value jet of 16384 points
-// fills one 8-wave block per CU and is latency-bound (layer-serial chain); two such jets
-// side by side keep two blocks per CU in flight, so one launch costs well under two.
-// Blocks [first[k], first[k + 1]) belong to job k; the per-point arithmetic is that of
-// jet_fwd_x6 (same results bit for bit, any T).
+// trainable one at the same collocation points, plus the boundary band) in ONE launch.  A
+// value jet of 16384 points fills one 8-wave block per CU and is latency-bound (layer-serial
+// chain); two such jets side by side keep two blocks per CU in flight, so one launch costs
+// well under two.  Small jobs (a boundary band of a few hundred points) run 1-tile blocks
+// (TB) placed FIRST in the grid: they take a slot on a few CUs, finish in about half the
+// time of a TA-tile block, and the remaining TA blocks take their slots -- instead of a
+// latency-bound launch of their own.  Blocks [first[k], first[k + 1]) belong to job k; the
+// per-point arithmetic is that of jet_fwd_x6 (same results bit for bit, any T).
 struct FwdJobsX6 {
   InsrJetJob job[kFwdJobs];
   int first[kFwdJobs + 1];
+  int small[kFwdJobs];  // 1: the job runs TB-tile blocks
   int njobs;
 };
 
-template <int NT, int S, bool LAP, int T>
-__global__ __launch_bounds__(X6Geo<NT>::THREADS) void jet_fwd_x6_multi(const FwdJobsX6 jobs, int din, int dout,
-                                                                       int L) {
+// value jets at W = 128: hold the kernel to 128 VGPRs (4 waves per SIMD = two 8-wave blocks
+// per CU), which the TA = 4 body meets on its own (116) and the 1-tile body is scheduled into
+template <int NT, int S>
+constexpr int x6_multi_min_waves() {
+  return (NT == 8 && S == 1) ? 4 : 1;
+}
+
+template <int NT, int S, bool LAP, int TA, int TB>
+__global__ __launch_bounds__(X6Geo<NT>::THREADS, (x6_multi_min_waves<NT, S>())) void jet_fwd_x6_multi(
+    const FwdJobsX6 jobs, int din, int dout, int L) {
   const int b = blockIdx.x;
   int k = 0;
 #pragma unroll
   for (int q = 1; q < kFwdJobs; ++q) k += (q < jobs.njobs && b >= jobs.first[q]) ? 1 : 0;
   const InsrJetJob& jb = jobs.job[k];
-  fwd_x6_block<NT, S, LAP, T>(jb.x, (int)jb.n, din, dout, L, jb.params, jb.y, jb.dy, jb.lap, jb.act,
-                              (b - jobs.first[k]) * T);
+  if constexpr (TA != TB) {
+    if (jobs.small[k]) {
+      fwd_x6_block<NT, S, LAP, TB>(jb.x, (int)jb.n, din, dout, L, jb.params, jb.y, jb.dy, jb.lap, jb.act,
+                                   (b - jobs.first[k]) * TB);
+      return;
+    }
+  }
+  fwd_x6_block<NT, S, LAP, TA>(jb.x, (int)jb.n, din, dout, L, jb.params, jb.y, jb.dy, jb.lap, jb.act,
+                               (b - jobs.first[k]) * TA);
 }
 
+// small[k] != 0: job k runs 1-tile blocks (ignored when T == 1)
 template <int NT, int S, bool LAP, int T>
-int launch_fwd_x6_multi_t(const InsrJetJob* jobs, int njobs, int din, int dout, int L, hipStream_t st) {
+int launch_fwd_x6_multi_t(const InsrJetJob* jobs, const int* small, int njobs, int din, int dout, int L,
+                          hipStream_t st) {
+  constexpr int TB = 1;
   constexpr size_t lds = fwd_x6_lds_bytes<NT, S, T>();
   if constexpr (lds > kLdsMax) {
     return INSR_EINVAL;
@@ -326,21 +347,27 @@ int launch_fwd_x6_multi_t(const InsrJetJob* jobs, int njobs, int din, int dout, 
     if (njobs < 1 || njobs > kFwdJobs) return INSR_EINVAL;
     static bool attr_set = false;
     if (!attr_set) {
-      (void)hipFuncSetAttribute((const void*)jet_fwd_x6_multi<NT, S, LAP, T>,
+      (void)hipFuncSetAttribute((const void*)jet_fwd_x6_multi<NT, S, LAP, T, TB>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       attr_set = true;
     }
     FwdJobsX6 pk{};
-    int nb = 0;
-    for (int k = 0; k < njobs; ++k) {
-      pk.job[k] = jobs[k];
-      pk.first[k] = nb;
-      nb += (int)(((jobs[k].n + 15) / 16 + T - 1) / T);
-    }
+    int nb = 0, m = 0;
+    for (int pass = 0; pass < 2; ++pass)  // small jobs' blocks first
+      for (int k = 0; k < njobs; ++k) {
+        const int sm = (T != TB && small && small[k]) ? 1 : 0;
+        if (sm != 1 - pass) continue;
+        pk.job[m] = jobs[k];
+        pk.small[m] = sm;
+        pk.first[m] = nb;
+        const int t = sm ? TB : T;
+        nb += (int)(((jobs[k].n + 15) / 16 + t - 1) / t);
+        ++m;
+      }
     pk.first[njobs] = nb;
     pk.njobs = njobs;
     if (nb == 0) return 0;
-    hipLaunchKernelGGL((jet_fwd_x6_multi<NT, S, LAP, T>), dim3(nb), dim3(X6Geo<NT>::THREADS), lds, st, pk, din,
+    hipLaunchKernelGGL((jet_fwd_x6_multi<NT, S, LAP, T, TB>), dim3(nb), dim3(X6Geo<NT>::THREADS), lds, st, pk, din,
                        dout, L);
     return (int)hipGetLastError();
   }

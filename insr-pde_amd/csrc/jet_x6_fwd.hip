@@ -15,26 +15,27 @@ int launch_fwd_x6(int T, const float* x, int N, int din, int dout, int L, const 
 }
 
 template <int NT, int S, bool LAP>
-int launch_fwd_x6_multi(int T, const InsrJetJob* jobs, int njobs, int din, int dout, int L, hipStream_t st) {
+int launch_fwd_x6_multi(int T, const InsrJetJob* jobs, const int* small, int njobs, int din, int dout, int L,
+                        hipStream_t st) {
   switch (T) {
-    case 1: return launch_fwd_x6_multi_t<NT, S, LAP, 1>(jobs, njobs, din, dout, L, st);
-    case 2: return launch_fwd_x6_multi_t<NT, S, LAP, 2>(jobs, njobs, din, dout, L, st);
-    case 4: return launch_fwd_x6_multi_t<NT, S, LAP, 4>(jobs, njobs, din, dout, L, st);
+    case 1: return launch_fwd_x6_multi_t<NT, S, LAP, 1>(jobs, small, njobs, din, dout, L, st);
+    case 2: return launch_fwd_x6_multi_t<NT, S, LAP, 2>(jobs, small, njobs, din, dout, L, st);
+    case 4: return launch_fwd_x6_multi_t<NT, S, LAP, 4>(jobs, small, njobs, din, dout, L, st);
     default: return INSR_EINVAL;
   }
 }
 
 // value and gradient jets (the fused pairs the models issue are value jets; the Laplacian
 // jet is never paired), widths 64 / 128 / 256
-int dispatch_fwd_x6_multi(int NT, int S, bool LAP, int T, const InsrJetJob* jobs, int njobs, int din, int dout,
-                          int L, hipStream_t st) {
+int dispatch_fwd_x6_multi(int NT, int S, bool LAP, int T, const InsrJetJob* jobs, const int* small, int njobs,
+                          int din, int dout, int L, hipStream_t st) {
   if (LAP) return INSR_EINVAL;
 #define INSR_MULTI_S(NTV)                                                          \
   switch (S) {                                                                     \
-    case 1: return launch_fwd_x6_multi<NTV, 1, false>(T, jobs, njobs, din, dout, L, st); \
-    case 2: return launch_fwd_x6_multi<NTV, 2, false>(T, jobs, njobs, din, dout, L, st); \
-    case 3: return launch_fwd_x6_multi<NTV, 3, false>(T, jobs, njobs, din, dout, L, st); \
-    case 4: return launch_fwd_x6_multi<NTV, 4, false>(T, jobs, njobs, din, dout, L, st); \
+    case 1: return launch_fwd_x6_multi<NTV, 1, false>(T, jobs, small, njobs, din, dout, L, st); \
+    case 2: return launch_fwd_x6_multi<NTV, 2, false>(T, jobs, small, njobs, din, dout, L, st); \
+    case 3: return launch_fwd_x6_multi<NTV, 3, false>(T, jobs, small, njobs, din, dout, L, st); \
+    case 4: return launch_fwd_x6_multi<NTV, 4, false>(T, jobs, small, njobs, din, dout, L, st); \
     default: return INSR_EINVAL;                                                   \
   }
   switch (NT) {

@@ -155,26 +155,28 @@ class Fluid2DModel(BaseModel):
     def _fused_pair(self):
         return getattr(self.cfg, "insr_fuse_forwards", True) and not getattr(self.cfg, "insr_nograd_stream", False)
 
+    # The boundary band's value jet (a few hundred points, a latency-bound launch of its own)
+    # joins the same launch as 1-tile blocks placed first in the grid (insr_siren_jet_fwd_multi).
     def _prev_and_current(self, x):
-        """(u_prev(x) detached, u(x)) -- one fused forward launch."""
+        """(wall loss, u_prev(x) detached, u(x)) -- the three value jets in one launch."""
         with fused_forwards():
+            bxy, nb = self._boundary_bands(x.shape[0])
+            y_band = self.velocity_field(bxy)
             with torch.no_grad():
                 u_prev = self.velocity_field_prev(x)
             u = self.velocity_field(x)
-        return u_prev.detach(), u
+        return wall_mse(y_band, nb), u_prev.detach(), u
 
     @BaseModel._training_loop
     def _advect_velocity(self):
         x = self._sample_in_training()
-        bc, join_bc = self._fork("insr_band_stream", self._wall_loss, x.shape[0])
-        if self._fused_pair():
-            u_prev, u = self._prev_and_current(x)
+        if self._fused_pair() and not getattr(self.cfg, "insr_band_stream", False):
+            bc, u_prev, u = self._prev_and_current(x)
             with torch.no_grad():
                 foot = torch.add(x, u_prev, alpha=-self.cfg.dt).clamp_(-1.0, 1.0)
                 u_target = self.velocity_field_prev(foot)
-            main = fused_mse(u, u_target)
-            join_bc()
-            return {'main': main, 'bc': bc}
+            return {'main': fused_mse(u, u_target), 'bc': bc}
+        bc, join_bc = self._fork("insr_band_stream", self._wall_loss, x.shape[0])
         u_target, join_t = self._fork("insr_nograd_stream", self._advect_target, x)
         u = self.velocity_field(x)
         join_t()
@@ -196,15 +198,15 @@ class Fluid2DModel(BaseModel):
     @BaseModel._training_loop
     def _projection(self):
         x = self._sample_in_training()
-        bc, join_bc = self._fork("insr_band_stream", self._wall_loss, x.shape[0])
-        if self._fused_pair():
-            u_prev, u = self._prev_and_current(x)
+        if self._fused_pair() and not getattr(self.cfg, "insr_band_stream", False):
+            bc, u_prev, u = self._prev_and_current(x)
             with torch.no_grad():
                 grad_p = gradient(self.pressure_field(x), x)
-        else:
-            (u_prev, grad_p), join_t = self._fork("insr_nograd_stream", self._projection_target, x)
-            u = self.velocity_field(x)
-            join_t()
+            return {'main': fused_mse(u, None, u_prev, grad_p, gamma=-1.0, delta=-1.0), 'bc': bc}
+        bc, join_bc = self._fork("insr_band_stream", self._wall_loss, x.shape[0])
+        (u_prev, grad_p), join_t = self._fork("insr_nograd_stream", self._projection_target, x)
+        u = self.velocity_field(x)
+        join_t()
         # mean((u - (u_prev - grad_p))^2): r = 1*(u + 0) + (-1)*(u_prev + (-1)*grad_p)
         main = fused_mse(u, None, u_prev, grad_p, gamma=-1.0, delta=-1.0)
         join_bc()

@@ -90,7 +90,7 @@ def _eq(a, b, n=None, layers=None):
 
 @pytest.mark.parametrize("name", list(NETS))
 @pytest.mark.parametrize("mode", [0, 1])
-@pytest.mark.parametrize("sizes", [(16384, 16384), (1000, 324, 0), (64, 20000, 5, 333)])
+@pytest.mark.parametrize("sizes", [(16384, 16384), (324, 16384, 16384), (1000, 324, 0), (64, 20000, 5, 333)])
 def test_multi_matches_single_launches(B, name, mode, sizes):
     din = NETS[name][0]
     nets = [_net(B, name, seed=10 + k) for k in range(len(sizes))]
