@@ -285,8 +285,18 @@ __device__ __forceinline__ void fwd_x6_block(const float* __restrict__ x, int N,
   }
 }
 
+// Minimum waves per SIMD the W = 128 forward is compiled for (4 = at most 128 VGPRs = two
+// 8-wave blocks per CU); 1 = no bound (the compiler's choice).
+#ifndef X6_FWD_MIN_WAVES
+#define X6_FWD_MIN_WAVES 1
+#endif
+template <int NT>
+constexpr int x6_fwd_min_waves() {
+  return NT == 8 ? X6_FWD_MIN_WAVES : 1;
+}
+
 template <int NT, int S, bool LAP, int T>
-__global__ __launch_bounds__(X6Geo<NT>::THREADS) void jet_fwd_x6(
+__global__ __launch_bounds__(X6Geo<NT>::THREADS, (x6_fwd_min_waves<NT>())) void jet_fwd_x6(
     const float* __restrict__ x, int N, int din, int dout, int L, const float* __restrict__ prm,
     float* __restrict__ y, float* __restrict__ dy, float* __restrict__ lap, float* __restrict__ act) {
   fwd_x6_block<NT, S, LAP, T>(x, N, din, dout, L, prm, y, dy, lap, act, blockIdx.x * T);
