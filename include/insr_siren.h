@@ -301,6 +301,27 @@ int insr_comm_init(void** comm, int rank, int world, const void* id);
 int insr_comm_allreduce_sum(void* comm, float* buf, long count, void* stream);
 int insr_comm_destroy(void* comm);
 
+/*
+ * Collocation draws of one phase iteration in ONE launch: n_boxes boxes of points in
+ * dim (1..3) dimensions, box k = boxes[k].n points with coordinate j uniform in
+ * [lo[j], hi[j]), written row-major (n, dim) to boxes[k].out. One Philox-4x32-10
+ * stream keyed by `seed`; `state` (insr_sampler_state_bytes, zero-initialised device
+ * memory, one per stream of draws) holds the stream position, which the launch
+ * advances itself -- a captured graph draws fresh points on every replay.
+ * Replaces: sample_random + sample_boundary2D_separate (base/sampling.py:14-64) as
+ * called by the phases (fluid/model.py:74,90-91,105,116-117,129,135-136).
+ */
+#define INSR_MAX_BOXES 8
+typedef struct InsrBox {
+  float* out;   /* (n, dim) */
+  long n;       /* points */
+  float lo[3];  /* per coordinate */
+  float hi[3];
+} InsrBox;
+long insr_sampler_state_bytes(void);
+int insr_sample_boxes(const InsrBox* boxes, int n_boxes, int dim, unsigned long long seed, void* state,
+                      void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -67,6 +67,8 @@ SIGNATURES = {
     "insr_adam_prepare": (_I, [_P, _F, _F, _P]),
     "insr_plateau_step": (_I, [_P, _P, _I, _I, _P]),
     "insr_adam_step_multi": (_I, [_I, _P, _P, _P, _P, _P, _P, _F, _F, _F, _I, _P]),
+    "insr_sampler_state_bytes": (_L, []),
+    "insr_sample_boxes": (_I, [_P, _I, _I, ctypes.c_ulonglong, _P, _P]),
     "insr_adam_step": (_I, [_P, _P, _P, _P, _L, _P, _F, _F, _F, _P]),
 }
 
@@ -77,6 +79,14 @@ MAX_FWD_JOBS = 4  # INSR_MAX_FWD_JOBS
 class JetJob(ctypes.Structure):
     """struct InsrJetJob (include/insr_siren.h): one forward jet of insr_siren_jet_fwd_multi."""
     _fields_ = [("x", _P), ("params", _P), ("y", _P), ("dy", _P), ("lap", _P), ("act", _P), ("n", _L)]
+
+
+MAX_BOXES = 8  # INSR_MAX_BOXES
+
+
+class Box(ctypes.Structure):
+    """struct InsrBox (include/insr_siren.h): one box of insr_sample_boxes."""
+    _fields_ = [("out", _P), ("n", _L), ("lo", _F * 3), ("hi", _F * 3)]
 
 
 class NativeUnavailable(RuntimeError):

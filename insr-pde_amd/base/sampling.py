@@ -12,7 +12,7 @@ import torch
 _AFFINE = {}  # (N, side-key, epsilon, device) -> (scale, shift) constant tensors
 
 __all__ = ["sample_uniform", "sample_random", "sample_boundary", "sample_boundary2D_separate",
-           "sample_boundary2D_pair", "merge_samples"]
+           "sample_boundary2D_pair", "sample_random_and_bands2D", "merge_samples"]
 
 
 def sample_uniform(resolution, sdim=1, device="cpu", flatten=True):
@@ -97,3 +97,48 @@ def merge_samples(*parts):
     runs one jet launch each way instead of one per set -- a band of a few hundred points
     would otherwise be a latency-bound launch of its own.  Row order = argument order."""
     return torch.cat([p.detach() for p in parts]).requires_grad_(True)
+
+
+_SAMPLER = {}  # device index -> (Philox stream position on the device, seed)
+
+
+def _sampler(dev):
+    """Per-device Philox state of the fused sampler (insr_sample_boxes).  Seeded from the
+    device's torch generator seed (torch.manual_seed / per-rank seeding applies).  Created
+    on the first eager call -- phase loops always run iteration 0 eagerly before capturing."""
+    from . import _native as nat
+    key = dev.index
+    if key not in _SAMPLER:
+        if torch.cuda.is_current_stream_capturing():
+            raise RuntimeError("sampler state must be created before graph capture (run one eager call)")
+        with torch.cuda.device(dev):
+            seed = torch.cuda.initial_seed()
+        _SAMPLER[key] = (torch.zeros(nat.lib().insr_sampler_state_bytes() // 8, device=dev, dtype=torch.int64),
+                         seed & 0xFFFFFFFFFFFFFFFF)
+    return _SAMPLER[key]
+
+
+def sample_random_and_bands2D(N, n_band, epsilon=1e-4, device="cuda"):
+    """(sample_random(N, 2), sample_boundary2D_pair(n_band)) -- the interior batch and the
+    four wall bands of one fluid phase iteration (fluid/model.py:74,90-91,105,116-117) --
+    drawn in ONE device launch (insr_sample_boxes: 3 launches -> 1).  Same distributions;
+    the device stream is Philox-4x32-10, not torch's (GPU only: the CPU samplers above
+    reproduce the reference bit for bit)."""
+    from . import _native as nat
+    dev = torch.device(device)
+    if dev.type != "cuda":
+        raise nat.NativeUnavailable("sample_random_and_bands2D draws on the GPU only")
+    state, seed = _sampler(dev)
+    h = n_band // 2
+    x = torch.empty(N, 2, device=dev)
+    bxy = torch.empty(4 * h, 2, device=dev)
+    full, lo, hi = (-1.0, 1.0), (-1 - epsilon, -1 + epsilon), (1 - epsilon, 1 + epsilon)
+    faces = [(lo, full), (hi, full), (full, lo), (full, hi)]  # sample_boundary2D_pair's order
+    f3 = nat._F * 3
+    boxes = (nat.Box * 5)()
+    boxes[0] = nat.Box(x.data_ptr(), N, f3(-1.0, -1.0, 0.0), f3(1.0, 1.0, 0.0))
+    for k, (rx, ry) in enumerate(faces):  # face k: rows [k h, (k + 1) h) of bxy, 8 bytes a row
+        boxes[1 + k] = nat.Box(bxy.data_ptr() + 8 * h * k, h, f3(rx[0], ry[0], 0.0), f3(rx[1], ry[1], 0.0))
+    nat.check(nat.lib().insr_sample_boxes(boxes, 5, 2, seed, nat.ptr(state), nat.stream_of(dev)),
+              "insr_sample_boxes")
+    return x, bxy

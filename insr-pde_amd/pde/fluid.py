@@ -16,7 +16,8 @@ import numpy as np
 import torch
 
 from base import (BaseModel, divergence, fused_forwards, fused_mse, gradient, jacobian, laplace,
-                  sample_boundary2D_pair, sample_boundary2D_separate, sample_random, sample_uniform, wall_mse)
+                  sample_boundary2D_pair, sample_boundary2D_separate, sample_random, sample_random_and_bands2D,
+                  sample_uniform, wall_mse)
 
 from .examples import get_examples
 
@@ -43,7 +44,14 @@ class Fluid2DModel(BaseModel):
         return int(fixed) if fixed else max(1, self.sample_resolution ** 2 // self._dp_world())
 
     def _sample_in_training(self):
-        return sample_random(self._n_interior(), 2, device=self.device).requires_grad_(True)
+        """The interior batch.  On the GPU the iteration's wall bands come from the same
+        launch (sample_random_and_bands2D) and wait in `_insr_bands` for _boundary_bands."""
+        n = self._n_interior()
+        if torch.device(self.device).type == "cuda":
+            x, bxy = sample_random_and_bands2D(n, n // 100, device=self.device)
+            self._insr_bands = (bxy.requires_grad_(True), bxy.shape[0] // 2)
+            return x.requires_grad_(True)
+        return sample_random(n, 2, device=self.device).requires_grad_(True)
 
     def _boundary_pair(self, n_interior):
         nb = n_interior // 100
@@ -59,6 +67,9 @@ class Fluid2DModel(BaseModel):
         if "_boundary_pair" in self.__dict__:
             bx, by = self._boundary_pair(n_interior)
             return torch.cat([bx, by]), bx.shape[0]
+        pre = self.__dict__.pop("_insr_bands", None)
+        if pre is not None and pre[0].shape[0] == 4 * ((n_interior // 100) // 2):
+            return pre
         bxy = sample_boundary2D_pair(n_interior // 100, device=self.device).requires_grad_(True)
         return bxy, bxy.shape[0] // 2
 

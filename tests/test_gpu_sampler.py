@@ -1,0 +1,127 @@
+"""Fused collocation sampler (insr_sample_boxes / base.sample_random_and_bands2D).
+
+The device stream is Philox-4x32-10: a numpy restatement here is pinned to the Random123
+known-answer vector, and the kernel's draws must equal it bit for bit (value v of a
+launch = Philox(seed, base + v // 4)[v % 4] -> lo + (hi - lo) * (bits >> 8) * 2^-24).
+Distribution checks cover the reference samplers' boxes (base/sampling.py:14-64).
+"""
+import numpy as np
+import pytest
+import torch
+
+M0, M1, W0, W1 = 0xD2511F53, 0xCD9E8D57, 0x9E3779B9, 0xBB67AE85
+
+
+def philox4x32_10(key, ctr):
+    """numpy Philox-4x32-10; key (k0, k1), ctr (N, 4) uint32 -> (N, 4) uint32."""
+    c = np.array(ctr, dtype=np.uint64)
+    k0, k1 = np.uint64(key[0]), np.uint64(key[1])
+    mask = np.uint64(0xFFFFFFFF)
+    for _ in range(10):
+        p0 = np.uint64(M0) * c[:, 0]
+        p1 = np.uint64(M1) * c[:, 2]
+        hi0, lo0 = p0 >> np.uint64(32), p0 & mask
+        hi1, lo1 = p1 >> np.uint64(32), p1 & mask
+        c = np.stack([hi1 ^ c[:, 1] ^ k0, lo1, hi0 ^ c[:, 3] ^ k1, lo0], axis=1)
+        k0, k1 = (k0 + np.uint64(W0)) & mask, (k1 + np.uint64(W1)) & mask
+    return c.astype(np.uint32)
+
+
+def test_numpy_philox_known_answer():
+    # Random123 kat_vectors: philox4x32 10 rounds, ctr = key = 0 and ctr = key = all ones
+    assert philox4x32_10((0, 0), [[0, 0, 0, 0]]).tolist() == [[0x6627E8D5, 0xE169C58D, 0xBC57AC4C, 0x9B00DBD8]]
+    f = 0xFFFFFFFF
+    assert philox4x32_10((f, f), [[f, f, f, f]]).tolist() == [[0x408F276D, 0x41C83B0E, 0xA20BC7C6, 0x6D5451FD]]
+
+
+@pytest.fixture(scope="module")
+def B():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import base
+    base._native.load()
+    return base
+
+
+def _draw(B, boxes, dim, seed, state):
+    nat = B._native
+    arr = (nat.Box * len(boxes))()
+    f3 = nat._F * 3
+    outs = []
+    for k, (n, lo, hi) in enumerate(boxes):
+        t = torch.empty(n, dim, device="cuda")
+        outs.append(t)
+        arr[k] = nat.Box(t.data_ptr(), n, f3(*(list(lo) + [0.0] * (3 - dim))), f3(*(list(hi) + [0.0] * (3 - dim))))
+    nat.check(nat.lib().insr_sample_boxes(arr, len(boxes), dim, seed, nat.ptr(state), nat.stream_of(0)), "sample")
+    return outs
+
+
+def _expected(boxes, dim, seed, base):
+    total = sum(n * dim for n, _, _ in boxes)
+    nthreads = (total + 3) // 4
+    ctr = np.zeros((nthreads, 4), dtype=np.uint64)
+    g = np.arange(nthreads, dtype=np.uint64) + np.uint64(base)
+    ctr[:, 0], ctr[:, 1] = g & np.uint64(0xFFFFFFFF), g >> np.uint64(32)
+    bits = philox4x32_10((seed & 0xFFFFFFFF, seed >> 32), ctr).reshape(-1)[:total]
+    u = (bits >> 8).astype(np.float32) * np.float32(2.0 ** -24)
+    out, v = [], 0
+    for n, lo, hi in boxes:
+        uu = u[v:v + n * dim].reshape(n, dim)
+        lo32, hi32 = np.array(lo, np.float32), np.array(hi, np.float32)
+        out.append(lo32 + (hi32 - lo32) * uu)
+        v += n * dim
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dim", [1, 2, 3])
+def test_kernel_equals_philox_restatement_and_advances(B, dim):
+    boxes = [(1000, [-1.0] * dim, [1.0] * dim), (7, [0.5] * dim, [0.75] * dim), (0, [0.0] * dim, [1.0] * dim),
+             (333, [-2.0 + j for j in range(dim)], [-1.0 + 2 * j for j in range(dim)])]
+    seed = 0x123456789ABCDEF
+    state = torch.zeros(2, dtype=torch.int64, device="cuda")
+    state[0] = (1 << 32) - 5  # counter carry into the high word inside the launch
+    base = int(state[0])
+    for _ in range(2):
+        got = _draw(B, boxes, dim, seed, state)
+        exp = _expected(boxes, dim, seed, base)
+        for g, e in zip(got, exp):
+            assert np.array_equal(g.cpu().numpy(), e)
+        total = sum(n * dim for n, _, _ in boxes)
+        assert int(state[0]) == base + (total + 3) // 4 and int(state[1]) == 0  # advanced; ticket reset
+        base = int(state[0])
+
+
+@pytest.mark.gpu
+def test_fluid_draw_boxes_and_moments(B):
+    torch.manual_seed(0)
+    x, bxy = B.sample_random_and_bands2D(1 << 20, 2000, epsilon=1e-4, device="cuda")
+    assert x.shape == (1 << 20, 2) and bxy.shape == (4000, 2)
+    xc = x.double().cpu()
+    assert float(xc.min()) >= -1.0 and float(xc.max()) < 1.0
+    assert abs(float(xc.mean())) < 3e-3 and abs(float(xc.var()) - 1.0 / 3.0) < 3e-3
+    b = bxy.cpu().view(4, 1000, 2)
+    eps = 1e-4
+    # face order of sample_boundary2D_pair: x = -1, x = +1, y = -1, y = +1 bands
+    for k, (axis, c) in enumerate([(0, -1.0), (0, 1.0), (1, -1.0), (1, 1.0)]):
+        assert float((b[k, :, axis] - c).abs().max()) <= eps + 2.5e-7  # fp32 rounding of 1 +- eps
+        other = b[k, :, 1 - axis]
+        assert float(other.min()) >= -1.0 and float(other.max()) < 1.0 and float(other.std()) > 0.5
+
+
+@pytest.mark.gpu
+def test_graph_replay_draws_fresh_points(B):
+    x0, _ = B.sample_random_and_bands2D(4096, 40, device="cuda")  # eager: creates the state
+    s = torch.cuda.Stream()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(g, stream=s):
+            xg, bg = B.sample_random_and_bands2D(4096, 40, device="cuda")
+    torch.cuda.synchronize()
+    g.replay()
+    torch.cuda.synchronize()
+    a = xg.clone()
+    g.replay()
+    torch.cuda.synchronize()
+    assert not torch.equal(a, xg) and not torch.equal(a, x0)
+    assert float(xg.abs().max()) <= 1.0
