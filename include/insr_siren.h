@@ -253,8 +253,9 @@ int insr_adam_step(float* params, const float* grads, float* exp_avg, float* exp
  *                    (a = y, (2n, m) row-major, m >= 2; b = c = d = NULL)
  * The forward reduction is deterministic (fixed order).  Up to 4096 terms it is one
  * launch; beyond, per-block partials go to `work` (insr_sq_loss_work_floats()
- * floats, not shared by concurrent launches) and a second one-block launch combines
- * them in block order.
+ * floats, ZERO-initialised once by the caller, not shared by concurrent launches)
+ * and the last block to finish combines them in block order (same launch; it
+ * leaves the work's ticket word zero again).
  * Backward: g = 2 scale gout r;  ga = alpha g, gb = alpha beta g, gc = gamma g,
  * gd = gamma delta g (bands: ga = the full (2n, m) gradient, zeros outside the
  * selected columns); any output may be NULL (bands: ga required).

@@ -29,7 +29,8 @@ def _workspace(dev):
     if key not in _WORK:
         if torch.cuda.is_current_stream_capturing():
             raise RuntimeError("fused loss workspace must be created before graph capture (run one eager call)")
-        _WORK[key] = torch.empty(nat.lib().insr_sq_loss_work_floats(), device=dev, dtype=torch.float32)
+        # zeros: the tail word is the in-launch combine's ticket (every launch leaves it 0)
+        _WORK[key] = torch.zeros(nat.lib().insr_sq_loss_work_floats(), device=dev, dtype=torch.float32)
     return _WORK[key]
 
 

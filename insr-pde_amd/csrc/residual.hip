@@ -10,8 +10,9 @@
 // hundred KB, so they cost more than they compute.  Here a loss is ONE launch
 // forward (a deterministic reduction in a fixed order) and ONE launch backward (the
 // residual is recomputed, every input gradient written in the same pass).  Losses
-// over more than 4096 terms use a second one-block launch to combine the per-block
-// partials in block order (deterministic, and no cross-XCD fences).
+// over more than 4096 terms combine the per-block partials in the same launch: the
+// last block to finish (an atomic ticket after an agent-scope release fence) sums
+// them in block order (deterministic) and resets the ticket -- no second launch.
 #include "jet_common.hpp"
 
 namespace insr {
@@ -53,9 +54,10 @@ __device__ __forceinline__ float loss_term(int kind, const LossIn& in, long n, i
   return v * v;
 }
 
+// work: kLossMaxBlocks partials + one ticket word (zero-initialised; every launch leaves it 0)
 __global__ __launch_bounds__(kLossThreads) void sq_loss_fwd_kernel(int kind, LossIn in, long n, int m, float scale,
-                                                                   float* __restrict__ out) {
-  // grid == 1: out[0] = scale * sum;  grid > 1: out[block] = partial sum (combined by sq_loss_combine_kernel)
+                                                                   float* __restrict__ out, float* __restrict__ work) {
+  // grid == 1: out[0] = scale * sum;  grid > 1: work[block] = partial sum, the last block combines
   __shared__ float red[kLossThreads / 64];
   const long count = kind == INSR_LOSS_COMBO ? n : 2 * n;
   float acc = 0.f;
@@ -70,15 +72,20 @@ __global__ __launch_bounds__(kLossThreads) void sq_loss_fwd_kernel(int kind, Los
   if (threadIdx.x != 0) return;
   float part = 0.f;
   for (int k = 0; k < kLossThreads / 64; ++k) part += red[k];
-  out[blockIdx.x] = gridDim.x == 1 ? scale * part : part;
-}
-
-__global__ __launch_bounds__(64) void sq_loss_combine_kernel(const float* __restrict__ part, int nb, float scale,
-                                                             float* __restrict__ out) {
-  float acc = 0.f;
-  for (int k = threadIdx.x; k < nb; k += 64) acc += part[k];
-  for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off);
-  if (threadIdx.x == 0) out[0] = scale * acc;
+  if (gridDim.x == 1) {
+    out[0] = scale * part;
+    return;
+  }
+  work[blockIdx.x] = part;
+  __threadfence();  // release this block's partial before taking a ticket
+  unsigned* ticket = reinterpret_cast<unsigned*>(work + kLossMaxBlocks);
+  if (atomicAdd(ticket, 1u) != gridDim.x - 1) return;
+  __threadfence();  // acquire: every other block's partial is visible
+  float tot = 0.f;
+  for (unsigned k = 0; k < gridDim.x; ++k)  // block order: the sum is deterministic
+    tot += __hip_atomic_load(work + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  out[0] = scale * tot;
+  atomicExch(ticket, 0u);
 }
 
 __global__ __launch_bounds__(256) void sq_loss_bwd_kernel(int kind, LossIn in, long n, int m, float scale,
@@ -113,7 +120,7 @@ using namespace insr;
 
 extern "C" {
 
-long insr_sq_loss_work_floats(void) { return kLossMaxBlocks; }
+long insr_sq_loss_work_floats(void) { return kLossMaxBlocks + 1; }  // partials + ticket
 
 int insr_sq_loss_fwd(int kind, const float* a, const float* b, const float* c, const float* d, long n, int m,
                      float alpha, float beta, float gamma, float delta, float scale, float* out, float* work,
@@ -129,9 +136,8 @@ int insr_sq_loss_fwd(int kind, const float* a, const float* b, const float* c, c
   if (nb > 1 && !work) return INSR_EINVAL;
   const LossIn in{a, b, c, d, alpha, beta, gamma, delta};
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(sq_loss_fwd_kernel, dim3((unsigned)nb), dim3(kLossThreads), 0, st, kind, in, n, m, scale,
-                     nb > 1 ? work : out);
-  if (nb > 1) hipLaunchKernelGGL(sq_loss_combine_kernel, dim3(1), dim3(64), 0, st, work, (int)nb, scale, out);
+  hipLaunchKernelGGL(sq_loss_fwd_kernel, dim3((unsigned)nb), dim3(kLossThreads), 0, st, kind, in, n, m, scale, out,
+                     work);
   return (int)hipGetLastError();
 }
 
