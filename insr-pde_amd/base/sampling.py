@@ -12,7 +12,7 @@ import torch
 _AFFINE = {}  # (N, side-key, epsilon, device) -> (scale, shift) constant tensors
 
 __all__ = ["sample_uniform", "sample_random", "sample_boundary", "sample_boundary2D_separate",
-           "sample_boundary2D_pair", "sample_random_and_bands2D", "merge_samples"]
+           "sample_boundary2D_pair", "sample_random_and_bands2D", "sample_boxes", "merge_samples"]
 
 
 def sample_uniform(resolution, sdim=1, device="cpu", flatten=True):
@@ -142,3 +142,27 @@ def sample_random_and_bands2D(N, n_band, epsilon=1e-4, device="cuda"):
     nat.check(nat.lib().insr_sample_boxes(boxes, 5, 2, seed, nat.ptr(state), nat.stream_of(dev)),
               "insr_sample_boxes")
     return x, bxy
+
+
+def sample_boxes(boxes, dim, device="cuda"):
+    """ONE device launch drawing every box of an iteration into one (sum n, dim) tensor,
+    rows in box order: boxes = [(n, lo[dim], hi[dim]), ...], coordinate j of box k uniform
+    in [lo[j], hi[j]) (insr_sample_boxes, the device stream of sample_random_and_bands2D)."""
+    from . import _native as nat
+    dev = torch.device(device)
+    if dev.type != "cuda":
+        raise nat.NativeUnavailable("sample_boxes draws on the GPU only")
+    if not 1 <= len(boxes) <= nat.MAX_BOXES:
+        raise ValueError(f"sample_boxes: 1..{nat.MAX_BOXES} boxes")
+    state, seed = _sampler(dev)
+    out = torch.empty(sum(int(b[0]) for b in boxes), dim, device=dev)
+    f3 = nat._F * 3
+    arr = (nat.Box * len(boxes))()
+    row = 0
+    for k, (n, lo, hi) in enumerate(boxes):
+        pad = [0.0] * (3 - dim)
+        arr[k] = nat.Box(out.data_ptr() + 4 * dim * row, int(n), f3(*(list(lo) + pad)), f3(*(list(hi) + pad)))
+        row += int(n)
+    nat.check(nat.lib().insr_sample_boxes(arr, len(boxes), dim, seed, nat.ptr(state), nat.stream_of(dev)),
+              "insr_sample_boxes")
+    return out

@@ -5,7 +5,8 @@ import os
 import numpy as np
 import torch
 
-from base import BaseModel, fused_mse, gradient, merge_samples, sample_boundary, sample_random, sample_uniform
+from base import (BaseModel, fused_forwards, fused_mse, gradient, merge_samples, sample_boundary, sample_boxes,
+                  sample_random, sample_uniform)
 
 from .examples import get_examples
 
@@ -57,20 +58,35 @@ class Advection1DModel(BaseModel):
     @BaseModel._training_loop
     def _advect(self):
         """advection/model.py:68-91 (midpoint rule + Dirichlet band term)."""
-        x = self._sample_in_training()
+        n_bc = max(self._n_interior() // 100, 10)
+        x, xa = self._advect_points(n_bc)
         n = x.shape[0]
-        u0 = self.field_prev(x)
+        # the frozen field at x and the trainable one at [x; band] are independent jets: one
+        # fused launch (insr_siren_jet_fwd_multi; after iteration 0 both run as gradient jets)
+        with fused_forwards():
+            u0 = self.field_prev(x)
+            ua = self.field(xa)  # interior points and the boundary band through ONE jet
         with torch.no_grad():
             u0x = gradient(u0, x)
-        # interior points and the boundary band through ONE jet launch of the field
-        n_bc = max(self._n_interior() // 100, 10)
-        xb = sample_boundary(n_bc, 1, device=self.device) * self.length / 2
-        xa = merge_samples(x, xb)
-        ua = self.field(xa)
         uxa = gradient(ua, xa)
+        xb = xa[n:]
         # mean(((u - u0)/dt + vel (ux + u0x)/2)^2) over the interior rows, one fused launch each way
         main = fused_mse(ua, u0, uxa, u0x, alpha=1.0 / self.dt, beta=-1.0, gamma=self.vel / 2., delta=1.0, count=n)
         return {'main': main, 'bc': fused_mse(ua, count=xb.shape[0], a_row0=n)}
+
+    def _advect_points(self, n_bc):
+        """(x, xa = [x; boundary band]) of one iteration.  On the GPU one sampler launch
+        (insr_sample_boxes) writes the interior U[-L/2, L/2) and the two half-width-eps bands
+        at +-L/2 (sample_boundary(n_bc, 1) * L/2, base/sampling.py:21-30) straight into xa's
+        rows -- no rand / affine / cat launches; x is a leaf view of xa's interior rows."""
+        if "_sample_in_training" in self.__dict__ or torch.device(self.device).type != "cuda":
+            x = self._sample_in_training()
+            xb = sample_boundary(n_bc, 1, device=self.device) * self.length / 2
+            return x, merge_samples(x, xb)
+        half, eps, n, h = self.length / 2, 1e-4, self._n_interior(), n_bc // 2
+        buf = sample_boxes([(n, [-half], [half]), (h, [(-1 - eps) * half], [(-1 + eps) * half]),
+                            (h, [(1 - eps) * half], [(1 + eps) * half])], 1, device=self.device)
+        return buf[:n].requires_grad_(True), buf.detach().requires_grad_(True)
 
     def write_output(self, output_folder):
         u, grid = self.sample_field(self.vis_resolution, return_samples=True)

@@ -67,7 +67,9 @@ def _worker(rank, world, port, reduction, q):
     m._dp_sync({"main": torch.tensor(0.0)})
     res2 = (m.a.flat_grad_buffer().clone(), m.b.grad_touched(),
             float(m._insr_dp_arena[m.a.param_count:m.a.param_count + m.b.param_count].abs().max()))
-    q.put(res + res2)
+    # plain numpy by value: a queued tensor travels as a shared-memory fd that the parent may
+    # try to fetch after this process has exited (ConnectionResetError)
+    q.put(tuple(v.numpy().copy() if isinstance(v, torch.Tensor) else v for v in res + res2))
     dist.destroy_process_group()
 
 
@@ -80,7 +82,8 @@ def test_dp_sync_two_ranks(reduction, world):
     procs = [ctx.Process(target=_worker, args=(r, world, port, reduction, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = [q.get(timeout=120) for _ in range(world)]
+    res = [tuple(torch.from_numpy(v) if hasattr(v, "dtype") and not isinstance(v, float) else v for v in q.get(timeout=120))
+           for _ in range(world)]
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0

@@ -125,3 +125,34 @@ def test_graph_replay_draws_fresh_points(B):
     torch.cuda.synchronize()
     assert not torch.equal(a, xg) and not torch.equal(a, x0)
     assert float(xg.abs().max()) <= 1.0
+
+
+@pytest.mark.gpu
+def test_sample_boxes_rows_in_box_order(B):
+    out = B.sample_boxes([(5000, [-2.0], [2.0]), (20, [-2.0002], [-1.9998]), (20, [1.9998], [2.0002])], 1)
+    assert out.shape == (5040, 1)
+    o = out.cpu()
+    assert float(o[:5000].min()) >= -2.0 and float(o[:5000].max()) < 2.0 and float(o[:5000].std()) > 1.0
+    assert float((o[5000:5020] + 2.0).abs().max()) <= 2e-4 + 5e-7
+    assert float((o[5020:] - 2.0).abs().max()) <= 2e-4 + 5e-7
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("graph", [False, True])
+def test_advection_device_sampler_phase_runs(B, graph):
+    """advect1D on the GPU draws x and the Dirichlet bands in one launch (rows of one xa
+    buffer) and fuses the frozen / trainable gradient jets; eager and graph replay train."""
+    from pde.advection import Advection1DModel
+    from pde.config import make_config
+    torch.manual_seed(0)
+    cfg = make_config("advection", proj_dir="/tmp/insr_test", insr_progress=False, early_stop=False,
+                      max_n_iters=8, lr=1e-4, insr_graph=graph, insr_sync_every=4, init_cond="example1")
+    model = Advection1DModel(cfg)
+    model.timestep = 1
+    model.initialize()
+    before = model.field.flat_params().detach().clone()
+    model.step()
+    after = model.field.flat_params().detach()
+    assert torch.isfinite(after).all() and not torch.equal(before, after)
+    if graph:
+        assert getattr(model, "_insr_capture_error", None) is None
