@@ -445,7 +445,8 @@ int insr_siren_jet_fwd_multi(const InsrJetJob* jobs, int njobs, int din, int dou
   const int NT = nt_for(W);
   // one fused launch where the x6 forward serves the combined batch; otherwise (another
   // kernel family, a Laplacian jet, a single job) the jobs launch one after another
-  if (live > 1 && mode != INSR_MODE_LAP && use_split_fwd(total, NT) && use_x6(0, NT)) {
+  // (the fused kernel is compiled for widths 64 / 128 / 256)
+  if (live > 1 && mode != INSR_MODE_LAP && NT >= 4 && use_split_fwd(total, NT) && use_x6(0, NT)) {
     // tiles per block from the combined batch; a job whose own batch would take fewer
     // (a boundary band) runs 1-tile blocks, placed first in the grid
     const int T = split_tiles(0, NT, S, total, false);

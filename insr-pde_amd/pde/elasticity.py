@@ -19,7 +19,7 @@ import os
 import numpy as np
 import torch
 
-from base import BaseModel, fused_mse, merge_samples, sample_random, sample_uniform, svd_energy
+from base import BaseModel, fused_forwards, fused_mse, merge_samples, sample_random, sample_uniform, svd_energy
 from base.diff_ops import jacobian_nosync
 
 
@@ -89,11 +89,21 @@ class ElasticityModel(BaseModel):
             if s == 'random':
                 parts.append(sample_random(resolution ** d, d, device=self.device).requires_grad_(True))
             elif s == 'uniform':
-                parts.append(sample_uniform(resolution, d, device=self.device).requires_grad_(True))
+                parts.append(self._uniform_grid(resolution, d))
             else:
                 raise NotImplementedError(s)
         x = torch.cat(parts, dim=0)
         return self._dp_shard(x)
+
+    def _uniform_grid(self, resolution, d):
+        """sample_uniform(resolution, d) -- the same cell-centred grid every iteration (no RNG):
+        built once per (resolution, d) instead of ~5 launches per iteration (a leaf that
+        requires grad, as the reference's; consumers only read it)."""
+        cache = self.__dict__.setdefault("_insr_grids", {})
+        key = (resolution, d)
+        if key not in cache:
+            cache[key] = sample_uniform(resolution, d, device=self.device).requires_grad_(True)
+        return cache[key]
 
     def _sample_fixed_in_training(self, resolution):
         """Points on the x = -1 face (left) and x = +1 face (right); none on a mesh (the
@@ -106,7 +116,7 @@ class ElasticityModel(BaseModel):
             if s == 'random':
                 faces = [sample_random(resolution, d - 1, device=self.device) for _ in range(2)]
             elif s == 'uniform':
-                g = sample_uniform(resolution, d - 1, device=self.device)
+                g = self._uniform_grid(resolution, d - 1).detach()
                 faces = [g, g]
             else:
                 raise NotImplementedError(s)
@@ -161,10 +171,17 @@ class ElasticityModel(BaseModel):
         xa = merge_samples(*parts) if len(parts) > 1 else x
         row_l = n
         row_r = n + (fixed_l.shape[0] if use_l else 0)
+        # the two frozen fields' value jets at x are independent of each other and of the
+        # trainable field's jet: one fused launch for the two value jets (the trainable one,
+        # a Jacobian jet after iteration 0, is grouped by itself)
+        with fused_forwards():
+            with torch.no_grad():
+                f_prev = self.deformation_field_prev(x)
+                f_pp = self.deformation_field_prev_prev(x)
+            fa = self.deformation_field(xa)
         with torch.no_grad():
-            q_prev = self.deformation_field_prev(x) + x
-            q_pp = self.deformation_field_prev_prev(x) + x
-        fa = self.deformation_field(xa)
+            q_prev = f_prev + x
+            q_pp = f_pp + x
         qa = fa + xa
         q = qa if xa is x else qa[:n]
         qdot = (q - q_prev) / dt

@@ -15,7 +15,7 @@ import torch
 pytestmark = pytest.mark.gpu
 
 NETS = {"fluid_vel": (2, 2, 4, 128), "fluid_pres": (2, 1, 4, 128), "advect": (1, 1, 3, 64),
-        "el3d": (3, 3, 5, 256)}
+        "el3d": (3, 3, 5, 256), "w32": (2, 3, 2, 32)}  # width 32: separate launches behind the same entry
 
 
 @pytest.fixture(scope="module")

@@ -19,9 +19,9 @@ for s in ${STEPS:-tests bench prof}; do
   case $s in
     tests) step tests ${TTO:-500} python -m pytest tests -q -m gpu -x ${TESTSEL:+-k "$TESTSEL"} ;;
     smoke) step smoke 200 python -c "import __graft_entry__ as g; g.smoke()" ;;
-    bench) step bench 400 python bench.py --steps ${BSTEPS:-20} --warmup 3 ;;
+    bench) step bench 400 python bench.py --steps ${BSTEPS:-20} --warmup ${BWARM:-3} ;;
     configs) for c in ${CONFIGS:-advect1D elasticity2Dstretch elasticity3Dbunny fluid2DtlgnM}; do
-               step bench_$c 400 python bench.py --config $c --steps ${CSTEPS:-10} --warmup 3 --cpu-seconds 10
+               step bench_$c 400 python bench.py --config $c --steps ${CSTEPS:-10} --warmup ${BWARM:-3} --cpu-seconds 10
              done ;;
     kbench) step kbench 400 python tools/kbench.py --sizes ${KSIZES:-324,2048,8192,16384} --nets ${KNETS:-fluid_pres,fluid_vel} ;;
     dp2)   step dp2 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --backend gloo --steps 5 --warmup 3 --no-cpu-baseline ;;
