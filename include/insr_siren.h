@@ -237,6 +237,15 @@ int insr_adam_step_multi(int count, float* const* params, const float* const* gr
                          float* const* exp_avg_sq, const long* sizes, const float* opt_state, float beta1,
                          float beta2, float eps, int step_offset, void* stream);
 
+/* insr_adam_step_multi (t = opt_state[STEP] + 1) followed by insr_plateau_step(loss,
+ * patience, advance 1) in the SAME launch: the last block to finish runs the scheduler
+ * step (Adam.step() + ReduceLROnPlateau.step(loss), base/baseModel.py:79-81, as one
+ * launch). ticket: one zero-initialised device word per state (left zero). */
+int insr_adam_plateau_step_multi(int count, float* const* params, const float* const* grads,
+                                 float* const* exp_avg, float* const* exp_avg_sq, const long* sizes,
+                                 float* opt_state, float beta1, float beta2, float eps,
+                                 const float* loss, int patience, unsigned* ticket, void* stream);
+
 /* Single-buffer Adam, explicit-prepare convention (t = opt_state[STEP]). */
 int insr_adam_step(float* params, const float* grads, float* exp_avg, float* exp_avg_sq,
                    long count, const float* opt_state, float beta1, float beta2, float eps,

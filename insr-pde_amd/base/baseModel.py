@@ -29,6 +29,11 @@ import torch
 from .networks import get_network
 from .optim import DevicePlateau, FusedAdam
 
+# Adam + plateau step in one launch (insr_adam_plateau_step_multi) with INSR_FUSED_PLATEAU=1.
+# Off by default: measured 0.893 vs 0.890 ms per headline step (profiles/r01/plateau_ab) --
+# inside a graph the removed launch costs less than the last block's serial tail.
+_FUSED_PLATEAU = os.environ.get("INSR_FUSED_PLATEAU", "0") == "1"
+
 try:  # tensorboardX is optional (not installed on the MI355X image)
     from tensorboardX import SummaryWriter
 except Exception:  # pragma: no cover - depends on the environment
@@ -182,6 +187,10 @@ class BaseModel(ABC):
         self.optimizer.zero_grad()
         self._backward(loss_dict)
         synced = self._dp_sync(loss_dict)
+        if (_FUSED_PLATEAU and isinstance(self.optimizer, FusedAdam) and isinstance(self.scheduler, DevicePlateau)
+                and self.scheduler.optimizer is self.optimizer and torch.device(self.device).type == "cuda"):
+            self.optimizer.step(plateau=(self.scheduler, synced['main']))  # one launch for both
+            return synced
         self.optimizer.step()
         if self.scheduler is not None:
             self.scheduler.step(synced['main'])

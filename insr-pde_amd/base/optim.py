@@ -94,10 +94,12 @@ class FusedAdam:
             self._pending_advance = False
 
     @torch.no_grad()
-    def step(self):
+    def step(self, plateau=None):
         """One Adam update of every buffer whose grad exists, in ONE launch.
         Uses t = state[STEP] + 1; the step counter itself is advanced by the
-        scheduler's plateau launch that follows (or lazily, without one)."""
+        scheduler's plateau launch that follows (or lazily, without one).
+        plateau = (DevicePlateau, metric): the scheduler step rides in the same
+        launch (insr_adam_plateau_step_multi) -- what BaseModel._update_network does."""
         import ctypes
         lib = nat.lib()
         self._advance_pending()
@@ -112,14 +114,27 @@ class FusedAdam:
                 bufs.append((p.data, p.grad if p.grad.is_contiguous() else p.grad.contiguous(), m, v))
         b1, b2 = self.betas
         st = nat.stream_of(self.device)
-        for i in range(0, len(bufs), nat.ADAM_MAX_TENSORS):
-            chunk = bufs[i:i + nat.ADAM_MAX_TENSORS]
+        chunks = [bufs[i:i + nat.ADAM_MAX_TENSORS] for i in range(0, len(bufs), nat.ADAM_MAX_TENSORS)]
+        for ci, chunk in enumerate(chunks):
             k = len(chunk)
             arr = lambda j: (ctypes.c_void_p * k)(*[c[j].data_ptr() for c in chunk])  # noqa: E731
             sizes = (ctypes.c_long * k)(*[c[0].numel() for c in chunk])
+            if plateau is not None and ci == len(chunks) - 1:  # the scheduler step rides in the last launch
+                sched, metric = plateau
+                m = sched._metric(metric)
+                if "_ticket" not in self.__dict__:
+                    self._ticket = torch.zeros(1, dtype=torch.int32, device=self.device)
+                nat.check(lib.insr_adam_plateau_step_multi(k, arr(0), arr(1), arr(2), arr(3), sizes,
+                                                           nat.ptr(self.state), b1, b2, self.eps, nat.ptr(m),
+                                                           sched.patience, nat.ptr(self._ticket), st),
+                          "insr_adam_plateau_step_multi")
+                self._pending_advance = False
+                return
             nat.check(lib.insr_adam_step_multi(k, arr(0), arr(1), arr(2), arr(3), sizes, nat.ptr(self.state), b1, b2,
                                                self.eps, 1, st), "insr_adam_step_multi")
         self._pending_advance = True
+        if plateau is not None:  # nothing to update (no grad reached any buffer): the scheduler still steps
+            plateau[0].step(plateau[1])
 
 
 class DevicePlateau:
@@ -133,14 +148,16 @@ class DevicePlateau:
             optimizer.state[nat.OPT_MINLR] = min_lr
         self._scratch = torch.zeros(1, device=optimizer.device)
 
-    def step(self, metrics):
+    def _metric(self, metrics):
+        """The metric as a 1-element fp32 device tensor."""
         if isinstance(metrics, torch.Tensor) and metrics.is_cuda:
             m = metrics.detach().reshape(1)
-            if m.dtype != torch.float32:
-                m = m.float()
-        else:
-            self._scratch.fill_(float(metrics))
-            m = self._scratch
+            return m if m.dtype == torch.float32 else m.float()
+        self._scratch.fill_(float(metrics))
+        return self._scratch
+
+    def step(self, metrics):
+        m = self._metric(metrics)
         opt = self.optimizer
         adv = 1 if opt._pending_advance else 0
         nat.check(nat.lib().insr_plateau_step(nat.ptr(opt.state), nat.ptr(m), self.patience, adv,

@@ -296,30 +296,33 @@ __global__ void adam_prepare_kernel(float* st, float b1, float b2) {
   }
 }
 
-__global__ void plateau_kernel(float* st, const float* loss, int patience, int advance_step) {
-  if (threadIdx.x == 0 && blockIdx.x == 0) {
-    if (advance_step) st[INSR_OPT_STEP] = st[INSR_OPT_STEP] + 1.f;
-    if (!loss) return;  // advance-only (optimiser without a scheduler)
-    const float cur = *loss;
-    float best = st[INSR_OPT_BEST];
-    float bad = st[INSR_OPT_BAD];
-    // torch: a < best * (1 - threshold), threshold = 1e-4 (python double math)
-    if ((double)cur < (double)best * (1.0 - 1e-4)) {
-      best = cur;
-      bad = 0.f;
-    } else {
-      bad += 1.f;
-    }
-    if (bad > (float)patience) {
-      const double old = st[INSR_OPT_LR];
-      double nw = old * (double)st[INSR_OPT_FACTOR];
-      if (nw < (double)st[INSR_OPT_MINLR]) nw = st[INSR_OPT_MINLR];
-      if (old - nw > 1e-8) st[INSR_OPT_LR] = (float)nw;
-      bad = 0.f;
-    }
-    st[INSR_OPT_BEST] = best;
-    st[INSR_OPT_BAD] = bad;
+// plateau scheduler step of one device state (torch ReduceLROnPlateau.step after Adam.step)
+__device__ void plateau_update(float* st, const float* loss, int patience, int advance_step) {
+  if (advance_step) st[INSR_OPT_STEP] = st[INSR_OPT_STEP] + 1.f;
+  if (!loss) return;  // advance-only (optimiser without a scheduler)
+  const float cur = *loss;
+  float best = st[INSR_OPT_BEST];
+  float bad = st[INSR_OPT_BAD];
+  // torch: a < best * (1 - threshold), threshold = 1e-4 (python double math)
+  if ((double)cur < (double)best * (1.0 - 1e-4)) {
+    best = cur;
+    bad = 0.f;
+  } else {
+    bad += 1.f;
   }
+  if (bad > (float)patience) {
+    const double old = st[INSR_OPT_LR];
+    double nw = old * (double)st[INSR_OPT_FACTOR];
+    if (nw < (double)st[INSR_OPT_MINLR]) nw = st[INSR_OPT_MINLR];
+    if (old - nw > 1e-8) st[INSR_OPT_LR] = (float)nw;
+    bad = 0.f;
+  }
+  st[INSR_OPT_BEST] = best;
+  st[INSR_OPT_BAD] = bad;
+}
+
+__global__ void plateau_kernel(float* st, const float* loss, int patience, int advance_step) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) plateau_update(st, loss, patience, advance_step);
 }
 
 struct AdamList {
@@ -337,8 +340,11 @@ struct AdamList {
 // so the bias corrections need no separate prepare launch); torch's op order:
 //   m.lerp_(g, 1-b1); v.mul_(b2).addcmul_(g, g, 1-b2);
 //   p.addcdiv_(m, sqrt(v)/sqrt(1-b2^t) + eps, -lr/(1-b1^t))
-__global__ void adam_multi_kernel(AdamList L, const float* __restrict__ st, float b1, float b2, float eps,
-                                  int step_offset) {
+// plateau != 0: after the update, the last block to finish (atomic ticket; every block read
+// the state before taking it) runs the plateau step in the same launch -- no second launch
+__global__ void adam_multi_kernel(AdamList L, float* __restrict__ st, float b1, float b2, float eps, int step_offset,
+                                  int plateau, const float* __restrict__ loss, int patience,
+                                  unsigned* __restrict__ ticket) {
   __shared__ float sc[2];
   if (threadIdx.x == 0) {
     const double t = (double)st[INSR_OPT_STEP] + (double)step_offset;
@@ -362,6 +368,11 @@ __global__ void adam_multi_kernel(AdamList L, const float* __restrict__ st, floa
     L.v[k][i] = vi;
     const float denom = sqrtf(vi) / bc2s + eps;
     L.p[k][i] = L.p[k][i] - step_size * (mi / denom);
+  }
+  if (!plateau) return;
+  if (threadIdx.x == 0 && atomicAdd(ticket, 1u) == gridDim.x - 1) {  // thread 0 read st above
+    plateau_update(st, loss, patience, 1);
+    atomicExch(ticket, 0u);
   }
 }
 
@@ -638,9 +649,10 @@ int insr_plateau_step(float* st, const float* loss, int patience, int advance_st
   return (int)hipGetLastError();
 }
 
-int insr_adam_step_multi(int count, float* const* params, const float* const* grads, float* const* exp_avg,
-                         float* const* exp_avg_sq, const long* sizes, const float* st, float b1, float b2,
-                         float eps, int step_offset, void* stream) {
+static int adam_launch(int count, float* const* params, const float* const* grads, float* const* exp_avg,
+                       float* const* exp_avg_sq, const long* sizes, float* st, float b1, float b2, float eps,
+                       int step_offset, int plateau, const float* loss, int patience, unsigned* ticket,
+                       void* stream) {
   if (count < 1 || count > INSR_ADAM_MAX_TENSORS || !st) return INSR_EINVAL;
   AdamList L;
   L.count = count;
@@ -658,9 +670,28 @@ int insr_adam_step_multi(int count, float* const* params, const float* const* gr
   if (total == 0) return 0;
   long blocks = (total + 255) / 256;
   if (blocks > 1024) blocks = 1024;
+  if (plateau && blocks > 256) blocks = 256;  // fewer tickets on the one word (grid-stride loop)
   hipLaunchKernelGGL(adam_multi_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, L, st, b1, b2,
-                     eps, step_offset);
+                     eps, step_offset, plateau, loss, patience, ticket);
   return (int)hipGetLastError();
+}
+
+int insr_adam_step_multi(int count, float* const* params, const float* const* grads, float* const* exp_avg,
+                         float* const* exp_avg_sq, const long* sizes, const float* st, float b1, float b2,
+                         float eps, int step_offset, void* stream) {
+  return adam_launch(count, params, grads, exp_avg, exp_avg_sq, sizes, const_cast<float*>(st), b1, b2, eps,
+                     step_offset, 0, nullptr, 0, nullptr, stream);
+}
+
+int insr_adam_plateau_step_multi(int count, float* const* params, const float* const* grads, float* const* exp_avg,
+                                 float* const* exp_avg_sq, const long* sizes, float* st, float b1, float b2,
+                                 float eps, const float* loss, int patience, unsigned* ticket, void* stream) {
+  if (!loss || !ticket) return INSR_EINVAL;
+  long total = 0;
+  for (int k = 0; k < count && k < INSR_ADAM_MAX_TENSORS; ++k) total += sizes ? sizes[k] : 0;
+  if (total == 0) return insr_plateau_step(st, loss, patience, 1, stream);  // no block would run the step
+  return adam_launch(count, params, grads, exp_avg, exp_avg_sq, sizes, st, b1, b2, eps, 1, 1, loss, patience,
+                     ticket, stream);
 }
 
 int insr_adam_step(float* p, const float* g, float* m, float* v, long n, const float* st, float b1, float b2,
