@@ -90,7 +90,8 @@ int insr_siren_jet_fwd(const float* x, long n_points, int d_in, int d_out, int n
  * velocity fields at the same collocation points (fluid/model.py:97-98 and
  * :143-147): a value jet of 16384 points is a latency-bound launch that holds
  * one block per CU, so two side by side cost well under two launches.
- * 1 <= n_jobs <= INSR_MAX_FWD_JOBS; jobs with n == 0 are allowed.
+ * 1 <= n_jobs <= INSR_MAX_FWD_JOBS; jobs with n == 0 are allowed. The output width
+ * may differ per job (InsrJetJob.d_out: e.g. the velocity and pressure fields).
  * Replaces: consecutive MLP.forward calls (base/networks.py:67-71).
  */
 #define INSR_MAX_FWD_JOBS 4
@@ -102,6 +103,7 @@ typedef struct InsrJetJob {
   float* lap;           /* (n, d_out) [LAP] else NULL */
   float* act;           /* insr_jet_act_bytes(n, ...) or NULL (no backward) */
   long n;               /* points of this job */
+  int d_out;            /* this job's output width (1..3); 0 = the call's d_out */
 } InsrJetJob;
 int insr_siren_jet_fwd_multi(const InsrJetJob* jobs, int n_jobs, int d_in, int d_out,
                              int num_hidden, int width, int mode, void* stream);

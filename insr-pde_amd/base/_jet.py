@@ -87,7 +87,7 @@ class _SirenJet(torch.autograd.Function):
             nbytes = lib.insr_jet_act_bytes(n, din, L, W, mode)
             act = torch.empty(max(nbytes // 4, 1), device=dev, dtype=torch.float32)
         if _Fused.pending is not None:  # launched with the other jets of the scope, at its exit
-            _Fused.pending.append(((din, dout, L, W, mode, dev), (x2, flat, y, dy, lap, act, n)))
+            _Fused.pending.append(((din, L, W, mode, dev), (x2, flat, y, dy, lap, act, n, dout)))
         else:
             with _timed("fwd", mode, n, W, (din, dout, L)):
                 rc = lib.insr_siren_jet_fwd(nat.ptr(x2), n, din, dout, L, W, mode, nat.ptr(flat), nat.ptr(y),
@@ -158,7 +158,8 @@ class _Fused:
 class fused_forwards:
     """`with fused_forwards(): a = f(x); b = g(x)` -- the forward jets issued inside the
     scope are launched together at its exit: jets of one architecture and mode go into ONE
-    insr_siren_jet_fwd_multi launch (horizontal fusion, up to MAX_FWD_JOBS per launch),
+    insr_siren_jet_fwd_multi launch (horizontal fusion, up to MAX_FWD_JOBS per launch; the
+    networks' output widths may differ),
     e.g. the frozen previous velocity field and the trainable one at the same collocation
     points (fluid/model.py:97-98, :143-147).  Outputs, autograd nodes and saved streams are
     those of separate calls, bit for bit.  The outputs hold no values until the scope
@@ -185,14 +186,15 @@ def _launch_fused(jobs):
     for key, job in jobs:
         groups.setdefault(key, []).append(job)
     lib = nat.lib()
-    for (din, dout, L, W, mode, dev), js in groups.items():
+    for (din, L, W, mode, dev), js in groups.items():  # output widths may differ per job
         for k in range(0, len(js), nat.MAX_FWD_JOBS):
             chunk = js[k:k + nat.MAX_FWD_JOBS]
             n = sum(j[6] for j in chunk)
+            dout = chunk[0][7]
             arr = (nat.JetJob * len(chunk))(*[
                 nat.JetJob(x2.data_ptr(), flat.data_ptr(), y.data_ptr(), None if dy is None else dy.data_ptr(),
-                           None if lap is None else lap.data_ptr(), None if act is None else act.data_ptr(), nj)
-                for x2, flat, y, dy, lap, act, nj in chunk])
+                           None if lap is None else lap.data_ptr(), None if act is None else act.data_ptr(), nj, dj)
+                for x2, flat, y, dy, lap, act, nj, dj in chunk])
             with _timed("fwd%d" % len(chunk) if len(chunk) > 1 else "fwd", mode, n, W, (din, dout, L)):
                 rc = lib.insr_siren_jet_fwd_multi(arr, len(chunk), din, dout, L, W, mode, nat.stream_of(dev))
             nat.check(rc, "insr_siren_jet_fwd_multi")

@@ -79,7 +79,7 @@ MAX_FWD_JOBS = 4  # INSR_MAX_FWD_JOBS
 
 class JetJob(ctypes.Structure):
     """struct InsrJetJob (include/insr_siren.h): one forward jet of insr_siren_jet_fwd_multi."""
-    _fields_ = [("x", _P), ("params", _P), ("y", _P), ("dy", _P), ("lap", _P), ("act", _P), ("n", _L)]
+    _fields_ = [("x", _P), ("params", _P), ("y", _P), ("dy", _P), ("lap", _P), ("act", _P), ("n", _L), ("d_out", _I)]
 
 
 MAX_BOXES = 8  # INSR_MAX_BOXES

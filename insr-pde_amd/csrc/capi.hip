@@ -443,6 +443,7 @@ int insr_siren_jet_fwd_multi(const InsrJetJob* jobs, int njobs, int din, int dou
   for (int k = 0; k < njobs; ++k) {
     const InsrJetJob& j = jobs[k];
     if (j.n < 0 || j.n > 0x7fffffffL) return INSR_EINVAL;
+    if (j.d_out < 0 || j.d_out > 3) return INSR_EINVAL;
     if (j.n == 0) continue;
     if (!j.x || !j.params || !j.y) return INSR_EINVAL;
     if (mode != INSR_MODE_VALUE && !j.dy) return INSR_EINVAL;
@@ -460,7 +461,9 @@ int insr_siren_jet_fwd_multi(const InsrJetJob* jobs, int njobs, int din, int dou
   if (live > 1 && mode != INSR_MODE_LAP && NT >= 4 && use_split_fwd(total, NT) && use_x6(0, NT)) {
     // tiles per block from the combined batch; a job whose own batch would take fewer
     // (a boundary band) runs 1-tile blocks, placed first in the grid
-    const int T = split_tiles(0, NT, S, total, false);
+    // (W = 128 gradient jets: T = 2 -- the fused kernel is held to 128 VGPRs, two blocks per CU;
+    // measured 50.9 vs 51.9 us for T = 4 at 16384 points, profiles/r01/fwd_minwaves_study)
+    const int T = (NT == 8 && S == 3) ? 2 : split_tiles(0, NT, S, total, false);
     InsrJetJob pk[INSR_MAX_FWD_JOBS];
     int small[INSR_MAX_FWD_JOBS];
     int m = 0;
@@ -474,7 +477,8 @@ int insr_siren_jet_fwd_multi(const InsrJetJob* jobs, int njobs, int din, int dou
   for (int k = 0; k < njobs; ++k) {
     const InsrJetJob& j = jobs[k];
     if (j.n == 0) continue;
-    const int rc = insr_siren_jet_fwd(j.x, j.n, din, dout, L, W, mode, j.params, j.y, j.dy, j.lap, j.act, stream);
+    const int rc = insr_siren_jet_fwd(j.x, j.n, din, j.d_out > 0 ? j.d_out : dout, L, W, mode, j.params, j.y, j.dy,
+                                      j.lap, j.act, stream);
     if (rc) return rc;
   }
   return 0;

@@ -319,11 +319,12 @@ struct FwdJobsX6 {
   int njobs;
 };
 
-// value jets at W = 128: hold the kernel to 128 VGPRs (4 waves per SIMD = two 8-wave blocks
-// per CU), which the TA = 4 body meets on its own (116) and the 1-tile body is scheduled into
+// value and 2-d gradient jets at W = 128: hold the kernel to 128 VGPRs (4 waves per SIMD = two
+// 8-wave blocks per CU), which the value TA = 4 body meets on its own (116), the gradient
+// TA = 2 and the 1-tile bodies are scheduled into without spills
 template <int NT, int S>
 constexpr int x6_multi_min_waves() {
-  return (NT == 8 && S == 1) ? 4 : 1;
+  return (NT == 8 && (S == 1 || S == 3)) ? 4 : 1;
 }
 
 template <int NT, int S, bool LAP, int TA, int TB>
@@ -334,14 +335,15 @@ __global__ __launch_bounds__(X6Geo<NT>::THREADS, (x6_multi_min_waves<NT, S>())) 
 #pragma unroll
   for (int q = 1; q < kFwdJobs; ++q) k += (q < jobs.njobs && b >= jobs.first[q]) ? 1 : 0;
   const InsrJetJob& jb = jobs.job[k];
+  const int dout_k = jb.d_out > 0 ? jb.d_out : dout;
   if constexpr (TA != TB) {
     if (jobs.small[k]) {
-      fwd_x6_block<NT, S, LAP, TB>(jb.x, (int)jb.n, din, dout, L, jb.params, jb.y, jb.dy, jb.lap, jb.act,
+      fwd_x6_block<NT, S, LAP, TB>(jb.x, (int)jb.n, din, dout_k, L, jb.params, jb.y, jb.dy, jb.lap, jb.act,
                                    (b - jobs.first[k]) * TB);
       return;
     }
   }
-  fwd_x6_block<NT, S, LAP, TA>(jb.x, (int)jb.n, din, dout, L, jb.params, jb.y, jb.dy, jb.lap, jb.act,
+  fwd_x6_block<NT, S, LAP, TA>(jb.x, (int)jb.n, din, dout_k, L, jb.params, jb.y, jb.dy, jb.lap, jb.act,
                                (b - jobs.first[k]) * TA);
 }
 

@@ -198,6 +198,19 @@ class Fluid2DModel(BaseModel):
     @BaseModel._training_loop
     def _solve_pressure(self):
         x = self._sample_in_training()
+        if self._fused_pair() and not getattr(self.cfg, "insr_band_stream", False):
+            # the pressure band's gradient jet and the velocity's (detached) gradient jet for
+            # div u are independent: one fused launch (output widths 1 and 2)
+            with fused_forwards():
+                bxy, nb = self._boundary_bands(x.shape[0])
+                p_band = self.pressure_field(bxy)
+                with torch.no_grad():
+                    u = self.velocity_field(x)
+            bc = wall_mse(gradient(p_band, bxy), nb)
+            with torch.no_grad():
+                div_u = divergence(u, x)
+            lap_p = laplace(self.pressure_field(x), x)
+            return {'main': fused_mse(div_u, lap_p), 'bc': bc}
         bc, join_bc = self._fork("insr_band_stream", self._pressure_wall_loss, x.shape[0])
         div_u, join_d = self._fork("insr_nograd_stream", self._velocity_divergence, x)
         lap_p = laplace(self.pressure_field(x), x)

@@ -65,7 +65,7 @@ def _multi(B, nets, xs, mode, saves):
         outs.append((y, dy, act))
         jobs.append(nat.JetJob(x.data_ptr(), net.flat_params().data_ptr(), y.data_ptr(),
                                None if dy is None else dy.data_ptr(), None,
-                               None if act is None else act.data_ptr(), x.shape[0]))
+                               None if act is None else act.data_ptr(), x.shape[0], net.out_features))
     arr = (nat.JetJob * len(jobs))(*jobs)
     n0 = nets[0]
     rc = lib.insr_siren_jet_fwd_multi(arr, len(jobs), n0.in_features, n0.out_features, n0.num_hidden_layers,
@@ -101,6 +101,19 @@ def test_multi_matches_single_launches(B, name, mode, sizes):
     for net, x, save, (y, dy, act) in zip(nets, xs, saves, fused):
         ys, dys, acts = _single(B, net, x, mode, save)
         assert _eq(y, ys) and _eq(dy, dys) and _eq(act, acts, x.shape[0], net.num_hidden_layers + 1), (name, mode, x.shape[0])
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_multi_mixed_output_widths(B, mode):
+    """Jobs of one launch may differ in d_out (the pressure band 2->1 and the velocity 2->2)."""
+    nets = [_net(B, "fluid_pres", 3), _net(B, "fluid_vel", 4), _net(B, "fluid_pres", 5)]
+    g = torch.Generator().manual_seed(8)
+    xs = [(torch.rand(n, 2, generator=g) * 2 - 1).cuda() for n in (324, 16384, 5000)]
+    saves = [True, False, True]
+    fused = _multi(B, nets, xs, mode, saves)
+    for net, x, save, (y, dy, act) in zip(nets, xs, saves, fused):
+        ys, dys, acts = _single(B, net, x, mode, save)
+        assert _eq(y, ys) and _eq(dy, dys) and _eq(act, acts, x.shape[0], net.num_hidden_layers + 1)
 
 
 def test_multi_rejects_bad_arguments(B):
@@ -148,7 +161,7 @@ def _fluid(ph_cfg, fuse, graph):
 
 
 @pytest.mark.parametrize("graph", [False, True])
-@pytest.mark.parametrize("phase", ["_advect_velocity", "_projection"])
+@pytest.mark.parametrize("phase", ["_advect_velocity", "_solve_pressure", "_projection"])
 def test_fluid_phase_fused_equals_unfused(B, phase, graph):
     g = torch.Generator().manual_seed(9)
     xs = [(torch.rand(4096, 2, generator=g) * 2 - 1).cuda() for _ in range(4)]
