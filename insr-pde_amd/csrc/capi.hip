@@ -458,7 +458,10 @@ int insr_siren_jet_fwd_multi(const InsrJetJob* jobs, int njobs, int din, int dou
   // one fused launch where the x6 forward serves the combined batch; otherwise (another
   // kernel family, a Laplacian jet, a single job) the jobs launch one after another
   // (the fused kernel is compiled for widths 64 / 128 / 256)
-  if (live > 1 && mode != INSR_MODE_LAP && NT >= 4 && use_split_fwd(total, NT) && use_x6(0, NT)) {
+  // W = 128 gradient jets fuse only while the batch fits one round of two 2-tile blocks per CU
+  // (at 65,536 + 1,308 points the fused launch measured 4% slower per step than two launches)
+  const bool grad128_big = NT == 8 && S == 3 && total > 2L * 2 * 16 * cu_count() + 4096;
+  if (live > 1 && mode != INSR_MODE_LAP && NT >= 4 && !grad128_big && use_split_fwd(total, NT) && use_x6(0, NT)) {
     // tiles per block from the combined batch; a job whose own batch would take fewer
     // (a boundary band) runs 1-tile blocks, placed first in the grid
     // (W = 128 gradient jets: T = 2 -- the fused kernel is held to 128 VGPRs, two blocks per CU;

@@ -22,7 +22,7 @@ PDE = {
 }
 # insr-pde_amd execution knobs (see base/_loop.py)
 EXEC = dict(insr_sync_every=1, insr_graph=False, insr_progress=True, insr_band_stream=False, insr_nograd_stream=False,
-            insr_fuse_forwards=True)
+            insr_fuse_forwards=os.environ.get("INSR_FUSE_FORWARDS", "1") != "0")
 
 
 def make_config(pde, **overrides):
