@@ -686,6 +686,22 @@ __global__ __launch_bounds__(X6Geo<NT>::THREADS) void jet_bwd_x6(
     }
   };
   load_zk(L);
+  // 1-tile value backward (the boundary bands: latency-bound chains): with X6_BWD_WPF=1 the
+  // W^T rows of layer j-1 are loaded while layer j runs (registers allow it only here: 182
+  // VGPRs before, 250 with).  Off: measured slower, 22.2 -> 23.3 us per band backward
+  // (same-box A/B, profiles/r01/wpf_ab).
+#ifndef X6_BWD_WPF
+#define X6_BWD_WPF 0
+#endif
+  constexpr bool WPF = X6_BWD_WPF && T == 1 && S == 1;
+  floatx4 wpre[WPF ? RPW : 1][WPF ? KC : 1][2];
+  auto load_wt = [&](const float* Wsrc, int i, int kc, floatx4(&dst)[2]) {
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) {
+      dst[0][jj] = Wsrc[(32 * kc + 8 * g + jj) * W + 16 * (rt0 + i) + c];
+      dst[1][jj] = Wsrc[(32 * kc + 8 * g + 4 + jj) * W + 16 * (rt0 + i) + c];
+    }
+  };
   for (int j = L; j >= 0; --j) {
     INSR_STAMP(L - j, 0);
 #pragma unroll
@@ -750,13 +766,27 @@ __global__ __launch_bounds__(X6Geo<NT>::THREADS) void jet_bwd_x6(
     for (int i = 0; i < RPW; ++i)
 #pragma unroll
       for (int kc = 0; kc < KC; ++kc) {
-#pragma unroll
-        for (int jj = 0; jj < 4; ++jj) {
-          wraw[i][kc][0][jj] = Wj[(32 * kc + 8 * g + jj) * W + 16 * (rt0 + i) + c];
-          wraw[i][kc][1][jj] = Wj[(32 * kc + 8 * g + 4 + jj) * W + 16 * (rt0 + i) + c];
+        if constexpr (WPF) {  // prefetched during the layer above (1-tile value backward)
+          if (j < L) {
+            wraw[i][kc][0] = wpre[i][kc][0];
+            wraw[i][kc][1] = wpre[i][kc][1];
+          } else {
+            load_wt(Wj, i, kc, wraw[i][kc]);
+          }
+        } else {
+          load_wt(Wj, i, kc, wraw[i][kc]);
         }
         if constexpr (NG == 1) wt[i][kc] = split_frag(wraw[i][kc][0], wraw[i][kc][1]);
       }
+    if constexpr (WPF) {  // next layer's W^T rows: the strided loads overlap this layer's work
+      if (j > 1) {
+        const float* Wn = prm + hidden_off(din, W, j - 1);
+#pragma unroll
+        for (int i = 0; i < RPW; ++i)
+#pragma unroll
+          for (int kc = 0; kc < KC; ++kc) load_wt(Wn, i, kc, wpre[i][kc]);
+      }
+    }
     floatx4 snp[T][RPW], csp[T][RPW];
     load_sc(j - 1, snp, csp);
     load_zk(j - 1);
