@@ -54,6 +54,10 @@ extern "C" {
 /* Library version (major*10000 + minor*100 + patch). */
 int insr_version(void);
 
+/* Build provenance: the first 16 hex digits of the SHA-256 of the sources the library was
+ * built from (csrc/*.hip and *.hpp in name order, then this header). */
+const char* insr_build_id(void);
+
 /* Number of fp32 parameters of an SIREN(d_in -> W x (L+1) -> d_out). */
 long insr_siren_param_count(int d_in, int d_out, int num_hidden, int width);
 
@@ -145,28 +149,12 @@ int insr_jet_bwd_is_wide(long n_points, int d_in, int width, int mode);
  * Env INSR_WIDE_MIN_WIDTH.  Process-wide tuning/testing knob. */
 int insr_jet_set_wide_min_width(int width);
 
-/* Number of partial-gradient rows insr_siren_jet_bwd writes for n points: one
- * per 64-point wave-tile block, or one per T-tile (16T-point) tile-split block,
- * whichever the backward selects for this size, width and mode. */
+/* Number of partial-gradient rows insr_siren_jet_bwd writes for n points: one per
+ * T-tile (16T-point) block, T as the backward selects for this size, width and mode. */
 int insr_jet_partial_blocks(long n_points, int d_in, int width, int mode);
 
-/* Largest batch (points) served by the tile-split backward of derivative jets
- * (the neurons of a layer split over the waves of a block); larger batches use
- * the wave-tile kernels (width <= 128 only).  The forward and value-jet thresholds
- * are separate (env INSR_SPLIT_MAX_N_FWD, INSR_SPLIT_MAX_N_BWD,
- * INSR_SPLIT_MAX_N_BWD_VALUE). */
-int insr_jet_split_threshold(void);
-
-/* Set all three thresholds to n_points (0 = always wave-tile).  Returns the old
- * backward threshold.  Process-wide tuning/testing knob, not thread-safe. */
-int insr_jet_set_split_threshold(int n_points);
-
-/* All three thresholds: forward, derivative-jet backward, value-jet backward. */
-void insr_jet_get_split_thresholds(int* fwd, int* bwd, int* bwd_value);
-void insr_jet_set_split_thresholds(int fwd, int bwd, int bwd_value);
-
 /* Tiles per tile-split block (1, 2 or 4) the forward (backward != 0: the
- * backward) uses for this batch, or 0 if it uses the wave-tile kernel. */
+ * backward) uses for this batch. */
 int insr_jet_split_tiles(long n_points, int d_in, int width, int mode, int backward);
 
 /* Tile-count policy: force T for forward / backward (0 = auto: the largest T
@@ -238,15 +226,6 @@ int insr_plateau_step(float* opt_state, const float* loss, int patience, int adv
 int insr_adam_step_multi(int count, float* const* params, const float* const* grads, float* const* exp_avg,
                          float* const* exp_avg_sq, const long* sizes, const float* opt_state, float beta1,
                          float beta2, float eps, int step_offset, void* stream);
-
-/* insr_adam_step_multi (t = opt_state[STEP] + 1) followed by insr_plateau_step(loss,
- * patience, advance 1) in the SAME launch: the last block to finish runs the scheduler
- * step (Adam.step() + ReduceLROnPlateau.step(loss), base/baseModel.py:79-81, as one
- * launch). ticket: one zero-initialised device word per state (left zero). */
-int insr_adam_plateau_step_multi(int count, float* const* params, const float* const* grads,
-                                 float* const* exp_avg, float* const* exp_avg_sq, const long* sizes,
-                                 float* opt_state, float beta1, float beta2, float eps,
-                                 const float* loss, int patience, unsigned* ticket, void* stream);
 
 /* Single-buffer Adam, explicit-prepare convention (t = opt_state[STEP]). */
 int insr_adam_step(float* params, const float* grads, float* exp_avg, float* exp_avg_sq,

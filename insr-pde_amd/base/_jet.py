@@ -190,12 +190,14 @@ def _launch_fused(jobs):
         for k in range(0, len(js), nat.MAX_FWD_JOBS):
             chunk = js[k:k + nat.MAX_FWD_JOBS]
             n = sum(j[6] for j in chunk)
+            douts = sorted({j[7] for j in chunk})
             dout = chunk[0][7]
+            key_dout = douts[0] if len(douts) == 1 else tuple(j[7] for j in chunk)  # per-job widths in the timing key
             arr = (nat.JetJob * len(chunk))(*[
                 nat.JetJob(x2.data_ptr(), flat.data_ptr(), y.data_ptr(), None if dy is None else dy.data_ptr(),
                            None if lap is None else lap.data_ptr(), None if act is None else act.data_ptr(), nj, dj)
                 for x2, flat, y, dy, lap, act, nj, dj in chunk])
-            with _timed("fwd%d" % len(chunk) if len(chunk) > 1 else "fwd", mode, n, W, (din, dout, L)):
+            with _timed("fwd%d" % len(chunk) if len(chunk) > 1 else "fwd", mode, n, W, (din, key_dout, L)):
                 rc = lib.insr_siren_jet_fwd_multi(arr, len(chunk), din, dout, L, W, mode, nat.stream_of(dev))
             nat.check(rc, "insr_siren_jet_fwd_multi")
 

@@ -76,8 +76,13 @@ class PhaseLoop:
         return synced
 
     def _capture_graph(self, fn):
+        from .losses import prepare_workspaces
         m = self.m
-        side = torch.cuda.Stream(device=m.device)
+        # one capture stream per model (its loss workspaces are created once, before capture)
+        side = m.__dict__.get("_insr_capture_stream")
+        if side is None:
+            side = m._insr_capture_stream = torch.cuda.Stream(device=m.device)
+        prepare_workspaces(side)
         side.wait_stream(torch.cuda.current_stream(m.device))
         g = torch.cuda.CUDAGraph()
         with torch.cuda.stream(side):

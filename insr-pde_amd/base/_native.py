@@ -28,6 +28,7 @@ _F = ctypes.c_float
 # name -> (restype, argtypes); mirrors include/insr_siren.h one to one
 SIGNATURES = {
     "insr_version": (_I, []),
+    "insr_build_id": (ctypes.c_char_p, []),
     "insr_siren_param_count": (_L, [_I, _I, _I, _I]),
     "insr_siren_supported": (_I, [_I, _I, _I, _I, _I]),
     "insr_jet_act_bytes": (_L, [_L, _I, _I, _I, _I]),
@@ -46,10 +47,6 @@ SIGNATURES = {
     "insr_comm_init": (_I, [_P, _I, _I, _P]),
     "insr_comm_allreduce_sum": (_I, [_P, _P, _L, _P]),
     "insr_comm_destroy": (_I, [_P]),
-    "insr_jet_split_threshold": (_I, []),
-    "insr_jet_set_split_threshold": (_I, [_I]),
-    "insr_jet_get_split_thresholds": (None, [_P, _P, _P]),
-    "insr_jet_set_split_thresholds": (None, [_I, _I, _I]),
     "insr_jet_split_tiles": (_I, [_L, _I, _I, _I, _I]),
     "insr_sq_loss_work_floats": (_L, []),
     "insr_svd_energy_work_floats": (_L, []),
@@ -69,7 +66,6 @@ SIGNATURES = {
     "insr_adam_step_multi": (_I, [_I, _P, _P, _P, _P, _P, _P, _F, _F, _F, _I, _P]),
     "insr_sampler_state_bytes": (_L, []),
     "insr_sample_boxes": (_I, [_P, _I, _I, ctypes.c_ulonglong, _P, _P]),
-    "insr_adam_plateau_step_multi": (_I, [_I, _P, _P, _P, _P, _P, _P, _F, _F, _F, _P, _I, _P, _P]),
     "insr_adam_step": (_I, [_P, _P, _P, _P, _L, _P, _F, _F, _F, _P]),
 }
 
@@ -101,6 +97,25 @@ class NativeError(RuntimeError):
 _lib = None
 _load_error = None
 
+CSRC = os.path.join(os.path.dirname(_HERE), "csrc")
+HEADER = os.path.join(os.path.dirname(os.path.dirname(_HERE)), "include", "insr_siren.h")
+
+
+def source_hash():
+    """What insr_build_id() must return for a library built from the checked-out sources
+    (the recipe of csrc/Makefile's SRC_HASH); None when the sources are not present."""
+    import glob
+    import hashlib
+    names = sorted(os.path.basename(p) for p in glob.glob(os.path.join(CSRC, "*.hip")) +
+                   glob.glob(os.path.join(CSRC, "*.hpp")))
+    if not names or not os.path.exists(HEADER):
+        return None
+    h = hashlib.sha256()
+    for p in [os.path.join(CSRC, n) for n in names] + [HEADER]:
+        with open(p, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
+
 
 def load(path=None):
     """Load (once) and return the CDLL with typed signatures."""
@@ -116,22 +131,17 @@ def load(path=None):
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    want, have = source_hash(), lib.insr_build_id().decode()
+    if want is not None and want != have:
+        _load_error = (f"{p} was built from other sources (build id {have}, checked-out sources {want}): "
+                       "rebuild with `python -c 'import __graft_entry__ as g; g.build()'`")
+        raise NativeUnavailable(_load_error)
     _lib = lib
     return lib
 
 
 def lib():
     return _lib if _lib is not None else load()
-
-
-def get_split_thresholds():
-    v = [ctypes.c_int(), ctypes.c_int(), ctypes.c_int()]
-    lib().insr_jet_get_split_thresholds(*[ctypes.byref(a) for a in v])
-    return tuple(a.value for a in v)
-
-
-def set_split_thresholds(fwd, bwd, bwd_value):
-    lib().insr_jet_set_split_thresholds(int(fwd), int(bwd), int(bwd_value))
 
 
 def get_split_tiles():

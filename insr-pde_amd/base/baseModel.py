@@ -29,11 +29,6 @@ import torch
 from .networks import get_network
 from .optim import DevicePlateau, FusedAdam
 
-# Adam + plateau step in one launch (insr_adam_plateau_step_multi) with INSR_FUSED_PLATEAU=1.
-# Off by default: measured 0.893 vs 0.890 ms per headline step (profiles/r01/plateau_ab) --
-# inside a graph the removed launch costs less than the last block's serial tail.
-_FUSED_PLATEAU = os.environ.get("INSR_FUSED_PLATEAU", "0") == "1"
-
 try:  # tensorboardX is optional (not installed on the MI355X image)
     from tensorboardX import SummaryWriter
 except Exception:  # pragma: no cover - depends on the environment
@@ -187,10 +182,6 @@ class BaseModel(ABC):
         self.optimizer.zero_grad()
         self._backward(loss_dict)
         synced = self._dp_sync(loss_dict)
-        if (_FUSED_PLATEAU and isinstance(self.optimizer, FusedAdam) and isinstance(self.scheduler, DevicePlateau)
-                and self.scheduler.optimizer is self.optimizer and torch.device(self.device).type == "cuda"):
-            self.optimizer.step(plateau=(self.scheduler, synced['main']))  # one launch for both
-            return synced
         self.optimizer.step()
         if self.scheduler is not None:
             self.scheduler.step(synced['main'])
@@ -254,7 +245,8 @@ class BaseModel(ABC):
         for key, net in self._trainable_networks.items():
             save_dict[f'net_{key}'] = {k: v.detach().cpu() for k, v in net.state_dict().items()}
         save_dict['timestep'] = self.timestep
-        if getattr(self, '_dp_rank0', True):
+        d = torch.distributed
+        if not (d.is_available() and d.is_initialized()) or d.get_rank() == 0:  # one writer under DP
             os.makedirs(os.path.dirname(save_path), exist_ok=True)
             torch.save(save_dict, save_path)
 

@@ -18,17 +18,34 @@ import torch
 
 from . import _native as nat
 
-_WORK = {}  # device index -> partials buffer of the (large-n) two-launch reduction
+_WORK = {}  # (device index, stream handle) -> partials buffer of the large-n in-launch reduction
+
+
+def _stream_key(dev, stream=None):
+    s = stream if stream is not None else torch.cuda.current_stream(dev)
+    return (dev.index, s.cuda_stream)
+
+
+def prepare_workspaces(stream):
+    """Create the reduction workspaces of `stream` (before a graph capture on it)."""
+    dev = stream.device
+    for table, floats, zero in ((_WORK, nat.lib().insr_sq_loss_work_floats(), True),
+                                (_SVD_WORK, nat.lib().insr_svd_energy_work_floats(), False)):
+        key = _stream_key(dev, stream)
+        if key not in table:
+            table[key] = (torch.zeros if zero else torch.empty)(floats, device=dev, dtype=torch.float32)
 
 
 def _workspace(dev):
-    """One partials buffer per device (loss launches are ordered on the caller's
-    stream).  Created on the first eager call -- phase loops always run iteration 0
-    eagerly before capturing -- so it lives outside any graph pool."""
-    key = dev.index
+    """One partials buffer per (device, stream): launches on one stream are ordered, launches
+    on two streams (a side-stream band loss next to the interior loss, two models on two
+    streams) never share one.  Created on the first eager call on that stream, or by
+    prepare_workspaces() before a capture -- never inside a capture (a graph-pool buffer)."""
+    key = _stream_key(dev)
     if key not in _WORK:
         if torch.cuda.is_current_stream_capturing():
-            raise RuntimeError("fused loss workspace must be created before graph capture (run one eager call)")
+            raise RuntimeError("fused loss workspace must be created before graph capture "
+                               "(base.losses.prepare_workspaces(stream) or one eager call on the stream)")
         # zeros: the tail word is the in-launch combine's ticket (every launch leaves it 0)
         _WORK[key] = torch.zeros(nat.lib().insr_sq_loss_work_floats(), device=dev, dtype=torch.float32)
     return _WORK[key]
@@ -62,9 +79,8 @@ class _SqLoss(torch.autograd.Function):
     def forward(ctx, kind, n, m, coef, scale, offs, a, b, c, d):
         lib = nat.lib()
         dev = a.device
-        # the partials workspace is needed (and shared per device: one stream at a time) only
-        # by losses over more than kLossPerBlock = 4096 terms; the small boundary-band losses
-        # a model runs on its side stream never touch it
+        # the partials workspace (one per device and stream) is needed only by losses over
+        # more than kLossPerBlock = 4096 terms
         terms = n if kind == nat.LOSS_COMBO else 2 * n
         work = _workspace(dev) if terms > 4096 else None
         out = torch.empty((), device=dev, dtype=torch.float32)
@@ -132,7 +148,7 @@ def wall_mse(y, n, row0=0):
                          (int(row0) * y.shape[1], 0, 0, 0), y, None, None, None)
 
 
-_SVD_WORK = {}  # device index -> partials buffer of the SVD-energy reduction
+_SVD_WORK = {}  # (device index, stream handle) -> partials buffer of the SVD-energy reduction
 
 
 class _SvdEnergy(torch.autograd.Function):
@@ -140,7 +156,7 @@ class _SvdEnergy(torch.autograd.Function):
     def forward(ctx, J, ratio_arap, ratio_volume, n):
         lib = nat.lib()
         dev = J.device
-        key = dev.index
+        key = _stream_key(dev)
         if key not in _SVD_WORK:
             if torch.cuda.is_current_stream_capturing():
                 raise RuntimeError("SVD-energy workspace must be created before graph capture (run one eager call)")

@@ -94,12 +94,10 @@ class FusedAdam:
             self._pending_advance = False
 
     @torch.no_grad()
-    def step(self, plateau=None):
+    def step(self):
         """One Adam update of every buffer whose grad exists, in ONE launch.
         Uses t = state[STEP] + 1; the step counter itself is advanced by the
-        scheduler's plateau launch that follows (or lazily, without one).
-        plateau = (DevicePlateau, metric): the scheduler step rides in the same
-        launch (insr_adam_plateau_step_multi) -- what BaseModel._update_network does."""
+        scheduler's plateau launch that follows (or lazily, without one)."""
         import ctypes
         lib = nat.lib()
         self._advance_pending()
@@ -119,22 +117,9 @@ class FusedAdam:
             k = len(chunk)
             arr = lambda j: (ctypes.c_void_p * k)(*[c[j].data_ptr() for c in chunk])  # noqa: E731
             sizes = (ctypes.c_long * k)(*[c[0].numel() for c in chunk])
-            if plateau is not None and ci == len(chunks) - 1:  # the scheduler step rides in the last launch
-                sched, metric = plateau
-                m = sched._metric(metric)
-                if "_ticket" not in self.__dict__:
-                    self._ticket = torch.zeros(1, dtype=torch.int32, device=self.device)
-                nat.check(lib.insr_adam_plateau_step_multi(k, arr(0), arr(1), arr(2), arr(3), sizes,
-                                                           nat.ptr(self.state), b1, b2, self.eps, nat.ptr(m),
-                                                           sched.patience, nat.ptr(self._ticket), st),
-                          "insr_adam_plateau_step_multi")
-                self._pending_advance = False
-                return
             nat.check(lib.insr_adam_step_multi(k, arr(0), arr(1), arr(2), arr(3), sizes, nat.ptr(self.state), b1, b2,
                                                self.eps, 1, st), "insr_adam_step_multi")
         self._pending_advance = True
-        if plateau is not None:  # nothing to update (no grad reached any buffer): the scheduler still steps
-            plateau[0].step(plateau[1])
 
 
 class DevicePlateau:

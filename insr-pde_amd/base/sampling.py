@@ -102,10 +102,22 @@ def merge_samples(*parts):
 _SAMPLER = {}  # device index -> (Philox stream position on the device, seed)
 
 
+def sampler_seed(torch_seed, rank):
+    """Philox key of the fused sampler: the device's torch seed with the data-parallel rank
+    folded in (golden-ratio stride), so ranks seeded alike (identical weights need it) still
+    draw independent collocation points."""
+    return (int(torch_seed) + int(rank) * 0x9E3779B97F4A7C15) & 0xFFFFFFFFFFFFFFFF
+
+
+def _dp_rank():
+    d = torch.distributed
+    return d.get_rank() if (d.is_available() and d.is_initialized()) else 0
+
+
 def _sampler(dev):
-    """Per-device Philox state of the fused sampler (insr_sample_boxes).  Seeded from the
-    device's torch generator seed (torch.manual_seed / per-rank seeding applies).  Created
-    on the first eager call -- phase loops always run iteration 0 eagerly before capturing."""
+    """Per-device Philox state of the fused sampler (insr_sample_boxes).  Keyed by the
+    device's torch generator seed and the distributed rank.  Created on the first eager
+    call -- phase loops always run iteration 0 eagerly before capturing."""
     from . import _native as nat
     key = dev.index
     if key not in _SAMPLER:
@@ -114,7 +126,7 @@ def _sampler(dev):
         with torch.cuda.device(dev):
             seed = torch.cuda.initial_seed()
         _SAMPLER[key] = (torch.zeros(nat.lib().insr_sampler_state_bytes() // 8, device=dev, dtype=torch.int64),
-                         seed & 0xFFFFFFFFFFFFFFFF)
+                         sampler_seed(seed, _dp_rank()))
     return _SAMPLER[key]
 
 

@@ -22,37 +22,9 @@ int nt_for(int width) {
   return -1;
 }
 
-// Kernel-variant choice.  Batches up to these sizes use the tile-split kernels
-// (jet_split.hpp: the neurons of a layer split over the waves of a block, T
-// 16-point tiles per block); larger ones the wave-tile kernels (jet_wave.hip: one
-// wave per 16 points, all neurons in its registers).  Both write/read the same
-// saved-activation layout, so forward and backward choose independently.  Width
-// 256 is served by the tile-split kernels only (its wave-tile state would not fit
-// the register file).  Env overrides: INSR_SPLIT_MAX_N_FWD / _BWD / _BWD_VALUE.
-static int g_thr[3] = {-1, -1, -1};  // fwd, bwd (S > 1), bwd value
-
 static int env_or(const char* name, int dflt) {
   const char* e = std::getenv(name);
   return e ? std::atoi(e) : dflt;
-}
-
-int split_max_n() {
-  if (g_thr[0] < 0) {
-    g_thr[0] = env_or("INSR_SPLIT_MAX_N_FWD", 1 << 30);
-    g_thr[1] = env_or("INSR_SPLIT_MAX_N_BWD", 1 << 30);
-    g_thr[2] = env_or("INSR_SPLIT_MAX_N_BWD_VALUE", 1 << 30);
-  }
-  return g_thr[1];
-}
-
-bool use_split_fwd(long n, int NT) {
-  split_max_n();
-  return NT > 8 || n <= g_thr[0];
-}
-
-bool use_split_bwd(long n, int S, int NT) {
-  split_max_n();
-  return NT > 8 || n <= (S == 1 ? g_thr[2] : g_thr[1]);
 }
 
 // Tiles per tile-split block.  The largest T in {1, 2, 4} whose LDS fits a CU,
@@ -99,7 +71,7 @@ static int g_wide_min = -1;
 bool use_wide(long n, int S, int NT, bool lap) {
   prec_init();
   if (g_wide_min < 0) g_wide_min = env_or("INSR_WIDE_MIN_WIDTH", 256);
-  if (NT < 8 || g_prec[1] != INSR_PREC_BF16X6 || !use_split_bwd(n, S, NT)) return false;
+  if (NT < 8 || g_prec[1] != INSR_PREC_BF16X6) return false;
   if (16 * NT >= g_wide_min) return true;
   return NT == 8 && lap && n >= 32768 && g_wide_min <= 256;  // Laplacian jets at width 128
 }
@@ -340,11 +312,8 @@ struct AdamList {
 // so the bias corrections need no separate prepare launch); torch's op order:
 //   m.lerp_(g, 1-b1); v.mul_(b2).addcmul_(g, g, 1-b2);
 //   p.addcdiv_(m, sqrt(v)/sqrt(1-b2^t) + eps, -lr/(1-b1^t))
-// plateau != 0: after the update, the last block to finish (atomic ticket; every block read
-// the state before taking it) runs the plateau step in the same launch -- no second launch
-__global__ void adam_multi_kernel(AdamList L, float* __restrict__ st, float b1, float b2, float eps, int step_offset,
-                                  int plateau, const float* __restrict__ loss, int patience,
-                                  unsigned* __restrict__ ticket) {
+__global__ void adam_multi_kernel(AdamList L, const float* __restrict__ st, float b1, float b2, float eps,
+                                  int step_offset) {
   __shared__ float sc[2];
   if (threadIdx.x == 0) {
     const double t = (double)st[INSR_OPT_STEP] + (double)step_offset;
@@ -368,11 +337,6 @@ __global__ void adam_multi_kernel(AdamList L, float* __restrict__ st, float b1, 
     L.v[k][i] = vi;
     const float denom = sqrtf(vi) / bc2s + eps;
     L.p[k][i] = L.p[k][i] - step_size * (mi / denom);
-  }
-  if (!plateau) return;
-  if (threadIdx.x == 0 && atomicAdd(ticket, 1u) == gridDim.x - 1) {  // thread 0 read st above
-    plateau_update(st, loss, patience, 1);
-    atomicExch(ticket, 0u);
   }
 }
 
@@ -406,7 +370,7 @@ int insr_siren_supported(int din, int dout, int L, int W, int mode) { return sha
 long insr_jet_act_bytes(long n, int din, int L, int W, int mode) {
   const int S = streams_for(din, mode);
   if (S < 0 || n < 0) return INSR_EINVAL;
-  const long tiles = ((n + kPts - 1) / kPts) * kWaves;
+  const long tiles = act_tiles(n);
   return (long)(L + 1) * tiles * 16 * W * S * (long)sizeof(float);
 }
 
@@ -425,14 +389,12 @@ int insr_siren_jet_fwd(const float* x, long n, int din, int dout, int L, int W, 
   if (mode == INSR_MODE_LAP && !lap) return INSR_EINVAL;
   const int S = streams_for(din, mode);
   const int NT = nt_for(W);
-  if (use_split_fwd(n, NT) && use_x6(0, NT))
-    return dispatch_fwd_x6(NT, S, mode == INSR_MODE_LAP, split_tiles(0, NT, S, n, mode == INSR_MODE_LAP), x, (int)n, din, dout, L, params,
-                           y, dy, lap, act, (hipStream_t)stream);
-  if (use_split_fwd(n, NT))
-    return dispatch_fwd_split(NT, S, mode == INSR_MODE_LAP, split_tiles(0, NT, S, n, mode == INSR_MODE_LAP), x, (int)n, din, dout, L,
-                              params, y, dy, lap, act, (hipStream_t)stream);
-  return dispatch_fwd_wave(NT, S, mode == INSR_MODE_LAP, x, (int)n, din, dout, L, params, y, dy, lap, act,
-                           (hipStream_t)stream);
+  const bool lapm = mode == INSR_MODE_LAP;
+  if (use_x6(0, NT))
+    return dispatch_fwd_x6(NT, S, lapm, split_tiles(0, NT, S, n, lapm), x, (int)n, din, dout, L, params, y, dy, lap,
+                           act, (hipStream_t)stream);
+  return dispatch_fwd_split(NT, S, lapm, split_tiles(0, NT, S, n, lapm), x, (int)n, din, dout, L, params, y, dy, lap,
+                            act, (hipStream_t)stream);
 }
 
 int insr_siren_jet_fwd_multi(const InsrJetJob* jobs, int njobs, int din, int dout, int L, int W, int mode,
@@ -461,7 +423,7 @@ int insr_siren_jet_fwd_multi(const InsrJetJob* jobs, int njobs, int din, int dou
   // W = 128 gradient jets fuse only while the batch fits one round of two 2-tile blocks per CU
   // (at 65,536 + 1,308 points the fused launch measured 4% slower per step than two launches)
   const bool grad128_big = NT == 8 && S == 3 && total > 2L * 2 * 16 * cu_count() + 4096;
-  if (live > 1 && mode != INSR_MODE_LAP && NT >= 4 && !grad128_big && use_split_fwd(total, NT) && use_x6(0, NT)) {
+  if (live > 1 && mode != INSR_MODE_LAP && NT >= 4 && !grad128_big && use_x6(0, NT)) {
     // tiles per block from the combined batch; a job whose own batch would take fewer
     // (a boundary band) runs 1-tile blocks, placed first in the grid
     // (W = 128 gradient jets: T = 2 -- the fused kernel is held to 128 VGPRs, two blocks per CU;
@@ -496,14 +458,12 @@ int insr_siren_jet_bwd(const float* x, long n, int din, int dout, int L, int W, 
   const long P = insr_jet_partial_stride(din, dout, L, W);  // row stride of the partial rows
   const int S = streams_for(din, mode);
   const int NT = nt_for(W);
-  if (use_split_bwd(n, S, NT) && use_x6(1, NT))
-    return dispatch_bwd_x6(NT, S, mode == INSR_MODE_LAP, split_tiles(1, NT, S, n, mode == INSR_MODE_LAP), x, (int)n, din, dout, L, params,
-                           act, gy, gdy, glap, partial, P, (hipStream_t)stream);
-  if (use_split_bwd(n, S, NT))
-    return dispatch_bwd_split(NT, S, mode == INSR_MODE_LAP, split_tiles(1, NT, S, n, mode == INSR_MODE_LAP), x, (int)n, din, dout, L,
-                              params, act, gy, gdy, glap, partial, P, (hipStream_t)stream);
-  return dispatch_bwd_wave(NT, S, mode == INSR_MODE_LAP, x, (int)n, din, dout, L, params, act, gy, gdy, glap,
-                           partial, P, (hipStream_t)stream);
+  const bool lapm = mode == INSR_MODE_LAP;
+  if (use_x6(1, NT))
+    return dispatch_bwd_x6(NT, S, lapm, split_tiles(1, NT, S, n, lapm), x, (int)n, din, dout, L, params, act, gy, gdy,
+                           glap, partial, P, (hipStream_t)stream);
+  return dispatch_bwd_split(NT, S, lapm, split_tiles(1, NT, S, n, lapm), x, (int)n, din, dout, L, params, act, gy, gdy,
+                            glap, partial, P, (hipStream_t)stream);
 }
 
 int insr_jet_set_wide_min_width(int width) {
@@ -546,7 +506,6 @@ int insr_jet_partial_blocks(long n, int din, int W, int mode) {
   const int S = streams_for(din, mode), NT = nt_for(W);
   if (S < 0 || NT < 0 || n < 0) return INSR_EINVAL;
   if (n == 0) return 0;
-  if (!use_split_bwd(n, S, NT)) return (int)((n + kPts - 1) / kPts);
   const int T = split_tiles(1, NT, S, n, mode == INSR_MODE_LAP);
   return (int)(((n + 15) / 16 + T - 1) / T);
 }
@@ -554,8 +513,7 @@ int insr_jet_partial_blocks(long n, int din, int W, int mode) {
 int insr_jet_split_tiles(long n, int din, int W, int mode, int backward) {
   const int S = streams_for(din, mode), NT = nt_for(W);
   if (S < 0 || NT < 0 || n < 0) return INSR_EINVAL;
-  const bool split = backward ? use_split_bwd(n, S, NT) : use_split_fwd(n, NT);
-  return split ? split_tiles(backward ? 1 : 0, NT, S, n, mode == INSR_MODE_LAP) : 0;
+  return split_tiles(backward ? 1 : 0, NT, S, n, mode == INSR_MODE_LAP);
 }
 
 void insr_jet_set_split_tiles(int fwd_tiles, int bwd_tiles, int min_blocks) {
@@ -582,29 +540,6 @@ void insr_jet_get_precision(int* fwd, int* bwd) {
   prec_init();
   if (fwd) *fwd = g_prec[0];
   if (bwd) *bwd = g_prec[1];
-}
-
-int insr_jet_split_threshold(void) { return split_max_n(); }
-
-int insr_jet_set_split_threshold(int n_points) {
-  const int old = split_max_n();
-  const int v = n_points < 0 ? 0 : n_points;
-  g_thr[0] = g_thr[1] = g_thr[2] = v;
-  return old;
-}
-
-void insr_jet_get_split_thresholds(int* fwd, int* bwd, int* bwd_value) {
-  split_max_n();
-  if (fwd) *fwd = g_thr[0];
-  if (bwd) *bwd = g_thr[1];
-  if (bwd_value) *bwd_value = g_thr[2];
-}
-
-void insr_jet_set_split_thresholds(int fwd, int bwd, int bwd_value) {
-  split_max_n();
-  g_thr[0] = fwd < 0 ? 0 : fwd;
-  g_thr[1] = bwd < 0 ? 0 : bwd;
-  g_thr[2] = bwd_value < 0 ? 0 : bwd_value;
 }
 
 int insr_reduce_partials_strided(const float* partial, int nb, long count, long stride, float* grad, int accumulate,
@@ -656,10 +591,9 @@ int insr_plateau_step(float* st, const float* loss, int patience, int advance_st
   return (int)hipGetLastError();
 }
 
-static int adam_launch(int count, float* const* params, const float* const* grads, float* const* exp_avg,
-                       float* const* exp_avg_sq, const long* sizes, float* st, float b1, float b2, float eps,
-                       int step_offset, int plateau, const float* loss, int patience, unsigned* ticket,
-                       void* stream) {
+int insr_adam_step_multi(int count, float* const* params, const float* const* grads, float* const* exp_avg,
+                         float* const* exp_avg_sq, const long* sizes, const float* st, float b1, float b2,
+                         float eps, int step_offset, void* stream) {
   if (count < 1 || count > INSR_ADAM_MAX_TENSORS || !st) return INSR_EINVAL;
   AdamList L;
   L.count = count;
@@ -677,28 +611,9 @@ static int adam_launch(int count, float* const* params, const float* const* grad
   if (total == 0) return 0;
   long blocks = (total + 255) / 256;
   if (blocks > 1024) blocks = 1024;
-  if (plateau && blocks > 256) blocks = 256;  // fewer tickets on the one word (grid-stride loop)
   hipLaunchKernelGGL(adam_multi_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, L, st, b1, b2,
-                     eps, step_offset, plateau, loss, patience, ticket);
+                     eps, step_offset);
   return (int)hipGetLastError();
-}
-
-int insr_adam_step_multi(int count, float* const* params, const float* const* grads, float* const* exp_avg,
-                         float* const* exp_avg_sq, const long* sizes, const float* st, float b1, float b2,
-                         float eps, int step_offset, void* stream) {
-  return adam_launch(count, params, grads, exp_avg, exp_avg_sq, sizes, const_cast<float*>(st), b1, b2, eps,
-                     step_offset, 0, nullptr, 0, nullptr, stream);
-}
-
-int insr_adam_plateau_step_multi(int count, float* const* params, const float* const* grads, float* const* exp_avg,
-                                 float* const* exp_avg_sq, const long* sizes, float* st, float b1, float b2,
-                                 float eps, const float* loss, int patience, unsigned* ticket, void* stream) {
-  if (!loss || !ticket) return INSR_EINVAL;
-  long total = 0;
-  for (int k = 0; k < count && k < INSR_ADAM_MAX_TENSORS; ++k) total += sizes ? sizes[k] : 0;
-  if (total == 0) return insr_plateau_step(st, loss, patience, 1, stream);  // no block would run the step
-  return adam_launch(count, params, grads, exp_avg, exp_avg_sq, sizes, st, b1, b2, eps, 1, 1, loss, patience,
-                     ticket, stream);
 }
 
 int insr_adam_step(float* p, const float* g, float* m, float* v, long n, const float* st, float b1, float b2,

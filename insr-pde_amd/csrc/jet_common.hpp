@@ -19,21 +19,16 @@
 //   tb_i = w c dhb_i - 2 w^2 s t_i ddhb,   qb = w c ddhb
 // Weight gradients: dW_k = sum_{streams,points} zb_stream (x) h_prev_stream.
 //
-// Layout on the chip ("transposed" orientation, MFMA v_mfma_f32_16x16x4_f32,
-// exact fp32 = the fp32 matrix rate, no xf32 on gfx950):
-//   * a wave owns 16 points = the 16 MFMA columns; neurons are MFMA rows.
-//   * activations of all W neurons x S streams live in VGPRs as floatx4
-//     h[rt][s] (rows 16rt+4g+r, column = point lane&15), which is exactly the
-//     MFMA C/D layout AND the B-operand layout of the next layer, so layers
-//     chain in registers with no LDS round trip.
-//   * weights are the A operand, staged once per layer per block into LDS
-//     (row stride W+8 floats: conflict-free ds_read_b128).
-//   * the forward saves pre-activation streams to HBM in the MFMA-native
-//     layout (each store = one contiguous 1 KiB wave write).
+// Layout on the chip ("transposed" orientation: neurons are MFMA rows, 16 points the
+// 16 MFMA columns; a lane (g = lane >> 4, c = lane & 15) holds rows 4g..4g+3 of a
+// 16-row tile at point c, which is both the MFMA C/D layout and the B-operand layout
+// of the next layer):
+//   * the forward saves pre-activation streams to HBM in that layout (each store =
+//     one contiguous 1 KiB wave write), [layer][16-point tile][stream][row tile][lane][4];
 //   * the backward rebuilds sin/cos from the saved z, runs the sine reverse
-//     lane-locally, and computes dW as an MFMA GEMM over the block's 64
-//     points (operands transposed through LDS), writing one partial gradient
-//     per block; insr_reduce_partials sums them in a fixed order.
+//     lane-locally and forms dW as an MFMA GEMM over points x streams.
+// Kernels: jet_split.hpp (exact fp32 MFMA), jet_x6.hpp (split-bf16, the default),
+// jet_x6w.hip (two-kernel backward for wide nets / large batches).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -49,10 +44,8 @@ typedef float floatx4 __attribute__((ext_vector_type(4)));
 namespace insr {
 
 
-constexpr int kThreads = 256;  // 4 waves
-constexpr int kWaves = 4;
-constexpr int kPts = 64;       // points per block (16 per wave)
-constexpr int kLdp = kPts + 8; // padded row of the point-major LDS planes
+// 16-point tiles of the saved-activation layout for n points (padded to 64 points)
+__host__ __device__ inline long act_tiles(long n) { return ((n + 63) / 64) * 4; }
 
 __device__ __forceinline__ floatx4 mfma4(float a, float b, floatx4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
@@ -307,13 +300,8 @@ static __device__ unsigned long long g_insr_stamps[kStampSlots];
 #endif
 
 // ---------------------------------------------------------------------------
-// launchers (defined in jet_wave.hip / jet_split_fwd.hip / jet_split_bwd.hip)
+// launchers (defined in jet_split_fwd.hip / jet_split_bwd.hip / jet_x6_*.hip / jet_x6w.hip)
 // ---------------------------------------------------------------------------
-int dispatch_fwd_wave(int NT, int S, bool LAP, const float* x, int N, int din, int dout, int L, const float* prm,
-                      float* y, float* dy, float* lap, float* act, hipStream_t st);
-int dispatch_bwd_wave(int NT, int S, bool LAP, const float* x, int N, int din, int dout, int L, const float* prm,
-                      const float* act, const float* gy, const float* gdy, const float* glap, float* part, long P,
-                      hipStream_t st);
 int dispatch_fwd_split(int NT, int S, bool LAP, int T, const float* x, int N, int din, int dout, int L,
                        const float* prm, float* y, float* dy, float* lap, float* act, hipStream_t st);
 int dispatch_bwd_split(int NT, int S, bool LAP, int T, const float* x, int N, int din, int dout, int L,

@@ -87,13 +87,10 @@ __device__ __forceinline__ floatx4 mfma_x6(const Frag3& a, const Frag3& b, float
   return c;
 }
 
-#ifndef X6_MAX_WAVES
-#define X6_MAX_WAVES 8
-#endif
 template <int NT>
 struct X6Geo {
   static constexpr int W = 16 * NT;
-  static constexpr int WV = NT < X6_MAX_WAVES ? NT : X6_MAX_WAVES;  // waves per block
+  static constexpr int WV = NT < 8 ? NT : 8;  // waves per block
   static constexpr int RPW = NT / WV;         // row tiles per wave
   static constexpr int KC = NT / 2;           // 32-deep K chunks of a hidden layer
   static constexpr int LDB = W + 8;           // point row of a bf16 plane (elements): conflict-free b128 reads
@@ -285,18 +282,8 @@ __device__ __forceinline__ void fwd_x6_block(const float* __restrict__ x, int N,
   }
 }
 
-// Minimum waves per SIMD the W = 128 forward is compiled for (4 = at most 128 VGPRs = two
-// 8-wave blocks per CU); 1 = no bound (the compiler's choice).
-#ifndef X6_FWD_MIN_WAVES
-#define X6_FWD_MIN_WAVES 1
-#endif
-template <int NT>
-constexpr int x6_fwd_min_waves() {
-  return NT == 8 ? X6_FWD_MIN_WAVES : 1;
-}
-
 template <int NT, int S, bool LAP, int T>
-__global__ __launch_bounds__(X6Geo<NT>::THREADS, (x6_fwd_min_waves<NT>())) void jet_fwd_x6(
+__global__ __launch_bounds__(X6Geo<NT>::THREADS) void jet_fwd_x6(
     const float* __restrict__ x, int N, int din, int dout, int L, const float* __restrict__ prm,
     float* __restrict__ y, float* __restrict__ dy, float* __restrict__ lap, float* __restrict__ act) {
   fwd_x6_block<NT, S, LAP, T>(x, N, din, dout, L, prm, y, dy, lap, act, blockIdx.x * T);
@@ -457,13 +444,7 @@ __device__ __forceinline__ floatx4 h_from_regs(int s, const floatx4 (&zd)[S - 1]
 // Scheduling fence between the unrolled fragment iterations of the backward: keeps the
 // compiler from hoisting every iteration's LDS reads to the top (register spills);
 // the MFMAs of one iteration still cover the next iteration's reads of the other wave.
-#ifndef X6_NO_FENCE
 #define X6_SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
-#else
-#define X6_SCHED_FENCE() \
-  do {                   \
-  } while (0)
-#endif
 
 // 4x4 transpose across a lane quad (lanes c & ~3 .. c | 3 of one lane group g): in, lane c
 // holds v[r] = M[neuron 4g + r][point c]; out, lane c holds neuron 4g + (c & 3) at points
@@ -497,13 +478,10 @@ __device__ __forceinline__ void put_neuron_major(unsigned short* P, const floatx
   *reinterpret_cast<u32x2*>(p + 2 * PLANE) = u32x2{l0, l1};
 }
 
-// ZT (opt-in, -DX6_ZT): a second, neuron-major image of z-bar ([q][n][16 p]) from which the
-// weight-gradient A operand is one b128 read per plane (instead of 24 u16 column reads of Z),
-// when it does not shrink the stream group.  Measured (profiles/r01/s51): the quad-transposed
-// H stores gain 1-5% on the GRAD / LAP backward at 16384 points; ZT on top costs 4-6% on the
-// LAP backward (extra spills, 50% more LDS traffic per group), gains ~3% only on 1-tile value
-// launches -- so it stays off.  -DX6_NO_HT restores the b16 H stores.
-template <int NT, bool ZT>
+// LDS images of one stream group: Z point-major [q][16 p][W + 8] (the propagation B operand,
+// and the dW A operand through u16 column reads), H neuron-major [q][m][16 p] (the dW B
+// operand, one b128 per plane; written through a quad transpose: one b64 store per plane).
+template <int NT>
 struct X6BwdGeo {
   using G = X6Geo<NT>;
   static constexpr int W = G::W;
@@ -513,36 +491,21 @@ struct X6BwdGeo {
                                                        // column read hit disjoint banks
   static constexpr int HPLANE = W * 16;
   static constexpr int HSET = 3 * HPLANE;
-  static constexpr int ZTSET = ZT ? HSET : 0;
-  static constexpr size_t SET_BYTES = (size_t)(ZSET + HSET + ZTSET) * 2;
+  static constexpr size_t SET_BYTES = (size_t)(ZSET + HSET) * 2;
 };
 
 // streams per LDS group: all S if T tiles of them fit, else S/2, else 1
-template <int NT, int S, int T, bool ZT>
-constexpr int x6_bwd_sg_z() {
-  constexpr size_t set = X6BwdGeo<NT, ZT>::SET_BYTES;
+template <int NT, int S, int T>
+constexpr int x6_bwd_sg() {
+  constexpr size_t set = X6BwdGeo<NT>::SET_BYTES;
   if ((size_t)T * S * set <= kLdsMax) return S;
   if (S % 2 == 0 && (size_t)T * (S / 2) * set <= kLdsMax) return S / 2;
   return 1;
 }
 
 template <int NT, int S, int T>
-constexpr bool x6_bwd_zt() {
-#ifndef X6_ZT
-  return false;
-#else
-  return x6_bwd_sg_z<NT, S, T, true>() == x6_bwd_sg_z<NT, S, T, false>();
-#endif
-}
-
-template <int NT, int S, int T>
-constexpr int x6_bwd_sg() {
-  return x6_bwd_sg_z<NT, S, T, x6_bwd_zt<NT, S, T>()>();
-}
-
-template <int NT, int S, int T>
 constexpr size_t bwd_x6_lds_bytes() {
-  return (size_t)T * x6_bwd_sg<NT, S, T>() * X6BwdGeo<NT, x6_bwd_zt<NT, S, T>()>::SET_BYTES;
+  return (size_t)T * x6_bwd_sg<NT, S, T>() * X6BwdGeo<NT>::SET_BYTES;
 }
 
 template <int NT, int S, bool LAP, int T>
@@ -551,8 +514,7 @@ __global__ __launch_bounds__(X6Geo<NT>::THREADS) void jet_bwd_x6(
     const float* __restrict__ act, const float* __restrict__ gy, const float* __restrict__ gdy,
     const float* __restrict__ glap, float* __restrict__ part, long P) {
   using G = X6Geo<NT>;
-  constexpr bool ZTX = x6_bwd_zt<NT, S, T>();
-  using BG = X6BwdGeo<NT, ZTX>;
+  using BG = X6BwdGeo<NT>;
   constexpr int W = G::W, RPW = G::RPW, KC = G::KC;
   constexpr int LDB = BG::ZROW, ZPLANE = BG::ZPLANE, ZSET = BG::ZSET, HPLANE = BG::HPLANE, HSET = BG::HSET;
   constexpr int NTAN = LAP ? S - 2 : S - 1;
@@ -565,7 +527,6 @@ __global__ __launch_bounds__(X6Geo<NT>::THREADS) void jet_bwd_x6(
   extern __shared__ __attribute__((aligned(16))) float lds_f[];
   unsigned short* Z = reinterpret_cast<unsigned short*>(lds_f);
   unsigned short* H = Z + NSET * ZSET;
-  unsigned short* ZTp = H + NSET * HSET;  // [set][q][n][16 p] when ZTX
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
   const int ntiles = ((N + 63) / 64) * 4;
   const int tile0 = blockIdx.x * T;
@@ -686,15 +647,7 @@ __global__ __launch_bounds__(X6Geo<NT>::THREADS) void jet_bwd_x6(
     }
   };
   load_zk(L);
-  // 1-tile value backward (the boundary bands: latency-bound chains): with X6_BWD_WPF=1 the
-  // W^T rows of layer j-1 are loaded while layer j runs (registers allow it only here: 182
-  // VGPRs before, 250 with).  Off: measured slower, 22.2 -> 23.3 us per band backward
-  // (same-box A/B, profiles/r01/wpf_ab).
-#ifndef X6_BWD_WPF
-#define X6_BWD_WPF 0
-#endif
-  constexpr bool WPF = X6_BWD_WPF && T == 1 && S == 1;
-  floatx4 wpre[WPF ? RPW : 1][WPF ? KC : 1][2];
+  // W^T rows m = 16 rt + c of layer matrix Wsrc, k = n = 32 kc + 8 g + jj (strided L2 loads)
   auto load_wt = [&](const float* Wsrc, int i, int kc, floatx4(&dst)[2]) {
 #pragma unroll
     for (int jj = 0; jj < 4; ++jj) {
@@ -766,27 +719,9 @@ __global__ __launch_bounds__(X6Geo<NT>::THREADS) void jet_bwd_x6(
     for (int i = 0; i < RPW; ++i)
 #pragma unroll
       for (int kc = 0; kc < KC; ++kc) {
-        if constexpr (WPF) {  // prefetched during the layer above (1-tile value backward)
-          if (j < L) {
-            wraw[i][kc][0] = wpre[i][kc][0];
-            wraw[i][kc][1] = wpre[i][kc][1];
-          } else {
-            load_wt(Wj, i, kc, wraw[i][kc]);
-          }
-        } else {
-          load_wt(Wj, i, kc, wraw[i][kc]);
-        }
+        load_wt(Wj, i, kc, wraw[i][kc]);
         if constexpr (NG == 1) wt[i][kc] = split_frag(wraw[i][kc][0], wraw[i][kc][1]);
       }
-    if constexpr (WPF) {  // next layer's W^T rows: the strided loads overlap this layer's work
-      if (j > 1) {
-        const float* Wn = prm + hidden_off(din, W, j - 1);
-#pragma unroll
-        for (int i = 0; i < RPW; ++i)
-#pragma unroll
-          for (int kc = 0; kc < KC; ++kc) load_wt(Wn, i, kc, wpre[i][kc]);
-      }
-    }
     floatx4 snp[T][RPW], csp[T][RPW];
     load_sc(j - 1, snp, csp);
     load_zk(j - 1);
@@ -819,32 +754,13 @@ __global__ __launch_bounds__(X6Geo<NT>::THREADS) void jet_bwd_x6(
             *reinterpret_cast<u32x2*>(pz) = u32x2{h0, h1};
             *reinterpret_cast<u32x2*>(pz + ZPLANE) = u32x2{m0, m1};
             *reinterpret_cast<u32x2*>(pz + 2 * ZPLANE) = u32x2{l0, l1};
-            if constexpr (ZTX) put_neuron_major<HPLANE>(ZTp + u * HSET, hb[t][i][s], col, c);
             floatx4 hs;
             if constexpr (KZ) {
               hs = h_from_regs<S, LAP>(s, zk[t][i], snp[t][i], csp[t][i]);
             } else {
               hs = h_stream<NT, S, LAP>(basep, s, rt0 + i, lane, snp[t][i], csp[t][i]);
             }
-#ifndef X6_NO_HT
             put_neuron_major<HPLANE>(H + u * HSET, hs, col, c);
-#else
-            split3(hs[0], hs[1], h0, m0, l0);
-            split3(hs[2], hs[3], h1, m1, l1);
-            unsigned short* ph = H + u * HSET + col * 16 + c;  // rows m = col + r, point c
-            ph[0] = (unsigned short)h0;
-            ph[16] = (unsigned short)(h0 >> 16);
-            ph[32] = (unsigned short)h1;
-            ph[48] = (unsigned short)(h1 >> 16);
-            ph[HPLANE] = (unsigned short)m0;
-            ph[HPLANE + 16] = (unsigned short)(m0 >> 16);
-            ph[HPLANE + 32] = (unsigned short)m1;
-            ph[HPLANE + 48] = (unsigned short)(m1 >> 16);
-            ph[2 * HPLANE] = (unsigned short)l0;
-            ph[2 * HPLANE + 16] = (unsigned short)(l0 >> 16);
-            ph[2 * HPLANE + 32] = (unsigned short)l1;
-            ph[2 * HPLANE + 48] = (unsigned short)(l1 >> 16);
-#endif
           }
       }
       INSR_STAMP(L - j, 4);
@@ -859,13 +775,7 @@ __global__ __launch_bounds__(X6Geo<NT>::THREADS) void jet_bwd_x6(
 #pragma unroll
         for (int i = 0; i < RPW; ++i) {
           Frag3 af;
-          if constexpr (ZTX) {
-            const unsigned short* pa = ZTp + (live ? u : 0) * HSET + (16 * (rt0 + i) + c) * 16 + p0;
-            const u32x4 zero4 = u32x4{0u, 0u, 0u, 0u};
-            af.h = live ? *reinterpret_cast<const u32x4*>(pa) : zero4;
-            af.m = live ? *reinterpret_cast<const u32x4*>(pa + HPLANE) : zero4;
-            af.l = live ? *reinterpret_cast<const u32x4*>(pa + 2 * HPLANE) : zero4;
-          } else {
+          {
             const unsigned short* pa = Z + (live ? u : 0) * ZSET + p0 * LDB + 16 * (rt0 + i) + c;
             unsigned hh[4], mm[4], ll[4];
 #pragma unroll

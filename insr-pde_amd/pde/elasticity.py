@@ -145,8 +145,24 @@ class ElasticityModel(BaseModel):
 
     @BaseModel._training_loop
     def _initialize(self):
+        """mean(f(x)^2) over the GLOBAL batch (elasticity/model.py:109-117): a sum over this
+        rank's shard / the global element count, so the 'sum' all-reduce of _dp_sync gives
+        the reference's mean at any world size."""
         x = self._sample_in_training(self.sample_resolution_init)
-        return {'main': torch.mean(self.deformation_field(x) ** 2)}
+        y = self.deformation_field(x)
+        world = self._dp_world()
+        if world == 1:
+            return {'main': torch.mean(y ** 2)}
+        count = y.numel() * (world if getattr(self.cfg, "insr_dp_weak", False) else 1)
+        if not getattr(self.cfg, "insr_dp_weak", False):
+            count = self._global_rows(self.sample_resolution_init) * y.shape[1]
+        return {'main': torch.sum(y ** 2) / count}
+
+    def _global_rows(self, resolution):
+        """Rows of the global draw _sample_in_training shards."""
+        if self.use_mesh:
+            return sum(resolution ** self.dim if s == 'random' else self.mesh_V.shape[0] for s in self.sample_pattern)
+        return len(self.sample_pattern) * resolution ** self.dim
 
     @BaseModel._timestepping
     def step(self):

@@ -11,7 +11,7 @@ HEADER = os.path.join(ROOT, "include", "insr_siren.h")
 
 def declared_symbols():
     txt = open(HEADER).read()
-    return sorted(set(re.findall(r"^\s*(?:int|long|void)\s+(insr_\w+)\s*\(", txt, flags=re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int|long|void|const char\*)\s+(insr_\w+)\s*\(", txt, flags=re.M)))
 
 
 @pytest.fixture(scope="module")
@@ -33,6 +33,12 @@ def test_exports_every_declared_symbol(lib):
         assert isinstance(getattr(lib, name), ctypes._CFuncPtr), name
 
 
+def test_build_id_matches_sources(lib):
+    """The loaded library was built from the checked-out csrc/ + header (load() enforces it)."""
+    from base import _native as nat
+    assert lib.insr_build_id().decode() == nat.source_hash()
+
+
 def test_host_queries(lib):
     assert lib.insr_version() >= 100
     # SURVEY.md §8 parameter counts, verified against the reference MLP
@@ -47,34 +53,25 @@ def test_host_queries(lib):
     # saved activations: (L+1) layers x 16 W floats per 16-point tile x S streams
     assert lib.insr_jet_act_bytes(64, 2, 4, 128, 2) == 5 * 4 * 16 * 128 * 4 * 4
     from base import _native as nat
-    saved, saved_tiles = nat.get_split_thresholds(), nat.get_split_tiles()
+    assert lib.insr_jet_partial_stride(2, 1, 4, 128) == 66564 and lib.insr_jet_partial_stride(2, 2, 4, 128) == 66692
+    assert lib.insr_jet_partial_blocks(0, 2, 128, 2) == 0
+    saved_tiles = nat.get_split_tiles()
     try:
-        old = lib.insr_jet_set_split_threshold(0)          # wave-tile kernels: one row per 64 points
-        assert lib.insr_jet_partial_bytes(65, 2, 1, 4, 128, 2) == 2 * 66564 * 4  # rows padded to 4 floats
-        assert lib.insr_jet_partial_stride(2, 1, 4, 128) == 66564 and lib.insr_jet_partial_stride(2, 2, 4, 128) == 66692
-        assert lib.insr_jet_partial_blocks(65, 2, 128, 2) == 2 and lib.insr_jet_partial_blocks(0, 2, 128, 2) == 0
-        assert lib.insr_jet_split_tiles(65, 2, 128, 2, 1) == 0
-        # width 256 has no wave-tile kernel: always tile-split, one tile per block
-        assert lib.insr_jet_split_tiles(65, 3, 256, 1, 1) == 1
-        assert lib.insr_jet_partial_blocks(65, 3, 256, 1) == 5
-        lib.insr_jet_set_split_threshold(1 << 20)           # tile-split kernels
         nat.set_split_tiles(0, 0, 512)                      # auto T, >= 512 blocks
         assert lib.insr_jet_partial_blocks(65, 2, 128, 2) == 5            # small: T = 1
+        assert lib.insr_jet_partial_bytes(65, 2, 1, 4, 128, 2) == 5 * 66564 * 4  # rows padded to 4 floats
+        assert lib.insr_jet_split_tiles(65, 3, 256, 1, 1) == 1
         # LAP (S=4) at W=128: 70 KB of LDS per tile -> T <= 2; 16384 points = 1024 tiles
         assert lib.insr_jet_split_tiles(16384, 2, 128, 2, 1) == 2
         assert lib.insr_jet_partial_blocks(16384, 2, 128, 2) == 512
         assert lib.insr_jet_split_tiles(16384, 2, 128, 0, 1) == 2         # T=4 would leave 256 blocks
-        assert lib.insr_jet_split_tiles(65536, 2, 128, 0, 1) == 4
         nat.set_split_tiles(1, 4, 512)                      # forced: fwd 1, bwd 4 (capped by LDS)
         assert lib.insr_jet_split_tiles(65536, 2, 128, 0, 0) == 1
         assert lib.insr_jet_split_tiles(65536, 2, 128, 2, 1) == 2
         assert lib.insr_jet_partial_blocks(65536, 2, 128, 2) == 2048
-        lib.insr_jet_set_split_threshold(old)
-        assert lib.insr_jet_split_threshold() == old
     finally:
-        nat.set_split_thresholds(*saved)
         nat.set_split_tiles(*saved_tiles)
-    assert nat.get_split_thresholds() == saved and nat.get_split_tiles() == saved_tiles
+    assert nat.get_split_tiles() == saved_tiles
 
 
 def test_invalid_arguments_rejected_without_launch(lib):

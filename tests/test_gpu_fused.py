@@ -191,29 +191,3 @@ def test_fluid_phase_fused_equals_unfused(B, phase, graph):
     assert out[True][2:] == out[False][2:]
     assert torch.equal(out[True][0], out[False][0]), phase
     assert torch.equal(out[True][1], out[False][1]), phase
-
-
-def test_adam_with_plateau_in_one_launch_equals_two_launches(B):
-    """FusedAdam.step(plateau=(sched, loss)) -- the scheduler step in the Adam launch's last
-    block -- gives the same parameters, moments and lr/step/best/bad state as Adam.step()
-    followed by DevicePlateau.step(loss), including lr reductions (patience 2)."""
-    res = {}
-    for fused in (False, True):
-        nets = [_net(B, "fluid_vel", 1), _net(B, "fluid_pres", 2)]
-        opt = B.FusedAdam([{"params": list(n.parameters()), "lr": 1e-3, "module": n} for n in nets])
-        sched = B.DevicePlateau(opt, factor=0.1, patience=2, min_lr=1e-8)
-        g = torch.Generator().manual_seed(4)
-        for it in range(9):
-            for n in nets:
-                n.flat_grad_buffer().copy_(torch.randn(n.param_count, generator=g).cuda())
-            loss = torch.tensor([1.0 if it < 3 else 2.0], device="cuda")  # plateaus from iteration 3
-            if fused:
-                opt.step(plateau=(sched, loss))
-            else:
-                opt.step()
-                sched.step(loss)
-        torch.cuda.synchronize()
-        res[fused] = [n.flat_params().detach().clone() for n in nets] + [opt.state.clone()]
-    for a, b in zip(res[False], res[True]):
-        assert torch.equal(a, b)
-    assert float(res[True][-1][B._native.OPT_LR]) < 1e-3  # the plateau did reduce the lr

@@ -28,22 +28,18 @@ NETS = {  # name: (d_in, d_out, L, W)
 }
 
 
-BIG = 1 << 30
 F32, X6 = 0, 1  # matrix-core precision of the tile-split kernels (insr_jet_set_precision)
-VARIANTS = {  # (fwd, bwd, bwd_value) split thresholds, (fwd, bwd) forced tiles per split block, (fwd, bwd) precision
-    "wave": ((0, 0, 0), (0, 0), (F32, F32)),                  # one wave per 16-point tile, both directions
-    "split": ((BIG, BIG, BIG), (1, 1), (F32, F32)),           # neurons split over a block's waves, 1 tile/block
-    "split_t2": ((BIG, BIG, BIG), (2, 2), (F32, F32)),        # 2 tiles per block (ragged last block)
-    "split_t4": ((BIG, BIG, BIG), (4, 4), (F32, F32)),        # 4 tiles per block (capped by LDS / registers)
-    "split_fwd_wave_bwd": ((BIG, 0, 0), (4, 0), (F32, F32)),  # mixed: the saved-activation layout is shared
-    "wave_fwd_split_bwd": ((0, BIG, BIG), (0, 2), (F32, F32)),
-    "x6": ((BIG, BIG, BIG), (1, 1), (X6, X6)),                # split-bf16 (6-product) matrix cores
-    "x6_t2": ((BIG, BIG, BIG), (2, 2), (X6, X6)),
-    "x6_t4": ((BIG, BIG, BIG), (4, 4), (X6, X6)),
-    "x6_fwd_f32_bwd": ((BIG, BIG, BIG), (4, 2), (X6, F32)),   # precisions mix: same saved layout
-    "f32_fwd_x6_bwd": ((BIG, BIG, BIG), (2, 4), (F32, X6)),
-    "x6_fwd_wave_bwd": ((BIG, 0, 0), (2, 0), (X6, F32)),
-    "x6_wide128": ((BIG, BIG, BIG), (0, 0), (X6, X6), 128),   # two-kernel backward (prop + dW GEMM) from W = 128
+VARIANTS = {  # (fwd, bwd) forced tiles per block, (fwd, bwd) precision[, smallest width of the two-kernel backward]
+    "split": ((1, 1), (F32, F32)),           # exact-fp32 MFMA, neurons split over a block's waves, 1 tile/block
+    "split_t2": ((2, 2), (F32, F32)),        # 2 tiles per block (ragged last block)
+    "split_t4": ((4, 4), (F32, F32)),        # 4 tiles per block (capped by LDS / registers)
+    "x6": ((1, 1), (X6, X6)),                # split-bf16 (6-product) matrix cores (the default precision)
+    "x6_t2": ((2, 2), (X6, X6)),
+    "x6_t4": ((4, 4), (X6, X6)),
+    "x6_fwd_f32_bwd": ((4, 2), (X6, F32)),   # precisions mix: same saved layout
+    "f32_fwd_x6_bwd": ((2, 4), (F32, X6)),
+    "x6_auto": ((0, 0), (X6, X6)),           # the default tile policy
+    "x6_wide128": ((0, 0), (X6, X6), 128),   # two-kernel backward (prop + dW GEMM) from W = 128
 }
 
 
@@ -54,16 +50,14 @@ def base(request):
         pytest.skip("no GPU")
     import base as B
     B._native.load()
-    old, old_tiles = B._native.get_split_thresholds(), B._native.get_split_tiles()
+    old_tiles = B._native.get_split_tiles()
     old_prec = B._native.get_precision()
-    thr, tiles, prec = VARIANTS[request.param][:3]
-    wide = VARIANTS[request.param][3] if len(VARIANTS[request.param]) > 3 else 256
-    B._native.set_split_thresholds(*thr)
+    tiles, prec = VARIANTS[request.param][:2]
+    wide = VARIANTS[request.param][2] if len(VARIANTS[request.param]) > 2 else 256
     B._native.set_split_tiles(tiles[0], tiles[1], old_tiles[2])
     B._native.set_precision(*prec)
     old_wide = B._native.lib().insr_jet_set_wide_min_width(wide)
     yield B
-    B._native.set_split_thresholds(*old)
     B._native.set_split_tiles(*old_tiles)
     B._native.set_precision(*old_prec)
     B._native.lib().insr_jet_set_wide_min_width(old_wide)

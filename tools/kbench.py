@@ -15,18 +15,16 @@ import torch  # noqa: E402
 
 NETS = {"fluid_pres": (2, 1, 4, 128), "fluid_vel": (2, 2, 4, 128), "advect": (1, 1, 3, 64),
         "el2d": (2, 2, 5, 128), "el3d": (3, 3, 5, 256)}
-BIG = 1 << 30
-VARIANTS = {  # label: ((fwd, bwd, bwd_value) thresholds, (fwd, bwd) forced tiles, (fwd, bwd) precision)
-    "wave": ((0, 0, 0), (0, 0), (0, 0)),
-    "split1": ((BIG, BIG, BIG), (1, 1), (0, 0)),
-    "split2": ((BIG, BIG, BIG), (2, 2), (0, 0)),
-    "split4": ((BIG, BIG, BIG), (4, 4), (0, 0)),
-    "auto": ((BIG, BIG, BIG), (0, 0), (0, 0)),
-    "x6": ((BIG, BIG, BIG), (0, 0), (1, 1)),
-    "x6_1": ((BIG, BIG, BIG), (1, 1), (1, 1)),
-    "x6_2": ((BIG, BIG, BIG), (2, 2), (1, 1)),
-    "x6_4": ((BIG, BIG, BIG), (4, 4), (1, 1)),
-    "x6w": ((BIG, BIG, BIG), (0, 0), (1, 1)),  # x6 with the two-kernel backward from width 128
+VARIANTS = {  # label: ((fwd, bwd) forced tiles, (fwd, bwd) precision)
+    "split1": ((1, 1), (0, 0)),
+    "split2": ((2, 2), (0, 0)),
+    "split4": ((4, 4), (0, 0)),
+    "auto": ((0, 0), (0, 0)),
+    "x6": ((0, 0), (1, 1)),
+    "x6_1": ((1, 1), (1, 1)),
+    "x6_2": ((2, 2), (1, 1)),
+    "x6_4": ((4, 4), (1, 1)),
+    "x6w": ((0, 0), (1, 1)),  # x6 with the two-kernel backward from width 128
 }
 MODES = {"value": 0, "grad": 1, "lap": 2}
 
@@ -81,10 +79,7 @@ def main():
                 g = torch.zeros(P, device="cuda")
                 st = nat.stream_of(x.device)
                 for variant in args.variants.split(","):
-                    thr, tiles, prec = VARIANTS[variant]
-                    if W > 128 and variant == "wave":
-                        continue
-                    nat.set_split_thresholds(*thr)
+                    tiles, prec = VARIANTS[variant]
                     nat.set_split_tiles(tiles[0], tiles[1], 256)
                     nat.set_precision(*prec)
                     lib.insr_jet_set_wide_min_width(128 if variant.endswith("w") else 256)

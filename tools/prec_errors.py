@@ -32,7 +32,6 @@ def main():
     args = ap.parse_args()
     import base
     base._native.load()
-    base._native.set_split_thresholds(1 << 30, 1 << 30, 1 << 30)
     for name in args.nets.split(","):
         din, dout, L, W = NETS[name]
         torch.manual_seed(0)
