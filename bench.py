@@ -19,8 +19,13 @@ Also reported: a roofline object for the dominant kernel (HIP events on its laun
 stream, eager re-run of the same step after the timed region) and a CPU baseline
 (the oracle restatement of the reference's torch graph, timed on this host).
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--scaling strong|weak] [--config NAME]
-       (N > 1: launched by torch.distributed.run, one rank per GPU, RCCL).
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--scaling auto|strong|weak] [--config NAME]
+  N > 1: one rank per GPU over RCCL.  Under torch.distributed.run (WORLD_SIZE set) the ranks
+  are the launcher's; otherwise bench.py starts `python -m torch.distributed.run
+  --nproc-per-node N` itself as a child process (before any GPU call) and exits with its code.
+  --scaling auto (default): strong for elasticity3Dbunny and fluid2DtlgnM (the global batch
+  split over the ranks, BASELINE.md "≥6× strong scaling" configs), weak otherwise.
+  --rehearse: the launcher + process-group plumbing alone on the CPU (gloo), no GPU work.
 """
 import argparse
 import json
@@ -52,30 +57,68 @@ def parse():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", default="fluid2Dtlgn", choices=sorted(WORKLOADS),
                     help="BASELINE.json workload (default: configs[1], the headline)")
-    ap.add_argument("--scaling", choices=["strong", "weak"], default="weak")
+    ap.add_argument("--scaling", choices=["auto", "strong", "weak"], default="auto")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--band-stream", action="store_true", help="fluid: boundary-band jets on a side stream")
     ap.add_argument("--nograd-stream", action="store_true", help="fluid: no-grad jets on a side stream")
-    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the CPU-baseline sample")
+    ap.add_argument("--cpu-seconds", type=float, default=25.0, help="budget of the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--backend", default="nccl", help="nccl (= RCCL) or gloo (functional rehearsal)")
-    return ap.parse_args()
+    ap.add_argument("--rehearse", action="store_true",
+                    help="CPU rehearsal of the multi-rank launch (gloo, no GPU work; tests)")
+    args = ap.parse_args()
+    if args.scaling == "auto":
+        args.scaling = "strong" if args.config in STRONG_CONFIGS else "weak"
+    return args
+
+
+STRONG_CONFIGS = ("elasticity3Dbunny", "fluid2DtlgnM")
+
+
+def launch_ranks(args):
+    """--gpus N > 1 without a launcher: run torch.distributed.run with N local ranks as a CHILD
+    process (nothing here has touched the GPU) and return its exit code."""
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    log("launching " + " ".join(cmd[2:8]) + " ...")
+    return subprocess.call(cmd, env=dict(os.environ, MASTER_ADDR="127.0.0.1"))
 
 
 def setup_dist(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    ndev = torch.cuda.device_count()
-    dev = local % max(ndev, 1)  # >1 rank per GPU only for functional rehearsal (--backend gloo)
-    os.environ["LOCAL_RANK"] = str(dev)
-    torch.cuda.set_device(dev)
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+    if args.rehearse:
+        dev = local
+        if world > 1:
+            dist.init_process_group("gloo")
+    else:
+        ndev = torch.cuda.device_count()
+        dev = local % max(ndev, 1)  # >1 rank per GPU only for functional rehearsal (--backend gloo)
+        os.environ["LOCAL_RANK"] = str(dev)
+        torch.cuda.set_device(dev)
+        if world > 1:
+            if args.backend == "nccl":
+                dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+            else:
+                dist.init_process_group(args.backend)
     if world > 1:
-        if args.backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
-        else:
-            dist.init_process_group(args.backend)
+        assert dist.get_world_size() == args.gpus, (dist.get_world_size(), args.gpus)
+        devs = [None] * world
+        dist.all_gather_object(devs, dev)
+        if args.backend == "nccl" and not args.rehearse:
+            assert len(set(devs)) == world, f"ranks share a GPU: {devs}"
+        args.rank_devices = devs
+    else:
+        args.rank_devices = [dev]
     return world, rank, local
 
 
@@ -320,7 +363,7 @@ def cpu_baseline(config, seconds):
                     circle_center=vec(cfg.collide_circle_x, cfg.collide_circle_y, cfg.collide_circle_z),
                     circle_radius=cfg.collide_circle_radius, external_force_timesteps=cfg.external_force_timesteps)
         full = interior_points(cfg, wl)
-        N = full if full <= 32768 else 16384
+        N = full if full <= 32768 else 16384  # el3D: a slice (per-point cost is independent of N)
         R = cfg.sample_resolution
 
         def one_step():
@@ -331,26 +374,73 @@ def cpu_baseline(config, seconds):
             fixed = [torch.cat([torch.full((R, 1), s), torch.rand(R, d - 1) * 2 - 1], 1) for s in (-1.0, 1.0)]
             O.update_step([f], O.elasticity_loss(f, fp, fpp, x, fixed[0], fixed[1], ecfg), opt)
         pts = N
-        what = f"1 phase x {N} pts" + (f" (slice of the {full}-point batch)" if N < full else "")
+        what = f"1 phase x {N} pts" + (f" (slice of the {full}-point batch; points/s scaled as per-point "
+                                        f"cost independent of the batch size)" if N < full else "")
 
-    one_step()  # warm-up
-    t0 = time.perf_counter()
-    one_step()
-    t1 = time.perf_counter() - t0
-    reps = max(1, int(seconds / max(t1, 1e-3)) - 1)
-    t0 = time.perf_counter()
-    for _ in range(reps):
+    for _ in range(2):  # 2 warm-up iterations, then the median of 10
         one_step()
-    dt = (time.perf_counter() - t0) / reps
+    times = []
+    t_all = time.perf_counter()
+    for _ in range(10):
+        t0 = time.perf_counter()
+        one_step()
+        times.append(time.perf_counter() - t0)
+        if time.perf_counter() - t_all > seconds and len(times) >= 3:  # bounded sample
+            break
+    times.sort()
+    dt = times[len(times) // 2]
     return {"value": round(pts / dt, 1), "unit": "collocation-points/s", "cores": cores, "kind": "port",
-            "sample": f"oracle/siren_oracle.py {config}: {reps} timed iterations ({what}, torch CPU autograd + "
-                      f"Adam), {torch.get_num_threads()} threads, {dt * 1e3:.1f} ms/iter"}
+            "cpu_model": cpu_model(), "statistic": f"median of {len(times)} iterations after 2 warm-up",
+            "sample": f"oracle/siren_oracle.py {config}: {what}, torch CPU autograd + Adam, "
+                      f"{torch.get_num_threads()} threads, median {dt * 1e3:.1f} ms/iter "
+                      f"(min {times[0] * 1e3:.1f}, max {times[-1] * 1e3:.1f})"}
+
+
+def cpu_model():
+    """`lscpu` model name of this host."""
+    try:
+        import subprocess
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for line in out.splitlines():
+            if line.startswith("Model name:"):
+                return line.split(":", 1)[1].strip()
+    except Exception:  # pragma: no cover - depends on the host
+        pass
+    return None
+
+
+def rehearse(args, world, rank):
+    """The multi-rank plumbing on the CPU: barrier-bracketed timed region, max over ranks,
+    one JSON line from rank 0 (no GPU work; value = timed barriers per second)."""
+    for _ in range(args.warmup):
+        if world > 1:
+            dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        if world > 1:
+            dist.barrier()
+    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    if rank == 0:
+        print(json.dumps({"metric": "rehearsal (no GPU work)", "value": round(args.steps / max(float(el), 1e-9), 1),
+                          "unit": "barriers/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                          "scaling": args.scaling, "rank_devices": args.rank_devices,
+                          "process_group": {"backend": "gloo", "world_size": world},
+                          "config": {"workload": args.config}}), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
 
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args))
     world, rank, local = setup_dist(args)
     log(f"world={world} rank={rank}")
+    if args.rehearse:
+        return rehearse(args, world, rank)
     model, cfg, wl, n_local = build_model(args, world, rank)
     nph = len(wl["phases"])
     loops = phase_loops(model, wl)
@@ -386,6 +476,8 @@ def main():
         "config": {"workload": args.config, "model": wl["model"],
                    "points_per_phase_iter": n_all, "phases": nph, "global_batch": n_all,
                    "seq_len": None, "parallelism": f"dp{world}", "graph": not args.no_graph},
+        "process_group": {"backend": args.backend if world > 1 else None, "world_size": world,
+                          "rank_devices": args.rank_devices},
     }
     if not args.no_roofline:  # every rank runs the eager steps (they contain the all-reduce)
         roof = roofline(loops, n_local)

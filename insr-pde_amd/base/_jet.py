@@ -76,7 +76,7 @@ class _SirenJet(torch.autograd.Function):
     def forward(ctx, x2, mode, mlp, save, *params):
         lib = nat.lib()
         n, din = x2.shape
-        L, W, dout = mlp.num_hidden_layers, mlp.hidden_features, mlp.out_features
+        L, W, dout = mlp.num_hidden_layers, mlp.kernel_width, mlp.out_features
         flat = mlp.flat_params()
         dev = x2.device
         y = torch.empty(n, dout, device=dev, dtype=torch.float32)
@@ -117,7 +117,7 @@ class _SirenJet(torch.autograd.Function):
             return none
         x2, act = ctx.x2, ctx.act
         n, din = x2.shape
-        L, W, dout = mlp.num_hidden_layers, mlp.hidden_features, mlp.out_features
+        L, W, dout = mlp.num_hidden_layers, mlp.kernel_width, mlp.out_features
         lib = nat.lib()
         gflat, accumulate = mlp.grad_for_backward()
         c = lambda t: None if t is None else (t if t.is_contiguous() else t.contiguous())  # noqa: E731
@@ -208,9 +208,9 @@ def run_jet(mlp, x, mode):
     mlp.ensure_packed()
     din = mlp.in_features
     lib = nat.lib()
-    if not lib.insr_siren_supported(din, mlp.out_features, mlp.num_hidden_layers, mlp.hidden_features, mode):
+    if not lib.insr_siren_supported(din, mlp.out_features, mlp.num_hidden_layers, mlp.kernel_width, mode):
         raise UnsupportedPattern(
-            f"no HIP kernel for SIREN(in={din}, out={mlp.out_features}, width={mlp.hidden_features}) "
+            f"no HIP kernel for SIREN(in={din}, out={mlp.out_features}, width={mlp.kernel_width}) "
             f"in {MODE_NAMES[mode]} mode")
     x2, lead = _flatten_x(x, din)
     params = tuple(mlp.parameters())
@@ -262,7 +262,7 @@ class call_scope:
 
 def _supported(mlp, mode):
     return bool(nat.lib().insr_siren_supported(mlp.in_features, mlp.out_features, mlp.num_hidden_layers,
-                                               mlp.hidden_features, mode))
+                                               mlp.kernel_width, mode))
 
 
 def siren_value(mlp, x):

@@ -10,6 +10,15 @@ What differs is storage and execution:
   * all parameters are views into ONE flat fp32 buffer in state_dict order --
     the layout the HIP kernels and the fused Adam consume directly (see
     include/insr_siren.h); `.grad` tensors are views into one flat gradient;
+  * any hidden width W <= 256 is served: the kernels are compiled for widths
+    32 / 64 / 128 / 256, and a net of another width (the paper scripts use 20, 66
+    and 68: scripts/advect1D.sh:5, elasticity3Dbunny.sh:4, elasticity2Dstretch.sh:4)
+    is stored ZERO-PADDED to the next compiled width Wp: the flat buffer has the
+    layout of an SIREN of width Wp, and each parameter is the (W-row, W-column)
+    corner view of its padded block.  Padding is exact: a padded neuron has zero
+    weights and bias, so z = 0, sin(0) = 0 and every derivative stream is 0; its
+    outgoing weights are 0, so it adds nothing downstream; every padded gradient
+    entry is exactly 0, so Adam leaves the padding at 0;
   * `forward` runs the fused HIP jet kernel (value stream) instead of the
     aten addmm/sin chain, and tags its output with its provenance so the
     diff ops (base/diff_ops.py) can dispatch derivative jets.
@@ -58,6 +67,17 @@ def _first_layer_sine_init(m):
             m.weight.uniform_(-1 / fan_in, 1 / fan_in)
 
 
+KERNEL_WIDTHS = (32, 64, 128, 256)  # hidden widths the HIP jets are compiled for
+
+
+def kernel_width(width):
+    """The compiled width a net of hidden width `width` runs at (zero-padded up to it)."""
+    for w in KERNEL_WIDTHS:
+        if width <= w:
+            return w
+    raise NotImplementedError(f"hidden width {width} > {KERNEL_WIDTHS[-1]}: no HIP kernel")
+
+
 class MLP(nn.Module):
     """SIREN MLP with flat parameter storage and a HIP forward (base/networks.py:30-71)."""
 
@@ -69,6 +89,7 @@ class MLP(nn.Module):
             raise NotImplementedError("insr-pde_amd implements the SIREN ('sine', outermost linear) network")
         self.in_features, self.out_features = in_features, out_features
         self.num_hidden_layers, self.hidden_features = num_hidden_layers, hidden_features
+        self.kernel_width = kernel_width(hidden_features)
         layers = [nn.Linear(in_features, hidden_features), Sine()]
         for _ in range(num_hidden_layers):
             layers += [nn.Linear(hidden_features, hidden_features), Sine()]
@@ -85,32 +106,53 @@ class MLP(nn.Module):
     # ---- flat storage ------------------------------------------------------
     @property
     def param_count(self):
-        return sum(p.numel() for p in self.parameters())
+        """Floats of the flat buffer (= the parameter count, plus the zero padding of a
+        net whose width is not a compiled one)."""
+        W, L, din, dout = self.kernel_width, self.num_hidden_layers, self.in_features, self.out_features
+        return W * din + W + L * (W * W + W) + dout * W + dout
 
     def flat_params(self):
         return self._flat
 
+    def _layout(self):
+        """(offset, padded shape, corner) of every parameter in the flat buffer, in
+        parameters() order: Linear weights are (out, in) row-major blocks of the padded
+        width, biases padded vectors; `corner` = the parameter's own (rows, cols)."""
+        W, din, dout = self.kernel_width, self.in_features, self.out_features
+        out, off = [], 0
+        for i, p in enumerate(self.parameters()):
+            layer = i // 2
+            rows = W if layer <= self.num_hidden_layers else dout
+            cols = din if layer == 0 else W
+            shape = (rows, cols) if p.dim() == 2 else (rows,)
+            out.append((off, shape, tuple(p.shape)))
+            off += int(np.prod(shape))
+        return out
+
+    def _view(self, buf, entry):
+        off, shape, corner = entry
+        block = buf[off:off + int(np.prod(shape))].view(*shape)
+        return block[tuple(slice(0, c) for c in corner)]
+
     def _repack(self):
-        """Move every parameter into one contiguous buffer (Parameter identity kept)."""
+        """Move every parameter into one flat (zero-padded) buffer (Parameter identity kept)."""
         params = list(self.parameters())
         if not params:
             return
         dev, dt = params[0].device, params[0].dtype
-        flat = torch.empty(sum(p.numel() for p in params), device=dev, dtype=dt)
+        lay = self._layout()
+        flat = torch.zeros(self.param_count, device=dev, dtype=dt)
         grads_present = any(p.grad is not None for p in params)
         gflat = torch.zeros_like(flat) if grads_present else None
-        off = 0
-        for p in params:
-            n = p.numel()
-            view = flat[off:off + n].view_as(p)
+        for p, e in zip(params, lay):
+            view = self._view(flat, e)
             view.copy_(p.data)
             p.data = view
             if gflat is not None:
-                gv = gflat[off:off + n].view_as(p)
+                gv = self._view(gflat, e)
                 if p.grad is not None:
                     gv.copy_(p.grad)
                 p.grad = gv
-            off += n
         self._flat = flat
         self._flat_grad = gflat
 
@@ -119,17 +161,15 @@ class MLP(nn.Module):
         self._repack()
         return out
 
+    def _is_view_of(self, t, buf, entry):
+        v = self._view(buf, entry)
+        return t.data_ptr() == v.data_ptr() and t.stride() == v.stride() and t.shape == v.shape
+
     def _is_packed(self):
         params = list(self.parameters())
-        if self._flat is None or not params:
+        if self._flat is None or not params or self._flat.numel() != self.param_count:
             return False
-        base = self._flat.data_ptr()
-        off = 0
-        for p in params:
-            if p.data_ptr() != base + off * p.element_size() or not p.is_contiguous():
-                return False
-            off += p.numel()
-        return off == self._flat.numel()
+        return all(self._is_view_of(p.data, self._flat, e) for p, e in zip(params, self._layout()))
 
     def ensure_packed(self):
         if not self._is_packed():
@@ -145,11 +185,10 @@ class MLP(nn.Module):
         if g is None or g.device != self._flat.device or g.numel() != self._flat.numel():
             g = torch.zeros_like(self._flat)
             self._flat_grad = g
-        off, folded = 0, False
-        for p in params:
-            n = p.numel()
-            if p.grad is None or p.grad.data_ptr() != g.data_ptr() + off * 4:
-                view = g[off:off + n].view_as(p)
+        folded = False
+        for p, e in zip(params, self._layout()):
+            if p.grad is None or not self._is_view_of(p.grad, g, e):
+                view = self._view(g, e)
                 if fold_foreign and p.grad is not None:
                     view.copy_(p.grad)
                     folded = True
@@ -157,7 +196,6 @@ class MLP(nn.Module):
                     view.zero_()
                     folded = True
                 p.grad = view
-            off += n
         return g, folded
 
     def mark_grad_stale(self, set_to_none=True):
@@ -248,5 +286,6 @@ class MLP(nn.Module):
         return out
 
     def extra_repr(self):
+        pad = "" if self.kernel_width == self.hidden_features else f" (kernel width {self.kernel_width}, zero-padded)"
         return (f"in={self.in_features}, out={self.out_features}, hidden_layers={self.num_hidden_layers}, "
-                f"width={self.hidden_features}, backend=hip")
+                f"width={self.hidden_features}{pad}, backend=hip")

@@ -419,9 +419,39 @@ def gen_samplers(base):
     return out
 
 
+def gen_extra(base):
+    """ref_extra.npz: the reference's initial conditions (fluid/examples.py:17-51) on grid +
+    random points (incl. the blend gaps), and more of its samplers (base/sampling.py:4-64)."""
+    sys.path.insert(0, os.path.join(REF, "fluid"))
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("ref_fluid_examples", os.path.join(REF, "fluid", "examples.py"))
+    ex = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(ex)
+    g = torch.Generator().manual_seed(40)
+    grid = base.sample_uniform(64, 2)
+    rnd = torch.rand(4096, 2, generator=g) * 2 - 1
+    gaps = torch.cat([torch.rand(512, 2, generator=g) * 0.2 - 0.1 + 0.05,          # around the (0.05, 0.05) corner
+                      torch.rand(512, 2, generator=g) * 0.1 + 0.7])                 # around p - gap_ = 0.725
+    x = torch.cat([grid, rnd, gaps])
+    out = {"examples/x": x.numpy(),
+           "examples/taylorgreen_multi": ex.taylorgreen_multi_velocity(x).numpy(),
+           "examples/taylorgreen": ex.get_examples("taylorgreen")(x).numpy()}
+    torch.manual_seed(10)
+    out["sampling/bnd2d_v_seed10_20"] = base.sample_boundary2D_separate(20, "vertical").numpy()
+    torch.manual_seed(11)
+    out["sampling/bnd2d_box_seed11_40"] = base.sample_boundary(40, 2).numpy()
+    torch.manual_seed(12)
+    out["sampling/random_seed12_50x3"] = base.sample_random(50, 3).numpy()
+    return out
+
+
 def main():
     torch.set_num_threads(8)
     base = load_reference()
+    if "--extra" in sys.argv:  # initial conditions + more samplers (ref_extra.npz)
+        np.savez_compressed(os.path.join(OUT, "ref_extra.npz"), **gen_extra(base))
+        print("ref_extra.npz", os.path.getsize(os.path.join(OUT, "ref_extra.npz")) / 1e6, "MB")
+        return
     if "--el3d" in sys.argv:  # the 3-D elasticity phase vectors alone (ref_phases_el3d.npz)
         np.savez_compressed(os.path.join(OUT, "ref_phases_el3d.npz"), **gen_elasticity3d(base))
         print("ref_phases_el3d.npz", os.path.getsize(os.path.join(OUT, "ref_phases_el3d.npz")) / 1e6, "MB")

@@ -80,3 +80,106 @@ def test_elasticity3d_jacobian_shard(base):
     assert st == 0
     assert nerr(Jg, Jr) < TOL
     assert nerr(grads(net), grads(ref)) < TOL
+
+
+# ---- fluid2DtlgnM (BASELINE.json configs[4]): 256^2 = 65,536 points, default kernel routing ----
+def test_fluid2dtlgnM_pressure_laplacian_65536(base):
+    """fluid/model.py:110-125 at 256^2 points: the W = 128 Laplacian backward takes the
+    two-kernel path by default at this size (propagation kernel + split-K dW GEMM over
+    K = 65,536 x 4); lap p and d/dtheta mean((g - lap p)^2) vs the oracle."""
+    lib = base._native.lib()
+    assert lib.insr_jet_bwd_is_wide(65536, 2, 128, base._native.MODE_LAP) == 1  # default routing
+    ref, net = pair(base, 2, 1, 4, 128, 31)
+    torch.manual_seed(32)
+    x = torch.rand(65536, 2) * 2 - 1
+    g = torch.randn(65536, 1)
+    xr = x.clone().requires_grad_(True)
+    lr_ = O.op_laplace(ref(xr), xr)
+    ((g - lr_) ** 2).mean().backward()
+    xg = x.cuda().requires_grad_(True)
+    lg = base.laplace(net(xg), xg)
+    ((g.cuda() - lg) ** 2).mean().backward()
+    assert nerr(lg, lr_) < TOL
+    assert nerr(grads(net), grads(ref)) < TOL
+    for (k, a), b in zip(ref.named_parameters(), net.parameters()):  # every tensor on its own
+        ga = a.grad if a.grad is not None else torch.zeros_like(a)
+        gb = b.grad if b.grad is not None else torch.zeros_like(b)
+        if ga.abs().max() > 0:
+            assert nerr(gb, ga) < TOL, k
+
+
+def test_fluid2dtlgnM_velocity_jets_65536(base):
+    """divergence (detached, fluid/model.py:109) and the trainable value + gradient jet of the
+    velocity net (wall terms / projection) at 65,536 points, with parameter gradients."""
+    ref, net = pair(base, 2, 2, 4, 128, 33)
+    x = torch.rand(65536, 2, generator=torch.Generator().manual_seed(34)) * 2 - 1
+    xr = x.clone().requires_grad_(True)
+    dr = O.op_divergence(ref(xr), xr)
+    xg = x.cuda().requires_grad_(True)
+    with torch.no_grad():
+        dg = base.divergence(net(xg), xg)
+    assert nerr(dg, dr) < TOL
+    R = torch.randn(65536, 2, generator=torch.Generator().manual_seed(35))
+    xr = x.clone().requires_grad_(True)
+    yr = ref(xr)
+    Gr = O.op_gradient(yr, xr)
+    ((yr * R).sum() + (Gr * R).sum()).backward()
+    xg = x.cuda().requires_grad_(True)
+    y = net(xg)
+    G = base.gradient(y, xg)
+    ((y * R.cuda()).sum() + (G * R.cuda()).sum()).backward()
+    assert nerr(G, Gr) < TOL and nerr(y, yr) < TOL
+    assert nerr(grads(net), grads(ref)) < TOL
+
+
+def test_taylorgreen_multi_on_device():
+    """pde.examples.taylor_green_multi on the GPU vs the reference's own values
+    (fluid/examples.py:34-51, tests/golden/ref_extra.npz)."""
+    import os
+    import numpy as np
+    from pde.examples import get_examples
+    d = np.load(os.path.join(os.path.dirname(__file__), "golden", "ref_extra.npz"))
+    got = get_examples("taylorgreen_multi")(torch.from_numpy(d["examples/x"]).cuda()).cpu().numpy()
+    want = d["examples/taylorgreen_multi"]
+    assert np.abs(got - want).max() <= 1e-6 * np.abs(want).max()
+
+
+def _fluidM(graph):
+    from pde.config import baseline_config
+    from pde.fluid import Fluid2DModel
+    cfg = baseline_config("fluid2DtlgnM", proj_dir="/tmp/insr_test_m", insr_progress=False, early_stop=False,
+                          max_n_iters=6, insr_graph=graph, insr_sync_every=1)
+    torch.manual_seed(7)
+    m = Fluid2DModel(cfg)
+    m.timestep = 1
+    torch.manual_seed(8)
+    m.velocity_field_prev.load_state_dict({k: v + 1e-3 * torch.randn_like(v)
+                                           for k, v in m.velocity_field.state_dict().items()})
+    return m
+
+
+def test_fluid2dtlgnM_full_phases_graph_equals_eager(base):
+    """One fluid2DtlgnM timestep's three phases at 65,536 points (+ 2 x 654 band points),
+    6 iterations each, device sampler: hipGraph replay equals eager execution bit for bit,
+    every loss finite, and the pressure fit decreasing."""
+    from base import sampling
+    res = {}
+    for graph in (False, True):
+        sampling._SAMPLER.clear()  # the same Philox draws in both runs
+        m = _fluidM(graph)
+        trace = {}
+        for phase in ("_advect_velocity", "_solve_pressure", "_projection"):
+            rec = []
+            m.tb = type("TB", (), {"add_scalars": lambda self, tag, vals, global_step: rec.append(vals)})()
+            getattr(m, phase)()
+            assert getattr(m, "_insr_capture_error", None) is None
+            trace[phase] = rec
+        torch.cuda.synchronize()
+        res[graph] = (m.velocity_field.flat_params().detach().cpu(), m.pressure_field.flat_params().detach().cpu(),
+                      trace)
+    assert torch.equal(res[True][0], res[False][0]) and torch.equal(res[True][1], res[False][1])
+    for phase, rec in res[True][2].items():
+        assert len(rec) == 6 and rec == res[False][2][phase], phase
+        assert all(torch.isfinite(torch.tensor(list(r.values()))).all() for r in rec), phase
+    pres = [r["main"] for r in res[True][2]["_solve_pressure"]]
+    assert pres[-1] < pres[0]

@@ -1,0 +1,106 @@
+"""DevicePlateau + early stop against torch's own scheduler (base/baseModel.py:55-62,
+80-81, 132-134): the device-resident ReduceLROnPlateau follows
+torch.optim.lr_scheduler.ReduceLROnPlateau(factor, patience, min_lr) step for step on a
+scripted loss sequence that crosses the patience, the relative threshold (1e-4) and the
+min_lr clamp; and PhaseLoop stops a phase at the iteration the reference's loop does
+(lr <= 1.1e-8 after ReduceLROnPlateau(factor 0.1, patience 500, min_lr 1e-8))."""
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def B():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import base
+    base._native.load()
+    return base
+
+
+def scripted_losses():
+    seq = [1.0, 0.9, 0.8]                      # improving
+    seq += [0.8 * (1 - 5e-5)] * 3              # below the 1e-4 relative threshold: not an improvement
+    seq += [0.5]                               # improvement
+    seq += [0.5] * 4                           # plateau > patience 3: lr 1e-4 -> 1e-5
+    seq += [0.4, 0.4, 0.4, 0.4, 0.4]           # one improvement, then patience again -> 1e-6
+    seq += [0.4] * 16                          # -> 1e-7 -> 1e-8 -> clamped at min_lr (no further change)
+    return seq
+
+
+def test_device_plateau_follows_torch_scheduler(B):
+    torch.manual_seed(0)
+    net = B.MLP(2, 1, 1, 32, nonlinearity="sine").cuda()
+    opt = B.FusedAdam([{"params": list(net.parameters()), "lr": 1e-4, "module": net}])
+    sched = B.DevicePlateau(opt, factor=0.1, patience=3, min_lr=1e-8)
+    dummy = torch.nn.Parameter(torch.zeros(1))
+    topt = torch.optim.SGD([dummy], lr=1e-4)
+    tsched = torch.optim.lr_scheduler.ReduceLROnPlateau(topt, factor=0.1, patience=3, min_lr=1e-8)
+    lrs, tlrs = [], []
+    for v in scripted_losses():
+        net.flat_grad_buffer().normal_()
+        opt.step()
+        sched.step(torch.tensor([v], device="cuda"))
+        tsched.step(v)
+        st = opt.state.cpu()
+        lrs.append(float(st[B._native.OPT_LR]))
+        tlrs.append(topt.param_groups[0]["lr"])
+        assert int(st[B._native.OPT_BAD]) == tsched.num_bad_epochs
+        assert float(st[B._native.OPT_BEST]) == pytest.approx(tsched.best, rel=1e-7)
+    for a, b in zip(lrs, tlrs):
+        assert a == pytest.approx(b, rel=1e-6)
+    assert min(tlrs) == pytest.approx(1e-8) and len(set(round(math.log10(v)) for v in tlrs)) == 5
+    assert int(opt.state[B._native.OPT_STEP]) == len(lrs)
+
+
+def _expected_stop():
+    """Iteration at which the reference's loop breaks for a constant loss."""
+    dummy = torch.nn.Parameter(torch.zeros(1))
+    topt = torch.optim.SGD([dummy], lr=1e-4)
+    ts = torch.optim.lr_scheduler.ReduceLROnPlateau(topt, factor=0.1, patience=500, min_lr=1e-8)
+    for i in range(10 ** 5):
+        ts.step(0.25)
+        if topt.param_groups[0]["lr"] <= 1.1e-8:
+            return i
+    raise AssertionError
+
+
+@pytest.mark.parametrize("graph", [False, True])
+def test_phase_loop_early_stop(B, graph):
+    from pde.config import make_config
+
+    class Const(B.BaseModel):
+        """A phase whose loss never improves (its gradient is exactly zero)."""
+        def __init__(self, cfg):
+            super().__init__(cfg)
+            self.field = self._create_network(1, 1)
+            self.x = torch.linspace(-1, 1, 64, device=self.device).reshape(-1, 1).requires_grad_(True)
+
+        @property
+        def _trainable_networks(self):
+            return {"field": self.field}
+
+        def _sample_in_training(self):
+            return self.x
+
+        def initialize(self):
+            pass
+
+        def step(self):
+            pass
+
+        @B.BaseModel._training_loop
+        def _fit(self):
+            y = self.field(self._sample_in_training())
+            return {"main": B.fused_mse(y, None, y.detach(), None, gamma=-1.0) + 0.25}
+
+    cfg = make_config("advection", proj_dir="/tmp/insr_test_es", insr_progress=False, max_n_iters=5000,
+                      num_hidden_layers=1, hidden_features=32, insr_graph=graph)
+    torch.manual_seed(0)
+    m = Const(cfg)
+    m._fit()
+    assert m.train_step == _expected_stop() + 1
+    assert m.optimizer.param_groups[0]["lr"] <= 1.1e-8

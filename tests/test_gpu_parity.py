@@ -25,6 +25,10 @@ NETS = {  # name: (d_in, d_out, L, W)
     "el3d_w64": (3, 3, 3, 64),
     "el3d": (3, 3, 5, 256),          # elasticity3D bunny: width 256
     "w256_lap": (2, 1, 2, 256),      # width 256 with the 4-stream Laplacian jet
+    # paper-script widths, zero-padded to the next compiled width (base/networks.py MLP):
+    "advect_w20": (1, 1, 2, 20),     # scripts/advect1D.sh:4-5 (2 x 20)
+    "el2d_w68": (2, 2, 3, 68),       # scripts/elasticity2Dstretch.sh:3-4 (3 x 68)
+    "el3d_w66": (3, 3, 3, 66),       # scripts/elasticity3Dbunny.sh:3-4 (3 x 66)
 }
 
 
@@ -221,3 +225,34 @@ def test_large_batch_default_policy(base, op):
             assert e < TOL, (op, k, e)
     finally:
         base._native.set_split_tiles(*old_tiles)
+
+
+@pytest.mark.parametrize("name", ["advect_w20", "el2d_w68", "el3d_w66"])
+def test_padded_width_adam_keeps_padding_zero(base, name):
+    """A padded net trains like the reference's: the padding's gradient is exactly 0, so
+    Adam (FusedAdam on the flat buffer) leaves it at 0 and the real parameters match the
+    oracle's torch Adam after 3 steps."""
+    din, dout, L, W = NETS[name]
+    ref, net = pair(base, name, seed=21)
+    opt_r = O.OracleAdam(list(ref.parameters()), lr=1e-3)
+    opt = base.FusedAdam([{"params": list(net.parameters()), "lr": 1e-3, "module": net}])
+    for it in range(3):
+        x = torch.rand(300, din, generator=torch.Generator().manual_seed(30 + it)) * 2 - 1
+        xr = x.clone().requires_grad_(True)
+        xg = x.cuda().requires_grad_(True)
+        for p in ref.parameters():
+            p.grad = None
+        (O.op_jacobian(ref(xr), xr)[0] ** 2).sum().backward()
+        opt_r.step()
+        opt.zero_grad()
+        (base.jacobian(net(xg), xg)[0] ** 2).sum().backward()
+        g = net.flat_grad_buffer()
+        opt.step()
+    flat = net.flat_params().detach().cpu()
+    mask = torch.zeros_like(flat, dtype=torch.bool)
+    for p, e in zip(net.parameters(), net._layout()):
+        net._view(mask, e).fill_(True)
+    assert bool((flat[~mask] == 0).all())
+    assert bool((g.detach().cpu()[~mask] == 0).all())
+    for a, b in zip(ref.parameters(), net.parameters()):
+        assert float((a.detach() - b.detach().cpu()).abs().max()) <= 1e-6 + 1e-5 * float(a.detach().abs().max())

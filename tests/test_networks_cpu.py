@@ -1,0 +1,76 @@
+"""base.MLP storage on the CPU (no kernel calls): reference init bit for bit, state_dict
+keys and shapes, the flat (zero-padded) layout of widths that are not compiled, and the
+checkpoint round trip in the reference's layout (base/baseModel.py:137-162)."""
+import pytest
+import torch
+
+from oracle import siren_oracle as O
+
+
+@pytest.fixture(scope="module")
+def B():
+    import base
+    return base
+
+
+@pytest.mark.parametrize("shape", [(1, 1, 2, 20), (2, 2, 3, 68), (3, 3, 3, 66), (2, 1, 4, 128), (2, 3, 1, 40)])
+def test_padded_layout_matches_reference_init(B, shape):
+    din, dout, L, W = shape
+    torch.manual_seed(3)
+    ref = O.OracleSiren(din, dout, L, W)
+    torch.manual_seed(3)
+    net = B.MLP(din, dout, L, W, nonlinearity="sine")
+    Wp = B.networks.kernel_width(W)
+    assert net.kernel_width == Wp and Wp in (32, 64, 128, 256) and Wp >= W
+    sd, rsd = net.state_dict(), ref.state_dict()
+    assert list(sd) == list(rsd)
+    for k in sd:
+        assert sd[k].shape == rsd[k].shape and torch.equal(sd[k], rsd[k]), k
+    flat = net.flat_params()
+    assert flat.numel() == net.param_count == Wp * din + Wp + L * (Wp * Wp + Wp) + dout * Wp + dout
+    # the flat buffer is the padded SIREN of width Wp: padding exactly zero, parameters in place
+    lay = net._layout()
+    mask = torch.zeros_like(flat, dtype=torch.bool)
+    for p, (off, pshape, corner) in zip(net.parameters(), lay):
+        block = flat[off:off + int(torch.tensor(pshape).prod())].view(*pshape)
+        inner = block[tuple(slice(0, c) for c in corner)]
+        assert inner.data_ptr() == p.data_ptr() and torch.equal(inner, p.detach())
+        mask[off:off + block.numel()].view(*pshape)[tuple(slice(0, c) for c in corner)] = True
+    assert int(mask.sum()) == sum(p.numel() for p in ref.parameters())
+    assert bool((flat[~mask] == 0).all())
+
+
+def test_load_state_dict_and_checkpoint_roundtrip(B, tmp_path):
+    torch.manual_seed(0)
+    a = B.MLP(2, 2, 3, 68, nonlinearity="sine")
+    torch.manual_seed(1)
+    b = B.MLP(2, 2, 3, 68, nonlinearity="sine")
+    b.load_state_dict(a.state_dict())
+    assert torch.equal(a.flat_params(), b.flat_params())
+    # reference checkpoint layout: {'net_<name>': state_dict, 'timestep': t}
+    path = tmp_path / "ckpt_step_t003.pth"
+    torch.save({"net_deformation": {k: v.detach().cpu() for k, v in a.state_dict().items()}, "timestep": 3}, path)
+    ck = torch.load(path, weights_only=True)
+    torch.manual_seed(2)
+    c = B.MLP(2, 2, 3, 68, nonlinearity="sine")
+    c.load_state_dict(ck["net_deformation"])
+    assert torch.equal(c.flat_params(), a.flat_params())
+    # and a reference-built network reads it unchanged
+    ref = O.OracleSiren(2, 2, 3, 68)
+    ref.load_state_dict(ck["net_deformation"])
+    for p, q in zip(ref.parameters(), a.parameters()):
+        assert torch.equal(p.detach(), q.detach())
+
+
+def test_grad_views_follow_the_padded_layout(B):
+    torch.manual_seed(0)
+    net = B.MLP(1, 1, 2, 20, nonlinearity="sine")
+    g = net.flat_grad_buffer()
+    g.copy_(torch.arange(g.numel(), dtype=torch.float32))
+    for p, e in zip(net.parameters(), net._layout()):
+        assert torch.equal(p.grad, net._view(g, e))
+
+
+def test_width_above_256_refused(B):
+    with pytest.raises(NotImplementedError):
+        B.MLP(2, 2, 1, 300, nonlinearity="sine")
