@@ -40,6 +40,9 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md chip table: dense fp32 matrix peak (spec)
+BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: ~2.5 PF dense bf16 (no sparsity)
+# per precision: (bench dtype, bf16 products per fp32-equivalent product, NQ of the kernel names)
+PRECISION = {"fp32": ("fp32", 6, 3), "bf16x3": ("bf16x3", 3, 2), "bf16": ("bf16", 1, 1)}
 HBM_PEAK_GBS = 8000.0
 
 
@@ -59,6 +62,10 @@ def parse():
                     help="BASELINE.json workload (default: configs[1], the headline)")
     ap.add_argument("--scaling", choices=["auto", "strong", "weak"], default="auto")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--precision", choices=sorted(PRECISION), default="fp32",
+                    help="matrix-core precision of every jet: fp32 (fp32-accurate split-bf16, the parity "
+                         "config), bf16x3 (3 bf16 products) or bf16 (1 product; BASELINE configs[4] "
+                         "'mixed fp32/bf16 MFMA')")
     ap.add_argument("--band-stream", action="store_true", help="fluid: boundary-band jets on a side stream")
     ap.add_argument("--nograd-stream", action="store_true", help="fluid: no-grad jets on a side stream")
     ap.add_argument("--cpu-seconds", type=float, default=25.0, help="budget of the CPU-baseline sample")
@@ -158,7 +165,8 @@ def build_model(args, world, rank):
     cfg = baseline_config(args.config, sample_resolution=res, insr_graph=not args.no_graph,
                           insr_sync_every=10 ** 9, insr_progress=False, early_stop=False,
                           proj_dir="/tmp/insr_bench", max_n_iters=10 ** 9,
-                          insr_band_stream=args.band_stream, insr_nograd_stream=args.nograd_stream)
+                          insr_band_stream=args.band_stream, insr_nograd_stream=args.nograd_stream,
+                          insr_precision=None if args.precision == "fp32" else args.precision)
     n_global = interior_points(cfg, wl)
     if wl["pde"] in ("fluid", "advection"):
         # strong: the global batch is split over ranks; weak: every rank keeps the full batch
@@ -211,7 +219,7 @@ def macs_per_point(din, dout, L, W):
     return din * W + L * W * W + W * dout
 
 
-def roofline(loops, n_local):
+def roofline(loops, n_local, precision="fp32"):
     """Eager re-run of one step with HIP events around every jet launch (on its launch stream)."""
     from base import _jet
     for pl in loops:  # eager path, same kernels and shapes as the captured graphs
@@ -244,39 +252,45 @@ def roofline(loops, n_local):
     for k, v in sorted(per_step.items(), key=lambda t: -t[1]):
         name = f"{k[0]}:{k[1]}:n{k[2]}:{k[4][0]}-{k[3]}x{k[4][2]}-{k[4][1]}"
         table[name] = round(table.get(name, 0.0) + v, 4)
-    kname, grid, x6 = kernel_identity(kind, mode, n, din, W)
+    nq = PRECISION[precision][2]
+    kname, grid, x6 = kernel_identity(kind, mode, n, din, W, nq)
     traffic, tsrc = pmc_traffic(kname, grid)
-    out = {"bound": "mfma", "achieved": round(achieved, 2), "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-           "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": traffic,
+    peak = FP32_MFMA_PEAK_TFLOPS if precision == "fp32" else BF16_MFMA_PEAK_TFLOPS
+    out = {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
+           "frac": round(achieved / peak, 4), "traffic": traffic,
            "traffic_unit": "bytes/launch (HBM: corrected FETCH_SIZE + WRITE_SIZE)", "traffic_source": tsrc,
            "kernel": f"{kname} grid={grid} (n={n}, {din}->{dout} {L}x{W}, {mode} jet {kind})", "avg_ms": round(ms, 4),
            "algorithmic_gflop_per_launch": round(flops / 1e9, 3), "per_step_ms_by_launch": table}
     if x6:
-        # the kernel runs split-bf16 products: 6 x v_mfma_f32_16x16x32_bf16 (16 cyc) per 16x16x32 fp32 MAC
-        # block = 85.3 fp32-equivalent MAC/clk/SIMD vs 32 for v_mfma_f32_16x16x4_f32 (MI355X_MICROARCH.md)
-        out["x6_ceiling"] = round(FP32_MFMA_PEAK_TFLOPS * (16 * 16 * 32 / 96.0) / 32.0, 1)
-        out["frac_of_x6_ceiling"] = round(achieved / out["x6_ceiling"], 4)
+        # the kernel runs split-bf16 products: NP x v_mfma_f32_16x16x32_bf16 (16 cyc) per 16x16x32 fp32-equivalent
+        # MAC block (NP = 6 / 3 / 1): 16*16*32 / (16 NP) MAC/clk/SIMD vs 32 for v_mfma_f32_16x16x4_f32
+        np_ = PRECISION[precision][1]
+        ceil = round(FP32_MFMA_PEAK_TFLOPS * (16 * 16 * 32 / (16.0 * np_)) / 32.0, 1)
+        out["products_per_mac"] = np_
+        out["precision_ceiling"] = ceil
+        out["frac_of_precision_ceiling"] = round(achieved / ceil, 4)
+        if precision == "fp32":
+            out["x6_ceiling"] = ceil
+            out["frac_of_x6_ceiling"] = out["frac_of_precision_ceiling"]
     return out
 
 
-def kernel_identity(kind, mode, n, din, W):
+def kernel_identity(kind, mode, n, din, W, nq=3):
     """The rocprof name and grid (threads) of the jet kernel the library picks for this launch."""
     from base import _native as nat
     lib = nat.lib()
-    m = {"value": nat.MODE_VALUE, "grad": nat.MODE_GRAD, "lap": nat.MODE_LAP}[mode]
+    prec = {3: nat.PREC_BF16X6, 2: nat.PREC_BF16X3, 1: nat.PREC_BF16}[nq]
+    m = {"value": nat.MODE_VALUE, "grad": nat.MODE_GRAD, "lap": nat.MODE_LAP}[mode] | nat.jet_prec(prec)
     S = {"value": 1, "grad": 1 + din, "lap": 2 + din}[mode]
     NT = W // 16
     lap = "true" if mode == "lap" else "false"
     if kind == "bwd" and lib.insr_jet_bwd_is_wide(n, din, W, m) == 1:  # W = 256: two kernels + reductions
         grid = ((n + 15) // 16) * 512
-        return (f"insr::jet_bwd_x6p<{S}, {lap}> + insr::dw_x6<{S}, {lap}> + reductions (wide path; time = all four)",
-                grid, True)
+        return (f"insr::jet_bwd_x6p<{nq}, {NT}, {S}, {lap}> + insr::dw_x6<{nq}, {NT}, {S}, {lap}> + reductions "
+                f"(wide path; time = all four)", grid, True)
     T = lib.insr_jet_split_tiles(n, din, W, m, 1 if kind == "bwd" else 0)
-    x6 = nat.get_precision()[1 if kind == "bwd" else 0] == nat.PREC_BF16X6 and (kind == "fwd" or NT <= 8)
-    if T > 0:
-        nb = ((n + 15) // 16 + T - 1) // T
-        return f"insr::jet_{kind}_{'x6' if x6 else 'split'}<{NT}, {S}, {lap}, {T}>", nb * 64 * min(NT, 8), x6
-    return f"insr::jet_{kind}_wave<{NT}, {S}, {lap}>", ((n + 63) // 64) * 256, False
+    nb = ((n + 15) // 16 + T - 1) // T
+    return f"insr::jet_{kind}_x6<{nq}, {NT}, {S}, {lap}, {T}>", nb * 64 * min(NT, 8), True
 
 
 def pmc_traffic(kname, grid):
@@ -471,16 +485,18 @@ def main():
         "metric": "collocation-points/sec/timestep (incl. ∇/Δ residual + Adam) at 1/2/4/8 GPUs",
         "value": round(value, 1), "unit": "collocation-points/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "warmup_effective": w_eff, "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
-        "scaling": args.scaling, "vs_baseline": None, "dtype": "fp32", "data": "synthetic (uniform-random "
+        "scaling": args.scaling, "vs_baseline": None, "dtype": PRECISION[args.precision][0],
+        "data": "synthetic (uniform-random "
         "collocation points, seeded SIREN init; no dataset exists for this path)",
         "config": {"workload": args.config, "model": wl["model"],
                    "points_per_phase_iter": n_all, "phases": nph, "global_batch": n_all,
-                   "seq_len": None, "parallelism": f"dp{world}", "graph": not args.no_graph},
+                   "seq_len": None, "parallelism": f"dp{world}", "graph": not args.no_graph,
+                   "precision": args.precision},
         "process_group": {"backend": args.backend if world > 1 else None, "world_size": world,
                           "rank_devices": args.rank_devices},
     }
     if not args.no_roofline:  # every rank runs the eager steps (they contain the all-reduce)
-        roof = roofline(loops, n_local)
+        roof = roofline(loops, n_local, args.precision)
         if rank == 0:
             result["roofline"] = roof
         log("roofline done")

@@ -45,6 +45,12 @@ extern "C" {
 #define INSR_MODE_VALUE 0 /* y                                  (1 stream)        */
 #define INSR_MODE_GRAD  1 /* y, dy/dx_i  (Jacobian rows)         (1 + d_in streams) */
 #define INSR_MODE_LAP   2 /* y, dy/dx_i, sum_i d2y/dx_i^2        (2 + d_in streams) */
+#define INSR_MODE_MASK  0xF
+/* Per-call matrix-core precision: OR INSR_JET_PREC(p) (p an INSR_PREC_* below) into the
+ * `mode` argument of any jet entry point or query; without it the process default
+ * (insr_jet_set_precision) applies.  The saved-activation layout does not depend on it. */
+#define INSR_MODE_PREC_SHIFT 4
+#define INSR_JET_PREC(p) (((p) + 1) << INSR_MODE_PREC_SHIFT)
 
 #define INSR_EINVAL   (-1) /* unsupported shape / mode / null pointer */
 #define INSR_EWIDTH   (-2) /* hidden width not in the compiled set      */
@@ -165,18 +171,25 @@ void insr_jet_set_split_tiles(int fwd_tiles, int bwd_tiles, int min_blocks);
 void insr_jet_get_split_tiles(int* fwd_tiles, int* bwd_tiles, int* min_blocks);
 
 /*
- * Matrix-core precision of the tile-split kernels (process-wide, per direction):
+ * Matrix-core precision of the hidden-layer GEMMs (process default per direction; a call
+ * may override it with INSR_JET_PREC(p) in its mode):
  *   INSR_PREC_F32     v_mfma_f32_16x16x4_f32: exact fp32 products, the fp32 matrix rate.
  *   INSR_PREC_BF16X6  every fp32 operand split in three bf16 terms, six
  *                     v_mfma_f32_16x16x32_bf16 products per K chunk, fp32 accumulation:
  *                     fp32-level accuracy (dropped terms <= 2^-26 |a||b|) at 2.67x
- *                     the fp32 matrix throughput.
+ *                     the fp32 matrix throughput.  The default.
+ *   INSR_PREC_BF16X3  two bf16 terms per operand, three products (dropped terms
+ *                     <= 2^-16 |a||b|): 5.3x the fp32 matrix rate.
+ *   INSR_PREC_BF16    plain bf16 operands, one product, fp32 accumulation: 16x.
+ * The first (K = d_in) and output (M = d_out) layers and every sine stay fp32.
  * Env: INSR_JET_PREC_FWD, INSR_JET_PREC_BWD.  The saved-activation and partial
  * layouts do not depend on it: a forward of one precision pairs with a backward of
- * the other.
+ * another.
  */
 #define INSR_PREC_F32    0
 #define INSR_PREC_BF16X6 1
+#define INSR_PREC_BF16X3 2
+#define INSR_PREC_BF16   3
 void insr_jet_set_precision(int fwd, int bwd);
 void insr_jet_get_precision(int* fwd, int* bwd);
 

@@ -77,6 +77,7 @@ class _SirenJet(torch.autograd.Function):
         lib = nat.lib()
         n, din = x2.shape
         L, W, dout = mlp.num_hidden_layers, mlp.kernel_width, mlp.out_features
+        cmode = mlp.call_mode(mode)  # + the network's precision bits
         flat = mlp.flat_params()
         dev = x2.device
         y = torch.empty(n, dout, device=dev, dtype=torch.float32)
@@ -84,13 +85,13 @@ class _SirenJet(torch.autograd.Function):
         lap = torch.empty(n, dout, device=dev, dtype=torch.float32) if mode == nat.MODE_LAP else None
         act = None
         if save:
-            nbytes = lib.insr_jet_act_bytes(n, din, L, W, mode)
+            nbytes = lib.insr_jet_act_bytes(n, din, L, W, cmode)
             act = torch.empty(max(nbytes // 4, 1), device=dev, dtype=torch.float32)
         if _Fused.pending is not None:  # launched with the other jets of the scope, at its exit
-            _Fused.pending.append(((din, L, W, mode, dev), (x2, flat, y, dy, lap, act, n, dout)))
+            _Fused.pending.append(((din, L, W, cmode, dev), (x2, flat, y, dy, lap, act, n, dout)))
         else:
             with _timed("fwd", mode, n, W, (din, dout, L)):
-                rc = lib.insr_siren_jet_fwd(nat.ptr(x2), n, din, dout, L, W, mode, nat.ptr(flat), nat.ptr(y),
+                rc = lib.insr_siren_jet_fwd(nat.ptr(x2), n, din, dout, L, W, cmode, nat.ptr(flat), nat.ptr(y),
                                             nat.ptr(dy), nat.ptr(lap), nat.ptr(act), nat.stream_of(dev))
             nat.check(rc, "insr_siren_jet_fwd")
         ctx.set_materialize_grads(False)  # unused outputs -> None -> NULL adjoint (no zero-fill launch)
@@ -118,6 +119,7 @@ class _SirenJet(torch.autograd.Function):
         x2, act = ctx.x2, ctx.act
         n, din = x2.shape
         L, W, dout = mlp.num_hidden_layers, mlp.kernel_width, mlp.out_features
+        cmode = mlp.call_mode(mode)
         lib = nat.lib()
         gflat, accumulate = mlp.grad_for_backward()
         c = lambda t: None if t is None else (t if t.is_contiguous() else t.contiguous())  # noqa: E731
@@ -125,25 +127,25 @@ class _SirenJet(torch.autograd.Function):
         st = nat.stream_of(x2.device)
         cur = torch.cuda.current_stream(x2.device)
         mlp.grad_write_begin(cur)  # order after a write of .grad made on another stream
-        if lib.insr_jet_bwd_is_wide(n, din, W, mode) == 1:
+        if lib.insr_jet_bwd_is_wide(n, din, W, cmode) == 1:
             # W = 256: propagation kernel + split-K dW GEMM + reductions, straight into .grad
-            work = torch.empty(max(lib.insr_jet_bwd_work_bytes(n, din, dout, L, W, mode) // 4, 1), device=x2.device,
+            work = torch.empty(max(lib.insr_jet_bwd_work_bytes(n, din, dout, L, W, cmode) // 4, 1), device=x2.device,
                                dtype=torch.float32)
             with _timed("bwd", mode, n, W, (din, dout, L)):
-                rc = lib.insr_siren_jet_bwd_grad(nat.ptr(x2), n, din, dout, L, W, mode, nat.ptr(mlp.flat_params()),
+                rc = lib.insr_siren_jet_bwd_grad(nat.ptr(x2), n, din, dout, L, W, cmode, nat.ptr(mlp.flat_params()),
                                                  nat.ptr(act), nat.ptr(gy), nat.ptr(gdy), nat.ptr(glap), nat.ptr(work),
                                                  nat.ptr(gflat), accumulate, st)
             nat.check(rc, "insr_siren_jet_bwd_grad")
             mlp.grad_write_end(cur)
             return none
-        part = torch.empty(max(lib.insr_jet_partial_bytes(n, din, dout, L, W, mode) // 4, 1), device=x2.device,
+        part = torch.empty(max(lib.insr_jet_partial_bytes(n, din, dout, L, W, cmode) // 4, 1), device=x2.device,
                            dtype=torch.float32)
         with _timed("bwd", mode, n, W, (din, dout, L)):
-            rc = lib.insr_siren_jet_bwd(nat.ptr(x2), n, din, dout, L, W, mode, nat.ptr(mlp.flat_params()),
+            rc = lib.insr_siren_jet_bwd(nat.ptr(x2), n, din, dout, L, W, cmode, nat.ptr(mlp.flat_params()),
                                         nat.ptr(act), nat.ptr(gy), nat.ptr(gdy), nat.ptr(glap), nat.ptr(part), st)
         nat.check(rc, "insr_siren_jet_bwd")
         with _timed("reduce", mode, n, W, (din, dout, L)):
-            rc = lib.insr_reduce_partials_strided(nat.ptr(part), lib.insr_jet_partial_blocks(n, din, W, mode),
+            rc = lib.insr_reduce_partials_strided(nat.ptr(part), lib.insr_jet_partial_blocks(n, din, W, cmode),
                                                   gflat.numel(), lib.insr_jet_partial_stride(din, dout, L, W),
                                                   nat.ptr(gflat), accumulate, st)
         nat.check(rc, "insr_reduce_partials_strided")
@@ -186,7 +188,8 @@ def _launch_fused(jobs):
     for key, job in jobs:
         groups.setdefault(key, []).append(job)
     lib = nat.lib()
-    for (din, L, W, mode, dev), js in groups.items():  # output widths may differ per job
+    for (din, L, W, cmode, dev), js in groups.items():  # output widths may differ per job
+        mode = cmode & nat.MODE_MASK
         for k in range(0, len(js), nat.MAX_FWD_JOBS):
             chunk = js[k:k + nat.MAX_FWD_JOBS]
             n = sum(j[6] for j in chunk)
@@ -198,7 +201,7 @@ def _launch_fused(jobs):
                            None if lap is None else lap.data_ptr(), None if act is None else act.data_ptr(), nj, dj)
                 for x2, flat, y, dy, lap, act, nj, dj in chunk])
             with _timed("fwd%d" % len(chunk) if len(chunk) > 1 else "fwd", mode, n, W, (din, key_dout, L)):
-                rc = lib.insr_siren_jet_fwd_multi(arr, len(chunk), din, dout, L, W, mode, nat.stream_of(dev))
+                rc = lib.insr_siren_jet_fwd_multi(arr, len(chunk), din, dout, L, W, cmode, nat.stream_of(dev))
             nat.check(rc, "insr_siren_jet_fwd_multi")
 
 
@@ -208,7 +211,8 @@ def run_jet(mlp, x, mode):
     mlp.ensure_packed()
     din = mlp.in_features
     lib = nat.lib()
-    if not lib.insr_siren_supported(din, mlp.out_features, mlp.num_hidden_layers, mlp.kernel_width, mode):
+    if not lib.insr_siren_supported(din, mlp.out_features, mlp.num_hidden_layers, mlp.kernel_width,
+                                    mlp.call_mode(mode)):
         raise UnsupportedPattern(
             f"no HIP kernel for SIREN(in={din}, out={mlp.out_features}, width={mlp.kernel_width}) "
             f"in {MODE_NAMES[mode]} mode")
@@ -262,7 +266,7 @@ class call_scope:
 
 def _supported(mlp, mode):
     return bool(nat.lib().insr_siren_supported(mlp.in_features, mlp.out_features, mlp.num_hidden_layers,
-                                               mlp.kernel_width, mode))
+                                               mlp.kernel_width, mlp.call_mode(mode)))
 
 
 def siren_value(mlp, x):

@@ -14,7 +14,14 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("INSR_HIP_LIB", os.path.join(os.path.dirname(_HERE), "lib", "libinsr_hip.so"))
 
 MODE_VALUE, MODE_GRAD, MODE_LAP = 0, 1, 2
-PREC_F32, PREC_BF16X6 = 0, 1
+MODE_MASK, MODE_PREC_SHIFT = 0xF, 4
+PREC_F32, PREC_BF16X6, PREC_BF16X3, PREC_BF16 = 0, 1, 2, 3
+PRECISIONS = {"fp32": PREC_F32, "bf16x6": PREC_BF16X6, "bf16x3": PREC_BF16X3, "bf16": PREC_BF16}
+
+
+def jet_prec(p):
+    """INSR_JET_PREC(p): the per-call precision bits OR-ed into a jet `mode`."""
+    return (int(p) + 1) << MODE_PREC_SHIFT
 LOSS_COMBO, LOSS_BANDS = 0, 1
 OPT_LR, OPT_STEP, OPT_BEST, OPT_BAD, OPT_STEPSIZE, OPT_BC2SQRT, OPT_FACTOR, OPT_MINLR = range(8)
 OPT_NFLOATS = 8

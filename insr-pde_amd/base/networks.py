@@ -35,10 +35,12 @@ OMEGA = 30.0
 
 
 def get_network(cfg, in_features, out_features):
-    """base/networks.py:12-17: only the 'siren' network exists."""
+    """base/networks.py:12-17: only the 'siren' network exists.  cfg.insr_precision (optional,
+    default None = the library default, fp32-accurate split-bf16) selects the matrix-core
+    precision of the net's jets: 'fp32', 'bf16x6', 'bf16x3' or 'bf16'."""
     if cfg.network == 'siren':
         return MLP(in_features, out_features, cfg.num_hidden_layers, cfg.hidden_features,
-                   nonlinearity=cfg.nonlinearity)
+                   nonlinearity=cfg.nonlinearity, precision=getattr(cfg, "insr_precision", None))
     raise NotImplementedError(cfg.network)
 
 
@@ -82,7 +84,7 @@ class MLP(nn.Module):
     """SIREN MLP with flat parameter storage and a HIP forward (base/networks.py:30-71)."""
 
     def __init__(self, in_features, out_features, num_hidden_layers, hidden_features,
-                 outermost_linear=True, nonlinearity='relu', weight_init=None):
+                 outermost_linear=True, nonlinearity='relu', weight_init=None, precision=None):
         super().__init__()
         if nonlinearity != 'sine' or not outermost_linear:
             # the reference also offers relu/elu nets; INSR-PDE only ever builds SIRENs
@@ -90,6 +92,7 @@ class MLP(nn.Module):
         self.in_features, self.out_features = in_features, out_features
         self.num_hidden_layers, self.hidden_features = num_hidden_layers, hidden_features
         self.kernel_width = kernel_width(hidden_features)
+        self.set_precision(precision)
         layers = [nn.Linear(in_features, hidden_features), Sine()]
         for _ in range(num_hidden_layers):
             layers += [nn.Linear(hidden_features, hidden_features), Sine()]
@@ -102,6 +105,20 @@ class MLP(nn.Module):
         self._flat = None
         self._flat_grad = None
         self._repack()
+
+    # ---- matrix-core precision ------------------------------------------------
+    def set_precision(self, precision):
+        """None (the library default: fp32-accurate split-bf16), or one of 'fp32', 'bf16x6',
+        'bf16x3', 'bf16' for every jet of this network (include/insr_siren.h INSR_PREC_*)."""
+        from ._native import PRECISIONS
+        if precision is not None and precision not in PRECISIONS:
+            raise ValueError(f"precision {precision!r}: one of {sorted(PRECISIONS)} or None")
+        self.precision = precision
+
+    def call_mode(self, mode):
+        """The jet `mode` argument of this network's library calls (precision bits added)."""
+        from ._native import PRECISIONS, jet_prec
+        return mode if self.precision is None else mode | jet_prec(PRECISIONS[self.precision])
 
     # ---- flat storage ------------------------------------------------------
     @property
@@ -287,5 +304,6 @@ class MLP(nn.Module):
 
     def extra_repr(self):
         pad = "" if self.kernel_width == self.hidden_features else f" (kernel width {self.kernel_width}, zero-padded)"
+        prec = "" if self.precision is None else f", precision={self.precision}"
         return (f"in={self.in_features}, out={self.out_features}, hidden_layers={self.num_hidden_layers}, "
-                f"width={self.hidden_features}{pad}, backend=hip")
+                f"width={self.hidden_features}{pad}{prec}, backend=hip")

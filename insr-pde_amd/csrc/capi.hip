@@ -42,9 +42,13 @@ static void tiles_init() {
   }
 }
 
-// Matrix-core precision of the tile-split kernels: INSR_PREC_F32 (v_mfma_f32_16x16x4_f32)
-// or INSR_PREC_BF16X6 (jet_x6.hpp: fp32-accurate split-bf16 products).  Env overrides
-// INSR_JET_PREC_FWD / INSR_JET_PREC_BWD.
+// Matrix-core precision of the tile-split kernels (process default per direction; env
+// INSR_JET_PREC_FWD / INSR_JET_PREC_BWD; a call may override it through INSR_JET_PREC(p) in
+// its mode argument -- base.MLP(precision=...) does, per network):
+//   INSR_PREC_F32     v_mfma_f32_16x16x4_f32 (jet_split.hpp)
+//   INSR_PREC_BF16X6  split-bf16, 6 products (jet_x6.hpp, NQ = 3): fp32-level accuracy (default)
+//   INSR_PREC_BF16X3  split-bf16, 3 products (NQ = 2)
+//   INSR_PREC_BF16    bf16 operands, fp32 accumulation (NQ = 1)
 static int g_prec[2] = {-1, -1};  // fwd, bwd
 
 static void prec_init() {
@@ -56,22 +60,30 @@ static void prec_init() {
   }
 }
 
-bool use_x6(int bwd, int NT) {
+static bool prec_ok(int p) { return p >= INSR_PREC_F32 && p <= INSR_PREC_BF16; }
+
+// precision of a call (direction bwd): the mode's override, else the process default
+int call_prec(int mode, int bwd) {
   prec_init();
-  // width 256 has no x6 backward (jet_x6_bwd.hip): fp32 tile-split there
-  return g_prec[bwd ? 1 : 0] == INSR_PREC_BF16X6 && (!bwd || NT <= 8);
+  const int po = (mode >> INSR_MODE_PREC_SHIFT) & 0xF;
+  return po ? po - 1 : g_prec[bwd ? 1 : 0];
 }
 
-// Backward on the x6 precision through the two-kernel path (jet_x6w.hip: propagation kernel +
-// split-K dW GEMM) for widths >= g_wide_min (default 256; env INSR_WIDE_MIN_WIDTH) and, at
-// width 128, for Laplacian jets of >= 32768 points.  Measured (profiles/r01/kbench_wide*.jsonl):
-// W = 256 el3D grad 20.7 -> 10.0 ms; W = 128 LAP 65536 points 949 -> 805 us, while W = 128
-// value / grad jets and LAP at 16384 points are as fast or faster fused.
+// bf16 terms per operand of a precision (0: the exact-fp32 tile-split kernels)
+int nq_of(int prec) {
+  return prec == INSR_PREC_BF16X6 ? 3 : prec == INSR_PREC_BF16X3 ? 2 : prec == INSR_PREC_BF16 ? 1 : 0;
+}
+
+// Backward through the two-kernel path (jet_x6w.hpp: propagation kernel + split-K dW GEMM)
+// for the split-bf16 precisions at widths >= g_wide_min (default 256; env
+// INSR_WIDE_MIN_WIDTH) and, at width 128, for Laplacian jets of >= 32768 points.  Measured
+// (profiles/r01/kbench_wide*.jsonl): W = 256 el3D grad 20.7 -> 10.0 ms; W = 128 LAP 65536
+// points 949 -> 805 us, while W = 128 value / grad jets and LAP at 16384 points are as fast
+// or faster fused.
 static int g_wide_min = -1;
-bool use_wide(long n, int S, int NT, bool lap) {
-  prec_init();
+bool use_wide(long n, int S, int NT, bool lap, int nq) {
   if (g_wide_min < 0) g_wide_min = env_or("INSR_WIDE_MIN_WIDTH", 256);
-  if (NT < 8 || g_prec[1] != INSR_PREC_BF16X6) return false;
+  if (NT < 8 || nq == 0) return false;
   if (16 * NT >= g_wide_min) return true;
   return NT == 8 && lap && n >= 32768 && g_wide_min <= 256;  // Laplacian jets at width 128
 }
@@ -86,34 +98,49 @@ static int cu_count() {
   return c;
 }
 
+// per-precision dispatch (nq = 0: exact fp32)
+static int fwd_q(int nq, int NT, int S, bool lap, int T, const float* x, int N, int din, int dout, int L,
+                 const float* prm, float* y, float* dy, float* lp, float* act, hipStream_t st) {
+  switch (nq) {
+    case 3: return dispatch_fwd_q<3>(NT, S, lap, T, x, N, din, dout, L, prm, y, dy, lp, act, st);
+    case 2: return dispatch_fwd_q<2>(NT, S, lap, T, x, N, din, dout, L, prm, y, dy, lp, act, st);
+    case 1: return dispatch_fwd_q<1>(NT, S, lap, T, x, N, din, dout, L, prm, y, dy, lp, act, st);
+    default: return dispatch_fwd_split(NT, S, lap, T, x, N, din, dout, L, prm, y, dy, lp, act, st);
+  }
+}
+static int bwd_q(int nq, int NT, int S, bool lap, int T, const float* x, int N, int din, int dout, int L,
+                 const float* prm, const float* act, const float* gy, const float* gdy, const float* glap, float* part,
+                 long P, hipStream_t st) {
+  switch (nq) {
+    case 3: return dispatch_bwd_q<3>(NT, S, lap, T, x, N, din, dout, L, prm, act, gy, gdy, glap, part, P, st);
+    case 2: return dispatch_bwd_q<2>(NT, S, lap, T, x, N, din, dout, L, prm, act, gy, gdy, glap, part, P, st);
+    case 1: return dispatch_bwd_q<1>(NT, S, lap, T, x, N, din, dout, L, prm, act, gy, gdy, glap, part, P, st);
+    default: return dispatch_bwd_split(NT, S, lap, T, x, N, din, dout, L, prm, act, gy, gdy, glap, part, P, st);
+  }
+}
+
 // resident blocks per CU of a tile-split kernel instantiation (launchers answer N < 0)
-static int occupancy(int bwd, bool x6, int NT, int S, bool lap, int T) {
+static int occupancy(int bwd, int nq, int NT, int S, bool lap, int T) {
   static std::map<int, int> cache;
-  const int key = (((((bwd * 2 + (x6 ? 1 : 0)) * 32 + NT) * 8 + S) * 2 + (lap ? 1 : 0)) * 8) + T;
+  const int key = (((((bwd * 4 + nq) * 32 + NT) * 8 + S) * 2 + (lap ? 1 : 0)) * 8) + T;
   auto it = cache.find(key);
   if (it != cache.end()) return it->second;
-  int r;
-  if (bwd)
-    r = x6 ? dispatch_bwd_x6(NT, S, lap, T, nullptr, -1, 0, 0, 0, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
-                             0, nullptr)
-           : dispatch_bwd_split(NT, S, lap, T, nullptr, -1, 0, 0, 0, nullptr, nullptr, nullptr, nullptr, nullptr,
-                                nullptr, 0, nullptr);
-  else
-    r = x6 ? dispatch_fwd_x6(NT, S, lap, T, nullptr, -1, 0, 0, 0, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr)
-           : dispatch_fwd_split(NT, S, lap, T, nullptr, -1, 0, 0, 0, nullptr, nullptr, nullptr, nullptr, nullptr,
-                                nullptr);
+  const int r = bwd ? bwd_q(nq, NT, S, lap, T, nullptr, -1, 0, 0, 0, nullptr, nullptr, nullptr, nullptr, nullptr,
+                            nullptr, 0, nullptr)
+                    : fwd_q(nq, NT, S, lap, T, nullptr, -1, 0, 0, 0, nullptr, nullptr, nullptr, nullptr, nullptr,
+                            nullptr);
   cache[key] = r;
   return r;
 }
 
-int split_tiles(int bwd, int NT, int S, long n, bool lap) {
+int split_tiles(int bwd, int NT, int S, long n, bool lap, int nq) {
   tiles_init();
-  const bool x6 = use_x6(bwd, NT);
-  // LDS per tile: fp32 planes [S][16][W+8] (+ backward h planes [S][16][W]); x6 forward:
-  // three bf16 planes [S][3][16][W+8]; x6 backward: one stream group of bf16 Z + H planes
+  const bool x6 = nq > 0;
+  // LDS per tile: fp32 planes [S][16][W+8] (+ backward h planes [S][16][W]); split-bf16
+  // forward: NQ bf16 planes [S][NQ][16][W+8]; backward: one stream group of bf16 Z + H planes
   // (the kernel picks the group size that fits, jet_x6.hpp x6_bwd_sg)
-  const size_t plane = x6 && !bwd ? (size_t)S * 3 * 16 * (16 * NT + 8) * 2
-                       : x6       ? (size_t)(3 * 16 * (16 * NT + 8) + 32 + 3 * 16 * 16 * NT) * 2
+  const size_t plane = x6 && !bwd ? (size_t)S * nq * 16 * (16 * NT + 8) * 2
+                       : x6       ? (size_t)(nq * 16 * (16 * NT + 8) + 32 + nq * 16 * 16 * NT) * 2
                                   : (size_t)S * 16 * ((16 * NT + 8) + (bwd ? 16 * NT : 0)) * sizeof(float);
   // width 256: fp32 kernels one tile (register budget of 8 waves x 2 row tiles); the x6
   // forward T x S <= 4 (its a[T][2][S] accumulators next to the 8 split W fragments);
@@ -137,7 +164,7 @@ int split_tiles(int bwd, int NT, int S, long n, bool lap) {
   if (T > 1) {
     const int cus = cu_count();
     auto cost = [&](int t) -> double {
-      const int o = occupancy(bwd, x6, NT, S, lap, t);
+      const int o = occupancy(bwd, nq, NT, S, lap, t);
       if (o <= 0) return 1e30;
       const long nb = (tiles + t - 1) / t, per = (long)o * cus;
       return (double)((nb + per - 1) / per) * t;
@@ -343,11 +370,31 @@ __global__ void adam_multi_kernel(AdamList L, const float* __restrict__ st, floa
 bool shape_ok(int din, int dout, int L, int width, int mode) {
   if (din < 1 || din > 3 || dout < 1 || dout > 3 || L < 0 || L > 64) return false;
   if (nt_for(width) < 0) return false;
-  const int S = streams_for(din, mode);
+  if (mode & ~(INSR_MODE_MASK | (0xF << INSR_MODE_PREC_SHIFT))) return false;
+  const int po = (mode >> INSR_MODE_PREC_SHIFT) & 0xF;
+  if (po && !prec_ok(po - 1)) return false;
+  const int jm = mode & INSR_MODE_MASK;
+  const int S = streams_for(din, jm);
   if (S < 1 || S > 4) return false;
-  if (mode == INSR_MODE_LAP && din > 2) return false;
+  if (jm == INSR_MODE_LAP && din > 2) return false;
   return true;
 }
+
+// one jet call's configuration: jet mode, streams, row tiles, bf16 terms per direction
+struct JetCall {
+  int jm, S, NT, nqf, nqb;
+  bool lap;
+  JetCall(int din, int W, int mode)
+      : jm(mode & INSR_MODE_MASK),
+        S(streams_for(din, mode & INSR_MODE_MASK)),
+        NT(nt_for(W)),
+        nqf(nq_of(call_prec(mode, 0))),
+        nqb(nq_of(call_prec(mode, 1))),
+        lap((mode & INSR_MODE_MASK) == INSR_MODE_LAP) {}
+  bool ok() const { return S > 0 && NT > 0; }
+  // width 256 has no fused split-bf16 backward: the two-kernel path serves it
+  bool wide(long n) const { return use_wide(n, S, NT, lap, nqb); }
+};
 
 }  // namespace insr
 
@@ -355,7 +402,7 @@ using namespace insr;
 
 extern "C" {
 
-int insr_version(void) { return 200; }
+int insr_version(void) { return 300; }
 
 long insr_siren_param_count(int din, int dout, int L, int W) {
   return (long)W * din + W + (long)L * ((long)W * W + W) + (long)dout * W + dout;
@@ -368,7 +415,7 @@ long insr_jet_partial_stride(int din, int dout, int L, int W) {
 int insr_siren_supported(int din, int dout, int L, int W, int mode) { return shape_ok(din, dout, L, W, mode) ? 1 : 0; }
 
 long insr_jet_act_bytes(long n, int din, int L, int W, int mode) {
-  const int S = streams_for(din, mode);
+  const int S = streams_for(din, mode & INSR_MODE_MASK);
   if (S < 0 || n < 0) return INSR_EINVAL;
   const long tiles = act_tiles(n);
   return (long)(L + 1) * tiles * 16 * W * S * (long)sizeof(float);
@@ -384,22 +431,18 @@ int insr_siren_jet_fwd(const float* x, long n, int din, int dout, int L, int W, 
                        float* y, float* dy, float* lap, float* act, void* stream) {
   if (!shape_ok(din, dout, L, W, mode) || n < 0 || n > 0x7fffffffL) return INSR_EINVAL;
   if (n == 0) return 0;
+  const JetCall c(din, W, mode);
   if (!x || !params || !y) return INSR_EINVAL;
-  if (mode != INSR_MODE_VALUE && !dy) return INSR_EINVAL;
-  if (mode == INSR_MODE_LAP && !lap) return INSR_EINVAL;
-  const int S = streams_for(din, mode);
-  const int NT = nt_for(W);
-  const bool lapm = mode == INSR_MODE_LAP;
-  if (use_x6(0, NT))
-    return dispatch_fwd_x6(NT, S, lapm, split_tiles(0, NT, S, n, lapm), x, (int)n, din, dout, L, params, y, dy, lap,
-                           act, (hipStream_t)stream);
-  return dispatch_fwd_split(NT, S, lapm, split_tiles(0, NT, S, n, lapm), x, (int)n, din, dout, L, params, y, dy, lap,
-                            act, (hipStream_t)stream);
+  if (c.jm != INSR_MODE_VALUE && !dy) return INSR_EINVAL;
+  if (c.lap && !lap) return INSR_EINVAL;
+  return fwd_q(c.nqf, c.NT, c.S, c.lap, split_tiles(0, c.NT, c.S, n, c.lap, c.nqf), x, (int)n, din, dout, L, params,
+               y, dy, lap, act, (hipStream_t)stream);
 }
 
 int insr_siren_jet_fwd_multi(const InsrJetJob* jobs, int njobs, int din, int dout, int L, int W, int mode,
                              void* stream) {
   if (!jobs || njobs < 1 || njobs > INSR_MAX_FWD_JOBS || !shape_ok(din, dout, L, W, mode)) return INSR_EINVAL;
+  const JetCall c(din, W, mode);
   long total = 0;
   int live = 0;
   for (int k = 0; k < njobs; ++k) {
@@ -408,36 +451,40 @@ int insr_siren_jet_fwd_multi(const InsrJetJob* jobs, int njobs, int din, int dou
     if (j.d_out < 0 || j.d_out > 3) return INSR_EINVAL;
     if (j.n == 0) continue;
     if (!j.x || !j.params || !j.y) return INSR_EINVAL;
-    if (mode != INSR_MODE_VALUE && !j.dy) return INSR_EINVAL;
-    if (mode == INSR_MODE_LAP && !j.lap) return INSR_EINVAL;
+    if (c.jm != INSR_MODE_VALUE && !j.dy) return INSR_EINVAL;
+    if (c.lap && !j.lap) return INSR_EINVAL;
     total += j.n;
     ++live;
   }
   if (total > 0x7fffffffL) return INSR_EINVAL;
   if (live == 0) return 0;
-  const int S = streams_for(din, mode);
-  const int NT = nt_for(W);
-  // one fused launch where the x6 forward serves the combined batch; otherwise (another
-  // kernel family, a Laplacian jet, a single job) the jobs launch one after another
-  // (the fused kernel is compiled for widths 64 / 128 / 256)
+  const int S = c.S, NT = c.NT;
+  // one fused launch where the split-bf16 forward serves the combined batch; otherwise
+  // (exact fp32, a Laplacian jet, a single job) the jobs launch one after another (the fused
+  // kernel is compiled for widths 64 / 128 / 256)
   // W = 128 gradient jets fuse only while the batch fits one round of two 2-tile blocks per CU
   // (at 65,536 + 1,308 points the fused launch measured 4% slower per step than two launches)
   const bool grad128_big = NT == 8 && S == 3 && total > 2L * 2 * 16 * cu_count() + 4096;
-  if (live > 1 && mode != INSR_MODE_LAP && NT >= 4 && !grad128_big && use_x6(0, NT)) {
+  if (live > 1 && !c.lap && NT >= 4 && !grad128_big && c.nqf > 0) {
     // tiles per block from the combined batch; a job whose own batch would take fewer
     // (a boundary band) runs 1-tile blocks, placed first in the grid
     // (W = 128 gradient jets: T = 2 -- the fused kernel is held to 128 VGPRs, two blocks per CU;
     // measured 50.9 vs 51.9 us for T = 4 at 16384 points, profiles/r01/fwd_minwaves_study)
-    const int T = (NT == 8 && S == 3) ? 2 : split_tiles(0, NT, S, total, false);
+    const int T = (NT == 8 && S == 3) ? 2 : split_tiles(0, NT, S, total, false, c.nqf);
     InsrJetJob pk[INSR_MAX_FWD_JOBS];
     int small[INSR_MAX_FWD_JOBS];
     int m = 0;
     for (int k = 0; k < njobs; ++k)
       if (jobs[k].n > 0) {
-        small[m] = split_tiles(0, NT, S, jobs[k].n, false) < T ? 1 : 0;
+        small[m] = split_tiles(0, NT, S, jobs[k].n, false, c.nqf) < T ? 1 : 0;
         pk[m++] = jobs[k];
       }
-    return dispatch_fwd_x6_multi(NT, S, false, T, pk, small, m, din, dout, L, (hipStream_t)stream);
+    hipStream_t st = (hipStream_t)stream;
+    switch (c.nqf) {
+      case 3: return dispatch_fwd_multi_q<3>(NT, S, false, T, pk, small, m, din, dout, L, st);
+      case 2: return dispatch_fwd_multi_q<2>(NT, S, false, T, pk, small, m, din, dout, L, st);
+      default: return dispatch_fwd_multi_q<1>(NT, S, false, T, pk, small, m, din, dout, L, st);
+    }
   }
   for (int k = 0; k < njobs; ++k) {
     const InsrJetJob& j = jobs[k];
@@ -455,15 +502,12 @@ int insr_siren_jet_bwd(const float* x, long n, int din, int dout, int L, int W, 
   if (!shape_ok(din, dout, L, W, mode) || n < 0 || n > 0x7fffffffL) return INSR_EINVAL;
   if (n == 0) return 0;
   if (!x || !params || !act || !partial) return INSR_EINVAL;
+  const JetCall c(din, W, mode);
   const long P = insr_jet_partial_stride(din, dout, L, W);  // row stride of the partial rows
-  const int S = streams_for(din, mode);
-  const int NT = nt_for(W);
-  const bool lapm = mode == INSR_MODE_LAP;
-  if (use_x6(1, NT))
-    return dispatch_bwd_x6(NT, S, lapm, split_tiles(1, NT, S, n, lapm), x, (int)n, din, dout, L, params, act, gy, gdy,
-                           glap, partial, P, (hipStream_t)stream);
-  return dispatch_bwd_split(NT, S, lapm, split_tiles(1, NT, S, n, lapm), x, (int)n, din, dout, L, params, act, gy, gdy,
-                            glap, partial, P, (hipStream_t)stream);
+  // width 256: the fused split-bf16 backward does not exist -- exact fp32 serves this entry
+  const int nq = c.NT > 8 ? 0 : c.nqb;
+  return bwd_q(nq, c.NT, c.S, c.lap, split_tiles(1, c.NT, c.S, n, c.lap, nq), x, (int)n, din, dout, L, params, act, gy,
+               gdy, glap, partial, P, (hipStream_t)stream);
 }
 
 int insr_jet_set_wide_min_width(int width) {
@@ -474,15 +518,15 @@ int insr_jet_set_wide_min_width(int width) {
 
 long insr_jet_bwd_work_bytes(long n, int din, int dout, int L, int W, int mode) {
   if (!shape_ok(din, dout, L, W, mode) || n < 0) return INSR_EINVAL;
-  const int S = streams_for(din, mode), NT = nt_for(W);
-  if (use_wide(n, S, NT, mode == INSR_MODE_LAP)) return wide_work_floats(n, din, dout, L, W, S) * (long)sizeof(float);
+  const JetCall c(din, W, mode);
+  if (c.wide(n)) return wide_work_floats(n, din, dout, L, W, c.S) * (long)sizeof(float);
   return insr_jet_partial_bytes(n, din, dout, L, W, mode);
 }
 
 int insr_jet_bwd_is_wide(long n, int din, int W, int mode) {
-  const int S = streams_for(din, mode), NT = nt_for(W);
-  if (S < 0 || NT < 0 || n < 0) return INSR_EINVAL;
-  return use_wide(n, S, NT, mode == INSR_MODE_LAP) ? 1 : 0;
+  const JetCall c(din, W, mode);
+  if (!c.ok() || n < 0) return INSR_EINVAL;
+  return c.wide(n) ? 1 : 0;
 }
 
 int insr_siren_jet_bwd_grad(const float* x, long n, int din, int dout, int L, int W, int mode, const float* params,
@@ -491,10 +535,21 @@ int insr_siren_jet_bwd_grad(const float* x, long n, int din, int dout, int L, in
   if (!shape_ok(din, dout, L, W, mode) || n < 0 || n > 0x7fffffffL) return INSR_EINVAL;
   if (n == 0) return 0;
   if (!x || !params || !act || !work || !grad) return INSR_EINVAL;
-  const int S = streams_for(din, mode), NT = nt_for(W);
-  if (use_wide(n, S, NT, mode == INSR_MODE_LAP))
-    return dispatch_wide_bwd(NT, S, mode == INSR_MODE_LAP, x, (int)n, din, dout, L, params, act, gy, gdy, glap, work, grad,
-                             accumulate, (hipStream_t)stream);
+  const JetCall c(din, W, mode);
+  if (c.wide(n)) {
+    hipStream_t st = (hipStream_t)stream;
+    switch (c.nqb) {
+      case 3:
+        return dispatch_wide_bwd_q<3>(c.NT, c.S, c.lap, x, (int)n, din, dout, L, params, act, gy, gdy, glap, work, grad,
+                                      accumulate, st);
+      case 2:
+        return dispatch_wide_bwd_q<2>(c.NT, c.S, c.lap, x, (int)n, din, dout, L, params, act, gy, gdy, glap, work, grad,
+                                      accumulate, st);
+      default:
+        return dispatch_wide_bwd_q<1>(c.NT, c.S, c.lap, x, (int)n, din, dout, L, params, act, gy, gdy, glap, work, grad,
+                                      accumulate, st);
+    }
+  }
   int rc = insr_siren_jet_bwd(x, n, din, dout, L, W, mode, params, act, gy, gdy, glap, work, stream);
   if (rc) return rc;
   return insr_reduce_partials_strided(work, insr_jet_partial_blocks(n, din, W, mode),
@@ -503,17 +558,19 @@ int insr_siren_jet_bwd_grad(const float* x, long n, int din, int dout, int L, in
 }
 
 int insr_jet_partial_blocks(long n, int din, int W, int mode) {
-  const int S = streams_for(din, mode), NT = nt_for(W);
-  if (S < 0 || NT < 0 || n < 0) return INSR_EINVAL;
+  const JetCall c(din, W, mode);
+  if (!c.ok() || n < 0) return INSR_EINVAL;
   if (n == 0) return 0;
-  const int T = split_tiles(1, NT, S, n, mode == INSR_MODE_LAP);
+  const int nq = c.NT > 8 ? 0 : c.nqb;
+  const int T = split_tiles(1, c.NT, c.S, n, c.lap, nq);
   return (int)(((n + 15) / 16 + T - 1) / T);
 }
 
 int insr_jet_split_tiles(long n, int din, int W, int mode, int backward) {
-  const int S = streams_for(din, mode), NT = nt_for(W);
-  if (S < 0 || NT < 0 || n < 0) return INSR_EINVAL;
-  return split_tiles(backward ? 1 : 0, NT, S, n, mode == INSR_MODE_LAP);
+  const JetCall c(din, W, mode);
+  if (!c.ok() || n < 0) return INSR_EINVAL;
+  const int nq = backward ? (c.NT > 8 ? 0 : c.nqb) : c.nqf;
+  return split_tiles(backward ? 1 : 0, c.NT, c.S, n, c.lap, nq);
 }
 
 void insr_jet_set_split_tiles(int fwd_tiles, int bwd_tiles, int min_blocks) {
@@ -532,8 +589,8 @@ void insr_jet_get_split_tiles(int* fwd_tiles, int* bwd_tiles, int* min_blocks) {
 
 void insr_jet_set_precision(int fwd, int bwd) {
   prec_init();
-  g_prec[0] = fwd == INSR_PREC_BF16X6 ? INSR_PREC_BF16X6 : INSR_PREC_F32;
-  g_prec[1] = bwd == INSR_PREC_BF16X6 ? INSR_PREC_BF16X6 : INSR_PREC_F32;
+  g_prec[0] = prec_ok(fwd) ? fwd : INSR_PREC_F32;
+  g_prec[1] = prec_ok(bwd) ? bwd : INSR_PREC_F32;
 }
 
 void insr_jet_get_precision(int* fwd, int* bwd) {

@@ -1,0 +1,14 @@
+// jet_bf_fwd.hip -- the reduced-precision forward jets: NQ = 2 ("x3", 3 bf16 products per
+// fp32 product) and NQ = 1 (plain bf16 operands, fp32 accumulation).
+#include "jet_x6_fwd.hpp"
+
+namespace insr {
+template int dispatch_fwd_q<1>(int, int, bool, int, const float*, int, int, int, int, const float*, float*, float*,
+                               float*, float*, hipStream_t);
+template int dispatch_fwd_multi_q<1>(int, int, bool, int, const InsrJetJob*, const int*, int, int, int, int,
+                                     hipStream_t);
+template int dispatch_fwd_q<2>(int, int, bool, int, const float*, int, int, int, int, const float*, float*, float*,
+                               float*, float*, hipStream_t);
+template int dispatch_fwd_multi_q<2>(int, int, bool, int, const InsrJetJob*, const int*, int, int, int, int,
+                                     hipStream_t);
+}  // namespace insr

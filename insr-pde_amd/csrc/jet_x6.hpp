@@ -53,21 +53,46 @@ __device__ __forceinline__ void split3(float a, float b, unsigned& h, unsigned& 
   l = pk_bf16(ra, rb);
 }
 
-struct Frag3 {
-  u32x4 h, m, l;
+// ---------------------------------------------------------------------------
+// Precision template NQ = bf16 terms per operand (the planes of every LDS image):
+//   NQ = 3  "x6"  a = a_h + a_m + a_l, six products (above): fp32-level accuracy
+//   NQ = 2  "x3"  a = a_h + a_m (16 significant bits), products a_h b_m + a_m b_h + a_h b_h
+//                 (dropped terms <= 2^-16 |a||b|): ~1e-5 relative per product
+//   NQ = 1  "bf16" one product a_h b_h: bf16 operands, fp32 accumulation
+// The geometry, layouts and numerics contract are otherwise identical.
+// ---------------------------------------------------------------------------
+template <int NQ>
+struct FragQ {
+  u32x4 q[NQ];  // q[0] = h, q[1] = m, q[2] = l
 };
+using Frag3 = FragQ<3>;
 
-// 8 fp32 (k = j, j = 0..7: v0[0..3], v1[0..3]) -> one A/B fragment in three planes
-__device__ __forceinline__ Frag3 split_frag(const floatx4& v0, const floatx4& v1) {
-  unsigned h[4], m[4], l[4];
-  split3(v0[0], v0[1], h[0], m[0], l[0]);
-  split3(v0[2], v0[3], h[1], m[1], l[1]);
-  split3(v1[0], v1[1], h[2], m[2], l[2]);
-  split3(v1[2], v1[3], h[3], m[3], l[3]);
-  Frag3 f;
-  f.h = u32x4{h[0], h[1], h[2], h[3]};
-  f.m = u32x4{m[0], m[1], m[2], m[3]};
-  f.l = u32x4{l[0], l[1], l[2], l[3]};
+// split of the pair (a, b) into NQ packed bf16 terms
+template <int NQ>
+__device__ __forceinline__ void splitq(float a, float b, unsigned (&o)[NQ]) {
+  o[0] = pk_bf16(a, b);
+  if constexpr (NQ > 1) {
+    float ra = a - bf_lo(o[0]), rb = b - bf_hi(o[0]);
+    o[1] = pk_bf16(ra, rb);
+    if constexpr (NQ > 2) {
+      ra -= bf_lo(o[1]);
+      rb -= bf_hi(o[1]);
+      o[2] = pk_bf16(ra, rb);
+    }
+  }
+}
+
+// 8 fp32 (k = j, j = 0..7: v0[0..3], v1[0..3]) -> one A/B fragment in NQ planes
+template <int NQ>
+__device__ __forceinline__ FragQ<NQ> split_frag(const floatx4& v0, const floatx4& v1) {
+  unsigned t[4][NQ];
+  splitq<NQ>(v0[0], v0[1], t[0]);
+  splitq<NQ>(v0[2], v0[3], t[1]);
+  splitq<NQ>(v1[0], v1[1], t[2]);
+  splitq<NQ>(v1[2], v1[3], t[3]);
+  FragQ<NQ> f;
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) f.q[q] = u32x4{t[0][q], t[1][q], t[2][q], t[3][q]};
   return f;
 }
 
@@ -76,15 +101,38 @@ __device__ __forceinline__ floatx4 mfma_bf(const u32x4& a, const u32x4& b, float
                                                  0, 0, 0);
 }
 
-// c += A B over one 32-deep K chunk at fp32-level accuracy (small terms first)
-__device__ __forceinline__ floatx4 mfma_x6(const Frag3& a, const Frag3& b, floatx4 c) {
-  c = mfma_bf(a.m, b.m, c);
-  c = mfma_bf(a.h, b.l, c);
-  c = mfma_bf(a.l, b.h, c);
-  c = mfma_bf(a.h, b.m, c);
-  c = mfma_bf(a.m, b.h, c);
-  c = mfma_bf(a.h, b.h, c);
-  return c;
+// c += A B over one 32-deep K chunk (small terms first)
+template <int NQ>
+__device__ __forceinline__ floatx4 mfma_q(const FragQ<NQ>& a, const FragQ<NQ>& b, floatx4 c) {
+  if constexpr (NQ == 3) {
+    c = mfma_bf(a.q[1], b.q[1], c);
+    c = mfma_bf(a.q[0], b.q[2], c);
+    c = mfma_bf(a.q[2], b.q[0], c);
+  }
+  if constexpr (NQ >= 2) {
+    c = mfma_bf(a.q[0], b.q[1], c);
+    c = mfma_bf(a.q[1], b.q[0], c);
+  }
+  return mfma_bf(a.q[0], b.q[0], c);
+}
+
+// one fragment (8 consecutive bf16 of each plane) from NQ planes PLANE elements apart
+template <int NQ, int PLANE>
+__device__ __forceinline__ FragQ<NQ> lds_frag(const unsigned short* p) {
+  FragQ<NQ> f;
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) f.q[q] = *reinterpret_cast<const u32x4*>(p + q * PLANE);
+  return f;
+}
+
+// 4 fp32 -> 4 consecutive bf16 of each of NQ planes (one b64 store per plane)
+template <int NQ, int PLANE>
+__device__ __forceinline__ void lds_put4(unsigned short* p, float a0, float a1, float a2, float a3) {
+  unsigned u0[NQ], u1[NQ];
+  splitq<NQ>(a0, a1, u0);
+  splitq<NQ>(a2, a3, u1);
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) *reinterpret_cast<u32x2*>(p + q * PLANE) = u32x2{u0[q], u1[q]};
 }
 
 template <int NT>
@@ -98,27 +146,27 @@ struct X6Geo {
   static constexpr int THREADS = 64 * WV;
 };
 
-template <int NT, int S, int T>
+template <int NQ, int NT, int S, int T>
 constexpr size_t fwd_x6_lds_bytes() {
   using G = X6Geo<NT>;
-  const size_t planes = (size_t)T * S * 3 * G::PLANE * 2;
+  const size_t planes = (size_t)T * S * NQ * G::PLANE * 2;
   const size_t red = (size_t)G::WV * T * S * 3 * 16 * sizeof(float);  // output-layer combine
   return planes > red ? planes : red;
 }
 
 // hidden-layer A fragments of this wave's row tile rt: W[16 rt + c][32 kc + 8 g + j]
-template <int NT>
-__device__ __forceinline__ Frag3 load_w_frag(const float* __restrict__ Wj, int rt, int kc, int g, int c) {
+template <int NQ, int NT>
+__device__ __forceinline__ FragQ<NQ> load_w_frag(const float* __restrict__ Wj, int rt, int kc, int g, int c) {
   constexpr int W = 16 * NT;
   const float* p = Wj + (16 * rt + c) * W + 32 * kc + 8 * g;
   const floatx4 v0 = *reinterpret_cast<const floatx4*>(p);
   const floatx4 v1 = *reinterpret_cast<const floatx4*>(p + 4);
-  return split_frag(v0, v1);
+  return split_frag<NQ>(v0, v1);
 }
 
 // The forward of one block (tiles tile0 .. tile0 + T - 1 of one network's batch): the body
 // of jet_fwd_x6 and of jet_fwd_x6_multi (several networks / batches in one launch).
-template <int NT, int S, bool LAP, int T>
+template <int NQ, int NT, int S, bool LAP, int T>
 __device__ __forceinline__ void fwd_x6_block(const float* __restrict__ x, int N, int din, int dout, int L,
                                              const float* __restrict__ prm, float* __restrict__ y,
                                              float* __restrict__ dy, float* __restrict__ lap,
@@ -170,9 +218,9 @@ __device__ __forceinline__ void fwd_x6_block(const float* __restrict__ x, int N,
 #pragma unroll
       for (int i = 0; i < RPW; ++i) {
         const int rt = rt0 + i;
-        Frag3 wf[KC];
+        FragQ<NQ> wf[KC];
 #pragma unroll
-        for (int kc = 0; kc < KC; ++kc) wf[kc] = load_w_frag<NT>(Wj, rt, kc, g, c);
+        for (int kc = 0; kc < KC; ++kc) wf[kc] = load_w_frag<NQ, NT>(Wj, rt, kc, g, c);
         const floatx4 bias = *reinterpret_cast<const floatx4*>(bj + 16 * rt + 4 * g);
 #pragma unroll
         for (int t = 0; t < T; ++t) {
@@ -186,12 +234,8 @@ __device__ __forceinline__ void fwd_x6_block(const float* __restrict__ x, int N,
           for (int t = 0; t < T; ++t)
 #pragma unroll
             for (int s = 0; s < S; ++s) {
-              const unsigned short* pb = lds + (t * S + s) * 3 * PLANE + c * LDB + 32 * kc + 8 * g;
-              Frag3 hf;
-              hf.h = *reinterpret_cast<const u32x4*>(pb);
-              hf.m = *reinterpret_cast<const u32x4*>(pb + PLANE);
-              hf.l = *reinterpret_cast<const u32x4*>(pb + 2 * PLANE);
-              a[t][i][s] = mfma_x6(wf[kc], hf, a[t][i][s]);
+              const unsigned short* pb = lds + (t * S + s) * NQ * PLANE + c * LDB + 32 * kc + 8 * g;
+              a[t][i][s] = mfma_q<NQ>(wf[kc], lds_frag<NQ, PLANE>(pb), a[t][i][s]);
             }
         }
       }
@@ -217,13 +261,8 @@ __device__ __forceinline__ void fwd_x6_block(const float* __restrict__ x, int N,
         for (int i = 0; i < RPW; ++i)
 #pragma unroll
           for (int s = 0; s < S; ++s) {
-            unsigned h0, m0, l0, h1, m1, l1;
-            split3(a[t][i][s][0], a[t][i][s][1], h0, m0, l0);
-            split3(a[t][i][s][2], a[t][i][s][3], h1, m1, l1);
-            unsigned short* pw = lds + (t * S + s) * 3 * PLANE + c * LDB + 16 * (rt0 + i) + 4 * g;
-            *reinterpret_cast<u32x2*>(pw) = u32x2{h0, h1};
-            *reinterpret_cast<u32x2*>(pw + PLANE) = u32x2{m0, m1};
-            *reinterpret_cast<u32x2*>(pw + 2 * PLANE) = u32x2{l0, l1};
+            unsigned short* pw = lds + (t * S + s) * NQ * PLANE + c * LDB + 16 * (rt0 + i) + 4 * g;
+            lds_put4<NQ, PLANE>(pw, a[t][i][s][0], a[t][i][s][1], a[t][i][s][2], a[t][i][s][3]);
           }
       __syncthreads();
     }
@@ -282,11 +321,11 @@ __device__ __forceinline__ void fwd_x6_block(const float* __restrict__ x, int N,
   }
 }
 
-template <int NT, int S, bool LAP, int T>
+template <int NQ, int NT, int S, bool LAP, int T>
 __global__ __launch_bounds__(X6Geo<NT>::THREADS) void jet_fwd_x6(
     const float* __restrict__ x, int N, int din, int dout, int L, const float* __restrict__ prm,
     float* __restrict__ y, float* __restrict__ dy, float* __restrict__ lap, float* __restrict__ act) {
-  fwd_x6_block<NT, S, LAP, T>(x, N, din, dout, L, prm, y, dy, lap, act, blockIdx.x * T);
+  fwd_x6_block<NQ, NT, S, LAP, T>(x, N, din, dout, L, prm, y, dy, lap, act, blockIdx.x * T);
 }
 
 // Horizontal fusion: up to kFwdJobs independent forward jets of one architecture and jet
@@ -314,7 +353,7 @@ constexpr int x6_multi_min_waves() {
   return (NT == 8 && (S == 1 || S == 3)) ? 4 : 1;
 }
 
-template <int NT, int S, bool LAP, int TA, int TB>
+template <int NQ, int NT, int S, bool LAP, int TA, int TB>
 __global__ __launch_bounds__(X6Geo<NT>::THREADS, (x6_multi_min_waves<NT, S>())) void jet_fwd_x6_multi(
     const FwdJobsX6 jobs, int din, int dout, int L) {
   const int b = blockIdx.x;
@@ -325,28 +364,28 @@ __global__ __launch_bounds__(X6Geo<NT>::THREADS, (x6_multi_min_waves<NT, S>())) 
   const int dout_k = jb.d_out > 0 ? jb.d_out : dout;
   if constexpr (TA != TB) {
     if (jobs.small[k]) {
-      fwd_x6_block<NT, S, LAP, TB>(jb.x, (int)jb.n, din, dout_k, L, jb.params, jb.y, jb.dy, jb.lap, jb.act,
+      fwd_x6_block<NQ, NT, S, LAP, TB>(jb.x, (int)jb.n, din, dout_k, L, jb.params, jb.y, jb.dy, jb.lap, jb.act,
                                    (b - jobs.first[k]) * TB);
       return;
     }
   }
-  fwd_x6_block<NT, S, LAP, TA>(jb.x, (int)jb.n, din, dout_k, L, jb.params, jb.y, jb.dy, jb.lap, jb.act,
+  fwd_x6_block<NQ, NT, S, LAP, TA>(jb.x, (int)jb.n, din, dout_k, L, jb.params, jb.y, jb.dy, jb.lap, jb.act,
                                (b - jobs.first[k]) * TA);
 }
 
 // small[k] != 0: job k runs 1-tile blocks (ignored when T == 1)
-template <int NT, int S, bool LAP, int T>
+template <int NQ, int NT, int S, bool LAP, int T>
 int launch_fwd_x6_multi_t(const InsrJetJob* jobs, const int* small, int njobs, int din, int dout, int L,
                           hipStream_t st) {
   constexpr int TB = 1;
-  constexpr size_t lds = fwd_x6_lds_bytes<NT, S, T>();
+  constexpr size_t lds = fwd_x6_lds_bytes<NQ, NT, S, T>();
   if constexpr (lds > kLdsMax) {
     return INSR_EINVAL;
   } else {
     if (njobs < 1 || njobs > kFwdJobs) return INSR_EINVAL;
     static bool attr_set = false;
     if (!attr_set) {
-      (void)hipFuncSetAttribute((const void*)jet_fwd_x6_multi<NT, S, LAP, T, TB>,
+      (void)hipFuncSetAttribute((const void*)jet_fwd_x6_multi<NQ, NT, S, LAP, T, TB>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       attr_set = true;
     }
@@ -366,32 +405,32 @@ int launch_fwd_x6_multi_t(const InsrJetJob* jobs, const int* small, int njobs, i
     pk.first[njobs] = nb;
     pk.njobs = njobs;
     if (nb == 0) return 0;
-    hipLaunchKernelGGL((jet_fwd_x6_multi<NT, S, LAP, T, TB>), dim3(nb), dim3(X6Geo<NT>::THREADS), lds, st, pk, din,
+    hipLaunchKernelGGL((jet_fwd_x6_multi<NQ, NT, S, LAP, T, TB>), dim3(nb), dim3(X6Geo<NT>::THREADS), lds, st, pk, din,
                        dout, L);
     return (int)hipGetLastError();
   }
 }
 
-template <int NT, int S, bool LAP, int T>
+template <int NQ, int NT, int S, bool LAP, int T>
 int launch_fwd_x6_t(const float* x, int N, int din, int dout, int L, const float* prm, float* y, float* dy,
                     float* lap, float* act, hipStream_t st) {
-  constexpr size_t lds = fwd_x6_lds_bytes<NT, S, T>();
+  constexpr size_t lds = fwd_x6_lds_bytes<NQ, NT, S, T>();
   if constexpr (lds > kLdsMax) {
     return INSR_EINVAL;
   } else {
     const int nb = ((N + 15) / 16 + T - 1) / T;
     static bool attr_set = false;
     if (!attr_set) {
-      (void)hipFuncSetAttribute((const void*)jet_fwd_x6<NT, S, LAP, T>, hipFuncAttributeMaxDynamicSharedMemorySize,
+      (void)hipFuncSetAttribute((const void*)jet_fwd_x6<NQ, NT, S, LAP, T>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)lds);
       attr_set = true;
     }
     if (N < 0) {  // occupancy query (split_tiles): resident blocks per CU
       int occ = 0;
-      (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)jet_fwd_x6<NT, S, LAP, T>, X6Geo<NT>::THREADS, lds);
+      (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)jet_fwd_x6<NQ, NT, S, LAP, T>, X6Geo<NT>::THREADS, lds);
       return occ;
     }
-    hipLaunchKernelGGL((jet_fwd_x6<NT, S, LAP, T>), dim3(nb), dim3(X6Geo<NT>::THREADS), lds, st, x, N, din, dout, L,
+    hipLaunchKernelGGL((jet_fwd_x6<NQ, NT, S, LAP, T>), dim3(nb), dim3(X6Geo<NT>::THREADS), lds, st, x, N, din, dout, L,
                        prm, y, dy, lap, act);
     return (int)hipGetLastError();
   }
@@ -466,59 +505,53 @@ __device__ __forceinline__ floatx4 quad_transpose(const floatx4& v, int c) {
 // one value granule (4 neurons x 1 point per lane, C layout) -> neuron-major bf16 planes
 // [q][m][16 p] at row0 = first neuron of the lane group: quad transpose, then one b64
 // store of 4 consecutive points per plane (instead of 12 b16 stores)
-template <int PLANE>
+template <int NQ, int PLANE>
 __device__ __forceinline__ void put_neuron_major(unsigned short* P, const floatx4& v, int row0, int c) {
   const floatx4 tv = quad_transpose(v, c);
-  unsigned h0, m0, l0, h1, m1, l1;
-  split3(tv[0], tv[1], h0, m0, l0);
-  split3(tv[2], tv[3], h1, m1, l1);
-  unsigned short* p = P + (row0 + (c & 3)) * 16 + (c & ~3);
-  *reinterpret_cast<u32x2*>(p) = u32x2{h0, h1};
-  *reinterpret_cast<u32x2*>(p + PLANE) = u32x2{m0, m1};
-  *reinterpret_cast<u32x2*>(p + 2 * PLANE) = u32x2{l0, l1};
+  lds_put4<NQ, PLANE>(P + (row0 + (c & 3)) * 16 + (c & ~3), tv[0], tv[1], tv[2], tv[3]);
 }
 
 // LDS images of one stream group: Z point-major [q][16 p][W + 8] (the propagation B operand,
 // and the dW A operand through u16 column reads), H neuron-major [q][m][16 p] (the dW B
 // operand, one b128 per plane; written through a quad transpose: one b64 store per plane).
-template <int NT>
+template <int NQ, int NT>
 struct X6BwdGeo {
   using G = X6Geo<NT>;
   static constexpr int W = G::W;
   static constexpr int ZROW = G::LDB;                  // elements of a Z point row
   static constexpr int ZPLANE = 16 * ZROW;
-  static constexpr int ZSET = 3 * ZPLANE + 32;         // +16 dwords: the four lane groups of a
+  static constexpr int ZSET = NQ * ZPLANE + 32;        // +16 dwords: the four lane groups of a
                                                        // column read hit disjoint banks
   static constexpr int HPLANE = W * 16;
-  static constexpr int HSET = 3 * HPLANE;
+  static constexpr int HSET = NQ * HPLANE;
   static constexpr size_t SET_BYTES = (size_t)(ZSET + HSET) * 2;
 };
 
 // streams per LDS group: all S if T tiles of them fit, else S/2, else 1
-template <int NT, int S, int T>
+template <int NQ, int NT, int S, int T>
 constexpr int x6_bwd_sg() {
-  constexpr size_t set = X6BwdGeo<NT>::SET_BYTES;
+  constexpr size_t set = X6BwdGeo<NQ, NT>::SET_BYTES;
   if ((size_t)T * S * set <= kLdsMax) return S;
   if (S % 2 == 0 && (size_t)T * (S / 2) * set <= kLdsMax) return S / 2;
   return 1;
 }
 
-template <int NT, int S, int T>
+template <int NQ, int NT, int S, int T>
 constexpr size_t bwd_x6_lds_bytes() {
-  return (size_t)T * x6_bwd_sg<NT, S, T>() * X6BwdGeo<NT>::SET_BYTES;
+  return (size_t)T * x6_bwd_sg<NQ, NT, S, T>() * X6BwdGeo<NQ, NT>::SET_BYTES;
 }
 
-template <int NT, int S, bool LAP, int T>
+template <int NQ, int NT, int S, bool LAP, int T>
 __global__ __launch_bounds__(X6Geo<NT>::THREADS) void jet_bwd_x6(
     const float* __restrict__ x, int N, int din, int dout, int L, const float* __restrict__ prm,
     const float* __restrict__ act, const float* __restrict__ gy, const float* __restrict__ gdy,
     const float* __restrict__ glap, float* __restrict__ part, long P) {
   using G = X6Geo<NT>;
-  using BG = X6BwdGeo<NT>;
+  using BG = X6BwdGeo<NQ, NT>;
   constexpr int W = G::W, RPW = G::RPW, KC = G::KC;
   constexpr int LDB = BG::ZROW, ZPLANE = BG::ZPLANE, ZSET = BG::ZSET, HPLANE = BG::HPLANE, HSET = BG::HSET;
   constexpr int NTAN = LAP ? S - 2 : S - 1;
-  constexpr int SG = x6_bwd_sg<NT, S, T>();
+  constexpr int SG = x6_bwd_sg<NQ, NT, S, T>();
   constexpr int NG = S / SG;            // stream groups per layer
   constexpr int NSET = T * SG;          // 16-point sets per group
   constexpr int NCH = (NSET + 1) / 2;   // 32-deep K chunks of the weight gradient
@@ -714,13 +747,13 @@ __global__ __launch_bounds__(X6Geo<NT>::THREADS) void jet_bwd_x6(
     // (strided L2 loads issued here).  One group: split once; several groups: the raw
     // values stay live and each group splits them again (fewer registers across groups)
     floatx4 wraw[RPW][KC][2];
-    Frag3 wt[RPW][KC];
+    FragQ<NQ> wt[RPW][KC];
 #pragma unroll
     for (int i = 0; i < RPW; ++i)
 #pragma unroll
       for (int kc = 0; kc < KC; ++kc) {
         load_wt(Wj, i, kc, wraw[i][kc]);
-        if constexpr (NG == 1) wt[i][kc] = split_frag(wraw[i][kc][0], wraw[i][kc][1]);
+        if constexpr (NG == 1) wt[i][kc] = split_frag<NQ>(wraw[i][kc][0], wraw[i][kc][1]);
       }
     floatx4 snp[T][RPW], csp[T][RPW];
     load_sc(j - 1, snp, csp);
@@ -747,20 +780,15 @@ __global__ __launch_bounds__(X6Geo<NT>::THREADS) void jet_bwd_x6(
             const int s = s0 + sl;
             const int u = t * SG + sl;
             const int col = 16 * (rt0 + i) + 4 * g;
-            unsigned h0, m0, l0, h1, m1, l1;
-            split3(hb[t][i][s][0], hb[t][i][s][1], h0, m0, l0);
-            split3(hb[t][i][s][2], hb[t][i][s][3], h1, m1, l1);
-            unsigned short* pz = Z + u * ZSET + c * LDB + col;
-            *reinterpret_cast<u32x2*>(pz) = u32x2{h0, h1};
-            *reinterpret_cast<u32x2*>(pz + ZPLANE) = u32x2{m0, m1};
-            *reinterpret_cast<u32x2*>(pz + 2 * ZPLANE) = u32x2{l0, l1};
+            lds_put4<NQ, ZPLANE>(Z + u * ZSET + c * LDB + col, hb[t][i][s][0], hb[t][i][s][1], hb[t][i][s][2],
+                                 hb[t][i][s][3]);
             floatx4 hs;
             if constexpr (KZ) {
               hs = h_from_regs<S, LAP>(s, zk[t][i], snp[t][i], csp[t][i]);
             } else {
               hs = h_stream<NT, S, LAP>(basep, s, rt0 + i, lane, snp[t][i], csp[t][i]);
             }
-            put_neuron_major<HPLANE>(H + u * HSET, hs, col, c);
+            put_neuron_major<NQ, HPLANE>(H + u * HSET, hs, col, c);
           }
       }
       INSR_STAMP(L - j, 4);
@@ -774,32 +802,25 @@ __global__ __launch_bounds__(X6Geo<NT>::THREADS) void jet_bwd_x6(
         const int p0 = 8 * (g & 1);
 #pragma unroll
         for (int i = 0; i < RPW; ++i) {
-          Frag3 af;
+          FragQ<NQ> af;
           {
             const unsigned short* pa = Z + (live ? u : 0) * ZSET + p0 * LDB + 16 * (rt0 + i) + c;
-            unsigned hh[4], mm[4], ll[4];
 #pragma unroll
-            for (int d = 0; d < 4; ++d) {
-              const unsigned short* q0 = pa + (2 * d) * LDB;
-              const unsigned short* q1 = pa + (2 * d + 1) * LDB;
-              hh[d] = live ? ((unsigned)q0[0] | ((unsigned)q1[0] << 16)) : 0u;
-              mm[d] = live ? ((unsigned)q0[ZPLANE] | ((unsigned)q1[ZPLANE] << 16)) : 0u;
-              ll[d] = live ? ((unsigned)q0[2 * ZPLANE] | ((unsigned)q1[2 * ZPLANE] << 16)) : 0u;
+            for (int q = 0; q < NQ; ++q) {
+              unsigned w[4];
+#pragma unroll
+              for (int d = 0; d < 4; ++d) {
+                const unsigned short* q0 = pa + (2 * d) * LDB + q * ZPLANE;
+                const unsigned short* q1 = pa + (2 * d + 1) * LDB + q * ZPLANE;
+                w[d] = live ? ((unsigned)q0[0] | ((unsigned)q1[0] << 16)) : 0u;
+              }
+              af.q[q] = u32x4{w[0], w[1], w[2], w[3]};
             }
-            af.h = u32x4{hh[0], hh[1], hh[2], hh[3]};
-            af.m = u32x4{mm[0], mm[1], mm[2], mm[3]};
-            af.l = u32x4{ll[0], ll[1], ll[2], ll[3]};
           }
 #pragma unroll
           for (int ct = 0; ct < NT; ++ct) {
-            Frag3 bf;
-            {
-              const unsigned short* pb = H + (live ? u : 0) * HSET + (16 * ct + c) * 16 + p0;
-              bf.h = *reinterpret_cast<const u32x4*>(pb);
-              bf.m = *reinterpret_cast<const u32x4*>(pb + HPLANE);
-              bf.l = *reinterpret_cast<const u32x4*>(pb + 2 * HPLANE);
-            }
-            dacc[i][ct] = mfma_x6(af, bf, dacc[i][ct]);
+            const FragQ<NQ> bf = lds_frag<NQ, HPLANE>(H + (live ? u : 0) * HSET + (16 * ct + c) * 16 + p0);
+            dacc[i][ct] = mfma_q<NQ>(af, bf, dacc[i][ct]);
             X6_SCHED_FENCE();
           }
         }
@@ -818,7 +839,7 @@ __global__ __launch_bounds__(X6Geo<NT>::THREADS) void jet_bwd_x6(
 #pragma unroll
         for (int i = 0; i < RPW; ++i)
 #pragma unroll
-          for (int kc = 0; kc < KC; ++kc) wt[i][kc] = split_frag(wraw[i][kc][0], wraw[i][kc][1]);
+          for (int kc = 0; kc < KC; ++kc) wt[i][kc] = split_frag<NQ>(wraw[i][kc][0], wraw[i][kc][1]);
       }
       // propagation of this group's streams
 #pragma unroll
@@ -831,15 +852,9 @@ __global__ __launch_bounds__(X6Geo<NT>::THREADS) void jet_bwd_x6(
           for (int i = 0; i < RPW; ++i) nh[t][i][s] = floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
           for (int kc = 0; kc < KC; ++kc) {
-            Frag3 bf;
-            {
-              const unsigned short* pb = Z + u * ZSET + c * LDB + 32 * kc + 8 * g;
-              bf.h = *reinterpret_cast<const u32x4*>(pb);
-              bf.m = *reinterpret_cast<const u32x4*>(pb + ZPLANE);
-              bf.l = *reinterpret_cast<const u32x4*>(pb + 2 * ZPLANE);
-            }
+            const FragQ<NQ> bf = lds_frag<NQ, ZPLANE>(Z + u * ZSET + c * LDB + 32 * kc + 8 * g);
 #pragma unroll
-            for (int i = 0; i < RPW; ++i) nh[t][i][s] = mfma_x6(wt[i][kc], bf, nh[t][i][s]);
+            for (int i = 0; i < RPW; ++i) nh[t][i][s] = mfma_q<NQ>(wt[i][kc], bf, nh[t][i][s]);
             X6_SCHED_FENCE();
           }
         }
@@ -866,26 +881,26 @@ __global__ __launch_bounds__(X6Geo<NT>::THREADS) void jet_bwd_x6(
   }
 }
 
-template <int NT, int S, bool LAP, int T>
+template <int NQ, int NT, int S, bool LAP, int T>
 int launch_bwd_x6_t(const float* x, int N, int din, int dout, int L, const float* prm, const float* act,
                     const float* gy, const float* gdy, const float* glap, float* part, long P, hipStream_t st) {
-  constexpr size_t lds = bwd_x6_lds_bytes<NT, S, T>();
+  constexpr size_t lds = bwd_x6_lds_bytes<NQ, NT, S, T>();
   if constexpr (lds > kLdsMax || NT > 8) {
     return INSR_EINVAL;
   } else {
     const int nb = ((N + 15) / 16 + T - 1) / T;
     static bool attr_set = false;
     if (!attr_set) {
-      (void)hipFuncSetAttribute((const void*)jet_bwd_x6<NT, S, LAP, T>,
+      (void)hipFuncSetAttribute((const void*)jet_bwd_x6<NQ, NT, S, LAP, T>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       attr_set = true;
     }
     if (N < 0) {  // occupancy query (split_tiles): resident blocks per CU
       int occ = 0;
-      (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)jet_bwd_x6<NT, S, LAP, T>, X6Geo<NT>::THREADS, lds);
+      (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)jet_bwd_x6<NQ, NT, S, LAP, T>, X6Geo<NT>::THREADS, lds);
       return occ;
     }
-    hipLaunchKernelGGL((jet_bwd_x6<NT, S, LAP, T>), dim3(nb), dim3(X6Geo<NT>::THREADS), lds, st, x, N, din, dout,
+    hipLaunchKernelGGL((jet_bwd_x6<NQ, NT, S, LAP, T>), dim3(nb), dim3(X6Geo<NT>::THREADS), lds, st, x, N, din, dout,
                        L, prm, act, gy, gdy, glap, part, P);
     return (int)hipGetLastError();
   }

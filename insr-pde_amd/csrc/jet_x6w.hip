@@ -1,526 +1,11 @@
-// jet_x6w.hip -- the backward of WIDE SIRENs (W = 256: elasticity3Dbunny, SIREN 5x256)
-// as two split-bf16 ("x6", jet_x6.hpp) kernels instead of one:
-//
-//   jet_bwd_x6p   per 16-point tile, the reverse sweep with ADJOINT PROPAGATION only:
-//                 h̄_{j-1} = W_j^T z̄_j on the matrix cores; it stores z̄_j (j >= 1) to HBM
-//                 in the saved-activation layout and writes a COMPACT partial row per
-//                 tile: the gradients of the first layer, every bias and the output layer.
-//   dw_x6         dW_j = sum over points p and streams s of z̄_j[p,s,:] (x) h_{j-1}[p,s,:]
-//                 for the hidden layers, as a split-K GEMM over K = points x streams: z̄
-//                 from HBM, h rebuilt from the forward's saved z (sin/cos + jet streams),
-//                 both split to bf16 planes in LDS; one partial W x W per (layer, K slice).
-//
-// Why: the fused tile-split backward keeps each wave's dW rows for all W columns in
-// registers (W = 256: 128 VGPRs) next to the propagation state, which does not fit for
-// the x6 path, and it writes one FULL partial-gradient row (330,755 floats = 1.3 MB) per
-// 16 points: 21.7 GB written and read again at 262,144 points.  Here the hidden-layer
-// gradient is a GEMM with K = N x S (one partial per K slice: ~100 per layer) and the
-// per-tile rows shrink to the 3,075 non-hidden parameters.
-//
-// Reference semantics: loss.backward() of base/baseModel.py:73-78 through the jets of
-// base/diff_ops.py:44-82 (the same math as jet_split.hpp / jet_x6.hpp).
-#include "jet_x6.hpp"
+// jet_x6w.hip -- the two-kernel backward (jet_x6w.hpp) at fp32-level accuracy (NQ = 3), and
+// the host helpers of the wide path.
+#include "jet_x6w.hpp"
 
 namespace insr {
-
-
-// compact partial row of the wide path: [W0 (W din) | b0 (W) | b_1 .. b_L (L W) | Wout (dout W) | bout]
-__host__ __device__ inline long small_count(int din, int dout, int L, int W) {
-  return (long)W * din + W + (long)L * W + (long)dout * W + dout;
-}
-
-// ---------------------------------------------------------------------------------------
-// kernel 1: propagation-only reverse sweep (one 16-point tile per block, 8 waves x 2 row tiles)
-// ---------------------------------------------------------------------------------------
-template <int NT, int S, bool LAP>
-__global__ __launch_bounds__(512) void jet_bwd_x6p(const float* __restrict__ x, int N, int din, int dout, int L,
-                                                   const float* __restrict__ prm, const float* __restrict__ act,
-                                                   const float* __restrict__ gy, const float* __restrict__ gdy,
-                                                   const float* __restrict__ glap, float* __restrict__ adj,
-                                                   float* __restrict__ part, long Ps) {
-  constexpr int W = 16 * NT, RPW = NT / 8, KC = NT / 2;
-  constexpr int LDB = W + 8, ZPLANE = 16 * LDB, ZSET = 3 * ZPLANE;
-  constexpr int NTAN = LAP ? S - 2 : S - 1;
-  extern __shared__ __attribute__((aligned(16))) float lds_f[];
-  unsigned short* Z = reinterpret_cast<unsigned short*>(lds_f);  // [s][q][16 p][W + 8]
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
-  const int ntiles = ((N + 63) / 64) * 4;
-  const int tile = blockIdx.x;
-  const int rt0 = wave * RPW;
-  const int p = tile * 16 + c;
-  const bool valid = p < N;
-  float* mypart = part + (long)blockIdx.x * Ps;
-  const long sb = (long)W * din + W;       // compact offset of b_1
-  const long so = sb + (long)L * W;        // compact offset of Wout
-
-  auto adjoint = [&](int s, int o) -> float {
-    if (!valid) return 0.f;
-    if (s == 0) return gy ? gy[(long)p * dout + o] : 0.f;
-    if (LAP && s == S - 1) return glap ? glap[(long)p * dout + o] : 0.f;
-    return gdy ? gdy[((long)p * dout + o) * din + (s - 1)] : 0.f;
-  };
-  auto load_sc = [&](int layer, floatx4(&s_)[RPW], floatx4(&c_)[RPW]) {
-    const float* base = act_base(act, layer, ntiles, tile, S, NT);
-    floatx4 z[RPW];
-    float amax = 0.f;
-#pragma unroll
-    for (int i = 0; i < RPW; ++i) {
-      z[i] = *reinterpret_cast<const floatx4*>(base + ((rt0 + i) * 64 + lane) * 4);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) amax = fmaxf(amax, fabsf(OMEGA * z[i][r]));
-    }
-    const bool big = wave_any_big(amax);
-#pragma unroll
-    for (int i = 0; i < RPW; ++i)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float sv, cv;
-        if (big)
-          sincosf(OMEGA * z[i][r], &sv, &cv);
-        else
-          sincos_fast(OMEGA * z[i][r], sv, cv);
-        s_[i][r] = sv;
-        c_[i][r] = cv;
-      }
-  };
-
-  // ---- output layer (exact fp32 VALU) ----
-  floatx4 sn[RPW], cs[RPW];
-  load_sc(L, sn, cs);
-  const float* Wo = prm + out_off(din, W, L);
-  floatx4 hb[RPW][S];
-#pragma unroll
-  for (int i = 0; i < RPW; ++i)
-#pragma unroll
-    for (int s = 0; s < S; ++s) hb[i][s] = floatx4{0.f, 0.f, 0.f, 0.f};
-  const float* baseL = act_base(act, L, ntiles, tile, S, NT);
-  for (int o = 0; o < dout; ++o) {
-    float ga[S];
-#pragma unroll
-    for (int s = 0; s < S; ++s) ga[s] = adjoint(s, o);
-#pragma unroll
-    for (int i = 0; i < RPW; ++i) {
-      const int rt = rt0 + i;
-      const floatx4 w4 = *reinterpret_cast<const floatx4*>(Wo + (o * W + 16 * rt + 4 * g));
-      floatx4 acc4 = floatx4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int s = 0; s < S; ++s) {
-        const floatx4 hs = h_stream<NT, S, LAP>(baseL, s, rt, lane, sn[i], cs[i]);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          acc4[r] = fmaf(ga[s], hs[r], acc4[r]);
-          hb[i][s][r] = fmaf(w4[r], ga[s], hb[i][s][r]);
-        }
-      }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float v = sum16(acc4[r]);
-        if (c == 0) mypart[so + (long)o * W + 16 * rt + 4 * g + r] = v;
-      }
-    }
-    if (wave == 0) {
-      float v = sum16(g == 0 ? ga[0] : 0.f);
-      if (lane == 0) mypart[so + (long)dout * W + o] = v;
-    }
-  }
-
-  // ---- sine layers j = L .. 0 ----
-  for (int j = L; j >= 0; --j) {
-    const float* basej = act_base(act, j, ntiles, tile, S, NT);
-#pragma unroll
-    for (int i = 0; i < RPW; ++i) {
-      floatx4 zs[S];
-#pragma unroll
-      for (int s = 0; s < S; ++s)
-        zs[s] = (s == 0) ? floatx4{0.f, 0.f, 0.f, 0.f}
-                         : *reinterpret_cast<const floatx4*>(basej + ((s * NT + rt0 + i) * 64 + lane) * 4);
-      sine_rev<S, LAP>(hb[i], zs, sn[i], cs[i]);  // hb = z̄_j
-    }
-    const long boff = (j == 0) ? (long)W * din : sb + (long)(j - 1) * W;
-#pragma unroll
-    for (int i = 0; i < RPW; ++i)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float v = sum16(hb[i][0][r]);
-        if (c == 0) mypart[boff + 16 * (rt0 + i) + 4 * g + r] = v;
-      }
-    if (j == 0) {
-      float xk[3];
-      for (int k = 0; k < 3; ++k) xk[k] = (valid && k < din) ? x[(long)p * din + k] : 0.f;
-#pragma unroll
-      for (int i = 0; i < RPW; ++i)
-        for (int k = 0; k < din; ++k)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            float v = hb[i][0][r] * xk[k];
-            if (k < NTAN) v += hb[i][1 + k][r];
-            v = sum16(v);
-            if (c == 0) mypart[(long)(16 * (rt0 + i) + 4 * g + r) * din + k] = v;
-          }
-      break;
-    }
-    // z̄_j -> HBM (layer slot j - 1), the A operand of dw_x6
-    {
-      float* ab = act_base(adj, j - 1, ntiles, tile, S, NT);
-#pragma unroll
-      for (int i = 0; i < RPW; ++i)
-#pragma unroll
-        for (int s = 0; s < S; ++s) *reinterpret_cast<floatx4*>(ab + ((s * NT + rt0 + i) * 64 + lane) * 4) = hb[i][s];
-    }
-    __syncthreads();  // the previous layer's readers of Z are done
-#pragma unroll
-    for (int i = 0; i < RPW; ++i)
-#pragma unroll
-      for (int s = 0; s < S; ++s) {
-        unsigned h0, m0, l0, h1, m1, l1;
-        split3(hb[i][s][0], hb[i][s][1], h0, m0, l0);
-        split3(hb[i][s][2], hb[i][s][3], h1, m1, l1);
-        unsigned short* pz = Z + s * ZSET + c * LDB + 16 * (rt0 + i) + 4 * g;
-        *reinterpret_cast<u32x2*>(pz) = u32x2{h0, h1};
-        *reinterpret_cast<u32x2*>(pz + ZPLANE) = u32x2{m0, m1};
-        *reinterpret_cast<u32x2*>(pz + 2 * ZPLANE) = u32x2{l0, l1};
-      }
-    __syncthreads();
-    // propagation: h̄_{j-1}[m] = sum_n W_j[n][m] z̄_j[n]; A = W^T rows m of this wave (split at
-    // load), B = Z rows (one b128 per plane)
-    const float* Wj = prm + hidden_off(din, W, j);
-    floatx4 nh[RPW][S];
-#pragma unroll
-    for (int i = 0; i < RPW; ++i)
-#pragma unroll
-      for (int s = 0; s < S; ++s) nh[i][s] = floatx4{0.f, 0.f, 0.f, 0.f};
-    floatx4 raw[RPW][2];
-    auto load_raw = [&](int kc) {
-#pragma unroll
-      for (int i = 0; i < RPW; ++i)
-#pragma unroll
-        for (int jj = 0; jj < 4; ++jj) {
-          raw[i][0][jj] = Wj[(32 * kc + 8 * g + jj) * W + 16 * (rt0 + i) + c];
-          raw[i][1][jj] = Wj[(32 * kc + 8 * g + 4 + jj) * W + 16 * (rt0 + i) + c];
-        }
-    };
-    load_raw(0);
-#pragma unroll 1
-    for (int kc = 0; kc < KC; ++kc) {
-      Frag3 wt[RPW];
-#pragma unroll
-      for (int i = 0; i < RPW; ++i) wt[i] = split_frag(raw[i][0], raw[i][1]);
-      if (kc + 1 < KC) load_raw(kc + 1);  // L2-resident W rows, in flight during this chunk's MFMAs
-#pragma unroll
-      for (int s = 0; s < S; ++s) {
-        Frag3 bf;
-        const unsigned short* pb = Z + s * ZSET + c * LDB + 32 * kc + 8 * g;
-        bf.h = *reinterpret_cast<const u32x4*>(pb);
-        bf.m = *reinterpret_cast<const u32x4*>(pb + ZPLANE);
-        bf.l = *reinterpret_cast<const u32x4*>(pb + 2 * ZPLANE);
-#pragma unroll
-        for (int i = 0; i < RPW; ++i) nh[i][s] = mfma_x6(wt[i], bf, nh[i][s]);
-        X6_SCHED_FENCE();  // keep the next stream's B reads from being hoisted (register budget)
-      }
-    }
-    load_sc(j - 1, sn, cs);  // sin/cos of layer j-1 for the next sine reverse
-#pragma unroll
-    for (int i = 0; i < RPW; ++i)
-#pragma unroll
-      for (int s = 0; s < S; ++s) hb[i][s] = nh[i][s];
-  }
-}
-
-// ---------------------------------------------------------------------------------------
-// kernel 2: hidden-layer weight gradients, split-K GEMM on the x6 matrix cores
-//   block (slice, layer j = blockIdx.y + 1): 8 waves; wave w owns dW rows n in row tiles
-//   {2w, 2w + 1} x all 16 column tiles (128 accumulator VGPRs).  K is walked in chunks of
-//   two (tile, stream) units = 32 = one v_mfma_f32_16x16x32_bf16 k-step.  LDS images:
-//   A = z̄ [q][n][k], B = h [q][m][k] (k minor, rows padded to 40: conflict-free b128 reads);
-//   the loaders pack two adjacent points per u32 (DPP lane swap) and split each value once.
-// ---------------------------------------------------------------------------------------
-constexpr int kDwKR = 40;  // k row (32 + 8 pad) in bf16 elements
-template <int NT>
-constexpr int dw_plane() { return 16 * NT * kDwKR; }  // one plane (bf16 elements)
-template <int NT>
-constexpr size_t dw_lds() { return (size_t)6 * dw_plane<NT>() * 2; }  // A + B, 3 planes each
-
-__device__ __forceinline__ float swap1(float v) {  // value of lane ^ 1 (quad_perm 1,0,3,2)
-  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, false));
-}
-
-// write one granule (4 neurons 4g..4g+3 of row tile rt, point c) as point pairs into the
-// k-minor planes: even lanes write neurons r = 0, 1 of points (c, c + 1), odd lanes r = 2, 3
-// of points (c - 1, c)
-template <int NT>
-__device__ __forceinline__ void dw_put(unsigned short* P, const floatx4& v, int rt, int ul, int lane) {
-  constexpr int kDwPL = dw_plane<NT>();
-  const int g = lane >> 4, c = lane & 15, odd = c & 1;
-  const float r0 = swap1(odd ? v[0] : v[2]);
-  const float r1 = swap1(odd ? v[1] : v[3]);
-  const float a0 = odd ? r0 : v[0], b0 = odd ? v[2] : r0;
-  const float a1 = odd ? r1 : v[1], b1 = odd ? v[3] : r1;
-  const int n0 = 16 * rt + 4 * g + (odd ? 2 : 0);
-  const int k = 16 * ul + (c & ~1);
-  unsigned h, m, l;
-  split3(a0, b0, h, m, l);
-  unsigned* q0 = reinterpret_cast<unsigned*>(P + n0 * kDwKR + k);
-  q0[0] = h;
-  q0[kDwPL / 2] = m;
-  q0[kDwPL] = l;
-  split3(a1, b1, h, m, l);
-  unsigned* q1 = reinterpret_cast<unsigned*>(P + (n0 + 1) * kDwKR + k);
-  q1[0] = h;
-  q1[kDwPL / 2] = m;
-  q1[kDwPL] = l;
-}
-
-template <int NT, int S, bool LAP>
-__global__ __launch_bounds__(512) void dw_x6(int N, const float* __restrict__ act, const float* __restrict__ adj,
-                                             float* __restrict__ dpart, int KS) {
-  constexpr int W = 16 * NT, RT = NT / 8;  // RT: dW row tiles per wave
-  constexpr int G = NT / 4;                   // granules per thread per chunk (2 units x NT row tiles / 8 waves)
-  constexpr int kDwPL = dw_plane<NT>();
-  extern __shared__ __attribute__((aligned(16))) float lds_f[];
-  unsigned short* A = reinterpret_cast<unsigned short*>(lds_f);
-  unsigned short* B = A + 3 * kDwPL;
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
-  const int j = blockIdx.y + 1;
-  const int ntiles = ((N + 63) / 64) * 4;
-  const int units = ((N + 15) / 16) * S;
-  const int chunks = (units + 1) / 2;
-  const int c0 = (int)((long)chunks * blockIdx.x / KS), c1 = (int)((long)chunks * (blockIdx.x + 1) / KS);
-
-  floatx4 dacc[RT][NT];
-#pragma unroll
-  for (int i = 0; i < RT; ++i)
-#pragma unroll
-    for (int ct = 0; ct < NT; ++ct) dacc[i][ct] = floatx4{0.f, 0.f, 0.f, 0.f};
-
-  // raw operands of one chunk, per thread: 4 granules (unit ul = it >> 1, row tile
-  // wave + 8 (it & 1)) of z̄_j, z_{j-1} (stream 0) and z_{j-1} (stream s).  The next chunk's
-  // loads are issued before the MFMA phase of the current one (software pipeline).
-  floatx4 rzb[G], rz0[G], rzs[G];
-  // branch-free: a granule past the end loads unit 0 (valid memory) and is zeroed in put(),
-  // so the compiler keeps every load of the chunk in flight (no waitcnt inside fetch)
-  auto fetch = [&](int ch) {
-#pragma unroll
-    for (int it = 0; it < G; ++it) {
-      const int ul = it / RT, rt = wave + 8 * (it % RT);
-      const int u = 2 * ch + ul;
-      const int uu = (ch < c1 && u < units) ? u : 0;
-      const int t = uu / S, s = uu - t * S;
-      const float* ba = act_base(act, j - 1, ntiles, t, S, NT);
-      rzb[it] = *reinterpret_cast<const floatx4*>(act_base(adj, j - 1, ntiles, t, S, NT) +
-                                                  ((s * NT + rt) * 64 + lane) * 4);
-      if (S % 2 != 0 || it < RT) rz0[it] = *reinterpret_cast<const floatx4*>(ba + (rt * 64 + lane) * 4);
-      rzs[it] = *reinterpret_cast<const floatx4*>(ba + ((s * NT + rt) * 64 + lane) * 4);
-    }
-  };
-  floatx4 ssv[G], scv[G];
-  auto put = [&](int ch) {
-#pragma unroll
-    for (int it = 0; it < G; ++it) {
-      const int ul = it / RT, rt = wave + 8 * (it % RT);
-      const int u = 2 * ch + ul;
-      const bool live = u < units;
-      const int uu = live ? u : 0;
-      const int t = uu / S, s = uu - t * S;
-      // even S: units 2ch, 2ch + 1 are streams of ONE tile, so granules it and it + RT share z0
-      constexpr bool kShare = S % 2 == 0;
-      if (!kShare || it < RT) {
-        float amax = 0.f;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) amax = fmaxf(amax, fabsf(OMEGA * rz0[it][r]));
-        const bool big = wave_any_big(amax);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          float a, b;
-          if (big)
-            sincosf(OMEGA * rz0[it][r], &a, &b);
-          else
-            sincos_fast(OMEGA * rz0[it][r], a, b);
-          ssv[kShare ? it % RT : it][r] = a;
-          scv[kShare ? it % RT : it][r] = b;
-        }
-      }
-      const floatx4 sv = ssv[kShare ? it % RT : it], cv = scv[kShare ? it % RT : it];
-      floatx4 hv;
-      if (LAP && s == S - 1) {  // Laplacian stream: needs the tangents (read here)
-        hv = h_stream<NT, S, LAP>(act_base(act, j - 1, ntiles, t, S, NT), s, rt, lane, sv, cv);
-      } else {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) hv[r] = s == 0 ? sv[r] : OMEGA * cv[r] * rzs[it][r];
-      }
-      const floatx4 zero = floatx4{0.f, 0.f, 0.f, 0.f};
-      dw_put<NT>(A, live ? rzb[it] : zero, rt, ul, lane);
-      dw_put<NT>(B, live ? hv : zero, rt, ul, lane);
-    }
-  };
-
-  fetch(c0);
-  for (int ch = c0; ch < c1; ++ch) {
-    __syncthreads();  // the previous chunk's MFMA readers are done
-    put(ch);
-    fetch(ch + 1);
-    __syncthreads();
-    Frag3 af[RT];
-#pragma unroll
-    for (int i = 0; i < RT; ++i) {
-      const unsigned short* pa = A + (16 * (RT * wave + i) + c) * kDwKR + 8 * g;
-      af[i].h = *reinterpret_cast<const u32x4*>(pa);
-      af[i].m = *reinterpret_cast<const u32x4*>(pa + kDwPL);
-      af[i].l = *reinterpret_cast<const u32x4*>(pa + 2 * kDwPL);
-    }
-#pragma unroll
-    for (int ct = 0; ct < NT; ++ct) {
-      Frag3 bf;
-      const unsigned short* pb = B + (16 * ct + c) * kDwKR + 8 * g;
-      bf.h = *reinterpret_cast<const u32x4*>(pb);
-      bf.m = *reinterpret_cast<const u32x4*>(pb + kDwPL);
-      bf.l = *reinterpret_cast<const u32x4*>(pb + 2 * kDwPL);
-#pragma unroll
-      for (int i = 0; i < RT; ++i) dacc[i][ct] = mfma_x6(af[i], bf, dacc[i][ct]);
-    }
-  }
-  float* out = dpart + ((long)(j - 1) * KS + blockIdx.x) * W * W;
-#pragma unroll
-  for (int i = 0; i < RT; ++i)
-#pragma unroll
-    for (int ct = 0; ct < NT; ++ct)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) out[(16 * (RT * wave + i) + 4 * g + r) * W + 16 * ct + c] = dacc[i][ct][r];
-}
-
-// ---------------------------------------------------------------------------------------
-// reductions of the wide path (fixed order, no atomics)
-// ---------------------------------------------------------------------------------------
-// compact rows -> the net's flat gradient (column i of the compact row -> its flat index)
-__global__ __launch_bounds__(256) void reduce_small_kernel(const float* __restrict__ part, int nb, long count,
-                                                           int din, int dout, int L, int W, float* __restrict__ grad,
-                                                           int accumulate) {
-  __shared__ float red[4][64];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const long i = (long)blockIdx.x * 64 + lane;
-  float acc = 0.f;
-  if (i < count)
-    for (int b = w; b < nb; b += 4) acc += part[(long)b * count + i];
-  red[w][lane] = acc;
-  __syncthreads();
-  if (w == 0 && i < count) {
-    const float t = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
-    const long head = (long)W * din + W, hid = (long)L * W;
-    long dst;
-    if (i < head)
-      dst = i;
-    else if (i < head + hid)
-      dst = hidden_off(din, W, 1 + (int)((i - head) / W)) + (long)W * W + (i - head) % W;
-    else
-      dst = out_off(din, W, L) + (i - head - hid);
-    grad[dst] = accumulate ? grad[dst] + t : t;
-  }
-}
-
-// first level of the compact-row reduction: RS row slices -> RS rows (fixed order)
-constexpr int kSmallRS = 32;
-__global__ __launch_bounds__(256) void reduce_rows_kernel(const float* __restrict__ part, int nb, long count,
-                                                          float* __restrict__ out) {
-  __shared__ float red[4][64];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const long i = (long)blockIdx.x * 64 + lane;
-  const int b0 = (int)((long)nb * blockIdx.y / gridDim.y), b1 = (int)((long)nb * (blockIdx.y + 1) / gridDim.y);
-  float acc = 0.f;
-  if (i < count)
-    for (int b = b0 + w; b < b1; b += 4) acc += part[(long)b * count + i];
-  red[w][lane] = acc;
-  __syncthreads();
-  if (w == 0 && i < count) out[(long)blockIdx.y * count + i] = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
-}
-
-// per hidden layer: sum of the KS partial W x W blocks
-__global__ __launch_bounds__(256) void reduce_dw_kernel(const float* __restrict__ dpart, int KS, int din, int W,
-                                                        float* __restrict__ grad, int accumulate) {
-  const int j = blockIdx.y + 1;
-  const long WW = (long)W * W;
-  const long i = (long)blockIdx.x * 256 + threadIdx.x;
-  if (i >= WW) return;
-  const float* src = dpart + (long)(j - 1) * KS * WW + i;
-  float acc = 0.f;
-  for (int k = 0; k < KS; ++k) acc += src[(long)k * WW];
-  float* dst = grad + hidden_off(din, W, j) + i;
-  *dst = accumulate ? *dst + acc : acc;
-}
-
-// ---------------------------------------------------------------------------------------
-// host side
-// ---------------------------------------------------------------------------------------
-int wide_ks(long n, int S, int L) {
-  const long chunks = (((n + 15) / 16) * S + 1) / 2;
-  long ks = 512 / (L > 0 ? L : 1);  // L x KS <= 512 blocks: two full rounds of 256 one-block CUs
-  if (ks > chunks) ks = chunks;
-  return ks < 1 ? 1 : (int)ks;
-}
-
-// workspace floats: z̄ of the L hidden layers | compact rows | dW partials
+template int dispatch_wide_bwd_q<3>(int, int, bool, const float*, int, int, int, int, const float*, const float*,
+                                    const float*, const float*, const float*, float*, float*, int, hipStream_t);
 long wide_work_floats(long n, int din, int dout, int L, int W, int S) {
-  const long ntiles = ((n + 63) / 64) * 4;
-  const long adj = (long)L * ntiles * S * (W / 16) * 256;
-  const long small = ((n + 15) / 16) * small_count(din, dout, L, W);
-  const long dw = (long)L * wide_ks(n, S, L) * W * W;
-  return adj + small + dw + (long)kSmallRS * small_count(din, dout, L, W);
+  return wide_work_floats_impl(n, din, dout, L, W, S);
 }
-
-template <int NT, int S, bool LAP>
-int wide_bwd_t(const float* x, int N, int din, int dout, int L, const float* prm, const float* act, const float* gy,
-               const float* gdy, const float* glap, float* work, float* grad, int accumulate, hipStream_t st) {
-  constexpr int W = 16 * NT;
-  const long ntiles = ((N + 63) / 64) * 4;
-  const int tiles = (N + 15) / 16;
-  const long Ps = small_count(din, dout, L, W);
-  float* adj = work;
-  float* small = adj + (long)L * ntiles * S * NT * 256;
-  float* dpart = small + (long)tiles * Ps;
-  float* rows = dpart + (long)L * wide_ks(N, S, L) * W * W;
-  constexpr size_t lds_p = (size_t)S * 3 * 16 * (W + 8) * 2;
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)jet_bwd_x6p<NT, S, LAP>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)lds_p);
-    (void)hipFuncSetAttribute((const void*)dw_x6<NT, S, LAP>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)dw_lds<NT>());
-    attr = true;
-  }
-  hipLaunchKernelGGL((jet_bwd_x6p<NT, S, LAP>), dim3(tiles), dim3(512), lds_p, st, x, N, din, dout, L, prm, act, gy,
-                     gdy, glap, adj, small, Ps);
-  if (L > 0) {
-    const int KS = wide_ks(N, S, L);
-    hipLaunchKernelGGL((dw_x6<NT, S, LAP>), dim3(KS, L), dim3(512), dw_lds<NT>(), st, N, act, adj, dpart, KS);
-    hipLaunchKernelGGL(reduce_dw_kernel, dim3((unsigned)((W * W + 255) / 256), L), dim3(256), 0, st, dpart, KS, din, W,
-                       grad, accumulate);
-  }
-  const int rs = tiles < kSmallRS ? tiles : kSmallRS;
-  hipLaunchKernelGGL(reduce_rows_kernel, dim3((unsigned)((Ps + 63) / 64), rs), dim3(256), 0, st, small, tiles, Ps, rows);
-  hipLaunchKernelGGL(reduce_small_kernel, dim3((unsigned)((Ps + 63) / 64)), dim3(256), 0, st, rows, rs, Ps, din, dout,
-                     L, W, grad, accumulate);
-  return (int)hipGetLastError();
-}
-
-template <int NT>
-int wide_bwd_nt(int S, bool LAP, const float* x, int N, int din, int dout, int L, const float* prm, const float* act,
-                const float* gy, const float* gdy, const float* glap, float* work, float* grad, int accumulate,
-                hipStream_t st) {
-  switch (S * 2 + (LAP ? 1 : 0)) {
-    case 2: return wide_bwd_t<NT, 1, false>(x, N, din, dout, L, prm, act, gy, gdy, glap, work, grad, accumulate, st);
-    case 4: return wide_bwd_t<NT, 2, false>(x, N, din, dout, L, prm, act, gy, gdy, glap, work, grad, accumulate, st);
-    case 6: return wide_bwd_t<NT, 3, false>(x, N, din, dout, L, prm, act, gy, gdy, glap, work, grad, accumulate, st);
-    case 8: return wide_bwd_t<NT, 4, false>(x, N, din, dout, L, prm, act, gy, gdy, glap, work, grad, accumulate, st);
-    case 7: return wide_bwd_t<NT, 3, true>(x, N, din, dout, L, prm, act, gy, gdy, glap, work, grad, accumulate, st);
-    case 9: return wide_bwd_t<NT, 4, true>(x, N, din, dout, L, prm, act, gy, gdy, glap, work, grad, accumulate, st);
-    default: return INSR_EINVAL;
-  }
-}
-
-int dispatch_wide_bwd(int NT, int S, bool LAP, const float* x, int N, int din, int dout, int L, const float* prm,
-                      const float* act, const float* gy, const float* gdy, const float* glap, float* work, float* grad,
-                      int accumulate, hipStream_t st) {
-  if (NT == 16) return wide_bwd_nt<16>(S, LAP, x, N, din, dout, L, prm, act, gy, gdy, glap, work, grad, accumulate, st);
-  if (NT == 8) return wide_bwd_nt<8>(S, LAP, x, N, din, dout, L, prm, act, gy, gdy, glap, work, grad, accumulate, st);
-  return INSR_EWIDTH;
-}
-
 }  // namespace insr

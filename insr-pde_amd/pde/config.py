@@ -21,7 +21,7 @@ PDE = {
                        collide_circle_y=-2e0, collide_circle_z=0.0, collide_circle_radius=1.0),
 }
 # insr-pde_amd execution knobs (see base/_loop.py)
-EXEC = dict(insr_sync_every=1, insr_graph=False, insr_progress=True, insr_band_stream=False, insr_nograd_stream=False,
+EXEC = dict(insr_precision=None, insr_sync_every=1, insr_graph=False, insr_progress=True, insr_band_stream=False, insr_nograd_stream=False,
             insr_fuse_forwards=os.environ.get("INSR_FUSE_FORWARDS", "1") != "0")
 
 

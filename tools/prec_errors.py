@@ -1,5 +1,5 @@
 """Normwise error of the HIP jets against the CPU oracle for each matrix-core
-precision (fp32 MFMA vs split-bf16 x6), per network / op: value, derivative and
+precision (fp32 MFMA, split-bf16 x6 / x3, plain bf16), per network / op: value, derivative and
 parameter gradients.  Prints one JSON line per (net, op, precision).
 
     python tools/prec_errors.py [--n 4000]
@@ -50,7 +50,7 @@ def main():
                 p.grad = None
             (vr * R).sum().backward()
             gref = [p.grad if p.grad is not None else torch.zeros_like(p) for p in ref.parameters()]
-            for prec in (0, 1):
+            for prec in (0, 1, 2, 3):
                 base._native.set_precision(prec, prec)
                 net.zero_grad(set_to_none=True)
                 xg = x.cuda().requires_grad_(True)
@@ -61,7 +61,7 @@ def main():
                 torch.cuda.synchronize()
                 pe = [nerr(p.grad if p.grad is not None else torch.zeros_like(p), g)
                       for p, g in zip(net.parameters(), gref)]
-                print(json.dumps({"net": name, "op": op, "prec": ["f32", "bf16x6"][prec], "n": args.n,
+                print(json.dumps({"net": name, "op": op, "prec": ["f32", "bf16x6", "bf16x3", "bf16"][prec], "n": args.n,
                                   "field_err": nerr(v, vr), "param_grad_err_max": max(pe),
                                   "param_grad_err": [round(e, 9) for e in pe]}), flush=True)
 
