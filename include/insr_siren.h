@@ -269,6 +269,28 @@ long insr_sq_loss_work_floats(void);
 int insr_sq_loss_fwd(int kind, const float* a, const float* b, const float* c, const float* d, long n, int m,
                      float alpha, float beta, float gamma, float delta, float scale, float* out, float* work,
                      void* stream);
+/* A group of up to INSR_LOSS_GROUP_MAX losses (every residual term of one phase iteration)
+ * in ONE launch, each with its gradient for a unit output seed (the training loop's backward
+ * seeds every loss with 1): loss k = insr_sq_loss_fwd of (kind, a..d, n, m, coefficients,
+ * scale) written to *out, and d(out)/d(input) to ga / gb / gc / gd (any may be NULL) over their
+ * full length (*_len elements): zeros outside the loss range.  The loss reads a from element
+ * a_off (COMBO: n terms; BANDS: rows a_off / m .. a_off / m + 2n of an (R, m) tensor, a_off a
+ * multiple of m), b, c, d from element 0.  work: insr_sq_loss_work_floats() floats,
+ * zero-initialised once (left zero).  The backward of a unit-seeded loss then needs no launch. */
+#define INSR_LOSS_GROUP_MAX 4
+typedef struct InsrLoss {
+  int kind;  /* INSR_LOSS_COMBO / INSR_LOSS_BANDS */
+  int m;     /* BANDS: columns of a */
+  long n;    /* COMBO: terms; BANDS: rows per band */
+  const float *a, *b, *c, *d;
+  float alpha, beta, gamma, delta, scale;
+  float* out;
+  float* ga;
+  long ga_len, a_off;
+  float *gb, *gc, *gd;
+  long gb_len, gc_len, gd_len;
+} InsrLoss;
+int insr_sq_loss_group(const InsrLoss* losses, int count, float* work, void* stream);
 int insr_sq_loss_bwd(int kind, const float* a, const float* b, const float* c, const float* d, long n, int m,
                      float alpha, float beta, float gamma, float delta, float scale, const float* gout, float* ga,
                      float* gb, float* gc, float* gd, void* stream);

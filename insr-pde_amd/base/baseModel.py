@@ -204,7 +204,8 @@ class BaseModel(ABC):
         seeds = self.__dict__.setdefault("_insr_seeds", {})
         key = (v.device, v.dtype, tuple(v.shape))
         if key not in seeds:
-            seeds[key] = torch.ones(v.shape, device=v.device, dtype=v.dtype)
+            from .losses import register_unit_seed
+            seeds[key] = register_unit_seed(torch.ones(v.shape, device=v.device, dtype=v.dtype))
         return seeds[key]
 
     def _set_require_grads(self, model, require_grad):

@@ -72,51 +72,29 @@ def _grad_like(t, n_used):
     return torch.empty_like(t) if t.numel() == n_used else torch.zeros_like(t)
 
 
-class _SqLoss(torch.autograd.Function):
-    # offs: element offset of the loss range in each of a, b, c, d (n terms for COMBO,
-    # the 2n x m band rows for BANDS)
-    @staticmethod
-    def forward(ctx, kind, n, m, coef, scale, offs, a, b, c, d):
-        lib = nat.lib()
-        dev = a.device
-        # the partials workspace (one per device and stream) is needed only by losses over
-        # more than kLossPerBlock = 4096 terms
-        terms = n if kind == nat.LOSS_COMBO else 2 * n
-        work = _workspace(dev) if terms > 4096 else None
-        out = torch.empty((), device=dev, dtype=torch.float32)
-        rc = lib.insr_sq_loss_fwd(kind, _at(a, offs[0]), _at(b, offs[1]), _at(c, offs[2]), _at(d, offs[3]), n, m,
-                                  *coef, scale, nat.ptr(out), nat.ptr(work), nat.stream_of(dev))
-        nat.check(rc, "insr_sq_loss_fwd")
-        ctx.save_for_backward(a, b, c, d)
-        ctx.args = (kind, n, m, coef, scale, offs)
-        return out
-
-    @staticmethod
-    def backward(ctx, gout):
-        a, b, c, d = ctx.saved_tensors
-        kind, n, m, coef, scale, offs = ctx.args
-        need = ctx.needs_input_grad[6:10]
-        if not any(need):
-            return (None,) * 10
-        used = n if kind == nat.LOSS_COMBO else 2 * n * m
-        grads = [_grad_like(t, used) if (t is not None and nd) else None for t, nd in zip((a, b, c, d), need)]
-        g = gout.reshape(1) if gout.is_contiguous() else gout.contiguous().reshape(1)
-        rc = nat.lib().insr_sq_loss_bwd(kind, _at(a, offs[0]), _at(b, offs[1]), _at(c, offs[2]), _at(d, offs[3]),
-                                        n, m, *coef, scale, nat.ptr(g),
-                                        *[_at(t, o) for t, o in zip(grads, offs)], nat.stream_of(a.device))
-        nat.check(rc, "insr_sq_loss_bwd")
-        return (None, None, None, None, None, None, *grads)
+# Unit seeds: 1-element tensors holding 1.0 that the training loop passes as the gradient of
+# every loss (BaseModel._unit_seed).  A loss whose backward receives one of them returns the
+# gradient its forward launch already wrote -- no backward launch.
+_UNIT_SEEDS = set()
 
 
-def fused_mse(a, b=None, c=None, d=None, alpha=1.0, beta=-1.0, gamma=1.0, delta=1.0, count=None, a_row0=0,
+def register_unit_seed(t):
+    """Declare `t` (a tensor of ones the caller never modifies) a unit seed for loss backwards."""
+    if t.numel() == 1:
+        _UNIT_SEEDS.add(t.data_ptr())
+    return t
+
+
+class LossSpec:
+    """One squared-residual loss, not yet launched (see sq_losses)."""
+
+    def __init__(self, kind, n, m, coef, scale, a, b, c, d, a_off):
+        self.meta = (kind, int(n), int(m), tuple(float(v) for v in coef), float(scale), int(a_off))
+        self.tensors = (a, b, c, d)
+
+
+def _mse_spec(a, b=None, c=None, d=None, alpha=1.0, beta=-1.0, gamma=1.0, delta=1.0, count=None, a_row0=0,
               reduction="mean"):
-    """mean((alpha*(a + beta*b) + gamma*(c + delta*d))**2) over all elements; b, c, d are
-    None or the shape of a (d needs c).  fused_mse(u, target) == F.mse_loss(u, target).
-
-    Merged jet launches (interior + boundary points of one network in one launch):
-    count = number of terms; every tensor is read from its first element except `a`,
-    which starts at row a_row0; elements outside the range get zero gradient.
-    reduction="sum" returns the sum instead of the mean."""
     if count is None:
         for t in (b, c, d):
             if t is not None and t.shape != a.shape:
@@ -131,21 +109,116 @@ def fused_mse(a, b=None, c=None, d=None, alpha=1.0, beta=-1.0, gamma=1.0, delta=
         raise ValueError("fused_mse: d needs c")
     if reduction not in ("mean", "sum"):
         raise ValueError(reduction)
-    a, b, c, d = _prep(a), _prep(b), _prep(c), _prep(d)
-    coef = (float(alpha), float(beta), float(gamma), float(delta))
     scale = 1.0 / max(count, 1) if reduction == "mean" else 1.0
-    return _SqLoss.apply(nat.LOSS_COMBO, int(count), 1, coef, scale, (a_off, 0, 0, 0), a, b, c, d)
+    return LossSpec(nat.LOSS_COMBO, count, 1, (alpha, beta, gamma, delta), scale, _prep(a), _prep(b), _prep(c),
+                    _prep(d), a_off)
+
+
+def _wall_spec(y, n, row0=0):
+    if y.dim() != 2 or y.shape[0] < row0 + 2 * n or y.shape[1] < 2 or (row0 == 0 and y.shape[0] != 2 * n):
+        raise ValueError(f"wall_mse: expected ({row0} + 2*{n} rows, m>=2), got {tuple(y.shape)}")
+    return LossSpec(nat.LOSS_BANDS, n, y.shape[1], (0.0, 0.0, 0.0, 0.0), 1.0 / max(n, 1), _prep(y), None, None, None,
+                    int(row0) * y.shape[1])
+
+
+def mse_term(*args, **kwargs):
+    """The loss of fused_mse(*args, **kwargs), unlaunched: an argument of sq_losses()."""
+    return _mse_spec(*args, **kwargs)
+
+
+def wall_term(y, n, row0=0):
+    """The loss of wall_mse(y, n, row0), unlaunched: an argument of sq_losses()."""
+    return _wall_spec(y, n, row0)
+
+
+class _SqLossGroup(torch.autograd.Function):
+    """Up to LOSS_GROUP_MAX losses in ONE launch forward (insr_sq_loss_group), each with the
+    gradient for a unit seed written by the same launch; inputs: 4 tensor slots per loss."""
+
+    @staticmethod
+    def forward(ctx, metas, *tensors):
+        lib = nat.lib()
+        k = len(metas)
+        dev = next(t for t in tensors if t is not None).device
+        need = ctx.needs_input_grad[1:]
+        outs = [torch.empty((), device=dev, dtype=torch.float32) for _ in range(k)]
+        arr = (nat.Loss * k)()
+        grads = []
+        multi = False
+        for i, (kind, n, m, coef, scale, a_off) in enumerate(metas):
+            slot = tensors[4 * i:4 * i + 4]
+            g = [torch.empty_like(t) if (t is not None and nd) else None for t, nd in zip(slot, need[4 * i:4 * i + 4])]
+            grads.extend(g)
+            lens = [0 if t is None else t.numel() for t in g]
+            span = max(lens + [n if kind == nat.LOSS_COMBO else 2 * n])
+            multi = multi or span > 1024
+            p = lambda t: None if t is None else t.data_ptr()  # noqa: E731
+            a, b, c, d = slot
+            arr[i] = nat.Loss(kind, m, n, p(a), p(b), p(c), p(d), *coef, scale, outs[i].data_ptr(),
+                              p(g[0]), lens[0], a_off, p(g[1]), p(g[2]), p(g[3]), lens[1], lens[2], lens[3])
+        work = _workspace(dev) if multi else None
+        nat.check(lib.insr_sq_loss_group(arr, k, nat.ptr(work), nat.stream_of(dev)), "insr_sq_loss_group")
+        ctx.save_for_backward(*tensors)
+        ctx.metas = metas
+        ctx.pre = grads
+        return tuple(outs)
+
+    @staticmethod
+    def backward(ctx, *gouts):
+        tensors = ctx.saved_tensors
+        need = ctx.needs_input_grad[1:]
+        res = [None] * len(tensors)
+        for i, (kind, n, m, coef, scale, a_off) in enumerate(ctx.metas):
+            sl = slice(4 * i, 4 * i + 4)
+            if not any(need[sl]):
+                continue
+            gout = gouts[i]
+            if gout is None:
+                continue
+            if gout.numel() == 1 and gout.data_ptr() in _UNIT_SEEDS:
+                res[sl] = ctx.pre[sl]
+                continue
+            a, b, c, d = tensors[sl]
+            offs = (a_off, 0, 0, 0)
+            used = n if kind == nat.LOSS_COMBO else 2 * n * m
+            g = [_grad_like(t, used) if (t is not None and nd) else None for t, nd in zip((a, b, c, d), need[sl])]
+            go = gout.reshape(1) if gout.is_contiguous() else gout.contiguous().reshape(1)
+            rc = nat.lib().insr_sq_loss_bwd(kind, _at(a, offs[0]), _at(b, 0), _at(c, 0), _at(d, 0), n, m, *coef,
+                                            scale, nat.ptr(go), *[_at(t, o) for t, o in zip(g, offs)],
+                                            nat.stream_of(a.device))
+            nat.check(rc, "insr_sq_loss_bwd")
+            res[sl] = g
+        ctx.pre = None
+        return (None, *res)
+
+
+def sq_losses(*specs):
+    """Launch every loss term of `specs` (mse_term / wall_term) in ONE kernel; returns their
+    scalar losses in order (each differentiable; a unit-seeded backward costs no launch)."""
+    if not 1 <= len(specs) <= nat.LOSS_GROUP_MAX:
+        raise ValueError(f"sq_losses: 1..{nat.LOSS_GROUP_MAX} losses")
+    metas = tuple(sp.meta for sp in specs)
+    tensors = [t for sp in specs for t in sp.tensors]
+    return _SqLossGroup.apply(metas, *tensors)
+
+
+def fused_mse(a, b=None, c=None, d=None, alpha=1.0, beta=-1.0, gamma=1.0, delta=1.0, count=None, a_row0=0,
+              reduction="mean"):
+    """mean((alpha*(a + beta*b) + gamma*(c + delta*d))**2) over all elements; b, c, d are
+    None or the shape of a (d needs c).  fused_mse(u, target) == F.mse_loss(u, target).
+
+    Merged jet launches (interior + boundary points of one network in one launch):
+    count = number of terms; every tensor is read from its first element except `a`,
+    which starts at row a_row0; elements outside the range get zero gradient.
+    reduction="sum" returns the sum instead of the mean."""
+    return sq_losses(_mse_spec(a, b, c, d, alpha, beta, gamma, delta, count, a_row0, reduction))[0]
 
 
 def wall_mse(y, n, row0=0):
     """mean(y[r:r+n, 0]**2) + mean(y[r+n:r+2n, 1]**2), r = row0, for y of shape (R, m),
     m >= 2, R >= r + 2n (the normal-component wall terms of both boundary bands in one
     launch; the other rows -- a merged launch's interior points -- get zero gradient)."""
-    if y.dim() != 2 or y.shape[0] < row0 + 2 * n or y.shape[1] < 2 or (row0 == 0 and y.shape[0] != 2 * n):
-        raise ValueError(f"wall_mse: expected ({row0} + 2*{n} rows, m>=2), got {tuple(y.shape)}")
-    y = _prep(y)
-    return _SqLoss.apply(nat.LOSS_BANDS, n, y.shape[1], (0.0, 0.0, 0.0, 0.0), 1.0 / max(n, 1),
-                         (int(row0) * y.shape[1], 0, 0, 0), y, None, None, None)
+    return sq_losses(_wall_spec(y, n, row0))[0]
 
 
 _SVD_WORK = {}  # (device index, stream handle) -> partials buffer of the SVD-energy reduction

@@ -76,16 +76,17 @@ int nq_of(int prec) {
 
 // Backward through the two-kernel path (jet_x6w.hpp: propagation kernel + split-K dW GEMM)
 // for the split-bf16 precisions at widths >= g_wide_min (default 256; env
-// INSR_WIDE_MIN_WIDTH) and, at width 128, for Laplacian jets of >= 32768 points.  Measured
-// (profiles/r01/kbench_wide*.jsonl): W = 256 el3D grad 20.7 -> 10.0 ms; W = 128 LAP 65536
-// points 949 -> 805 us, while W = 128 value / grad jets and LAP at 16384 points are as fast
-// or faster fused.
+// INSR_WIDE_MIN_WIDTH) and, at width 128, for Laplacian jets of >= 8192 points and 3-4
+// stream gradient jets of >= 32768 points.  Measured (profiles/r02/kbench_wide_vs_fused.jsonl,
+// backward into .grad incl. reductions): LAP 16384 points 244 -> 182 us, LAP 65536 813 -> 698,
+// GRAD (S = 3) 65536 595 -> 548; GRAD 16384 140 vs 144 and every value jet stay fused.
 static int g_wide_min = -1;
 bool use_wide(long n, int S, int NT, bool lap, int nq) {
   if (g_wide_min < 0) g_wide_min = env_or("INSR_WIDE_MIN_WIDTH", 256);
   if (NT < 8 || nq == 0) return false;
   if (16 * NT >= g_wide_min) return true;
-  return NT == 8 && lap && n >= 32768 && g_wide_min <= 256;  // Laplacian jets at width 128
+  if (NT != 8 || g_wide_min > 256) return false;
+  return lap ? n >= 8192 : (S >= 3 && n >= 32768);
 }
 
 static int cu_count() {

@@ -37,8 +37,13 @@ __host__ __device__ inline long small_count(int din, int dout, int L, int W) {
 // ---------------------------------------------------------------------------------------
 // kernel 1: propagation-only reverse sweep (one 16-point tile per block, 8 waves x 2 row tiles)
 // ---------------------------------------------------------------------------------------
+// W = 128: held to 128 VGPRs (4 waves per SIMD = two 8-wave blocks per CU; its 52 KB of LDS
+// allow three) -- the one-tile sweep is latency-bound, a second resident block hides it
+template <int NT>
+constexpr int x6p_min_waves() { return NT == 8 ? 4 : 1; }
+
 template <int NQ, int NT, int S, bool LAP>
-__global__ __launch_bounds__(512) void jet_bwd_x6p(const float* __restrict__ x, int N, int din, int dout, int L,
+__global__ __launch_bounds__(512, (x6p_min_waves<NT>())) void jet_bwd_x6p(const float* __restrict__ x, int N, int din, int dout, int L,
                                                    const float* __restrict__ prm, const float* __restrict__ act,
                                                    const float* __restrict__ gy, const float* __restrict__ gdy,
                                                    const float* __restrict__ glap, float* __restrict__ adj,
@@ -411,25 +416,62 @@ __global__ __launch_bounds__(256) void reduce_rows_kernel(const float* __restric
   const long i = (long)blockIdx.x * 64 + lane;
   const int b0 = (int)((long)nb * blockIdx.y / gridDim.y), b1 = (int)((long)nb * (blockIdx.y + 1) / gridDim.y);
   float acc = 0.f;
-  if (i < count)
-    for (int b = b0 + w; b < b1; b += 4) acc += part[(long)b * count + i];
+  if (i < count) {
+    int b = b0 + w;
+    for (; b + 28 < b1; b += 32) {  // 8 independent loads in flight per thread (fixed order)
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = part[(long)(b + 4 * u) * count + i];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc += v[u];
+    }
+    for (; b < b1; b += 4) acc += part[(long)b * count + i];
+  }
   red[w][lane] = acc;
   __syncthreads();
   if (w == 0 && i < count) out[(long)blockIdx.y * count + i] = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
 }
 
-// per hidden layer: sum of the KS partial W x W blocks
-__global__ __launch_bounds__(256) void reduce_dw_kernel(const float* __restrict__ dpart, int KS, int din, int W,
-                                                        float* __restrict__ grad, int accumulate) {
+// per hidden layer (blockIdx.y): sum of the KS partial W x W blocks.  A block = 64 column quads
+// (16-B loads, 1 KiB per wave-instruction) x 8 waves over the slices, 8 independent loads in
+// flight per thread; fixed summation order (deterministic, no atomics).
+__global__ __launch_bounds__(512) void reduce_dw_kernel(const float* __restrict__ dpart, int KS, int din, int W,
+                                                        float* __restrict__ grad, int accumulate, int grad16) {
+  __shared__ floatx4 red[8][64];
   const int j = blockIdx.y + 1;
   const long WW = (long)W * W;
-  const long i = (long)blockIdx.x * 256 + threadIdx.x;
-  if (i >= WW) return;
-  const float* src = dpart + (long)(j - 1) * KS * WW + i;
-  float acc = 0.f;
-  for (int k = 0; k < KS; ++k) acc += src[(long)k * WW];
-  float* dst = grad + hidden_off(din, W, j) + i;
-  *dst = accumulate ? *dst + acc : acc;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const long q = (long)blockIdx.x * 64 + lane;  // column quad
+  floatx4 acc = floatx4{0.f, 0.f, 0.f, 0.f};
+  if (4 * q < WW) {
+    const floatx4* col = reinterpret_cast<const floatx4*>(dpart + (long)(j - 1) * KS * WW) + q;
+    const long rs = WW / 4;
+    int k = w;
+    for (; k + 56 < KS; k += 64) {
+      floatx4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = col[(long)(k + 8 * u) * rs];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc += v[u];
+    }
+    for (; k < KS; k += 8) acc += col[(long)k * rs];
+  }
+  red[w][lane] = acc;
+  __syncthreads();
+  if (w == 0 && 4 * q < WW) {
+    floatx4 t = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < 8; ++k) t += red[k][lane];
+    float* dst = grad + hidden_off(din, W, j) + 4 * q;
+    if (grad16) {  // the gradient buffer's hidden blocks are 16-B aligned (a net's own flat .grad)
+      floatx4* d4 = reinterpret_cast<floatx4*>(dst);
+      if (accumulate) t += *d4;
+      *d4 = t;
+    } else {  // e.g. a slice of a data-parallel gradient arena
+#pragma unroll
+      for (int r = 0; r < 4; ++r) dst[r] = accumulate ? dst[r] + t[r] : t[r];
+    }
+  }
 }
 
 }  // namespace
@@ -478,8 +520,9 @@ int wide_bwd_t(const float* x, int N, int din, int dout, int L, const float* prm
   if (L > 0) {
     const int KS = wide_ks(N, S, L);
     hipLaunchKernelGGL((dw_x6<NQ, NT, S, LAP>), dim3(KS, L), dim3(512), (dw_lds<NQ, NT>()), st, N, act, adj, dpart, KS);
-    hipLaunchKernelGGL(reduce_dw_kernel, dim3((unsigned)((W * W + 255) / 256), L), dim3(256), 0, st, dpart, KS, din, W,
-                       grad, accumulate);
+    const int grad16 = (((uintptr_t)(grad + hidden_off(din, W, 1))) & 15) == 0 ? 1 : 0;  // W % 4 == 0: all layers alike
+    hipLaunchKernelGGL(reduce_dw_kernel, dim3((unsigned)((W * W / 4 + 63) / 64), L), dim3(512), 0, st, dpart, KS, din,
+                       W, grad, accumulate, grad16);
   }
   const int rs = tiles < kSmallRS ? tiles : kSmallRS;
   hipLaunchKernelGGL(reduce_rows_kernel, dim3((unsigned)((Ps + 63) / 64), rs), dim3(256), 0, st, small, tiles, Ps, rows);

@@ -114,13 +114,105 @@ __global__ __launch_bounds__(256) void sq_loss_bwd_kernel(int kind, LossIn in, l
   }
 }
 
+// A GROUP of losses (every squared-residual term of a phase iteration) in ONE launch, each
+// with the gradient for a unit output seed (the training loop seeds every loss with 1,
+// base/baseModel.py:77): blocks [first[k], first[k + 1]) serve loss k.  A loss's blocks
+// grid-stride over every element of its gradient buffers -- each thread writes the gradient of
+// the terms it sums, zeros outside the loss range (the other rows of a merged jet launch) --
+// then the same deterministic reduction as sq_loss_fwd_kernel (last block of the loss combines
+// its partials in block order; work slot k = kLossMaxBlocks partials + a ticket).
+constexpr long kGroupPerBlock = 1024;  // elements per block of a group loss
+
+struct LossGroup {
+  InsrLoss l[INSR_LOSS_GROUP_MAX];
+  int first[INSR_LOSS_GROUP_MAX + 1];
+  int count;
+};
+
+__device__ __forceinline__ long loss_span(const InsrLoss& L) {
+  long span = L.kind == INSR_LOSS_COMBO ? L.n : 2 * L.n;
+  const long lens[4] = {L.ga ? L.ga_len : 0, L.gb ? L.gb_len : 0, L.gc ? L.gc_len : 0, L.gd ? L.gd_len : 0};
+  for (int k = 0; k < 4; ++k) span = lens[k] > span ? lens[k] : span;
+  return span;
+}
+
+__global__ __launch_bounds__(kLossThreads) void sq_loss_group_kernel(const LossGroup G, float* __restrict__ work) {
+  __shared__ float red[kLossThreads / 64];
+  int k = 0;
+#pragma unroll
+  for (int q = 1; q < INSR_LOSS_GROUP_MAX; ++q) k += (q < G.count && (int)blockIdx.x >= G.first[q]) ? 1 : 0;
+  const InsrLoss& L = G.l[k];
+  const int blk = blockIdx.x - G.first[k], nblk = G.first[k + 1] - G.first[k];
+  const LossIn in{L.a + L.a_off, L.b, L.c, L.d, L.alpha, L.beta, L.gamma, L.delta};
+  const long n = L.n;
+  const int m = L.m;
+  const float g2 = 2.f * L.scale;
+  const float cf[4] = {L.alpha, L.alpha * L.beta, L.gamma, L.gamma * L.delta};
+  float* const gp[4] = {L.ga, L.gb, L.gc, L.gd};
+  const long gl[4] = {L.ga_len, L.gb_len, L.gc_len, L.gd_len};
+  const long span = loss_span(L);
+  const long count = L.kind == INSR_LOSS_COMBO ? n : 2 * n;
+  float acc = 0.f;
+  for (long e = (long)blk * kLossThreads + threadIdx.x; e < span; e += (long)nblk * kLossThreads) {
+    if (L.kind == INSR_LOSS_COMBO) {
+      float r = 0.f;
+      if (e < n) {
+        r = combo_residual(in, e);
+        acc += r * r;
+      }
+      const float g = g2 * r;
+      if (gp[0] && e < gl[0]) {  // a: the loss range starts at a_off
+        const long t = e - L.a_off;
+        gp[0][e] = (t >= 0 && t < n) ? cf[0] * (t == e ? g : g2 * combo_residual(in, t)) : 0.f;
+      }
+#pragma unroll
+      for (int q = 1; q < 4; ++q)
+        if (gp[q] && e < gl[q]) gp[q][e] = e < n ? cf[q] * g : 0.f;
+    } else {  // BANDS: element e of a's gradient; term (row) e of the loss
+      if (e < count) {
+        const float v = in.a[e * m + (e < n ? 0 : 1)];
+        acc += v * v;
+      }
+      if (gp[0] && e < gl[0]) {
+        const long row = e / m - L.a_off / m;
+        const int col = (int)(e % m);
+        const bool hit = row >= 0 && row < 2 * n && col == (row < n ? 0 : 1);
+        gp[0][e] = hit ? g2 * in.a[row * m + col] : 0.f;
+      }
+    }
+  }
+  for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane == 0) red[w] = acc;
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  float part = 0.f;
+  for (int q = 0; q < kLossThreads / 64; ++q) part += red[q];
+  if (nblk == 1) {
+    L.out[0] = L.scale * part;
+    return;
+  }
+  float* wk = work + (long)k * (kLossMaxBlocks + 1);
+  wk[blk] = part;
+  __threadfence();  // release this block's partial before taking a ticket
+  unsigned* ticket = reinterpret_cast<unsigned*>(wk + kLossMaxBlocks);
+  if (atomicAdd(ticket, 1u) != (unsigned)nblk - 1) return;
+  __threadfence();  // acquire: every other block's partial is visible
+  float tot = 0.f;
+  for (int q = 0; q < nblk; ++q)  // block order: the sum is deterministic
+    tot += __hip_atomic_load(wk + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  L.out[0] = L.scale * tot;
+  atomicExch(ticket, 0u);
+}
+
 }  // namespace insr
 
 using namespace insr;
 
 extern "C" {
 
-long insr_sq_loss_work_floats(void) { return kLossMaxBlocks + 1; }  // partials + ticket
+// partials + ticket per group slot (slot 0 is the single-loss kernels' layout)
+long insr_sq_loss_work_floats(void) { return (long)INSR_LOSS_GROUP_MAX * (kLossMaxBlocks + 1); }
 
 int insr_sq_loss_fwd(int kind, const float* a, const float* b, const float* c, const float* d, long n, int m,
                      float alpha, float beta, float gamma, float delta, float scale, float* out, float* work,
@@ -138,6 +230,36 @@ int insr_sq_loss_fwd(int kind, const float* a, const float* b, const float* c, c
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(sq_loss_fwd_kernel, dim3((unsigned)nb), dim3(kLossThreads), 0, st, kind, in, n, m, scale, out,
                      work);
+  return (int)hipGetLastError();
+}
+
+int insr_sq_loss_group(const InsrLoss* losses, int count, float* work, void* stream) {
+  if (!losses || count < 1 || count > INSR_LOSS_GROUP_MAX) return INSR_EINVAL;
+  LossGroup G;
+  G.count = count;
+  G.first[0] = 0;
+  bool multi = false;
+  for (int k = 0; k < count; ++k) {
+    const InsrLoss& L = losses[k];
+    if (!L.a || !L.out || L.n < 0 || L.a_off < 0) return INSR_EINVAL;
+    if (L.kind != INSR_LOSS_COMBO && L.kind != INSR_LOSS_BANDS) return INSR_EINVAL;
+    if (L.kind == INSR_LOSS_BANDS && (L.m < 2 || L.b || L.c || L.d || L.gb || L.gc || L.gd || L.a_off % L.m))
+      return INSR_EINVAL;
+    if (L.d && !L.c) return INSR_EINVAL;
+    G.l[k] = L;
+    long span = L.kind == INSR_LOSS_COMBO ? L.n : 2 * L.n;
+    const long lens[4] = {L.ga ? L.ga_len : 0, L.gb ? L.gb_len : 0, L.gc ? L.gc_len : 0, L.gd ? L.gd_len : 0};
+    for (int q = 0; q < 4; ++q) span = lens[q] > span ? lens[q] : span;
+    long nb = (span + kGroupPerBlock - 1) / kGroupPerBlock;
+    if (nb < 1) nb = 1;
+    if (nb > kLossMaxBlocks) nb = kLossMaxBlocks;
+    multi = multi || nb > 1;
+    G.first[k + 1] = G.first[k] + (int)nb;
+  }
+  for (int k = count + 1; k <= INSR_LOSS_GROUP_MAX; ++k) G.first[k] = G.first[count];
+  if (multi && !work) return INSR_EINVAL;
+  hipLaunchKernelGGL(sq_loss_group_kernel, dim3((unsigned)G.first[count]), dim3(kLossThreads), 0, (hipStream_t)stream,
+                     G, work);
   return (int)hipGetLastError();
 }
 

