@@ -130,20 +130,21 @@ def _sampler(dev):
     return _SAMPLER[key]
 
 
-def sample_random_and_bands2D(N, n_band, epsilon=1e-4, device="cuda"):
+def sample_random_and_bands2D(N, n_band, epsilon=1e-4, device="cuda", merged=False):
     """(sample_random(N, 2), sample_boundary2D_pair(n_band)) -- the interior batch and the
     four wall bands of one fluid phase iteration (fluid/model.py:74,90-91,105,116-117) --
     drawn in ONE device launch (insr_sample_boxes: 3 launches -> 1).  Same distributions;
     the device stream is Philox-4x32-10, not torch's (GPU only: the CPU samplers above
-    reproduce the reference bit for bit)."""
+    reproduce the reference bit for bit).  merged=True returns the one (N + 2 (n_band // 2) * 2, 2)
+    buffer [interior; bands] instead (both are consecutive rows of it)."""
     from . import _native as nat
     dev = torch.device(device)
     if dev.type != "cuda":
         raise nat.NativeUnavailable("sample_random_and_bands2D draws on the GPU only")
     state, seed = _sampler(dev)
     h = n_band // 2
-    x = torch.empty(N, 2, device=dev)
-    bxy = torch.empty(4 * h, 2, device=dev)
+    buf = torch.empty(N + 4 * h, 2, device=dev)  # [interior; bands]: one jet can take both (merged=True)
+    x, bxy = buf[:N], buf[N:]
     full, lo, hi = (-1.0, 1.0), (-1 - epsilon, -1 + epsilon), (1 - epsilon, 1 + epsilon)
     faces = [(lo, full), (hi, full), (full, lo), (full, hi)]  # sample_boundary2D_pair's order
     f3 = nat._F * 3
@@ -153,6 +154,8 @@ def sample_random_and_bands2D(N, n_band, epsilon=1e-4, device="cuda"):
         boxes[1 + k] = nat.Box(bxy.data_ptr() + 8 * h * k, h, f3(rx[0], ry[0], 0.0), f3(rx[1], ry[1], 0.0))
     nat.check(nat.lib().insr_sample_boxes(boxes, 5, 2, seed, nat.ptr(state), nat.stream_of(dev)),
               "insr_sample_boxes")
+    if merged:
+        return buf
     return x, bxy
 
 

@@ -101,21 +101,21 @@ static int cu_count() {
 
 // per-precision dispatch (nq = 0: exact fp32)
 static int fwd_q(int nq, int NT, int S, bool lap, int T, const float* x, int N, int din, int dout, int L,
-                 const float* prm, float* y, float* dy, float* lp, float* act, hipStream_t st) {
+                 const float* prm, float* y, float* dy, float* lp, float* act, int nbal, hipStream_t st) {
   switch (nq) {
-    case 3: return dispatch_fwd_q<3>(NT, S, lap, T, x, N, din, dout, L, prm, y, dy, lp, act, st);
-    case 2: return dispatch_fwd_q<2>(NT, S, lap, T, x, N, din, dout, L, prm, y, dy, lp, act, st);
-    case 1: return dispatch_fwd_q<1>(NT, S, lap, T, x, N, din, dout, L, prm, y, dy, lp, act, st);
+    case 3: return dispatch_fwd_q<3>(NT, S, lap, T, x, N, din, dout, L, prm, y, dy, lp, act, nbal, st);
+    case 2: return dispatch_fwd_q<2>(NT, S, lap, T, x, N, din, dout, L, prm, y, dy, lp, act, nbal, st);
+    case 1: return dispatch_fwd_q<1>(NT, S, lap, T, x, N, din, dout, L, prm, y, dy, lp, act, nbal, st);
     default: return dispatch_fwd_split(NT, S, lap, T, x, N, din, dout, L, prm, y, dy, lp, act, st);
   }
 }
 static int bwd_q(int nq, int NT, int S, bool lap, int T, const float* x, int N, int din, int dout, int L,
                  const float* prm, const float* act, const float* gy, const float* gdy, const float* glap, float* part,
-                 long P, hipStream_t st) {
+                 long P, int nbal, hipStream_t st) {
   switch (nq) {
-    case 3: return dispatch_bwd_q<3>(NT, S, lap, T, x, N, din, dout, L, prm, act, gy, gdy, glap, part, P, st);
-    case 2: return dispatch_bwd_q<2>(NT, S, lap, T, x, N, din, dout, L, prm, act, gy, gdy, glap, part, P, st);
-    case 1: return dispatch_bwd_q<1>(NT, S, lap, T, x, N, din, dout, L, prm, act, gy, gdy, glap, part, P, st);
+    case 3: return dispatch_bwd_q<3>(NT, S, lap, T, x, N, din, dout, L, prm, act, gy, gdy, glap, part, P, nbal, st);
+    case 2: return dispatch_bwd_q<2>(NT, S, lap, T, x, N, din, dout, L, prm, act, gy, gdy, glap, part, P, nbal, st);
+    case 1: return dispatch_bwd_q<1>(NT, S, lap, T, x, N, din, dout, L, prm, act, gy, gdy, glap, part, P, nbal, st);
     default: return dispatch_bwd_split(NT, S, lap, T, x, N, din, dout, L, prm, act, gy, gdy, glap, part, P, st);
   }
 }
@@ -127,8 +127,8 @@ static int occupancy(int bwd, int nq, int NT, int S, bool lap, int T) {
   auto it = cache.find(key);
   if (it != cache.end()) return it->second;
   const int r = bwd ? bwd_q(nq, NT, S, lap, T, nullptr, -1, 0, 0, 0, nullptr, nullptr, nullptr, nullptr, nullptr,
-                            nullptr, 0, nullptr)
-                    : fwd_q(nq, NT, S, lap, T, nullptr, -1, 0, 0, 0, nullptr, nullptr, nullptr, nullptr, nullptr,
+                            nullptr, 0, 0, nullptr)
+                    : fwd_q(nq, NT, S, lap, T, nullptr, -1, 0, 0, 0, nullptr, nullptr, nullptr, nullptr, nullptr, 0,
                             nullptr);
   cache[key] = r;
   return r;
@@ -178,6 +178,37 @@ int split_tiles(int bwd, int NT, int S, long n, bool lap, int nq) {
       }
   }
   return T;
+}
+
+// Balanced launch shape: T tiles per block from split_tiles; if the batch overflows the last
+// round of resident blocks by a little (16384 interior + 324 band points = 1045 tiles on
+// 256 one-block CUs: 262 blocks, 2 rounds), blocks of up to T + 1 tiles (T = 4 -> 5 for
+// value jets, 2 -> 3 for 2-3 stream jets) spread the tiles evenly over fewer blocks when that
+// saves a round.  nbal = the block count (0: plain T-tile blocks).
+struct LaunchShape {
+  int T, nbal;
+};
+LaunchShape launch_shape(int bwd, int nq, int NT, int S, bool lap, long n) {
+  LaunchShape sh{split_tiles(bwd, NT, S, n, lap, nq), 0};
+  tiles_init();
+  if (nq == 0 || NT > 8 || lap || g_tiles[bwd ? 1 : 0] > 0) return sh;  // exact fp32 / forced T: plain
+  // backward: value jets only (the 3-tile gradient backward spills: 280 B of scratch per lane)
+  const int T1 = sh.T == 4 && S == 1 ? 5 : (!bwd && sh.T == 2 && (S == 2 || S == 3) ? 3 : 0);
+  if (!T1) return sh;
+  const int cus = cu_count();
+  const int o = occupancy(bwd, nq, NT, S, lap, sh.T), o1 = occupancy(bwd, nq, NT, S, lap, T1);
+  if (o <= 0 || o1 <= 0) return sh;
+  const long tiles = (n + 15) / 16;
+  const long nb = (tiles + sh.T - 1) / sh.T, slots = (long)o * cus, slots1 = (long)o1 * cus;
+  const long rounds = (nb + slots - 1) / slots;
+  const long nb1 = (tiles + T1 - 1) / T1, rounds1 = (nb1 + slots1 - 1) / slots1;
+  if (rounds1 >= rounds) return sh;
+  long nbal = rounds1 * slots1;  // as many blocks as the rounds hold (fewest tiles per block) ...
+  if (nbal > nb) nbal = nb;      // ... but never below the plain shape's tiles per block
+  if (nbal < nb1) nbal = nb1;
+  sh.T = T1;
+  sh.nbal = (int)nbal;
+  return sh;
 }
 
 constexpr int kRedWaves = 8;
@@ -436,8 +467,9 @@ int insr_siren_jet_fwd(const float* x, long n, int din, int dout, int L, int W, 
   if (!x || !params || !y) return INSR_EINVAL;
   if (c.jm != INSR_MODE_VALUE && !dy) return INSR_EINVAL;
   if (c.lap && !lap) return INSR_EINVAL;
-  return fwd_q(c.nqf, c.NT, c.S, c.lap, split_tiles(0, c.NT, c.S, n, c.lap, c.nqf), x, (int)n, din, dout, L, params,
-               y, dy, lap, act, (hipStream_t)stream);
+  const LaunchShape sh = launch_shape(0, c.nqf, c.NT, c.S, c.lap, n);
+  return fwd_q(c.nqf, c.NT, c.S, c.lap, sh.T, x, (int)n, din, dout, L, params, y, dy, lap, act, sh.nbal,
+               (hipStream_t)stream);
 }
 
 int insr_siren_jet_fwd_multi(const InsrJetJob* jobs, int njobs, int din, int dout, int L, int W, int mode,
@@ -471,20 +503,34 @@ int insr_siren_jet_fwd_multi(const InsrJetJob* jobs, int njobs, int din, int dou
     // (a boundary band) runs 1-tile blocks, placed first in the grid
     // (W = 128 gradient jets: T = 2 -- the fused kernel is held to 128 VGPRs, two blocks per CU;
     // measured 50.9 vs 51.9 us for T = 4 at 16384 points, profiles/r01/fwd_minwaves_study)
-    const int T = (NT == 8 && S == 3) ? 2 : split_tiles(0, NT, S, total, false, c.nqf);
+    int T = (NT == 8 && S == 3) ? 2 : split_tiles(0, NT, S, total, false, c.nqf);
     InsrJetJob pk[INSR_MAX_FWD_JOBS];
-    int small[INSR_MAX_FWD_JOBS];
+    int small[INSR_MAX_FWD_JOBS], nbal[INSR_MAX_FWD_JOBS];
     int m = 0;
     for (int k = 0; k < njobs; ++k)
       if (jobs[k].n > 0) {
         small[m] = split_tiles(0, NT, S, jobs[k].n, false, c.nqf) < T ? 1 : 0;
+        nbal[m] = 0;
         pk[m++] = jobs[k];
       }
+    // value jets at T = 4 (two resident blocks per CU): when the jobs' blocks overflow a whole
+    // round by a little (u_prev at 16384 points + u at 16384 + 324 band points: 518 blocks for
+    // 512 slots), 5-tile blocks fit them in one round fewer
+    if (T == 4 && S == 1 && NT <= 8) {
+      const long slots = 2L * cu_count();
+      long b4 = 0, b5 = 0;
+      for (int k = 0; k < m; ++k) {
+        const long tiles = (pk[k].n + 15) / 16;
+        b4 += small[k] ? tiles : (tiles + 3) / 4;
+        b5 += small[k] ? tiles : (tiles + 4) / 5;
+      }
+      if ((b5 + slots - 1) / slots < (b4 + slots - 1) / slots) T = 5;
+    }
     hipStream_t st = (hipStream_t)stream;
     switch (c.nqf) {
-      case 3: return dispatch_fwd_multi_q<3>(NT, S, false, T, pk, small, m, din, dout, L, st);
-      case 2: return dispatch_fwd_multi_q<2>(NT, S, false, T, pk, small, m, din, dout, L, st);
-      default: return dispatch_fwd_multi_q<1>(NT, S, false, T, pk, small, m, din, dout, L, st);
+      case 3: return dispatch_fwd_multi_q<3>(NT, S, false, T, pk, small, nbal, m, din, dout, L, st);
+      case 2: return dispatch_fwd_multi_q<2>(NT, S, false, T, pk, small, nbal, m, din, dout, L, st);
+      default: return dispatch_fwd_multi_q<1>(NT, S, false, T, pk, small, nbal, m, din, dout, L, st);
     }
   }
   for (int k = 0; k < njobs; ++k) {
@@ -507,8 +553,9 @@ int insr_siren_jet_bwd(const float* x, long n, int din, int dout, int L, int W, 
   const long P = insr_jet_partial_stride(din, dout, L, W);  // row stride of the partial rows
   // width 256: the fused split-bf16 backward does not exist -- exact fp32 serves this entry
   const int nq = c.NT > 8 ? 0 : c.nqb;
-  return bwd_q(nq, c.NT, c.S, c.lap, split_tiles(1, c.NT, c.S, n, c.lap, nq), x, (int)n, din, dout, L, params, act, gy,
-               gdy, glap, partial, P, (hipStream_t)stream);
+  const LaunchShape sh = launch_shape(1, nq, c.NT, c.S, c.lap, n);
+  return bwd_q(nq, c.NT, c.S, c.lap, sh.T, x, (int)n, din, dout, L, params, act, gy, gdy, glap, partial, P, sh.nbal,
+               (hipStream_t)stream);
 }
 
 int insr_jet_set_wide_min_width(int width) {
@@ -563,15 +610,15 @@ int insr_jet_partial_blocks(long n, int din, int W, int mode) {
   if (!c.ok() || n < 0) return INSR_EINVAL;
   if (n == 0) return 0;
   const int nq = c.NT > 8 ? 0 : c.nqb;
-  const int T = split_tiles(1, c.NT, c.S, n, c.lap, nq);
-  return (int)(((n + 15) / 16 + T - 1) / T);
+  const LaunchShape sh = launch_shape(1, nq, c.NT, c.S, c.lap, n);
+  return sh.nbal > 0 ? sh.nbal : (int)(((n + 15) / 16 + sh.T - 1) / sh.T);
 }
 
 int insr_jet_split_tiles(long n, int din, int W, int mode, int backward) {
   const JetCall c(din, W, mode);
   if (!c.ok() || n < 0) return INSR_EINVAL;
   const int nq = backward ? (c.NT > 8 ? 0 : c.nqb) : c.nqf;
-  return split_tiles(backward ? 1 : 0, c.NT, c.S, n, c.lap, nq);
+  return launch_shape(backward ? 1 : 0, nq, c.NT, c.S, c.lap, n).T;
 }
 
 void insr_jet_set_split_tiles(int fwd_tiles, int bwd_tiles, int min_blocks) {

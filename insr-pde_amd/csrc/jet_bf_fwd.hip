@@ -4,11 +4,11 @@
 
 namespace insr {
 template int dispatch_fwd_q<1>(int, int, bool, int, const float*, int, int, int, int, const float*, float*, float*,
-                               float*, float*, hipStream_t);
-template int dispatch_fwd_multi_q<1>(int, int, bool, int, const InsrJetJob*, const int*, int, int, int, int,
-                                     hipStream_t);
+                               float*, float*, int, hipStream_t);
+template int dispatch_fwd_multi_q<1>(int, int, bool, int, const InsrJetJob*, const int*, const int*, int, int, int,
+                                     int, hipStream_t);
 template int dispatch_fwd_q<2>(int, int, bool, int, const float*, int, int, int, int, const float*, float*, float*,
-                               float*, float*, hipStream_t);
-template int dispatch_fwd_multi_q<2>(int, int, bool, int, const InsrJetJob*, const int*, int, int, int, int,
-                                     hipStream_t);
+                               float*, float*, int, hipStream_t);
+template int dispatch_fwd_multi_q<2>(int, int, bool, int, const InsrJetJob*, const int*, const int*, int, int, int,
+                                     int, hipStream_t);
 }  // namespace insr

@@ -310,15 +310,15 @@ int dispatch_bwd_split(int NT, int S, bool LAP, int T, const float* x, int N, in
 // split-bf16 kernels, per precision NQ (bf16 terms per operand: 3 = x6, 2 = x3, 1 = bf16)
 template <int NQ>
 int dispatch_fwd_q(int NT, int S, bool LAP, int T, const float* x, int N, int din, int dout, int L,
-                   const float* prm, float* y, float* dy, float* lap, float* act, hipStream_t st);
+                   const float* prm, float* y, float* dy, float* lap, float* act, int nbal, hipStream_t st);
 constexpr int kFwdJobs = INSR_MAX_FWD_JOBS;
 template <int NQ>
-int dispatch_fwd_multi_q(int NT, int S, bool LAP, int T, const InsrJetJob* jobs, const int* small, int njobs,
-                         int din, int dout, int L, hipStream_t st);
+int dispatch_fwd_multi_q(int NT, int S, bool LAP, int T, const InsrJetJob* jobs, const int* small, const int* nbal,
+                         int njobs, int din, int dout, int L, hipStream_t st);
 template <int NQ>
 int dispatch_bwd_q(int NT, int S, bool LAP, int T, const float* x, int N, int din, int dout, int L,
                    const float* prm, const float* act, const float* gy, const float* gdy, const float* glap,
-                   float* part, long P, hipStream_t st);
+                   float* part, long P, int nbal, hipStream_t st);
 // two-kernel backward (W = 128 / 256): propagation kernel + dW GEMM + reductions (jet_x6w.hpp)
 template <int NQ>
 int dispatch_wide_bwd_q(int NT, int S, bool LAP, const float* x, int N, int din, int dout, int L, const float* prm,

@@ -164,16 +164,35 @@ __device__ __forceinline__ FragQ<NQ> load_w_frag(const float* __restrict__ Wj, i
   return split_frag<NQ>(v0, v1);
 }
 
-// The forward of one block (tiles tile0 .. tile0 + T - 1 of one network's batch): the body
+// Balanced tiles per block: with nbal > 0 the tiles of a batch are split over nbal blocks as
+// evenly as possible (block b: tiles [b tiles / nbal, (b + 1) tiles / nbal), at most T), so a
+// batch a little above a multiple of the resident block slots (16384 interior + 324 band
+// points = 1045 tiles on 256 CUs) takes no extra block round; nbal = 0: T tiles per block.
+__device__ __forceinline__ void block_tiles(int b, int N, int T, int nbal, int& tile0, int& cnt) {
+  if (nbal > 0) {
+    const long tiles = (N + 15) / 16;
+    tile0 = (int)(((long)b * tiles) / nbal);
+    cnt = (int)((((long)b + 1) * tiles) / nbal) - tile0;
+  } else {  // T-tile blocks; the last one may hold fewer (T = 3 / 5 do not divide the act layout's 4)
+    const int tiles = (N + 15) / 16;
+    tile0 = b * T;
+    cnt = tiles - tile0 < T ? tiles - tile0 : T;
+  }
+}
+
+// The forward of one block (tiles tile0 .. tile0 + cnt - 1 of one network's batch): the body
 // of jet_fwd_x6 and of jet_fwd_x6_multi (several networks / batches in one launch).
 template <int NQ, int NT, int S, bool LAP, int T>
 __device__ __forceinline__ void fwd_x6_block(const float* __restrict__ x, int N, int din, int dout, int L,
                                              const float* __restrict__ prm, float* __restrict__ y,
                                              float* __restrict__ dy, float* __restrict__ lap,
-                                             float* __restrict__ act, const int tile0) {
+                                             float* __restrict__ act, const int tile0, const int cnt_rt) {
   using G = X6Geo<NT>;
   constexpr int W = G::W, RPW = G::RPW, LDB = G::LDB, WV = G::WV, PLANE = G::PLANE, KC = G::KC;
   constexpr int NTAN = LAP ? S - 2 : S - 1;
+  // the tile count is a run-time value only for the balanced shapes (T = 3, 5): the T = 1, 2, 4
+  // instantiations keep compile-time loops (a run-time guard there serialises the MFMA chains)
+  const int cnt = (T == 3 || T == 5) ? cnt_rt : T;
   extern __shared__ __attribute__((aligned(16))) float lds_f[];
   unsigned short* lds = reinterpret_cast<unsigned short*>(lds_f);
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
@@ -184,7 +203,7 @@ __device__ __forceinline__ void fwd_x6_block(const float* __restrict__ x, int N,
 #pragma unroll
   for (int t = 0; t < T; ++t) {
     const int p = (tile0 + t) * 16 + c;
-    for (int k = 0; k < 3; ++k) xv[t][k] = (p < N && k < din) ? x[(long)p * din + k] : 0.f;
+    for (int k = 0; k < 3; ++k) xv[t][k] = (t < cnt && p < N && k < din) ? x[(long)p * din + k] : 0.f;
   }
 
   floatx4 a[T][RPW][S];
@@ -231,12 +250,14 @@ __device__ __forceinline__ void fwd_x6_block(const float* __restrict__ x, int N,
 #pragma unroll
         for (int kc = 0; kc < KC; ++kc) {
 #pragma unroll
-          for (int t = 0; t < T; ++t)
+          for (int t = 0; t < T; ++t) {
+            if (t >= cnt) break;  // unused slots of a balanced block
 #pragma unroll
             for (int s = 0; s < S; ++s) {
               const unsigned short* pb = lds + (t * S + s) * NQ * PLANE + c * LDB + 32 * kc + 8 * g;
               a[t][i][s] = mfma_q<NQ>(wf[kc], lds_frag<NQ, PLANE>(pb), a[t][i][s]);
             }
+          }
         }
       }
       __syncthreads();  // every wave has read layer j-1
@@ -244,6 +265,7 @@ __device__ __forceinline__ void fwd_x6_block(const float* __restrict__ x, int N,
     if (act) {
 #pragma unroll
       for (int t = 0; t < T; ++t) {
+        if (t >= cnt) break;  // a balanced block's unused tile slots
         float* base = act_base(act, j, ntiles, tile0 + t, S, NT);
 #pragma unroll
         for (int i = 0; i < RPW; ++i)
@@ -298,8 +320,9 @@ __device__ __forceinline__ void fwd_x6_block(const float* __restrict__ x, int N,
       }
   }
   __syncthreads();
-  if (wave == 0 && g < T) {  // lane group g finishes tile g
-    const int t = g;
+  static_assert(T <= 4 * WV, "output stage: one lane group per tile");
+  if (wave * 4 + g < cnt) {  // lane group g of wave w finishes tile 4 w + g
+    const int t = wave * 4 + g;
     const int p = (tile0 + t) * 16 + c;
     if (p < N) {
       for (int o = 0; o < dout; ++o) {
@@ -324,8 +347,10 @@ __device__ __forceinline__ void fwd_x6_block(const float* __restrict__ x, int N,
 template <int NQ, int NT, int S, bool LAP, int T>
 __global__ __launch_bounds__(X6Geo<NT>::THREADS) void jet_fwd_x6(
     const float* __restrict__ x, int N, int din, int dout, int L, const float* __restrict__ prm,
-    float* __restrict__ y, float* __restrict__ dy, float* __restrict__ lap, float* __restrict__ act) {
-  fwd_x6_block<NQ, NT, S, LAP, T>(x, N, din, dout, L, prm, y, dy, lap, act, blockIdx.x * T);
+    float* __restrict__ y, float* __restrict__ dy, float* __restrict__ lap, float* __restrict__ act, int nbal) {
+  int tile0, cnt;
+  block_tiles(blockIdx.x, N, T, nbal, tile0, cnt);
+  fwd_x6_block<NQ, NT, S, LAP, T>(x, N, din, dout, L, prm, y, dy, lap, act, tile0, cnt);
 }
 
 // Horizontal fusion: up to kFwdJobs independent forward jets of one architecture and jet
@@ -342,6 +367,7 @@ struct FwdJobsX6 {
   InsrJetJob job[kFwdJobs];
   int first[kFwdJobs + 1];
   int small[kFwdJobs];  // 1: the job runs TB-tile blocks
+  int nbal[kFwdJobs];   // > 0: the job's tiles balanced over its nbal TA-tile blocks
   int njobs;
 };
 
@@ -365,18 +391,19 @@ __global__ __launch_bounds__(X6Geo<NT>::THREADS, (x6_multi_min_waves<NT, S>())) 
   if constexpr (TA != TB) {
     if (jobs.small[k]) {
       fwd_x6_block<NQ, NT, S, LAP, TB>(jb.x, (int)jb.n, din, dout_k, L, jb.params, jb.y, jb.dy, jb.lap, jb.act,
-                                   (b - jobs.first[k]) * TB);
+                                       (b - jobs.first[k]) * TB, TB);
       return;
     }
   }
-  fwd_x6_block<NQ, NT, S, LAP, TA>(jb.x, (int)jb.n, din, dout_k, L, jb.params, jb.y, jb.dy, jb.lap, jb.act,
-                               (b - jobs.first[k]) * TA);
+  int tile0, cnt;
+  block_tiles(b - jobs.first[k], (int)jb.n, TA, jobs.nbal[k], tile0, cnt);
+  fwd_x6_block<NQ, NT, S, LAP, TA>(jb.x, (int)jb.n, din, dout_k, L, jb.params, jb.y, jb.dy, jb.lap, jb.act, tile0, cnt);
 }
 
 // small[k] != 0: job k runs 1-tile blocks (ignored when T == 1)
 template <int NQ, int NT, int S, bool LAP, int T>
-int launch_fwd_x6_multi_t(const InsrJetJob* jobs, const int* small, int njobs, int din, int dout, int L,
-                          hipStream_t st) {
+int launch_fwd_x6_multi_t(const InsrJetJob* jobs, const int* small, const int* nbal, int njobs, int din, int dout,
+                          int L, hipStream_t st) {
   constexpr int TB = 1;
   constexpr size_t lds = fwd_x6_lds_bytes<NQ, NT, S, T>();
   if constexpr (lds > kLdsMax) {
@@ -397,9 +424,10 @@ int launch_fwd_x6_multi_t(const InsrJetJob* jobs, const int* small, int njobs, i
         if (sm != 1 - pass) continue;
         pk.job[m] = jobs[k];
         pk.small[m] = sm;
+        pk.nbal[m] = sm ? 0 : (nbal ? nbal[k] : 0);
         pk.first[m] = nb;
         const int t = sm ? TB : T;
-        nb += (int)(((jobs[k].n + 15) / 16 + t - 1) / t);
+        nb += pk.nbal[m] > 0 ? pk.nbal[m] : (int)(((jobs[k].n + 15) / 16 + t - 1) / t);
         ++m;
       }
     pk.first[njobs] = nb;
@@ -413,7 +441,7 @@ int launch_fwd_x6_multi_t(const InsrJetJob* jobs, const int* small, int njobs, i
 
 template <int NQ, int NT, int S, bool LAP, int T>
 int launch_fwd_x6_t(const float* x, int N, int din, int dout, int L, const float* prm, float* y, float* dy,
-                    float* lap, float* act, hipStream_t st) {
+                    float* lap, float* act, int nbal, hipStream_t st) {
   constexpr size_t lds = fwd_x6_lds_bytes<NQ, NT, S, T>();
   if constexpr (lds > kLdsMax) {
     return INSR_EINVAL;
@@ -430,8 +458,8 @@ int launch_fwd_x6_t(const float* x, int N, int din, int dout, int L, const float
       (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)jet_fwd_x6<NQ, NT, S, LAP, T>, X6Geo<NT>::THREADS, lds);
       return occ;
     }
-    hipLaunchKernelGGL((jet_fwd_x6<NQ, NT, S, LAP, T>), dim3(nb), dim3(X6Geo<NT>::THREADS), lds, st, x, N, din, dout, L,
-                       prm, y, dy, lap, act);
+    hipLaunchKernelGGL((jet_fwd_x6<NQ, NT, S, LAP, T>), dim3(nbal > 0 ? nbal : nb), dim3(X6Geo<NT>::THREADS), lds, st,
+                       x, N, din, dout, L, prm, y, dy, lap, act, nbal);
     return (int)hipGetLastError();
   }
 }
@@ -545,7 +573,7 @@ template <int NQ, int NT, int S, bool LAP, int T>
 __global__ __launch_bounds__(X6Geo<NT>::THREADS) void jet_bwd_x6(
     const float* __restrict__ x, int N, int din, int dout, int L, const float* __restrict__ prm,
     const float* __restrict__ act, const float* __restrict__ gy, const float* __restrict__ gdy,
-    const float* __restrict__ glap, float* __restrict__ part, long P) {
+    const float* __restrict__ glap, float* __restrict__ part, long P, int nbal) {
   using G = X6Geo<NT>;
   using BG = X6BwdGeo<NQ, NT>;
   constexpr int W = G::W, RPW = G::RPW, KC = G::KC;
@@ -562,7 +590,12 @@ __global__ __launch_bounds__(X6Geo<NT>::THREADS) void jet_bwd_x6(
   unsigned short* H = Z + NSET * ZSET;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
   const int ntiles = ((N + 63) / 64) * 4;
-  const int tile0 = blockIdx.x * T;
+  int tile0, cnt_rt;
+  block_tiles(blockIdx.x, N, T, nbal, tile0, cnt_rt);
+  const int cnt = (T == 3 || T == 5) ? cnt_rt : T;  // run-time only for the balanced shapes
+  // tile of slot t for memory reads: an unused slot of a balanced block re-reads the block's
+  // first tile (valid memory) -- its adjoints and x are zero, so it contributes nothing
+  auto tt = [&](int t) { return tile0 + (t < cnt ? t : 0); };
   const int rt0 = wave * RPW;
   float* mypart = part + (long)blockIdx.x * P;
 
@@ -570,7 +603,7 @@ __global__ __launch_bounds__(X6Geo<NT>::THREADS) void jet_bwd_x6(
   // read where used: the backward's register budget is tight
   auto adjoint = [&](int t, int s, int o) -> float {
     const int p = (tile0 + t) * 16 + c;
-    if (p >= N) return 0.f;
+    if (t >= cnt || p >= N) return 0.f;
     if (s == 0) return gy ? gy[(long)p * dout + o] : 0.f;
     if (LAP && s == S - 1) return glap ? glap[(long)p * dout + o] : 0.f;
     return gdy ? gdy[((long)p * dout + o) * din + (s - 1)] : 0.f;
@@ -581,7 +614,7 @@ __global__ __launch_bounds__(X6Geo<NT>::THREADS) void jet_bwd_x6(
     float amax = 0.f;
 #pragma unroll
     for (int t = 0; t < T; ++t) {
-      const float* base = act_base(act, layer, ntiles, tile0 + t, S, NT);
+      const float* base = act_base(act, layer, ntiles, tt(t), S, NT);
 #pragma unroll
       for (int i = 0; i < RPW; ++i) {
         z[t][i] = *reinterpret_cast<const floatx4*>(base + ((rt0 + i) * 64 + lane) * 4);
@@ -631,7 +664,7 @@ __global__ __launch_bounds__(X6Geo<NT>::THREADS) void jet_bwd_x6(
       floatx4 acc4 = floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int t = 0; t < T; ++t) {
-        const float* baseL = act_base(act, L, ntiles, tile0 + t, S, NT);
+        const float* baseL = act_base(act, L, ntiles, tt(t), S, NT);
 #pragma unroll
         for (int s = 0; s < S; ++s) {
           const floatx4 hs = h_stream<NT, S, LAP>(baseL, s, rt, lane, sn[t][i], cs[t][i]);
@@ -670,7 +703,7 @@ __global__ __launch_bounds__(X6Geo<NT>::THREADS) void jet_bwd_x6(
     if constexpr (KZ) {
 #pragma unroll
       for (int t = 0; t < T; ++t) {
-        const float* base = act_base(act, layer, ntiles, tile0 + t, S, NT);
+        const float* base = act_base(act, layer, ntiles, tt(t), S, NT);
 #pragma unroll
         for (int i = 0; i < RPW; ++i)
 #pragma unroll
@@ -692,7 +725,7 @@ __global__ __launch_bounds__(X6Geo<NT>::THREADS) void jet_bwd_x6(
     INSR_STAMP(L - j, 0);
 #pragma unroll
     for (int t = 0; t < T; ++t) {
-      const float* basej = act_base(act, j, ntiles, tile0 + t, S, NT);
+      const float* basej = act_base(act, j, ntiles, tt(t), S, NT);
 #pragma unroll
       for (int i = 0; i < RPW; ++i) {
         if constexpr (KZ) {
@@ -732,7 +765,7 @@ __global__ __launch_bounds__(X6Geo<NT>::THREADS) void jet_bwd_x6(
 #pragma unroll
             for (int t = 0; t < T; ++t) {
               const int p = (tile0 + t) * 16 + c;
-              const float xk = p < N ? x[(long)p * din + k] : 0.f;
+              const float xk = (t < cnt && p < N) ? x[(long)p * din + k] : 0.f;
               v = fmaf(hb[t][i][0][r], xk, v);
               if (k < NTAN) v += hb[t][i][1 + k][r];
             }
@@ -772,7 +805,7 @@ __global__ __launch_bounds__(X6Geo<NT>::THREADS) void jet_bwd_x6(
       INSR_STAMP(L - j, 3);
 #pragma unroll
       for (int t = 0; t < T; ++t) {
-        const float* basep = act_base(act, j - 1, ntiles, tile0 + t, S, NT);
+        const float* basep = act_base(act, j - 1, ntiles, tt(t), S, NT);
 #pragma unroll
         for (int i = 0; i < RPW; ++i)
 #pragma unroll
@@ -797,8 +830,9 @@ __global__ __launch_bounds__(X6Geo<NT>::THREADS) void jet_bwd_x6(
       // dW_j rows n = 16 rt + c (A), columns m (B); K = sets x 16 points
 #pragma unroll
       for (int ch = 0; ch < NCH; ++ch) {
+        if (2 * ch >= cnt * SG) break;  // unused tile slots of a balanced block (sets t SG + sl)
         const int u = 2 * ch + (g >> 1);
-        const bool live = u < NSET;
+        const bool live = u < cnt * SG;
         const int p0 = 8 * (g & 1);
 #pragma unroll
         for (int i = 0; i < RPW; ++i) {
@@ -841,7 +875,8 @@ __global__ __launch_bounds__(X6Geo<NT>::THREADS) void jet_bwd_x6(
 #pragma unroll
           for (int kc = 0; kc < KC; ++kc) wt[i][kc] = split_frag<NQ>(wraw[i][kc][0], wraw[i][kc][1]);
       }
-      // propagation of this group's streams
+      // propagation of this group's streams (an unused slot of a balanced block keeps zero
+      // adjoints: its bias / first-layer sums must add nothing)
 #pragma unroll
       for (int t = 0; t < T; ++t)
 #pragma unroll
@@ -850,6 +885,7 @@ __global__ __launch_bounds__(X6Geo<NT>::THREADS) void jet_bwd_x6(
           const int u = t * SG + sl;
 #pragma unroll
           for (int i = 0; i < RPW; ++i) nh[t][i][s] = floatx4{0.f, 0.f, 0.f, 0.f};
+          if (t >= cnt) continue;
 #pragma unroll
           for (int kc = 0; kc < KC; ++kc) {
             const FragQ<NQ> bf = lds_frag<NQ, ZPLANE>(Z + u * ZSET + c * LDB + 32 * kc + 8 * g);
@@ -883,7 +919,8 @@ __global__ __launch_bounds__(X6Geo<NT>::THREADS) void jet_bwd_x6(
 
 template <int NQ, int NT, int S, bool LAP, int T>
 int launch_bwd_x6_t(const float* x, int N, int din, int dout, int L, const float* prm, const float* act,
-                    const float* gy, const float* gdy, const float* glap, float* part, long P, hipStream_t st) {
+                    const float* gy, const float* gdy, const float* glap, float* part, long P, int nbal,
+                    hipStream_t st) {
   constexpr size_t lds = bwd_x6_lds_bytes<NQ, NT, S, T>();
   if constexpr (lds > kLdsMax || NT > 8) {
     return INSR_EINVAL;
@@ -900,8 +937,8 @@ int launch_bwd_x6_t(const float* x, int N, int din, int dout, int L, const float
       (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)jet_bwd_x6<NQ, NT, S, LAP, T>, X6Geo<NT>::THREADS, lds);
       return occ;
     }
-    hipLaunchKernelGGL((jet_bwd_x6<NQ, NT, S, LAP, T>), dim3(nb), dim3(X6Geo<NT>::THREADS), lds, st, x, N, din, dout,
-                       L, prm, act, gy, gdy, glap, part, P);
+    hipLaunchKernelGGL((jet_bwd_x6<NQ, NT, S, LAP, T>), dim3(nbal > 0 ? nbal : nb), dim3(X6Geo<NT>::THREADS), lds, st,
+                       x, N, din, dout, L, prm, act, gy, gdy, glap, part, P, nbal);
     return (int)hipGetLastError();
   }
 }

@@ -5,24 +5,37 @@
 
 namespace insr {
 
+// T in {1, 2, 4}; the balanced modes add T = 3 (2-3 stream jets) and T = 5 (value jets) at W <= 128
 template <int NQ, int NT, int S, bool LAP>
 int launch_fwd_x6(int T, const float* x, int N, int din, int dout, int L, const float* prm, float* y, float* dy,
-                  float* lap, float* act, hipStream_t st) {
+                  float* lap, float* act, int nbal, hipStream_t st) {
   switch (T) {
-    case 1: return launch_fwd_x6_t<NQ, NT, S, LAP, 1>(x, N, din, dout, L, prm, y, dy, lap, act, st);
-    case 2: return launch_fwd_x6_t<NQ, NT, S, LAP, 2>(x, N, din, dout, L, prm, y, dy, lap, act, st);
-    case 4: return launch_fwd_x6_t<NQ, NT, S, LAP, 4>(x, N, din, dout, L, prm, y, dy, lap, act, st);
+    case 1: return launch_fwd_x6_t<NQ, NT, S, LAP, 1>(x, N, din, dout, L, prm, y, dy, lap, act, nbal, st);
+    case 2: return launch_fwd_x6_t<NQ, NT, S, LAP, 2>(x, N, din, dout, L, prm, y, dy, lap, act, nbal, st);
+    case 4: return launch_fwd_x6_t<NQ, NT, S, LAP, 4>(x, N, din, dout, L, prm, y, dy, lap, act, nbal, st);
+    case 3:
+      if constexpr (NT <= 8 && (S == 2 || S == 3) && !LAP)
+        return launch_fwd_x6_t<NQ, NT, S, LAP, 3>(x, N, din, dout, L, prm, y, dy, lap, act, nbal, st);
+      return INSR_EINVAL;
+    case 5:
+      if constexpr (NT <= 8 && S == 1)
+        return launch_fwd_x6_t<NQ, NT, S, LAP, 5>(x, N, din, dout, L, prm, y, dy, lap, act, nbal, st);
+      return INSR_EINVAL;
     default: return INSR_EINVAL;
   }
 }
 
 template <int NQ, int NT, int S, bool LAP>
-int launch_fwd_x6_multi(int T, const InsrJetJob* jobs, const int* small, int njobs, int din, int dout, int L,
-                        hipStream_t st) {
+int launch_fwd_x6_multi(int T, const InsrJetJob* jobs, const int* small, const int* nbal, int njobs, int din,
+                        int dout, int L, hipStream_t st) {
   switch (T) {
-    case 1: return launch_fwd_x6_multi_t<NQ, NT, S, LAP, 1>(jobs, small, njobs, din, dout, L, st);
-    case 2: return launch_fwd_x6_multi_t<NQ, NT, S, LAP, 2>(jobs, small, njobs, din, dout, L, st);
-    case 4: return launch_fwd_x6_multi_t<NQ, NT, S, LAP, 4>(jobs, small, njobs, din, dout, L, st);
+    case 1: return launch_fwd_x6_multi_t<NQ, NT, S, LAP, 1>(jobs, small, nbal, njobs, din, dout, L, st);
+    case 2: return launch_fwd_x6_multi_t<NQ, NT, S, LAP, 2>(jobs, small, nbal, njobs, din, dout, L, st);
+    case 4: return launch_fwd_x6_multi_t<NQ, NT, S, LAP, 4>(jobs, small, nbal, njobs, din, dout, L, st);
+    case 5:
+      if constexpr (NT <= 8 && S == 1)
+        return launch_fwd_x6_multi_t<NQ, NT, S, LAP, 5>(jobs, small, nbal, njobs, din, dout, L, st);
+      return INSR_EINVAL;
     default: return INSR_EINVAL;
   }
 }
@@ -30,15 +43,15 @@ int launch_fwd_x6_multi(int T, const InsrJetJob* jobs, const int* small, int njo
 // value and gradient jets (the fused pairs the models issue are value jets; the Laplacian
 // jet is never paired), widths 64 / 128 / 256
 template <int NQ>
-int dispatch_fwd_multi_q(int NT, int S, bool LAP, int T, const InsrJetJob* jobs, const int* small, int njobs,
-                         int din, int dout, int L, hipStream_t st) {
+int dispatch_fwd_multi_q(int NT, int S, bool LAP, int T, const InsrJetJob* jobs, const int* small, const int* nbal,
+                         int njobs, int din, int dout, int L, hipStream_t st) {
   if (LAP) return INSR_EINVAL;
 #define INSR_MULTI_S(NTV)                                                                        \
   switch (S) {                                                                                   \
-    case 1: return launch_fwd_x6_multi<NQ, NTV, 1, false>(T, jobs, small, njobs, din, dout, L, st); \
-    case 2: return launch_fwd_x6_multi<NQ, NTV, 2, false>(T, jobs, small, njobs, din, dout, L, st); \
-    case 3: return launch_fwd_x6_multi<NQ, NTV, 3, false>(T, jobs, small, njobs, din, dout, L, st); \
-    case 4: return launch_fwd_x6_multi<NQ, NTV, 4, false>(T, jobs, small, njobs, din, dout, L, st); \
+    case 1: return launch_fwd_x6_multi<NQ, NTV, 1, false>(T, jobs, small, nbal, njobs, din, dout, L, st); \
+    case 2: return launch_fwd_x6_multi<NQ, NTV, 2, false>(T, jobs, small, nbal, njobs, din, dout, L, st); \
+    case 3: return launch_fwd_x6_multi<NQ, NTV, 3, false>(T, jobs, small, nbal, njobs, din, dout, L, st); \
+    case 4: return launch_fwd_x6_multi<NQ, NTV, 4, false>(T, jobs, small, nbal, njobs, din, dout, L, st); \
     default: return INSR_EINVAL;                                                                 \
   }
   switch (NT) {
@@ -52,15 +65,15 @@ int dispatch_fwd_multi_q(int NT, int S, bool LAP, int T, const InsrJetJob* jobs,
 
 template <int NQ>
 int dispatch_fwd_q(int NT, int S, bool LAP, int T, const float* x, int N, int din, int dout, int L,
-                   const float* prm, float* y, float* dy, float* lap, float* act, hipStream_t st) {
+                   const float* prm, float* y, float* dy, float* lap, float* act, int nbal, hipStream_t st) {
 #define INSR_FWD_Q(NTV)                                                                                  \
   switch (S * 2 + (LAP ? 1 : 0)) {                                                                       \
-    case 2: return launch_fwd_x6<NQ, NTV, 1, false>(T, x, N, din, dout, L, prm, y, dy, lap, act, st);    \
-    case 4: return launch_fwd_x6<NQ, NTV, 2, false>(T, x, N, din, dout, L, prm, y, dy, lap, act, st);    \
-    case 6: return launch_fwd_x6<NQ, NTV, 3, false>(T, x, N, din, dout, L, prm, y, dy, lap, act, st);    \
-    case 8: return launch_fwd_x6<NQ, NTV, 4, false>(T, x, N, din, dout, L, prm, y, dy, lap, act, st);    \
-    case 7: return launch_fwd_x6<NQ, NTV, 3, true>(T, x, N, din, dout, L, prm, y, dy, lap, act, st);     \
-    case 9: return launch_fwd_x6<NQ, NTV, 4, true>(T, x, N, din, dout, L, prm, y, dy, lap, act, st);     \
+    case 2: return launch_fwd_x6<NQ, NTV, 1, false>(T, x, N, din, dout, L, prm, y, dy, lap, act, nbal, st);    \
+    case 4: return launch_fwd_x6<NQ, NTV, 2, false>(T, x, N, din, dout, L, prm, y, dy, lap, act, nbal, st);    \
+    case 6: return launch_fwd_x6<NQ, NTV, 3, false>(T, x, N, din, dout, L, prm, y, dy, lap, act, nbal, st);    \
+    case 8: return launch_fwd_x6<NQ, NTV, 4, false>(T, x, N, din, dout, L, prm, y, dy, lap, act, nbal, st);    \
+    case 7: return launch_fwd_x6<NQ, NTV, 3, true>(T, x, N, din, dout, L, prm, y, dy, lap, act, nbal, st);     \
+    case 9: return launch_fwd_x6<NQ, NTV, 4, true>(T, x, N, din, dout, L, prm, y, dy, lap, act, nbal, st);     \
     default: return INSR_EINVAL;                                                                         \
   }
   switch (NT) {

@@ -45,13 +45,25 @@ class Fluid2DModel(BaseModel):
 
     def _sample_in_training(self):
         """The interior batch.  On the GPU the iteration's wall bands come from the same
-        launch (sample_random_and_bands2D) and wait in `_insr_bands` for _boundary_bands."""
+        launch (sample_random_and_bands2D) into the same buffer [interior; bands]: x is its
+        first rows, and _merged(x) hands the whole buffer to the jets that take both."""
         n = self._n_interior()
         if torch.device(self.device).type == "cuda":
-            x, bxy = sample_random_and_bands2D(n, n // 100, device=self.device)
-            self._insr_bands = (bxy.requires_grad_(True), bxy.shape[0] // 2)
-            return x.requires_grad_(True)
+            buf = sample_random_and_bands2D(n, n // 100, device=self.device, merged=True).requires_grad_(True)
+            x = buf[:n]
+            self._insr_merged = (buf, x, (buf.shape[0] - n) // 2)
+            return x
         return sample_random(n, 2, device=self.device).requires_grad_(True)
+
+    def _merged(self, x):
+        """([x; bands] as one leaf, n interior rows, nb rows per band pair): the sampler's
+        buffer when x came from it, else x and _boundary_bands(n) concatenated."""
+        n = x.shape[0]
+        pre = self.__dict__.pop("_insr_merged", None)
+        if pre is not None and pre[1] is x and "_boundary_pair" not in self.__dict__:
+            return pre[0], n, pre[2]
+        bxy, nb = self._boundary_bands(n)
+        return merge_samples(x, bxy), n, nb
 
     def _boundary_pair(self, n_interior):
         nb = n_interior // 100
@@ -67,9 +79,9 @@ class Fluid2DModel(BaseModel):
         if "_boundary_pair" in self.__dict__:
             bx, by = self._boundary_pair(n_interior)
             return torch.cat([bx, by]), bx.shape[0]
-        pre = self.__dict__.pop("_insr_bands", None)
-        if pre is not None and pre[0].shape[0] == 4 * ((n_interior // 100) // 2):
-            return pre
+        pre = self.__dict__.pop("_insr_merged", None)
+        if pre is not None and pre[1].shape[0] == n_interior:
+            return pre[0][n_interior:].detach().requires_grad_(True), pre[2]
         bxy = sample_boundary2D_pair(n_interior // 100, device=self.device).requires_grad_(True)
         return bxy, bxy.shape[0] // 2
 
@@ -169,24 +181,27 @@ class Fluid2DModel(BaseModel):
     # The boundary band's value jet (a few hundred points, a latency-bound launch of its own)
     # joins the same launch as 1-tile blocks placed first in the grid (insr_siren_jet_fwd_multi).
     def _prev_and_current(self, x):
-        """(wall term (unlaunched), u_prev(x) detached, u(x)) -- the three value jets in one launch."""
+        """(u over [x; bands], n, nb, u_prev(x) detached): the trainable field's value jet over
+        the merged batch (interior + wall bands: one jet and one reverse jet) and the frozen
+        field's at x, in one launch."""
+        xa, n, nb = self._merged(x)
         with fused_forwards():
-            bxy, nb = self._boundary_bands(x.shape[0])
-            y_band = self.velocity_field(bxy)
             with torch.no_grad():
                 u_prev = self.velocity_field_prev(x)
-            u = self.velocity_field(x)
-        return wall_term(y_band, nb), u_prev.detach(), u
+            ua = self.velocity_field(xa)
+        return ua, n, nb, u_prev.detach()
 
     @BaseModel._training_loop
     def _advect_velocity(self):
         x = self._sample_in_training()
         if self._fused_pair() and not getattr(self.cfg, "insr_band_stream", False):
-            bc, u_prev, u = self._prev_and_current(x)
+            ua, n, nb, u_prev = self._prev_and_current(x)
             with torch.no_grad():
                 foot = torch.add(x, u_prev, alpha=-self.cfg.dt).clamp_(-1.0, 1.0)
                 u_target = self.velocity_field_prev(foot)
-            main, bc = sq_losses(mse_term(u, u_target), bc)  # both residuals in one launch
+            # mean((u - u_target)^2) over the interior rows and the wall terms on the band rows,
+            # one launch
+            main, bc = sq_losses(mse_term(ua, u_target, count=u_target.numel()), wall_term(ua, nb, row0=n))
             return {'main': main, 'bc': bc}
         bc, join_bc = self._fork("insr_band_stream", self._wall_loss, x.shape[0])
         u_target, join_t = self._fork("insr_nograd_stream", self._advect_target, x)
@@ -204,9 +219,7 @@ class Fluid2DModel(BaseModel):
             # (its tangent streams): ONE pressure jet over [interior; bands] (base.merge_samples)
             # instead of a separate gradient jet + reverse jet for 2% of the points.  The
             # Laplacian rows of the band points get zero adjoint.
-            n = x.shape[0]
-            bxy, nb = self._boundary_bands(n)
-            xa = merge_samples(x, bxy)
+            xa, n, nb = self._merged(x)
             with torch.no_grad():
                 div_u = divergence(self.velocity_field(x), x)
             lap_p, grad_p = laplace(self.pressure_field(xa), xa, return_grad=True)
@@ -226,10 +239,11 @@ class Fluid2DModel(BaseModel):
     def _projection(self):
         x = self._sample_in_training()
         if self._fused_pair() and not getattr(self.cfg, "insr_band_stream", False):
-            bc, u_prev, u = self._prev_and_current(x)
+            ua, n, nb, u_prev = self._prev_and_current(x)
             with torch.no_grad():
                 grad_p = gradient(self.pressure_field(x), x)
-            main, bc = sq_losses(mse_term(u, None, u_prev, grad_p, gamma=-1.0, delta=-1.0), bc)
+            main, bc = sq_losses(mse_term(ua, None, u_prev, grad_p, gamma=-1.0, delta=-1.0, count=u_prev.numel()),
+                                 wall_term(ua, nb, row0=n))
             return {'main': main, 'bc': bc}
         bc, join_bc = self._fork("insr_band_stream", self._wall_loss, x.shape[0])
         (u_prev, grad_p), join_t = self._fork("insr_nograd_stream", self._projection_target, x)

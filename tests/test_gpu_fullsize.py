@@ -183,3 +183,53 @@ def test_fluid2dtlgnM_full_phases_graph_equals_eager(base):
         assert all(torch.isfinite(torch.tensor(list(r.values()))).all() for r in rec), phase
     pres = [r["main"] for r in res[True][2]["_solve_pressure"]]
     assert pres[-1] < pres[0]
+
+
+@pytest.mark.parametrize("case", ["value16708", "value20400"])
+def test_balanced_launch_shapes(base, case):
+    """Batches just above a multiple of the resident block slots run balanced blocks of T + 1
+    tiles (16384 interior + 324 band points: value jets 4 -> 5 tiles per block, gradient jets
+    2 -> 3 in the forward): values, derivatives and parameter gradients vs the oracle."""
+    mode, n = case[:-5], int(case[-5:])
+    lib = base._native.lib()
+    m = base._native.MODE_VALUE if mode == "value" else base._native.MODE_GRAD
+    T_fwd, T_bwd = lib.insr_jet_split_tiles(n, 2, 128, m, 0), lib.insr_jet_split_tiles(n, 2, 128, m, 1)
+    assert {T_fwd, T_bwd} & {3, 5}, (T_fwd, T_bwd)  # the case runs a balanced shape
+    ref, net = pair(base, 2, 2, 4, 128, 41)
+    x = torch.rand(n, 2, generator=torch.Generator().manual_seed(42)) * 2 - 1
+    R = torch.randn(n, 2, 2, generator=torch.Generator().manual_seed(43))
+    xr = x.clone().requires_grad_(True)
+    yr = ref(xr)
+    vr = yr if mode == "value" else O.op_jacobian(yr, xr)[0]
+    (vr * (R[..., 0] if mode == "value" else R)).sum().backward()
+    xg = x.cuda().requires_grad_(True)
+    y = net(xg)
+    v = y if mode == "value" else base.jacobian(y, xg)[0]
+    (v * (R[..., 0] if mode == "value" else R).cuda()).sum().backward()
+    assert nerr(v, vr) < TOL
+    assert nerr(grads(net), grads(ref)) < TOL
+
+
+def test_fused_multi_five_tile_blocks(base):
+    """The fluid advection's fused forward: the frozen field at 16384 interior points and the
+    trainable one at 16384 + 324 band points in one launch of 5-tile blocks (518 four-tile
+    blocks would overflow the 512 resident slots): both outputs and the trainable field's
+    parameter gradients vs the oracle."""
+    refp, prev = pair(base, 2, 2, 4, 128, 51)
+    refc, cur = pair(base, 2, 2, 4, 128, 52)
+    for p in prev.parameters():
+        p.requires_grad_(False)
+    buf = torch.rand(16708, 2, generator=torch.Generator().manual_seed(53)) * 2 - 1
+    R = torch.randn(16708, 2, generator=torch.Generator().manual_seed(54))
+    xb = buf.cuda().requires_grad_(True)
+    with base.fused_forwards():
+        with torch.no_grad():
+            up = prev(xb[:16384])
+        ua = cur(xb)
+    (ua * R.cuda()).sum().backward()
+    assert nerr(up, refp(buf[:16384])) < TOL
+    xr = buf.clone().requires_grad_(True)
+    yr = refc(xr)
+    (yr * R).sum().backward()
+    assert nerr(ua, yr) < TOL
+    assert nerr(grads(cur), grads(refc)) < TOL
