@@ -61,7 +61,7 @@ extern "C" {
 int insr_version(void);
 
 /* Build provenance: the first 16 hex digits of the SHA-256 of the sources the library was
- * built from (csrc/*.hip and *.hpp in name order, then this header). */
+ * built from (the csrc .hip and .hpp files in name order, then this header). */
 const char* insr_build_id(void);
 
 /* Number of fp32 parameters of an SIREN(d_in -> W x (L+1) -> d_out). */
@@ -272,21 +272,31 @@ int insr_sq_loss_fwd(int kind, const float* a, const float* b, const float* c, c
 /* A group of up to INSR_LOSS_GROUP_MAX losses (every residual term of one phase iteration)
  * in ONE launch, each with its gradient for a unit output seed (the training loop's backward
  * seeds every loss with 1): loss k = insr_sq_loss_fwd of (kind, a..d, n, m, coefficients,
- * scale) written to *out, and d(out)/d(input) to ga / gb / gc / gd (any may be NULL) over their
- * full length (*_len elements): zeros outside the loss range.  The loss reads a from element
- * a_off (COMBO: n terms; BANDS: rows a_off / m .. a_off / m + 2n of an (R, m) tensor, a_off a
- * multiple of m), b, c, d from element 0.  work: insr_sq_loss_work_floats() floats,
- * zero-initialised once (left zero).  The backward of a unit-seeded loss then needs no launch. */
+ * scale) written to *out, and d(out)/d(input) to ga / gb / gc / gd (any may be NULL).
+ * The loss reads a from element a_off (COMBO: n terms; BANDS: rows a_off / m .. a_off / m + 2n
+ * of an (R, m) tensor, a_off a multiple of m), b, c, d from element 0 with element strides
+ * sb, sc, sd (e.g. the diagonal of a Jacobian).  ga is written on elements [ga_lo, ga_hi):
+ * the loss's terms, zeros elsewhere in that range -- two losses over disjoint rows of ONE
+ * tensor (a merged jet's interior and band rows) share one gradient buffer; gb / gc / gd are
+ * n contiguous elements (gb_len ... = n, or 0 when NULL).  work: insr_sq_loss_work_floats()
+ * floats, zero-initialised once (left zero).  A unit-seeded loss's backward then needs no
+ * launch. */
+/* out[i] = clamp(x[i] + alpha y[i], lo, hi), i < n: the semi-Lagrangian foot of the fluid
+ * advection, clamp(x - dt u_prev(x), -1, 1) (fluid/model.py:97), in one launch. */
+int insr_axpy_clamp(const float* x, const float* y, float alpha, float lo, float hi, float* out, long n,
+                    void* stream);
+
 #define INSR_LOSS_GROUP_MAX 4
 typedef struct InsrLoss {
   int kind;  /* INSR_LOSS_COMBO / INSR_LOSS_BANDS */
   int m;     /* BANDS: columns of a */
   long n;    /* COMBO: terms; BANDS: rows per band */
   const float *a, *b, *c, *d;
+  long sb, sc, sd; /* element strides of b, c, d */
   float alpha, beta, gamma, delta, scale;
   float* out;
   float* ga;
-  long ga_len, a_off;
+  long ga_lo, ga_hi, a_off;
   float *gb, *gc, *gd;
   long gb_len, gc_len, gd_len;
 } InsrLoss;

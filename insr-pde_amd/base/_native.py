@@ -61,6 +61,7 @@ SIGNATURES = {
     "insr_svd_energy_bwd": (_I, [_P, _L, _I, _F, _F, _P, _P, _P]),
     "insr_sq_loss_fwd": (_I, [_I, _P, _P, _P, _P, _L, _I, _F, _F, _F, _F, _F, _P, _P, _P]),
     "insr_sq_loss_group": (_I, [_P, _I, _P, _P]),
+    "insr_axpy_clamp": (_I, [_P, _P, _F, _F, _F, _P, _L, _P]),
     "insr_sq_loss_bwd": (_I, [_I, _P, _P, _P, _P, _L, _I, _F, _F, _F, _F, _F, _P, _P, _P, _P, _P, _P]),
     "insr_jet_set_split_tiles": (None, [_I, _I, _I]),
     "insr_jet_set_precision": (None, [_I, _I]),
@@ -92,8 +93,9 @@ LOSS_GROUP_MAX = 4  # INSR_LOSS_GROUP_MAX
 class Loss(ctypes.Structure):
     """struct InsrLoss (include/insr_siren.h): one loss of insr_sq_loss_group."""
     _fields_ = [("kind", _I), ("m", _I), ("n", _L), ("a", _P), ("b", _P), ("c", _P), ("d", _P),
+                ("sb", _L), ("sc", _L), ("sd", _L),
                 ("alpha", _F), ("beta", _F), ("gamma", _F), ("delta", _F), ("scale", _F), ("out", _P),
-                ("ga", _P), ("ga_len", _L), ("a_off", _L), ("gb", _P), ("gc", _P), ("gd", _P),
+                ("ga", _P), ("ga_lo", _L), ("ga_hi", _L), ("a_off", _L), ("gb", _P), ("gc", _P), ("gd", _P),
                 ("gb_len", _L), ("gc_len", _L), ("gd_len", _L)]
 
 

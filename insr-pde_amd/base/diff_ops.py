@@ -105,11 +105,17 @@ def jacobian(y: torch.FloatTensor, x: torch.FloatTensor):
 
 def jacobian_nosync(y, x):
     """jacobian() without the NaN status host sync (returns the device flag instead)."""
+    J = jacobian_only(y, x)
+    return J, torch.isnan(J).any()
+
+
+def jacobian_only(y, x):
+    """The (N, dim_y, dim_x) Jacobian of jacobian() alone: no status (no NaN scan launches)."""
     mlp, value, affine = _resolve(y, x, "jacobian")
     _, J, _ = _jet.jet_of(mlp, value, x, nat.MODE_GRAD)
     if affine:
         J = J + torch.eye(J.shape[-1], device=J.device, dtype=J.dtype)
-    return J, torch.isnan(J).any()
+    return J
 
 
 def hessian(y, x):

@@ -75,22 +75,44 @@ def _grad_like(t, n_used):
 # Unit seeds: 1-element tensors holding 1.0 that the training loop passes as the gradient of
 # every loss (BaseModel._unit_seed).  A loss whose backward receives one of them returns the
 # gradient its forward launch already wrote -- no backward launch.
-_UNIT_SEEDS = set()
+# data_ptr -> the seed tensor itself: the registry holds a reference, so a registered address
+# can never be recycled by the caching allocator for another (non-unit) gradient tensor
+_UNIT_SEEDS = {}
 
 
 def register_unit_seed(t):
     """Declare `t` (a tensor of ones the caller never modifies) a unit seed for loss backwards."""
     if t.numel() == 1:
-        _UNIT_SEEDS.add(t.data_ptr())
+        _UNIT_SEEDS[t.data_ptr()] = t
     return t
+
+
+def _prep_strided(t):
+    """(tensor, element stride) of a b / c / d input: contiguous tensors and 1-D (or (n, 1))
+    strided views are read in place (e.g. the diagonal of a Jacobian, J[:, i, i])."""
+    if t is None:
+        return None, 1
+    if not t.is_cuda or t.dtype != torch.float32:
+        raise nat.NativeUnavailable("fused losses run on fp32 GPU tensors only")
+    if t.is_contiguous():
+        return t, 1
+    if t.dim() == 1 or (t.dim() == 2 and t.shape[1] == 1):
+        return t, t.stride(0)
+    return t.contiguous(), 1
 
 
 class LossSpec:
     """One squared-residual loss, not yet launched (see sq_losses)."""
 
-    def __init__(self, kind, n, m, coef, scale, a, b, c, d, a_off):
-        self.meta = (kind, int(n), int(m), tuple(float(v) for v in coef), float(scale), int(a_off))
+    def __init__(self, kind, n, m, coef, scale, a, b, c, d, a_off, strides=(1, 1, 1)):
+        self.meta = (kind, int(n), int(m), tuple(float(v) for v in coef), float(scale), int(a_off),
+                     tuple(int(v) for v in strides))
         self.tensors = (a, b, c, d)
+
+    def a_range(self):
+        """Elements of `a` the loss reads: [a_off, a_off + terms) (BANDS: 2n rows of m)."""
+        kind, n, m, _, _, a_off, _ = self.meta
+        return a_off, a_off + (n if kind == nat.LOSS_COMBO else 2 * n * m)
 
 
 def _mse_spec(a, b=None, c=None, d=None, alpha=1.0, beta=-1.0, gamma=1.0, delta=1.0, count=None, a_row0=0,
@@ -110,8 +132,9 @@ def _mse_spec(a, b=None, c=None, d=None, alpha=1.0, beta=-1.0, gamma=1.0, delta=
     if reduction not in ("mean", "sum"):
         raise ValueError(reduction)
     scale = 1.0 / max(count, 1) if reduction == "mean" else 1.0
-    return LossSpec(nat.LOSS_COMBO, count, 1, (alpha, beta, gamma, delta), scale, _prep(a), _prep(b), _prep(c),
-                    _prep(d), a_off)
+    (b, sb), (c, sc), (d, sd) = _prep_strided(b), _prep_strided(c), _prep_strided(d)
+    return LossSpec(nat.LOSS_COMBO, count, 1, (alpha, beta, gamma, delta), scale, _prep(a), b, c, d, a_off,
+                    (sb, sc, sd))
 
 
 def _wall_spec(y, n, row0=0):
@@ -131,65 +154,105 @@ def wall_term(y, n, row0=0):
     return _wall_spec(y, n, row0)
 
 
+def _shared_a(specs):
+    """For each loss, the index of the earlier loss whose `a` (the same tensor) it shares a
+    gradient buffer with, or None.  Sharing needs disjoint ranges that together cover the whole
+    tensor (e.g. a merged jet's interior rows and its band rows)."""
+    owner = [None] * len(specs)
+    groups = {}
+    for i, sp in enumerate(specs):
+        groups.setdefault(id(sp.tensors[0]), []).append(i)
+    for idx in groups.values():
+        if len(idx) < 2:
+            continue
+        rs = sorted(specs[i].a_range() for i in idx)
+        numel = specs[idx[0]].tensors[0].numel()
+        if rs[0][0] != 0 or rs[-1][1] != numel or any(rs[k][1] != rs[k + 1][0] for k in range(len(rs) - 1)):
+            continue
+        for i in idx[1:]:
+            owner[i] = idx[0]
+    return owner
+
+
 class _SqLossGroup(torch.autograd.Function):
     """Up to LOSS_GROUP_MAX losses in ONE launch forward (insr_sq_loss_group), each with the
-    gradient for a unit seed written by the same launch; inputs: 4 tensor slots per loss."""
+    gradient for a unit seed written by the same launch; inputs: 4 tensor slots per loss (a
+    loss that shares its `a` with an earlier one passes None there: one gradient buffer)."""
 
     @staticmethod
-    def forward(ctx, metas, *tensors):
+    def forward(ctx, metas, owner, real_a, *tensors):
         lib = nat.lib()
         k = len(metas)
         dev = next(t for t in tensors if t is not None).device
-        need = ctx.needs_input_grad[1:]
+        need = ctx.needs_input_grad[3:]
         outs = [torch.empty((), device=dev, dtype=torch.float32) for _ in range(k)]
         arr = (nat.Loss * k)()
         grads = []
         multi = False
-        for i, (kind, n, m, coef, scale, a_off) in enumerate(metas):
-            slot = tensors[4 * i:4 * i + 4]
-            g = [torch.empty_like(t) if (t is not None and nd) else None for t, nd in zip(slot, need[4 * i:4 * i + 4])]
+        p = lambda t: None if t is None else t.data_ptr()  # noqa: E731
+        for i, (kind, n, m, coef, scale, a_off, (sb, sc, sd)) in enumerate(metas):
+            slot = list(tensors[4 * i:4 * i + 4])
+            nd = list(need[4 * i:4 * i + 4])
+            if owner[i] is not None:  # a shared with loss owner[i]: write into its buffer
+                slot[0], nd[0] = real_a[i], need[4 * owner[i]]
+            g = [torch.empty_like(t) if (t is not None and q) else None for t, q in zip(slot, nd)]
+            if owner[i] is not None:
+                g[0] = grads[4 * owner[i]]
             grads.extend(g)
-            lens = [0 if t is None else t.numel() for t in g]
-            span = max(lens + [n if kind == nat.LOSS_COMBO else 2 * n])
+            terms = n if kind == nat.LOSS_COMBO else 2 * n
+            a_lo, a_hi = (a_off, a_off + terms * (1 if kind == nat.LOSS_COMBO else m))
+            shared = owner[i] is not None or any(o == i for o in owner)
+            lo, hi = (a_lo, a_hi) if shared else (0, 0 if g[0] is None else g[0].numel())
+            lens = [0 if t is None else t.numel() for t in g[1:]]
+            span = max([hi - lo] + lens + [terms])
             multi = multi or span > 1024
-            p = lambda t: None if t is None else t.data_ptr()  # noqa: E731
             a, b, c, d = slot
-            arr[i] = nat.Loss(kind, m, n, p(a), p(b), p(c), p(d), *coef, scale, outs[i].data_ptr(),
-                              p(g[0]), lens[0], a_off, p(g[1]), p(g[2]), p(g[3]), lens[1], lens[2], lens[3])
+            arr[i] = nat.Loss(kind, m, n, p(a), p(b), p(c), p(d), sb, sc, sd, *coef, scale, outs[i].data_ptr(),
+                              p(g[0]), lo, hi, a_off, p(g[1]), p(g[2]), p(g[3]), *lens)
         work = _workspace(dev) if multi else None
         nat.check(lib.insr_sq_loss_group(arr, k, nat.ptr(work), nat.stream_of(dev)), "insr_sq_loss_group")
-        ctx.save_for_backward(*tensors)
-        ctx.metas = metas
-        ctx.pre = grads
+        ctx.save_for_backward(*[real_a[i] if owner[i] is not None and j == 0 else t
+                                for i in range(k) for j, t in enumerate(tensors[4 * i:4 * i + 4])])
+        ctx.metas, ctx.owner = metas, owner
+        ctx.pre = [None if (owner[i // 4] is not None and i % 4 == 0) else g for i, g in enumerate(grads)]
         return tuple(outs)
 
     @staticmethod
     def backward(ctx, *gouts):
         tensors = ctx.saved_tensors
-        need = ctx.needs_input_grad[1:]
+        need = ctx.needs_input_grad[3:]
+        owner = ctx.owner
+        k = len(ctx.metas)
         res = [None] * len(tensors)
-        for i, (kind, n, m, coef, scale, a_off) in enumerate(ctx.metas):
-            sl = slice(4 * i, 4 * i + 4)
-            if not any(need[sl]):
+        unit = [g is not None and g.numel() == 1 and g.data_ptr() in _UNIT_SEEDS for g in gouts]
+        for o in range(k):
+            if owner[o] is not None:
                 continue
-            gout = gouts[i]
-            if gout is None:
+            members = [o] + [j for j in range(k) if owner[j] == o]
+            if all(unit[j] for j in members):  # the forward wrote exactly these gradients
+                res[4 * o:4 * o + 4] = ctx.pre[4 * o:4 * o + 4]
+                for j in members[1:]:
+                    res[4 * j + 1:4 * j + 4] = ctx.pre[4 * j + 1:4 * j + 4]
                 continue
-            if gout.numel() == 1 and gout.data_ptr() in _UNIT_SEEDS:
-                res[sl] = ctx.pre[sl]
-                continue
-            a, b, c, d = tensors[sl]
-            offs = (a_off, 0, 0, 0)
-            used = n if kind == nat.LOSS_COMBO else 2 * n * m
-            g = [_grad_like(t, used) if (t is not None and nd) else None for t, nd in zip((a, b, c, d), need[sl])]
-            go = gout.reshape(1) if gout.is_contiguous() else gout.contiguous().reshape(1)
-            rc = nat.lib().insr_sq_loss_bwd(kind, _at(a, offs[0]), _at(b, 0), _at(c, 0), _at(d, 0), n, m, *coef,
-                                            scale, nat.ptr(go), *[_at(t, o) for t, o in zip(g, offs)],
-                                            nat.stream_of(a.device))
-            nat.check(rc, "insr_sq_loss_bwd")
-            res[sl] = g
+            for j in members:  # general seeds: one backward launch per loss, a-gradients summed
+                if gouts[j] is None:
+                    continue
+                kind, n, m, coef, scale, a_off, strides = ctx.metas[j]
+                a, b, c, d = tensors[4 * j:4 * j + 4]
+                nd = [need[4 * o]] + list(need[4 * j + 1:4 * j + 4])
+                used = n if kind == nat.LOSS_COMBO else 2 * n * m
+                g = [_grad_like(t, used) if (t is not None and q) else None for t, q in zip((a, b, c, d), nd)]
+                b, c, d = [None if t is None else (t if s_ == 1 else t.contiguous()) for t, s_ in zip((b, c, d), strides)]
+                go = gouts[j].reshape(1) if gouts[j].is_contiguous() else gouts[j].contiguous().reshape(1)
+                rc = nat.lib().insr_sq_loss_bwd(kind, _at(a, a_off), _at(b, 0), _at(c, 0), _at(d, 0), n, m, *coef,
+                                                scale, nat.ptr(go), _at(g[0], a_off), _at(g[1], 0), _at(g[2], 0),
+                                                _at(g[3], 0), nat.stream_of(a.device))
+                nat.check(rc, "insr_sq_loss_bwd")
+                if g[0] is not None:
+                    res[4 * o] = g[0] if res[4 * o] is None else res[4 * o] + g[0]
+                res[4 * j + 1:4 * j + 4] = g[1:]
         ctx.pre = None
-        return (None, *res)
+        return (None, None, None, *res)
 
 
 def sq_losses(*specs):
@@ -198,8 +261,11 @@ def sq_losses(*specs):
     if not 1 <= len(specs) <= nat.LOSS_GROUP_MAX:
         raise ValueError(f"sq_losses: 1..{nat.LOSS_GROUP_MAX} losses")
     metas = tuple(sp.meta for sp in specs)
-    tensors = [t for sp in specs for t in sp.tensors]
-    return _SqLossGroup.apply(metas, *tensors)
+    owner = _shared_a(specs)
+    real_a = [sp.tensors[0] for sp in specs]
+    tensors = [None if (owner[i] is not None and j == 0) else t
+               for i, sp in enumerate(specs) for j, t in enumerate(sp.tensors)]
+    return _SqLossGroup.apply(metas, owner, real_a, *tensors)
 
 
 def fused_mse(a, b=None, c=None, d=None, alpha=1.0, beta=-1.0, gamma=1.0, delta=1.0, count=None, a_row0=0,
@@ -219,6 +285,18 @@ def wall_mse(y, n, row0=0):
     m >= 2, R >= r + 2n (the normal-component wall terms of both boundary bands in one
     launch; the other rows -- a merged launch's interior points -- get zero gradient)."""
     return sq_losses(_wall_spec(y, n, row0))[0]
+
+
+def axpy_clamp(x, y, alpha, lo, hi):
+    """clamp(x + alpha y, lo, hi) in one launch (no autograd: the fluid advection's foot,
+    computed under no_grad, fluid/model.py:97)."""
+    x, y = _prep(x), _prep(y)
+    if x.shape != y.shape:
+        raise ValueError(f"axpy_clamp: {tuple(x.shape)} vs {tuple(y.shape)}")
+    out = torch.empty_like(x)
+    nat.check(nat.lib().insr_axpy_clamp(nat.ptr(x), nat.ptr(y), float(alpha), float(lo), float(hi), nat.ptr(out),
+                                        x.numel(), nat.stream_of(x.device)), "insr_axpy_clamp")
+    return out
 
 
 _SVD_WORK = {}  # (device index, stream handle) -> partials buffer of the SVD-energy reduction

@@ -268,15 +268,53 @@ __device__ __forceinline__ void dw_put(unsigned short* P, const floatx4& v, int 
   for (int q = 0; q < NQ; ++q) q1[q * (kDwPL / 2)] = u[q];
 }
 
+// first level of the compact-row reduction, 8 waves: column block bx of out row by (of nby)
+// = the fixed-order sum of part rows [nb by / nby, nb (by+1) / nby).  red: 512 floats of LDS.
+__device__ __forceinline__ void rows_level1(const float* __restrict__ part, int nb, long count, float* __restrict__ out,
+                                            int bx, int by, int nby, float* red) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const long i = (long)bx * 64 + lane;
+  const int b0 = (int)((long)nb * by / nby), b1 = (int)((long)nb * (by + 1) / nby);
+  float acc = 0.f;
+  if (i < count) {
+    int b = b0 + w;
+    for (; b + 56 < b1; b += 64) {  // 8 independent loads in flight per thread
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = part[(long)(b + 8 * u) * count + i];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc += v[u];
+    }
+    for (; b < b1; b += 8) acc += part[(long)b * count + i];
+  }
+  red[w * 64 + lane] = acc;
+  __syncthreads();
+  if (w == 0 && i < count) {
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) t += red[k * 64 + lane];
+    out[(long)by * count + i] = t;
+  }
+}
+
+// dW of hidden layer blockIdx.y + 1 over chunk slice blockIdx.x (y < L).  Planes y >= L carry
+// the first level of the compact-row reduction (small -> rows, block id (y - L) KS + x), so it
+// runs on the CUs the dW tail leaves idle instead of in a launch of its own.
 template <int NQ, int NT, int S, bool LAP>
 __global__ __launch_bounds__(512) void dw_x6(int N, const float* __restrict__ act, const float* __restrict__ adj,
-                                             float* __restrict__ dpart, int KS) {
+                                             float* __restrict__ dpart, int KS, int L, const float* __restrict__ small,
+                                             int tiles, long Ps, float* __restrict__ rows, int rs, int rows_x) {
   constexpr int W = 16 * NT, RT = NT / 8;  // RT: dW row tiles per wave
   constexpr int G = NT / 4;                   // granules per thread per chunk (2 units x NT row tiles / 8 waves)
   constexpr int kDwPL = dw_plane<NT>();
   extern __shared__ __attribute__((aligned(16))) float lds_f[];
   unsigned short* A = reinterpret_cast<unsigned short*>(lds_f);
   unsigned short* B = A + NQ * kDwPL;
+  if ((int)blockIdx.y >= L) {
+    const int rb = ((int)blockIdx.y - L) * KS + (int)blockIdx.x;
+    if (rb < rows_x * rs) rows_level1(small, tiles, Ps, rows, rb % rows_x, rb / rows_x, rs, lds_f);
+    return;
+  }
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
   const int j = blockIdx.y + 1;
   const int ntiles = ((N + 63) / 64) * 4;
@@ -432,12 +470,39 @@ __global__ __launch_bounds__(256) void reduce_rows_kernel(const float* __restric
   if (w == 0 && i < count) out[(long)blockIdx.y * count + i] = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
 }
 
-// per hidden layer (blockIdx.y): sum of the KS partial W x W blocks.  A block = 64 column quads
-// (16-B loads, 1 KiB per wave-instruction) x 8 waves over the slices, 8 independent loads in
-// flight per thread; fixed summation order (deterministic, no atomics).
+// per hidden layer (blockIdx.y < L): sum of the KS partial W x W blocks.  A block = 64 column
+// quads (16-B loads, 1 KiB per wave-instruction) x 8 waves over the slices, 8 independent loads
+// in flight per thread; fixed summation order (deterministic, no atomics).  Plane y == L: the
+// second level of the compact-row reduction (rs rows -> the flat gradient), same launch.
 __global__ __launch_bounds__(512) void reduce_dw_kernel(const float* __restrict__ dpart, int KS, int din, int W,
-                                                        float* __restrict__ grad, int accumulate, int grad16) {
+                                                        float* __restrict__ grad, int accumulate, int grad16, int L,
+                                                        const float* __restrict__ rows, int rs, long Ps, int dout) {
   __shared__ floatx4 red[8][64];
+  if ((int)blockIdx.y == L) {
+    float* r = reinterpret_cast<float*>(&red[0][0]);
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const long i = (long)blockIdx.x * 64 + lane;
+    float acc = 0.f;
+    if (i < Ps)
+      for (int b = w; b < rs; b += 8) acc += rows[(long)b * Ps + i];
+    r[w * 64 + lane] = acc;
+    __syncthreads();
+    if (w == 0 && i < Ps) {
+      float t = 0.f;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) t += r[k * 64 + lane];
+      const long head = (long)W * din + W, hid = (long)L * W;
+      long dst;
+      if (i < head)
+        dst = i;
+      else if (i < head + hid)
+        dst = hidden_off(din, W, 1 + (int)((i - head) / W)) + (long)W * W + (i - head) % W;
+      else
+        dst = out_off(din, W, L) + (i - head - hid);
+      grad[dst] = accumulate ? grad[dst] + t : t;
+    }
+    return;
+  }
   const int j = blockIdx.y + 1;
   const long WW = (long)W * W;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -517,17 +582,22 @@ int wide_bwd_t(const float* x, int N, int din, int dout, int L, const float* prm
   }
   hipLaunchKernelGGL((jet_bwd_x6p<NQ, NT, S, LAP>), dim3(tiles), dim3(512), lds_p, st, x, N, din, dout, L, prm, act, gy,
                      gdy, glap, adj, small, Ps);
-  if (L > 0) {
-    const int KS = wide_ks(N, S, L);
-    hipLaunchKernelGGL((dw_x6<NQ, NT, S, LAP>), dim3(KS, L), dim3(512), (dw_lds<NQ, NT>()), st, N, act, adj, dpart, KS);
-    const int grad16 = (((uintptr_t)(grad + hidden_off(din, W, 1))) & 15) == 0 ? 1 : 0;  // W % 4 == 0: all layers alike
-    hipLaunchKernelGGL(reduce_dw_kernel, dim3((unsigned)((W * W / 4 + 63) / 64), L), dim3(512), 0, st, dpart, KS, din,
-                       W, grad, accumulate, grad16);
-  }
   const int rs = tiles < kSmallRS ? tiles : kSmallRS;
-  hipLaunchKernelGGL(reduce_rows_kernel, dim3((unsigned)((Ps + 63) / 64), rs), dim3(256), 0, st, small, tiles, Ps, rows);
-  hipLaunchKernelGGL(reduce_small_kernel, dim3((unsigned)((Ps + 63) / 64)), dim3(256), 0, st, rows, rs, Ps, din, dout,
-                     L, W, grad, accumulate);
+  const int rows_x = (int)((Ps + 63) / 64);
+  if (L > 0) {  // 3 launches: propagation | dW partials + compact rows level 1 | dW sums + rows level 2
+    const int KS = wide_ks(N, S, L);
+    const int planes = (rows_x * rs + KS - 1) / KS;
+    hipLaunchKernelGGL((dw_x6<NQ, NT, S, LAP>), dim3(KS, L + planes), dim3(512), (dw_lds<NQ, NT>()), st, N, act, adj,
+                       dpart, KS, L, small, tiles, Ps, rows, rs, rows_x);
+    const int grad16 = (((uintptr_t)(grad + hidden_off(din, W, 1))) & 15) == 0 ? 1 : 0;  // W % 4 == 0: all layers alike
+    const int wq = (W * W / 4 + 63) / 64;
+    hipLaunchKernelGGL(reduce_dw_kernel, dim3((unsigned)(wq > rows_x ? wq : rows_x), L + 1), dim3(512), 0, st, dpart,
+                       KS, din, W, grad, accumulate, grad16, L, rows, rs, Ps, dout);
+    return (int)hipGetLastError();
+  }
+  hipLaunchKernelGGL(reduce_rows_kernel, dim3((unsigned)rows_x, rs), dim3(256), 0, st, small, tiles, Ps, rows);
+  hipLaunchKernelGGL(reduce_small_kernel, dim3((unsigned)rows_x), dim3(256), 0, st, rows, rs, Ps, din, dout, L, W, grad,
+                     accumulate);
   return (int)hipGetLastError();
 }
 

@@ -27,17 +27,18 @@ struct LossIn {
   const float* c;
   const float* d;
   float alpha, beta, gamma, delta;
+  long sb = 1, sc = 1, sd = 1;  // element strides of b, c, d
 };
 
 // r = alpha (a + beta b) + gamma (c + delta d), evaluated in exactly that order
 // (the reference's rounding for (u - u0)/dt + v (ux + u0x)/2 and u - (u_prev - grad_p))
 __device__ __forceinline__ float combo_residual(const LossIn& in, long i) {
   float p = in.a[i];
-  if (in.b) p = p + in.beta * in.b[i];
+  if (in.b) p = p + in.beta * in.b[i * in.sb];
   p = in.alpha * p;
   if (in.c) {
-    float q = in.c[i];
-    if (in.d) q = q + in.delta * in.d[i];
+    float q = in.c[i * in.sc];
+    if (in.d) q = q + in.delta * in.d[i * in.sd];
     p = p + in.gamma * q;
   }
   return p;
@@ -129,9 +130,11 @@ struct LossGroup {
   int count;
 };
 
+// elements a loss's blocks walk: its terms, and every gradient element it writes (ga: its
+// range [ga_lo, ga_hi) walked as e = ga_lo + i)
 __device__ __forceinline__ long loss_span(const InsrLoss& L) {
   long span = L.kind == INSR_LOSS_COMBO ? L.n : 2 * L.n;
-  const long lens[4] = {L.ga ? L.ga_len : 0, L.gb ? L.gb_len : 0, L.gc ? L.gc_len : 0, L.gd ? L.gd_len : 0};
+  const long lens[4] = {L.ga ? L.ga_hi - L.ga_lo : 0, L.gb ? L.gb_len : 0, L.gc ? L.gc_len : 0, L.gd ? L.gd_len : 0};
   for (int k = 0; k < 4; ++k) span = lens[k] > span ? lens[k] : span;
   return span;
 }
@@ -143,13 +146,13 @@ __global__ __launch_bounds__(kLossThreads) void sq_loss_group_kernel(const LossG
   for (int q = 1; q < INSR_LOSS_GROUP_MAX; ++q) k += (q < G.count && (int)blockIdx.x >= G.first[q]) ? 1 : 0;
   const InsrLoss& L = G.l[k];
   const int blk = blockIdx.x - G.first[k], nblk = G.first[k + 1] - G.first[k];
-  const LossIn in{L.a + L.a_off, L.b, L.c, L.d, L.alpha, L.beta, L.gamma, L.delta};
+  const LossIn in{L.a + L.a_off, L.b, L.c, L.d, L.alpha, L.beta, L.gamma, L.delta, L.sb, L.sc, L.sd};
   const long n = L.n;
   const int m = L.m;
   const float g2 = 2.f * L.scale;
   const float cf[4] = {L.alpha, L.alpha * L.beta, L.gamma, L.gamma * L.delta};
   float* const gp[4] = {L.ga, L.gb, L.gc, L.gd};
-  const long gl[4] = {L.ga_len, L.gb_len, L.gc_len, L.gd_len};
+  const long gl[4] = {L.ga_hi - L.ga_lo, L.gb_len, L.gc_len, L.gd_len};
   const long span = loss_span(L);
   const long count = L.kind == INSR_LOSS_COMBO ? n : 2 * n;
   float acc = 0.f;
@@ -161,9 +164,9 @@ __global__ __launch_bounds__(kLossThreads) void sq_loss_group_kernel(const LossG
         acc += r * r;
       }
       const float g = g2 * r;
-      if (gp[0] && e < gl[0]) {  // a: the loss range starts at a_off
-        const long t = e - L.a_off;
-        gp[0][e] = (t >= 0 && t < n) ? cf[0] * (t == e ? g : g2 * combo_residual(in, t)) : 0.f;
+      if (gp[0] && e < gl[0]) {  // a: element ea = ga_lo + e; the loss range starts at a_off
+        const long ea = L.ga_lo + e, t = ea - L.a_off;
+        gp[0][ea] = (t >= 0 && t < n) ? cf[0] * (t == e ? g : g2 * combo_residual(in, t)) : 0.f;
       }
 #pragma unroll
       for (int q = 1; q < 4; ++q)
@@ -174,10 +177,11 @@ __global__ __launch_bounds__(kLossThreads) void sq_loss_group_kernel(const LossG
         acc += v * v;
       }
       if (gp[0] && e < gl[0]) {
-        const long row = e / m - L.a_off / m;
-        const int col = (int)(e % m);
+        const long ea = L.ga_lo + e;
+        const long row = ea / m - L.a_off / m;
+        const int col = (int)(ea % m);
         const bool hit = row >= 0 && row < 2 * n && col == (row < n ? 0 : 1);
-        gp[0][e] = hit ? g2 * in.a[row * m + col] : 0.f;
+        gp[0][ea] = hit ? g2 * in.a[row * m + col] : 0.f;
       }
     }
   }
@@ -203,6 +207,15 @@ __global__ __launch_bounds__(kLossThreads) void sq_loss_group_kernel(const LossG
     tot += __hip_atomic_load(wk + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   L.out[0] = L.scale * tot;
   atomicExch(ticket, 0u);
+}
+
+// out = clamp(x + alpha y, lo, hi): the semi-Lagrangian foot of the fluid advection,
+// clamp(x - dt u_prev(x), -1, 1) (fluid/model.py:97), one launch instead of add + clamp
+__global__ __launch_bounds__(256) void axpy_clamp_kernel(const float* __restrict__ x, const float* __restrict__ y,
+                                                         float alpha, float lo, float hi, float* __restrict__ out,
+                                                         long n) {
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256)
+    out[i] = fminf(fmaxf(x[i] + alpha * y[i], lo), hi);
 }
 
 }  // namespace insr
@@ -233,6 +246,16 @@ int insr_sq_loss_fwd(int kind, const float* a, const float* b, const float* c, c
   return (int)hipGetLastError();
 }
 
+int insr_axpy_clamp(const float* x, const float* y, float alpha, float lo, float hi, float* out, long n, void* stream) {
+  if (!x || !y || !out || n < 0) return INSR_EINVAL;
+  if (n == 0) return 0;
+  long nb = (n + 255) / 256;
+  if (nb > 2048) nb = 2048;
+  hipLaunchKernelGGL(axpy_clamp_kernel, dim3((unsigned)nb), dim3(256), 0, (hipStream_t)stream, x, y, alpha, lo, hi, out,
+                     n);
+  return (int)hipGetLastError();
+}
+
 int insr_sq_loss_group(const InsrLoss* losses, int count, float* work, void* stream) {
   if (!losses || count < 1 || count > INSR_LOSS_GROUP_MAX) return INSR_EINVAL;
   LossGroup G;
@@ -241,14 +264,15 @@ int insr_sq_loss_group(const InsrLoss* losses, int count, float* work, void* str
   bool multi = false;
   for (int k = 0; k < count; ++k) {
     const InsrLoss& L = losses[k];
-    if (!L.a || !L.out || L.n < 0 || L.a_off < 0) return INSR_EINVAL;
+    if (!L.a || !L.out || L.n < 0 || L.a_off < 0 || L.ga_lo < 0 || (L.ga && L.ga_hi < L.ga_lo)) return INSR_EINVAL;
+    if (L.sb < 1 || L.sc < 1 || L.sd < 1) return INSR_EINVAL;
     if (L.kind != INSR_LOSS_COMBO && L.kind != INSR_LOSS_BANDS) return INSR_EINVAL;
     if (L.kind == INSR_LOSS_BANDS && (L.m < 2 || L.b || L.c || L.d || L.gb || L.gc || L.gd || L.a_off % L.m))
       return INSR_EINVAL;
     if (L.d && !L.c) return INSR_EINVAL;
     G.l[k] = L;
     long span = L.kind == INSR_LOSS_COMBO ? L.n : 2 * L.n;
-    const long lens[4] = {L.ga ? L.ga_len : 0, L.gb ? L.gb_len : 0, L.gc ? L.gc_len : 0, L.gd ? L.gd_len : 0};
+    const long lens[4] = {L.ga ? L.ga_hi - L.ga_lo : 0, L.gb ? L.gb_len : 0, L.gc ? L.gc_len : 0, L.gd ? L.gd_len : 0};
     for (int q = 0; q < 4; ++q) span = lens[q] > span ? lens[q] : span;
     long nb = (span + kGroupPerBlock - 1) / kGroupPerBlock;
     if (nb < 1) nb = 1;

@@ -15,9 +15,10 @@ import os
 import numpy as np
 import torch
 
-from base import (BaseModel, divergence, fused_forwards, fused_mse, gradient, jacobian, laplace, merge_samples,
-                  mse_term, sample_boundary2D_pair, sample_boundary2D_separate, sample_random,
+from base import (BaseModel, axpy_clamp, divergence, fused_forwards, fused_mse, gradient, jacobian, laplace,
+                  merge_samples, mse_term, sample_boundary2D_pair, sample_boundary2D_separate, sample_random,
                   sample_random_and_bands2D, sample_uniform, sq_losses, wall_mse, wall_term)
+from base.diff_ops import jacobian_only
 
 from .examples import get_examples
 
@@ -160,7 +161,7 @@ class Fluid2DModel(BaseModel):
     def _advect_target(self, x):
         with torch.no_grad():
             u_prev = self.velocity_field_prev(x).detach()
-            foot = torch.add(x, u_prev, alpha=-self.cfg.dt).clamp_(-1.0, 1.0)
+            foot = axpy_clamp(x.detach(), u_prev, -self.cfg.dt, -1.0, 1.0)  # clamp(x - dt u_prev, -1, 1)
             return self.velocity_field_prev(foot)
 
     def _velocity_divergence(self, x):
@@ -197,7 +198,7 @@ class Fluid2DModel(BaseModel):
         if self._fused_pair() and not getattr(self.cfg, "insr_band_stream", False):
             ua, n, nb, u_prev = self._prev_and_current(x)
             with torch.no_grad():
-                foot = torch.add(x, u_prev, alpha=-self.cfg.dt).clamp_(-1.0, 1.0)
+                foot = axpy_clamp(x.detach(), u_prev, -self.cfg.dt, -1.0, 1.0)  # clamp(x - dt u_prev, -1, 1)
                 u_target = self.velocity_field_prev(foot)
             # mean((u - u_target)^2) over the interior rows and the wall terms on the band rows,
             # one launch
@@ -220,12 +221,13 @@ class Fluid2DModel(BaseModel):
             # instead of a separate gradient jet + reverse jet for 2% of the points.  The
             # Laplacian rows of the band points get zero adjoint.
             xa, n, nb = self._merged(x)
-            with torch.no_grad():
-                div_u = divergence(self.velocity_field(x), x)
+            with torch.no_grad():  # div u = du/dx + dv/dy, read off the velocity's Jacobian
+                Ju = jacobian_only(self.velocity_field(x), x)
             lap_p, grad_p = laplace(self.pressure_field(xa), xa, return_grad=True)
-            # mean((lap p - div u)^2) over the interior rows == mean((div u - lap p)^2); both
-            # residuals in one launch
-            main, bc = sq_losses(mse_term(lap_p, div_u, count=n), wall_term(grad_p, nb, row0=n))
+            # mean((lap p - du/dx - dv/dy)^2) over the interior rows (= mean((div u - lap p)^2))
+            # and the wall terms, one launch; the diagonal of J is read in place (stride 4)
+            main, bc = sq_losses(mse_term(lap_p, Ju[:, 0, 0], Ju[:, 1, 1], alpha=1.0, beta=-1.0, gamma=-1.0, count=n),
+                                 wall_term(grad_p, nb, row0=n))
             return {'main': main, 'bc': bc}
         bc, join_bc = self._fork("insr_band_stream", self._pressure_wall_loss, x.shape[0])
         div_u, join_d = self._fork("insr_nograd_stream", self._velocity_divergence, x)

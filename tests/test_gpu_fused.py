@@ -4,8 +4,9 @@ A fused launch runs each job's blocks with the single-launch arithmetic, so ever
 output (value, Jacobian, saved streams) must equal the separate launches BIT FOR BIT,
 whatever tile count the combined batch selects; the oracle parity of the single launch
 (test_gpu_parity.py) then carries over.  Model level: the fluid phases with
-insr_fuse_forwards on and off give identical losses, gradients and Adam updates, in
-eager mode and under hipGraph replay (the oracle check of the fused default is
+insr_fuse_forwards on and off give identical losses and Adam updates equal up to the
+fp32 rounding of the gradients (one merged reverse jet vs two), in eager mode and under
+hipGraph replay (the oracle check of the fused default is
 test_gpu_phases.py::test_fluid_phases[False]).
 """
 
@@ -189,14 +190,11 @@ def test_fluid_phase_fused_equals_unfused(B, phase, graph):
                      model.pressure_field.flat_params().detach().clone(),
                      float(model.optimizer.state[0]), float(model.optimizer.state[1]))
     assert out[True][2:] == out[False][2:]
-    if phase != "_solve_pressure":
-        assert torch.equal(out[True][0], out[False][0]), phase
-        assert torch.equal(out[True][1], out[False][1]), phase
-        return
-    # the fused pressure phase evaluates the wall term on the Laplacian jet of the merged
-    # [interior; band] batch (other kernels, other summation order): equal up to fp32
-    # rounding of the gradients -- Adam moves an entry by at most 2 lr per step either way,
-    # and only entries with noise-floor gradients differ visibly
+    # the fused phases run ONE reverse jet over the merged [interior; band] batch (other
+    # block partition, other fixed summation order of the parameter gradient) where the
+    # unfused ones run two and add: equal up to fp32 rounding of the gradients -- Adam moves
+    # an entry by at most 2 lr per step either way, and only entries with noise-floor
+    # gradients differ visibly
     for a, b in zip(out[True][:2], out[False][:2]):
         d = (a - b).abs()
         assert float(d.max()) <= 4 * 2 * 1e-4 * 1.01, phase
