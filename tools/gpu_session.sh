@@ -31,7 +31,7 @@ for s in ${STEPS:-tests bench prof}; do
     pmc)   export TMPDIR=/tmp
            # HBM traffic of the jet kernels in the bench workload (eager: one counter sample per dispatch);
            # FETCH_SIZE and WRITE_SIZE need separate passes (TCC slots), SQ stall counters a third
-           PRX='jet_|reduce_partials'
+           PRX='jet_|dw_x6|reduce_'
            step pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$PRX" -d "$PWD/$OUT/pmc_fetch" -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-graph --no-cpu-baseline --no-roofline
            step pmc_write 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$PRX" -d "$PWD/$OUT/pmc_write" -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-graph --no-cpu-baseline --no-roofline
            step pmc_sq 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT --kernel-include-regex "$PRX" -d "$PWD/$OUT/pmc_sq" -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-graph --no-cpu-baseline --no-roofline ;;
