@@ -253,13 +253,13 @@ def roofline(loops, n_local, precision="fp32"):
         name = f"{k[0]}:{k[1]}:n{k[2]}:{k[4][0]}-{k[3]}x{k[4][2]}-{k[4][1]}"
         table[name] = round(table.get(name, 0.0) + v, 4)
     nq = PRECISION[precision][2]
-    kname, grid, x6 = kernel_identity(kind, mode, n, din, W, nq)
+    kname, grid, x6 = kernel_identity(kind, mode, n, din, dout, L, W, nq)
     traffic, tsrc = pmc_traffic(kname, grid)
     peak = FP32_MFMA_PEAK_TFLOPS if precision == "fp32" else BF16_MFMA_PEAK_TFLOPS
     out = {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
            "frac": round(achieved / peak, 4), "traffic": traffic,
            "traffic_unit": "bytes/launch (HBM: corrected FETCH_SIZE + WRITE_SIZE)", "traffic_source": tsrc,
-           "kernel": f"{kname} grid={grid} (n={n}, {din}->{dout} {L}x{W}, {mode} jet {kind})", "avg_ms": round(ms, 4),
+           "kernel": f"{kname}{'' if isinstance(grid, list) else f' grid={grid}'} (n={n}, {din}->{dout} {L}x{W}, {mode} jet {kind})", "avg_ms": round(ms, 4),
            "algorithmic_gflop_per_launch": round(flops / 1e9, 3), "per_step_ms_by_launch": table}
     if x6:
         # the kernel runs split-bf16 products: NP x v_mfma_f32_16x16x32_bf16 (16 cyc) per 16x16x32 fp32-equivalent
@@ -275,7 +275,7 @@ def roofline(loops, n_local, precision="fp32"):
     return out
 
 
-def kernel_identity(kind, mode, n, din, W, nq=3):
+def kernel_identity(kind, mode, n, din, dout, L, W, nq=3):
     """The rocprof name and grid (threads) of the jet kernel the library picks for this launch."""
     from base import _native as nat
     lib = nat.lib()
@@ -284,10 +284,14 @@ def kernel_identity(kind, mode, n, din, W, nq=3):
     S = {"value": 1, "grad": 1 + din, "lap": 2 + din}[mode]
     NT = W // 16
     lap = "true" if mode == "lap" else "false"
-    if kind == "bwd" and lib.insr_jet_bwd_is_wide(n, din, W, m) == 1:  # W = 256: two kernels + reductions
-        grid = ((n + 15) // 16) * 512
-        return (f"insr::jet_bwd_x6p<{nq}, {NT}, {S}, {lap}> + insr::dw_x6<{nq}, {NT}, {S}, {lap}> + reductions "
-                f"(wide path; time = all four)", grid, True)
+    if kind == "bwd" and lib.insr_jet_bwd_is_wide(n, din, W, m) == 1:  # two kernels + the dW sums
+        import ctypes
+        thr = (ctypes.c_long * 3)()
+        nat.check(lib.insr_jet_wide_launch_threads(n, din, dout, L, W, m, thr), "insr_jet_wide_launch_threads")
+        parts = [(f"insr::jet_bwd_x6p<{nq}, {NT}, {S}, {lap}>", thr[0]), (f"insr::dw_x6<{nq}, {NT}, {S}, {lap}>", thr[1]),
+                 ("insr::reduce_dw_kernel", thr[2])]
+        return " + ".join(f"{k}|grid={g}" for k, g in parts) + " (two-kernel backward; time = all three launches)", \
+            parts, True
     T = lib.insr_jet_split_tiles(n, din, W, m, 1 if kind == "bwd" else 0)
     nb = ((n + 15) // 16 + T - 1) // T
     return f"insr::jet_{kind}_x6<{nq}, {NT}, {S}, {lap}, {T}>", nb * 64 * min(NT, 8), True
@@ -302,10 +306,14 @@ def pmc_traffic(kname, grid):
         tab = json.load(open(path))
     except (OSError, ValueError):
         return None, None
-    e = tab.get(f"{kname}|grid={grid}")
-    if not e or "fetch_bytes" not in e or "write_bytes" not in e:
-        return None, None
-    return e["fetch_bytes"] + e["write_bytes"], tab.get("_source")
+    parts = grid if isinstance(grid, list) else [(kname, grid)]  # a multi-launch path: the sum of its launches
+    tot = 0
+    for name, g in parts:
+        e = tab.get(f"{name}|grid={g}")
+        if not e or "fetch_bytes" not in e or "write_bytes" not in e:
+            return None, None
+        tot += e["fetch_bytes"] + e["write_bytes"]
+    return tot, tab.get("_source")
 
 
 def cpu_baseline(config, seconds):

@@ -151,6 +151,10 @@ int insr_siren_jet_bwd_grad(const float* x, long n_points, int d_in, int d_out, 
 long insr_jet_bwd_work_bytes(long n_points, int d_in, int d_out, int num_hidden, int width, int mode);
 /* 1 if insr_siren_jet_bwd_grad takes the wide path for this batch / width / mode. */
 int insr_jet_bwd_is_wide(long n_points, int d_in, int width, int mode);
+/* Threads of the three launches of a two-kernel backward (propagation, dW partials, dW sums),
+ * as profilers report them; INSR_EINVAL when (n, shape, mode) does not take that path. */
+int insr_jet_wide_launch_threads(long n_points, int d_in, int d_out, int num_hidden, int width, int mode,
+                                 long* threads3);
 /* Smallest width (128 or 256) that takes the wide path; returns the old value.
  * Env INSR_WIDE_MIN_WIDTH.  Process-wide tuning/testing knob. */
 int insr_jet_set_wide_min_width(int width);

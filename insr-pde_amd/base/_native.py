@@ -62,6 +62,7 @@ SIGNATURES = {
     "insr_sq_loss_fwd": (_I, [_I, _P, _P, _P, _P, _L, _I, _F, _F, _F, _F, _F, _P, _P, _P]),
     "insr_sq_loss_group": (_I, [_P, _I, _P, _P]),
     "insr_axpy_clamp": (_I, [_P, _P, _F, _F, _F, _P, _L, _P]),
+    "insr_jet_wide_launch_threads": (_I, [_L, _I, _I, _I, _I, _I, _P]),
     "insr_sq_loss_bwd": (_I, [_I, _P, _P, _P, _P, _L, _I, _F, _F, _F, _F, _F, _P, _P, _P, _P, _P, _P]),
     "insr_jet_set_split_tiles": (None, [_I, _I, _I]),
     "insr_jet_set_precision": (None, [_I, _I]),

@@ -157,6 +157,10 @@ int split_tiles(int bwd, int NT, int S, long n, bool lap, int nq) {
   // than the LDS-capped T = 2 (16384 points: 66.6 vs 71.5 us, kbench s32)
   if (x6 && !bwd && S >= 4 && NT <= 8) T = 1;
   const long tiles = (n + 15) / 16;
+  // x6 forward of 2-3 stream jets at W = 128: two register-capped (<= 128 VGPR) 2-tile blocks
+  // per CU beat one 4-tile block and 1-tile blocks from 8192 points (kbench r2s21, fluid
+  // gradient jets: 16384 points 51.3 vs 55.5 us, 33092: 120 vs 135, 65536: 211 vs 215)
+  if (x6 && !bwd && (S == 2 || S == 3) && NT == 8 && !lap && tiles >= 512) return 2;
   while (T > 1 && (tiles + T - 1) / T < g_tiles[2]) T >>= 1;
   // occupancy-aware: a T whose last round of blocks (resident blocks per CU x CUs) is
   // nearly empty loses to a smaller T that packs the CUs, e.g. the x6 gradient forward at
@@ -569,6 +573,14 @@ long insr_jet_bwd_work_bytes(long n, int din, int dout, int L, int W, int mode) 
   const JetCall c(din, W, mode);
   if (c.wide(n)) return wide_work_floats(n, din, dout, L, W, c.S) * (long)sizeof(float);
   return insr_jet_partial_bytes(n, din, dout, L, W, mode);
+}
+
+int insr_jet_wide_launch_threads(long n, int din, int dout, int L, int W, int mode, long* threads3) {
+  if (!shape_ok(din, dout, L, W, mode) || n <= 0 || !threads3 || L < 1) return INSR_EINVAL;
+  const JetCall c(din, W, mode);
+  if (!c.wide(n)) return INSR_EINVAL;
+  wide_launch_threads(n, din, dout, L, W, c.S, threads3);
+  return 0;
 }
 
 int insr_jet_bwd_is_wide(long n, int din, int W, int mode) {

@@ -325,6 +325,7 @@ int dispatch_wide_bwd_q(int NT, int S, bool LAP, const float* x, int N, int din,
                         const float* act, const float* gy, const float* gdy, const float* glap, float* work,
                         float* grad, int accumulate, hipStream_t st);
 long wide_work_floats(long n, int din, int dout, int L, int W, int S);
+void wide_launch_threads(long n, int din, int dout, int L, int W, int S, long* out);
 
 // (S, LAP) combinations: value (1), grad d=1..3 (2..4), lap d=1,2 (3,4)
 #define INSR_DISPATCH(NTV, FN, ...)                \

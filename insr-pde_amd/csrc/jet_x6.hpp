@@ -344,8 +344,15 @@ __device__ __forceinline__ void fwd_x6_block(const float* __restrict__ x, int N,
   }
 }
 
+// register cap of the single-network forward: 4 waves / SIMD (two 512-thread blocks per CU)
+// where the body fits 128 VGPRs without spilling (unconstrained, T = 2 takes ~200)
+template <int NT, int S, int T>
+constexpr int x6_fwd_min_waves() {
+  return (NT == 8 && (S == 1 || (S == 3 && T <= 2))) ? 4 : 1;  // capped vs uncapped: kbench r2s21
+}
+
 template <int NQ, int NT, int S, bool LAP, int T>
-__global__ __launch_bounds__(X6Geo<NT>::THREADS) void jet_fwd_x6(
+__global__ __launch_bounds__(X6Geo<NT>::THREADS, (x6_fwd_min_waves<NT, S, T>())) void jet_fwd_x6(
     const float* __restrict__ x, int N, int din, int dout, int L, const float* __restrict__ prm,
     float* __restrict__ y, float* __restrict__ dy, float* __restrict__ lap, float* __restrict__ act, int nbal) {
   int tile0, cnt;

@@ -8,4 +8,7 @@ template int dispatch_wide_bwd_q<3>(int, int, bool, const float*, int, int, int,
 long wide_work_floats(long n, int din, int dout, int L, int W, int S) {
   return wide_work_floats_impl(n, din, dout, L, W, S);
 }
+void wide_launch_threads(long n, int din, int dout, int L, int W, int S, long* out) {
+  wide_launch_threads_impl(n, din, dout, L, W, S, out);
+}
 }  // namespace insr

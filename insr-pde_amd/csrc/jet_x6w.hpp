@@ -560,6 +560,18 @@ inline long wide_work_floats_impl(long n, int din, int dout, int L, int W, int S
   return adj + small + dw + (long)kSmallRS * small_count(din, dout, L, W);
 }
 
+// threads of the three launches of wide_bwd_t (L > 0): propagation, dW + rows level 1,
+// dW sums + rows level 2 (the launch shapes rocprof reports; bench.py's traffic lookup)
+inline void wide_launch_threads_impl(long n, int din, int dout, int L, int W, int S, long* out) {
+  const long tiles = (n + 15) / 16, Ps = small_count(din, dout, L, W);
+  const long rs = tiles < kSmallRS ? tiles : kSmallRS, rows_x = (Ps + 63) / 64;
+  const long KS = wide_ks(n, S, L), planes = (rows_x * rs + KS - 1) / KS;
+  const long wq = ((long)W * W / 4 + 63) / 64;
+  out[0] = tiles * 512;
+  out[1] = KS * (L + planes) * 512;
+  out[2] = (wq > rows_x ? wq : rows_x) * (L + 1) * 512;
+}
+
 template <int NQ, int NT, int S, bool LAP>
 int wide_bwd_t(const float* x, int N, int din, int dout, int L, const float* prm, const float* act, const float* gy,
                const float* gdy, const float* glap, float* work, float* grad, int accumulate, hipStream_t st) {

@@ -22,7 +22,7 @@ def load(path):
     agg = defaultdict(lambda: defaultdict(list))
     for f in glob.glob(os.path.join(path, "*counter_collection.csv")):
         for r in csv.DictReader(open(f)):
-            name = r["Kernel_Name"].split("(")[0].replace("void ", "").strip()
+            name = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "").strip()
             agg[f"{name}|grid={r['Grid_Size']}"][r["Counter_Name"]].append(float(r["Counter_Value"]))
     return agg
 
