@@ -139,8 +139,9 @@ def source_hash():
     return h.hexdigest()[:16]
 
 
-def load(path=None):
-    """Load (once) and return the CDLL with typed signatures."""
+def load(path=None, check_build=True):
+    """Load (once) and return the CDLL with typed signatures.  check_build=False only for
+    study tools that load an explicit alternative build (tools/kbench.py --lib)."""
     global _lib, _load_error
     if _lib is not None:
         return _lib
@@ -154,7 +155,7 @@ def load(path=None):
         fn.restype = res
         fn.argtypes = args
     want, have = source_hash(), lib.insr_build_id().decode()
-    if want is not None and want != have:
+    if check_build and want is not None and want != have:
         _load_error = (f"{p} was built from other sources (build id {have}, checked-out sources {want}): "
                        "rebuild with `python -c 'import __graft_entry__ as g; g.build()'`")
         raise NativeUnavailable(_load_error)

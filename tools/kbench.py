@@ -58,7 +58,7 @@ def main():
     args = ap.parse_args()
     import base
     from base import _native as nat
-    lib = nat.load(args.lib)
+    lib = nat.load(args.lib, check_build=args.lib is None)
     out = []
     for name in args.nets.split(","):
         din, dout, L, W = NETS[name]
