@@ -87,34 +87,30 @@ __device__ __forceinline__ float sum16(float v) {
 }
 
 // ---------------------------------------------------------------------------
-// sin / cos of w*z.  Straight-line Cody-Waite reduction by pi/2 (3-part constant,
-// valid for |x| <= 8192) + minimax polynomials on [-pi/4, pi/4]: ~1 ulp, ~20 VALU
-// ops for the pair, no branches, so the compiler can interleave it with MFMAs.
-// A wave with any |x| > 8192 takes the libm (ocml) path instead (uniform branch).
+// sin / cos of w*z.  Two-part Cody-Waite reduction by 2 pi (n = rint(x / 2 pi); 6.28125 n is
+// exact for |n| < 2^16) to r in [-pi, pi], then the hardware v_sin_f32 / v_cos_f32 on
+// r / 2 pi (|r / 2 pi| <= 1/2 revolution, where they are accurate): max abs error 3.8e-7 over
+// |x| <= 200 (tools/study/sin_acc.hip on MI355X; the fp32 rounding of the argument w z
+// itself is 7.6e-6 there).  5 + 1 (+1 for cos) VALU ops instead of a ~20-op polynomial pair;
+// no branches.  Valid for |x| <= 8192; a wave with any larger |x| takes the libm (ocml)
+// path instead (uniform branch).
 // ---------------------------------------------------------------------------
 constexpr float kFastArgMax = 8192.0f;
 
-__device__ __forceinline__ void sincos_fast(float x, float& s, float& c) {
-  const float n = rintf(x * 0.636619772367581343f);
-  float r = fmaf(-n, 1.5703125f, x);
-  r = fmaf(-n, 4.837512969970703125e-4f, r);
-  r = fmaf(-n, 7.54978995489188216e-8f, r);
-  const float z = r * r;
-  const float ps = fmaf(r * z, fmaf(z, fmaf(z, -1.9515295891e-4f, 8.3321608736e-3f), -1.6666654611e-1f), r);
-  const float pc = fmaf(z * z, fmaf(z, fmaf(z, 2.443315711809948e-5f, -1.388731625493765e-3f),
-                                    4.166664568298827e-2f), fmaf(-0.5f, z, 1.0f));
-  const int q = (int)n;
-  const float a = (q & 1) ? pc : ps;   // |sin|
-  const float b = (q & 1) ? ps : pc;   // |cos|
-  s = (q & 2) ? -a : a;
-  c = ((q + 1) & 2) ? -b : b;
+__device__ __forceinline__ float revs_reduced(float x) {
+  const float n = rintf(x * 0.15915494309189535f);
+  float r = fmaf(-n, 6.28125f, x);
+  r = fmaf(-n, 1.9353071795864769e-3f, r);
+  return r * 0.15915494309189535f;  // revolutions in [-1/2, 1/2]
 }
 
-__device__ __forceinline__ float sin_fast(float x) {
-  float s, c;
-  sincos_fast(x, s, c);
-  return s;
+__device__ __forceinline__ void sincos_fast(float x, float& s, float& c) {
+  const float t = revs_reduced(x);
+  s = __builtin_amdgcn_sinf(t);
+  c = __builtin_amdgcn_cosf(t);
 }
+
+__device__ __forceinline__ float sin_fast(float x) { return __builtin_amdgcn_sinf(revs_reduced(x)); }
 
 // true if any lane of the wave holds an argument outside the fast range
 __device__ __forceinline__ bool wave_any_big(float amax) {
