@@ -51,10 +51,17 @@ extern "C" {
  * (insr_jet_set_precision) applies.  The saved-activation layout does not depend on it. */
 #define INSR_MODE_PREC_SHIFT 4
 #define INSR_JET_PREC(p) (((p) + 1) << INSR_MODE_PREC_SHIFT)
+/* INSR_MODE_WSPLIT: the params buffer carries the pre-split weight planes of
+ * insr_siren_wsplit() after the parameters (at insr_siren_wsplit_offset() floats), up to date
+ * with the parameters.  Without it an entry point that runs split-bf16 kernels splits the
+ * weights itself, into a per-stream scratch copy (one copy + one launch per call). */
+#define INSR_MODE_WSPLIT (1 << 8)
 
 #define INSR_EINVAL   (-1) /* unsupported shape / mode / null pointer */
 #define INSR_EWIDTH   (-2) /* hidden width not in the compiled set      */
 #define INSR_ENOCOMM  (-3) /* RCCL (librccl.so.1) could not be loaded   */
+#define INSR_ECAPTURE (-4) /* a per-stream scratch would be allocated during stream capture:
+                              run the call once outside the capture, or pass INSR_MODE_WSPLIT */
 #define INSR_ECOMM_BASE 1000 /* + ncclResult_t of a failed RCCL call     */
 
 /* Library version (major*10000 + minor*100 + patch). */
@@ -66,6 +73,17 @@ const char* insr_build_id(void);
 
 /* Number of fp32 parameters of an SIREN(d_in -> W x (L+1) -> d_out). */
 long insr_siren_param_count(int d_in, int d_out, int num_hidden, int width);
+
+/* Pre-split weight planes (split-bf16 kernels).  Every hidden weight W_j is stored split in
+ * three bf16 terms (jet_x6.hpp) in the matrix-core fragment order of the forward (W_j rows)
+ * and of the backward (W_j^T rows): 3 L W^2 floats in all, at insr_siren_wsplit_offset()
+ * floats (param_count rounded up to 16 B) after the start of the params buffer.
+ * insr_siren_wsplit() writes them from the parameters in place (one launch); the kernels then
+ * read fragments instead of re-splitting W in every block.  Replaces nothing in the
+ * reference (its fp32 addmm reads W directly, torch/nn/modules/linear.py). */
+long insr_siren_wsplit_offset(int d_in, int d_out, int num_hidden, int width);
+long insr_siren_wsplit_floats(int num_hidden, int width);
+int insr_siren_wsplit(float* params, int d_in, int d_out, int num_hidden, int width, void* stream);
 
 /* 1 if (d_in, d_out, width, mode) is served by a compiled kernel, else 0. */
 int insr_siren_supported(int d_in, int d_out, int num_hidden, int width, int mode);

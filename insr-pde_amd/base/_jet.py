@@ -77,7 +77,8 @@ class _SirenJet(torch.autograd.Function):
         lib = nat.lib()
         n, din = x2.shape
         L, W, dout = mlp.num_hidden_layers, mlp.kernel_width, mlp.out_features
-        cmode = mlp.call_mode(mode)  # + the network's precision bits
+        cmode = mlp.call_mode(mode)  # + the network's precision bits and INSR_MODE_WSPLIT
+        mlp.ensure_wsplit()          # the pre-split weight planes follow the parameters
         flat = mlp.flat_params()
         dev = x2.device
         y = torch.empty(n, dout, device=dev, dtype=torch.float32)
@@ -120,6 +121,7 @@ class _SirenJet(torch.autograd.Function):
         n, din = x2.shape
         L, W, dout = mlp.num_hidden_layers, mlp.kernel_width, mlp.out_features
         cmode = mlp.call_mode(mode)
+        mlp.ensure_wsplit()
         lib = nat.lib()
         gflat, accumulate = mlp.grad_for_backward()
         c = lambda t: None if t is None else (t if t.is_contiguous() else t.contiguous())  # noqa: E731

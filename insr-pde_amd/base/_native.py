@@ -15,6 +15,7 @@ LIB_PATH = os.environ.get("INSR_HIP_LIB", os.path.join(os.path.dirname(_HERE), "
 
 MODE_VALUE, MODE_GRAD, MODE_LAP = 0, 1, 2
 MODE_MASK, MODE_PREC_SHIFT = 0xF, 4
+MODE_WSPLIT = 1 << 8  # the params buffer carries up-to-date pre-split weight planes
 PREC_F32, PREC_BF16X6, PREC_BF16X3, PREC_BF16 = 0, 1, 2, 3
 PRECISIONS = {"fp32": PREC_F32, "bf16x6": PREC_BF16X6, "bf16x3": PREC_BF16X3, "bf16": PREC_BF16}
 
@@ -62,6 +63,9 @@ SIGNATURES = {
     "insr_sq_loss_fwd": (_I, [_I, _P, _P, _P, _P, _L, _I, _F, _F, _F, _F, _F, _P, _P, _P]),
     "insr_sq_loss_group": (_I, [_P, _I, _P, _P]),
     "insr_axpy_clamp": (_I, [_P, _P, _F, _F, _F, _P, _L, _P]),
+    "insr_siren_wsplit_offset": (_L, [_I, _I, _I, _I]),
+    "insr_siren_wsplit_floats": (_L, [_I, _I]),
+    "insr_siren_wsplit": (_I, [_P, _I, _I, _I, _I, _P]),
     "insr_jet_wide_launch_threads": (_I, [_L, _I, _I, _I, _I, _I, _P]),
     "insr_sq_loss_bwd": (_I, [_I, _P, _P, _P, _P, _L, _I, _F, _F, _F, _F, _F, _P, _P, _P, _P, _P, _P]),
     "insr_jet_set_split_tiles": (None, [_I, _I, _I]),
@@ -151,7 +155,11 @@ def load(path=None, check_build=True):
         raise NativeUnavailable(_load_error)
     lib = ctypes.CDLL(p)
     for name, (res, args) in SIGNATURES.items():
-        fn = getattr(lib, name)
+        fn = getattr(lib, name, None)
+        if fn is None:
+            if check_build:
+                raise NativeUnavailable(f"{p} does not export {name}: rebuild")
+            continue  # an older study build (tools/kbench.py --lib): its missing entries stay unused
         fn.restype = res
         fn.argtypes = args
     want, have = source_hash(), lib.insr_build_id().decode()

@@ -104,7 +104,9 @@ class MLP(nn.Module):
         self.first_layer_init = None
         self._flat = None
         self._flat_grad = None
+        self._wsplit_stamp = None
         self._repack()
+        self.register_load_state_dict_post_hook(lambda m, keys: m.refresh_wsplit())
 
     # ---- matrix-core precision ------------------------------------------------
     def set_precision(self, precision):
@@ -116,9 +118,43 @@ class MLP(nn.Module):
         self.precision = precision
 
     def call_mode(self, mode):
-        """The jet `mode` argument of this network's library calls (precision bits added)."""
-        from ._native import PRECISIONS, jet_prec
+        """The jet `mode` argument of this network's library calls (precision bits added; the
+        flat buffer carries the pre-split weight planes: INSR_MODE_WSPLIT)."""
+        from ._native import MODE_WSPLIT, PRECISIONS, jet_prec
+        mode |= MODE_WSPLIT
         return mode if self.precision is None else mode | jet_prec(PRECISIONS[self.precision])
+
+    # ---- pre-split weight planes (include/insr_siren.h insr_siren_wsplit) -----------
+    # The flat storage is [parameters | pad to 16 B | planes]: every hidden weight split in three
+    # bf16 terms in the matrix-core fragment order (forward W rows, backward W^T rows), so the
+    # split-bf16 kernels read fragments instead of re-splitting W in every block.  The planes
+    # are derived data: rewritten after every parameter change -- by FusedAdam.step (captured
+    # with it in a hipGraph), after load_state_dict, and before a jet whenever the parameters'
+    # version counters moved (any torch in-place write).
+    def wsplit_offset(self):
+        return (self.param_count + 3) & ~3
+
+    def wsplit_floats(self):
+        return 3 * self.num_hidden_layers * self.kernel_width ** 2
+
+    def _param_versions(self):
+        return (self._flat.data_ptr(), self._flat._version) + tuple(p._version for p in self.parameters())
+
+    def refresh_wsplit(self, stream=None):
+        """Rewrite the planes from the parameters now (one launch on `stream` / the current one)."""
+        if self._flat is None or not self._flat.is_cuda or self.num_hidden_layers == 0:
+            return
+        from . import _native as nat
+        W, L = self.kernel_width, self.num_hidden_layers
+        st = stream.cuda_stream if stream is not None else nat.stream_of(self._flat.device)
+        nat.check(nat.lib().insr_siren_wsplit(nat.ptr(self._flat), self.in_features, self.out_features, L, W, st),
+                  "insr_siren_wsplit")
+        self._wsplit_stamp = self._param_versions()
+
+    def ensure_wsplit(self):
+        """Before a jet: refresh the planes if the parameters changed behind our back."""
+        if self._wsplit_stamp != self._param_versions():
+            self.refresh_wsplit()
 
     # ---- flat storage ------------------------------------------------------
     @property
@@ -158,7 +194,8 @@ class MLP(nn.Module):
             return
         dev, dt = params[0].device, params[0].dtype
         lay = self._layout()
-        flat = torch.zeros(self.param_count, device=dev, dtype=dt)
+        store = torch.zeros(self.wsplit_offset() + self.wsplit_floats(), device=dev, dtype=dt)
+        flat = store[:self.param_count]  # parameters; the pre-split weight planes follow
         grads_present = any(p.grad is not None for p in params)
         gflat = torch.zeros_like(flat) if grads_present else None
         for p, e in zip(params, lay):
@@ -172,6 +209,7 @@ class MLP(nn.Module):
                 p.grad = gv
         self._flat = flat
         self._flat_grad = gflat
+        self._wsplit_stamp = None
 
     def _apply(self, fn, *args, **kwargs):
         out = super()._apply(fn, *args, **kwargs)

@@ -102,11 +102,13 @@ class FusedAdam:
         lib = nat.lib()
         self._advance_pending()
         bufs = []
+        stepped = []
         cur = torch.cuda.current_stream(self.device)
         for mlp, m, v in self._nets:
             if mlp.grad_touched():  # torch skips params whose .grad is None
                 mlp.grad_read_sync(cur)  # a backward may have written .grad on a side stream
                 bufs.append((mlp.flat_params(), mlp.flat_grad_buffer(), m, v))
+                stepped.append(mlp)
         for p, m, v in self._loose:
             if p.grad is not None:
                 bufs.append((p.data, p.grad if p.grad.is_contiguous() else p.grad.contiguous(), m, v))
@@ -119,6 +121,9 @@ class FusedAdam:
             sizes = (ctypes.c_long * k)(*[c[0].numel() for c in chunk])
             nat.check(lib.insr_adam_step_multi(k, arr(0), arr(1), arr(2), arr(3), sizes, nat.ptr(self.state), b1, b2,
                                                self.eps, 1, st), "insr_adam_step_multi")
+        for mlp in stepped:  # the updated weights' pre-split planes (part of a captured step)
+            if hasattr(mlp, "refresh_wsplit"):
+                mlp.refresh_wsplit()
         self._pending_advance = True
 
 

@@ -2,6 +2,8 @@
 // kernel-variant selection, the partial reducer and the device-resident optimiser.
 #include <cstdlib>
 #include <map>
+#include <mutex>
+#include <tuple>
 
 #include "jet_common.hpp"
 
@@ -86,7 +88,11 @@ bool use_wide(long n, int S, int NT, bool lap, int nq) {
   if (NT < 8 || nq == 0) return false;
   if (16 * NT >= g_wide_min) return true;
   if (NT != 8 || g_wide_min > 256) return false;
-  return lap ? n >= 8192 : (S >= 3 && n >= 32768);
+  // with the pre-split weight planes (kbench r2s31, profiles/r02/wide_vs_fused_wsplit.jsonl):
+  // Laplacian and 2-d gradient jets from 8,192 points (gradient 16,708: 143 vs 175 us fused),
+  // value jets only from ~48K points (16,708: 75 vs 67 us fused; 65,536: 228 vs 241)
+  if (lap || S >= 3) return n >= 8192;
+  return S == 1 && n >= 49152;
 }
 
 static int cu_count() {
@@ -157,10 +163,14 @@ int split_tiles(int bwd, int NT, int S, long n, bool lap, int nq) {
   // than the LDS-capped T = 2 (16384 points: 66.6 vs 71.5 us, kbench s32)
   if (x6 && !bwd && S >= 4 && NT <= 8) T = 1;
   const long tiles = (n + 15) / 16;
-  // x6 forward of 2-3 stream jets at W = 128: two register-capped (<= 128 VGPR) 2-tile blocks
-  // per CU beat one 4-tile block and 1-tile blocks from 8192 points (kbench r2s21, fluid
-  // gradient jets: 16384 points 51.3 vs 55.5 us, 33092: 120 vs 135, 65536: 211 vs 215)
-  if (x6 && !bwd && (S == 2 || S == 3) && NT == 8 && !lap && tiles >= 512) return 2;
+  // x6 forward at W = 128 with the pre-split weight planes (62-90 VGPRs: 2-4 blocks per CU),
+  // measured per tile count (kbench r2s29, profiles/r02/tiles_after_wsplit.jsonl): value jets
+  // T = 2 up to ~40K points (16,708: 26.4 vs 29.8 us at T = 4; 33,092: 41.5 vs 47.2), T = 4
+  // above (65,536: 60.2 vs 64.9); 2-4 stream jets T = 1 (16,708: 48.2 vs 58.3 at T = 2)
+  if (x6 && !bwd && NT == 8) {
+    if (S > 1) return 1;
+    return tiles <= 512 ? 1 : (tiles <= 2600 ? 2 : 4);
+  }
   while (T > 1 && (tiles + T - 1) / T < g_tiles[2]) T >>= 1;
   // occupancy-aware: a T whose last round of blocks (resident blocks per CU x CUs) is
   // nearly empty loses to a smaller T that packs the CUs, e.g. the x6 gradient forward at
@@ -406,7 +416,7 @@ __global__ void adam_multi_kernel(AdamList L, const float* __restrict__ st, floa
 bool shape_ok(int din, int dout, int L, int width, int mode) {
   if (din < 1 || din > 3 || dout < 1 || dout > 3 || L < 0 || L > 64) return false;
   if (nt_for(width) < 0) return false;
-  if (mode & ~(INSR_MODE_MASK | (0xF << INSR_MODE_PREC_SHIFT))) return false;
+  if (mode & ~(INSR_MODE_MASK | (0xF << INSR_MODE_PREC_SHIFT) | INSR_MODE_WSPLIT)) return false;
   const int po = (mode >> INSR_MODE_PREC_SHIFT) & 0xF;
   if (po && !prec_ok(po - 1)) return false;
   const int jm = mode & INSR_MODE_MASK;
@@ -448,6 +458,64 @@ long insr_jet_partial_stride(int din, int dout, int L, int W) {
   return (insr_siren_param_count(din, dout, L, W) + 3) & ~3L;  // 16-B aligned rows
 }
 
+// ---- pre-split weight planes --------------------------------------------------------------
+long insr_siren_wsplit_offset(int din, int dout, int L, int W) {
+  if (!shape_ok(din, dout, L, W, 0)) return INSR_EINVAL;
+  return wsplit_offset(din, dout, L, W);
+}
+long insr_siren_wsplit_floats(int L, int W) {
+  if (L < 0 || nt_for(W) < 0) return INSR_EINVAL;
+  return 3L * L * W * W;
+}
+int insr_siren_wsplit(float* params, int din, int dout, int L, int W, void* stream) {
+  if (!params || !shape_ok(din, dout, L, W, 0)) return INSR_EINVAL;
+  return wsplit_launch(params, din, dout, L, W, params + wsplit_offset(din, dout, L, W), (hipStream_t)stream);
+}
+
+// A call without INSR_MODE_WSPLIT whose kernels read weight planes: a per-(device, stream,
+// slot) scratch [copy of the parameters | planes] is filled (one copy + one split launch) and
+// used as the params buffer.  Allocation happens outside stream capture only.
+namespace {
+struct Scratch {
+  void* ptr = nullptr;
+  size_t bytes = 0;
+};
+std::mutex g_scratch_mu;
+std::map<std::tuple<int, hipStream_t, int>, Scratch> g_scratch;
+}  // namespace
+
+static const float* with_planes(const float* params, int din, int dout, int L, int W, int mode, hipStream_t st,
+                                int slot, int* rc) {
+  *rc = 0;
+  if ((mode & INSR_MODE_WSPLIT) || L < 1) return params;
+  const long pc = insr_siren_param_count(din, dout, L, W);
+  const size_t bytes = (size_t)(wsplit_offset(din, dout, L, W) + 3L * L * W * W) * sizeof(float);
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  std::lock_guard<std::mutex> lk(g_scratch_mu);
+  Scratch& e = g_scratch[std::make_tuple(dev, st, slot)];
+  if (e.bytes < bytes) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    (void)hipStreamIsCapturing(st, &cs);
+    if (cs != hipStreamCaptureStatusNone) {
+      *rc = INSR_ECAPTURE;
+      return nullptr;
+    }
+    if (e.ptr) (void)hipFree(e.ptr);  // synchronous: no launch still reads the old copy
+    e.ptr = nullptr;
+    e.bytes = 0;
+    if (hipMalloc(&e.ptr, bytes) != hipSuccess) {
+      *rc = (int)hipErrorOutOfMemory;
+      return nullptr;
+    }
+    e.bytes = bytes;
+  }
+  float* buf = static_cast<float*>(e.ptr);
+  if ((*rc = (int)hipMemcpyAsync(buf, params, (size_t)pc * sizeof(float), hipMemcpyDeviceToDevice, st))) return nullptr;
+  if ((*rc = wsplit_launch(buf, din, dout, L, W, buf + wsplit_offset(din, dout, L, W), st))) return nullptr;
+  return buf;
+}
+
 int insr_siren_supported(int din, int dout, int L, int W, int mode) { return shape_ok(din, dout, L, W, mode) ? 1 : 0; }
 
 long insr_jet_act_bytes(long n, int din, int L, int W, int mode) {
@@ -472,6 +540,8 @@ int insr_siren_jet_fwd(const float* x, long n, int din, int dout, int L, int W, 
   if (c.jm != INSR_MODE_VALUE && !dy) return INSR_EINVAL;
   if (c.lap && !lap) return INSR_EINVAL;
   const LaunchShape sh = launch_shape(0, c.nqf, c.NT, c.S, c.lap, n);
+  int rc = 0;
+  if (c.nqf > 0 && !(params = with_planes(params, din, dout, L, W, mode, (hipStream_t)stream, 0, &rc))) return rc;
   return fwd_q(c.nqf, c.NT, c.S, c.lap, sh.T, x, (int)n, din, dout, L, params, y, dy, lap, act, sh.nbal,
                (hipStream_t)stream);
 }
@@ -505,9 +575,7 @@ int insr_siren_jet_fwd_multi(const InsrJetJob* jobs, int njobs, int din, int dou
   if (live > 1 && !c.lap && NT >= 4 && !grad128_big && c.nqf > 0) {
     // tiles per block from the combined batch; a job whose own batch would take fewer
     // (a boundary band) runs 1-tile blocks, placed first in the grid
-    // (W = 128 gradient jets: T = 2 -- the fused kernel is held to 128 VGPRs, two blocks per CU;
-    // measured 50.9 vs 51.9 us for T = 4 at 16384 points, profiles/r01/fwd_minwaves_study)
-    int T = (NT == 8 && S == 3) ? 2 : split_tiles(0, NT, S, total, false, c.nqf);
+    int T = split_tiles(0, NT, S, total, false, c.nqf);
     InsrJetJob pk[INSR_MAX_FWD_JOBS];
     int small[INSR_MAX_FWD_JOBS], nbal[INSR_MAX_FWD_JOBS];
     int m = 0;
@@ -515,7 +583,11 @@ int insr_siren_jet_fwd_multi(const InsrJetJob* jobs, int njobs, int din, int dou
       if (jobs[k].n > 0) {
         small[m] = split_tiles(0, NT, S, jobs[k].n, false, c.nqf) < T ? 1 : 0;
         nbal[m] = 0;
-        pk[m++] = jobs[k];
+        pk[m] = jobs[k];
+        int rc = 0;
+        const int dk = jobs[k].d_out > 0 ? jobs[k].d_out : dout;
+        if (!(pk[m].params = with_planes(jobs[k].params, din, dk, L, W, mode, (hipStream_t)stream, k, &rc))) return rc;
+        ++m;
       }
     // value jets at T = 4 (two resident blocks per CU): when the jobs' blocks overflow a whole
     // round by a little (u_prev at 16384 points + u at 16384 + 324 band points: 518 blocks for
@@ -558,6 +630,8 @@ int insr_siren_jet_bwd(const float* x, long n, int din, int dout, int L, int W, 
   // width 256: the fused split-bf16 backward does not exist -- exact fp32 serves this entry
   const int nq = c.NT > 8 ? 0 : c.nqb;
   const LaunchShape sh = launch_shape(1, nq, c.NT, c.S, c.lap, n);
+  int rc = 0;
+  if (nq > 0 && !(params = with_planes(params, din, dout, L, W, mode, (hipStream_t)stream, 0, &rc))) return rc;
   return bwd_q(nq, c.NT, c.S, c.lap, sh.T, x, (int)n, din, dout, L, params, act, gy, gdy, glap, partial, P, sh.nbal,
                (hipStream_t)stream);
 }
@@ -598,6 +672,8 @@ int insr_siren_jet_bwd_grad(const float* x, long n, int din, int dout, int L, in
   const JetCall c(din, W, mode);
   if (c.wide(n)) {
     hipStream_t st = (hipStream_t)stream;
+    int rc = 0;
+    if (!(params = with_planes(params, din, dout, L, W, mode, st, 0, &rc))) return rc;
     switch (c.nqb) {
       case 3:
         return dispatch_wide_bwd_q<3>(c.NT, c.S, c.lap, x, (int)n, din, dout, L, params, act, gy, gdy, glap, work, grad,

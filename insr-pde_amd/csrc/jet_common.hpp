@@ -59,6 +59,15 @@ __host__ __device__ inline long out_off(int din, int W, int L) {
   return (long)W * din + W + (long)L * ((long)W * W + W);
 }
 
+// pre-split weight planes after the parameters (INSR_MODE_WSPLIT): orientation o (0: W_j rows,
+// the forward's A operand; 1: W_j^T rows, the backward's), layer j - 1, fragment rt (W / 16)
+// x kc (W / 32), term q (3), lane: 16 B = 8 bf16 of one term -- 3 L W^2 / 8 u32x4 per
+// orientation, 3 L W^2 floats in all
+__host__ __device__ inline long wsplit_offset(int din, int dout, int L, int W) {
+  return (out_off(din, W, L) + (long)dout * W + dout + 3) & ~3L;
+}
+__host__ __device__ inline long wsplit_orient_vecs(int L, int W) { return (long)L * W * W * 3 / 8; }
+
 // wave-tile base of layer `layer` in the saved-activation buffer
 __device__ __forceinline__ float* act_base(float* act, int layer, int ntiles, int tile, int S, int NT) {
   return act + ((long)layer * ntiles + tile) * (long)(S * NT) * 256;
@@ -321,6 +330,9 @@ int dispatch_wide_bwd_q(int NT, int S, bool LAP, const float* x, int N, int din,
                         const float* act, const float* gy, const float* gdy, const float* glap, float* work,
                         float* grad, int accumulate, hipStream_t st);
 long wide_work_floats(long n, int din, int dout, int L, int W, int S);
+// the pre-split weight planes of (prm, shape) written to `planes` (wsplit_offset floats after prm
+// in a params buffer of INSR_MODE_WSPLIT), one launch
+int wsplit_launch(const float* prm, int din, int dout, int L, int W, float* planes, hipStream_t st);
 void wide_launch_threads(long n, int din, int dout, int L, int W, int S, long* out);
 
 // (S, LAP) combinations: value (1), grad d=1..3 (2..4), lap d=1,2 (3,4)

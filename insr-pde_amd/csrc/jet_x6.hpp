@@ -154,14 +154,21 @@ constexpr size_t fwd_x6_lds_bytes() {
   return planes > red ? planes : red;
 }
 
-// hidden-layer A fragments of this wave's row tile rt: W[16 rt + c][32 kc + 8 g + j]
+// fragment (row tile rt, K chunk kc) of hidden layer j in orientation o (0: W_j rows, the
+// forward's A operand; 1: W_j^T rows, the backward's) from the pre-split planes that follow
+// the parameters (INSR_MODE_WSPLIT; capi.hip guarantees them): NQ of the 3 terms, one b128 each
+__device__ __forceinline__ const u32x4* wsp_base(const float* prm, int din, int dout, int L, int W) {
+  return reinterpret_cast<const u32x4*>(prm + wsplit_offset(din, dout, L, W));
+}
 template <int NQ, int NT>
-__device__ __forceinline__ FragQ<NQ> load_w_frag(const float* __restrict__ Wj, int rt, int kc, int g, int c) {
-  constexpr int W = 16 * NT;
-  const float* p = Wj + (16 * rt + c) * W + 32 * kc + 8 * g;
-  const floatx4 v0 = *reinterpret_cast<const floatx4*>(p);
-  const floatx4 v1 = *reinterpret_cast<const floatx4*>(p + 4);
-  return split_frag<NQ>(v0, v1);
+__device__ __forceinline__ FragQ<NQ> wsp_frag(const u32x4* __restrict__ wsp, int L, int o, int j, int rt, int kc,
+                                              int lane) {
+  constexpr int W = 16 * NT, KC = NT / 2;
+  const u32x4* p = wsp + o * wsplit_orient_vecs(L, W) + ((((long)(j - 1) * NT + rt) * KC + kc) * 3) * 64 + lane;
+  FragQ<NQ> f;
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) f.q[q] = p[q * 64];
+  return f;
 }
 
 // Balanced tiles per block: with nbal > 0 the tiles of a batch are split over nbal blocks as
@@ -198,6 +205,7 @@ __device__ __forceinline__ void fwd_x6_block(const float* __restrict__ x, int N,
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
   const int ntiles = ((N + 63) / 64) * 4;
   const int rt0 = wave * RPW;
+  const u32x4* wsp = wsp_base(prm, din, dout, L, W);
 
   float xv[T][3];
 #pragma unroll
@@ -239,7 +247,7 @@ __device__ __forceinline__ void fwd_x6_block(const float* __restrict__ x, int N,
         const int rt = rt0 + i;
         FragQ<NQ> wf[KC];
 #pragma unroll
-        for (int kc = 0; kc < KC; ++kc) wf[kc] = load_w_frag<NQ, NT>(Wj, rt, kc, g, c);
+        for (int kc = 0; kc < KC; ++kc) wf[kc] = wsp_frag<NQ, NT>(wsp, L, 0, j, rt, kc, lane);
         const floatx4 bias = *reinterpret_cast<const floatx4*>(bj + 16 * rt + 4 * g);
 #pragma unroll
         for (int t = 0; t < T; ++t) {
@@ -411,7 +419,9 @@ __global__ __launch_bounds__(X6Geo<NT>::THREADS, (x6_multi_min_waves<NT, S>())) 
 template <int NQ, int NT, int S, bool LAP, int T>
 int launch_fwd_x6_multi_t(const InsrJetJob* jobs, const int* small, const int* nbal, int njobs, int din, int dout,
                           int L, hipStream_t st) {
-  constexpr int TB = 1;
+  // 1-tile blocks for small jobs only beside T >= 4 blocks: with T <= 2 the second body would
+  // raise the kernel's registers (T = 2 value: 84 vs 62 VGPRs, two blocks per CU fewer)
+  constexpr int TB = T <= 2 ? T : 1;
   constexpr size_t lds = fwd_x6_lds_bytes<NQ, NT, S, T>();
   if constexpr (lds > kLdsMax) {
     return INSR_EINVAL;
@@ -720,14 +730,7 @@ __global__ __launch_bounds__(X6Geo<NT>::THREADS) void jet_bwd_x6(
     }
   };
   load_zk(L);
-  // W^T rows m = 16 rt + c of layer matrix Wsrc, k = n = 32 kc + 8 g + jj (strided L2 loads)
-  auto load_wt = [&](const float* Wsrc, int i, int kc, floatx4(&dst)[2]) {
-#pragma unroll
-    for (int jj = 0; jj < 4; ++jj) {
-      dst[0][jj] = Wsrc[(32 * kc + 8 * g + jj) * W + 16 * (rt0 + i) + c];
-      dst[1][jj] = Wsrc[(32 * kc + 8 * g + 4 + jj) * W + 16 * (rt0 + i) + c];
-    }
-  };
+  const u32x4* wsp = wsp_base(prm, din, dout, L, W);
   for (int j = L; j >= 0; --j) {
     INSR_STAMP(L - j, 0);
 #pragma unroll
@@ -782,19 +785,16 @@ __global__ __launch_bounds__(X6Geo<NT>::THREADS) void jet_bwd_x6(
       break;
     }
     INSR_STAMP(L - j, 1);
-    const float* Wj = prm + hidden_off(din, W, j);
-    // A operand of the propagation: W^T rows m = 16 rt + c, k = n = 32 kc + 8 g + jj
-    // (strided L2 loads issued here).  One group: split once; several groups: the raw
-    // values stay live and each group splits them again (fewer registers across groups)
-    floatx4 wraw[RPW][KC][2];
+    // A operand of the propagation: W^T rows m = 16 rt + c, k = n = 32 kc + 8 g + jj, from the
+    // pre-split planes (issued here, in flight during the dW phase).  Several stream groups:
+    // re-read per group (L2 hits) instead of holding the fragments across groups
     FragQ<NQ> wt[RPW][KC];
+    if constexpr (NG == 1) {
 #pragma unroll
-    for (int i = 0; i < RPW; ++i)
+      for (int i = 0; i < RPW; ++i)
 #pragma unroll
-      for (int kc = 0; kc < KC; ++kc) {
-        load_wt(Wj, i, kc, wraw[i][kc]);
-        if constexpr (NG == 1) wt[i][kc] = split_frag<NQ>(wraw[i][kc][0], wraw[i][kc][1]);
-      }
+        for (int kc = 0; kc < KC; ++kc) wt[i][kc] = wsp_frag<NQ, NT>(wsp, L, 1, j, rt0 + i, kc, lane);
+    }
     floatx4 snp[T][RPW], csp[T][RPW];
     load_sc(j - 1, snp, csp);
     load_zk(j - 1);
@@ -880,7 +880,7 @@ __global__ __launch_bounds__(X6Geo<NT>::THREADS) void jet_bwd_x6(
 #pragma unroll
         for (int i = 0; i < RPW; ++i)
 #pragma unroll
-          for (int kc = 0; kc < KC; ++kc) wt[i][kc] = split_frag<NQ>(wraw[i][kc][0], wraw[i][kc][1]);
+          for (int kc = 0; kc < KC; ++kc) wt[i][kc] = wsp_frag<NQ, NT>(wsp, L, 1, j, rt0 + i, kc, lane);
       }
       // propagation of this group's streams (an unused slot of a balanced block keeps zero
       // adjoints: its bias / first-layer sums must add nothing)

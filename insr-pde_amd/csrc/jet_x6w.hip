@@ -8,6 +8,21 @@ template int dispatch_wide_bwd_q<3>(int, int, bool, const float*, int, int, int,
 long wide_work_floats(long n, int din, int dout, int L, int W, int S) {
   return wide_work_floats_impl(n, din, dout, L, W, S);
 }
+int wsplit_launch(const float* prm, int din, int dout, int L, int W, float* planes, hipStream_t st) {
+  if (L < 1) return 0;
+  const long threads = 2L * L * (W / 16) * (W / 32) * 64;
+  const dim3 grid((unsigned)((threads + 255) / 256));
+  u32x4* out = reinterpret_cast<u32x4*>(planes);
+  switch (W) {
+    case 32: hipLaunchKernelGGL((wsplit_kernel<2>), grid, dim3(256), 0, st, prm, din, L, out); break;
+    case 64: hipLaunchKernelGGL((wsplit_kernel<4>), grid, dim3(256), 0, st, prm, din, L, out); break;
+    case 128: hipLaunchKernelGGL((wsplit_kernel<8>), grid, dim3(256), 0, st, prm, din, L, out); break;
+    case 256: hipLaunchKernelGGL((wsplit_kernel<16>), grid, dim3(256), 0, st, prm, din, L, out); break;
+    default: return INSR_EWIDTH;
+  }
+  (void)dout;
+  return (int)hipGetLastError();
+}
 void wide_launch_threads(long n, int din, int dout, int L, int W, int S, long* out) {
   wide_launch_threads_impl(n, din, dout, L, W, S, out);
 }

@@ -35,34 +35,38 @@ __host__ __device__ inline long small_count(int din, int dout, int L, int W) {
 }
 
 // ---------------------------------------------------------------------------------------
-// kernel 0: the A operands of the propagation, W_j^T split ONCE per backward call (instead of
-// by every tile's block: 1045 blocks x L layers at 16,708 points) into NQ bf16 planes in the
-// fragment order jet_bwd_x6p reads: frag (layer j, row tile rt, K chunk kc), plane q, lane
-// (g, c) = W_j^T[16 rt + c][32 kc + 8 g + 0..7] = W_j[32 kc + 8 g + 0..7][16 rt + c], 16 B.
+// the pre-split weight planes (INSR_MODE_WSPLIT, jet_common.hpp wsplit_offset): one thread per
+// (orientation o, layer j - 1, fragment (rt, kc), lane (g, c)): the 8 weights
+//   o = 0: W_j[16 rt + c][32 kc + 8 g + 0..7]   (forward A operand, contiguous)
+//   o = 1: W_j[32 kc + 8 g + 0..7][16 rt + c]   (backward A operand = W_j^T rows)
+// split in three bf16 terms (split_frag<3>); kernels of NQ < 3 read the first NQ terms
 // ---------------------------------------------------------------------------------------
 template <int NT>
-__host__ __device__ constexpr long wt_frags() { return (long)NT * (NT / 2); }  // frags per layer
-
-template <int NQ, int NT>
-__global__ __launch_bounds__(256) void split_wt_kernel(const float* __restrict__ prm, int din, int L,
-                                                       u32x4* __restrict__ out) {
-  constexpr int W = 16 * NT, KC = NT / 2;
-  const long gid = (long)blockIdx.x * 256 + threadIdx.x;  // (layer - 1, frag, lane)
+__global__ __launch_bounds__(256) void wsplit_kernel(const float* __restrict__ prm, int din, int L,
+                                                     u32x4* __restrict__ out) {
+  constexpr int W = 16 * NT, KC = NT / 2, NF = NT * KC;
+  const long gid = (long)blockIdx.x * 256 + threadIdx.x;
   const int lane = (int)(gid & 63), g = lane >> 4, c = lane & 15;
-  const long f = gid >> 6;
-  if (f >= (long)L * wt_frags<NT>()) return;
-  const int j = 1 + (int)(f / wt_frags<NT>());
-  const int rt = (int)((f % wt_frags<NT>()) / KC), kc = (int)(f % KC);
+  const long fa = gid >> 6;  // (o, layer, frag)
+  if (fa >= 2L * L * NF) return;
+  const int o = (int)(fa / ((long)L * NF));
+  const long f = fa % ((long)L * NF);
+  const int j = 1 + (int)(f / NF), rt = (int)((f % NF) / KC), kc = (int)(f % KC);
   const float* Wj = prm + hidden_off(din, W, j);
   floatx4 v0, v1;
+  if (o == 0) {
+    v0 = *reinterpret_cast<const floatx4*>(Wj + (16 * rt + c) * W + 32 * kc + 8 * g);
+    v1 = *reinterpret_cast<const floatx4*>(Wj + (16 * rt + c) * W + 32 * kc + 8 * g + 4);
+  } else {
 #pragma unroll
-  for (int jj = 0; jj < 4; ++jj) {
-    v0[jj] = Wj[(32 * kc + 8 * g + jj) * W + 16 * rt + c];
-    v1[jj] = Wj[(32 * kc + 8 * g + 4 + jj) * W + 16 * rt + c];
+    for (int jj = 0; jj < 4; ++jj) {
+      v0[jj] = Wj[(32 * kc + 8 * g + jj) * W + 16 * rt + c];
+      v1[jj] = Wj[(32 * kc + 8 * g + 4 + jj) * W + 16 * rt + c];
+    }
   }
-  const FragQ<NQ> q = split_frag<NQ>(v0, v1);
+  const FragQ<3> q = split_frag<3>(v0, v1);
 #pragma unroll
-  for (int k = 0; k < NQ; ++k) out[(f * NQ + k) * 64 + lane] = q.q[k];
+  for (int k = 0; k < 3; ++k) out[(fa * 3 + k) * 64 + lane] = q.q[k];
 }
 
 // ---------------------------------------------------------------------------------------
@@ -78,7 +82,7 @@ __global__ __launch_bounds__(512, (x6p_min_waves<NT>())) void jet_bwd_x6p(const 
                                                    const float* __restrict__ prm, const float* __restrict__ act,
                                                    const float* __restrict__ gy, const float* __restrict__ gdy,
                                                    const float* __restrict__ glap, float* __restrict__ adj,
-                                                   float* __restrict__ part, long Ps, const u32x4* __restrict__ wsp) {
+                                                   float* __restrict__ part, long Ps) {
   constexpr int W = 16 * NT, RPW = NT / 8, KC = NT / 2;
   constexpr int LDB = W + 8, ZPLANE = 16 * LDB, ZSET = NQ * ZPLANE;
   constexpr int NTAN = LAP ? S - 2 : S - 1;
@@ -217,8 +221,8 @@ __global__ __launch_bounds__(512, (x6p_min_waves<NT>())) void jet_bwd_x6p(const 
                              hb[i][s][3]);
     __syncthreads();
     // propagation: h̄_{j-1}[m] = sum_n W_j[n][m] z̄_j[n]; A = W^T rows m of this wave (pre-split
-    // planes of kernel 0: NQ b128 loads per fragment), B = Z rows (one b128 per plane)
-    const u32x4* Wt = wsp + (long)(j - 1) * wt_frags<NT>() * NQ * 64 + lane;
+    // planes, orientation 1: NQ b128 loads per fragment), B = Z rows (one b128 per plane)
+    const u32x4* wsp = wsp_base(prm, din, dout, L, W);
     floatx4 nh[RPW][S];
 #pragma unroll
     for (int i = 0; i < RPW; ++i)
@@ -227,9 +231,7 @@ __global__ __launch_bounds__(512, (x6p_min_waves<NT>())) void jet_bwd_x6p(const 
     FragQ<NQ> wn[RPW];
     auto load_wt = [&](int kc) {
 #pragma unroll
-      for (int i = 0; i < RPW; ++i)
-#pragma unroll
-        for (int q = 0; q < NQ; ++q) wn[i].q[q] = Wt[(((long)(rt0 + i) * KC + kc) * NQ + q) * 64];
+      for (int i = 0; i < RPW; ++i) wn[i] = wsp_frag<NQ, NT>(wsp, L, 1, j, rt0 + i, kc, lane);
     };
     load_wt(0);
 #pragma unroll 1
@@ -579,17 +581,13 @@ inline int wide_ks(long n, int S, int L) {
   return ks < 1 ? 1 : (int)ks;
 }
 
-// workspace floats: z̄ of the L hidden layers | compact rows | dW partials | rows | W^T planes
-// (16-B aligned; NQ <= 3 planes of L W^2 / 2 u32 each)
-inline long wide_wt_offset(long n, int din, int dout, int L, int W, int S) {
+// workspace floats: z̄ of the L hidden layers | compact rows | dW partials | rows
+inline long wide_work_floats_impl(long n, int din, int dout, int L, int W, int S) {
   const long ntiles = ((n + 63) / 64) * 4;
   const long adj = (long)L * ntiles * S * (W / 16) * 256;
   const long small = ((n + 15) / 16) * small_count(din, dout, L, W);
   const long dw = (long)L * wide_ks(n, S, L) * W * W;
-  return (adj + small + dw + (long)kSmallRS * small_count(din, dout, L, W) + 3) & ~3L;
-}
-inline long wide_work_floats_impl(long n, int din, int dout, int L, int W, int S) {
-  return wide_wt_offset(n, din, dout, L, W, S) + 3L * L * W * W / 2;
+  return adj + small + dw + (long)kSmallRS * small_count(din, dout, L, W);
 }
 
 // threads of the three launches of wide_bwd_t (L > 0): propagation, dW + rows level 1,
@@ -624,14 +622,8 @@ int wide_bwd_t(const float* x, int N, int din, int dout, int L, const float* prm
                               (int)dw_lds<NQ, NT>());
     attr = true;
   }
-  u32x4* wsp = reinterpret_cast<u32x4*>(work + wide_wt_offset(N, din, dout, L, W, S));
-  if (L > 0) {
-    const long threads = (long)L * wt_frags<NT>() * 64;
-    hipLaunchKernelGGL((split_wt_kernel<NQ, NT>), dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st, prm, din, L,
-                       wsp);
-  }
   hipLaunchKernelGGL((jet_bwd_x6p<NQ, NT, S, LAP>), dim3(tiles), dim3(512), lds_p, st, x, N, din, dout, L, prm, act, gy,
-                     gdy, glap, adj, small, Ps, wsp);
+                     gdy, glap, adj, small, Ps);
   const int rs = tiles < kSmallRS ? tiles : kSmallRS;
   const int rows_x = (int)((Ps + 63) / 64);
   if (L > 0) {  // 3 launches: propagation | dW partials + compact rows level 1 | dW sums + rows level 2

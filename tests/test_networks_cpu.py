@@ -74,3 +74,22 @@ def test_grad_views_follow_the_padded_layout(B):
 def test_width_above_256_refused(B):
     with pytest.raises(NotImplementedError):
         B.MLP(2, 2, 1, 300, nonlinearity="sine")
+
+
+@pytest.mark.parametrize("shape", [(2, 1, 3, 128), (3, 3, 4, 256), (1, 1, 2, 32), (2, 3, 1, 64)])
+def test_weight_planes_follow_the_parameters(B, shape):
+    """The flat storage reserves the pre-split weight planes right after the parameters, at the
+    offset and size the library computes (insr_siren_wsplit_offset / _floats), and the
+    parameter views never reach into them."""
+    din, dout, L, W = shape
+    net = B.MLP(din, dout, L, W, nonlinearity="sine")
+    lib = B._native.lib()
+    assert net.wsplit_offset() == lib.insr_siren_wsplit_offset(din, dout, L, W)
+    assert net.wsplit_floats() == lib.insr_siren_wsplit_floats(L, W) == 3 * L * W * W
+    flat = net.flat_params()
+    store = flat._base if flat._base is not None else flat
+    assert store.numel() == net.wsplit_offset() + net.wsplit_floats()
+    assert flat.numel() == net.param_count and net.wsplit_offset() % 4 == 0
+    end = flat.data_ptr() + 4 * net.param_count
+    for p in net.parameters():
+        assert p.data_ptr() >= flat.data_ptr() and p.data_ptr() + 4 * p.numel() <= end

@@ -65,12 +65,18 @@ def main():
         torch.manual_seed(0)
         net = base.MLP(din, dout, L, W, nonlinearity="sine").cuda()
         flat = net.flat_params()
+        try:  # libraries with pre-split weight planes: prepare them once, pass INSR_MODE_WSPLIT
+            lib.insr_siren_wsplit
+            net.refresh_wsplit()
+            wbit = nat.MODE_WSPLIT
+        except AttributeError:
+            wbit = 0
         P = net.param_count
         for mname in args.modes.split(","):
-            mode = MODES[mname]
-            if mode == 2 and din > 2:
+            mode = MODES[mname] | wbit
+            if (mode & 0xF) == 2 and din > 2:
                 continue
-            S = {0: 1, 1: 1 + din, 2: 2 + din}[mode]
+            S = {0: 1, 1: 1 + din, 2: 2 + din}[mode & 0xF]
             for n in [int(v) for v in args.sizes.split(",")]:
                 x = (torch.rand(n, din, device="cuda") * 2 - 1).contiguous()
                 y = torch.empty(n, dout, device="cuda")
