@@ -258,6 +258,13 @@ int insr_plateau_step(float* opt_state, const float* loss, int patience, int adv
 /* Adam over up to INSR_ADAM_MAX_TENSORS flat buffers in ONE launch (torch op order).
  * Bias corrections use t = opt_state[STEP] + step_offset. */
 #define INSR_ADAM_MAX_TENSORS 8
+/* insr_adam_step_multi plus, per buffer, shapes[4 k .. 4 k + 3] = (d_in, d_out, num_hidden,
+ * width) of a SIREN flat params buffer (param_count floats) that carries pre-split weight
+ * planes (INSR_MODE_WSPLIT): the launch rewrites the planes of every updated hidden weight as
+ * well (all zeros / shapes == NULL: a plain buffer). */
+int insr_adam_step_nets(int count, float* const* params, const float* const* grads, float* const* exp_avg,
+                        float* const* exp_avg_sq, const long* sizes, const int* shapes, const float* opt_state,
+                        float beta1, float beta2, float eps, int step_offset, void* stream);
 int insr_adam_step_multi(int count, float* const* params, const float* const* grads, float* const* exp_avg,
                          float* const* exp_avg_sq, const long* sizes, const float* opt_state, float beta1,
                          float beta2, float eps, int step_offset, void* stream);

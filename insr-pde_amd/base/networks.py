@@ -151,6 +151,10 @@ class MLP(nn.Module):
                   "insr_siren_wsplit")
         self._wsplit_stamp = self._param_versions()
 
+    def mark_wsplit_current(self):
+        """The planes were rewritten with the parameters (insr_adam_step_nets)."""
+        self._wsplit_stamp = self._param_versions()
+
     def ensure_wsplit(self):
         """Before a jet: refresh the planes if the parameters changed behind our back."""
         if self._wsplit_stamp != self._param_versions():

@@ -107,11 +107,12 @@ class FusedAdam:
         for mlp, m, v in self._nets:
             if mlp.grad_touched():  # torch skips params whose .grad is None
                 mlp.grad_read_sync(cur)  # a backward may have written .grad on a side stream
-                bufs.append((mlp.flat_params(), mlp.flat_grad_buffer(), m, v))
+                bufs.append((mlp.flat_params(), mlp.flat_grad_buffer(), m, v,
+                             (mlp.in_features, mlp.out_features, mlp.num_hidden_layers, mlp.kernel_width)))
                 stepped.append(mlp)
         for p, m, v in self._loose:
             if p.grad is not None:
-                bufs.append((p.data, p.grad if p.grad.is_contiguous() else p.grad.contiguous(), m, v))
+                bufs.append((p.data, p.grad if p.grad.is_contiguous() else p.grad.contiguous(), m, v, (0, 0, 0, 0)))
         b1, b2 = self.betas
         st = nat.stream_of(self.device)
         chunks = [bufs[i:i + nat.ADAM_MAX_TENSORS] for i in range(0, len(bufs), nat.ADAM_MAX_TENSORS)]
@@ -119,11 +120,12 @@ class FusedAdam:
             k = len(chunk)
             arr = lambda j: (ctypes.c_void_p * k)(*[c[j].data_ptr() for c in chunk])  # noqa: E731
             sizes = (ctypes.c_long * k)(*[c[0].numel() for c in chunk])
-            nat.check(lib.insr_adam_step_multi(k, arr(0), arr(1), arr(2), arr(3), sizes, nat.ptr(self.state), b1, b2,
-                                               self.eps, 1, st), "insr_adam_step_multi")
-        for mlp in stepped:  # the updated weights' pre-split planes (part of a captured step)
-            if hasattr(mlp, "refresh_wsplit"):
-                mlp.refresh_wsplit()
+            # network buffers: the same launch rewrites their pre-split weight planes
+            shapes = (ctypes.c_int * (4 * k))(*[v for c in chunk for v in c[4]])
+            nat.check(lib.insr_adam_step_nets(k, arr(0), arr(1), arr(2), arr(3), sizes, shapes, nat.ptr(self.state),
+                                              b1, b2, self.eps, 1, st), "insr_adam_step_nets")
+        for mlp in stepped:  # planes current: no refresh before the next jet
+            mlp.mark_wsplit_current()
         self._pending_advance = True
 
 

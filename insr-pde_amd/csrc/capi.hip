@@ -377,8 +377,46 @@ struct AdamList {
   float* v[INSR_ADAM_MAX_TENSORS];
   long n[INSR_ADAM_MAX_TENSORS];
   long start[INSR_ADAM_MAX_TENSORS + 1];  // prefix sums of n
+  int shape[INSR_ADAM_MAX_TENSORS][4];    // SIREN (d_in, d_out, L, W) of a flat buffer with weight planes, else 0s
   int count;
 };
+
+// the updated hidden weight (layer j, row n, column m) of a buffer with pre-split planes:
+// its three bf16 terms (jet_x6.hpp split, element-wise identical to wsplit_kernel) stored
+// into both fragment orientations (jet_common.hpp wsplit_offset) -- the planes stay current
+// without a launch of their own
+__device__ __forceinline__ void adam_wsplit(float* base, const int (&sh)[4], long i, float w) {
+  const int din = sh[0], dout = sh[1], L = sh[2], W = sh[3];
+  const long off = i - ((long)W * din + W);
+  const long per = (long)W * W + W;
+  if (off < 0 || off >= (long)L * per) return;
+  const long r = off % per;
+  if (r >= (long)W * W) return;  // a bias
+  const int j = 1 + (int)(off / per), n = (int)(r / W), m = (int)(r % W);
+  const int NT = W / 16, KC = W / 32;
+  unsigned short t[3];
+  {
+    const __bf16 h = (__bf16)w;
+    float rs = w - (float)h;
+    const __bf16 md = (__bf16)rs;
+    rs -= (float)md;
+    const __bf16 lo = (__bf16)rs;
+    t[0] = __builtin_bit_cast(unsigned short, h);
+    t[1] = __builtin_bit_cast(unsigned short, md);
+    t[2] = __builtin_bit_cast(unsigned short, lo);
+  }
+  unsigned short* pl = reinterpret_cast<unsigned short*>(base + wsplit_offset(din, dout, L, W));
+  const long ov = wsplit_orient_vecs(L, W) * 8;  // u16 per orientation
+  // orientation 0: A row n, k = m; orientation 1: A row m (W^T), k = n
+  const int rr[2] = {n, m}, kk[2] = {m, n};
+#pragma unroll
+  for (int o = 0; o < 2; ++o) {
+    const int rt = rr[o] >> 4, c = rr[o] & 15, kc = kk[o] >> 5, g = (kk[o] & 31) >> 3, jj = kk[o] & 7;
+    const long fr = (((long)(j - 1) * NT + rt) * KC + kc) * 3;
+#pragma unroll
+    for (int q = 0; q < 3; ++q) pl[o * ov + ((fr + q) * 64 + 16 * g + c) * 8 + jj] = t[q];
+  }
+}
 
 // One launch over up to INSR_ADAM_MAX_TENSORS flat buffers.  The step t used is
 // st[STEP] + step_offset (the plateau kernel advances st[STEP] after the update,
@@ -409,7 +447,9 @@ __global__ void adam_multi_kernel(AdamList L, const float* __restrict__ st, floa
     L.m[k][i] = mi;
     L.v[k][i] = vi;
     const float denom = sqrtf(vi) / bc2s + eps;
-    L.p[k][i] = L.p[k][i] - step_size * (mi / denom);
+    const float pn = L.p[k][i] - step_size * (mi / denom);
+    L.p[k][i] = pn;
+    if (L.shape[k][2] > 0) adam_wsplit(L.p[k], L.shape[k], i, pn);
   }
 }
 
@@ -787,11 +827,24 @@ int insr_plateau_step(float* st, const float* loss, int patience, int advance_st
 int insr_adam_step_multi(int count, float* const* params, const float* const* grads, float* const* exp_avg,
                          float* const* exp_avg_sq, const long* sizes, const float* st, float b1, float b2,
                          float eps, int step_offset, void* stream) {
+  return insr_adam_step_nets(count, params, grads, exp_avg, exp_avg_sq, sizes, nullptr, st, b1, b2, eps, step_offset,
+                             stream);
+}
+
+int insr_adam_step_nets(int count, float* const* params, const float* const* grads, float* const* exp_avg,
+                        float* const* exp_avg_sq, const long* sizes, const int* shapes, const float* st, float b1,
+                        float b2, float eps, int step_offset, void* stream) {
   if (count < 1 || count > INSR_ADAM_MAX_TENSORS || !st) return INSR_EINVAL;
   AdamList L;
   L.count = count;
   L.start[0] = 0;
   for (int k = 0; k < count; ++k) {
+    for (int q = 0; q < 4; ++q) L.shape[k][q] = shapes ? shapes[4 * k + q] : 0;
+    if (L.shape[k][2] > 0) {  // a SIREN flat buffer with weight planes: its shape must match its size
+      const int* sh = L.shape[k];
+      if (!shape_ok(sh[0], sh[1], sh[2], sh[3], 0) || sizes[k] != insr_siren_param_count(sh[0], sh[1], sh[2], sh[3]))
+        return INSR_EINVAL;
+    }
     if (!params[k] || !grads[k] || !exp_avg[k] || !exp_avg_sq[k] || sizes[k] < 0) return INSR_EINVAL;
     L.p[k] = params[k];
     L.g[k] = grads[k];
