@@ -142,7 +142,7 @@ WORKLOADS = {
                                 model="SIREN 5x128 deformation(2->2), arap+constraint+constraint_right+volume"),
     "elasticity3Dbunny": dict(pde="elasticity", phases=("_solve_deformation",), res=64,
                               model="SIREN 5x256 deformation(3->3), arap+kinematics+collision+external+volume "
-                                    "(synthetic box volume)"),
+                                    "(the reference's bunny volume, tests/golden/bunny_mesh.npz)"),
 }
 
 

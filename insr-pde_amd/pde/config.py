@@ -20,6 +20,10 @@ PDE = {
                        constraint_right_offset_z=0.0, plane_height=-2.0, collide_circle_x=0.0,
                        collide_circle_y=-2e0, collide_circle_z=0.0, collide_circle_radius=1.0),
 }
+# the reference's elasticity/data/bunny.mesh as a data fixture (tests/golden/make_bunny_fixture.py)
+BUNNY_FIXTURE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "..", "tests", "golden",
+                             "bunny_mesh.npz")
+
 # insr-pde_amd execution knobs (see base/_loop.py)
 EXEC = dict(insr_precision=None, insr_sync_every=1, insr_graph=False, insr_progress=True, insr_band_stream=False, insr_nograd_stream=False,
             insr_fuse_forwards=os.environ.get("INSR_FUSE_FORWARDS", "1") != "0")
@@ -56,7 +60,11 @@ BASELINE_CONFIGS = {
                                              energy=["arap", "kinematics", "collision", "external", "volume"],
                                              ratio_volume=1e3, ratio_arap=1e2, ratio_collide=1e6,
                                              ratio_kinematics=1e0, external_force_z=-1e2,
-                                             external_force_timesteps=5, plane_height=-2.0)),
+                                             external_force_timesteps=5, plane_height=-2.0,
+                                             # the reference's bunny (scripts/elasticity3Dbunny.sh:
+                                             # --use_mesh 1 --mesh_path elasticity/data/bunny.mesh),
+                                             # as the derived fixture that travels with the repo
+                                             use_mesh=True, mesh_path=BUNNY_FIXTURE)),
     "fluid2DtlgnM": ("fluid", dict(num_hidden_layers=4, hidden_features=128, sample_resolution=256,
                                    init_cond="taylorgreen_multi", dt=0.05)),
 }

@@ -162,7 +162,13 @@ def load_mesh(path, dim, device="cpu"):
     elif path.endswith(".obj"):
         V, E = read_obj(path)
         SF = E
+    elif path.endswith(".npz"):  # a fixture derived from a .mesh (tests/golden/make_bunny_fixture.py)
+        with np.load(path) as z:  # arrays only (allow_pickle stays False)
+            V, E = z["V"].astype(np.float64), z["T"].astype(np.int64)
+        if dim != 3 or E.shape[1] != 4:
+            raise ValueError(f"{path}: a tetrahedral (3-D) mesh fixture is expected")
+        SF = boundary_faces(E)
     else:
-        raise ValueError(f"unsupported mesh file {path!r} (.mesh or .obj)")
+        raise ValueError(f"unsupported mesh file {path!r} (.mesh, .obj or a .npz fixture)")
     V = normalize(torch.as_tensor(V, dtype=torch.float64)) * 2.0
     return V.to(device, torch.float32), E, SF

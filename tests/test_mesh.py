@@ -168,3 +168,21 @@ def test_reference_bunny_mesh():
     assert bool(torch.all(vol > 0))
     Vn, E, _ = M.load_mesh(REF_BUNNY, 3)
     assert abs(float(Vn.norm(dim=1).max()) - 2.0) < 1e-5
+
+
+BUNNY_NPZ = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "bunny_mesh.npz")
+
+
+def test_bunny_fixture_loads_like_the_reference_mesh():
+    """The derived fixture (tests/golden/make_bunny_fixture.py) is what the elasticity3Dbunny
+    bench trains on: same vertex / tet counts as the reference's bunny.mesh, positive tet
+    volumes, normalised radius 2, and -- where the reference tree is mounted -- the same
+    loaded arrays as reading the .mesh itself."""
+    Vn, E, SF = M.load_mesh(BUNNY_NPZ, 3)
+    assert Vn.shape == (18592, 3) and E.shape == (76854, 4) and SF.shape == (20522, 3)
+    assert abs(float(Vn.norm(dim=1).max()) - 2.0) < 1e-5
+    vol = M.tet_volumes(Vn.double(), torch.as_tensor(E))
+    assert bool(torch.all(vol > 0))
+    if os.path.exists(REF_BUNNY):
+        Vr, Er, SFr = M.load_mesh(REF_BUNNY, 3)
+        assert torch.equal(Vn, Vr) and np.array_equal(E, Er) and np.array_equal(SF, SFr)
