@@ -79,7 +79,7 @@ def test_el3d_full_iteration_and_slice_parity(model):
     xs = x.detach()[:n].clone()
     f, fp, fpp = _oracle_nets(m)
     xr = xs.cpu().clone().requires_grad_(True)
-    e_ref = O.elasticity_loss(f, fp, fpp, xr, None, None, _ecfg(m), timestep=m.timestep)
+    e_ref = O.elasticity_loss(f, fp, fpp, xr, None, None, _ecfg(m), timestep=m.timestep)["main"]
     e_ref.backward()
     m.deformation_field.zero_grad(set_to_none=True)
     e = m.energy_of(xs.clone().requires_grad_(True), fl, fr)
