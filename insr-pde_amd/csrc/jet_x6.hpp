@@ -547,6 +547,12 @@ __device__ __forceinline__ floatx4 quad_transpose(const floatx4& v, int c) {
   return floatx4{o2 ? t0 : a[0], o2 ? t1 : a[1], o2 ? a[2] : t0, o2 ? a[3] : t1};
 }
 
+// ds_read_b64_tr_b16 (gfx950 LDS transpose read, 8-B aligned address in LDS)
+typedef short v4s __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ v4s ds_read_tr16(const unsigned short* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(p));
+}
+
 // one value granule (4 neurons x 1 point per lane, C layout) -> neuron-major bf16 planes
 // [q][m][16 p] at row0 = first neuron of the lane group: quad transpose, then one b64
 // store of 4 consecutive points per plane (instead of 12 b16 stores)
@@ -845,17 +851,18 @@ __global__ __launch_bounds__(X6Geo<NT>::THREADS) void jet_bwd_x6(
         for (int i = 0; i < RPW; ++i) {
           FragQ<NQ> af;
           {
-            const unsigned short* pa = Z + (live ? u : 0) * ZSET + p0 * LDB + 16 * (rt0 + i) + c;
+            // column reads of the point-major Z image with the gfx950 transpose read: per
+            // 16-lane group, lane 4 r + p4 addresses row p0 + r (+ 4), columns 4 p4 .. 4 p4 + 3
+            // of this wave's 16 neurons; lane c receives neuron c at 4 consecutive points
+            // (2 reads per plane instead of 8 u16 reads; every lane takes part: EXEC full)
+            const unsigned short* pa =
+                Z + (live ? u : 0) * ZSET + (p0 + (c >> 2)) * LDB + 16 * (rt0 + i) + 4 * (c & 3);
 #pragma unroll
             for (int q = 0; q < NQ; ++q) {
-              unsigned w[4];
-#pragma unroll
-              for (int d = 0; d < 4; ++d) {
-                const unsigned short* q0 = pa + (2 * d) * LDB + q * ZPLANE;
-                const unsigned short* q1 = pa + (2 * d + 1) * LDB + q * ZPLANE;
-                w[d] = live ? ((unsigned)q0[0] | ((unsigned)q1[0] << 16)) : 0u;
-              }
-              af.q[q] = u32x4{w[0], w[1], w[2], w[3]};
+              const v4s lo = ds_read_tr16(pa + q * ZPLANE);
+              const v4s hi = ds_read_tr16(pa + q * ZPLANE + 4 * LDB);
+              const u32x2 wl = __builtin_bit_cast(u32x2, lo), wh = __builtin_bit_cast(u32x2, hi);
+              af.q[q] = live ? u32x4{wl[0], wl[1], wh[0], wh[1]} : u32x4{0u, 0u, 0u, 0u};
             }
           }
 #pragma unroll
