@@ -407,8 +407,27 @@ __global__ __launch_bounds__(512) void dw_x6(int N, const float* __restrict__ ac
       }
       const floatx4 sv = ssv[kShare ? it % RT : it], cv = scv[kShare ? it % RT : it];
       floatx4 hv;
-      if (LAP && s == S - 1) {  // Laplacian stream: needs the tangents (read here)
-        hv = h_stream<NT, S, LAP>(act_base(act, j - 1, ntiles, t, S, NT), s, rt, lane, sv, cv);
+      if (LAP && s == S - 1) {  // Laplacian stream: h = w c q - w^2 s sum_i t_i^2
+        if constexpr (S % 2 == 0) {
+          // even S: this chunk's first unit is stream S - 2 of the same tile (its z is in
+          // registers), and q is this granule's own load -- only tangents 1 .. S - 3 are read
+          // (summed in stream order 1 .. S - 2, as h_stream and the forward do)
+          const floatx4 zsib = rzs[it >= RT ? it - RT : 0];
+          floatx4 t2 = floatx4{0.f, 0.f, 0.f, 0.f};
+          const float* ba = act_base(act, j - 1, ntiles, t, S, NT);
+#pragma unroll
+          for (int ti = 1; ti < S - 2; ++ti) {
+            const floatx4 z = *reinterpret_cast<const floatx4*>(ba + ((ti * NT + rt) * 64 + lane) * 4);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) t2[r] = fmaf(z[r], z[r], t2[r]);
+          }
+#pragma unroll
+          for (int r = 0; r < 4; ++r) t2[r] = fmaf(zsib[r], zsib[r], t2[r]);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) hv[r] = OMEGA * cv[r] * rzs[it][r] - OMEGA2 * sv[r] * t2[r];
+        } else {
+          hv = h_stream<NT, S, LAP>(act_base(act, j - 1, ntiles, t, S, NT), s, rt, lane, sv, cv);
+        }
       } else {
 #pragma unroll
         for (int r = 0; r < 4; ++r) hv[r] = s == 0 ? sv[r] : OMEGA * cv[r] * rzs[it][r];
