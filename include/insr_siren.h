@@ -133,6 +133,14 @@ typedef struct InsrJetJob {
   long n;               /* points of this job */
   int d_out;            /* this job's output width (1..3); 0 = the call's d_out */
 } InsrJetJob;
+/* Independent forward jets of one width / d_in / depth with DIFFERENT jet modes in one launch
+ * (modes[k] = INSR_MODE_VALUE / GRAD / LAP of job k; prec_mode = the common precision and
+ * INSR_MODE_WSPLIT bits, no jet-mode bits).  Each job's outputs and saved streams equal its
+ * own insr_siren_jet_fwd call bit for bit (its own body and tile count; one launch at
+ * W = 128 split-bf16, one launch per job otherwise).  Replaces: consecutive MLP.forward +
+ * diff-op calls of a phase (fluid/model.py:106-111, :143-147). */
+int insr_siren_jet_fwd_mixed(const InsrJetJob* jobs, const int* modes, int n_jobs, int d_in, int d_out,
+                             int num_hidden, int width, int prec_mode, void* stream);
 int insr_siren_jet_fwd_multi(const InsrJetJob* jobs, int n_jobs, int d_in, int d_out,
                              int num_hidden, int width, int mode, void* stream);
 

@@ -16,6 +16,9 @@ Recognised shapes of `y` (everything the reference models use):
   * y = gradient(mlp(x), x)  inside divergence  (-> Laplacian stream)
 Anything else raises UnsupportedPattern (there is no silent fallback).
 """
+import ctypes
+import os
+
 import torch
 from torch.autograd.function import once_differentiable
 
@@ -185,11 +188,40 @@ class fused_forwards:
         return False
 
 
+_MIXED = os.environ.get("INSR_FUSE_MIXED", "1") != "0"
+
+
+def _job_array(chunk):
+    return (nat.JetJob * len(chunk))(*[
+        nat.JetJob(x2.data_ptr(), flat.data_ptr(), y.data_ptr(), None if dy is None else dy.data_ptr(),
+                   None if lap is None else lap.data_ptr(), None if act is None else act.data_ptr(), nj, dj)
+        for x2, flat, y, dy, lap, act, nj, dj in chunk])
+
+
 def _launch_fused(jobs):
     groups = {}
     for key, job in jobs:
         groups.setdefault(key, []).append(job)
     lib = nat.lib()
+    # jets that differ only in their jet mode (W = 128, batches in the 2-tile value regime):
+    # ONE insr_siren_jet_fwd_mixed launch, each job with its own body
+    by_arch = {}
+    for (din, L, W, cmode, dev), js in groups.items():
+        by_arch.setdefault((din, L, W, cmode & ~nat.MODE_MASK, dev), []).append((cmode & nat.MODE_MASK, js))
+    for (din, L, W, pbits, dev), parts in by_arch.items():
+        alljobs = [(m, j) for m, js in parts for j in js]
+        if (_MIXED and len(parts) > 1 and W == 128 and len(alljobs) <= nat.MAX_FWD_JOBS
+                and all(j[6] <= 40000 for _, j in alljobs)):
+            chunk = [j for _, j in alljobs]
+            modes = (ctypes.c_int * len(chunk))(*[m for m, _ in alljobs])
+            n = sum(j[6] for j in chunk)
+            key_dout = tuple(j[7] for j in chunk)
+            with _timed("fwdmix%d" % len(chunk), max(m for m, _ in alljobs), n, W, (din, key_dout, L)):
+                rc = lib.insr_siren_jet_fwd_mixed(_job_array(chunk), modes, len(chunk), din, chunk[0][7], L, W, pbits,
+                                                  nat.stream_of(dev))
+            nat.check(rc, "insr_siren_jet_fwd_mixed")
+            for m, js in parts:
+                groups.pop((din, L, W, pbits | m, dev))
     for (din, L, W, cmode, dev), js in groups.items():  # output widths may differ per job
         mode = cmode & nat.MODE_MASK
         for k in range(0, len(js), nat.MAX_FWD_JOBS):
@@ -198,10 +230,7 @@ def _launch_fused(jobs):
             douts = sorted({j[7] for j in chunk})
             dout = chunk[0][7]
             key_dout = douts[0] if len(douts) == 1 else tuple(j[7] for j in chunk)  # per-job widths in the timing key
-            arr = (nat.JetJob * len(chunk))(*[
-                nat.JetJob(x2.data_ptr(), flat.data_ptr(), y.data_ptr(), None if dy is None else dy.data_ptr(),
-                           None if lap is None else lap.data_ptr(), None if act is None else act.data_ptr(), nj, dj)
-                for x2, flat, y, dy, lap, act, nj, dj in chunk])
+            arr = _job_array(chunk)
             with _timed("fwd%d" % len(chunk) if len(chunk) > 1 else "fwd", mode, n, W, (din, key_dout, L)):
                 rc = lib.insr_siren_jet_fwd_multi(arr, len(chunk), din, dout, L, W, cmode, nat.stream_of(dev))
             nat.check(rc, "insr_siren_jet_fwd_multi")

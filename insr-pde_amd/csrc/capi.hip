@@ -659,6 +659,54 @@ int insr_siren_jet_fwd_multi(const InsrJetJob* jobs, int njobs, int din, int dou
   return 0;
 }
 
+int insr_siren_jet_fwd_mixed(const InsrJetJob* jobs, const int* modes, int njobs, int din, int dout, int L, int W,
+                             int prec_mode, void* stream) {
+  if (!jobs || !modes || njobs < 1 || njobs > INSR_MAX_FWD_JOBS) return INSR_EINVAL;
+  if (prec_mode & INSR_MODE_MASK) return INSR_EINVAL;  // the per-job jet modes come from `modes`
+  long total = 0;
+  for (int k = 0; k < njobs; ++k) {
+    const InsrJetJob& j = jobs[k];
+    const int m = modes[k] | prec_mode;
+    if (modes[k] & ~INSR_MODE_MASK) return INSR_EINVAL;
+    if (!shape_ok(din, j.d_out > 0 ? j.d_out : dout, L, W, m)) return INSR_EINVAL;
+    if (j.n < 0 || j.n > 0x7fffffffL || (j.n > 0 && (!j.x || !j.params || !j.y))) return INSR_EINVAL;
+    if (j.n > 0 && modes[k] != INSR_MODE_VALUE && !j.dy) return INSR_EINVAL;
+    if (j.n > 0 && modes[k] == INSR_MODE_LAP && !j.lap) return INSR_EINVAL;
+    total += j.n;
+  }
+  if (total > 0x7fffffffL) return INSR_EINVAL;
+  const JetCall c(din, W, INSR_MODE_VALUE | prec_mode);
+  hipStream_t st = (hipStream_t)stream;
+  if (c.NT == 8 && c.nqf > 0) {
+    InsrJetJob pk[INSR_MAX_FWD_JOBS];
+    int md[INSR_MAX_FWD_JOBS];
+    int m = 0;
+    for (int k = 0; k < njobs; ++k) {
+      if (jobs[k].n == 0) continue;
+      pk[m] = jobs[k];
+      md[m] = modes[k];
+      int rc = 0;
+      const int dk = jobs[k].d_out > 0 ? jobs[k].d_out : dout;
+      if (!(pk[m].params = with_planes(jobs[k].params, din, dk, L, W, prec_mode, st, k, &rc))) return rc;
+      ++m;
+    }
+    if (m == 0) return 0;
+    switch (c.nqf) {
+      case 3: return dispatch_fwd_mixed_q<3>(c.NT, din, pk, md, m, dout, L, st);
+      case 2: return dispatch_fwd_mixed_q<2>(c.NT, din, pk, md, m, dout, L, st);
+      default: return dispatch_fwd_mixed_q<1>(c.NT, din, pk, md, m, dout, L, st);
+    }
+  }
+  for (int k = 0; k < njobs; ++k) {  // other widths / exact fp32: one launch per job
+    const InsrJetJob& j = jobs[k];
+    if (j.n == 0) continue;
+    const int rc = insr_siren_jet_fwd(j.x, j.n, din, j.d_out > 0 ? j.d_out : dout, L, W, modes[k] | prec_mode,
+                                      j.params, j.y, j.dy, j.lap, j.act, stream);
+    if (rc) return rc;
+  }
+  return 0;
+}
+
 int insr_siren_jet_bwd(const float* x, long n, int din, int dout, int L, int W, int mode, const float* params,
                        const float* act, const float* gy, const float* gdy, const float* glap, float* partial,
                        void* stream) {

@@ -415,6 +415,85 @@ __global__ __launch_bounds__(X6Geo<NT>::THREADS, (x6_multi_min_waves<NT, S>())) 
   fwd_x6_block<NQ, NT, S, LAP, TA>(jb.x, (int)jb.n, din, dout_k, L, jb.params, jb.y, jb.dy, jb.lap, jb.act, tile0, cnt);
 }
 
+// Mixed-mode horizontal fusion: independent forward jets of one width and d_in but DIFFERENT
+// jet modes (the pressure phase's detached velocity Jacobian beside the pressure Laplacian
+// jet; the projection's two value jets beside the pressure gradient) in ONE launch.  Each
+// block runs one job with that job's own body and tile count (value T = 2, gradient and
+// Laplacian T = 1: the forward tile policy at W = 128), so outputs are bit-identical to the
+// job's own launch; the kernel's registers / LDS are the largest body's.
+struct FwdMixX6 {
+  InsrJetJob job[kFwdJobs];
+  int first[kFwdJobs + 1];
+  int mode[kFwdJobs];  // INSR_MODE_VALUE / GRAD / LAP
+  int njobs;
+};
+
+template <int NQ, int NT, int DIN>
+constexpr size_t fwd_mix_lds_bytes() {
+  constexpr size_t a = fwd_x6_lds_bytes<NQ, NT, 1, 2>(), b = fwd_x6_lds_bytes<NQ, NT, 1 + DIN, 1>();
+  constexpr size_t c = DIN <= 2 ? fwd_x6_lds_bytes<NQ, NT, 2 + DIN, 1>() : 0;
+  return a > b ? (a > c ? a : c) : (b > c ? b : c);
+}
+
+template <int NQ, int NT, int DIN>
+__global__ __launch_bounds__(X6Geo<NT>::THREADS, 4) void jet_fwd_x6_mixed(const FwdMixX6 jobs, int dout, int L) {
+  const int b = blockIdx.x;
+  int k = 0;
+#pragma unroll
+  for (int q = 1; q < kFwdJobs; ++q) k += (q < jobs.njobs && b >= jobs.first[q]) ? 1 : 0;
+  const InsrJetJob& jb = jobs.job[k];
+  const int dk = jb.d_out > 0 ? jb.d_out : dout;
+  const int lb = b - jobs.first[k];
+  int tile0, cnt;
+  switch (jobs.mode[k]) {
+    case INSR_MODE_VALUE:
+      block_tiles(lb, (int)jb.n, 2, 0, tile0, cnt);
+      fwd_x6_block<NQ, NT, 1, false, 2>(jb.x, (int)jb.n, DIN, dk, L, jb.params, jb.y, jb.dy, jb.lap, jb.act, tile0,
+                                        cnt);
+      break;
+    case INSR_MODE_GRAD:
+      fwd_x6_block<NQ, NT, 1 + DIN, false, 1>(jb.x, (int)jb.n, DIN, dk, L, jb.params, jb.y, jb.dy, jb.lap, jb.act, lb,
+                                              1);
+      break;
+    default:
+      if constexpr (DIN <= 2)
+        fwd_x6_block<NQ, NT, 2 + DIN, true, 1>(jb.x, (int)jb.n, DIN, dk, L, jb.params, jb.y, jb.dy, jb.lap, jb.act,
+                                               lb, 1);
+      break;
+  }
+}
+
+template <int NQ, int NT, int DIN>
+int launch_fwd_x6_mixed_t(const InsrJetJob* jobs, const int* modes, int njobs, int dout, int L, hipStream_t st) {
+  constexpr size_t lds = fwd_mix_lds_bytes<NQ, NT, DIN>();
+  if constexpr (lds > kLdsMax) {
+    return INSR_EINVAL;
+  } else {
+    if (njobs < 1 || njobs > kFwdJobs) return INSR_EINVAL;
+    static bool attr_set = false;
+    if (!attr_set) {
+      (void)hipFuncSetAttribute((const void*)jet_fwd_x6_mixed<NQ, NT, DIN>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)lds);
+      attr_set = true;
+    }
+    FwdMixX6 pk{};
+    int nb = 0;
+    for (int k = 0; k < njobs; ++k) {
+      if (modes[k] == INSR_MODE_LAP && DIN > 2) return INSR_EINVAL;
+      pk.job[k] = jobs[k];
+      pk.mode[k] = modes[k];
+      pk.first[k] = nb;
+      const long tiles = (jobs[k].n + 15) / 16;
+      nb += (int)(modes[k] == INSR_MODE_VALUE ? (tiles + 1) / 2 : tiles);
+    }
+    pk.first[njobs] = nb;
+    pk.njobs = njobs;
+    if (nb == 0) return 0;
+    hipLaunchKernelGGL((jet_fwd_x6_mixed<NQ, NT, DIN>), dim3(nb), dim3(X6Geo<NT>::THREADS), lds, st, pk, dout, L);
+    return (int)hipGetLastError();
+  }
+}
+
 // small[k] != 0: job k runs 1-tile blocks (ignored when T == 1)
 template <int NQ, int NT, int S, bool LAP, int T>
 int launch_fwd_x6_multi_t(const InsrJetJob* jobs, const int* small, const int* nbal, int njobs, int din, int dout,

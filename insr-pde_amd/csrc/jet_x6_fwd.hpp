@@ -63,6 +63,19 @@ int dispatch_fwd_multi_q(int NT, int S, bool LAP, int T, const InsrJetJob* jobs,
 #undef INSR_MULTI_S
 }
 
+// mixed-mode fused forward (W = 128 only: the tile policy it encodes is the W = 128 one)
+template <int NQ>
+int dispatch_fwd_mixed_q(int NT, int din, const InsrJetJob* jobs, const int* modes, int njobs, int dout, int L,
+                         hipStream_t st) {
+  if (NT != 8) return INSR_EWIDTH;
+  switch (din) {
+    case 1: return launch_fwd_x6_mixed_t<NQ, 8, 1>(jobs, modes, njobs, dout, L, st);
+    case 2: return launch_fwd_x6_mixed_t<NQ, 8, 2>(jobs, modes, njobs, dout, L, st);
+    case 3: return launch_fwd_x6_mixed_t<NQ, 8, 3>(jobs, modes, njobs, dout, L, st);
+    default: return INSR_EINVAL;
+  }
+}
+
 template <int NQ>
 int dispatch_fwd_q(int NT, int S, bool LAP, int T, const float* x, int N, int din, int dout, int L,
                    const float* prm, float* y, float* dy, float* lap, float* act, int nbal, hipStream_t st) {

@@ -221,9 +221,12 @@ class Fluid2DModel(BaseModel):
             # instead of a separate gradient jet + reverse jet for 2% of the points.  The
             # Laplacian rows of the band points get zero adjoint.
             xa, n, nb = self._merged(x)
-            with torch.no_grad():  # div u = du/dx + dv/dy, read off the velocity's Jacobian
-                Ju = jacobian_only(self.velocity_field(x), x)
-            lap_p, grad_p = laplace(self.pressure_field(xa), xa, return_grad=True)
+            # the velocity's Jacobian jet and the pressure's Laplacian jet are independent: one
+            # mixed-mode launch (base.fused_forwards); outputs are read after the scope
+            with fused_forwards():
+                with torch.no_grad():  # div u = du/dx + dv/dy, read off the velocity's Jacobian
+                    Ju = jacobian_only(self.velocity_field(x), x)
+                lap_p, grad_p = laplace(self.pressure_field(xa), xa, return_grad=True)
             # mean((lap p - du/dx - dv/dy)^2) over the interior rows (= mean((div u - lap p)^2))
             # and the wall terms, one launch; the diagonal of J is read in place (stride 4)
             main, bc = sq_losses(mse_term(lap_p, Ju[:, 0, 0], Ju[:, 1, 1], alpha=1.0, beta=-1.0, gamma=-1.0, count=n),
@@ -241,9 +244,15 @@ class Fluid2DModel(BaseModel):
     def _projection(self):
         x = self._sample_in_training()
         if self._fused_pair() and not getattr(self.cfg, "insr_band_stream", False):
-            ua, n, nb, u_prev = self._prev_and_current(x)
-            with torch.no_grad():
-                grad_p = gradient(self.pressure_field(x), x)
+            xa, n, nb = self._merged(x)
+            # frozen velocity (value), pressure gradient (detached) and the trainable velocity
+            # over [x; bands]: independent jets, one mixed-mode launch
+            with fused_forwards():
+                with torch.no_grad():
+                    u_prev = self.velocity_field_prev(x)
+                    grad_p = gradient(self.pressure_field(x), x)
+                ua = self.velocity_field(xa)
+            u_prev = u_prev.detach()
             main, bc = sq_losses(mse_term(ua, None, u_prev, grad_p, gamma=-1.0, delta=-1.0, count=u_prev.numel()),
                                  wall_term(ua, nb, row0=n))
             return {'main': main, 'bc': bc}

@@ -10,6 +10,8 @@ hipGraph replay (the oracle check of the fused default is
 test_gpu_phases.py::test_fluid_phases[False]).
 """
 
+import contextlib
+
 import pytest
 import torch
 
@@ -199,3 +201,40 @@ def test_fluid_phase_fused_equals_unfused(B, phase, graph):
         d = (a - b).abs()
         assert float(d.max()) <= 4 * 2 * 1e-4 * 1.01, phase
         assert float((d > 1e-6).float().mean()) < 0.02, phase
+
+
+@pytest.mark.parametrize("n", [4096, 16708])
+def test_mixed_mode_launch_matches_single_launches(B, n):
+    """insr_siren_jet_fwd_mixed (jets of different modes in one launch) gives each job its own
+    single-launch outputs bit for bit: velocity Jacobian + pressure Laplacian/gradient (the
+    pressure phase), and frozen value + pressure gradient + trainable value (projection)."""
+    from base import _jet
+    from base.diff_ops import jacobian_only
+    vel, pres, prev = _net(B, "fluid_vel", 1), _net(B, "fluid_pres", 2), _net(B, "fluid_vel", 3)
+    g = torch.Generator().manual_seed(21)
+    x = (torch.rand(n, 2, generator=g) * 2 - 1).cuda()
+    xa = (torch.rand(n + 324, 2, generator=g) * 2 - 1).cuda()
+
+    def pressure_phase(fused):
+        xg, xag = x.clone().requires_grad_(True), xa.clone().requires_grad_(True)
+        ctx = B.fused_forwards() if fused else contextlib.nullcontext()
+        with ctx:
+            with torch.no_grad():
+                J = jacobian_only(vel(xg), xg)
+            lap, gp = B.laplace(pres(xag), xag, return_grad=True)
+        return J, lap, gp
+
+    def projection(fused):
+        xg, xag = x.clone().requires_grad_(True), xa.clone().requires_grad_(True)
+        ctx = B.fused_forwards() if fused else contextlib.nullcontext()
+        with ctx:
+            with torch.no_grad():
+                up = prev(xg)
+                gp = B.gradient(pres(xg), xg)
+            ua = vel(xag)
+        return up, gp, ua
+
+    assert _jet._MIXED
+    for phase in (pressure_phase, projection):
+        for u, v in zip(phase(False), phase(True)):
+            assert torch.equal(u, v), phase.__name__
