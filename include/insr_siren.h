@@ -139,8 +139,13 @@ typedef struct InsrJetJob {
  * own insr_siren_jet_fwd call bit for bit (its own body and tile count; one launch at
  * W = 128 split-bf16, one launch per job otherwise).  Replaces: consecutive MLP.forward +
  * diff-op calls of a phase (fluid/model.py:106-111, :143-147). */
-int insr_siren_jet_fwd_mixed(const InsrJetJob* jobs, const int* modes, int n_jobs, int d_in, int d_out,
-                             int num_hidden, int width, int prec_mode, void* stream);
+/* modes[k] = INSR_MIX_ADVECT: the semi-Lagrangian target of the fluid advection
+ * (fluid/model.py:96-97) in one job: y = f(clamp(x - dt f(x), lo, hi)) with the job's
+ * network f (value jets, d_out == d_in), f(x) written to the job's dy field (n, d_out) and
+ * the foot to its lap field (n, d_in); scalars[3 k .. 3 k + 2] = (dt, lo, hi). */
+#define INSR_MIX_ADVECT 3
+int insr_siren_jet_fwd_mixed(const InsrJetJob* jobs, const int* modes, const float* scalars, int n_jobs, int d_in,
+                             int d_out, int num_hidden, int width, int prec_mode, void* stream);
 int insr_siren_jet_fwd_multi(const InsrJetJob* jobs, int n_jobs, int d_in, int d_out,
                              int num_hidden, int width, int mode, void* stream);
 

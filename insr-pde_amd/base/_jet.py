@@ -191,11 +191,52 @@ class fused_forwards:
 _MIXED = os.environ.get("INSR_FUSE_MIXED", "1") != "0"
 
 
+MIX_ADVECT = 3  # include/insr_siren.h INSR_MIX_ADVECT: a job mode of insr_siren_jet_fwd_mixed
+
+
 def _job_array(chunk):
     return (nat.JetJob * len(chunk))(*[
         nat.JetJob(x2.data_ptr(), flat.data_ptr(), y.data_ptr(), None if dy is None else dy.data_ptr(),
                    None if lap is None else lap.data_ptr(), None if act is None else act.data_ptr(), nj, dj)
-        for x2, flat, y, dy, lap, act, nj, dj in chunk])
+        for x2, flat, y, dy, lap, act, nj, dj, *_ in chunk])
+
+
+def _launch_mixed(din, L, W, pbits, dev, alljobs):
+    """One insr_siren_jet_fwd_mixed launch: alljobs = [(jet mode, job tuple)]."""
+    chunk = [j for _, j in alljobs]
+    modes = (ctypes.c_int * len(chunk))(*[m for m, _ in alljobs])
+    sc = (ctypes.c_float * (3 * len(chunk)))(*[v for _, j in alljobs for v in (j[8] if len(j) > 8 else (0., 0., 0.))])
+    n = sum(j[6] for j in chunk)
+    key_dout = tuple(j[7] for j in chunk)
+    with _timed("fwdmix%d" % len(chunk), max(m for m, _ in alljobs if m != MIX_ADVECT) if any(
+            m != MIX_ADVECT for m, _ in alljobs) else 0, n, W, (din, key_dout, L)):
+        rc = nat.lib().insr_siren_jet_fwd_mixed(_job_array(chunk), modes, sc, len(chunk), din, chunk[0][7], L, W,
+                                                pbits, nat.stream_of(dev))
+    nat.check(rc, "insr_siren_jet_fwd_mixed")
+
+
+def advect_target(mlp, x, dt, lo=-1.0, hi=1.0):
+    """(f(clamp(x - dt f(x), lo, hi)), f(x)) of a frozen field f (fluid/model.py:96-97, the
+    semi-Lagrangian target of the advection) as ONE job of a mixed launch -- inside a
+    fused_forwards scope together with the phase's other jets.  No autograd (a target)."""
+    mlp.ensure_packed()
+    mlp.ensure_wsplit()
+    n, din = x.shape
+    if mlp.out_features != din or x.dtype != torch.float32 or not x.is_cuda:
+        raise UnsupportedPattern("advect_target: a d -> d fp32 GPU field")
+    x2 = x.detach() if x.is_contiguous() else x.detach().contiguous()
+    dev = x2.device
+    y = torch.empty(n, din, device=dev, dtype=torch.float32)
+    up = torch.empty(n, din, device=dev, dtype=torch.float32)
+    foot = torch.empty(n, din, device=dev, dtype=torch.float32)
+    cmode = (mlp.call_mode(nat.MODE_VALUE) & ~nat.MODE_MASK) | MIX_ADVECT
+    job = (x2, mlp.flat_params(), y, up, foot, None, n, din, (float(dt), float(lo), float(hi)))
+    key = (din, mlp.num_hidden_layers, mlp.kernel_width, cmode, dev)
+    if _Fused.pending is not None:
+        _Fused.pending.append((key, job))
+    else:
+        _launch_mixed(din, mlp.num_hidden_layers, mlp.kernel_width, cmode & ~nat.MODE_MASK, dev, [(MIX_ADVECT, job)])
+    return y, up
 
 
 def _launch_fused(jobs):
@@ -210,16 +251,16 @@ def _launch_fused(jobs):
         by_arch.setdefault((din, L, W, cmode & ~nat.MODE_MASK, dev), []).append((cmode & nat.MODE_MASK, js))
     for (din, L, W, pbits, dev), parts in by_arch.items():
         alljobs = [(m, j) for m, js in parts for j in js]
-        if (_MIXED and len(parts) > 1 and W == 128 and len(alljobs) <= nat.MAX_FWD_JOBS
-                and all(j[6] <= 40000 for _, j in alljobs)):
-            chunk = [j for _, j in alljobs]
-            modes = (ctypes.c_int * len(chunk))(*[m for m, _ in alljobs])
-            n = sum(j[6] for j in chunk)
-            key_dout = tuple(j[7] for j in chunk)
-            with _timed("fwdmix%d" % len(chunk), max(m for m, _ in alljobs), n, W, (din, key_dout, L)):
-                rc = lib.insr_siren_jet_fwd_mixed(_job_array(chunk), modes, len(chunk), din, chunk[0][7], L, W, pbits,
-                                                  nat.stream_of(dev))
-            nat.check(rc, "insr_siren_jet_fwd_mixed")
+        adv = any(m == MIX_ADVECT for m, _ in alljobs)
+        if adv or (_MIXED and len(parts) > 1 and W == 128 and len(alljobs) <= nat.MAX_FWD_JOBS
+                   and all(j[6] <= 40000 for _, j in alljobs)):
+            if adv and not (_MIXED and len(alljobs) <= nat.MAX_FWD_JOBS):  # targets alone, the rest as usual
+                tg = [(m, j) for m, j in alljobs if m == MIX_ADVECT]
+                for m, j in tg:
+                    _launch_mixed(din, L, W, pbits, dev, [(m, j)])
+                groups.pop((din, L, W, pbits | MIX_ADVECT, dev))
+                continue
+            _launch_mixed(din, L, W, pbits, dev, alljobs)
             for m, js in parts:
                 groups.pop((din, L, W, pbits | m, dev))
     for (din, L, W, cmode, dev), js in groups.items():  # output widths may differ per job

@@ -66,7 +66,7 @@ SIGNATURES = {
     "insr_siren_wsplit_offset": (_L, [_I, _I, _I, _I]),
     "insr_siren_wsplit_floats": (_L, [_I, _I]),
     "insr_siren_wsplit": (_I, [_P, _I, _I, _I, _I, _P]),
-    "insr_siren_jet_fwd_mixed": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _P]),
+    "insr_siren_jet_fwd_mixed": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _I, _P]),
     "insr_adam_step_nets": (_I, [_I, _P, _P, _P, _P, _P, _P, _P, _F, _F, _F, _I, _P]),
     "insr_jet_wide_launch_threads": (_I, [_L, _I, _I, _I, _I, _I, _P]),
     "insr_sq_loss_bwd": (_I, [_I, _P, _P, _P, _P, _L, _I, _F, _F, _F, _F, _F, _P, _P, _P, _P, _P, _P]),

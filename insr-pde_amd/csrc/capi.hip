@@ -659,16 +659,24 @@ int insr_siren_jet_fwd_multi(const InsrJetJob* jobs, int njobs, int din, int dou
   return 0;
 }
 
-int insr_siren_jet_fwd_mixed(const InsrJetJob* jobs, const int* modes, int njobs, int din, int dout, int L, int W,
-                             int prec_mode, void* stream) {
+int insr_siren_jet_fwd_mixed(const InsrJetJob* jobs, const int* modes, const float* scalars, int njobs, int din,
+                             int dout, int L, int W, int prec_mode, void* stream) {
   if (!jobs || !modes || njobs < 1 || njobs > INSR_MAX_FWD_JOBS) return INSR_EINVAL;
   if (prec_mode & INSR_MODE_MASK) return INSR_EINVAL;  // the per-job jet modes come from `modes`
   long total = 0;
   for (int k = 0; k < njobs; ++k) {
     const InsrJetJob& j = jobs[k];
+    const int dk = j.d_out > 0 ? j.d_out : dout;
+    if (modes[k] == INSR_MIX_ADVECT) {  // two value jets + the foot: f maps R^d -> R^d
+      if (dk != din || !scalars || (j.n > 0 && (!j.dy || !j.lap))) return INSR_EINVAL;
+      if (!shape_ok(din, dk, L, W, INSR_MODE_VALUE | prec_mode)) return INSR_EINVAL;
+      if (j.n < 0 || j.n > 0x7fffffffL || (j.n > 0 && (!j.x || !j.params || !j.y))) return INSR_EINVAL;
+      total += j.n;
+      continue;
+    }
     const int m = modes[k] | prec_mode;
     if (modes[k] & ~INSR_MODE_MASK) return INSR_EINVAL;
-    if (!shape_ok(din, j.d_out > 0 ? j.d_out : dout, L, W, m)) return INSR_EINVAL;
+    if (!shape_ok(din, dk, L, W, m)) return INSR_EINVAL;
     if (j.n < 0 || j.n > 0x7fffffffL || (j.n > 0 && (!j.x || !j.params || !j.y))) return INSR_EINVAL;
     if (j.n > 0 && modes[k] != INSR_MODE_VALUE && !j.dy) return INSR_EINVAL;
     if (j.n > 0 && modes[k] == INSR_MODE_LAP && !j.lap) return INSR_EINVAL;
@@ -691,15 +699,31 @@ int insr_siren_jet_fwd_mixed(const InsrJetJob* jobs, const int* modes, int njobs
       ++m;
     }
     if (m == 0) return 0;
+    float sc[3 * INSR_MAX_FWD_JOBS] = {};
+    for (int k = 0, q = 0; k < njobs; ++k)
+      if (jobs[k].n > 0) {
+        for (int r = 0; r < 3; ++r) sc[3 * q + r] = scalars ? scalars[3 * k + r] : 0.f;
+        ++q;
+      }
     switch (c.nqf) {
-      case 3: return dispatch_fwd_mixed_q<3>(c.NT, din, pk, md, m, dout, L, st);
-      case 2: return dispatch_fwd_mixed_q<2>(c.NT, din, pk, md, m, dout, L, st);
-      default: return dispatch_fwd_mixed_q<1>(c.NT, din, pk, md, m, dout, L, st);
+      case 3: return dispatch_fwd_mixed_q<3>(c.NT, din, pk, md, sc, m, dout, L, st);
+      case 2: return dispatch_fwd_mixed_q<2>(c.NT, din, pk, md, sc, m, dout, L, st);
+      default: return dispatch_fwd_mixed_q<1>(c.NT, din, pk, md, sc, m, dout, L, st);
     }
   }
   for (int k = 0; k < njobs; ++k) {  // other widths / exact fp32: one launch per job
     const InsrJetJob& j = jobs[k];
     if (j.n == 0) continue;
+    if (modes[k] == INSR_MIX_ADVECT) {  // f(x), the foot, f(foot)
+      int rc = insr_siren_jet_fwd(j.x, j.n, din, din, L, W, INSR_MODE_VALUE | prec_mode, j.params, j.dy, nullptr,
+                                  nullptr, nullptr, stream);
+      if (!rc) rc = insr_axpy_clamp(j.x, j.dy, -scalars[3 * k], scalars[3 * k + 1], scalars[3 * k + 2], j.lap,
+                                    j.n * din, stream);
+      if (!rc) rc = insr_siren_jet_fwd(j.lap, j.n, din, din, L, W, INSR_MODE_VALUE | prec_mode, j.params, j.y,
+                                       nullptr, nullptr, nullptr, stream);
+      if (rc) return rc;
+      continue;
+    }
     const int rc = insr_siren_jet_fwd(j.x, j.n, din, j.d_out > 0 ? j.d_out : dout, L, W, modes[k] | prec_mode,
                                       j.params, j.y, j.dy, j.lap, j.act, stream);
     if (rc) return rc;

@@ -331,8 +331,8 @@ int dispatch_wide_bwd_q(int NT, int S, bool LAP, const float* x, int N, int din,
                         float* grad, int accumulate, hipStream_t st);
 long wide_work_floats(long n, int din, int dout, int L, int W, int S);
 template <int NQ>
-int dispatch_fwd_mixed_q(int NT, int din, const InsrJetJob* jobs, const int* modes, int njobs, int dout, int L,
-                         hipStream_t st);
+int dispatch_fwd_mixed_q(int NT, int din, const InsrJetJob* jobs, const int* modes, const float* scalars, int njobs,
+                         int dout, int L, hipStream_t st);
 // the pre-split weight planes of (prm, shape) written to `planes` (wsplit_offset floats after prm
 // in a params buffer of INSR_MODE_WSPLIT), one launch
 int wsplit_launch(const float* prm, int din, int dout, int L, int W, float* planes, hipStream_t st);

@@ -424,18 +424,26 @@ __global__ __launch_bounds__(X6Geo<NT>::THREADS, (x6_multi_min_waves<NT, S>())) 
 struct FwdMixX6 {
   InsrJetJob job[kFwdJobs];
   int first[kFwdJobs + 1];
-  int mode[kFwdJobs];  // INSR_MODE_VALUE / GRAD / LAP
+  int mode[kFwdJobs];     // INSR_MODE_VALUE / GRAD / LAP / INSR_MIX_ADVECT
+  float sc[kFwdJobs][3];  // INSR_MIX_ADVECT: dt, lo, hi
   int njobs;
 };
 
-template <int NQ, int NT, int DIN>
+// BODIES: the job kinds a kernel instance carries (bit m = jet mode m, bit 3 = INSR_MIX_ADVECT):
+// its registers and LDS are those of the largest body it holds, so a launch takes the smallest
+// instance that covers its jobs (value + advect: 62 VGPRs, four blocks per CU; with a
+// Laplacian body: 90)
+constexpr int kMixV = 1, kMixG = 2, kMixL = 4, kMixA = 8;
+
+template <int NQ, int NT, int DIN, int BODIES>
 constexpr size_t fwd_mix_lds_bytes() {
-  constexpr size_t a = fwd_x6_lds_bytes<NQ, NT, 1, 2>(), b = fwd_x6_lds_bytes<NQ, NT, 1 + DIN, 1>();
-  constexpr size_t c = DIN <= 2 ? fwd_x6_lds_bytes<NQ, NT, 2 + DIN, 1>() : 0;
+  constexpr size_t a = (BODIES & (kMixV | kMixA)) ? fwd_x6_lds_bytes<NQ, NT, 1, 2>() : 0;
+  constexpr size_t b = (BODIES & kMixG) ? fwd_x6_lds_bytes<NQ, NT, 1 + DIN, 1>() : 0;
+  constexpr size_t c = (DIN <= 2 && (BODIES & kMixL)) ? fwd_x6_lds_bytes<NQ, NT, 2 + DIN, 1>() : 0;
   return a > b ? (a > c ? a : c) : (b > c ? b : c);
 }
 
-template <int NQ, int NT, int DIN>
+template <int NQ, int NT, int DIN, int BODIES>
 __global__ __launch_bounds__(X6Geo<NT>::THREADS, 4) void jet_fwd_x6_mixed(const FwdMixX6 jobs, int dout, int L) {
   const int b = blockIdx.x;
   int k = 0;
@@ -447,33 +455,61 @@ __global__ __launch_bounds__(X6Geo<NT>::THREADS, 4) void jet_fwd_x6_mixed(const 
   int tile0, cnt;
   switch (jobs.mode[k]) {
     case INSR_MODE_VALUE:
-      block_tiles(lb, (int)jb.n, 2, 0, tile0, cnt);
-      fwd_x6_block<NQ, NT, 1, false, 2>(jb.x, (int)jb.n, DIN, dk, L, jb.params, jb.y, jb.dy, jb.lap, jb.act, tile0,
-                                        cnt);
+      if constexpr ((BODIES & kMixV) != 0) {
+        block_tiles(lb, (int)jb.n, 2, 0, tile0, cnt);
+        fwd_x6_block<NQ, NT, 1, false, 2>(jb.x, (int)jb.n, DIN, dk, L, jb.params, jb.y, jb.dy, jb.lap, jb.act, tile0,
+                                          cnt);
+      }
       break;
     case INSR_MODE_GRAD:
-      fwd_x6_block<NQ, NT, 1 + DIN, false, 1>(jb.x, (int)jb.n, DIN, dk, L, jb.params, jb.y, jb.dy, jb.lap, jb.act, lb,
-                                              1);
+      if constexpr ((BODIES & kMixG) != 0)
+        fwd_x6_block<NQ, NT, 1 + DIN, false, 1>(jb.x, (int)jb.n, DIN, dk, L, jb.params, jb.y, jb.dy, jb.lap, jb.act,
+                                                lb, 1);
       break;
-    default:
-      if constexpr (DIN <= 2)
+    case INSR_MODE_LAP:
+      if constexpr (DIN <= 2 && (BODIES & kMixL) != 0)
         fwd_x6_block<NQ, NT, 2 + DIN, true, 1>(jb.x, (int)jb.n, DIN, dk, L, jb.params, jb.y, jb.dy, jb.lap, jb.act,
                                                lb, 1);
       break;
+    default: {  // INSR_MIX_ADVECT: y = f(clamp(x - dt f(x), lo, hi)), f(x) -> dy, the foot -> lap
+      if constexpr ((BODIES & kMixA) == 0) break;
+      // (fluid/model.py:96-97; every quantity of a point stays in its block: one launch for
+      // the frozen field's two value jets and the foot between them)
+      const int n = (int)jb.n;
+      block_tiles(lb, n, 2, 0, tile0, cnt);
+      float* up = jb.dy;
+      float* foot = jb.lap;
+      fwd_x6_block<NQ, NT, 1, false, 2>(jb.x, n, DIN, dk, L, jb.params, up, nullptr, nullptr, nullptr, tile0, cnt);
+      // the block's own global writes, read back by its other waves: workgroup scope (the
+      // stores drain before the barrier; the lines were never cached in this CU's L1)
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+      __syncthreads();
+      const float a = -jobs.sc[k][0], lo = jobs.sc[k][1], hi = jobs.sc[k][2];
+      for (int i = threadIdx.x; i < cnt * 16 * DIN; i += blockDim.x) {
+        const long p = (long)tile0 * 16 + i / DIN;
+        const int kk = i % DIN;
+        if (p < n) foot[p * DIN + kk] = fminf(fmaxf(fmaf(a, up[p * dk + kk], jb.x[p * DIN + kk]), lo), hi);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+      __syncthreads();
+      fwd_x6_block<NQ, NT, 1, false, 2>(foot, n, DIN, dk, L, jb.params, jb.y, nullptr, nullptr, nullptr, tile0, cnt);
+      break;
+    }
   }
 }
 
-template <int NQ, int NT, int DIN>
-int launch_fwd_x6_mixed_t(const InsrJetJob* jobs, const int* modes, int njobs, int dout, int L, hipStream_t st) {
-  constexpr size_t lds = fwd_mix_lds_bytes<NQ, NT, DIN>();
+template <int NQ, int NT, int DIN, int BODIES>
+int launch_fwd_x6_mixed_t(const InsrJetJob* jobs, const int* modes, const float* scalars, int njobs, int dout, int L,
+                          hipStream_t st) {
+  constexpr size_t lds = fwd_mix_lds_bytes<NQ, NT, DIN, BODIES>();
   if constexpr (lds > kLdsMax) {
     return INSR_EINVAL;
   } else {
     if (njobs < 1 || njobs > kFwdJobs) return INSR_EINVAL;
     static bool attr_set = false;
     if (!attr_set) {
-      (void)hipFuncSetAttribute((const void*)jet_fwd_x6_mixed<NQ, NT, DIN>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)lds);
+      (void)hipFuncSetAttribute((const void*)jet_fwd_x6_mixed<NQ, NT, DIN, BODIES>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       attr_set = true;
     }
     FwdMixX6 pk{};
@@ -482,14 +518,16 @@ int launch_fwd_x6_mixed_t(const InsrJetJob* jobs, const int* modes, int njobs, i
       if (modes[k] == INSR_MODE_LAP && DIN > 2) return INSR_EINVAL;
       pk.job[k] = jobs[k];
       pk.mode[k] = modes[k];
+      for (int q = 0; q < 3; ++q) pk.sc[k][q] = scalars ? scalars[3 * k + q] : 0.f;
       pk.first[k] = nb;
       const long tiles = (jobs[k].n + 15) / 16;
-      nb += (int)(modes[k] == INSR_MODE_VALUE ? (tiles + 1) / 2 : tiles);
+      nb += (int)(modes[k] == INSR_MODE_VALUE || modes[k] == INSR_MIX_ADVECT ? (tiles + 1) / 2 : tiles);
     }
     pk.first[njobs] = nb;
     pk.njobs = njobs;
     if (nb == 0) return 0;
-    hipLaunchKernelGGL((jet_fwd_x6_mixed<NQ, NT, DIN>), dim3(nb), dim3(X6Geo<NT>::THREADS), lds, st, pk, dout, L);
+    hipLaunchKernelGGL((jet_fwd_x6_mixed<NQ, NT, DIN, BODIES>), dim3(nb), dim3(X6Geo<NT>::THREADS), lds, st, pk, dout,
+                       L);
     return (int)hipGetLastError();
   }
 }

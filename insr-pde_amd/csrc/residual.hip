@@ -215,7 +215,7 @@ __global__ __launch_bounds__(256) void axpy_clamp_kernel(const float* __restrict
                                                          float alpha, float lo, float hi, float* __restrict__ out,
                                                          long n) {
   for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256)
-    out[i] = fminf(fmaxf(x[i] + alpha * y[i], lo), hi);
+    out[i] = fminf(fmaxf(fmaf(alpha, y[i], x[i]), lo), hi);
 }
 
 }  // namespace insr

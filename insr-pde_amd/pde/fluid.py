@@ -15,7 +15,8 @@ import os
 import numpy as np
 import torch
 
-from base import (BaseModel, axpy_clamp, divergence, fused_forwards, fused_mse, gradient, jacobian, laplace,
+from base import (BaseModel, advect_target, axpy_clamp, divergence, fused_forwards, fused_mse, gradient, jacobian,
+                  laplace,
                   merge_samples, mse_term, sample_boundary2D_pair, sample_boundary2D_separate, sample_random,
                   sample_random_and_bands2D, sample_uniform, sq_losses, wall_mse, wall_term)
 from base.diff_ops import jacobian_only
@@ -179,27 +180,17 @@ class Fluid2DModel(BaseModel):
     def _fused_pair(self):
         return getattr(self.cfg, "insr_fuse_forwards", True) and not getattr(self.cfg, "insr_nograd_stream", False)
 
-    # The boundary band's value jet (a few hundred points, a latency-bound launch of its own)
-    # joins the same launch as 1-tile blocks placed first in the grid (insr_siren_jet_fwd_multi).
-    def _prev_and_current(self, x):
-        """(u over [x; bands], n, nb, u_prev(x) detached): the trainable field's value jet over
-        the merged batch (interior + wall bands: one jet and one reverse jet) and the frozen
-        field's at x, in one launch."""
-        xa, n, nb = self._merged(x)
-        with fused_forwards():
-            with torch.no_grad():
-                u_prev = self.velocity_field_prev(x)
-            ua = self.velocity_field(xa)
-        return ua, n, nb, u_prev.detach()
-
     @BaseModel._training_loop
     def _advect_velocity(self):
         x = self._sample_in_training()
         if self._fused_pair() and not getattr(self.cfg, "insr_band_stream", False):
-            ua, n, nb, u_prev = self._prev_and_current(x)
-            with torch.no_grad():
-                foot = axpy_clamp(x.detach(), u_prev, -self.cfg.dt, -1.0, 1.0)  # clamp(x - dt u_prev, -1, 1)
-                u_target = self.velocity_field_prev(foot)
+            xa, n, nb = self._merged(x)
+            # the frozen field's semi-Lagrangian target u_prev(clamp(x - dt u_prev(x), -1, 1))
+            # (two value jets and the foot, point-local: one job) beside the trainable field's
+            # value jet over [x; bands]: one mixed launch
+            with fused_forwards():
+                u_target, _ = advect_target(self.velocity_field_prev, x, self.cfg.dt, -1.0, 1.0)
+                ua = self.velocity_field(xa)
             # mean((u - u_target)^2) over the interior rows and the wall terms on the band rows,
             # one launch
             main, bc = sq_losses(mse_term(ua, u_target, count=u_target.numel()), wall_term(ua, nb, row0=n))

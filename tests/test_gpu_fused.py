@@ -238,3 +238,26 @@ def test_mixed_mode_launch_matches_single_launches(B, n):
     for phase in (pressure_phase, projection):
         for u, v in zip(phase(False), phase(True)):
             assert torch.equal(u, v), phase.__name__
+
+
+@pytest.mark.parametrize("fused", [False, True])
+def test_advect_target_matches_the_three_steps(B, fused):
+    """base.advect_target (INSR_MIX_ADVECT: two value jets of the frozen field and the foot
+    clamp(x - dt f(x), -1, 1) in one job, fluid/model.py:96-97) equals f(x), the axpy foot and
+    f(foot) launched separately, bit for bit -- alone and inside a mixed launch beside the
+    trainable field's value jet."""
+    prev, cur = _net(B, "fluid_vel", 4), _net(B, "fluid_vel", 5)
+    g = torch.Generator().manual_seed(23)
+    x = (torch.rand(16384, 2, generator=g) * 2 - 1).cuda()
+    xa = (torch.rand(16708, 2, generator=g) * 2 - 1).cuda()
+    dt = 0.05
+    with torch.no_grad():
+        up_ref = prev(x)
+        foot = B.axpy_clamp(x, up_ref, -dt, -1.0, 1.0)
+        tgt_ref = prev(foot)
+        ua_ref = cur(xa)
+    ctx = B.fused_forwards() if fused else contextlib.nullcontext()
+    with torch.no_grad(), ctx:
+        tgt, up = B.advect_target(prev, x, dt, -1.0, 1.0)
+        ua = cur(xa)
+    assert torch.equal(up, up_ref) and torch.equal(tgt, tgt_ref) and torch.equal(ua, ua_ref)
