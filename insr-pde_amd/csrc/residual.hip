@@ -77,11 +77,13 @@ __global__ __launch_bounds__(kLossThreads) void sq_loss_fwd_kernel(int kind, Los
     out[0] = scale * part;
     return;
   }
-  work[blockIdx.x] = part;
-  __threadfence();  // release this block's partial before taking a ticket
+  // cross-block hand-off without an L2 write-back (MI355X_MICROARCH.md, hand-off table row 1):
+  // the partial leaves as an sc1 store, this lane waits for it, then takes the ticket with an
+  // agent-scope atomic; the last block reads every partial with sc1 loads
+  __hip_atomic_store(work + blockIdx.x, part, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   unsigned* ticket = reinterpret_cast<unsigned*>(work + kLossMaxBlocks);
   if (atomicAdd(ticket, 1u) != gridDim.x - 1) return;
-  __threadfence();  // acquire: every other block's partial is visible
   float tot = 0.f;
   for (unsigned k = 0; k < gridDim.x; ++k)  // block order: the sum is deterministic
     tot += __hip_atomic_load(work + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -197,11 +199,11 @@ __global__ __launch_bounds__(kLossThreads) void sq_loss_group_kernel(const LossG
     return;
   }
   float* wk = work + (long)k * (kLossMaxBlocks + 1);
-  wk[blk] = part;
-  __threadfence();  // release this block's partial before taking a ticket
+  // sc1 store + wait + agent atomic ticket; sc1 loads by the last block (no L2 write-back)
+  __hip_atomic_store(wk + blk, part, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   unsigned* ticket = reinterpret_cast<unsigned*>(wk + kLossMaxBlocks);
   if (atomicAdd(ticket, 1u) != (unsigned)nblk - 1) return;
-  __threadfence();  // acquire: every other block's partial is visible
   float tot = 0.f;
   for (int q = 0; q < nblk; ++q)  // block order: the sum is deterministic
     tot += __hip_atomic_load(wk + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
