@@ -443,8 +443,11 @@ constexpr size_t fwd_mix_lds_bytes() {
   return a > b ? (a > c ? a : c) : (b > c ? b : c);
 }
 
+// with a Laplacian body: 6 waves per SIMD (80 VGPRs, 11 spills; three blocks per CU) measured
+// 0.5% faster per headline step than 4 (profiles/r02/mix_lap_waves_ab)
 template <int NQ, int NT, int DIN, int BODIES>
-__global__ __launch_bounds__(X6Geo<NT>::THREADS, 4) void jet_fwd_x6_mixed(const FwdMixX6 jobs, int dout, int L) {
+__global__ __launch_bounds__(X6Geo<NT>::THREADS, (BODIES & kMixL) ? 6 : 4) void jet_fwd_x6_mixed(const FwdMixX6 jobs,
+                                                                                              int dout, int L) {
   const int b = blockIdx.x;
   int k = 0;
 #pragma unroll
