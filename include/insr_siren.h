@@ -257,7 +257,8 @@ int insr_reduce_partials_strided(const float* partial, int n_blocks, long count,
 #define INSR_OPT_BC2SQRT 5
 #define INSR_OPT_FACTOR 6
 #define INSR_OPT_MINLR 7
-#define INSR_OPT_NFLOATS 8
+#define INSR_OPT_TICKET 8 /* (as unsigned) insr_adam_plateau_step_nets' last-block ticket, 0 */
+#define INSR_OPT_NFLOATS 9
 
 /* t += 1; refresh step_size and sqrt(1-b2^t) (explicit-prepare convention). */
 int insr_adam_prepare(float* opt_state, float beta1, float beta2, void* stream);
@@ -278,6 +279,13 @@ int insr_plateau_step(float* opt_state, const float* loss, int patience, int adv
 int insr_adam_step_nets(int count, float* const* params, const float* const* grads, float* const* exp_avg,
                         float* const* exp_avg_sq, const long* sizes, const int* shapes, const float* opt_state,
                         float beta1, float beta2, float eps, int step_offset, void* stream);
+/* insr_adam_step_nets (step_offset 1) followed by insr_plateau_step(opt_state, loss, patience,
+ * advance_step = 1) in the SAME launch: the last block to finish (agent-scope ticket in
+ * opt_state[INSR_OPT_TICKET], reset by it) runs the scheduler step after every block has read
+ * the lr it updates.  base/baseModel.py:79-81 (optimizer.step(); scheduler.step(loss)). */
+int insr_adam_plateau_step_nets(int count, float* const* params, const float* const* grads, float* const* exp_avg,
+                                float* const* exp_avg_sq, const long* sizes, const int* shapes, float* opt_state,
+                                float beta1, float beta2, float eps, const float* loss, int patience, void* stream);
 int insr_adam_step_multi(int count, float* const* params, const float* const* grads, float* const* exp_avg,
                          float* const* exp_avg_sq, const long* sizes, const float* opt_state, float beta1,
                          float beta2, float eps, int step_offset, void* stream);

@@ -25,7 +25,8 @@ def jet_prec(p):
     return (int(p) + 1) << MODE_PREC_SHIFT
 LOSS_COMBO, LOSS_BANDS = 0, 1
 OPT_LR, OPT_STEP, OPT_BEST, OPT_BAD, OPT_STEPSIZE, OPT_BC2SQRT, OPT_FACTOR, OPT_MINLR = range(8)
-OPT_NFLOATS = 8
+OPT_TICKET = 8  # the fused Adam + plateau launch's last-block ticket (0 between launches)
+OPT_NFLOATS = 9
 ADAM_MAX_TENSORS = 8
 
 _P = ctypes.c_void_p
@@ -68,6 +69,7 @@ SIGNATURES = {
     "insr_siren_wsplit": (_I, [_P, _I, _I, _I, _I, _P]),
     "insr_siren_jet_fwd_mixed": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _I, _P]),
     "insr_adam_step_nets": (_I, [_I, _P, _P, _P, _P, _P, _P, _P, _F, _F, _F, _I, _P]),
+    "insr_adam_plateau_step_nets": (_I, [_I, _P, _P, _P, _P, _P, _P, _P, _F, _F, _F, _P, _I, _P]),
     "insr_jet_wide_launch_threads": (_I, [_L, _I, _I, _I, _I, _I, _P]),
     "insr_sq_loss_bwd": (_I, [_I, _P, _P, _P, _P, _L, _I, _F, _F, _F, _F, _F, _P, _P, _P, _P, _P, _P]),
     "insr_jet_set_split_tiles": (None, [_I, _I, _I]),

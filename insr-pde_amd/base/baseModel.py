@@ -182,9 +182,12 @@ class BaseModel(ABC):
         self.optimizer.zero_grad()
         self._backward(loss_dict)
         synced = self._dp_sync(loss_dict)
-        self.optimizer.step()
-        if self.scheduler is not None:
-            self.scheduler.step(synced['main'])
+        if self.scheduler is not None and getattr(self.scheduler, "fusable", False):
+            self.optimizer.step(plateau=(self.scheduler, synced['main']))  # Adam + plateau: one launch
+        else:
+            self.optimizer.step()
+            if self.scheduler is not None:
+                self.scheduler.step(synced['main'])
         return synced
 
     def _backward(self, loss_dict):

@@ -94,10 +94,11 @@ class FusedAdam:
             self._pending_advance = False
 
     @torch.no_grad()
-    def step(self):
+    def step(self, plateau=None):
         """One Adam update of every buffer whose grad exists, in ONE launch.
         Uses t = state[STEP] + 1; the step counter itself is advanced by the
-        scheduler's plateau launch that follows (or lazily, without one)."""
+        scheduler's plateau launch that follows (or lazily, without one).
+        plateau = (DevicePlateau, metric): its step runs in the same launch (last block)."""
         import ctypes
         lib = nat.lib()
         self._advance_pending()
@@ -116,21 +117,31 @@ class FusedAdam:
         b1, b2 = self.betas
         st = nat.stream_of(self.device)
         chunks = [bufs[i:i + nat.ADAM_MAX_TENSORS] for i in range(0, len(bufs), nat.ADAM_MAX_TENSORS)]
+        metric = plateau[0]._metric(plateau[1]) if plateau is not None else None
+        if metric is not None and not chunks:
+            plateau[0].step(plateau[1])
+            metric = None
         for ci, chunk in enumerate(chunks):
             k = len(chunk)
             arr = lambda j: (ctypes.c_void_p * k)(*[c[j].data_ptr() for c in chunk])  # noqa: E731
             sizes = (ctypes.c_long * k)(*[c[0].numel() for c in chunk])
             # network buffers: the same launch rewrites their pre-split weight planes
             shapes = (ctypes.c_int * (4 * k))(*[v for c in chunk for v in c[4]])
-            nat.check(lib.insr_adam_step_nets(k, arr(0), arr(1), arr(2), arr(3), sizes, shapes, nat.ptr(self.state),
-                                              b1, b2, self.eps, 1, st), "insr_adam_step_nets")
+            if metric is not None and ci == len(chunks) - 1:  # + the scheduler step (advances t)
+                nat.check(lib.insr_adam_plateau_step_nets(k, arr(0), arr(1), arr(2), arr(3), sizes, shapes,
+                                                          nat.ptr(self.state), b1, b2, self.eps, nat.ptr(metric),
+                                                          plateau[0].patience, st), "insr_adam_plateau_step_nets")
+            else:
+                nat.check(lib.insr_adam_step_nets(k, arr(0), arr(1), arr(2), arr(3), sizes, shapes,
+                                                  nat.ptr(self.state), b1, b2, self.eps, 1, st), "insr_adam_step_nets")
         for mlp in stepped:  # planes current: no refresh before the next jet
             mlp.mark_wsplit_current()
-        self._pending_advance = True
+        self._pending_advance = plateau is None
 
 
 class DevicePlateau:
     """ReduceLROnPlateau(mode='min', threshold=1e-4 rel, cooldown=0, eps=1e-8) on the device."""
+    fusable = True  # FusedAdam.step(plateau=(self, metric)) runs this step in the Adam launch
 
     def __init__(self, optimizer, factor=0.1, patience=10, min_lr=0.0, verbose=None):
         self.optimizer = optimizer

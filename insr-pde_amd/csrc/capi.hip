@@ -378,6 +378,8 @@ struct AdamList {
   long n[INSR_ADAM_MAX_TENSORS];
   long start[INSR_ADAM_MAX_TENSORS + 1];  // prefix sums of n
   int shape[INSR_ADAM_MAX_TENSORS][4];    // SIREN (d_in, d_out, L, W) of a flat buffer with weight planes, else 0s
+  const float* loss;                      // != NULL: the last block runs the plateau step on it
+  int patience;
   int count;
 };
 
@@ -423,7 +425,7 @@ __device__ __forceinline__ void adam_wsplit(float* base, const int (&sh)[4], lon
 // so the bias corrections need no separate prepare launch); torch's op order:
 //   m.lerp_(g, 1-b1); v.mul_(b2).addcmul_(g, g, 1-b2);
 //   p.addcdiv_(m, sqrt(v)/sqrt(1-b2^t) + eps, -lr/(1-b1^t))
-__global__ void adam_multi_kernel(AdamList L, const float* __restrict__ st, float b1, float b2, float eps,
+__global__ void adam_multi_kernel(AdamList L, float* __restrict__ st, float b1, float b2, float eps,
                                   int step_offset) {
   __shared__ float sc[2];
   if (threadIdx.x == 0) {
@@ -450,6 +452,16 @@ __global__ void adam_multi_kernel(AdamList L, const float* __restrict__ st, floa
     const float pn = L.p[k][i] - step_size * (mi / denom);
     L.p[k][i] = pn;
     if (L.shape[k][2] > 0) adam_wsplit(L.p[k], L.shape[k], i, pn);
+  }
+  if (L.loss) {  // fused scheduler step: every block read lr / t above before it takes a ticket
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      unsigned* ticket = reinterpret_cast<unsigned*>(st + INSR_OPT_TICKET);
+      if (atomicAdd(ticket, 1u) == gridDim.x - 1) {
+        plateau_update(st, L.loss, L.patience, 1);
+        atomicExch(ticket, 0u);
+      }
+    }
   }
 }
 
@@ -903,11 +915,32 @@ int insr_adam_step_multi(int count, float* const* params, const float* const* gr
                              stream);
 }
 
+static int adam_launch(int count, float* const* params, const float* const* grads, float* const* exp_avg,
+                       float* const* exp_avg_sq, const long* sizes, const int* shapes, float* st, float b1, float b2,
+                       float eps, int step_offset, const float* loss, int patience, void* stream);
+
 int insr_adam_step_nets(int count, float* const* params, const float* const* grads, float* const* exp_avg,
                         float* const* exp_avg_sq, const long* sizes, const int* shapes, const float* st, float b1,
                         float b2, float eps, int step_offset, void* stream) {
+  return adam_launch(count, params, grads, exp_avg, exp_avg_sq, sizes, shapes, const_cast<float*>(st), b1, b2, eps,
+                     step_offset, nullptr, 0, stream);
+}
+
+int insr_adam_plateau_step_nets(int count, float* const* params, const float* const* grads, float* const* exp_avg,
+                                float* const* exp_avg_sq, const long* sizes, const int* shapes, float* st, float b1,
+                                float b2, float eps, const float* loss, int patience, void* stream) {
+  if (!loss) return INSR_EINVAL;
+  return adam_launch(count, params, grads, exp_avg, exp_avg_sq, sizes, shapes, st, b1, b2, eps, 1, loss, patience,
+                     stream);
+}
+
+static int adam_launch(int count, float* const* params, const float* const* grads, float* const* exp_avg,
+                       float* const* exp_avg_sq, const long* sizes, const int* shapes, float* st, float b1, float b2,
+                       float eps, int step_offset, const float* loss, int patience, void* stream) {
   if (count < 1 || count > INSR_ADAM_MAX_TENSORS || !st) return INSR_EINVAL;
   AdamList L;
+  L.loss = loss;
+  L.patience = patience;
   L.count = count;
   L.start[0] = 0;
   for (int k = 0; k < count; ++k) {
@@ -926,7 +959,7 @@ int insr_adam_step_nets(int count, float* const* params, const float* const* gra
     L.start[k + 1] = L.start[k] + sizes[k];
   }
   const long total = L.start[count];
-  if (total == 0) return 0;
+  if (total == 0) return loss ? insr_plateau_step(st, loss, patience, 1, stream) : 0;
   long blocks = (total + 255) / 256;
   if (blocks > 1024) blocks = 1024;
   hipLaunchKernelGGL(adam_multi_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, L, st, b1, b2,

@@ -31,7 +31,10 @@ def scripted_losses():
     return seq
 
 
-def test_device_plateau_follows_torch_scheduler(B):
+@pytest.mark.parametrize("fused", [False, True])
+def test_device_plateau_follows_torch_scheduler(B, fused):
+    """fused: FusedAdam.step(plateau=...) -- the scheduler step in the Adam launch's last block
+    (insr_adam_plateau_step_nets), as BaseModel._update_network issues it."""
     torch.manual_seed(0)
     net = B.MLP(2, 1, 1, 32, nonlinearity="sine").cuda()
     opt = B.FusedAdam([{"params": list(net.parameters()), "lr": 1e-4, "module": net}])
@@ -42,8 +45,11 @@ def test_device_plateau_follows_torch_scheduler(B):
     lrs, tlrs = [], []
     for v in scripted_losses():
         net.flat_grad_buffer().normal_()
-        opt.step()
-        sched.step(torch.tensor([v], device="cuda"))
+        if fused:
+            opt.step(plateau=(sched, torch.tensor([v], device="cuda")))
+        else:
+            opt.step()
+            sched.step(torch.tensor([v], device="cuda"))
         tsched.step(v)
         st = opt.state.cpu()
         lrs.append(float(st[B._native.OPT_LR]))
@@ -104,3 +110,29 @@ def test_phase_loop_early_stop(B, graph):
     m._fit()
     assert m.train_step == _expected_stop() + 1
     assert m.optimizer.param_groups[0]["lr"] <= 1.1e-8
+
+
+def test_fused_adam_plateau_equals_two_launches(B):
+    """Parameters, moments and optimiser state after 12 fused Adam + plateau launches equal the
+    separate insr_adam_step_nets + insr_plateau_step launches bit for bit."""
+    out = []
+    for fused in (False, True):
+        torch.manual_seed(1)
+        net = B.MLP(2, 2, 2, 64, nonlinearity="sine").cuda()
+        opt = B.FusedAdam([{"params": list(net.parameters()), "lr": 1e-3, "module": net}])
+        sched = B.DevicePlateau(opt, factor=0.5, patience=2, min_lr=1e-6)
+        g = torch.Generator(device="cuda").manual_seed(2)
+        for v in scripted_losses()[:12]:
+            net.flat_grad_buffer().copy_(torch.randn(net.param_count, device="cuda", generator=g))
+            loss = torch.tensor([v], device="cuda")
+            if fused:
+                opt.step(plateau=(sched, loss))
+            else:
+                opt.step()
+                sched.step(loss)
+        torch.cuda.synchronize()
+        out.append((net.flat_params().clone(), opt._nets[0][1].clone(), opt._nets[0][2].clone(),
+                    opt.state[:B._native.OPT_TICKET].clone(), int(opt.state[B._native.OPT_TICKET].view(torch.int32))))
+    for u, v in zip(out[0][:4], out[1][:4]):
+        assert torch.equal(u, v)
+    assert out[1][4] == 0  # the ticket is left at zero
