@@ -20,7 +20,7 @@ import numpy as np
 import torch
 
 from base import BaseModel, fused_forwards, fused_mse, merge_samples, sample_random, sample_uniform, svd_energy
-from base.diff_ops import jacobian_nosync
+from base.diff_ops import jacobian_only
 
 
 
@@ -204,7 +204,7 @@ class ElasticityModel(BaseModel):
         total = 0
         if 'arap' in self.energy or 'volume' in self.energy:
             # both singular-value terms in one fused HIP launch each way (torch.svd + ~12 ops in the reference)
-            J, _ = jacobian_nosync(qa, xa)  # status unused (as in the reference): no host sync
+            J = jacobian_only(qa, xa)  # the status is unused (as in the reference): no NaN scan
             total = svd_energy(J, self.ratio_arap if 'arap' in self.energy else 0.0,
                                self.ratio_volume if 'volume' in self.energy else 0.0, count=n)
         for term in self.energy:
