@@ -66,6 +66,9 @@ def parse():
                     help="matrix-core precision of every jet: fp32 (fp32-accurate split-bf16, the parity "
                          "config), bf16x3 (3 bf16 products) or bf16 (1 product; BASELINE configs[4] "
                          "'mixed fp32/bf16 MFMA')")
+    ap.add_argument("--api", choices=["fused", "plain"], default="fused",
+                    help="fluid: 'plain' runs pde/fluid_plain.py, phase bodies written only against the "
+                         "reference's base API (separate band samplers, torch residuals) -- the drop-in case")
     ap.add_argument("--band-stream", action="store_true", help="fluid: boundary-band jets on a side stream")
     ap.add_argument("--nograd-stream", action="store_true", help="fluid: no-grad jets on a side stream")
     ap.add_argument("--cpu-seconds", type=float, default=25.0, help="budget of the CPU-baseline sample")
@@ -175,7 +178,9 @@ def build_model(args, world, rank):
         # elasticity draws the global batch and keeps its rank's slice (strong); weak: no slicing
         cfg.insr_dp_weak = args.scaling == "weak"
     torch.manual_seed(1234)  # identical weights on every rank
-    if wl["pde"] == "fluid":
+    if wl["pde"] == "fluid" and args.api == "plain":
+        from pde.fluid_plain import Fluid2DPlainModel as M
+    elif wl["pde"] == "fluid":
         from pde.fluid import Fluid2DModel as M
     elif wl["pde"] == "advection":
         from pde.advection import Advection1DModel as M
@@ -499,7 +504,7 @@ def main():
         "config": {"workload": args.config, "model": wl["model"],
                    "points_per_phase_iter": n_all, "phases": nph, "global_batch": n_all,
                    "seq_len": None, "parallelism": f"dp{world}", "graph": not args.no_graph,
-                   "precision": args.precision},
+                   "precision": args.precision, "api": args.api},
         "process_group": {"backend": args.backend if world > 1 else None, "world_size": world,
                           "rank_devices": args.rank_devices},
     }

@@ -371,6 +371,63 @@ int insr_svd_energy_bwd(const float* J, long n, int d, float ratio_arap, float r
                         float* gJ, void* stream);
 
 /*
+ * The elastodynamics energy of one elasticity iteration in ONE launch, with its gradient
+ * for a unit seed (elasticity/model.py:131-186, elasticity/losses.py:6-20 and the 2-D case
+ * of :22-39).  Replaces the jacobian + torch.svd + ~20 aten launches per direction of the
+ * reference's energy, and insr_svd_energy_fwd/bwd + the torch terms here.
+ * Rows [0, n) of f / J are the interior points x (q = f + x, q_prev = f_prev + x, q_pp =
+ * f_pp + x, qdot = (q - q_prev) / dt); rows [row_l, row_l + n_l) and [row_r, row_r + n_r)
+ * the fixed points of the positional constraints.  Terms (ratio[t] = 0 switches one off):
+ *   ARAP            ratio * sum (s_i - 1)^2          s = singular values of J + I
+ *   VOLUME          ratio * sum (prod s_i - 1)^2
+ *   KINEMATICS      ratio * sum (qdot - qdot_prev)^2, qdot_prev = (q_prev - q_pp) / dt
+ *   EXTERNAL        -dt * sum qdot . ext               (ratio: on / off)
+ *   CONSTRAINT      ratio * sum |f(x_l)|^2
+ *   CONSTRAINT_RIGHT ratio * sum |f(x_r) - target|^2  (target = +-offset)
+ *   COLLISION       -dt * sum_{q_z < h} qdot_z ratio (h - q_z)   (plane, z = last coordinate)
+ *   SPHERE          -dt * sum_{|q - c| < R} qdot . ratio |q - c| dir   (d = 2 only)
+ * *out = the terms of order[0 .. n_order) added in that order (cfg.energy); terms[t] = term t
+ * (terms may be NULL).  gf (rows, d) / gJ (rows, d, d) (either may be NULL): d out[0] / d f, d out[0] / dJ,
+ * zeros on rows no term reads.  Each term's sum is reduced in a fixed order; work:
+ * insr_elastic_work_floats() floats, zero-initialised once (the launch leaves it zero).
+ */
+#define INSR_EL_ARAP 0
+#define INSR_EL_VOLUME 1
+#define INSR_EL_KINEMATICS 2
+#define INSR_EL_EXTERNAL 3
+#define INSR_EL_CONSTRAINT 4
+#define INSR_EL_CONSTRAINT_RIGHT 5
+#define INSR_EL_COLLISION 6
+#define INSR_EL_SPHERE 7
+#define INSR_EL_TERMS 8
+typedef struct InsrElastic {
+  int d;               /* 2 or 3 */
+  int n_order;         /* terms in order[] */
+  long n;              /* interior rows */
+  long rows;           /* rows of f / J / gf / gJ */
+  const float* f;      /* (rows, d) trainable field */
+  const float* J;      /* (rows, d, d) its Jacobian (no identity); NULL without ARAP / VOLUME */
+  const float* x;      /* (n, d) interior points */
+  const float* f_prev; /* (n, d) */
+  const float* f_pp;   /* (n, d) */
+  float dt;
+  float ratio[INSR_EL_TERMS];
+  float ext[3];
+  float target[3];
+  float plane_height;
+  float center[3];
+  float radius;
+  long row_l, n_l, row_r, n_r;
+  int order[INSR_EL_TERMS];
+  float* out;          /* 1 float: the total */
+  float* terms;        /* INSR_EL_TERMS floats, or NULL */
+  float* gf;
+  float* gJ;
+} InsrElastic;
+long insr_elastic_work_floats(void);
+int insr_elastic_energy(const InsrElastic* e, float* work, void* stream);
+
+/*
  * Data-parallel collective (one process per GPU): the single sum all-reduce per optimiser
  * step of the flat gradients (+ loss scalars) -- what BaseModel._dp_sync does through
  * torch.distributed (backend "nccl" = RCCL), for hosts without PyTorch.  RCCL is loaded at

@@ -11,6 +11,6 @@ from .sampling import *  # noqa: F401,F403
 from .networks import *  # noqa: F401,F403
 from .networks import MLP, Sine, get_network  # noqa: F401
 from .optim import DevicePlateau, FusedAdam  # noqa: F401
-from .losses import axpy_clamp, fused_mse, mse_term, sq_losses, svd_energy, wall_mse, wall_term  # noqa: F401
+from .losses import axpy_clamp, elastic_energy, fused_mse, mse_term, sq_losses, svd_energy, wall_mse, wall_term  # noqa: F401
 from ._jet import UnsupportedPattern, advect_target, fused_forwards  # noqa: F401
 from ._native import NativeUnavailable, NativeError  # noqa: F401

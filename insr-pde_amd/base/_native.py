@@ -61,6 +61,8 @@ SIGNATURES = {
     "insr_svd_energy_work_floats": (_L, []),
     "insr_svd_energy_fwd": (_I, [_P, _L, _I, _F, _F, _P, _P, _P]),
     "insr_svd_energy_bwd": (_I, [_P, _L, _I, _F, _F, _P, _P, _P]),
+    "insr_elastic_work_floats": (_L, []),
+    "insr_elastic_energy": (_I, [_P, _P, _P]),
     "insr_sq_loss_fwd": (_I, [_I, _P, _P, _P, _P, _L, _I, _F, _F, _F, _F, _F, _P, _P, _P]),
     "insr_sq_loss_group": (_I, [_P, _I, _P, _P]),
     "insr_axpy_clamp": (_I, [_P, _P, _F, _F, _F, _P, _L, _P]),
@@ -114,6 +116,20 @@ MAX_BOXES = 8  # INSR_MAX_BOXES
 class Box(ctypes.Structure):
     """struct InsrBox (include/insr_siren.h): one box of insr_sample_boxes."""
     _fields_ = [("out", _P), ("n", _L), ("lo", _F * 3), ("hi", _F * 3)]
+
+
+EL_TERMS = 8  # INSR_EL_TERMS; term ids INSR_EL_ARAP ... INSR_EL_SPHERE
+EL_IDS = {"arap": 0, "volume": 1, "kinematics": 2, "external": 3, "constraint": 4, "constraint_right": 5,
+          "collision": 6, "collision_sphere": 7}
+
+
+class Elastic(ctypes.Structure):
+    """struct InsrElastic (include/insr_siren.h): one elasticity energy of insr_elastic_energy."""
+    _fields_ = [("d", _I), ("n_order", _I), ("n", _L), ("rows", _L), ("f", _P), ("J", _P), ("x", _P),
+                ("f_prev", _P), ("f_pp", _P), ("dt", _F), ("ratio", _F * EL_TERMS), ("ext", _F * 3),
+                ("target", _F * 3), ("plane_height", _F), ("center", _F * 3), ("radius", _F),
+                ("row_l", _L), ("n_l", _L), ("row_r", _L), ("n_r", _L), ("order", _I * EL_TERMS),
+                ("out", _P), ("terms", _P), ("gf", _P), ("gJ", _P)]
 
 
 class NativeUnavailable(RuntimeError):

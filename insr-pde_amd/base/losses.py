@@ -30,7 +30,8 @@ def prepare_workspaces(stream):
     """Create the reduction workspaces of `stream` (before a graph capture on it)."""
     dev = stream.device
     for table, floats, zero in ((_WORK, nat.lib().insr_sq_loss_work_floats(), True),
-                                (_SVD_WORK, nat.lib().insr_svd_energy_work_floats(), False)):
+                                (_SVD_WORK, nat.lib().insr_svd_energy_work_floats(), False),
+                                (_EL_WORK, nat.lib().insr_elastic_work_floats(), True)):
         key = _stream_key(dev, stream)
         if key not in table:
             table[key] = (torch.zeros if zero else torch.empty)(floats, device=dev, dtype=torch.float32)
@@ -347,3 +348,100 @@ def svd_energy(J, ratio_arap=1.0, ratio_volume=0.0, count=None):
     if n > J.shape[0] or n < 0:
         raise ValueError(f"svd_energy: count {n} > {J.shape[0]} blocks")
     return _SvdEnergy.apply(_prep(J), ratio_arap, ratio_volume, n)
+
+
+_EL_WORK = {}  # (device index, stream handle) -> per-term partials + ticket of insr_elastic_energy
+
+
+class _ElasticEnergy(torch.autograd.Function):
+    """insr_elastic_energy: the energy and, in the same launch, its gradient for a unit seed
+    w.r.t. the field rows f and the Jacobian J (the backward of a unit-seeded loss costs no
+    launch; any other seed scales the written gradients)."""
+
+    @staticmethod
+    def forward(ctx, f, J, spec, consts):
+        x, f_prev, f_pp = consts
+        dev = f.device
+        key = _stream_key(dev)
+        if key not in _EL_WORK:
+            if torch.cuda.is_current_stream_capturing():
+                raise RuntimeError("elastic-energy workspace must be created before graph capture "
+                                   "(base.losses.prepare_workspaces(stream) or one eager call on the stream)")
+            _EL_WORK[key] = torch.zeros(nat.lib().insr_elastic_work_floats(), device=dev, dtype=torch.float32)
+        out = torch.empty((), device=dev, dtype=torch.float32)
+        terms = torch.empty(nat.EL_TERMS, device=dev, dtype=torch.float32)
+        need_f, need_J = ctx.needs_input_grad[0], J is not None and ctx.needs_input_grad[1]
+        gf = torch.empty_like(f) if need_f else None
+        gJ = torch.empty_like(J) if need_J else None
+        e = nat.Elastic()
+        d = f.shape[1]
+        e.d, e.n, e.rows = d, spec["n"], f.shape[0]
+        e.f, e.J, e.x, e.f_prev, e.f_pp = nat.ptr(f), nat.ptr(J), nat.ptr(x), nat.ptr(f_prev), nat.ptr(f_pp)
+        e.dt = spec["dt"]
+        for t, r in spec["ratio"].items():
+            e.ratio[t] = r
+        for k in range(d):
+            e.ext[k], e.target[k], e.center[k] = spec["ext"][k], spec["target"][k], spec["center"][k]
+        e.plane_height, e.radius = spec["plane_height"], spec["radius"]
+        e.row_l, e.n_l, e.row_r, e.n_r = spec["rows_l"] + spec["rows_r"]
+        e.n_order = len(spec["order"])
+        for k, t in enumerate(spec["order"]):
+            e.order[k] = t
+        e.out, e.terms, e.gf, e.gJ = nat.ptr(out), nat.ptr(terms), nat.ptr(gf), nat.ptr(gJ)
+        nat.check(nat.lib().insr_elastic_energy(ctypes.byref(e), nat.ptr(_EL_WORK[key]), nat.stream_of(dev)),
+                  "insr_elastic_energy")
+        ctx.pre = (gf, gJ)
+        ctx.mark_non_differentiable(terms)
+        return out, terms
+
+    @staticmethod
+    def backward(ctx, gtotal, _gterms):
+        gf, gJ = ctx.pre  # kept (retain_graph=True may run the backward again)
+        if gtotal is None:
+            return None, None, None, None
+        if not (gtotal.numel() == 1 and gtotal.data_ptr() in _UNIT_SEEDS):
+            gf = None if gf is None else gf * gtotal
+            gJ = None if gJ is None else gJ * gtotal
+        return gf, gJ, None, None
+
+
+def elastic_energy(f, J, x, f_prev, f_pp, *, n, dt, energy, ratios, ext=(0.0, 0.0, 0.0), external_on=True,
+                   rows_l=(0, 0), rows_r=(0, 0), target=(0.0, 0.0, 0.0), plane_height=0.0, center=(0.0, 0.0, 0.0),
+                   radius=0.0):
+    """The elastodynamics energy of elasticity/model.py:131-186 in ONE launch (insr_elastic_energy).
+
+    f: (rows, d) trainable field values of one merged jet launch -- rows [0, n) at the interior
+    points x, rows_l = (first row, count) / rows_r the fixed points of the positional
+    constraints; J: (rows, d, d) the field's Jacobian df/dx (None without arap / volume);
+    f_prev, f_pp: the frozen fields at x.  energy: cfg.energy (terms are added in that order);
+    ratios: {term: ratio}.  Returns (total, terms) -- total differentiable w.r.t. f and J,
+    terms (8 floats, non-differentiable) the per-term values (index INSR_EL_*, base._native.EL_IDS)."""
+    ids = nat.EL_IDS
+    order, ratio = [], {}
+    for term in energy:
+        if term == "constraint_right_compress":
+            t = ids["constraint_right"]
+        elif term in ids:
+            t = ids[term]
+        else:
+            raise NotImplementedError(term)
+        if term == "external" and not external_on:
+            continue
+        order.append(t)
+        ratio[t] = 1.0 if term == "external" else float(ratios[term])
+    d = f.shape[1]
+    if ids["collision_sphere"] in ratio and d != 2:
+        raise _unsupported("3-D collision_sphere (a product of two sums) is not fused")
+    spec = {"n": int(n), "dt": float(dt), "ratio": ratio, "order": order, "ext": [float(v) for v in ext],
+            "target": [float(v) for v in target], "center": [float(v) for v in center],
+            "plane_height": float(plane_height), "radius": float(radius),
+            "rows_l": tuple(int(v) for v in rows_l), "rows_r": tuple(int(v) for v in rows_r)}
+    f = _prep(f)
+    J = None if J is None else _prep(J)
+    x, f_prev, f_pp = _prep(x.detach()), _prep(f_prev.detach()), _prep(f_pp.detach())
+    return _ElasticEnergy.apply(f, J, spec, (x, f_prev, f_pp))
+
+
+def _unsupported(msg):
+    from ._jet import UnsupportedPattern
+    return UnsupportedPattern(msg)

@@ -132,6 +132,43 @@ __device__ __forceinline__ void svd3_sorted(float (&B)[3][3], float (&V)[3][3], 
   cswap_cols(B, V, s, 0, 1);
 }
 
+// d(sum_k g de_k s_k)/dJ = g U diag(de) V^T for the 3x3 Jacobi SVD (B = J V, sorted).
+// U columns: u_k = B[:, k] / s_k; a (near-)zero smallest singular value takes u_0 x u_1,
+// signed so that det(U) det(V) = sign det(J)
+__device__ __forceinline__ void grad3(const float* Ji, const float (&B)[3][3], const float (&V)[3][3],
+                                      const float (&s)[3], float go, const float (&de)[3], float* out) {
+  float U[3][3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const float inv = s[k] > 1e-30f ? 1.f / s[k] : 0.f;
+#pragma unroll
+    for (int r = 0; r < 3; ++r) U[r][k] = B[r][k] * inv;
+  }
+  if (!(s[2] > 1e-6f * s[0])) {
+    float cx = U[1][0] * U[2][1] - U[2][0] * U[1][1];
+    float cy = U[2][0] * U[0][1] - U[0][0] * U[2][1];
+    float cz = U[0][0] * U[1][1] - U[1][0] * U[0][1];
+    const float detJ = Ji[0] * (Ji[4] * Ji[8] - Ji[5] * Ji[7]) - Ji[1] * (Ji[3] * Ji[8] - Ji[5] * Ji[6]) +
+                       Ji[2] * (Ji[3] * Ji[7] - Ji[4] * Ji[6]);
+    const float detV = V[0][0] * (V[1][1] * V[2][2] - V[2][1] * V[1][2]) -
+                       V[1][0] * (V[0][1] * V[2][2] - V[2][1] * V[0][2]) +
+                       V[2][0] * (V[0][1] * V[1][2] - V[1][1] * V[0][2]);
+    const float sgn = (detJ < 0.f) == (detV < 0.f) ? 1.f : -1.f;
+    U[0][2] = sgn * cx;
+    U[1][2] = sgn * cy;
+    U[2][2] = sgn * cz;
+  }
+#pragma unroll
+  for (int r = 0; r < 3; ++r)
+#pragma unroll
+    for (int col = 0; col < 3; ++col) {
+      float v = 0.f;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) v = fmaf(U[r][k] * de[k], V[col][k], v);
+      out[r * 3 + col] = go * v;
+    }
+}
+
 __global__ __launch_bounds__(kSvdThreads) void svd_energy_fwd_kernel(const float* __restrict__ J, long n, int d,
                                                                      float ra, float rv, float* __restrict__ out) {
   __shared__ float red[kSvdThreads / 64];
@@ -183,40 +220,175 @@ __global__ __launch_bounds__(kSvdThreads) void svd_energy_bwd_kernel(const float
       jacobi3(Ji, B, V);
       svd3_sorted(B, V, s);
       svd_e<3>(s, ra, rv, de);
-      // U columns: u_k = B[:, k] / s_k; a (near-)zero smallest singular value
-      // takes u_0 x u_1, signed so that det(U) det(V) = sign det(J)
-      float U[3][3];
+      grad3(Ji, B, V, s, go, de, gJ + i * 9);
+    }
+  }
+}
+
+
+// ---------------------------------------------------------------------------------------
+// The whole elastodynamics energy of one iteration (insr_elastic_energy): one thread per row
+// of the trainable field's merged jet; interior rows (< n) carry ARAP / volume (the SVD of
+// dq/dx = J + I), kinematics, external force and collision terms, the constraint rows their
+// positional terms.  Each term's raw sum is reduced separately (deterministic, block order,
+// last block combines), scaled like the reference and added in cfg.energy order; the
+// gradient for a unit seed is written in the same pass.
+// ---------------------------------------------------------------------------------------
+constexpr int kElThreads = 256;
+constexpr int kElMaxBlocks = 256;
+
+__global__ __launch_bounds__(kElThreads) void elastic_energy_kernel(const InsrElastic E, float* __restrict__ work) {
+  __shared__ float red[INSR_EL_TERMS][kElThreads / 64];
+  const int d = E.d;
+  const float dt = E.dt;
+  const bool svd = E.ratio[INSR_EL_ARAP] != 0.f || E.ratio[INSR_EL_VOLUME] != 0.f;
+  float acc[INSR_EL_TERMS];
+#pragma unroll
+  for (int t = 0; t < INSR_EL_TERMS; ++t) acc[t] = 0.f;
+  for (long r = (long)blockIdx.x * kElThreads + threadIdx.x; r < E.rows; r += (long)gridDim.x * kElThreads) {
+    float gf[3] = {0.f, 0.f, 0.f};
+    if (r < E.n) {
+      float q[3], qd[3];
 #pragma unroll
       for (int k = 0; k < 3; ++k) {
-        const float inv = s[k] > 1e-30f ? 1.f / s[k] : 0.f;
-#pragma unroll
-        for (int r = 0; r < 3; ++r) U[r][k] = B[r][k] * inv;
-      }
-      if (!(s[2] > 1e-6f * s[0])) {
-        float cx = U[1][0] * U[2][1] - U[2][0] * U[1][1];
-        float cy = U[2][0] * U[0][1] - U[0][0] * U[2][1];
-        float cz = U[0][0] * U[1][1] - U[1][0] * U[0][1];
-        const float detJ = Ji[0] * (Ji[4] * Ji[8] - Ji[5] * Ji[7]) - Ji[1] * (Ji[3] * Ji[8] - Ji[5] * Ji[6]) +
-                           Ji[2] * (Ji[3] * Ji[7] - Ji[4] * Ji[6]);
-        const float detV = V[0][0] * (V[1][1] * V[2][2] - V[2][1] * V[1][2]) -
-                           V[1][0] * (V[0][1] * V[2][2] - V[2][1] * V[0][2]) +
-                           V[2][0] * (V[0][1] * V[1][2] - V[1][1] * V[0][2]);
-        const float sgn = (detJ < 0.f) == (detV < 0.f) ? 1.f : -1.f;
-        U[0][2] = sgn * cx;
-        U[1][2] = sgn * cy;
-        U[2][2] = sgn * cz;
-      }
-      // gJ = go * U diag(de) V^T
-#pragma unroll
-      for (int r = 0; r < 3; ++r)
-#pragma unroll
-        for (int col = 0; col < 3; ++col) {
-          float v = 0.f;
-#pragma unroll
-          for (int k = 0; k < 3; ++k) v = fmaf(U[r][k] * de[k], V[col][k], v);
-          gJ[i * 9 + r * 3 + col] = go * v;
+        if (k >= d) break;
+        const float xk = E.x[r * d + k];
+        q[k] = E.f[r * d + k] + xk;                 // q = f(x) + x
+        const float qp = E.f_prev[r * d + k] + xk;  // q_prev, q_prev_prev (no grad)
+        const float qpp = E.f_pp[r * d + k] + xk;
+        qd[k] = (q[k] - qp) / dt;
+        if (E.ratio[INSR_EL_KINEMATICS] != 0.f) {  // rk sum (qdot - qdot_prev)^2
+          const float a = qd[k] - (qp - qpp) / dt;
+          acc[INSR_EL_KINEMATICS] += a * a;
+          gf[k] += (E.ratio[INSR_EL_KINEMATICS] * (2.f * a)) / dt;
         }
+        if (E.ratio[INSR_EL_EXTERNAL] != 0.f) {  // -dt sum qdot . f_ext
+          acc[INSR_EL_EXTERNAL] += qd[k] * E.ext[k];
+          gf[k] += (-dt * E.ext[k]) / dt;
+        }
+      }
+      if (E.ratio[INSR_EL_COLLISION] != 0.f) {  // plane: -dt sum qdot_z rc (h - q_z) over q_z < h
+        const float qz = q[d - 1];
+        if (qz < E.plane_height) {
+          const float force = E.ratio[INSR_EL_COLLISION] * (E.plane_height - qz);
+          acc[INSR_EL_COLLISION] += qd[d - 1] * force;
+          gf[d - 1] += (-dt * force) / dt + dt * qd[d - 1] * E.ratio[INSR_EL_COLLISION];
+        }
+      }
+      if (E.ratio[INSR_EL_SPHERE] != 0.f) {  // 2-D sphere: -dt sum qdot . rc dist dir over dist < R
+        float vec[3], ss = 0.f;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          if (k >= d) break;
+          vec[k] = q[k] - E.center[k];
+          ss += vec[k] * vec[k];
+        }
+        const float dist = sqrtf(ss);
+        if (dist < E.radius) {
+          const float rd = E.ratio[INSR_EL_SPHERE] * dist;
+#pragma unroll
+          for (int k = 0; k < 3; ++k) {
+            if (k >= d) break;
+            acc[INSR_EL_SPHERE] += qd[k] * (rd * (vec[k] / dist));
+            gf[k] += -E.ratio[INSR_EL_SPHERE] * vec[k] - dt * E.ratio[INSR_EL_SPHERE] * qd[k];
+          }
+        }
+      }
+      if (svd) {  // singular values of dq/dx = J + I
+        const float ra = E.ratio[INSR_EL_ARAP], rv = E.ratio[INSR_EL_VOLUME];
+        if (d == 2) {
+          float Jq[4];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) Jq[k] = E.J[r * 4 + k] + ((k == 0 || k == 3) ? 1.f : 0.f);
+          float s[2], de[2];
+          svd2(Jq, s);
+          svd_e<2>(s, ra, rv, de);
+          acc[INSR_EL_ARAP] += (s[0] - 1.f) * (s[0] - 1.f) + (s[1] - 1.f) * (s[1] - 1.f);
+          const float pm = s[0] * s[1] - 1.f;
+          acc[INSR_EL_VOLUME] += pm * pm;
+          if (E.gJ) grad2(Jq, de[0], de[1], E.gJ + r * 4);
+        } else {
+          float Jq[9];
+#pragma unroll
+          for (int k = 0; k < 9; ++k) Jq[k] = E.J[r * 9 + k] + ((k % 4 == 0) ? 1.f : 0.f);
+          float B[3][3], V[3][3], s[3], de[3];
+          jacobi3(Jq, B, V);
+          svd3_sorted(B, V, s);
+          svd_e<3>(s, ra, rv, de);
+          acc[INSR_EL_ARAP] += (s[0] - 1.f) * (s[0] - 1.f) + (s[1] - 1.f) * (s[1] - 1.f) + (s[2] - 1.f) * (s[2] - 1.f);
+          const float pm = s[0] * s[1] * s[2] - 1.f;
+          acc[INSR_EL_VOLUME] += pm * pm;
+          if (E.gJ) grad3(Jq, B, V, s, 1.f, de, E.gJ + r * 9);
+        }
+      }
+    } else {
+      if (r >= E.row_l && r < E.row_l + E.n_l) {  // rc sum |f(x_l)|^2
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          if (k >= d) break;
+          const float v = E.f[r * d + k];
+          acc[INSR_EL_CONSTRAINT] += v * v;
+          gf[k] += E.ratio[INSR_EL_CONSTRAINT] * (2.f * v);
+        }
+      }
+      if (r >= E.row_r && r < E.row_r + E.n_r) {  // rc sum |f(x_r) - target|^2
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          if (k >= d) break;
+          const float v = E.f[r * d + k] - E.target[k];
+          acc[INSR_EL_CONSTRAINT_RIGHT] += v * v;
+          gf[k] += E.ratio[INSR_EL_CONSTRAINT_RIGHT] * (2.f * v);
+        }
+      }
+      if (E.gJ && svd)
+        for (int k = 0; k < d * d; ++k) E.gJ[r * d * d + k] = 0.f;
     }
+    if (E.gf)
+#pragma unroll
+      for (int k = 0; k < 3; ++k)
+        if (k < d) E.gf[r * d + k] = gf[k];
+  }
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int t = 0; t < INSR_EL_TERMS; ++t) {
+    float v = acc[t];
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+    if (lane == 0) red[t][w] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x >= INSR_EL_TERMS) return;
+  const int t = threadIdx.x;  // lanes 0..7 of wave 0: one term each
+  float part = 0.f;
+#pragma unroll
+  for (int k = 0; k < kElThreads / 64; ++k) part += red[t][k];
+  // scale of each raw sum (the reference's ratio * torch.sum(...), -dt * torch.sum(...))
+  const float scale = (t == INSR_EL_EXTERNAL || t == INSR_EL_COLLISION || t == INSR_EL_SPHERE) ? -dt : E.ratio[t];
+  float tot = part;
+  if (gridDim.x > 1) {
+    // sc1 partial store + wait + agent-scope ticket (as sq_loss_group_kernel); the last block's
+    // eight lanes read every partial of their term in block order
+    __hip_atomic_store(work + t * kElMaxBlocks + blockIdx.x, part, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    unsigned* ticket = reinterpret_cast<unsigned*>(work + INSR_EL_TERMS * kElMaxBlocks);
+    unsigned last = 0;
+    if (t == 0) last = atomicAdd(ticket, 1u) == gridDim.x - 1 ? 1u : 0u;
+    last = __shfl(last, 0);
+    if (!last) return;
+    tot = 0.f;
+    for (unsigned k = 0; k < gridDim.x; ++k)
+      tot += __hip_atomic_load(work + t * kElMaxBlocks + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (t == 0) atomicExch(ticket, 0u);
+  }
+  const float et = scale * tot;
+  if (E.terms) E.terms[t] = et;
+  // total in cfg.energy order (loss = 0; loss = loss + E_t), lane 0 gathers the terms
+  float terms[INSR_EL_TERMS];
+#pragma unroll
+  for (int k = 0; k < INSR_EL_TERMS; ++k) terms[k] = __shfl(et, k);
+  if (t == 0) {
+    float loss = 0.f;
+    for (int k = 0; k < E.n_order; ++k) loss += terms[E.order[k]];
+    E.out[0] = loss;
   }
 }
 
@@ -250,6 +422,30 @@ int insr_svd_energy_bwd(const float* J, long n, int d, float ratio_arap, float r
   if (nb > 4096) nb = 4096;
   hipLaunchKernelGGL(svd_energy_bwd_kernel, dim3((unsigned)nb), dim3(kSvdThreads), 0, (hipStream_t)stream, J, n, d,
                      ratio_arap, ratio_volume, gout, gJ);
+  return (int)hipGetLastError();
+}
+
+
+long insr_elastic_work_floats(void) { return (long)INSR_EL_TERMS * kElMaxBlocks + 4; }
+
+int insr_elastic_energy(const InsrElastic* e, float* work, void* stream) {
+  if (!e || (e->d != 2 && e->d != 3) || e->n < 0 || e->rows < e->n || !e->out) return INSR_EINVAL;
+  if (e->n > 0 && (!e->f || !e->x || !e->f_prev || !e->f_pp)) return INSR_EINVAL;
+  if (e->rows > e->n && !e->f) return INSR_EINVAL;
+  const bool svd = e->ratio[INSR_EL_ARAP] != 0.f || e->ratio[INSR_EL_VOLUME] != 0.f;
+  if (svd && e->n > 0 && !e->J) return INSR_EINVAL;
+  if (!(e->dt > 0.f) || e->n_order < 0 || e->n_order > INSR_EL_TERMS) return INSR_EINVAL;
+  if (e->ratio[INSR_EL_SPHERE] != 0.f && e->d != 2) return INSR_EINVAL;  // 3-D: a product of two sums
+  for (int k = 0; k < e->n_order; ++k)
+    if (e->order[k] < 0 || e->order[k] >= INSR_EL_TERMS) return INSR_EINVAL;
+  if (e->n_l < 0 || e->n_r < 0 || (e->n_l > 0 && (e->row_l < e->n || e->row_l + e->n_l > e->rows)) ||
+      (e->n_r > 0 && (e->row_r < e->n || e->row_r + e->n_r > e->rows)))
+    return INSR_EINVAL;
+  long nb = (e->rows + 4L * kElThreads - 1) / (4L * kElThreads);  // ~4 rows per thread
+  if (nb < 1) nb = 1;
+  if (nb > kElMaxBlocks) nb = kElMaxBlocks;
+  if (nb > 1 && !work) return INSR_EINVAL;
+  hipLaunchKernelGGL(elastic_energy_kernel, dim3((unsigned)nb), dim3(kElThreads), 0, (hipStream_t)stream, *e, work);
   return (int)hipGetLastError();
 }
 

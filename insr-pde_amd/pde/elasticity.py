@@ -19,7 +19,8 @@ import os
 import numpy as np
 import torch
 
-from base import BaseModel, fused_forwards, fused_mse, merge_samples, sample_random, sample_uniform, svd_energy
+from base import (BaseModel, elastic_energy, fused_forwards, fused_mse, merge_samples, sample_random, sample_uniform,
+                  svd_energy)
 from base.diff_ops import jacobian_only
 
 
@@ -195,6 +196,24 @@ class ElasticityModel(BaseModel):
                 f_prev = self.deformation_field_prev(x)
                 f_pp = self.deformation_field_prev_prev(x)
             fa = self.deformation_field(xa)
+        if not (self.dim == 3 and 'collision_sphere' in self.energy):
+            # every term in ONE launch with its unit-seed gradient (base.elastic_energy): the
+            # singular values of dq/dx = J + I, kinematics, external force, collisions and the
+            # positional constraints; J is the Jacobian jet of the same field launch
+            J = jacobian_only(fa, xa) if ('arap' in self.energy or 'volume' in self.energy) else None
+            sign = -1.0 if 'constraint_right_compress' in self.energy else 1.0
+            ratios = {'arap': self.ratio_arap, 'volume': self.ratio_volume, 'kinematics': self.ratio_kinematics,
+                      'constraint': self.ratio_constraint, 'constraint_right': self.ratio_constraint,
+                      'constraint_right_compress': self.ratio_constraint, 'collision': self.ratio_collide,
+                      'collision_sphere': self.ratio_collide}
+            total, _ = elastic_energy(
+                fa, J, x, f_prev, f_pp, n=n, dt=dt, energy=self.energy, ratios=ratios,
+                ext=self._host_vec('external_force'), external_on=self.timestep <= self.external_force_timesteps,
+                rows_l=(row_l, fixed_l.shape[0] if use_l else 0), rows_r=(row_r, fixed_r.shape[0] if use_r else 0),
+                target=[sign * v for v in self._host_vec('constraint_offset_right')], plane_height=self.plane_height,
+                center=self._host_vec('circle_center'), radius=self.circle_radius)
+            return total
+        # 3-D collision_sphere (the reference's broadcast makes it a product of two sums): torch terms
         with torch.no_grad():
             q_prev = f_prev + x
             q_pp = f_pp + x
@@ -231,6 +250,13 @@ class ElasticityModel(BaseModel):
             else:
                 raise NotImplementedError(term)
         return total
+
+    def _host_vec(self, name):
+        """A cfg vector (external force, offsets, sphere centre) as host floats, cached."""
+        cache = self.__dict__.setdefault("_insr_host_vecs", {})
+        if name not in cache:
+            cache[name] = [float(v) for v in getattr(self, name).cpu()]
+        return cache[name]
 
     def _target_rows(self, sign, rows):
         """sign * constraint_offset_right repeated over the fixed points (cached constant)."""

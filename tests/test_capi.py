@@ -87,3 +87,27 @@ def test_comm_library_resolves(lib):
     assert lib.insr_comm_available() == 1
     assert lib.insr_comm_id_bytes() == 128
     assert lib.insr_comm_init(None, 0, 1, None) == -1  # INSR_EINVAL, no RCCL call made
+
+
+def test_struct_layouts_match_header(tmp_path):
+    """The ctypes mirrors of the header's structs have the C compiler's size and field offsets."""
+    import ctypes
+    import subprocess
+    from base import _native as nat
+    structs = {"InsrJetJob": nat.JetJob, "InsrLoss": nat.Loss, "InsrBox": nat.Box, "InsrElastic": nat.Elastic}
+    lines = ['#include <stdio.h>', '#include <stddef.h>', f'#include "{HEADER}"', "int main(void) {"]
+    for cname, py in structs.items():
+        lines.append(f'  printf("{cname} size %zu\\n", sizeof({cname}));')
+        for fname, _ in py._fields_:
+            lines.append(f'  printf("{cname} {fname} %zu\\n", offsetof({cname}, {fname}));')
+    lines.append("  return 0;\n}")
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-o", str(exe), str(src)], check=True)
+    got = dict(line.rsplit(" ", 1) for line in subprocess.run([str(exe)], check=True, capture_output=True,
+                                                                text=True).stdout.splitlines())
+    for cname, py in structs.items():
+        assert int(got[f"{cname} size"]) == ctypes.sizeof(py), cname
+        for fname, _ in py._fields_:
+            assert int(got[f"{cname} {fname}"]) == getattr(py, fname).offset, (cname, fname)
