@@ -55,6 +55,43 @@ __device__ __forceinline__ float loss_term(int kind, const LossIn& in, long n, i
   return v * v;
 }
 
+// The block's partial sum (fixed order: wave butterfly, then the waves in order) and, over a
+// grid of nblk blocks, the cross-block combine in the same launch: the partial leaves as an sc1
+// store, thread 0 waits for it and takes the ticket with an agent-scope atomic (no L2 write-back,
+// MI355X_MICROARCH.md hand-off table row 1); the LAST block's first wave loads every partial with
+// sc1 loads in parallel (lane l: partials l, l + 64, ...) and sums them by a fixed butterfly --
+// deterministic, and no serial chain of nblk dependent loads.  Leaves the ticket zero.
+__device__ __forceinline__ void block_partial_combine(float acc, float* red, int blk, int nblk, float scale,
+                                                      float* __restrict__ out, float* __restrict__ wk,
+                                                      float* ticket_word) {
+  __shared__ int last;
+  for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane == 0) red[w] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float part = 0.f;
+    for (int k = 0; k < (int)(blockDim.x / 64); ++k) part += red[k];
+    if (nblk == 1) {
+      out[0] = scale * part;
+      last = 0;
+    } else {
+      __hip_atomic_store(wk + blk, part, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      last = atomicAdd(reinterpret_cast<unsigned*>(ticket_word), 1u) == (unsigned)nblk - 1 ? 1 : 0;
+    }
+  }
+  __syncthreads();
+  if (!last || w != 0) return;
+  float tot = 0.f;
+  for (int q = lane; q < nblk; q += 64) tot += __hip_atomic_load(wk + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (int off = 32; off > 0; off >>= 1) tot += __shfl_xor(tot, off);
+  if (lane == 0) {
+    out[0] = scale * tot;
+    atomicExch(reinterpret_cast<unsigned*>(ticket_word), 0u);
+  }
+}
+
 // work: kLossMaxBlocks partials + one ticket word (zero-initialised; every launch leaves it 0)
 __global__ __launch_bounds__(kLossThreads) void sq_loss_fwd_kernel(int kind, LossIn in, long n, int m, float scale,
                                                                    float* __restrict__ out, float* __restrict__ work) {
@@ -66,29 +103,7 @@ __global__ __launch_bounds__(kLossThreads) void sq_loss_fwd_kernel(int kind, Los
   for (long i = (long)blockIdx.x * kLossThreads + threadIdx.x; i < count; i += (long)gridDim.x * kLossThreads)
     acc += loss_term(kind, in, n, m, i);
   // wave reduction (fixed butterfly order), then the block's waves in order
-  for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off);
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  if (lane == 0) red[w] = acc;
-  __syncthreads();
-  if (threadIdx.x != 0) return;
-  float part = 0.f;
-  for (int k = 0; k < kLossThreads / 64; ++k) part += red[k];
-  if (gridDim.x == 1) {
-    out[0] = scale * part;
-    return;
-  }
-  // cross-block hand-off without an L2 write-back (MI355X_MICROARCH.md, hand-off table row 1):
-  // the partial leaves as an sc1 store, this lane waits for it, then takes the ticket with an
-  // agent-scope atomic; the last block reads every partial with sc1 loads
-  __hip_atomic_store(work + blockIdx.x, part, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  unsigned* ticket = reinterpret_cast<unsigned*>(work + kLossMaxBlocks);
-  if (atomicAdd(ticket, 1u) != gridDim.x - 1) return;
-  float tot = 0.f;
-  for (unsigned k = 0; k < gridDim.x; ++k)  // block order: the sum is deterministic
-    tot += __hip_atomic_load(work + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  out[0] = scale * tot;
-  atomicExch(ticket, 0u);
+  block_partial_combine(acc, red, (int)blockIdx.x, (int)gridDim.x, scale, out, work, work + kLossMaxBlocks);
 }
 
 __global__ __launch_bounds__(256) void sq_loss_bwd_kernel(int kind, LossIn in, long n, int m, float scale,
@@ -187,28 +202,8 @@ __global__ __launch_bounds__(kLossThreads) void sq_loss_group_kernel(const LossG
       }
     }
   }
-  for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off);
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  if (lane == 0) red[w] = acc;
-  __syncthreads();
-  if (threadIdx.x != 0) return;
-  float part = 0.f;
-  for (int q = 0; q < kLossThreads / 64; ++q) part += red[q];
-  if (nblk == 1) {
-    L.out[0] = L.scale * part;
-    return;
-  }
   float* wk = work + (long)k * (kLossMaxBlocks + 1);
-  // sc1 store + wait + agent atomic ticket; sc1 loads by the last block (no L2 write-back)
-  __hip_atomic_store(wk + blk, part, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  unsigned* ticket = reinterpret_cast<unsigned*>(wk + kLossMaxBlocks);
-  if (atomicAdd(ticket, 1u) != (unsigned)nblk - 1) return;
-  float tot = 0.f;
-  for (int q = 0; q < nblk; ++q)  // block order: the sum is deterministic
-    tot += __hip_atomic_load(wk + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  L.out[0] = L.scale * tot;
-  atomicExch(ticket, 0u);
+  block_partial_combine(acc, red, blk, nblk, L.scale, L.out, wk, wk + kLossMaxBlocks);
 }
 
 // out = clamp(x + alpha y, lo, hi): the semi-Lagrangian foot of the fluid advection,

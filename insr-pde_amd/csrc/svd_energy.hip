@@ -355,41 +355,62 @@ __global__ __launch_bounds__(kElThreads) void elastic_energy_kernel(const InsrEl
     for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
     if (lane == 0) red[t][w] = v;
   }
+  __shared__ float tot[INSR_EL_TERMS];
+  __shared__ int last;
   __syncthreads();
-  if (threadIdx.x >= INSR_EL_TERMS) return;
-  const int t = threadIdx.x;  // lanes 0..7 of wave 0: one term each
-  float part = 0.f;
+  if (threadIdx.x < INSR_EL_TERMS) {  // the block's partial of term t (waves in order)
+    const int t = threadIdx.x;
+    float part = 0.f;
 #pragma unroll
-  for (int k = 0; k < kElThreads / 64; ++k) part += red[t][k];
-  // scale of each raw sum (the reference's ratio * torch.sum(...), -dt * torch.sum(...))
-  const float scale = (t == INSR_EL_EXTERNAL || t == INSR_EL_COLLISION || t == INSR_EL_SPHERE) ? -dt : E.ratio[t];
-  float tot = part;
+    for (int k = 0; k < kElThreads / 64; ++k) part += red[t][k];
+    tot[t] = part;
+    if (gridDim.x > 1)  // sc1 partial store; the wait below covers all eight lanes' stores
+      __hip_atomic_store(work + t * kElMaxBlocks + blockIdx.x, part, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (threadIdx.x == 0) {
+    last = 1;
+    if (gridDim.x > 1) {  // agent-scope ticket (as block_partial_combine in residual.hip)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      unsigned* ticket = reinterpret_cast<unsigned*>(work + INSR_EL_TERMS * kElMaxBlocks);
+      last = atomicAdd(ticket, 1u) == gridDim.x - 1 ? 1 : 0;
+    }
+  }
+  __syncthreads();
+  if (!last) return;
   if (gridDim.x > 1) {
-    // sc1 partial store + wait + agent-scope ticket (as sq_loss_group_kernel); the last block's
-    // eight lanes read every partial of their term in block order
-    __hip_atomic_store(work + t * kElMaxBlocks + blockIdx.x, part, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    unsigned* ticket = reinterpret_cast<unsigned*>(work + INSR_EL_TERMS * kElMaxBlocks);
-    unsigned last = 0;
-    if (t == 0) last = atomicAdd(ticket, 1u) == gridDim.x - 1 ? 1u : 0u;
-    last = __shfl(last, 0);
-    if (!last) return;
-    tot = 0.f;
-    for (unsigned k = 0; k < gridDim.x; ++k)
-      tot += __hip_atomic_load(work + t * kElMaxBlocks + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (t == 0) atomicExch(ticket, 0u);
-  }
-  const float et = scale * tot;
-  if (E.terms) E.terms[t] = et;
-  // total in cfg.energy order (loss = 0; loss = loss + E_t), lane 0 gathers the terms
-  float terms[INSR_EL_TERMS];
+    // the last block: wave w sums terms w and w + 4 over every block's partial, lanes load in
+    // parallel (lane l: blocks l, l + 64, ...), fixed butterfly -- deterministic
 #pragma unroll
-  for (int k = 0; k < INSR_EL_TERMS; ++k) terms[k] = __shfl(et, k);
-  if (t == 0) {
-    float loss = 0.f;
-    for (int k = 0; k < E.n_order; ++k) loss += terms[E.order[k]];
-    E.out[0] = loss;
+    for (int h = 0; h < 2; ++h) {
+      const int t = w + 4 * h;
+      float v = 0.f;
+      for (int q = lane; q < (int)gridDim.x; q += 64)
+        v += __hip_atomic_load(work + t * kElMaxBlocks + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+      __syncthreads();
+      if (lane == 0) tot[t] = v;
+    }
+    __syncthreads();
   }
+  if (threadIdx.x != 0) return;
+  // scale of each raw sum (the reference's ratio * torch.sum(...), -dt * torch.sum(...)); the
+  // total in cfg.energy order (loss = 0; loss = loss + E_t)
+  float et[INSR_EL_TERMS];
+#pragma unroll
+  for (int t = 0; t < INSR_EL_TERMS; ++t) {
+    const float scale = (t == INSR_EL_EXTERNAL || t == INSR_EL_COLLISION || t == INSR_EL_SPHERE) ? -dt : E.ratio[t];
+    et[t] = scale * tot[t];
+    if (E.terms) E.terms[t] = et[t];
+  }
+  float loss = 0.f;
+  for (int k = 0; k < E.n_order; ++k) {
+    const int t = E.order[k];
+#pragma unroll
+    for (int q = 0; q < INSR_EL_TERMS; ++q)
+      if (q == t) loss += et[q];
+  }
+  E.out[0] = loss;
+  if (gridDim.x > 1) atomicExch(reinterpret_cast<unsigned*>(work + INSR_EL_TERMS * kElMaxBlocks), 0u);
 }
 
 }  // namespace insr

@@ -123,3 +123,33 @@ def test_elastic_energy_rejects(B):
     with pytest.raises(B.NativeUnavailable):
         B.elastic_energy(torch.zeros(10, 2), None, torch.zeros(10, 2), torch.zeros(10, 2), torch.zeros(10, 2), n=10,
                          dt=0.1, energy=["kinematics"], ratios={"kinematics": 1.0})
+
+
+def test_box_batch_layout_and_energy(B):
+    """ElasticityModel._box_batch (one sampler launch into a persistent [x; fixed_l; fixed_r]
+    buffer): the layout _sample_in_training / _sample_fixed_in_training / merge_samples give --
+    random rows in the box / on the faces, grid rows equal to sample_uniform, fresh draws every
+    iteration -- and the energy on it equals energy_of on the same points merged by merge_samples."""
+    from pde.config import baseline_config
+    from pde.elasticity import ElasticityModel
+    cfg = baseline_config("elasticity2Dstretch", proj_dir="/tmp/insr_test", insr_progress=False, sample_resolution=20,
+                          num_hidden_layers=2, hidden_features=64)
+    torch.manual_seed(0)
+    m = ElasticityModel(cfg)
+    m.timestep = 1
+    xa, x, fl, fr = m._box_batch(20)
+    n = 2 * 400
+    assert x.shape == (n, 2) and fl.shape == (40, 2) and fr.shape == (40, 2) and xa.shape == (n + 80, 2)
+    a = xa.detach().clone()
+    grid = B.sample_uniform(20, 2, device="cuda")
+    assert torch.equal(a[400:800], grid)
+    assert float(a[:400].abs().max()) <= 1.0
+    assert torch.equal(a[n:n + 20, 0], torch.full((20,), -1.0, device="cuda"))
+    assert torch.equal(a[n + 20:n + 40, 1], B.sample_uniform(20, 1, device="cuda")[:, 0])
+    assert torch.equal(a[n + 40:, 0], torch.full((40,), 1.0, device="cuda"))
+    xa2 = m._box_batch(20)[0]
+    assert xa2 is xa and not torch.equal(xa.detach()[:400], a[:400]) and torch.equal(xa.detach()[400:800], grid)
+    e_fast = m.energy_of(x, fl, fr, xa=xa)
+    xs, fls, frs = (t.detach().clone().requires_grad_(True) for t in (x, fl, fr))
+    e_ref = m.energy_of(xs, fls, frs)
+    assert float(e_fast) == float(e_ref)

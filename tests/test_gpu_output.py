@@ -77,3 +77,45 @@ def test_elasticity_output(base, tmp_path):
     ply = open(out / "t002_deformation.ply").read().split("end_header\n")
     pts = np.loadtxt(ply[1].splitlines())
     assert pts.shape == (440, 3) and np.all(pts[:, 2] == 0) and nerr(pts[:, :2], qr.numpy()) < 1e-6
+
+
+@pytest.mark.parametrize("pde,kw,nets", [
+    ("fluid", dict(num_hidden_layers=4, hidden_features=128), {"velocity": (2, 2), "pressure": (2, 1)}),
+    ("elasticity", dict(dim=2, num_hidden_layers=3, hidden_features=68), {"deformation": (2, 2)}),  # padded width
+])
+def test_model_checkpoint_roundtrip(base, tmp_path, pde, kw, nets):
+    """BaseModel.save_ckpt / load_ckpt (base/baseModel.py:137-162): the file holds the reference's
+    layout ({'net_<name>': state_dict with the reference MLP's keys and shapes, 'timestep'}), a
+    reference network loads it and computes the same field, and load_ckpt into a fresh model
+    restores the parameters bit for bit (jets included: the weight planes follow the load)."""
+    from pde.config import make_config
+    import pde.fluid as F
+    import pde.elasticity as E
+    M = F.Fluid2DModel if pde == "fluid" else E.ElasticityModel
+    cfg = make_config(pde, proj_dir=str(tmp_path), insr_progress=False, **kw)
+    torch.manual_seed(3)
+    a = M(cfg)
+    a.timestep = 7
+    a.save_ckpt("rt")
+    path = os.path.join(cfg.model_dir, "ckpt_rt.pth")
+    ck = torch.load(path, map_location="cpu", weights_only=True)
+    assert sorted(ck) == sorted([f"net_{k}" for k in nets] + ["timestep"]) and ck["timestep"] == 7
+    x = torch.rand(300, 2) * 2 - 1
+    L, W = kw["num_hidden_layers"], kw["hidden_features"]
+    for key, (din, dout) in nets.items():
+        ref = O.OracleSiren(din, dout, L, W)
+        assert [(k, tuple(v.shape)) for k, v in ck[f"net_{key}"].items()] == \
+            [(k, tuple(v.shape)) for k, v in ref.state_dict().items()]
+        ref.load_state_dict(ck[f"net_{key}"])
+        net = a._trainable_networks[key]
+        with torch.no_grad():
+            assert nerr(net(x.cuda()).cpu(), ref(x)) < TOL
+    torch.manual_seed(4)
+    b = M(cfg)
+    b.load_ckpt("rt")
+    assert b.timestep == 7
+    for key in nets:
+        na, nb = a._trainable_networks[key], b._trainable_networks[key]
+        assert torch.equal(na.flat_params(), nb.flat_params())
+        xg = x.cuda().requires_grad_(True)
+        assert torch.equal(base.jacobian(na(xg), xg)[0], base.jacobian(nb(xg), xg)[0])

@@ -5,7 +5,8 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out/${SESSION:-s}
 mkdir -p "$OUT"
-fatal() { [ "$1" -ge 124 ] && { echo "FATAL step exit $1 -- stopping" | tee -a "$OUT/status.log"; exit "$1"; }; return 0; }
+# any failing GPU step ends the session: a fault in one step must not be followed by more GPU work
+fatal() { [ "$1" -ne 0 ] && { echo "FATAL step exit $1 -- stopping" | tee -a "$OUT/status.log"; exit "$1"; }; return 0; }
 step() {  # name timeout cmd...
   local name=$1 to=$2; shift 2
   echo "== $name: $*" >> "$OUT/status.log"
