@@ -148,26 +148,6 @@ int insr_siren_jet_fwd_mixed(const InsrJetJob* jobs, const int* modes, const flo
                              int d_out, int num_hidden, int width, int prec_mode, void* stream);
 int insr_siren_jet_fwd_multi(const InsrJetJob* jobs, int n_jobs, int d_in, int d_out,
                              int num_hidden, int width, int mode, void* stream);
-/* insr_siren_jet_fwd_mixed with the phase iteration's collocation draw generated INSIDE the
- * launch: the points insr_sample_boxes(draw->boxes, draw->n_boxes, d_in, draw->seed,
- * draw->state) would write (the same values and the same advance of the device stream
- * position) are computed by every job whose x lies in the boxes' rows -- the boxes must be
- * consecutive rows of one (rows, d_in) buffer starting at boxes[0].out -- and stored by job
- * draw->writer, whose x must be that whole buffer.  Replaces the sampler launch in front of a
- * phase's first forward (fluid/model.py:74,90-91 draws).  Shapes without a mixed kernel draw
- * with insr_sample_boxes first. */
-typedef struct InsrBox InsrBox;
-typedef struct InsrDraw {
-  const InsrBox* boxes;
-  int n_boxes;
-  int dim;
-  unsigned long long seed;
-  void* state;  /* insr_sampler_state_bytes, as insr_sample_boxes */
-  int writer;   /* index of the job that stores the draw */
-} InsrDraw;
-int insr_siren_jet_fwd_mixed_draw(const InsrJetJob* jobs, const int* modes, const float* scalars, int n_jobs,
-                                  int d_in, int d_out, int num_hidden, int width, int prec_mode,
-                                  const InsrDraw* draw, void* stream);
 
 /*
  * Backward of the jet to the parameters.  Adjoints (any may be NULL = zero):

@@ -23,7 +23,6 @@ import torch
 from torch.autograd.function import once_differentiable
 
 from . import _native as nat
-from .sampling import consume_draw, ensure_drawn, pending_draw
 
 MODE_NAMES = {nat.MODE_VALUE: "value", nat.MODE_GRAD: "grad", nat.MODE_LAP: "lap"}
 
@@ -95,7 +94,6 @@ class _SirenJet(torch.autograd.Function):
         if _Fused.pending is not None:  # launched with the other jets of the scope, at its exit
             _Fused.pending.append(((din, L, W, cmode, dev), (x2, flat, y, dy, lap, act, n, dout)))
         else:
-            ensure_drawn(x2)
             with _timed("fwd", mode, n, W, (din, dout, L)):
                 rc = lib.insr_siren_jet_fwd(nat.ptr(x2), n, din, dout, L, W, cmode, nat.ptr(flat), nat.ptr(y),
                                             nat.ptr(dy), nat.ptr(lap), nat.ptr(act), nat.stream_of(dev))
@@ -203,31 +201,8 @@ def _job_array(chunk):
         for x2, flat, y, dy, lap, act, nj, dj, *_ in chunk])
 
 
-def _mixed_draw(alljobs):
-    """(InsrDraw, base) when the jobs read ONE deferred draw (base.sampling.sample_random_and_bands2D
-    defer=True) and a jet job takes its whole buffer (the writer), else (None, None) after
-    drawing whatever they read the usual way."""
-    found = {}
-    for k, (m, j) in enumerate(alljobs):
-        pd = pending_draw(j[0])
-        if pd is not None:
-            found.setdefault(pd[0], [pd, None])
-            if m != MIX_ADVECT and j[0].data_ptr() == pd[0] and j[0].numel() == pd[1].numel():
-                found[pd[0]][1] = k
-    if len(found) == 1:
-        (pd, writer), = found.values()
-        if writer is not None:
-            base, buf, boxes, seed, state = pd
-            return nat.Draw(ctypes.cast(boxes, ctypes.c_void_p), len(boxes), buf.shape[1], seed, state.data_ptr(),
-                            writer), base
-    for m, j in alljobs:
-        ensure_drawn(j[0])
-    return None, None
-
-
 def _launch_mixed(din, L, W, pbits, dev, alljobs):
-    """One insr_siren_jet_fwd_mixed launch: alljobs = [(jet mode, job tuple)]; generates the
-    iteration's deferred draw inside the launch when the jobs allow it (_mixed_draw)."""
+    """One insr_siren_jet_fwd_mixed launch: alljobs = [(jet mode, job tuple)]."""
     chunk = [j for _, j in alljobs]
     modes = (ctypes.c_int * len(chunk))(*[m for m, _ in alljobs])
     sc = (ctypes.c_float * (3 * len(chunk)))(*[v for _, j in alljobs for v in (j[8] if len(j) > 8 else (0., 0., 0.))])
@@ -235,13 +210,9 @@ def _launch_mixed(din, L, W, pbits, dev, alljobs):
     key_dout = tuple(j[7] for j in chunk)
     with _timed("fwdmix%d" % len(chunk), max(m for m, _ in alljobs if m != MIX_ADVECT) if any(
             m != MIX_ADVECT for m, _ in alljobs) else 0, n, W, (din, key_dout, L)):
-        draw, base = _mixed_draw(alljobs)
-        rc = nat.lib().insr_siren_jet_fwd_mixed_draw(_job_array(chunk), modes, sc, len(chunk), din, chunk[0][7], L,
-                                                     W, pbits, None if draw is None else ctypes.byref(draw),
-                                                     nat.stream_of(dev))
-        if base is not None:
-            consume_draw(base)
-    nat.check(rc, "insr_siren_jet_fwd_mixed_draw")
+        rc = nat.lib().insr_siren_jet_fwd_mixed(_job_array(chunk), modes, sc, len(chunk), din, chunk[0][7], L, W,
+                                                pbits, nat.stream_of(dev))
+    nat.check(rc, "insr_siren_jet_fwd_mixed")
 
 
 def advect_target(mlp, x, dt, lo=-1.0, hi=1.0):
@@ -300,8 +271,6 @@ def _launch_fused(jobs):
             douts = sorted({j[7] for j in chunk})
             dout = chunk[0][7]
             key_dout = douts[0] if len(douts) == 1 else tuple(j[7] for j in chunk)  # per-job widths in the timing key
-            for j in chunk:
-                ensure_drawn(j[0])
             arr = _job_array(chunk)
             with _timed("fwd%d" % len(chunk) if len(chunk) > 1 else "fwd", mode, n, W, (din, key_dout, L)):
                 rc = lib.insr_siren_jet_fwd_multi(arr, len(chunk), din, dout, L, W, cmode, nat.stream_of(dev))

@@ -70,7 +70,6 @@ SIGNATURES = {
     "insr_siren_wsplit_floats": (_L, [_I, _I]),
     "insr_siren_wsplit": (_I, [_P, _I, _I, _I, _I, _P]),
     "insr_siren_jet_fwd_mixed": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _I, _P]),
-    "insr_siren_jet_fwd_mixed_draw": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P]),
     "insr_adam_step_nets": (_I, [_I, _P, _P, _P, _P, _P, _P, _P, _F, _F, _F, _I, _P]),
     "insr_adam_plateau_step_nets": (_I, [_I, _P, _P, _P, _P, _P, _P, _P, _F, _F, _F, _P, _I, _P]),
     "insr_jet_wide_launch_threads": (_I, [_L, _I, _I, _I, _I, _I, _P]),
@@ -131,12 +130,6 @@ class Elastic(ctypes.Structure):
                 ("target", _F * 3), ("plane_height", _F), ("center", _F * 3), ("radius", _F),
                 ("row_l", _L), ("n_l", _L), ("row_r", _L), ("n_r", _L), ("order", _I * EL_TERMS),
                 ("out", _P), ("terms", _P), ("gf", _P), ("gJ", _P)]
-
-
-class Draw(ctypes.Structure):
-    """struct InsrDraw (include/insr_siren.h): a sampler draw generated inside a mixed launch."""
-    _fields_ = [("boxes", _P), ("n_boxes", _I), ("dim", _I), ("seed", ctypes.c_ulonglong), ("state", _P),
-                ("writer", _I)]
 
 
 class NativeUnavailable(RuntimeError):

@@ -7,8 +7,6 @@ device-RNG draw plus at most one fused affine map (graph-capturable, 2 launches
 instead of up to 13 for a pair of boundary bands): same distribution, different
 stream order -- parity tests pass explicit sample tensors.
 """
-import weakref
-
 import torch
 
 _AFFINE = {}  # (N, side-key, epsilon, device) -> (scale, shift) constant tensors
@@ -133,19 +131,13 @@ def _sampler(dev):
     return _SAMPLER[key]
 
 
-def sample_random_and_bands2D(N, n_band, epsilon=1e-4, device="cuda", merged=False, defer=False):
+def sample_random_and_bands2D(N, n_band, epsilon=1e-4, device="cuda", merged=False):
     """(sample_random(N, 2), sample_boundary2D_pair(n_band)) -- the interior batch and the
     four wall bands of one fluid phase iteration (fluid/model.py:74,90-91,105,116-117) --
     drawn in ONE device launch (insr_sample_boxes: 3 launches -> 1).  Same distributions;
     the device stream is Philox-4x32-10, not torch's (GPU only: the CPU samplers above
     reproduce the reference bit for bit).  merged=True returns the one (N + 2 (n_band // 2) * 2, 2)
-    buffer [interior; bands] instead (both are consecutive rows of it).
-
-    defer=True (with merged=True): no launch here -- the draw is registered on the buffer and the
-    phase's mixed forward launch that takes the whole buffer generates the points itself
-    (insr_siren_jet_fwd_mixed_draw: same values, same stream advance, one launch fewer); any
-    other jet launch reading the buffer first draws it with insr_sample_boxes (ensure_drawn).
-    The buffer's values are defined only for the jets until then."""
+    buffer [interior; bands] instead (both are consecutive rows of it)."""
     from . import _native as nat
     dev = torch.device(device)
     if dev.type != "cuda":
@@ -161,51 +153,11 @@ def sample_random_and_bands2D(N, n_band, epsilon=1e-4, device="cuda", merged=Fal
     boxes[0] = nat.Box(x.data_ptr(), N, f3(-1.0, -1.0, 0.0), f3(1.0, 1.0, 0.0))
     for k, (rx, ry) in enumerate(faces):  # face k: rows [k h, (k + 1) h) of bxy, 8 bytes a row
         boxes[1 + k] = nat.Box(bxy.data_ptr() + 8 * h * k, h, f3(rx[0], ry[0], 0.0), f3(rx[1], ry[1], 0.0))
-    if merged and defer:
-        _PENDING[buf.data_ptr()] = (weakref.ref(buf), boxes, seed, state, buf.numel())
-        return buf
     nat.check(nat.lib().insr_sample_boxes(boxes, 5, 2, seed, nat.ptr(state), nat.stream_of(dev)),
               "insr_sample_boxes")
     if merged:
         return buf
     return x, bxy
-
-
-# deferred draws: buffer data_ptr -> (weakref to the buffer, InsrBox array, seed, state, numel)
-_PENDING = {}
-
-
-def pending_draw(t):
-    """(base pointer, buffer, boxes, seed, state) of the deferred draw whose buffer t lies in,
-    or None."""
-    if not _PENDING or not t.is_cuda:
-        return None
-    p = t.data_ptr()
-    for base, (ref, boxes, seed, state, numel) in list(_PENDING.items()):
-        b = ref()
-        if b is None or b.data_ptr() != base:  # freed (its memory may serve another tensor now)
-            del _PENDING[base]
-            continue
-        if base <= p < base + 4 * numel:
-            return base, b, boxes, seed, state
-    return None
-
-
-def consume_draw(base):
-    """The draw at `base` is generated by the launch being issued (insr_siren_jet_fwd_mixed_draw)."""
-    _PENDING.pop(base, None)
-
-
-def ensure_drawn(t):
-    """Run the deferred draw t's buffer waits for (one insr_sample_boxes launch), if any."""
-    pd = pending_draw(t)
-    if pd is None:
-        return
-    from . import _native as nat
-    base, buf, boxes, seed, state = pd
-    del _PENDING[base]
-    nat.check(nat.lib().insr_sample_boxes(boxes, len(boxes), buf.shape[1], seed, nat.ptr(state),
-                                          nat.stream_of(buf.device)), "insr_sample_boxes")
 
 
 def sample_boxes(boxes, dim, device="cuda"):

@@ -377,96 +377,46 @@ struct AdamList {
   float* v[INSR_ADAM_MAX_TENSORS];
   long n[INSR_ADAM_MAX_TENSORS];
   long start[INSR_ADAM_MAX_TENSORS + 1];  // prefix sums of n
-  long start8[INSR_ADAM_MAX_TENSORS + 1]; // prefix sums of the 8 x 32 hidden-weight tiles (nets with planes)
   int shape[INSR_ADAM_MAX_TENSORS][4];    // SIREN (d_in, d_out, L, W) of a flat buffer with weight planes, else 0s
   const float* loss;                      // != NULL: the last block runs the plateau step on it
   int patience;
   int count;
 };
 
-// is flat index i a hidden-layer weight (W x W, j >= 1) of the SIREN shape sh?
-__device__ __forceinline__ bool hidden_weight(const int (&sh)[4], long i) {
-  const int din = sh[0], L = sh[2], W = sh[3];
+// the updated hidden weight (layer j, row n, column m) of a buffer with pre-split planes:
+// its three bf16 terms (jet_x6.hpp split, element-wise identical to wsplit_kernel) stored
+// into both fragment orientations (jet_common.hpp wsplit_offset) -- the planes stay current
+// without a launch of their own
+__device__ __forceinline__ void adam_wsplit(float* base, const int (&sh)[4], long i, float w) {
+  const int din = sh[0], dout = sh[1], L = sh[2], W = sh[3];
   const long off = i - ((long)W * din + W);
   const long per = (long)W * W + W;
-  return off >= 0 && off < (long)L * per && off % per < (long)W * W;
-}
-
-typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ unsigned short bf16_bits(float v) { return __builtin_bit_cast(unsigned short, (__bf16)v); }
-
-// hidden weights of a net with weight planes, one BLOCK per 8 x 32 tile of W_j (rows n0..n0+7,
-// columns m0..m0+31; L W^2 / 256 blocks): each thread updates one weight (torch's op order,
-// bit-identical to the element-wise path; a wave reads two 128-B row segments) and stages it in
-// LDS; then the tile's fragments -- W_j rows (k = 8 consecutive m: 32 of them) and W_j^T rows
-// (k = n0..n0+7: 32) -- leave as three 16-B stores each, instead of 6 scattered 2-B stores per
-// weight.  Block of kAdamThreads = 256 threads.
-constexpr int kAdamThreads = 256;
-__device__ __forceinline__ void split3_u16(float w, unsigned short& h16, unsigned short& m16, unsigned short& l16) {
-  const __bf16 h = (__bf16)w;
-  float rs = w - (float)h;
-  const __bf16 md = (__bf16)rs;
-  rs -= (float)md;
-  h16 = __builtin_bit_cast(unsigned short, h);
-  m16 = __builtin_bit_cast(unsigned short, md);
-  l16 = bf16_bits(rs);
-}
-
-__device__ __forceinline__ void store_frag3(unsigned short* pl, long ov, int o, long fr, int g, int row,
-                                            const float (&v)[8]) {
-  unsigned short t[3][8];
-#pragma unroll
-  for (int jj = 0; jj < 8; ++jj) split3_u16(v[jj], t[0][jj], t[1][jj], t[2][jj]);
-#pragma unroll
-  for (int q = 0; q < 3; ++q) {
-    u32x4 u;
-#pragma unroll
-    for (int w4 = 0; w4 < 4; ++w4) u[w4] = (unsigned)t[q][2 * w4] | ((unsigned)t[q][2 * w4 + 1] << 16);
-    *reinterpret_cast<u32x4*>(pl + o * ov + ((fr + q) * 64 + 16 * g + (row & 15)) * 8) = u;
-  }
-}
-
-__device__ __forceinline__ void adam_tile(const AdamList& L, int k, long tile, float step_size, float bc2s, float w1,
-                                          float w2, float b2, float eps) {
-  __shared__ float sw[8][33];
-  const int din = L.shape[k][0], dout = L.shape[k][1], Ln = L.shape[k][2], W = L.shape[k][3];
-  const int NT = W / 16, KC = W / 32, per_layer = (W / 8) * KC;
-  const int j = 1 + (int)(tile / per_layer);
-  const int tl = (int)(tile % per_layer);
-  const int n0 = 8 * (tl / KC), m0 = 32 * (tl % KC);
-  float* P = L.p[k];
-  const int r = threadIdx.x >> 5, c = threadIdx.x & 31;
+  if (off < 0 || off >= (long)L * per) return;
+  const long r = off % per;
+  if (r >= (long)W * W) return;  // a bias
+  const int j = 1 + (int)(off / per), n = (int)(r / W), m = (int)(r % W);
+  const int NT = W / 16, KC = W / 32;
+  unsigned short t[3];
   {
-    const long i = hidden_off(din, W, j) + (long)(n0 + r) * W + m0 + c;
-    const float g = L.g[k][i];
-    const float mv = L.m[k][i];
-    const float mi = mv + w1 * (g - mv);
-    const float vi = L.v[k][i] * b2 + w2 * g * g;
-    L.m[k][i] = mi;
-    L.v[k][i] = vi;
-    const float denom = sqrtf(vi) / bc2s + eps;
-    const float pv = P[i] - step_size * (mi / denom);
-    P[i] = pv;
-    sw[r][c] = pv;
+    const __bf16 h = (__bf16)w;
+    float rs = w - (float)h;
+    const __bf16 md = (__bf16)rs;
+    rs -= (float)md;
+    const __bf16 lo = (__bf16)rs;
+    t[0] = __builtin_bit_cast(unsigned short, h);
+    t[1] = __builtin_bit_cast(unsigned short, md);
+    t[2] = __builtin_bit_cast(unsigned short, lo);
   }
-  __syncthreads();
-  if (threadIdx.x >= 64) return;
-  unsigned short* pl = reinterpret_cast<unsigned short*>(P + wsplit_offset(din, dout, Ln, W));
-  const long ov = wsplit_orient_vecs(Ln, W) * 8;  // u16 per orientation
-  float v[8];
-  if (threadIdx.x < 32) {  // orientation 0: lane row n = n0 + rr, k = m0 + 8 q8 .. + 7
-    const int rr = threadIdx.x >> 2, q8 = threadIdx.x & 3;
+  unsigned short* pl = reinterpret_cast<unsigned short*>(base + wsplit_offset(din, dout, L, W));
+  const long ov = wsplit_orient_vecs(L, W) * 8;  // u16 per orientation
+  // orientation 0: A row n, k = m; orientation 1: A row m (W^T), k = n
+  const int rr[2] = {n, m}, kk[2] = {m, n};
 #pragma unroll
-    for (int jj = 0; jj < 8; ++jj) v[jj] = sw[rr][8 * q8 + jj];
-    const int kb = m0 + 8 * q8;
-    const long fr = (((long)(j - 1) * NT + ((n0 + rr) >> 4)) * KC + (kb >> 5)) * 3;
-    store_frag3(pl, ov, 0, fr, (kb & 31) >> 3, n0 + rr, v);
-  } else {  // orientation 1: lane row m = m0 + cc (of W^T), k = n0 .. n0 + 7
-    const int cc = threadIdx.x - 32, m = m0 + cc;
+  for (int o = 0; o < 2; ++o) {
+    const int rt = rr[o] >> 4, c = rr[o] & 15, kc = kk[o] >> 5, g = (kk[o] & 31) >> 3, jj = kk[o] & 7;
+    const long fr = (((long)(j - 1) * NT + rt) * KC + kc) * 3;
 #pragma unroll
-    for (int jj = 0; jj < 8; ++jj) v[jj] = sw[jj][cc];
-    const long fr = (((long)(j - 1) * NT + (m >> 4)) * KC + (n0 >> 5)) * 3;
-    store_frag3(pl, ov, 1, fr, (n0 & 31) >> 3, m, v);
+    for (int q = 0; q < 3; ++q) pl[o * ov + ((fr + q) * 64 + 16 * g + c) * 8 + jj] = t[q];
   }
 }
 
@@ -488,27 +438,20 @@ __global__ void adam_multi_kernel(AdamList L, float* __restrict__ st, float b1, 
   const float w1 = (float)(1.0 - (double)b1);
   const float w2 = (float)(1.0 - (double)b2);
   const long total = L.start[L.count];
-  const int nbe = (int)gridDim.x - (int)L.start8[L.count];  // blocks of the element-wise part
-  if ((int)blockIdx.x >= nbe) {  // an 8 x 32 tile of hidden weights (nets with planes)
-    const long ti = (long)blockIdx.x - nbe;
+  for (long gi = (long)blockIdx.x * blockDim.x + threadIdx.x; gi < total; gi += (long)gridDim.x * blockDim.x) {
     int k = 0;
-    while (k + 1 < L.count && ti >= L.start8[k + 1]) ++k;
-    adam_tile(L, k, ti - L.start8[k], step_size, bc2s, w1, w2, b2, eps);
-  } else {
-    for (long gi = (long)blockIdx.x * blockDim.x + threadIdx.x; gi < total; gi += (long)nbe * blockDim.x) {
-      int k = 0;
-      while (k + 1 < L.count && gi >= L.start[k + 1]) ++k;
-      const long i = gi - L.start[k];
-      if (L.shape[k][2] > 0 && hidden_weight(L.shape[k], i)) continue;  // adam_tile's
-      const float g = L.g[k][i];
-      const float m0 = L.m[k][i];
-      const float mi = m0 + w1 * (g - m0);
-      const float vi = L.v[k][i] * b2 + w2 * g * g;
-      L.m[k][i] = mi;
-      L.v[k][i] = vi;
-      const float denom = sqrtf(vi) / bc2s + eps;
-      L.p[k][i] = L.p[k][i] - step_size * (mi / denom);
-    }
+    while (k + 1 < L.count && gi >= L.start[k + 1]) ++k;
+    const long i = gi - L.start[k];
+    const float g = L.g[k][i];
+    const float m0 = L.m[k][i];
+    const float mi = m0 + w1 * (g - m0);
+    const float vi = L.v[k][i] * b2 + w2 * g * g;
+    L.m[k][i] = mi;
+    L.v[k][i] = vi;
+    const float denom = sqrtf(vi) / bc2s + eps;
+    const float pn = L.p[k][i] - step_size * (mi / denom);
+    L.p[k][i] = pn;
+    if (L.shape[k][2] > 0) adam_wsplit(L.p[k], L.shape[k], i, pn);
   }
   if (L.loss) {  // fused scheduler step: every block read lr / t above before it takes a ticket
     __syncthreads();
@@ -730,39 +673,7 @@ int insr_siren_jet_fwd_multi(const InsrJetJob* jobs, int njobs, int din, int dou
 
 int insr_siren_jet_fwd_mixed(const InsrJetJob* jobs, const int* modes, const float* scalars, int njobs, int din,
                              int dout, int L, int W, int prec_mode, void* stream) {
-  return insr_siren_jet_fwd_mixed_draw(jobs, modes, scalars, njobs, din, dout, L, W, prec_mode, nullptr, stream);
-}
-
-int insr_siren_jet_fwd_mixed_draw(const InsrJetJob* jobs, const int* modes, const float* scalars, int njobs, int din,
-                                  int dout, int L, int W, int prec_mode, const InsrDraw* draw, void* stream) {
   if (!jobs || !modes || njobs < 1 || njobs > INSR_MAX_FWD_JOBS) return INSR_EINVAL;
-  // the draw: consecutive boxes of one (rows, din) buffer, a writer whose x covers all of it
-  DrawPk dp{};
-  if (draw) {
-    if (!draw->boxes || !draw->state || draw->n_boxes < 1 || draw->n_boxes > INSR_MAX_BOXES || draw->dim != din ||
-        draw->writer < 0 || draw->writer >= njobs)
-      return INSR_EINVAL;
-    dp.buf = draw->boxes[0].out;
-    dp.nbox = draw->n_boxes;
-    dp.dim = din;
-    dp.seed = draw->seed;
-    dp.state = (unsigned long long*)draw->state;
-    long rows = 0;
-    for (int b = 0; b < draw->n_boxes; ++b) {
-      const InsrBox& bx = draw->boxes[b];
-      if (bx.n < 0 || bx.out != dp.buf + rows * din) return INSR_EINVAL;
-      dp.row_first[b] = rows;
-      for (int j = 0; j < 3; ++j) {
-        dp.lo[b][j] = bx.lo[j];
-        dp.hi[b][j] = bx.hi[j];
-      }
-      rows += bx.n;
-    }
-    for (int b = draw->n_boxes; b <= INSR_MAX_BOXES; ++b) dp.row_first[b] = rows;
-    dp.rows = rows;
-    const InsrJetJob& wj = jobs[draw->writer];
-    if (wj.x != dp.buf || wj.n != rows || modes[draw->writer] == INSR_MIX_ADVECT) return INSR_EINVAL;
-  }
   if (prec_mode & INSR_MODE_MASK) return INSR_EINVAL;  // the per-job jet modes come from `modes`
   long total = 0;
   for (int k = 0; k < njobs; ++k) {
@@ -786,30 +697,14 @@ int insr_siren_jet_fwd_mixed_draw(const InsrJetJob* jobs, const int* modes, cons
   if (total > 0x7fffffffL) return INSR_EINVAL;
   const JetCall c(din, W, INSR_MODE_VALUE | prec_mode);
   hipStream_t st = (hipStream_t)stream;
-  if (draw && !(c.NT == 8 && c.nqf > 0)) {  // no mixed kernel for this shape: draw first, then as usual
-    const int rc = insr_sample_boxes(draw->boxes, draw->n_boxes, din, draw->seed, draw->state, stream);
-    if (rc) return rc;
-    draw = nullptr;
-  }
   if (c.NT == 8 && c.nqf > 0) {
     InsrJetJob pk[INSR_MAX_FWD_JOBS];
     int md[INSR_MAX_FWD_JOBS];
-    long row0[INSR_MAX_FWD_JOBS];
-    int writer = -1;
     int m = 0;
     for (int k = 0; k < njobs; ++k) {
       if (jobs[k].n == 0) continue;
       pk[m] = jobs[k];
       md[m] = modes[k];
-      row0[m] = -1;
-      if (draw) {  // a job reading rows of the draw generates them
-        const float* xj = jobs[k].x;
-        if (xj >= dp.buf && xj < dp.buf + dp.rows * din) {
-          if ((xj - dp.buf) % din || (xj - dp.buf) / din + jobs[k].n > dp.rows) return INSR_EINVAL;
-          row0[m] = (long)((xj - dp.buf) / din);
-        }
-        if (k == draw->writer) writer = m;
-      }
       int rc = 0;
       const int dk = jobs[k].d_out > 0 ? jobs[k].d_out : dout;
       if (!(pk[m].params = with_planes(jobs[k].params, din, dk, L, W, prec_mode, st, k, &rc))) return rc;
@@ -822,11 +717,10 @@ int insr_siren_jet_fwd_mixed_draw(const InsrJetJob* jobs, const int* modes, cons
         for (int r = 0; r < 3; ++r) sc[3 * q + r] = scalars ? scalars[3 * k + r] : 0.f;
         ++q;
       }
-    const DrawPk* dpp = draw ? &dp : nullptr;
     switch (c.nqf) {
-      case 3: return dispatch_fwd_mixed_q<3>(c.NT, din, pk, md, sc, m, dout, L, dpp, row0, writer, st);
-      case 2: return dispatch_fwd_mixed_q<2>(c.NT, din, pk, md, sc, m, dout, L, dpp, row0, writer, st);
-      default: return dispatch_fwd_mixed_q<1>(c.NT, din, pk, md, sc, m, dout, L, dpp, row0, writer, st);
+      case 3: return dispatch_fwd_mixed_q<3>(c.NT, din, pk, md, sc, m, dout, L, st);
+      case 2: return dispatch_fwd_mixed_q<2>(c.NT, din, pk, md, sc, m, dout, L, st);
+      default: return dispatch_fwd_mixed_q<1>(c.NT, din, pk, md, sc, m, dout, L, st);
     }
   }
   for (int k = 0; k < njobs; ++k) {  // other widths / exact fp32: one launch per job
@@ -1049,7 +943,6 @@ static int adam_launch(int count, float* const* params, const float* const* grad
   L.patience = patience;
   L.count = count;
   L.start[0] = 0;
-  L.start8[0] = 0;
   for (int k = 0; k < count; ++k) {
     for (int q = 0; q < 4; ++q) L.shape[k][q] = shapes ? shapes[4 * k + q] : 0;
     if (L.shape[k][2] > 0) {  // a SIREN flat buffer with weight planes: its shape must match its size
@@ -1064,17 +957,12 @@ static int adam_launch(int count, float* const* params, const float* const* grad
     L.v[k] = exp_avg_sq[k];
     L.n[k] = sizes[k];
     L.start[k + 1] = L.start[k] + sizes[k];
-    L.start8[k + 1] = L.start8[k] + (L.shape[k][2] > 0 ? (long)L.shape[k][2] * L.shape[k][3] * L.shape[k][3] / 256 : 0);
   }
-  const long total = L.start[count] + L.start8[count];
+  const long total = L.start[count];
   if (total == 0) return loss ? insr_plateau_step(st, loss, patience, 1, stream) : 0;
-  // element-wise blocks (every parameter outside the planes' hidden weights; a net without
-  // planes entirely) + one block per 8 x 32 hidden tile
-  long blocks = (L.start[count] + kAdamThreads - 1) / kAdamThreads;
+  long blocks = (total + 255) / 256;
   if (blocks > 1024) blocks = 1024;
-  if (blocks < 1) blocks = 1;
-  blocks += L.start8[count];
-  hipLaunchKernelGGL(adam_multi_kernel, dim3((unsigned)blocks), dim3(kAdamThreads), 0, (hipStream_t)stream, L, st, b1, b2,
+  hipLaunchKernelGGL(adam_multi_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, L, st, b1, b2,
                      eps, step_offset);
   return (int)hipGetLastError();
 }

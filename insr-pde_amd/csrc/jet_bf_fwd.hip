@@ -12,7 +12,7 @@ template int dispatch_fwd_q<2>(int, int, bool, int, const float*, int, int, int,
 template int dispatch_fwd_multi_q<2>(int, int, bool, int, const InsrJetJob*, const int*, const int*, int, int, int,
                                      int, hipStream_t);
 template int dispatch_fwd_mixed_q<1>(int, int, const InsrJetJob*, const int*, const float*, int, int, int,
-                                     const DrawPk*, const long*, int, hipStream_t);
+                                     hipStream_t);
 template int dispatch_fwd_mixed_q<2>(int, int, const InsrJetJob*, const int*, const float*, int, int, int,
-                                     const DrawPk*, const long*, int, hipStream_t);
+                                     hipStream_t);
 }  // namespace insr

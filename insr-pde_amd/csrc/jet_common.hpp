@@ -317,58 +317,6 @@ template <int NQ>
 int dispatch_fwd_q(int NT, int S, bool LAP, int T, const float* x, int N, int din, int dout, int L,
                    const float* prm, float* y, float* dy, float* lap, float* act, int nbal, hipStream_t st);
 constexpr int kFwdJobs = INSR_MAX_FWD_JOBS;
-
-// Philox-4x32-10 (Random123; the generator cuRAND / rocRAND / torch use): the collocation
-// sampler's stream (sampler.hip) and the draw generated inside a forward (DrawPk)
-__device__ __forceinline__ uint4 philox4x32_10(unsigned long long key, unsigned long long ctr) {
-  unsigned c0 = (unsigned)ctr, c1 = (unsigned)(ctr >> 32), c2 = 0u, c3 = 0u;
-  unsigned k0 = (unsigned)key, k1 = (unsigned)(key >> 32);
-#pragma unroll
-  for (int r = 0; r < 10; ++r) {
-    const unsigned hi0 = __umulhi(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
-    const unsigned hi1 = __umulhi(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
-    const unsigned n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
-    c0 = n0;
-    c1 = lo1;
-    c2 = n2;
-    c3 = lo0;
-    k0 += 0x9E3779B9u;
-    k1 += 0xBB67AE85u;
-  }
-  return uint4{c0, c1, c2, c3};
-}
-
-// An iteration's collocation draw generated INSIDE a mixed forward launch
-// (insr_siren_jet_fwd_mixed_draw): the insr_sample_boxes values of boxes that are consecutive rows
-// of one (rows, dim) buffer -- value v = row * dim + j of the launch is Philox(seed, base + v / 4)
-// [v % 4] -> lo + (hi - lo) u, u = (bits >> 8) 2^-24, exactly as sample_boxes_kernel.
-struct DrawPk {
-  float* buf;                  // NULL: no draw in this launch
-  long rows;
-  int nbox, dim;
-  long row_first[INSR_MAX_BOXES + 1];
-  float lo[INSR_MAX_BOXES][3], hi[INSR_MAX_BOXES][3];
-  unsigned long long seed;
-  unsigned long long* state;   // [0] stream position, [1] (low 32 bits) ticket
-};
-__device__ __forceinline__ float draw_value(const DrawPk& d, unsigned long long base, long row, int j) {
-  // selects only: no dynamic (per-lane) indexing of the kernel argument
-  auto pick = [j](const float (&a)[3]) { return j == 0 ? a[0] : (j == 1 ? a[1] : a[2]); };
-  float lo = pick(d.lo[0]), hi = pick(d.hi[0]);
-#pragma unroll
-  for (int b = 1; b < INSR_MAX_BOXES; ++b)
-    if (b < d.nbox && row >= d.row_first[b]) {
-      lo = pick(d.lo[b]);
-      hi = pick(d.hi[b]);
-    }
-  const long v = row * d.dim + j;
-  const uint4 r = philox4x32_10(d.seed, base + (unsigned long long)(v >> 2));
-  const int e = (int)(v & 3);
-  const unsigned bits = e == 0 ? r.x : e == 1 ? r.y : e == 2 ? r.z : r.w;
-  const float u = (float)(bits >> 8) * 5.9604644775390625e-8f;  // 2^-24
-  return lo + (hi - lo) * u;
-}
-
 template <int NQ>
 int dispatch_fwd_multi_q(int NT, int S, bool LAP, int T, const InsrJetJob* jobs, const int* small, const int* nbal,
                          int njobs, int din, int dout, int L, hipStream_t st);
@@ -384,7 +332,7 @@ int dispatch_wide_bwd_q(int NT, int S, bool LAP, const float* x, int N, int din,
 long wide_work_floats(long n, int din, int dout, int L, int W, int S);
 template <int NQ>
 int dispatch_fwd_mixed_q(int NT, int din, const InsrJetJob* jobs, const int* modes, const float* scalars, int njobs,
-                         int dout, int L, const DrawPk* draw, const long* row0, int writer, hipStream_t st);
+                         int dout, int L, hipStream_t st);
 // the pre-split weight planes of (prm, shape) written to `planes` (wsplit_offset floats after prm
 // in a params buffer of INSR_MODE_WSPLIT), one launch
 int wsplit_launch(const float* prm, int din, int dout, int L, int W, float* planes, hipStream_t st);

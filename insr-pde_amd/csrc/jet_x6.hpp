@@ -193,8 +193,7 @@ template <int NQ, int NT, int S, bool LAP, int T>
 __device__ __forceinline__ void fwd_x6_block(const float* __restrict__ x, int N, int din, int dout, int L,
                                              const float* __restrict__ prm, float* __restrict__ y,
                                              float* __restrict__ dy, float* __restrict__ lap,
-                                             float* __restrict__ act, const int tile0, const int cnt_rt,
-                                             const long x_row0 = 0) {
+                                             float* __restrict__ act, const int tile0, const int cnt_rt) {
   using G = X6Geo<NT>;
   constexpr int W = G::W, RPW = G::RPW, LDB = G::LDB, WV = G::WV, PLANE = G::PLANE, KC = G::KC;
   constexpr int NTAN = LAP ? S - 2 : S - 1;
@@ -212,8 +211,7 @@ __device__ __forceinline__ void fwd_x6_block(const float* __restrict__ x, int N,
 #pragma unroll
   for (int t = 0; t < T; ++t) {
     const int p = (tile0 + t) * 16 + c;
-    // x holds points x_row0.. (0: the whole batch; a mixed launch's generated draw: the block's)
-    for (int k = 0; k < 3; ++k) xv[t][k] = (t < cnt && p < N && k < din) ? x[(long)(p - x_row0) * din + k] : 0.f;
+    for (int k = 0; k < 3; ++k) xv[t][k] = (t < cnt && p < N && k < din) ? x[(long)p * din + k] : 0.f;
   }
 
   floatx4 a[T][RPW][S];
@@ -429,9 +427,6 @@ struct FwdMixX6 {
   int mode[kFwdJobs];     // INSR_MODE_VALUE / GRAD / LAP / INSR_MIX_ADVECT
   float sc[kFwdJobs][3];  // INSR_MIX_ADVECT: dt, lo, hi
   int njobs;
-  DrawPk draw;             // draw.buf != NULL: the iteration's points generated in this launch
-  long row0[kFwdJobs];     // >= 0: job k's x starts at row row0[k] of draw.buf
-  int writer;              // the job that stores the draw (its x covers every row)
 };
 
 // BODIES: the job kinds a kernel instance carries (bit m = jet mode m, bit 3 = INSR_MIX_ADVECT):
@@ -460,57 +455,24 @@ __global__ __launch_bounds__(X6Geo<NT>::THREADS, (BODIES & kMixL) ? 6 : 4) void 
   const InsrJetJob& jb = jobs.job[k];
   const int dk = jb.d_out > 0 ? jb.d_out : dout;
   const int lb = b - jobs.first[k];
-  // the iteration's draw (jobs.draw.buf != NULL): a job reading its rows generates the block's
-  // points (one Philox value per thread) into a small LDS array and runs its body on that (the
-  // writer job also stores them for the backward); the stream position is read once per block
-  // and the last block to finish advances it (every block has read it by then), as
-  // sample_boxes_kernel does
-  __shared__ unsigned long long s_base;
-  __shared__ float s_x[2 * 16 * 3];  // <= 2 tiles of a block, d_in <= 3
-  const float* xj = jb.x;
-  long xr0 = 0;  // the first point xj holds
-  const bool adv = jobs.mode[k] == INSR_MIX_ADVECT;
-  const int tb = (jobs.mode[k] == INSR_MODE_VALUE || adv) ? 2 : 1;  // tiles per block of this body
-  if (jobs.draw.buf) {
-    if (threadIdx.x == 0) s_base = jobs.draw.state[0];
-    __syncthreads();
-    if (jobs.row0[k] >= 0) {
-      int t0, cn = 1;
-      if (tb == 2)
-        block_tiles(lb, (int)jb.n, 2, 0, t0, cn);
-      else
-        t0 = lb;
-      const long p0 = (long)t0 * 16;
-      for (int i = threadIdx.x; i < cn * 16 * DIN; i += blockDim.x) {
-        const long p = p0 + i / DIN;
-        if (p >= jb.n) continue;
-        const float v = draw_value(jobs.draw, s_base, jobs.row0[k] + p, i % DIN);
-        s_x[i] = v;
-        if (k == jobs.writer) const_cast<float*>(jb.x)[p * DIN + i % DIN] = v;
-      }
-      __syncthreads();
-      xj = s_x;  // the block's points, from point p0 on
-      xr0 = p0;
-    }
-  }
   int tile0, cnt;
   switch (jobs.mode[k]) {
     case INSR_MODE_VALUE:
       if constexpr ((BODIES & kMixV) != 0) {
         block_tiles(lb, (int)jb.n, 2, 0, tile0, cnt);
-        fwd_x6_block<NQ, NT, 1, false, 2>(xj, (int)jb.n, DIN, dk, L, jb.params, jb.y, jb.dy, jb.lap, jb.act, tile0,
-                                          cnt, xr0);
+        fwd_x6_block<NQ, NT, 1, false, 2>(jb.x, (int)jb.n, DIN, dk, L, jb.params, jb.y, jb.dy, jb.lap, jb.act, tile0,
+                                          cnt);
       }
       break;
     case INSR_MODE_GRAD:
       if constexpr ((BODIES & kMixG) != 0)
-        fwd_x6_block<NQ, NT, 1 + DIN, false, 1>(xj, (int)jb.n, DIN, dk, L, jb.params, jb.y, jb.dy, jb.lap, jb.act,
-                                                lb, 1, xr0);
+        fwd_x6_block<NQ, NT, 1 + DIN, false, 1>(jb.x, (int)jb.n, DIN, dk, L, jb.params, jb.y, jb.dy, jb.lap, jb.act,
+                                                lb, 1);
       break;
     case INSR_MODE_LAP:
       if constexpr (DIN <= 2 && (BODIES & kMixL) != 0)
-        fwd_x6_block<NQ, NT, 2 + DIN, true, 1>(xj, (int)jb.n, DIN, dk, L, jb.params, jb.y, jb.dy, jb.lap, jb.act,
-                                               lb, 1, xr0);
+        fwd_x6_block<NQ, NT, 2 + DIN, true, 1>(jb.x, (int)jb.n, DIN, dk, L, jb.params, jb.y, jb.dy, jb.lap, jb.act,
+                                               lb, 1);
       break;
     default: {  // INSR_MIX_ADVECT: y = f(clamp(x - dt f(x), lo, hi)), f(x) -> dy, the foot -> lap
       if constexpr ((BODIES & kMixA) == 0) break;
@@ -520,7 +482,7 @@ __global__ __launch_bounds__(X6Geo<NT>::THREADS, (BODIES & kMixL) ? 6 : 4) void 
       block_tiles(lb, n, 2, 0, tile0, cnt);
       float* up = jb.dy;
       float* foot = jb.lap;
-      fwd_x6_block<NQ, NT, 1, false, 2>(xj, n, DIN, dk, L, jb.params, up, nullptr, nullptr, nullptr, tile0, cnt, xr0);
+      fwd_x6_block<NQ, NT, 1, false, 2>(jb.x, n, DIN, dk, L, jb.params, up, nullptr, nullptr, nullptr, tile0, cnt);
       // the block's own global writes, read back by its other waves: workgroup scope (the
       // stores drain before the barrier; the lines were never cached in this CU's L1)
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
@@ -529,7 +491,7 @@ __global__ __launch_bounds__(X6Geo<NT>::THREADS, (BODIES & kMixL) ? 6 : 4) void 
       for (int i = threadIdx.x; i < cnt * 16 * DIN; i += blockDim.x) {
         const long p = (long)tile0 * 16 + i / DIN;
         const int kk = i % DIN;
-        if (p < n) foot[p * DIN + kk] = fminf(fmaxf(fmaf(a, up[p * dk + kk], xj[(p - xr0) * DIN + kk]), lo), hi);
+        if (p < n) foot[p * DIN + kk] = fminf(fmaxf(fmaf(a, up[p * dk + kk], jb.x[p * DIN + kk]), lo), hi);
       }
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
       __syncthreads();
@@ -537,18 +499,11 @@ __global__ __launch_bounds__(X6Geo<NT>::THREADS, (BODIES & kMixL) ? 6 : 4) void 
       break;
     }
   }
-  if (jobs.draw.buf && threadIdx.x == 0) {
-    unsigned* ticket = reinterpret_cast<unsigned*>(jobs.draw.state + 1);
-    if (atomicAdd(ticket, 1u) == gridDim.x - 1) {
-      jobs.draw.state[0] = s_base + (unsigned long long)((jobs.draw.rows * jobs.draw.dim + 3) / 4);
-      atomicExch(ticket, 0u);
-    }
-  }
 }
 
 template <int NQ, int NT, int DIN, int BODIES>
 int launch_fwd_x6_mixed_t(const InsrJetJob* jobs, const int* modes, const float* scalars, int njobs, int dout, int L,
-                          const DrawPk* draw, const long* row0, int writer, hipStream_t st) {
+                          hipStream_t st) {
   constexpr size_t lds = fwd_mix_lds_bytes<NQ, NT, DIN, BODIES>();
   if constexpr (lds > kLdsMax) {
     return INSR_EINVAL;
@@ -573,11 +528,6 @@ int launch_fwd_x6_mixed_t(const InsrJetJob* jobs, const int* modes, const float*
     }
     pk.first[njobs] = nb;
     pk.njobs = njobs;
-    if (draw) {
-      pk.draw = *draw;
-      for (int k = 0; k < njobs; ++k) pk.row0[k] = row0[k];
-      pk.writer = writer;
-    }
     if (nb == 0) return 0;
     hipLaunchKernelGGL((jet_fwd_x6_mixed<NQ, NT, DIN, BODIES>), dim3(nb), dim3(X6Geo<NT>::THREADS), lds, st, pk, dout,
                        L);

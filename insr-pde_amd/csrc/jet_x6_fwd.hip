@@ -7,5 +7,5 @@ template int dispatch_fwd_q<3>(int, int, bool, int, const float*, int, int, int,
 template int dispatch_fwd_multi_q<3>(int, int, bool, int, const InsrJetJob*, const int*, const int*, int, int, int,
                                      int, hipStream_t);
 template int dispatch_fwd_mixed_q<3>(int, int, const InsrJetJob*, const int*, const float*, int, int, int,
-                                     const DrawPk*, const long*, int, hipStream_t);
+                                     hipStream_t);
 }  // namespace insr

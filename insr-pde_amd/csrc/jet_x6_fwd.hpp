@@ -66,16 +66,16 @@ int dispatch_fwd_multi_q(int NT, int S, bool LAP, int T, const InsrJetJob* jobs,
 // mixed-mode fused forward (W = 128 only: the tile policy it encodes is the W = 128 one)
 template <int NQ>
 int dispatch_fwd_mixed_q(int NT, int din, const InsrJetJob* jobs, const int* modes, const float* scalars, int njobs,
-                         int dout, int L, const DrawPk* draw, const long* row0, int writer, hipStream_t st) {
+                         int dout, int L, hipStream_t st) {
   if (NT != 8) return INSR_EWIDTH;
   int need = 0;
   for (int k = 0; k < njobs; ++k) need |= 1 << modes[k];
   // the smallest compiled body set that covers the jobs
 #define INSR_MIX_DIN(B)                                                                  \
   switch (din) {                                                                         \
-    case 1: return launch_fwd_x6_mixed_t<NQ, 8, 1, B>(jobs, modes, scalars, njobs, dout, L, draw, row0, writer, st); \
-    case 2: return launch_fwd_x6_mixed_t<NQ, 8, 2, B>(jobs, modes, scalars, njobs, dout, L, draw, row0, writer, st); \
-    case 3: return launch_fwd_x6_mixed_t<NQ, 8, 3, B>(jobs, modes, scalars, njobs, dout, L, draw, row0, writer, st); \
+    case 1: return launch_fwd_x6_mixed_t<NQ, 8, 1, B>(jobs, modes, scalars, njobs, dout, L, st); \
+    case 2: return launch_fwd_x6_mixed_t<NQ, 8, 2, B>(jobs, modes, scalars, njobs, dout, L, st); \
+    case 3: return launch_fwd_x6_mixed_t<NQ, 8, 3, B>(jobs, modes, scalars, njobs, dout, L, st); \
     default: return INSR_EINVAL;                                                         \
   }
   if ((need & ~(kMixV | kMixA)) == 0) INSR_MIX_DIN(kMixV | kMixA)

@@ -25,6 +25,24 @@ struct BoxesPk {
   unsigned long long seed;
 };
 
+__device__ __forceinline__ uint4 philox4x32_10(unsigned long long key, unsigned long long ctr) {
+  unsigned c0 = (unsigned)ctr, c1 = (unsigned)(ctr >> 32), c2 = 0u, c3 = 0u;
+  unsigned k0 = (unsigned)key, k1 = (unsigned)(key >> 32);
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const unsigned hi0 = __umulhi(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
+    const unsigned hi1 = __umulhi(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
+    const unsigned n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+    c0 = n0;
+    c1 = lo1;
+    c2 = n2;
+    c3 = lo0;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  return uint4{c0, c1, c2, c3};
+}
+
 // state[0] = stream position (Philox counter), state[1] (low 32 bits) = the launch's ticket
 __global__ __launch_bounds__(kSampThreads) void sample_boxes_kernel(const BoxesPk pk, long total,
                                                                     unsigned long long* __restrict__ state) {

@@ -20,7 +20,6 @@ from base import (BaseModel, advect_target, axpy_clamp, divergence, fused_forwar
                   merge_samples, mse_term, sample_boundary2D_pair, sample_boundary2D_separate, sample_random,
                   sample_random_and_bands2D, sample_uniform, sq_losses, wall_mse, wall_term)
 from base.diff_ops import jacobian_only
-from base.sampling import ensure_drawn
 
 from .examples import get_examples
 
@@ -52,10 +51,7 @@ class Fluid2DModel(BaseModel):
         first rows, and _merged(x) hands the whole buffer to the jets that take both."""
         n = self._n_interior()
         if torch.device(self.device).type == "cuda":
-            # deferred: the phase's mixed forward launch generates the points itself (one launch
-            # fewer); any other consumer of x draws first (base.sampling.ensure_drawn)
-            buf = sample_random_and_bands2D(n, n // 100, device=self.device, merged=True,
-                                            defer=True).requires_grad_(True)
+            buf = sample_random_and_bands2D(n, n // 100, device=self.device, merged=True).requires_grad_(True)
             x = buf[:n]
             self._insr_merged = (buf, x, (buf.shape[0] - n) // 2)
             return x
@@ -106,7 +102,6 @@ class Fluid2DModel(BaseModel):
     @BaseModel._training_loop
     def _initialize(self):
         x = self._sample_in_training()
-        ensure_drawn(x)  # the initial condition reads the points with torch ops
         return {'main': fused_mse(self.velocity_field(x), self.init_cond_func(x))}
 
     @BaseModel._timestepping

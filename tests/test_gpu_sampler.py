@@ -156,39 +156,3 @@ def test_advection_device_sampler_phase_runs(B, graph):
     assert torch.isfinite(after).all() and not torch.equal(before, after)
     if graph:
         assert getattr(model, "_insr_capture_error", None) is None
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("graph", [False, True])
-def test_deferred_draw_matches_sampler_launch(B, graph, monkeypatch):
-    """The fluid phases with their draws generated inside the mixed forward launch
-    (sample_random_and_bands2D(defer=True) -> insr_siren_jet_fwd_mixed_draw) give bit-identical
-    losses to the same phases with the draw as its own insr_sample_boxes launch: same values,
-    same stream advance (eager and hipGraph-replayed)."""
-    import base.sampling as S
-    import pde.fluid as F
-    from base._loop import PhaseLoop
-    from pde.config import make_config
-    real = S.sample_random_and_bands2D
-    out = []
-    for defer in (True, False):
-        S._SAMPLER.clear()
-        if not defer:
-            monkeypatch.setattr(F, "sample_random_and_bands2D", lambda *a, **k: real(*a, **dict(k, defer=False)))
-        torch.manual_seed(5)
-        cfg = make_config("fluid", proj_dir="/tmp/insr_test", insr_progress=False, early_stop=False, lr=1e-4,
-                          dt=0.05, num_hidden_layers=4, hidden_features=128, sample_resolution=64,
-                          insr_graph=graph, insr_sync_every=10 ** 9)
-        model = F.Fluid2DModel(cfg)
-        model.timestep = 1
-        losses = []
-        for name in ("_advect_velocity", "_solve_pressure", "_projection"):
-            pl = PhaseLoop(model, getattr(F.Fluid2DModel, name)._insr_phase, name, (), {})
-            pl.start()
-            for i in range(4):
-                res = pl.step(i)
-                losses.append([float(v) for v in res.values()])
-        assert not S._PENDING or all(r() is None for r, *_ in S._PENDING.values())
-        out.append(losses)
-        monkeypatch.undo()
-    assert out[0] == out[1]
