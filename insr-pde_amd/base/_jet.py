@@ -252,7 +252,9 @@ def _launch_fused(jobs):
     for (din, L, W, pbits, dev), parts in by_arch.items():
         alljobs = [(m, j) for m, js in parts for j in js]
         adv = any(m == MIX_ADVECT for m, _ in alljobs)
-        if adv or (_MIXED and len(parts) > 1 and W == 128 and len(alljobs) <= nat.MAX_FWD_JOBS
+        # (the mixed kernel's Laplacian body is compiled for d_in <= 2)
+        lap3 = din > 2 and any(m == nat.MODE_LAP for m, _ in alljobs)
+        if adv or (_MIXED and not lap3 and len(parts) > 1 and W == 128 and len(alljobs) <= nat.MAX_FWD_JOBS
                    and all(j[6] <= 40000 for _, j in alljobs)):
             if adv and not (_MIXED and len(alljobs) <= nat.MAX_FWD_JOBS):  # targets alone, the rest as usual
                 tg = [(m, j) for m, j in alljobs if m == MIX_ADVECT]

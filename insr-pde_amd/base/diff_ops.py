@@ -9,7 +9,7 @@ base/_jet.py) and assembles the requested quantity from its streams:
   gradient   :53-58  d(sum_c g_c y_c)/dx   sum_c g_c J[c, :]           (GRAD jet)
   divergence :44-50  sum_i dy_i/dx_i       trace of J                  (GRAD jet)
   jacobian   :61-82  (N, dy, dx), status   J (+ I if y = f(x) + x)    (GRAD jet)
-  laplace    :33-41  div(grad y)           sum_c Lap y_c              (LAP jet)
+  laplace    :33-41  div(grad y)           sum_c Lap y_c              (LAP jet, d_in <= 3)
   hessian    :6-30   (.., dy, dx, dx)      not on the INSR-PDE path: raises
 
 All results stay differentiable w.r.t. the network parameters (loss.backward()

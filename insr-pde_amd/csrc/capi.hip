@@ -473,8 +473,9 @@ bool shape_ok(int din, int dout, int L, int width, int mode) {
   if (po && !prec_ok(po - 1)) return false;
   const int jm = mode & INSR_MODE_MASK;
   const int S = streams_for(din, jm);
-  if (S < 1 || S > 4) return false;
-  if (jm == INSR_MODE_LAP && din > 2) return false;
+  if (S < 1 || S > 5) return false;  // the Laplacian jet of a 3-d input carries 5 streams
+  // ... whose exact-fp32 backward at width 256 does not fit a CU's LDS (5 x 16 x 520 floats)
+  if (S == 5 && nt_for(width) == 16 && (nq_of(call_prec(mode, 0)) == 0 || nq_of(call_prec(mode, 1)) == 0)) return false;
   return true;
 }
 

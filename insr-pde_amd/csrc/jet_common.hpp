@@ -338,7 +338,7 @@ int dispatch_fwd_mixed_q(int NT, int din, const InsrJetJob* jobs, const int* mod
 int wsplit_launch(const float* prm, int din, int dout, int L, int W, float* planes, hipStream_t st);
 void wide_launch_threads(long n, int din, int dout, int L, int W, int S, long* out);
 
-// (S, LAP) combinations: value (1), grad d=1..3 (2..4), lap d=1,2 (3,4)
+// (S, LAP) combinations: value (1), grad d=1..3 (2..4), lap d=1..3 (3..5)
 #define INSR_DISPATCH(NTV, FN, ...)                \
   switch (S * 2 + (LAP ? 1 : 0)) {                 \
     case 2: return FN<NTV, 1, false>(__VA_ARGS__); \
@@ -347,6 +347,7 @@ void wide_launch_threads(long n, int din, int dout, int L, int W, int S, long* o
     case 8: return FN<NTV, 4, false>(__VA_ARGS__); \
     case 7: return FN<NTV, 3, true>(__VA_ARGS__);  \
     case 9: return FN<NTV, 4, true>(__VA_ARGS__);  \
+    case 11: return FN<NTV, 5, true>(__VA_ARGS__); \
     default: return INSR_EINVAL;                   \
   }
 

@@ -40,6 +40,7 @@ int dispatch_bwd_q(int NT, int S, bool LAP, int T, const float* x, int N, int di
     case 8: return launch_bwd_x6<NQ, NTV, 4, false>(T, x, N, din, dout, L, prm, act, gy, gdy, glap, part, P, nbal, st); \
     case 7: return launch_bwd_x6<NQ, NTV, 3, true>(T, x, N, din, dout, L, prm, act, gy, gdy, glap, part, P, nbal, st);  \
     case 9: return launch_bwd_x6<NQ, NTV, 4, true>(T, x, N, din, dout, L, prm, act, gy, gdy, glap, part, P, nbal, st);  \
+    case 11: return launch_bwd_x6<NQ, NTV, 5, true>(T, x, N, din, dout, L, prm, act, gy, gdy, glap, part, P, nbal, st); \
     default: return INSR_EINVAL;                                                                              \
   }
   switch (NT) {

@@ -673,6 +673,7 @@ int wide_bwd_nt(int S, bool LAP, const float* x, int N, int din, int dout, int L
     case 8: return wide_bwd_t<NQ, NT, 4, false>(x, N, din, dout, L, prm, act, gy, gdy, glap, work, grad, accumulate, st);
     case 7: return wide_bwd_t<NQ, NT, 3, true>(x, N, din, dout, L, prm, act, gy, gdy, glap, work, grad, accumulate, st);
     case 9: return wide_bwd_t<NQ, NT, 4, true>(x, N, din, dout, L, prm, act, gy, gdy, glap, work, grad, accumulate, st);
+    case 11: return wide_bwd_t<NQ, NT, 5, true>(x, N, din, dout, L, prm, act, gy, gdy, glap, work, grad, accumulate, st);
     default: return INSR_EINVAL;
   }
 }

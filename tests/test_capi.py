@@ -48,7 +48,8 @@ def test_host_queries(lib):
     assert lib.insr_siren_param_count(2, 2, 5, 128) == 83202
     assert lib.insr_siren_param_count(3, 3, 5, 256) == 330755
     assert lib.insr_siren_supported(2, 1, 4, 128, 2) == 1
-    assert lib.insr_siren_supported(3, 1, 4, 128, 2) == 0   # Laplacian jet: d_in <= 2
+    assert lib.insr_siren_supported(3, 1, 4, 128, 2) == 1   # 5-stream Laplacian jet (d_in = 3)
+    assert lib.insr_siren_supported(4, 1, 4, 128, 2) == 0   # d_in <= 3
     assert lib.insr_siren_supported(2, 1, 4, 100, 0) == 0   # width not compiled
     # saved activations: (L+1) layers x 16 W floats per 16-point tile x S streams
     assert lib.insr_jet_act_bytes(64, 2, 4, 128, 2) == 5 * 4 * 16 * 128 * 4 * 4

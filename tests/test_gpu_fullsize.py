@@ -233,3 +233,22 @@ def test_fused_multi_five_tile_blocks(base):
     (yr * R).sum().backward()
     assert nerr(ua, yr) < TOL
     assert nerr(grads(cur), grads(refc)) < TOL
+
+
+@pytest.mark.parametrize("shape,n", [((3, 1, 4, 128), 10000), ((3, 2, 3, 256), 4096)])
+def test_laplacian_3d_input(base, shape, n):
+    """laplace with a 3-d input (5-stream jet; base/diff_ops.py:33-41): values and parameter
+    gradients vs the oracle, through the default routing (W = 128 from 8,192 points and W = 256:
+    the two-kernel backward)."""
+    din, dout, L, W = shape
+    ref, net = pair(base, din, dout, L, W, 21)
+    x = torch.rand(n, din, generator=torch.Generator().manual_seed(7)) * 2 - 1
+    g = torch.randn(n, 1, generator=torch.Generator().manual_seed(8))
+    xr = x.clone().requires_grad_(True)
+    lr_ = O.op_laplace(ref(xr), xr)
+    ((g - lr_) ** 2).mean().backward()
+    xg = x.cuda().requires_grad_(True)
+    lg = base.laplace(net(xg), xg)
+    ((g.cuda() - lg) ** 2).mean().backward()
+    assert nerr(lg, lr_) < TOL
+    assert nerr(grads(net), grads(ref)) < TOL
