@@ -360,7 +360,9 @@ def siren_value(mlp, x):
     jets = {} if mode == nat.MODE_VALUE else {mode: res}
     y._insr_src, y._insr_jets, y._insr_key = (mlp, x), jets, key
     node = y.grad_fn
-    if node is not None:
+    if node is not None and type(node).__name__ != "ViewBackward0":
+        # (batched x (..., d): y is a view of the jet's 2-D output -- a C++ node that takes no
+        # attributes; the tensor's own provenance serves diff ops on y itself)
         node._insr_src, node._insr_jets, node._insr_key = (mlp, x), jets, key
     return y
 
