@@ -295,7 +295,7 @@ def kernel_identity(kind, mode, n, din, dout, L, W, nq=3):
         nat.check(lib.insr_jet_wide_launch_threads(n, din, dout, L, W, m, thr), "insr_jet_wide_launch_threads")
         parts = [(f"insr::jet_bwd_x6p<{nq}, {NT}, {S}, {lap}>", thr[0]), (f"insr::dw_x6<{nq}, {NT}, {S}, {lap}>", thr[1]),
                  ("insr::reduce_dw_kernel", thr[2])]
-        return " + ".join(f"{k}|grid={g}" for k, g in parts) + " (two-kernel backward; time = all its launches, incl. the W^T split)", \
+        return " + ".join(f"{k}|grid={g}" for k, g in parts) + " (two-kernel backward: propagation, dW GEMM + row partials, sums; time = all three launches)", \
             parts, True
     T = lib.insr_jet_split_tiles(n, din, W, m, 1 if kind == "bwd" else 0)
     nb = ((n + 15) // 16 + T - 1) // T
