@@ -200,7 +200,7 @@ int insr_jet_split_tiles(long n_points, int d_in, int width, int mode, int backw
 
 /* Tile-count policy: force T for forward / backward (0 = auto: the largest T
  * whose LDS fits, lowered while the grid has fewer than min_blocks blocks).
- * Env: INSR_SPLIT_TILES_FWD, INSR_SPLIT_TILES_BWD, INSR_SPLIT_MIN_BLOCKS. */
+ * A/B-study knob (tools/); the default policy needs no call. */
 void insr_jet_set_split_tiles(int fwd_tiles, int bwd_tiles, int min_blocks);
 
 void insr_jet_get_split_tiles(int* fwd_tiles, int* bwd_tiles, int* min_blocks);

@@ -226,14 +226,18 @@ class _SqLossGroup(torch.autograd.Function):
         k = len(ctx.metas)
         res = [None] * len(tensors)
         unit = [g is not None and g.numel() == 1 and g.data_ptr() in _UNIT_SEEDS for g in gouts]
+        # the forward's precomputed gradients are handed out once; a repeated backward
+        # (retain_graph=True) gets copies, so nothing downstream can alias the kept buffers
+        pre = ctx.pre if not getattr(ctx, "pre_used", False) else [None if g is None else g.clone() for g in ctx.pre]
+        ctx.pre_used = True
         for o in range(k):
             if owner[o] is not None:
                 continue
             members = [o] + [j for j in range(k) if owner[j] == o]
             if all(unit[j] for j in members):  # the forward wrote exactly these gradients
-                res[4 * o:4 * o + 4] = ctx.pre[4 * o:4 * o + 4]
+                res[4 * o:4 * o + 4] = pre[4 * o:4 * o + 4]
                 for j in members[1:]:
-                    res[4 * j + 1:4 * j + 4] = ctx.pre[4 * j + 1:4 * j + 4]
+                    res[4 * j + 1:4 * j + 4] = pre[4 * j + 1:4 * j + 4]
                 continue
             for j in members:  # general seeds: one backward launch per loss, a-gradients summed
                 if gouts[j] is None:
@@ -252,7 +256,6 @@ class _SqLossGroup(torch.autograd.Function):
                 if g[0] is not None:
                     res[4 * o] = g[0] if res[4 * o] is None else res[4 * o] + g[0]
                 res[4 * j + 1:4 * j + 4] = g[1:]
-        ctx.pre = None
         return (None, None, None, *res)
 
 
@@ -372,7 +375,10 @@ class _ElasticEnergy(torch.autograd.Function):
         terms = torch.empty(nat.EL_TERMS, device=dev, dtype=torch.float32)
         need_f, need_J = ctx.needs_input_grad[0], J is not None and ctx.needs_input_grad[1]
         gf = torch.empty_like(f) if need_f else None
-        gJ = torch.empty_like(J) if need_J else None
+        # the kernel writes dE/dJ only when an SVD term (arap / volume) has a nonzero ratio
+        # (svd_energy.hip); otherwise the gradient w.r.t. J is exactly zero
+        svd_on = any(spec["ratio"].get(nat.EL_IDS[t], 0.0) != 0.0 for t in ("arap", "volume"))
+        gJ = (torch.empty_like(J) if svd_on else torch.zeros_like(J)) if need_J else None
         e = nat.Elastic()
         d = f.shape[1]
         e.d, e.n, e.rows = d, spec["n"], f.shape[0]
@@ -418,6 +424,9 @@ def elastic_energy(f, J, x, f_prev, f_pp, *, n, dt, energy, ratios, ext=(0.0, 0.
     terms (8 floats, non-differentiable) the per-term values (index INSR_EL_*, base._native.EL_IDS)."""
     ids = nat.EL_IDS
     order, ratio = [], {}
+    if "constraint_right" in energy and "constraint_right_compress" in energy:
+        # the reference adds two terms with opposite targets; the fused launch has one slot
+        raise _unsupported("constraint_right and constraint_right_compress together are not fused")
     for term in energy:
         if term == "constraint_right_compress":
             t = ids["constraint_right"]

@@ -32,17 +32,11 @@ static int env_or(const char* name, int dflt) {
 // Tiles per tile-split block.  The largest T in {1, 2, 4} whose LDS fits a CU,
 // lowered while the grid would have fewer than `min_blocks` blocks (small batches
 // want many short blocks, large ones fewer blocks that share W fetches, barriers
-// and partial rows).  Env/API overrides: INSR_SPLIT_TILES_FWD / _BWD (force T,
-// 0 = auto), INSR_SPLIT_MIN_BLOCKS.
-static int g_tiles[3] = {-1, -1, -1};  // forced fwd T, forced bwd T, min blocks
+// and partial rows).  Overrides only through the C ABI (insr_jet_set_split_tiles: force T,
+// 0 = auto; min blocks) -- no environment knobs in the product library.
+static int g_tiles[3] = {0, 0, 256};  // forced fwd T, forced bwd T, min blocks
 
-static void tiles_init() {
-  if (g_tiles[0] < 0) {
-    g_tiles[0] = env_or("INSR_SPLIT_TILES_FWD", 0);
-    g_tiles[1] = env_or("INSR_SPLIT_TILES_BWD", 0);
-    g_tiles[2] = env_or("INSR_SPLIT_MIN_BLOCKS", 256);
-  }
-}
+static void tiles_init() {}
 
 // Matrix-core precision of the tile-split kernels (process default per direction; env
 // INSR_JET_PREC_FWD / INSR_JET_PREC_BWD; a call may override it through INSR_JET_PREC(p) in
@@ -454,6 +448,9 @@ __global__ void adam_multi_kernel(AdamList L, float* __restrict__ st, float b1, 
     if (L.shape[k][2] > 0) adam_wsplit(L.p[k], L.shape[k], i, pn);
   }
   if (L.loss) {  // fused scheduler step: every block read lr / t above before it takes a ticket
+    // (relaxed ticket, no release/acquire: the last block only reads the loss -- written by an
+    // earlier launch -- and st, which no other block writes; the plain loads of lr / t above
+    // completed before each block's barrier)
     __syncthreads();
     if (threadIdx.x == 0) {
       unsigned* ticket = reinterpret_cast<unsigned*>(st + INSR_OPT_TICKET);
@@ -672,30 +669,48 @@ int insr_siren_jet_fwd_multi(const InsrJetJob* jobs, int njobs, int din, int dou
   return 0;
 }
 
-int insr_siren_jet_fwd_mixed(const InsrJetJob* jobs, const int* modes, const float* scalars, int njobs, int din,
-                             int dout, int L, int W, int prec_mode, void* stream) {
-  if (!jobs || !modes || njobs < 1 || njobs > INSR_MAX_FWD_JOBS) return INSR_EINVAL;
-  if (prec_mode & INSR_MODE_MASK) return INSR_EINVAL;  // the per-job jet modes come from `modes`
+// Host-side validation of a mixed launch's jobs, before anything touches the device.  Every
+// field the kernel (jet_fwd_x6_mixed) indexes with is checked here: the job mode selects the
+// body (an unknown mode runs nothing, but is refused first), d_out sizes the output rows, n the
+// tiles / block ranges (first[] is built from n alone), and the advect job writes its foot and
+// f(x) rows while other jobs of the same launch may read their x: those buffers must not alias
+// any job's input.  (Round-2 record: an aperture violation in this kernel came from a job
+// layout whose x could point into LDS -- the backed-out in-kernel draw)
+static int mixed_jobs_ok(const InsrJetJob* jobs, const int* modes, const float* scalars, int njobs, int din, int dout,
+                         int L, int W, int prec_mode, long* total_out) {
+  if (!jobs || !modes || njobs < 1 || njobs > INSR_MAX_FWD_JOBS) return 0;
+  if (prec_mode & INSR_MODE_MASK) return 0;  // the per-job jet modes come from `modes`
   long total = 0;
   for (int k = 0; k < njobs; ++k) {
     const InsrJetJob& j = jobs[k];
+    const int md = modes[k];
+    if (md != INSR_MODE_VALUE && md != INSR_MODE_GRAD && md != INSR_MODE_LAP && md != INSR_MIX_ADVECT) return 0;
+    if (j.d_out < 0 || j.d_out > 3) return 0;
     const int dk = j.d_out > 0 ? j.d_out : dout;
-    if (modes[k] == INSR_MIX_ADVECT) {  // two value jets + the foot: f maps R^d -> R^d
-      if (dk != din || !scalars || (j.n > 0 && (!j.dy || !j.lap))) return INSR_EINVAL;
-      if (!shape_ok(din, dk, L, W, INSR_MODE_VALUE | prec_mode)) return INSR_EINVAL;
-      if (j.n < 0 || j.n > 0x7fffffffL || (j.n > 0 && (!j.x || !j.params || !j.y))) return INSR_EINVAL;
-      total += j.n;
-      continue;
+    if (j.n < 0 || j.n > 0x7fffffffL || (j.n > 0 && (!j.x || !j.params || !j.y))) return 0;
+    if (md == INSR_MIX_ADVECT) {  // two value jets + the foot: f maps R^d -> R^d
+      if (dk != din || !scalars || !shape_ok(din, dk, L, W, INSR_MODE_VALUE | prec_mode)) return 0;
+      if (j.n > 0) {
+        if (!j.dy || !j.lap || j.dy == j.lap || j.dy == j.y || j.lap == j.y) return 0;
+        for (int q = 0; q < njobs; ++q)  // the foot / f(x) rows must not alias an input of the launch
+          if (jobs[q].n > 0 && (jobs[q].x == j.dy || jobs[q].x == j.lap)) return 0;
+      }
+    } else {
+      if (!shape_ok(din, dk, L, W, md | prec_mode)) return 0;
+      if (j.n > 0 && md != INSR_MODE_VALUE && !j.dy) return 0;
+      if (j.n > 0 && md == INSR_MODE_LAP && !j.lap) return 0;
     }
-    const int m = modes[k] | prec_mode;
-    if (modes[k] & ~INSR_MODE_MASK) return INSR_EINVAL;
-    if (!shape_ok(din, dk, L, W, m)) return INSR_EINVAL;
-    if (j.n < 0 || j.n > 0x7fffffffL || (j.n > 0 && (!j.x || !j.params || !j.y))) return INSR_EINVAL;
-    if (j.n > 0 && modes[k] != INSR_MODE_VALUE && !j.dy) return INSR_EINVAL;
-    if (j.n > 0 && modes[k] == INSR_MODE_LAP && !j.lap) return INSR_EINVAL;
     total += j.n;
   }
-  if (total > 0x7fffffffL) return INSR_EINVAL;
+  if (total > 0x7fffffffL) return 0;
+  *total_out = total;
+  return 1;
+}
+
+int insr_siren_jet_fwd_mixed(const InsrJetJob* jobs, const int* modes, const float* scalars, int njobs, int din,
+                             int dout, int L, int W, int prec_mode, void* stream) {
+  long total = 0;
+  if (!mixed_jobs_ok(jobs, modes, scalars, njobs, din, dout, L, W, prec_mode, &total)) return INSR_EINVAL;
   const JetCall c(din, W, INSR_MODE_VALUE | prec_mode);
   hipStream_t st = (hipStream_t)stream;
   if (c.NT == 8 && c.nqf > 0) {

@@ -474,7 +474,7 @@ __global__ __launch_bounds__(X6Geo<NT>::THREADS, (BODIES & kMixL) ? 6 : 4) void 
         fwd_x6_block<NQ, NT, 2 + DIN, true, 1>(jb.x, (int)jb.n, DIN, dk, L, jb.params, jb.y, jb.dy, jb.lap, jb.act,
                                                lb, 1);
       break;
-    default: {  // INSR_MIX_ADVECT: y = f(clamp(x - dt f(x), lo, hi)), f(x) -> dy, the foot -> lap
+    case INSR_MIX_ADVECT: {  // y = f(clamp(x - dt f(x), lo, hi)), f(x) -> dy, the foot -> lap
       if constexpr ((BODIES & kMixA) == 0) break;
       // (fluid/model.py:96-97; every quantity of a point stays in its block: one launch for
       // the frozen field's two value jets and the foot between them)
@@ -498,6 +498,8 @@ __global__ __launch_bounds__(X6Geo<NT>::THREADS, (BODIES & kMixL) ? 6 : 4) void 
       fwd_x6_block<NQ, NT, 1, false, 2>(foot, n, DIN, dk, L, jb.params, jb.y, nullptr, nullptr, nullptr, tile0, cnt);
       break;
     }
+    default:  // never reached: the host validates every job's mode (mixed_jobs_ok, capi.hip)
+      break;
   }
 }
 

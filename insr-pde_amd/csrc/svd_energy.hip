@@ -369,7 +369,8 @@ __global__ __launch_bounds__(kElThreads) void elastic_energy_kernel(const InsrEl
   }
   if (threadIdx.x == 0) {
     last = 1;
-    if (gridDim.x > 1) {  // agent-scope ticket (as block_partial_combine in residual.hip)
+    if (gridDim.x > 1) {  // relaxed ticket after the sc1 stores complete: the hardware hand-off
+                          // of block_partial_combine (residual.hip header; no release/acquire)
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       unsigned* ticket = reinterpret_cast<unsigned*>(work + INSR_EL_TERMS * kElMaxBlocks);
       last = atomicAdd(ticket, 1u) == gridDim.x - 1 ? 1 : 0;

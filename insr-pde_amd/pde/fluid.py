@@ -112,16 +112,11 @@ class Fluid2DModel(BaseModel):
         self.velocity_field_prev.load_state_dict(self.velocity_field.state_dict())
         self._projection()
 
-    # The wall terms evaluate the network on the boundary bands (~1% of the points) in their
-    # own jet launches -- latency-bound chains of a few tiles.  They are issued FIRST; with
-    # cfg.insr_band_stream = True on a side stream forked from the phase's stream, to overlap
-    # the interior launches (autograd runs their backward on that stream as well; the
-    # networks order the .grad writes across streams with events; hipGraph capture works).
-    # Off by default: measured 1.031 vs 1.009 ms per step -- the interior jets hold every
-    # CU's registers / LDS, so the band blocks cannot co-reside and only add the join.
-    # (Merging the bands into the interior launch -- base.merge_samples, as the advection and
-    # elasticity models do -- was measured neutral at 128^2 points: the 2% extra points push
-    # the 1024-tile launches into one more block round on 256 CUs; 1.09 vs 1.01 ms per step.)
+    # The wall terms evaluate the network on the boundary bands (~1% of the points).  In the
+    # fused path (default) they are rows of the merged [interior; bands] batch; the unfused
+    # path (cfg.insr_fuse_forwards = False) evaluates them in jets of their own.  (Measured and
+    # removed: band / no-grad jets on a side stream -- 1.031 vs 1.009 ms per step, 46.3 vs 48.0
+    # M pts/s: the interior jets hold every CU's registers / LDS, so nothing co-resides.)
     def _wall_loss(self, n_interior):
         """u_x = 0 on the x-faces, u_y = 0 on the y-faces: mean(u_x^2) + mean(u_y^2)
         (fluid/model.py:90-94) as one jet launch and one fused loss launch."""
@@ -134,31 +129,6 @@ class Fluid2DModel(BaseModel):
         gp = gradient(self.pressure_field(bxy), bxy)
         return wall_mse(gp, nb)
 
-    def _fork(self, flag, fn, *args):
-        """Run fn(*args) on the model's side stream (forked from the current stream) when
-        cfg.<flag> is set; returns (result, join) -- call join() before the result (a tensor
-        or a tuple of tensors) meets main-stream work."""
-        if not getattr(self.cfg, flag, False) or torch.device(self.device).type != "cuda":
-            return fn(*args), (lambda: None)
-        main = torch.cuda.current_stream(self.device)
-        side = self.__dict__.get("_insr_side")
-        if side is None:
-            side = self._insr_side = torch.cuda.Stream(device=self.device)
-        side.wait_stream(main)
-        with torch.cuda.stream(side):
-            out = fn(*args)
-
-        def join():
-            main.wait_stream(side)
-            for t in (out if isinstance(out, tuple) else (out,)):
-                t.record_stream(main)
-        return out, join
-
-    # no-grad parts of the phases (frozen previous field, detached operators): with
-    # cfg.insr_nograd_stream they run on the side stream, concurrently with the trainable
-    # forward jet on the phase's stream (they have no backward, so no .grad ordering).
-    # Off by default: measured 46.3 vs 48.0 M pts/s (the concurrent jets contend for the
-    # same CUs; a value-jet block fills half a CU, but co-scheduling did not pay).
     def _advect_target(self, x):
         with torch.no_grad():
             u_prev = self.velocity_field_prev(x).detach()
@@ -173,17 +143,17 @@ class Fluid2DModel(BaseModel):
         with torch.no_grad():  # both detached in the reference as well
             return self.velocity_field_prev(x).detach(), gradient(self.pressure_field(x), x)
 
-    # Horizontal fusion (cfg.insr_fuse_forwards, default on; not with insr_nograd_stream):
+    # Horizontal fusion (cfg.insr_fuse_forwards, default on):
     # the frozen field's value jet and the trainable field's value jet at the same points
     # are independent -- ONE insr_siren_jet_fwd_multi launch holds two blocks per CU
     # instead of two latency-bound launches of one block per CU each.
     def _fused_pair(self):
-        return getattr(self.cfg, "insr_fuse_forwards", True) and not getattr(self.cfg, "insr_nograd_stream", False)
+        return getattr(self.cfg, "insr_fuse_forwards", True)
 
     @BaseModel._training_loop
     def _advect_velocity(self):
         x = self._sample_in_training()
-        if self._fused_pair() and not getattr(self.cfg, "insr_band_stream", False):
+        if self._fused_pair():
             xa, n, nb = self._merged(x)
             # the frozen field's semi-Lagrangian target u_prev(clamp(x - dt u_prev(x), -1, 1))
             # (two value jets and the foot, point-local: one job) beside the trainable field's
@@ -195,18 +165,14 @@ class Fluid2DModel(BaseModel):
             # one launch
             main, bc = sq_losses(mse_term(ua, u_target, count=u_target.numel()), wall_term(ua, nb, row0=n))
             return {'main': main, 'bc': bc}
-        bc, join_bc = self._fork("insr_band_stream", self._wall_loss, x.shape[0])
-        u_target, join_t = self._fork("insr_nograd_stream", self._advect_target, x)
-        u = self.velocity_field(x)
-        join_t()
-        main = fused_mse(u, u_target)
-        join_bc()
-        return {'main': main, 'bc': bc}
+        bc = self._wall_loss(x.shape[0])
+        u_target = self._advect_target(x)
+        return {'main': fused_mse(self.velocity_field(x), u_target), 'bc': bc}
 
     @BaseModel._training_loop
     def _solve_pressure(self):
         x = self._sample_in_training()
-        if self._fused_pair() and not getattr(self.cfg, "insr_band_stream", False):
+        if self._fused_pair():
             # The wall term needs grad p on the bands, which the Laplacian jet carries anyway
             # (its tangent streams): ONE pressure jet over [interior; bands] (base.merge_samples)
             # instead of a separate gradient jet + reverse jet for 2% of the points.  The
@@ -223,18 +189,15 @@ class Fluid2DModel(BaseModel):
             main, bc = sq_losses(mse_term(lap_p, Ju[:, 0, 0], Ju[:, 1, 1], alpha=1.0, beta=-1.0, gamma=-1.0, count=n),
                                  wall_term(grad_p, nb, row0=n))
             return {'main': main, 'bc': bc}
-        bc, join_bc = self._fork("insr_band_stream", self._pressure_wall_loss, x.shape[0])
-        div_u, join_d = self._fork("insr_nograd_stream", self._velocity_divergence, x)
-        lap_p = laplace(self.pressure_field(x), x)
-        join_d()
-        main = fused_mse(div_u, lap_p)  # mean((div u - lap p)^2), rho = 1
-        join_bc()
+        bc = self._pressure_wall_loss(x.shape[0])
+        div_u = self._velocity_divergence(x)
+        main = fused_mse(div_u, laplace(self.pressure_field(x), x))  # mean((div u - lap p)^2), rho = 1
         return {'main': main, 'bc': bc}
 
     @BaseModel._training_loop
     def _projection(self):
         x = self._sample_in_training()
-        if self._fused_pair() and not getattr(self.cfg, "insr_band_stream", False):
+        if self._fused_pair():
             xa, n, nb = self._merged(x)
             # frozen velocity (value), pressure gradient (detached) and the trainable velocity
             # over [x; bands]: independent jets, one mixed-mode launch
@@ -247,13 +210,10 @@ class Fluid2DModel(BaseModel):
             main, bc = sq_losses(mse_term(ua, None, u_prev, grad_p, gamma=-1.0, delta=-1.0, count=u_prev.numel()),
                                  wall_term(ua, nb, row0=n))
             return {'main': main, 'bc': bc}
-        bc, join_bc = self._fork("insr_band_stream", self._wall_loss, x.shape[0])
-        (u_prev, grad_p), join_t = self._fork("insr_nograd_stream", self._projection_target, x)
-        u = self.velocity_field(x)
-        join_t()
+        bc = self._wall_loss(x.shape[0])
+        u_prev, grad_p = self._projection_target(x)
         # mean((u - (u_prev - grad_p))^2): r = 1*(u + 0) + (-1)*(u_prev + (-1)*grad_p)
-        main = fused_mse(u, None, u_prev, grad_p, gamma=-1.0, delta=-1.0)
-        join_bc()
+        main = fused_mse(self.velocity_field(x), None, u_prev, grad_p, gamma=-1.0, delta=-1.0)
         return {'main': main, 'bc': bc}
 
     # ---- output (host side; PNG figures are out of scope) ---------------------

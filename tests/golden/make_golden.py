@@ -405,6 +405,70 @@ def gen_elasticity3d(base):
     return out
 
 
+def gen_init(base):
+    """ref_init.npz: the three `_initialize` phases (the t = 0 fits every run starts with):
+    advection/model.py:43-52 (mse to the 'example1' Gaussian), fluid/model.py:42-51 (mse to
+    'taylorgreen'), elasticity/model.py:109-117 (mean(f(x)^2)) -- loss, parameter gradients
+    of one backward, and the loss trace + parameters after 2 reference iterations (phase body
+    + _update_network) on explicit samples."""
+    from advection.model import Advection1DModel
+    from fluid.model import Fluid2DModel
+    from elasticity.model import ElasticityModel
+    out = {}
+    iters = 2
+    cases = [
+        ("advect", Advection1DModel, "field",
+         base_cfg(num_hidden_layers=3, hidden_features=64, sample_resolution=512, dt=0.05, vel=0.25, length=4.0,
+                  init_cond="example1"), (1, 1, 3, 64), 61,
+         lambda g: [(torch.rand(512, 1, generator=g) * 2 - 1) * 2.0 for _ in range(iters)], False),
+        ("fluid", Fluid2DModel, "velocity_field",
+         base_cfg(num_hidden_layers=4, hidden_features=128, sample_resolution=32, dt=0.05, init_cond="taylorgreen"),
+         (2, 2, 4, 128), 62, lambda g: [torch.rand(1024, 2, generator=g) * 2 - 1 for _ in range(iters)], False),
+        ("el2d", ElasticityModel, "deformation_field",
+         base_cfg(num_hidden_layers=5, hidden_features=128, sample_resolution=16, dt=0.1, dim=2, energy=["arap"],
+                  sample_pattern=["random", "uniform"], ratio_constraint=1e4, ratio_volume=1e3, ratio_arap=1.0,
+                  ratio_collide=1e2, ratio_kinematics=1.0, use_mesh=False, mesh_path="",
+                  external_force_timesteps=5, external_force_x=0.0, external_force_y=-1.0, external_force_z=0.0,
+                  constraint_right_offset_x=2.0, constraint_right_offset_y=0.0, constraint_right_offset_z=0.0,
+                  plane_height=-0.9, collide_circle_x=0.0, collide_circle_y=-2.0, collide_circle_z=0.0,
+                  collide_circle_radius=1.0),
+         (2, 2, 5, 128), 63,
+         lambda g: [torch.cat([torch.rand(512, 2, generator=g) * 2 - 1, base.sample_uniform(16, 2)]) for _ in
+                    range(iters)], True),
+    ]
+    for name, cls, attr, cfg, (din, dout, L, W), seed, draw, takes_res in cases:
+        model = cls(cfg)
+        model.timestep = 0
+        if name != "el2d":
+            model.init_cond_func = __import__(cls.__module__.split(".")[0] + ".examples",
+                                              fromlist=["get_examples"]).get_examples(cfg.init_cond)
+        net = getattr(model, attr)
+        set_flat(net, flat(seeded_net(base, din, dout, L, W, seed)))
+        p0 = flat(net)
+        out[f"init/{name}/params0"] = p0
+        xs = draw(torch.Generator().manual_seed(seed + 1000))
+        for it in range(iters):
+            out[f"init/{name}/x{it}"] = xs[it].numpy()
+
+        def samples_fn(it):
+            return (lambda res: xs[it].clone().requires_grad_(True)) if takes_res else \
+                (lambda: xs[it].clone().requires_grad_(True))
+
+        body = raw_phase(cls, "_initialize")
+        model._reset_optimizer()
+        model._sample_in_training = samples_fn(0)
+        ld = body(model)
+        out[f"init/{name}/loss_main"] = np.array(float(ld["main"].detach()))
+        model.optimizer.zero_grad()
+        ld["main"].backward()
+        out[f"init/{name}/grad"] = flat_grad(net)
+        set_flat(net, p0)
+        rec = run_phase(model, cls, "_initialize", iters, samples_fn, lambda it: [])
+        out[f"init/{name}/loss_trace"] = np.array([[r[k] for k in sorted(r)] for r in rec])
+        out[f"init/{name}/after"] = flat(net)
+    return out
+
+
 def gen_samplers(base):
     torch.manual_seed(5)
     out = {"sampling/uniform_8_2": base.sample_uniform(8, 2).numpy(),
@@ -451,6 +515,10 @@ def main():
     if "--extra" in sys.argv:  # initial conditions + more samplers (ref_extra.npz)
         np.savez_compressed(os.path.join(OUT, "ref_extra.npz"), **gen_extra(base))
         print("ref_extra.npz", os.path.getsize(os.path.join(OUT, "ref_extra.npz")) / 1e6, "MB")
+        return
+    if "--init" in sys.argv:  # the three _initialize phases (ref_init.npz)
+        np.savez_compressed(os.path.join(OUT, "ref_init.npz"), **gen_init(base))
+        print("ref_init.npz", os.path.getsize(os.path.join(OUT, "ref_init.npz")) / 1e6, "MB")
         return
     if "--el3d" in sys.argv:  # the 3-D elasticity phase vectors alone (ref_phases_el3d.npz)
         np.savez_compressed(os.path.join(OUT, "ref_phases_el3d.npz"), **gen_elasticity3d(base))

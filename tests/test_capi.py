@@ -112,3 +112,48 @@ def test_struct_layouts_match_header(tmp_path):
         assert int(got[f"{cname} size"]) == ctypes.sizeof(py), cname
         for fname, _ in py._fields_:
             assert int(got[f"{cname} {fname}"]) == getattr(py, fname).offset, (cname, fname)
+
+
+def test_mixed_launch_rejects_malformed_jobs(lib):
+    """insr_siren_jet_fwd_mixed validates every field jet_fwd_x6_mixed indexes with on the host
+    (capi.hip mixed_jobs_ok): a malformed job returns INSR_EINVAL before any device call, so
+    these run without a GPU.  Pointers are dummies that are never dereferenced."""
+    import ctypes
+    from base import _native as nat
+    P = [0x10000 * (i + 1) for i in range(12)]  # distinct fake device addresses
+
+    def job(x=P[0], prm=P[1], y=P[2], dy=P[3], lap=P[4], n=64, d_out=0):
+        return nat.JetJob(x, prm, y, dy, lap, None, n, d_out)
+
+    def call(jobs, modes, scalars=(0.05, -1.0, 1.0) * 4, din=2, dout=2, prec=0):
+        arr = (nat.JetJob * len(jobs))(*jobs)
+        md = (ctypes.c_int * len(modes))(*modes)
+        sc = None if scalars is None else (ctypes.c_float * len(scalars))(*scalars)
+        return lib.insr_siren_jet_fwd_mixed(arr, md, sc, len(jobs), din, dout, 4, 128, prec, None)
+
+    V, G, LAP, ADV = nat.MODE_VALUE, nat.MODE_GRAD, nat.MODE_LAP, 3
+    bad = [
+        ([job()], [5]),                                   # unknown job mode
+        ([job()], [-1]),
+        ([job()], [V | 0x10]),                            # precision bits in a job mode
+        ([job(d_out=4)], [V]),                            # output width out of range
+        ([job(d_out=-1)], [V]),
+        ([job(n=-3)], [V]),                               # negative batch
+        ([job(n=1 << 31)], [V]),                          # batch beyond int range
+        ([job(x=None)], [V]),                             # NULL input of a live job
+        ([job(dy=None)], [G]),                            # gradient job without its dy rows
+        ([job(lap=None)], [LAP]),                         # Laplacian job without its lap rows
+        ([job(lap=None)], [ADV]),                         # advect job without its foot buffer
+        ([job(lap=P[3])], [ADV]),                         # foot aliases f(x)
+        ([job(d_out=1)], [ADV]),                          # advect needs f: R^d -> R^d
+        ([job(), job(x=P[4], y=P[6], dy=P[7], lap=P[8])], [ADV, V]),  # the foot is another job's input
+        ([job()], [ADV], None),                           # advect without its (dt, lo, hi)
+        ([job()] * 5, [V] * 5),                           # more jobs than INSR_MAX_FWD_JOBS
+        ([job(n=0x40000000), job(n=0x40000000, x=P[5])], [V, V]),  # total beyond int range
+    ]
+    for case in bad:
+        jobs, modes = case[0], case[1]
+        args = {} if len(case) == 2 else {"scalars": case[2]}
+        assert call(jobs, modes, **args) == -1, (modes, [(j.n, j.d_out) for j in jobs])
+    assert call([job()], [V], prec=V | 1) == -1           # a jet mode inside prec_mode
+    assert lib.insr_siren_jet_fwd_mixed(None, None, None, 1, 2, 2, 4, 128, 0, None) == -1

@@ -1,0 +1,147 @@
+"""The data-parallel path `bench.py --gpus N` takes, executed on the GPU: PhaseLoop with
+insr_graph=True at world 2 replays TWO hipGraphs per iteration -- [phase + backward] and
+[Adam + plateau] -- with the one eager all-reduce of BaseModel._dp_sync between them
+(base/_loop.py PhaseLoop.step).  Both ranks run on cuda:0 over gloo (a functional rehearsal:
+RCCL needs one GPU per rank); each takes half of the reference golden sample set.
+
+Checks, 4 iterations of each fluid phase (_advect_velocity, _solve_pressure, _projection):
+  * graph DP == eager DP bit for bit (parameters and the synced loss trace);
+  * DP == the single-process full-batch run: losses at 1e-5 relative, Adam updates as in
+    test_gpu_phases.check_update (Adam's first steps are ~lr sign(g));
+  * rank 0 == rank 1 bit for bit (replicated optimiser, no parameter broadcast).
+Plus the launcher itself: `bench.py --gpus 2 --backend gloo` as a subprocess."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLD = os.path.join(ROOT, "tests", "golden", "ref_phases.npz")
+PHASES = ("_advect_velocity", "_solve_pressure", "_projection")
+ITERS = 4
+
+
+def _model(world, rank, graph):
+    from pde.config import make_config
+    from pde.fluid import Fluid2DModel
+    ph = dict(np.load(GOLD))
+    cfg = make_config("fluid", num_hidden_layers=4, hidden_features=128, sample_resolution=32, dt=0.05,
+                      proj_dir="/tmp/insr_dp_graph_test", insr_progress=False, early_stop=False,
+                      max_n_iters=ITERS, insr_graph=graph, insr_sync_every=1, lr=1e-4)
+    m = Fluid2DModel(cfg)
+    m.timestep = 1
+    for k, net in (("vel", m.velocity_field), ("vel_prev", m.velocity_field_prev), ("pres", m.pressure_field)):
+        with torch.no_grad():
+            net.flat_params().copy_(torch.from_numpy(ph[f"fluid/{k}/params0"]).cuda())
+
+    def part(a):  # this rank's share of the golden samples, a static tensor (graph-replay safe)
+        a = torch.from_numpy(a).cuda()
+        n = a.shape[0] // world
+        return a[rank * n:(rank + 1) * n].clone()
+
+    x, bx, by = part(ph["fluid/x0"]), part(ph["fluid/bcx0"]), part(ph["fluid/bcy0"])
+    m._sample_in_training = lambda: x.clone().requires_grad_(True)
+    m._boundary_pair = lambda n: (bx.clone().requires_grad_(True), by.clone().requires_grad_(True))
+    return m
+
+
+def _run(m):
+    """The three phases through the real loop (PhaseLoop.run); returns the synced loss
+    trace per phase and the final parameters."""
+    trace = {}
+    for phase in PHASES:
+        rec = []
+        m.tb = type("TB", (), {"add_scalars": lambda self, tag, vals, global_step: rec.append(vals)})()
+        getattr(m, phase)()
+        assert getattr(m, "_insr_capture_error", None) is None, m._insr_capture_error
+        trace[phase] = rec
+    torch.cuda.synchronize()
+    return trace, m.velocity_field.flat_params().detach().cpu().numpy().copy(), \
+        m.pressure_field.flat_params().detach().cpu().numpy().copy()
+
+
+def _worker(rank, world, port, q):
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "insr-pde_amd")]
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), LOCAL_RANK="0")
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    out = {}
+    for graph in (False, True):
+        m = _model(world, rank, graph)
+        out[graph] = _run(m)
+        if graph:  # the split DP capture really ran: two graphs per phase loop
+            assert m.__dict__.get("_insr_capture_stream") is not None
+    q.put((rank, out))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _check_update(after, before, after_ref):
+    d, d_ref = after - before, after_ref - before
+    mask = np.abs(d_ref) > 0.5 * np.abs(d_ref).max()  # entries that moved ~lr per step (no sign flips)
+    assert mask.sum() > 0.25 * mask.size
+    assert np.abs(d[mask] - d_ref[mask]).max() <= 1e-3 * np.abs(d_ref[mask]).max()
+    assert np.abs(d - d_ref).max() <= 2 * ITERS * 1e-4 * 1.01  # flips at the gradient noise floor
+
+
+def test_two_rank_graph_dp_equals_eager_and_full_batch():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "insr-pde_amd")]
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=400) for _ in range(2))
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    # single-process, full batch, eager (this process)
+    import base
+    base._native.load()
+    ph = dict(np.load(GOLD))
+    full = _run(_model(1, 0, False))
+    for graph in (False, True):
+        for a, b in zip(res[0][graph][1:], res[1][graph][1:]):
+            assert np.array_equal(a, b)  # replicas stay identical
+    (tr_e, v_e, p_e), (tr_g, v_g, p_g) = res[0][False], res[0][True]
+    assert np.array_equal(v_g, v_e) and np.array_equal(p_g, p_e)
+    for phase in PHASES:
+        assert tr_g[phase] == tr_e[phase] and len(tr_g[phase]) == ITERS, phase
+        for got, want in zip(tr_g[phase], full[0][phase]):
+            for k in want:
+                assert abs(got[k] - want[k]) <= 1e-5 * abs(want[k]) + 1e-12, (phase, k, got[k], want[k])
+    _check_update(v_g, ph["fluid/vel/params0"], full[1])
+    _check_update(p_g, ph["fluid/pres/params0"], full[2])
+
+
+def test_bench_two_ranks_gloo_subprocess():
+    """`bench.py --gpus 2 --backend gloo --config fluid2DtlgnM` (both ranks on cuda:0): the
+    launcher starts torch.distributed.run as a child, every rank runs the hipGraph DP step,
+    rank 0 prints one JSON line for the 2-rank process group."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--backend", "gloo", "--config",
+           "fluid2DtlgnM", "--steps", "3", "--warmup", "2", "--no-roofline"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=420, cwd=ROOT,
+                       env=dict(os.environ, MASTER_ADDR="127.0.0.1"))
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["process_group"]["world_size"] == 2
+    assert out["process_group"]["backend"] == "gloo" and out["scaling"] == "strong"
+    assert out["config"]["points_per_phase_iter"] == 65536 and out["value"] > 0

@@ -125,6 +125,24 @@ def test_elastic_energy_rejects(B):
                          dt=0.1, energy=["kinematics"], ratios={"kinematics": 1.0})
 
 
+def test_svd_terms_with_zero_ratio_give_zero_jacobian_gradient(B):
+    """arap / volume listed with ratio 0: the kernel writes no dE/dJ, the gradient is exactly zero
+    (not uninitialised memory), and constraint_right with _compress together is refused."""
+    f, J, x, fp, fpp, rows_l, rows_r, cfg = make_case(2, 3000, 0, 0, 77)
+    fg, Jg = f.cuda().requires_grad_(True), J.cuda().requires_grad_(True)
+    torch.empty(8 << 20, device="cuda").fill_(float("nan"))  # dirty the caching allocator's blocks
+    total, _ = B.elastic_energy(fg, Jg, x.cuda(), fp.cuda(), fpp.cuda(), n=3000, dt=0.1,
+                                energy=["arap", "volume", "kinematics"],
+                                ratios={"arap": 0.0, "volume": 0.0, "kinematics": 2.0})
+    seed = B.losses.register_unit_seed(torch.ones((), device="cuda"))
+    gf, gJ = torch.autograd.grad(total, (fg, Jg), grad_outputs=seed)
+    assert float(gJ.abs().sum()) == 0.0 and torch.isfinite(gf).all()
+    with pytest.raises(B.UnsupportedPattern):
+        B.elastic_energy(fg, None, x.cuda(), fp.cuda(), fpp.cuda(), n=3000, dt=0.1,
+                         energy=["constraint_right", "constraint_right_compress"],
+                         ratios={"constraint_right": 1.0, "constraint_right_compress": 1.0})
+
+
 def test_box_batch_layout_and_energy(B):
     """ElasticityModel._box_batch (one sampler launch into a persistent [x; fixed_l; fixed_r]
     buffer): the layout _sample_in_training / _sample_fixed_in_training / merge_samples give --

@@ -1,0 +1,210 @@
+"""One full iteration of the headline models at their BASELINE.json sizes, against the CPU
+oracle (oracle/siren_oracle.py, pinned to the reference's own vectors by
+tests/test_oracle_golden.py) on the SAME points:
+
+  * fluid2Dtlgn   fused pde/fluid.py phases at 128^2 = 16,384 interior points + 2 x 162 bands
+  * fluid2DtlgnM  the same at 256^2 = 65,536 + 2 x 654
+  * elasticity2Dstretch  _solve_deformation at 20,000 points (SIREN 5x128) + 2 x 200 fixed
+
+The GPU runs the product path exactly as bench.py does -- device sampler into the merged
+[interior; bands] buffer (fluid) / the persistent box batch (elasticity), mixed launches,
+loss groups, the fused energy, Adam + plateau in one launch -- and the test reads back the
+points that path drew and hands them to the oracle (fluid/model.py:72-151,
+elasticity/model.py:127-189, base/baseModel.py:73-81).  A second fluid2Dtlgn case feeds
+recorded samples through the _sample_in_training / _boundary_pair hooks (as
+test_gpu_phases.py does at 32^2).
+
+Checks per phase: every loss (1e-5 relative), every parameter tensor's gradient (1e-5
+normwise, each weight and bias on its own), and the parameters after the Adam step (updates
+compared on entries whose gradient is well above the noise floor, as test_gpu_phases)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import siren_oracle as O
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-5
+
+
+@pytest.fixture(scope="module")
+def B():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import base
+    base._native.load()
+    torch.set_num_threads(min(16, torch.get_num_threads()))
+    return base
+
+
+def nerr(a, b):
+    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    return float(np.abs(a - b).max() / max(np.abs(b).max(), 1e-30))
+
+
+def seeded(din, dout, L, W, seed):
+    torch.manual_seed(seed)
+    return O.OracleSiren(din, dout, L, W)
+
+
+def load(net, ref):
+    with torch.no_grad():
+        net.flat_params().copy_(O.flat_params(ref).cuda())
+
+
+def per_tensor(flat, ref):
+    """Split a flat vector in the reference's state_dict order: {name: array}."""
+    out, off = {}, 0
+    for k, p in ref.named_parameters():
+        out[k] = flat[off:off + p.numel()]
+        off += p.numel()
+    return out
+
+
+def check_grads(net, ref, what):
+    got = net.flat_grad_buffer().detach().cpu().numpy() if net.grad_touched() else np.zeros(net.param_count)
+    want = O.flat_grads(ref).numpy()
+    if np.abs(want).max() == 0:
+        assert not net.grad_touched(), what
+        return
+    g, w = per_tensor(got, ref), per_tensor(want, ref)
+    for k in w:
+        if np.abs(w[k]).max() > 0:
+            assert nerr(g[k], w[k]) < TOL, (what, k, nerr(g[k], w[k]))
+        else:
+            assert np.abs(g[k]).max() == 0, (what, k)
+
+
+def check_update(net, ref, p0, lr):
+    got = net.flat_params().detach().cpu().numpy() - p0
+    want = O.flat_params(ref).numpy() - p0
+    g = O.flat_grads(ref).numpy()
+    if np.abs(g).max() == 0:
+        assert np.abs(got).max() == 0
+        return
+    mask = np.abs(g) > 1e-3 * np.abs(g).max()
+    assert mask.sum() > 0.5 * mask.size
+    assert nerr(got[mask], want[mask]) < 1e-3
+    assert np.abs(got - want).max() <= 2 * lr * 1.01  # noise-floor entries may flip sign
+
+
+# ---------------------------------------------------------------------------------------------
+def _fluid(B, config, hooks):
+    from pde.config import baseline_config
+    from pde.fluid import Fluid2DModel
+    import pde.fluid as fl
+    cfg = baseline_config(config, proj_dir="/tmp/insr_fullsize_phases", insr_progress=False, early_stop=False,
+                          max_n_iters=1, insr_graph=False, insr_sync_every=1)
+    m = Fluid2DModel(cfg)
+    m.timestep = 1
+    refs = {"vel": seeded(2, 2, 4, 128, 201), "vel_prev": seeded(2, 2, 4, 128, 202), "pres": seeded(2, 1, 4, 128, 203)}
+    nets = {"vel": m.velocity_field, "vel_prev": m.velocity_field_prev, "pres": m.pressure_field}
+    N = cfg.sample_resolution ** 2
+    nb = N // 100
+    gen = torch.Generator().manual_seed(301)
+    drawn = {}
+    if hooks:
+        x = torch.rand(N, 2, generator=gen) * 2 - 1
+        bx = O.sample_boundary2d_side(nb, "horizontal", generator=gen)
+        by = O.sample_boundary2d_side(nb, "vertical", generator=gen)
+        m._sample_in_training = lambda: x.cuda().requires_grad_(True)
+        m._boundary_pair = lambda n: (bx.cuda().requires_grad_(True), by.cuda().requires_grad_(True))
+        drawn["pts"] = (x, bx, by)
+    else:  # the product sampler: record the merged buffer it draws
+        orig = fl.sample_random_and_bands2D
+
+        def rec(n, n_band, **kw):
+            buf = orig(n, n_band, **kw)
+            h = (buf.shape[0] - n) // 2
+            b = buf.detach().cpu()
+            drawn["pts"] = (b[:n].clone(), b[n:n + h].clone(), b[n + h:].clone())
+            return buf
+        fl.sample_random_and_bands2D = rec
+        drawn["restore"] = lambda: setattr(fl, "sample_random_and_bands2D", orig)
+    oracle = {
+        "_advect_velocity": lambda r, x, bx, by: O.fluid_advect_loss(r["vel"], r["vel_prev"], x, bx, by, cfg.dt),
+        "_solve_pressure": lambda r, x, bx, by: O.fluid_pressure_loss(r["vel"], r["pres"], x, bx, by),
+        "_projection": lambda r, x, bx, by: O.fluid_projection_loss(r["vel"], r["vel_prev"], r["pres"], x, bx, by),
+    }
+    try:
+        for phase, fn in oracle.items():
+            for k in nets:
+                load(nets[k], refs[k])
+            p0 = {k: O.flat_params(refs[k]).numpy().copy() for k in ("vel", "pres")}
+            m._reset_optimizer()
+            ld = getattr(Fluid2DModel, phase)._insr_phase(m)
+            m._update_network(ld)
+            torch.cuda.synchronize()
+            assert len(ld) == 2
+            x, bx, by = drawn["pts"]
+            assert x.shape[0] == N and bx.shape[0] == by.shape[0] == 2 * (nb // 2)
+            r = {k: seeded(*s, seed) for k, s, seed in (("vel", (2, 2, 4, 128), 201), ("vel_prev", (2, 2, 4, 128), 202),
+                                                         ("pres", (2, 1, 4, 128), 203))}
+            for p in r["vel_prev"].parameters():
+                p.requires_grad_(False)
+            opt = O.OracleAdam([p for k in ("vel", "pres") for p in r[k].parameters()], lr=cfg.lr)
+            ldo = fn(r, x.clone().requires_grad_(True), bx.clone().requires_grad_(True), by.clone().requires_grad_(True))
+            O.update_step([r["vel"], r["pres"]], ldo, opt)
+            for k, v in ldo.items():
+                assert abs(float(ld[k]) - float(v)) <= TOL * abs(float(v)) + 1e-12, (phase, k, float(ld[k]), float(v))
+            for k in ("vel", "pres"):
+                check_grads(nets[k], r[k], (phase, k))
+                check_update(nets[k], r[k], p0[k], cfg.lr)
+    finally:
+        if "restore" in drawn:
+            drawn["restore"]()
+
+
+def test_fluid2dtlgn_phases_full_size(B):
+    _fluid(B, "fluid2Dtlgn", hooks=False)
+
+
+def test_fluid2dtlgn_phases_full_size_recorded_samples(B):
+    _fluid(B, "fluid2Dtlgn", hooks=True)
+
+
+def test_fluid2dtlgnM_phases_full_size(B):
+    _fluid(B, "fluid2DtlgnM", hooks=False)
+
+
+def test_elasticity2dstretch_full_size(B):
+    """elasticity2Dstretch (scripts/elasticity2Dstretch.sh: SIREN 5x128, sample_resolution 100,
+    arap + constraint + constraint_right + volume): one iteration on the 20,000 interior + 400
+    fixed points the persistent box batch draws, vs the oracle's energy on the same points."""
+    from pde.config import baseline_config
+    from pde.elasticity import ElasticityModel
+    cfg = baseline_config("elasticity2Dstretch", proj_dir="/tmp/insr_fullsize_el2d", insr_progress=False,
+                          early_stop=False, max_n_iters=1, insr_graph=False, insr_sync_every=1)
+    m = ElasticityModel(cfg)
+    m.timestep = 1
+    refs = {"f": seeded(2, 2, 5, 128, 211), "f_prev": seeded(2, 2, 5, 128, 212), "f_pp": seeded(2, 2, 5, 128, 213)}
+    for k, net in (("f", m.deformation_field), ("f_prev", m.deformation_field_prev),
+                   ("f_pp", m.deformation_field_prev_prev)):
+        load(net, refs[k])
+    p0 = O.flat_params(refs["f"]).numpy().copy()
+    m._reset_optimizer()
+    ld = ElasticityModel._solve_deformation._insr_phase(m)
+    m._update_network(ld)
+    torch.cuda.synchronize()
+    (buf, _, x, fixed_l, fixed_r), = m.__dict__["_insr_box_batch"].values()
+    x, fl_, fr_ = (t.detach().cpu().clone() for t in (x, fixed_l, fixed_r))
+    assert x.shape[0] == 20000 and fl_.shape[0] == fr_.shape[0] == 200
+    ecfg = dict(dt=cfg.dt, energy=list(cfg.energy), ratio_arap=cfg.ratio_arap, ratio_volume=cfg.ratio_volume,
+                ratio_kinematics=cfg.ratio_kinematics, ratio_constraint=cfg.ratio_constraint,
+                ratio_collide=cfg.ratio_collide, plane_height=cfg.plane_height,
+                external_force=[cfg.external_force_x, cfg.external_force_y],
+                constraint_offset_right=[cfg.constraint_right_offset_x, cfg.constraint_right_offset_y],
+                circle_center=[cfg.collide_circle_x, cfg.collide_circle_y], circle_radius=cfg.collide_circle_radius,
+                external_force_timesteps=cfg.external_force_timesteps)
+    r = {k: seeded(2, 2, 5, 128, s) for k, s in (("f", 211), ("f_prev", 212), ("f_pp", 213))}
+    for k in ("f_prev", "f_pp"):
+        for p in r[k].parameters():
+            p.requires_grad_(False)
+    opt = O.OracleAdam(list(r["f"].parameters()), lr=cfg.lr)
+    ldo = O.elasticity_loss(r["f"], r["f_prev"], r["f_pp"], x.requires_grad_(True), fl_.requires_grad_(True),
+                            fr_.requires_grad_(True), ecfg, timestep=1)
+    O.update_step([r["f"]], ldo, opt)
+    assert abs(float(ld["main"]) - float(ldo["main"])) <= TOL * abs(float(ldo["main"])), (float(ld["main"]),
+                                                                                             float(ldo["main"]))
+    check_grads(m.deformation_field, r["f"], "el2d")
+    check_update(m.deformation_field, r["f"], p0, cfg.lr)

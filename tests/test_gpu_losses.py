@@ -183,3 +183,16 @@ def test_merge_samples(B):
     m = B.merge_samples(x, b)
     assert m.is_leaf and m.requires_grad and m.shape == (14, 2)
     assert torch.equal(m[:10], x.detach()) and torch.equal(m[10:], b)
+
+
+def test_loss_group_repeated_unit_backward(B):
+    """A unit-seeded backward hands out the gradients the forward launch wrote; a second
+    backward through the same graph (retain_graph=True) gets equal copies, not None."""
+    a = torch.randn(5000, 2, device="cuda", requires_grad=True)
+    b = torch.randn(5000, 2, device="cuda")
+    loss = B.fused_mse(a, b)
+    seed = B.losses.register_unit_seed(torch.ones((), device="cuda"))
+    g1, = torch.autograd.grad(loss, (a,), grad_outputs=seed, retain_graph=True)
+    g2, = torch.autograd.grad(loss, (a,), grad_outputs=seed, retain_graph=True)
+    want = 2.0 * (a.detach() - b) / a.numel()
+    assert rel(g1, want) < 1e-6 and torch.equal(g1, g2) and g1.data_ptr() != g2.data_ptr()

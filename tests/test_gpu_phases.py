@@ -67,11 +67,11 @@ def _cfg(pde, **kw):
     return make_config(pde, proj_dir="/tmp/insr_test", **kw)
 
 
-@pytest.mark.parametrize("band_stream", [False, True])
-def test_fluid_phases(ph, band_stream):
+@pytest.mark.parametrize("fused", [True, False])
+def test_fluid_phases(ph, fused):
     from pde.fluid import Fluid2DModel
     cfg = _cfg("fluid", num_hidden_layers=4, hidden_features=128, sample_resolution=32, dt=0.05,
-               insr_band_stream=band_stream, insr_nograd_stream=band_stream)
+               insr_fuse_forwards=fused)
     model = Fluid2DModel(cfg)
     T = lambda k: torch.from_numpy(ph[k]).cuda()  # noqa: E731
     nets = {"vel": model.velocity_field, "vel_prev": model.velocity_field_prev, "pres": model.pressure_field}
@@ -258,17 +258,72 @@ def test_elasticity3d_phase(ph):
                  g3["el3d/_solve_deformation/grad_f"])
 
 
-@pytest.mark.parametrize("band_stream", [False, True])
-def test_training_loop_graph_matches_eager(ph, band_stream):
-    """insr_graph=True (hipGraph replay) gives the same trajectory as eager execution (also
-    with the boundary-band jets on a side stream: the capture must join it)."""
+INIT = {"advect": ("advection", "pde.advection", "Advection1DModel", "field",
+                   dict(num_hidden_layers=3, hidden_features=64, sample_resolution=512, dt=0.05, vel=0.25, length=4.0,
+                        init_cond="example1"), False),
+        "fluid": ("fluid", "pde.fluid", "Fluid2DModel", "velocity_field",
+                  dict(num_hidden_layers=4, hidden_features=128, sample_resolution=32, dt=0.05,
+                       init_cond="taylorgreen"), False),
+        "el2d": ("elasticity", "pde.elasticity", "ElasticityModel", "deformation_field",
+                 dict(num_hidden_layers=5, hidden_features=128, sample_resolution=16, dt=0.1, dim=2,
+                      energy=["arap"]), True)}
+
+
+@pytest.mark.parametrize("name", sorted(INIT))
+def test_initialize_phase(name):
+    """The `_initialize` phases (advection/model.py:43-52, fluid/model.py:42-51,
+    elasticity/model.py:109-117) vs the reference's own vectors (tests/golden/ref_init.npz):
+    loss, parameter gradients, and 2 iterations of phase + Adam + plateau."""
+    import importlib
+    from pde.examples import get_examples
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    g = dict(np.load(GOLD.replace("ref_phases.npz", "ref_init.npz")))
+    pde, mod, cls_name, attr, kw, takes_res = INIT[name]
+    cls = getattr(importlib.import_module(mod), cls_name)
+    model = cls(_cfg(pde, **kw))
+    model.timestep = 0
+    if "init_cond" in kw:
+        model.init_cond_func = get_examples(kw["init_cond"])
+    net = getattr(model, attr)
+    T = lambda k: torch.from_numpy(g[k]).cuda()  # noqa: E731
+
+    def patch(it):
+        x = lambda *a: T(f"init/{name}/x{it}").clone().requires_grad_(True)  # noqa: E731
+        model._sample_in_training = x
+
+    body = cls._initialize._insr_phase
+    set_flat(net, g[f"init/{name}/params0"])
+    patch(0)
+    model._reset_optimizer()
+    ld = body(model)
+    ref = float(g[f"init/{name}/loss_main"])
+    assert abs(float(ld["main"]) - ref) <= TOL * abs(ref), (float(ld["main"]), ref)
+    model.optimizer.zero_grad()
+    ld["main"].backward()
+    assert nerr(flat_grad(net), g[f"init/{name}/grad"]) < TOL
+    set_flat(net, g[f"init/{name}/params0"])
+    model._reset_optimizer()
+    trace = []
+    for it in range(2):
+        patch(it)
+        ld = body(model)
+        model._update_network(ld)
+        trace.append([float(ld[k]) for k in sorted(ld)])
+    assert nerr(np.array(trace), g[f"init/{name}/loss_trace"]) < TOL
+    check_update(flat(net), g[f"init/{name}/params0"], g[f"init/{name}/after"], g[f"init/{name}/grad"])
+
+
+@pytest.mark.parametrize("fused", [True, False])
+def test_training_loop_graph_matches_eager(ph, fused):
+    """insr_graph=True (hipGraph replay) gives the same trajectory as eager execution (fused
+    mixed launches and the unfused per-jet path)."""
     from pde.fluid import Fluid2DModel
     res = {}
     for graph in (False, True):
         torch.manual_seed(0)
         cfg = _cfg("fluid", num_hidden_layers=4, hidden_features=128, sample_resolution=32, max_n_iters=6,
-                   insr_graph=graph, insr_sync_every=3, insr_band_stream=band_stream,
-                   insr_nograd_stream=band_stream)
+                   insr_graph=graph, insr_sync_every=3, insr_fuse_forwards=fused)
         model = Fluid2DModel(cfg)
         set_flat(model.velocity_field, ph["fluid/vel/params0"])
         set_flat(model.velocity_field_prev, ph["fluid/vel_prev/params0"])

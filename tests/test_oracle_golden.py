@@ -220,6 +220,32 @@ def test_elasticity3d_phase():
     assert nrm(trace, ph["el3d/_solve_deformation/loss_trace"]) < 1e-5
 
 
+INIT_CASES = {"advect": ((1, 1, 3, 64), O.advect1d_init_loss), "fluid": ((2, 2, 4, 128), O.fluid_init_loss),
+              "el2d": ((2, 2, 5, 128), O.elasticity_init_loss)}
+
+
+@pytest.mark.parametrize("name", sorted(INIT_CASES))
+def test_initialize_phases(name):
+    """The `_initialize` phases (advection/model.py:43-52, fluid/model.py:42-51,
+    elasticity/model.py:109-117) vs tests/golden/ref_init.npz: loss, parameter gradients, and
+    the loss trace + update of 2 reference iterations."""
+    ph = dict(np.load(os.path.join(GOLD, "ref_init.npz")))
+    shape, fn = INIT_CASES[name]
+    X = lambda it: torch.from_numpy(ph[f"init/{name}/x{it}"]).clone().requires_grad_(True)  # noqa: E731
+    nets = _nets(ph, "init", {name: shape})
+    ld = fn(nets[name], X(0))
+    ref = float(ph[f"init/{name}/loss_main"])
+    assert abs(float(ld["main"]) - ref) <= 1e-6 * abs(ref)
+    ld["main"].backward()
+    assert nrm(O.flat_grads(nets[name]), ph[f"init/{name}/grad"]) < 1e-5
+    nets = _nets(ph, "init", {name: shape})
+    trace = _run(nets, [name], lambda it: fn(nets[name], X(it)), 2)
+    assert nrm(trace, ph[f"init/{name}/loss_trace"]) < 1e-5
+    d_ref = ph[f"init/{name}/after"] - ph[f"init/{name}/params0"]
+    d_got = O.flat_params(nets[name]).numpy() - ph[f"init/{name}/params0"]
+    assert nrm(d_got, d_ref) < 1e-3
+
+
 def test_plateau_matches_torch():
     p = torch.nn.Parameter(torch.zeros(1))
     opt = torch.optim.SGD([p], lr=1e-4)

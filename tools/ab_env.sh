@@ -1,6 +1,7 @@
 #!/bin/bash
 # Same-box A/B of run-time knobs: the headline bench with the default policy and with each
 # "VAR=value" of $KNOBS (space separated), 100 steps each, alternating twice.
+# (Tile-count overrides are no longer environment variables: tools/ab_tiles.py.)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 O=gpurun_out/${SESSION:-abenv}; mkdir -p $O
