@@ -72,6 +72,8 @@ def parse():
     ap.add_argument("--api", choices=["fused", "plain"], default="fused",
                     help="fluid: 'plain' runs pde/fluid_plain.py, phase bodies written only against the "
                          "reference's base API (separate band samplers, torch residuals) -- the drop-in case")
+    ap.add_argument("--bwd-policy", type=int, default=0, choices=[0, 1, 2, 3],
+                    help="backward path (A/B studies): 0 auto, 1 fused tile-split, 2 two-kernel, 3 resident dW")
     ap.add_argument("--cpu-seconds", type=float, default=25.0, help="budget of the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
@@ -164,6 +166,7 @@ def build_model(args, world, rank):
     import base
     from pde.config import baseline_config
     base._native.load()
+    base._native.lib().insr_jet_set_bwd_policy(args.bwd_policy)
     wl = WORKLOADS[args.config]
     res = wl["res"]
     cfg = baseline_config(args.config, sample_resolution=res, insr_graph=not args.no_graph,
@@ -313,7 +316,15 @@ def kernel_identity(kind, mode, n, din, dout, L, W, nq=3):
     S = {"value": 1, "grad": 1 + din, "lap": 2 + din}[mode]
     NT = W // 16
     lap = "true" if mode == "lap" else "false"
-    if kind == "bwd" and lib.insr_jet_bwd_is_wide(n, din, W, m) == 1:  # two kernels + the dW sums
+    path = lib.insr_jet_bwd_path(n, din, dout, L, W, m) if kind == "bwd" else 0
+    if path == 2:  # the resident-dW persistent kernel + the fixed-order sums
+        import ctypes
+        thr = (ctypes.c_long * 3)()
+        nat.check(lib.insr_jet_wide_launch_threads(n, din, dout, L, W, m, thr), "insr_jet_wide_launch_threads")
+        parts = [(f"insr::jet_bwd_x6r<{nq}, {S}, {lap}, {L}>", thr[0]), ("insr::reduce_dw_kernel", thr[1])]
+        return " + ".join(f"{k}|grid={g}" for k, g in parts) + " (resident-dW backward: persistent tile loop, " \
+            "then the dW / compact-row sums; time = both launches)", parts, True
+    if path == 1:  # two kernels + the dW sums
         import ctypes
         thr = (ctypes.c_long * 3)()
         nat.check(lib.insr_jet_wide_launch_threads(n, din, dout, L, W, m, thr), "insr_jet_wide_launch_threads")
@@ -553,6 +564,7 @@ def main():
                    "points_per_phase_iter": n_all, "phases": nph, "global_batch": n_all,
                    "seq_len": None, "parallelism": f"dp{world}", "graph": not args.no_graph,
                    "precision": args.precision, "api": args.api, "sync_every": cfg.insr_sync_every,
+                   "bwd_policy": args.bwd_policy,
                    "timestep_order": f"{nts} timesteps x ({'/'.join(str(k) for k in ks)}) iterations per phase, "
                                      "phases in step() order with the prev-net snapshots"},
         "timesteps": {"count": nts, "iters_per_phase": ks, "ms": [round(v, 3) for v in ts_ms],

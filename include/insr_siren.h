@@ -182,6 +182,17 @@ int insr_siren_jet_bwd_grad(const float* x, long n_points, int d_in, int d_out, 
 long insr_jet_bwd_work_bytes(long n_points, int d_in, int d_out, int num_hidden, int width, int mode);
 /* 1 if insr_siren_jet_bwd_grad takes the wide path for this batch / width / mode. */
 int insr_jet_bwd_is_wide(long n_points, int d_in, int width, int mode);
+
+/* Which backward serves this jet: 0 = the fused tile-split kernel writing partial rows
+ * (insr_siren_jet_bwd + insr_reduce_partials_strided), 1 = the two-kernel path, 2 = the
+ * resident-dW persistent kernel (W = 128, <= 4 hidden layers: every hidden layer's weight
+ * gradient held in registers across the batch).  1 and 2 run through insr_siren_jet_bwd_grad
+ * with an insr_jet_bwd_work_bytes workspace. */
+int insr_jet_bwd_path(long n_points, int d_in, int d_out, int num_hidden, int width, int mode);
+
+/* Backward-path policy (A/B studies): 0 = auto (default), 1 = fused where it exists,
+ * 2 = two-kernel, 3 = resident dW where it applies.  Returns the previous policy. */
+int insr_jet_set_bwd_policy(int policy);
 /* Threads of the three launches of a two-kernel backward (propagation, dW partials, dW sums),
  * as profilers report them; INSR_EINVAL when (n, shape, mode) does not take that path. */
 int insr_jet_wide_launch_threads(long n_points, int d_in, int d_out, int num_hidden, int width, int mode,

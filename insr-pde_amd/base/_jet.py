@@ -132,8 +132,9 @@ class _SirenJet(torch.autograd.Function):
         st = nat.stream_of(x2.device)
         cur = torch.cuda.current_stream(x2.device)
         mlp.grad_write_begin(cur)  # order after a write of .grad made on another stream
-        if lib.insr_jet_bwd_is_wide(n, din, W, cmode) == 1:
-            # W = 256: propagation kernel + split-K dW GEMM + reductions, straight into .grad
+        if lib.insr_jet_bwd_path(n, din, dout, L, W, cmode) > 0:
+            # two-kernel path (propagation + split-K dW GEMM) or the resident-dW persistent kernel,
+            # with their fixed-order sums straight into .grad
             work = torch.empty(max(lib.insr_jet_bwd_work_bytes(n, din, dout, L, W, cmode) // 4, 1), device=x2.device,
                                dtype=torch.float32)
             with _timed("bwd", mode, n, W, (din, dout, L)):

@@ -49,6 +49,8 @@ SIGNATURES = {
     "insr_siren_jet_bwd_grad": (_I, [_P, _L, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _I, _P]),
     "insr_jet_bwd_work_bytes": (_L, [_L, _I, _I, _I, _I, _I]),
     "insr_jet_bwd_is_wide": (_I, [_L, _I, _I, _I]),
+    "insr_jet_bwd_path": (_I, [_L, _I, _I, _I, _I, _I]),
+    "insr_jet_set_bwd_policy": (_I, [_I]),
     "insr_jet_set_wide_min_width": (_I, [_I]),
     "insr_comm_available": (_I, []),
     "insr_comm_id_bytes": (_L, []),

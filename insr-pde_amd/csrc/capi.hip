@@ -29,6 +29,23 @@ static int env_or(const char* name, int dflt) {
   return e ? std::atoi(e) : dflt;
 }
 
+// Backward-path policy (insr_jet_set_bwd_policy): 0 auto, 1 fused tile-split + partial rows,
+// 2 two-kernel (jet_x6w.hpp), 3 resident dW (jet_x6r.hpp) where it applies.
+static int g_bwd_policy = 0;
+
+// The resident-dW backward (jet_x6r.hpp) serves W = 128 nets of <= 4 hidden layers at x6
+// precision: value, 2-d gradient and 2-d Laplacian jets, once the batch fills the CUs.
+bool resident_ok(int S, int NT, bool lap, int nq, int L) {
+  if (NT != 8 || nq != 3 || L < 1 || L > 4) return false;
+  return (S == 1 && !lap) || (S == 3 && !lap) || (S == 4 && lap);
+}
+bool use_resident(long n, int S, int NT, bool lap, int nq, int L) {
+  if (!resident_ok(S, NT, lap, nq, L)) return false;
+  if (g_bwd_policy == 3) return true;
+  if (g_bwd_policy != 0) return false;
+  return n >= 4096 && L == 4;
+}
+
 // Tiles per tile-split block.  The largest T in {1, 2, 4} whose LDS fits a CU,
 // lowered while the grid would have fewer than `min_blocks` blocks (small batches
 // want many short blocks, large ones fewer blocks that share W fetches, barriers
@@ -80,6 +97,8 @@ static int g_wide_min = -1;
 bool use_wide(long n, int S, int NT, bool lap, int nq) {
   if (g_wide_min < 0) g_wide_min = env_or("INSR_WIDE_MIN_WIDTH", 256);
   if (NT < 8 || nq == 0) return false;
+  if (g_bwd_policy == 2) return true;
+  if (g_bwd_policy == 1 && NT == 8) return false;
   if (16 * NT >= g_wide_min) return true;
   if (NT != 8 || g_wide_min > 256) return false;
   // with the pre-split weight planes (kbench r2s31, profiles/r02/wide_vs_fused_wsplit.jsonl):
@@ -490,6 +509,9 @@ struct JetCall {
   bool ok() const { return S > 0 && NT > 0; }
   // width 256 has no fused split-bf16 backward: the two-kernel path serves it
   bool wide(long n) const { return use_wide(n, S, NT, lap, nqb); }
+  bool resident(long n, int L) const { return use_resident(n, S, NT, lap, nqb, L); }
+  // 0: fused tile-split + partial rows (insr_siren_jet_bwd), 1: two-kernel, 2: resident dW
+  int path(long n, int L) const { return resident(n, L) ? 2 : (wide(n) ? 1 : 0); }
 };
 
 }  // namespace insr
@@ -785,6 +807,7 @@ int insr_jet_set_wide_min_width(int width) {
 long insr_jet_bwd_work_bytes(long n, int din, int dout, int L, int W, int mode) {
   if (!shape_ok(din, dout, L, W, mode) || n < 0) return INSR_EINVAL;
   const JetCall c(din, W, mode);
+  if (c.resident(n, L)) return resident_work_floats(n, din, dout, L) * (long)sizeof(float);
   if (c.wide(n)) return wide_work_floats(n, din, dout, L, W, c.S) * (long)sizeof(float);
   return insr_jet_partial_bytes(n, din, dout, L, W, mode);
 }
@@ -792,6 +815,14 @@ long insr_jet_bwd_work_bytes(long n, int din, int dout, int L, int W, int mode) 
 int insr_jet_wide_launch_threads(long n, int din, int dout, int L, int W, int mode, long* threads3) {
   if (!shape_ok(din, dout, L, W, mode) || n <= 0 || !threads3 || L < 1) return INSR_EINVAL;
   const JetCall c(din, W, mode);
+  if (c.resident(n, L)) {  // the persistent launch (256-thread blocks) + the dW / compact-row sums
+    const long Ps = (long)W * din + W + (long)L * W + (long)dout * W + dout;
+    const long wq = ((long)W * W / 4 + 63) / 64, rows_x = (Ps + 63) / 64;
+    threads3[0] = (long)resident_blocks(n) * 256;
+    threads3[1] = (wq > rows_x ? wq : rows_x) * (L + 1) * 512;
+    threads3[2] = 0;
+    return 0;
+  }
   if (!c.wide(n)) return INSR_EINVAL;
   wide_launch_threads(n, din, dout, L, W, c.S, threads3);
   return 0;
@@ -803,6 +834,17 @@ int insr_jet_bwd_is_wide(long n, int din, int W, int mode) {
   return c.wide(n) ? 1 : 0;
 }
 
+int insr_jet_bwd_path(long n, int din, int dout, int L, int W, int mode) {
+  if (!shape_ok(din, dout, L, W, mode) || n < 0) return INSR_EINVAL;
+  return JetCall(din, W, mode).path(n, L);
+}
+
+int insr_jet_set_bwd_policy(int policy) {
+  const int old = g_bwd_policy;
+  if (policy >= 0 && policy <= 3) g_bwd_policy = policy;
+  return old;
+}
+
 int insr_siren_jet_bwd_grad(const float* x, long n, int din, int dout, int L, int W, int mode, const float* params,
                             const float* act, const float* gy, const float* gdy, const float* glap, float* work,
                             float* grad, int accumulate, void* stream) {
@@ -810,6 +852,13 @@ int insr_siren_jet_bwd_grad(const float* x, long n, int din, int dout, int L, in
   if (n == 0) return 0;
   if (!x || !params || !act || !work || !grad) return INSR_EINVAL;
   const JetCall c(din, W, mode);
+  if (c.resident(n, L)) {
+    hipStream_t st = (hipStream_t)stream;
+    int rc = 0;
+    if (!(params = with_planes(params, din, dout, L, W, mode, st, 0, &rc))) return rc;
+    return dispatch_resident_bwd(c.S, c.lap, L, x, (int)n, din, dout, params, act, gy, gdy, glap, work, grad,
+                                 accumulate, st);
+  }
   if (c.wide(n)) {
     hipStream_t st = (hipStream_t)stream;
     int rc = 0;

@@ -337,6 +337,13 @@ int dispatch_fwd_mixed_q(int NT, int din, const InsrJetJob* jobs, const int* mod
 // in a params buffer of INSR_MODE_WSPLIT), one launch
 int wsplit_launch(const float* prm, int din, int dout, int L, int W, float* planes, hipStream_t st);
 void wide_launch_threads(long n, int din, int dout, int L, int W, int S, long* out);
+// resident-dW backward (jet_x6r.hpp: W = 128, L <= 4, split-bf16 x6): one persistent launch + the
+// fixed-order partial sums
+int dispatch_resident_bwd(int S, bool LAP, int L, const float* x, int N, int din, int dout, const float* prm,
+                          const float* act, const float* gy, const float* gdy, const float* glap, float* work,
+                          float* grad, int accumulate, hipStream_t st);
+long resident_work_floats(long n, int din, int dout, int L);
+int resident_blocks(long n);
 
 // (S, LAP) combinations: value (1), grad d=1..3 (2..4), lap d=1..3 (3..5)
 #define INSR_DISPATCH(NTV, FN, ...)                \

@@ -1,0 +1,346 @@
+// jet_x6r.hpp -- the resident-dW backward of W = 128 SIRENs (jet_bwd_x6r): ONE launch walks
+// every tile of the batch in a persistent per-CU loop and keeps the weight gradients of ALL
+// hidden layers in the waves' registers from the first tile to the last, so the saved
+// streams are read once and nothing per tile (no z̄, no dW partial) goes to HBM.
+//
+// Why (round-3 profiles, fluid2Dtlgn): the two-kernel path (jet_x6w.hpp) moves ~700 MB per
+// Laplacian backward at 16,708 points -- the saved streams read twice (propagation kernel and
+// dW GEMM) and z̄ written and read once -- and the fused tile-split backward (jet_x6.hpp) writes
+// one full partial-gradient row per 5-tile block (209 x 266 KB) that a second kernel re-reads.
+// Here: block b of nb (nb = CUs) takes tiles [b T / nb, (b + 1) T / nb); per tile, layer
+// j = L .. 1: sine reverse, z̄_j and h_{j-1} split into bf16 planes in LDS, then
+//   dW_j += z̄_j h_{j-1}^T   (MFMA into dacc[j - 1], 8 x 16 rows x 128 columns per wave)
+//   h̄_{j-1} = W_j^T z̄_j    (MFMA, A from the pre-split W^T planes)
+// The biases, the first layer and the output layer (~1.4 K floats) accumulate in LDS (one owner
+// lane per entry: a fixed order).  At the end the block writes its dW (L W^2 floats) and its
+// compact row once; reduce_dw_kernel (jet_x6w.hpp) sums the nb partials in a fixed order.
+// Traffic per launch: saved streams once + nb (L W^2 + compact) floats written and re-read.
+//
+// Registers: the block is 4 waves (one per SIMD, 512 VGPR + AGPR per lane); wave w owns row tiles
+// 2w, 2w + 1 (32 rows) of every layer.  Its dW accumulators, L x 2 x 8 floatx4 = 256 registers at
+// L = 4, live in the AGPRs (MFMA C/D operands); the 256 VGPRs hold the propagation state.
+//
+// Reference semantics: loss.backward() (base/baseModel.py:73-78) through the jets of
+// base/diff_ops.py:44-82 -- the math of jet_x6.hpp / jet_x6w.hpp, another summation order.
+#pragma once
+#include <type_traits>
+
+#include "jet_x6w.hpp"
+
+namespace insr {
+
+constexpr int kX6rSmallMax = 1412;  // compact floats for W = 128, d_in, d_out <= 3, L <= 4 (16-B multiple)
+
+template <int NQ, int S>
+constexpr size_t x6r_lds_bytes() {
+  using BG = X6BwdGeo<NQ, 8>;
+  return (size_t)S * (BG::ZSET + BG::HSET) * 2 + (size_t)kX6rSmallMax * sizeof(float);
+}
+
+// h-stream s of a sine layer from sin / cos and the derivative z-streams held in registers
+template <int S, bool LAP>
+__device__ __forceinline__ floatx4 x6r_h(int s, const floatx4 (&zk)[S > 1 ? S - 1 : 1], const floatx4& sn,
+                                         const floatx4& cs) {
+  if constexpr (S == 1) {
+    return sn;
+  } else {
+    return h_from_regs<S, LAP>(s, zk, sn, cs);
+  }
+}
+
+template <int NQ, int S, bool LAP, int L>
+__global__ __launch_bounds__(256, 1) void jet_bwd_x6r(const float* __restrict__ x, int N, int din, int dout,
+                                                      const float* __restrict__ prm, const float* __restrict__ act,
+                                                      const float* __restrict__ gy, const float* __restrict__ gdy,
+                                                      const float* __restrict__ glap, float* __restrict__ dpart,
+                                                      float* __restrict__ small, long Ps, int nb) {
+  constexpr int NT = 8, W = 128, KC = 4, RPW = 2, TB = 256;
+  using BG = X6BwdGeo<NQ, NT>;
+  constexpr int LDB = BG::ZROW, ZPLANE = BG::ZPLANE, ZSET = BG::ZSET, HPLANE = BG::HPLANE, HSET = BG::HSET;
+  constexpr int NTAN = LAP ? S - 2 : S - 1;
+  constexpr int NCH = (S + 1) / 2;  // 32-deep K chunks of one tile's dW (S sets of 16 points)
+  constexpr int ZK = S > 1 ? S - 1 : 1;
+  extern __shared__ __attribute__((aligned(16))) float lds_f[];
+  unsigned short* Z = reinterpret_cast<unsigned short*>(lds_f);
+  unsigned short* H = Z + S * ZSET;
+  float* sacc = reinterpret_cast<float*>(H + S * HSET);  // compact accumulators (Ps floats)
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
+  const int rt0 = wave * RPW;  // this wave's row tiles: propagation outputs and dW rows
+  const int ntiles = ((N + 63) / 64) * 4;
+  const int tiles = (N + 15) / 16;
+  const int t0 = (int)((long)blockIdx.x * tiles / nb), t1 = (int)((long)(blockIdx.x + 1) * tiles / nb);
+  const long sb = (long)W * din + W;   // compact offset of b_1 (small_count layout, jet_x6w.hpp)
+  const long so = sb + (long)L * W;    // compact offset of W_out
+  const u32x4* wsp = wsp_base(prm, din, dout, L, W);
+  const float* Wo = prm + out_off(din, W, L);
+  for (int i = threadIdx.x; i < Ps; i += TB) sacc[i] = 0.f;
+
+  floatx4 dacc[L][RPW][NT];
+#pragma unroll
+  for (int j = 0; j < L; ++j)
+#pragma unroll
+    for (int i = 0; i < RPW; ++i)
+#pragma unroll
+      for (int ct = 0; ct < NT; ++ct) dacc[j][i][ct] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  // sin / cos of layer `layer` at this lane's 4 rows of each row tile of one tile, and its
+  // derivative z-streams
+  auto load_layer = [&](int layer, int tile, floatx4(&s_)[RPW], floatx4(&c_)[RPW], floatx4(&zk)[RPW][ZK]) {
+    const float* base = act_base(act, layer, ntiles, tile, S, NT);
+    floatx4 z[RPW];
+    float amax = 0.f;
+#pragma unroll
+    for (int i = 0; i < RPW; ++i) {
+      z[i] = *reinterpret_cast<const floatx4*>(base + ((rt0 + i) * 64 + lane) * 4);
+#pragma unroll
+      for (int s = 1; s < S; ++s)
+        zk[i][s - 1] = *reinterpret_cast<const floatx4*>(base + ((s * NT + rt0 + i) * 64 + lane) * 4);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) amax = fmaxf(amax, fabsf(OMEGA * z[i][r]));
+    }
+    const bool big = wave_any_big(amax);
+#pragma unroll
+    for (int i = 0; i < RPW; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float sv, cv;
+        if (big)
+          sincosf(OMEGA * z[i][r], &sv, &cv);
+        else
+          sincos_fast(OMEGA * z[i][r], sv, cv);
+        s_[i][r] = sv;
+        c_[i][r] = cv;
+      }
+  };
+  __syncthreads();  // sacc zeroed
+
+  for (int tile = t0; tile < t1; ++tile) {
+    const int p = tile * 16 + c;
+    const bool valid = p < N;
+    auto adjoint = [&](int s, int o) -> float {
+      if (!valid) return 0.f;
+      if (s == 0) return gy ? gy[(long)p * dout + o] : 0.f;
+      if (LAP && s == S - 1) return glap ? glap[(long)p * dout + o] : 0.f;
+      return gdy ? gdy[((long)p * dout + o) * din + (s - 1)] : 0.f;
+    };
+    floatx4 sn[RPW], cs[RPW], zk[RPW][ZK];
+    load_layer(L, tile, sn, cs, zk);
+
+    // ---- output layer (exact fp32 VALU): hb = W_out^T g, dW_out / db_out into the compact row ----
+    floatx4 hb[RPW][S];
+#pragma unroll
+    for (int i = 0; i < RPW; ++i)
+#pragma unroll
+      for (int s = 0; s < S; ++s) hb[i][s] = floatx4{0.f, 0.f, 0.f, 0.f};
+    for (int o = 0; o < dout; ++o) {
+      float ga[S];
+#pragma unroll
+      for (int s = 0; s < S; ++s) ga[s] = adjoint(s, o);
+#pragma unroll
+      for (int i = 0; i < RPW; ++i) {
+        const floatx4 w4 = *reinterpret_cast<const floatx4*>(Wo + (o * W + 16 * (rt0 + i) + 4 * g));
+        floatx4 acc4 = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < S; ++s) {
+          const floatx4 hs = x6r_h<S, LAP>(s, zk[i], sn[i], cs[i]);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            acc4[r] = fmaf(ga[s], hs[r], acc4[r]);
+            hb[i][s][r] = fmaf(w4[r], ga[s], hb[i][s][r]);
+          }
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float v = sum16(acc4[r]);
+          if (c == 0) sacc[so + (long)o * W + 16 * (rt0 + i) + 4 * g + r] += v;
+        }
+      }
+      if (wave == 0) {
+        const float v = sum16(g == 0 ? ga[0] : 0.f);
+        if (lane == 0) sacc[so + (long)dout * W + o] += v;
+      }
+    }
+
+    // ---- hidden layers j = L .. 1, each a compile-time j (dacc[j - 1] stays in registers) ----
+    auto layer = [&](auto jc) {
+      constexpr int j = decltype(jc)::value;
+      // the W^T planes through an opaque pointer: their loads are tile-invariant, and hoisting
+      // them out of the tile loop would pin L x KC fragments in registers
+      const u32x4* wsl = wsp;
+      asm volatile("" : "+s"(wsl));
+#pragma unroll
+      for (int i = 0; i < RPW; ++i) {
+        floatx4 zs[S];
+        zs[0] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 1; s < S; ++s) zs[s] = zk[i][s - 1];
+        sine_rev<S, LAP>(hb[i], zs, sn[i], cs[i]);  // hb = z̄_j
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float v = sum16(hb[i][0][r]);
+          if (c == 0) sacc[sb + (long)(j - 1) * W + 16 * (rt0 + i) + 4 * g + r] += v;
+        }
+      }
+      floatx4 snp[RPW], csp[RPW], zkp[RPW][ZK];
+      load_layer(j - 1, tile, snp, csp, zkp);
+      __syncthreads();  // the previous layer's / tile's LDS readers are done
+#pragma unroll
+      for (int i = 0; i < RPW; ++i)
+#pragma unroll
+        for (int s = 0; s < S; ++s) {
+          lds_put4<NQ, ZPLANE>(Z + s * ZSET + c * LDB + 16 * (rt0 + i) + 4 * g, hb[i][s][0], hb[i][s][1], hb[i][s][2],
+                               hb[i][s][3]);
+          put_neuron_major<NQ, HPLANE>(H + s * HSET, x6r_h<S, LAP>(s, zkp[i], snp[i], csp[i]), 16 * (rt0 + i) + 4 * g,
+                                       c);
+        }
+      __syncthreads();
+      // dW_j rows 16 rt + c (A: z̄ column reads of the point-major Z sets), columns m (B: H)
+#pragma unroll
+      for (int ch = 0; ch < NCH; ++ch) {
+        const int u = 2 * ch + (g >> 1);
+        const bool live = u < S;
+        const int p0 = 8 * (g & 1);
+        FragQ<NQ> af[RPW];
+#pragma unroll
+        for (int i = 0; i < RPW; ++i) {
+          const unsigned short* pa = Z + (live ? u : 0) * ZSET + (p0 + (c >> 2)) * LDB + 16 * (rt0 + i) + 4 * (c & 3);
+#pragma unroll
+          for (int q = 0; q < NQ; ++q) {
+            const v4s lo = ds_read_tr16(pa + q * ZPLANE);
+            const v4s hi = ds_read_tr16(pa + q * ZPLANE + 4 * LDB);
+            const u32x2 wl = __builtin_bit_cast(u32x2, lo), wh = __builtin_bit_cast(u32x2, hi);
+            af[i].q[q] = live ? u32x4{wl[0], wl[1], wh[0], wh[1]} : u32x4{0u, 0u, 0u, 0u};
+          }
+        }
+#pragma unroll
+        for (int ct = 0; ct < NT; ++ct) {
+          const FragQ<NQ> bf = lds_frag<NQ, HPLANE>(H + (live ? u : 0) * HSET + (16 * ct + c) * 16 + p0);
+#pragma unroll
+          for (int i = 0; i < RPW; ++i) dacc[j - 1][i][ct] = mfma_q<NQ>(af[i], bf, dacc[j - 1][i][ct]);
+          X6_SCHED_FENCE();
+        }
+      }
+      // propagation: h̄_{j-1}[m] = sum_n W_j[n][m] z̄_j[n] (A = W^T fragments, B = Z rows)
+      floatx4 nh[RPW][S];
+#pragma unroll
+      for (int i = 0; i < RPW; ++i)
+#pragma unroll
+        for (int s = 0; s < S; ++s) nh[i][s] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kc = 0; kc < KC; ++kc) {
+        FragQ<NQ> wt[RPW];
+#pragma unroll
+        for (int i = 0; i < RPW; ++i) wt[i] = wsp_frag<NQ, NT>(wsl, L, 1, j, rt0 + i, kc, lane);
+#pragma unroll
+        for (int s = 0; s < S; ++s) {
+          const FragQ<NQ> bf = lds_frag<NQ, ZPLANE>(Z + s * ZSET + c * LDB + 32 * kc + 8 * g);
+#pragma unroll
+          for (int i = 0; i < RPW; ++i) nh[i][s] = mfma_q<NQ>(wt[i], bf, nh[i][s]);
+          X6_SCHED_FENCE();
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < RPW; ++i) {
+#pragma unroll
+        for (int s = 0; s < S; ++s) hb[i][s] = nh[i][s];
+        sn[i] = snp[i];
+        cs[i] = csp[i];
+#pragma unroll
+        for (int s = 0; s < ZK; ++s) zk[i][s] = zkp[i][s];
+      }
+    };
+    if constexpr (L >= 4) layer(std::integral_constant<int, 4>{});
+    if constexpr (L >= 3) layer(std::integral_constant<int, 3>{});
+    if constexpr (L >= 2) layer(std::integral_constant<int, 2>{});
+    layer(std::integral_constant<int, 1>{});
+
+    // ---- first layer (K = d_in: exact fp32 VALU) ----
+    float xk[3];
+    for (int k = 0; k < 3; ++k) xk[k] = (valid && k < din) ? x[(long)p * din + k] : 0.f;
+#pragma unroll
+    for (int i = 0; i < RPW; ++i) {
+      floatx4 zs[S];
+      zs[0] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 1; s < S; ++s) zs[s] = zk[i][s - 1];
+      sine_rev<S, LAP>(hb[i], zs, sn[i], cs[i]);  // hb = z̄_0
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float v = sum16(hb[i][0][r]);
+        if (c == 0) sacc[(long)W * din + 16 * (rt0 + i) + 4 * g + r] += v;
+      }
+      for (int k = 0; k < din; ++k)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float v = hb[i][0][r] * xk[k];
+          if (k < NTAN) v += hb[i][1 + k][r];
+          v = sum16(v);
+          if (c == 0) sacc[(long)(16 * (rt0 + i) + 4 * g + r) * din + k] += v;
+        }
+    }
+  }
+
+  // ---- the block's partials: dW of every hidden layer, then the compact row ----
+#pragma unroll
+  for (int jl = 0; jl < L; ++jl) {
+    float* out = dpart + ((long)jl * nb + blockIdx.x) * W * W;
+#pragma unroll
+    for (int i = 0; i < RPW; ++i)
+#pragma unroll
+      for (int ct = 0; ct < NT; ++ct)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) out[(16 * (rt0 + i) + 4 * g + r) * W + 16 * ct + c] = dacc[jl][i][ct][r];
+  }
+  __syncthreads();  // every owner lane's last compact update
+  for (int i = threadIdx.x; i < Ps; i += TB) small[(long)blockIdx.x * Ps + i] = sacc[i];
+}
+
+// ---------------------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------------------
+inline int x6r_blocks(long n) {
+  static int cus = -1;
+  if (cus < 0) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+  }
+  const long tiles = (n + 15) / 16;
+  return (int)(tiles < cus ? tiles : cus);
+}
+
+// workspace floats: dW partials [layer][block][W^2] | compact rows [block][Ps]
+inline long x6r_work_floats(long n, int din, int dout, int L) {
+  const long nb = x6r_blocks(n);
+  return (long)L * nb * 128 * 128 + nb * small_count(din, dout, L, 128);
+}
+
+template <int NQ, int S, bool LAP, int L>
+int resident_bwd_t(const float* x, int N, int din, int dout, const float* prm, const float* act, const float* gy,
+                   const float* gdy, const float* glap, float* work, float* grad, int accumulate, hipStream_t st) {
+  constexpr int W = 128;
+  const int nb = x6r_blocks(N);
+  const long Ps = small_count(din, dout, L, W);
+  if (Ps > kX6rSmallMax) return INSR_EINVAL;
+  float* dpart = work;
+  float* small = dpart + (long)L * nb * W * W;
+  constexpr size_t lds = x6r_lds_bytes<NQ, S>();
+  static_assert(lds <= 163840, "LDS");
+  static_assert(L >= 1 && L <= 4, "resident dW: 1..4 hidden layers");
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)jet_bwd_x6r<NQ, S, LAP, L>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)lds);
+    attr = true;
+  }
+  hipLaunchKernelGGL((jet_bwd_x6r<NQ, S, LAP, L>), dim3(nb), dim3(256), lds, st, x, N, din, dout, prm, act, gy, gdy,
+                     glap, dpart, small, Ps, nb);
+  const int grad16 = (((uintptr_t)(grad + hidden_off(din, W, 1))) & 15) == 0 ? 1 : 0;
+  const int wq = (W * W / 4 + 63) / 64;
+  const int rows_x = (int)((Ps + 63) / 64);
+  hipLaunchKernelGGL(reduce_dw_kernel, dim3((unsigned)(wq > rows_x ? wq : rows_x), L + 1), dim3(512), 0, st, dpart, nb,
+                     din, W, grad, accumulate, grad16, L, small, nb, Ps, dout);
+  return (int)hipGetLastError();
+}
+
+}  // namespace insr

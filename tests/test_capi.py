@@ -157,3 +157,29 @@ def test_mixed_launch_rejects_malformed_jobs(lib):
         assert call(jobs, modes, **args) == -1, (modes, [(j.n, j.d_out) for j in jobs])
     assert call([job()], [V], prec=V | 1) == -1           # a jet mode inside prec_mode
     assert lib.insr_siren_jet_fwd_mixed(None, None, None, 1, 2, 2, 4, 128, 0, None) == -1
+
+
+def test_backward_path_policy(lib):
+    """insr_jet_bwd_path answers on the host: the resident-dW kernel for the fluid nets' value /
+    Laplacian backwards at the headline batch, the fused kernel for small batches, the two-kernel
+    path at W = 256; insr_jet_set_bwd_policy forces a path for A/B studies."""
+    from base import _native as nat
+    V, G, LAP = nat.MODE_VALUE, nat.MODE_GRAD, nat.MODE_LAP
+    old = lib.insr_jet_set_bwd_policy(0)
+    try:
+        assert lib.insr_jet_bwd_path(16708, 2, 1, 4, 128, LAP) == 2
+        assert lib.insr_jet_bwd_path(16708, 2, 2, 4, 128, V) == 2
+        assert lib.insr_jet_bwd_path(1024, 2, 2, 4, 128, V) == 0
+        assert lib.insr_jet_bwd_path(32768, 3, 3, 5, 256, G) == 1
+        assert lib.insr_jet_bwd_path(20400, 2, 2, 5, 128, G) != 2       # 5 hidden layers: not resident
+        assert lib.insr_jet_bwd_path(16708, 2, 1, 4, 128, LAP | nat.jet_prec(nat.PREC_BF16)) != 2  # x6 only
+        lib.insr_jet_set_bwd_policy(2)
+        assert lib.insr_jet_bwd_path(16708, 2, 1, 4, 128, LAP) == 1
+        lib.insr_jet_set_bwd_policy(1)
+        assert lib.insr_jet_bwd_path(16708, 2, 1, 4, 128, LAP) == 0
+        lib.insr_jet_set_bwd_policy(3)
+        assert lib.insr_jet_bwd_path(17, 2, 1, 3, 128, LAP) == 2
+        assert lib.insr_jet_bwd_path(17, 2, 1, 3, 64, LAP) != 2          # W = 128 only
+        assert lib.insr_jet_set_bwd_policy(9) == 3                      # out of range: unchanged
+    finally:
+        lib.insr_jet_set_bwd_policy(old)

@@ -28,6 +28,10 @@ for s in ${STEPS:-tests bench prof}; do
     dp2)   step dp2 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --backend gloo --steps 5 --warmup 3 --no-cpu-baseline ;;
     eager) step eager 150 python bench.py --steps 5 --warmup 2 --no-graph --no-cpu-baseline ;;
     graph) step graph 150 python bench.py --steps 5 --warmup 3 --no-cpu-baseline --no-roofline ;;
+    ab)    # same-box A/B of the backward-path policy (POLICIES, default "0 2 1"), 100 steps each, twice
+           for rep in 1 2; do for pol in ${POLICIES:-0 2 1}; do
+             step ab_p${pol}_$rep 200 python bench.py --steps 100 --warmup 5 --no-cpu-baseline --no-roofline --bwd-policy $pol ${ABARGS:-}
+           done; done ;;
     prof)  export TMPDIR=/tmp; step prof 400 rocprofv3 --kernel-trace --stats -d "$PWD/$OUT/prof" -o run --output-format csv -- python bench.py --steps 10 --warmup 3 --no-cpu-baseline ;;
     pmc)   export TMPDIR=/tmp
            # HBM traffic of the jet kernels in the bench workload (eager: one counter sample per dispatch);
