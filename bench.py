@@ -45,7 +45,10 @@ import torch.distributed as dist  # noqa: E402
 FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md chip table: dense fp32 matrix peak (spec)
 BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: ~2.5 PF dense bf16 (no sparsity)
 # per precision: (bench dtype, bf16 products per fp32-equivalent product, NQ of the kernel names)
-PRECISION = {"fp32": ("fp32", 6, 3), "bf16x3": ("bf16x3", 3, 2), "bf16": ("bf16", 1, 1)}
+PRECISION = {"fp32": ("fp32", 6, 3), "bf16x3": ("bf16x3", 3, 2), "bf16": ("bf16", 1, 1),
+             # BASELINE configs[4] "mixed fp32/bf16 MFMA": bf16x3 forwards, bf16 backwards (the
+             # dominant launch is a backward: its products and kernel names are the bf16 ones)
+             "mixed": ("bf16x3/bf16", 1, 1)}
 HBM_PEAK_GBS = 8000.0
 
 
@@ -67,11 +70,14 @@ def parse():
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--precision", choices=sorted(PRECISION), default="fp32",
                     help="matrix-core precision of every jet: fp32 (fp32-accurate split-bf16, the parity "
-                         "config), bf16x3 (3 bf16 products) or bf16 (1 product; BASELINE configs[4] "
-                         "'mixed fp32/bf16 MFMA')")
+                         "config), bf16x3 (3 bf16 products), bf16 (1 product) or mixed (bf16x3 forwards, bf16 "
+                         "backwards: BASELINE configs[4] 'mixed fp32/bf16 MFMA', within 1e-2)")
     ap.add_argument("--api", choices=["fused", "plain"], default="fused",
                     help="fluid: 'plain' runs pde/fluid_plain.py, phase bodies written only against the "
                          "reference's base API (separate band samplers, torch residuals) -- the drop-in case")
+    ap.add_argument("--shard-of", type=int, default=1,
+                    help="one process runs the per-rank shard of a K-rank strong-scaling run (global batch / K "
+                         "points per phase iteration; elasticity: the draw at resolution / K^(1/3)); 1 GPU")
     ap.add_argument("--bwd-policy", type=int, default=0, choices=[0, 1, 2, 3],
                     help="backward path (A/B studies): 0 auto, 1 fused tile-split, 2 two-kernel, 3 resident dW")
     ap.add_argument("--cpu-seconds", type=float, default=25.0, help="budget of the CPU-baseline sample")
@@ -174,12 +180,28 @@ def build_model(args, world, rank):
                           proj_dir="/tmp/insr_bench", max_n_iters=10 ** 9,
                           insr_precision=None if args.precision == "fp32" else args.precision)
     n_global = interior_points(cfg, wl)
+    if args.shard_of > 1:  # one rank's shard of a shard_of-rank strong-scaling run, measured alone
+        if world != 1:
+            raise SystemExit("--shard-of is a single-process measurement")
+        if wl["pde"] in ("fluid", "advection"):
+            cfg.insr_points_per_rank = n_global // args.shard_of
+            return finish_model(args, cfg, wl, world, rank, n_global // args.shard_of)
+        r = round(res / args.shard_of ** (1.0 / cfg.dim))
+        if r ** cfg.dim * args.shard_of != res ** cfg.dim:
+            raise SystemExit(f"--shard-of {args.shard_of}: {res}^{cfg.dim} points do not split into cubes")
+        cfg.sample_resolution = r
+        cfg.insr_dp_weak = True
+        return finish_model(args, cfg, wl, world, rank, interior_points(cfg, wl))
     if wl["pde"] in ("fluid", "advection"):
         # strong: the global batch is split over ranks; weak: every rank keeps the full batch
         cfg.insr_points_per_rank = n_global // world if args.scaling == "strong" else n_global
     else:
         # elasticity draws the global batch and keeps its rank's slice (strong); weak: no slicing
         cfg.insr_dp_weak = args.scaling == "weak"
+    return finish_model(args, cfg, wl, world, rank, n_global // world if args.scaling == "strong" else n_global)
+
+
+def finish_model(args, cfg, wl, world, rank, per_rank):
     torch.manual_seed(1234)  # identical weights on every rank
     if wl["pde"] == "fluid" and args.api == "plain":
         from pde.fluid_plain import Fluid2DPlainModel as M
@@ -193,7 +215,6 @@ def build_model(args, world, rank):
     model.timestep = 1
     model.init_cond_func = None
     torch.cuda.manual_seed(1234 + 7919 * rank)  # independent collocation points per rank
-    per_rank = n_global // world if args.scaling == "strong" else n_global
     return model, cfg, wl, per_rank
 
 
@@ -549,7 +570,7 @@ def main():
     elapsed, ts_ms = float(t[0]), [float(v) for v in t[1:]]
     log(f"timed {args.steps} steps ({nts} timesteps): {elapsed * 1e3:.2f} ms")
     # points all ranks processed: strong = the global batch, weak = world x the per-rank batch
-    n_all = interior_points(cfg, wl) if args.scaling == "strong" else n_local * world
+    n_all = interior_points(cfg, wl) if (args.scaling == "strong" and args.shard_of == 1) else n_local * world
     total_points = n_all * nph * args.steps
     value = total_points / elapsed
     per_ts = sorted((n_all * nph * k) / (ms * 1e-3) for k, ms in zip(ks, ts_ms))
@@ -564,7 +585,7 @@ def main():
                    "points_per_phase_iter": n_all, "phases": nph, "global_batch": n_all,
                    "seq_len": None, "parallelism": f"dp{world}", "graph": not args.no_graph,
                    "precision": args.precision, "api": args.api, "sync_every": cfg.insr_sync_every,
-                   "bwd_policy": args.bwd_policy,
+                   "bwd_policy": args.bwd_policy, "shard_of": args.shard_of,
                    "timestep_order": f"{nts} timesteps x ({'/'.join(str(k) for k in ks)}) iterations per phase, "
                                      "phases in step() order with the prev-net snapshots"},
         "timesteps": {"count": nts, "iters_per_phase": ks, "ms": [round(v, 3) for v in ts_ms],

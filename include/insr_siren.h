@@ -51,6 +51,11 @@ extern "C" {
  * (insr_jet_set_precision) applies.  The saved-activation layout does not depend on it. */
 #define INSR_MODE_PREC_SHIFT 4
 #define INSR_JET_PREC(p) (((p) + 1) << INSR_MODE_PREC_SHIFT)
+/* Backward-only override (a "mixed" precision: e.g. a bf16x3 forward with a bf16 backward):
+ * OR INSR_JET_BPREC(p) as well; the backward of the call then runs at p, the forward at the
+ * INSR_JET_PREC / process-default precision. */
+#define INSR_MODE_BPREC_SHIFT 12
+#define INSR_JET_BPREC(p) (((p) + 1) << INSR_MODE_BPREC_SHIFT)
 /* INSR_MODE_WSPLIT: the params buffer carries the pre-split weight planes of
  * insr_siren_wsplit() after the parameters (at insr_siren_wsplit_offset() floats), up to date
  * with the parameters.  Without it an entry point that runs split-bf16 kernels splits the

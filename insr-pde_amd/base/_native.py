@@ -23,6 +23,14 @@ PRECISIONS = {"fp32": PREC_F32, "bf16x6": PREC_BF16X6, "bf16x3": PREC_BF16X3, "b
 def jet_prec(p):
     """INSR_JET_PREC(p): the per-call precision bits OR-ed into a jet `mode`."""
     return (int(p) + 1) << MODE_PREC_SHIFT
+
+
+MODE_BPREC_SHIFT = 12
+
+
+def jet_bprec(p):
+    """INSR_JET_BPREC(p): a backward-only precision override OR-ed into a jet `mode`."""
+    return (int(p) + 1) << MODE_BPREC_SHIFT
 LOSS_COMBO, LOSS_BANDS = 0, 1
 OPT_LR, OPT_STEP, OPT_BEST, OPT_BAD, OPT_STEPSIZE, OPT_BC2SQRT, OPT_FACTOR, OPT_MINLR = range(8)
 OPT_TICKET = 8  # the fused Adam + plateau launch's last-block ticket (0 between launches)

@@ -80,6 +80,25 @@ def kernel_width(width):
     raise NotImplementedError(f"hidden width {width} > {KERNEL_WIDTHS[-1]}: no HIP kernel")
 
 
+# 'mixed' (BASELINE.json configs[4] "mixed fp32/bf16 MFMA"): the forward / backward precision pair
+# measured fastest within 1e-2 normwise on every op and parameter gradient (profiles/r03/prec_*).
+MIXED_PRECISION = "bf16x3/bf16"
+
+
+def _parse_precision(precision):
+    """None, a name of _native.PRECISIONS, 'fwd/bwd' names or 'mixed' -> (fwd, bwd) ints or None."""
+    from ._native import PRECISIONS
+    if precision is None:
+        return None
+    name = MIXED_PRECISION if precision == "mixed" else precision
+    parts = name.split("/")
+    if len(parts) == 1:
+        parts = parts * 2
+    if len(parts) != 2 or any(p not in PRECISIONS for p in parts):
+        raise ValueError(f"precision {precision!r}: one of {sorted(PRECISIONS)}, 'fwd/bwd' of those, 'mixed' or None")
+    return PRECISIONS[parts[0]], PRECISIONS[parts[1]]
+
+
 class MLP(nn.Module):
     """SIREN MLP with flat parameter storage and a HIP forward (base/networks.py:30-71)."""
 
@@ -110,19 +129,22 @@ class MLP(nn.Module):
 
     # ---- matrix-core precision ------------------------------------------------
     def set_precision(self, precision):
-        """None (the library default: fp32-accurate split-bf16), or one of 'fp32', 'bf16x6',
-        'bf16x3', 'bf16' for every jet of this network (include/insr_siren.h INSR_PREC_*)."""
-        from ._native import PRECISIONS
-        if precision is not None and precision not in PRECISIONS:
-            raise ValueError(f"precision {precision!r}: one of {sorted(PRECISIONS)} or None")
+        """None (the library default: fp32-accurate split-bf16), one of 'fp32', 'bf16x6', 'bf16x3',
+        'bf16' for every jet of this network (include/insr_siren.h INSR_PREC_*), 'fwd/bwd' with one
+        name per direction (e.g. 'bf16x3/bf16'), or 'mixed' (= MIXED_PRECISION: the fastest
+        forward/backward pair measured within 1e-2 normwise, tools/prec_errors.py)."""
+        self._prec_pair = _parse_precision(precision)
         self.precision = precision
 
     def call_mode(self, mode):
         """The jet `mode` argument of this network's library calls (precision bits added; the
         flat buffer carries the pre-split weight planes: INSR_MODE_WSPLIT)."""
-        from ._native import MODE_WSPLIT, PRECISIONS, jet_prec
+        from ._native import MODE_WSPLIT, jet_bprec, jet_prec
         mode |= MODE_WSPLIT
-        return mode if self.precision is None else mode | jet_prec(PRECISIONS[self.precision])
+        if self._prec_pair is None:
+            return mode
+        pf, pb = self._prec_pair
+        return mode | jet_prec(pf) | (jet_bprec(pb) if pb != pf else 0)
 
     # ---- pre-split weight planes (include/insr_siren.h insr_siren_wsplit) -----------
     # The flat storage is [parameters | pad to 16 B | planes]: every hidden weight split in three

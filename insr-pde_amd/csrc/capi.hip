@@ -33,10 +33,11 @@ static int env_or(const char* name, int dflt) {
 // 2 two-kernel (jet_x6w.hpp), 3 resident dW (jet_x6r.hpp) where it applies.
 static int g_bwd_policy = 0;
 
-// The resident-dW backward (jet_x6r.hpp) serves W = 128 nets of <= 4 hidden layers at x6
-// precision: value, 2-d gradient and 2-d Laplacian jets, once the batch fills the CUs.
+// The resident-dW backward (jet_x6r.hpp) serves W = 128 nets of 4 hidden layers (the fluid
+// nets; compiled for that depth only) at x6 precision: value, 2-d gradient and 2-d Laplacian
+// jets, once the batch fills the CUs.
 bool resident_ok(int S, int NT, bool lap, int nq, int L) {
-  if (NT != 8 || nq != 3 || L < 1 || L > 4) return false;
+  if (NT != 8 || nq != 3 || L != 4) return false;
   return (S == 1 && !lap) || (S == 3 && !lap) || (S == 4 && lap);
 }
 bool use_resident(long n, int S, int NT, bool lap, int nq, int L) {
@@ -75,9 +76,12 @@ static void prec_init() {
 
 static bool prec_ok(int p) { return p >= INSR_PREC_F32 && p <= INSR_PREC_BF16; }
 
-// precision of a call (direction bwd): the mode's override, else the process default
+// precision of a call (direction bwd): the mode's backward override (bwd), else its
+// override, else the process default
 int call_prec(int mode, int bwd) {
   prec_init();
+  const int pb = (mode >> INSR_MODE_BPREC_SHIFT) & 0xF;
+  if (bwd && pb) return pb - 1;
   const int po = (mode >> INSR_MODE_PREC_SHIFT) & 0xF;
   return po ? po - 1 : g_prec[bwd ? 1 : 0];
 }
@@ -484,9 +488,10 @@ __global__ void adam_multi_kernel(AdamList L, float* __restrict__ st, float b1, 
 bool shape_ok(int din, int dout, int L, int width, int mode) {
   if (din < 1 || din > 3 || dout < 1 || dout > 3 || L < 0 || L > 64) return false;
   if (nt_for(width) < 0) return false;
-  if (mode & ~(INSR_MODE_MASK | (0xF << INSR_MODE_PREC_SHIFT) | INSR_MODE_WSPLIT)) return false;
-  const int po = (mode >> INSR_MODE_PREC_SHIFT) & 0xF;
-  if (po && !prec_ok(po - 1)) return false;
+  if (mode & ~(INSR_MODE_MASK | (0xF << INSR_MODE_PREC_SHIFT) | (0xF << INSR_MODE_BPREC_SHIFT) | INSR_MODE_WSPLIT))
+    return false;
+  const int po = (mode >> INSR_MODE_PREC_SHIFT) & 0xF, pb = (mode >> INSR_MODE_BPREC_SHIFT) & 0xF;
+  if ((po && !prec_ok(po - 1)) || (pb && !prec_ok(pb - 1))) return false;
   const int jm = mode & INSR_MODE_MASK;
   const int S = streams_for(din, jm);
   if (S < 1 || S > 5) return false;  // the Laplacian jet of a 3-d input carries 5 streams

@@ -7,10 +7,11 @@
 // Laplacian backward at 16,708 points -- the saved streams read twice (propagation kernel and
 // dW GEMM) and z̄ written and read once -- and the fused tile-split backward (jet_x6.hpp) writes
 // one full partial-gradient row per 5-tile block (209 x 266 KB) that a second kernel re-reads.
-// Here: block b of nb (nb = CUs) takes tiles [b T / nb, (b + 1) T / nb); per tile, layer
-// j = L .. 1: sine reverse, z̄_j and h_{j-1} split into bf16 planes in LDS, then
-//   dW_j += z̄_j h_{j-1}^T   (MFMA into dacc[j - 1], 8 x 16 rows x 128 columns per wave)
-//   h̄_{j-1} = W_j^T z̄_j    (MFMA, A from the pre-split W^T planes)
+// Here: block b of nb (nb = CUs) takes tiles [b T / nb, (b + 1) T / nb), TS at a time (a
+// "step": 2 tiles for value jets, so one dW K-chunk is 32 points; 1 tile otherwise); per step,
+// layer j = L .. 1: sine reverse, z̄_j and h_{j-1} split into bf16 planes in LDS, then
+//   dW_j += z̄_j h_{j-1}^T   (MFMA into dacc[j - 1]: 32 rows x 128 columns per wave)
+//   h̄_{j-1} = W_j^T z̄_j    (MFMA, A from the pre-split W^T planes, next fragment prefetched)
 // The biases, the first layer and the output layer (~1.4 K floats) accumulate in LDS (one owner
 // lane per entry: a fixed order).  At the end the block writes its dW (L W^2 floats) and its
 // compact row once; reduce_dw_kernel (jet_x6w.hpp) sums the nb partials in a fixed order.
@@ -18,7 +19,10 @@
 //
 // Registers: the block is 4 waves (one per SIMD, 512 VGPR + AGPR per lane); wave w owns row tiles
 // 2w, 2w + 1 (32 rows) of every layer.  Its dW accumulators, L x 2 x 8 floatx4 = 256 registers at
-// L = 4, live in the AGPRs (MFMA C/D operands); the 256 VGPRs hold the propagation state.
+// L = 4, live in the AGPRs (MFMA C/D operands); the 256 VGPRs hold the propagation state.  With
+// one wave per SIMD nothing hides latency but the wave's own schedule: the saved streams of
+// layer j - 1 are loaded one layer ahead (value jets; the Laplacian state has no registers to
+// spare) and every W^T fragment one fragment ahead.
 //
 // Reference semantics: loss.backward() (base/baseModel.py:73-78) through the jets of
 // base/diff_ops.py:44-82 -- the math of jet_x6.hpp / jet_x6w.hpp, another summation order.
@@ -31,10 +35,13 @@ namespace insr {
 
 constexpr int kX6rSmallMax = 1412;  // compact floats for W = 128, d_in, d_out <= 3, L <= 4 (16-B multiple)
 
+template <int S>
+constexpr int x6r_ts() { return S == 1 ? 2 : 1; }  // tiles per step
+
 template <int NQ, int S>
 constexpr size_t x6r_lds_bytes() {
   using BG = X6BwdGeo<NQ, 8>;
-  return (size_t)S * (BG::ZSET + BG::HSET) * 2 + (size_t)kX6rSmallMax * sizeof(float);
+  return (size_t)x6r_ts<S>() * S * (BG::ZSET + BG::HSET) * 2 + (size_t)kX6rSmallMax * sizeof(float);
 }
 
 // h-stream s of a sine layer from sin / cos and the derivative z-streams held in registers
@@ -55,15 +62,18 @@ __global__ __launch_bounds__(256, 1) void jet_bwd_x6r(const float* __restrict__ 
                                                       const float* __restrict__ glap, float* __restrict__ dpart,
                                                       float* __restrict__ small, long Ps, int nb) {
   constexpr int NT = 8, W = 128, KC = 4, RPW = 2, TB = 256;
+  constexpr int TS = x6r_ts<S>();      // tiles per step
+  constexpr int NSET = TS * S;          // 16-point sets of a step (set u = t S + s)
+  constexpr int NCH = (NSET + 1) / 2;   // 32-deep K chunks of the step's dW
+  constexpr bool PF = S <= 2;           // saved streams loaded one layer ahead
   using BG = X6BwdGeo<NQ, NT>;
   constexpr int LDB = BG::ZROW, ZPLANE = BG::ZPLANE, ZSET = BG::ZSET, HPLANE = BG::HPLANE, HSET = BG::HSET;
   constexpr int NTAN = LAP ? S - 2 : S - 1;
-  constexpr int NCH = (S + 1) / 2;  // 32-deep K chunks of one tile's dW (S sets of 16 points)
   constexpr int ZK = S > 1 ? S - 1 : 1;
   extern __shared__ __attribute__((aligned(16))) float lds_f[];
   unsigned short* Z = reinterpret_cast<unsigned short*>(lds_f);
-  unsigned short* H = Z + S * ZSET;
-  float* sacc = reinterpret_cast<float*>(H + S * HSET);  // compact accumulators (Ps floats)
+  unsigned short* H = Z + NSET * ZSET;
+  float* sacc = reinterpret_cast<float*>(H + NSET * HSET);  // compact accumulators (Ps floats)
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
   const int rt0 = wave * RPW;  // this wave's row tiles: propagation outputs and dW rows
   const int ntiles = ((N + 63) / 64) * 4;
@@ -83,72 +93,94 @@ __global__ __launch_bounds__(256, 1) void jet_bwd_x6r(const float* __restrict__ 
 #pragma unroll
       for (int ct = 0; ct < NT; ++ct) dacc[j][i][ct] = floatx4{0.f, 0.f, 0.f, 0.f};
 
-  // sin / cos of layer `layer` at this lane's 4 rows of each row tile of one tile, and its
-  // derivative z-streams
-  auto load_layer = [&](int layer, int tile, floatx4(&s_)[RPW], floatx4(&c_)[RPW], floatx4(&zk)[RPW][ZK]) {
-    const float* base = act_base(act, layer, ntiles, tile, S, NT);
-    floatx4 z[RPW];
+  // raw saved streams of one layer for the step's tiles (slot t of a short step re-reads tile
+  // tb: valid memory; its adjoints are zero, so it contributes nothing)
+  auto fetch = [&](int layer, int tb, int cnt, floatx4(&zr)[TS][RPW][S]) {
+#pragma unroll
+    for (int t = 0; t < TS; ++t) {
+      const float* base = act_base(act, layer, ntiles, tb + (t < cnt ? t : 0), S, NT);
+#pragma unroll
+      for (int i = 0; i < RPW; ++i)
+#pragma unroll
+        for (int s = 0; s < S; ++s)
+          zr[t][i][s] = *reinterpret_cast<const floatx4*>(base + ((s * NT + rt0 + i) * 64 + lane) * 4);
+    }
+  };
+  // sin / cos and the derivative z-streams from the raw streams
+  auto unpack = [&](const floatx4(&zr)[TS][RPW][S], floatx4(&s_)[TS][RPW], floatx4(&c_)[TS][RPW],
+                    floatx4(&zk)[TS][RPW][ZK]) {
     float amax = 0.f;
 #pragma unroll
-    for (int i = 0; i < RPW; ++i) {
-      z[i] = *reinterpret_cast<const floatx4*>(base + ((rt0 + i) * 64 + lane) * 4);
+    for (int t = 0; t < TS; ++t)
 #pragma unroll
-      for (int s = 1; s < S; ++s)
-        zk[i][s - 1] = *reinterpret_cast<const floatx4*>(base + ((s * NT + rt0 + i) * 64 + lane) * 4);
+      for (int i = 0; i < RPW; ++i) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) amax = fmaxf(amax, fabsf(OMEGA * z[i][r]));
-    }
+        for (int s = 1; s < S; ++s) zk[t][i][s - 1] = zr[t][i][s];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) amax = fmaxf(amax, fabsf(OMEGA * zr[t][i][0][r]));
+      }
     const bool big = wave_any_big(amax);
 #pragma unroll
-    for (int i = 0; i < RPW; ++i)
+    for (int t = 0; t < TS; ++t)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float sv, cv;
-        if (big)
-          sincosf(OMEGA * z[i][r], &sv, &cv);
-        else
-          sincos_fast(OMEGA * z[i][r], sv, cv);
-        s_[i][r] = sv;
-        c_[i][r] = cv;
-      }
+      for (int i = 0; i < RPW; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float sv, cv;
+          if (big)
+            sincosf(OMEGA * zr[t][i][0][r], &sv, &cv);
+          else
+            sincos_fast(OMEGA * zr[t][i][0][r], sv, cv);
+          s_[t][i][r] = sv;
+          c_[t][i][r] = cv;
+        }
   };
   __syncthreads();  // sacc zeroed
 
-  for (int tile = t0; tile < t1; ++tile) {
-    const int p = tile * 16 + c;
-    const bool valid = p < N;
-    auto adjoint = [&](int s, int o) -> float {
-      if (!valid) return 0.f;
+  for (int tb = t0; tb < t1; tb += TS) {
+    const int cnt = t1 - tb < TS ? t1 - tb : TS;
+    auto adjoint = [&](int t, int s, int o) -> float {
+      const int p = (tb + t) * 16 + c;
+      if (t >= cnt || p >= N) return 0.f;
       if (s == 0) return gy ? gy[(long)p * dout + o] : 0.f;
       if (LAP && s == S - 1) return glap ? glap[(long)p * dout + o] : 0.f;
       return gdy ? gdy[((long)p * dout + o) * din + (s - 1)] : 0.f;
     };
-    floatx4 sn[RPW], cs[RPW], zk[RPW][ZK];
-    load_layer(L, tile, sn, cs, zk);
+    floatx4 sn[TS][RPW], cs[TS][RPW], zk[TS][RPW][ZK];
+    floatx4 zr[TS][RPW][S];  // the next layer's raw streams (PF: one layer ahead)
+    fetch(L, tb, cnt, zr);
+    unpack(zr, sn, cs, zk);
+    if constexpr (PF) fetch(L - 1, tb, cnt, zr);
 
     // ---- output layer (exact fp32 VALU): hb = W_out^T g, dW_out / db_out into the compact row ----
-    floatx4 hb[RPW][S];
+    floatx4 hb[TS][RPW][S];
 #pragma unroll
-    for (int i = 0; i < RPW; ++i)
+    for (int t = 0; t < TS; ++t)
 #pragma unroll
-      for (int s = 0; s < S; ++s) hb[i][s] = floatx4{0.f, 0.f, 0.f, 0.f};
+      for (int i = 0; i < RPW; ++i)
+#pragma unroll
+        for (int s = 0; s < S; ++s) hb[t][i][s] = floatx4{0.f, 0.f, 0.f, 0.f};
     for (int o = 0; o < dout; ++o) {
-      float ga[S];
+      float ga[TS][S];
 #pragma unroll
-      for (int s = 0; s < S; ++s) ga[s] = adjoint(s, o);
+      for (int t = 0; t < TS; ++t)
+#pragma unroll
+        for (int s = 0; s < S; ++s) ga[t][s] = adjoint(t, s, o);
 #pragma unroll
       for (int i = 0; i < RPW; ++i) {
         const floatx4 w4 = *reinterpret_cast<const floatx4*>(Wo + (o * W + 16 * (rt0 + i) + 4 * g));
         floatx4 acc4 = floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int s = 0; s < S; ++s) {
-          const floatx4 hs = x6r_h<S, LAP>(s, zk[i], sn[i], cs[i]);
+        for (int t = 0; t < TS; ++t)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            acc4[r] = fmaf(ga[s], hs[r], acc4[r]);
-            hb[i][s][r] = fmaf(w4[r], ga[s], hb[i][s][r]);
+          for (int s = 0; s < S; ++s) {
+            const floatx4 hs = x6r_h<S, LAP>(s, zk[t][i], sn[t][i], cs[t][i]);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              acc4[r] = fmaf(ga[t][s], hs[r], acc4[r]);
+              hb[t][i][s][r] = fmaf(w4[r], ga[t][s], hb[t][i][s][r]);
+            }
           }
-        }
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const float v = sum16(acc4[r]);
@@ -156,7 +188,10 @@ __global__ __launch_bounds__(256, 1) void jet_bwd_x6r(const float* __restrict__ 
         }
       }
       if (wave == 0) {
-        const float v = sum16(g == 0 ? ga[0] : 0.f);
+        float gsum = 0.f;
+#pragma unroll
+        for (int t = 0; t < TS; ++t) gsum += (g == 0) ? ga[t][0] : 0.f;
+        const float v = sum16(gsum);
         if (lane == 0) sacc[so + (long)dout * W + o] += v;
       }
     }
@@ -164,41 +199,55 @@ __global__ __launch_bounds__(256, 1) void jet_bwd_x6r(const float* __restrict__ 
     // ---- hidden layers j = L .. 1, each a compile-time j (dacc[j - 1] stays in registers) ----
     auto layer = [&](auto jc) {
       constexpr int j = decltype(jc)::value;
-      // the W^T planes through an opaque pointer: their loads are tile-invariant, and hoisting
+      // the W^T planes through an opaque pointer: their loads are step-invariant, and hoisting
       // them out of the tile loop would pin L x KC fragments in registers
       const u32x4* wsl = wsp;
       asm volatile("" : "+s"(wsl));
 #pragma unroll
-      for (int i = 0; i < RPW; ++i) {
-        floatx4 zs[S];
-        zs[0] = floatx4{0.f, 0.f, 0.f, 0.f};
+      for (int t = 0; t < TS; ++t)
 #pragma unroll
-        for (int s = 1; s < S; ++s) zs[s] = zk[i][s - 1];
-        sine_rev<S, LAP>(hb[i], zs, sn[i], cs[i]);  // hb = z̄_j
+        for (int i = 0; i < RPW; ++i) {
+          floatx4 zs[S];
+          zs[0] = floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float v = sum16(hb[i][0][r]);
-          if (c == 0) sacc[sb + (long)(j - 1) * W + 16 * (rt0 + i) + 4 * g + r] += v;
+          for (int s = 1; s < S; ++s) zs[s] = zk[t][i][s - 1];
+          sine_rev<S, LAP>(hb[t][i], zs, sn[t][i], cs[t][i]);  // hb = z̄_j
         }
-      }
-      floatx4 snp[RPW], csp[RPW], zkp[RPW][ZK];
-      load_layer(j - 1, tile, snp, csp, zkp);
-      __syncthreads();  // the previous layer's / tile's LDS readers are done
 #pragma unroll
       for (int i = 0; i < RPW; ++i)
 #pragma unroll
-        for (int s = 0; s < S; ++s) {
-          lds_put4<NQ, ZPLANE>(Z + s * ZSET + c * LDB + 16 * (rt0 + i) + 4 * g, hb[i][s][0], hb[i][s][1], hb[i][s][2],
-                               hb[i][s][3]);
-          put_neuron_major<NQ, HPLANE>(H + s * HSET, x6r_h<S, LAP>(s, zkp[i], snp[i], csp[i]), 16 * (rt0 + i) + 4 * g,
-                                       c);
+        for (int r = 0; r < 4; ++r) {
+          float bsum = 0.f;
+#pragma unroll
+          for (int t = 0; t < TS; ++t) bsum += hb[t][i][0][r];
+          const float v = sum16(bsum);
+          if (c == 0) sacc[sb + (long)(j - 1) * W + 16 * (rt0 + i) + 4 * g + r] += v;
         }
+      floatx4 snp[TS][RPW], csp[TS][RPW], zkp[TS][RPW][ZK];
+      if constexpr (!PF) fetch(j - 1, tb, cnt, zr);
+      unpack(zr, snp, csp, zkp);
+      if constexpr (PF) {
+        if (j >= 2) fetch(j - 2, tb, cnt, zr);  // one layer ahead, in flight through this layer's MFMAs
+      }
+      __syncthreads();  // the previous layer's / step's LDS readers are done
+#pragma unroll
+      for (int t = 0; t < TS; ++t)
+#pragma unroll
+        for (int i = 0; i < RPW; ++i)
+#pragma unroll
+          for (int s = 0; s < S; ++s) {
+            const int u = t * S + s;
+            lds_put4<NQ, ZPLANE>(Z + u * ZSET + c * LDB + 16 * (rt0 + i) + 4 * g, hb[t][i][s][0], hb[t][i][s][1],
+                                 hb[t][i][s][2], hb[t][i][s][3]);
+            put_neuron_major<NQ, HPLANE>(H + u * HSET, x6r_h<S, LAP>(s, zkp[t][i], snp[t][i], csp[t][i]),
+                                         16 * (rt0 + i) + 4 * g, c);
+          }
       __syncthreads();
       // dW_j rows 16 rt + c (A: z̄ column reads of the point-major Z sets), columns m (B: H)
 #pragma unroll
       for (int ch = 0; ch < NCH; ++ch) {
         const int u = 2 * ch + (g >> 1);
-        const bool live = u < S;
+        const bool live = u < NSET;
         const int p0 = 8 * (g & 1);
         FragQ<NQ> af[RPW];
 #pragma unroll
@@ -220,34 +269,41 @@ __global__ __launch_bounds__(256, 1) void jet_bwd_x6r(const float* __restrict__ 
           X6_SCHED_FENCE();
         }
       }
-      // propagation: h̄_{j-1}[m] = sum_n W_j[n][m] z̄_j[n] (A = W^T fragments, B = Z rows)
-      floatx4 nh[RPW][S];
+      // propagation: h̄_{j-1}[m] = sum_n W_j[n][m] z̄_j[n] (A = W^T fragments, B = Z rows); the
+      // fragments in (row tile, K chunk) order, each prefetched one ahead
+      floatx4 nh[TS][RPW][S];
 #pragma unroll
-      for (int i = 0; i < RPW; ++i)
+      for (int t = 0; t < TS; ++t)
 #pragma unroll
-        for (int s = 0; s < S; ++s) nh[i][s] = floatx4{0.f, 0.f, 0.f, 0.f};
+        for (int i = 0; i < RPW; ++i)
 #pragma unroll
-      for (int kc = 0; kc < KC; ++kc) {
-        FragQ<NQ> wt[RPW];
+          for (int s = 0; s < S; ++s) nh[t][i][s] = floatx4{0.f, 0.f, 0.f, 0.f};
+      FragQ<NQ> wn = wsp_frag<NQ, NT>(wsl, L, 1, j, rt0, 0, lane);
 #pragma unroll
-        for (int i = 0; i < RPW; ++i) wt[i] = wsp_frag<NQ, NT>(wsl, L, 1, j, rt0 + i, kc, lane);
+      for (int f = 0; f < RPW * KC; ++f) {
+        const int i = f / KC, kc = f % KC;
+        const FragQ<NQ> wt = wn;
+        if (f + 1 < RPW * KC) wn = wsp_frag<NQ, NT>(wsl, L, 1, j, rt0 + (f + 1) / KC, (f + 1) % KC, lane);
 #pragma unroll
-        for (int s = 0; s < S; ++s) {
-          const FragQ<NQ> bf = lds_frag<NQ, ZPLANE>(Z + s * ZSET + c * LDB + 32 * kc + 8 * g);
+        for (int t = 0; t < TS; ++t)
 #pragma unroll
-          for (int i = 0; i < RPW; ++i) nh[i][s] = mfma_q<NQ>(wt[i], bf, nh[i][s]);
-          X6_SCHED_FENCE();
+          for (int s = 0; s < S; ++s) {
+            const FragQ<NQ> bf = lds_frag<NQ, ZPLANE>(Z + (t * S + s) * ZSET + c * LDB + 32 * kc + 8 * g);
+            nh[t][i][s] = mfma_q<NQ>(wt, bf, nh[t][i][s]);
+            X6_SCHED_FENCE();
+          }
+      }
+#pragma unroll
+      for (int t = 0; t < TS; ++t)
+#pragma unroll
+        for (int i = 0; i < RPW; ++i) {
+#pragma unroll
+          for (int s = 0; s < S; ++s) hb[t][i][s] = nh[t][i][s];
+          sn[t][i] = snp[t][i];
+          cs[t][i] = csp[t][i];
+#pragma unroll
+          for (int s = 0; s < ZK; ++s) zk[t][i][s] = zkp[t][i][s];
         }
-      }
-#pragma unroll
-      for (int i = 0; i < RPW; ++i) {
-#pragma unroll
-        for (int s = 0; s < S; ++s) hb[i][s] = nh[i][s];
-        sn[i] = snp[i];
-        cs[i] = csp[i];
-#pragma unroll
-        for (int s = 0; s < ZK; ++s) zk[i][s] = zkp[i][s];
-      }
     };
     if constexpr (L >= 4) layer(std::integral_constant<int, 4>{});
     if constexpr (L >= 3) layer(std::integral_constant<int, 3>{});
@@ -255,25 +311,41 @@ __global__ __launch_bounds__(256, 1) void jet_bwd_x6r(const float* __restrict__ 
     layer(std::integral_constant<int, 1>{});
 
     // ---- first layer (K = d_in: exact fp32 VALU) ----
-    float xk[3];
-    for (int k = 0; k < 3; ++k) xk[k] = (valid && k < din) ? x[(long)p * din + k] : 0.f;
+    float xk[TS][3];
+#pragma unroll
+    for (int t = 0; t < TS; ++t) {
+      const int p = (tb + t) * 16 + c;
+      for (int k = 0; k < 3; ++k) xk[t][k] = (t < cnt && p < N && k < din) ? x[(long)p * din + k] : 0.f;
+    }
+#pragma unroll
+    for (int t = 0; t < TS; ++t)
+#pragma unroll
+      for (int i = 0; i < RPW; ++i) {
+        floatx4 zs[S];
+        zs[0] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 1; s < S; ++s) zs[s] = zk[t][i][s - 1];
+        sine_rev<S, LAP>(hb[t][i], zs, sn[t][i], cs[t][i]);  // hb = z̄_0
+      }
 #pragma unroll
     for (int i = 0; i < RPW; ++i) {
-      floatx4 zs[S];
-      zs[0] = floatx4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int s = 1; s < S; ++s) zs[s] = zk[i][s - 1];
-      sine_rev<S, LAP>(hb[i], zs, sn[i], cs[i]);  // hb = z̄_0
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float v = sum16(hb[i][0][r]);
+        float bsum = 0.f;
+#pragma unroll
+        for (int t = 0; t < TS; ++t) bsum += hb[t][i][0][r];
+        const float v = sum16(bsum);
         if (c == 0) sacc[(long)W * din + 16 * (rt0 + i) + 4 * g + r] += v;
       }
       for (int k = 0; k < din; ++k)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          float v = hb[i][0][r] * xk[k];
-          if (k < NTAN) v += hb[i][1 + k][r];
+          float v = 0.f;
+#pragma unroll
+          for (int t = 0; t < TS; ++t) {
+            v = fmaf(hb[t][i][0][r], xk[t][k], v);
+            if (k < NTAN) v += hb[t][i][1 + k][r];
+          }
           v = sum16(v);
           if (c == 0) sacc[(long)(16 * (rt0 + i) + 4 * g + r) * din + k] += v;
         }

@@ -178,8 +178,9 @@ def test_backward_path_policy(lib):
         lib.insr_jet_set_bwd_policy(1)
         assert lib.insr_jet_bwd_path(16708, 2, 1, 4, 128, LAP) == 0
         lib.insr_jet_set_bwd_policy(3)
-        assert lib.insr_jet_bwd_path(17, 2, 1, 3, 128, LAP) == 2
-        assert lib.insr_jet_bwd_path(17, 2, 1, 3, 64, LAP) != 2          # W = 128 only
+        assert lib.insr_jet_bwd_path(17, 2, 1, 4, 128, LAP) == 2
+        assert lib.insr_jet_bwd_path(17, 2, 1, 3, 128, LAP) != 2         # 4 hidden layers only
+        assert lib.insr_jet_bwd_path(17, 2, 1, 4, 64, LAP) != 2          # W = 128 only
         assert lib.insr_jet_set_bwd_policy(9) == 3                      # out of range: unchanged
     finally:
         lib.insr_jet_set_bwd_policy(old)

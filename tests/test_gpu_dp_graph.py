@@ -85,11 +85,14 @@ def _worker(rank, world, port, q):
 
 
 def _check_update(after, before, after_ref):
+    """The accumulated Adam updates of 3 phases x ITERS steps: equal to the full-batch run's
+    except at entries whose gradient sits at the fp32 noise floor (Adam's early steps are
+    ~lr sign(g), so those may flip): < 1 % of the entries off by more than 1e-3 of the largest
+    update, none by more than 2 lr per step."""
     d, d_ref = after - before, after_ref - before
-    mask = np.abs(d_ref) > 0.5 * np.abs(d_ref).max()  # entries that moved ~lr per step (no sign flips)
-    assert mask.sum() > 0.25 * mask.size
-    assert np.abs(d[mask] - d_ref[mask]).max() <= 1e-3 * np.abs(d_ref[mask]).max()
-    assert np.abs(d - d_ref).max() <= 2 * ITERS * 1e-4 * 1.01  # flips at the gradient noise floor
+    off = np.abs(d - d_ref) > 1e-3 * np.abs(d_ref).max()
+    assert off.mean() < 0.01, off.mean()
+    assert np.abs(d - d_ref).max() <= 2 * 3 * ITERS * 1e-4 * 1.01
 
 
 def test_two_rank_graph_dp_equals_eager_and_full_batch():

@@ -18,7 +18,7 @@ step() {  # name timeout cmd...
 }
 for s in ${STEPS:-tests bench prof}; do
   case $s in
-    tests) step tests ${TTO:-900} python -u -m pytest tests -q -m gpu -x --timeout 120 --timeout-method thread ${TESTSEL:+-k "$TESTSEL"} ${TESTFILES:-} ;;
+    tests) step tests ${TTO:-900} python -u -m pytest ${TESTFILES:-tests} -q -m gpu -x --timeout 120 --timeout-method thread ${TESTSEL:+-k "$TESTSEL"} ;;
     smoke) step smoke 200 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 400 python bench.py --steps ${BSTEPS:-20} --warmup ${BWARM:-3} ;;
     configs) for c in ${CONFIGS:-advect1D elasticity2Dstretch elasticity3Dbunny fluid2DtlgnM}; do

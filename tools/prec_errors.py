@@ -29,7 +29,11 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=4000)
     ap.add_argument("--nets", default=",".join(NETS))
+    ap.add_argument("--combos", default="0:0,1:1,2:2,3:3",
+                    help="forward:backward precision pairs (0 fp32, 1 bf16x6, 2 bf16x3, 3 bf16), comma separated")
     args = ap.parse_args()
+    combos = [tuple(int(v) for v in c.split(":")) for c in args.combos.split(",")]
+    names = ["f32", "bf16x6", "bf16x3", "bf16"]
     import base
     base._native.load()
     for name in args.nets.split(","):
@@ -50,8 +54,8 @@ def main():
                 p.grad = None
             (vr * R).sum().backward()
             gref = [p.grad if p.grad is not None else torch.zeros_like(p) for p in ref.parameters()]
-            for prec in (0, 1, 2, 3):
-                base._native.set_precision(prec, prec)
+            for pf, pb in combos:
+                base._native.set_precision(pf, pb)
                 net.zero_grad(set_to_none=True)
                 xg = x.cuda().requires_grad_(True)
                 y = net(xg)
@@ -61,7 +65,7 @@ def main():
                 torch.cuda.synchronize()
                 pe = [nerr(p.grad if p.grad is not None else torch.zeros_like(p), g)
                       for p, g in zip(net.parameters(), gref)]
-                print(json.dumps({"net": name, "op": op, "prec": ["f32", "bf16x6", "bf16x3", "bf16"][prec], "n": args.n,
+                print(json.dumps({"net": name, "op": op, "prec": names[pf] if pf == pb else f"{names[pf]}/{names[pb]}", "n": args.n,
                                   "field_err": nerr(v, vr), "param_grad_err_max": max(pe),
                                   "param_grad_err": [round(e, 9) for e in pe]}), flush=True)
 
