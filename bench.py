@@ -342,7 +342,7 @@ def kernel_identity(kind, mode, n, din, dout, L, W, nq=3):
         import ctypes
         thr = (ctypes.c_long * 3)()
         nat.check(lib.insr_jet_wide_launch_threads(n, din, dout, L, W, m, thr), "insr_jet_wide_launch_threads")
-        parts = [(f"insr::jet_bwd_x6r<{nq}, {S}, {lap}, {L}>", thr[0]), ("insr::reduce_dw_kernel", thr[1])]
+        parts = [(f"insr::jet_bwd_x6r<{nq}, {S}, {lap}, {L}, 1>", thr[0]), ("insr::reduce_dw_kernel", thr[1])]
         return " + ".join(f"{k}|grid={g}" for k, g in parts) + " (resident-dW backward: persistent tile loop, " \
             "then the dW / compact-row sums; time = both launches)", parts, True
     if path == 1:  # two kernels + the dW sums

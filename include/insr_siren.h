@@ -196,7 +196,8 @@ int insr_jet_bwd_is_wide(long n_points, int d_in, int width, int mode);
 int insr_jet_bwd_path(long n_points, int d_in, int d_out, int num_hidden, int width, int mode);
 
 /* Backward-path policy (A/B studies): 0 = auto (default), 1 = fused where it exists,
- * 2 = two-kernel, 3 = resident dW where it applies.  Returns the previous policy. */
+ * 2 = two-kernel, 3 = resident dW where it applies.  Returns the previous policy (a policy
+ * outside 0..3 changes nothing: -1 queries). */
 int insr_jet_set_bwd_policy(int policy);
 /* Threads of the three launches of a two-kernel backward (propagation, dW partials, dW sums),
  * as profilers report them; INSR_EINVAL when (n, shape, mode) does not take that path. */

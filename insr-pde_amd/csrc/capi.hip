@@ -35,7 +35,10 @@ static int g_bwd_policy = 0;
 
 // The resident-dW backward (jet_x6r.hpp) serves W = 128 nets of 4 hidden layers (the fluid
 // nets; compiled for that depth only) at x6 precision: value, 2-d gradient and 2-d Laplacian
-// jets, once the batch fills the CUs.
+// jets.  Auto policy (8-wave blocks; kbench r3c, profiles/r03/kbench_policies.jsonl, backward
+// into .grad incl. sums): Laplacian jets from 32,768 points (33,092: 325 vs 340 us two-kernel;
+// 65,536: 544 vs 632), value jets from 49,152 (65,536: 171-177 vs 224-234; 33,092 equal;
+// 16,708: 80 vs 64-69 fused -- below ~8 tiles per CU the 64 MB of per-CU dW partials dominate).
 bool resident_ok(int S, int NT, bool lap, int nq, int L) {
   if (NT != 8 || nq != 3 || L != 4) return false;
   return (S == 1 && !lap) || (S == 3 && !lap) || (S == 4 && lap);
@@ -44,7 +47,7 @@ bool use_resident(long n, int S, int NT, bool lap, int nq, int L) {
   if (!resident_ok(S, NT, lap, nq, L)) return false;
   if (g_bwd_policy == 3) return true;
   if (g_bwd_policy != 0) return false;
-  return n >= 4096 && L == 4;
+  return lap ? n >= 32768 : (S == 1 && n >= 49152);
 }
 
 // Tiles per tile-split block.  The largest T in {1, 2, 4} whose LDS fits a CU,
@@ -823,7 +826,7 @@ int insr_jet_wide_launch_threads(long n, int din, int dout, int L, int W, int mo
   if (c.resident(n, L)) {  // the persistent launch (256-thread blocks) + the dW / compact-row sums
     const long Ps = (long)W * din + W + (long)L * W + (long)dout * W + dout;
     const long wq = ((long)W * W / 4 + 63) / 64, rows_x = (Ps + 63) / 64;
-    threads3[0] = (long)resident_blocks(n) * 256;
+    threads3[0] = (long)resident_blocks(n) * 512;
     threads3[1] = (wq > rows_x ? wq : rows_x) * (L + 1) * 512;
     threads3[2] = 0;
     return 0;

@@ -17,13 +17,13 @@
 // compact row once; reduce_dw_kernel (jet_x6w.hpp) sums the nb partials in a fixed order.
 // Traffic per launch: saved streams once + nb (L W^2 + compact) floats written and re-read.
 //
-// Registers: the block is 4 waves (one per SIMD, 512 VGPR + AGPR per lane); wave w owns row tiles
-// 2w, 2w + 1 (32 rows) of every layer.  Its dW accumulators, L x 2 x 8 floatx4 = 256 registers at
-// L = 4, live in the AGPRs (MFMA C/D operands); the 256 VGPRs hold the propagation state.  With
-// one wave per SIMD nothing hides latency but the wave's own schedule: the saved streams of
-// layer j - 1 are loaded one layer ahead (value jets; the Laplacian state has no registers to
-// spare) and every W^T fragment one fragment ahead.
-//
+// Registers: the block is 8 waves (two per SIMD, 256 registers per lane); wave w owns row tile w
+// (16 rows) of every layer.  Its dW accumulators, L x 8 floatx4 = 128 registers at L = 4, stay
+// in registers across the whole tile loop; the other 128 hold the propagation state.  The saved
+// streams of layer j - 1 are loaded one layer ahead (value jets; the Laplacian state has no
+// registers to spare), every W^T fragment one fragment ahead, the first one under the dW MFMAs.
+// (4-wave blocks with 32 rows per wave and the dW in AGPRs -- one wave per SIMD -- measured
+// slower at every size: RPW = 2, not instantiated.)  The partials are stored in fragment order.
 // Reference semantics: loss.backward() (base/baseModel.py:73-78) through the jets of
 // base/diff_ops.py:44-82 -- the math of jet_x6.hpp / jet_x6w.hpp, another summation order.
 #pragma once
@@ -55,13 +55,13 @@ __device__ __forceinline__ floatx4 x6r_h(int s, const floatx4 (&zk)[S > 1 ? S - 
   }
 }
 
-template <int NQ, int S, bool LAP, int L>
-__global__ __launch_bounds__(256, 1) void jet_bwd_x6r(const float* __restrict__ x, int N, int din, int dout,
+template <int NQ, int S, bool LAP, int L, int RPW>
+__global__ __launch_bounds__(512 / RPW, 1) void jet_bwd_x6r(const float* __restrict__ x, int N, int din, int dout,
                                                       const float* __restrict__ prm, const float* __restrict__ act,
                                                       const float* __restrict__ gy, const float* __restrict__ gdy,
                                                       const float* __restrict__ glap, float* __restrict__ dpart,
                                                       float* __restrict__ small, long Ps, int nb) {
-  constexpr int NT = 8, W = 128, KC = 4, RPW = 2, TB = 256;
+  constexpr int NT = 8, W = 128, KC = 4, TB = 512 / RPW;  // 8 / RPW waves
   constexpr int TS = x6r_ts<S>();      // tiles per step
   constexpr int NSET = TS * S;          // 16-point sets of a step (set u = t S + s)
   constexpr int NCH = (NSET + 1) / 2;   // 32-deep K chunks of the step's dW
@@ -243,6 +243,8 @@ __global__ __launch_bounds__(256, 1) void jet_bwd_x6r(const float* __restrict__ 
                                          16 * (rt0 + i) + 4 * g, c);
           }
       __syncthreads();
+      // the propagation's first W^T fragment is issued here: its L2 latency runs under the dW MFMAs
+      FragQ<NQ> wn = wsp_frag<NQ, NT>(wsl, L, 1, j, rt0, 0, lane);
       // dW_j rows 16 rt + c (A: z̄ column reads of the point-major Z sets), columns m (B: H)
 #pragma unroll
       for (int ch = 0; ch < NCH; ++ch) {
@@ -278,7 +280,6 @@ __global__ __launch_bounds__(256, 1) void jet_bwd_x6r(const float* __restrict__ 
         for (int i = 0; i < RPW; ++i)
 #pragma unroll
           for (int s = 0; s < S; ++s) nh[t][i][s] = floatx4{0.f, 0.f, 0.f, 0.f};
-      FragQ<NQ> wn = wsp_frag<NQ, NT>(wsl, L, 1, j, rt0, 0, lane);
 #pragma unroll
       for (int f = 0; f < RPW * KC; ++f) {
         const int i = f / KC, kc = f % KC;
@@ -352,16 +353,15 @@ __global__ __launch_bounds__(256, 1) void jet_bwd_x6r(const float* __restrict__ 
     }
   }
 
-  // ---- the block's partials: dW of every hidden layer, then the compact row ----
+  // ---- the block's partials: dW of every hidden layer in fragment order (one 1 KiB wave store per
+  // accumulator; reduce_dw_kernel frag = 1 scatters the sums), then the compact row ----
 #pragma unroll
   for (int jl = 0; jl < L; ++jl) {
-    float* out = dpart + ((long)jl * nb + blockIdx.x) * W * W;
+    floatx4* out = reinterpret_cast<floatx4*>(dpart + ((long)jl * nb + blockIdx.x) * W * W);
 #pragma unroll
     for (int i = 0; i < RPW; ++i)
 #pragma unroll
-      for (int ct = 0; ct < NT; ++ct)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) out[(16 * (rt0 + i) + 4 * g + r) * W + 16 * ct + c] = dacc[jl][i][ct][r];
+      for (int ct = 0; ct < NT; ++ct) out[((rt0 + i) * NT + ct) * 64 + lane] = dacc[jl][i][ct];
   }
   __syncthreads();  // every owner lane's last compact update
   for (int i = threadIdx.x; i < Ps; i += TB) small[(long)blockIdx.x * Ps + i] = sacc[i];
@@ -387,7 +387,7 @@ inline long x6r_work_floats(long n, int din, int dout, int L) {
   return (long)L * nb * 128 * 128 + nb * small_count(din, dout, L, 128);
 }
 
-template <int NQ, int S, bool LAP, int L>
+template <int NQ, int S, bool LAP, int L, int RPW>
 int resident_bwd_t(const float* x, int N, int din, int dout, const float* prm, const float* act, const float* gy,
                    const float* gdy, const float* glap, float* work, float* grad, int accumulate, hipStream_t st) {
   constexpr int W = 128;
@@ -401,17 +401,17 @@ int resident_bwd_t(const float* x, int N, int din, int dout, const float* prm, c
   static_assert(L >= 1 && L <= 4, "resident dW: 1..4 hidden layers");
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)jet_bwd_x6r<NQ, S, LAP, L>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)jet_bwd_x6r<NQ, S, LAP, L, RPW>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)lds);
     attr = true;
   }
-  hipLaunchKernelGGL((jet_bwd_x6r<NQ, S, LAP, L>), dim3(nb), dim3(256), lds, st, x, N, din, dout, prm, act, gy, gdy,
+  hipLaunchKernelGGL((jet_bwd_x6r<NQ, S, LAP, L, RPW>), dim3(nb), dim3(512 / RPW), lds, st, x, N, din, dout, prm, act, gy, gdy,
                      glap, dpart, small, Ps, nb);
   const int grad16 = (((uintptr_t)(grad + hidden_off(din, W, 1))) & 15) == 0 ? 1 : 0;
   const int wq = (W * W / 4 + 63) / 64;
   const int rows_x = (int)((Ps + 63) / 64);
   hipLaunchKernelGGL(reduce_dw_kernel, dim3((unsigned)(wq > rows_x ? wq : rows_x), L + 1), dim3(512), 0, st, dpart, nb,
-                     din, W, grad, accumulate, grad16, L, small, nb, Ps, dout);
+                     din, W, grad, accumulate, grad16, 1, L, small, nb, Ps, dout);
   return (int)hipGetLastError();
 }
 

@@ -523,8 +523,11 @@ __global__ __launch_bounds__(256) void reduce_rows_kernel(const float* __restric
 // quads (16-B loads, 1 KiB per wave-instruction) x 8 waves over the slices, 8 independent loads
 // in flight per thread; fixed summation order (deterministic, no atomics).  Plane y == L: the
 // second level of the compact-row reduction (rs rows -> the flat gradient), same launch.
+// frag = 1: the partials are in matrix-core fragment order (jet_x6r.hpp: float4 q = (row tile x W / 16 +
+// column tile) x 64 + lane holds rows 16 rt + 4 (lane >> 4) + r of column 16 ct + (lane & 15)), so the
+// producer's stores are whole 1 KiB wave writes; the sums are scattered to row-major .grad here.
 __global__ __launch_bounds__(512) void reduce_dw_kernel(const float* __restrict__ dpart, int KS, int din, int W,
-                                                        float* __restrict__ grad, int accumulate, int grad16, int L,
+                                                        float* __restrict__ grad, int accumulate, int grad16, int frag, int L,
                                                         const float* __restrict__ rows, int rs, long Ps, int dout) {
   __shared__ floatx4 red[8][64];
   if ((int)blockIdx.y == L) {
@@ -576,6 +579,13 @@ __global__ __launch_bounds__(512) void reduce_dw_kernel(const float* __restrict_
     floatx4 t = floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int k = 0; k < 8; ++k) t += red[k][lane];
+    if (frag) {
+      const int ln = (int)(q & 63), f = (int)(q >> 6), nt = W / 16;
+      float* dst = grad + hidden_off(din, W, j) + (long)(16 * (f / nt) + 4 * (ln >> 4)) * W + 16 * (f % nt) + (ln & 15);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) dst[(long)r * W] = accumulate ? dst[(long)r * W] + t[r] : t[r];
+      return;
+    }
     float* dst = grad + hidden_off(din, W, j) + 4 * q;
     if (grad16) {  // the gradient buffer's hidden blocks are 16-B aligned (a net's own flat .grad)
       floatx4* d4 = reinterpret_cast<floatx4*>(dst);
@@ -653,7 +663,7 @@ int wide_bwd_t(const float* x, int N, int din, int dout, int L, const float* prm
     const int grad16 = (((uintptr_t)(grad + hidden_off(din, W, 1))) & 15) == 0 ? 1 : 0;  // W % 4 == 0: all layers alike
     const int wq = (W * W / 4 + 63) / 64;
     hipLaunchKernelGGL(reduce_dw_kernel, dim3((unsigned)(wq > rows_x ? wq : rows_x), L + 1), dim3(512), 0, st, dpart,
-                       KS, din, W, grad, accumulate, grad16, L, rows, rs, Ps, dout);
+                       KS, din, W, grad, accumulate, grad16, 0, L, rows, rs, Ps, dout);
     return (int)hipGetLastError();
   }
   hipLaunchKernelGGL(reduce_rows_kernel, dim3((unsigned)rows_x, rs), dim3(256), 0, st, small, tiles, Ps, rows);

@@ -160,16 +160,21 @@ def test_mixed_launch_rejects_malformed_jobs(lib):
 
 
 def test_backward_path_policy(lib):
-    """insr_jet_bwd_path answers on the host: the resident-dW kernel for the fluid nets' value /
-    Laplacian backwards at the headline batch, the fused kernel for small batches, the two-kernel
-    path at W = 256; insr_jet_set_bwd_policy forces a path for A/B studies."""
+    """insr_jet_bwd_path answers on the host: the two-kernel path for the fluid nets' Laplacian
+    backward at the headline batch and at W = 256, the fused kernel for value jets; the resident-dW
+    kernel for the fluid2DtlgnM batch (Laplacian from 32,768 points, value from 49,152) or when
+    forced (policy 3 / 4);
+    insr_jet_set_bwd_policy forces a path for A/B studies."""
     from base import _native as nat
     V, G, LAP = nat.MODE_VALUE, nat.MODE_GRAD, nat.MODE_LAP
     old = lib.insr_jet_set_bwd_policy(0)
     try:
-        assert lib.insr_jet_bwd_path(16708, 2, 1, 4, 128, LAP) == 2
-        assert lib.insr_jet_bwd_path(16708, 2, 2, 4, 128, V) == 2
+        assert lib.insr_jet_bwd_path(16708, 2, 1, 4, 128, LAP) == 1
+        assert lib.insr_jet_bwd_path(16708, 2, 2, 4, 128, V) == 0
         assert lib.insr_jet_bwd_path(1024, 2, 2, 4, 128, V) == 0
+        assert lib.insr_jet_bwd_path(65536 + 1308, 2, 1, 4, 128, LAP) == 2  # fluid2DtlgnM: resident
+        assert lib.insr_jet_bwd_path(65536 + 1308, 2, 2, 4, 128, V) == 2
+        assert lib.insr_jet_bwd_path(33092, 2, 2, 4, 128, V) == 0
         assert lib.insr_jet_bwd_path(32768, 3, 3, 5, 256, G) == 1
         assert lib.insr_jet_bwd_path(20400, 2, 2, 5, 128, G) != 2       # 5 hidden layers: not resident
         assert lib.insr_jet_bwd_path(16708, 2, 1, 4, 128, LAP | nat.jet_prec(nat.PREC_BF16)) != 2  # x6 only

@@ -5,7 +5,7 @@ point (one block) to 65,536 (16 tiles per block), ragged tails, value / gradient
 jets of the fluid nets (4 hidden layers), against the CPU oracle (base/diff_ops.py:44-82 and
 loss.backward(), base/baseModel.py:73-78).  Tolerance 1e-5 normwise per parameter tensor.
 Also: bit-for-bit determinism, gradient accumulation (accumulate=1) and that the default
-policy routes the fluid nets' 16K-point value and Laplacian backwards here."""
+policy routes only the fluid2DtlgnM-sized batches here (slower at the headline's 16K)."""
 import pytest
 import torch
 
@@ -136,11 +136,14 @@ def test_resident_accumulates(B, resident):
 
 
 def test_default_routing(B):
-    """Auto policy: the fluid nets' value and Laplacian backwards at the headline batch
-    (16,384 interior + 324 band points) run resident; small batches keep the fused kernel."""
+    """Auto policy: the fluid nets' Laplacian backward at the headline batch (16,384 interior +
+    324 band points) runs the two-kernel path, value backwards the fused kernel; the fluid2DtlgnM
+    batch (65,536 + 1,308 band points) runs resident."""
     lib = B._native.lib()
     nat = B._native
-    assert lib.insr_jet_bwd_path(16708, 2, 1, 4, 128, nat.MODE_LAP) == 2
-    assert lib.insr_jet_bwd_path(16708, 2, 2, 4, 128, nat.MODE_VALUE) == 2
+    assert lib.insr_jet_bwd_path(16708, 2, 1, 4, 128, nat.MODE_LAP) == 1
+    assert lib.insr_jet_bwd_path(16708, 2, 2, 4, 128, nat.MODE_VALUE) == 0
     assert lib.insr_jet_bwd_path(1024, 2, 2, 4, 128, nat.MODE_VALUE) == 0
+    assert lib.insr_jet_bwd_path(66844, 2, 1, 4, 128, nat.MODE_LAP) == 2    # fluid2DtlgnM batch
+    assert lib.insr_jet_bwd_path(66844, 2, 2, 4, 128, nat.MODE_VALUE) == 2
     assert lib.insr_jet_bwd_path(20400, 2, 2, 5, 128, nat.MODE_GRAD) != 2  # 5 hidden layers: not resident

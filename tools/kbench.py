@@ -54,6 +54,8 @@ def main():
     ap.add_argument("--modes", default="value,grad,lap")
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--variants", default=",".join(VARIANTS))
+    ap.add_argument("--policies", default="0", help="backward-path policies (insr_jet_set_bwd_policy) to time")
+    ap.add_argument("--bwd-only", action="store_true", help="time only the backward into .grad")
     ap.add_argument("--lib", default=None, help="alternative build of libinsr_hip.so (flag studies)")
     args = ap.parse_args()
     import base
@@ -86,7 +88,8 @@ def main():
                 act = torch.empty(lib.insr_jet_act_bytes(n, din, L, W, mode) // 4, device="cuda")
                 g = torch.zeros(P, device="cuda")
                 st = nat.stream_of(x.device)
-                for variant in args.variants.split(","):
+                for variant, pol in [(v, int(p)) for v in args.variants.split(",") for p in args.policies.split(",")]:
+                    lib.insr_jet_set_bwd_policy(pol)
                     tiles, prec = VARIANTS[variant]
                     nat.set_split_tiles(tiles[0], tiles[1], 256)
                     nat.set_precision(*prec)
@@ -122,11 +125,12 @@ def main():
 
                     tf = time_it(fwd, args.reps)
                     fwd()
-                    tb = time_it(bwd, args.reps)
-                    tr = time_it(red, args.reps)
+                    tb = 1e9 if args.bwd_only else time_it(bwd, args.reps)
+                    tr = 1e9 if args.bwd_only else time_it(red, args.reps)
                     tg = time_it(bwdg, args.reps)
                     macs = P_macs(din, dout, L, W)
-                    rec = {"net": name, "mode": mname, "n": n, "variant": variant, "T": [tf_, tb_], "nb": nb,
+                    rec = {"net": name, "mode": mname, "n": n, "variant": variant, "policy": pol,
+                           "path": lib.insr_jet_bwd_path(n, din, dout, L, W, mode), "T": [tf_, tb_], "nb": nb,
                            "fwd_us": round(tf, 2),
                            "bwd_us": round(tb, 2), "reduce_us": round(tr, 2), "bwd_grad_us": round(tg, 2),
                            "wide": wide, "bwd_grad_tflops": round(n * S * 4 * macs / tg / 1e6, 2),
