@@ -55,7 +55,8 @@ bool use_resident(long n, int S, int NT, bool lap, int nq, int L) {
 // want many short blocks, large ones fewer blocks that share W fetches, barriers
 // and partial rows).  Overrides only through the C ABI (insr_jet_set_split_tiles: force T,
 // 0 = auto; min blocks) -- no environment knobs in the product library.
-static int g_tiles[3] = {0, 0, 256};  // forced fwd T, forced bwd T, min blocks
+constexpr int kMinBlocksDefault = 256;
+static int g_tiles[3] = {0, 0, kMinBlocksDefault};  // forced fwd T, forced bwd T, min blocks
 
 static void tiles_init() {}
 
@@ -226,6 +227,18 @@ LaunchShape launch_shape(int bwd, int nq, int NT, int S, bool lap, long n) {
   LaunchShape sh{split_tiles(bwd, NT, S, n, lap, nq), 0};
   tiles_init();
   if (nq == 0 || NT > 8 || lap || g_tiles[bwd ? 1 : 0] > 0) return sh;  // exact fp32 / forced T: plain
+  if (bwd && S == 1 && NT == 8 && g_tiles[2] == kMinBlocksDefault) {
+    // x6 value backward at W = 128 (unless an A/B study set its own minimum block count): every block writes one full partial-gradient row (P floats)
+    // that reduce_partials re-reads, so below ~5 tiles per CU the block count, not the CU fill,
+    // sets the time.  About half as many blocks as CUs wins (kbench r3d, fluid_vel, backward +
+    // reduction): 4,178 points 131 x T = 2 35.4 us vs 262 x T = 1 58.5; 8,354 points 131 x T = 4
+    // 45.6 vs 262 x T = 2 66.4; 16,708 points 209 x 5 (balanced) 63.1 vs 262 x T = 4 86.8.
+    const long tiles = (n + 15) / 16, half = (cu_count() + 1) / 2, lim = half + half / 20;
+    if (tiles <= lim) return LaunchShape{1, 0};
+    if (tiles <= 2 * lim) return LaunchShape{2, 0};
+    if (tiles <= 4 * lim) return LaunchShape{4, 0};
+    if (tiles <= 5L * cu_count()) return LaunchShape{5, (int)((tiles + 4) / 5)};
+  }
   // backward: value jets only (the 3-tile gradient backward spills: 280 B of scratch per lane)
   const int T1 = sh.T == 4 && S == 1 ? 5 : (!bwd && sh.T == 2 && (S == 2 || S == 3) ? 3 : 0);
   if (!T1) return sh;

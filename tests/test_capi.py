@@ -159,6 +159,18 @@ def test_mixed_launch_rejects_malformed_jobs(lib):
     assert lib.insr_siren_jet_fwd_mixed(None, None, None, 1, 2, 2, 4, 128, 0, None) == -1
 
 
+def test_value_backward_launch_shape(lib):
+    """The x6 value backward at W = 128 runs about half as many blocks as CUs (each block's
+    partial row is re-read by the reduction; capi.hip launch_shape, kbench r3d): 4,178 points
+    -> 131 blocks of 2 tiles, 8,354 -> 131 of 4, 16,708 -> 209 balanced blocks of <= 5
+    (256 CUs: the host answer without a GPU)."""
+    V = 0
+    assert (lib.insr_jet_split_tiles(4178, 2, 128, V, 1), lib.insr_jet_partial_blocks(4178, 2, 128, V)) == (2, 131)
+    assert (lib.insr_jet_split_tiles(8354, 2, 128, V, 1), lib.insr_jet_partial_blocks(8354, 2, 128, V)) == (4, 131)
+    assert (lib.insr_jet_split_tiles(16708, 2, 128, V, 1), lib.insr_jet_partial_blocks(16708, 2, 128, V)) == (5, 209)
+    assert lib.insr_jet_partial_blocks(1000, 2, 128, V) == 63   # 63 tiles: one per block
+
+
 def test_backward_path_policy(lib):
     """insr_jet_bwd_path answers on the host: the two-kernel path for the fluid nets' Laplacian
     backward at the headline batch and at W = 256, the fused kernel for value jets; the resident-dW

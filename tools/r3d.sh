@@ -16,4 +16,6 @@ run kbT 300 python tools/kbench.py --nets fluid_vel --modes value --sizes 4178,8
 run bench 300 python bench.py --steps 20 --warmup 3 --no-cpu-baseline
 run benchM 300 python bench.py --config fluid2DtlgnM --steps 20 --warmup 3 --no-cpu-baseline
 run benchMmixed 300 python bench.py --config fluid2DtlgnM --precision mixed --steps 20 --warmup 3 --no-cpu-baseline
+run stampsV16 120 python tools/diag_stamps.py --net fluid_vel --mode value --n 16708 --prec 1
+run stampsV8 120 python tools/diag_stamps.py --net fluid_vel --mode value --n 8354 --prec 1
 echo done >> $O/status.log
