@@ -24,6 +24,7 @@ What differs is storage and execution:
     diff ops (base/diff_ops.py) can dispatch derivative jets.
 """
 import math
+import weakref
 
 import numpy as np
 import torch
@@ -97,6 +98,10 @@ def _parse_precision(precision):
     if len(parts) != 2 or any(p not in PRECISIONS for p in parts):
         raise ValueError(f"precision {precision!r}: one of {sorted(PRECISIONS)}, 'fwd/bwd' of those, 'mixed' or None")
     return PRECISIONS[parts[0]], PRECISIONS[parts[1]]
+
+
+# flat storage address -> the MLP that owns it (load_state_dict's one-copy snapshot)
+_FLAT_OWNERS = weakref.WeakValueDictionary()
 
 
 class MLP(nn.Module):
@@ -234,8 +239,43 @@ class MLP(nn.Module):
                     gv.copy_(p.grad)
                 p.grad = gv
         self._flat = flat
+        self._store = store
         self._flat_grad = gflat
         self._wsplit_stamp = None
+        _FLAT_OWNERS[flat.data_ptr()] = self
+
+    # ---- snapshots: prev = net.state_dict() ----------------------------------------
+    def _snapshot_source(self, state_dict):
+        """The MLP whose live parameters `state_dict` holds (net.state_dict() of a packed net of
+        this geometry with current weight planes), else None."""
+        keys = list(state_dict.keys()) if hasattr(state_dict, "keys") else None
+        own = [k for k, _ in self.named_parameters()]
+        if keys != own or self._flat is None or not all(torch.is_tensor(v) for v in state_dict.values()):
+            return None
+        src = _FLAT_OWNERS.get(state_dict[own[0]].data_ptr())
+        geo = ("in_features", "out_features", "num_hidden_layers", "hidden_features", "kernel_width")
+        if (src is None or src is self or type(src) is not type(self)
+                or any(getattr(src, a) != getattr(self, a) for a in geo)
+                or src._flat is None or src._flat.device != self._flat.device or src._flat.dtype != self._flat.dtype
+                or not src._is_packed() or src._wsplit_stamp != src._param_versions()):
+            return None
+        if not all(src._is_view_of(state_dict[k], src._flat, e) for k, e in zip(own, src._layout())):
+            return None
+        return src
+
+    def load_state_dict(self, state_dict, strict=True, assign=False):
+        """torch's load_state_dict; when `state_dict` is another packed net's live state_dict()
+        (the timestep snapshot prev.load_state_dict(net.state_dict()), fluid/model.py:64,69,
+        advection/model.py:64) the parameters AND their pre-split weight planes are copied as
+        ONE device copy of the flat storage (instead of a copy per tensor + a plane rewrite)."""
+        src = None if assign else self._snapshot_source(state_dict)
+        if src is None:
+            return super().load_state_dict(state_dict, strict=strict, assign=assign)
+        self.ensure_packed()
+        with torch.no_grad():
+            self._store.copy_(src._store)
+        self._wsplit_stamp = self._param_versions()
+        return nn.modules.module._IncompatibleKeys([], [])
 
     def _apply(self, fn, *args, **kwargs):
         out = super()._apply(fn, *args, **kwargs)

@@ -27,7 +27,7 @@ def _twin(B, net):
     """A fresh network with net's parameters (its planes built from scratch)."""
     t = B.MLP(net.in_features, net.out_features, net.num_hidden_layers, net.hidden_features,
               nonlinearity="sine").cuda()
-    t.load_state_dict(net.state_dict())
+    t.load_state_dict({k: v.clone() for k, v in net.state_dict().items()})  # clones: planes from scratch
     return t
 
 
@@ -123,3 +123,29 @@ def test_wsplit_planes_are_the_exact_three_term_split(B):
                         idx = [32 * kc + 8 * g + jj for jj in range(8)]
                         want = Wj[16 * rt + c, idx] if o == 0 else Wj[idx, 16 * rt + c]
                         assert torch.allclose(tot, want.double(), rtol=2.0 ** -23, atol=0), (o, j, rt, kc, lane)
+
+
+def test_snapshot_copies_flat_storage_once(B):
+    """prev.load_state_dict(net.state_dict()) -- the per-timestep snapshot of the reference
+    (fluid/model.py:64,69) -- copies the parameters and the current planes as ONE flat copy; the
+    result equals a net whose planes were built from scratch, bit for bit.  With net's planes
+    stale (a torch in-place write and no jet since) it takes the per-tensor path + a rewrite."""
+    torch.manual_seed(3)
+    net = B.MLP(2, 2, 4, 128, nonlinearity="sine").cuda()
+    prev = B.MLP(2, 2, 4, 128, nonlinearity="sine").cuda()
+    opt = B.FusedAdam([{"params": net.parameters(), "module": net, "lr": 1e-3}])
+    x = torch.rand(2000, 2, device="cuda") * 2 - 1
+    for _ in range(2):
+        opt.zero_grad()
+        (net(x) ** 2).mean().backward()
+        opt.step()
+    assert prev._snapshot_source(net.state_dict()) is net
+    prev.load_state_dict(net.state_dict())
+    assert torch.equal(prev._store, _twin(B, net)._store)
+    assert torch.equal(prev(x), net(x))
+    with torch.no_grad():
+        net.net[2].weight.mul_(0.5)  # planes of net now stale
+    assert prev._snapshot_source(net.state_dict()) is None
+    prev.load_state_dict(net.state_dict())
+    assert torch.equal(prev._store, _twin(B, net)._store)
+    assert torch.equal(prev(x), net(x))
