@@ -81,8 +81,9 @@ long insr_siren_param_count(int d_in, int d_out, int num_hidden, int width);
 
 /* Pre-split weight planes (split-bf16 kernels).  Every hidden weight W_j is stored split in
  * three bf16 terms (jet_x6.hpp) in the matrix-core fragment order of the forward (W_j rows)
- * and of the backward (W_j^T rows): 3 L W^2 floats in all, at insr_siren_wsplit_offset()
- * floats (param_count rounded up to 16 B) after the start of the params buffer.
+ * and of the backward (W_j^T rows), then 2^8 W_j split in two fp16 terms in the forward order
+ * (INSR_PREC_F16X3): 4 L W^2 floats in all, at insr_siren_wsplit_offset() floats (param_count
+ * rounded up to 16 B) after the start of the params buffer.
  * insr_siren_wsplit() writes them from the parameters in place (one launch); the kernels then
  * read fragments instead of re-splitting W in every block.  Replaces nothing in the
  * reference (its fp32 addmm reads W directly, torch/nn/modules/linear.py). */
@@ -233,6 +234,13 @@ void insr_jet_get_split_tiles(int* fwd_tiles, int* bwd_tiles, int* min_blocks);
  *   INSR_PREC_BF16X3  two bf16 terms per operand, three products (dropped terms
  *                     <= 2^-16 |a||b|): 5.3x the fp32 matrix rate.
  *   INSR_PREC_BF16    plain bf16 operands, one product, fp32 accumulation: 16x.
+ *   INSR_PREC_F16X3   FORWARD ONLY: every operand scaled by a power of two (weights 2^8,
+ *                     Laplacian stream 2^-4) and split in two fp16 terms (11 + 11
+ *                     significant bits), three v_mfma_f32_16x16x32_f16 products per K chunk
+ *                     (dropped term <= 2^-22 |a||b|): fp32-level accuracy at 5.3x the fp32
+ *                     matrix rate.  A backward asked for at this precision runs BF16X6.
+ *                     Range: |W| < 255, |tangent streams| < 65504, |Laplacian stream| < 2^20
+ *                     (beyond them the outputs turn inf/NaN -- never silently wrong).
  * The first (K = d_in) and output (M = d_out) layers and every sine stay fp32.
  * Env: INSR_JET_PREC_FWD, INSR_JET_PREC_BWD.  The saved-activation and partial
  * layouts do not depend on it: a forward of one precision pairs with a backward of
@@ -242,6 +250,7 @@ void insr_jet_get_split_tiles(int* fwd_tiles, int* bwd_tiles, int* min_blocks);
 #define INSR_PREC_BF16X6 1
 #define INSR_PREC_BF16X3 2
 #define INSR_PREC_BF16   3
+#define INSR_PREC_F16X3  4
 void insr_jet_set_precision(int fwd, int bwd);
 void insr_jet_get_precision(int* fwd, int* bwd);
 

@@ -16,8 +16,9 @@ LIB_PATH = os.environ.get("INSR_HIP_LIB", os.path.join(os.path.dirname(_HERE), "
 MODE_VALUE, MODE_GRAD, MODE_LAP = 0, 1, 2
 MODE_MASK, MODE_PREC_SHIFT = 0xF, 4
 MODE_WSPLIT = 1 << 8  # the params buffer carries up-to-date pre-split weight planes
-PREC_F32, PREC_BF16X6, PREC_BF16X3, PREC_BF16 = 0, 1, 2, 3
-PRECISIONS = {"fp32": PREC_F32, "bf16x6": PREC_BF16X6, "bf16x3": PREC_BF16X3, "bf16": PREC_BF16}
+PREC_F32, PREC_BF16X6, PREC_BF16X3, PREC_BF16, PREC_F16X3 = 0, 1, 2, 3, 4
+PRECISIONS = {"fp32": PREC_F32, "bf16x6": PREC_BF16X6, "bf16x3": PREC_BF16X3, "bf16": PREC_BF16,
+              "f16x3": PREC_F16X3}  # f16x3: forward only (its backward runs bf16x6)
 
 
 def jet_prec(p):

@@ -162,7 +162,7 @@ class MLP(nn.Module):
         return (self.param_count + 3) & ~3
 
     def wsplit_floats(self):
-        return 3 * self.num_hidden_layers * self.kernel_width ** 2
+        return 4 * self.num_hidden_layers * self.kernel_width ** 2  # bf16 x 3 (both orientations) + fp16 x 2
 
     def _param_versions(self):
         return (self._flat.data_ptr(), self._flat._version) + tuple(p._version for p in self.parameters())

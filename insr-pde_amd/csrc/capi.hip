@@ -78,21 +78,23 @@ static void prec_init() {
   }
 }
 
-static bool prec_ok(int p) { return p >= INSR_PREC_F32 && p <= INSR_PREC_BF16; }
+static bool prec_ok(int p) { return p >= INSR_PREC_F32 && p <= INSR_PREC_F16X3; }
 
 // precision of a call (direction bwd): the mode's backward override (bwd), else its
 // override, else the process default
 int call_prec(int mode, int bwd) {
   prec_init();
   const int pb = (mode >> INSR_MODE_BPREC_SHIFT) & 0xF;
-  if (bwd && pb) return pb - 1;
   const int po = (mode >> INSR_MODE_PREC_SHIFT) & 0xF;
-  return po ? po - 1 : g_prec[bwd ? 1 : 0];
+  const int p = (bwd && pb) ? pb - 1 : (po ? po - 1 : g_prec[bwd ? 1 : 0]);
+  // f16x3 is a forward precision: its backward runs the fp32-level split-bf16 kernels
+  return (bwd && p == INSR_PREC_F16X3) ? INSR_PREC_BF16X6 : p;
 }
 
 // bf16 terms per operand of a precision (0: the exact-fp32 tile-split kernels)
 int nq_of(int prec) {
-  return prec == INSR_PREC_BF16X6 ? 3 : prec == INSR_PREC_BF16X3 ? 2 : prec == INSR_PREC_BF16 ? 1 : 0;
+  return prec == INSR_PREC_F16X3 ? 4 : prec == INSR_PREC_BF16X6 ? 3 : prec == INSR_PREC_BF16X3 ? 2
+                                                                     : prec == INSR_PREC_BF16 ? 1 : 0;
 }
 
 // Backward through the two-kernel path (jet_x6w.hpp: propagation kernel + split-K dW GEMM)
@@ -130,6 +132,7 @@ static int cu_count() {
 static int fwd_q(int nq, int NT, int S, bool lap, int T, const float* x, int N, int din, int dout, int L,
                  const float* prm, float* y, float* dy, float* lp, float* act, int nbal, hipStream_t st) {
   switch (nq) {
+    case 4: return dispatch_fwd_q<4>(NT, S, lap, T, x, N, din, dout, L, prm, y, dy, lp, act, nbal, st);
     case 3: return dispatch_fwd_q<3>(NT, S, lap, T, x, N, din, dout, L, prm, y, dy, lp, act, nbal, st);
     case 2: return dispatch_fwd_q<2>(NT, S, lap, T, x, N, din, dout, L, prm, y, dy, lp, act, nbal, st);
     case 1: return dispatch_fwd_q<1>(NT, S, lap, T, x, N, din, dout, L, prm, y, dy, lp, act, nbal, st);
@@ -150,7 +153,7 @@ static int bwd_q(int nq, int NT, int S, bool lap, int T, const float* x, int N, 
 // resident blocks per CU of a tile-split kernel instantiation (launchers answer N < 0)
 static int occupancy(int bwd, int nq, int NT, int S, bool lap, int T) {
   static std::map<int, int> cache;
-  const int key = (((((bwd * 4 + nq) * 32 + NT) * 8 + S) * 2 + (lap ? 1 : 0)) * 8) + T;
+  const int key = (((((bwd * 8 + nq) * 32 + NT) * 8 + S) * 2 + (lap ? 1 : 0)) * 8) + T;
   auto it = cache.find(key);
   if (it != cache.end()) return it->second;
   const int r = bwd ? bwd_q(nq, NT, S, lap, T, nullptr, -1, 0, 0, 0, nullptr, nullptr, nullptr, nullptr, nullptr,
@@ -167,7 +170,8 @@ int split_tiles(int bwd, int NT, int S, long n, bool lap, int nq) {
   // LDS per tile: fp32 planes [S][16][W+8] (+ backward h planes [S][16][W]); split-bf16
   // forward: NQ bf16 planes [S][NQ][16][W+8]; backward: one stream group of bf16 Z + H planes
   // (the kernel picks the group size that fits, jet_x6.hpp x6_bwd_sg)
-  const size_t plane = x6 && !bwd ? (size_t)S * nq * 16 * (16 * NT + 8) * 2
+  const int np = nq == 4 ? 2 : nq;  // LDS planes per value (f16x3: two fp16 terms)
+  const size_t plane = x6 && !bwd ? (size_t)S * np * 16 * (16 * NT + 8) * 2
                        : x6       ? (size_t)(nq * 16 * (16 * NT + 8) + 32 + nq * 16 * 16 * NT) * 2
                                   : (size_t)S * 16 * ((16 * NT + 8) + (bwd ? 16 * NT : 0)) * sizeof(float);
   // width 256: fp32 kernels one tile (register budget of 8 waves x 2 row tiles); the x6
@@ -451,6 +455,14 @@ __device__ __forceinline__ void adam_wsplit(float* base, const int (&sh)[4], lon
 #pragma unroll
     for (int q = 0; q < 3; ++q) pl[o * ov + ((fr + q) * 64 + 16 * g + c) * 8 + jj] = t[q];
   }
+  // the fp16 forward planes (INSR_PREC_F16X3): 2^8 w in two fp16 terms, orientation 0
+  unsigned short* ph = reinterpret_cast<unsigned short*>(base + wsplit_f16_offset(din, dout, L, W));
+  const float ws = w * kF16WScale;
+  const _Float16 hh = (_Float16)ws, hl = (_Float16)(ws - (float)hh);
+  const int rt = n >> 4, c = n & 15, kc = m >> 5, g = (m & 31) >> 3, jj = m & 7;
+  const long fr = (((long)(j - 1) * NT + rt) * KC + kc) * 2;
+  ph[(fr * 64 + 16 * g + c) * 8 + jj] = __builtin_bit_cast(unsigned short, hh);
+  ph[((fr + 1) * 64 + 16 * g + c) * 8 + jj] = __builtin_bit_cast(unsigned short, hl);
 }
 
 // One launch over up to INSR_ADAM_MAX_TENSORS flat buffers.  The step t used is
@@ -558,7 +570,7 @@ long insr_siren_wsplit_offset(int din, int dout, int L, int W) {
 }
 long insr_siren_wsplit_floats(int L, int W) {
   if (L < 0 || nt_for(W) < 0) return INSR_EINVAL;
-  return 3L * L * W * W;
+  return wsplit_total_floats(L, W);
 }
 int insr_siren_wsplit(float* params, int din, int dout, int L, int W, void* stream) {
   if (!params || !shape_ok(din, dout, L, W, 0)) return INSR_EINVAL;
@@ -582,7 +594,7 @@ static const float* with_planes(const float* params, int din, int dout, int L, i
   *rc = 0;
   if ((mode & INSR_MODE_WSPLIT) || L < 1) return params;
   const long pc = insr_siren_param_count(din, dout, L, W);
-  const size_t bytes = (size_t)(wsplit_offset(din, dout, L, W) + 3L * L * W * W) * sizeof(float);
+  const size_t bytes = (size_t)(wsplit_offset(din, dout, L, W) + wsplit_total_floats(L, W)) * sizeof(float);
   int dev = 0;
   (void)hipGetDevice(&dev);
   std::lock_guard<std::mutex> lk(g_scratch_mu);
@@ -697,6 +709,7 @@ int insr_siren_jet_fwd_multi(const InsrJetJob* jobs, int njobs, int din, int dou
     }
     hipStream_t st = (hipStream_t)stream;
     switch (c.nqf) {
+      case 4: return dispatch_fwd_multi_q<4>(NT, S, false, T, pk, small, nbal, m, din, dout, L, st);
       case 3: return dispatch_fwd_multi_q<3>(NT, S, false, T, pk, small, nbal, m, din, dout, L, st);
       case 2: return dispatch_fwd_multi_q<2>(NT, S, false, T, pk, small, nbal, m, din, dout, L, st);
       default: return dispatch_fwd_multi_q<1>(NT, S, false, T, pk, small, nbal, m, din, dout, L, st);
@@ -777,6 +790,7 @@ int insr_siren_jet_fwd_mixed(const InsrJetJob* jobs, const int* modes, const flo
         ++q;
       }
     switch (c.nqf) {
+      case 4: return dispatch_fwd_mixed_q<4>(c.NT, din, pk, md, sc, m, dout, L, st);
       case 3: return dispatch_fwd_mixed_q<3>(c.NT, din, pk, md, sc, m, dout, L, st);
       case 2: return dispatch_fwd_mixed_q<2>(c.NT, din, pk, md, sc, m, dout, L, st);
       default: return dispatch_fwd_mixed_q<1>(c.NT, din, pk, md, sc, m, dout, L, st);

@@ -67,6 +67,13 @@ __host__ __device__ inline long wsplit_offset(int din, int dout, int L, int W) {
   return (out_off(din, W, L) + (long)dout * W + dout + 3) & ~3L;
 }
 __host__ __device__ inline long wsplit_orient_vecs(int L, int W) { return (long)L * W * W * 3 / 8; }
+// ... followed by the fp16 planes of the forward orientation (INSR_PREC_F16X3): 2^8 W_j in two
+// fp16 terms, [layer][rt][kc][term][lane] 16 B each -- L W^2 floats; 4 L W^2 floats of planes in all
+constexpr float kF16WScale = 256.0f;  // weights' power-of-two scale in the fp16 planes
+__host__ __device__ inline long wsplit_f16_offset(int din, int dout, int L, int W) {
+  return wsplit_offset(din, dout, L, W) + 3L * L * W * W;
+}
+__host__ __device__ inline long wsplit_total_floats(int L, int W) { return 4L * L * W * W; }
 
 // wave-tile base of layer `layer` in the saved-activation buffer
 __device__ __forceinline__ float* act_base(float* act, int layer, int ntiles, int tile, int S, int NT) {
@@ -312,7 +319,8 @@ int dispatch_fwd_split(int NT, int S, bool LAP, int T, const float* x, int N, in
 int dispatch_bwd_split(int NT, int S, bool LAP, int T, const float* x, int N, int din, int dout, int L,
                        const float* prm, const float* act, const float* gy, const float* gdy, const float* glap,
                        float* part, long P, hipStream_t st);
-// split-bf16 kernels, per precision NQ (bf16 terms per operand: 3 = x6, 2 = x3, 1 = bf16)
+// split-bf16 kernels, per precision NQ (bf16 terms per operand: 3 = x6, 2 = x3, 1 = bf16; 4 = the
+// fp16 two-term forward f16x3)
 template <int NQ>
 int dispatch_fwd_q(int NT, int S, bool LAP, int T, const float* x, int N, int din, int dout, int L,
                    const float* prm, float* y, float* dy, float* lap, float* act, int nbal, hipStream_t st);

@@ -59,17 +59,39 @@ __device__ __forceinline__ void split3(float a, float b, unsigned& h, unsigned& 
 //   NQ = 2  "x3"  a = a_h + a_m (16 significant bits), products a_h b_m + a_m b_h + a_h b_h
 //                 (dropped terms <= 2^-16 |a||b|): ~1e-5 relative per product
 //   NQ = 1  "bf16" one product a_h b_h: bf16 operands, fp32 accumulation
+//   NQ = 4  "f16x3" (forward only): a (scaled by a power of two) = a_h + a_l in FP16 terms
+//                 (11 + 11 significant bits), products a_h b_l + a_l b_h + a_h b_h on
+//                 v_mfma_f32_16x16x32_f16 (the bf16 rate), dropped a_l b_l <= 2^-22 |a||b|:
+//                 fp32-level accuracy with half the x6 products.  fp16's range needs the
+//                 scales: weights x 2^8 (kF16WScale, the planes), the Laplacian stream x 2^-4.
 // The geometry, layouts and numerics contract are otherwise identical.
 // ---------------------------------------------------------------------------
 template <int NQ>
+constexpr int np_of() { return NQ == 4 ? 2 : NQ; }  // LDS / fragment planes of a precision
+
+template <int NQ>
 struct FragQ {
-  u32x4 q[NQ];  // q[0] = h, q[1] = m, q[2] = l
+  u32x4 q[np_of<NQ>()];  // q[0] = h, q[1] = m, q[2] = l
 };
+
+typedef _Float16 f16x2v __attribute__((ext_vector_type(2)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+// (a, b) -> packed fp16 pair, round to nearest even; a in the low half
+__device__ __forceinline__ unsigned pk_f16(float a, float b) {
+  const f16x2v v = {(_Float16)a, (_Float16)b};
+  return __builtin_bit_cast(unsigned, v);
+}
 using Frag3 = FragQ<3>;
 
 // split of the pair (a, b) into NQ packed bf16 terms
 template <int NQ>
-__device__ __forceinline__ void splitq(float a, float b, unsigned (&o)[NQ]) {
+__device__ __forceinline__ void splitq(float a, float b, unsigned (&o)[np_of<NQ>()]) {
+  if constexpr (NQ == 4) {  // fp16 hi + lo (the caller applied the power-of-two scale)
+    o[0] = pk_f16(a, b);
+    const f16x2v h = __builtin_bit_cast(f16x2v, o[0]);
+    o[1] = pk_f16(a - (float)h[0], b - (float)h[1]);
+    return;
+  }
   o[0] = pk_bf16(a, b);
   if constexpr (NQ > 1) {
     float ra = a - bf_lo(o[0]), rb = b - bf_hi(o[0]);
@@ -85,14 +107,14 @@ __device__ __forceinline__ void splitq(float a, float b, unsigned (&o)[NQ]) {
 // 8 fp32 (k = j, j = 0..7: v0[0..3], v1[0..3]) -> one A/B fragment in NQ planes
 template <int NQ>
 __device__ __forceinline__ FragQ<NQ> split_frag(const floatx4& v0, const floatx4& v1) {
-  unsigned t[4][NQ];
+  unsigned t[4][np_of<NQ>()];
   splitq<NQ>(v0[0], v0[1], t[0]);
   splitq<NQ>(v0[2], v0[3], t[1]);
   splitq<NQ>(v1[0], v1[1], t[2]);
   splitq<NQ>(v1[2], v1[3], t[3]);
   FragQ<NQ> f;
 #pragma unroll
-  for (int q = 0; q < NQ; ++q) f.q[q] = u32x4{t[0][q], t[1][q], t[2][q], t[3][q]};
+  for (int q = 0; q < np_of<NQ>(); ++q) f.q[q] = u32x4{t[0][q], t[1][q], t[2][q], t[3][q]};
   return f;
 }
 
@@ -101,9 +123,18 @@ __device__ __forceinline__ floatx4 mfma_bf(const u32x4& a, const u32x4& b, float
                                                  0, 0, 0);
 }
 
+__device__ __forceinline__ floatx4 mfma_h(const u32x4& a, const u32x4& b, floatx4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0, 0, 0);
+}
+
 // c += A B over one 32-deep K chunk (small terms first)
 template <int NQ>
 __device__ __forceinline__ floatx4 mfma_q(const FragQ<NQ>& a, const FragQ<NQ>& b, floatx4 c) {
+  if constexpr (NQ == 4) {
+    c = mfma_h(a.q[0], b.q[1], c);
+    c = mfma_h(a.q[1], b.q[0], c);
+    return mfma_h(a.q[0], b.q[0], c);
+  }
   if constexpr (NQ == 3) {
     c = mfma_bf(a.q[1], b.q[1], c);
     c = mfma_bf(a.q[0], b.q[2], c);
@@ -121,18 +152,18 @@ template <int NQ, int PLANE>
 __device__ __forceinline__ FragQ<NQ> lds_frag(const unsigned short* p) {
   FragQ<NQ> f;
 #pragma unroll
-  for (int q = 0; q < NQ; ++q) f.q[q] = *reinterpret_cast<const u32x4*>(p + q * PLANE);
+  for (int q = 0; q < np_of<NQ>(); ++q) f.q[q] = *reinterpret_cast<const u32x4*>(p + q * PLANE);
   return f;
 }
 
 // 4 fp32 -> 4 consecutive bf16 of each of NQ planes (one b64 store per plane)
 template <int NQ, int PLANE>
 __device__ __forceinline__ void lds_put4(unsigned short* p, float a0, float a1, float a2, float a3) {
-  unsigned u0[NQ], u1[NQ];
+  unsigned u0[np_of<NQ>()], u1[np_of<NQ>()];
   splitq<NQ>(a0, a1, u0);
   splitq<NQ>(a2, a3, u1);
 #pragma unroll
-  for (int q = 0; q < NQ; ++q) *reinterpret_cast<u32x2*>(p + q * PLANE) = u32x2{u0[q], u1[q]};
+  for (int q = 0; q < np_of<NQ>(); ++q) *reinterpret_cast<u32x2*>(p + q * PLANE) = u32x2{u0[q], u1[q]};
 }
 
 template <int NT>
@@ -149,7 +180,7 @@ struct X6Geo {
 template <int NQ, int NT, int S, int T>
 constexpr size_t fwd_x6_lds_bytes() {
   using G = X6Geo<NT>;
-  const size_t planes = (size_t)T * S * NQ * G::PLANE * 2;
+  const size_t planes = (size_t)T * S * np_of<NQ>() * G::PLANE * 2;
   const size_t red = (size_t)G::WV * T * S * 3 * 16 * sizeof(float);  // output-layer combine
   return planes > red ? planes : red;
 }
@@ -164,11 +195,30 @@ template <int NQ, int NT>
 __device__ __forceinline__ FragQ<NQ> wsp_frag(const u32x4* __restrict__ wsp, int L, int o, int j, int rt, int kc,
                                               int lane) {
   constexpr int W = 16 * NT, KC = NT / 2;
+  if constexpr (NQ == 4) {  // the fp16 forward planes (o = 0 only), after both bf16 orientations
+    const u32x4* p = wsp + 2 * wsplit_orient_vecs(L, W) + ((((long)(j - 1) * NT + rt) * KC + kc) * 2) * 64 + lane;
+    FragQ<NQ> f;
+    f.q[0] = p[0];
+    f.q[1] = p[64];
+    return f;
+  }
   const u32x4* p = wsp + o * wsplit_orient_vecs(L, W) + ((((long)(j - 1) * NT + rt) * KC + kc) * 3) * 64 + lane;
   FragQ<NQ> f;
 #pragma unroll
   for (int q = 0; q < NQ; ++q) f.q[q] = p[q * 64];
   return f;
+}
+
+// f16x3 (NQ = 4) stream scales: the Laplacian stream (|ddh| ~ w^2 |t|^2, thousands) enters the
+// fp16 products x 2^-4, the value (sin) and tangent streams unscaled; an output stream of the
+// products is unscaled by 2^-8 (the weights' scale) x the input stream's inverse scale
+template <bool LAP, int S>
+__device__ __forceinline__ constexpr float f16_stream_scale(int s) {
+  return (LAP && s == S - 1) ? 0.0625f : 1.f;
+}
+template <bool LAP, int S>
+__device__ __forceinline__ constexpr float f16_unscale(int s) {
+  return (LAP && s == S - 1) ? 16.f / kF16WScale : 1.f / kF16WScale;
 }
 
 // Balanced tiles per block: with nbal > 0 the tiles of a batch are split over nbal blocks as
@@ -248,7 +298,8 @@ __device__ __forceinline__ void fwd_x6_block(const float* __restrict__ x, int N,
         FragQ<NQ> wf[KC];
 #pragma unroll
         for (int kc = 0; kc < KC; ++kc) wf[kc] = wsp_frag<NQ, NT>(wsp, L, 0, j, rt, kc, lane);
-        const floatx4 bias = *reinterpret_cast<const floatx4*>(bj + 16 * rt + 4 * g);
+        floatx4 bias = *reinterpret_cast<const floatx4*>(bj + 16 * rt + 4 * g);
+        if constexpr (NQ == 4) bias *= kF16WScale;  // the fp16 products carry the weights' 2^8
 #pragma unroll
         for (int t = 0; t < T; ++t) {
           a[t][i][0] = bias;
@@ -262,10 +313,16 @@ __device__ __forceinline__ void fwd_x6_block(const float* __restrict__ x, int N,
             if (t >= cnt) break;  // unused slots of a balanced block
 #pragma unroll
             for (int s = 0; s < S; ++s) {
-              const unsigned short* pb = lds + (t * S + s) * NQ * PLANE + c * LDB + 32 * kc + 8 * g;
+              const unsigned short* pb = lds + (t * S + s) * np_of<NQ>() * PLANE + c * LDB + 32 * kc + 8 * g;
               a[t][i][s] = mfma_q<NQ>(wf[kc], lds_frag<NQ, PLANE>(pb), a[t][i][s]);
             }
           }
+        }
+        if constexpr (NQ == 4) {  // undo the operand scales (powers of two: exact)
+#pragma unroll
+          for (int t = 0; t < T; ++t)
+#pragma unroll
+            for (int s = 0; s < S; ++s) a[t][i][s] *= f16_unscale<LAP, S>(s);
         }
       }
       __syncthreads();  // every wave has read layer j-1
@@ -291,8 +348,9 @@ __device__ __forceinline__ void fwd_x6_block(const float* __restrict__ x, int N,
         for (int i = 0; i < RPW; ++i)
 #pragma unroll
           for (int s = 0; s < S; ++s) {
-            unsigned short* pw = lds + (t * S + s) * NQ * PLANE + c * LDB + 16 * (rt0 + i) + 4 * g;
-            lds_put4<NQ, PLANE>(pw, a[t][i][s][0], a[t][i][s][1], a[t][i][s][2], a[t][i][s][3]);
+            unsigned short* pw = lds + (t * S + s) * np_of<NQ>() * PLANE + c * LDB + 16 * (rt0 + i) + 4 * g;
+            const float sc = NQ == 4 ? f16_stream_scale<LAP, S>(s) : 1.f;
+            lds_put4<NQ, PLANE>(pw, sc * a[t][i][s][0], sc * a[t][i][s][1], sc * a[t][i][s][2], sc * a[t][i][s][3]);
           }
       __syncthreads();
     }

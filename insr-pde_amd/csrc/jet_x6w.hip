@@ -10,7 +10,7 @@ long wide_work_floats(long n, int din, int dout, int L, int W, int S) {
 }
 int wsplit_launch(const float* prm, int din, int dout, int L, int W, float* planes, hipStream_t st) {
   if (L < 1) return 0;
-  const long threads = 2L * L * (W / 16) * (W / 32) * 64;
+  const long threads = 3L * L * (W / 16) * (W / 32) * 64;  // two bf16 orientations + the fp16 one
   const dim3 grid((unsigned)((threads + 255) / 256));
   u32x4* out = reinterpret_cast<u32x4*>(planes);
   switch (W) {

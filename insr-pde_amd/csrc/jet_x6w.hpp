@@ -39,7 +39,9 @@ __host__ __device__ inline long small_count(int din, int dout, int L, int W) {
 // (orientation o, layer j - 1, fragment (rt, kc), lane (g, c)): the 8 weights
 //   o = 0: W_j[16 rt + c][32 kc + 8 g + 0..7]   (forward A operand, contiguous)
 //   o = 1: W_j[32 kc + 8 g + 0..7][16 rt + c]   (backward A operand = W_j^T rows)
-// split in three bf16 terms (split_frag<3>); kernels of NQ < 3 read the first NQ terms
+// split in three bf16 terms (split_frag<3>); kernels of NQ < 3 read the first NQ terms;
+//   o = 2: the o = 0 weights times 2^8 in two fp16 terms (split_frag<4>: INSR_PREC_F16X3),
+//          after the two bf16 orientations
 // ---------------------------------------------------------------------------------------
 template <int NT>
 __global__ __launch_bounds__(256) void wsplit_kernel(const float* __restrict__ prm, int din, int L,
@@ -48,13 +50,13 @@ __global__ __launch_bounds__(256) void wsplit_kernel(const float* __restrict__ p
   const long gid = (long)blockIdx.x * 256 + threadIdx.x;
   const int lane = (int)(gid & 63), g = lane >> 4, c = lane & 15;
   const long fa = gid >> 6;  // (o, layer, frag)
-  if (fa >= 2L * L * NF) return;
+  if (fa >= 3L * L * NF) return;
   const int o = (int)(fa / ((long)L * NF));
   const long f = fa % ((long)L * NF);
   const int j = 1 + (int)(f / NF), rt = (int)((f % NF) / KC), kc = (int)(f % KC);
   const float* Wj = prm + hidden_off(din, W, j);
   floatx4 v0, v1;
-  if (o == 0) {
+  if (o != 1) {
     v0 = *reinterpret_cast<const floatx4*>(Wj + (16 * rt + c) * W + 32 * kc + 8 * g);
     v1 = *reinterpret_cast<const floatx4*>(Wj + (16 * rt + c) * W + 32 * kc + 8 * g + 4);
   } else {
@@ -63,6 +65,14 @@ __global__ __launch_bounds__(256) void wsplit_kernel(const float* __restrict__ p
       v0[jj] = Wj[(32 * kc + 8 * g + jj) * W + 16 * rt + c];
       v1[jj] = Wj[(32 * kc + 8 * g + 4 + jj) * W + 16 * rt + c];
     }
+  }
+  if (o == 2) {
+    const FragQ<4> h = split_frag<4>(v0 * kF16WScale, v1 * kF16WScale);
+    u32x4* oh = out + 6L * L * NF * 64;  // after both bf16 orientations (3 L W^2 floats)
+    const long fh = f;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) oh[(fh * 2 + k) * 64 + lane] = h.q[k];
+    return;
   }
   const FragQ<3> q = split_frag<3>(v0, v1);
 #pragma unroll

@@ -4,6 +4,7 @@ the CPU oracle.  The fp32 parity configs run at the default 'bf16x6' (test_gpu_p
 tolerance (max |hip - oracle| / max |oracle|, per tensor) it is documented with in DESIGN.md:
 
     bf16x6  6 bf16 products per fp32 product (default)   1e-5   (measured <= 5e-6)
+    f16x3   forward: 2^k-scaled operands in two fp16 terms, 3 products; backward bf16x6   1e-5
     bf16x3  3 products (hi*hi + hi*lo + lo*hi)             5e-5   (measured <= 3.3e-5)
     bf16    1 product, fp32 accumulation                   2.5e-2 (measured <= 1.6e-2)
     mixed   bf16x3 forwards / bf16 backwards              1e-2   (measured: fields <= 2.1e-5,
@@ -23,7 +24,7 @@ from oracle import siren_oracle as O
 
 pytestmark = pytest.mark.gpu
 
-TOLS = {"bf16x6": 1e-5, "bf16x3": 5e-5, "bf16": 2.5e-2, "mixed": 1e-2}
+TOLS = {"bf16x6": 1e-5, "f16x3": 1e-5, "bf16x3": 5e-5, "bf16": 2.5e-2, "mixed": 1e-2}
 
 
 def nerr(a, b):
@@ -86,7 +87,7 @@ def test_precision_jet_and_param_grads(base, precision, name, op):
     check_grads(ref, net, tol)
 
 
-@pytest.mark.parametrize("precision", ["bf16", "bf16x3", "mixed"])
+@pytest.mark.parametrize("precision", ["bf16", "bf16x3", "mixed", "f16x3"])
 def test_fluid2dtlgnM_reduced_precision_65536(base, precision):
     """The fluid2DtlgnM bench line's networks at their precision (bench.py --config
     fluid2DtlgnM --precision ...): the pressure Laplacian jet (two-kernel backward at 65,536

@@ -125,6 +125,52 @@ def test_wsplit_planes_are_the_exact_three_term_split(B):
                         assert torch.allclose(tot, want.double(), rtol=2.0 ** -23, atol=0), (o, j, rt, kc, lane)
 
 
+def test_wsplit_fp16_planes_are_the_scaled_two_term_split(B):
+    """The fp16 forward planes (INSR_PREC_F16X3, after both bf16 orientations) hold 2^8 w as
+    fp16 terms h + l == 2^8 w to 2^-22 relative, in the forward (W_j rows) fragment order --
+    written by insr_siren_wsplit and, after an optimiser step, by the Adam launch."""
+    torch.manual_seed(4)
+    net = B.MLP(2, 2, 2, 64, nonlinearity="sine").cuda()
+    opt = B.FusedAdam([{"params": net.parameters(), "module": net, "lr": 1e-2}])
+    x = torch.rand(500, 2, device="cuda") * 2 - 1
+    W, L, NT, KC = 64, 2, 4, 2
+    for step in range(2):
+        if step:
+            opt.zero_grad()
+            (net(x) ** 2).mean().backward()
+            opt.step()  # the planes now come from adam_wsplit
+        else:
+            net.refresh_wsplit()
+        torch.cuda.synchronize()
+        store = net.flat_params()._base
+        h16 = store[net.wsplit_offset() + 3 * L * W * W:].view(torch.float16).cpu().double()
+        for j in (1, 2):
+            Wj = net.net[2 * j].weight.detach().cpu().double() * 256.0
+            for rt in range(NT):
+                for kc in range(KC):
+                    fr = ((j - 1) * NT + rt) * KC + kc
+                    for lane in (0, 17, 63):
+                        g, c = lane >> 4, lane & 15
+                        hi = h16[((fr * 2) * 64 + lane) * 8:((fr * 2) * 64 + lane) * 8 + 8]
+                        lo = h16[((fr * 2 + 1) * 64 + lane) * 8:((fr * 2 + 1) * 64 + lane) * 8 + 8]
+                        want = Wj[16 * rt + c, [32 * kc + 8 * g + jj for jj in range(8)]]
+                        assert torch.allclose(hi + lo, want, rtol=2.0 ** -21, atol=2.0 ** -24), (step, j, rt, kc, lane)
+
+
+def test_f16x3_forward_matches_x6_to_fp32_level(B):
+    """The f16x3 forward (MLP(precision='f16x3')) against the default x6 forward of the same
+    weights: value, gradient and Laplacian jets agree to 1e-5 normwise."""
+    torch.manual_seed(5)
+    a = B.MLP(2, 1, 4, 128, nonlinearity="sine").cuda()
+    b = B.MLP(2, 1, 4, 128, nonlinearity="sine", precision="f16x3").cuda()
+    b.load_state_dict({k: v.clone() for k, v in a.state_dict().items()})
+    x = torch.rand(3000, 2, device="cuda") * 2 - 1
+    for net_out in (lambda n: n(x), lambda n: B.gradient(n(x.requires_grad_(True)), x),
+                    lambda n: B.laplace(n(x.requires_grad_(True)), x)):
+        u, v = net_out(a).detach(), net_out(b).detach()
+        assert float((u - v).abs().max() / u.abs().max()) < 1e-5
+
+
 def test_snapshot_copies_flat_storage_once(B):
     """prev.load_state_dict(net.state_dict()) -- the per-timestep snapshot of the reference
     (fluid/model.py:64,69) -- copies the parameters and the current planes as ONE flat copy; the

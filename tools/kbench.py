@@ -27,6 +27,7 @@ VARIANTS = {  # label: ((fwd, bwd) forced tiles, (fwd, bwd) precision)
     "x6w": ((0, 0), (1, 1)),  # x6 with the two-kernel backward from width 128
     "x3": ((0, 0), (2, 2)),   # 3 bf16 products per fp32 product
     "bf": ((0, 0), (3, 3)),   # plain bf16 operands
+    "h3": ((0, 0), (4, 1)),   # fp16 two-term forward (f16x3), x6 backward
 }
 MODES = {"value": 0, "grad": 1, "lap": 2}
 

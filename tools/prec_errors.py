@@ -33,7 +33,7 @@ def main():
                     help="forward:backward precision pairs (0 fp32, 1 bf16x6, 2 bf16x3, 3 bf16), comma separated")
     args = ap.parse_args()
     combos = [tuple(int(v) for v in c.split(":")) for c in args.combos.split(",")]
-    names = ["f32", "bf16x6", "bf16x3", "bf16"]
+    names = ["f32", "bf16x6", "bf16x3", "bf16", "f16x3"]
     import base
     base._native.load()
     for name in args.nets.split(","):
