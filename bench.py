@@ -272,6 +272,19 @@ def macs_per_point(din, dout, L, W):
     return din * W + L * W * W + W * dout
 
 
+def jet_precision_names(precision):
+    """The matrix-core precisions the jets actually run (forward / backward): 'fp32' is the
+    fp32-level default pair (f16x3 forwards, bf16x6 backwards, include/insr_siren.h)."""
+    from base import _native as nat
+    if precision != "fp32":
+        return {"mixed": "bf16x3/bf16"}.get(precision, precision)
+    import ctypes
+    f, b = ctypes.c_int(), ctypes.c_int()
+    nat.lib().insr_jet_get_precision(ctypes.byref(f), ctypes.byref(b))
+    names = {v: k for k, v in nat.PRECISIONS.items()}
+    return f"{names[f.value]}/{names[b.value]}"
+
+
 def roofline(loops, n_local, precision="fp32"):
     """Eager re-run of one step with HIP events around every jet launch (on its launch stream)."""
     from base import _jet
@@ -585,6 +598,7 @@ def main():
                    "points_per_phase_iter": n_all, "phases": nph, "global_batch": n_all,
                    "seq_len": None, "parallelism": f"dp{world}", "graph": not args.no_graph,
                    "precision": args.precision, "api": args.api, "sync_every": cfg.insr_sync_every,
+                   "jet_precision": jet_precision_names(args.precision),
                    "bwd_policy": args.bwd_policy, "shard_of": args.shard_of,
                    "timestep_order": f"{nts} timesteps x ({'/'.join(str(k) for k in ks)}) iterations per phase, "
                                      "phases in step() order with the prev-net snapshots"},

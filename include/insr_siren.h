@@ -230,7 +230,7 @@ void insr_jet_get_split_tiles(int* fwd_tiles, int* bwd_tiles, int* min_blocks);
  *   INSR_PREC_BF16X6  every fp32 operand split in three bf16 terms, six
  *                     v_mfma_f32_16x16x32_bf16 products per K chunk, fp32 accumulation:
  *                     fp32-level accuracy (dropped terms <= 2^-26 |a||b|) at 2.67x
- *                     the fp32 matrix throughput.  The default.
+ *                     the fp32 matrix throughput.  The default backward.
  *   INSR_PREC_BF16X3  two bf16 terms per operand, three products (dropped terms
  *                     <= 2^-16 |a||b|): 5.3x the fp32 matrix rate.
  *   INSR_PREC_BF16    plain bf16 operands, one product, fp32 accumulation: 16x.
@@ -238,7 +238,8 @@ void insr_jet_get_split_tiles(int* fwd_tiles, int* bwd_tiles, int* min_blocks);
  *                     Laplacian stream 2^-4) and split in two fp16 terms (11 + 11
  *                     significant bits), three v_mfma_f32_16x16x32_f16 products per K chunk
  *                     (dropped term <= 2^-22 |a||b|): fp32-level accuracy at 5.3x the fp32
- *                     matrix rate.  A backward asked for at this precision runs BF16X6.
+ *                     matrix rate.  The default forward.  A backward asked for at this
+ *                     precision runs BF16X6.
  *                     Range: |W| < 255, |tangent streams| < 65504, |Laplacian stream| < 2^20
  *                     (beyond them the outputs turn inf/NaN -- never silently wrong).
  * The first (K = d_in) and output (M = d_out) layers and every sine stay fp32.

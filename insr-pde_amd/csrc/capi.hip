@@ -64,16 +64,19 @@ static void tiles_init() {}
 // INSR_JET_PREC_FWD / INSR_JET_PREC_BWD; a call may override it through INSR_JET_PREC(p) in
 // its mode argument -- base.MLP(precision=...) does, per network):
 //   INSR_PREC_F32     v_mfma_f32_16x16x4_f32 (jet_split.hpp)
-//   INSR_PREC_BF16X6  split-bf16, 6 products (jet_x6.hpp, NQ = 3): fp32-level accuracy (default)
+//   INSR_PREC_BF16X6  split-bf16, 6 products (jet_x6.hpp, NQ = 3): fp32-level accuracy (default backward)
+//   INSR_PREC_F16X3   fp16 two terms, 3 products (NQ = 4): fp32-level accuracy, forward only (default forward)
 //   INSR_PREC_BF16X3  split-bf16, 3 products (NQ = 2)
 //   INSR_PREC_BF16    bf16 operands, fp32 accumulation (NQ = 1)
 static int g_prec[2] = {-1, -1};  // fwd, bwd
 
 static void prec_init() {
   if (g_prec[0] < 0) {
-    // default: split-bf16 matrix cores (same accuracy as fp32 MFMA, measured faster:
-    // tools/prec_errors.py, tools/kbench.py, profiles/r01/kbench_x6.jsonl)
-    g_prec[0] = env_or("INSR_JET_PREC_FWD", INSR_PREC_BF16X6);
+    // default: the fp16 two-term forward (f16x3: fields <= 4.2e-6, gradients <= 5.1e-6 vs the
+    // oracle like x6's 3.5e-6 / 5.1e-6, profiles/r03/prec_f16x3.jsonl; forward jets 15-30 %
+    // faster, headline 71-74 -> 78.6-78.9 M pts/s same box, profiles/r03/f16x3_ab) and the
+    // split-bf16 x6 backward (same accuracy as fp32 MFMA, measured faster: profiles/r01/kbench_x6.jsonl)
+    g_prec[0] = env_or("INSR_JET_PREC_FWD", INSR_PREC_F16X3);
     g_prec[1] = env_or("INSR_JET_PREC_BWD", INSR_PREC_BF16X6);
   }
 }

@@ -4,7 +4,9 @@ the CPU oracle.  The fp32 parity configs run at the default 'bf16x6' (test_gpu_p
 tolerance (max |hip - oracle| / max |oracle|, per tensor) it is documented with in DESIGN.md:
 
     bf16x6  6 bf16 products per fp32 product (default)   1e-5   (measured <= 5e-6)
-    f16x3   forward: 2^k-scaled operands in two fp16 terms, 3 products; backward bf16x6   1e-5
+    f16x3   forward: 2^k-scaled operands in two fp16 terms, 3 products; backward bf16x6
+            1e-5   (the default forward since round 3; measured fields <= 4.2e-6, gradients
+            <= 5.1e-6, profiles/r03/prec_f16x3.jsonl -- x6: 3.5e-6 / 5.1e-6)
     bf16x3  3 products (hi*hi + hi*lo + lo*hi)             5e-5   (measured <= 3.3e-5)
     bf16    1 product, fp32 accumulation                   2.5e-2 (measured <= 1.6e-2)
     mixed   bf16x3 forwards / bf16 backwards              1e-2   (measured: fields <= 2.1e-5,
@@ -87,26 +89,31 @@ def test_precision_jet_and_param_grads(base, precision, name, op):
     check_grads(ref, net, tol)
 
 
-@pytest.mark.parametrize("precision", ["bf16", "bf16x3", "mixed", "f16x3"])
+@pytest.mark.parametrize("precision", ["bf16", "bf16x3", "mixed", "f16x3", "bf16x6"])
 def test_fluid2dtlgnM_reduced_precision_65536(base, precision):
     """The fluid2DtlgnM bench line's networks at their precision (bench.py --config
     fluid2DtlgnM --precision ...): the pressure Laplacian jet (two-kernel backward at 65,536
-    points) and the velocity divergence, with the parameter gradients of the pressure loss."""
+    points) and the velocity divergence, with the parameter gradients of the pressure loss.
+    The oracle runs in fp64: at this size the fp32 oracle's own summation error reaches the
+    1e-5 bound on the output-layer gradient (measured: bf16x6 and f16x3 both 1.10e-5 against
+    the fp32 oracle, gpurun_out r3i), so it would test the oracle, not the kernels."""
     tol = TOLS[precision]
     ref, net = pair(base, 2, 1, 4, 128, 51, precision)
+    ref = ref.double()
     torch.manual_seed(52)
     x = torch.rand(65536, 2) * 2 - 1
     g = torch.randn(65536, 1)
-    xr = x.clone().requires_grad_(True)
+    xr = x.clone().double().requires_grad_(True)
     lr_ = O.op_laplace(ref(xr), xr)
-    ((g - lr_) ** 2).mean().backward()
+    ((g.double() - lr_) ** 2).mean().backward()
     xg = x.cuda().requires_grad_(True)
     lg = base.laplace(net(xg), xg)
     ((g.cuda() - lg) ** 2).mean().backward()
     assert nerr(lg, lr_) < tol
     check_grads(ref, net, tol)
     refv, vel = pair(base, 2, 2, 4, 128, 53, precision)
-    xr = x.clone().requires_grad_(True)
+    refv = refv.double()
+    xr = x.clone().double().requires_grad_(True)
     dr = O.op_divergence(refv(xr), xr)
     with torch.no_grad():
         dg = base.divergence(vel(xg), xg)
