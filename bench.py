@@ -80,6 +80,8 @@ def parse():
                          "points per phase iteration; elasticity: the draw at resolution / K^(1/3)); 1 GPU")
     ap.add_argument("--bwd-policy", type=int, default=0, choices=[0, 1, 2, 3],
                     help="backward path (A/B studies): 0 auto, 1 fused tile-split, 2 two-kernel, 3 resident dW")
+    ap.add_argument("--dw-f16", type=int, default=-1, choices=[-1, 0, 1],
+                    help="dW GEMM of the two-kernel backward on the fp16 matrix cores (A/B studies; -1 = library default)")
     ap.add_argument("--cpu-seconds", type=float, default=25.0, help="budget of the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
@@ -173,6 +175,7 @@ def build_model(args, world, rank):
     from pde.config import baseline_config
     base._native.load()
     base._native.lib().insr_jet_set_bwd_policy(args.bwd_policy)
+    base._native.lib().insr_jet_set_dw_precision(args.dw_f16)
     wl = WORKLOADS[args.config]
     res = wl["res"]
     cfg = baseline_config(args.config, sample_resolution=res, insr_graph=not args.no_graph,
@@ -561,22 +564,24 @@ def main():
         log(f"warmup step {i} done" + "".join(f" [{pl.tag}: capture failed {pl.capture_error}]"
                                               for pl in loops if getattr(pl, "capture_error", None)))
     # timed region: --steps iterations of every phase, as `nts` timesteps in step() order
-    # (K iterations per phase, phases in order, median of 5 timesteps); the
-    # host syncs at timestep boundaries only (no loss reads inside: sync_every = 1e9)
+    # (K iterations per phase, phases in order, median of 5 timesteps); no loss
+    # reads inside (sync_every = 1e9) and no host sync at the timestep boundaries either: the
+    # per-timestep times come from HIP events recorded there, and the host's snapshot work
+    # overlaps the device's previous timestep as it does in a run
     nts = max(1, min(5, args.steps))
     ks = [args.steps // nts + (1 if t < args.steps % nts else 0) for t in range(nts)]
-    ts_ms = []
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(nts + 1)]
     sync_all(world)
     t0 = time.perf_counter()
+    evs[0].record()
     i = w_eff
-    for k in ks:
-        a = time.perf_counter()
+    for t, k in enumerate(ks):
         run_timestep(model, wl, loops, i, k)
-        torch.cuda.synchronize()
-        ts_ms.append((time.perf_counter() - a) * 1e3)
+        evs[t + 1].record()
         i += k
     sync_all(world)
     elapsed = time.perf_counter() - t0
+    ts_ms = [evs[t].elapsed_time(evs[t + 1]) for t in range(nts)]
     t = torch.tensor([elapsed] + ts_ms, device="cuda", dtype=torch.float64)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -600,8 +605,9 @@ def main():
                    "precision": args.precision, "api": args.api, "sync_every": cfg.insr_sync_every,
                    "jet_precision": jet_precision_names(args.precision),
                    "bwd_policy": args.bwd_policy, "shard_of": args.shard_of,
+                   "dw_f16": base._native.lib().insr_jet_set_dw_precision(-1),
                    "timestep_order": f"{nts} timesteps x ({'/'.join(str(k) for k in ks)}) iterations per phase, "
-                                     "phases in step() order with the prev-net snapshots"},
+                                     "phases in step() order with the prev-net snapshots; per-timestep times from HIP events"},
         "timesteps": {"count": nts, "iters_per_phase": ks, "ms": [round(v, 3) for v in ts_ms],
                       "value_median": round(per_ts[len(per_ts) // 2], 1), "value_min": round(per_ts[0], 1),
                       "value_max": round(per_ts[-1], 1)},

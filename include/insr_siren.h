@@ -186,6 +186,35 @@ int insr_siren_jet_bwd_grad(const float* x, long n_points, int d_in, int d_out, 
                             const float* gy, const float* gdy, const float* glap, float* work,
                             float* grad, int accumulate, void* stream);
 long insr_jet_bwd_work_bytes(long n_points, int d_in, int d_out, int num_hidden, int width, int mode);
+
+/*
+ * Several backward jobs of ONE network and jet mode -- the network's forward jets of one
+ * loss.backward(), e.g. a phase's interior batch and its boundary bands evaluated by
+ * separate network calls (fluid/model.py:80,96-97: curr_u, vel_x, vel_y) -- straight into
+ * its flat gradient:  grad = (accumulate ? grad : 0) + sum_k d(loss)/d(params) of job k.
+ * Jobs the fused tile-split backward serves share ONE launch (blocks [first[k], first[k+1])
+ * run job k; a 162-point band adds its tiles to the interior's launch instead of a
+ * latency-bound launch of its own) and ONE fixed-order reduction of all their partial rows;
+ * a job another path serves at its size (two-kernel, resident) runs as its own
+ * insr_siren_jet_bwd_grad.  work: insr_jet_bwd_multi_work_bytes(...) of scratch.
+ * 1 <= n_jobs <= INSR_MAX_BWD_JOBS; jobs with n == 0 are skipped.
+ * Replaces: the per-call autograd backwards of loss.backward() (base/baseModel.py:77).
+ */
+#define INSR_MAX_BWD_JOBS 8
+typedef struct InsrBwdJob {
+  const float* x;     /* (n, d_in) points of the forward */
+  const float* act;   /* the forward's saved streams (insr_jet_act_bytes(n, ...)) */
+  const float* gy;    /* (n, d_out) or NULL */
+  const float* gdy;   /* (n, d_out, d_in) or NULL */
+  const float* glap;  /* (n, d_out) or NULL */
+  long n;
+} InsrBwdJob;
+int insr_siren_jet_bwd_grad_multi(const InsrBwdJob* jobs, int n_jobs, int d_in, int d_out, int num_hidden,
+                                  int width, int mode, const float* params, float* work, float* grad,
+                                  int accumulate, void* stream);
+/* Scratch bytes of insr_siren_jet_bwd_grad_multi for jobs of n[0..n_jobs) points. */
+long insr_jet_bwd_multi_work_bytes(const long* n, int n_jobs, int d_in, int d_out, int num_hidden, int width,
+                                   int mode);
 /* 1 if insr_siren_jet_bwd_grad takes the wide path for this batch / width / mode. */
 int insr_jet_bwd_is_wide(long n_points, int d_in, int width, int mode);
 
@@ -200,6 +229,11 @@ int insr_jet_bwd_path(long n_points, int d_in, int d_out, int num_hidden, int wi
  * 2 = two-kernel, 3 = resident dW where it applies.  Returns the previous policy (a policy
  * outside 0..3 changes nothing: -1 queries). */
 int insr_jet_set_bwd_policy(int policy);
+/* dW GEMM of the two-kernel backward at the x6 backward precision: 1 = on the fp16 matrix cores
+ * (f16x3: two fp16 terms per operand, three products; each K slice's adjoints scaled by the power
+ * of two that maps its largest |value| into [2^14, 2^15), undone exactly on its partial), 0 =
+ * bf16x6.  Returns the previous setting (-1 queries).  Process-wide. */
+int insr_jet_set_dw_precision(int f16);
 /* Threads of the three launches of a two-kernel backward (propagation, dW partials, dW sums),
  * as profilers report them; INSR_EINVAL when (n, shape, mode) does not take that path. */
 int insr_jet_wide_launch_threads(long n_points, int d_in, int d_out, int num_hidden, int width, int mode,

@@ -45,7 +45,7 @@ def _flatten_x(x, din):
 
 
 def _needs_save(mlp):
-    return torch.is_grad_enabled() and any(p.requires_grad for p in mlp.parameters())
+    return torch.is_grad_enabled() and any(p.requires_grad for p in mlp.plist())
 
 
 # Optional per-launch HIP-event timing (bench.py's roofline leg).  When enabled,
@@ -112,51 +112,155 @@ class _SirenJet(torch.autograd.Function):
     @once_differentiable
     def backward(ctx, *grads):
         mlp, mode = ctx.mlp, ctx.mode
-        none = (None,) * (4 + len(list(mlp.parameters())))
-        if not ctx.save or not any(p.requires_grad for p in mlp.parameters()):
+        none = (None,) * (4 + len(mlp.plist()))
+        if not ctx.save or not any(p.requires_grad for p in mlp.plist()):
             return none
         gy = grads[0]
         gdy = grads[1] if mode != nat.MODE_VALUE else None
         glap = grads[2] if mode == nat.MODE_LAP else None
         if gy is None and gdy is None and glap is None:
             return none
-        x2, act = ctx.x2, ctx.act
-        n, din = x2.shape
-        L, W, dout = mlp.num_hidden_layers, mlp.kernel_width, mlp.out_features
-        cmode = mlp.call_mode(mode)
-        mlp.ensure_wsplit()
-        lib = nat.lib()
-        gflat, accumulate = mlp.grad_for_backward()
         c = lambda t: None if t is None else (t if t.is_contiguous() else t.contiguous())  # noqa: E731
-        gy, gdy, glap = c(gy), c(gdy), c(glap)
-        st = nat.stream_of(x2.device)
-        cur = torch.cuda.current_stream(x2.device)
-        mlp.grad_write_begin(cur)  # order after a write of .grad made on another stream
-        if lib.insr_jet_bwd_path(n, din, dout, L, W, cmode) > 0:
-            # two-kernel path (propagation + split-K dW GEMM) or the resident-dW persistent kernel,
-            # with their fixed-order sums straight into .grad
-            work = torch.empty(max(lib.insr_jet_bwd_work_bytes(n, din, dout, L, W, cmode) // 4, 1), device=x2.device,
-                               dtype=torch.float32)
-            with _timed("bwd", mode, n, W, (din, dout, L)):
-                rc = lib.insr_siren_jet_bwd_grad(nat.ptr(x2), n, din, dout, L, W, cmode, nat.ptr(mlp.flat_params()),
-                                                 nat.ptr(act), nat.ptr(gy), nat.ptr(gdy), nat.ptr(glap), nat.ptr(work),
-                                                 nat.ptr(gflat), accumulate, st)
-            nat.check(rc, "insr_siren_jet_bwd_grad")
-            mlp.grad_write_end(cur)
-            return none
-        part = torch.empty(max(lib.insr_jet_partial_bytes(n, din, dout, L, W, cmode) // 4, 1), device=x2.device,
+        job = _BwdJob(mlp, mode, ctx.x2, ctx.act, c(gy), c(gdy), c(glap))
+        if _BwdBatch.pending is not None:  # launched with the network's other jobs at the scope's exit
+            _BwdBatch.pending.append(job)
+        else:
+            _launch_bwd(job)
+        return none
+
+
+class _BwdJob:
+    """One reverse jet: the network, its jet mode, the forward's points / saved streams, the
+    adjoints, and the stream autograd ran its backward on."""
+    __slots__ = ("mlp", "mode", "x2", "act", "gy", "gdy", "glap", "cur")
+
+    def __init__(self, mlp, mode, x2, act, gy, gdy, glap):
+        self.mlp, self.mode, self.x2, self.act = mlp, mode, x2, act
+        self.gy, self.gdy, self.glap = gy, gdy, glap
+        self.cur = torch.cuda.current_stream(x2.device)
+
+
+def _launch_bwd(job):
+    """One reverse jet into its network's flat .grad (first write of an iteration overwrites)."""
+    mlp, mode, x2, act, gy, gdy, glap = job.mlp, job.mode, job.x2, job.act, job.gy, job.gdy, job.glap
+    n, din = x2.shape
+    L, W, dout = mlp.num_hidden_layers, mlp.kernel_width, mlp.out_features
+    cmode = mlp.call_mode(mode)
+    mlp.ensure_wsplit()
+    lib = nat.lib()
+    gflat, accumulate = mlp.grad_for_backward()
+    cur = job.cur
+    st = ctypes.c_void_p(cur.cuda_stream)
+    mlp.grad_write_begin(cur)  # order after a write of .grad made on another stream
+    if lib.insr_jet_bwd_path(n, din, dout, L, W, cmode) > 0:
+        # two-kernel path (propagation + split-K dW GEMM) or the resident-dW persistent kernel,
+        # with their fixed-order sums straight into .grad
+        work = torch.empty(max(lib.insr_jet_bwd_work_bytes(n, din, dout, L, W, cmode) // 4, 1), device=x2.device,
                            dtype=torch.float32)
         with _timed("bwd", mode, n, W, (din, dout, L)):
-            rc = lib.insr_siren_jet_bwd(nat.ptr(x2), n, din, dout, L, W, cmode, nat.ptr(mlp.flat_params()),
-                                        nat.ptr(act), nat.ptr(gy), nat.ptr(gdy), nat.ptr(glap), nat.ptr(part), st)
-        nat.check(rc, "insr_siren_jet_bwd")
-        with _timed("reduce", mode, n, W, (din, dout, L)):
-            rc = lib.insr_reduce_partials_strided(nat.ptr(part), lib.insr_jet_partial_blocks(n, din, W, cmode),
-                                                  gflat.numel(), lib.insr_jet_partial_stride(din, dout, L, W),
-                                                  nat.ptr(gflat), accumulate, st)
-        nat.check(rc, "insr_reduce_partials_strided")
+            rc = lib.insr_siren_jet_bwd_grad(nat.ptr(x2), n, din, dout, L, W, cmode, nat.ptr(mlp.flat_params()),
+                                             nat.ptr(act), nat.ptr(gy), nat.ptr(gdy), nat.ptr(glap), nat.ptr(work),
+                                             nat.ptr(gflat), accumulate, st)
+        nat.check(rc, "insr_siren_jet_bwd_grad")
         mlp.grad_write_end(cur)
-        return none
+        return
+    part = torch.empty(max(lib.insr_jet_partial_bytes(n, din, dout, L, W, cmode) // 4, 1), device=x2.device,
+                       dtype=torch.float32)
+    with _timed("bwd", mode, n, W, (din, dout, L)):
+        rc = lib.insr_siren_jet_bwd(nat.ptr(x2), n, din, dout, L, W, cmode, nat.ptr(mlp.flat_params()),
+                                    nat.ptr(act), nat.ptr(gy), nat.ptr(gdy), nat.ptr(glap), nat.ptr(part), st)
+    nat.check(rc, "insr_siren_jet_bwd")
+    with _timed("reduce", mode, n, W, (din, dout, L)):
+        rc = lib.insr_reduce_partials_strided(nat.ptr(part), lib.insr_jet_partial_blocks(n, din, W, cmode),
+                                              gflat.numel(), lib.insr_jet_partial_stride(din, dout, L, W),
+                                              nat.ptr(gflat), accumulate, st)
+    nat.check(rc, "insr_reduce_partials_strided")
+    mlp.grad_write_end(cur)
+
+
+def _launch_bwd_multi(jobs):
+    """Reverse jets of ONE network, jet mode and stream (e.g. a phase's interior batch and its
+    wall bands from separate network calls, fluid/model.py:80,96-97) in one call of
+    insr_siren_jet_bwd_grad_multi: the jobs the fused tile-split kernel serves share one launch
+    and one fixed-order partial-row reduction."""
+    mlp, mode, cur = jobs[0].mlp, jobs[0].mode, jobs[0].cur
+    din = jobs[0].x2.shape[1]
+    L, W, dout = mlp.num_hidden_layers, mlp.kernel_width, mlp.out_features
+    cmode = mlp.call_mode(mode)
+    mlp.ensure_wsplit()
+    lib = nat.lib()
+    gflat, accumulate = mlp.grad_for_backward()
+    st = ctypes.c_void_p(cur.cuda_stream)
+    mlp.grad_write_begin(cur)
+    for k in range(0, len(jobs), nat.MAX_BWD_JOBS):
+        chunk = jobs[k:k + nat.MAX_BWD_JOBS]
+        arr = (nat.BwdJob * len(chunk))(*[
+            nat.BwdJob(j.x2.data_ptr(), j.act.data_ptr(), nat.ptr(j.gy), nat.ptr(j.gdy), nat.ptr(j.glap), j.x2.shape[0])
+            for j in chunk])
+        ns = (ctypes.c_long * len(chunk))(*[j.x2.shape[0] for j in chunk])
+        wb = lib.insr_jet_bwd_multi_work_bytes(ns, len(chunk), din, dout, L, W, cmode)
+        nat.check(wb if wb < 0 else 0, "insr_jet_bwd_multi_work_bytes")
+        work = torch.empty(max(wb // 4, 1), device=jobs[0].x2.device, dtype=torch.float32)
+        with _timed("bwd%d" % len(chunk), mode, sum(ns), W, (din, dout, L)):
+            rc = lib.insr_siren_jet_bwd_grad_multi(arr, len(chunk), din, dout, L, W, cmode,
+                                                   nat.ptr(mlp.flat_params()), nat.ptr(work), nat.ptr(gflat),
+                                                   accumulate, st)
+        nat.check(rc, "insr_siren_jet_bwd_grad_multi")
+        accumulate = 1
+    mlp.grad_write_end(cur)
+
+
+class _BwdBatch:
+    pending = None  # list of _BwdJob while a batched_backward scope is open
+
+
+class batched_backward:
+    """`with batched_backward(): torch.autograd.backward(...)` -- the HIP reverse jets autograd
+    asks for inside the scope are launched at its exit, grouped per (network, jet mode, stream)
+    in first-request order: a group of one job launches as usual, a larger group through
+    insr_siren_jet_bwd_grad_multi (one launch + one reduction for all of its fused-path jobs).
+    Valid because the reverse jets return no gradient to autograd (they write the networks'
+    flat .grad directly, and x gets none), so nothing inside the backward pass reads their
+    results; .grad holds them when the scope exits.  BaseModel._backward opens it around the
+    loss backward of every iteration."""
+
+    def __enter__(self):
+        self.outer = _BwdBatch.pending is None
+        if self.outer:
+            _BwdBatch.pending = []
+        return self
+
+    def __exit__(self, exc_type, *exc):
+        if not self.outer:
+            return False
+        jobs, _BwdBatch.pending = _BwdBatch.pending, None
+        if exc_type is None:
+            _flush_backward(jobs)
+        return False
+
+
+class immediate_backward:
+    """Suspends an open batched_backward scope: a backward run inside (a custom autograd node that
+    reads .grad right after its own nested backward, diff_ops._AugLaplacian) launches at once."""
+
+    def __enter__(self):
+        self.saved, _BwdBatch.pending = _BwdBatch.pending, None
+        return self
+
+    def __exit__(self, *exc):
+        _BwdBatch.pending = self.saved
+        return False
+
+
+def _flush_backward(jobs):
+    groups = {}
+    for j in jobs:
+        groups.setdefault((id(j.mlp), j.mlp.call_mode(j.mode), j.cur.cuda_stream), []).append(j)
+    for js in groups.values():
+        if len(js) == 1:
+            _launch_bwd(js[0])
+        else:
+            _launch_bwd_multi(js)
 
 
 class _Fused:
@@ -292,7 +396,7 @@ def run_jet(mlp, x, mode):
             f"no HIP kernel for SIREN(in={din}, out={mlp.out_features}, width={mlp.kernel_width}) "
             f"in {MODE_NAMES[mode]} mode")
     x2, lead = _flatten_x(x, din)
-    params = tuple(mlp.parameters())
+    params = tuple(mlp.plist())
     outs = _SirenJet.apply(x2, mode, mlp, _needs_save(mlp), *params)
     if x.dim() == 2:  # no view node: keeps y.grad_fn == our node (identity-stable, see match())
         y = outs[0]

@@ -57,9 +57,12 @@ SIGNATURES = {
     "insr_jet_partial_blocks": (_I, [_L, _I, _I, _I]),
     "insr_siren_jet_bwd_grad": (_I, [_P, _L, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _I, _P]),
     "insr_jet_bwd_work_bytes": (_L, [_L, _I, _I, _I, _I, _I]),
+    "insr_siren_jet_bwd_grad_multi": (_I, [_P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _I, _P]),
+    "insr_jet_bwd_multi_work_bytes": (_L, [_P, _I, _I, _I, _I, _I, _I]),
     "insr_jet_bwd_is_wide": (_I, [_L, _I, _I, _I]),
     "insr_jet_bwd_path": (_I, [_L, _I, _I, _I, _I, _I]),
     "insr_jet_set_bwd_policy": (_I, [_I]),
+    "insr_jet_set_dw_precision": (_I, [_I]),
     "insr_jet_set_wide_min_width": (_I, [_I]),
     "insr_comm_available": (_I, []),
     "insr_comm_id_bytes": (_L, []),
@@ -107,6 +110,14 @@ MAX_FWD_JOBS = 4  # INSR_MAX_FWD_JOBS
 class JetJob(ctypes.Structure):
     """struct InsrJetJob (include/insr_siren.h): one forward jet of insr_siren_jet_fwd_multi."""
     _fields_ = [("x", _P), ("params", _P), ("y", _P), ("dy", _P), ("lap", _P), ("act", _P), ("n", _L), ("d_out", _I)]
+
+
+MAX_BWD_JOBS = 8  # INSR_MAX_BWD_JOBS
+
+
+class BwdJob(ctypes.Structure):
+    """struct InsrBwdJob (include/insr_siren.h): one backward job of insr_siren_jet_bwd_grad_multi."""
+    _fields_ = [("x", _P), ("act", _P), ("gy", _P), ("gdy", _P), ("glap", _P), ("n", _L)]
 
 
 LOSS_GROUP_MAX = 4  # INSR_LOSS_GROUP_MAX

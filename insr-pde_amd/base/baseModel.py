@@ -26,6 +26,7 @@ from abc import ABC, abstractmethod
 
 import torch
 
+from . import _jet
 from .networks import get_network
 from .optim import DevicePlateau, FusedAdam
 
@@ -193,7 +194,10 @@ class BaseModel(ABC):
     def _backward(self, loss_dict):
         terms = [v for v in loss_dict.values() if v.requires_grad]
         if terms:
-            torch.autograd.backward(terms, grad_tensors=[self._unit_seed(v) for v in terms])
+            # the reverse jets of one network (its interior batch and boundary bands from separate
+            # calls) launch together when autograd is done with the pass (_jet.batched_backward)
+            with _jet.batched_backward():
+                torch.autograd.backward(terms, grad_tensors=[self._unit_seed(v) for v in terms])
             # join .grad writes a side-stream backward made (fluid boundary bands): the
             # caller's stream -- and a hipGraph capture -- must see them
             cur = torch.cuda.current_stream(self.device) if (torch.device(self.device).type == "cuda"

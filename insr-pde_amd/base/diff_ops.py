@@ -175,7 +175,8 @@ class _AugLaplacian(torch.autograd.Function):
         with torch.no_grad():
             aug.flat_params().copy_(ctx.snap)
         aug.zero_grad(set_to_none=True)
-        torch.autograd.backward(ctx.lap, glap.contiguous(), retain_graph=True)
+        with _jet.immediate_backward():  # aug's .grad is read right below
+            torch.autograd.backward(ctx.lap, glap.contiguous(), retain_graph=True)
         gq = [q.grad if q.grad is not None else torch.zeros_like(q) for q in aug.parameters()]
         d = gq[0].shape[1] - 1
         g0 = gq[0][:, :d] + gq[0][:, d:] * ctx.vt[None, :]

@@ -164,8 +164,27 @@ class MLP(nn.Module):
     def wsplit_floats(self):
         return 4 * self.num_hidden_layers * self.kernel_width ** 2  # bf16 x 3 (both orientations) + fp16 x 2
 
+    def plist(self):
+        """list(self.parameters()) without the module-tree walk (the checks before every jet and
+        snapshot read it): the (module, name) slots holding parameters are found once, the
+        parameters re-read from them on every call (a replaced Parameter is seen)."""
+        slots = self.__dict__.get("_insr_pslots")
+        if slots is None:
+            slots, seen = [], set()
+            for mname, m in self.named_modules():
+                for pname, q in m._parameters.items():
+                    if q is not None and id(q) not in seen:
+                        seen.add(id(q))
+                        slots.append((m, pname, f"{mname}.{pname}" if mname else pname))
+            self.__dict__["_insr_pslots"] = slots
+        return [m._parameters[n] for m, n, _ in slots]
+
+    def _param_names(self):
+        self.plist()
+        return [k for *_, k in self.__dict__["_insr_pslots"]]
+
     def _param_versions(self):
-        return (self._flat.data_ptr(), self._flat._version) + tuple(p._version for p in self.parameters())
+        return (self._flat.data_ptr(), self._flat._version) + tuple(p._version for p in self.plist())
 
     def refresh_wsplit(self, stream=None):
         """Rewrite the planes from the parameters now (one launch on `stream` / the current one)."""
@@ -204,7 +223,7 @@ class MLP(nn.Module):
         width, biases padded vectors; `corner` = the parameter's own (rows, cols)."""
         W, din, dout = self.kernel_width, self.in_features, self.out_features
         out, off = [], 0
-        for i, p in enumerate(self.parameters()):
+        for i, p in enumerate(self.plist()):
             layer = i // 2
             rows = W if layer <= self.num_hidden_layers else dout
             cols = din if layer == 0 else W
@@ -220,7 +239,7 @@ class MLP(nn.Module):
 
     def _repack(self):
         """Move every parameter into one flat (zero-padded) buffer (Parameter identity kept)."""
-        params = list(self.parameters())
+        params = self.plist()
         if not params:
             return
         dev, dt = params[0].device, params[0].dtype
@@ -249,7 +268,7 @@ class MLP(nn.Module):
         """The MLP whose live parameters `state_dict` holds (net.state_dict() of a packed net of
         this geometry with current weight planes), else None."""
         keys = list(state_dict.keys()) if hasattr(state_dict, "keys") else None
-        own = [k for k, _ in self.named_parameters()]
+        own = self._param_names()
         if keys != own or self._flat is None or not all(torch.is_tensor(v) for v in state_dict.values()):
             return None
         src = _FLAT_OWNERS.get(state_dict[own[0]].data_ptr())
@@ -259,7 +278,7 @@ class MLP(nn.Module):
                 or src._flat is None or src._flat.device != self._flat.device or src._flat.dtype != self._flat.dtype
                 or not src._is_packed() or src._wsplit_stamp != src._param_versions()):
             return None
-        if not all(src._is_view_of(state_dict[k], src._flat, e) for k, e in zip(own, src._layout())):
+        if not all(self._sig_of(state_dict[k]) == sg for k, sg in zip(own, src._view_sigs(src._flat))):
             return None
         return src
 
@@ -286,11 +305,25 @@ class MLP(nn.Module):
         v = self._view(buf, entry)
         return t.data_ptr() == v.data_ptr() and t.stride() == v.stride() and t.shape == v.shape
 
+    def _view_sigs(self, buf):
+        """(data_ptr, stride, shape) of every parameter's view into `buf` -- cached per buffer
+        (the checks run at every timestep snapshot and jet call; building the views is the cost)."""
+        key = (buf.data_ptr(), buf.numel())
+        cache = self.__dict__.get("_insr_sigs")
+        if cache is None or cache[0] != key:
+            sigs = [(v.data_ptr(), v.stride(), tuple(v.shape)) for v in (self._view(buf, e) for e in self._layout())]
+            cache = self.__dict__["_insr_sigs"] = (key, sigs)
+        return cache[1]
+
+    @staticmethod
+    def _sig_of(t):
+        return (t.data_ptr(), t.stride(), tuple(t.shape))
+
     def _is_packed(self):
-        params = list(self.parameters())
+        params = self.plist()
         if self._flat is None or not params or self._flat.numel() != self.param_count:
             return False
-        return all(self._is_view_of(p.data, self._flat, e) for p, e in zip(params, self._layout()))
+        return all(self._sig_of(p.data) == sg for p, sg in zip(params, self._view_sigs(self._flat)))
 
     def ensure_packed(self):
         if not self._is_packed():
@@ -301,7 +334,7 @@ class MLP(nn.Module):
     # backward overwrites it (no memset launch).  'live': it holds the sum of
     # the backward passes since then.
     def _attach_grad_views(self, fold_foreign):
-        params = list(self.parameters())
+        params = self.plist()
         g = self._flat_grad
         if g is None or g.device != self._flat.device or g.numel() != self._flat.numel():
             g = torch.zeros_like(self._flat)
@@ -322,7 +355,7 @@ class MLP(nn.Module):
     def mark_grad_stale(self, set_to_none=True):
         self.ensure_packed()
         if set_to_none:
-            for p in self.parameters():
+            for p in self.plist():
                 p.grad = None
         else:
             g, _ = self._attach_grad_views(fold_foreign=False)
@@ -333,7 +366,7 @@ class MLP(nn.Module):
     def grad_for_backward(self):
         """(flat grad buffer, accumulate flag) for the next HIP backward."""
         self.ensure_packed()
-        if getattr(self, '_grad_state', 'stale') == 'stale' and all(p.grad is None for p in self.parameters()):
+        if getattr(self, '_grad_state', 'stale') == 'stale' and all(p.grad is None for p in self.plist()):
             g, _ = self._attach_grad_views(fold_foreign=False)
             self._grad_state = 'live'
             return g, 0
@@ -352,7 +385,7 @@ class MLP(nn.Module):
         self.ensure_packed()
         if buf.numel() != self._flat.numel() or buf.dtype != self._flat.dtype or buf.device != self._flat.device:
             raise ValueError("bind_flat_grad: buffer does not match the flat parameters")
-        live = any(p.grad is not None for p in self.parameters())
+        live = any(p.grad is not None for p in self.plist())
         if live:
             old, _ = self._attach_grad_views(fold_foreign=True)
             buf.copy_(old)
@@ -387,12 +420,12 @@ class MLP(nn.Module):
         self.grad_write_begin(stream)
 
     def grad_touched(self):
-        return getattr(self, '_grad_state', 'stale') == 'live' or any(p.grad is not None for p in self.parameters())
+        return getattr(self, '_grad_state', 'stale') == 'live' or any(p.grad is not None for p in self.plist())
 
     def flat_grad_buffer(self):
         """Flat gradient with every parameter's .grad attached to it (None grads -> 0)."""
         self.ensure_packed()
-        if self._flat_grad is None or any(p.grad is None for p in self.parameters()):
+        if self._flat_grad is None or any(p.grad is None for p in self.plist()):
             g, _ = self._attach_grad_views(fold_foreign=True)
             self._grad_state = 'live'
             return g

@@ -3,9 +3,11 @@
 Same signatures (including `device=`) and distributions.  On the CPU the torch
 RNG is consumed exactly as the reference does, so a seeded CPU generator yields
 the reference's points bit for bit.  On a GPU device each sampler is ONE
-device-RNG draw plus at most one fused affine map (graph-capturable, 2 launches
-instead of up to 13 for a pair of boundary bands): same distribution, different
-stream order -- parity tests pass explicit sample tensors.
+insr_sample_boxes launch (the device Philox-4x32-10 stream, graph-capturable: the
+kernel advances its own stream position, so a replayed graph draws fresh points
+with no host-side generator update), instead of up to 13 launches for a pair of
+boundary bands: same distributions, another stream -- parity tests pass explicit
+sample tensors.
 """
 import torch
 
@@ -24,15 +26,33 @@ def sample_uniform(resolution, sdim=1, device="cpu", flatten=True):
 
 
 def sample_random(N, sdim=1, device="cpu"):
-    """N points uniform in [-1, 1)^sdim (base/sampling.py:14-18)."""
-    if torch.device(device).type == "cuda":
-        return torch.empty(N, sdim, device=device).uniform_(-1.0, 1.0)  # == rand*2-1, one launch
+    """N points uniform in [-1, 1)^sdim (base/sampling.py:14-18).  On the GPU: one
+    insr_sample_boxes launch (the device Philox stream, advanced by the kernel itself -- inside a
+    replayed hipGraph torch's generator would add a seed / offset fill and copy per replay); before
+    that stream exists and while a capture runs, one uniform_ draw (== rand * 2 - 1)."""
+    dev = torch.device(device)
+    if dev.type == "cuda":
+        if dev.index is None:
+            dev = torch.device("cuda", torch.cuda.current_device())
+        if N > 0 and 1 <= sdim <= 3 and (dev.index in _SAMPLER or not torch.cuda.is_current_stream_capturing()):
+            return sample_boxes([(N, (-1.0,) * sdim, (1.0,) * sdim)], sdim, device=dev)
+        return torch.empty(N, sdim, device=dev).uniform_(-1.0, 1.0)
     return torch.rand(N, sdim, device=device) * 2 - 1
 
 
 def _fused_bands(n_per, faces, key, device):
-    """One rand draw + one fused multiply-add for len(faces) bands of n_per points."""
-    k = (n_per, key, torch.device(device))
+    """len(faces) bands of n_per points on the GPU: ONE insr_sample_boxes launch (the device Philox
+    stream of sample_random_and_bands2D), rows in face order; before that stream exists and a
+    hipGraph capture is running, one rand draw + one fused multiply-add instead."""
+    dev = torch.device(device)
+    if dev.index is None:
+        dev = torch.device("cuda", torch.cuda.current_device())
+    if n_per == 0:
+        return torch.empty(0, len(faces[0]), device=dev)
+    if dev.index in _SAMPLER or not torch.cuda.is_current_stream_capturing():
+        return sample_boxes([(n_per, tuple(r[0] for r in f), tuple(r[1] for r in f)) for f in faces], len(faces[0]),
+                            device=dev)
+    k = (n_per, key, dev)
     if k not in _AFFINE:
         d = len(faces[0])
         lo = torch.tensor([[f[j][0] for j in range(d)] for f in faces], dtype=torch.float32)

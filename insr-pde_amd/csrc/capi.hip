@@ -142,14 +142,20 @@ static int fwd_q(int nq, int NT, int S, bool lap, int T, const float* x, int N, 
     default: return dispatch_fwd_split(NT, S, lap, T, x, N, din, dout, L, prm, y, dy, lp, act, st);
   }
 }
-static int bwd_q(int nq, int NT, int S, bool lap, int T, const float* x, int N, int din, int dout, int L,
-                 const float* prm, const float* act, const float* gy, const float* gdy, const float* glap, float* part,
-                 long P, int nbal, hipStream_t st) {
+// J == NULL: occupancy query; the exact-fp32 kernel takes one job per launch
+static int bwd_q(int nq, int NT, int S, bool lap, int T, const BwdJobsX6* J, int din, int dout, int L,
+                 const float* prm, float* part, long P, hipStream_t st) {
   switch (nq) {
-    case 3: return dispatch_bwd_q<3>(NT, S, lap, T, x, N, din, dout, L, prm, act, gy, gdy, glap, part, P, nbal, st);
-    case 2: return dispatch_bwd_q<2>(NT, S, lap, T, x, N, din, dout, L, prm, act, gy, gdy, glap, part, P, nbal, st);
-    case 1: return dispatch_bwd_q<1>(NT, S, lap, T, x, N, din, dout, L, prm, act, gy, gdy, glap, part, P, nbal, st);
-    default: return dispatch_bwd_split(NT, S, lap, T, x, N, din, dout, L, prm, act, gy, gdy, glap, part, P, st);
+    case 3: return dispatch_bwd_q<3>(NT, S, lap, T, J, din, dout, L, prm, part, P, st);
+    case 2: return dispatch_bwd_q<2>(NT, S, lap, T, J, din, dout, L, prm, part, P, st);
+    case 1: return dispatch_bwd_q<1>(NT, S, lap, T, J, din, dout, L, prm, part, P, st);
+    default:
+      if (!J)
+        return dispatch_bwd_split(NT, S, lap, T, nullptr, -1, 0, 0, 0, nullptr, nullptr, nullptr, nullptr, nullptr,
+                                  nullptr, 0, nullptr);
+      if (J->njobs != 1) return INSR_EINVAL;
+      return dispatch_bwd_split(NT, S, lap, T, J->x[0], J->n[0], din, dout, L, prm, J->act[0], J->gy[0], J->gdy[0],
+                                J->glap[0], part, P, st);
   }
 }
 
@@ -159,8 +165,7 @@ static int occupancy(int bwd, int nq, int NT, int S, bool lap, int T) {
   const int key = (((((bwd * 8 + nq) * 32 + NT) * 8 + S) * 2 + (lap ? 1 : 0)) * 8) + T;
   auto it = cache.find(key);
   if (it != cache.end()) return it->second;
-  const int r = bwd ? bwd_q(nq, NT, S, lap, T, nullptr, -1, 0, 0, 0, nullptr, nullptr, nullptr, nullptr, nullptr,
-                            nullptr, 0, 0, nullptr)
+  const int r = bwd ? bwd_q(nq, NT, S, lap, T, nullptr, 0, 0, 0, nullptr, nullptr, 0, nullptr)
                     : fwd_q(nq, NT, S, lap, T, nullptr, -1, 0, 0, 0, nullptr, nullptr, nullptr, nullptr, nullptr, 0,
                             nullptr);
   cache[key] = r;
@@ -832,8 +837,128 @@ int insr_siren_jet_bwd(const float* x, long n, int din, int dout, int L, int W, 
   const LaunchShape sh = launch_shape(1, nq, c.NT, c.S, c.lap, n);
   int rc = 0;
   if (nq > 0 && !(params = with_planes(params, din, dout, L, W, mode, (hipStream_t)stream, 0, &rc))) return rc;
-  return bwd_q(nq, c.NT, c.S, c.lap, sh.T, x, (int)n, din, dout, L, params, act, gy, gdy, glap, partial, P, sh.nbal,
-               (hipStream_t)stream);
+  BwdJobsX6 J{};
+  J.x[0] = x;
+  J.act[0] = act;
+  J.gy[0] = gy;
+  J.gdy[0] = gdy;
+  J.glap[0] = glap;
+  J.n[0] = (int)n;
+  J.nbal[0] = sh.nbal;
+  J.first[0] = 0;
+  J.first[1] = sh.nbal > 0 ? sh.nbal : (int)(((n + 15) / 16 + sh.T - 1) / sh.T);
+  J.njobs = 1;
+  return bwd_q(nq, c.NT, c.S, c.lap, sh.T, &J, din, dout, L, params, partial, P, (hipStream_t)stream);
+}
+
+// Plan of a multi-job backward (insr_siren_jet_bwd_grad_multi): the jobs whose own size takes the
+// fused tile-split path share one launch, T from the launch shape of their combined batch; a
+// balanced shape (T = 3 / 5) gives each job its share of the balanced block count (never fewer
+// blocks than T-tile blocks need); every other job runs alone on its own path.
+namespace {
+struct MultiPlan {
+  int nq, T, nf, ns, nb;
+  int fused[kBwdJobs], solo[kBwdJobs], blocks[kBwdJobs], nbal[kBwdJobs];
+};
+}  // namespace
+
+static int plan_multi(const long* n, int njobs, int din, int dout, int L, int W, int mode, MultiPlan& p) {
+  if (!n || njobs < 1 || njobs > kBwdJobs || !shape_ok(din, dout, L, W, mode)) return INSR_EINVAL;
+  const JetCall c(din, W, mode);
+  p = MultiPlan{};
+  p.nq = c.NT > 8 ? 0 : c.nqb;
+  long total = 0, tiles = 0;
+  for (int k = 0; k < njobs; ++k) {
+    if (n[k] < 0 || n[k] > 0x7fffffffL) return INSR_EINVAL;
+    if (n[k] == 0) continue;
+    if (p.nq > 0 && c.path(n[k], L) == 0) {
+      p.fused[p.nf++] = k;
+      total += n[k];
+      tiles += (n[k] + 15) / 16;
+    } else {
+      p.solo[p.ns++] = k;
+    }
+  }
+  if (total > 0x7fffffffL) return INSR_EINVAL;
+  if (p.nf == 0) return 0;
+  const LaunchShape sh = launch_shape(1, p.nq, c.NT, c.S, c.lap, total);
+  p.T = sh.T;
+  for (int q = 0; q < p.nf; ++q) {
+    const long tk = (n[p.fused[q]] + 15) / 16, plain = (tk + sh.T - 1) / sh.T;
+    long nbk = plain;
+    if (sh.nbal > 0) {
+      const long share = (tk * sh.nbal + tiles / 2) / tiles;
+      nbk = share > plain ? share : plain;
+    }
+    p.blocks[q] = (int)nbk;
+    p.nbal[q] = sh.nbal > 0 ? (int)nbk : 0;
+    p.nb += (int)nbk;
+  }
+  return 0;
+}
+
+long insr_jet_bwd_multi_work_bytes(const long* n, int njobs, int din, int dout, int L, int W, int mode) {
+  MultiPlan p;
+  const int rc = plan_multi(n, njobs, din, dout, L, W, mode, p);
+  if (rc) return rc;
+  long bytes = (long)p.nb * insr_jet_partial_stride(din, dout, L, W) * (long)sizeof(float);
+  for (int q = 0; q < p.ns; ++q) {
+    const long b = insr_jet_bwd_work_bytes(n[p.solo[q]], din, dout, L, W, mode);
+    if (b < 0) return b;
+    if (b > bytes) bytes = b;
+  }
+  return bytes;
+}
+
+int insr_siren_jet_bwd_grad_multi(const InsrBwdJob* jobs, int njobs, int din, int dout, int L, int W, int mode,
+                                  const float* params, float* work, float* grad, int accumulate, void* stream) {
+  if (!jobs || njobs < 1 || njobs > kBwdJobs) return INSR_EINVAL;
+  long ns[kBwdJobs];
+  for (int k = 0; k < njobs; ++k) {
+    ns[k] = jobs[k].n;
+    if (jobs[k].n > 0 && (!jobs[k].x || !jobs[k].act)) return INSR_EINVAL;
+  }
+  MultiPlan p;
+  int rc = plan_multi(ns, njobs, din, dout, L, W, mode, p);
+  if (rc) return rc;
+  if (p.nf + p.ns == 0) return 0;
+  if (!params || !work || !grad) return INSR_EINVAL;
+  hipStream_t st = (hipStream_t)stream;
+  int acc = accumulate ? 1 : 0;
+  if (p.nf > 0) {
+    const JetCall c(din, W, mode);
+    const float* prm = params;
+    if (!(prm = with_planes(params, din, dout, L, W, mode, st, 0, &rc))) return rc;
+    BwdJobsX6 J{};
+    int b = 0;
+    for (int q = 0; q < p.nf; ++q) {
+      const InsrBwdJob& jb = jobs[p.fused[q]];
+      J.x[q] = jb.x;
+      J.act[q] = jb.act;
+      J.gy[q] = jb.gy;
+      J.gdy[q] = jb.gdy;
+      J.glap[q] = jb.glap;
+      J.n[q] = (int)jb.n;
+      J.nbal[q] = p.nbal[q];
+      J.first[q] = b;
+      b += p.blocks[q];
+    }
+    J.first[p.nf] = b;
+    J.njobs = p.nf;
+    const long P = insr_jet_partial_stride(din, dout, L, W);
+    if ((rc = bwd_q(p.nq, c.NT, c.S, c.lap, p.T, &J, din, dout, L, prm, work, P, st))) return rc;
+    if ((rc = insr_reduce_partials_strided(work, p.nb, insr_siren_param_count(din, dout, L, W), P, grad, acc, stream)))
+      return rc;
+    acc = 1;
+  }
+  for (int q = 0; q < p.ns; ++q) {  // stream order: the previous job's reduction has read `work`
+    const InsrBwdJob& jb = jobs[p.solo[q]];
+    if ((rc = insr_siren_jet_bwd_grad(jb.x, jb.n, din, dout, L, W, mode, params, jb.act, jb.gy, jb.gdy, jb.glap, work,
+                                      grad, acc, stream)))
+      return rc;
+    acc = 1;
+  }
+  return 0;
 }
 
 int insr_jet_set_wide_min_width(int width) {
@@ -875,6 +1000,12 @@ int insr_jet_bwd_is_wide(long n, int din, int W, int mode) {
 int insr_jet_bwd_path(long n, int din, int dout, int L, int W, int mode) {
   if (!shape_ok(din, dout, L, W, mode) || n < 0) return INSR_EINVAL;
   return JetCall(din, W, mode).path(n, L);
+}
+
+int insr_jet_set_dw_precision(int f16) {
+  const int old = g_wide_dw_f16;
+  if (f16 == 0 || f16 == 1) g_wide_dw_f16 = f16;
+  return old;
 }
 
 int insr_jet_set_bwd_policy(int policy) {

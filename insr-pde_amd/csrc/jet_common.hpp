@@ -133,6 +133,13 @@ __device__ __forceinline__ bool wave_any_big(float amax) {
   return __any(amax > kFastArgMax);
 }
 
+// max over the wave's 64 lanes (every lane gets it)
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
 
 template <int NT, int S, bool LAP, bool FAST>
 __device__ __forceinline__ void sine_jet_impl(floatx4 (&a)[NT][S]) {
@@ -328,16 +335,34 @@ constexpr int kFwdJobs = INSR_MAX_FWD_JOBS;
 template <int NQ>
 int dispatch_fwd_multi_q(int NT, int S, bool LAP, int T, const InsrJetJob* jobs, const int* small, const int* nbal,
                          int njobs, int din, int dout, int L, hipStream_t st);
+// The jobs of one tile-split backward launch: batches of ONE network and jet mode (its weights
+// are the launch's), blocks [first[k], first[k + 1]) run job k -- nbal[k] > 0: its tiles balanced
+// over that many blocks (T = 3 / 5 shapes), else T-tile blocks.  One job = insr_siren_jet_bwd.
+constexpr int kBwdJobs = INSR_MAX_BWD_JOBS;
+struct BwdJobsX6 {
+  const float* x[kBwdJobs];
+  const float* act[kBwdJobs];
+  const float* gy[kBwdJobs];
+  const float* gdy[kBwdJobs];
+  const float* glap[kBwdJobs];
+  int n[kBwdJobs];
+  int nbal[kBwdJobs];
+  int first[kBwdJobs + 1];
+  int njobs;
+};
+// jobs == NULL: occupancy query (resident blocks per CU of the instantiation)
 template <int NQ>
-int dispatch_bwd_q(int NT, int S, bool LAP, int T, const float* x, int N, int din, int dout, int L,
-                   const float* prm, const float* act, const float* gy, const float* gdy, const float* glap,
-                   float* part, long P, int nbal, hipStream_t st);
+int dispatch_bwd_q(int NT, int S, bool LAP, int T, const BwdJobsX6* jobs, int din, int dout, int L,
+                   const float* prm, float* part, long P, hipStream_t st);
 // two-kernel backward (W = 128 / 256): propagation kernel + dW GEMM + reductions (jet_x6w.hpp)
 template <int NQ>
 int dispatch_wide_bwd_q(int NT, int S, bool LAP, const float* x, int N, int din, int dout, int L, const float* prm,
                         const float* act, const float* gy, const float* gdy, const float* glap, float* work,
                         float* grad, int accumulate, hipStream_t st);
 long wide_work_floats(long n, int din, int dout, int L, int W, int S);
+// two-kernel backward of the x6 precision: 1 = its dW GEMM on the fp16 matrix cores (f16x3 with
+// a power-of-two scale of the adjoints per K slice), 0 = bf16x6 (jet_x6w.hip; insr_jet_set_dw_precision)
+extern int g_wide_dw_f16;
 template <int NQ>
 int dispatch_fwd_mixed_q(int NT, int din, const InsrJetJob* jobs, const int* modes, const float* scalars, int njobs,
                          int dout, int L, hipStream_t st);

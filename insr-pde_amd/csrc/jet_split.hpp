@@ -241,6 +241,10 @@ __global__ __launch_bounds__(SplitGeo<NT>::THREADS) void jet_bwd_split(
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
   const int ntiles = ((N + 63) / 64) * 4;
   const int tile0 = blockIdx.x * T;
+  // saved streams of slot t: a slot past the batch's last tile re-reads tile0 (the forward, whose
+  // T may be smaller, never wrote it; its adjoints are zero, so it contributes nothing)
+  const int tiles_n = (N + 15) / 16;
+  auto tl = [&](int t) { return tile0 + t < tiles_n ? tile0 + t : tile0; };
   const int rt0 = wave * RPW;
   float* mypart = part + (long)blockIdx.x * P;
 
@@ -273,7 +277,7 @@ __global__ __launch_bounds__(SplitGeo<NT>::THREADS) void jet_bwd_split(
     float amax = 0.f;
 #pragma unroll
     for (int t = 0; t < T; ++t) {
-      const float* base = act_base(act, layer, ntiles, tile0 + t, S, NT);
+      const float* base = act_base(act, layer, ntiles, tl(t), S, NT);
 #pragma unroll
       for (int i = 0; i < RPW; ++i) {
         z[t][i] = *reinterpret_cast<const floatx4*>(base + ((rt0 + i) * 64 + lane) * 4);
@@ -318,7 +322,7 @@ __global__ __launch_bounds__(SplitGeo<NT>::THREADS) void jet_bwd_split(
       floatx4 acc4 = floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int t = 0; t < T; ++t) {
-        const float* baseL = act_base(act, L, ntiles, tile0 + t, S, NT);
+        const float* baseL = act_base(act, L, ntiles, tl(t), S, NT);
 #pragma unroll
         for (int s = 0; s < S; ++s) {
           const floatx4 hs = h_stream<NT, S, LAP>(baseL, s, rt, lane, sn[t][i], cs[t][i]);
@@ -356,7 +360,7 @@ __global__ __launch_bounds__(SplitGeo<NT>::THREADS) void jet_bwd_split(
   if constexpr (kKeepZ) {
 #pragma unroll
     for (int t = 0; t < T; ++t) {
-      const float* baseL = act_base(act, L, ntiles, tile0 + t, S, NT);
+      const float* baseL = act_base(act, L, ntiles, tl(t), S, NT);
 #pragma unroll
       for (int i = 0; i < RPW; ++i)
 #pragma unroll
@@ -377,7 +381,7 @@ __global__ __launch_bounds__(SplitGeo<NT>::THREADS) void jet_bwd_split(
     }
 #pragma unroll
     for (int t = 0; t < T; ++t) {
-      const float* basej = act_base(act, j, ntiles, tile0 + t, S, NT);
+      const float* basej = act_base(act, j, ntiles, tl(t), S, NT);
 #pragma unroll
       for (int i = 0; i < RPW; ++i) {
         floatx4 zs[S];
@@ -429,7 +433,7 @@ __global__ __launch_bounds__(SplitGeo<NT>::THREADS) void jet_bwd_split(
     INSR_STAMP(L - j, 3);
 #pragma unroll
     for (int t = 0; t < T; ++t) {
-      const float* basep = act_base(act, j - 1, ntiles, tile0 + t, S, NT);
+      const float* basep = act_base(act, j - 1, ntiles, tl(t), S, NT);
 #pragma unroll
       for (int i = 0; i < RPW; ++i)
 #pragma unroll

@@ -773,10 +773,9 @@ constexpr size_t bwd_x6_lds_bytes() {
 }
 
 template <int NQ, int NT, int S, bool LAP, int T>
-__global__ __launch_bounds__(X6Geo<NT>::THREADS) void jet_bwd_x6(
-    const float* __restrict__ x, int N, int din, int dout, int L, const float* __restrict__ prm,
-    const float* __restrict__ act, const float* __restrict__ gy, const float* __restrict__ gdy,
-    const float* __restrict__ glap, float* __restrict__ part, long P, int nbal) {
+__global__ __launch_bounds__(X6Geo<NT>::THREADS) void jet_bwd_x6(const BwdJobsX6 J, int din, int dout, int L,
+                                                                  const float* __restrict__ prm,
+                                                                  float* __restrict__ part, long P) {
   using G = X6Geo<NT>;
   using BG = X6BwdGeo<NQ, NT>;
   constexpr int W = G::W, RPW = G::RPW, KC = G::KC;
@@ -792,13 +791,26 @@ __global__ __launch_bounds__(X6Geo<NT>::THREADS) void jet_bwd_x6(
   unsigned short* Z = reinterpret_cast<unsigned short*>(lds_f);
   unsigned short* H = Z + NSET * ZSET;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
+  // this block's job (a batch of the launch's network) and its tiles within that batch
+  const int b = blockIdx.x;
+  int jk = 0;
+#pragma unroll
+  for (int q = 1; q < kBwdJobs; ++q) jk += (q < J.njobs && b >= J.first[q]) ? 1 : 0;
+  const float* __restrict__ x = J.x[jk];
+  const float* __restrict__ act = J.act[jk];
+  const float* __restrict__ gy = J.gy[jk];
+  const float* __restrict__ gdy = J.gdy[jk];
+  const float* __restrict__ glap = J.glap[jk];
+  const int N = J.n[jk];
   const int ntiles = ((N + 63) / 64) * 4;
   int tile0, cnt_rt;
-  block_tiles(blockIdx.x, N, T, nbal, tile0, cnt_rt);
+  block_tiles(b - J.first[jk], N, T, J.nbal[jk], tile0, cnt_rt);
   const int cnt = (T == 3 || T == 5) ? cnt_rt : T;  // run-time only for the balanced shapes
-  // tile of slot t for memory reads: an unused slot of a balanced block re-reads the block's
-  // first tile (valid memory) -- its adjoints and x are zero, so it contributes nothing
-  auto tt = [&](int t) { return tile0 + (t < cnt ? t : 0); };
+  // tile of slot t for memory reads: a slot past the batch's last tile (a balanced block's unused
+  // slot, or the tail of a T-tile block) re-reads the block's first tile -- saved streams the
+  // forward wrote (its own T may have been smaller: tiles past ceil(n / 16) hold no data) -- and
+  // its adjoints and x are zero, so it contributes nothing
+  auto tt = [&](int t) { return tile0 + (t < cnt_rt ? t : 0); };
   const int rt0 = wave * RPW;
   float* mypart = part + (long)blockIdx.x * P;
 
@@ -1112,27 +1124,28 @@ __global__ __launch_bounds__(X6Geo<NT>::THREADS) void jet_bwd_x6(
 }
 
 template <int NQ, int NT, int S, bool LAP, int T>
-int launch_bwd_x6_t(const float* x, int N, int din, int dout, int L, const float* prm, const float* act,
-                    const float* gy, const float* gdy, const float* glap, float* part, long P, int nbal,
+int launch_bwd_x6_t(const BwdJobsX6* J, int din, int dout, int L, const float* prm, float* part, long P,
                     hipStream_t st) {
   constexpr size_t lds = bwd_x6_lds_bytes<NQ, NT, S, T>();
   if constexpr (lds > kLdsMax || NT > 8) {
     return INSR_EINVAL;
   } else {
-    const int nb = ((N + 15) / 16 + T - 1) / T;
     static bool attr_set = false;
     if (!attr_set) {
       (void)hipFuncSetAttribute((const void*)jet_bwd_x6<NQ, NT, S, LAP, T>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       attr_set = true;
     }
-    if (N < 0) {  // occupancy query (split_tiles): resident blocks per CU
+    if (!J) {  // occupancy query (split_tiles): resident blocks per CU
       int occ = 0;
       (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)jet_bwd_x6<NQ, NT, S, LAP, T>, X6Geo<NT>::THREADS, lds);
       return occ;
     }
-    hipLaunchKernelGGL((jet_bwd_x6<NQ, NT, S, LAP, T>), dim3(nbal > 0 ? nbal : nb), dim3(X6Geo<NT>::THREADS), lds, st,
-                       x, N, din, dout, L, prm, act, gy, gdy, glap, part, P, nbal);
+    if (J->njobs < 1 || J->njobs > kBwdJobs) return INSR_EINVAL;
+    const int nb = J->first[J->njobs];
+    if (nb <= 0) return 0;
+    hipLaunchKernelGGL((jet_bwd_x6<NQ, NT, S, LAP, T>), dim3(nb), dim3(X6Geo<NT>::THREADS), lds, st, *J, din, dout, L,
+                       prm, part, P);
     return (int)hipGetLastError();
   }
 }

@@ -2,8 +2,8 @@
 #include "jet_x6_bwd.hpp"
 
 namespace insr {
-template int dispatch_bwd_q<3>(int, int, bool, int, const float*, int, int, int, int, const float*, const float*,
-                               const float*, const float*, const float*, float*, long, int, hipStream_t);
+template int dispatch_bwd_q<3>(int, int, bool, int, const BwdJobsX6*, int, int, int, const float*, float*, long,
+                               hipStream_t);
 }  // namespace insr
 
 #ifdef INSR_STAMPS

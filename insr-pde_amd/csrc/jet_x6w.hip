@@ -3,6 +3,7 @@
 #include "jet_x6w.hpp"
 
 namespace insr {
+int g_wide_dw_f16 = 0;
 template int dispatch_wide_bwd_q<3>(int, int, bool, const float*, int, int, int, int, const float*, const float*,
                                     const float*, const float*, const float*, float*, float*, int, hipStream_t);
 long wide_work_floats(long n, int din, int dout, int L, int W, int S) {

@@ -92,12 +92,13 @@ __global__ __launch_bounds__(512, (x6p_min_waves<NT>())) void jet_bwd_x6p(const 
                                                    const float* __restrict__ prm, const float* __restrict__ act,
                                                    const float* __restrict__ gy, const float* __restrict__ gdy,
                                                    const float* __restrict__ glap, float* __restrict__ adj,
-                                                   float* __restrict__ part, long Ps) {
+                                                   float* __restrict__ part, long Ps, float* __restrict__ zmax) {
   constexpr int W = 16 * NT, RPW = NT / 8, KC = NT / 2;
   constexpr int LDB = W + 8, ZPLANE = 16 * LDB, ZSET = NQ * ZPLANE;
   constexpr int NTAN = LAP ? S - 2 : S - 1;
   extern __shared__ __attribute__((aligned(16))) float lds_f[];
   unsigned short* Z = reinterpret_cast<unsigned short*>(lds_f);  // [s][q][16 p][W + 8]
+  float* zred = lds_f + S * ZSET / 2;                             // [2][8 waves]: tile maxima
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
   const int ntiles = ((N + 63) / 64) * 4;
   const int tile = blockIdx.x;
@@ -222,6 +223,17 @@ __global__ __launch_bounds__(512, (x6p_min_waves<NT>())) void jet_bwd_x6p(const 
 #pragma unroll
         for (int s = 0; s < S; ++s) *reinterpret_cast<floatx4*>(ab + ((s * NT + rt0 + i) * 64 + lane) * 4) = hb[i][s];
     }
+    if (zmax) {  // this tile's max |z̄_j| (Laplacian stream x 16): the scale of dw_x6's fp16 operands
+      float m = 0.f;
+#pragma unroll
+      for (int i = 0; i < RPW; ++i)
+#pragma unroll
+        for (int s = 0; s < S; ++s)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) m = fmaxf(m, fabsf(hb[i][s][r]) * ((LAP && s == S - 1) ? 16.f : 1.f));
+      m = wave_max(m);
+      if (lane == 0) zred[(j & 1) * 8 + wave] = m;  // two slots: layer j - 1 writes the other
+    }
     __syncthreads();  // the previous layer's readers of Z are done
 #pragma unroll
     for (int i = 0; i < RPW; ++i)
@@ -230,6 +242,12 @@ __global__ __launch_bounds__(512, (x6p_min_waves<NT>())) void jet_bwd_x6p(const 
         lds_put4<NQ, ZPLANE>(Z + s * ZSET + c * LDB + 16 * (rt0 + i) + 4 * g, hb[i][s][0], hb[i][s][1], hb[i][s][2],
                              hb[i][s][3]);
     __syncthreads();
+    if (zmax && threadIdx.x == 0) {
+      float m = zred[(j & 1) * 8];
+#pragma unroll
+      for (int w = 1; w < 8; ++w) m = fmaxf(m, zred[(j & 1) * 8 + w]);
+      zmax[(long)(j - 1) * ((N + 15) / 16) + tile] = m;
+    }
     // propagation: h̄_{j-1}[m] = sum_n W_j[n][m] z̄_j[n]; A = W^T rows m of this wave (pre-split
     // planes, orientation 1: NQ b128 loads per fragment), B = Z rows (one b128 per plane)
     const u32x4* wsp = wsp_base(prm, din, dout, L, W);
@@ -278,7 +296,7 @@ constexpr int kDwKR = 40;  // k row (32 + 8 pad) in bf16 elements
 template <int NT>
 constexpr int dw_plane() { return 16 * NT * kDwKR; }  // one plane (bf16 elements)
 template <int NQ, int NT>
-constexpr size_t dw_lds() { return (size_t)2 * NQ * dw_plane<NT>() * 2; }  // A + B, NQ planes each
+constexpr size_t dw_lds() { return (size_t)2 * np_of<NQ>() * dw_plane<NT>() * 2; }  // A + B, np_of<NQ> planes each
 
 __device__ __forceinline__ float swap1(float v) {  // value of lane ^ 1 (quad_perm 1,0,3,2)
   return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, false));
@@ -297,15 +315,15 @@ __device__ __forceinline__ void dw_put(unsigned short* P, const floatx4& v, int 
   const float a1 = odd ? r1 : v[1], b1 = odd ? v[3] : r1;
   const int n0 = 16 * rt + 4 * g + (odd ? 2 : 0);
   const int k = 16 * ul + (c & ~1);
-  unsigned u[NQ];
+  unsigned u[np_of<NQ>()];
   splitq<NQ>(a0, b0, u);
   unsigned* q0 = reinterpret_cast<unsigned*>(P + n0 * kDwKR + k);
 #pragma unroll
-  for (int q = 0; q < NQ; ++q) q0[q * (kDwPL / 2)] = u[q];
+  for (int q = 0; q < np_of<NQ>(); ++q) q0[q * (kDwPL / 2)] = u[q];
   splitq<NQ>(a1, b1, u);
   unsigned* q1 = reinterpret_cast<unsigned*>(P + (n0 + 1) * kDwKR + k);
 #pragma unroll
-  for (int q = 0; q < NQ; ++q) q1[q * (kDwPL / 2)] = u[q];
+  for (int q = 0; q < np_of<NQ>(); ++q) q1[q * (kDwPL / 2)] = u[q];
 }
 
 // first level of the compact-row reduction, 8 waves: column block bx of out row by (of nby)
@@ -340,16 +358,22 @@ __device__ __forceinline__ void rows_level1(const float* __restrict__ part, int 
 // dW of hidden layer blockIdx.y + 1 over chunk slice blockIdx.x (y < L).  Planes y >= L carry
 // the first level of the compact-row reduction (small -> rows, block id (y - L) KS + x), so it
 // runs on the CUs the dW tail leaves idle instead of in a launch of its own.
+// NQ = 4 (f16x3, the x6 backward's dW when g_wide_dw_f16): fp16 has 11 significant bits but a
+// narrow range, and an adjoint has no a-priori scale, so each K slice scales its z̄ by the power of
+// two 2^e that maps the slice's largest |z̄| (zmax: the propagation kernel's tile maxima) into
+// [2^14, 2^15) -- exact, undone on the partial -- and h enters as the forward's f16x3 does (value and
+// tangent streams unscaled, the Laplacian stream x 2^-4, its z̄ x 2^4: every product keeps 2^e).
 template <int NQ, int NT, int S, bool LAP>
 __global__ __launch_bounds__(512) void dw_x6(int N, const float* __restrict__ act, const float* __restrict__ adj,
                                              float* __restrict__ dpart, int KS, int L, const float* __restrict__ small,
-                                             int tiles, long Ps, float* __restrict__ rows, int rs, int rows_x) {
+                                             int tiles, long Ps, float* __restrict__ rows, int rs, int rows_x,
+                                             const float* __restrict__ zmax) {
   constexpr int W = 16 * NT, RT = NT / 8;  // RT: dW row tiles per wave
   constexpr int G = NT / 4;                   // granules per thread per chunk (2 units x NT row tiles / 8 waves)
   constexpr int kDwPL = dw_plane<NT>();
   extern __shared__ __attribute__((aligned(16))) float lds_f[];
   unsigned short* A = reinterpret_cast<unsigned short*>(lds_f);
-  unsigned short* B = A + NQ * kDwPL;
+  unsigned short* B = A + np_of<NQ>() * kDwPL;
   if ((int)blockIdx.y >= L) {
     const int rb = ((int)blockIdx.y - L) * KS + (int)blockIdx.x;
     if (rb < rows_x * rs) rows_level1(small, tiles, Ps, rows, rb % rows_x, rb / rows_x, rs, lds_f);
@@ -361,6 +385,23 @@ __global__ __launch_bounds__(512) void dw_x6(int N, const float* __restrict__ ac
   const int units = ((N + 15) / 16) * S;
   const int chunks = (units + 1) / 2;
   const int c0 = (int)((long)chunks * blockIdx.x / KS), c1 = (int)((long)chunks * (blockIdx.x + 1) / KS);
+  float asc = 1.f, osc = 1.f;  // fp16 operand scale of z̄ and its inverse on the partial (NQ = 4)
+  if constexpr (NQ == 4) {
+    float m = 0.f;
+    if (c1 > c0) {
+      const int ta = (2 * c0) / S, tb = min((2 * c1 - 1) / S, tiles - 1);
+      for (int t = ta + lane; t <= tb; t += 64) m = fmaxf(m, zmax[(long)(j - 1) * tiles + t]);
+    }
+    m = wave_max(m);
+    int e = 0;
+    if (m > 0.f && m <= 3.0e38f) {
+      int k;
+      (void)frexpf(m, &k);                  // m = f 2^k, f in [1/2, 1)
+      e = min(max(15 - k, -100), 100);      // m 2^e in [2^14, 2^15)
+    }
+    asc = ldexpf(1.f, e);
+    osc = ldexpf(1.f, -e);
+  }
 
   floatx4 dacc[RT][NT];
 #pragma unroll
@@ -443,8 +484,14 @@ __global__ __launch_bounds__(512) void dw_x6(int N, const float* __restrict__ ac
         for (int r = 0; r < 4; ++r) hv[r] = s == 0 ? sv[r] : OMEGA * cv[r] * rzs[it][r];
       }
       const floatx4 zero = floatx4{0.f, 0.f, 0.f, 0.f};
-      dw_put<NQ, NT>(A, live ? rzb[it] : zero, rt, ul, lane);
-      dw_put<NQ, NT>(B, live ? hv : zero, rt, ul, lane);
+      if constexpr (NQ == 4) {
+        const bool lq = LAP && s == S - 1;
+        dw_put<NQ, NT>(A, live ? rzb[it] * (lq ? 16.f * asc : asc) : zero, rt, ul, lane);
+        dw_put<NQ, NT>(B, live ? (lq ? hv * 0.0625f : hv) : zero, rt, ul, lane);
+      } else {
+        dw_put<NQ, NT>(A, live ? rzb[it] : zero, rt, ul, lane);
+        dw_put<NQ, NT>(B, live ? hv : zero, rt, ul, lane);
+      }
     }
   };
 
@@ -470,7 +517,7 @@ __global__ __launch_bounds__(512) void dw_x6(int N, const float* __restrict__ ac
 #pragma unroll
     for (int ct = 0; ct < NT; ++ct)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) out[(16 * (RT * wave + i) + 4 * g + r) * W + 16 * ct + c] = dacc[i][ct][r];
+      for (int r = 0; r < 4; ++r) out[(16 * (RT * wave + i) + 4 * g + r) * W + 16 * ct + c] = dacc[i][ct][r] * osc;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -626,7 +673,8 @@ inline long wide_work_floats_impl(long n, int din, int dout, int L, int W, int S
   const long adj = (long)L * ntiles * S * (W / 16) * 256;
   const long small = ((n + 15) / 16) * small_count(din, dout, L, W);
   const long dw = (long)L * wide_ks(n, S, L) * W * W;
-  return adj + small + dw + (long)kSmallRS * small_count(din, dout, L, W);
+  const long zmax = (long)L * ((n + 15) / 16);  // tile maxima of the adjoints (fp16 dW)
+  return adj + small + dw + (long)kSmallRS * small_count(din, dout, L, W) + zmax;
 }
 
 // threads of the three launches of wide_bwd_t (L > 0): propagation, dW + rows level 1,
@@ -652,24 +700,39 @@ int wide_bwd_t(const float* x, int N, int din, int dout, int L, const float* prm
   float* small = adj + (long)L * ntiles * S * NT * 256;
   float* dpart = small + (long)tiles * Ps;
   float* rows = dpart + (long)L * wide_ks(N, S, L) * W * W;
-  constexpr size_t lds_p = (size_t)S * NQ * 16 * (W + 8) * 2;
+  float* zmax = rows + (long)kSmallRS * Ps;
+  // the x6 precision's dW GEMM on the fp16 matrix cores (dw_x6 NQ = 4, above)
+  const bool f16dw = NQ == 3 && g_wide_dw_f16 && L > 0;
+  constexpr size_t lds_p = (size_t)S * NQ * 16 * (W + 8) * 2 + 2 * 8 * sizeof(float);
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)jet_bwd_x6p<NQ, NT, S, LAP>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)lds_p);
     (void)hipFuncSetAttribute((const void*)dw_x6<NQ, NT, S, LAP>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)dw_lds<NQ, NT>());
+    if constexpr (NQ == 3)
+      (void)hipFuncSetAttribute((const void*)dw_x6<4, NT, S, LAP>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)dw_lds<4, NT>());
     attr = true;
   }
   hipLaunchKernelGGL((jet_bwd_x6p<NQ, NT, S, LAP>), dim3(tiles), dim3(512), lds_p, st, x, N, din, dout, L, prm, act, gy,
-                     gdy, glap, adj, small, Ps);
+                     gdy, glap, adj, small, Ps, f16dw ? zmax : nullptr);
   const int rs = tiles < kSmallRS ? tiles : kSmallRS;
   const int rows_x = (int)((Ps + 63) / 64);
   if (L > 0) {  // 3 launches: propagation | dW partials + compact rows level 1 | dW sums + rows level 2
     const int KS = wide_ks(N, S, L);
     const int planes = (rows_x * rs + KS - 1) / KS;
-    hipLaunchKernelGGL((dw_x6<NQ, NT, S, LAP>), dim3(KS, L + planes), dim3(512), (dw_lds<NQ, NT>()), st, N, act, adj,
-                       dpart, KS, L, small, tiles, Ps, rows, rs, rows_x);
+    bool done = false;
+    if constexpr (NQ == 3) {
+      if (f16dw) {
+        hipLaunchKernelGGL((dw_x6<4, NT, S, LAP>), dim3(KS, L + planes), dim3(512), (dw_lds<4, NT>()), st, N, act, adj,
+                           dpart, KS, L, small, tiles, Ps, rows, rs, rows_x, zmax);
+        done = true;
+      }
+    }
+    if (!done)
+      hipLaunchKernelGGL((dw_x6<NQ, NT, S, LAP>), dim3(KS, L + planes), dim3(512), (dw_lds<NQ, NT>()), st, N, act, adj,
+                         dpart, KS, L, small, tiles, Ps, rows, rs, rows_x, zmax);
     const int grad16 = (((uintptr_t)(grad + hidden_off(din, W, 1))) & 15) == 0 ? 1 : 0;  // W % 4 == 0: all layers alike
     const int wq = (W * W / 4 + 63) / 64;
     hipLaunchKernelGGL(reduce_dw_kernel, dim3((unsigned)(wq > rows_x ? wq : rows_x), L + 1), dim3(512), 0, st, dpart,

@@ -95,7 +95,7 @@ def test_struct_layouts_match_header(tmp_path):
     import ctypes
     import subprocess
     from base import _native as nat
-    structs = {"InsrJetJob": nat.JetJob, "InsrLoss": nat.Loss, "InsrBox": nat.Box, "InsrElastic": nat.Elastic}
+    structs = {"InsrJetJob": nat.JetJob, "InsrBwdJob": nat.BwdJob, "InsrLoss": nat.Loss, "InsrBox": nat.Box, "InsrElastic": nat.Elastic}
     lines = ['#include <stdio.h>', '#include <stddef.h>', f'#include "{HEADER}"', "int main(void) {"]
     for cname, py in structs.items():
         lines.append(f'  printf("{cname} size %zu\\n", sizeof({cname}));')
@@ -199,5 +199,38 @@ def test_backward_path_policy(lib):
         assert lib.insr_jet_bwd_path(17, 2, 1, 3, 128, LAP) != 2         # 4 hidden layers only
         assert lib.insr_jet_bwd_path(17, 2, 1, 4, 64, LAP) != 2          # W = 128 only
         assert lib.insr_jet_set_bwd_policy(9) == 3                      # out of range: unchanged
+    finally:
+        lib.insr_jet_set_bwd_policy(old)
+
+
+def test_multi_backward_plan(lib):
+    """insr_siren_jet_bwd_grad_multi's plan, answered on the host: the value jobs of one
+    network's loss.backward() -- the fluid interior (16,384 points) and its two 162-point wall
+    bands -- share ONE fused launch whose blocks follow the balanced 5-tile shape of their combined
+    batch (1024 tiles -> 205 blocks, 11 tiles -> 3 blocks each: 211 partial rows); a job whose own
+    size takes another backward path keeps that path's workspace; malformed job lists are refused."""
+    import ctypes
+    from base import _native as nat
+    V, LAP = nat.MODE_VALUE, nat.MODE_LAP
+    stride = lib.insr_jet_partial_stride(2, 2, 4, 128)
+
+    def work(ns, din=2, dout=2, mode=V):
+        arr = (ctypes.c_long * len(ns))(*ns)
+        return lib.insr_jet_bwd_multi_work_bytes(arr, len(ns), din, dout, 4, 128, mode)
+
+    old = lib.insr_jet_set_bwd_policy(0)
+    try:
+        assert work([16384, 162, 162]) == 211 * stride * 4
+        assert work([16384]) == lib.insr_jet_bwd_work_bytes(16384, 2, 2, 4, 128, V)
+        assert work([162, 0, 162]) == 22 * stride * 4  # 1-tile blocks (324 points), 11 per band
+        # Laplacian interior: the two-kernel path alone; bands beside it in the fused launch
+        lw = lib.insr_jet_bwd_work_bytes(16708, 2, 1, 4, 128, LAP)
+        pw = work([162, 162], dout=1, mode=LAP)
+        assert work([16708, 162, 162], dout=1, mode=LAP) == max(lw, pw)
+        for bad in ([], [-1], [1] * (nat.MAX_BWD_JOBS + 1), [1 << 31]):
+            assert work(bad) == -1, bad
+        assert lib.insr_siren_jet_bwd_grad_multi(None, 1, 2, 2, 4, 128, V, None, None, None, 0, None) == -1
+        jobs = (nat.BwdJob * 1)(nat.BwdJob(None, None, None, None, None, 64))  # live job without x / act
+        assert lib.insr_siren_jet_bwd_grad_multi(jobs, 1, 2, 2, 4, 128, V, 1, 1, 1, 0, None) == -1
     finally:
         lib.insr_jet_set_bwd_policy(old)

@@ -156,3 +156,42 @@ def test_advection_device_sampler_phase_runs(B, graph):
     assert torch.isfinite(after).all() and not torch.equal(before, after)
     if graph:
         assert getattr(model, "_insr_capture_error", None) is None
+
+
+@pytest.mark.gpu
+def test_reference_band_samplers_on_the_device(B):
+    """The reference's band samplers called with a cuda device (base/sampling.py:21-64: what an
+    unchanged model file calls) draw through ONE insr_sample_boxes launch: face k in rows
+    [k n, (k + 1) n), each coordinate uniform in its face's range, a fresh draw per call."""
+    eps = 1e-4
+    lo, hi, full = (-1 - eps, -1 + eps), (1 - eps, 1 + eps), (-1.0, 1.0)
+    cases = [
+        (lambda: B.sample_boundary2D_separate(4000, side="horizontal", device="cuda"), [(lo, full), (hi, full)]),
+        (lambda: B.sample_boundary2D_separate(4000, side="vertical", device="cuda"), [(full, lo), (full, hi)]),
+        (lambda: B.sample_boundary(8000, 2, device="cuda"), [(full, lo), (full, hi), (lo, full), (hi, full)]),
+        (lambda: B.sample_boundary2D_pair(4000, device="cuda"), [(lo, full), (hi, full), (full, lo), (full, hi)]),
+    ]
+    for draw, faces in cases:
+        a, b = draw(), draw()
+        n = 2000
+        assert a.shape == (n * len(faces), 2) and a.is_cuda and a.dtype == torch.float32
+        assert not torch.equal(a, b)
+        for k, face in enumerate(faces):
+            rows = a[k * n:(k + 1) * n].cpu().double()
+            for j, (l, h) in enumerate(face):
+                col = rows[:, j]
+                assert float(col.min()) >= np.float32(l) and float(col.max()) <= np.float32(h), (k, j)
+                assert abs(float(col.mean()) - (l + h) / 2) < 0.05 * (h - l), (k, j)
+    assert B.sample_boundary2D_separate(1, side="horizontal", device="cuda").shape == (0, 2)
+
+
+@pytest.mark.gpu
+def test_sample_random_on_the_device(B):
+    """sample_random(N, d, device='cuda') (base/sampling.py:14-18): one insr_sample_boxes launch,
+    uniform in [-1, 1)^d, fresh per call."""
+    for d in (1, 2, 3):
+        a, b = B.sample_random(20000, d, device="cuda"), B.sample_random(20000, d, device="cuda")
+        assert a.shape == (20000, d) and a.is_cuda and not torch.equal(a, b)
+        assert float(a.min()) >= -1.0 and float(a.max()) < 1.0
+        assert abs(float(a.mean())) < 0.02 and abs(float(a.var()) - 1 / 3) < 0.02
+    assert B.sample_random(0, 2, device="cuda").shape == (0, 2)
