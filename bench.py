@@ -80,8 +80,9 @@ def parse():
                          "points per phase iteration; elasticity: the draw at resolution / K^(1/3)); 1 GPU")
     ap.add_argument("--bwd-policy", type=int, default=0, choices=[0, 1, 2, 3],
                     help="backward path (A/B studies): 0 auto, 1 fused tile-split, 2 two-kernel, 3 resident dW")
-    ap.add_argument("--dw-f16", type=int, default=-1, choices=[-1, 0, 1],
-                    help="dW GEMM of the two-kernel backward on the fp16 matrix cores (A/B studies; -1 = library default)")
+    ap.add_argument("--bwd-f16", type=int, default=-1, choices=list(range(-1, 8)),
+                    help="x6 backward products on the fp16 matrix cores, INSR_BWD_F16_* mask (A/B studies; "
+                         "-1 = library default)")
     ap.add_argument("--cpu-seconds", type=float, default=25.0, help="budget of the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
@@ -175,7 +176,7 @@ def build_model(args, world, rank):
     from pde.config import baseline_config
     base._native.load()
     base._native.lib().insr_jet_set_bwd_policy(args.bwd_policy)
-    base._native.lib().insr_jet_set_dw_precision(args.dw_f16)
+    base._native.lib().insr_jet_set_bwd_f16(args.bwd_f16)
     wl = WORKLOADS[args.config]
     res = wl["res"]
     cfg = baseline_config(args.config, sample_resolution=res, insr_graph=not args.no_graph,
@@ -552,6 +553,8 @@ def main():
     if args.rehearse:
         return rehearse(args, world, rank)
     model, cfg, wl, n_local = build_model(args, world, rank)
+    from base import _native
+    bwd_f16 = _native.lib().insr_jet_set_bwd_f16(-1)  # the backward products on fp16 matrix cores in effect
     nph = len(wl["phases"])
     loops = phase_loops(model, wl)
     log(f"model built, {n_local} points per rank per phase")
@@ -605,7 +608,7 @@ def main():
                    "precision": args.precision, "api": args.api, "sync_every": cfg.insr_sync_every,
                    "jet_precision": jet_precision_names(args.precision),
                    "bwd_policy": args.bwd_policy, "shard_of": args.shard_of,
-                   "dw_f16": base._native.lib().insr_jet_set_dw_precision(-1),
+                   "bwd_f16": bwd_f16,
                    "timestep_order": f"{nts} timesteps x ({'/'.join(str(k) for k in ks)}) iterations per phase, "
                                      "phases in step() order with the prev-net snapshots; per-timestep times from HIP events"},
         "timesteps": {"count": nts, "iters_per_phase": ks, "ms": [round(v, 3) for v in ts_ms],

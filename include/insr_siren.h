@@ -81,8 +81,8 @@ long insr_siren_param_count(int d_in, int d_out, int num_hidden, int width);
 
 /* Pre-split weight planes (split-bf16 kernels).  Every hidden weight W_j is stored split in
  * three bf16 terms (jet_x6.hpp) in the matrix-core fragment order of the forward (W_j rows)
- * and of the backward (W_j^T rows), then 2^8 W_j split in two fp16 terms in the forward order
- * (INSR_PREC_F16X3): 4 L W^2 floats in all, at insr_siren_wsplit_offset() floats (param_count
+ * and of the backward (W_j^T rows), then 2^8 W_j split in two fp16 terms in the forward and in
+ * the backward order (INSR_PREC_F16X3): 5 L W^2 floats in all, at insr_siren_wsplit_offset() floats (param_count
  * rounded up to 16 B) after the start of the params buffer.
  * insr_siren_wsplit() writes them from the parameters in place (one launch); the kernels then
  * read fragments instead of re-splitting W in every block.  Replaces nothing in the
@@ -229,11 +229,17 @@ int insr_jet_bwd_path(long n_points, int d_in, int d_out, int num_hidden, int wi
  * 2 = two-kernel, 3 = resident dW where it applies.  Returns the previous policy (a policy
  * outside 0..3 changes nothing: -1 queries). */
 int insr_jet_set_bwd_policy(int policy);
-/* dW GEMM of the two-kernel backward at the x6 backward precision: 1 = on the fp16 matrix cores
- * (f16x3: two fp16 terms per operand, three products; each K slice's adjoints scaled by the power
- * of two that maps its largest |value| into [2^14, 2^15), undone exactly on its partial), 0 =
- * bf16x6.  Returns the previous setting (-1 queries).  Process-wide. */
-int insr_jet_set_dw_precision(int f16);
+/* Matrix products of the x6 (fp32-level) backward that run on the fp16 matrix cores instead of
+ * six bf16 products: f16x3 (two fp16 terms per operand, three products, 22 significant bits),
+ * the adjoints scaled by the power of two that maps the largest |value| of their K slice / tile
+ * into [2^14, 2^15) (undone exactly), the weights by 2^8 (the fp16 planes).  Bit mask:
+ * INSR_BWD_F16_DW the two-kernel path's dW GEMM, INSR_BWD_F16_PROP its adjoint propagation,
+ * INSR_BWD_F16_FUSED the fused tile-split kernel.
+ * Returns the previous mask (-1 queries).  Process-wide. */
+#define INSR_BWD_F16_DW 1
+#define INSR_BWD_F16_PROP 2
+#define INSR_BWD_F16_FUSED 4 /* the fused tile-split backward (dW and propagation, per-block scales) */
+int insr_jet_set_bwd_f16(int mask);
 /* Threads of the three launches of a two-kernel backward (propagation, dW partials, dW sums),
  * as profilers report them; INSR_EINVAL when (n, shape, mode) does not take that path. */
 int insr_jet_wide_launch_threads(long n_points, int d_in, int d_out, int num_hidden, int width, int mode,

@@ -62,7 +62,7 @@ SIGNATURES = {
     "insr_jet_bwd_is_wide": (_I, [_L, _I, _I, _I]),
     "insr_jet_bwd_path": (_I, [_L, _I, _I, _I, _I, _I]),
     "insr_jet_set_bwd_policy": (_I, [_I]),
-    "insr_jet_set_dw_precision": (_I, [_I]),
+    "insr_jet_set_bwd_f16": (_I, [_I]),
     "insr_jet_set_wide_min_width": (_I, [_I]),
     "insr_comm_available": (_I, []),
     "insr_comm_id_bytes": (_L, []),

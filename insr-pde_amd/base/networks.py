@@ -162,7 +162,7 @@ class MLP(nn.Module):
         return (self.param_count + 3) & ~3
 
     def wsplit_floats(self):
-        return 4 * self.num_hidden_layers * self.kernel_width ** 2  # bf16 x 3 (both orientations) + fp16 x 2
+        return 5 * self.num_hidden_layers * self.kernel_width ** 2  # bf16 x 3 + fp16 x 2, both orientations each
 
     def plist(self):
         """list(self.parameters()) without the module-tree walk (the checks before every jet and

@@ -136,19 +136,25 @@ def _dp_rank():
 
 
 def _sampler(dev):
-    """Per-device Philox state of the fused sampler (insr_sample_boxes).  Keyed by the
-    device's torch generator seed and the distributed rank.  Created on the first eager
-    call -- phase loops always run iteration 0 eagerly before capturing."""
+    """Per-device Philox state of the fused sampler (insr_sample_boxes): (stream position on
+    the device, key).  The key is the device's torch seed with the distributed rank folded in;
+    re-seeding torch (torch.cuda.manual_seed) restarts the stream, so seeded runs repeat their
+    draws.  Created / restarted on an eager call -- phase loops always run iteration 0 eagerly
+    before capturing (a capture keeps the current stream)."""
     from . import _native as nat
     key = dev.index
-    if key not in _SAMPLER:
+    with torch.cuda.device(dev):
+        seed = torch.cuda.initial_seed()
+    ent = _SAMPLER.get(key)
+    if ent is None or ent[2] != seed:
         if torch.cuda.is_current_stream_capturing():
-            raise RuntimeError("sampler state must be created before graph capture (run one eager call)")
-        with torch.cuda.device(dev):
-            seed = torch.cuda.initial_seed()
-        _SAMPLER[key] = (torch.zeros(nat.lib().insr_sampler_state_bytes() // 8, device=dev, dtype=torch.int64),
-                         sampler_seed(seed, _dp_rank()))
-    return _SAMPLER[key]
+            if ent is None:
+                raise RuntimeError("sampler state must be created before graph capture (run one eager call)")
+            return ent[:2]
+        state = ent[0].zero_() if ent is not None else torch.zeros(nat.lib().insr_sampler_state_bytes() // 8,
+                                                                    device=dev, dtype=torch.int64)
+        ent = _SAMPLER[key] = (state, sampler_seed(seed, _dp_rank()), seed)
+    return ent[:2]
 
 
 def sample_random_and_bands2D(N, n_band, epsilon=1e-4, device="cuda", merged=False):

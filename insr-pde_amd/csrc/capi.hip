@@ -142,10 +142,15 @@ static int fwd_q(int nq, int NT, int S, bool lap, int T, const float* x, int N, 
     default: return dispatch_fwd_split(NT, S, lap, T, x, N, din, dout, L, prm, y, dy, lp, act, st);
   }
 }
+// the kernel precision of a fused tile-split backward at precision nq: the x6 backward's products on
+// the fp16 matrix cores under INSR_BWD_F16_FUSED (jet_h_bwd.hip)
+static int fused_bwd_nq(int nq) { return (nq == 3 && (g_bwd_f16 & INSR_BWD_F16_FUSED)) ? 4 : nq; }
+
 // J == NULL: occupancy query; the exact-fp32 kernel takes one job per launch
 static int bwd_q(int nq, int NT, int S, bool lap, int T, const BwdJobsX6* J, int din, int dout, int L,
                  const float* prm, float* part, long P, hipStream_t st) {
   switch (nq) {
+    case 4: return dispatch_bwd_q<4>(NT, S, lap, T, J, din, dout, L, prm, part, P, st);
     case 3: return dispatch_bwd_q<3>(NT, S, lap, T, J, din, dout, L, prm, part, P, st);
     case 2: return dispatch_bwd_q<2>(NT, S, lap, T, J, din, dout, L, prm, part, P, st);
     case 1: return dispatch_bwd_q<1>(NT, S, lap, T, J, din, dout, L, prm, part, P, st);
@@ -463,14 +468,18 @@ __device__ __forceinline__ void adam_wsplit(float* base, const int (&sh)[4], lon
 #pragma unroll
     for (int q = 0; q < 3; ++q) pl[o * ov + ((fr + q) * 64 + 16 * g + c) * 8 + jj] = t[q];
   }
-  // the fp16 forward planes (INSR_PREC_F16X3): 2^8 w in two fp16 terms, orientation 0
+  // the fp16 planes (INSR_PREC_F16X3): 2^8 w in two fp16 terms, orientation 0 then 1
   unsigned short* ph = reinterpret_cast<unsigned short*>(base + wsplit_f16_offset(din, dout, L, W));
   const float ws = w * kF16WScale;
   const _Float16 hh = (_Float16)ws, hl = (_Float16)(ws - (float)hh);
-  const int rt = n >> 4, c = n & 15, kc = m >> 5, g = (m & 31) >> 3, jj = m & 7;
-  const long fr = (((long)(j - 1) * NT + rt) * KC + kc) * 2;
-  ph[(fr * 64 + 16 * g + c) * 8 + jj] = __builtin_bit_cast(unsigned short, hh);
-  ph[((fr + 1) * 64 + 16 * g + c) * 8 + jj] = __builtin_bit_cast(unsigned short, hl);
+  const long oh = 2L * L * W * W;  // u16 per fp16 orientation
+#pragma unroll
+  for (int o = 0; o < 2; ++o) {
+    const int rt = rr[o] >> 4, c = rr[o] & 15, kc = kk[o] >> 5, g = (kk[o] & 31) >> 3, jj = kk[o] & 7;
+    const long fr = (((long)(j - 1) * NT + rt) * KC + kc) * 2;
+    ph[o * oh + (fr * 64 + 16 * g + c) * 8 + jj] = __builtin_bit_cast(unsigned short, hh);
+    ph[o * oh + ((fr + 1) * 64 + 16 * g + c) * 8 + jj] = __builtin_bit_cast(unsigned short, hl);
+  }
 }
 
 // One launch over up to INSR_ADAM_MAX_TENSORS flat buffers.  The step t used is
@@ -848,7 +857,7 @@ int insr_siren_jet_bwd(const float* x, long n, int din, int dout, int L, int W, 
   J.first[0] = 0;
   J.first[1] = sh.nbal > 0 ? sh.nbal : (int)(((n + 15) / 16 + sh.T - 1) / sh.T);
   J.njobs = 1;
-  return bwd_q(nq, c.NT, c.S, c.lap, sh.T, &J, din, dout, L, params, partial, P, (hipStream_t)stream);
+  return bwd_q(fused_bwd_nq(nq), c.NT, c.S, c.lap, sh.T, &J, din, dout, L, params, partial, P, (hipStream_t)stream);
 }
 
 // Plan of a multi-job backward (insr_siren_jet_bwd_grad_multi): the jobs whose own size takes the
@@ -946,7 +955,7 @@ int insr_siren_jet_bwd_grad_multi(const InsrBwdJob* jobs, int njobs, int din, in
     J.first[p.nf] = b;
     J.njobs = p.nf;
     const long P = insr_jet_partial_stride(din, dout, L, W);
-    if ((rc = bwd_q(p.nq, c.NT, c.S, c.lap, p.T, &J, din, dout, L, prm, work, P, st))) return rc;
+    if ((rc = bwd_q(fused_bwd_nq(p.nq), c.NT, c.S, c.lap, p.T, &J, din, dout, L, prm, work, P, st))) return rc;
     if ((rc = insr_reduce_partials_strided(work, p.nb, insr_siren_param_count(din, dout, L, W), P, grad, acc, stream)))
       return rc;
     acc = 1;
@@ -1002,9 +1011,9 @@ int insr_jet_bwd_path(long n, int din, int dout, int L, int W, int mode) {
   return JetCall(din, W, mode).path(n, L);
 }
 
-int insr_jet_set_dw_precision(int f16) {
-  const int old = g_wide_dw_f16;
-  if (f16 == 0 || f16 == 1) g_wide_dw_f16 = f16;
+int insr_jet_set_bwd_f16(int mask) {
+  const int old = g_bwd_f16;
+  if (mask >= 0 && mask <= 7) g_bwd_f16 = mask;
   return old;
 }
 

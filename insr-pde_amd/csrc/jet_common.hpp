@@ -68,12 +68,18 @@ __host__ __device__ inline long wsplit_offset(int din, int dout, int L, int W) {
 }
 __host__ __device__ inline long wsplit_orient_vecs(int L, int W) { return (long)L * W * W * 3 / 8; }
 // ... followed by the fp16 planes of the forward orientation (INSR_PREC_F16X3): 2^8 W_j in two
-// fp16 terms, [layer][rt][kc][term][lane] 16 B each -- L W^2 floats; 4 L W^2 floats of planes in all
+// fp16 terms, [layer][rt][kc][term][lane] 16 B each -- L W^2 floats
 constexpr float kF16WScale = 256.0f;  // weights' power-of-two scale in the fp16 planes
 __host__ __device__ inline long wsplit_f16_offset(int din, int dout, int L, int W) {
   return wsplit_offset(din, dout, L, W) + 3L * L * W * W;
 }
-__host__ __device__ inline long wsplit_total_floats(int L, int W) { return 4L * L * W * W; }
+// ... then 2^8 W_j^T likewise (the backward orientation of the fp16 planes: the f16x3 backward's
+// propagation A operand) -- 5 L W^2 floats of planes in all
+__host__ __device__ inline long wsplit_f16t_offset(int din, int dout, int L, int W) {
+  return wsplit_f16_offset(din, dout, L, W) + (long)L * W * W;
+}
+__host__ __device__ inline long wsplit_f16_vecs(int L, int W) { return (long)L * W * W / 4; }  // u32x4 per fp16 orientation
+__host__ __device__ inline long wsplit_total_floats(int L, int W) { return 5L * L * W * W; }
 
 // wave-tile base of layer `layer` in the saved-activation buffer
 __device__ __forceinline__ float* act_base(float* act, int layer, int ntiles, int tile, int S, int NT) {
@@ -360,9 +366,9 @@ int dispatch_wide_bwd_q(int NT, int S, bool LAP, const float* x, int N, int din,
                         const float* act, const float* gy, const float* gdy, const float* glap, float* work,
                         float* grad, int accumulate, hipStream_t st);
 long wide_work_floats(long n, int din, int dout, int L, int W, int S);
-// two-kernel backward of the x6 precision: 1 = its dW GEMM on the fp16 matrix cores (f16x3 with
-// a power-of-two scale of the adjoints per K slice), 0 = bf16x6 (jet_x6w.hip; insr_jet_set_dw_precision)
-extern int g_wide_dw_f16;
+// x6 backward products on the fp16 matrix cores (f16x3 with power-of-two adjoint scales; mask of
+// INSR_BWD_F16_*: jet_x6w.hip, insr_jet_set_bwd_f16)
+extern int g_bwd_f16;
 template <int NQ>
 int dispatch_fwd_mixed_q(int NT, int din, const InsrJetJob* jobs, const int* modes, const float* scalars, int njobs,
                          int dout, int L, hipStream_t st);

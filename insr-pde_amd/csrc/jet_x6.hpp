@@ -195,8 +195,9 @@ template <int NQ, int NT>
 __device__ __forceinline__ FragQ<NQ> wsp_frag(const u32x4* __restrict__ wsp, int L, int o, int j, int rt, int kc,
                                               int lane) {
   constexpr int W = 16 * NT, KC = NT / 2;
-  if constexpr (NQ == 4) {  // the fp16 forward planes (o = 0 only), after both bf16 orientations
-    const u32x4* p = wsp + 2 * wsplit_orient_vecs(L, W) + ((((long)(j - 1) * NT + rt) * KC + kc) * 2) * 64 + lane;
+  if constexpr (NQ == 4) {  // the fp16 planes (o = 0: forward, o = 1: backward), after both bf16 orientations
+    const u32x4* p = wsp + 2 * wsplit_orient_vecs(L, W) + o * wsplit_f16_vecs(L, W) +
+                     ((((long)(j - 1) * NT + rt) * KC + kc) * 2) * 64 + lane;
     FragQ<NQ> f;
     f.q[0] = p[0];
     f.q[1] = p[64];
@@ -751,10 +752,10 @@ struct X6BwdGeo {
   static constexpr int W = G::W;
   static constexpr int ZROW = G::LDB;                  // elements of a Z point row
   static constexpr int ZPLANE = 16 * ZROW;
-  static constexpr int ZSET = NQ * ZPLANE + 32;        // +16 dwords: the four lane groups of a
-                                                       // column read hit disjoint banks
+  static constexpr int ZSET = np_of<NQ>() * ZPLANE + 32;  // +16 dwords: the four lane groups of a
+                                                          // column read hit disjoint banks
   static constexpr int HPLANE = W * 16;
-  static constexpr int HSET = NQ * HPLANE;
+  static constexpr int HSET = np_of<NQ>() * HPLANE;
   static constexpr size_t SET_BYTES = (size_t)(ZSET + HSET) * 2;
 };
 
@@ -768,8 +769,8 @@ constexpr int x6_bwd_sg() {
 }
 
 template <int NQ, int NT, int S, int T>
-constexpr size_t bwd_x6_lds_bytes() {
-  return (size_t)T * x6_bwd_sg<NQ, NT, S, T>() * X6BwdGeo<NQ, NT>::SET_BYTES;
+constexpr size_t bwd_x6_lds_bytes() {  // + 2 x 8 floats: the per-layer adjoint maxima of the waves (NQ = 4)
+  return (size_t)T * x6_bwd_sg<NQ, NT, S, T>() * X6BwdGeo<NQ, NT>::SET_BYTES + 2 * 8 * sizeof(float);
 }
 
 template <int NQ, int NT, int S, bool LAP, int T>
@@ -790,7 +791,12 @@ __global__ __launch_bounds__(X6Geo<NT>::THREADS) void jet_bwd_x6(const BwdJobsX6
   extern __shared__ __attribute__((aligned(16))) float lds_f[];
   unsigned short* Z = reinterpret_cast<unsigned short*>(lds_f);
   unsigned short* H = Z + NSET * ZSET;
+  float* zred = lds_f + NSET * (ZSET + HSET) / 2;  // [2][waves]: per-layer max |z̄| of each wave (NQ = 4)
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
+  // NQ = 4 (INSR_BWD_F16_FUSED, the x6 backward's products on the fp16 matrix cores): per layer the
+  // block's z̄ is scaled by the power of two 2^e that maps its largest |z̄| (Laplacian stream x 16)
+  // into [2^14, 2^15), h's Laplacian stream by 2^-4 and W^T comes from the fp16 backward planes
+  // (x 2^8); dW is unscaled by 2^-e, the propagation by 2^-(8 + e) -- exact powers of two
   // this block's job (a batch of the launch's network) and its tiles within that batch
   const int b = blockIdx.x;
   int jk = 0;
@@ -983,6 +989,19 @@ __global__ __launch_bounds__(X6Geo<NT>::THREADS) void jet_bwd_x6(const BwdJobsX6
       break;
     }
     INSR_STAMP(L - j, 1);
+    if constexpr (NQ == 4) {  // this wave's max |z̄_j| over the block's tiles (read after the group barrier)
+      float m = 0.f;
+#pragma unroll
+      for (int t = 0; t < T; ++t)
+#pragma unroll
+        for (int i = 0; i < RPW; ++i)
+#pragma unroll
+          for (int s = 0; s < S; ++s)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) m = fmaxf(m, fabsf(hb[t][i][s][r]) * ((LAP && s == S - 1) ? 16.f : 1.f));
+      m = wave_max(m);
+      if (lane == 0) zred[(j & 1) * 8 + wave] = m;  // two slots: layer j - 1 writes the other
+    }
     // A operand of the propagation: W^T rows m = 16 rt + c, k = n = 32 kc + 8 g + jj, from the
     // pre-split planes (issued here, in flight during the dW phase).  Several stream groups:
     // re-read per group (L2 hits) instead of holding the fragments across groups
@@ -1002,12 +1021,28 @@ __global__ __launch_bounds__(X6Geo<NT>::THREADS) void jet_bwd_x6(const BwdJobsX6
 #pragma unroll
       for (int ct = 0; ct < NT; ++ct) dacc[i][ct] = floatx4{0.f, 0.f, 0.f, 0.f};
     floatx4 nh[T][RPW][S];
+    float zsc = 1.f, zun = 1.f;  // NQ = 4: the block's adjoint scale 2^e and its inverse
 #pragma unroll
     for (int gi = 0; gi < NG; ++gi) {
       const int s0 = gi * SG;
       INSR_STAMP(L - j, 2);
       __syncthreads();  // the previous group's / layer's LDS readers are done
       INSR_STAMP(L - j, 3);
+      if constexpr (NQ == 4) {
+        if (gi == 0) {
+          float m = zred[(j & 1) * 8];
+#pragma unroll
+          for (int w = 1; w < G::WV; ++w) m = fmaxf(m, zred[(j & 1) * 8 + w]);
+          int e = 0;
+          if (m > 0.f && m <= 3.0e38f) {
+            int k;
+            (void)frexpf(m, &k);
+            e = min(max(15 - k, -100), 100);
+          }
+          zsc = ldexpf(1.f, e);
+          zun = ldexpf(1.f, -e);
+        }
+      }
 #pragma unroll
       for (int t = 0; t < T; ++t) {
         const float* basep = act_base(act, j - 1, ntiles, tt(t), S, NT);
@@ -1018,14 +1053,17 @@ __global__ __launch_bounds__(X6Geo<NT>::THREADS) void jet_bwd_x6(const BwdJobsX6
             const int s = s0 + sl;
             const int u = t * SG + sl;
             const int col = 16 * (rt0 + i) + 4 * g;
-            lds_put4<NQ, ZPLANE>(Z + u * ZSET + c * LDB + col, hb[t][i][s][0], hb[t][i][s][1], hb[t][i][s][2],
-                                 hb[t][i][s][3]);
+            const bool lq = NQ == 4 && LAP && s == S - 1;  // the fp16 Laplacian-stream scales
+            const float fz = lq ? 16.f * zsc : zsc;
+            lds_put4<NQ, ZPLANE>(Z + u * ZSET + c * LDB + col, hb[t][i][s][0] * fz, hb[t][i][s][1] * fz,
+                                 hb[t][i][s][2] * fz, hb[t][i][s][3] * fz);
             floatx4 hs;
             if constexpr (KZ) {
               hs = h_from_regs<S, LAP>(s, zk[t][i], snp[t][i], csp[t][i]);
             } else {
               hs = h_stream<NT, S, LAP>(basep, s, rt0 + i, lane, snp[t][i], csp[t][i]);
             }
+            if (lq) hs *= 0.0625f;
             put_neuron_major<NQ, HPLANE>(H + u * HSET, hs, col, c);
           }
       }
@@ -1050,7 +1088,7 @@ __global__ __launch_bounds__(X6Geo<NT>::THREADS) void jet_bwd_x6(const BwdJobsX6
             const unsigned short* pa =
                 Z + (live ? u : 0) * ZSET + (p0 + (c >> 2)) * LDB + 16 * (rt0 + i) + 4 * (c & 3);
 #pragma unroll
-            for (int q = 0; q < NQ; ++q) {
+            for (int q = 0; q < np_of<NQ>(); ++q) {
               const v4s lo = ds_read_tr16(pa + q * ZPLANE);
               const v4s hi = ds_read_tr16(pa + q * ZPLANE + 4 * LDB);
               const u32x2 wl = __builtin_bit_cast(u32x2, lo), wh = __builtin_bit_cast(u32x2, hi);
@@ -1072,7 +1110,7 @@ __global__ __launch_bounds__(X6Geo<NT>::THREADS) void jet_bwd_x6(const BwdJobsX6
 #pragma unroll
           for (int ct = 0; ct < NT; ++ct)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) dW[(16 * (rt0 + i) + 4 * g + r) * W + 16 * ct + c] = dacc[i][ct][r];
+            for (int r = 0; r < 4; ++r) dW[(16 * (rt0 + i) + 4 * g + r) * W + 16 * ct + c] = dacc[i][ct][r] * zun;
       }
       INSR_STAMP(L - j, 6);
       if constexpr (NG > 1) {
@@ -1109,7 +1147,7 @@ __global__ __launch_bounds__(X6Geo<NT>::THREADS) void jet_bwd_x6(const BwdJobsX6
 #pragma unroll
         for (int ct = 0; ct < NT; ++ct)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) dW[(16 * (rt0 + i) + 4 * g + r) * W + 16 * ct + c] = dacc[i][ct][r];
+          for (int r = 0; r < 4; ++r) dW[(16 * (rt0 + i) + 4 * g + r) * W + 16 * ct + c] = dacc[i][ct][r] * zun;
     }
 #pragma unroll
     for (int t = 0; t < T; ++t)
@@ -1118,7 +1156,9 @@ __global__ __launch_bounds__(X6Geo<NT>::THREADS) void jet_bwd_x6(const BwdJobsX6
         sn[t][i] = snp[t][i];
         cs[t][i] = csp[t][i];
 #pragma unroll
-        for (int s = 0; s < S; ++s) hb[t][i][s] = nh[t][i][s];
+        for (int s = 0; s < S; ++s)
+          hb[t][i][s] = (NQ == 4) ? nh[t][i][s] * (((LAP && s == S - 1) ? 0.0625f : 1.f) * zun / kF16WScale)
+                                  : nh[t][i][s];
       }
   }
 }

@@ -3,7 +3,7 @@
 #include "jet_x6w.hpp"
 
 namespace insr {
-int g_wide_dw_f16 = 0;
+int g_bwd_f16 = INSR_BWD_F16_DW;  // measured: profiles/r03/bwd_f16_ab
 template int dispatch_wide_bwd_q<3>(int, int, bool, const float*, int, int, int, int, const float*, const float*,
                                     const float*, const float*, const float*, float*, float*, int, hipStream_t);
 long wide_work_floats(long n, int din, int dout, int L, int W, int S) {
@@ -11,7 +11,7 @@ long wide_work_floats(long n, int din, int dout, int L, int W, int S) {
 }
 int wsplit_launch(const float* prm, int din, int dout, int L, int W, float* planes, hipStream_t st) {
   if (L < 1) return 0;
-  const long threads = 3L * L * (W / 16) * (W / 32) * 64;  // two bf16 orientations + the fp16 one
+  const long threads = 4L * L * (W / 16) * (W / 32) * 64;  // two bf16 orientations + two fp16 ones
   const dim3 grid((unsigned)((threads + 255) / 256));
   u32x4* out = reinterpret_cast<u32x4*>(planes);
   switch (W) {

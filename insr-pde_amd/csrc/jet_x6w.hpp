@@ -41,7 +41,7 @@ __host__ __device__ inline long small_count(int din, int dout, int L, int W) {
 //   o = 1: W_j[32 kc + 8 g + 0..7][16 rt + c]   (backward A operand = W_j^T rows)
 // split in three bf16 terms (split_frag<3>); kernels of NQ < 3 read the first NQ terms;
 //   o = 2: the o = 0 weights times 2^8 in two fp16 terms (split_frag<4>: INSR_PREC_F16X3),
-//          after the two bf16 orientations
+//          after the two bf16 orientations; o = 3: the o = 1 weights likewise (the f16x3 backward)
 // ---------------------------------------------------------------------------------------
 template <int NT>
 __global__ __launch_bounds__(256) void wsplit_kernel(const float* __restrict__ prm, int din, int L,
@@ -50,13 +50,13 @@ __global__ __launch_bounds__(256) void wsplit_kernel(const float* __restrict__ p
   const long gid = (long)blockIdx.x * 256 + threadIdx.x;
   const int lane = (int)(gid & 63), g = lane >> 4, c = lane & 15;
   const long fa = gid >> 6;  // (o, layer, frag)
-  if (fa >= 3L * L * NF) return;
+  if (fa >= 4L * L * NF) return;
   const int o = (int)(fa / ((long)L * NF));
   const long f = fa % ((long)L * NF);
   const int j = 1 + (int)(f / NF), rt = (int)((f % NF) / KC), kc = (int)(f % KC);
   const float* Wj = prm + hidden_off(din, W, j);
   floatx4 v0, v1;
-  if (o != 1) {
+  if (o == 0 || o == 2) {
     v0 = *reinterpret_cast<const floatx4*>(Wj + (16 * rt + c) * W + 32 * kc + 8 * g);
     v1 = *reinterpret_cast<const floatx4*>(Wj + (16 * rt + c) * W + 32 * kc + 8 * g + 4);
   } else {
@@ -66,9 +66,9 @@ __global__ __launch_bounds__(256) void wsplit_kernel(const float* __restrict__ p
       v1[jj] = Wj[(32 * kc + 8 * g + 4 + jj) * W + 16 * rt + c];
     }
   }
-  if (o == 2) {
+  if (o >= 2) {  // fp16: o = 2 forward rows, o = 3 backward (W^T) rows
     const FragQ<4> h = split_frag<4>(v0 * kF16WScale, v1 * kF16WScale);
-    u32x4* oh = out + 6L * L * NF * 64;  // after both bf16 orientations (3 L W^2 floats)
+    u32x4* oh = out + (o == 2 ? 6L : 8L) * L * NF * 64;  // after both bf16 orientations (3 L W^2 floats)
     const long fh = f;
 #pragma unroll
     for (int k = 0; k < 2; ++k) oh[(fh * 2 + k) * 64 + lane] = h.q[k];
@@ -94,8 +94,11 @@ __global__ __launch_bounds__(512, (x6p_min_waves<NT>())) void jet_bwd_x6p(const 
                                                    const float* __restrict__ glap, float* __restrict__ adj,
                                                    float* __restrict__ part, long Ps, float* __restrict__ zmax) {
   constexpr int W = 16 * NT, RPW = NT / 8, KC = NT / 2;
-  constexpr int LDB = W + 8, ZPLANE = 16 * LDB, ZSET = NQ * ZPLANE;
+  constexpr int LDB = W + 8, ZPLANE = 16 * LDB, ZSET = np_of<NQ>() * ZPLANE;
   constexpr int NTAN = LAP ? S - 2 : S - 1;
+  // NQ = 4 (INSR_BWD_F16_PROP): the propagation on the fp16 matrix cores -- W^T from the fp16
+  // backward planes (x 2^8), z̄ scaled per tile by the power of two 2^e that maps the tile's largest
+  // |z̄| (Laplacian stream x 16) into [2^14, 2^15), the product unscaled by 2^-(8 + e) (exact)
   extern __shared__ __attribute__((aligned(16))) float lds_f[];
   unsigned short* Z = reinterpret_cast<unsigned short*>(lds_f);  // [s][q][16 p][W + 8]
   float* zred = lds_f + S * ZSET / 2;                             // [2][8 waves]: tile maxima
@@ -223,7 +226,7 @@ __global__ __launch_bounds__(512, (x6p_min_waves<NT>())) void jet_bwd_x6p(const 
 #pragma unroll
         for (int s = 0; s < S; ++s) *reinterpret_cast<floatx4*>(ab + ((s * NT + rt0 + i) * 64 + lane) * 4) = hb[i][s];
     }
-    if (zmax) {  // this tile's max |z̄_j| (Laplacian stream x 16): the scale of dw_x6's fp16 operands
+    if (zmax || NQ == 4) {  // this tile's max |z̄_j| (Laplacian stream x 16): the fp16 operand scales
       float m = 0.f;
 #pragma unroll
       for (int i = 0; i < RPW; ++i)
@@ -235,12 +238,28 @@ __global__ __launch_bounds__(512, (x6p_min_waves<NT>())) void jet_bwd_x6p(const 
       if (lane == 0) zred[(j & 1) * 8 + wave] = m;  // two slots: layer j - 1 writes the other
     }
     __syncthreads();  // the previous layer's readers of Z are done
+    float zsc = 1.f, zun = 1.f;  // NQ = 4: the tile's adjoint scale 2^e, the products' unscale 2^-(8 + e)
+    if constexpr (NQ == 4) {
+      float m = zred[(j & 1) * 8];
+#pragma unroll
+      for (int w = 1; w < 8; ++w) m = fmaxf(m, zred[(j & 1) * 8 + w]);
+      int e = 0;
+      if (m > 0.f && m <= 3.0e38f) {
+        int k;
+        (void)frexpf(m, &k);
+        e = min(max(15 - k, -100), 100);
+      }
+      zsc = ldexpf(1.f, e);
+      zun = ldexpf(1.f, -e) / kF16WScale;
+    }
 #pragma unroll
     for (int i = 0; i < RPW; ++i)
 #pragma unroll
-      for (int s = 0; s < S; ++s)
-        lds_put4<NQ, ZPLANE>(Z + s * ZSET + c * LDB + 16 * (rt0 + i) + 4 * g, hb[i][s][0], hb[i][s][1], hb[i][s][2],
-                             hb[i][s][3]);
+      for (int s = 0; s < S; ++s) {
+        const float f = (NQ == 4 && LAP && s == S - 1) ? 16.f * zsc : zsc;
+        lds_put4<NQ, ZPLANE>(Z + s * ZSET + c * LDB + 16 * (rt0 + i) + 4 * g, hb[i][s][0] * f, hb[i][s][1] * f,
+                             hb[i][s][2] * f, hb[i][s][3] * f);
+      }
     __syncthreads();
     if (zmax && threadIdx.x == 0) {
       float m = zred[(j & 1) * 8];
@@ -280,7 +299,7 @@ __global__ __launch_bounds__(512, (x6p_min_waves<NT>())) void jet_bwd_x6p(const 
 #pragma unroll
     for (int i = 0; i < RPW; ++i)
 #pragma unroll
-      for (int s = 0; s < S; ++s) hb[i][s] = nh[i][s];
+      for (int s = 0; s < S; ++s) hb[i][s] = nh[i][s] * ((NQ == 4 && LAP && s == S - 1) ? 0.0625f * zun : zun);
   }
 }
 
@@ -358,7 +377,7 @@ __device__ __forceinline__ void rows_level1(const float* __restrict__ part, int 
 // dW of hidden layer blockIdx.y + 1 over chunk slice blockIdx.x (y < L).  Planes y >= L carry
 // the first level of the compact-row reduction (small -> rows, block id (y - L) KS + x), so it
 // runs on the CUs the dW tail leaves idle instead of in a launch of its own.
-// NQ = 4 (f16x3, the x6 backward's dW when g_wide_dw_f16): fp16 has 11 significant bits but a
+// NQ = 4 (f16x3, the x6 backward's dW under INSR_BWD_F16_DW): fp16 has 11 significant bits but a
 // narrow range, and an adjoint has no a-priori scale, so each K slice scales its z̄ by the power of
 // two 2^e that maps the slice's largest |z̄| (zmax: the propagation kernel's tile maxima) into
 // [2^14, 2^15) -- exact, undone on the partial -- and h enters as the forward's f16x3 does (value and
@@ -701,22 +720,36 @@ int wide_bwd_t(const float* x, int N, int din, int dout, int L, const float* prm
   float* dpart = small + (long)tiles * Ps;
   float* rows = dpart + (long)L * wide_ks(N, S, L) * W * W;
   float* zmax = rows + (long)kSmallRS * Ps;
-  // the x6 precision's dW GEMM on the fp16 matrix cores (dw_x6 NQ = 4, above)
-  const bool f16dw = NQ == 3 && g_wide_dw_f16 && L > 0;
-  constexpr size_t lds_p = (size_t)S * NQ * 16 * (W + 8) * 2 + 2 * 8 * sizeof(float);
+  // the x6 precision's products on the fp16 matrix cores (dw_x6 / jet_bwd_x6p NQ = 4, above)
+  const bool f16dw = NQ == 3 && (g_bwd_f16 & INSR_BWD_F16_DW) && L > 0;
+  const bool f16p = NQ == 3 && (g_bwd_f16 & INSR_BWD_F16_PROP) && L > 0;
+  constexpr size_t lds_p = (size_t)S * np_of<NQ>() * 16 * (W + 8) * 2 + 2 * 8 * sizeof(float);
+  constexpr size_t lds_p4 = (size_t)S * 2 * 16 * (W + 8) * 2 + 2 * 8 * sizeof(float);
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)jet_bwd_x6p<NQ, NT, S, LAP>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)lds_p);
     (void)hipFuncSetAttribute((const void*)dw_x6<NQ, NT, S, LAP>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)dw_lds<NQ, NT>());
-    if constexpr (NQ == 3)
+    if constexpr (NQ == 3) {
       (void)hipFuncSetAttribute((const void*)dw_x6<4, NT, S, LAP>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)dw_lds<4, NT>());
+      (void)hipFuncSetAttribute((const void*)jet_bwd_x6p<4, NT, S, LAP>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)lds_p4);
+    }
     attr = true;
   }
-  hipLaunchKernelGGL((jet_bwd_x6p<NQ, NT, S, LAP>), dim3(tiles), dim3(512), lds_p, st, x, N, din, dout, L, prm, act, gy,
-                     gdy, glap, adj, small, Ps, f16dw ? zmax : nullptr);
+  bool launched = false;
+  if constexpr (NQ == 3) {
+    if (f16p) {
+      hipLaunchKernelGGL((jet_bwd_x6p<4, NT, S, LAP>), dim3(tiles), dim3(512), lds_p4, st, x, N, din, dout, L, prm, act,
+                         gy, gdy, glap, adj, small, Ps, f16dw ? zmax : nullptr);
+      launched = true;
+    }
+  }
+  if (!launched)
+    hipLaunchKernelGGL((jet_bwd_x6p<NQ, NT, S, LAP>), dim3(tiles), dim3(512), lds_p, st, x, N, din, dout, L, prm, act,
+                       gy, gdy, glap, adj, small, Ps, f16dw ? zmax : nullptr);
   const int rs = tiles < kSmallRS ? tiles : kSmallRS;
   const int rows_x = (int)((Ps + 63) / 64);
   if (L > 0) {  // 3 launches: propagation | dW partials + compact rows level 1 | dW sums + rows level 2

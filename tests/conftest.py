@@ -13,3 +13,12 @@ for p in (ROOT, PKG):
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (HIP path); run with -m gpu")
     config.addinivalue_line("markers", "slow: longer CPU test")
+
+
+def pytest_sessionstart(session):
+    """INSR_TEST_BWD_F16=<mask>: run the suite with that insr_jet_set_bwd_f16 mask (A/B of a
+    default before it is made one; test infrastructure only)."""
+    mask = os.environ.get("INSR_TEST_BWD_F16")
+    if mask is not None:
+        import base
+        base._native.load().insr_jet_set_bwd_f16(int(mask))

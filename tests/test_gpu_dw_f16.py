@@ -1,9 +1,9 @@
-"""The two-kernel backward's dW GEMM on the fp16 matrix cores (insr_jet_set_dw_precision(1)).
+"""The x6 backward's products on the fp16 matrix cores (insr_jet_set_bwd_f16): the two-kernel
+path's dW GEMM and propagation, the fused tile-split kernel.
 
 f16x3 (two fp16 terms per operand, three products) keeps 22 significant bits but fp16's narrow
-range: each K slice scales its adjoints by the power of two that maps the slice's largest |z̄|
-(the propagation kernel's per-tile maxima) into [2^14, 2^15) and undoes it exactly on its
-partial.  Held to the parity tolerance (1e-5 normwise per parameter tensor vs the CPU oracle) for
+range: each dW K slice / propagated tile / fused block scales its adjoints by the power of two
+that maps its largest |z̄| into [2^14, 2^15) and undoes it exactly on its output.  Held to the parity tolerance (1e-5 normwise per parameter tensor vs the CPU oracle) for
 the Laplacian, gradient and value jets of the fluid nets through the two-kernel path, the 5x256
 elasticity3Dbunny net, and adjoint seeds scaled by 1e-12 and 1e12 (the scale is found per slice,
 so fp16's range never binds the adjoints).
@@ -18,16 +18,18 @@ pytestmark = pytest.mark.gpu
 TOL = 1e-5
 
 
-@pytest.fixture(scope="module")
-def B():
+# (INSR_BWD_F16_* mask, backward-path policy): the two-kernel path's dW, its propagation, both;
+# the fused tile-split kernel (policy 1: fused wherever it exists -- W = 256 stays two-kernel)
+@pytest.fixture(scope="module", params=[(1, 2), (2, 2), (3, 2), (4, 1), (7, 0)])
+def B(request):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     import base
     lib = base._native.load()
-    old_dw = lib.insr_jet_set_dw_precision(1)
-    old_pol = lib.insr_jet_set_bwd_policy(2)  # the two-kernel path wherever it exists
+    old_dw = lib.insr_jet_set_bwd_f16(request.param[0])
+    old_pol = lib.insr_jet_set_bwd_policy(request.param[1])
     yield base
-    lib.insr_jet_set_dw_precision(old_dw)
+    lib.insr_jet_set_bwd_f16(old_dw)
     lib.insr_jet_set_bwd_policy(old_pol)
 
 

@@ -126,9 +126,9 @@ def test_wsplit_planes_are_the_exact_three_term_split(B):
 
 
 def test_wsplit_fp16_planes_are_the_scaled_two_term_split(B):
-    """The fp16 forward planes (INSR_PREC_F16X3, after both bf16 orientations) hold 2^8 w as
-    fp16 terms h + l == 2^8 w to 2^-22 relative, in the forward (W_j rows) fragment order --
-    written by insr_siren_wsplit and, after an optimiser step, by the Adam launch."""
+    """The fp16 planes (INSR_PREC_F16X3, after both bf16 orientations) hold 2^8 w as fp16 terms
+    h + l == 2^8 w to 2^-22 relative, in the forward (W_j rows) and then the backward (W_j^T rows)
+    fragment order -- written by insr_siren_wsplit and, after an optimiser step, by the Adam launch."""
     torch.manual_seed(4)
     net = B.MLP(2, 2, 2, 64, nonlinearity="sine").cuda()
     opt = B.FusedAdam([{"params": net.parameters(), "module": net, "lr": 1e-2}])
@@ -143,18 +143,22 @@ def test_wsplit_fp16_planes_are_the_scaled_two_term_split(B):
             net.refresh_wsplit()
         torch.cuda.synchronize()
         store = net.flat_params()._base
-        h16 = store[net.wsplit_offset() + 3 * L * W * W:].view(torch.float16).cpu().double()
-        for j in (1, 2):
-            Wj = net.net[2 * j].weight.detach().cpu().double() * 256.0
-            for rt in range(NT):
-                for kc in range(KC):
-                    fr = ((j - 1) * NT + rt) * KC + kc
-                    for lane in (0, 17, 63):
-                        g, c = lane >> 4, lane & 15
-                        hi = h16[((fr * 2) * 64 + lane) * 8:((fr * 2) * 64 + lane) * 8 + 8]
-                        lo = h16[((fr * 2 + 1) * 64 + lane) * 8:((fr * 2 + 1) * 64 + lane) * 8 + 8]
-                        want = Wj[16 * rt + c, [32 * kc + 8 * g + jj for jj in range(8)]]
-                        assert torch.allclose(hi + lo, want, rtol=2.0 ** -21, atol=2.0 ** -24), (step, j, rt, kc, lane)
+        for o in (0, 1):
+            h16 = store[net.wsplit_offset() + (3 + o) * L * W * W:].view(torch.float16).cpu().double()
+            for j in (1, 2):
+                Wj = net.net[2 * j].weight.detach().cpu().double() * 256.0
+                if o:
+                    Wj = Wj.t()
+                for rt in range(NT):
+                    for kc in range(KC):
+                        fr = ((j - 1) * NT + rt) * KC + kc
+                        for lane in (0, 17, 63):
+                            g, c = lane >> 4, lane & 15
+                            hi = h16[((fr * 2) * 64 + lane) * 8:((fr * 2) * 64 + lane) * 8 + 8]
+                            lo = h16[((fr * 2 + 1) * 64 + lane) * 8:((fr * 2 + 1) * 64 + lane) * 8 + 8]
+                            want = Wj[16 * rt + c, [32 * kc + 8 * g + jj for jj in range(8)]]
+                            assert torch.allclose(hi + lo, want, rtol=2.0 ** -21, atol=2.0 ** -24), \
+                                (step, o, j, rt, kc, lane)
 
 
 def test_f16x3_forward_matches_x6_to_fp32_level(B):

@@ -57,14 +57,14 @@ def main():
     ap.add_argument("--variants", default=",".join(VARIANTS))
     ap.add_argument("--policies", default="0", help="backward-path policies (insr_jet_set_bwd_policy) to time")
     ap.add_argument("--bwd-only", action="store_true", help="time only the backward into .grad")
-    ap.add_argument("--dw-f16", type=int, default=-1, help="insr_jet_set_dw_precision (-1: library default)")
+    ap.add_argument("--bwd-f16", type=int, default=-1, help="insr_jet_set_bwd_f16 mask (-1: library default)")
     ap.add_argument("--lib", default=None, help="alternative build of libinsr_hip.so (flag studies)")
     args = ap.parse_args()
     import base
     from base import _native as nat
     lib = nat.load(args.lib, check_build=args.lib is None)
-    if args.dw_f16 >= 0:
-        lib.insr_jet_set_dw_precision(args.dw_f16)
+    if args.bwd_f16 >= 0:
+        lib.insr_jet_set_bwd_f16(args.bwd_f16)
     out = []
     for name in args.nets.split(","):
         din, dout, L, W = NETS[name]
