@@ -323,7 +323,7 @@ def roofline(loops, n_local, precision="fp32"):
         name = f"{k[0]}:{k[1]}:n{k[2]}:{k[4][0]}-{k[3]}x{k[4][2]}-{k[4][1]}"
         table[name] = round(table.get(name, 0.0) + v, 4)
     nq = PRECISION[precision][2]
-    kname, grid, x6 = kernel_identity(kind, mode, n, din, dout, L, W, nq)
+    kname, grid, x6, np_run = kernel_identity(kind, mode, n, din, dout, L, W, nq)
     traffic, tsrc = pmc_traffic(kname, grid)
     peak = FP32_MFMA_PEAK_TFLOPS if precision == "fp32" else BF16_MFMA_PEAK_TFLOPS
     out = {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
@@ -332,47 +332,63 @@ def roofline(loops, n_local, precision="fp32"):
            "kernel": f"{kname}{'' if isinstance(grid, list) else f' grid={grid}'} (n={n}, {din}->{dout} {L}x{W}, {mode} jet {kind})", "avg_ms": round(ms, 4),
            "algorithmic_gflop_per_launch": round(flops / 1e9, 3), "per_step_ms_by_launch": table}
     if x6:
-        # the kernel runs split-bf16 products: NP x v_mfma_f32_16x16x32_bf16 (16 cyc) per 16x16x32 fp32-equivalent
-        # MAC block (NP = 6 / 3 / 1): 16*16*32 / (16 NP) MAC/clk/SIMD vs 32 for v_mfma_f32_16x16x4_f32
-        np_ = PRECISION[precision][1]
+        # the kernel runs split products: NP x v_mfma_f32_16x16x32_{bf16,f16} (16 cyc) per 16x16x32 fp32-equivalent
+        # MAC block (NP = 6 bf16x6 / 3 f16x3 or bf16x3 / 1): 16*16*32 / (16 NP) MAC/clk/SIMD vs 32 for
+        # v_mfma_f32_16x16x4_f32 -- the ceiling of the products the launch actually ran
+        np_ = np_run
         ceil = round(FP32_MFMA_PEAK_TFLOPS * (16 * 16 * 32 / (16.0 * np_)) / 32.0, 1)
         out["products_per_mac"] = np_
         out["precision_ceiling"] = ceil
         out["frac_of_precision_ceiling"] = round(achieved / ceil, 4)
         if precision == "fp32":
-            out["x6_ceiling"] = ceil
-            out["frac_of_x6_ceiling"] = out["frac_of_precision_ceiling"]
+            x6c = round(FP32_MFMA_PEAK_TFLOPS * (16 * 16 * 32 / (16.0 * 6)) / 32.0, 1)
+            out["x6_ceiling"] = x6c
+            out["frac_of_x6_ceiling"] = round(achieved / x6c, 4)
     return out
 
 
 def kernel_identity(kind, mode, n, din, dout, L, W, nq=3):
-    """The rocprof name and grid (threads) of the jet kernel the library picks for this launch."""
+    """The rocprof name and grid (threads) of the jet kernel the library picks for this launch, and
+    the split products per fp32-equivalent MAC it runs (6 bf16x6, 3 f16x3 / bf16x3, 1 bf16).
+    nq = 3 (the fp32-level precision): the forward runs f16x3 (template NQ = 4), the backward's
+    products per the insr_jet_set_bwd_f16 mask (NQ = 4 where on)."""
     from base import _native as nat
     lib = nat.lib()
     prec = {3: nat.PREC_BF16X6, 2: nat.PREC_BF16X3, 1: nat.PREC_BF16}[nq]
-    m = {"value": nat.MODE_VALUE, "grad": nat.MODE_GRAD, "lap": nat.MODE_LAP}[mode] | nat.jet_prec(prec)
+    m = {"value": nat.MODE_VALUE, "grad": nat.MODE_GRAD, "lap": nat.MODE_LAP}[mode]
+    m_b = m | nat.jet_prec(prec)
     S = {"value": 1, "grad": 1 + din, "lap": 2 + din}[mode]
     NT = W // 16
     lap = "true" if mode == "lap" else "false"
-    path = lib.insr_jet_bwd_path(n, din, dout, L, W, m) if kind == "bwd" else 0
+    f16 = lib.insr_jet_set_bwd_f16(-1) if nq == 3 else 0
+    nprod = {4: 3, 3: 6, 2: 3, 1: 1}
+    path = lib.insr_jet_bwd_path(n, din, dout, L, W, m_b) if kind == "bwd" else 0
     if path == 2:  # the resident-dW persistent kernel + the fixed-order sums
         import ctypes
         thr = (ctypes.c_long * 3)()
-        nat.check(lib.insr_jet_wide_launch_threads(n, din, dout, L, W, m, thr), "insr_jet_wide_launch_threads")
+        nat.check(lib.insr_jet_wide_launch_threads(n, din, dout, L, W, m_b, thr), "insr_jet_wide_launch_threads")
         parts = [(f"insr::jet_bwd_x6r<{nq}, {S}, {lap}, {L}, 1>", thr[0]), ("insr::reduce_dw_kernel", thr[1])]
         return " + ".join(f"{k}|grid={g}" for k, g in parts) + " (resident-dW backward: persistent tile loop, " \
-            "then the dW / compact-row sums; time = both launches)", parts, True
+            "then the dW / compact-row sums; time = both launches)", parts, True, nprod[nq]
     if path == 1:  # two kernels + the dW sums
         import ctypes
         thr = (ctypes.c_long * 3)()
-        nat.check(lib.insr_jet_wide_launch_threads(n, din, dout, L, W, m, thr), "insr_jet_wide_launch_threads")
-        parts = [(f"insr::jet_bwd_x6p<{nq}, {NT}, {S}, {lap}>", thr[0]), (f"insr::dw_x6<{nq}, {NT}, {S}, {lap}>", thr[1]),
+        nat.check(lib.insr_jet_wide_launch_threads(n, din, dout, L, W, m_b, thr), "insr_jet_wide_launch_threads")
+        qp, qd = (4 if f16 & 2 else nq), (4 if f16 & 1 else nq)
+        parts = [(f"insr::jet_bwd_x6p<{qp}, {NT}, {S}, {lap}>", thr[0]), (f"insr::dw_x6<{qd}, {NT}, {S}, {lap}>", thr[1]),
                  ("insr::reduce_dw_kernel", thr[2])]
         return " + ".join(f"{k}|grid={g}" for k, g in parts) + " (two-kernel backward: propagation, dW GEMM + row partials, sums; time = all three launches)", \
-            parts, True
-    T = lib.insr_jet_split_tiles(n, din, W, m, 1 if kind == "bwd" else 0)
-    nb = ((n + 15) // 16 + T - 1) // T
-    return f"insr::jet_{kind}_x6<{nq}, {NT}, {S}, {lap}, {T}>", nb * 64 * min(NT, 8), True
+            parts, True, max(nprod[qp], nprod[qd])
+    if kind == "bwd":
+        T = lib.insr_jet_split_tiles(n, din, W, m_b, 1)
+        nb = lib.insr_jet_partial_blocks(n, din, W, m_b)
+        q = 4 if f16 & 4 else nq
+    else:
+        mf = m if nq == 3 else m_b  # the process-default forward precision (f16x3) serves the fp32-level runs
+        T = lib.insr_jet_split_tiles(n, din, W, mf, 0)
+        nb = ((n + 15) // 16 + T - 1) // T
+        q = 4 if nq == 3 else nq
+    return f"insr::jet_{kind}_x6<{q}, {NT}, {S}, {lap}, {T}>", nb * 64 * min(NT, 8), True, nprod[q]
 
 
 def pmc_traffic(kname, grid):

@@ -6,8 +6,9 @@ RCCL needs one GPU per rank); each takes half of the reference golden sample set
 
 Checks, 4 iterations of each fluid phase (_advect_velocity, _solve_pressure, _projection):
   * graph DP == eager DP bit for bit (parameters and the synced loss trace);
-  * DP == the single-process full-batch run: losses at 1e-5 relative, Adam updates as in
-    test_gpu_phases.check_update (Adam's first steps are ~lr sign(g));
+  * DP == the single-process full-batch run: the first iteration's losses at 1e-5 relative, later
+    ones at 5e-5 (after Adam steps), Adam updates as in test_gpu_phases.check_update (Adam's first
+    steps are ~lr sign(g));
   * rank 0 == rank 1 bit for bit (replicated optimiser, no parameter broadcast).
 Plus the launcher itself: `bench.py --gpus 2 --backend gloo` as a subprocess."""
 import json
@@ -124,9 +125,13 @@ def test_two_rank_graph_dp_equals_eager_and_full_batch():
     assert np.array_equal(v_g, v_e) and np.array_equal(p_g, p_e)
     for phase in PHASES:
         assert tr_g[phase] == tr_e[phase] and len(tr_g[phase]) == ITERS, phase
-        for got, want in zip(tr_g[phase], full[0][phase]):
+        for it, (got, want) in enumerate(zip(tr_g[phase], full[0][phase])):
+            # iteration 0: the same parameters, gradients summed in another order -> 1e-5; later
+            # iterations follow Adam steps whose noise-floor entries (~lr sign(g)) may differ
+            # (_check_update bounds them), so their losses are held to 5e-5
+            tol = 1e-5 if it == 0 else 5e-5
             for k in want:
-                assert abs(got[k] - want[k]) <= 1e-5 * abs(want[k]) + 1e-12, (phase, k, got[k], want[k])
+                assert abs(got[k] - want[k]) <= tol * abs(want[k]) + 1e-12, (phase, it, k, got[k], want[k])
     _check_update(v_g, ph["fluid/vel/params0"], full[1])
     _check_update(p_g, ph["fluid/pres/params0"], full[2])
 

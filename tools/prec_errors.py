@@ -31,11 +31,15 @@ def main():
     ap.add_argument("--nets", default=",".join(NETS))
     ap.add_argument("--combos", default="0:0,1:1,2:2,3:3",
                     help="forward:backward precision pairs (0 fp32, 1 bf16x6, 2 bf16x3, 3 bf16), comma separated")
+    ap.add_argument("--bwd-f16", type=int, default=-1, help="insr_jet_set_bwd_f16 mask (-1: library default)")
     args = ap.parse_args()
     combos = [tuple(int(v) for v in c.split(":")) for c in args.combos.split(",")]
     names = ["f32", "bf16x6", "bf16x3", "bf16", "f16x3"]
     import base
-    base._native.load()
+    lib = base._native.load()
+    if args.bwd_f16 >= 0:
+        lib.insr_jet_set_bwd_f16(args.bwd_f16)
+    mask = lib.insr_jet_set_bwd_f16(-1)
     for name in args.nets.split(","):
         din, dout, L, W = NETS[name]
         torch.manual_seed(0)
@@ -66,6 +70,7 @@ def main():
                 pe = [nerr(p.grad if p.grad is not None else torch.zeros_like(p), g)
                       for p, g in zip(net.parameters(), gref)]
                 print(json.dumps({"net": name, "op": op, "prec": names[pf] if pf == pb else f"{names[pf]}/{names[pb]}", "n": args.n,
+                                  "bwd_f16": mask,
                                   "field_err": nerr(v, vr), "param_grad_err_max": max(pe),
                                   "param_grad_err": [round(e, 9) for e in pe]}), flush=True)
 
