@@ -43,11 +43,16 @@ bool resident_ok(int S, int NT, bool lap, int nq, int L) {
   if (NT != 8 || nq != 3 || L != 4) return false;
   return (S == 1 && !lap) || (S == 3 && !lap) || (S == 4 && lap);
 }
+// Round 3: with the two-kernel path's products on the fp16 matrix cores (INSR_BWD_F16_DW | PROP;
+// the resident kernel stays bf16x6) the two-kernel Laplacian backward wins at the fluid2DtlgnM batch
+// (66,844 points: 553-561 vs 590-601 us; value jets tie at 199-205, profiles/r03/final_r3o/
+// kbench_policy_M.jsonl), so the auto policy keeps the resident kernel for value jets only then.
 bool use_resident(long n, int S, int NT, bool lap, int nq, int L) {
   if (!resident_ok(S, NT, lap, nq, L)) return false;
   if (g_bwd_policy == 3) return true;
   if (g_bwd_policy != 0) return false;
-  return lap ? n >= 32768 : (S == 1 && n >= 49152);
+  const bool f16w = (g_bwd_f16 & (INSR_BWD_F16_DW | INSR_BWD_F16_PROP)) == (INSR_BWD_F16_DW | INSR_BWD_F16_PROP);
+  return lap ? (!f16w && n >= 32768) : (S == 1 && n >= 49152);
 }
 
 // Tiles per tile-split block.  The largest T in {1, 2, 4} whose LDS fits a CU,

@@ -84,11 +84,15 @@ __global__ __launch_bounds__(256) void wsplit_kernel(const float* __restrict__ p
 // ---------------------------------------------------------------------------------------
 // W = 128: held to 128 VGPRs (4 waves per SIMD = two 8-wave blocks per CU; its 52 KB of LDS
 // allow three) -- the one-tile sweep is latency-bound, a second resident block hides it
-template <int NT>
-constexpr int x6p_min_waves() { return NT == 8 ? 4 : 1; }
+// (the f16x3 variant: INSR_F16_BWD_WAVES waves per SIMD, A/B builds only)
+#ifndef INSR_F16_BWD_WAVES
+#define INSR_F16_BWD_WAVES 4
+#endif
+template <int NQ, int NT>
+constexpr int x6p_min_waves() { return NT == 8 ? (NQ == 4 ? INSR_F16_BWD_WAVES : 4) : 1; }
 
 template <int NQ, int NT, int S, bool LAP>
-__global__ __launch_bounds__(512, (x6p_min_waves<NT>())) void jet_bwd_x6p(const float* __restrict__ x, int N, int din, int dout, int L,
+__global__ __launch_bounds__(512, (x6p_min_waves<NQ, NT>())) void jet_bwd_x6p(const float* __restrict__ x, int N, int din, int dout, int L,
                                                    const float* __restrict__ prm, const float* __restrict__ act,
                                                    const float* __restrict__ gy, const float* __restrict__ gdy,
                                                    const float* __restrict__ glap, float* __restrict__ adj,
@@ -383,7 +387,7 @@ __device__ __forceinline__ void rows_level1(const float* __restrict__ part, int 
 // [2^14, 2^15) -- exact, undone on the partial -- and h enters as the forward's f16x3 does (value and
 // tangent streams unscaled, the Laplacian stream x 2^-4, its z̄ x 2^4: every product keeps 2^e).
 template <int NQ, int NT, int S, bool LAP>
-__global__ __launch_bounds__(512) void dw_x6(int N, const float* __restrict__ act, const float* __restrict__ adj,
+__global__ __launch_bounds__(512, (NQ == 4 && NT == 8) ? INSR_F16_BWD_WAVES : 1) void dw_x6(int N, const float* __restrict__ act, const float* __restrict__ adj,
                                              float* __restrict__ dpart, int KS, int L, const float* __restrict__ small,
                                              int tiles, long Ps, float* __restrict__ rows, int rs, int rows_x,
                                              const float* __restrict__ zmax) {

@@ -184,7 +184,11 @@ def test_backward_path_policy(lib):
         assert lib.insr_jet_bwd_path(16708, 2, 1, 4, 128, LAP) == 1
         assert lib.insr_jet_bwd_path(16708, 2, 2, 4, 128, V) == 0
         assert lib.insr_jet_bwd_path(1024, 2, 2, 4, 128, V) == 0
-        assert lib.insr_jet_bwd_path(65536 + 1308, 2, 1, 4, 128, LAP) == 2  # fluid2DtlgnM: resident
+        # fluid2DtlgnM: the two-kernel f16x3 Laplacian backward (resident when its products are bf16x6)
+        assert lib.insr_jet_bwd_path(65536 + 1308, 2, 1, 4, 128, LAP) == 1
+        old_f16 = lib.insr_jet_set_bwd_f16(0)
+        assert lib.insr_jet_bwd_path(65536 + 1308, 2, 1, 4, 128, LAP) == 2
+        lib.insr_jet_set_bwd_f16(old_f16)
         assert lib.insr_jet_bwd_path(65536 + 1308, 2, 2, 4, 128, V) == 2
         assert lib.insr_jet_bwd_path(33092, 2, 2, 4, 128, V) == 0
         assert lib.insr_jet_bwd_path(32768, 3, 3, 5, 256, G) == 1

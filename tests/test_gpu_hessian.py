@@ -96,3 +96,30 @@ def test_hessian_3d_input_refused():
     x = torch.rand(10, 3, device="cuda").requires_grad_(True)
     with pytest.raises(B.UnsupportedPattern):
         B.hessian(net(x), x)
+
+
+@pytest.mark.parametrize("scale_x,scale_w0", [(4.0, 1.0), (1.0, 3.0), (8.0, 3.0)])
+def test_hessian_polarisation_off_domain_and_high_frequency(scale_x, scale_w0):
+    """The d_in = 2 Hessian subtracts Laplacian jets of similar size ((Lap_aug(8v) - tr H) / 64).
+    Stress: points up to |x| = 8 (outside the [-1, 1]^2 training box) and a first layer scaled x3
+    (3x the spatial frequencies: second derivatives x9); judged against fp64 autograd of the
+    oracle, the HIP error must stay within 5x the oracle's own fp32 autograd error (or 1e-5)."""
+    import copy
+    import base as B
+    torch.manual_seed(17)
+    net = B.MLP(2, 1, 4, 128, nonlinearity="sine").cuda()
+    with torch.no_grad():
+        net.net[0].weight.mul_(scale_w0)
+    ref32 = O.OracleSiren(2, 1, 4, 128)
+    ref32.load_state_dict({k: v.detach().cpu() for k, v in net.state_dict().items()})
+    ref64 = copy.deepcopy(ref32).double()
+    x = (torch.rand(512, 2, generator=torch.Generator().manual_seed(18)) * 2 - 1) * scale_x
+    xg = x.cuda().requires_grad_(True)
+    h, st = B.hessian(net(xg), xg)
+    x64 = x.double().requires_grad_(True)
+    h64, _ = O.op_hessian(ref64(x64), x64)
+    x32 = x.clone().requires_grad_(True)
+    h32, _ = O.op_hessian(ref32(x32), x32)
+    e_hip = nerr(h.detach().cpu(), h64.detach())
+    e32 = nerr(h32.detach(), h64.detach())
+    assert st == 0 and e_hip <= max(5 * e32, 1e-5), (e_hip, e32)
