@@ -180,7 +180,8 @@ struct X6Geo {
 template <int NQ, int NT, int S, int T>
 constexpr size_t fwd_x6_lds_bytes() {
   using G = X6Geo<NT>;
-  const size_t planes = (size_t)T * S * np_of<NQ>() * G::PLANE * 2;
+  // f16x3: + [2][T][S][waves] floats after the planes (the per-tile stream maxima, fwd_x6_block)
+  const size_t planes = (size_t)T * S * np_of<NQ>() * G::PLANE * 2 + (NQ == 4 ? 2 * T * S * 8 * sizeof(float) : 0);
   const size_t red = (size_t)G::WV * T * S * 3 * 16 * sizeof(float);  // output-layer combine
   return planes > red ? planes : red;
 }
@@ -210,17 +211,20 @@ __device__ __forceinline__ FragQ<NQ> wsp_frag(const u32x4* __restrict__ wsp, int
   return f;
 }
 
-// f16x3 (NQ = 4) stream scales: the Laplacian stream (|ddh| ~ w^2 |t|^2, thousands) enters the
-// fp16 products x 2^-4, the value (sin) and tangent streams unscaled; an output stream of the
-// products is unscaled by 2^-8 (the weights' scale) x the input stream's inverse scale
-template <bool LAP, int S>
-__device__ __forceinline__ constexpr float f16_stream_scale(int s) {
-  return (LAP && s == S - 1) ? 0.0625f : 1.f;
+// f16x3 (NQ = 4) operand scales of the forward: the value stream (sin, |h| <= 1) enters the fp16
+// products unscaled; the tangent and Laplacian streams (|dh| <= w |t|, |ddh| <= w |q| + w^2 sum t^2:
+// no a-priori bound) are scaled per tile and stream by the power of two 2^e that maps the bound's
+// maximum into [2^14, 2^15) (fwd_x6_block); the products are unscaled by 2^-8 (the weights' scale)
+// x 2^-e -- all exact
+__device__ __forceinline__ int f16_exp_for(float m) {  // 2^e maps m into [2^14, 2^15); 0 for 0 / inf / NaN
+  if (!(m > 0.f && m <= 3.0e38f)) return 0;
+  int k;
+  (void)frexpf(m, &k);
+  return min(max(15 - k, -100), 100);
 }
-template <bool LAP, int S>
-__device__ __forceinline__ constexpr float f16_unscale(int s) {
-  return (LAP && s == S - 1) ? 16.f / kF16WScale : 1.f / kF16WScale;
-}
+// the static factor of the backward's h Laplacian stream (H planes, dW B operand): h x 2^-10, its z̄
+// x 2^10 (the dynamic z̄ scale absorbs it) -- fp16's range then holds |h_lap| < 6.7e7 (|t| < ~270)
+constexpr float kF16LapB = 1024.f;
 
 // Balanced tiles per block: with nbal > 0 the tiles of a batch are split over nbal blocks as
 // evenly as possible (block b: tiles [b tiles / nbal, (b + 1) tiles / nbal), at most T), so a
@@ -257,6 +261,14 @@ __device__ __forceinline__ void fwd_x6_block(const float* __restrict__ x, int N,
   const int ntiles = ((N + 63) / 64) * 4;
   const int rt0 = wave * RPW;
   const u32x4* wsp = wsp_base(prm, din, dout, L, W);
+  // f16x3: per-(tile, stream) maxima of the waves [2][T][S][8] after the planes, and the unscale of
+  // the next layer's products per (tile, stream)
+  float* zmx = lds_f + (T * S * np_of<NQ>() * PLANE) / 2;
+  float usc[T][S];
+#pragma unroll
+  for (int t = 0; t < T; ++t)
+#pragma unroll
+    for (int s = 0; s < S; ++s) usc[t][s] = 1.f / kF16WScale;
 
   float xv[T][3];
 #pragma unroll
@@ -323,11 +335,41 @@ __device__ __forceinline__ void fwd_x6_block(const float* __restrict__ x, int N,
 #pragma unroll
           for (int t = 0; t < T; ++t)
 #pragma unroll
-            for (int s = 0; s < S; ++s) a[t][i][s] *= f16_unscale<LAP, S>(s);
+            for (int s = 0; s < S; ++s) a[t][i][s] *= usc[t][s];
         }
       }
-      __syncthreads();  // every wave has read layer j-1
     }
+    // f16x3: this wave's bounds of |h| per (tile, stream) for the planes of layer j (before the
+    // barrier the next layer's operand writes wait on anyway; j = 0 adds one)
+    if constexpr (NQ == 4 && S > 1) {
+      if (j < L) {
+#pragma unroll
+        for (int t = 0; t < T; ++t) {
+          float mt[S];
+#pragma unroll
+          for (int s = 0; s < S; ++s) mt[s] = 0.f;
+#pragma unroll
+          for (int i = 0; i < RPW; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              float t2 = 0.f;
+#pragma unroll
+              for (int k = 0; k < NTAN; ++k) {
+                const float tk = a[t][i][1 + k][r];
+                mt[1 + k] = fmaxf(mt[1 + k], OMEGA * fabsf(tk));
+                t2 = fmaf(tk, tk, t2);
+              }
+              if constexpr (LAP) mt[S - 1] = fmaxf(mt[S - 1], fmaf(OMEGA, fabsf(a[t][i][S - 1][r]), OMEGA2 * t2));
+            }
+#pragma unroll
+          for (int s = 1; s < S; ++s) {
+            const float m = wave_max(mt[s]);
+            if (lane == 0) zmx[(((j & 1) * T + t) * S + s) * 8 + wave] = m;
+          }
+        }
+      }
+    }
+    if (j > 0 || (NQ == 4 && S > 1)) __syncthreads();  // every wave has read layer j-1 (and wrote its bounds)
     if (act) {
 #pragma unroll
       for (int t = 0; t < T; ++t) {
@@ -343,6 +385,24 @@ __device__ __forceinline__ void fwd_x6_block(const float* __restrict__ x, int N,
 #pragma unroll
     for (int t = 0; t < T; ++t) sine_jet<RPW, S, LAP>(a[t]);
     if (j < L) {
+      float scl[T][S];  // this layer's operand scales (value stream 1)
+#pragma unroll
+      for (int t = 0; t < T; ++t)
+#pragma unroll
+        for (int s = 0; s < S; ++s) {
+          scl[t][s] = 1.f;
+          usc[t][s] = 1.f / kF16WScale;
+          if constexpr (NQ == 4) {
+            if (s > 0) {
+              float m = zmx[(((j & 1) * T + t) * S + s) * 8];
+#pragma unroll
+              for (int w = 1; w < WV; ++w) m = fmaxf(m, zmx[(((j & 1) * T + t) * S + s) * 8 + w]);
+              const int e = f16_exp_for(m);
+              scl[t][s] = ldexpf(1.f, e);
+              usc[t][s] = ldexpf(1.f, -e) / kF16WScale;
+            }
+          }
+        }
 #pragma unroll
       for (int t = 0; t < T; ++t)
 #pragma unroll
@@ -350,7 +410,7 @@ __device__ __forceinline__ void fwd_x6_block(const float* __restrict__ x, int N,
 #pragma unroll
           for (int s = 0; s < S; ++s) {
             unsigned short* pw = lds + (t * S + s) * np_of<NQ>() * PLANE + c * LDB + 16 * (rt0 + i) + 4 * g;
-            const float sc = NQ == 4 ? f16_stream_scale<LAP, S>(s) : 1.f;
+            const float sc = scl[t][s];
             lds_put4<NQ, PLANE>(pw, sc * a[t][i][s][0], sc * a[t][i][s][1], sc * a[t][i][s][2], sc * a[t][i][s][3]);
           }
       __syncthreads();
@@ -998,7 +1058,7 @@ __global__ __launch_bounds__(X6Geo<NT>::THREADS) void jet_bwd_x6(const BwdJobsX6
 #pragma unroll
           for (int s = 0; s < S; ++s)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) m = fmaxf(m, fabsf(hb[t][i][s][r]) * ((LAP && s == S - 1) ? 16.f : 1.f));
+            for (int r = 0; r < 4; ++r) m = fmaxf(m, fabsf(hb[t][i][s][r]) * ((LAP && s == S - 1) ? kF16LapB : 1.f));
       m = wave_max(m);
       if (lane == 0) zred[(j & 1) * 8 + wave] = m;  // two slots: layer j - 1 writes the other
     }
@@ -1054,7 +1114,7 @@ __global__ __launch_bounds__(X6Geo<NT>::THREADS) void jet_bwd_x6(const BwdJobsX6
             const int u = t * SG + sl;
             const int col = 16 * (rt0 + i) + 4 * g;
             const bool lq = NQ == 4 && LAP && s == S - 1;  // the fp16 Laplacian-stream scales
-            const float fz = lq ? 16.f * zsc : zsc;
+            const float fz = lq ? kF16LapB * zsc : zsc;
             lds_put4<NQ, ZPLANE>(Z + u * ZSET + c * LDB + col, hb[t][i][s][0] * fz, hb[t][i][s][1] * fz,
                                  hb[t][i][s][2] * fz, hb[t][i][s][3] * fz);
             floatx4 hs;
@@ -1063,7 +1123,7 @@ __global__ __launch_bounds__(X6Geo<NT>::THREADS) void jet_bwd_x6(const BwdJobsX6
             } else {
               hs = h_stream<NT, S, LAP>(basep, s, rt0 + i, lane, snp[t][i], csp[t][i]);
             }
-            if (lq) hs *= 0.0625f;
+            if (lq) hs *= 1.f / kF16LapB;
             put_neuron_major<NQ, HPLANE>(H + u * HSET, hs, col, c);
           }
       }
@@ -1157,7 +1217,7 @@ __global__ __launch_bounds__(X6Geo<NT>::THREADS) void jet_bwd_x6(const BwdJobsX6
         cs[t][i] = csp[t][i];
 #pragma unroll
         for (int s = 0; s < S; ++s)
-          hb[t][i][s] = (NQ == 4) ? nh[t][i][s] * (((LAP && s == S - 1) ? 0.0625f : 1.f) * zun / kF16WScale)
+          hb[t][i][s] = (NQ == 4) ? nh[t][i][s] * (((LAP && s == S - 1) ? 1.f / kF16LapB : 1.f) * zun / kF16WScale)
                                   : nh[t][i][s];
       }
   }

@@ -237,7 +237,7 @@ __global__ __launch_bounds__(512, (x6p_min_waves<NQ, NT>())) void jet_bwd_x6p(co
 #pragma unroll
         for (int s = 0; s < S; ++s)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) m = fmaxf(m, fabsf(hb[i][s][r]) * ((LAP && s == S - 1) ? 16.f : 1.f));
+          for (int r = 0; r < 4; ++r) m = fmaxf(m, fabsf(hb[i][s][r]) * ((LAP && s == S - 1) ? kF16LapB : 1.f));
       m = wave_max(m);
       if (lane == 0) zred[(j & 1) * 8 + wave] = m;  // two slots: layer j - 1 writes the other
     }
@@ -260,7 +260,7 @@ __global__ __launch_bounds__(512, (x6p_min_waves<NQ, NT>())) void jet_bwd_x6p(co
     for (int i = 0; i < RPW; ++i)
 #pragma unroll
       for (int s = 0; s < S; ++s) {
-        const float f = (NQ == 4 && LAP && s == S - 1) ? 16.f * zsc : zsc;
+        const float f = (NQ == 4 && LAP && s == S - 1) ? kF16LapB * zsc : zsc;
         lds_put4<NQ, ZPLANE>(Z + s * ZSET + c * LDB + 16 * (rt0 + i) + 4 * g, hb[i][s][0] * f, hb[i][s][1] * f,
                              hb[i][s][2] * f, hb[i][s][3] * f);
       }
@@ -303,7 +303,7 @@ __global__ __launch_bounds__(512, (x6p_min_waves<NQ, NT>())) void jet_bwd_x6p(co
 #pragma unroll
     for (int i = 0; i < RPW; ++i)
 #pragma unroll
-      for (int s = 0; s < S; ++s) hb[i][s] = nh[i][s] * ((NQ == 4 && LAP && s == S - 1) ? 0.0625f * zun : zun);
+      for (int s = 0; s < S; ++s) hb[i][s] = nh[i][s] * ((NQ == 4 && LAP && s == S - 1) ? zun / kF16LapB : zun);
   }
 }
 
@@ -509,8 +509,8 @@ __global__ __launch_bounds__(512, (NQ == 4 && NT == 8) ? INSR_F16_BWD_WAVES : 1)
       const floatx4 zero = floatx4{0.f, 0.f, 0.f, 0.f};
       if constexpr (NQ == 4) {
         const bool lq = LAP && s == S - 1;
-        dw_put<NQ, NT>(A, live ? rzb[it] * (lq ? 16.f * asc : asc) : zero, rt, ul, lane);
-        dw_put<NQ, NT>(B, live ? (lq ? hv * 0.0625f : hv) : zero, rt, ul, lane);
+        dw_put<NQ, NT>(A, live ? rzb[it] * (lq ? kF16LapB * asc : asc) : zero, rt, ul, lane);
+        dw_put<NQ, NT>(B, live ? (lq ? hv * (1.f / kF16LapB) : hv) : zero, rt, ul, lane);
       } else {
         dw_put<NQ, NT>(A, live ? rzb[it] : zero, rt, ul, lane);
         dw_put<NQ, NT>(B, live ? hv : zero, rt, ul, lane);

@@ -161,17 +161,24 @@ def test_wsplit_fp16_planes_are_the_scaled_two_term_split(B):
                                 (step, o, j, rt, kc, lane)
 
 
-def test_f16x3_forward_matches_x6_to_fp32_level(B):
-    """The f16x3 forward (MLP(precision='f16x3')) against the default x6 forward of the same
-    weights: value, gradient and Laplacian jets agree to 1e-5 normwise."""
+@pytest.mark.parametrize("w0_scale", [1.0, 10.0, 40.0])
+def test_f16x3_forward_matches_x6_to_fp32_level(B, w0_scale):
+    """The f16x3 forward (MLP(precision='f16x3'), the default) against the bf16x6 forward of the
+    same weights: value, gradient and Laplacian jets agree to 1e-5 normwise -- also with the first
+    layer scaled x10 / x40 (tangents ~10-40x, Laplacians ~100-1600x the init's: the per-tile
+    dynamic scales of the tangent and Laplacian planes keep fp16 in range; the static 2^-4 of the
+    first version overflowed to inf there)."""
     torch.manual_seed(5)
-    a = B.MLP(2, 1, 4, 128, nonlinearity="sine").cuda()
+    a = B.MLP(2, 1, 4, 128, nonlinearity="sine", precision="bf16x6").cuda()
     b = B.MLP(2, 1, 4, 128, nonlinearity="sine", precision="f16x3").cuda()
+    with torch.no_grad():
+        a.net[0].weight.mul_(w0_scale)
     b.load_state_dict({k: v.clone() for k, v in a.state_dict().items()})
     x = torch.rand(3000, 2, device="cuda") * 2 - 1
     for net_out in (lambda n: n(x), lambda n: B.gradient(n(x.requires_grad_(True)), x),
                     lambda n: B.laplace(n(x.requires_grad_(True)), x)):
         u, v = net_out(a).detach(), net_out(b).detach()
+        assert torch.isfinite(v).all()
         assert float((u - v).abs().max() / u.abs().max()) < 1e-5
 
 
