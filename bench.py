@@ -83,6 +83,7 @@ def parse():
     ap.add_argument("--bwd-f16", type=int, default=-1, choices=list(range(-1, 8)),
                     help="x6 backward products on the fp16 matrix cores, INSR_BWD_F16_* mask (A/B studies; "
                          "-1 = library default)")
+    ap.add_argument("--lib", default=None, help="an alternative build of libinsr_hip.so (same-box A/B studies only)")
     ap.add_argument("--cpu-seconds", type=float, default=25.0, help="budget of the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
@@ -174,7 +175,7 @@ def interior_points(cfg, wl):
 def build_model(args, world, rank):
     import base
     from pde.config import baseline_config
-    base._native.load()
+    base._native.load(args.lib, check_build=args.lib is None)
     base._native.lib().insr_jet_set_bwd_policy(args.bwd_policy)
     base._native.lib().insr_jet_set_bwd_f16(args.bwd_f16)
     wl = WORKLOADS[args.config]

@@ -180,8 +180,8 @@ struct X6Geo {
 template <int NQ, int NT, int S, int T>
 constexpr size_t fwd_x6_lds_bytes() {
   using G = X6Geo<NT>;
-  // f16x3: + [2][T][S][waves] floats after the planes (the per-tile stream maxima, fwd_x6_block)
-  const size_t planes = (size_t)T * S * np_of<NQ>() * G::PLANE * 2 + (NQ == 4 ? 2 * T * S * 8 * sizeof(float) : 0);
+  // f16x3: + [2][T][waves] floats after the planes (the per-tile Laplacian-stream maxima, fwd_x6_block)
+  const size_t planes = (size_t)T * S * np_of<NQ>() * G::PLANE * 2 + (NQ == 4 ? 2 * T * 8 * sizeof(float) : 0);
   const size_t red = (size_t)G::WV * T * S * 3 * 16 * sizeof(float);  // output-layer combine
   return planes > red ? planes : red;
 }
@@ -211,20 +211,19 @@ __device__ __forceinline__ FragQ<NQ> wsp_frag(const u32x4* __restrict__ wsp, int
   return f;
 }
 
-// f16x3 (NQ = 4) operand scales of the forward: the value stream (sin, |h| <= 1) enters the fp16
-// products unscaled; the tangent and Laplacian streams (|dh| <= w |t|, |ddh| <= w |q| + w^2 sum t^2:
-// no a-priori bound) are scaled per tile and stream by the power of two 2^e that maps the bound's
-// maximum into [2^14, 2^15) (fwd_x6_block); the products are unscaled by 2^-8 (the weights' scale)
-// x 2^-e -- all exact
+// f16x3 (NQ = 4) operand scales of the forward: the value (sin, |h| <= 1) and tangent streams
+// (|dh| <= w |t|: fp16 holds |t| < 2183) enter the fp16 products unscaled; the Laplacian stream
+// (|ddh| <= w |q| + w^2 sum t^2: ~900x the tangents' square) is scaled per tile by the power of two
+// 2^e that maps its bound's maximum into [2^14, 2^15) (fwd_x6_block); the products are unscaled by
+// 2^-8 (the weights' scale) x 2^-e -- all exact
 __device__ __forceinline__ int f16_exp_for(float m) {  // 2^e maps m into [2^14, 2^15); 0 for 0 / inf / NaN
   if (!(m > 0.f && m <= 3.0e38f)) return 0;
   int k;
   (void)frexpf(m, &k);
   return min(max(15 - k, -100), 100);
 }
-// the static factor of the backward's h Laplacian stream (H planes, dW B operand): h x 2^-10, its z̄
-// x 2^10 (the dynamic z̄ scale absorbs it) -- fp16's range then holds |h_lap| < 6.7e7 (|t| < ~270)
-constexpr float kF16LapB = 1024.f;
+// The backward's h Laplacian stream (H planes, the dW B operand) takes the same bound, per block /
+// dW slice: h_lap x 2^eh, z̄_lap x 2^-eh x the adjoints' 2^e (jet_bwd_x6, jet_bwd_x6p + dw_x6)
 
 // Balanced tiles per block: with nbal > 0 the tiles of a batch are split over nbal blocks as
 // evenly as possible (block b: tiles [b tiles / nbal, (b + 1) tiles / nbal), at most T), so a
@@ -261,14 +260,12 @@ __device__ __forceinline__ void fwd_x6_block(const float* __restrict__ x, int N,
   const int ntiles = ((N + 63) / 64) * 4;
   const int rt0 = wave * RPW;
   const u32x4* wsp = wsp_base(prm, din, dout, L, W);
-  // f16x3: per-(tile, stream) maxima of the waves [2][T][S][8] after the planes, and the unscale of
-  // the next layer's products per (tile, stream)
+  // f16x3 Laplacian jets: the waves' per-tile maxima of the Laplacian-stream bound [2][T][8] after the
+  // planes, and the unscale of the next layer's Laplacian-stream products per tile
   float* zmx = lds_f + (T * S * np_of<NQ>() * PLANE) / 2;
-  float usc[T][S];
+  float usl[T];
 #pragma unroll
-  for (int t = 0; t < T; ++t)
-#pragma unroll
-    for (int s = 0; s < S; ++s) usc[t][s] = 1.f / kF16WScale;
+  for (int t = 0; t < T; ++t) usl[t] = 1.f / kF16WScale;
 
   float xv[T][3];
 #pragma unroll
@@ -335,41 +332,32 @@ __device__ __forceinline__ void fwd_x6_block(const float* __restrict__ x, int N,
 #pragma unroll
           for (int t = 0; t < T; ++t)
 #pragma unroll
-            for (int s = 0; s < S; ++s) a[t][i][s] *= usc[t][s];
+            for (int s = 0; s < S; ++s) a[t][i][s] *= (LAP && s == S - 1) ? usl[t] : 1.f / kF16WScale;
         }
       }
     }
-    // f16x3: this wave's bounds of |h| per (tile, stream) for the planes of layer j (before the
+    // f16x3 Laplacian jets: this wave's bound of |ddh| per tile for the planes of layer j (before the
     // barrier the next layer's operand writes wait on anyway; j = 0 adds one)
-    if constexpr (NQ == 4 && S > 1) {
+    if constexpr (NQ == 4 && LAP) {
       if (j < L) {
 #pragma unroll
         for (int t = 0; t < T; ++t) {
-          float mt[S];
-#pragma unroll
-          for (int s = 0; s < S; ++s) mt[s] = 0.f;
+          float mt = 0.f;
 #pragma unroll
           for (int i = 0; i < RPW; ++i)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
               float t2 = 0.f;
 #pragma unroll
-              for (int k = 0; k < NTAN; ++k) {
-                const float tk = a[t][i][1 + k][r];
-                mt[1 + k] = fmaxf(mt[1 + k], OMEGA * fabsf(tk));
-                t2 = fmaf(tk, tk, t2);
-              }
-              if constexpr (LAP) mt[S - 1] = fmaxf(mt[S - 1], fmaf(OMEGA, fabsf(a[t][i][S - 1][r]), OMEGA2 * t2));
+              for (int k = 0; k < NTAN; ++k) t2 = fmaf(a[t][i][1 + k][r], a[t][i][1 + k][r], t2);
+              mt = fmaxf(mt, fmaf(OMEGA, fabsf(a[t][i][S - 1][r]), OMEGA2 * t2));
             }
-#pragma unroll
-          for (int s = 1; s < S; ++s) {
-            const float m = wave_max(mt[s]);
-            if (lane == 0) zmx[(((j & 1) * T + t) * S + s) * 8 + wave] = m;
-          }
+          mt = wave_max(mt);
+          if (lane == 0) zmx[((j & 1) * T + t) * 8 + wave] = mt;
         }
       }
     }
-    if (j > 0 || (NQ == 4 && S > 1)) __syncthreads();  // every wave has read layer j-1 (and wrote its bounds)
+    if (j > 0 || (NQ == 4 && LAP)) __syncthreads();  // every wave has read layer j-1 (and wrote its bounds)
     if (act) {
 #pragma unroll
       for (int t = 0; t < T; ++t) {
@@ -385,24 +373,19 @@ __device__ __forceinline__ void fwd_x6_block(const float* __restrict__ x, int N,
 #pragma unroll
     for (int t = 0; t < T; ++t) sine_jet<RPW, S, LAP>(a[t]);
     if (j < L) {
-      float scl[T][S];  // this layer's operand scales (value stream 1)
+      float sll[T];  // this layer's Laplacian-stream operand scale per tile (f16x3)
 #pragma unroll
-      for (int t = 0; t < T; ++t)
+      for (int t = 0; t < T; ++t) {
+        sll[t] = 1.f;
+        if constexpr (NQ == 4 && LAP) {
+          float m = zmx[((j & 1) * T + t) * 8];
 #pragma unroll
-        for (int s = 0; s < S; ++s) {
-          scl[t][s] = 1.f;
-          usc[t][s] = 1.f / kF16WScale;
-          if constexpr (NQ == 4) {
-            if (s > 0) {
-              float m = zmx[(((j & 1) * T + t) * S + s) * 8];
-#pragma unroll
-              for (int w = 1; w < WV; ++w) m = fmaxf(m, zmx[(((j & 1) * T + t) * S + s) * 8 + w]);
-              const int e = f16_exp_for(m);
-              scl[t][s] = ldexpf(1.f, e);
-              usc[t][s] = ldexpf(1.f, -e) / kF16WScale;
-            }
-          }
+          for (int w = 1; w < WV; ++w) m = fmaxf(m, zmx[((j & 1) * T + t) * 8 + w]);
+          const int e = f16_exp_for(m);
+          sll[t] = ldexpf(1.f, e);
+          usl[t] = ldexpf(1.f, -e) / kF16WScale;
         }
+      }
 #pragma unroll
       for (int t = 0; t < T; ++t)
 #pragma unroll
@@ -410,7 +393,7 @@ __device__ __forceinline__ void fwd_x6_block(const float* __restrict__ x, int N,
 #pragma unroll
           for (int s = 0; s < S; ++s) {
             unsigned short* pw = lds + (t * S + s) * np_of<NQ>() * PLANE + c * LDB + 16 * (rt0 + i) + 4 * g;
-            const float sc = scl[t][s];
+            const float sc = (LAP && s == S - 1) ? sll[t] : 1.f;
             lds_put4<NQ, PLANE>(pw, sc * a[t][i][s][0], sc * a[t][i][s][1], sc * a[t][i][s][2], sc * a[t][i][s][3]);
           }
       __syncthreads();
@@ -829,8 +812,8 @@ constexpr int x6_bwd_sg() {
 }
 
 template <int NQ, int NT, int S, int T>
-constexpr size_t bwd_x6_lds_bytes() {  // + 2 x 8 floats: the per-layer adjoint maxima of the waves (NQ = 4)
-  return (size_t)T * x6_bwd_sg<NQ, NT, S, T>() * X6BwdGeo<NQ, NT>::SET_BYTES + 2 * 8 * sizeof(float);
+constexpr size_t bwd_x6_lds_bytes() {  // + 2 x 3 x 8 floats: the waves' per-layer maxima (NQ = 4)
+  return (size_t)T * x6_bwd_sg<NQ, NT, S, T>() * X6BwdGeo<NQ, NT>::SET_BYTES + 2 * 3 * 8 * sizeof(float);
 }
 
 template <int NQ, int NT, int S, bool LAP, int T>
@@ -851,7 +834,9 @@ __global__ __launch_bounds__(X6Geo<NT>::THREADS) void jet_bwd_x6(const BwdJobsX6
   extern __shared__ __attribute__((aligned(16))) float lds_f[];
   unsigned short* Z = reinterpret_cast<unsigned short*>(lds_f);
   unsigned short* H = Z + NSET * ZSET;
-  float* zred = lds_f + NSET * (ZSET + HSET) / 2;  // [2][waves]: per-layer max |z̄| of each wave (NQ = 4)
+  // NQ = 4, [2][3][waves]: each wave's per-layer max |z̄| over the value / tangent streams and over the
+  // Laplacian stream, and its bound of h_{j-1}'s Laplacian stream
+  float* zred = lds_f + NSET * (ZSET + HSET) / 2;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
   // NQ = 4 (INSR_BWD_F16_FUSED, the x6 backward's products on the fp16 matrix cores): per layer the
   // block's z̄ is scaled by the power of two 2^e that maps its largest |z̄| (Laplacian stream x 16)
@@ -1050,7 +1035,7 @@ __global__ __launch_bounds__(X6Geo<NT>::THREADS) void jet_bwd_x6(const BwdJobsX6
     }
     INSR_STAMP(L - j, 1);
     if constexpr (NQ == 4) {  // this wave's max |z̄_j| over the block's tiles (read after the group barrier)
-      float m = 0.f;
+      float mo = 0.f, ml = 0.f;
 #pragma unroll
       for (int t = 0; t < T; ++t)
 #pragma unroll
@@ -1058,9 +1043,18 @@ __global__ __launch_bounds__(X6Geo<NT>::THREADS) void jet_bwd_x6(const BwdJobsX6
 #pragma unroll
           for (int s = 0; s < S; ++s)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) m = fmaxf(m, fabsf(hb[t][i][s][r]) * ((LAP && s == S - 1) ? kF16LapB : 1.f));
-      m = wave_max(m);
-      if (lane == 0) zred[(j & 1) * 8 + wave] = m;  // two slots: layer j - 1 writes the other
+            for (int r = 0; r < 4; ++r) {
+              if (LAP && s == S - 1)
+                ml = fmaxf(ml, fabsf(hb[t][i][s][r]));
+              else
+                mo = fmaxf(mo, fabsf(hb[t][i][s][r]));
+            }
+      mo = wave_max(mo);
+      if constexpr (LAP) ml = wave_max(ml);
+      if (lane == 0) {  // two slots: layer j - 1 writes the other
+        zred[((j & 1) * 3) * 8 + wave] = mo;
+        zred[((j & 1) * 3 + 1) * 8 + wave] = ml;
+      }
     }
     // A operand of the propagation: W^T rows m = 16 rt + c, k = n = 32 kc + 8 g + jj, from the
     // pre-split planes (issued here, in flight during the dW phase).  Several stream groups:
@@ -1075,13 +1069,42 @@ __global__ __launch_bounds__(X6Geo<NT>::THREADS) void jet_bwd_x6(const BwdJobsX6
     floatx4 snp[T][RPW], csp[T][RPW];
     load_sc(j - 1, snp, csp);
     load_zk(j - 1);
+    if constexpr (NQ == 4 && LAP) {  // this wave's bound of h_{j-1}'s Laplacian stream, w |q| + w^2 sum t^2
+      float hl = 0.f;
+#pragma unroll
+      for (int t = 0; t < T; ++t) {
+        const float* basep = act_base(act, j - 1, ntiles, tt(t), S, NT);
+#pragma unroll
+        for (int i = 0; i < RPW; ++i) {
+          floatx4 zd[S - 1];
+#pragma unroll
+          for (int s = 1; s < S; ++s) {
+            if constexpr (KZ)
+              zd[s - 1] = zk[t][i][s - 1];
+            else
+              zd[s - 1] = *reinterpret_cast<const floatx4*>(basep + ((s * NT + rt0 + i) * 64 + lane) * 4);
+          }
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float t2 = 0.f;
+#pragma unroll
+            for (int k = 0; k < S - 2; ++k) t2 = fmaf(zd[k][r], zd[k][r], t2);
+            hl = fmaxf(hl, fmaf(OMEGA, fabsf(zd[S - 2][r]), OMEGA2 * t2));
+          }
+        }
+      }
+      hl = wave_max(hl);
+      if (lane == 0) zred[((j & 1) * 3 + 2) * 8 + wave] = hl;
+    }
     floatx4 dacc[RPW][NT];
 #pragma unroll
     for (int i = 0; i < RPW; ++i)
 #pragma unroll
       for (int ct = 0; ct < NT; ++ct) dacc[i][ct] = floatx4{0.f, 0.f, 0.f, 0.f};
     floatx4 nh[T][RPW][S];
-    float zsc = 1.f, zun = 1.f;  // NQ = 4: the block's adjoint scale 2^e and its inverse
+    // NQ = 4: the block's adjoint scale 2^e and its inverse; h_{j-1}'s Laplacian stream x hll = 2^eh,
+    // the Laplacian adjoint x zll = 2^-eh more (e maps max(|z̄|, |z̄_lap| 2^-eh) into [2^14, 2^15))
+    float zsc = 1.f, zun = 1.f, zll = 1.f, hll = 1.f;
 #pragma unroll
     for (int gi = 0; gi < NG; ++gi) {
       const int s0 = gi * SG;
@@ -1090,15 +1113,19 @@ __global__ __launch_bounds__(X6Geo<NT>::THREADS) void jet_bwd_x6(const BwdJobsX6
       INSR_STAMP(L - j, 3);
       if constexpr (NQ == 4) {
         if (gi == 0) {
-          float m = zred[(j & 1) * 8];
+          const float* zr = zred + (j & 1) * 3 * 8;
+          float mo = zr[0], ml = zr[8], mh = zr[16];
 #pragma unroll
-          for (int w = 1; w < G::WV; ++w) m = fmaxf(m, zred[(j & 1) * 8 + w]);
-          int e = 0;
-          if (m > 0.f && m <= 3.0e38f) {
-            int k;
-            (void)frexpf(m, &k);
-            e = min(max(15 - k, -100), 100);
+          for (int w = 1; w < G::WV; ++w) {
+            mo = fmaxf(mo, zr[w]);
+            ml = fmaxf(ml, zr[8 + w]);
+            mh = fmaxf(mh, zr[16 + w]);
           }
+          if constexpr (LAP) {
+            hll = ldexpf(1.f, f16_exp_for(mh));
+            zll = 1.f / hll;
+          }
+          const int e = f16_exp_for(fmaxf(mo, ml * zll));
           zsc = ldexpf(1.f, e);
           zun = ldexpf(1.f, -e);
         }
@@ -1114,16 +1141,17 @@ __global__ __launch_bounds__(X6Geo<NT>::THREADS) void jet_bwd_x6(const BwdJobsX6
             const int u = t * SG + sl;
             const int col = 16 * (rt0 + i) + 4 * g;
             const bool lq = NQ == 4 && LAP && s == S - 1;  // the fp16 Laplacian-stream scales
-            const float fz = lq ? kF16LapB * zsc : zsc;
-            lds_put4<NQ, ZPLANE>(Z + u * ZSET + c * LDB + col, hb[t][i][s][0] * fz, hb[t][i][s][1] * fz,
-                                 hb[t][i][s][2] * fz, hb[t][i][s][3] * fz);
+            const float fl = lq ? zll : 1.f;  // after zsc: each factor within fp32's range
+            lds_put4<NQ, ZPLANE>(Z + u * ZSET + c * LDB + col, (hb[t][i][s][0] * zsc) * fl,
+                                 (hb[t][i][s][1] * zsc) * fl, (hb[t][i][s][2] * zsc) * fl,
+                                 (hb[t][i][s][3] * zsc) * fl);
             floatx4 hs;
             if constexpr (KZ) {
               hs = h_from_regs<S, LAP>(s, zk[t][i], snp[t][i], csp[t][i]);
             } else {
               hs = h_stream<NT, S, LAP>(basep, s, rt0 + i, lane, snp[t][i], csp[t][i]);
             }
-            if (lq) hs *= 1.f / kF16LapB;
+            if (lq) hs *= hll;
             put_neuron_major<NQ, HPLANE>(H + u * HSET, hs, col, c);
           }
       }
@@ -1217,7 +1245,7 @@ __global__ __launch_bounds__(X6Geo<NT>::THREADS) void jet_bwd_x6(const BwdJobsX6
         cs[t][i] = csp[t][i];
 #pragma unroll
         for (int s = 0; s < S; ++s)
-          hb[t][i][s] = (NQ == 4) ? nh[t][i][s] * (((LAP && s == S - 1) ? 1.f / kF16LapB : 1.f) * zun / kF16WScale)
+          hb[t][i][s] = (NQ == 4) ? (nh[t][i][s] * zun) * (((LAP && s == S - 1) ? hll : 1.f) / kF16WScale)
                                   : nh[t][i][s];
       }
   }

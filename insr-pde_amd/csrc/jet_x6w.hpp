@@ -105,7 +105,13 @@ __global__ __launch_bounds__(512, (x6p_min_waves<NQ, NT>())) void jet_bwd_x6p(co
   // |z̄| (Laplacian stream x 16) into [2^14, 2^15), the product unscaled by 2^-(8 + e) (exact)
   extern __shared__ __attribute__((aligned(16))) float lds_f[];
   unsigned short* Z = reinterpret_cast<unsigned short*>(lds_f);  // [s][q][16 p][W + 8]
-  float* zred = lds_f + S * ZSET / 2;                             // [2][8 waves]: tile maxima
+  float* zred = lds_f + S * ZSET / 2;                             // [2][2][8 waves]: tile maxima
+  const int tiles_n = (N + 15) / 16;
+  // f16 dW (zmax != NULL): zq [L][tiles][2] = this tile's max |z̄_j| over the value / tangent streams
+  // and over the Laplacian stream (slot j - 1), then hq [L][tiles][8] = each wave's bound of the
+  // Laplacian stream of h_j = w c q - w^2 s sum t^2, i.e. w |q| + w^2 sum t^2 (slot j, j < L)
+  float* zq = zmax;
+  float* hq = zmax ? zmax + 2L * L * tiles_n : nullptr;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
   const int ntiles = ((N + 63) / 64) * 4;
   const int tile = blockIdx.x;
@@ -190,6 +196,7 @@ __global__ __launch_bounds__(512, (x6p_min_waves<NQ, NT>())) void jet_bwd_x6p(co
   // ---- sine layers j = L .. 0 ----
   for (int j = L; j >= 0; --j) {
     const float* basej = act_base(act, j, ntiles, tile, S, NT);
+    float hl = 0.f;  // this wave's bound of |h_j|'s Laplacian stream
 #pragma unroll
     for (int i = 0; i < RPW; ++i) {
       floatx4 zs[S];
@@ -197,7 +204,24 @@ __global__ __launch_bounds__(512, (x6p_min_waves<NQ, NT>())) void jet_bwd_x6p(co
       for (int s = 0; s < S; ++s)
         zs[s] = (s == 0) ? floatx4{0.f, 0.f, 0.f, 0.f}
                          : *reinterpret_cast<const floatx4*>(basej + ((s * NT + rt0 + i) * 64 + lane) * 4);
+      if constexpr (LAP) {
+        if (hq && j < L) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float t2 = 0.f;
+#pragma unroll
+            for (int k = 1; k < S - 1; ++k) t2 = fmaf(zs[k][r], zs[k][r], t2);
+            hl = fmaxf(hl, fmaf(OMEGA, fabsf(zs[S - 1][r]), OMEGA2 * t2));
+          }
+        }
+      }
       sine_rev<S, LAP>(hb[i], zs, sn[i], cs[i]);  // hb = z̄_j
+    }
+    if constexpr (LAP) {
+      if (hq && j < L) {
+        hl = wave_max(hl);
+        if (lane == 0) hq[((long)j * tiles_n + tile) * 8 + wave] = hl;
+      }
     }
     const long boff = (j == 0) ? (long)W * din : sb + (long)(j - 1) * W;
 #pragma unroll
@@ -230,46 +254,61 @@ __global__ __launch_bounds__(512, (x6p_min_waves<NQ, NT>())) void jet_bwd_x6p(co
 #pragma unroll
         for (int s = 0; s < S; ++s) *reinterpret_cast<floatx4*>(ab + ((s * NT + rt0 + i) * 64 + lane) * 4) = hb[i][s];
     }
-    if (zmax || NQ == 4) {  // this tile's max |z̄_j| (Laplacian stream x 16): the fp16 operand scales
-      float m = 0.f;
+    if (zmax || NQ == 4) {  // this wave's max |z̄_j| over the value / tangent streams and the Laplacian one
+      float mo = 0.f, ml = 0.f;
 #pragma unroll
       for (int i = 0; i < RPW; ++i)
 #pragma unroll
         for (int s = 0; s < S; ++s)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) m = fmaxf(m, fabsf(hb[i][s][r]) * ((LAP && s == S - 1) ? kF16LapB : 1.f));
-      m = wave_max(m);
-      if (lane == 0) zred[(j & 1) * 8 + wave] = m;  // two slots: layer j - 1 writes the other
+          for (int r = 0; r < 4; ++r) {
+            if (LAP && s == S - 1)
+              ml = fmaxf(ml, fabsf(hb[i][s][r]));
+            else
+              mo = fmaxf(mo, fabsf(hb[i][s][r]));
+          }
+      mo = wave_max(mo);
+      if constexpr (LAP) ml = wave_max(ml);
+      if (lane == 0) {  // two slots: layer j - 1 writes the other
+        zred[((j & 1) * 2) * 8 + wave] = mo;
+        zred[((j & 1) * 2 + 1) * 8 + wave] = ml;
+      }
     }
     __syncthreads();  // the previous layer's readers of Z are done
-    float zsc = 1.f, zun = 1.f;  // NQ = 4: the tile's adjoint scale 2^e, the products' unscale 2^-(8 + e)
+    // NQ = 4: the tile's adjoint scales 2^e (value / tangent streams, Laplacian stream: each its own
+    // accumulators here) and the products' unscales 2^-(8 + e)
+    float zso = 1.f, zsl = 1.f, zuo = 1.f, zul = 1.f;
     if constexpr (NQ == 4) {
-      float m = zred[(j & 1) * 8];
+      float mo = zred[((j & 1) * 2) * 8], ml = zred[((j & 1) * 2 + 1) * 8];
 #pragma unroll
-      for (int w = 1; w < 8; ++w) m = fmaxf(m, zred[(j & 1) * 8 + w]);
-      int e = 0;
-      if (m > 0.f && m <= 3.0e38f) {
-        int k;
-        (void)frexpf(m, &k);
-        e = min(max(15 - k, -100), 100);
+      for (int w = 1; w < 8; ++w) {
+        mo = fmaxf(mo, zred[((j & 1) * 2) * 8 + w]);
+        ml = fmaxf(ml, zred[((j & 1) * 2 + 1) * 8 + w]);
       }
-      zsc = ldexpf(1.f, e);
-      zun = ldexpf(1.f, -e) / kF16WScale;
+      const int eo = f16_exp_for(mo), el = f16_exp_for(ml);
+      zso = ldexpf(1.f, eo);
+      zuo = ldexpf(1.f, -eo) / kF16WScale;
+      zsl = ldexpf(1.f, el);
+      zul = ldexpf(1.f, -el) / kF16WScale;
     }
 #pragma unroll
     for (int i = 0; i < RPW; ++i)
 #pragma unroll
       for (int s = 0; s < S; ++s) {
-        const float f = (NQ == 4 && LAP && s == S - 1) ? kF16LapB * zsc : zsc;
+        const float f = (LAP && s == S - 1) ? zsl : zso;
         lds_put4<NQ, ZPLANE>(Z + s * ZSET + c * LDB + 16 * (rt0 + i) + 4 * g, hb[i][s][0] * f, hb[i][s][1] * f,
                              hb[i][s][2] * f, hb[i][s][3] * f);
       }
     __syncthreads();
-    if (zmax && threadIdx.x == 0) {
-      float m = zred[(j & 1) * 8];
+    if (zq && threadIdx.x == 0) {
+      float mo = zred[((j & 1) * 2) * 8], ml = zred[((j & 1) * 2 + 1) * 8];
 #pragma unroll
-      for (int w = 1; w < 8; ++w) m = fmaxf(m, zred[(j & 1) * 8 + w]);
-      zmax[(long)(j - 1) * ((N + 15) / 16) + tile] = m;
+      for (int w = 1; w < 8; ++w) {
+        mo = fmaxf(mo, zred[((j & 1) * 2) * 8 + w]);
+        ml = fmaxf(ml, zred[((j & 1) * 2 + 1) * 8 + w]);
+      }
+      zq[((long)(j - 1) * tiles_n + tile) * 2] = mo;
+      zq[((long)(j - 1) * tiles_n + tile) * 2 + 1] = ml;
     }
     // propagation: h̄_{j-1}[m] = sum_n W_j[n][m] z̄_j[n]; A = W^T rows m of this wave (pre-split
     // planes, orientation 1: NQ b128 loads per fragment), B = Z rows (one b128 per plane)
@@ -303,7 +342,7 @@ __global__ __launch_bounds__(512, (x6p_min_waves<NQ, NT>())) void jet_bwd_x6p(co
 #pragma unroll
     for (int i = 0; i < RPW; ++i)
 #pragma unroll
-      for (int s = 0; s < S; ++s) hb[i][s] = nh[i][s] * ((NQ == 4 && LAP && s == S - 1) ? zun / kF16LapB : zun);
+      for (int s = 0; s < S; ++s) hb[i][s] = (NQ == 4) ? nh[i][s] * ((LAP && s == S - 1) ? zul : zuo) : nh[i][s];
   }
 }
 
@@ -382,10 +421,11 @@ __device__ __forceinline__ void rows_level1(const float* __restrict__ part, int 
 // the first level of the compact-row reduction (small -> rows, block id (y - L) KS + x), so it
 // runs on the CUs the dW tail leaves idle instead of in a launch of its own.
 // NQ = 4 (f16x3, the x6 backward's dW under INSR_BWD_F16_DW): fp16 has 11 significant bits but a
-// narrow range, and an adjoint has no a-priori scale, so each K slice scales its z̄ by the power of
-// two 2^e that maps the slice's largest |z̄| (zmax: the propagation kernel's tile maxima) into
-// [2^14, 2^15) -- exact, undone on the partial -- and h enters as the forward's f16x3 does (value and
-// tangent streams unscaled, the Laplacian stream x 2^-4, its z̄ x 2^4: every product keeps 2^e).
+// narrow range, and neither an adjoint nor h's Laplacian stream has an a-priori scale, so each K
+// slice takes powers of two from the propagation kernel's tile maxima (zq, hq): h's Laplacian stream
+// x 2^eh (its bound's maximum into [2^14, 2^15)), value / tangent streams of h unscaled (|dh| <= w |t|),
+// z̄ x 2^e on the value / tangent streams and x 2^(e - eh) on the Laplacian one, e mapping the larger
+// of the two maxima into [2^14, 2^15) -- every product carries 2^e, undone on the partial (exact).
 template <int NQ, int NT, int S, bool LAP>
 __global__ __launch_bounds__(512, (NQ == 4 && NT == 8) ? INSR_F16_BWD_WAVES : 1) void dw_x6(int N, const float* __restrict__ act, const float* __restrict__ adj,
                                              float* __restrict__ dpart, int KS, int L, const float* __restrict__ small,
@@ -408,21 +448,30 @@ __global__ __launch_bounds__(512, (NQ == 4 && NT == 8) ? INSR_F16_BWD_WAVES : 1)
   const int units = ((N + 15) / 16) * S;
   const int chunks = (units + 1) / 2;
   const int c0 = (int)((long)chunks * blockIdx.x / KS), c1 = (int)((long)chunks * (blockIdx.x + 1) / KS);
-  float asc = 1.f, osc = 1.f;  // fp16 operand scale of z̄ and its inverse on the partial (NQ = 4)
+  // fp16 operand scales (NQ = 4): z̄ x asc (x ascl more on the Laplacian stream), h's Laplacian
+  // stream x bscl, the partial x osc
+  float asc = 1.f, ascl = 1.f, bscl = 1.f, osc = 1.f;
   if constexpr (NQ == 4) {
-    float m = 0.f;
+    float mo = 0.f, ml = 0.f, mh = 0.f;
     if (c1 > c0) {
       const int ta = (2 * c0) / S, tb = min((2 * c1 - 1) / S, tiles - 1);
-      for (int t = ta + lane; t <= tb; t += 64) m = fmaxf(m, zmax[(long)(j - 1) * tiles + t]);
+      const float* hq = zmax + 2L * L * tiles;
+      for (int t = ta + lane; t <= tb; t += 64) {
+        mo = fmaxf(mo, zmax[((long)(j - 1) * tiles + t) * 2]);
+        ml = fmaxf(ml, zmax[((long)(j - 1) * tiles + t) * 2 + 1]);
+      }
+      if constexpr (LAP)
+        for (int q = lane; q < (tb - ta + 1) * 8; q += 64) mh = fmaxf(mh, hq[((long)(j - 1) * tiles + ta) * 8 + q]);
     }
-    m = wave_max(m);
-    int e = 0;
-    if (m > 0.f && m <= 3.0e38f) {
-      int k;
-      (void)frexpf(m, &k);                  // m = f 2^k, f in [1/2, 1)
-      e = min(max(15 - k, -100), 100);      // m 2^e in [2^14, 2^15)
-    }
+    mo = wave_max(mo);
+    ml = wave_max(ml);
+    mh = wave_max(mh);
+    const int eh = LAP ? f16_exp_for(mh) : 0;
+    const float bl = ldexpf(1.f, eh);
+    const int e = f16_exp_for(fmaxf(mo, ml / bl));
     asc = ldexpf(1.f, e);
+    ascl = 1.f / bl;  // applied after asc: z̄_lap 2^e 2^-eh, each factor within fp32's range
+    bscl = bl;
     osc = ldexpf(1.f, -e);
   }
 
@@ -509,8 +558,8 @@ __global__ __launch_bounds__(512, (NQ == 4 && NT == 8) ? INSR_F16_BWD_WAVES : 1)
       const floatx4 zero = floatx4{0.f, 0.f, 0.f, 0.f};
       if constexpr (NQ == 4) {
         const bool lq = LAP && s == S - 1;
-        dw_put<NQ, NT>(A, live ? rzb[it] * (lq ? kF16LapB * asc : asc) : zero, rt, ul, lane);
-        dw_put<NQ, NT>(B, live ? (lq ? hv * (1.f / kF16LapB) : hv) : zero, rt, ul, lane);
+        dw_put<NQ, NT>(A, live ? (lq ? (rzb[it] * asc) * ascl : rzb[it] * asc) : zero, rt, ul, lane);
+        dw_put<NQ, NT>(B, live ? (lq ? hv * bscl : hv) : zero, rt, ul, lane);
       } else {
         dw_put<NQ, NT>(A, live ? rzb[it] : zero, rt, ul, lane);
         dw_put<NQ, NT>(B, live ? hv : zero, rt, ul, lane);
@@ -696,7 +745,7 @@ inline long wide_work_floats_impl(long n, int din, int dout, int L, int W, int S
   const long adj = (long)L * ntiles * S * (W / 16) * 256;
   const long small = ((n + 15) / 16) * small_count(din, dout, L, W);
   const long dw = (long)L * wide_ks(n, S, L) * W * W;
-  const long zmax = (long)L * ((n + 15) / 16);  // tile maxima of the adjoints (fp16 dW)
+  const long zmax = 10L * L * ((n + 15) / 16);  // tile maxima of the adjoints and h bounds (fp16 dW)
   return adj + small + dw + (long)kSmallRS * small_count(din, dout, L, W) + zmax;
 }
 
@@ -727,8 +776,8 @@ int wide_bwd_t(const float* x, int N, int din, int dout, int L, const float* prm
   // the x6 precision's products on the fp16 matrix cores (dw_x6 / jet_bwd_x6p NQ = 4, above)
   const bool f16dw = NQ == 3 && (g_bwd_f16 & INSR_BWD_F16_DW) && L > 0;
   const bool f16p = NQ == 3 && (g_bwd_f16 & INSR_BWD_F16_PROP) && L > 0;
-  constexpr size_t lds_p = (size_t)S * np_of<NQ>() * 16 * (W + 8) * 2 + 2 * 8 * sizeof(float);
-  constexpr size_t lds_p4 = (size_t)S * 2 * 16 * (W + 8) * 2 + 2 * 8 * sizeof(float);
+  constexpr size_t lds_p = (size_t)S * np_of<NQ>() * 16 * (W + 8) * 2 + 2 * 2 * 8 * sizeof(float);
+  constexpr size_t lds_p4 = (size_t)S * 2 * 16 * (W + 8) * 2 + 2 * 2 * 8 * sizeof(float);
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)jet_bwd_x6p<NQ, NT, S, LAP>, hipFuncAttributeMaxDynamicSharedMemorySize,

@@ -166,8 +166,8 @@ def test_f16x3_forward_matches_x6_to_fp32_level(B, w0_scale):
     """The f16x3 forward (MLP(precision='f16x3'), the default) against the bf16x6 forward of the
     same weights: value, gradient and Laplacian jets agree to 1e-5 normwise -- also with the first
     layer scaled x10 / x40 (tangents ~10-40x, Laplacians ~100-1600x the init's: the per-tile
-    dynamic scales of the tangent and Laplacian planes keep fp16 in range; the static 2^-4 of the
-    first version overflowed to inf there)."""
+    dynamic scale of the Laplacian planes keeps fp16 in range; the static 2^-4 of the first
+    version overflowed to inf there)."""
     torch.manual_seed(5)
     a = B.MLP(2, 1, 4, 128, nonlinearity="sine", precision="bf16x6").cuda()
     b = B.MLP(2, 1, 4, 128, nonlinearity="sine", precision="f16x3").cuda()
