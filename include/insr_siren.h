@@ -245,7 +245,7 @@ int insr_jet_set_bwd_f16(int mask);
 int insr_jet_wide_launch_threads(long n_points, int d_in, int d_out, int num_hidden, int width, int mode,
                                  long* threads3);
 /* Smallest width (128 or 256) that takes the wide path; returns the old value.
- * Env INSR_WIDE_MIN_WIDTH.  Process-wide tuning/testing knob. */
+ * Default 256.  Process-wide A/B knob (no environment override). */
 int insr_jet_set_wide_min_width(int width);
 
 /* Number of partial-gradient rows insr_siren_jet_bwd writes for n points: one per

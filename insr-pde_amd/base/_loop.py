@@ -18,6 +18,7 @@ Differences, all controlled by cfg attributes:
 import torch
 
 from . import _jet
+from .sampling import draw_plan
 
 try:
     from tqdm import tqdm
@@ -47,7 +48,7 @@ class PhaseLoop:
 
     def _body(self):
         self.m.optimizer, self.m.scheduler = self.opt, self.sched
-        with _jet.call_scope(self):
+        with _jet.call_scope(self), draw_plan(self):
             loss_dict = self.func(self.m, *self.args, **self.kwargs)
         synced = self.m._update_network(loss_dict)
         return synced if isinstance(synced, dict) else loss_dict
@@ -56,7 +57,7 @@ class PhaseLoop:
     def _stage1(self):
         m = self.m
         m.optimizer, m.scheduler = self.opt, self.sched
-        with _jet.call_scope(self):
+        with _jet.call_scope(self), draw_plan(self):
             loss_dict = self.func(m, *self.args, **self.kwargs)
         m.optimizer.zero_grad()
         m._backward(loss_dict)

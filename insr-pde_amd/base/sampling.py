@@ -186,27 +186,93 @@ def sample_random_and_bands2D(N, n_band, epsilon=1e-4, device="cuda", merged=Fal
     return x, bxy
 
 
+class draw_plan:
+    """`with draw_plan(owner):` around one iteration of a phase body (base/_loop.py).  The
+    sampler calls of an iteration (sample_random, the band samplers) are recorded on `owner`;
+    on the next iteration the FIRST call draws every request the previous iteration made, in
+    ONE insr_sample_boxes launch (each request its own output tensor), and the later calls
+    take their pre-drawn tensors as long as they ask for the same (dim, boxes) in the same
+    order -- the reference's phase bodies call the samplers 3 times per iteration
+    (fluid/model.py:75,94-95): 3 launches -> 1.  Independent uniform draws, so drawing them
+    early changes which Philox numbers a request gets, not its distribution.  A request that
+    departs from the plan draws on its own (and ends the plan for that iteration)."""
+
+    active = None  # the innermost scope's state
+
+    def __init__(self, owner):
+        self.owner = owner
+
+    def __enter__(self):
+        self.saved = draw_plan.active
+        self.prev = self.owner.__dict__.get("_insr_draw_plan")
+        self.rec, self.pos, self.ready = [], 0, None
+        draw_plan.active = self
+        return self
+
+    def __exit__(self, *exc):
+        draw_plan.active = self.saved
+        if exc[0] is None:
+            self.owner._insr_draw_plan = self.rec
+        return False
+
+    def take(self, key, dev):
+        """The pre-drawn tensor for request `key` = (dim, boxes, device index), or None (draw it now)."""
+        from . import _native as nat
+        pos, self.pos = self.pos, self.pos + 1
+        self.rec.append(key)
+        plan = self.prev
+        if not plan or pos >= len(plan) or plan[pos] != key:
+            self.prev = None  # off the plan: every later request draws on its own
+            return None
+        if pos == 0:
+            if len(plan) < 2 or len({(k[0], k[2]) for k in plan}) != 1 or sum(len(k[1]) for k in plan) > nat.MAX_BOXES:
+                self.prev = None
+                return None
+            outs = [torch.empty(sum(int(b[0]) for b in k[1]), k[0], device=dev) for k in plan]
+            _launch_boxes([(o, k[1]) for o, k in zip(outs, plan)], key[0], dev)
+            self.ready = outs
+        return self.ready[pos] if self.ready is not None else None
+
+
+def _launch_boxes(reqs, dim, dev):
+    """One insr_sample_boxes launch: reqs = [(out tensor (sum n, dim), boxes), ...]; the boxes of
+    a request fill its tensor's rows in order."""
+    from . import _native as nat
+    state, seed = _sampler(dev)
+    f3 = nat._F * 3
+    nbox = sum(len(b) for _, b in reqs)
+    arr = (nat.Box * nbox)()
+    k, pad = 0, [0.0] * (3 - dim)
+    for out, boxes in reqs:
+        row = 0
+        for n, lo, hi in boxes:
+            arr[k] = nat.Box(out.data_ptr() + 4 * dim * row, int(n), f3(*(list(lo) + pad)), f3(*(list(hi) + pad)))
+            row, k = row + int(n), k + 1
+    nat.check(nat.lib().insr_sample_boxes(arr, nbox, dim, seed, nat.ptr(state), nat.stream_of(dev)),
+              "insr_sample_boxes")
+
+
 def sample_boxes(boxes, dim, device="cuda"):
     """ONE device launch drawing every box of an iteration into one (sum n, dim) tensor,
     rows in box order: boxes = [(n, lo[dim], hi[dim]), ...], coordinate j of box k uniform
-    in [lo[j], hi[j]) (insr_sample_boxes, the device stream of sample_random_and_bands2D)."""
+    in [lo[j], hi[j]) (insr_sample_boxes, the device stream of sample_random_and_bands2D).
+    Inside a phase loop's draw_plan the tensor may have been drawn by the iteration's first
+    sampler call (same distribution)."""
     from . import _native as nat
     dev = torch.device(device)
     if dev.type != "cuda":
         raise nat.NativeUnavailable("sample_boxes draws on the GPU only")
     if not 1 <= len(boxes) <= nat.MAX_BOXES:
         raise ValueError(f"sample_boxes: 1..{nat.MAX_BOXES} boxes")
-    state, seed = _sampler(dev)
+    plan = draw_plan.active
+    if plan is not None:
+        key = (dim, tuple((int(n), tuple(float(v) for v in lo), tuple(float(v) for v in hi)) for n, lo, hi in boxes),
+               dev.index)
+        out = plan.take(key, dev)
+        if out is not None:
+            return out
     out = torch.empty(sum(int(b[0]) for b in boxes), dim, device=dev)
-    f3 = nat._F * 3
-    arr = (nat.Box * len(boxes))()
-    row = 0
-    for k, (n, lo, hi) in enumerate(boxes):
-        pad = [0.0] * (3 - dim)
-        arr[k] = nat.Box(out.data_ptr() + 4 * dim * row, int(n), f3(*(list(lo) + pad)), f3(*(list(hi) + pad)))
-        row += int(n)
-    nat.check(nat.lib().insr_sample_boxes(arr, len(boxes), dim, seed, nat.ptr(state), nat.stream_of(dev)),
-              "insr_sample_boxes")
+    _launch_boxes([(out, boxes)], dim, dev)
     return out
 
 

@@ -106,14 +106,13 @@ int nq_of(int prec) {
 }
 
 // Backward through the two-kernel path (jet_x6w.hpp: propagation kernel + split-K dW GEMM)
-// for the split-bf16 precisions at widths >= g_wide_min (default 256; env
-// INSR_WIDE_MIN_WIDTH) and, at width 128, for Laplacian jets of >= 8192 points and 3-4
+// for the split-bf16 precisions at widths >= g_wide_min (default 256; insr_jet_set_wide_min_width,
+// A/B studies only) and, at width 128, for Laplacian jets of >= 8192 points and 3-4
 // stream gradient jets of >= 32768 points.  Measured (profiles/r02/kbench_wide_vs_fused.jsonl,
 // backward into .grad incl. reductions): LAP 16384 points 244 -> 182 us, LAP 65536 813 -> 698,
 // GRAD (S = 3) 65536 595 -> 548; GRAD 16384 140 vs 144 and every value jet stay fused.
-static int g_wide_min = -1;
+static int g_wide_min = 256;
 bool use_wide(long n, int S, int NT, bool lap, int nq) {
-  if (g_wide_min < 0) g_wide_min = env_or("INSR_WIDE_MIN_WIDTH", 256);
   if (NT < 8 || nq == 0) return false;
   if (g_bwd_policy == 2) return true;
   if (g_bwd_policy == 1 && NT == 8) return false;
@@ -976,7 +975,7 @@ int insr_siren_jet_bwd_grad_multi(const InsrBwdJob* jobs, int njobs, int din, in
 }
 
 int insr_jet_set_wide_min_width(int width) {
-  const int old = g_wide_min < 0 ? env_or("INSR_WIDE_MIN_WIDTH", 256) : g_wide_min;
+  const int old = g_wide_min;
   g_wide_min = width;
   return old;
 }

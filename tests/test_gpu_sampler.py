@@ -195,3 +195,53 @@ def test_sample_random_on_the_device(B):
         assert float(a.min()) >= -1.0 and float(a.max()) < 1.0
         assert abs(float(a.mean())) < 0.02 and abs(float(a.var()) - 1 / 3) < 0.02
     assert B.sample_random(0, 2, device="cuda").shape == (0, 2)
+
+
+@pytest.mark.gpu
+def test_draw_plan_one_launch_per_iteration(B):
+    """Inside a phase loop's draw_plan (base/_loop.py) the reference's per-iteration sampler calls
+    (fluid/model.py:75,94-95: sample_random + two sample_boundary2D_separate) draw in ONE
+    insr_sample_boxes launch from the second iteration on: same shapes and boxes, fresh points
+    every iteration, every request its own tensor; a request off the recorded plan draws alone."""
+    from base import _native as nat
+    from base.sampling import draw_plan
+    lib = nat.lib()
+    orig, calls = lib.insr_sample_boxes, []
+
+    def counting(*a):
+        calls.append(a[1])
+        return orig(*a)
+
+    class Owner:
+        pass
+
+    eps = 1e-4
+    lo, hi, full = (-1 - eps, -1 + eps), (1 - eps, 1 + eps), (-1.0, 1.0)
+    owner, seen = Owner(), []
+    lib.insr_sample_boxes = counting
+    try:
+        for it in range(3):
+            calls.clear()
+            with draw_plan(owner):
+                x = B.sample_random(16384, 2, device="cuda").requires_grad_(True)
+                bx = B.sample_boundary2D_separate(163, side="horizontal", device="cuda").requires_grad_(True)
+                by = B.sample_boundary2D_separate(163, side="vertical", device="cuda").requires_grad_(True)
+            assert calls == ([1, 2, 2] if it == 0 else [5]), (it, calls)
+            assert x.shape == (16384, 2) and bx.shape == (162, 2) and by.shape == (162, 2)
+            assert x.is_leaf and bx.is_leaf and by.is_leaf
+            assert float(x.min()) >= -1.0 and float(x.max()) < 1.0 and abs(float(x.mean())) < 0.03
+            for t, faces in ((bx, [(lo, full), (hi, full)]), (by, [(full, lo), (full, hi)])):
+                for k, face in enumerate(faces):
+                    rows = t[k * 81:(k + 1) * 81].detach().cpu().double()
+                    for j, (l, h) in enumerate(face):
+                        assert float(rows[:, j].min()) >= np.float32(l) and float(rows[:, j].max()) <= np.float32(h)
+            seen.append(x.detach().clone())
+        assert not torch.equal(seen[1], seen[2]) and not torch.equal(seen[0], seen[1])
+        # off the plan: another size draws alone, and so does every later request of that iteration
+        calls.clear()
+        with draw_plan(owner):
+            B.sample_random(8192, 2, device="cuda")
+            B.sample_boundary2D_separate(163, side="horizontal", device="cuda")
+        assert calls == [1, 2], calls
+    finally:
+        lib.insr_sample_boxes = orig
