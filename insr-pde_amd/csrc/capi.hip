@@ -120,9 +120,11 @@ bool use_wide(long n, int S, int NT, bool lap, int nq) {
   if (NT != 8 || g_wide_min > 256) return false;
   // with the pre-split weight planes (kbench r2s31, profiles/r02/wide_vs_fused_wsplit.jsonl):
   // Laplacian and 2-d gradient jets from 8,192 points (gradient 16,708: 143 vs 175 us fused),
-  // value jets only from ~48K points (16,708: 75 vs 67 us fused; 65,536: 228 vs 241)
+  // value jets from ~24K points: round 3, f16x3 products on both paths (kbench r3aa, backward
+  // into .grad incl. sums, profiles/r03/kbench_value_routing.jsonl): 16,708 fused 54.4-56.1 vs
+  // two-kernel 60.9-62.4 us; 33,092 fused 101.7-103.7 vs two-kernel 93.4-95.3 (>= 49,152: resident)
   if (lap || S >= 3) return n >= 8192;
-  return S == 1 && n >= 49152;
+  return S == 1 && n >= 24576;
 }
 
 static int cu_count() {

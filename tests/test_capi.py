@@ -173,7 +173,8 @@ def test_value_backward_launch_shape(lib):
 
 def test_backward_path_policy(lib):
     """insr_jet_bwd_path answers on the host: the two-kernel path for the fluid nets' Laplacian
-    backward at the headline batch and at W = 256, the fused kernel for value jets; the resident-dW
+    backward at the headline batch and at W = 256, the fused kernel for value jets below 24,576 points
+    (two-kernel from there); the resident-dW
     kernel for the fluid2DtlgnM batch (Laplacian from 32,768 points, value from 49,152) or when
     forced (policy 3 / 4);
     insr_jet_set_bwd_policy forces a path for A/B studies."""
@@ -190,7 +191,8 @@ def test_backward_path_policy(lib):
         assert lib.insr_jet_bwd_path(65536 + 1308, 2, 1, 4, 128, LAP) == 2
         lib.insr_jet_set_bwd_f16(old_f16)
         assert lib.insr_jet_bwd_path(65536 + 1308, 2, 2, 4, 128, V) == 2
-        assert lib.insr_jet_bwd_path(33092, 2, 2, 4, 128, V) == 0
+        assert lib.insr_jet_bwd_path(33092, 2, 2, 4, 128, V) == 1   # value jets two-kernel from 24,576
+        assert lib.insr_jet_bwd_path(24000, 2, 2, 4, 128, V) == 0
         assert lib.insr_jet_bwd_path(32768, 3, 3, 5, 256, G) == 1
         assert lib.insr_jet_bwd_path(20400, 2, 2, 5, 128, G) != 2       # 5 hidden layers: not resident
         assert lib.insr_jet_bwd_path(16708, 2, 1, 4, 128, LAP | nat.jet_prec(nat.PREC_BF16)) != 2  # x6 only
