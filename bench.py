@@ -583,6 +583,11 @@ def main():
         torch.cuda.synchronize()
         log(f"warmup step {i} done" + "".join(f" [{pl.tag}: capture failed {pl.capture_error}]"
                                               for pl in loops if getattr(pl, "capture_error", None)))
+    # one more untimed step as a timestep in step() order (the prev-net snapshots, then each phase
+    # loop in turn), so the timed region's first timestep is not the first use of that sequence
+    run_timestep(model, wl, loops, w_eff, 1)
+    torch.cuda.synchronize()
+    w_eff += 1
     # timed region: --steps iterations of every phase, as `nts` timesteps in step() order
     # (K iterations per phase, phases in order, median of 5 timesteps); no loss
     # reads inside (sync_every = 1e9) and no host sync at the timestep boundaries either: the
