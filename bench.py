@@ -78,8 +78,9 @@ def parse():
     ap.add_argument("--shard-of", type=int, default=1,
                     help="one process runs the per-rank shard of a K-rank strong-scaling run (global batch / K "
                          "points per phase iteration; elasticity: the draw at resolution / K^(1/3)); 1 GPU")
-    ap.add_argument("--bwd-policy", type=int, default=0, choices=[0, 1, 2, 3],
-                    help="backward path (A/B studies): 0 auto, 1 fused tile-split, 2 two-kernel, 3 resident dW")
+    ap.add_argument("--bwd-policy", type=int, default=0, choices=[0, 1, 2, 3, 4],
+                    help="backward path (A/B studies): 0 auto, 1 fused tile-split, 2 two-kernel, 3 resident dW, "
+                         "4 recompute")
     ap.add_argument("--bwd-f16", type=int, default=-1, choices=list(range(-1, 8)),
                     help="x6 backward products on the fp16 matrix cores, INSR_BWD_F16_* mask (A/B studies; "
                          "-1 = library default)")
@@ -278,8 +279,10 @@ def macs_per_point(din, dout, L, W):
 
 
 def jet_precision_names(precision):
-    """The matrix-core precisions the jets actually run (forward / backward): 'fp32' is the
-    fp32-level default pair (f16x3 forwards, bf16x6 backwards, include/insr_siren.h)."""
+    """The matrix-core PRODUCTS the jets actually run (forward / backward).  'fp32' is the fp32-level
+    contract: f16x3 forwards; backwards whose contract is bf16x6 run f16x3 products on every path the
+    insr_jet_set_bwd_f16 mask covers and on the recompute path (always f16x3), bf16x6 products on the
+    resident-dW kernel and on paths the mask leaves out."""
     from base import _native as nat
     if precision != "fp32":
         return {"mixed": "bf16x3/bf16"}.get(precision, precision)
@@ -287,7 +290,12 @@ def jet_precision_names(precision):
     f, b = ctypes.c_int(), ctypes.c_int()
     nat.lib().insr_jet_get_precision(ctypes.byref(f), ctypes.byref(b))
     names = {v: k for k, v in nat.PRECISIONS.items()}
-    return f"{names[f.value]}/{names[b.value]}"
+    bwd = names[b.value]
+    if b.value == nat.PREC_BF16X6:
+        mask = nat.lib().insr_jet_set_bwd_f16(-1)
+        bwd = "f16x3" if mask == 7 else (f"bf16x6+f16x3(mask {mask})" if mask else "bf16x6")
+        bwd += " (resident-dW kernel: bf16x6)" if mask else ""
+    return f"{names[f.value]}/{bwd}"
 
 
 def roofline(loops, n_local, precision="fp32"):
@@ -326,25 +334,25 @@ def roofline(loops, n_local, precision="fp32"):
     nq = PRECISION[precision][2]
     kname, grid, x6, np_run = kernel_identity(kind, mode, n, din, dout, L, W, nq)
     traffic, tsrc = pmc_traffic(kname, grid)
-    peak = FP32_MFMA_PEAK_TFLOPS if precision == "fp32" else BF16_MFMA_PEAK_TFLOPS
-    out = {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
-           "frac": round(achieved / peak, 4), "traffic": traffic,
+    # peak = the dense matrix ceiling of the products the launch actually runs: its split kernels run NP
+    # v_mfma_f32_16x16x32_{bf16,f16} (16 cyc, the ~2.5 PF dense rate) per fp32-level 16x16x32 MAC block
+    # (NP = 6 bf16x6 / 3 f16x3 or bf16x3 / 1 bf16), i.e. 2500 / NP TFLOP/s of fp32-equivalent work
+    # (= 157.3 x 16 / NP: the fp32 MFMA runs at 1/16 of the bf16 rate); achieved counts the algorithmic
+    # fp32-equivalent flops, so frac <= 1 on every path and config
+    np_ = np_run if x6 else None
+    ceil = round(FP32_MFMA_PEAK_TFLOPS * 16.0 / np_, 1) if np_ else FP32_MFMA_PEAK_TFLOPS
+    out = {"bound": "mfma", "achieved": round(achieved, 2), "peak": ceil, "unit": "TFLOP/s",
+           "frac": round(achieved / ceil, 4), "traffic": traffic,
+           "peak_basis": (f"dense fp16/bf16 matrix rate / {np_} products per fp32-level MAC (the products this launch "
+                          f"runs; MI355X_MICROARCH.md: 157.3 TF fp32 = 1/16 of ~2.5 PF bf16/fp16)") if np_ else
+                         "dense fp32 matrix peak (exact-fp32 v_mfma_f32_16x16x4_f32)",
            "traffic_unit": "bytes/launch (HBM: corrected FETCH_SIZE + WRITE_SIZE)", "traffic_source": tsrc,
            "kernel": f"{kname}{'' if isinstance(grid, list) else f' grid={grid}'} (n={n}, {din}->{dout} {L}x{W}, {mode} jet {kind})", "avg_ms": round(ms, 4),
-           "algorithmic_gflop_per_launch": round(flops / 1e9, 3), "per_step_ms_by_launch": table}
-    if x6:
-        # the kernel runs split products: NP x v_mfma_f32_16x16x32_{bf16,f16} (16 cyc) per 16x16x32 fp32-equivalent
-        # MAC block (NP = 6 bf16x6 / 3 f16x3 or bf16x3 / 1): 16*16*32 / (16 NP) MAC/clk/SIMD vs 32 for
-        # v_mfma_f32_16x16x4_f32 -- the ceiling of the products the launch actually ran
-        np_ = np_run
-        ceil = round(FP32_MFMA_PEAK_TFLOPS * (16 * 16 * 32 / (16.0 * np_)) / 32.0, 1)
+           "algorithmic_gflop_per_launch": round(flops / 1e9, 3), "per_step_ms_by_launch": table,
+           "fp32_matrix_peak": FP32_MFMA_PEAK_TFLOPS,
+           "frac_of_fp32_matrix_peak": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4)}
+    if np_:
         out["products_per_mac"] = np_
-        out["precision_ceiling"] = ceil
-        out["frac_of_precision_ceiling"] = round(achieved / ceil, 4)
-        if precision == "fp32":
-            x6c = round(FP32_MFMA_PEAK_TFLOPS * (16 * 16 * 32 / (16.0 * 6)) / 32.0, 1)
-            out["x6_ceiling"] = x6c
-            out["frac_of_x6_ceiling"] = round(achieved / x6c, 4)
     return out
 
 
@@ -364,6 +372,16 @@ def kernel_identity(kind, mode, n, din, dout, L, W, nq=3):
     f16 = lib.insr_jet_set_bwd_f16(-1) if nq == 3 else 0
     nprod = {4: 3, 3: 6, 2: 3, 1: 1}
     path = lib.insr_jet_bwd_path(n, din, dout, L, W, m_b) if kind == "bwd" else 0
+    if path == 3:  # the recompute backward (forward + reverse jet per tile, f16x3) + the fixed-order sums
+        import ctypes
+        thr = (ctypes.c_long * 3)()
+        nat.check(lib.insr_jet_wide_launch_threads(n, din, dout, L, W, m_b, thr), "insr_jet_wide_launch_threads")
+        zr = 4 if S == 1 else 2  # jet_fb.hip: hidden layers whose z-streams stay in registers
+        parts = [(f"insr::jet_fb_x6<{S}, {lap}, {L}, {zr}>", thr[0]), ("insr::reduce_dw_kernel", thr[1])]
+        return " + ".join(f"{k}|grid={g}" for k, g in parts) + " (recompute backward: forward + reverse jet per " \
+            "tile in one persistent launch, no saved streams, then the dW / compact-row sums; time = both " \
+            "launches; achieved counts the backward's algorithmic flops only, not the recomputed forward)", \
+            parts, True, 3
     if path == 2:  # the resident-dW persistent kernel + the fixed-order sums
         import ctypes
         thr = (ctypes.c_long * 3)()
@@ -518,6 +536,8 @@ def cpu_baseline(config, seconds):
     return {"value": round(pts / dt, 1), "unit": "collocation-points/s", "cores": cores, "kind": "port",
             "cpu_model": cpu_model(), "statistic": f"median of {len(times)} iterations after 2 warm-up",
             "spread_max_over_min": round(times[-1] / times[0], 3),
+            # the explicit uncertainty of `value`: the sample's iteration rates span median x (1 +- u)
+            "uncertainty_pct": round(50.0 * (times[-1] - times[0]) / dt, 1),
             "rounds": [{"n": len(t), "min_ms": round(t[0] * 1e3, 1), "max_ms": round(t[-1] * 1e3, 1)} for t in rounds],
             "sample": f"oracle/siren_oracle.py {config}: {what}, torch CPU autograd + Adam, "
                       f"{torch.get_num_threads()} threads, median {dt * 1e3:.1f} ms/iter "

@@ -171,7 +171,8 @@ int insr_siren_jet_bwd(const float* x, long n_points, int d_in, int d_out, int n
                        void* stream);
 
 /*
- * Backward of the jet straight into the network's flat gradient:
+ * Backward of the jet straight into the network's flat gradient (act may be NULL when
+ * insr_jet_bwd_path() is 3: the recompute backward reads only x, the params and the adjoints):
  *   grad = (accumulate ? grad : 0) + d(loss)/d(params)   (fixed summation order)
  *   work  insr_jet_bwd_work_bytes(...) of scratch.
  * Width <= 128 (and F32 backward precision): insr_siren_jet_bwd + insr_reduce_partials.
@@ -221,13 +222,17 @@ int insr_jet_bwd_is_wide(long n_points, int d_in, int width, int mode);
 /* Which backward serves this jet: 0 = the fused tile-split kernel writing partial rows
  * (insr_siren_jet_bwd + insr_reduce_partials_strided), 1 = the two-kernel path, 2 = the
  * resident-dW persistent kernel (W = 128, <= 4 hidden layers: every hidden layer's weight
- * gradient held in registers across the batch).  1 and 2 run through insr_siren_jet_bwd_grad
- * with an insr_jet_bwd_work_bytes workspace. */
+ * gradient held in registers across the batch), 3 = the RECOMPUTE backward (W = 128, 4 hidden
+ * layers, fp32-level backward precision: one persistent launch that reruns the forward jet of
+ * each 16-point tile next to its reverse jet, dW resident per CU -- it reads no saved streams,
+ * so the forward of such a call passes act = NULL and saves nothing).  1, 2 and 3 run through
+ * insr_siren_jet_bwd_grad with an insr_jet_bwd_work_bytes workspace; path 3 never depends on
+ * n_points (the forward's decision and the backward's agree). */
 int insr_jet_bwd_path(long n_points, int d_in, int d_out, int num_hidden, int width, int mode);
 
 /* Backward-path policy (A/B studies): 0 = auto (default), 1 = fused where it exists,
- * 2 = two-kernel, 3 = resident dW where it applies.  Returns the previous policy (a policy
- * outside 0..3 changes nothing: -1 queries). */
+ * 2 = two-kernel, 3 = resident dW, 4 = recompute where it applies.  Returns the previous policy
+ * (a policy outside 0..4 changes nothing: -1 queries). */
 int insr_jet_set_bwd_policy(int policy);
 /* Matrix products of the x6 (fp32-level) backward that run on the fp16 matrix cores instead of
  * six bf16 products: f16x3 (two fp16 terms per operand, three products, 22 significant bits),
@@ -274,14 +279,17 @@ void insr_jet_get_split_tiles(int* fwd_tiles, int* bwd_tiles, int* min_blocks);
  *   INSR_PREC_BF16X3  two bf16 terms per operand, three products (dropped terms
  *                     <= 2^-16 |a||b|): 5.3x the fp32 matrix rate.
  *   INSR_PREC_BF16    plain bf16 operands, one product, fp32 accumulation: 16x.
- *   INSR_PREC_F16X3   FORWARD ONLY: every operand scaled by a power of two (weights 2^8,
- *                     Laplacian stream 2^-4) and split in two fp16 terms (11 + 11
- *                     significant bits), three v_mfma_f32_16x16x32_f16 products per K chunk
- *                     (dropped term <= 2^-22 |a||b|): fp32-level accuracy at 5.3x the fp32
- *                     matrix rate.  The default forward.  A backward asked for at this
- *                     precision runs BF16X6.
- *                     Range: |W| < 255, |tangent streams| < 65504, |Laplacian stream| < 2^20
- *                     (beyond them the outputs turn inf/NaN -- never silently wrong).
+ *   INSR_PREC_F16X3   FORWARD ONLY: every operand scaled by a power of two and split in two
+ *                     fp16 terms (11 + 11 significant bits), three v_mfma_f32_16x16x32_f16 products
+ *                     per K chunk (dropped term <= 2^-22 |a||b|): fp32-level accuracy at 5.3x the
+ *                     fp32 matrix rate.  The default forward.  A backward asked for at this
+ *                     precision runs BF16X6.  Scales: the weights x 2^8 (the fp16 planes); the
+ *                     Laplacian stream per tile by the power of two that maps its block maximum
+ *                     into [2^14, 2^15); the tangent streams unscaled while their bound w |t| stays
+ *                     below 2^15, else (a uniform branch, rare) by their own block power of two; all
+ *                     undone exactly on the products.  Range: |W| < 255 (the weight planes), the
+ *                     streams fp32's.  The f16 backward products (insr_jet_set_bwd_f16, the
+ *                     recompute path) scale their adjoints and h operands the same way.
  * The first (K = d_in) and output (M = d_out) layers and every sine stay fp32.
  * Env: INSR_JET_PREC_FWD, INSR_JET_PREC_BWD.  The saved-activation and partial
  * layouts do not depend on it: a forward of one precision pairs with a backward of

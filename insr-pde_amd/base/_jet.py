@@ -88,7 +88,8 @@ class _SirenJet(torch.autograd.Function):
         dy = torch.empty(n, dout, din, device=dev, dtype=torch.float32) if mode != nat.MODE_VALUE else None
         lap = torch.empty(n, dout, device=dev, dtype=torch.float32) if mode == nat.MODE_LAP else None
         act = None
-        if save:
+        # the recompute backward (path 3) reruns the forward per tile: nothing to save
+        if save and lib.insr_jet_bwd_path(n, din, dout, L, W, cmode) != 3:
             nbytes = lib.insr_jet_act_bytes(n, din, L, W, cmode)
             act = torch.empty(max(nbytes // 4, 1), device=dev, dtype=torch.float32)
         if _Fused.pending is not None:  # launched with the other jets of the scope, at its exit
@@ -153,10 +154,12 @@ def _launch_bwd(job):
     st = ctypes.c_void_p(cur.cuda_stream)
     mlp.grad_write_begin(cur)  # order after a write of .grad made on another stream
     if lib.insr_jet_bwd_path(n, din, dout, L, W, cmode) > 0:
-        # two-kernel path (propagation + split-K dW GEMM) or the resident-dW persistent kernel,
-        # with their fixed-order sums straight into .grad
-        work = torch.empty(max(lib.insr_jet_bwd_work_bytes(n, din, dout, L, W, cmode) // 4, 1), device=x2.device,
-                           dtype=torch.float32)
+        # two-kernel path (propagation + split-K dW GEMM), the resident-dW or the recompute persistent
+        # kernel, with their fixed-order sums straight into .grad.  Scratch comes from the pool of the
+        # stream the kernels run on (a deferred job's autograd stream may differ from the current one)
+        with torch.cuda.stream(cur):
+            work = torch.empty(max(lib.insr_jet_bwd_work_bytes(n, din, dout, L, W, cmode) // 4, 1),
+                               device=x2.device, dtype=torch.float32)
         with _timed("bwd", mode, n, W, (din, dout, L)):
             rc = lib.insr_siren_jet_bwd_grad(nat.ptr(x2), n, din, dout, L, W, cmode, nat.ptr(mlp.flat_params()),
                                              nat.ptr(act), nat.ptr(gy), nat.ptr(gdy), nat.ptr(glap), nat.ptr(work),
@@ -164,8 +167,9 @@ def _launch_bwd(job):
         nat.check(rc, "insr_siren_jet_bwd_grad")
         mlp.grad_write_end(cur)
         return
-    part = torch.empty(max(lib.insr_jet_partial_bytes(n, din, dout, L, W, cmode) // 4, 1), device=x2.device,
-                       dtype=torch.float32)
+    with torch.cuda.stream(cur):
+        part = torch.empty(max(lib.insr_jet_partial_bytes(n, din, dout, L, W, cmode) // 4, 1), device=x2.device,
+                           dtype=torch.float32)
     with _timed("bwd", mode, n, W, (din, dout, L)):
         rc = lib.insr_siren_jet_bwd(nat.ptr(x2), n, din, dout, L, W, cmode, nat.ptr(mlp.flat_params()),
                                     nat.ptr(act), nat.ptr(gy), nat.ptr(gdy), nat.ptr(glap), nat.ptr(part), st)
@@ -195,12 +199,13 @@ def _launch_bwd_multi(jobs):
     for k in range(0, len(jobs), nat.MAX_BWD_JOBS):
         chunk = jobs[k:k + nat.MAX_BWD_JOBS]
         arr = (nat.BwdJob * len(chunk))(*[
-            nat.BwdJob(j.x2.data_ptr(), j.act.data_ptr(), nat.ptr(j.gy), nat.ptr(j.gdy), nat.ptr(j.glap), j.x2.shape[0])
+            nat.BwdJob(j.x2.data_ptr(), nat.ptr(j.act), nat.ptr(j.gy), nat.ptr(j.gdy), nat.ptr(j.glap), j.x2.shape[0])
             for j in chunk])
         ns = (ctypes.c_long * len(chunk))(*[j.x2.shape[0] for j in chunk])
         wb = lib.insr_jet_bwd_multi_work_bytes(ns, len(chunk), din, dout, L, W, cmode)
         nat.check(wb if wb < 0 else 0, "insr_jet_bwd_multi_work_bytes")
-        work = torch.empty(max(wb // 4, 1), device=jobs[0].x2.device, dtype=torch.float32)
+        with torch.cuda.stream(cur):  # scratch from the pool of the stream the kernels run on
+            work = torch.empty(max(wb // 4, 1), device=jobs[0].x2.device, dtype=torch.float32)
         with _timed("bwd%d" % len(chunk), mode, sum(ns), W, (din, dout, L)):
             rc = lib.insr_siren_jet_bwd_grad_multi(arr, len(chunk), din, dout, L, W, cmode,
                                                    nat.ptr(mlp.flat_params()), nat.ptr(work), nat.ptr(gflat),

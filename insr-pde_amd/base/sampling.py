@@ -120,7 +120,7 @@ def merge_samples(*parts):
     return torch.cat([p.detach() for p in parts]).requires_grad_(True)
 
 
-_SAMPLER = {}  # device index -> (Philox stream position on the device, seed)
+_SAMPLER = {}  # device index -> (Philox stream position on the device, key, torch seed, reseed mark)
 
 
 def sampler_seed(torch_seed, rank):
@@ -135,25 +135,43 @@ def _dp_rank():
     return d.get_rank() if (d.is_available() and d.is_initialized()) else 0
 
 
+def _torch_rng_offset(dev):
+    """(seed, Philox offset) of the device's default torch generator (torch.cuda.get_rng_state: 8 bytes
+    seed, 8 bytes offset); manual_seed resets the offset to 0."""
+    st = torch.cuda.get_rng_state(dev)
+    seed = int.from_bytes(bytes(st[:8].tolist()), "little")
+    off = int.from_bytes(bytes(st[8:16].tolist()), "little")
+    return st, seed, off
+
+
+_MARK = 4  # the generator offset step a sampler call leaves behind (torch's Philox offsets step by 4)
+
+
 def _sampler(dev):
     """Per-device Philox state of the fused sampler (insr_sample_boxes): (stream position on
-    the device, key).  The key is the device's torch seed with the distributed rank folded in;
-    re-seeding torch (torch.cuda.manual_seed) restarts the stream, so seeded runs repeat their
-    draws.  Created / restarted on an eager call -- phase loops always run iteration 0 eagerly
-    before capturing (a capture keeps the current stream)."""
+    the device, key).  The key is the device's torch seed with the distributed rank folded in.
+    EVERY re-seed of torch (torch.manual_seed / torch.cuda.manual_seed, the same seed again
+    included) restarts the stream, so seeded runs repeat their draws as the reference's torch
+    samplers do: each eager call leaves torch's generator offset _MARK past where it found it, and a
+    re-seed -- which resets that offset to 0 -- shows as an offset below the last mark.  Created /
+    restarted on an eager call -- phase loops always run iteration 0 eagerly before capturing (a
+    capture keeps the current stream)."""
     from . import _native as nat
     key = dev.index
-    with torch.cuda.device(dev):
-        seed = torch.cuda.initial_seed()
     ent = _SAMPLER.get(key)
-    if ent is None or ent[2] != seed:
-        if torch.cuda.is_current_stream_capturing():
-            if ent is None:
-                raise RuntimeError("sampler state must be created before graph capture (run one eager call)")
-            return ent[:2]
+    if torch.cuda.is_current_stream_capturing():
+        if ent is None:
+            raise RuntimeError("sampler state must be created before graph capture (run one eager call)")
+        return ent[:2]
+    st, seed, off = _torch_rng_offset(dev)
+    if ent is None or ent[2] != seed or off < ent[3]:
         state = ent[0].zero_() if ent is not None else torch.zeros(nat.lib().insr_sampler_state_bytes() // 8,
                                                                     device=dev, dtype=torch.int64)
-        ent = _SAMPLER[key] = (state, sampler_seed(seed, _dp_rank()), seed)
+        ent = (state, sampler_seed(seed, _dp_rank()), seed, 0)
+    mark = off + _MARK
+    st[8:16] = torch.tensor(list(mark.to_bytes(8, "little")), dtype=torch.uint8)
+    torch.cuda.set_rng_state(st, dev)
+    ent = _SAMPLER[key] = ent[:3] + (mark,)
     return ent[:2]
 
 

@@ -30,8 +30,19 @@ static int env_or(const char* name, int dflt) {
 }
 
 // Backward-path policy (insr_jet_set_bwd_policy): 0 auto, 1 fused tile-split + partial rows,
-// 2 two-kernel (jet_x6w.hpp), 3 resident dW (jet_x6r.hpp) where it applies.
+// 2 two-kernel (jet_x6w.hpp), 3 resident dW (jet_x6r.hpp), 4 recompute (jet_fb.hpp) where it applies.
 static int g_bwd_policy = 0;
+
+// The recompute backward (jet_fb.hpp: forward + reverse jet per tile in one persistent launch, no
+// saved streams) serves W = 128 nets of 4 hidden layers at the fp32-level backward precision
+// (its products are f16x3 with per-tile scales).  The decision must not depend on n (the forward
+// of the same call skips its saved streams).  Forced by policy 4 only: its first build measured
+// 203 us at 16,708 Laplacian points vs 166 us for the two-kernel backward (gpurun_out r4c,
+// profiles/r04/recompute_v1/) -- VALU / barrier-latency bound, see DESIGN.md.
+bool use_fb(int S, int NT, bool lap, int nq, int L) {
+  if (NT != 8 || nq != 3 || !fb_supported(S, lap, L)) return false;
+  return g_bwd_policy == 4;
+}
 
 // The resident-dW backward (jet_x6r.hpp) serves W = 128 nets of 4 hidden layers (the fluid
 // nets; compiled for that depth only) at x6 precision: value, 2-d gradient and 2-d Laplacian
@@ -566,8 +577,10 @@ struct JetCall {
   // width 256 has no fused split-bf16 backward: the two-kernel path serves it
   bool wide(long n) const { return use_wide(n, S, NT, lap, nqb); }
   bool resident(long n, int L) const { return use_resident(n, S, NT, lap, nqb, L); }
-  // 0: fused tile-split + partial rows (insr_siren_jet_bwd), 1: two-kernel, 2: resident dW
-  int path(long n, int L) const { return resident(n, L) ? 2 : (wide(n) ? 1 : 0); }
+  bool recompute(int L) const { return use_fb(S, NT, lap, nqb, L); }
+  // 0: fused tile-split + partial rows (insr_siren_jet_bwd), 1: two-kernel, 2: resident dW,
+  // 3: recompute (no saved streams)
+  int path(long n, int L) const { return recompute(L) ? 3 : (resident(n, L) ? 2 : (wide(n) ? 1 : 0)); }
 };
 
 }  // namespace insr
@@ -916,6 +929,11 @@ long insr_jet_bwd_multi_work_bytes(const long* n, int njobs, int din, int dout, 
   MultiPlan p;
   const int rc = plan_multi(n, njobs, din, dout, L, W, mode, p);
   if (rc) return rc;
+  if (JetCall(din, W, mode).recompute(L)) {
+    long tiles = 0;
+    for (int k = 0; k < njobs; ++k) tiles += n[k] > 0 ? (n[k] + 15) / 16 : 0;
+    return fb_work_floats(tiles, din, dout, L) * (long)sizeof(float);
+  }
   long bytes = (long)p.nb * insr_jet_partial_stride(din, dout, L, W) * (long)sizeof(float);
   for (int q = 0; q < p.ns; ++q) {
     const long b = insr_jet_bwd_work_bytes(n[p.solo[q]], din, dout, L, W, mode);
@@ -929,9 +947,10 @@ int insr_siren_jet_bwd_grad_multi(const InsrBwdJob* jobs, int njobs, int din, in
                                   const float* params, float* work, float* grad, int accumulate, void* stream) {
   if (!jobs || njobs < 1 || njobs > kBwdJobs) return INSR_EINVAL;
   long ns[kBwdJobs];
+  const bool fb = shape_ok(din, dout, L, W, mode) && JetCall(din, W, mode).recompute(L);
   for (int k = 0; k < njobs; ++k) {
     ns[k] = jobs[k].n;
-    if (jobs[k].n > 0 && (!jobs[k].x || !jobs[k].act)) return INSR_EINVAL;
+    if (jobs[k].n > 0 && (!jobs[k].x || (!jobs[k].act && !fb))) return INSR_EINVAL;
   }
   MultiPlan p;
   int rc = plan_multi(ns, njobs, din, dout, L, W, mode, p);
@@ -940,6 +959,29 @@ int insr_siren_jet_bwd_grad_multi(const InsrBwdJob* jobs, int njobs, int din, in
   if (!params || !work || !grad) return INSR_EINVAL;
   hipStream_t st = (hipStream_t)stream;
   int acc = accumulate ? 1 : 0;
+  {
+    const JetCall c(din, W, mode);
+    if (c.recompute(L)) {  // every job in ONE recompute launch (act is not read)
+      FbJobs J{};
+      int m = 0, t = 0;
+      for (int k = 0; k < njobs; ++k) {
+        if (jobs[k].n <= 0) continue;
+        J.x[m] = jobs[k].x;
+        J.gy[m] = jobs[k].gy;
+        J.gdy[m] = jobs[k].gdy;
+        J.glap[m] = jobs[k].glap;
+        J.n[m] = (int)jobs[k].n;
+        J.tstart[m] = t;
+        t += (int)((jobs[k].n + 15) / 16);
+        ++m;
+      }
+      J.tstart[m] = t;
+      J.njobs = m;
+      const float* prm = params;
+      if (!(prm = with_planes(params, din, dout, L, W, mode, st, 0, &rc))) return rc;
+      return dispatch_fb_bwd(c.S, c.lap, L, J, din, dout, prm, work, grad, acc, st);
+    }
+  }
   if (p.nf > 0) {
     const JetCall c(din, W, mode);
     const float* prm = params;
@@ -985,6 +1027,7 @@ int insr_jet_set_wide_min_width(int width) {
 long insr_jet_bwd_work_bytes(long n, int din, int dout, int L, int W, int mode) {
   if (!shape_ok(din, dout, L, W, mode) || n < 0) return INSR_EINVAL;
   const JetCall c(din, W, mode);
+  if (c.recompute(L)) return fb_work_floats((n + 15) / 16, din, dout, L) * (long)sizeof(float);
   if (c.resident(n, L)) return resident_work_floats(n, din, dout, L) * (long)sizeof(float);
   if (c.wide(n)) return wide_work_floats(n, din, dout, L, W, c.S) * (long)sizeof(float);
   return insr_jet_partial_bytes(n, din, dout, L, W, mode);
@@ -993,10 +1036,10 @@ long insr_jet_bwd_work_bytes(long n, int din, int dout, int L, int W, int mode) 
 int insr_jet_wide_launch_threads(long n, int din, int dout, int L, int W, int mode, long* threads3) {
   if (!shape_ok(din, dout, L, W, mode) || n <= 0 || !threads3 || L < 1) return INSR_EINVAL;
   const JetCall c(din, W, mode);
-  if (c.resident(n, L)) {  // the persistent launch (256-thread blocks) + the dW / compact-row sums
+  if (c.recompute(L) || c.resident(n, L)) {  // the persistent launch + the dW / compact-row sums
     const long Ps = (long)W * din + W + (long)L * W + (long)dout * W + dout;
     const long wq = ((long)W * W / 4 + 63) / 64, rows_x = (Ps + 63) / 64;
-    threads3[0] = (long)resident_blocks(n) * 512;
+    threads3[0] = (long)(c.recompute(L) ? fb_launch_blocks((n + 15) / 16) : resident_blocks(n)) * 512;
     threads3[1] = (wq > rows_x ? wq : rows_x) * (L + 1) * 512;
     threads3[2] = 0;
     return 0;
@@ -1025,7 +1068,7 @@ int insr_jet_set_bwd_f16(int mask) {
 
 int insr_jet_set_bwd_policy(int policy) {
   const int old = g_bwd_policy;
-  if (policy >= 0 && policy <= 3) g_bwd_policy = policy;
+  if (policy >= 0 && policy <= 4) g_bwd_policy = policy;
   return old;
 }
 
@@ -1034,8 +1077,23 @@ int insr_siren_jet_bwd_grad(const float* x, long n, int din, int dout, int L, in
                             float* grad, int accumulate, void* stream) {
   if (!shape_ok(din, dout, L, W, mode) || n < 0 || n > 0x7fffffffL) return INSR_EINVAL;
   if (n == 0) return 0;
-  if (!x || !params || !act || !work || !grad) return INSR_EINVAL;
   const JetCall c(din, W, mode);
+  if (!x || !params || (!act && !c.recompute(L)) || !work || !grad) return INSR_EINVAL;
+  if (c.recompute(L)) {  // act is not read: the kernel recomputes the forward per tile
+    hipStream_t st = (hipStream_t)stream;
+    int rc = 0;
+    if (!(params = with_planes(params, din, dout, L, W, mode, st, 0, &rc))) return rc;
+    FbJobs J{};
+    J.x[0] = x;
+    J.gy[0] = gy;
+    J.gdy[0] = gdy;
+    J.glap[0] = glap;
+    J.n[0] = (int)n;
+    J.tstart[0] = 0;
+    J.tstart[1] = (int)((n + 15) / 16);
+    J.njobs = 1;
+    return dispatch_fb_bwd(c.S, c.lap, L, J, din, dout, params, work, grad, accumulate, st);
+  }
   if (c.resident(n, L)) {
     hipStream_t st = (hipStream_t)stream;
     int rc = 0;

@@ -139,6 +139,27 @@ __device__ __forceinline__ bool wave_any_big(float amax) {
   return __any(amax > kFastArgMax);
 }
 
+template <int CTRL>
+__device__ __forceinline__ float max_dpp(float v) {
+  const int o = __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false);
+  return fmaxf(v, __builtin_bit_cast(float, o));
+}
+// max over the wave's 64 lanes of NON-NEGATIVE values as a wave-uniform (scalar) result: the max of
+// each 16-lane row by four DPP steps (as sum16), then the four rows' maxima read into scalars and
+// combined as unsigned integers (non-negative floats order like their bit patterns) -- no LDS
+// crossbar round trips (__shfl_xor's ds_bpermute chain)
+__device__ __forceinline__ float wave_max_nn(float v) {
+  v = max_dpp<0xB1>(v);
+  v = max_dpp<0x4E>(v);
+  v = max_dpp<0x141>(v);
+  v = max_dpp<0x140>(v);
+  const int b = __builtin_bit_cast(int, v);
+  const unsigned r0 = (unsigned)__builtin_amdgcn_readlane(b, 0), r1 = (unsigned)__builtin_amdgcn_readlane(b, 16);
+  const unsigned r2 = (unsigned)__builtin_amdgcn_readlane(b, 32), r3 = (unsigned)__builtin_amdgcn_readlane(b, 48);
+  const unsigned m01 = r0 > r1 ? r0 : r1, m23 = r2 > r3 ? r2 : r3;
+  return __builtin_bit_cast(float, m01 > m23 ? m01 : m23);
+}
+
 // max over the wave's 64 lanes (every lane gets it)
 __device__ __forceinline__ float wave_max(float v) {
 #pragma unroll
@@ -383,6 +404,25 @@ int dispatch_resident_bwd(int S, bool LAP, int L, const float* x, int N, int din
                           float* grad, int accumulate, hipStream_t st);
 long resident_work_floats(long n, int din, int dout, int L);
 int resident_blocks(long n);
+
+// The jobs of one launch: batches of ONE network (its params), e.g. a phase's interior points and
+// its wall bands from separate network calls; job k covers global tiles [tstart[k], tstart[k + 1]).
+struct FbJobs {
+  const float* x[kBwdJobs];
+  const float* gy[kBwdJobs];
+  const float* gdy[kBwdJobs];
+  const float* glap[kBwdJobs];
+  int n[kBwdJobs];
+  int tstart[kBwdJobs + 1];
+  int njobs;
+};
+// recompute backward (jet_fb.hpp: W = 128, L = 4, f16x3 with per-tile scales): ONE persistent launch
+// (forward + reverse jet per tile, dW resident per CU) + the fixed-order sums; act is not read
+int dispatch_fb_bwd(int S, bool LAP, int L, const FbJobs& J, int din, int dout, const float* prm, float* work,
+                    float* grad, int accumulate, hipStream_t st);
+bool fb_supported(int S, bool LAP, int L);
+long fb_work_floats(long tiles, int din, int dout, int L);
+int fb_launch_blocks(long tiles);
 
 // (S, LAP) combinations: value (1), grad d=1..3 (2..4), lap d=1..3 (3..5)
 #define INSR_DISPATCH(NTV, FN, ...)                \

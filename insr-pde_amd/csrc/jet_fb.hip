@@ -1,0 +1,40 @@
+// jet_fb.hip -- the recompute backward (jet_fb.hpp): W = 128, 4 hidden layers (the fluid nets:
+// velocity 2 -> 2, pressure 2 -> 1), products f16x3 (fp32-level) with per-tile power-of-two scales.
+#include "jet_fb.hpp"
+
+namespace insr {
+
+// (S, LAP) served: the 2-d Laplacian jet (S = 4), the 2-d gradient jet (S = 3), the value jet (S = 1);
+// ZR = hidden layers whose z-streams stay in registers (the rest in LDS)
+bool fb_supported(int S, bool LAP, int L) {
+  if (L != 4) return false;
+  return (S == 4 && LAP) || (S == 3 && !LAP) || (S == 1 && !LAP);
+}
+
+int dispatch_fb_bwd(int S, bool LAP, int L, const FbJobs& J, int din, int dout, const float* prm, float* work,
+                    float* grad, int accumulate, hipStream_t st) {
+  if (!fb_supported(S, LAP, L)) return INSR_EINVAL;
+  switch (S * 2 + (LAP ? 1 : 0)) {
+    case 9: return fb_bwd_t<4, true, 4, 2>(J, din, dout, prm, work, grad, accumulate, st);
+    case 6: return fb_bwd_t<3, false, 4, 2>(J, din, dout, prm, work, grad, accumulate, st);
+    case 2: return fb_bwd_t<1, false, 4, 4>(J, din, dout, prm, work, grad, accumulate, st);
+    default: return INSR_EINVAL;
+  }
+}
+
+long fb_work_floats(long tiles, int din, int dout, int L) { return fb_work_floats_impl(tiles, din, dout, L); }
+int fb_launch_blocks(long tiles) { return fb_blocks(tiles); }
+
+}  // namespace insr
+
+#ifdef INSR_STAMPS
+// diagnostic build only: the recompute kernel's phase stamps of its last launch
+extern "C" int insr_diag_fb_stamps(unsigned long long* out, int n) {
+  const int m = n < 8 * 8 * insr::kFbStampPts ? n : 8 * 8 * insr::kFbStampPts;
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(insr::g_fb_stamps), (size_t)m * sizeof(unsigned long long));
+}
+#endif
+
+namespace insr {
+
+}  // namespace insr

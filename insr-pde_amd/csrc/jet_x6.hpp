@@ -181,7 +181,7 @@ template <int NQ, int NT, int S, int T>
 constexpr size_t fwd_x6_lds_bytes() {
   using G = X6Geo<NT>;
   // f16x3: + [2][T][waves] floats after the planes (the per-tile Laplacian-stream maxima, fwd_x6_block)
-  const size_t planes = (size_t)T * S * np_of<NQ>() * G::PLANE * 2 + (NQ == 4 ? 2 * T * 8 * sizeof(float) : 0);
+  const size_t planes = (size_t)T * S * np_of<NQ>() * G::PLANE * 2 + (NQ == 4 ? (2 * T * 8 + 2 + 8) * sizeof(float) : 0);
   const size_t red = (size_t)G::WV * T * S * 3 * 16 * sizeof(float);  // output-layer combine
   return planes > red ? planes : red;
 }
@@ -212,7 +212,9 @@ __device__ __forceinline__ FragQ<NQ> wsp_frag(const u32x4* __restrict__ wsp, int
 }
 
 // f16x3 (NQ = 4) operand scales of the forward: the value (sin, |h| <= 1) and tangent streams
-// (|dh| <= w |t|: fp16 holds |t| < 2183) enter the fp16 products unscaled; the Laplacian stream
+// (|dh| <= w |t|) enter the fp16 products unscaled -- unless a layer's tangent bound leaves fp16's
+// window (w |t| >= 2^15): then that layer's tangent planes take a block power of two too
+// (fwd_x6_block, a uniform branch); the Laplacian stream
 // (|ddh| <= w |q| + w^2 sum t^2: ~900x the tangents' square) is scaled per tile by the power of two
 // 2^e that maps its bound's maximum into [2^14, 2^15) (fwd_x6_block); the products are unscaled by
 // 2^-8 (the weights' scale) x 2^-e -- all exact
@@ -266,6 +268,18 @@ __device__ __forceinline__ void fwd_x6_block(const float* __restrict__ x, int N,
   float usl[T];
 #pragma unroll
   for (int t = 0; t < T; ++t) usl[t] = 1.f / kF16WScale;
+  // f16x3 tangent streams: unscaled while every |dh| <= w |t| stays below 2^15 -- the common case,
+  // fp16's window holds them with 22 bits.  A wave whose tangent bound leaves the window raises the
+  // layer's LDS flag before the barrier the layer waits on anyway; every wave reads it after that
+  // barrier, and only then (a uniform branch) the block exchanges its maxima and scales the layer's
+  // tangent planes by the power of two 2^e that maps the block maximum into [2^14, 2^15) (layer 0:
+  // t = the W_0 columns, bounded by every wave from W_0 itself).  ust: the next layer's tangent
+  // unscale (block-uniform, scalar).
+  float ust = 1.f / kF16WScale;
+  int* tflag = reinterpret_cast<int*>(zmx + 2 * T * 8);  // [2] by layer parity, then [8] wave maxima
+  if constexpr (NQ == 4 && NTAN > 0) {
+    if (threadIdx.x < 2) tflag[threadIdx.x] = 0;  // ordered before the first reader by layer 0's barrier
+  }
 
   float xv[T][3];
 #pragma unroll
@@ -332,7 +346,8 @@ __device__ __forceinline__ void fwd_x6_block(const float* __restrict__ x, int N,
 #pragma unroll
           for (int t = 0; t < T; ++t)
 #pragma unroll
-            for (int s = 0; s < S; ++s) a[t][i][s] *= (LAP && s == S - 1) ? usl[t] : 1.f / kF16WScale;
+            for (int s = 0; s < S; ++s)
+              a[t][i][s] *= (LAP && s == S - 1) ? usl[t] : (s > 0 ? ust : 1.f / kF16WScale);
         }
       }
     }
@@ -357,7 +372,53 @@ __device__ __forceinline__ void fwd_x6_block(const float* __restrict__ x, int N,
         }
       }
     }
+    // f16x3 tangent streams of layer j's planes: this wave's bound w |t| against fp16's window
+    auto tan_bound = [&]() -> float {
+      float mt = 0.f;
+      if (j == 0) {  // t = W_0 columns at every point: the bound of ALL rows, the same in every wave
+        for (int n = lane; n < W; n += 64)
+          for (int k = 0; k < NTAN; ++k) mt = fmaxf(mt, fabsf(prm[n * din + k]));
+      } else {
+#pragma unroll
+        for (int t = 0; t < T; ++t)
+#pragma unroll
+          for (int i = 0; i < RPW; ++i)
+#pragma unroll
+            for (int k = 0; k < NTAN; ++k)
+#pragma unroll
+              for (int r = 0; r < 4; ++r) mt = fmaxf(mt, fabsf(a[t][i][1 + k][r]));
+      }
+      return OMEGA * mt;
+    };
+    bool tbig = false;
+    if constexpr (NQ == 4 && NTAN > 0) {
+      if (j < L) {
+        tbig = __any(tan_bound() >= 32768.f);
+        if (j > 0 && tbig && lane == 0) tflag[j & 1] = 1;
+      }
+    }
     if (j > 0 || (NQ == 4 && LAP)) __syncthreads();  // every wave has read layer j-1 (and wrote its bounds)
+    float sct = 1.f;  // this layer's tangent-plane scale
+    if constexpr (NQ == 4 && NTAN > 0) {
+      ust = 1.f / kF16WScale;
+      if (j < L) {
+        if (j > 0) tbig = __builtin_amdgcn_readfirstlane(tflag[j & 1]) != 0;
+        if (tbig) {  // rare: the block maximum (layer 0: already every wave's own)
+          float mt = wave_max(tan_bound());
+          if (j > 0) {
+            float* tmx = reinterpret_cast<float*>(tflag + 2);
+            if (lane == 0) tmx[wave] = mt;
+            __syncthreads();
+#pragma unroll
+            for (int w = 0; w < WV; ++w) mt = fmaxf(mt, tmx[w]);
+          }
+          const int e = __builtin_amdgcn_readfirstlane(f16_exp_for(mt));
+          sct = ldexpf(1.f, e);
+          ust = ldexpf(1.f, -e) / kF16WScale;
+        }
+        if (j > 0 && threadIdx.x == 0) tflag[(j + 1) & 1] = 0;  // the other parity's readers passed the barrier
+      }
+    }
     if (act) {
 #pragma unroll
       for (int t = 0; t < T; ++t) {
@@ -393,7 +454,7 @@ __device__ __forceinline__ void fwd_x6_block(const float* __restrict__ x, int N,
 #pragma unroll
           for (int s = 0; s < S; ++s) {
             unsigned short* pw = lds + (t * S + s) * np_of<NQ>() * PLANE + c * LDB + 16 * (rt0 + i) + 4 * g;
-            const float sc = (LAP && s == S - 1) ? sll[t] : 1.f;
+            const float sc = (LAP && s == S - 1) ? sll[t] : (s > 0 ? sct : 1.f);
             lds_put4<NQ, PLANE>(pw, sc * a[t][i][s][0], sc * a[t][i][s][1], sc * a[t][i][s][2], sc * a[t][i][s][3]);
           }
       __syncthreads();
@@ -812,8 +873,8 @@ constexpr int x6_bwd_sg() {
 }
 
 template <int NQ, int NT, int S, int T>
-constexpr size_t bwd_x6_lds_bytes() {  // + 2 x 3 x 8 floats: the waves' per-layer maxima (NQ = 4)
-  return (size_t)T * x6_bwd_sg<NQ, NT, S, T>() * X6BwdGeo<NQ, NT>::SET_BYTES + 2 * 3 * 8 * sizeof(float);
+constexpr size_t bwd_x6_lds_bytes() {  // + 2 x 5 x 8 floats: the waves' per-layer maxima (NQ = 4)
+  return (size_t)T * x6_bwd_sg<NQ, NT, S, T>() * X6BwdGeo<NQ, NT>::SET_BYTES + 2 * 5 * 8 * sizeof(float);
 }
 
 template <int NQ, int NT, int S, bool LAP, int T>
@@ -834,8 +895,8 @@ __global__ __launch_bounds__(X6Geo<NT>::THREADS) void jet_bwd_x6(const BwdJobsX6
   extern __shared__ __attribute__((aligned(16))) float lds_f[];
   unsigned short* Z = reinterpret_cast<unsigned short*>(lds_f);
   unsigned short* H = Z + NSET * ZSET;
-  // NQ = 4, [2][3][waves]: each wave's per-layer max |z̄| over the value / tangent streams and over the
-  // Laplacian stream, and its bound of h_{j-1}'s Laplacian stream
+  // NQ = 4, [2][5][waves]: each wave's per-layer max |z̄| over the value stream, the Laplacian stream, its
+  // bound of h_{j-1}'s Laplacian stream, max |z̄| over the tangent streams, its bound of h_{j-1}'s tangents
   float* zred = lds_f + NSET * (ZSET + HSET) / 2;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
   // NQ = 4 (INSR_BWD_F16_FUSED, the x6 backward's products on the fp16 matrix cores): per layer the
@@ -1035,7 +1096,7 @@ __global__ __launch_bounds__(X6Geo<NT>::THREADS) void jet_bwd_x6(const BwdJobsX6
     }
     INSR_STAMP(L - j, 1);
     if constexpr (NQ == 4) {  // this wave's max |z̄_j| over the block's tiles (read after the group barrier)
-      float mo = 0.f, ml = 0.f;
+      float mv = 0.f, mt = 0.f, ml = 0.f;
 #pragma unroll
       for (int t = 0; t < T; ++t)
 #pragma unroll
@@ -1046,14 +1107,18 @@ __global__ __launch_bounds__(X6Geo<NT>::THREADS) void jet_bwd_x6(const BwdJobsX6
             for (int r = 0; r < 4; ++r) {
               if (LAP && s == S - 1)
                 ml = fmaxf(ml, fabsf(hb[t][i][s][r]));
+              else if (s == 0)
+                mv = fmaxf(mv, fabsf(hb[t][i][s][r]));
               else
-                mo = fmaxf(mo, fabsf(hb[t][i][s][r]));
+                mt = fmaxf(mt, fabsf(hb[t][i][s][r]));
             }
-      mo = wave_max(mo);
+      mv = wave_max(mv);
+      if constexpr (S > 1) mt = wave_max(mt);
       if constexpr (LAP) ml = wave_max(ml);
       if (lane == 0) {  // two slots: layer j - 1 writes the other
-        zred[((j & 1) * 3) * 8 + wave] = mo;
-        zred[((j & 1) * 3 + 1) * 8 + wave] = ml;
+        zred[((j & 1) * 5) * 8 + wave] = mv;
+        zred[((j & 1) * 5 + 1) * 8 + wave] = ml;
+        zred[((j & 1) * 5 + 3) * 8 + wave] = mt;
       }
     }
     // A operand of the propagation: W^T rows m = 16 rt + c, k = n = 32 kc + 8 g + jj, from the
@@ -1069,8 +1134,8 @@ __global__ __launch_bounds__(X6Geo<NT>::THREADS) void jet_bwd_x6(const BwdJobsX6
     floatx4 snp[T][RPW], csp[T][RPW];
     load_sc(j - 1, snp, csp);
     load_zk(j - 1);
-    if constexpr (NQ == 4 && LAP) {  // this wave's bound of h_{j-1}'s Laplacian stream, w |q| + w^2 sum t^2
-      float hl = 0.f;
+    if constexpr (NQ == 4 && S > 1) {  // this wave's bounds of h_{j-1}'s Laplacian (w |q| + w^2 sum t^2)
+      float hl = 0.f, htb = 0.f;       // and tangent streams (w |t|)
 #pragma unroll
       for (int t = 0; t < T; ++t) {
         const float* basep = act_base(act, j - 1, ntiles, tt(t), S, NT);
@@ -1088,13 +1153,20 @@ __global__ __launch_bounds__(X6Geo<NT>::THREADS) void jet_bwd_x6(const BwdJobsX6
           for (int r = 0; r < 4; ++r) {
             float t2 = 0.f;
 #pragma unroll
-            for (int k = 0; k < S - 2; ++k) t2 = fmaf(zd[k][r], zd[k][r], t2);
-            hl = fmaxf(hl, fmaf(OMEGA, fabsf(zd[S - 2][r]), OMEGA2 * t2));
+            for (int k = 0; k < NTAN; ++k) {
+              t2 = fmaf(zd[k][r], zd[k][r], t2);
+              htb = fmaxf(htb, fabsf(zd[k][r]));
+            }
+            if constexpr (LAP) hl = fmaxf(hl, fmaf(OMEGA, fabsf(zd[S - 2][r]), OMEGA2 * t2));
           }
         }
       }
-      hl = wave_max(hl);
-      if (lane == 0) zred[((j & 1) * 3 + 2) * 8 + wave] = hl;
+      if constexpr (LAP) hl = wave_max(hl);
+      htb = wave_max(htb) * OMEGA;
+      if (lane == 0) {
+        zred[((j & 1) * 5 + 2) * 8 + wave] = hl;
+        zred[((j & 1) * 5 + 4) * 8 + wave] = htb;
+      }
     }
     floatx4 dacc[RPW][NT];
 #pragma unroll
@@ -1104,7 +1176,7 @@ __global__ __launch_bounds__(X6Geo<NT>::THREADS) void jet_bwd_x6(const BwdJobsX6
     floatx4 nh[T][RPW][S];
     // NQ = 4: the block's adjoint scale 2^e and its inverse; h_{j-1}'s Laplacian stream x hll = 2^eh,
     // the Laplacian adjoint x zll = 2^-eh more (e maps max(|z̄|, |z̄_lap| 2^-eh) into [2^14, 2^15))
-    float zsc = 1.f, zun = 1.f, zll = 1.f, hll = 1.f;
+    float zsc = 1.f, zun = 1.f, zll = 1.f, hll = 1.f, ztl = 1.f, htl = 1.f;
 #pragma unroll
     for (int gi = 0; gi < NG; ++gi) {
       const int s0 = gi * SG;
@@ -1113,19 +1185,27 @@ __global__ __launch_bounds__(X6Geo<NT>::THREADS) void jet_bwd_x6(const BwdJobsX6
       INSR_STAMP(L - j, 3);
       if constexpr (NQ == 4) {
         if (gi == 0) {
-          const float* zr = zred + (j & 1) * 3 * 8;
-          float mo = zr[0], ml = zr[8], mh = zr[16];
+          // h's tangent streams: unscaled while their bound stays below 2^15 (the common case); else
+          // x 2^eht, and the z̄ tangent streams x 2^-eht (every dW product keeps the block's 2^e)
+          const float* zr = zred + (j & 1) * 5 * 8;
+          float mv = zr[0], ml = zr[8], mh = zr[16], mt = zr[24], mht = zr[32];
 #pragma unroll
           for (int w = 1; w < G::WV; ++w) {
-            mo = fmaxf(mo, zr[w]);
+            mv = fmaxf(mv, zr[w]);
             ml = fmaxf(ml, zr[8 + w]);
             mh = fmaxf(mh, zr[16 + w]);
+            mt = fmaxf(mt, zr[24 + w]);
+            mht = fmaxf(mht, zr[32 + w]);
           }
           if constexpr (LAP) {
             hll = ldexpf(1.f, f16_exp_for(mh));
             zll = 1.f / hll;
           }
-          const int e = f16_exp_for(fmaxf(mo, ml * zll));
+          if constexpr (S > 1) {
+            htl = ldexpf(1.f, mht >= 32768.f ? f16_exp_for(mht) : 0);
+            ztl = 1.f / htl;
+          }
+          const int e = f16_exp_for(fmaxf(mv, fmaxf(mt * ztl, ml * zll)));
           zsc = ldexpf(1.f, e);
           zun = ldexpf(1.f, -e);
         }
@@ -1141,7 +1221,8 @@ __global__ __launch_bounds__(X6Geo<NT>::THREADS) void jet_bwd_x6(const BwdJobsX6
             const int u = t * SG + sl;
             const int col = 16 * (rt0 + i) + 4 * g;
             const bool lq = NQ == 4 && LAP && s == S - 1;  // the fp16 Laplacian-stream scales
-            const float fl = lq ? zll : 1.f;  // after zsc: each factor within fp32's range
+            const bool tq = NQ == 4 && s > 0 && !lq;        // ... and the tangent streams'
+            const float fl = lq ? zll : (tq ? ztl : 1.f);   // after zsc: each factor within fp32's range
             lds_put4<NQ, ZPLANE>(Z + u * ZSET + c * LDB + col, (hb[t][i][s][0] * zsc) * fl,
                                  (hb[t][i][s][1] * zsc) * fl, (hb[t][i][s][2] * zsc) * fl,
                                  (hb[t][i][s][3] * zsc) * fl);
@@ -1152,6 +1233,7 @@ __global__ __launch_bounds__(X6Geo<NT>::THREADS) void jet_bwd_x6(const BwdJobsX6
               hs = h_stream<NT, S, LAP>(basep, s, rt0 + i, lane, snp[t][i], csp[t][i]);
             }
             if (lq) hs *= hll;
+            if (tq) hs *= htl;
             put_neuron_major<NQ, HPLANE>(H + u * HSET, hs, col, c);
           }
       }
@@ -1245,7 +1327,8 @@ __global__ __launch_bounds__(X6Geo<NT>::THREADS) void jet_bwd_x6(const BwdJobsX6
         cs[t][i] = csp[t][i];
 #pragma unroll
         for (int s = 0; s < S; ++s)
-          hb[t][i][s] = (NQ == 4) ? (nh[t][i][s] * zun) * (((LAP && s == S - 1) ? hll : 1.f) / kF16WScale)
+          hb[t][i][s] = (NQ == 4) ? (nh[t][i][s] * zun) *
+                                        (((LAP && s == S - 1) ? hll : (s > 0 ? htl : 1.f)) / kF16WScale)
                                   : nh[t][i][s];
       }
   }

@@ -105,13 +105,15 @@ __global__ __launch_bounds__(512, (x6p_min_waves<NQ, NT>())) void jet_bwd_x6p(co
   // |z̄| (Laplacian stream x 16) into [2^14, 2^15), the product unscaled by 2^-(8 + e) (exact)
   extern __shared__ __attribute__((aligned(16))) float lds_f[];
   unsigned short* Z = reinterpret_cast<unsigned short*>(lds_f);  // [s][q][16 p][W + 8]
-  float* zred = lds_f + S * ZSET / 2;                             // [2][2][8 waves]: tile maxima
+  float* zred = lds_f + S * ZSET / 2;                             // [2][3][8 waves]: tile maxima
   const int tiles_n = (N + 15) / 16;
-  // f16 dW (zmax != NULL): zq [L][tiles][2] = this tile's max |z̄_j| over the value / tangent streams
-  // and over the Laplacian stream (slot j - 1), then hq [L][tiles][8] = each wave's bound of the
-  // Laplacian stream of h_j = w c q - w^2 s sum t^2, i.e. w |q| + w^2 sum t^2 (slot j, j < L)
+  // f16 dW (zmax != NULL): zq [L][tiles][3] = this tile's max |z̄_j| over the value stream, the tangent
+  // streams and the Laplacian stream (slot j - 1), then hq [L][tiles][8] = each wave's bound of the
+  // Laplacian stream of h_j = w c q - w^2 s sum t^2, i.e. w |q| + w^2 sum t^2 (slot j, j < L), then
+  // ht [L][tiles][8] = each wave's bound of h_j's tangent streams, w |t|
   float* zq = zmax;
-  float* hq = zmax ? zmax + 2L * L * tiles_n : nullptr;
+  float* hq = zmax ? zmax + 3L * L * tiles_n : nullptr;
+  float* ht = zmax ? hq + 8L * L * tiles_n : nullptr;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
   const int ntiles = ((N + 63) / 64) * 4;
   const int tile = blockIdx.x;
@@ -196,7 +198,8 @@ __global__ __launch_bounds__(512, (x6p_min_waves<NQ, NT>())) void jet_bwd_x6p(co
   // ---- sine layers j = L .. 0 ----
   for (int j = L; j >= 0; --j) {
     const float* basej = act_base(act, j, ntiles, tile, S, NT);
-    float hl = 0.f;  // this wave's bound of |h_j|'s Laplacian stream
+    float hl = 0.f, htb = 0.f;  // this wave's bounds of |h_j|'s Laplacian and tangent streams
+    constexpr int NTAN = LAP ? S - 2 : S - 1;
 #pragma unroll
     for (int i = 0; i < RPW; ++i) {
       floatx4 zs[S];
@@ -204,23 +207,28 @@ __global__ __launch_bounds__(512, (x6p_min_waves<NQ, NT>())) void jet_bwd_x6p(co
       for (int s = 0; s < S; ++s)
         zs[s] = (s == 0) ? floatx4{0.f, 0.f, 0.f, 0.f}
                          : *reinterpret_cast<const floatx4*>(basej + ((s * NT + rt0 + i) * 64 + lane) * 4);
-      if constexpr (LAP) {
-        if (hq && j < L) {
+      if (hq && j < L) {
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            float t2 = 0.f;
+        for (int r = 0; r < 4; ++r) {
+          float t2 = 0.f;
 #pragma unroll
-            for (int k = 1; k < S - 1; ++k) t2 = fmaf(zs[k][r], zs[k][r], t2);
-            hl = fmaxf(hl, fmaf(OMEGA, fabsf(zs[S - 1][r]), OMEGA2 * t2));
+          for (int k = 1; k <= NTAN; ++k) {
+            t2 = fmaf(zs[k][r], zs[k][r], t2);
+            htb = fmaxf(htb, fabsf(zs[k][r]));
           }
+          if constexpr (LAP) hl = fmaxf(hl, fmaf(OMEGA, fabsf(zs[S - 1][r]), OMEGA2 * t2));
         }
       }
       sine_rev<S, LAP>(hb[i], zs, sn[i], cs[i]);  // hb = z̄_j
     }
-    if constexpr (LAP) {
-      if (hq && j < L) {
+    if (hq && j < L) {
+      if constexpr (LAP) {
         hl = wave_max(hl);
         if (lane == 0) hq[((long)j * tiles_n + tile) * 8 + wave] = hl;
+      }
+      if constexpr (NTAN > 0) {
+        htb = wave_max(htb) * OMEGA;
+        if (lane == 0) ht[((long)j * tiles_n + tile) * 8 + wave] = htb;
       }
     }
     const long boff = (j == 0) ? (long)W * din : sb + (long)(j - 1) * W;
@@ -254,8 +262,8 @@ __global__ __launch_bounds__(512, (x6p_min_waves<NQ, NT>())) void jet_bwd_x6p(co
 #pragma unroll
         for (int s = 0; s < S; ++s) *reinterpret_cast<floatx4*>(ab + ((s * NT + rt0 + i) * 64 + lane) * 4) = hb[i][s];
     }
-    if (zmax || NQ == 4) {  // this wave's max |z̄_j| over the value / tangent streams and the Laplacian one
-      float mo = 0.f, ml = 0.f;
+    if (zmax || NQ == 4) {  // this wave's max |z̄_j| over the value, tangent and Laplacian streams
+      float mv = 0.f, mt = 0.f, ml = 0.f;
 #pragma unroll
       for (int i = 0; i < RPW; ++i)
 #pragma unroll
@@ -264,14 +272,18 @@ __global__ __launch_bounds__(512, (x6p_min_waves<NQ, NT>())) void jet_bwd_x6p(co
           for (int r = 0; r < 4; ++r) {
             if (LAP && s == S - 1)
               ml = fmaxf(ml, fabsf(hb[i][s][r]));
+            else if (s == 0)
+              mv = fmaxf(mv, fabsf(hb[i][s][r]));
             else
-              mo = fmaxf(mo, fabsf(hb[i][s][r]));
+              mt = fmaxf(mt, fabsf(hb[i][s][r]));
           }
-      mo = wave_max(mo);
+      mv = wave_max(mv);
+      if constexpr (S > 1) mt = wave_max(mt);
       if constexpr (LAP) ml = wave_max(ml);
       if (lane == 0) {  // two slots: layer j - 1 writes the other
-        zred[((j & 1) * 2) * 8 + wave] = mo;
-        zred[((j & 1) * 2 + 1) * 8 + wave] = ml;
+        zred[((j & 1) * 3) * 8 + wave] = mv;
+        zred[((j & 1) * 3 + 1) * 8 + wave] = mt;
+        zred[((j & 1) * 3 + 2) * 8 + wave] = ml;
       }
     }
     __syncthreads();  // the previous layer's readers of Z are done
@@ -279,11 +291,11 @@ __global__ __launch_bounds__(512, (x6p_min_waves<NQ, NT>())) void jet_bwd_x6p(co
     // accumulators here) and the products' unscales 2^-(8 + e)
     float zso = 1.f, zsl = 1.f, zuo = 1.f, zul = 1.f;
     if constexpr (NQ == 4) {
-      float mo = zred[((j & 1) * 2) * 8], ml = zred[((j & 1) * 2 + 1) * 8];
+      float mo = fmaxf(zred[((j & 1) * 3) * 8], zred[((j & 1) * 3 + 1) * 8]), ml = zred[((j & 1) * 3 + 2) * 8];
 #pragma unroll
       for (int w = 1; w < 8; ++w) {
-        mo = fmaxf(mo, zred[((j & 1) * 2) * 8 + w]);
-        ml = fmaxf(ml, zred[((j & 1) * 2 + 1) * 8 + w]);
+        mo = fmaxf(mo, fmaxf(zred[((j & 1) * 3) * 8 + w], zred[((j & 1) * 3 + 1) * 8 + w]));
+        ml = fmaxf(ml, zred[((j & 1) * 3 + 2) * 8 + w]);
       }
       const int eo = f16_exp_for(mo), el = f16_exp_for(ml);
       zso = ldexpf(1.f, eo);
@@ -301,14 +313,14 @@ __global__ __launch_bounds__(512, (x6p_min_waves<NQ, NT>())) void jet_bwd_x6p(co
       }
     __syncthreads();
     if (zq && threadIdx.x == 0) {
-      float mo = zred[((j & 1) * 2) * 8], ml = zred[((j & 1) * 2 + 1) * 8];
+      float m3[3];
 #pragma unroll
-      for (int w = 1; w < 8; ++w) {
-        mo = fmaxf(mo, zred[((j & 1) * 2) * 8 + w]);
-        ml = fmaxf(ml, zred[((j & 1) * 2 + 1) * 8 + w]);
+      for (int k = 0; k < 3; ++k) {
+        m3[k] = zred[((j & 1) * 3 + k) * 8];
+#pragma unroll
+        for (int w = 1; w < 8; ++w) m3[k] = fmaxf(m3[k], zred[((j & 1) * 3 + k) * 8 + w]);
+        zq[((long)(j - 1) * tiles_n + tile) * 3 + k] = m3[k];
       }
-      zq[((long)(j - 1) * tiles_n + tile) * 2] = mo;
-      zq[((long)(j - 1) * tiles_n + tile) * 2 + 1] = ml;
     }
     // propagation: h̄_{j-1}[m] = sum_n W_j[n][m] z̄_j[n]; A = W^T rows m of this wave (pre-split
     // planes, orientation 1: NQ b128 loads per fragment), B = Z rows (one b128 per plane)
@@ -450,28 +462,40 @@ __global__ __launch_bounds__(512, (NQ == 4 && NT == 8) ? INSR_F16_BWD_WAVES : 1)
   const int c0 = (int)((long)chunks * blockIdx.x / KS), c1 = (int)((long)chunks * (blockIdx.x + 1) / KS);
   // fp16 operand scales (NQ = 4): z̄ x asc (x ascl more on the Laplacian stream), h's Laplacian
   // stream x bscl, the partial x osc
-  float asc = 1.f, ascl = 1.f, bscl = 1.f, osc = 1.f;
+  // h's tangent streams enter unscaled while their bound w |t| stays below 2^15 (the common case, as
+  // before); a slice holding a larger bound scales them x 2^eht and the z̄ tangent streams x 2^-eht
+  // (every product keeps 2^e); ascl / asct / bsct: those factors
+  float asc = 1.f, ascl = 1.f, bscl = 1.f, osc = 1.f, asct = 1.f, bsct = 1.f;
   if constexpr (NQ == 4) {
-    float mo = 0.f, ml = 0.f, mh = 0.f;
+    float mv = 0.f, mt = 0.f, ml = 0.f, mh = 0.f, mht = 0.f;
     if (c1 > c0) {
       const int ta = (2 * c0) / S, tb = min((2 * c1 - 1) / S, tiles - 1);
-      const float* hq = zmax + 2L * L * tiles;
+      const float* hq = zmax + 3L * L * tiles;
+      const float* htq = hq + 8L * L * tiles;
       for (int t = ta + lane; t <= tb; t += 64) {
-        mo = fmaxf(mo, zmax[((long)(j - 1) * tiles + t) * 2]);
-        ml = fmaxf(ml, zmax[((long)(j - 1) * tiles + t) * 2 + 1]);
+        mv = fmaxf(mv, zmax[((long)(j - 1) * tiles + t) * 3]);
+        mt = fmaxf(mt, zmax[((long)(j - 1) * tiles + t) * 3 + 1]);
+        ml = fmaxf(ml, zmax[((long)(j - 1) * tiles + t) * 3 + 2]);
       }
-      if constexpr (LAP)
-        for (int q = lane; q < (tb - ta + 1) * 8; q += 64) mh = fmaxf(mh, hq[((long)(j - 1) * tiles + ta) * 8 + q]);
+      for (int q = lane; q < (tb - ta + 1) * 8; q += 64) {
+        if constexpr (LAP) mh = fmaxf(mh, hq[((long)(j - 1) * tiles + ta) * 8 + q]);
+        if constexpr (S > 1) mht = fmaxf(mht, htq[((long)(j - 1) * tiles + ta) * 8 + q]);
+      }
     }
-    mo = wave_max(mo);
+    mv = wave_max(mv);
+    mt = wave_max(mt);
     ml = wave_max(ml);
     mh = wave_max(mh);
+    mht = wave_max(mht);
     const int eh = LAP ? f16_exp_for(mh) : 0;
-    const float bl = ldexpf(1.f, eh);
-    const int e = f16_exp_for(fmaxf(mo, ml / bl));
+    const int eht = mht >= 32768.f ? f16_exp_for(mht) : 0;
+    const float bl = ldexpf(1.f, eh), bt = ldexpf(1.f, eht);
+    const int e = f16_exp_for(fmaxf(mv, fmaxf(mt / bt, ml / bl)));
     asc = ldexpf(1.f, e);
     ascl = 1.f / bl;  // applied after asc: z̄_lap 2^e 2^-eh, each factor within fp32's range
+    asct = 1.f / bt;
     bscl = bl;
+    bsct = bt;
     osc = ldexpf(1.f, -e);
   }
 
@@ -558,8 +582,9 @@ __global__ __launch_bounds__(512, (NQ == 4 && NT == 8) ? INSR_F16_BWD_WAVES : 1)
       const floatx4 zero = floatx4{0.f, 0.f, 0.f, 0.f};
       if constexpr (NQ == 4) {
         const bool lq = LAP && s == S - 1;
-        dw_put<NQ, NT>(A, live ? (lq ? (rzb[it] * asc) * ascl : rzb[it] * asc) : zero, rt, ul, lane);
-        dw_put<NQ, NT>(B, live ? (lq ? hv * bscl : hv) : zero, rt, ul, lane);
+        const float fa = lq ? ascl : (s > 0 ? asct : 1.f), fb = lq ? bscl : (s > 0 ? bsct : 1.f);
+        dw_put<NQ, NT>(A, live ? (rzb[it] * asc) * fa : zero, rt, ul, lane);
+        dw_put<NQ, NT>(B, live ? hv * fb : zero, rt, ul, lane);
       } else {
         dw_put<NQ, NT>(A, live ? rzb[it] : zero, rt, ul, lane);
         dw_put<NQ, NT>(B, live ? hv : zero, rt, ul, lane);
@@ -745,7 +770,7 @@ inline long wide_work_floats_impl(long n, int din, int dout, int L, int W, int S
   const long adj = (long)L * ntiles * S * (W / 16) * 256;
   const long small = ((n + 15) / 16) * small_count(din, dout, L, W);
   const long dw = (long)L * wide_ks(n, S, L) * W * W;
-  const long zmax = 10L * L * ((n + 15) / 16);  // tile maxima of the adjoints and h bounds (fp16 dW)
+  const long zmax = 19L * L * ((n + 15) / 16);  // tile maxima of the adjoints and h bounds (fp16 dW)
   return adj + small + dw + (long)kSmallRS * small_count(din, dout, L, W) + zmax;
 }
 
@@ -776,8 +801,8 @@ int wide_bwd_t(const float* x, int N, int din, int dout, int L, const float* prm
   // the x6 precision's products on the fp16 matrix cores (dw_x6 / jet_bwd_x6p NQ = 4, above)
   const bool f16dw = NQ == 3 && (g_bwd_f16 & INSR_BWD_F16_DW) && L > 0;
   const bool f16p = NQ == 3 && (g_bwd_f16 & INSR_BWD_F16_PROP) && L > 0;
-  constexpr size_t lds_p = (size_t)S * np_of<NQ>() * 16 * (W + 8) * 2 + 2 * 2 * 8 * sizeof(float);
-  constexpr size_t lds_p4 = (size_t)S * 2 * 16 * (W + 8) * 2 + 2 * 2 * 8 * sizeof(float);
+  constexpr size_t lds_p = (size_t)S * np_of<NQ>() * 16 * (W + 8) * 2 + 2 * 3 * 8 * sizeof(float);
+  constexpr size_t lds_p4 = (size_t)S * 2 * 16 * (W + 8) * 2 + 2 * 3 * 8 * sizeof(float);
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)jet_bwd_x6p<NQ, NT, S, LAP>, hipFuncAttributeMaxDynamicSharedMemorySize,

@@ -79,15 +79,12 @@ class ElasticityModel(BaseModel):
     def _sample_in_training(self, resolution):
         d, parts = self.dim, []
         if self.use_mesh:  # elasticity/model.py:200-207
-            # weak scaling: every rank draws the same world-sized batch (default generator, same
-            # seed: graph-capturable) and keeps its own slice, so ranks train on disjoint points
-            world = self._dp_world()
-            w, r = (world, torch.distributed.get_rank()) if (
-                world > 1 and getattr(self.cfg, "insr_dp_weak", False)) else (1, 0)
+            # weak scaling: each rank draws its own n points -- ranks seed their CUDA generators
+            # differently (bench.py: 1234 + 7919 rank; BaseModel._dp_shard), so the draws are
+            # independent without drawing a world-sized batch and discarding most of it
             for s in self.sample_pattern:
                 if s == 'random':
-                    n = resolution ** d
-                    parts.append(self.mesh_sampler.sample(n * w)[r * n:(r + 1) * n, :d])
+                    parts.append(self.mesh_sampler.sample(resolution ** d)[:, :d])
                 elif s == 'uniform':
                     parts.append(self.mesh_V[:, :d])
                 else:

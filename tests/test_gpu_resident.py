@@ -139,7 +139,8 @@ def test_default_routing(B):
     """Auto policy: the fluid nets' Laplacian backward at the headline batch (16,384 interior +
     324 band points) runs the two-kernel path, value backwards the fused kernel; at the fluid2DtlgnM
     batch (65,536 + 1,308 band points) the value backward runs resident and the Laplacian one the
-    two-kernel path while its products run f16x3 (resident with bf16x6 products)."""
+    two-kernel path while its products run f16x3 (resident with bf16x6 products); the recompute
+    path (3) only when forced (policy 4)."""
     lib = B._native.lib()
     nat = B._native
     assert lib.insr_jet_bwd_path(16708, 2, 1, 4, 128, nat.MODE_LAP) == 1
@@ -150,4 +151,4 @@ def test_default_routing(B):
     assert lib.insr_jet_bwd_path(66844, 2, 1, 4, 128, nat.MODE_LAP) == 2
     lib.insr_jet_set_bwd_f16(old)
     assert lib.insr_jet_bwd_path(66844, 2, 2, 4, 128, nat.MODE_VALUE) == 2
-    assert lib.insr_jet_bwd_path(20400, 2, 2, 5, 128, nat.MODE_GRAD) != 2  # 5 hidden layers: not resident
+    assert lib.insr_jet_bwd_path(20400, 2, 2, 5, 128, nat.MODE_GRAD) not in (2, 3)  # 5 hidden layers

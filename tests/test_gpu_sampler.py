@@ -245,3 +245,23 @@ def test_draw_plan_one_launch_per_iteration(B):
         assert calls == [1, 2], calls
     finally:
         lib.insr_sample_boxes = orig
+
+
+@pytest.mark.gpu
+def test_same_seed_reseed_repeats_draws(B):
+    """Re-seeding torch with the SAME seed restarts the device sampler's stream, as the reference's
+    torch samplers repeat their draws (base/sampling.py:14-18); torch's own CUDA draws in between
+    (which only advance torch's generator) do not restart it."""
+    for reseed in (torch.manual_seed, torch.cuda.manual_seed):
+        reseed(0)
+        a = B.sample_random(1000, 2, device="cuda")
+        a2 = B.sample_random(1000, 2, device="cuda")
+        reseed(0)
+        b = B.sample_random(1000, 2, device="cuda")
+        torch.rand(10, device="cuda")  # torch's own CUDA RNG in between
+        b2 = B.sample_random(1000, 2, device="cuda")
+        assert torch.equal(a, b) and not torch.equal(a, a2)
+        assert not torch.equal(b, b2)
+    torch.manual_seed(1)
+    c = B.sample_random(1000, 2, device="cuda")
+    assert not torch.equal(a, c)
