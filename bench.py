@@ -177,8 +177,8 @@ def build_model(args, world, rank):
     import base
     from pde.config import baseline_config
     base._native.load(args.lib, check_build=args.lib is None)
-    base._native.lib().insr_jet_set_bwd_policy(args.bwd_policy)
-    base._native.lib().insr_jet_set_bwd_f16(args.bwd_f16)
+    # the run's knobs (per-call mode bits of every jet this thread launches; none: library defaults)
+    base._native.set_default_knobs(policy=args.bwd_policy or None, bwd_f16=None if args.bwd_f16 < 0 else args.bwd_f16)
     wl = WORKLOADS[args.config]
     res = wl["res"]
     cfg = baseline_config(args.config, sample_resolution=res, insr_graph=not args.no_graph,
@@ -281,21 +281,15 @@ def macs_per_point(din, dout, L, W):
 def jet_precision_names(precision):
     """The matrix-core PRODUCTS the jets actually run (forward / backward).  'fp32' is the fp32-level
     contract: f16x3 forwards; backwards whose contract is bf16x6 run f16x3 products on every path the
-    insr_jet_set_bwd_f16 mask covers and on the recompute path (always f16x3), bf16x6 products on the
+    INSR_JET_BWD_F16 mask covers and on the recompute path (always f16x3), bf16x6 products on the
     resident-dW kernel and on paths the mask leaves out."""
     from base import _native as nat
     if precision != "fp32":
         return {"mixed": "bf16x3/bf16"}.get(precision, precision)
-    import ctypes
-    f, b = ctypes.c_int(), ctypes.c_int()
-    nat.lib().insr_jet_get_precision(ctypes.byref(f), ctypes.byref(b))
-    names = {v: k for k, v in nat.PRECISIONS.items()}
-    bwd = names[b.value]
-    if b.value == nat.PREC_BF16X6:
-        mask = nat.lib().insr_jet_set_bwd_f16(-1)
-        bwd = "f16x3" if mask == 7 else (f"bf16x6+f16x3(mask {mask})" if mask else "bf16x6")
-        bwd += " (resident-dW kernel: bf16x6)" if mask else ""
-    return f"{names[f.value]}/{bwd}"
+    mask = nat.bwd_f16_mask()
+    bwd = "f16x3" if mask == 7 else (f"bf16x6+f16x3(mask {mask})" if mask else "bf16x6")
+    bwd += " (resident-dW kernel: bf16x6)" if mask else ""
+    return f"f16x3/{bwd}"  # the library's default pair: f16x3 forward, bf16x6-contract backward
 
 
 def roofline(loops, n_local, precision="fp32"):
@@ -360,16 +354,16 @@ def kernel_identity(kind, mode, n, din, dout, L, W, nq=3):
     """The rocprof name and grid (threads) of the jet kernel the library picks for this launch, and
     the split products per fp32-equivalent MAC it runs (6 bf16x6, 3 f16x3 / bf16x3, 1 bf16).
     nq = 3 (the fp32-level precision): the forward runs f16x3 (template NQ = 4), the backward's
-    products per the insr_jet_set_bwd_f16 mask (NQ = 4 where on)."""
+    products per the INSR_JET_BWD_F16 mask (NQ = 4 where on)."""
     from base import _native as nat
     lib = nat.lib()
     prec = {3: nat.PREC_BF16X6, 2: nat.PREC_BF16X3, 1: nat.PREC_BF16}[nq]
     m = {"value": nat.MODE_VALUE, "grad": nat.MODE_GRAD, "lap": nat.MODE_LAP}[mode]
-    m_b = m | nat.jet_prec(prec)
+    m_b = m | nat.jet_prec(prec) | nat.scope_bits()  # + the run's knobs (policy, f16 mask)
     S = {"value": 1, "grad": 1 + din, "lap": 2 + din}[mode]
     NT = W // 16
     lap = "true" if mode == "lap" else "false"
-    f16 = lib.insr_jet_set_bwd_f16(-1) if nq == 3 else 0
+    f16 = nat.bwd_f16_mask() if nq == 3 else 0
     nprod = {4: 3, 3: 6, 2: 3, 1: 1}
     path = lib.insr_jet_bwd_path(n, din, dout, L, W, m_b) if kind == "bwd" else 0
     if path == 3:  # the recompute backward (forward + reverse jet per tile, f16x3) + the fixed-order sums
@@ -403,7 +397,7 @@ def kernel_identity(kind, mode, n, din, dout, L, W, nq=3):
         nb = lib.insr_jet_partial_blocks(n, din, W, m_b)
         q = 4 if f16 & 4 else nq
     else:
-        mf = m if nq == 3 else m_b  # the process-default forward precision (f16x3) serves the fp32-level runs
+        mf = (m | nat.scope_bits()) if nq == 3 else m_b  # the default forward precision (f16x3) serves the fp32-level runs
         T = lib.insr_jet_split_tiles(n, din, W, mf, 0)
         nb = ((n + 15) // 16 + T - 1) // T
         q = 4 if nq == 3 else nq
@@ -591,7 +585,7 @@ def main():
         return rehearse(args, world, rank)
     model, cfg, wl, n_local = build_model(args, world, rank)
     from base import _native
-    bwd_f16 = _native.lib().insr_jet_set_bwd_f16(-1)  # the backward products on fp16 matrix cores in effect
+    bwd_f16 = _native.bwd_f16_mask()  # the backward products on fp16 matrix cores in effect
     nph = len(wl["phases"])
     loops = phase_loops(model, wl)
     log(f"model built, {n_local} points per rank per phase")

@@ -47,8 +47,8 @@ extern "C" {
 #define INSR_MODE_LAP   2 /* y, dy/dx_i, sum_i d2y/dx_i^2        (2 + d_in streams) */
 #define INSR_MODE_MASK  0xF
 /* Per-call matrix-core precision: OR INSR_JET_PREC(p) (p an INSR_PREC_* below) into the
- * `mode` argument of any jet entry point or query; without it the process default
- * (insr_jet_set_precision) applies.  The saved-activation layout does not depend on it. */
+ * `mode` argument of any jet entry point or query; without it the default (f16x3 forward,
+ * bf16x6 backward) applies.  The saved-activation layout does not depend on it. */
 #define INSR_MODE_PREC_SHIFT 4
 #define INSR_JET_PREC(p) (((p) + 1) << INSR_MODE_PREC_SHIFT)
 /* Backward-only override (a "mixed" precision: e.g. a bf16x3 forward with a bf16 backward):
@@ -61,6 +61,33 @@ extern "C" {
  * with the parameters.  Without it an entry point that runs split-bf16 kernels splits the
  * weights itself, into a per-stream scratch copy (one copy + one launch per call). */
 #define INSR_MODE_WSPLIT (1 << 8)
+/* Per-call knobs (A/B studies; every field 0 = the library's measured policy).  The library keeps
+ * no mutable process-wide configuration and reads no environment: calls on distinct streams or
+ * host threads with different knobs are independent (re-entrant).  OR them into `mode` of the
+ * jet entry points and of the host queries (insr_jet_bwd_path, *_work_bytes, ...); a forward and
+ * the backward of its saved streams must carry the same knobs.
+ *   INSR_JET_POLICY(p)     backward path: 0 auto, 1 fused tile-split where it exists, 2 two-kernel,
+ *                          3 resident dW, 4 recompute where it applies (insr_jet_bwd_path)
+ *   INSR_JET_BWD_F16(m)    mask of INSR_BWD_F16_* products of the x6 backward on the fp16 matrix
+ *                          cores (0..7; without the field: all three)
+ *   INSR_JET_TILES(f,b,m)  tile-split blocks: forced forward / backward tiles per block (0 auto,
+ *                          1, 2, 4: the largest feasible T not above) and the minimum block count
+ *                          of the auto choice (INSR_MINB_256 (default) / _512 / _128 / _1024)
+ *   INSR_MODE_WIDE128      the two-kernel backward from width 128 (else from 256, plus the
+ *                          measured width-128 batch thresholds) */
+#define INSR_MODE_WIDE128 (1 << 9)
+#define INSR_MODE_POLICY_SHIFT 16
+#define INSR_JET_POLICY(p) (((p) + 1) << INSR_MODE_POLICY_SHIFT)
+#define INSR_MODE_F16_SHIFT 19
+#define INSR_JET_BWD_F16(m) (((m) + 1) << INSR_MODE_F16_SHIFT)
+#define INSR_MODE_TILES_SHIFT 23
+#define INSR_TILES_CODE(t) ((t) == 4 ? 3 : ((t) == 2 ? 2 : ((t) == 1 ? 1 : 0)))
+#define INSR_MINB_256 0
+#define INSR_MINB_512 1
+#define INSR_MINB_128 2
+#define INSR_MINB_1024 3
+#define INSR_JET_TILES(f, b, minb) \
+  ((INSR_TILES_CODE(f) | (INSR_TILES_CODE(b) << 2) | ((minb) << 4)) << INSR_MODE_TILES_SHIFT)
 
 #define INSR_EINVAL   (-1) /* unsupported shape / mode / null pointer */
 #define INSR_EWIDTH   (-2) /* hidden width not in the compiled set      */
@@ -230,29 +257,20 @@ int insr_jet_bwd_is_wide(long n_points, int d_in, int width, int mode);
  * n_points (the forward's decision and the backward's agree). */
 int insr_jet_bwd_path(long n_points, int d_in, int d_out, int num_hidden, int width, int mode);
 
-/* Backward-path policy (A/B studies): 0 = auto (default), 1 = fused where it exists,
- * 2 = two-kernel, 3 = resident dW, 4 = recompute where it applies.  Returns the previous policy
- * (a policy outside 0..4 changes nothing: -1 queries). */
-int insr_jet_set_bwd_policy(int policy);
 /* Matrix products of the x6 (fp32-level) backward that run on the fp16 matrix cores instead of
  * six bf16 products: f16x3 (two fp16 terms per operand, three products, 22 significant bits),
  * the adjoints scaled by the power of two that maps the largest |value| of their K slice / tile
- * into [2^14, 2^15) (undone exactly), the weights by 2^8 (the fp16 planes).  Bit mask:
+ * into [2^14, 2^15) (undone exactly), the weights by 2^8 (the fp16 planes).  Bits of the per-call
+ * INSR_JET_BWD_F16 mask (default: all three):
  * INSR_BWD_F16_DW the two-kernel path's dW GEMM, INSR_BWD_F16_PROP its adjoint propagation,
- * INSR_BWD_F16_FUSED the fused tile-split kernel.
- * Returns the previous mask (-1 queries).  Process-wide. */
+ * INSR_BWD_F16_FUSED the fused tile-split kernel. */
 #define INSR_BWD_F16_DW 1
 #define INSR_BWD_F16_PROP 2
 #define INSR_BWD_F16_FUSED 4 /* the fused tile-split backward (dW and propagation, per-block scales) */
-int insr_jet_set_bwd_f16(int mask);
 /* Threads of the three launches of a two-kernel backward (propagation, dW partials, dW sums),
  * as profilers report them; INSR_EINVAL when (n, shape, mode) does not take that path. */
 int insr_jet_wide_launch_threads(long n_points, int d_in, int d_out, int num_hidden, int width, int mode,
                                  long* threads3);
-/* Smallest width (128 or 256) that takes the wide path; returns the old value.
- * Default 256.  Process-wide A/B knob (no environment override). */
-int insr_jet_set_wide_min_width(int width);
-
 /* Number of partial-gradient rows insr_siren_jet_bwd writes for n points: one per
  * T-tile (16T-point) block, T as the backward selects for this size, width and mode. */
 int insr_jet_partial_blocks(long n_points, int d_in, int width, int mode);
@@ -261,16 +279,9 @@ int insr_jet_partial_blocks(long n_points, int d_in, int width, int mode);
  * backward) uses for this batch. */
 int insr_jet_split_tiles(long n_points, int d_in, int width, int mode, int backward);
 
-/* Tile-count policy: force T for forward / backward (0 = auto: the largest T
- * whose LDS fits, lowered while the grid has fewer than min_blocks blocks).
- * A/B-study knob (tools/); the default policy needs no call. */
-void insr_jet_set_split_tiles(int fwd_tiles, int bwd_tiles, int min_blocks);
-
-void insr_jet_get_split_tiles(int* fwd_tiles, int* bwd_tiles, int* min_blocks);
-
 /*
- * Matrix-core precision of the hidden-layer GEMMs (process default per direction; a call
- * may override it with INSR_JET_PREC(p) in its mode):
+ * Matrix-core precision of the hidden-layer GEMMs (per call: INSR_JET_PREC(p) / INSR_JET_BPREC(p)
+ * in its mode; the defaults are f16x3 forward, bf16x6 backward):
  *   INSR_PREC_F32     v_mfma_f32_16x16x4_f32: exact fp32 products, the fp32 matrix rate.
  *   INSR_PREC_BF16X6  every fp32 operand split in three bf16 terms, six
  *                     v_mfma_f32_16x16x32_bf16 products per K chunk, fp32 accumulation:
@@ -288,10 +299,10 @@ void insr_jet_get_split_tiles(int* fwd_tiles, int* bwd_tiles, int* min_blocks);
  *                     into [2^14, 2^15); the tangent streams unscaled while their bound w |t| stays
  *                     below 2^15, else (a uniform branch, rare) by their own block power of two; all
  *                     undone exactly on the products.  Range: |W| < 255 (the weight planes), the
- *                     streams fp32's.  The f16 backward products (insr_jet_set_bwd_f16, the
+ *                     streams fp32's.  The f16 backward products (INSR_JET_BWD_F16, the
  *                     recompute path) scale their adjoints and h operands the same way.
  * The first (K = d_in) and output (M = d_out) layers and every sine stay fp32.
- * Env: INSR_JET_PREC_FWD, INSR_JET_PREC_BWD.  The saved-activation and partial
+ * The saved-activation and partial
  * layouts do not depend on it: a forward of one precision pairs with a backward of
  * another.
  */
@@ -300,8 +311,6 @@ void insr_jet_get_split_tiles(int* fwd_tiles, int* bwd_tiles, int* min_blocks);
 #define INSR_PREC_BF16X3 2
 #define INSR_PREC_BF16   3
 #define INSR_PREC_F16X3  4
-void insr_jet_set_precision(int fwd, int bwd);
-void insr_jet_get_precision(int* fwd, int* bwd);
 
 /* grad[i] = (accumulate ? grad[i] : 0) + sum_b partial[b * count + i], fixed order. */
 int insr_reduce_partials(const float* partial, int n_blocks, long count, float* grad,

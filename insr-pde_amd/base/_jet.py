@@ -100,7 +100,7 @@ class _SirenJet(torch.autograd.Function):
                                             nat.ptr(dy), nat.ptr(lap), nat.ptr(act), nat.stream_of(dev))
             nat.check(rc, "insr_siren_jet_fwd")
         ctx.set_materialize_grads(False)  # unused outputs -> None -> NULL adjoint (no zero-fill launch)
-        ctx.mode, ctx.mlp, ctx.save = mode, mlp, save
+        ctx.mode, ctx.cmode, ctx.mlp, ctx.save = mode, cmode, mlp, save  # the backward reuses the forward's mode
         ctx.x2, ctx.act = x2, act
         outs = [y]
         if dy is not None:
@@ -122,7 +122,7 @@ class _SirenJet(torch.autograd.Function):
         if gy is None and gdy is None and glap is None:
             return none
         c = lambda t: None if t is None else (t if t.is_contiguous() else t.contiguous())  # noqa: E731
-        job = _BwdJob(mlp, mode, ctx.x2, ctx.act, c(gy), c(gdy), c(glap))
+        job = _BwdJob(mlp, mode, ctx.cmode, ctx.x2, ctx.act, c(gy), c(gdy), c(glap))
         if _BwdBatch.pending is not None:  # launched with the network's other jobs at the scope's exit
             _BwdBatch.pending.append(job)
         else:
@@ -131,12 +131,14 @@ class _SirenJet(torch.autograd.Function):
 
 
 class _BwdJob:
-    """One reverse jet: the network, its jet mode, the forward's points / saved streams, the
-    adjoints, and the stream autograd ran its backward on."""
-    __slots__ = ("mlp", "mode", "x2", "act", "gy", "gdy", "glap", "cur")
+    """One reverse jet: the network, its jet mode and its forward's full call mode (precision and
+    knob bits: the backward runs with the knobs its forward ran with, whatever scope is open
+    when autograd reaches it), the forward's points / saved streams, the adjoints, and the
+    stream autograd ran its backward on."""
+    __slots__ = ("mlp", "mode", "cmode", "x2", "act", "gy", "gdy", "glap", "cur")
 
-    def __init__(self, mlp, mode, x2, act, gy, gdy, glap):
-        self.mlp, self.mode, self.x2, self.act = mlp, mode, x2, act
+    def __init__(self, mlp, mode, cmode, x2, act, gy, gdy, glap):
+        self.mlp, self.mode, self.cmode, self.x2, self.act = mlp, mode, cmode, x2, act
         self.gy, self.gdy, self.glap = gy, gdy, glap
         self.cur = torch.cuda.current_stream(x2.device)
 
@@ -146,7 +148,7 @@ def _launch_bwd(job):
     mlp, mode, x2, act, gy, gdy, glap = job.mlp, job.mode, job.x2, job.act, job.gy, job.gdy, job.glap
     n, din = x2.shape
     L, W, dout = mlp.num_hidden_layers, mlp.kernel_width, mlp.out_features
-    cmode = mlp.call_mode(mode)
+    cmode = job.cmode
     mlp.ensure_wsplit()
     lib = nat.lib()
     gflat, accumulate = mlp.grad_for_backward()
@@ -190,7 +192,7 @@ def _launch_bwd_multi(jobs):
     mlp, mode, cur = jobs[0].mlp, jobs[0].mode, jobs[0].cur
     din = jobs[0].x2.shape[1]
     L, W, dout = mlp.num_hidden_layers, mlp.kernel_width, mlp.out_features
-    cmode = mlp.call_mode(mode)
+    cmode = jobs[0].cmode
     mlp.ensure_wsplit()
     lib = nat.lib()
     gflat, accumulate = mlp.grad_for_backward()
@@ -260,7 +262,7 @@ class immediate_backward:
 def _flush_backward(jobs):
     groups = {}
     for j in jobs:
-        groups.setdefault((id(j.mlp), j.mlp.call_mode(j.mode), j.cur.cuda_stream), []).append(j)
+        groups.setdefault((id(j.mlp), j.cmode, j.cur.cuda_stream), []).append(j)
     for js in groups.values():
         if len(js) == 1:
             _launch_bwd(js[0])

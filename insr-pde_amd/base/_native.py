@@ -5,8 +5,10 @@ If it is missing or was not built, every hot-path call raises NativeUnavailable.
 torch is imported first so the library binds to the HIP runtime torch already
 loaded (both carry SONAME libamdhip64.so.7).
 """
+import contextlib
 import ctypes
 import os
+import threading
 
 import torch  # noqa: F401  (must precede the CDLL load: shared HIP runtime)
 
@@ -32,6 +34,92 @@ MODE_BPREC_SHIFT = 12
 def jet_bprec(p):
     """INSR_JET_BPREC(p): a backward-only precision override OR-ed into a jet `mode`."""
     return (int(p) + 1) << MODE_BPREC_SHIFT
+
+
+# Per-call knobs (include/insr_siren.h INSR_JET_POLICY / INSR_JET_BWD_F16 / INSR_JET_TILES /
+# INSR_MODE_WIDE128): bits of the `mode` argument.  The library keeps no mutable configuration.
+MODE_WIDE128 = 1 << 9
+MODE_POLICY_SHIFT, MODE_F16_SHIFT, MODE_TILES_SHIFT = 16, 19, 23
+BWD_F16_DW, BWD_F16_PROP, BWD_F16_FUSED = 1, 2, 4
+_TCODE = {0: 0, 1: 1, 2: 2, 4: 3}
+_MINB = {256: 0, 512: 1, 128: 2, 1024: 3}
+_PREC_BITS = (0xF << MODE_PREC_SHIFT) | (0xF << MODE_BPREC_SHIFT)
+_FIELDS = {"policy": 7 << MODE_POLICY_SHIFT, "bwd_f16": 0xF << MODE_F16_SHIFT, "tiles": 0x3F << MODE_TILES_SHIFT,
+           "wide128": MODE_WIDE128, "prec": _PREC_BITS}
+
+
+def jet_policy(p):
+    """INSR_JET_POLICY(p): backward path 0 auto, 1 fused, 2 two-kernel, 3 resident dW, 4 recompute."""
+    return (int(p) + 1) << MODE_POLICY_SHIFT
+
+
+def jet_bwd_f16(mask):
+    """INSR_JET_BWD_F16(mask): the x6 backward's products on the fp16 matrix cores (BWD_F16_* bits)."""
+    return (int(mask) + 1) << MODE_F16_SHIFT
+
+
+def jet_tiles(fwd=0, bwd=0, min_blocks=256):
+    """INSR_JET_TILES: forced tiles per block (0 auto, 1, 2, 4) and the auto choice's minimum block count."""
+    return (_TCODE[int(fwd)] | (_TCODE[int(bwd)] << 2) | (_MINB[int(min_blocks)] << 4)) << MODE_TILES_SHIFT
+
+
+def knob_bits(policy=None, bwd_f16=None, tiles=None, wide128=None, prec=None):
+    """Mode bits of the given knobs (None: the field stays at the library default).
+    tiles = (fwd, bwd[, min_blocks]); prec = (fwd, bwd) INSR_PREC_* codes."""
+    b = 0
+    if policy is not None:
+        b |= jet_policy(policy)
+    if bwd_f16 is not None:
+        b |= jet_bwd_f16(bwd_f16)
+    if tiles is not None:
+        b |= jet_tiles(*tiles)
+    if wide128:
+        b |= MODE_WIDE128
+    if prec is not None:
+        b |= jet_prec(prec[0]) | jet_bprec(prec[1])
+    return b
+
+
+# A knob scope of the calling thread: the bits base.MLP.call_mode adds to the jets it launches
+# (forward time: the backward of a jet reuses its forward's mode, so the two always agree).
+# A network's own precision (MLP(precision=...)) wins over a scope's `prec`.
+_scope = threading.local()
+
+
+def scope_bits():
+    return getattr(_scope, "bits", 0)
+
+
+def _merged(old, kw):
+    clear = 0
+    for k, v in kw.items():
+        if v is not None:
+            clear |= _FIELDS[k]
+    return (old & ~clear) | knob_bits(**kw)
+
+
+def set_default_knobs(**kw):
+    """The calling thread's knob scope for the rest of its life (drivers: bench.py, tools/)."""
+    _scope.bits = _merged(scope_bits(), kw)
+    return _scope.bits
+
+
+def bwd_f16_mask(bits=None):
+    """The INSR_BWD_F16_* mask a call with these mode bits (default: the scope's) runs with."""
+    f = ((scope_bits() if bits is None else bits) >> MODE_F16_SHIFT) & 0xF
+    return f - 1 if f else BWD_F16_DW | BWD_F16_PROP | BWD_F16_FUSED
+
+
+@contextlib.contextmanager
+def knobs(**kw):
+    """with knobs(policy=4, bwd_f16=0, tiles=(1, 4, 512), wide128=True, prec=(1, 1)): ... -- A/B
+    studies and tests; fields not named keep the enclosing scope's value."""
+    old = scope_bits()
+    _scope.bits = _merged(old, kw)
+    try:
+        yield _scope.bits
+    finally:
+        _scope.bits = old
 LOSS_COMBO, LOSS_BANDS = 0, 1
 OPT_LR, OPT_STEP, OPT_BEST, OPT_BAD, OPT_STEPSIZE, OPT_BC2SQRT, OPT_FACTOR, OPT_MINLR = range(8)
 OPT_TICKET = 8  # the fused Adam + plateau launch's last-block ticket (0 between launches)
@@ -61,9 +149,6 @@ SIGNATURES = {
     "insr_jet_bwd_multi_work_bytes": (_L, [_P, _I, _I, _I, _I, _I, _I]),
     "insr_jet_bwd_is_wide": (_I, [_L, _I, _I, _I]),
     "insr_jet_bwd_path": (_I, [_L, _I, _I, _I, _I, _I]),
-    "insr_jet_set_bwd_policy": (_I, [_I]),
-    "insr_jet_set_bwd_f16": (_I, [_I]),
-    "insr_jet_set_wide_min_width": (_I, [_I]),
     "insr_comm_available": (_I, []),
     "insr_comm_id_bytes": (_L, []),
     "insr_comm_unique_id": (_I, [_P]),
@@ -88,10 +173,6 @@ SIGNATURES = {
     "insr_adam_plateau_step_nets": (_I, [_I, _P, _P, _P, _P, _P, _P, _P, _F, _F, _F, _P, _I, _P]),
     "insr_jet_wide_launch_threads": (_I, [_L, _I, _I, _I, _I, _I, _P]),
     "insr_sq_loss_bwd": (_I, [_I, _P, _P, _P, _P, _L, _I, _F, _F, _F, _F, _F, _P, _P, _P, _P, _P, _P]),
-    "insr_jet_set_split_tiles": (None, [_I, _I, _I]),
-    "insr_jet_set_precision": (None, [_I, _I]),
-    "insr_jet_get_precision": (None, [_P, _P]),
-    "insr_jet_get_split_tiles": (None, [_P, _P, _P]),
     "insr_reduce_partials": (_I, [_P, _I, _L, _P, _I, _P]),
     "insr_reduce_partials_strided": (_I, [_P, _I, _L, _L, _P, _I, _P]),
     "insr_jet_partial_stride": (_L, [_I, _I, _I, _I]),
@@ -215,26 +296,6 @@ def load(path=None, check_build=True):
 
 def lib():
     return _lib if _lib is not None else load()
-
-
-def get_split_tiles():
-    v = [ctypes.c_int(), ctypes.c_int(), ctypes.c_int()]
-    lib().insr_jet_get_split_tiles(*[ctypes.byref(a) for a in v])
-    return tuple(a.value for a in v)
-
-
-def set_split_tiles(fwd_tiles, bwd_tiles, min_blocks):
-    lib().insr_jet_set_split_tiles(int(fwd_tiles), int(bwd_tiles), int(min_blocks))
-
-
-def get_precision():
-    v = [ctypes.c_int(), ctypes.c_int()]
-    lib().insr_jet_get_precision(*[ctypes.byref(a) for a in v])
-    return tuple(a.value for a in v)
-
-
-def set_precision(fwd, bwd):
-    lib().insr_jet_set_precision(int(fwd), int(bwd))
 
 
 def ptr(t):

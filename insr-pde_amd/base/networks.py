@@ -144,12 +144,12 @@ class MLP(nn.Module):
     def call_mode(self, mode):
         """The jet `mode` argument of this network's library calls (precision bits added; the
         flat buffer carries the pre-split weight planes: INSR_MODE_WSPLIT)."""
-        from ._native import MODE_WSPLIT, jet_bprec, jet_prec
-        mode |= MODE_WSPLIT
+        from ._native import _PREC_BITS, MODE_WSPLIT, jet_bprec, jet_prec, scope_bits
+        mode |= MODE_WSPLIT | scope_bits()  # + the caller's knob scope (_native.knobs)
         if self._prec_pair is None:
             return mode
         pf, pb = self._prec_pair
-        return mode | jet_prec(pf) | (jet_bprec(pb) if pb != pf else 0)
+        return (mode & ~_PREC_BITS) | jet_prec(pf) | (jet_bprec(pb) if pb != pf else 0)
 
     # ---- pre-split weight planes (include/insr_siren.h insr_siren_wsplit) -----------
     # The flat storage is [parameters | pad to 16 B | planes]: every hidden weight split in three

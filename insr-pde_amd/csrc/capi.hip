@@ -24,24 +24,50 @@ int nt_for(int width) {
   return -1;
 }
 
-static int env_or(const char* name, int dflt) {
-  const char* e = std::getenv(name);
-  return e ? std::atoi(e) : dflt;
+// Per-call knobs, decoded from the `mode` argument of every call (include/insr_siren.h:
+// INSR_JET_POLICY, INSR_JET_BWD_F16, INSR_JET_TILES, INSR_MODE_WIDE128; the precisions are
+// INSR_JET_PREC / INSR_JET_BPREC).  The library holds no mutable process-wide configuration and
+// reads no environment: two calls on distinct streams (threads) with different knobs never see
+// each other's, and a field left 0 takes the measured default below.
+constexpr int kMinBlocksDefault = 256;
+constexpr int kBwdF16Default = INSR_BWD_F16_DW | INSR_BWD_F16_PROP | INSR_BWD_F16_FUSED;  // profiles/r03/bwd_f16_ab
+struct Knobs {
+  int policy;    // backward path: 0 auto, 1 fused, 2 two-kernel, 3 resident dW, 4 recompute
+  int f16;       // INSR_BWD_F16_* mask: x6 backward products on the fp16 matrix cores
+  int wide_min;  // smallest width of the two-kernel backward (128 or 256)
+  int tiles[3];  // forced forward T, forced backward T (0 = auto), minimum block count
+};
+static int tiles_of_code(int c) { return c == 3 ? 4 : c; }  // 0 auto, 1, 2, 4
+static int min_blocks_of_code(int c) {
+  static constexpr int v[4] = {kMinBlocksDefault, 512, 128, 1024};
+  return v[c & 3];
 }
-
-// Backward-path policy (insr_jet_set_bwd_policy): 0 auto, 1 fused tile-split + partial rows,
-// 2 two-kernel (jet_x6w.hpp), 3 resident dW (jet_x6r.hpp), 4 recompute (jet_fb.hpp) where it applies.
-static int g_bwd_policy = 0;
+Knobs knobs_of(int mode) {
+  Knobs k;
+  const int pol = (mode >> INSR_MODE_POLICY_SHIFT) & 7, f = (mode >> INSR_MODE_F16_SHIFT) & 0xF;
+  const int t = (mode >> INSR_MODE_TILES_SHIFT) & 0x3F;
+  k.policy = pol ? pol - 1 : 0;
+  k.f16 = f ? f - 1 : kBwdF16Default;
+  k.wide_min = (mode & INSR_MODE_WIDE128) ? 128 : 256;
+  k.tiles[0] = tiles_of_code(t & 3);
+  k.tiles[1] = tiles_of_code((t >> 2) & 3);
+  k.tiles[2] = min_blocks_of_code(t >> 4);
+  return k;
+}
+static bool knobs_ok(int mode) {
+  const int pol = (mode >> INSR_MODE_POLICY_SHIFT) & 7, f = (mode >> INSR_MODE_F16_SHIFT) & 0xF;
+  return pol <= 5 && f <= 8;
+}
 
 // The recompute backward (jet_fb.hpp: forward + reverse jet per tile in one persistent launch, no
 // saved streams) serves W = 128 nets of 4 hidden layers at the fp32-level backward precision
 // (its products are f16x3 with per-tile scales).  The decision must not depend on n (the forward
-// of the same call skips its saved streams).  Forced by policy 4 only: its first build measured
-// 203 us at 16,708 Laplacian points vs 166 us for the two-kernel backward (gpurun_out r4c,
-// profiles/r04/recompute_v1/) -- VALU / barrier-latency bound, see DESIGN.md.
-bool use_fb(int S, int NT, bool lap, int nq, int L) {
+// of the same call skips its saved streams).  Forced by policy 4 only: measured 196 us at 16,708
+// Laplacian points vs 172 us for the two-kernel backward (kbench r4e, profiles/r04/) --
+// VALU / barrier-latency bound, see DESIGN.md.
+bool use_fb(int S, int NT, bool lap, int nq, int L, const Knobs& k) {
   if (NT != 8 || nq != 3 || !fb_supported(S, lap, L)) return false;
-  return g_bwd_policy == 4;
+  return k.policy == 4;
 }
 
 // The resident-dW backward (jet_x6r.hpp) serves W = 128 nets of 4 hidden layers (the fluid
@@ -58,54 +84,34 @@ bool resident_ok(int S, int NT, bool lap, int nq, int L) {
 // the resident kernel stays bf16x6) the two-kernel Laplacian backward wins at the fluid2DtlgnM batch
 // (66,844 points: 553-561 vs 590-601 us; value jets tie at 199-205, profiles/r03/final_r3o/
 // kbench_policy_M.jsonl), so the auto policy keeps the resident kernel for value jets only then.
-bool use_resident(long n, int S, int NT, bool lap, int nq, int L) {
+bool use_resident(long n, int S, int NT, bool lap, int nq, int L, const Knobs& k) {
   if (!resident_ok(S, NT, lap, nq, L)) return false;
-  if (g_bwd_policy == 3) return true;
-  if (g_bwd_policy != 0) return false;
-  const bool f16w = (g_bwd_f16 & (INSR_BWD_F16_DW | INSR_BWD_F16_PROP)) == (INSR_BWD_F16_DW | INSR_BWD_F16_PROP);
+  if (k.policy == 3) return true;
+  if (k.policy != 0) return false;
+  const bool f16w = (k.f16 & (INSR_BWD_F16_DW | INSR_BWD_F16_PROP)) == (INSR_BWD_F16_DW | INSR_BWD_F16_PROP);
   return lap ? (!f16w && n >= 32768) : (S == 1 && n >= 49152);
 }
 
-// Tiles per tile-split block.  The largest T in {1, 2, 4} whose LDS fits a CU,
-// lowered while the grid would have fewer than `min_blocks` blocks (small batches
-// want many short blocks, large ones fewer blocks that share W fetches, barriers
-// and partial rows).  Overrides only through the C ABI (insr_jet_set_split_tiles: force T,
-// 0 = auto; min blocks) -- no environment knobs in the product library.
-constexpr int kMinBlocksDefault = 256;
-static int g_tiles[3] = {0, 0, kMinBlocksDefault};  // forced fwd T, forced bwd T, min blocks
-
-static void tiles_init() {}
-
-// Matrix-core precision of the tile-split kernels (process default per direction; env
-// INSR_JET_PREC_FWD / INSR_JET_PREC_BWD; a call may override it through INSR_JET_PREC(p) in
-// its mode argument -- base.MLP(precision=...) does, per network):
+// Matrix-core precision of the tile-split kernels (a call's INSR_JET_PREC(p) / INSR_JET_BPREC(p);
+// base.MLP(precision=...) sets them per network), else the defaults:
 //   INSR_PREC_F32     v_mfma_f32_16x16x4_f32 (jet_split.hpp)
 //   INSR_PREC_BF16X6  split-bf16, 6 products (jet_x6.hpp, NQ = 3): fp32-level accuracy (default backward)
 //   INSR_PREC_F16X3   fp16 two terms, 3 products (NQ = 4): fp32-level accuracy, forward only (default forward)
 //   INSR_PREC_BF16X3  split-bf16, 3 products (NQ = 2)
 //   INSR_PREC_BF16    bf16 operands, fp32 accumulation (NQ = 1)
-static int g_prec[2] = {-1, -1};  // fwd, bwd
-
-static void prec_init() {
-  if (g_prec[0] < 0) {
-    // default: the fp16 two-term forward (f16x3: fields <= 4.2e-6, gradients <= 5.1e-6 vs the
-    // oracle like x6's 3.5e-6 / 5.1e-6, profiles/r03/prec_f16x3.jsonl; forward jets 15-30 %
-    // faster, headline 71-74 -> 78.6-78.9 M pts/s same box, profiles/r03/f16x3_ab) and the
-    // split-bf16 x6 backward (same accuracy as fp32 MFMA, measured faster: profiles/r01/kbench_x6.jsonl)
-    g_prec[0] = env_or("INSR_JET_PREC_FWD", INSR_PREC_F16X3);
-    g_prec[1] = env_or("INSR_JET_PREC_BWD", INSR_PREC_BF16X6);
-  }
-}
+// Default forward f16x3 (fields <= 4.2e-6, gradients <= 5.1e-6 vs the oracle like x6's 3.5e-6 /
+// 5.1e-6, profiles/r03/prec_f16x3.jsonl; forward jets 15-30 % faster, profiles/r03/f16x3_ab) and the
+// split-bf16 x6 backward (same accuracy as fp32 MFMA, measured faster: profiles/r01/kbench_x6.jsonl)
+constexpr int kPrecDefault[2] = {INSR_PREC_F16X3, INSR_PREC_BF16X6};
 
 static bool prec_ok(int p) { return p >= INSR_PREC_F32 && p <= INSR_PREC_F16X3; }
 
 // precision of a call (direction bwd): the mode's backward override (bwd), else its
-// override, else the process default
+// override, else the default
 int call_prec(int mode, int bwd) {
-  prec_init();
   const int pb = (mode >> INSR_MODE_BPREC_SHIFT) & 0xF;
   const int po = (mode >> INSR_MODE_PREC_SHIFT) & 0xF;
-  const int p = (bwd && pb) ? pb - 1 : (po ? po - 1 : g_prec[bwd ? 1 : 0]);
+  const int p = (bwd && pb) ? pb - 1 : (po ? po - 1 : kPrecDefault[bwd ? 1 : 0]);
   // f16x3 is a forward precision: its backward runs the fp32-level split-bf16 kernels
   return (bwd && p == INSR_PREC_F16X3) ? INSR_PREC_BF16X6 : p;
 }
@@ -117,18 +123,17 @@ int nq_of(int prec) {
 }
 
 // Backward through the two-kernel path (jet_x6w.hpp: propagation kernel + split-K dW GEMM)
-// for the split-bf16 precisions at widths >= g_wide_min (default 256; insr_jet_set_wide_min_width,
-// A/B studies only) and, at width 128, for Laplacian jets of >= 8192 points and 3-4
+// for the split-bf16 precisions at widths >= wide_min (default 256; INSR_MODE_WIDE128 for A/B
+// studies) and, at width 128, for Laplacian jets of >= 8192 points and 3-4
 // stream gradient jets of >= 32768 points.  Measured (profiles/r02/kbench_wide_vs_fused.jsonl,
 // backward into .grad incl. reductions): LAP 16384 points 244 -> 182 us, LAP 65536 813 -> 698,
 // GRAD (S = 3) 65536 595 -> 548; GRAD 16384 140 vs 144 and every value jet stay fused.
-static int g_wide_min = 256;
-bool use_wide(long n, int S, int NT, bool lap, int nq) {
+bool use_wide(long n, int S, int NT, bool lap, int nq, const Knobs& k) {
   if (NT < 8 || nq == 0) return false;
-  if (g_bwd_policy == 2) return true;
-  if (g_bwd_policy == 1 && NT == 8) return false;
-  if (16 * NT >= g_wide_min) return true;
-  if (NT != 8 || g_wide_min > 256) return false;
+  if (k.policy == 2) return true;
+  if (k.policy == 1 && NT == 8) return false;
+  if (16 * NT >= k.wide_min) return true;
+  if (NT != 8 || k.wide_min > 256) return false;
   // with the pre-split weight planes (kbench r2s31, profiles/r02/wide_vs_fused_wsplit.jsonl):
   // Laplacian and 2-d gradient jets from 8,192 points (gradient 16,708: 143 vs 175 us fused),
   // value jets from ~24K points: round 3, f16x3 products on both paths (kbench r3aa, backward
@@ -138,15 +143,7 @@ bool use_wide(long n, int S, int NT, bool lap, int nq) {
   return S == 1 && n >= 24576;
 }
 
-static int cu_count() {
-  static int c = -1;
-  if (c < 0) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c <= 0) c = 256;
-  }
-  return c;
-}
+static int cu_count() { return device_cus(); }
 
 // per-precision dispatch (nq = 0: exact fp32)
 static int fwd_q(int nq, int NT, int S, bool lap, int T, const float* x, int N, int din, int dout, int L,
@@ -161,7 +158,7 @@ static int fwd_q(int nq, int NT, int S, bool lap, int T, const float* x, int N, 
 }
 // the kernel precision of a fused tile-split backward at precision nq: the x6 backward's products on
 // the fp16 matrix cores under INSR_BWD_F16_FUSED (jet_h_bwd.hip)
-static int fused_bwd_nq(int nq) { return (nq == 3 && (g_bwd_f16 & INSR_BWD_F16_FUSED)) ? 4 : nq; }
+static int fused_bwd_nq(int nq, const Knobs& k) { return (nq == 3 && (k.f16 & INSR_BWD_F16_FUSED)) ? 4 : nq; }
 
 // J == NULL: occupancy query; the exact-fp32 kernel takes one job per launch
 static int bwd_q(int nq, int NT, int S, bool lap, int T, const BwdJobsX6* J, int din, int dout, int L,
@@ -183,19 +180,27 @@ static int bwd_q(int nq, int NT, int S, bool lap, int T, const BwdJobsX6* J, int
 
 // resident blocks per CU of a tile-split kernel instantiation (launchers answer N < 0)
 static int occupancy(int bwd, int nq, int NT, int S, bool lap, int T) {
+  static std::mutex mu;  // calls from several host threads (one per stream) share the cache
   static std::map<int, int> cache;
   const int key = (((((bwd * 8 + nq) * 32 + NT) * 8 + S) * 2 + (lap ? 1 : 0)) * 8) + T;
-  auto it = cache.find(key);
-  if (it != cache.end()) return it->second;
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = cache.find(key);
+    if (it != cache.end()) return it->second;
+  }
   const int r = bwd ? bwd_q(nq, NT, S, lap, T, nullptr, 0, 0, 0, nullptr, nullptr, 0, nullptr)
                     : fwd_q(nq, NT, S, lap, T, nullptr, -1, 0, 0, 0, nullptr, nullptr, nullptr, nullptr, nullptr, 0,
                             nullptr);
+  std::lock_guard<std::mutex> lk(mu);
   cache[key] = r;
   return r;
 }
 
-int split_tiles(int bwd, int NT, int S, long n, bool lap, int nq) {
-  tiles_init();
+// Tiles per tile-split block.  The largest T in {1, 2, 4} whose LDS fits a CU,
+// lowered while the grid would have fewer than the call's minimum block count (small batches
+// want many short blocks, large ones fewer blocks that share W fetches, barriers
+// and partial rows).  A call may force T per direction (INSR_JET_TILES: A/B studies).
+int split_tiles(int bwd, int NT, int S, long n, bool lap, int nq, const Knobs& k) {
   const bool x6 = nq > 0;
   // LDS per tile: fp32 planes [S][16][W+8] (+ backward h planes [S][16][W]); split-bf16
   // forward: NQ bf16 planes [S][NQ][16][W+8]; backward: one stream group of bf16 Z + H planes
@@ -209,7 +214,7 @@ int split_tiles(int bwd, int NT, int S, long n, bool lap, int nq) {
   // backward T = 4 only for value jets (register budget of the derivative streams)
   int T = NT > 8 ? ((x6 && !bwd) ? (S == 1 ? 4 : (S == 2 ? 2 : 1)) : 1) : ((bwd && S > 1) ? 2 : 4);
   while (T > 1 && (size_t)T * plane > 163840) T >>= 1;
-  const int forced = g_tiles[bwd ? 1 : 0];
+  const int forced = k.tiles[bwd ? 1 : 0];
   if (forced > 0) {  // the largest feasible T not above the forced one
     while (T > forced) T >>= 1;
     return T;
@@ -226,7 +231,7 @@ int split_tiles(int bwd, int NT, int S, long n, bool lap, int nq) {
     if (S > 1) return 1;
     return tiles <= 512 ? 1 : (tiles <= 2600 ? 2 : 4);
   }
-  while (T > 1 && (tiles + T - 1) / T < g_tiles[2]) T >>= 1;
+  while (T > 1 && (tiles + T - 1) / T < k.tiles[2]) T >>= 1;
   // occupancy-aware: a T whose last round of blocks (resident blocks per CU x CUs) is
   // nearly empty loses to a smaller T that packs the CUs, e.g. the x6 gradient forward at
   // 20,000 points: T = 4 -> 313 one-per-CU blocks = 2 rounds (97 us) vs T = 1 -> 1250
@@ -257,11 +262,10 @@ int split_tiles(int bwd, int NT, int S, long n, bool lap, int nq) {
 struct LaunchShape {
   int T, nbal;
 };
-LaunchShape launch_shape(int bwd, int nq, int NT, int S, bool lap, long n) {
-  LaunchShape sh{split_tiles(bwd, NT, S, n, lap, nq), 0};
-  tiles_init();
-  if (nq == 0 || NT > 8 || lap || g_tiles[bwd ? 1 : 0] > 0) return sh;  // exact fp32 / forced T: plain
-  if (bwd && S == 1 && NT == 8 && g_tiles[2] == kMinBlocksDefault) {
+LaunchShape launch_shape(int bwd, int nq, int NT, int S, bool lap, long n, const Knobs& k) {
+  LaunchShape sh{split_tiles(bwd, NT, S, n, lap, nq, k), 0};
+  if (nq == 0 || NT > 8 || lap || k.tiles[bwd ? 1 : 0] > 0) return sh;  // exact fp32 / forced T: plain
+  if (bwd && S == 1 && NT == 8 && k.tiles[2] == kMinBlocksDefault) {
     // x6 value backward at W = 128 (unless an A/B study set its own minimum block count): every block writes one full partial-gradient row (P floats)
     // that reduce_partials re-reads, so below ~5 tiles per CU the block count, not the CU fill,
     // sets the time.  About half as many blocks as CUs wins (kbench r3d, fluid_vel, backward +
@@ -550,8 +554,11 @@ __global__ void adam_multi_kernel(AdamList L, float* __restrict__ st, float b1, 
 bool shape_ok(int din, int dout, int L, int width, int mode) {
   if (din < 1 || din > 3 || dout < 1 || dout > 3 || L < 0 || L > 64) return false;
   if (nt_for(width) < 0) return false;
-  if (mode & ~(INSR_MODE_MASK | (0xF << INSR_MODE_PREC_SHIFT) | (0xF << INSR_MODE_BPREC_SHIFT) | INSR_MODE_WSPLIT))
+  if (mode & ~(INSR_MODE_MASK | (0xF << INSR_MODE_PREC_SHIFT) | (0xF << INSR_MODE_BPREC_SHIFT) | INSR_MODE_WSPLIT |
+               INSR_MODE_WIDE128 | (7 << INSR_MODE_POLICY_SHIFT) | (0xF << INSR_MODE_F16_SHIFT) |
+               (0x3F << INSR_MODE_TILES_SHIFT)))
     return false;
+  if (!knobs_ok(mode)) return false;
   const int po = (mode >> INSR_MODE_PREC_SHIFT) & 0xF, pb = (mode >> INSR_MODE_BPREC_SHIFT) & 0xF;
   if ((po && !prec_ok(po - 1)) || (pb && !prec_ok(pb - 1))) return false;
   const int jm = mode & INSR_MODE_MASK;
@@ -562,22 +569,24 @@ bool shape_ok(int din, int dout, int L, int width, int mode) {
   return true;
 }
 
-// one jet call's configuration: jet mode, streams, row tiles, bf16 terms per direction
+// one jet call's configuration: jet mode, streams, row tiles, bf16 terms per direction, knobs
 struct JetCall {
   int jm, S, NT, nqf, nqb;
   bool lap;
+  Knobs k;
   JetCall(int din, int W, int mode)
       : jm(mode & INSR_MODE_MASK),
         S(streams_for(din, mode & INSR_MODE_MASK)),
         NT(nt_for(W)),
         nqf(nq_of(call_prec(mode, 0))),
         nqb(nq_of(call_prec(mode, 1))),
-        lap((mode & INSR_MODE_MASK) == INSR_MODE_LAP) {}
+        lap((mode & INSR_MODE_MASK) == INSR_MODE_LAP),
+        k(knobs_of(mode)) {}
   bool ok() const { return S > 0 && NT > 0; }
   // width 256 has no fused split-bf16 backward: the two-kernel path serves it
-  bool wide(long n) const { return use_wide(n, S, NT, lap, nqb); }
-  bool resident(long n, int L) const { return use_resident(n, S, NT, lap, nqb, L); }
-  bool recompute(int L) const { return use_fb(S, NT, lap, nqb, L); }
+  bool wide(long n) const { return use_wide(n, S, NT, lap, nqb, k); }
+  bool resident(long n, int L) const { return use_resident(n, S, NT, lap, nqb, L, k); }
+  bool recompute(int L) const { return use_fb(S, NT, lap, nqb, L, k); }
   // 0: fused tile-split + partial rows (insr_siren_jet_bwd), 1: two-kernel, 2: resident dW,
   // 3: recompute (no saved streams)
   int path(long n, int L) const { return recompute(L) ? 3 : (resident(n, L) ? 2 : (wide(n) ? 1 : 0)); }
@@ -680,7 +689,7 @@ int insr_siren_jet_fwd(const float* x, long n, int din, int dout, int L, int W, 
   if (!x || !params || !y) return INSR_EINVAL;
   if (c.jm != INSR_MODE_VALUE && !dy) return INSR_EINVAL;
   if (c.lap && !lap) return INSR_EINVAL;
-  const LaunchShape sh = launch_shape(0, c.nqf, c.NT, c.S, c.lap, n);
+  const LaunchShape sh = launch_shape(0, c.nqf, c.NT, c.S, c.lap, n, c.k);
   int rc = 0;
   if (c.nqf > 0 && !(params = with_planes(params, din, dout, L, W, mode, (hipStream_t)stream, 0, &rc))) return rc;
   return fwd_q(c.nqf, c.NT, c.S, c.lap, sh.T, x, (int)n, din, dout, L, params, y, dy, lap, act, sh.nbal,
@@ -716,13 +725,13 @@ int insr_siren_jet_fwd_multi(const InsrJetJob* jobs, int njobs, int din, int dou
   if (live > 1 && !c.lap && NT >= 4 && !grad128_big && c.nqf > 0) {
     // tiles per block from the combined batch; a job whose own batch would take fewer
     // (a boundary band) runs 1-tile blocks, placed first in the grid
-    int T = split_tiles(0, NT, S, total, false, c.nqf);
+    int T = split_tiles(0, NT, S, total, false, c.nqf, c.k);
     InsrJetJob pk[INSR_MAX_FWD_JOBS];
     int small[INSR_MAX_FWD_JOBS], nbal[INSR_MAX_FWD_JOBS];
     int m = 0;
     for (int k = 0; k < njobs; ++k)
       if (jobs[k].n > 0) {
-        small[m] = split_tiles(0, NT, S, jobs[k].n, false, c.nqf) < T ? 1 : 0;
+        small[m] = split_tiles(0, NT, S, jobs[k].n, false, c.nqf, c.k) < T ? 1 : 0;
         nbal[m] = 0;
         pk[m] = jobs[k];
         int rc = 0;
@@ -862,7 +871,7 @@ int insr_siren_jet_bwd(const float* x, long n, int din, int dout, int L, int W, 
   const long P = insr_jet_partial_stride(din, dout, L, W);  // row stride of the partial rows
   // width 256: the fused split-bf16 backward does not exist -- exact fp32 serves this entry
   const int nq = c.NT > 8 ? 0 : c.nqb;
-  const LaunchShape sh = launch_shape(1, nq, c.NT, c.S, c.lap, n);
+  const LaunchShape sh = launch_shape(1, nq, c.NT, c.S, c.lap, n, c.k);
   int rc = 0;
   if (nq > 0 && !(params = with_planes(params, din, dout, L, W, mode, (hipStream_t)stream, 0, &rc))) return rc;
   BwdJobsX6 J{};
@@ -876,7 +885,7 @@ int insr_siren_jet_bwd(const float* x, long n, int din, int dout, int L, int W, 
   J.first[0] = 0;
   J.first[1] = sh.nbal > 0 ? sh.nbal : (int)(((n + 15) / 16 + sh.T - 1) / sh.T);
   J.njobs = 1;
-  return bwd_q(fused_bwd_nq(nq), c.NT, c.S, c.lap, sh.T, &J, din, dout, L, params, partial, P, (hipStream_t)stream);
+  return bwd_q(fused_bwd_nq(nq, c.k), c.NT, c.S, c.lap, sh.T, &J, din, dout, L, params, partial, P, (hipStream_t)stream);
 }
 
 // Plan of a multi-job backward (insr_siren_jet_bwd_grad_multi): the jobs whose own size takes the
@@ -909,7 +918,7 @@ static int plan_multi(const long* n, int njobs, int din, int dout, int L, int W,
   }
   if (total > 0x7fffffffL) return INSR_EINVAL;
   if (p.nf == 0) return 0;
-  const LaunchShape sh = launch_shape(1, p.nq, c.NT, c.S, c.lap, total);
+  const LaunchShape sh = launch_shape(1, p.nq, c.NT, c.S, c.lap, total, c.k);
   p.T = sh.T;
   for (int q = 0; q < p.nf; ++q) {
     const long tk = (n[p.fused[q]] + 15) / 16, plain = (tk + sh.T - 1) / sh.T;
@@ -1003,7 +1012,7 @@ int insr_siren_jet_bwd_grad_multi(const InsrBwdJob* jobs, int njobs, int din, in
     J.first[p.nf] = b;
     J.njobs = p.nf;
     const long P = insr_jet_partial_stride(din, dout, L, W);
-    if ((rc = bwd_q(fused_bwd_nq(p.nq), c.NT, c.S, c.lap, p.T, &J, din, dout, L, prm, work, P, st))) return rc;
+    if ((rc = bwd_q(fused_bwd_nq(p.nq, c.k), c.NT, c.S, c.lap, p.T, &J, din, dout, L, prm, work, P, st))) return rc;
     if ((rc = insr_reduce_partials_strided(work, p.nb, insr_siren_param_count(din, dout, L, W), P, grad, acc, stream)))
       return rc;
     acc = 1;
@@ -1016,12 +1025,6 @@ int insr_siren_jet_bwd_grad_multi(const InsrBwdJob* jobs, int njobs, int din, in
     acc = 1;
   }
   return 0;
-}
-
-int insr_jet_set_wide_min_width(int width) {
-  const int old = g_wide_min;
-  g_wide_min = width;
-  return old;
 }
 
 long insr_jet_bwd_work_bytes(long n, int din, int dout, int L, int W, int mode) {
@@ -1060,18 +1063,6 @@ int insr_jet_bwd_path(long n, int din, int dout, int L, int W, int mode) {
   return JetCall(din, W, mode).path(n, L);
 }
 
-int insr_jet_set_bwd_f16(int mask) {
-  const int old = g_bwd_f16;
-  if (mask >= 0 && mask <= 7) g_bwd_f16 = mask;
-  return old;
-}
-
-int insr_jet_set_bwd_policy(int policy) {
-  const int old = g_bwd_policy;
-  if (policy >= 0 && policy <= 4) g_bwd_policy = policy;
-  return old;
-}
-
 int insr_siren_jet_bwd_grad(const float* x, long n, int din, int dout, int L, int W, int mode, const float* params,
                             const float* act, const float* gy, const float* gdy, const float* glap, float* work,
                             float* grad, int accumulate, void* stream) {
@@ -1108,13 +1099,13 @@ int insr_siren_jet_bwd_grad(const float* x, long n, int din, int dout, int L, in
     switch (c.nqb) {
       case 3:
         return dispatch_wide_bwd_q<3>(c.NT, c.S, c.lap, x, (int)n, din, dout, L, params, act, gy, gdy, glap, work, grad,
-                                      accumulate, st);
+                                      accumulate, c.k.f16, st);
       case 2:
         return dispatch_wide_bwd_q<2>(c.NT, c.S, c.lap, x, (int)n, din, dout, L, params, act, gy, gdy, glap, work, grad,
-                                      accumulate, st);
+                                      accumulate, c.k.f16, st);
       default:
         return dispatch_wide_bwd_q<1>(c.NT, c.S, c.lap, x, (int)n, din, dout, L, params, act, gy, gdy, glap, work, grad,
-                                      accumulate, st);
+                                      accumulate, c.k.f16, st);
     }
   }
   int rc = insr_siren_jet_bwd(x, n, din, dout, L, W, mode, params, act, gy, gdy, glap, work, stream);
@@ -1129,7 +1120,7 @@ int insr_jet_partial_blocks(long n, int din, int W, int mode) {
   if (!c.ok() || n < 0) return INSR_EINVAL;
   if (n == 0) return 0;
   const int nq = c.NT > 8 ? 0 : c.nqb;
-  const LaunchShape sh = launch_shape(1, nq, c.NT, c.S, c.lap, n);
+  const LaunchShape sh = launch_shape(1, nq, c.NT, c.S, c.lap, n, c.k);
   return sh.nbal > 0 ? sh.nbal : (int)(((n + 15) / 16 + sh.T - 1) / sh.T);
 }
 
@@ -1137,33 +1128,7 @@ int insr_jet_split_tiles(long n, int din, int W, int mode, int backward) {
   const JetCall c(din, W, mode);
   if (!c.ok() || n < 0) return INSR_EINVAL;
   const int nq = backward ? (c.NT > 8 ? 0 : c.nqb) : c.nqf;
-  return launch_shape(backward ? 1 : 0, nq, c.NT, c.S, c.lap, n).T;
-}
-
-void insr_jet_set_split_tiles(int fwd_tiles, int bwd_tiles, int min_blocks) {
-  tiles_init();
-  g_tiles[0] = fwd_tiles < 0 ? 0 : fwd_tiles;
-  g_tiles[1] = bwd_tiles < 0 ? 0 : bwd_tiles;
-  g_tiles[2] = min_blocks < 1 ? 1 : min_blocks;
-}
-
-void insr_jet_get_split_tiles(int* fwd_tiles, int* bwd_tiles, int* min_blocks) {
-  tiles_init();
-  if (fwd_tiles) *fwd_tiles = g_tiles[0];
-  if (bwd_tiles) *bwd_tiles = g_tiles[1];
-  if (min_blocks) *min_blocks = g_tiles[2];
-}
-
-void insr_jet_set_precision(int fwd, int bwd) {
-  prec_init();
-  g_prec[0] = prec_ok(fwd) ? fwd : INSR_PREC_F32;
-  g_prec[1] = prec_ok(bwd) ? bwd : INSR_PREC_F32;
-}
-
-void insr_jet_get_precision(int* fwd, int* bwd) {
-  prec_init();
-  if (fwd) *fwd = g_prec[0];
-  if (bwd) *bwd = g_prec[1];
+  return launch_shape(backward ? 1 : 0, nq, c.NT, c.S, c.lap, n, c.k).T;
 }
 
 int insr_reduce_partials_strided(const float* partial, int nb, long count, long stride, float* grad, int accumulate,

@@ -82,6 +82,16 @@ __host__ __device__ inline long wsplit_f16_vecs(int L, int W) { return (long)L *
 __host__ __device__ inline long wsplit_total_floats(int L, int W) { return 5L * L * W * W; }
 
 // wave-tile base of layer `layer` in the saved-activation buffer
+// CUs of the current device, queried once (thread-safe function-local static; one device per process)
+inline int device_cus() {
+  static const int c = [] {
+    int dev = 0, v = 0;
+    (void)hipGetDevice(&dev);
+    return (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) ? 256 : v;
+  }();
+  return c;
+}
+
 __device__ __forceinline__ float* act_base(float* act, int layer, int ntiles, int tile, int S, int NT) {
   return act + ((long)layer * ntiles + tile) * (long)(S * NT) * 256;
 }
@@ -385,11 +395,8 @@ int dispatch_bwd_q(int NT, int S, bool LAP, int T, const BwdJobsX6* jobs, int di
 template <int NQ>
 int dispatch_wide_bwd_q(int NT, int S, bool LAP, const float* x, int N, int din, int dout, int L, const float* prm,
                         const float* act, const float* gy, const float* gdy, const float* glap, float* work,
-                        float* grad, int accumulate, hipStream_t st);
+                        float* grad, int accumulate, int f16, hipStream_t st);
 long wide_work_floats(long n, int din, int dout, int L, int W, int S);
-// x6 backward products on the fp16 matrix cores (f16x3 with power-of-two adjoint scales; mask of
-// INSR_BWD_F16_*: jet_x6w.hip, insr_jet_set_bwd_f16)
-extern int g_bwd_f16;
 template <int NQ>
 int dispatch_fwd_mixed_q(int NT, int din, const InsrJetJob* jobs, const int* modes, const float* scalars, int njobs,
                          int dout, int L, hipStream_t st);

@@ -576,12 +576,7 @@ __global__ __launch_bounds__(512, 1) void jet_fb_x6(const FbJobs J, int din, int
 // host side
 // ---------------------------------------------------------------------------------------
 inline int fb_blocks(long tiles) {
-  static int cus = -1;
-  if (cus < 0) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
-  }
+  const int cus = device_cus();
   return (int)(tiles < cus ? tiles : cus);
 }
 
@@ -604,12 +599,9 @@ int fb_bwd_t(const FbJobs& J, int din, int dout, const float* prm, float* work, 
   float* small = dpart + (long)L * nb * W * W;
   constexpr size_t lds = FbGeo<S, L, ZR>::BYTES;
   static_assert(lds <= 163840, "LDS");
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)jet_fb_x6<S, LAP, L, ZR>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)lds);
-    attr = true;
-  }
+  static const bool attr = (hipFuncSetAttribute((const void*)jet_fb_x6<S, LAP, L, ZR>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)lds), true);  // once per instantiation (thread-safe static init)
+  (void)attr;
   hipLaunchKernelGGL((jet_fb_x6<S, LAP, L, ZR>), dim3(nb), dim3(512), lds, st, J, din, dout, prm, dpart, small, Ps, nb,
                      tiles);
   const int grad16 = (((uintptr_t)(grad + hidden_off(din, W, 1))) & 15) == 0 ? 1 : 0;

@@ -565,12 +565,9 @@ int launch_fwd_split_t(const float* x, int N, int din, int dout, int L, const fl
     return INSR_EINVAL;
   } else {
     const int nb = ((N + 15) / 16 + T - 1) / T;
-    static bool attr_set = false;
-    if (!attr_set) {
-      (void)hipFuncSetAttribute((const void*)jet_fwd_split<NT, S, LAP, T>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-      attr_set = true;
-    }
+    static const bool attr_set = (hipFuncSetAttribute((const void*)jet_fwd_split<NT, S, LAP, T>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds), true);  // once per instantiation (thread-safe static init)
+    (void)attr_set;
     if (N < 0) {  // occupancy query (split_tiles): resident blocks per CU
       int occ = 0;
       (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)jet_fwd_split<NT, S, LAP, T>, SplitGeo<NT>::THREADS, lds);
@@ -590,12 +587,9 @@ int launch_bwd_split_t(const float* x, int N, int din, int dout, int L, const fl
     return INSR_EINVAL;
   } else {
     const int nb = ((N + 15) / 16 + T - 1) / T;
-    static bool attr_set = false;
-    if (!attr_set) {
-      (void)hipFuncSetAttribute((const void*)jet_bwd_split<NT, S, LAP, T>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-      attr_set = true;
-    }
+    static const bool attr_set = (hipFuncSetAttribute((const void*)jet_bwd_split<NT, S, LAP, T>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds), true);  // once per instantiation (thread-safe static init)
+    (void)attr_set;
     if (N < 0) {  // occupancy query (split_tiles): resident blocks per CU
       int occ = 0;
       (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)jet_bwd_split<NT, S, LAP, T>, SplitGeo<NT>::THREADS, lds);

@@ -371,12 +371,7 @@ __global__ __launch_bounds__(512 / RPW, 1) void jet_bwd_x6r(const float* __restr
 // host side
 // ---------------------------------------------------------------------------------------
 inline int x6r_blocks(long n) {
-  static int cus = -1;
-  if (cus < 0) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
-  }
+  const int cus = device_cus();
   const long tiles = (n + 15) / 16;
   return (int)(tiles < cus ? tiles : cus);
 }
@@ -399,12 +394,9 @@ int resident_bwd_t(const float* x, int N, int din, int dout, const float* prm, c
   constexpr size_t lds = x6r_lds_bytes<NQ, S>();
   static_assert(lds <= 163840, "LDS");
   static_assert(L >= 1 && L <= 4, "resident dW: 1..4 hidden layers");
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)jet_bwd_x6r<NQ, S, LAP, L, RPW>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)lds);
-    attr = true;
-  }
+  static const bool attr = (hipFuncSetAttribute((const void*)jet_bwd_x6r<NQ, S, LAP, L, RPW>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)lds), true);  // once per instantiation (thread-safe static init)
+  (void)attr;
   hipLaunchKernelGGL((jet_bwd_x6r<NQ, S, LAP, L, RPW>), dim3(nb), dim3(512 / RPW), lds, st, x, N, din, dout, prm, act, gy, gdy,
                      glap, dpart, small, Ps, nb);
   const int grad16 = (((uintptr_t)(grad + hidden_off(din, W, 1))) & 15) == 0 ? 1 : 0;

@@ -3,9 +3,8 @@
 #include "jet_x6w.hpp"
 
 namespace insr {
-int g_bwd_f16 = INSR_BWD_F16_DW | INSR_BWD_F16_PROP | INSR_BWD_F16_FUSED;  // measured: profiles/r03/bwd_f16_ab
 template int dispatch_wide_bwd_q<3>(int, int, bool, const float*, int, int, int, int, const float*, const float*,
-                                    const float*, const float*, const float*, float*, float*, int, hipStream_t);
+                                    const float*, const float*, const float*, float*, float*, int, int, hipStream_t);
 long wide_work_floats(long n, int din, int dout, int L, int W, int S) {
   return wide_work_floats_impl(n, din, dout, L, W, S);
 }

@@ -788,7 +788,8 @@ inline void wide_launch_threads_impl(long n, int din, int dout, int L, int W, in
 
 template <int NQ, int NT, int S, bool LAP>
 int wide_bwd_t(const float* x, int N, int din, int dout, int L, const float* prm, const float* act, const float* gy,
-               const float* gdy, const float* glap, float* work, float* grad, int accumulate, hipStream_t st) {
+               const float* gdy, const float* glap, float* work, float* grad, int accumulate, int f16,
+               hipStream_t st) {
   constexpr int W = 16 * NT;
   const long ntiles = ((N + 63) / 64) * 4;
   const int tiles = (N + 15) / 16;
@@ -799,12 +800,11 @@ int wide_bwd_t(const float* x, int N, int din, int dout, int L, const float* prm
   float* rows = dpart + (long)L * wide_ks(N, S, L) * W * W;
   float* zmax = rows + (long)kSmallRS * Ps;
   // the x6 precision's products on the fp16 matrix cores (dw_x6 / jet_bwd_x6p NQ = 4, above)
-  const bool f16dw = NQ == 3 && (g_bwd_f16 & INSR_BWD_F16_DW) && L > 0;
-  const bool f16p = NQ == 3 && (g_bwd_f16 & INSR_BWD_F16_PROP) && L > 0;
+  const bool f16dw = NQ == 3 && (f16 & INSR_BWD_F16_DW) && L > 0;
+  const bool f16p = NQ == 3 && (f16 & INSR_BWD_F16_PROP) && L > 0;
   constexpr size_t lds_p = (size_t)S * np_of<NQ>() * 16 * (W + 8) * 2 + 2 * 3 * 8 * sizeof(float);
   constexpr size_t lds_p4 = (size_t)S * 2 * 16 * (W + 8) * 2 + 2 * 3 * 8 * sizeof(float);
-  static bool attr = false;
-  if (!attr) {
+  static const bool attr = [] {  // once per instantiation (thread-safe static init)
     (void)hipFuncSetAttribute((const void*)jet_bwd_x6p<NQ, NT, S, LAP>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)lds_p);
     (void)hipFuncSetAttribute((const void*)dw_x6<NQ, NT, S, LAP>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -815,8 +815,9 @@ int wide_bwd_t(const float* x, int N, int din, int dout, int L, const float* prm
       (void)hipFuncSetAttribute((const void*)jet_bwd_x6p<4, NT, S, LAP>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)lds_p4);
     }
-    attr = true;
-  }
+    return true;
+  }();
+  (void)attr;
   bool launched = false;
   if constexpr (NQ == 3) {
     if (f16p) {
@@ -859,15 +860,15 @@ int wide_bwd_t(const float* x, int N, int din, int dout, int L, const float* prm
 template <int NQ, int NT>
 int wide_bwd_nt(int S, bool LAP, const float* x, int N, int din, int dout, int L, const float* prm, const float* act,
                 const float* gy, const float* gdy, const float* glap, float* work, float* grad, int accumulate,
-                hipStream_t st) {
+                int f16, hipStream_t st) {
   switch (S * 2 + (LAP ? 1 : 0)) {
-    case 2: return wide_bwd_t<NQ, NT, 1, false>(x, N, din, dout, L, prm, act, gy, gdy, glap, work, grad, accumulate, st);
-    case 4: return wide_bwd_t<NQ, NT, 2, false>(x, N, din, dout, L, prm, act, gy, gdy, glap, work, grad, accumulate, st);
-    case 6: return wide_bwd_t<NQ, NT, 3, false>(x, N, din, dout, L, prm, act, gy, gdy, glap, work, grad, accumulate, st);
-    case 8: return wide_bwd_t<NQ, NT, 4, false>(x, N, din, dout, L, prm, act, gy, gdy, glap, work, grad, accumulate, st);
-    case 7: return wide_bwd_t<NQ, NT, 3, true>(x, N, din, dout, L, prm, act, gy, gdy, glap, work, grad, accumulate, st);
-    case 9: return wide_bwd_t<NQ, NT, 4, true>(x, N, din, dout, L, prm, act, gy, gdy, glap, work, grad, accumulate, st);
-    case 11: return wide_bwd_t<NQ, NT, 5, true>(x, N, din, dout, L, prm, act, gy, gdy, glap, work, grad, accumulate, st);
+    case 2: return wide_bwd_t<NQ, NT, 1, false>(x, N, din, dout, L, prm, act, gy, gdy, glap, work, grad, accumulate, f16, st);
+    case 4: return wide_bwd_t<NQ, NT, 2, false>(x, N, din, dout, L, prm, act, gy, gdy, glap, work, grad, accumulate, f16, st);
+    case 6: return wide_bwd_t<NQ, NT, 3, false>(x, N, din, dout, L, prm, act, gy, gdy, glap, work, grad, accumulate, f16, st);
+    case 8: return wide_bwd_t<NQ, NT, 4, false>(x, N, din, dout, L, prm, act, gy, gdy, glap, work, grad, accumulate, f16, st);
+    case 7: return wide_bwd_t<NQ, NT, 3, true>(x, N, din, dout, L, prm, act, gy, gdy, glap, work, grad, accumulate, f16, st);
+    case 9: return wide_bwd_t<NQ, NT, 4, true>(x, N, din, dout, L, prm, act, gy, gdy, glap, work, grad, accumulate, f16, st);
+    case 11: return wide_bwd_t<NQ, NT, 5, true>(x, N, din, dout, L, prm, act, gy, gdy, glap, work, grad, accumulate, f16, st);
     default: return INSR_EINVAL;
   }
 }
@@ -875,11 +876,11 @@ int wide_bwd_nt(int S, bool LAP, const float* x, int N, int din, int dout, int L
 template <int NQ>
 int dispatch_wide_bwd_q(int NT, int S, bool LAP, const float* x, int N, int din, int dout, int L, const float* prm,
                         const float* act, const float* gy, const float* gdy, const float* glap, float* work,
-                        float* grad, int accumulate, hipStream_t st) {
+                        float* grad, int accumulate, int f16, hipStream_t st) {
   if (NT == 16)
-    return wide_bwd_nt<NQ, 16>(S, LAP, x, N, din, dout, L, prm, act, gy, gdy, glap, work, grad, accumulate, st);
+    return wide_bwd_nt<NQ, 16>(S, LAP, x, N, din, dout, L, prm, act, gy, gdy, glap, work, grad, accumulate, f16, st);
   if (NT == 8)
-    return wide_bwd_nt<NQ, 8>(S, LAP, x, N, din, dout, L, prm, act, gy, gdy, glap, work, grad, accumulate, st);
+    return wide_bwd_nt<NQ, 8>(S, LAP, x, N, din, dout, L, prm, act, gy, gdy, glap, work, grad, accumulate, f16, st);
   return INSR_EWIDTH;
 }
 

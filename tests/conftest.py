@@ -16,9 +16,9 @@ def pytest_configure(config):
 
 
 def pytest_sessionstart(session):
-    """INSR_TEST_BWD_F16=<mask>: run the suite with that insr_jet_set_bwd_f16 mask (A/B of a
-    default before it is made one; test infrastructure only)."""
+    """INSR_TEST_BWD_F16=<mask>: run the suite with that INSR_JET_BWD_F16 mask in every jet call of
+    the test thread (A/B of a default before it is made one; test infrastructure only)."""
     mask = os.environ.get("INSR_TEST_BWD_F16")
     if mask is not None:
         import base
-        base._native.load().insr_jet_set_bwd_f16(int(mask))
+        base._native.set_default_knobs(bwd_f16=int(mask))

@@ -56,23 +56,20 @@ def test_host_queries(lib):
     from base import _native as nat
     assert lib.insr_jet_partial_stride(2, 1, 4, 128) == 66564 and lib.insr_jet_partial_stride(2, 2, 4, 128) == 66692
     assert lib.insr_jet_partial_blocks(0, 2, 128, 2) == 0
-    saved_tiles = nat.get_split_tiles()
-    try:
-        nat.set_split_tiles(0, 0, 512)                      # auto T, >= 512 blocks
-        assert lib.insr_jet_partial_blocks(65, 2, 128, 2) == 5            # small: T = 1
-        assert lib.insr_jet_partial_bytes(65, 2, 1, 4, 128, 2) == 5 * 66564 * 4  # rows padded to 4 floats
-        assert lib.insr_jet_split_tiles(65, 3, 256, 1, 1) == 1
-        # LAP (S=4) at W=128: 70 KB of LDS per tile -> T <= 2; 16384 points = 1024 tiles
-        assert lib.insr_jet_split_tiles(16384, 2, 128, 2, 1) == 2
-        assert lib.insr_jet_partial_blocks(16384, 2, 128, 2) == 512
-        assert lib.insr_jet_split_tiles(16384, 2, 128, 0, 1) == 2         # T=4 would leave 256 blocks
-        nat.set_split_tiles(1, 4, 512)                      # forced: fwd 1, bwd 4 (capped by LDS)
-        assert lib.insr_jet_split_tiles(65536, 2, 128, 0, 0) == 1
-        assert lib.insr_jet_split_tiles(65536, 2, 128, 2, 1) == 2
-        assert lib.insr_jet_partial_blocks(65536, 2, 128, 2) == 2048
-    finally:
-        nat.set_split_tiles(*saved_tiles)
-    assert nat.get_split_tiles() == saved_tiles
+    k = nat.jet_tiles(0, 0, 512)                            # per-call knob: auto T, >= 512 blocks
+    assert lib.insr_jet_partial_blocks(65, 2, 128, 2 | k) == 5            # small: T = 1
+    assert lib.insr_jet_partial_bytes(65, 2, 1, 4, 128, 2 | k) == 5 * 66564 * 4  # rows padded to 4 floats
+    assert lib.insr_jet_split_tiles(65, 3, 256, 1 | k, 1) == 1
+    # LAP (S=4) at W=128: 70 KB of LDS per tile -> T <= 2; 16384 points = 1024 tiles
+    assert lib.insr_jet_split_tiles(16384, 2, 128, 2 | k, 1) == 2
+    assert lib.insr_jet_partial_blocks(16384, 2, 128, 2 | k) == 512
+    assert lib.insr_jet_split_tiles(16384, 2, 128, 0 | k, 1) == 2         # T=4 would leave 256 blocks
+    k = nat.jet_tiles(1, 4, 512)                            # forced: fwd 1, bwd 4 (capped by LDS)
+    assert lib.insr_jet_split_tiles(65536, 2, 128, 0 | k, 0) == 1
+    assert lib.insr_jet_split_tiles(65536, 2, 128, 2 | k, 1) == 2
+    assert lib.insr_jet_partial_blocks(65536, 2, 128, 2 | k) == 2048
+    # the knobs live in the call, not in the library: a call without them is unaffected
+    assert lib.insr_jet_partial_blocks(16384, 2, 128, 2) == lib.insr_jet_partial_blocks(16384, 2, 128, 2 | nat.jet_tiles())
 
 
 def test_invalid_arguments_rejected_without_launch(lib):
@@ -177,45 +174,39 @@ def test_backward_path_policy(lib):
     (two-kernel from there), the resident-dW kernel for the fluid2DtlgnM value batch (from 49,152
     points) or when forced (policy 3); policy 4 forces the recompute backward (path 3: no saved
     streams) where it applies, independently of n (the forward's skip-the-saves decision must match
-    the backward's); insr_jet_set_bwd_policy forces a path for A/B studies."""
+    the backward's); the per-call INSR_JET_POLICY bits force a path for A/B studies."""
     from base import _native as nat
     V, G, LAP = nat.MODE_VALUE, nat.MODE_GRAD, nat.MODE_LAP
-    old = lib.insr_jet_set_bwd_policy(0)
-    try:
-        assert lib.insr_jet_bwd_path(16708, 2, 1, 4, 128, LAP) == 1
-        assert lib.insr_jet_bwd_path(16708, 2, 2, 4, 128, V) == 0
-        assert lib.insr_jet_bwd_path(1024, 2, 2, 4, 128, V) == 0
-        # fluid2DtlgnM: the two-kernel f16x3 Laplacian backward (resident when its products are bf16x6)
-        assert lib.insr_jet_bwd_path(65536 + 1308, 2, 1, 4, 128, LAP) == 1
-        old_f16 = lib.insr_jet_set_bwd_f16(0)
-        assert lib.insr_jet_bwd_path(65536 + 1308, 2, 1, 4, 128, LAP) == 2
-        lib.insr_jet_set_bwd_f16(old_f16)
-        assert lib.insr_jet_bwd_path(65536 + 1308, 2, 2, 4, 128, V) == 2
-        assert lib.insr_jet_bwd_path(33092, 2, 2, 4, 128, V) == 1   # value jets two-kernel from 24,576
-        assert lib.insr_jet_bwd_path(24000, 2, 2, 4, 128, V) == 0
-        assert lib.insr_jet_bwd_path(32768, 3, 3, 5, 256, G) == 1
-        assert lib.insr_jet_bwd_path(20400, 2, 2, 5, 128, G) not in (2, 3)  # 5 hidden layers
-        assert lib.insr_jet_bwd_path(16708, 2, 1, 4, 128, LAP | nat.jet_prec(nat.PREC_BF16)) not in (2, 3)
-        lib.insr_jet_set_bwd_policy(2)
-        assert lib.insr_jet_bwd_path(16708, 2, 1, 4, 128, LAP) == 1
-        lib.insr_jet_set_bwd_policy(1)
-        assert lib.insr_jet_bwd_path(16708, 2, 1, 4, 128, LAP) == 0
-        lib.insr_jet_set_bwd_policy(3)
-        assert lib.insr_jet_bwd_path(17, 2, 1, 4, 128, LAP) == 2
-        assert lib.insr_jet_bwd_path(17, 2, 1, 3, 128, LAP) != 2         # 4 hidden layers only
-        assert lib.insr_jet_bwd_path(17, 2, 1, 4, 64, LAP) != 2          # W = 128 only
-        lib.insr_jet_set_bwd_policy(4)
-        for n in (1, 17, 16708, 65536 + 1308):
-            assert lib.insr_jet_bwd_path(n, 2, 1, 4, 128, LAP) == 3
-        assert lib.insr_jet_bwd_path(17, 2, 2, 4, 128, V) == 3
-        assert lib.insr_jet_bwd_path(17, 2, 2, 4, 128, G) == 3
-        assert lib.insr_jet_bwd_path(16708, 1, 1, 4, 128, LAP) != 3        # 1-d Laplacian: 3 streams
-        assert lib.insr_jet_bwd_path(16708, 2, 1, 3, 128, LAP) != 3        # 4 hidden layers only
-        assert lib.insr_jet_bwd_path(16708, 2, 1, 4, 64, LAP) != 3         # W = 128 only
-        assert lib.insr_jet_bwd_path(16708, 2, 1, 4, 128, LAP | nat.jet_prec(nat.PREC_BF16)) != 3  # fp32-level only
-        assert lib.insr_jet_set_bwd_policy(9) == 4                      # out of range: unchanged
-    finally:
-        lib.insr_jet_set_bwd_policy(old)
+    P = nat.jet_policy
+    assert lib.insr_jet_bwd_path(16708, 2, 1, 4, 128, LAP) == 1
+    assert lib.insr_jet_bwd_path(16708, 2, 2, 4, 128, V) == 0
+    assert lib.insr_jet_bwd_path(1024, 2, 2, 4, 128, V) == 0
+    # fluid2DtlgnM: the two-kernel f16x3 Laplacian backward (resident when its products are bf16x6)
+    assert lib.insr_jet_bwd_path(65536 + 1308, 2, 1, 4, 128, LAP) == 1
+    assert lib.insr_jet_bwd_path(65536 + 1308, 2, 1, 4, 128, LAP | nat.jet_bwd_f16(0)) == 2
+    assert lib.insr_jet_bwd_path(65536 + 1308, 2, 2, 4, 128, V) == 2
+    assert lib.insr_jet_bwd_path(33092, 2, 2, 4, 128, V) == 1   # value jets two-kernel from 24,576
+    assert lib.insr_jet_bwd_path(24000, 2, 2, 4, 128, V) == 0
+    assert lib.insr_jet_bwd_path(32768, 3, 3, 5, 256, G) == 1
+    assert lib.insr_jet_bwd_path(20400, 2, 2, 5, 128, G) not in (2, 3)  # 5 hidden layers
+    assert lib.insr_jet_bwd_path(16708, 2, 1, 4, 128, LAP | nat.jet_prec(nat.PREC_BF16)) not in (2, 3)
+    assert lib.insr_jet_bwd_path(16708, 2, 1, 4, 128, LAP | P(2)) == 1
+    assert lib.insr_jet_bwd_path(16708, 2, 1, 4, 128, LAP | P(1)) == 0
+    assert lib.insr_jet_bwd_path(17, 2, 1, 4, 128, LAP | P(3)) == 2
+    assert lib.insr_jet_bwd_path(17, 2, 1, 3, 128, LAP | P(3)) != 2         # 4 hidden layers only
+    assert lib.insr_jet_bwd_path(17, 2, 1, 4, 64, LAP | P(3)) != 2          # W = 128 only
+    for n in (1, 17, 16708, 65536 + 1308):
+        assert lib.insr_jet_bwd_path(n, 2, 1, 4, 128, LAP | P(4)) == 3
+    assert lib.insr_jet_bwd_path(17, 2, 2, 4, 128, V | P(4)) == 3
+    assert lib.insr_jet_bwd_path(17, 2, 2, 4, 128, G | P(4)) == 3
+    assert lib.insr_jet_bwd_path(16708, 1, 1, 4, 128, LAP | P(4)) != 3        # 1-d Laplacian: 3 streams
+    assert lib.insr_jet_bwd_path(16708, 2, 1, 3, 128, LAP | P(4)) != 3        # 4 hidden layers only
+    assert lib.insr_jet_bwd_path(16708, 2, 1, 4, 64, LAP | P(4)) != 3         # W = 128 only
+    assert lib.insr_jet_bwd_path(16708, 2, 1, 4, 128, LAP | P(4) | nat.jet_prec(nat.PREC_BF16)) != 3  # fp32-level only
+    assert lib.insr_jet_bwd_path(16708, 2, 1, 4, 128, LAP) == 1              # no state left behind
+    # malformed knob fields are refused like any bad mode
+    assert lib.insr_jet_bwd_path(16708, 2, 1, 4, 128, LAP | (6 << nat.MODE_POLICY_SHIFT)) == -1
+    assert lib.insr_jet_bwd_path(16708, 2, 1, 4, 128, LAP | (9 << nat.MODE_F16_SHIFT)) == -1
 
 
 def test_multi_backward_plan(lib):
@@ -233,19 +224,15 @@ def test_multi_backward_plan(lib):
         arr = (ctypes.c_long * len(ns))(*ns)
         return lib.insr_jet_bwd_multi_work_bytes(arr, len(ns), din, dout, 4, 128, mode)
 
-    old = lib.insr_jet_set_bwd_policy(0)
-    try:
-        assert work([16384, 162, 162]) == 211 * stride * 4
-        assert work([16384]) == lib.insr_jet_bwd_work_bytes(16384, 2, 2, 4, 128, V)
-        assert work([162, 0, 162]) == 22 * stride * 4  # 1-tile blocks (324 points), 11 per band
-        # Laplacian interior: the two-kernel path alone; bands beside it in the fused launch
-        lw = lib.insr_jet_bwd_work_bytes(16708, 2, 1, 4, 128, LAP)
-        pw = work([162, 162], dout=1, mode=LAP)
-        assert work([16708, 162, 162], dout=1, mode=LAP) == max(lw, pw)
-        for bad in ([], [-1], [1] * (nat.MAX_BWD_JOBS + 1), [1 << 31]):
-            assert work(bad) == -1, bad
-        assert lib.insr_siren_jet_bwd_grad_multi(None, 1, 2, 2, 4, 128, V, None, None, None, 0, None) == -1
-        jobs = (nat.BwdJob * 1)(nat.BwdJob(None, None, None, None, None, 64))  # live job without x / act
-        assert lib.insr_siren_jet_bwd_grad_multi(jobs, 1, 2, 2, 4, 128, V, 1, 1, 1, 0, None) == -1
-    finally:
-        lib.insr_jet_set_bwd_policy(old)
+    assert work([16384, 162, 162]) == 211 * stride * 4
+    assert work([16384]) == lib.insr_jet_bwd_work_bytes(16384, 2, 2, 4, 128, V)
+    assert work([162, 0, 162]) == 22 * stride * 4  # 1-tile blocks (324 points), 11 per band
+    # Laplacian interior: the two-kernel path alone; bands beside it in the fused launch
+    lw = lib.insr_jet_bwd_work_bytes(16708, 2, 1, 4, 128, LAP)
+    pw = work([162, 162], dout=1, mode=LAP)
+    assert work([16708, 162, 162], dout=1, mode=LAP) == max(lw, pw)
+    for bad in ([], [-1], [1] * (nat.MAX_BWD_JOBS + 1), [1 << 31]):
+        assert work(bad) == -1, bad
+    assert lib.insr_siren_jet_bwd_grad_multi(None, 1, 2, 2, 4, 128, V, None, None, None, 0, None) == -1
+    jobs = (nat.BwdJob * 1)(nat.BwdJob(None, None, None, None, None, 64))  # live job without x / act
+    assert lib.insr_siren_jet_bwd_grad_multi(jobs, 1, 2, 2, 4, 128, V, 1, 1, 1, 0, None) == -1

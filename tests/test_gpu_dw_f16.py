@@ -1,4 +1,4 @@
-"""The x6 backward's products on the fp16 matrix cores (insr_jet_set_bwd_f16): the two-kernel
+"""The x6 backward's products on the fp16 matrix cores (INSR_JET_BWD_F16 mode bits): the two-kernel
 path's dW GEMM and propagation, the fused tile-split kernel.
 
 f16x3 (two fp16 terms per operand, three products) keeps 22 significant bits but fp16's narrow
@@ -25,12 +25,9 @@ def B(request):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     import base
-    lib = base._native.load()
-    old_dw = lib.insr_jet_set_bwd_f16(request.param[0])
-    old_pol = lib.insr_jet_set_bwd_policy(request.param[1])
-    yield base
-    lib.insr_jet_set_bwd_f16(old_dw)
-    lib.insr_jet_set_bwd_policy(old_pol)
+    base._native.load()
+    with base._native.knobs(bwd_f16=request.param[0], policy=request.param[1]):  # per-call mode bits
+        yield base
 
 
 def nerr(a, b):
@@ -113,11 +110,8 @@ def test_dw_f16_large_tangents(B, w0_scale):
         return [q.grad.clone() if q.grad is not None else torch.zeros_like(q) for q in hip.parameters()]
 
     g16 = grads()
-    mask = lib.insr_jet_set_bwd_f16(0)
-    try:
+    with B._native.knobs(bwd_f16=0):
         g6 = grads()
-    finally:
-        lib.insr_jet_set_bwd_f16(mask)
     for (k, p), a, b in zip(ref.named_parameters(), g16, g6):
         assert torch.isfinite(a).all(), k
         g = p.grad if p.grad is not None else torch.zeros_like(p)  # the output bias: no Laplacian

@@ -198,11 +198,8 @@ def test_backward_never_reads_tiles_the_forward_left_unwritten(B, prec, tiles):
     memory just filled with NaN (the caching allocator hands the freed block back), so a read of
     an unwritten tile poisons the gradient; n = 4,500 points = 282 tiles (not a multiple of 4)."""
     nat = B._native
-    old_t, old_p = nat.get_split_tiles(), nat.get_precision()
     p = {"x6": 1, "f32": 0}[prec]
-    try:
-        nat.set_split_tiles(tiles[0], tiles[1], old_t[2])
-        nat.set_precision(p, p)
+    with nat.knobs(tiles=tiles, prec=(p, p)):
         ref, net = pair(B, 2, 2, 4, 128, seed=9)
         n = 4500
         x = pts(n, 2, 70)
@@ -217,6 +214,3 @@ def test_backward_never_reads_tiles_the_forward_left_unwritten(B, prec, tiles):
         for (k, q), g in zip(ref.named_parameters(), grads(net)):
             assert torch.isfinite(g).all(), k
             assert nerr(g, q.grad) < TOL, k
-    finally:
-        nat.set_split_tiles(*old_t)
-        nat.set_precision(*old_p)

@@ -32,7 +32,7 @@ NETS = {  # name: (d_in, d_out, L, W)
 }
 
 
-F32, X6 = 0, 1  # matrix-core precision of the tile-split kernels (insr_jet_set_precision)
+F32, X6 = 0, 1  # matrix-core precision of the tile-split kernels (INSR_JET_PREC mode bits)
 VARIANTS = {  # (fwd, bwd) forced tiles per block, (fwd, bwd) precision[, smallest width of the two-kernel backward]
     "split": ((1, 1), (F32, F32)),           # exact-fp32 MFMA, neurons split over a block's waves, 1 tile/block
     "split_t2": ((2, 2), (F32, F32)),        # 2 tiles per block (ragged last block)
@@ -54,17 +54,11 @@ def base(request):
         pytest.skip("no GPU")
     import base as B
     B._native.load()
-    old_tiles = B._native.get_split_tiles()
-    old_prec = B._native.get_precision()
     tiles, prec = VARIANTS[request.param][:2]
     wide = VARIANTS[request.param][2] if len(VARIANTS[request.param]) > 2 else 256
-    B._native.set_split_tiles(tiles[0], tiles[1], old_tiles[2])
-    B._native.set_precision(*prec)
-    old_wide = B._native.lib().insr_jet_set_wide_min_width(wide)
-    yield B
-    B._native.set_split_tiles(*old_tiles)
-    B._native.set_precision(*old_prec)
-    B._native.lib().insr_jet_set_wide_min_width(old_wide)
+    # the variant's knobs ride in every jet call's mode (INSR_JET_TILES / INSR_JET_PREC / WIDE128)
+    with B._native.knobs(tiles=tiles, prec=prec, wide128=wide == 128):
+        yield B
 
 
 def nerr(a, b):
@@ -203,9 +197,7 @@ def test_no_grad_jets_skip_saving(base):
 @pytest.mark.parametrize("op", ["value", "laplace", "divergence"])
 def test_large_batch_default_policy(base, op):
     """Batches large enough for the automatic multi-tile choice (T = 2 / 4)."""
-    old_tiles = base._native.get_split_tiles()
-    base._native.set_split_tiles(0, 0, old_tiles[2])
-    try:
+    with base._native.knobs(tiles=(0, 0)):
         name = "fluid_pres" if op != "divergence" else "fluid_vel"
         din = NETS[name][0]
         ref, net = pair(base, name, seed=6)
@@ -223,8 +215,6 @@ def test_large_batch_default_policy(base, op):
         (v * R.cuda()).sum().backward()
         for k, e in param_errs(ref, net):
             assert e < TOL, (op, k, e)
-    finally:
-        base._native.set_split_tiles(*old_tiles)
 
 
 @pytest.mark.parametrize("name", ["advect_w20", "el2d_w68", "el3d_w66"])

@@ -19,15 +19,15 @@ V, G, LAP = 0, 1, 2
 
 @pytest.fixture(scope="module")
 def B():
-    """The recompute path forced on (policy 4) for the module: its own tests below switch to other
-    paths explicitly where they compare against them."""
+    """The recompute path forced on (policy 4: the per-call INSR_JET_POLICY bits every jet of the
+    test thread carries) for the module: its own tests below switch to other paths explicitly where
+    they compare against them."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     import base
-    lib = base._native.load()
-    old = lib.insr_jet_set_bwd_policy(4)
-    yield base
-    lib.insr_jet_set_bwd_policy(old)
+    base._native.load()
+    with base._native.knobs(policy=4):
+        yield base
 
 
 def nerr(a, b):
@@ -52,15 +52,15 @@ def ref_grads(ref):
     return [(p.grad if p.grad is not None else torch.zeros_like(p)).detach() for p in ref.parameters()]
 
 
-class policy:
-    def __init__(self, lib, p):
-        self.lib, self.p = lib, p
+def policy(lib, p, **kw):
+    from base import _native as nat
+    return nat.knobs(policy=p, **kw)
 
-    def __enter__(self):
-        self.old = self.lib.insr_jet_set_bwd_policy(self.p)
 
-    def __exit__(self, *exc):
-        self.lib.insr_jet_set_bwd_policy(self.old)
+def knob(mode):
+    """A jet mode with the test thread's knob bits (what base.MLP.call_mode adds)."""
+    from base import _native as nat
+    return mode | nat.scope_bits()
 
 
 @pytest.mark.parametrize("n", [1, 15, 17, 300, 4111, 16708])
@@ -69,7 +69,7 @@ def test_laplace_jet_all_adjoints_vs_oracle(B, n):
     on the walls) with adjoints on the value, both gradient streams and the Laplacian stream: every
     parameter gradient vs the oracle; the forward of a path-3 call saves nothing."""
     lib = B._native.lib()
-    assert lib.insr_jet_bwd_path(n, 2, 1, 4, 128, LAP) == 3
+    assert lib.insr_jet_bwd_path(n, 2, 1, 4, 128, knob(LAP)) == 3
     ref, net = pair(B, 2, 1, 4, 128, seed=41)
     x = torch.rand(n, 2, generator=torch.Generator().manual_seed(n)) * 2 - 1
     xr = x.clone().requires_grad_(True)
@@ -131,7 +131,7 @@ def test_forced_recompute_value_and_gradient_jets(B, kind):
         ref, net = pair(B, 2, 2, 4, 128, seed=44)
         n = 5000
         mode = V if kind == "value" else G
-        assert lib.insr_jet_bwd_path(n, 2, 2, 4, 128, mode) == 3
+        assert lib.insr_jet_bwd_path(n, 2, 2, 4, 128, knob(mode)) == 3
         x = torch.rand(n, 2, generator=torch.Generator().manual_seed(3)) * 2 - 1
         xr = x.clone().requires_grad_(True)
         xg = x.cuda().requires_grad_(True)
@@ -181,8 +181,7 @@ def test_large_tangents_stay_finite(B):
     out = []
     for pol, prec in ((4, None), (2, "bf16x6")):
         # the reference run: saved streams, every product bf16x6 (no fp16 operand anywhere)
-        old_f16 = lib.insr_jet_set_bwd_f16(7 if pol == 4 else 0)
-        with policy(lib, pol):
+        with policy(lib, pol, bwd_f16=7 if pol == 4 else 0):
             torch.manual_seed(46)
             net = B.MLP(2, 1, 4, 128, nonlinearity="sine", precision=prec).cuda()
             with torch.no_grad():
@@ -194,7 +193,6 @@ def test_large_tangents_stay_finite(B):
             ((lp * R).sum() + (gp ** 2).sum()).backward()
             torch.cuda.synchronize()
             out.append(grads(net))
-        lib.insr_jet_set_bwd_f16(old_f16)
     for a, b in zip(*out):
         assert torch.isfinite(a).all() and torch.isfinite(b).all()
         assert nerr(a, b) < TOL
@@ -208,22 +206,20 @@ def test_large_tangents_gradient_jets(B, shape):
     din, dout, L, W = shape
     lib = B._native.lib()
     out = []
-    old_pol = lib.insr_jet_set_bwd_policy(0)  # the default (saved-stream) paths
     for prec in (None, "bf16x6"):
-        old_f16 = lib.insr_jet_set_bwd_f16(7 if prec is None else 0)  # reference: no fp16 operand anywhere
-        torch.manual_seed(47)
-        net = B.MLP(din, dout, L, W, nonlinearity="sine", precision=prec).cuda()
-        with torch.no_grad():
-            net.net[0].weight.mul_(4000.0)
-        x = (torch.rand(3000, din, generator=torch.Generator().manual_seed(7)) * 2 - 1).cuda().requires_grad_(True)
-        J = B.jacobian(net(x), x)[0]
-        assert torch.isfinite(J).all()
-        R = torch.randn(J.shape, generator=torch.Generator().manual_seed(8)).cuda()
-        (J * R).sum().backward()
-        torch.cuda.synchronize()
-        lib.insr_jet_set_bwd_f16(old_f16)
-        out.append([J.detach().clone()] + grads(net))
-    lib.insr_jet_set_bwd_policy(old_pol)
+        # the default (saved-stream) paths; reference: no fp16 operand anywhere
+        with policy(lib, 0, bwd_f16=7 if prec is None else 0):
+            torch.manual_seed(47)
+            net = B.MLP(din, dout, L, W, nonlinearity="sine", precision=prec).cuda()
+            with torch.no_grad():
+                net.net[0].weight.mul_(4000.0)
+            x = (torch.rand(3000, din, generator=torch.Generator().manual_seed(7)) * 2 - 1).cuda().requires_grad_(True)
+            J = B.jacobian(net(x), x)[0]
+            assert torch.isfinite(J).all()
+            R = torch.randn(J.shape, generator=torch.Generator().manual_seed(8)).cuda()
+            (J * R).sum().backward()
+            torch.cuda.synchronize()
+            out.append([J.detach().clone()] + grads(net))
     for a, b in zip(*out):
         assert torch.isfinite(a).all() and torch.isfinite(b).all()
         assert nerr(a, b) < TOL

@@ -1,6 +1,6 @@
 """The resident-dW backward (csrc/jet_x6r.hpp, insr_jet_bwd_path == 2): one persistent launch
 holding every hidden layer's weight gradient in registers across the batch, then the
-fixed-order partial sums.  Forced with insr_jet_set_bwd_policy(3) over batch sizes from one
+fixed-order partial sums.  Forced with the INSR_JET_POLICY(3) mode bits over batch sizes from one
 point (one block) to 65,536 (16 tiles per block), ragged tails, value / gradient / Laplacian
 jets of the fluid nets (4 hidden layers), against the CPU oracle (base/diff_ops.py:44-82 and
 loss.backward(), base/baseModel.py:73-78).  Tolerance 1e-5 normwise per parameter tensor.
@@ -26,10 +26,8 @@ def B():
 
 @pytest.fixture
 def resident(B):
-    lib = B._native.lib()
-    old = lib.insr_jet_set_bwd_policy(3)
-    yield lib
-    lib.insr_jet_set_bwd_policy(old)
+    with B._native.knobs(policy=3):
+        yield B._native.lib()
 
 
 def nerr(a, b):
@@ -147,8 +145,6 @@ def test_default_routing(B):
     assert lib.insr_jet_bwd_path(16708, 2, 2, 4, 128, nat.MODE_VALUE) == 0
     assert lib.insr_jet_bwd_path(1024, 2, 2, 4, 128, nat.MODE_VALUE) == 0
     assert lib.insr_jet_bwd_path(66844, 2, 1, 4, 128, nat.MODE_LAP) == 1    # fluid2DtlgnM batch
-    old = lib.insr_jet_set_bwd_f16(0)
-    assert lib.insr_jet_bwd_path(66844, 2, 1, 4, 128, nat.MODE_LAP) == 2
-    lib.insr_jet_set_bwd_f16(old)
+    assert lib.insr_jet_bwd_path(66844, 2, 1, 4, 128, nat.MODE_LAP | nat.jet_bwd_f16(0)) == 2
     assert lib.insr_jet_bwd_path(66844, 2, 2, 4, 128, nat.MODE_VALUE) == 2
     assert lib.insr_jet_bwd_path(20400, 2, 2, 5, 128, nat.MODE_GRAD) not in (2, 3)  # 5 hidden layers

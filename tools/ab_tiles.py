@@ -1,5 +1,6 @@
 """A/B helper: run bench.py with a forced tile count (the former INSR_SPLIT_TILES_* env knobs,
-now only the C-ABI call insr_jet_set_split_tiles).  Usage:
+now the per-call INSR_JET_TILES mode bits, set as the bench thread's knob scope).  MIN_BLOCKS one of
+128 / 256 / 512 / 1024.  Usage:
     python tools/ab_tiles.py FWD BWD MIN_BLOCKS -- <bench.py args>"""
 import os
 import runpy
@@ -12,6 +13,6 @@ if __name__ == "__main__":
     fwd, bwd, mb = (int(v) for v in sys.argv[1:4])
     import base
     base._native.load()
-    base._native.lib().insr_jet_set_split_tiles(fwd, bwd, mb)
+    base._native.set_default_knobs(tiles=(fwd, bwd, mb))
     sys.argv = [os.path.join(ROOT, "bench.py")] + sys.argv[5:]
     runpy.run_path(sys.argv[0], run_name="__main__")

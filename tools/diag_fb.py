@@ -46,13 +46,12 @@ def main():
     lib = nat.load(os.path.join(ROOT, "insr-pde_amd", "lib", "libinsr_hip_diag.so"), check_build=False)
     lib.insr_diag_fb_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
     din, dout, L, W, mode = NETS[args.net]
-    lib.insr_jet_set_bwd_policy(4)
     n = args.n
     torch.manual_seed(0)
     net = base.MLP(din, dout, L, W, nonlinearity="sine").cuda()
     net.refresh_wsplit()
     flat = net.flat_params()
-    cm = mode | nat.MODE_WSPLIT
+    cm = mode | nat.MODE_WSPLIT | nat.jet_policy(4)
     assert lib.insr_jet_bwd_path(n, din, dout, L, W, cm) == 3
     x = (torch.rand(n, din, device="cuda") * 2 - 1).contiguous()
     gy = torch.randn(n, dout, device="cuda")

@@ -34,10 +34,9 @@ def main():
     lib = nat.load(os.path.join(ROOT, "insr-pde_amd", "lib", "libinsr_hip_diag.so"))
     lib.insr_diag_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
     lib.insr_diag_stamps_x6.argtypes = [ctypes.c_void_p, ctypes.c_int]
-    nat.set_precision(args.prec, args.prec)
     ph = PH_X6 if args.prec else PH
     din, dout, L, W = NETS[args.net]
-    mode = {"value": 0, "grad": 1, "lap": 2}[args.mode]
+    mode = {"value": 0, "grad": 1, "lap": 2}[args.mode] | nat.knob_bits(prec=(args.prec, args.prec))
     n = args.n
     torch.manual_seed(0)
     net = base.MLP(din, dout, L, W, nonlinearity="sine").cuda()

@@ -55,16 +55,15 @@ def main():
     ap.add_argument("--modes", default="value,grad,lap")
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--variants", default=",".join(VARIANTS))
-    ap.add_argument("--policies", default="0", help="backward-path policies (insr_jet_set_bwd_policy) to time")
+    ap.add_argument("--policies", default="0", help="backward-path policies (INSR_JET_POLICY mode bits) to time")
     ap.add_argument("--bwd-only", action="store_true", help="time only the backward into .grad")
-    ap.add_argument("--bwd-f16", type=int, default=-1, help="insr_jet_set_bwd_f16 mask (-1: library default)")
+    ap.add_argument("--bwd-f16", type=int, default=-1, help="INSR_JET_BWD_F16 mask (-1: library default)")
     ap.add_argument("--lib", default=None, help="alternative build of libinsr_hip.so (flag studies)")
     args = ap.parse_args()
     import base
     from base import _native as nat
     lib = nat.load(args.lib, check_build=args.lib is None)
-    if args.bwd_f16 >= 0:
-        lib.insr_jet_set_bwd_f16(args.bwd_f16)
+    f16bits = nat.jet_bwd_f16(args.bwd_f16) if args.bwd_f16 >= 0 else 0
     out = []
     for name in args.nets.split(","):
         din, dout, L, W = NETS[name]
@@ -79,25 +78,23 @@ def main():
             wbit = 0
         P = net.param_count
         for mname in args.modes.split(","):
-            mode = MODES[mname] | wbit
-            if (mode & 0xF) == 2 and din > 2:
+            mode0 = MODES[mname] | wbit | f16bits
+            if (mode0 & 0xF) == 2 and din > 2:
                 continue
-            S = {0: 1, 1: 1 + din, 2: 2 + din}[mode & 0xF]
+            S = {0: 1, 1: 1 + din, 2: 2 + din}[mode0 & 0xF]
             for n in [int(v) for v in args.sizes.split(",")]:
                 x = (torch.rand(n, din, device="cuda") * 2 - 1).contiguous()
                 y = torch.empty(n, dout, device="cuda")
                 dy = torch.empty(n, dout, din, device="cuda")
                 lap = torch.empty(n, dout, device="cuda")
                 gy, gdy, glap = torch.randn_like(y), torch.randn_like(dy), torch.randn_like(lap)
-                act = torch.empty(lib.insr_jet_act_bytes(n, din, L, W, mode) // 4, device="cuda")
+                act = torch.empty(lib.insr_jet_act_bytes(n, din, L, W, mode0) // 4, device="cuda")
                 g = torch.zeros(P, device="cuda")
                 st = nat.stream_of(x.device)
                 for variant, pol in [(v, int(p)) for v in args.variants.split(",") for p in args.policies.split(",")]:
-                    lib.insr_jet_set_bwd_policy(pol)
                     tiles, prec = VARIANTS[variant]
-                    nat.set_split_tiles(tiles[0], tiles[1], 256)
-                    nat.set_precision(*prec)
-                    lib.insr_jet_set_wide_min_width(128 if variant.endswith("w") else 256)
+                    # the variant as per-call mode bits (the library keeps no configuration)
+                    mode = mode0 | nat.knob_bits(policy=pol, tiles=tiles, prec=prec, wide128=variant.endswith("w"))
                     part = torch.empty(max(lib.insr_jet_partial_bytes(n, din, dout, L, W, mode) // 4, 1), device="cuda")
                     nb = lib.insr_jet_partial_blocks(n, din, W, mode)
                     tf_, tb_ = (lib.insr_jet_split_tiles(n, din, W, mode, 0),

@@ -31,15 +31,15 @@ def main():
     ap.add_argument("--nets", default=",".join(NETS))
     ap.add_argument("--combos", default="0:0,1:1,2:2,3:3",
                     help="forward:backward precision pairs (0 fp32, 1 bf16x6, 2 bf16x3, 3 bf16), comma separated")
-    ap.add_argument("--bwd-f16", type=int, default=-1, help="insr_jet_set_bwd_f16 mask (-1: library default)")
+    ap.add_argument("--bwd-f16", type=int, default=-1, help="INSR_JET_BWD_F16 mask (-1: library default)")
     args = ap.parse_args()
     combos = [tuple(int(v) for v in c.split(":")) for c in args.combos.split(",")]
     names = ["f32", "bf16x6", "bf16x3", "bf16", "f16x3"]
     import base
     lib = base._native.load()
     if args.bwd_f16 >= 0:
-        lib.insr_jet_set_bwd_f16(args.bwd_f16)
-    mask = lib.insr_jet_set_bwd_f16(-1)
+        base._native.set_default_knobs(bwd_f16=args.bwd_f16)
+    mask = base._native.bwd_f16_mask()
     for name in args.nets.split(","):
         din, dout, L, W = NETS[name]
         torch.manual_seed(0)
@@ -59,7 +59,7 @@ def main():
             (vr * R).sum().backward()
             gref = [p.grad if p.grad is not None else torch.zeros_like(p) for p in ref.parameters()]
             for pf, pb in combos:
-                base._native.set_precision(pf, pb)
+                base._native.set_default_knobs(prec=(pf, pb))
                 net.zero_grad(set_to_none=True)
                 xg = x.cuda().requires_grad_(True)
                 y = net(xg)
