@@ -94,6 +94,7 @@ extern "C" {
 #define INSR_ENOCOMM  (-3) /* RCCL (librccl.so.1) could not be loaded   */
 #define INSR_ECAPTURE (-4) /* a per-stream scratch would be allocated during stream capture:
                               run the call once outside the capture, or pass INSR_MODE_WSPLIT */
+#define INSR_ERANGE   (-5) /* a hidden weight |w| >= 255 reached the fp16 weight planes (insr_siren_wsplit_status) */
 #define INSR_ECOMM_BASE 1000 /* + ncclResult_t of a failed RCCL call     */
 
 /* Library version (major*10000 + minor*100 + patch). */
@@ -109,14 +110,22 @@ long insr_siren_param_count(int d_in, int d_out, int num_hidden, int width);
 /* Pre-split weight planes (split-bf16 kernels).  Every hidden weight W_j is stored split in
  * three bf16 terms (jet_x6.hpp) in the matrix-core fragment order of the forward (W_j rows)
  * and of the backward (W_j^T rows), then 2^8 W_j split in two fp16 terms in the forward and in
- * the backward order (INSR_PREC_F16X3): 5 L W^2 floats in all, at insr_siren_wsplit_offset() floats (param_count
- * rounded up to 16 B) after the start of the params buffer.
+ * the backward order (INSR_PREC_F16X3): 5 L W^2 floats, then a status quad (4 floats) -- in all
+ * insr_siren_wsplit_floats(), at insr_siren_wsplit_offset() floats (param_count rounded up to 16 B)
+ * after the start of the params buffer.
  * insr_siren_wsplit() writes them from the parameters in place (one launch); the kernels then
  * read fragments instead of re-splitting W in every block.  Replaces nothing in the
  * reference (its fp32 addmm reads W directly, torch/nn/modules/linear.py). */
 long insr_siren_wsplit_offset(int d_in, int d_out, int num_hidden, int width);
 long insr_siren_wsplit_floats(int num_hidden, int width);
 int insr_siren_wsplit(float* params, int d_in, int d_out, int num_hidden, int width, void* stream);
+/* Range guard of the fp16 planes: 2^8 w in fp16 needs |w| < 255.  insr_siren_wsplit and the Adam launches
+ * that keep the planes current (insr_adam_step_nets / insr_adam_plateau_step_nets with shapes) flag any
+ * hidden weight outside that range in the status quad (and clamp its fp16 terms, so nothing overflows;
+ * the f16x3 products of that layer are then not the network's -- the bf16 planes, fp32's range, are
+ * exact).  Returns INSR_ERANGE when flagged, 0 when not (waits for `stream`; a host sync point).
+ * insr_siren_wsplit clears the flag; the Adam launches only set it. */
+int insr_siren_wsplit_status(const float* params, int d_in, int d_out, int num_hidden, int width, void* stream);
 
 /* 1 if (d_in, d_out, width, mode) is served by a compiled kernel, else 0. */
 int insr_siren_supported(int d_in, int d_out, int num_hidden, int width, int mode);

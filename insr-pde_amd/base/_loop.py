@@ -139,6 +139,8 @@ class PhaseLoop:
             last = (i == m.max_n_iters - 1)
             if (i + 1) % self.sync_every == 0 or last or i == 0:
                 vals = {k: float(v) for k, v in loss_dict.items()}
+                for net in m._trainable_networks.values():  # the fp16 weight planes' range guard
+                    net.check_weight_planes()
                 if m.tb is not None:
                     m.tb.add_scalars(self.tag, vals, global_step=i)
                 if tqdm is not None and hasattr(pbar, "set_postfix"):

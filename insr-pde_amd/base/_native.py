@@ -38,6 +38,7 @@ def jet_bprec(p):
 
 # Per-call knobs (include/insr_siren.h INSR_JET_POLICY / INSR_JET_BWD_F16 / INSR_JET_TILES /
 # INSR_MODE_WIDE128): bits of the `mode` argument.  The library keeps no mutable configuration.
+ERANGE = -5  # INSR_ERANGE
 MODE_WIDE128 = 1 << 9
 MODE_POLICY_SHIFT, MODE_F16_SHIFT, MODE_TILES_SHIFT = 16, 19, 23
 BWD_F16_DW, BWD_F16_PROP, BWD_F16_FUSED = 1, 2, 4
@@ -168,6 +169,7 @@ SIGNATURES = {
     "insr_siren_wsplit_offset": (_L, [_I, _I, _I, _I]),
     "insr_siren_wsplit_floats": (_L, [_I, _I]),
     "insr_siren_wsplit": (_I, [_P, _I, _I, _I, _I, _P]),
+    "insr_siren_wsplit_status": (_I, [_P, _I, _I, _I, _I, _P]),
     "insr_siren_jet_fwd_mixed": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _I, _P]),
     "insr_adam_step_nets": (_I, [_I, _P, _P, _P, _P, _P, _P, _P, _F, _F, _F, _I, _P]),
     "insr_adam_plateau_step_nets": (_I, [_I, _P, _P, _P, _P, _P, _P, _P, _F, _F, _F, _P, _I, _P]),

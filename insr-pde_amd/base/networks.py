@@ -197,6 +197,33 @@ class MLP(nn.Module):
                   "insr_siren_wsplit")
         self._wsplit_stamp = self._param_versions()
 
+    def uses_f16_planes(self):
+        """Whether this network's jets read the fp16 weight planes: an f16x3 forward (the default) or a
+        bf16x6-contract backward with fp16 products (the default INSR_JET_BWD_F16 mask)."""
+        from ._native import PREC_BF16X6, PREC_F16X3, bwd_f16_mask, scope_bits
+        if self._prec_pair is None:
+            bits = scope_bits()
+            pf = ((bits >> 4) & 0xF) - 1
+            return pf < 0 or pf == PREC_F16X3 or bwd_f16_mask() != 0
+        pf, pb = self._prec_pair
+        return pf == PREC_F16X3 or (pb in (PREC_BF16X6, PREC_F16X3) and bwd_f16_mask() != 0)
+
+    def check_weight_planes(self):
+        """Host sync point (the training loop's loss reads): raise NativeError when a hidden weight left
+        the fp16 planes' range (|w| >= 255, include/insr_siren.h insr_siren_wsplit_status) while this
+        network's jets read those planes -- the f16x3 products would not be the network's.  Remedy:
+        MLP(precision='bf16x6') with INSR_JET_BWD_F16(0) (fp32's range everywhere)."""
+        if self._flat is None or not self._flat.is_cuda or self.num_hidden_layers == 0 or not self.uses_f16_planes():
+            return
+        from . import _native as nat
+        rc = nat.lib().insr_siren_wsplit_status(nat.ptr(self._flat), self.in_features, self.out_features,
+                                                self.num_hidden_layers, self.kernel_width,
+                                                nat.stream_of(self._flat.device))
+        if rc == nat.ERANGE:
+            raise nat.NativeError("a hidden weight reached |w| >= 255: outside the fp16 weight planes' range "
+                                  "(f16x3 products); run this network at precision='bf16x6' with bwd_f16=0")
+        nat.check(rc, "insr_siren_wsplit_status")
+
     def mark_wsplit_current(self):
         """The planes were rewritten with the parameters (insr_adam_step_nets)."""
         self._wsplit_stamp = self._param_versions()

@@ -489,8 +489,13 @@ __device__ __forceinline__ void adam_wsplit(float* base, const int (&sh)[4], lon
 #pragma unroll
     for (int q = 0; q < 3; ++q) pl[o * ov + ((fr + q) * 64 + 16 * g + c) * 8 + jj] = t[q];
   }
-  // the fp16 planes (INSR_PREC_F16X3): 2^8 w in two fp16 terms, orientation 0 then 1
+  // the fp16 planes (INSR_PREC_F16X3): 2^8 w in two fp16 terms, orientation 0 then 1; a weight outside
+  // their range is flagged in the status word (insr_siren_wsplit_status) and clamped there
   unsigned short* ph = reinterpret_cast<unsigned short*>(base + wsplit_f16_offset(din, dout, L, W));
+  if (!(fabsf(w) < kF16WMax)) {
+    atomicOr(reinterpret_cast<unsigned*>(base + wsplit_status_offset(din, dout, L, W)), 1u);
+    w = fminf(fmaxf(w, -kF16WMax), kF16WMax);
+  }
   const float ws = w * kF16WScale;
   const _Float16 hh = (_Float16)ws, hl = (_Float16)(ws - (float)hh);
   const long oh = 2L * L * W * W;  // u16 per fp16 orientation
@@ -664,6 +669,17 @@ static const float* with_planes(const float* params, int din, int dout, int L, i
   if ((*rc = (int)hipMemcpyAsync(buf, params, (size_t)pc * sizeof(float), hipMemcpyDeviceToDevice, st))) return nullptr;
   if ((*rc = wsplit_launch(buf, din, dout, L, W, buf + wsplit_offset(din, dout, L, W), st))) return nullptr;
   return buf;
+}
+
+int insr_siren_wsplit_status(const float* params, int din, int dout, int L, int W, void* stream) {
+  if (!params || !shape_ok(din, dout, L, W, 0)) return INSR_EINVAL;
+  if (L < 1) return 0;
+  unsigned word = 0;
+  if (const int rc = (int)hipStreamSynchronize((hipStream_t)stream)) return rc;
+  if (const int rc = (int)hipMemcpy(&word, params + wsplit_status_offset(din, dout, L, W), sizeof(word),
+                                    hipMemcpyDeviceToHost))
+    return rc;
+  return word ? INSR_ERANGE : 0;
 }
 
 int insr_siren_supported(int din, int dout, int L, int W, int mode) { return shape_ok(din, dout, L, W, mode) ? 1 : 0; }

@@ -79,7 +79,15 @@ __host__ __device__ inline long wsplit_f16t_offset(int din, int dout, int L, int
   return wsplit_f16_offset(din, dout, L, W) + (long)L * W * W;
 }
 __host__ __device__ inline long wsplit_f16_vecs(int L, int W) { return (long)L * W * W / 4; }  // u32x4 per fp16 orientation
-__host__ __device__ inline long wsplit_total_floats(int L, int W) { return 5L * L * W * W; }
+// ... then one status quad: word 0 != 0 once a hidden weight with |w| >= kF16WMax was split into the fp16
+// planes (2^8 w would leave fp16's range: its terms are clamped, so the f16x3 products of that layer are
+// not the network's).  Set by wsplit_kernel (cleared by the host launch first) and by the Adam launch
+// (sticky); read by insr_siren_wsplit_status.
+constexpr float kF16WMax = 255.0f;
+__host__ __device__ inline long wsplit_status_offset(int din, int dout, int L, int W) {
+  return wsplit_f16t_offset(din, dout, L, W) + (long)L * W * W;
+}
+__host__ __device__ inline long wsplit_total_floats(int L, int W) { return 5L * L * W * W + 4; }
 
 // wave-tile base of layer `layer` in the saved-activation buffer
 // CUs of the current device, queried once (thread-safe function-local static; one device per process)

@@ -45,7 +45,7 @@ __host__ __device__ inline long small_count(int din, int dout, int L, int W) {
 // ---------------------------------------------------------------------------------------
 template <int NT>
 __global__ __launch_bounds__(256) void wsplit_kernel(const float* __restrict__ prm, int din, int L,
-                                                     u32x4* __restrict__ out) {
+                                                     u32x4* __restrict__ out, unsigned* __restrict__ status) {
   constexpr int W = 16 * NT, KC = NT / 2, NF = NT * KC;
   const long gid = (long)blockIdx.x * 256 + threadIdx.x;
   const int lane = (int)(gid & 63), g = lane >> 4, c = lane & 15;
@@ -67,6 +67,17 @@ __global__ __launch_bounds__(256) void wsplit_kernel(const float* __restrict__ p
     }
   }
   if (o >= 2) {  // fp16: o = 2 forward rows, o = 3 backward (W^T) rows
+    float m = 0.f;
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) m = fmaxf(m, fmaxf(fabsf(v0[jj]), fabsf(v1[jj])));
+    if (!(m < kF16WMax)) {  // outside the planes' range (or NaN): flag it, keep the terms finite
+      if (o == 2) atomicOr(status, 1u);
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        v0[jj] = fminf(fmaxf(v0[jj], -kF16WMax), kF16WMax);
+        v1[jj] = fminf(fmaxf(v1[jj], -kF16WMax), kF16WMax);
+      }
+    }
     const FragQ<4> h = split_frag<4>(v0 * kF16WScale, v1 * kF16WScale);
     u32x4* oh = out + (o == 2 ? 6L : 8L) * L * NF * 64;  // after both bf16 orientations (3 L W^2 floats)
     const long fh = f;
