@@ -162,7 +162,9 @@ class MLP(nn.Module):
         return (self.param_count + 3) & ~3
 
     def wsplit_floats(self):
-        return 5 * self.num_hidden_layers * self.kernel_width ** 2  # bf16 x 3 + fp16 x 2, both orientations each
+        # bf16 x 3 + fp16 x 2 planes, both orientations each, then the status quad
+        # (include/insr_siren.h insr_siren_wsplit_floats; tests/test_capi.py pins the two together)
+        return 5 * self.num_hidden_layers * self.kernel_width ** 2 + 4
 
     def plist(self):
         """list(self.parameters()) without the module-tree walk (the checks before every jet and

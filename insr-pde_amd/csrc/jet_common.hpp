@@ -293,19 +293,40 @@ __device__ __forceinline__ void load_z_sincos(const float* base, int S, int lane
   }
 }
 
+// ---- saved-stream reads ----
+// A forward saves every z-stream of hidden layers 1..L but only the VALUE stream of the first layer
+// (when L > 0): its tangent streams are the columns of W_0 and its Laplacian stream is 0 at every
+// point (x enters linearly), so readers rebuild them from the parameters (W_0 row-major W x d_in at
+// offset 0 of prm) instead of reading (S - 1) / S of that layer's bytes.
+__device__ __forceinline__ bool l0_rebuilt(int layer, int L) { return layer == 0 && L > 0; }
+template <int S, bool LAP>
+__device__ __forceinline__ floatx4 l0_stream(const float* w0, int din, int s, int rt, int lane) {
+  if (LAP && s == S - 1) return floatx4{0.f, 0.f, 0.f, 0.f};
+  const float* p = w0 + (long)(16 * rt + 4 * (lane >> 4)) * din + (s - 1);
+  return floatx4{p[0], p[din], p[2 * din], p[3 * din]};
+}
+// z-stream s of row tile rt at this lane's point: saved, or rebuilt (l0 = l0_rebuilt(layer, L), s >= 1)
+template <int NT, int S, bool LAP>
+__device__ __forceinline__ floatx4 load_zs(const float* base, int s, int rt, int lane, bool l0, const float* w0,
+                                           int din) {
+  if (l0 && s > 0) return l0_stream<S, LAP>(w0, din, s, rt, lane);
+  return *reinterpret_cast<const floatx4*>(base + ((s * NT + rt) * 64 + lane) * 4);
+}
+
 // h-stream s of a sine layer (for the weight gradient of the layer above),
-// rebuilt from saved z-streams + cached sin/cos.
+// rebuilt from saved z-streams + cached sin/cos (l0: the first layer's rebuilt streams, above).
 template <int NT, int S, bool LAP>
 __device__ __forceinline__ floatx4 h_stream(const float* base, int s, int rt, int lane, const floatx4& sn,
-                                            const floatx4& cs) {
+                                            const floatx4& cs, bool l0 = false, const float* w0 = nullptr,
+                                            int din = 0) {
   constexpr int NTAN = LAP ? S - 2 : S - 1;
   if (s == 0) return sn;
-  const floatx4 zs = *reinterpret_cast<const floatx4*>(base + ((s * NT + rt) * 64 + lane) * 4);
+  const floatx4 zs = load_zs<NT, S, LAP>(base, s, rt, lane, l0, w0, din);
   floatx4 out;
   if (LAP && s == S - 1) {
     floatx4 t2 = floatx4{0.f, 0.f, 0.f, 0.f};
     for (int i = 0; i < NTAN; ++i) {
-      const floatx4 t = *reinterpret_cast<const floatx4*>(base + (((1 + i) * NT + rt) * 64 + lane) * 4);
+      const floatx4 t = load_zs<NT, S, LAP>(base, 1 + i, rt, lane, l0, w0, din);
 #pragma unroll
       for (int r = 0; r < 4; ++r) t2[r] = fmaf(t[r], t[r], t2[r]);
     }
@@ -323,10 +344,11 @@ __device__ __forceinline__ floatx4 h_stream(const float* base, int s, int rt, in
 // caller fills in stream order 1..S-1 before stream S-1).
 template <int NT, int S, bool LAP>
 __device__ __forceinline__ floatx4 h_from_z(const float* base, int s, int rt, int lane, const floatx4& sn,
-                                            const floatx4& cs, floatx4 (&zkeep)[S]) {
+                                            const floatx4& cs, floatx4 (&zkeep)[S], bool l0 = false,
+                                            const float* w0 = nullptr, int din = 0) {
   constexpr int NTAN = LAP ? S - 2 : S - 1;
   if (s == 0) return sn;
-  const floatx4 zs = *reinterpret_cast<const floatx4*>(base + ((s * NT + rt) * 64 + lane) * 4);
+  const floatx4 zs = load_zs<NT, S, LAP>(base, s, rt, lane, l0, w0, din);
   zkeep[s] = zs;
   floatx4 out;
   if (LAP && s == S - 1) {

@@ -145,7 +145,8 @@ __global__ __launch_bounds__(SplitGeo<NT>::THREADS) void jet_fwd_split(
       }
       __syncthreads();  // every wave has read layer j-1
     }
-    if (act) {
+    if (act) {  // the first layer: its value stream only (l0_rebuilt, jet_common.hpp)
+      const int ns = l0_rebuilt(j, L) ? 1 : S;
 #pragma unroll
       for (int t = 0; t < T; ++t) {
         float* base = act_base(act, j, ntiles, tile0 + t, S, NT);
@@ -153,7 +154,7 @@ __global__ __launch_bounds__(SplitGeo<NT>::THREADS) void jet_fwd_split(
         for (int i = 0; i < RPW; ++i)
 #pragma unroll
           for (int s = 0; s < S; ++s)
-            *reinterpret_cast<floatx4*>(base + ((s * NT + rt0 + i) * 64 + lane) * 4) = a[t][i][s];
+            if (s < ns) *reinterpret_cast<floatx4*>(base + ((s * NT + rt0 + i) * 64 + lane) * 4) = a[t][i][s];
       }
     }
 #pragma unroll
@@ -365,7 +366,7 @@ __global__ __launch_bounds__(SplitGeo<NT>::THREADS) void jet_bwd_split(
       for (int i = 0; i < RPW; ++i)
 #pragma unroll
         for (int s = 1; s < S; ++s)
-          zk[t][i][s] = *reinterpret_cast<const floatx4*>(baseL + ((s * NT + rt0 + i) * 64 + lane) * 4);
+          zk[t][i][s] = load_zs<NT, S, LAP>(baseL, s, rt0 + i, lane, l0_rebuilt(L, L), prm, din);
     }
   }
   for (int j = L; j >= 0; --j) {
@@ -391,7 +392,7 @@ __global__ __launch_bounds__(SplitGeo<NT>::THREADS) void jet_bwd_split(
             zs[s] = (s == 0) ? floatx4{0.f, 0.f, 0.f, 0.f} : zk[t][i][s];
           else
             zs[s] = (s == 0) ? floatx4{0.f, 0.f, 0.f, 0.f}
-                             : *reinterpret_cast<const floatx4*>(basej + ((s * NT + rt0 + i) * 64 + lane) * 4);
+                             : load_zs<NT, S, LAP>(basej, s, rt0 + i, lane, l0_rebuilt(j, L), prm, din);
         }
         sine_rev<S, LAP>(hb[t][i], zs, sn[t][i], cs[t][i]);
       }
@@ -442,9 +443,10 @@ __global__ __launch_bounds__(SplitGeo<NT>::THREADS) void jet_bwd_split(
           *reinterpret_cast<floatx4*>(zbp + (t * S + s) * PLANE + c * LDH + col) = hb[t][i][s];
           floatx4 hs;
           if constexpr (kKeepZ) {
-            hs = h_from_z<NT, S, LAP>(basep, s, rt0 + i, lane, snp[t][i], csp[t][i], zk[t][i]);
+            hs = h_from_z<NT, S, LAP>(basep, s, rt0 + i, lane, snp[t][i], csp[t][i], zk[t][i], l0_rebuilt(j - 1, L),
+                                      prm, din);
           } else {
-            hs = h_stream<NT, S, LAP>(basep, s, rt0 + i, lane, snp[t][i], csp[t][i]);
+            hs = h_stream<NT, S, LAP>(basep, s, rt0 + i, lane, snp[t][i], csp[t][i], l0_rebuilt(j - 1, L), prm, din);
           }
           float* hp_ts = hpp + (t * S + s) * PLANEH;
 #pragma unroll

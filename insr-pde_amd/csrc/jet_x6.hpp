@@ -419,7 +419,8 @@ __device__ __forceinline__ void fwd_x6_block(const float* __restrict__ x, int N,
         if (j > 0 && threadIdx.x == 0) tflag[(j + 1) & 1] = 0;  // the other parity's readers passed the barrier
       }
     }
-    if (act) {
+    if (act) {  // the first layer: its value stream only (l0_rebuilt, jet_common.hpp)
+      const int ns = l0_rebuilt(j, L) ? 1 : S;
 #pragma unroll
       for (int t = 0; t < T; ++t) {
         if (t >= cnt) break;  // a balanced block's unused tile slots
@@ -428,7 +429,7 @@ __device__ __forceinline__ void fwd_x6_block(const float* __restrict__ x, int N,
         for (int i = 0; i < RPW; ++i)
 #pragma unroll
           for (int s = 0; s < S; ++s)
-            *reinterpret_cast<floatx4*>(base + ((s * NT + rt0 + i) * 64 + lane) * 4) = a[t][i][s];
+            if (s < ns) *reinterpret_cast<floatx4*>(base + ((s * NT + rt0 + i) * 64 + lane) * 4) = a[t][i][s];
       }
     }
 #pragma unroll
@@ -1022,11 +1023,11 @@ __global__ __launch_bounds__(X6Geo<NT>::THREADS) void jet_bwd_x6(const BwdJobsX6
 #pragma unroll
       for (int t = 0; t < T; ++t) {
         const float* base = act_base(act, layer, ntiles, tt(t), S, NT);
+        const bool l0 = l0_rebuilt(layer, L);
 #pragma unroll
         for (int i = 0; i < RPW; ++i)
 #pragma unroll
-          for (int s = 1; s < S; ++s)
-            zk[t][i][s - 1] = *reinterpret_cast<const floatx4*>(base + ((s * NT + rt0 + i) * 64 + lane) * 4);
+          for (int s = 1; s < S; ++s) zk[t][i][s - 1] = load_zs<NT, S, LAP>(base, s, rt0 + i, lane, l0, prm, din);
       }
     }
   };
@@ -1050,7 +1051,7 @@ __global__ __launch_bounds__(X6Geo<NT>::THREADS) void jet_bwd_x6(const BwdJobsX6
 #pragma unroll
           for (int s = 0; s < S; ++s)
             zs[s] = (s == 0) ? floatx4{0.f, 0.f, 0.f, 0.f}
-                             : *reinterpret_cast<const floatx4*>(basej + ((s * NT + rt0 + i) * 64 + lane) * 4);
+                             : load_zs<NT, S, LAP>(basej, s, rt0 + i, lane, l0_rebuilt(j, L), prm, din);
           sine_rev<S, LAP>(hb[t][i], zs, sn[t][i], cs[t][i]);
         }
       }
@@ -1138,7 +1139,7 @@ __global__ __launch_bounds__(X6Geo<NT>::THREADS) void jet_bwd_x6(const BwdJobsX6
             if constexpr (KZ)
               zd[s - 1] = zk[t][i][s - 1];
             else
-              zd[s - 1] = *reinterpret_cast<const floatx4*>(basep + ((s * NT + rt0 + i) * 64 + lane) * 4);
+              zd[s - 1] = load_zs<NT, S, LAP>(basep, s, rt0 + i, lane, l0_rebuilt(j - 1, L), prm, din);
           }
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
@@ -1221,7 +1222,8 @@ __global__ __launch_bounds__(X6Geo<NT>::THREADS) void jet_bwd_x6(const BwdJobsX6
             if constexpr (KZ) {
               hs = h_from_regs<S, LAP>(s, zk[t][i], snp[t][i], csp[t][i]);
             } else {
-              hs = h_stream<NT, S, LAP>(basep, s, rt0 + i, lane, snp[t][i], csp[t][i]);
+              hs = h_stream<NT, S, LAP>(basep, s, rt0 + i, lane, snp[t][i], csp[t][i], l0_rebuilt(j - 1, L), prm,
+                                        din);
             }
             if (lq) hs *= hll;
             if (tq) hs *= htl;

@@ -99,11 +99,11 @@ __global__ __launch_bounds__(512 / RPW, 1) void jet_bwd_x6r(const float* __restr
 #pragma unroll
     for (int t = 0; t < TS; ++t) {
       const float* base = act_base(act, layer, ntiles, tb + (t < cnt ? t : 0), S, NT);
+      const bool l0 = l0_rebuilt(layer, L);  // the first layer's derivative streams: from W_0
 #pragma unroll
       for (int i = 0; i < RPW; ++i)
 #pragma unroll
-        for (int s = 0; s < S; ++s)
-          zr[t][i][s] = *reinterpret_cast<const floatx4*>(base + ((s * NT + rt0 + i) * 64 + lane) * 4);
+        for (int s = 0; s < S; ++s) zr[t][i][s] = load_zs<NT, S, LAP>(base, s, rt0 + i, lane, l0, prm, din);
     }
   };
   // sin / cos and the derivative z-streams from the raw streams

@@ -217,7 +217,7 @@ __global__ __launch_bounds__(512, (x6p_min_waves<NQ, NT>())) void jet_bwd_x6p(co
 #pragma unroll
       for (int s = 0; s < S; ++s)
         zs[s] = (s == 0) ? floatx4{0.f, 0.f, 0.f, 0.f}
-                         : *reinterpret_cast<const floatx4*>(basej + ((s * NT + rt0 + i) * 64 + lane) * 4);
+                         : load_zs<NT, S, LAP>(basej, s, rt0 + i, lane, l0_rebuilt(j, L), prm, din);
       if (hq && j < L) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -453,7 +453,7 @@ template <int NQ, int NT, int S, bool LAP>
 __global__ __launch_bounds__(512, (NQ == 4 && NT == 8) ? INSR_F16_BWD_WAVES : 1) void dw_x6(int N, const float* __restrict__ act, const float* __restrict__ adj,
                                              float* __restrict__ dpart, int KS, int L, const float* __restrict__ small,
                                              int tiles, long Ps, float* __restrict__ rows, int rs, int rows_x,
-                                             const float* __restrict__ zmax) {
+                                             const float* __restrict__ zmax, const float* __restrict__ w0, int din) {
   constexpr int W = 16 * NT, RT = NT / 8;  // RT: dW row tiles per wave
   constexpr int G = NT / 4;                   // granules per thread per chunk (2 units x NT row tiles / 8 waves)
   constexpr int kDwPL = dw_plane<NT>();
@@ -467,6 +467,7 @@ __global__ __launch_bounds__(512, (NQ == 4 && NT == 8) ? INSR_F16_BWD_WAVES : 1)
   }
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
   const int j = blockIdx.y + 1;
+  const bool l0 = l0_rebuilt(j - 1, L);  // h_0's derivative streams: rebuilt from W_0 (not saved)
   const int ntiles = ((N + 63) / 64) * 4;
   const int units = ((N + 15) / 16) * S;
   const int chunks = (units + 1) / 2;
@@ -533,7 +534,7 @@ __global__ __launch_bounds__(512, (NQ == 4 && NT == 8) ? INSR_F16_BWD_WAVES : 1)
       rzb[it] = *reinterpret_cast<const floatx4*>(act_base(adj, j - 1, ntiles, t, S, NT) +
                                                   ((s * NT + rt) * 64 + lane) * 4);
       if (S % 2 != 0 || it < RT) rz0[it] = *reinterpret_cast<const floatx4*>(ba + (rt * 64 + lane) * 4);
-      rzs[it] = *reinterpret_cast<const floatx4*>(ba + ((s * NT + rt) * 64 + lane) * 4);
+      rzs[it] = load_zs<NT, S, LAP>(ba, s, rt, lane, l0, w0, din);
     }
   };
   floatx4 ssv[G], scv[G];
@@ -575,7 +576,7 @@ __global__ __launch_bounds__(512, (NQ == 4 && NT == 8) ? INSR_F16_BWD_WAVES : 1)
           const float* ba = act_base(act, j - 1, ntiles, t, S, NT);
 #pragma unroll
           for (int ti = 1; ti < S - 2; ++ti) {
-            const floatx4 z = *reinterpret_cast<const floatx4*>(ba + ((ti * NT + rt) * 64 + lane) * 4);
+            const floatx4 z = load_zs<NT, S, LAP>(ba, ti, rt, lane, l0, w0, din);
 #pragma unroll
             for (int r = 0; r < 4; ++r) t2[r] = fmaf(z[r], z[r], t2[r]);
           }
@@ -584,7 +585,7 @@ __global__ __launch_bounds__(512, (NQ == 4 && NT == 8) ? INSR_F16_BWD_WAVES : 1)
 #pragma unroll
           for (int r = 0; r < 4; ++r) hv[r] = OMEGA * cv[r] * rzs[it][r] - OMEGA2 * sv[r] * t2[r];
         } else {
-          hv = h_stream<NT, S, LAP>(act_base(act, j - 1, ntiles, t, S, NT), s, rt, lane, sv, cv);
+          hv = h_stream<NT, S, LAP>(act_base(act, j - 1, ntiles, t, S, NT), s, rt, lane, sv, cv, l0, w0, din);
         }
       } else {
 #pragma unroll
@@ -849,13 +850,13 @@ int wide_bwd_t(const float* x, int N, int din, int dout, int L, const float* prm
     if constexpr (NQ == 3) {
       if (f16dw) {
         hipLaunchKernelGGL((dw_x6<4, NT, S, LAP>), dim3(KS, L + planes), dim3(512), (dw_lds<4, NT>()), st, N, act, adj,
-                           dpart, KS, L, small, tiles, Ps, rows, rs, rows_x, zmax);
+                           dpart, KS, L, small, tiles, Ps, rows, rs, rows_x, zmax, prm, din);
         done = true;
       }
     }
     if (!done)
       hipLaunchKernelGGL((dw_x6<NQ, NT, S, LAP>), dim3(KS, L + planes), dim3(512), (dw_lds<NQ, NT>()), st, N, act, adj,
-                         dpart, KS, L, small, tiles, Ps, rows, rs, rows_x, zmax);
+                         dpart, KS, L, small, tiles, Ps, rows, rs, rows_x, zmax, prm, din);
     const int grad16 = (((uintptr_t)(grad + hidden_off(din, W, 1))) & 15) == 0 ? 1 : 0;  // W % 4 == 0: all layers alike
     const int wq = (W * W / 4 + 63) / 64;
     hipLaunchKernelGGL(reduce_dw_kernel, dim3((unsigned)(wq > rows_x ? wq : rows_x), L + 1), dim3(512), 0, st, dpart,

@@ -236,3 +236,16 @@ def test_multi_backward_plan(lib):
     assert lib.insr_siren_jet_bwd_grad_multi(None, 1, 2, 2, 4, 128, V, None, None, None, 0, None) == -1
     jobs = (nat.BwdJob * 1)(nat.BwdJob(None, None, None, None, None, 64))  # live job without x / act
     assert lib.insr_siren_jet_bwd_grad_multi(jobs, 1, 2, 2, 4, 128, V, 1, 1, 1, 0, None) == -1
+
+
+def test_weight_plane_layout_matches_python(lib):
+    """base.MLP sizes its flat storage [parameters | pad | planes | status quad] itself (no library call
+    on the CPU path): both sizes must equal the library's (an undersized store would put the fp16 range
+    guard's status word past the allocation)."""
+    import base
+    for din, dout, L, W in ((2, 1, 4, 128), (2, 2, 4, 128), (3, 3, 5, 256), (1, 1, 3, 64), (2, 2, 5, 68)):
+        net = base.MLP(din, dout, L, W, nonlinearity="sine")
+        kw = net.kernel_width
+        assert net.wsplit_offset() == lib.insr_siren_wsplit_offset(din, dout, L, kw)
+        assert net.wsplit_floats() == lib.insr_siren_wsplit_floats(L, kw)
+        assert net._store.numel() == lib.insr_siren_wsplit_offset(din, dout, L, kw) + lib.insr_siren_wsplit_floats(L, kw)

@@ -5,6 +5,7 @@ tests/test_oracle_golden.py) on the SAME points:
   * fluid2Dtlgn   fused pde/fluid.py phases at 128^2 = 16,384 interior points + 2 x 162 bands
   * fluid2DtlgnM  the same at 256^2 = 65,536 + 2 x 654
   * elasticity2Dstretch  _solve_deformation at 20,000 points (SIREN 5x128) + 2 x 200 fixed
+  * advect1D     _advect at 4,096 interior + 2 x 20 band points (SIREN 3x64)
 
 The GPU runs the product path exactly as bench.py does -- device sampler into the merged
 [interior; bands] buffer (fluid) / the persistent box batch (elasticity), mixed launches,
@@ -208,3 +209,57 @@ def test_elasticity2dstretch_full_size(B):
                                                                                              float(ldo["main"]))
     check_grads(m.deformation_field, r["f"], "el2d")
     check_update(m.deformation_field, r["f"], p0, cfg.lr)
+
+
+def test_advect1d_full_size(B):
+    """advect1D (BASELINE.json configs[0]: SIREN 3x64, sample_resolution 4,096): one _advect iteration
+    on the product sampler path -- ONE insr_sample_boxes launch writes the 4,096 interior points and the
+    2 x 20 band points at +-L/2 into the merged buffer (pde/advection.py _advect_points), the frozen and
+    the trainable field run as one fused jet launch, the loss is fused_mse, Adam + plateau one launch --
+    vs the oracle's advection/model.py:68-91 loss on the points that launch drew: both losses, every
+    parameter gradient, the Adam update."""
+    import pde.advection as adv
+    from pde.config import baseline_config
+    cfg = baseline_config("advect1D", proj_dir="/tmp/insr_fullsize_adv", insr_progress=False, early_stop=False,
+                          max_n_iters=1, insr_graph=False, insr_sync_every=1)
+    m = adv.Advection1DModel(cfg)
+    m.timestep = 1
+    refs = {"f": seeded(1, 1, 3, 64, 221), "f_prev": seeded(1, 1, 3, 64, 222)}
+    load(m.field, refs["f"])
+    load(m.field_prev, refs["f_prev"])
+    p0 = O.flat_params(refs["f"]).numpy().copy()
+    drawn = {}
+    orig = adv.sample_boxes
+
+    def rec(boxes, d, **kw):
+        buf = orig(boxes, d, **kw)
+        drawn["buf"] = buf.detach().cpu().clone()
+        drawn["n"] = [b[0] for b in boxes]
+        return buf
+    adv.sample_boxes = rec
+    try:
+        m._reset_optimizer()
+        ld = adv.Advection1DModel._advect._insr_phase(m)
+        m._update_network(ld)
+        torch.cuda.synchronize()
+    finally:
+        adv.sample_boxes = orig
+    n, h, h2 = drawn["n"]
+    assert (n, h, h2) == (4096, 20, 20)
+    buf = drawn["buf"]
+    x, bc = buf[:n], buf[n:]
+    half = cfg.length / 2
+    assert float(x.min()) >= -half and float(x.max()) < half
+    assert (bc.abs() > half * (1 - 1.01e-4)).all() and (bc.abs() < half * (1 + 1.01e-4)).all()
+    r = {k: seeded(1, 1, 3, 64, s) for k, s in (("f", 221), ("f_prev", 222))}
+    for p in r["f_prev"].parameters():
+        p.requires_grad_(False)
+    opt = O.OracleAdam(list(r["f"].parameters()), lr=cfg.lr)
+    ldo = O.advect1d_loss(r["f"], r["f_prev"], x.clone().requires_grad_(True), bc.clone().requires_grad_(True),
+                          cfg.dt, cfg.vel)
+    O.update_step([r["f"]], ldo, opt)
+    assert set(ld) == set(ldo) == {"main", "bc"}
+    for k, v in ldo.items():
+        assert abs(float(ld[k]) - float(v)) <= TOL * abs(float(v)) + 1e-12, (k, float(ld[k]), float(v))
+    check_grads(m.field, r["f"], "advect1D")
+    check_update(m.field, r["f"], p0, cfg.lr)

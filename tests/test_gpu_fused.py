@@ -77,10 +77,11 @@ def _multi(B, nets, xs, mode, saves):
     return outs
 
 
-def _eq(a, b, n=None, layers=None):
+def _eq(a, b, n=None, layers=None, w=None):
     """Bit equality; for saved streams (n points, `layers` = L + 1) only the tiles of real
     points: the 16-point tiles past the last one are padding that a launch writes or skips
-    depending on its tiles per block."""
+    depending on its tiles per block; and of the first layer only its value stream (its
+    derivative streams are point-independent, rebuilt from W_0 by every backward: not saved)."""
     if a is None or b is None:
         return a is None and b is None
     if n == 0:
@@ -88,6 +89,8 @@ def _eq(a, b, n=None, layers=None):
     if n is not None:
         ntiles = ((n + 63) // 64) * 4  # [layer][tile][stream][row tile][lane][4]
         a, b = a.view(layers, ntiles, -1)[:, :(n + 15) // 16], b.view(layers, ntiles, -1)[:, :(n + 15) // 16]
+        if layers > 1:  # the first layer's value stream: 16 points x w floats per tile
+            return torch.equal(a[1:], b[1:]) and torch.equal(a[0, :, :16 * w], b[0, :, :16 * w])
     return torch.equal(a, b)
 
 
@@ -103,7 +106,7 @@ def test_multi_matches_single_launches(B, name, mode, sizes):
     fused = _multi(B, nets, xs, mode, saves)
     for net, x, save, (y, dy, act) in zip(nets, xs, saves, fused):
         ys, dys, acts = _single(B, net, x, mode, save)
-        assert _eq(y, ys) and _eq(dy, dys) and _eq(act, acts, x.shape[0], net.num_hidden_layers + 1), (name, mode, x.shape[0])
+        assert _eq(y, ys) and _eq(dy, dys) and _eq(act, acts, x.shape[0], net.num_hidden_layers + 1, net.kernel_width), (name, mode, x.shape[0])
 
 
 @pytest.mark.parametrize("mode", [0, 1])
@@ -116,7 +119,7 @@ def test_multi_mixed_output_widths(B, mode):
     fused = _multi(B, nets, xs, mode, saves)
     for net, x, save, (y, dy, act) in zip(nets, xs, saves, fused):
         ys, dys, acts = _single(B, net, x, mode, save)
-        assert _eq(y, ys) and _eq(dy, dys) and _eq(act, acts, x.shape[0], net.num_hidden_layers + 1)
+        assert _eq(y, ys) and _eq(dy, dys) and _eq(act, acts, x.shape[0], net.num_hidden_layers + 1, net.kernel_width)
 
 
 def test_multi_rejects_bad_arguments(B):
