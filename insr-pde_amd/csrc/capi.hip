@@ -32,7 +32,8 @@ int nt_for(int width) {
 constexpr int kMinBlocksDefault = 256;
 constexpr int kBwdF16Default = INSR_BWD_F16_DW | INSR_BWD_F16_PROP | INSR_BWD_F16_FUSED;  // profiles/r03/bwd_f16_ab
 struct Knobs {
-  int policy;    // backward path: 0 auto, 1 fused, 2 two-kernel, 3 resident dW, 4 recompute
+  int policy;    // backward path: 0 auto, 1 fused, 2 two-kernel, 3 resident dW, 4 recompute,
+                 // 5 resident dW with f16x3 products (the saved-stream jet_fb variant)
   int f16;       // INSR_BWD_F16_* mask: x6 backward products on the fp16 matrix cores
   int wide_min;  // smallest width of the two-kernel backward (128 or 256)
   int tiles[3];  // forced forward T, forced backward T (0 = auto), minimum block count
@@ -56,7 +57,7 @@ Knobs knobs_of(int mode) {
 }
 static bool knobs_ok(int mode) {
   const int pol = (mode >> INSR_MODE_POLICY_SHIFT) & 7, f = (mode >> INSR_MODE_F16_SHIFT) & 0xF;
-  return pol <= 5 && f <= 8;
+  return pol <= 6 && f <= 8;
 }
 
 // The recompute backward (jet_fb.hpp: forward + reverse jet per tile in one persistent launch, no
@@ -86,10 +87,18 @@ bool resident_ok(int S, int NT, bool lap, int nq, int L) {
 // kbench_policy_M.jsonl), so the auto policy keeps the resident kernel for value jets only then.
 bool use_resident(long n, int S, int NT, bool lap, int nq, int L, const Knobs& k) {
   if (!resident_ok(S, NT, lap, nq, L)) return false;
-  if (k.policy == 3) return true;
+  if (k.policy == 3 || k.policy == 5) return true;
   if (k.policy != 0) return false;
   const bool f16w = (k.f16 & (INSR_BWD_F16_DW | INSR_BWD_F16_PROP)) == (INSR_BWD_F16_DW | INSR_BWD_F16_PROP);
   return lap ? (!f16w && n >= 32768) : (S == 1 && n >= 49152);
+}
+
+// Which kernel serves the resident path: the saved-stream variant of the recompute kernel (jet_fb.hpp
+// SAVED: the reverse sweep on the forward's saved streams, f16x3 products with per-tile scales) or
+// jet_x6r.hpp (bf16x6 products).  Policy 5 forces the former.
+bool use_resident_f16(int S, int NT, bool lap, int nq, int L, const Knobs& k) {
+  if (NT != 8 || nq != 3 || !fb_supported(S, lap, L)) return false;
+  return k.policy == 5;
 }
 
 // Matrix-core precision of the tile-split kernels (a call's INSR_JET_PREC(p) / INSR_JET_BPREC(p);
@@ -592,6 +601,7 @@ struct JetCall {
   bool wide(long n) const { return use_wide(n, S, NT, lap, nqb, k); }
   bool resident(long n, int L) const { return use_resident(n, S, NT, lap, nqb, L, k); }
   bool recompute(int L) const { return use_fb(S, NT, lap, nqb, L, k); }
+  bool resident_f16(long n, int L) const { return resident(n, L) && use_resident_f16(S, NT, lap, nqb, L, k); }
   // 0: fused tile-split + partial rows (insr_siren_jet_bwd), 1: two-kernel, 2: resident dW,
   // 3: recompute (no saved streams)
   int path(long n, int L) const { return recompute(L) ? 3 : (resident(n, L) ? 2 : (wide(n) ? 1 : 0)); }
@@ -1004,7 +1014,7 @@ int insr_siren_jet_bwd_grad_multi(const InsrBwdJob* jobs, int njobs, int din, in
       J.njobs = m;
       const float* prm = params;
       if (!(prm = with_planes(params, din, dout, L, W, mode, st, 0, &rc))) return rc;
-      return dispatch_fb_bwd(c.S, c.lap, L, J, din, dout, prm, work, grad, acc, st);
+      return dispatch_fb_bwd(c.S, c.lap, L, J, din, dout, prm, work, grad, acc, 0, st);
     }
   }
   if (p.nf > 0) {
@@ -1046,7 +1056,7 @@ int insr_siren_jet_bwd_grad_multi(const InsrBwdJob* jobs, int njobs, int din, in
 long insr_jet_bwd_work_bytes(long n, int din, int dout, int L, int W, int mode) {
   if (!shape_ok(din, dout, L, W, mode) || n < 0) return INSR_EINVAL;
   const JetCall c(din, W, mode);
-  if (c.recompute(L)) return fb_work_floats((n + 15) / 16, din, dout, L) * (long)sizeof(float);
+  if (c.recompute(L) || c.resident_f16(n, L)) return fb_work_floats((n + 15) / 16, din, dout, L) * (long)sizeof(float);
   if (c.resident(n, L)) return resident_work_floats(n, din, dout, L) * (long)sizeof(float);
   if (c.wide(n)) return wide_work_floats(n, din, dout, L, W, c.S) * (long)sizeof(float);
   return insr_jet_partial_bytes(n, din, dout, L, W, mode);
@@ -1058,7 +1068,7 @@ int insr_jet_wide_launch_threads(long n, int din, int dout, int L, int W, int mo
   if (c.recompute(L) || c.resident(n, L)) {  // the persistent launch + the dW / compact-row sums
     const long Ps = (long)W * din + W + (long)L * W + (long)dout * W + dout;
     const long wq = ((long)W * W / 4 + 63) / 64, rows_x = (Ps + 63) / 64;
-    threads3[0] = (long)(c.recompute(L) ? fb_launch_blocks((n + 15) / 16) : resident_blocks(n)) * 512;
+    threads3[0] = (long)((c.recompute(L) || c.resident_f16(n, L)) ? fb_launch_blocks((n + 15) / 16) : resident_blocks(n)) * 512;
     threads3[1] = (wq > rows_x ? wq : rows_x) * (L + 1) * 512;
     threads3[2] = 0;
     return 0;
@@ -1099,12 +1109,25 @@ int insr_siren_jet_bwd_grad(const float* x, long n, int din, int dout, int L, in
     J.tstart[0] = 0;
     J.tstart[1] = (int)((n + 15) / 16);
     J.njobs = 1;
-    return dispatch_fb_bwd(c.S, c.lap, L, J, din, dout, params, work, grad, accumulate, st);
+    return dispatch_fb_bwd(c.S, c.lap, L, J, din, dout, params, work, grad, accumulate, 0, st);
   }
   if (c.resident(n, L)) {
     hipStream_t st = (hipStream_t)stream;
     int rc = 0;
     if (!(params = with_planes(params, din, dout, L, W, mode, st, 0, &rc))) return rc;
+    if (c.resident_f16(n, L)) {  // the reverse sweep of jet_fb.hpp on the saved streams
+      FbJobs J{};
+      J.x[0] = x;
+      J.act[0] = act;
+      J.gy[0] = gy;
+      J.gdy[0] = gdy;
+      J.glap[0] = glap;
+      J.n[0] = (int)n;
+      J.tstart[0] = 0;
+      J.tstart[1] = (int)((n + 15) / 16);
+      J.njobs = 1;
+      return dispatch_fb_bwd(c.S, c.lap, L, J, din, dout, params, work, grad, accumulate, 1, st);
+    }
     return dispatch_resident_bwd(c.S, c.lap, L, x, (int)n, din, dout, params, act, gy, gdy, glap, work, grad,
                                  accumulate, st);
   }

@@ -446,6 +446,7 @@ int resident_blocks(long n);
 // its wall bands from separate network calls; job k covers global tiles [tstart[k], tstart[k + 1]).
 struct FbJobs {
   const float* x[kBwdJobs];
+  const float* act[kBwdJobs];  // the forward's saved streams (the saved-stream variant; unread by recompute)
   const float* gy[kBwdJobs];
   const float* gdy[kBwdJobs];
   const float* glap[kBwdJobs];
@@ -456,7 +457,7 @@ struct FbJobs {
 // recompute backward (jet_fb.hpp: W = 128, L = 4, f16x3 with per-tile scales): ONE persistent launch
 // (forward + reverse jet per tile, dW resident per CU) + the fixed-order sums; act is not read
 int dispatch_fb_bwd(int S, bool LAP, int L, const FbJobs& J, int din, int dout, const float* prm, float* work,
-                    float* grad, int accumulate, hipStream_t st);
+                    float* grad, int accumulate, int saved, hipStream_t st);
 bool fb_supported(int S, bool LAP, int L);
 long fb_work_floats(long tiles, int din, int dout, int L);
 int fb_launch_blocks(long tiles);

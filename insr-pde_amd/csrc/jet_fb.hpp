@@ -61,10 +61,10 @@ static __device__ unsigned long long g_fb_stamps[8 * 8 * kFbStampPts];
 // operand, read by transpose reads as the A operand); ZS = fp32 z-streams of hidden layers 1..NZL
 // [layer][s][wave][lane]; SW = the small weights;
 // then the compact accumulators, the tile's seeds [S][3][16] and the block-maximum slots [2][4][8]
-template <int S, int L, int ZR>
+template <int S, int L, int ZR, bool SAVED = false>
 struct FbGeo {
   using BG = X6BwdGeo<4, 8>;
-  static constexpr int NZL = (L - ZR) > 0 ? (L - ZR) : 0;
+  static constexpr int NZL = (!SAVED && (L - ZR) > 0) ? (L - ZR) : 0;
   static constexpr size_t P_BYTES = (size_t)S * BG::ZSET * 2;
   static constexpr size_t H_BYTES = (size_t)S * BG::ZSET * 2;  // point-major as P (dW B via transpose reads)
   static constexpr size_t ZS_BYTES = (size_t)NZL * S * 8 * 64 * 16;
@@ -75,7 +75,7 @@ struct FbGeo {
   static constexpr size_t SACC_OFF = SW_OFF + (size_t)SW_FLOATS * 4;
   static constexpr size_t SEED_OFF = SACC_OFF + (size_t)kFbSmallMax * 4;
   static constexpr size_t MX_OFF = SEED_OFF + (size_t)S * 3 * 16 * 4;
-  static constexpr size_t BYTES = MX_OFF + 2 * 4 * 8 * 4;
+  static constexpr size_t BYTES = MX_OFF + 2 * 5 * 8 * 4;
 };
 
 // sin / cos of w z (4 values).  A wave holding any |w z| > 8192 takes the libm path, out of line:
@@ -154,13 +154,13 @@ __device__ __forceinline__ void fb_h_bounds(const floatx4 (&z)[S], float& mt, fl
   mt *= OMEGA;
 }
 
-template <int S, bool LAP, int L, int ZR>
+template <int S, bool LAP, int L, int ZR, bool SAVED>
 __global__ __launch_bounds__(512, 1) void jet_fb_x6(const FbJobs J, int din, int dout, const float* __restrict__ prm,
                                                     float* __restrict__ dpart, float* __restrict__ small, long Ps,
                                                     int nb, int tiles) {
   constexpr int NT = 8, W = 128, KC = 4;
   using BG = X6BwdGeo<4, NT>;
-  using GG = FbGeo<S, L, ZR>;
+  using GG = FbGeo<S, L, ZR, SAVED>;
   constexpr int LDB = BG::ZROW, ZPLANE = BG::ZPLANE, ZSET = BG::ZSET;
   constexpr int NTAN = LAP ? S - 2 : S - 1;
   constexpr int NZL = GG::NZL;
@@ -219,9 +219,9 @@ __global__ __launch_bounds__(512, 1) void jet_fb_x6(const FbJobs J, int din, int
     float* sacc = reinterpret_cast<float*>(lbt + GG::SACC_OFF);
     float* seed = reinterpret_cast<float*>(lbt + GG::SEED_OFF);
     float* mx = reinterpret_cast<float*>(lbt + GG::MX_OFF);
-    // block maxima of NC (<= 4) classes of non-negative values: each wave's values in, the block's out
+    // block maxima of NC (<= 5) classes of non-negative values: each wave's values in, the block's out
     // (wave-uniform); one barrier.  Slot [class][wave], two slots alternate (each exchange has a barrier)
-    auto exchange = [&](float (&m)[4], auto ncls) __attribute__((always_inline)) {
+    auto exchange = [&](float (&m)[5], auto ncls) __attribute__((always_inline)) {
       constexpr int NC = decltype(ncls)::value;
 #pragma unroll
       for (int k = 0; k < NC; ++k) m[k] = wave_max_nn(m[k]);
@@ -229,13 +229,13 @@ __global__ __launch_bounds__(512, 1) void jet_fb_x6(const FbJobs J, int din, int
         float v = m[0];
 #pragma unroll
         for (int k = 1; k < NC; ++k) v = lane == k ? m[k] : v;
-        mx[(slot * 4 + lane) * 8 + wave] = v;
+        mx[(slot * 5 + lane) * 8 + wave] = v;
       }
       __syncthreads();
 #pragma unroll
       for (int k = 0; k < NC; ++k) {
-        const floatx4 a = *reinterpret_cast<const floatx4*>(mx + (slot * 4 + k) * 8);
-        const floatx4 b = *reinterpret_cast<const floatx4*>(mx + (slot * 4 + k) * 8 + 4);
+        const floatx4 a = *reinterpret_cast<const floatx4*>(mx + (slot * 5 + k) * 8);
+        const floatx4 b = *reinterpret_cast<const floatx4*>(mx + (slot * 5 + k) * 8 + 4);
         const float v = fmaxf(fmaxf(fmaxf(a[0], a[1]), fmaxf(a[2], a[3])), fmaxf(fmaxf(b[0], b[1]), fmaxf(b[2], b[3])));
         m[k] = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, v)));
       }
@@ -254,10 +254,35 @@ __global__ __launch_bounds__(512, 1) void jet_fb_x6(const FbJobs J, int din, int
 #pragma unroll
     for (int kk = 0; kk < 3; ++kk) xk[kk] = (valid && kk < din) ? x[(long)p * din + kk] : 0.f;
     FB_STAMP(0);
-    // the tile's adjoint seeds, thread i -> (stream s, output o, point): issued now, in flight
-    // under the forward, staged into LDS before its last barrier
+    // the tile's adjoint seeds.  Recompute: thread i -> (stream s, output o, point), issued now, in
+    // flight under the forward, staged into LDS before its last barrier.  Saved streams (no forward):
+    // every lane loads its own point's seeds
     float sdv = 0.f;
-    {
+    float gsd[SAVED ? S : 1][3];
+    if constexpr (SAVED) {
+#pragma unroll
+      for (int s = 0; s < S; ++s)
+#pragma unroll
+        for (int o = 0; o < 3; ++o) {
+          float v = 0.f;
+          if (valid && o < dout) {
+            const float* g0 = s == 0 ? J.gy[k] : ((LAP && s == S - 1) ? J.glap[k] : J.gdy[k]);
+            const long at = (s == 0 || (LAP && s == S - 1)) ? (long)p * dout + o : ((long)p * dout + o) * din + (s - 1);
+            if (g0) v = g0[at];
+          }
+          gsd[s][o] = v;
+        }
+    }
+    // z-streams of hidden layer `layer` (1..L) of this tile from the forward's saved streams
+    // (act layout: [layer][tile][stream][row tile][lane][4], jet_common.hpp act_base)
+    const float* actk = SAVED ? J.act[k] : nullptr;
+    const int ntk = ((N + 63) / 64) * 4;
+    auto zload = [&](int layer, floatx4 (&z)[S]) __attribute__((always_inline)) {
+      const float* base = act_base(actk, layer, ntk, lt, S, NT);
+#pragma unroll
+      for (int s = 0; s < S; ++s) z[s] = *reinterpret_cast<const floatx4*>(base + ((s * NT + rt) * 64 + lane) * 4);
+    };
+    if constexpr (!SAVED) {
       const int i = tid, s = i / 48, o = (i / 16) % 3, pp = lt * 16 + (i & 15);
       if (s < S && o < dout && pp < N) {
         const float* gy = J.gy[k];
@@ -272,8 +297,10 @@ __global__ __launch_bounds__(512, 1) void jet_fb_x6(const FbJobs J, int din, int
       }
     }
 
+    floatx4 zr[SAVED ? 1 : ZR][S];  // z-streams of hidden layers NZL + 1 .. L (registers)
+    int eh[L][2];  // per layer j < L: the powers of two of h_j's tangent / Laplacian planes (block-uniform)
+    if constexpr (!SAVED) {
     // ---------------- forward ----------------
-    floatx4 zr[ZR][S];  // z-streams of hidden layers NZL + 1 .. L (registers)
     floatx4 a[S];       // z-streams of the current layer
     // layer 0 (K = d_in: exact fp32 VALU); tangents = W_0 columns, Laplacian stream 0
 #pragma unroll
@@ -290,11 +317,10 @@ __global__ __launch_bounds__(512, 1) void jet_fb_x6(const FbJobs J, int din, int
     }
     // unscale of the next layer's products per stream class (value, tangents, Laplacian)
     float usv = 1.f / kF16WScale, ust = 1.f / kF16WScale, usl = 1.f / kF16WScale;
-    int eh[L][2];  // per layer j < L: the powers of two of h_j's tangent / Laplacian planes (block-uniform)
     // h_j of the current layer -> P planes (block scales per class); two barriers
     auto put_h = [&](auto jc, bool stage_seeds) __attribute__((always_inline)) {
       constexpr int j = decltype(jc)::value;
-      float m[4] = {0.f, 0.f, 0.f, 0.f};
+      float m[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
       if constexpr (S > 1) fb_h_bounds<S, LAP>(a, m[0], m[1]);
       if (stage_seeds && tid < S * 48) seed[tid] = sdv;
       // + every wave's reads of P (this layer's B operand) done
@@ -360,12 +386,17 @@ __global__ __launch_bounds__(512, 1) void jet_fb_x6(const FbJobs J, int din, int
     if constexpr (L >= 2) fwd_layer(std::integral_constant<int, 2>{});
     if constexpr (L >= 3) fwd_layer(std::integral_constant<int, 3>{});
     if constexpr (L >= 4) fwd_layer(std::integral_constant<int, 4>{});
+    }  // forward (recompute only)
 
     // ---------------- reverse ----------------
     // output layer (exact fp32 VALU): hb = W_out^T g, dW_out / db_out into the compact row
     floatx4 zc[S];  // z-streams of the current layer
+    if constexpr (SAVED) {
+      zload(L, zc);
+    } else {
 #pragma unroll
-    for (int s = 0; s < S; ++s) zc[s] = zr[ZR - 1][s];
+      for (int s = 0; s < S; ++s) zc[s] = zr[ZR - 1][s];
+    }
     floatx4 sn, cs;
     fb_sincos(zc[0], sn, cs);
     floatx4 hb[S];
@@ -374,7 +405,12 @@ __global__ __launch_bounds__(512, 1) void jet_fb_x6(const FbJobs J, int din, int
     for (int o = 0; o < dout; ++o) {
       float ga[S];
 #pragma unroll
-      for (int s = 0; s < S; ++s) ga[s] = seed[(s * 3 + o) * 16 + c];
+      for (int s = 0; s < S; ++s) {
+        if constexpr (SAVED)
+          ga[s] = o == 0 ? gsd[s][0] : (o == 1 ? gsd[s][1] : gsd[s][2]);
+        else
+          ga[s] = seed[(s * 3 + o) * 16 + c];
+      }
       const floatx4 w4 = *reinterpret_cast<const floatx4*>(Wos + (o * W + n0));
       floatx4 acc4 = floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -402,14 +438,16 @@ __global__ __launch_bounds__(512, 1) void jet_fb_x6(const FbJobs J, int din, int
       constexpr int j = decltype(jc)::value;
       constexpr int sp = 11 + 5 * (L - j);
       const u32x4* wsl = wsp;
+      // z-streams of layer j - 1 (layer 0: recomputed from x) and their sin / cos; the saved-stream
+      // variant issues their loads here, under the sine reverse and the sums
+      floatx4 zp[S];
+      if constexpr (SAVED && j > 1) zload(j - 1, zp);
       sine_rev<S, LAP>(hb, zc, sn, cs);  // hb = z̄_j
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const float v = sum16(hb[0][r]);
         if (c == 0) sacc[sb + (long)(j - 1) * W + n0 + r] += v;
       }
-      // z-streams of layer j - 1 (layer 0: recomputed from x) and their sin / cos
-      floatx4 zp[S];
       if constexpr (j == 1) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -423,6 +461,8 @@ __global__ __launch_bounds__(512, 1) void jet_fb_x6(const FbJobs J, int din, int
           for (int i = 0; i < NTAN; ++i) zp[1 + i][r] = W0s[3 * n + i];
           if constexpr (LAP) zp[S - 1][r] = 0.f;
         }
+      } else if constexpr (SAVED) {
+        // loaded above
       } else if constexpr (j - 1 <= NZL) {
 #pragma unroll
         for (int s = 0; s < S; ++s) zp[s] = ZS[(((j - 2) * S + s) * 8 + wave) * 64 + lane];
@@ -430,8 +470,9 @@ __global__ __launch_bounds__(512, 1) void jet_fb_x6(const FbJobs J, int din, int
 #pragma unroll
         for (int s = 0; s < S; ++s) zp[s] = zr[j - 1 - NZL - 1][s];
       }
-      // classes: |z̄| value, tangents, Laplacian (h_{j-1}'s scales: the forward's, eh[j - 1])
-      float m[4] = {0.f, 0.f, 0.f, 0.f};
+      // classes: |z̄| value, tangents, Laplacian; h_{j-1}'s bounds (tangents, Laplacian): the forward's
+      // scales eh[j - 1], or (saved streams) this exchange's classes 3, 4
+      float m[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int s = 0; s < S; ++s)
 #pragma unroll
@@ -439,11 +480,19 @@ __global__ __launch_bounds__(512, 1) void jet_fb_x6(const FbJobs J, int din, int
           const int cl = s == 0 ? 0 : ((LAP && s == S - 1) ? 2 : 1);
           m[cl] = fmaxf(m[cl], fabsf(hb[s][r]));
         }
+      if constexpr (SAVED && S > 1) fb_h_bounds<S, LAP>(zp, m[3], m[4]);
       FB_STAMP(sp);
       // + every wave's reads of P / H (the previous layer's / the forward's) done
-      exchange(m, std::integral_constant<int, (S == 1 ? 1 : (LAP ? 3 : 2))>{});
+      exchange(m, std::integral_constant<int, (S == 1 ? 1 : (SAVED ? 5 : (LAP ? 3 : 2)))>{});
       FB_STAMP(sp + 1);
-      const int eht = S > 1 ? eh[j - 1][0] : 0, ehl = LAP ? eh[j - 1][1] : 0;
+      int eht = 0, ehl = 0;
+      if constexpr (SAVED) {
+        if constexpr (S > 1) eht = f16_exp_for(m[3]);
+        if constexpr (LAP) ehl = f16_exp_for(m[4]);
+      } else {
+        if constexpr (S > 1) eht = eh[j - 1][0];
+        if constexpr (LAP) ehl = eh[j - 1][1];
+      }
       const float bht = ldexpf(1.f, eht), bhl = ldexpf(1.f, ehl);   // h's tangent / Laplacian scales
       const float zht = ldexpf(1.f, -eht), zhl = ldexpf(1.f, -ehl);  // ... and the matching z̄ factors
       int e = f16_exp_for(fmaxf(m[0], fmaxf(m[1] * zht, m[2] * zhl)));
@@ -586,7 +635,7 @@ inline long fb_work_floats_impl(long tiles, int din, int dout, int L) {
   return (long)L * nb * 128 * 128 + nb * small_count(din, dout, L, 128);
 }
 
-template <int S, bool LAP, int L, int ZR>
+template <int S, bool LAP, int L, int ZR, bool SAVED>
 int fb_bwd_t(const FbJobs& J, int din, int dout, const float* prm, float* work, float* grad, int accumulate,
              hipStream_t st) {
   constexpr int W = 128;
@@ -597,12 +646,12 @@ int fb_bwd_t(const FbJobs& J, int din, int dout, const float* prm, float* work, 
   if (Ps > kFbSmallMax || dout < 1 || dout > 3 || din < 1 || din > 3) return INSR_EINVAL;
   float* dpart = work;
   float* small = dpart + (long)L * nb * W * W;
-  constexpr size_t lds = FbGeo<S, L, ZR>::BYTES;
+  constexpr size_t lds = FbGeo<S, L, ZR, SAVED>::BYTES;
   static_assert(lds <= 163840, "LDS");
-  static const bool attr = (hipFuncSetAttribute((const void*)jet_fb_x6<S, LAP, L, ZR>, hipFuncAttributeMaxDynamicSharedMemorySize,
+  static const bool attr = ((void)hipFuncSetAttribute((const void*)jet_fb_x6<S, LAP, L, ZR, SAVED>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)lds), true);  // once per instantiation (thread-safe static init)
   (void)attr;
-  hipLaunchKernelGGL((jet_fb_x6<S, LAP, L, ZR>), dim3(nb), dim3(512), lds, st, J, din, dout, prm, dpart, small, Ps, nb,
+  hipLaunchKernelGGL((jet_fb_x6<S, LAP, L, ZR, SAVED>), dim3(nb), dim3(512), lds, st, J, din, dout, prm, dpart, small, Ps, nb,
                      tiles);
   const int grad16 = (((uintptr_t)(grad + hidden_off(din, W, 1))) & 15) == 0 ? 1 : 0;
   const int wq = (W * W / 4 + 63) / 64;

@@ -567,7 +567,7 @@ int launch_fwd_split_t(const float* x, int N, int din, int dout, int L, const fl
     return INSR_EINVAL;
   } else {
     const int nb = ((N + 15) / 16 + T - 1) / T;
-    static const bool attr_set = (hipFuncSetAttribute((const void*)jet_fwd_split<NT, S, LAP, T>,
+    static const bool attr_set = ((void)hipFuncSetAttribute((const void*)jet_fwd_split<NT, S, LAP, T>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds), true);  // once per instantiation (thread-safe static init)
     (void)attr_set;
     if (N < 0) {  // occupancy query (split_tiles): resident blocks per CU
@@ -589,7 +589,7 @@ int launch_bwd_split_t(const float* x, int N, int din, int dout, int L, const fl
     return INSR_EINVAL;
   } else {
     const int nb = ((N + 15) / 16 + T - 1) / T;
-    static const bool attr_set = (hipFuncSetAttribute((const void*)jet_bwd_split<NT, S, LAP, T>,
+    static const bool attr_set = ((void)hipFuncSetAttribute((const void*)jet_bwd_split<NT, S, LAP, T>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds), true);  // once per instantiation (thread-safe static init)
     (void)attr_set;
     if (N < 0) {  // occupancy query (split_tiles): resident blocks per CU

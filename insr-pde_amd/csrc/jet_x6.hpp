@@ -675,7 +675,7 @@ int launch_fwd_x6_mixed_t(const InsrJetJob* jobs, const int* modes, const float*
     return INSR_EINVAL;
   } else {
     if (njobs < 1 || njobs > kFwdJobs) return INSR_EINVAL;
-    static const bool attr_set = (hipFuncSetAttribute((const void*)jet_fwd_x6_mixed<NQ, NT, DIN, BODIES>,
+    static const bool attr_set = ((void)hipFuncSetAttribute((const void*)jet_fwd_x6_mixed<NQ, NT, DIN, BODIES>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds), true);  // once per instantiation (thread-safe static init)
     (void)attr_set;
     FwdMixX6 pk{};
@@ -710,7 +710,7 @@ int launch_fwd_x6_multi_t(const InsrJetJob* jobs, const int* small, const int* n
     return INSR_EINVAL;
   } else {
     if (njobs < 1 || njobs > kFwdJobs) return INSR_EINVAL;
-    static const bool attr_set = (hipFuncSetAttribute((const void*)jet_fwd_x6_multi<NQ, NT, S, LAP, T, TB>,
+    static const bool attr_set = ((void)hipFuncSetAttribute((const void*)jet_fwd_x6_multi<NQ, NT, S, LAP, T, TB>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds), true);  // once per instantiation (thread-safe static init)
     (void)attr_set;
     FwdJobsX6 pk{};
@@ -744,7 +744,7 @@ int launch_fwd_x6_t(const float* x, int N, int din, int dout, int L, const float
     return INSR_EINVAL;
   } else {
     const int nb = ((N + 15) / 16 + T - 1) / T;
-    static const bool attr_set = (hipFuncSetAttribute((const void*)jet_fwd_x6<NQ, NT, S, LAP, T>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    static const bool attr_set = ((void)hipFuncSetAttribute((const void*)jet_fwd_x6<NQ, NT, S, LAP, T>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)lds), true);  // once per instantiation (thread-safe static init)
     (void)attr_set;
     if (N < 0) {  // occupancy query (split_tiles): resident blocks per CU
@@ -1334,7 +1334,7 @@ int launch_bwd_x6_t(const BwdJobsX6* J, int din, int dout, int L, const float* p
   if constexpr (lds > kLdsMax || NT > 8) {
     return INSR_EINVAL;
   } else {
-    static const bool attr_set = (hipFuncSetAttribute((const void*)jet_bwd_x6<NQ, NT, S, LAP, T>,
+    static const bool attr_set = ((void)hipFuncSetAttribute((const void*)jet_bwd_x6<NQ, NT, S, LAP, T>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds), true);  // once per instantiation (thread-safe static init)
     (void)attr_set;
     if (!J) {  // occupancy query (split_tiles): resident blocks per CU

@@ -394,7 +394,7 @@ int resident_bwd_t(const float* x, int N, int din, int dout, const float* prm, c
   constexpr size_t lds = x6r_lds_bytes<NQ, S>();
   static_assert(lds <= 163840, "LDS");
   static_assert(L >= 1 && L <= 4, "resident dW: 1..4 hidden layers");
-  static const bool attr = (hipFuncSetAttribute((const void*)jet_bwd_x6r<NQ, S, LAP, L, RPW>, hipFuncAttributeMaxDynamicSharedMemorySize,
+  static const bool attr = ((void)hipFuncSetAttribute((const void*)jet_bwd_x6r<NQ, S, LAP, L, RPW>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)lds), true);  // once per instantiation (thread-safe static init)
   (void)attr;
   hipLaunchKernelGGL((jet_bwd_x6r<NQ, S, LAP, L, RPW>), dim3(nb), dim3(512 / RPW), lds, st, x, N, din, dout, prm, act, gy, gdy,

@@ -90,7 +90,7 @@ CASES = [  # (mode, d_in, d_out, L): the kernel is compiled for the fluid nets' 
 def test_resident_matches_oracle(B, resident, case, n):
     mode, din, dout, L = case
     m = {"value": B._native.MODE_VALUE, "grad": B._native.MODE_GRAD, "lap": B._native.MODE_LAP}[mode]
-    assert resident.insr_jet_bwd_path(n, din, dout, L, 128, m) == 2
+    assert resident.insr_jet_bwd_path(n, din, dout, L, 128, m | B._native.scope_bits()) == 2
     ref, net = pair(B, din, dout, L, 128, 100 + n % 97 + L)
     x = torch.rand(n, din, generator=torch.Generator().manual_seed(n)) * 2 - 1
     run(B, ref, net, x, mode, n + 1)
