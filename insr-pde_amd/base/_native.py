@@ -50,7 +50,8 @@ _FIELDS = {"policy": 7 << MODE_POLICY_SHIFT, "bwd_f16": 0xF << MODE_F16_SHIFT, "
 
 
 def jet_policy(p):
-    """INSR_JET_POLICY(p): backward path 0 auto, 1 fused, 2 two-kernel, 3 resident dW, 4 recompute."""
+    """INSR_JET_POLICY(p): backward path 0 auto, 1 fused, 2 two-kernel, 3 resident dW (bf16x6), 4 recompute,
+    5 resident dW with f16x3 products (the recompute kernel's reverse sweep on the saved streams)."""
     return (int(p) + 1) << MODE_POLICY_SHIFT
 
 

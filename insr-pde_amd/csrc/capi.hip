@@ -85,20 +85,28 @@ bool resident_ok(int S, int NT, bool lap, int nq, int L) {
 // the resident kernel stays bf16x6) the two-kernel Laplacian backward wins at the fluid2DtlgnM batch
 // (66,844 points: 553-561 vs 590-601 us; value jets tie at 199-205, profiles/r03/final_r3o/
 // kbench_policy_M.jsonl), so the auto policy keeps the resident kernel for value jets only then.
+bool use_resident_f16(long n, int S, int NT, bool lap, int nq, int L, const Knobs& k);
 bool use_resident(long n, int S, int NT, bool lap, int nq, int L, const Knobs& k) {
   if (!resident_ok(S, NT, lap, nq, L)) return false;
   if (k.policy == 3 || k.policy == 5) return true;
   if (k.policy != 0) return false;
+  if (use_resident_f16(n, S, NT, lap, nq, L, k)) return true;
   const bool f16w = (k.f16 & (INSR_BWD_F16_DW | INSR_BWD_F16_PROP)) == (INSR_BWD_F16_DW | INSR_BWD_F16_PROP);
   return lap ? (!f16w && n >= 32768) : (S == 1 && n >= 49152);
 }
 
 // Which kernel serves the resident path: the saved-stream variant of the recompute kernel (jet_fb.hpp
-// SAVED: the reverse sweep on the forward's saved streams, f16x3 products with per-tile scales) or
-// jet_x6r.hpp (bf16x6 products).  Policy 5 forces the former.
-bool use_resident_f16(int S, int NT, bool lap, int nq, int L, const Knobs& k) {
+// SAVED: the reverse sweep on the forward's saved streams, f16x3 products with per-tile scales; the
+// INSR_BWD_F16_FUSED bit of the call's mask) or jet_x6r.hpp (bf16x6 products).  Policy 5 forces the
+// former.  Auto: 2-d Laplacian jets from 12,288 points -- backward into .grad incl. sums (kbench r4j,
+// profiles/r04/kbench_resident_f16.jsonl): 16,708 points 142 vs 166 us two-kernel, 33,092 239 vs
+// 296-301, 66,844 428 vs 577-582; 8,192 79 vs 73 (two-kernel); value jets lose at every size (S = 1:
+// 16-point tiles, 90 vs 57 fused at 16,708), so they keep their paths.
+bool use_resident_f16(long n, int S, int NT, bool lap, int nq, int L, const Knobs& k) {
   if (NT != 8 || nq != 3 || !fb_supported(S, lap, L)) return false;
-  return k.policy == 5;
+  if (k.policy == 5) return true;
+  if (k.policy != 0 || !(k.f16 & INSR_BWD_F16_FUSED)) return false;
+  return lap && S == 4 && n >= 12288;
 }
 
 // Matrix-core precision of the tile-split kernels (a call's INSR_JET_PREC(p) / INSR_JET_BPREC(p);
@@ -601,7 +609,7 @@ struct JetCall {
   bool wide(long n) const { return use_wide(n, S, NT, lap, nqb, k); }
   bool resident(long n, int L) const { return use_resident(n, S, NT, lap, nqb, L, k); }
   bool recompute(int L) const { return use_fb(S, NT, lap, nqb, L, k); }
-  bool resident_f16(long n, int L) const { return resident(n, L) && use_resident_f16(S, NT, lap, nqb, L, k); }
+  bool resident_f16(long n, int L) const { return resident(n, L) && use_resident_f16(n, S, NT, lap, nqb, L, k); }
   // 0: fused tile-split + partial rows (insr_siren_jet_bwd), 1: two-kernel, 2: resident dW,
   // 3: recompute (no saved streams)
   int path(long n, int L) const { return recompute(L) ? 3 : (resident(n, L) ? 2 : (wide(n) ? 1 : 0)); }

@@ -169,8 +169,9 @@ def test_value_backward_launch_shape(lib):
 
 
 def test_backward_path_policy(lib):
-    """insr_jet_bwd_path answers on the host: the two-kernel path for the fluid nets' Laplacian
-    backward at the headline batch and at W = 256, the fused kernel for value jets below 24,576 points
+    """insr_jet_bwd_path answers on the host: the resident-dW path for the fluid nets' Laplacian
+    backward from 12,288 points (its f16x3 saved-stream kernel while the INSR_BWD_F16_FUSED bit is on,
+    else -- with bf16x6 products -- the two-kernel path below 32,768 points), two-kernel at W = 256, the fused kernel for value jets below 24,576 points
     (two-kernel from there), the resident-dW kernel for the fluid2DtlgnM value batch (from 49,152
     points) or when forced (policy 3); policy 4 forces the recompute backward (path 3: no saved
     streams) where it applies, independently of n (the forward's skip-the-saves decision must match
@@ -178,11 +179,14 @@ def test_backward_path_policy(lib):
     from base import _native as nat
     V, G, LAP = nat.MODE_VALUE, nat.MODE_GRAD, nat.MODE_LAP
     P = nat.jet_policy
-    assert lib.insr_jet_bwd_path(16708, 2, 1, 4, 128, LAP) == 1
+    assert lib.insr_jet_bwd_path(16708, 2, 1, 4, 128, LAP) == 2
+    assert lib.insr_jet_bwd_path(12288, 2, 1, 4, 128, LAP) == 2
+    assert lib.insr_jet_bwd_path(12287, 2, 1, 4, 128, LAP) == 1
+    assert lib.insr_jet_bwd_path(16708, 2, 1, 4, 128, LAP | nat.jet_bwd_f16(3)) == 1  # bf16x6 resident: >= 32,768
     assert lib.insr_jet_bwd_path(16708, 2, 2, 4, 128, V) == 0
     assert lib.insr_jet_bwd_path(1024, 2, 2, 4, 128, V) == 0
     # fluid2DtlgnM: the two-kernel f16x3 Laplacian backward (resident when its products are bf16x6)
-    assert lib.insr_jet_bwd_path(65536 + 1308, 2, 1, 4, 128, LAP) == 1
+    assert lib.insr_jet_bwd_path(65536 + 1308, 2, 1, 4, 128, LAP) == 2
     assert lib.insr_jet_bwd_path(65536 + 1308, 2, 1, 4, 128, LAP | nat.jet_bwd_f16(0)) == 2
     assert lib.insr_jet_bwd_path(65536 + 1308, 2, 2, 4, 128, V) == 2
     assert lib.insr_jet_bwd_path(33092, 2, 2, 4, 128, V) == 1   # value jets two-kernel from 24,576
@@ -203,9 +207,9 @@ def test_backward_path_policy(lib):
     assert lib.insr_jet_bwd_path(16708, 2, 1, 3, 128, LAP | P(4)) != 3        # 4 hidden layers only
     assert lib.insr_jet_bwd_path(16708, 2, 1, 4, 64, LAP | P(4)) != 3         # W = 128 only
     assert lib.insr_jet_bwd_path(16708, 2, 1, 4, 128, LAP | P(4) | nat.jet_prec(nat.PREC_BF16)) != 3  # fp32-level only
-    assert lib.insr_jet_bwd_path(16708, 2, 1, 4, 128, LAP) == 1              # no state left behind
+    assert lib.insr_jet_bwd_path(16708, 2, 1, 4, 128, LAP) == 2              # no state left behind
     # malformed knob fields are refused like any bad mode
-    assert lib.insr_jet_bwd_path(16708, 2, 1, 4, 128, LAP | (6 << nat.MODE_POLICY_SHIFT)) == -1
+    assert lib.insr_jet_bwd_path(16708, 2, 1, 4, 128, LAP | (7 << nat.MODE_POLICY_SHIFT)) == -1
     assert lib.insr_jet_bwd_path(16708, 2, 1, 4, 128, LAP | (9 << nat.MODE_F16_SHIFT)) == -1
 
 

@@ -141,10 +141,10 @@ def test_default_routing(B):
     path (3) only when forced (policy 4)."""
     lib = B._native.lib()
     nat = B._native
-    assert lib.insr_jet_bwd_path(16708, 2, 1, 4, 128, nat.MODE_LAP) == 1
+    assert lib.insr_jet_bwd_path(16708, 2, 1, 4, 128, nat.MODE_LAP) == 2    # the f16x3 saved-stream kernel
     assert lib.insr_jet_bwd_path(16708, 2, 2, 4, 128, nat.MODE_VALUE) == 0
     assert lib.insr_jet_bwd_path(1024, 2, 2, 4, 128, nat.MODE_VALUE) == 0
-    assert lib.insr_jet_bwd_path(66844, 2, 1, 4, 128, nat.MODE_LAP) == 1    # fluid2DtlgnM batch
+    assert lib.insr_jet_bwd_path(66844, 2, 1, 4, 128, nat.MODE_LAP) == 2    # fluid2DtlgnM batch
     assert lib.insr_jet_bwd_path(66844, 2, 1, 4, 128, nat.MODE_LAP | nat.jet_bwd_f16(0)) == 2
     assert lib.insr_jet_bwd_path(66844, 2, 2, 4, 128, nat.MODE_VALUE) == 2
     assert lib.insr_jet_bwd_path(20400, 2, 2, 5, 128, nat.MODE_GRAD) not in (2, 3)  # 5 hidden layers

@@ -19,7 +19,18 @@ import torch  # noqa: E402
 NETS = {"fluid_pres": (2, 1, 4, 128, 2), "fluid_vel": (2, 2, 4, 128, 0)}
 
 
-def phases(L):
+def phases(L, saved=False):
+    if saved:  # the saved-stream variant (policy 5): no forward, the output layer reads z_L
+        names = [(0, 10, "out-layer rev (+ z_L load)")]
+        prev = 10
+        for j in range(L, 0, -1):
+            sp = 11 + 5 * (L - j)
+            names += [(prev, sp, f"rev L{j} sine_rev+z"), (sp, sp + 1, f"rev L{j} exchange"),
+                      (sp + 1, sp + 2, f"rev L{j} P/H writes"), (sp + 2, sp + 3, f"rev L{j} dW"),
+                      (sp + 3, sp + 4, f"rev L{j} prop")]
+            prev = sp + 4
+        names.append((prev, 31, "rev L0"))
+        return names
     names = [(0, 1, "fwd L0 + planes")]
     for j in range(1, L + 1):
         names.append((2 * j - 1, 2 * j, f"fwd L{j} MFMA"))
@@ -40,6 +51,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--net", default="fluid_pres")
     ap.add_argument("--n", type=int, default=16708)
+    ap.add_argument("--policy", type=int, default=4, choices=[4, 5], help="4 recompute, 5 saved-stream variant")
     args = ap.parse_args()
     import base
     from base import _native as nat
@@ -51,9 +63,16 @@ def main():
     net = base.MLP(din, dout, L, W, nonlinearity="sine").cuda()
     net.refresh_wsplit()
     flat = net.flat_params()
-    cm = mode | nat.MODE_WSPLIT | nat.jet_policy(4)
-    assert lib.insr_jet_bwd_path(n, din, dout, L, W, cm) == 3
+    cm = mode | nat.MODE_WSPLIT | nat.jet_policy(args.policy)
+    assert lib.insr_jet_bwd_path(n, din, dout, L, W, cm) == (3 if args.policy == 4 else 2)
     x = (torch.rand(n, din, device="cuda") * 2 - 1).contiguous()
+    act = None
+    if args.policy == 5:  # the forward's saved streams
+        act = torch.empty(lib.insr_jet_act_bytes(n, din, L, W, cm) // 4, device="cuda")
+        y, dy, lp = (torch.empty(n, dout, device="cuda"), torch.empty(n, dout, din, device="cuda"),
+                     torch.empty(n, dout, device="cuda"))
+        nat.check(lib.insr_siren_jet_fwd(nat.ptr(x), n, din, dout, L, W, cm, nat.ptr(flat), nat.ptr(y), nat.ptr(dy),
+                                         nat.ptr(lp), nat.ptr(act), nat.stream_of(x.device)), "fwd")
     gy = torch.randn(n, dout, device="cuda")
     gdy = torch.randn(n, dout, din, device="cuda") if mode else None
     glap = torch.randn(n, dout, device="cuda") if mode == 2 else None
@@ -61,12 +80,12 @@ def main():
     grad = torch.zeros(net.param_count, device="cuda")
     st = nat.stream_of(x.device)
     for _ in range(3):
-        nat.check(lib.insr_siren_jet_bwd_grad(nat.ptr(x), n, din, dout, L, W, cm, nat.ptr(flat), None, nat.ptr(gy),
+        nat.check(lib.insr_siren_jet_bwd_grad(nat.ptr(x), n, din, dout, L, W, cm, nat.ptr(flat), nat.ptr(act), nat.ptr(gy),
                                               nat.ptr(gdy), nat.ptr(glap), nat.ptr(work), nat.ptr(grad), 0, st), "bwd")
     torch.cuda.synchronize()
     buf = (ctypes.c_ulonglong * (8 * 8 * 32))()
     nat.check(lib.insr_diag_fb_stamps(buf, len(buf)), "stamps")
-    ph = phases(L)
+    ph = phases(L, args.policy == 5)
     rows = []
     for wave in range(8):
         for t in range(8):
