@@ -85,7 +85,7 @@ def test_weight_planes_follow_the_parameters(B, shape):
     net = B.MLP(din, dout, L, W, nonlinearity="sine")
     lib = B._native.lib()
     assert net.wsplit_offset() == lib.insr_siren_wsplit_offset(din, dout, L, W)
-    assert net.wsplit_floats() == lib.insr_siren_wsplit_floats(L, W) == 5 * L * W * W
+    assert net.wsplit_floats() == lib.insr_siren_wsplit_floats(L, W) == 5 * L * W * W + 4  # + the status quad
     flat = net.flat_params()
     store = flat._base if flat._base is not None else flat
     assert store.numel() == net.wsplit_offset() + net.wsplit_floats()
