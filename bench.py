@@ -288,7 +288,7 @@ def jet_precision_names(precision):
         return {"mixed": "bf16x3/bf16"}.get(precision, precision)
     mask = nat.bwd_f16_mask()
     bwd = "f16x3" if mask == 7 else (f"bf16x6+f16x3(mask {mask})" if mask else "bf16x6")
-    bwd += " (resident-dW kernel: bf16x6)" if mask else ""
+    bwd += " (the bf16x6 resident-dW kernel of value jets >= 49,152 points: bf16x6)" if mask else ""
     return f"f16x3/{bwd}"  # the library's default pair: f16x3 forward, bf16x6-contract backward
 
 
@@ -371,11 +371,20 @@ def kernel_identity(kind, mode, n, din, dout, L, W, nq=3):
         thr = (ctypes.c_long * 3)()
         nat.check(lib.insr_jet_wide_launch_threads(n, din, dout, L, W, m_b, thr), "insr_jet_wide_launch_threads")
         zr = 4 if S == 1 else 2  # jet_fb.hip: hidden layers whose z-streams stay in registers
-        parts = [(f"insr::jet_fb_x6<{S}, {lap}, {L}, {zr}>", thr[0]), ("insr::reduce_dw_kernel", thr[1])]
+        parts = [(f"insr::jet_fb_x6<{S}, {lap}, {L}, {zr}, false>", thr[0]), ("insr::reduce_dw_kernel", thr[1])]
         return " + ".join(f"{k}|grid={g}" for k, g in parts) + " (recompute backward: forward + reverse jet per " \
             "tile in one persistent launch, no saved streams, then the dW / compact-row sums; time = both " \
             "launches; achieved counts the backward's algorithmic flops only, not the recomputed forward)", \
             parts, True, 3
+    if path == 2 and lib.insr_jet_bwd_kernel(n, din, dout, L, W, m_b) == 1:
+        # the resident-dW backward on jet_fb_x6's saved-stream variant (f16x3 products) + the sums
+        import ctypes
+        thr = (ctypes.c_long * 3)()
+        nat.check(lib.insr_jet_wide_launch_threads(n, din, dout, L, W, m_b, thr), "insr_jet_wide_launch_threads")
+        parts = [(f"insr::jet_fb_x6<{S}, {lap}, {L}, 1, true>", thr[0]), ("insr::reduce_dw_kernel", thr[1])]
+        return " + ".join(f"{k}|grid={g}" for k, g in parts) + " (resident-dW backward, f16x3: the reverse " \
+            "sweep on the saved streams, dW in registers per CU, no adjoint round trip; then the dW / " \
+            "compact-row sums; time = both launches)", parts, True, 3
     if path == 2:  # the resident-dW persistent kernel + the fixed-order sums
         import ctypes
         thr = (ctypes.c_long * 3)()

@@ -270,6 +270,9 @@ int insr_jet_bwd_is_wide(long n_points, int d_in, int width, int mode);
  * insr_siren_jet_bwd_grad with an insr_jet_bwd_work_bytes workspace; path 3 never depends on
  * n_points (the forward's decision and the backward's agree). */
 int insr_jet_bwd_path(long n_points, int d_in, int d_out, int num_hidden, int width, int mode);
+/* Which kernel family serves the path above: 1 = jet_fb_x6 (the recompute kernel, path 3, or its
+ * saved-stream variant on path 2: f16x3 products), 0 = the path's other kernels (profilers, bench.py). */
+int insr_jet_bwd_kernel(long n_points, int d_in, int d_out, int num_hidden, int width, int mode);
 
 /* Matrix products of the x6 (fp32-level) backward that run on the fp16 matrix cores instead of
  * six bf16 products: f16x3 (two fp16 terms per operand, three products, 22 significant bits),

@@ -151,6 +151,7 @@ SIGNATURES = {
     "insr_jet_bwd_multi_work_bytes": (_L, [_P, _I, _I, _I, _I, _I, _I]),
     "insr_jet_bwd_is_wide": (_I, [_L, _I, _I, _I]),
     "insr_jet_bwd_path": (_I, [_L, _I, _I, _I, _I, _I]),
+    "insr_jet_bwd_kernel": (_I, [_L, _I, _I, _I, _I, _I]),
     "insr_comm_available": (_I, []),
     "insr_comm_id_bytes": (_L, []),
     "insr_comm_unique_id": (_I, [_P]),

@@ -1097,6 +1097,13 @@ int insr_jet_bwd_path(long n, int din, int dout, int L, int W, int mode) {
   return JetCall(din, W, mode).path(n, L);
 }
 
+int insr_jet_bwd_kernel(long n, int din, int dout, int L, int W, int mode) {
+  if (!shape_ok(din, dout, L, W, mode) || n < 0) return INSR_EINVAL;
+  const JetCall c(din, W, mode);
+  const int p = c.path(n, L);
+  return (p == 3 || (p == 2 && c.resident_f16(n, L))) ? 1 : 0;
+}
+
 int insr_siren_jet_bwd_grad(const float* x, long n, int din, int dout, int L, int W, int mode, const float* params,
                             const float* act, const float* gy, const float* gdy, const float* glap, float* work,
                             float* grad, int accumulate, void* stream) {

@@ -205,6 +205,7 @@ __global__ __launch_bounds__(512, 1) void jet_fb_x6(const FbJobs J, int din, int
     const float* prmt = prm + po;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63, g = lane >> 4, c = lane & 15;
     const int rt = wave;             // this wave's row tile of every hidden layer
+    const int ra = wave >> 1, cb = wave & 1;  // its dW tiles: rows 2 ra, 2 ra + 1 x columns 4 cb .. 4 cb + 3
     const int n0 = 16 * rt + 4 * g;  // this lane's first neuron
     const u32x4* wsp = wsp_base(prmt, din, dout, L, W);
     unsigned char* lbt = lb + zo;
@@ -524,23 +525,30 @@ __global__ __launch_bounds__(512, 1) void jet_fb_x6(const FbJobs J, int din, int
       FB_STAMP(sp + 2);
       // the propagation's first W^T fragment: its L2 latency runs under the dW MFMAs
       FragQ<4> wn = wsp_frag<4, NT>(wsl, L, 1, j, rt, 0, lane);
-      // dW_j rows 16 rt + c (A: z̄ column reads of the point-major P sets), columns m (B: H)
+      // dW_j: wave (ra, cb) = (wave >> 1, wave & 1) owns row tiles 2 ra, 2 ra + 1 (A: z̄ column reads
+      // of the point-major P sets) x column tiles 4 cb .. 4 cb + 3 (B: transpose reads of H) -- 6
+      // fragment reads per 8 MFMA triples (a wave owning one row tile x all 8 column tiles: 9)
 #pragma unroll
       for (int ch = 0; ch < NCH; ++ch) {
         const int u = 2 * ch + (g >> 1);
         const bool live = u < S;
         const int p0 = 8 * (g & 1);
-        FragQ<4> af;
-        const unsigned short* pa = P + (live ? u : 0) * ZSET + (p0 + (c >> 2)) * LDB + 16 * rt + 4 * (c & 3);
+        FragQ<4> af[2];
 #pragma unroll
-        for (int q = 0; q < 2; ++q) {
-          const v4s lo = ds_read_tr16(pa + q * ZPLANE);
-          const v4s hi = ds_read_tr16(pa + q * ZPLANE + 4 * LDB);
-          const u32x2 wl = __builtin_bit_cast(u32x2, lo), wh = __builtin_bit_cast(u32x2, hi);
-          af.q[q] = live ? u32x4{wl[0], wl[1], wh[0], wh[1]} : u32x4{0u, 0u, 0u, 0u};
+        for (int i = 0; i < 2; ++i) {
+          const unsigned short* pa =
+              P + (live ? u : 0) * ZSET + (p0 + (c >> 2)) * LDB + 16 * (2 * ra + i) + 4 * (c & 3);
+#pragma unroll
+          for (int q = 0; q < 2; ++q) {
+            const v4s lo = ds_read_tr16(pa + q * ZPLANE);
+            const v4s hi = ds_read_tr16(pa + q * ZPLANE + 4 * LDB);
+            const u32x2 wl = __builtin_bit_cast(u32x2, lo), wh = __builtin_bit_cast(u32x2, hi);
+            af[i].q[q] = live ? u32x4{wl[0], wl[1], wh[0], wh[1]} : u32x4{0u, 0u, 0u, 0u};
+          }
         }
 #pragma unroll
-        for (int ct = 0; ct < NT; ++ct) {
+        for (int q4 = 0; q4 < 4; ++q4) {
+          const int ct = 4 * cb + q4;
           FragQ<4> bf;  // B: h_{j-1} rows 16 ct + c at the chunk's 8 points -- transpose reads as A
 #pragma unroll
           for (int q = 0; q < 2; ++q) {
@@ -550,7 +558,8 @@ __global__ __launch_bounds__(512, 1) void jet_fb_x6(const FbJobs J, int din, int
             const u32x2 wl = __builtin_bit_cast(u32x2, lo), wh = __builtin_bit_cast(u32x2, hi);
             bf.q[q] = u32x4{wl[0], wl[1], wh[0], wh[1]};
           }
-          dacc[j - 1][ct] = mfma_q<4>(af, bf, dacc[j - 1][ct]);
+#pragma unroll
+          for (int i = 0; i < 2; ++i) dacc[j - 1][4 * i + q4] = mfma_q<4>(af[i], bf, dacc[j - 1][4 * i + q4]);
           X6_SCHED_FENCE();
         }
       }
@@ -609,13 +618,13 @@ __global__ __launch_bounds__(512, 1) void jet_fb_x6(const FbJobs J, int din, int
   // ---- the block's partials: dW of every hidden layer in fragment order (one 1 KiB wave store per
   // accumulator, the accumulator's power of two undone; reduce_dw_kernel frag = 1 scatters the
   // sums), then the compact row ----
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, rt = wave;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, ra = wave >> 1, cb = wave & 1;
 #pragma unroll
   for (int jl = 0; jl < L; ++jl) {
     floatx4* out = reinterpret_cast<floatx4*>(dpart + ((long)jl * nb + blockIdx.x) * W * W);
     const float f = E[jl] == kNoE ? 1.f : ldexpf(1.f, -E[jl]);
 #pragma unroll
-    for (int ct = 0; ct < NT; ++ct) out[(rt * NT + ct) * 64 + lane] = dacc[jl][ct] * f;
+    for (int q = 0; q < NT; ++q) out[((2 * ra + q / 4) * NT + 4 * cb + q % 4) * 64 + lane] = dacc[jl][q] * f;
   }
   __syncthreads();  // every owner lane's last compact update
   for (int i = threadIdx.x; i < Ps; i += 512) small[(long)blockIdx.x * Ps + i] = sacc0[i];
