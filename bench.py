@@ -78,9 +78,12 @@ def parse():
     ap.add_argument("--shard-of", type=int, default=1,
                     help="one process runs the per-rank shard of a K-rank strong-scaling run (global batch / K "
                          "points per phase iteration; elasticity: the draw at resolution / K^(1/3)); 1 GPU")
-    ap.add_argument("--bwd-policy", type=int, default=0, choices=[0, 1, 2, 3, 4],
+    ap.add_argument("--graph-unroll", type=int, default=4,
+                    help="iterations per hipGraph replay inside a timestep's phase loop (PhaseLoop "
+                         "insr_graph_unroll; 1 = one replay per iteration)")
+    ap.add_argument("--bwd-policy", type=int, default=0, choices=[0, 1, 2, 3, 4, 5],
                     help="backward path (A/B studies): 0 auto, 1 fused tile-split, 2 two-kernel, 3 resident dW, "
-                         "4 recompute")
+                         "4 recompute, 5 resident f16x3")
     ap.add_argument("--bwd-f16", type=int, default=-1, choices=list(range(-1, 8)),
                     help="x6 backward products on the fp16 matrix cores, INSR_BWD_F16_* mask (A/B studies; "
                          "-1 = library default)")
@@ -182,6 +185,7 @@ def build_model(args, world, rank):
     wl = WORKLOADS[args.config]
     res = wl["res"]
     cfg = baseline_config(args.config, sample_resolution=res, insr_graph=not args.no_graph,
+                          insr_graph_unroll=max(1, args.graph_unroll),
                           insr_sync_every=10 ** 9, insr_progress=False, early_stop=False,
                           proj_dir="/tmp/insr_bench", max_n_iters=10 ** 9,
                           insr_precision=None if args.precision == "fp32" else args.precision)
@@ -262,8 +266,7 @@ def run_timestep(model, wl, loops, i0, k):
     their optimiser and hipGraphs across bench timesteps.)"""
     for p, pl in enumerate(loops):
         snapshot(model, wl, p)
-        for i in range(i0, i0 + k):
-            pl.step(i)
+        pl.run_iters(i0, k)  # groups of insr_graph_unroll iterations per graph replay
 
 
 def sync_all(world):
@@ -611,6 +614,13 @@ def main():
     run_timestep(model, wl, loops, w_eff, 1)
     torch.cuda.synchronize()
     w_eff += 1
+    # and, with --graph-unroll U > 1, one untimed timestep of U iterations per phase: it captures
+    # (and so runs) each phase loop's U-iteration graph outside the timed region
+    U = max(1, args.graph_unroll)
+    if U > 1 and not args.no_graph:
+        run_timestep(model, wl, loops, w_eff, U)
+        torch.cuda.synchronize()
+        w_eff += U
     # timed region: --steps iterations of every phase, as `nts` timesteps in step() order
     # (K iterations per phase, phases in order, median of 5 timesteps); no loss
     # reads inside (sync_every = 1e9) and no host sync at the timestep boundaries either: the
@@ -651,6 +661,7 @@ def main():
                    "points_per_phase_iter": n_all, "phases": nph, "global_batch": n_all,
                    "seq_len": None, "parallelism": f"dp{world}", "graph": not args.no_graph,
                    "precision": args.precision, "api": args.api, "sync_every": cfg.insr_sync_every,
+                   "graph_unroll": 1 if args.no_graph else max(1, args.graph_unroll),
                    "jet_precision": jet_precision_names(args.precision),
                    "bwd_policy": args.bwd_policy, "shard_of": args.shard_of,
                    "bwd_f16": bwd_f16,

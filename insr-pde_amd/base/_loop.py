@@ -14,6 +14,12 @@ Differences, all controlled by cfg attributes:
       Under data parallelism the iteration is two graphs -- [phase + backward]
       and [Adam + plateau] -- with the single RCCL all-reduce of gradients and
       losses issued eagerly between them (no collective inside a capture).
+  insr_graph_unroll (int, default 1) -- single process only: U > 1 also captures U
+      consecutive iterations into ONE graph and replays that for every group of U
+      iterations that holds no host read (sync / vis point) before its last one.  Each
+      iteration inside is a full one (its own sampler draw, backward, Adam + plateau
+      step); what it saves is the per-replay launch gap between graphs (~8.5 us on
+      MI355X, ROCm 7.2: profiles/r04/graph_unroll).
 """
 import torch
 
@@ -39,12 +45,16 @@ class PhaseLoop:
         self.graph = self.graph2 = None
         self.static = None
         self.static_main = None
+        self.unroll = max(1, int(getattr(cfg, "insr_graph_unroll", 1)))
+        self.graphU = None
+        self.staticU = None
 
     def start(self):
         """Fresh optimiser + scheduler for this phase (base/baseModel.py:106)."""
         self.m._reset_optimizer()
         self.opt, self.sched = self.m.optimizer, self.m.scheduler
         self.graph, self.graph2, self.static = None, None, None
+        self.graphU, self.staticU = None, None
 
     def _body(self):
         self.m.optimizer, self.m.scheduler = self.opt, self.sched
@@ -111,6 +121,49 @@ class PhaseLoop:
         self.static = {k: v.detach() for k, v in out.items()}
         return self.static
 
+    def _bodies(self):
+        out = None
+        for _ in range(self.unroll):
+            out = self._body()
+        return out
+
+    def can_group(self):
+        """Whether run_group() may serve the next `unroll` iterations (graph mode, one process,
+        the single-iteration graph already captured: iterations 0 and 1 ran)."""
+        return (self.unroll > 1 and self.use_graph and self.graph is not None and self.graph2 is None
+                and self.m._dp_world() == 1)
+
+    def run_group(self):
+        """`unroll` consecutive iterations as ONE graph replay (captured -- and so executed -- on
+        first use); returns the device loss dict of the group's last iteration."""
+        if self.graphU is None:
+            try:
+                self.graphU, out = self._capture_graph(self._bodies)
+            except Exception as e:  # not capturable as a group: iterate singly from now on
+                torch.cuda.synchronize(self.m.device)
+                self.unroll = 1
+                self.capture_error = repr(e)
+                self.graphU = None
+                return None
+            self.staticU = {k: v.detach() for k, v in out.items()}
+            return self.staticU
+        self.graphU.replay()
+        return self.staticU
+
+    def run_iters(self, i0, k):
+        """Iterations i0 .. i0 + k - 1 (no host reads in between): groups of `unroll` as one
+        replay where possible, the rest one by one.  Returns the last iteration's loss dict."""
+        out, i = None, i0
+        while i < i0 + k:
+            if i0 + k - i >= self.unroll and i >= 2 and self.can_group():
+                out = self.run_group()
+                if out is not None:
+                    i += self.unroll
+                    continue
+            out = self.step(i)
+            i += 1
+        return out
+
     def step(self, i):
         """Run iteration i; returns the device loss dict of that iteration."""
         dp = self.m._dp_world() > 1
@@ -133,9 +186,29 @@ class PhaseLoop:
         pbar = tqdm(range(m.max_n_iters), desc=f"{self.tag}[{m.timestep}]", disable=not self.show) \
             if tqdm is not None else range(m.max_n_iters)
         min_loss, accum = float("inf"), 0
+        U = self.unroll
+        skip = 0
         for i in pbar:
-            loss_dict = self.step(i)
-            m.train_step += 1
+            if skip:  # inside a group run_group() already executed
+                skip -= 1
+                m.train_step += 1
+                if skip:
+                    continue
+                # the group's last iteration: loss_dict is its losses -- read below as usual
+            else:
+                def host_reads(q):
+                    return (q + 1) % self.sync_every == 0 or q == m.max_n_iters - 1 or q == 0 or \
+                        (q + 1) % self.vis_every == 0
+                grouped = None
+                if (U > 1 and i >= 2 and i + U <= m.max_n_iters and self.can_group()
+                        and not any(host_reads(q) for q in range(i, i + U - 1))):
+                    grouped = self.run_group()
+                if grouped is not None:
+                    loss_dict, skip = grouped, U - 1
+                    m.train_step += 1
+                    continue
+                loss_dict = self.step(i)
+                m.train_step += 1
             last = (i == m.max_n_iters - 1)
             if (i + 1) % self.sync_every == 0 or last or i == 0:
                 vals = {k: float(v) for k, v in loss_dict.items()}

@@ -546,21 +546,30 @@ __global__ __launch_bounds__(512, 1) void jet_fb_x6(const FbJobs J, int din, int
             af[i].q[q] = live ? u32x4{wl[0], wl[1], wh[0], wh[1]} : u32x4{0u, 0u, 0u, 0u};
           }
         }
-#pragma unroll
-        for (int q4 = 0; q4 < 4; ++q4) {
-          const int ct = 4 * cb + q4;
-          FragQ<4> bf;  // B: h_{j-1} rows 16 ct + c at the chunk's 8 points -- transpose reads as A
+        // B: h_{j-1} rows 16 ct + c at the chunk's 8 points -- transpose reads as A; the next column
+        // tile's fragment is issued before this one's MFMAs (its LDS latency runs under them)
+        auto bfrag = [&](int q4) __attribute__((always_inline)) {
+          FragQ<4> bf;
 #pragma unroll
           for (int q = 0; q < 2; ++q) {
-            const unsigned short* pb = H + (live ? u : 0) * ZSET + (p0 + (c >> 2)) * LDB + 16 * ct + 4 * (c & 3);
+            const unsigned short* pb =
+                H + (live ? u : 0) * ZSET + (p0 + (c >> 2)) * LDB + 16 * (4 * cb + q4) + 4 * (c & 3);
             const v4s lo = ds_read_tr16(pb + q * ZPLANE);
             const v4s hi = ds_read_tr16(pb + q * ZPLANE + 4 * LDB);
             const u32x2 wl = __builtin_bit_cast(u32x2, lo), wh = __builtin_bit_cast(u32x2, hi);
             bf.q[q] = u32x4{wl[0], wl[1], wh[0], wh[1]};
           }
+          return bf;
+        };
+        FragQ<4> bf = bfrag(0);
+#pragma unroll
+        for (int q4 = 0; q4 < 4; ++q4) {
+          FragQ<4> bn;
+          if (q4 < 3) bn = bfrag(q4 + 1);
 #pragma unroll
           for (int i = 0; i < 2; ++i) dacc[j - 1][4 * i + q4] = mfma_q<4>(af[i], bf, dacc[j - 1][4 * i + q4]);
           X6_SCHED_FENCE();
+          if (q4 < 3) bf = bn;
         }
       }
       FB_STAMP(sp + 3);
@@ -568,15 +577,20 @@ __global__ __launch_bounds__(512, 1) void jet_fb_x6(const FbJobs J, int din, int
       floatx4 nh[S];
 #pragma unroll
       for (int s = 0; s < S; ++s) nh[s] = floatx4{0.f, 0.f, 0.f, 0.f};
+      // the next (K chunk, stream) B fragment is issued before this one's MFMAs
+      FragQ<4> pb = lds_frag<4, ZPLANE>(P + c * LDB + 8 * g);
 #pragma unroll
       for (int kc = 0; kc < KC; ++kc) {
         const FragQ<4> wt = wn;
         if (kc + 1 < KC) wn = wsp_frag<4, NT>(wsl, L, 1, j, rt, kc + 1, lane);
 #pragma unroll
         for (int s = 0; s < S; ++s) {
-          const FragQ<4> bf = lds_frag<4, ZPLANE>(P + s * ZSET + c * LDB + 32 * kc + 8 * g);
-          nh[s] = mfma_q<4>(wt, bf, nh[s]);
+          const int nk = s + 1 < S ? kc : kc + 1, ns = s + 1 < S ? s + 1 : 0;
+          FragQ<4> pn;
+          if (nk < KC) pn = lds_frag<4, ZPLANE>(P + ns * ZSET + c * LDB + 32 * nk + 8 * g);
+          nh[s] = mfma_q<4>(wt, pb, nh[s]);
           X6_SCHED_FENCE();
+          if (nk < KC) pb = pn;
         }
       }
       const float zun = ldexpf(1.f, -e) / kF16WScale;

@@ -25,7 +25,7 @@ BUNNY_FIXTURE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "
                              "bunny_mesh.npz")
 
 # insr-pde_amd execution knobs (see base/_loop.py)
-EXEC = dict(insr_precision=None, insr_sync_every=1, insr_graph=False, insr_progress=True,
+EXEC = dict(insr_precision=None, insr_sync_every=1, insr_graph=False, insr_graph_unroll=1, insr_progress=True,
             insr_fuse_forwards=os.environ.get("INSR_FUSE_FORWARDS", "1") != "0")
 
 

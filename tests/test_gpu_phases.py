@@ -342,3 +342,31 @@ def test_training_loop_graph_matches_eager(ph, fused):
                       float(model.optimizer.state[1]))
     assert res[True][2] == res[False][2] == 6.0
     assert nerr(res[True][0], res[False][0]) < 1e-6
+
+
+def test_training_loop_unrolled_graph_matches(ph):
+    """insr_graph_unroll = U: groups of U iterations replayed as ONE graph (between the loop's host
+    reads) -- the same kernels in the same order as one replay per iteration, on the product sampler
+    path (each iteration's device draw advances the Philox stream inside the graph): parameters, step
+    count and the device sampler position bit for bit equal to U = 1, and the losses the loop reads."""
+    from pde.fluid import Fluid2DModel
+    res = {}
+    for U in (1, 2, 4):
+        torch.manual_seed(0)
+        cfg = _cfg("fluid", num_hidden_layers=4, hidden_features=128, sample_resolution=32, max_n_iters=10,
+                   insr_graph=True, insr_sync_every=4, insr_graph_unroll=U)
+        model = Fluid2DModel(cfg)
+        set_flat(model.velocity_field, ph["fluid/vel/params0"])
+        set_flat(model.velocity_field_prev, ph["fluid/vel_prev/params0"])
+        set_flat(model.pressure_field, ph["fluid/pres/params0"])
+        model.timestep = 1
+        seen = []
+        model.tb = type("TB", (), {"add_scalars": lambda self, tag, vals, global_step: seen.append(
+            (global_step, vals["main"]))})()
+        model._solve_pressure()
+        assert getattr(model, "_insr_capture_error", None) is None
+        res[U] = (flat(model.pressure_field), float(model.optimizer.state[1]), seen)
+    for U in (2, 4):
+        assert res[U][1] == res[1][1] == 10.0
+        assert np.array_equal(res[U][0], res[1][0]), U
+        assert res[U][2] == res[1][2], U  # the same iterations read, the same losses
