@@ -19,7 +19,7 @@ Differences, all controlled by cfg attributes:
       iterations that holds no host read (sync / vis point) before its last one.  Each
       iteration inside is a full one (its own sampler draw, backward, Adam + plateau
       step); what it saves is the per-replay launch gap between graphs (~8.5 us on
-      MI355X, ROCm 7.2: profiles/r04/graph_unroll).
+      MI355X, ROCm 7.2).
 """
 import torch
 
@@ -134,8 +134,9 @@ class PhaseLoop:
                 and self.m._dp_world() == 1)
 
     def run_group(self):
-        """`unroll` consecutive iterations as ONE graph replay (captured -- and so executed -- on
-        first use); returns the device loss dict of the group's last iteration."""
+        """`unroll` consecutive iterations as ONE graph replay (captured on first use -- a capture
+        records, the replay that follows runs); returns the device loss dict of the group's last
+        iteration."""
         if self.graphU is None:
             try:
                 self.graphU, out = self._capture_graph(self._bodies)
@@ -146,7 +147,6 @@ class PhaseLoop:
                 self.graphU = None
                 return None
             self.staticU = {k: v.detach() for k, v in out.items()}
-            return self.staticU
         self.graphU.replay()
         return self.staticU
 
