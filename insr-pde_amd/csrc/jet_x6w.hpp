@@ -692,9 +692,11 @@ __global__ __launch_bounds__(256) void reduce_rows_kernel(const float* __restric
 // frag = 1: the partials are in matrix-core fragment order (jet_x6r.hpp: float4 q = (row tile x W / 16 +
 // column tile) x 64 + lane holds rows 16 rt + 4 (lane >> 4) + r of column 16 ct + (lane & 15)), so the
 // producer's stores are whole 1 KiB wave writes; the sums are scattered to row-major .grad here.
+// kstep / kslots: partial k of layer j sits at slot k kstep of the layer's kslots (pair sums: 2, nb)
 __global__ __launch_bounds__(512) void reduce_dw_kernel(const float* __restrict__ dpart, int KS, int din, int W,
                                                         float* __restrict__ grad, int accumulate, int grad16, int frag, int L,
-                                                        const float* __restrict__ rows, int rs, long Ps, int dout) {
+                                                        const float* __restrict__ rows, int rs, long Ps, int dout,
+                                                        int kstep, int kslots) {
   __shared__ floatx4 red[8][64];
   if ((int)blockIdx.y == L) {
     float* r = reinterpret_cast<float*>(&red[0][0]);
@@ -727,8 +729,8 @@ __global__ __launch_bounds__(512) void reduce_dw_kernel(const float* __restrict_
   const long q = (long)blockIdx.x * 64 + lane;  // column quad
   floatx4 acc = floatx4{0.f, 0.f, 0.f, 0.f};
   if (4 * q < WW) {
-    const floatx4* col = reinterpret_cast<const floatx4*>(dpart + (long)(j - 1) * KS * WW) + q;
-    const long rs = WW / 4;
+    const floatx4* col = reinterpret_cast<const floatx4*>(dpart + (long)(j - 1) * kslots * WW) + q;
+    const long rs = WW / 4 * kstep;
     int k = w;
     for (; k + 56 < KS; k += 64) {
       floatx4 v[8];
@@ -860,7 +862,7 @@ int wide_bwd_t(const float* x, int N, int din, int dout, int L, const float* prm
     const int grad16 = (((uintptr_t)(grad + hidden_off(din, W, 1))) & 15) == 0 ? 1 : 0;  // W % 4 == 0: all layers alike
     const int wq = (W * W / 4 + 63) / 64;
     hipLaunchKernelGGL(reduce_dw_kernel, dim3((unsigned)(wq > rows_x ? wq : rows_x), L + 1), dim3(512), 0, st, dpart,
-                       KS, din, W, grad, accumulate, grad16, 0, L, rows, rs, Ps, dout);
+                       KS, din, W, grad, accumulate, grad16, 0, L, rows, rs, Ps, dout, 1, KS);
     return (int)hipGetLastError();
   }
   hipLaunchKernelGGL(reduce_rows_kernel, dim3((unsigned)rows_x, rs), dim3(256), 0, st, small, tiles, Ps, rows);
