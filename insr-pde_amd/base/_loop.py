@@ -11,9 +11,11 @@ Differences, all controlled by cfg attributes:
       allocator settle); iteration 1 is captured into a hipGraph and every
       later iteration is one graph replay.  If capture fails (e.g. a phase
       with data-dependent shapes or host syncs) the loop stays eager.
-      Under data parallelism the iteration is two graphs -- [phase + backward]
-      and [Adam + plateau] -- with the single RCCL all-reduce of gradients and
-      losses issued eagerly between them (no collective inside a capture).
+      Under data parallelism the iteration is two graphs -- [phase + backward +
+      the gradients' and losses' arena pack] and [1/world + Adam + plateau, which
+      read the arena in place] -- with the single RCCL all-reduce of that arena
+      issued eagerly between them (no collective inside a capture; nothing else
+      eager).
   insr_graph_unroll (int, default 1) -- single process only: U > 1 also captures U
       consecutive iterations into ONE graph and replays that for every group of U
       iterations that holds no host read (sync / vis point) before its last one.  Each
@@ -63,7 +65,8 @@ class PhaseLoop:
         synced = self.m._update_network(loss_dict)
         return synced if isinstance(synced, dict) else loss_dict
 
-    # ---- data-parallel split: [phase + backward] graph | eager RCCL all-reduce | [Adam + plateau] graph
+    # ---- data-parallel split: [phase + backward + arena pack] graph | eager RCCL all-reduce |
+    # [1/world + Adam + plateau] graph -- the collective is the only eager launch of an iteration
     def _stage1(self):
         m = self.m
         m.optimizer, m.scheduler = self.opt, self.sched
@@ -71,20 +74,25 @@ class PhaseLoop:
             loss_dict = self.func(m, *self.args, **self.kwargs)
         m.optimizer.zero_grad()
         m._backward(loss_dict)
-        return loss_dict
+        packed = m._dp_pack(loss_dict)  # gradients + losses in the arena (views of its tail)
+        self.static_main = packed['main'].detach().reshape(1)
+        return packed
 
     def _stage2(self):
         m = self.m
-        m.optimizer.step()
-        if m.scheduler is not None:
-            m.scheduler.step(self.static_main)
+        m._dp_finish()
+        if m.scheduler is not None and getattr(m.scheduler, "fusable", False):
+            m.optimizer.step(plateau=(m.scheduler, self.static_main))  # Adam + plateau: one launch
+        else:
+            m.optimizer.step()
+            if m.scheduler is not None:
+                m.scheduler.step(self.static_main)
 
     def _dp_step_eager(self):
-        ld = self._stage1()
-        synced = self.m._dp_sync(ld)
-        self.static_main = synced['main'].detach().reshape(1).clone()
+        packed = self._stage1()
+        self.m._dp_allreduce()
         self._stage2()
-        return synced
+        return packed
 
     def _capture_graph(self, fn):
         from .losses import prepare_workspaces
@@ -173,10 +181,9 @@ class PhaseLoop:
             self.graph.replay()
             if self.graph2 is None:
                 return self.static
-            synced = self.m._dp_sync(self.static)  # one RCCL all-reduce, eager
-            self.static_main.copy_(synced['main'].detach().reshape(1))
+            self.m._dp_allreduce()  # one RCCL all-reduce, eager (the arena the graphs read in place)
             self.graph2.replay()
-            return synced
+            return self.static
         return self._dp_step_eager() if dp else self._body()
 
     def run(self):

@@ -139,11 +139,33 @@ class BaseModel(ABC):
         model's gradient arena -- every trainable network's flat .grad is a view into it (bound
         on the first call), followed by one slot per loss -- so there is no concatenation and
         no copy-back.  A network no gradient reached this iteration contributes zeros (one
-        memset) and stays untouched for Adam (torch skips params whose .grad is None)."""
+        memset) and stays untouched for Adam (torch skips params whose .grad is None).
+
+        Three pieces, so that the graph-replayed loop (base/_loop.py) issues only the collective
+        eagerly: _dp_pack (device ops: zero-fill + the losses into the arena tail; captured with
+        the phase and its backward), _dp_allreduce (the RCCL call), _dp_finish (the 1/world of a
+        mean reduction; captured with Adam + plateau, which read the arena in place)."""
+        if self._dp_world() == 1:
+            return loss_dict
+        synced = self._dp_pack(loss_dict)
+        self._dp_allreduce()
+        self._dp_finish()
+        return synced
+
+    def _dp_allreduce(self):
+        d = torch.distributed
+        d.all_reduce(self._insr_dp_red, op=d.ReduceOp.SUM)
+
+    def _dp_finish(self):
+        if self._dp_loss_reduction == 'mean':
+            self._insr_dp_red.div_(self._dp_world())
+
+    def _dp_pack(self, loss_dict):
+        """The iteration's gradients and losses as one contiguous arena slice (self._insr_dp_red);
+        returns the losses as views of its tail (the values after _dp_allreduce/_dp_finish)."""
         world = self._dp_world()
         if world == 1:
             return loss_dict
-        d = torch.distributed
         nets = list(self._trainable_networks.values())
         keys = list(loss_dict.keys())
         dev = nets[0].flat_params().device
@@ -170,10 +192,7 @@ class BaseModel(ABC):
             off += n
         tail = arena[total:total + len(keys)]
         torch.stack([torch.as_tensor(loss_dict[k], device=dev).detach().float().reshape(()) for k in keys], out=tail)
-        red = arena[:total + len(keys)]
-        d.all_reduce(red, op=d.ReduceOp.SUM)
-        if self._dp_loss_reduction == 'mean':
-            red.div_(world)
+        self._insr_dp_red = arena[:total + len(keys)]
         return {k: tail[i] for i, k in enumerate(keys)}
 
     def _update_network(self, loss_dict):

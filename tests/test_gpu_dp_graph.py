@@ -1,7 +1,7 @@
 """The data-parallel path `bench.py --gpus N` takes, executed on the GPU: PhaseLoop with
-insr_graph=True at world 2 replays TWO hipGraphs per iteration -- [phase + backward] and
-[Adam + plateau] -- with the one eager all-reduce of BaseModel._dp_sync between them
-(base/_loop.py PhaseLoop.step).  Both ranks run on cuda:0 over gloo (a functional rehearsal:
+insr_graph=True at world 2 replays TWO hipGraphs per iteration -- [phase + backward + arena
+pack] and [1/world + Adam + plateau] -- with the one eager all-reduce of the arena between them
+(BaseModel._dp_pack / _dp_allreduce / _dp_finish, base/_loop.py PhaseLoop.step).  Both ranks run on cuda:0 over gloo (a functional rehearsal:
 RCCL needs one GPU per rank); each takes half of the reference golden sample set.
 
 Checks, 4 iterations of each fluid phase (_advect_velocity, _solve_pressure, _projection):
