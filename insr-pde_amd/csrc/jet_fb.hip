@@ -1,9 +1,5 @@
 // jet_fb.hip -- the recompute backward (jet_fb.hpp): W = 128, 4 hidden layers (the fluid nets:
 // velocity 2 -> 2, pressure 2 -> 1), products f16x3 (fp32-level) with per-tile power-of-two scales.
-#include <map>
-#include <mutex>
-#include <utility>
-
 #include "jet_fb.hpp"
 
 namespace insr {
@@ -15,50 +11,18 @@ bool fb_supported(int S, bool LAP, int L) {
   return (S == 4 && LAP) || (S == 3 && !LAP) || (S == 1 && !LAP);
 }
 
-// The pair tickets of jet_fb_x6's partial hand-off, per (device, stream): allocated and zeroed once,
-// outside any capture (INSR_ECAPTURE otherwise, as the weight-plane scratch); every complete launch adds
-// exactly 2 per pair it uses, so the parity of a ticket is 0 between launches.  Calls on different
-// streams use different tickets (re-entrant); calls on one stream are ordered by the stream.
-namespace {
-std::mutex g_tick_mu;
-std::map<std::pair<int, hipStream_t>, unsigned*> g_tick;
-constexpr int kFbTickets = 512;  // >= CUs / 2 pairs
-}  // namespace
-static unsigned* fb_tickets(hipStream_t st, int* rc) {
-  int dev = 0;
-  (void)hipGetDevice(&dev);
-  std::lock_guard<std::mutex> lk(g_tick_mu);
-  unsigned*& p = g_tick[std::make_pair(dev, st)];
-  if (!p) {
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    (void)hipStreamIsCapturing(st, &cs);
-    if (cs != hipStreamCaptureStatusNone) {
-      *rc = INSR_ECAPTURE;
-      return nullptr;
-    }
-    void* q = nullptr;
-    if ((*rc = (int)hipMalloc(&q, kFbTickets * sizeof(unsigned)))) return nullptr;
-    if ((*rc = (int)hipMemset(q, 0, kFbTickets * sizeof(unsigned)))) return nullptr;
-    p = static_cast<unsigned*>(q);
-  }
-  return p;
-}
-
 // saved = 0: the recompute backward (reruns the forward per tile); 1: the same reverse sweep on the
 // forward's saved streams (J.act) -- dW resident per CU, f16x3 products, no z̄ round trip
 int dispatch_fb_bwd(int S, bool LAP, int L, const FbJobs& J, int din, int dout, const float* prm, float* work,
                     float* grad, int accumulate, int saved, hipStream_t st) {
   if (!fb_supported(S, LAP, L)) return INSR_EINVAL;
-  int rc = 0;
-  unsigned* tk = fb_tickets(st, &rc);
-  if (!tk) return rc;
   switch ((S * 2 + (LAP ? 1 : 0)) * 2 + (saved ? 1 : 0)) {
-    case 18: return fb_bwd_t<4, true, 4, 2, false>(J, din, dout, prm, work, grad, accumulate, tk, st);
-    case 12: return fb_bwd_t<3, false, 4, 2, false>(J, din, dout, prm, work, grad, accumulate, tk, st);
-    case 4: return fb_bwd_t<1, false, 4, 4, false>(J, din, dout, prm, work, grad, accumulate, tk, st);
-    case 19: return fb_bwd_t<4, true, 4, 1, true>(J, din, dout, prm, work, grad, accumulate, tk, st);
-    case 13: return fb_bwd_t<3, false, 4, 1, true>(J, din, dout, prm, work, grad, accumulate, tk, st);
-    case 5: return fb_bwd_t<1, false, 4, 1, true>(J, din, dout, prm, work, grad, accumulate, tk, st);
+    case 18: return fb_bwd_t<4, true, 4, 2, false>(J, din, dout, prm, work, grad, accumulate, st);
+    case 12: return fb_bwd_t<3, false, 4, 2, false>(J, din, dout, prm, work, grad, accumulate, st);
+    case 4: return fb_bwd_t<1, false, 4, 4, false>(J, din, dout, prm, work, grad, accumulate, st);
+    case 19: return fb_bwd_t<4, true, 4, 1, true>(J, din, dout, prm, work, grad, accumulate, st);
+    case 13: return fb_bwd_t<3, false, 4, 1, true>(J, din, dout, prm, work, grad, accumulate, st);
+    case 5: return fb_bwd_t<1, false, 4, 1, true>(J, din, dout, prm, work, grad, accumulate, st);
     default: return INSR_EINVAL;
   }
 }

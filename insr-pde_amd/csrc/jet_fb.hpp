@@ -157,7 +157,7 @@ __device__ __forceinline__ void fb_h_bounds(const floatx4 (&z)[S], float& mt, fl
 template <int S, bool LAP, int L, int ZR, bool SAVED>
 __global__ __launch_bounds__(512, 1) void jet_fb_x6(const FbJobs J, int din, int dout, const float* __restrict__ prm,
                                                     float* __restrict__ dpart, float* __restrict__ small, long Ps,
-                                                    int nb, int tiles, unsigned* __restrict__ tickets) {
+                                                    int nb, int tiles) {
   constexpr int NT = 8, W = 128, KC = 4;
   using BG = X6BwdGeo<4, NT>;
   using GG = FbGeo<S, L, ZR, SAVED>;
@@ -631,56 +631,16 @@ __global__ __launch_bounds__(512, 1) void jet_fb_x6(const FbJobs J, int din, int
 
   // ---- the block's partials: dW of every hidden layer in fragment order (one 1 KiB wave store per
   // accumulator, the accumulator's power of two undone; reduce_dw_kernel frag = 1 scatters the
-  // sums), then the compact row.  Blocks pair up (2p, 2p + 1): both store their partial write-through
-  // (sc1) into their own slot, then take the pair's ticket; the one that arrives second adds its
-  // buddy's partial (sc1 loads) to its own, still in registers, lower block index first (fp32 addition
-  // is commutative: the same bits whoever arrives last), into slot 2p -- the sums read nb / 2 slots.
-  // Hand-off: MI355X_MICROARCH.md row 1 (sc1 stores, every wave's vmcnt(0), one lane's agent atomic
-  // after a workgroup barrier; the last adder's waves load after a barrier); one block per CU.  The
-  // tickets persist per stream and only ever grow by 2 per pair and launch (a lone last block takes
-  // none), so "arrived second" is the parity of the returned count. ----
+  // sums), then the compact row ----
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, ra = wave >> 1, cb = wave & 1;
-  const int buddy = blockIdx.x ^ 1;
-  const bool paired = buddy < nb;
 #pragma unroll
   for (int jl = 0; jl < L; ++jl) {
     floatx4* out = reinterpret_cast<floatx4*>(dpart + ((long)jl * nb + blockIdx.x) * W * W);
     const float f = E[jl] == kNoE ? 1.f : ldexpf(1.f, -E[jl]);
 #pragma unroll
-    for (int q = 0; q < NT; ++q) {
-      dacc[jl][q] *= f;
-      floatx4* a = out + ((2 * ra + q / 4) * NT + 4 * cb + q % 4) * 64 + lane;
-      if (paired)
-        asm volatile("global_store_dwordx4 %0, %1, off sc1" : : "v"(a), "v"(dacc[jl][q]) : "memory");
-      else
-        *a = dacc[jl][q];
-    }
+    for (int q = 0; q < NT; ++q) out[((2 * ra + q / 4) * NT + 4 * cb + q % 4) * 64 + lane] = dacc[jl][q] * f;
   }
-  __shared__ int fb_last;
-  if (paired) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) fb_last = (int)(atomicAdd(tickets + (blockIdx.x >> 1), 1u) & 1u);
-  }
-  __syncthreads();  // + every owner lane's last compact update
-  if (paired && fb_last) {
-#pragma unroll
-    for (int jl = 0; jl < L; ++jl) {
-      const floatx4* in = reinterpret_cast<const floatx4*>(dpart + ((long)jl * nb + buddy) * W * W);
-      floatx4* out = reinterpret_cast<floatx4*>(dpart + ((long)jl * nb + (blockIdx.x & ~1)) * W * W);
-      floatx4 v[NT];
-#pragma unroll
-      for (int q = 0; q < NT; ++q) {
-        const floatx4* b = in + ((2 * ra + q / 4) * NT + 4 * cb + q % 4) * 64 + lane;
-        asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(v[q]) : "v"(b) : "memory");
-      }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll
-      for (int q = 0; q < NT; ++q)
-        out[((2 * ra + q / 4) * NT + 4 * cb + q % 4) * 64 + lane] =
-            (blockIdx.x & 1) ? v[q] + dacc[jl][q] : dacc[jl][q] + v[q];
-    }
-  }
+  __syncthreads();  // every owner lane's last compact update
   for (int i = threadIdx.x; i < Ps; i += 512) small[(long)blockIdx.x * Ps + i] = sacc0[i];
 }
 
@@ -700,7 +660,7 @@ inline long fb_work_floats_impl(long tiles, int din, int dout, int L) {
 
 template <int S, bool LAP, int L, int ZR, bool SAVED>
 int fb_bwd_t(const FbJobs& J, int din, int dout, const float* prm, float* work, float* grad, int accumulate,
-             unsigned* tickets, hipStream_t st) {
+             hipStream_t st) {
   constexpr int W = 128;
   const int tiles = J.tstart[J.njobs];
   if (tiles <= 0) return 0;
@@ -715,13 +675,12 @@ int fb_bwd_t(const FbJobs& J, int din, int dout, const float* prm, float* work, 
                               (int)lds), true);  // once per instantiation (thread-safe static init)
   (void)attr;
   hipLaunchKernelGGL((jet_fb_x6<S, LAP, L, ZR, SAVED>), dim3(nb), dim3(512), lds, st, J, din, dout, prm, dpart, small, Ps, nb,
-                     tiles, tickets);
+                     tiles);
   const int grad16 = (((uintptr_t)(grad + hidden_off(din, W, 1))) & 15) == 0 ? 1 : 0;
   const int wq = (W * W / 4 + 63) / 64;
   const int rows_x = (int)((Ps + 63) / 64);
-  // the pair sums sit in the even slots (a lone last block's own partial too): (nb + 1) / 2 of them
-  hipLaunchKernelGGL(reduce_dw_kernel, dim3((unsigned)(wq > rows_x ? wq : rows_x), L + 1), dim3(512), 0, st, dpart,
-                     (nb + 1) / 2, din, W, grad, accumulate, grad16, 1, L, small, nb, Ps, dout, 2, nb);
+  hipLaunchKernelGGL(reduce_dw_kernel, dim3((unsigned)(wq > rows_x ? wq : rows_x), L + 1), dim3(512), 0, st, dpart, nb,
+                     din, W, grad, accumulate, grad16, 1, L, small, nb, Ps, dout, 1, nb);
   return (int)hipGetLastError();
 }
 
