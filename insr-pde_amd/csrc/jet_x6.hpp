@@ -517,14 +517,18 @@ __device__ __forceinline__ void fwd_x6_block(const float* __restrict__ x, int N,
 }
 
 // register cap of the single-network forward: 4 waves / SIMD (two 512-thread blocks per CU)
-// where the body fits 128 VGPRs without spilling (unconstrained, T = 2 takes ~200)
-template <int NT, int S, int T>
-constexpr int x6_fwd_min_waves() {
-  return (NT == 8 && (S == 1 || (S == 3 && T <= 2))) ? 4 : 1;  // capped vs uncapped: kbench r2s21
+// where the body fits 128 VGPRs without spilling (unconstrained, T = 2 takes ~200).  W = 256
+// 4-stream gradient jets (elasticity3Dbunny's 3-d gradient): 125 VGPRs in round 3, 131 after the
+// f16x3 tangent-stream guard -- one block per CU instead of two, the forward 2.39 -> 3.59 ms per step
+template <int NQ, int NT, int S, bool LAP, int T>
+constexpr int x6_fwd_min_waves() {  // (the bf16x6 variant of the W = 256 case would spill 14 VGPRs)
+  return ((NT == 8 && (S == 1 || (S == 3 && T <= 2))) || (NQ == 4 && NT == 16 && S == 4 && !LAP && T == 1))
+             ? 4
+             : 1;  // capped vs uncapped: kbench r2s21
 }
 
 template <int NQ, int NT, int S, bool LAP, int T>
-__global__ __launch_bounds__(X6Geo<NT>::THREADS, (x6_fwd_min_waves<NT, S, T>())) void jet_fwd_x6(
+__global__ __launch_bounds__(X6Geo<NT>::THREADS, (x6_fwd_min_waves<NQ, NT, S, LAP, T>())) void jet_fwd_x6(
     const float* __restrict__ x, int N, int din, int dout, int L, const float* __restrict__ prm,
     float* __restrict__ y, float* __restrict__ dy, float* __restrict__ lap, float* __restrict__ act, int nbal) {
   int tile0, cnt;
@@ -553,13 +557,13 @@ struct FwdJobsX6 {
 // value and 2-d gradient jets at W = 128: hold the kernel to 128 VGPRs (4 waves per SIMD = two
 // 8-wave blocks per CU), which the value TA = 4 body meets on its own (116), the gradient
 // TA = 2 and the 1-tile bodies are scheduled into without spills
-template <int NT, int S>
-constexpr int x6_multi_min_waves() {
-  return (NT == 8 && (S == 1 || S == 3)) ? 4 : 1;
+template <int NQ, int NT, int S, bool LAP, int TA>
+constexpr int x6_multi_min_waves() {  // + the W = 256 4-stream gradient case of x6_fwd_min_waves
+  return ((NT == 8 && (S == 1 || S == 3)) || (NQ == 4 && NT == 16 && S == 4 && !LAP && TA == 1)) ? 4 : 1;
 }
 
 template <int NQ, int NT, int S, bool LAP, int TA, int TB>
-__global__ __launch_bounds__(X6Geo<NT>::THREADS, (x6_multi_min_waves<NT, S>())) void jet_fwd_x6_multi(
+__global__ __launch_bounds__(X6Geo<NT>::THREADS, (x6_multi_min_waves<NQ, NT, S, LAP, TA>())) void jet_fwd_x6_multi(
     const FwdJobsX6 jobs, int din, int dout, int L) {
   const int b = blockIdx.x;
   int k = 0;
