@@ -645,6 +645,9 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed, ts_ms = float(t[0]), [float(v) for v in t[1:]]
     log(f"timed {args.steps} steps ({nts} timesteps): {elapsed * 1e3:.2f} ms")
+    for pl in loops:  # which replay form each phase loop ended up with
+        log(f"  {pl.tag}: graph {pl.graph is not None}, unroll {pl.unroll}, group graph {pl.graphU is not None}"
+            + (f", capture error {pl.capture_error}" if getattr(pl, "capture_error", None) else ""))
     # points all ranks processed: strong = the global batch, weak = world x the per-rank batch
     n_all = interior_points(cfg, wl) if (args.scaling == "strong" and args.shard_of == 1) else n_local * world
     total_points = n_all * nph * args.steps
