@@ -359,7 +359,8 @@ int insr_reduce_partials_strided(const float* partial, int n_blocks, long count,
 #define INSR_OPT_FACTOR 6
 #define INSR_OPT_MINLR 7
 #define INSR_OPT_TICKET 8 /* (as unsigned) insr_adam_plateau_step_nets' last-block ticket, 0 */
-#define INSR_OPT_NFLOATS 9
+#define INSR_OPT_TICKET_SHARDS 9 /* [9, 17): its 8 first-level shards (as unsigned), 0 */
+#define INSR_OPT_NFLOATS 17
 
 /* t += 1; refresh step_size and sqrt(1-b2^t) (explicit-prepare convention). */
 int insr_adam_prepare(float* opt_state, float beta1, float beta2, void* stream);
@@ -381,9 +382,11 @@ int insr_adam_step_nets(int count, float* const* params, const float* const* gra
                         float* const* exp_avg_sq, const long* sizes, const int* shapes, const float* opt_state,
                         float beta1, float beta2, float eps, int step_offset, void* stream);
 /* insr_adam_step_nets (step_offset 1) followed by insr_plateau_step(opt_state, loss, patience,
- * advance_step = 1) in the SAME launch: the last block to finish (agent-scope ticket in
- * opt_state[INSR_OPT_TICKET], reset by it) runs the scheduler step after every block has read
- * the lr it updates.  base/baseModel.py:79-81 (optimizer.step(); scheduler.step(loss)). */
+ * advance_step = 1) in the SAME launch: the last block to finish runs the scheduler step after
+ * every block has read the lr it updates -- a two-level agent-scope ticket (block b adds to shard
+ * b % 8, the last adder of a shard to opt_state[INSR_OPT_TICKET]; the last of those resets all
+ * nine words), so no word takes more than ~1/8 of the blocks' atomics.
+ * base/baseModel.py:79-81 (optimizer.step(); scheduler.step(loss)). */
 int insr_adam_plateau_step_nets(int count, float* const* params, const float* const* grads, float* const* exp_avg,
                                 float* const* exp_avg_sq, const long* sizes, const int* shapes, float* opt_state,
                                 float beta1, float beta2, float eps, const float* loss, int patience, void* stream);

@@ -20,8 +20,10 @@ Differences, all controlled by cfg attributes:
       consecutive iterations into ONE graph and replays that for every group of U
       iterations that holds no host read (sync / vis point) before its last one.  Each
       iteration inside is a full one (its own sampler draw, backward, Adam + plateau
-      step); what it saves is the per-replay launch gap between graphs (~8.5 us on
-      MI355X, ROCm 7.2).
+      step); what it saves is the host's replay call per iteration (under a kernel
+      trace, whose per-launch host work makes the host the bottleneck, ~8.7 us of idle
+      device between two replays; without a profiler the host stays ahead and U = 1 and
+      U = 4 measure the same, profiles/r04/final_v1/unroll_ab_*).
 """
 import torch
 

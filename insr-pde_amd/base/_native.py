@@ -125,7 +125,8 @@ def knobs(**kw):
 LOSS_COMBO, LOSS_BANDS = 0, 1
 OPT_LR, OPT_STEP, OPT_BEST, OPT_BAD, OPT_STEPSIZE, OPT_BC2SQRT, OPT_FACTOR, OPT_MINLR = range(8)
 OPT_TICKET = 8  # the fused Adam + plateau launch's last-block ticket (0 between launches)
-OPT_NFLOATS = 9
+OPT_TICKET_SHARDS = 9  # [9, 17): its first-level shards (0 between launches)
+OPT_NFLOATS = 17
 ADAM_MAX_TENSORS = 8
 
 _P = ctypes.c_void_p

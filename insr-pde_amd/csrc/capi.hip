@@ -530,13 +530,31 @@ __device__ __forceinline__ void adam_wsplit(float* base, const int (&sh)[4], lon
 // so the bias corrections need no separate prepare launch); torch's op order:
 //   m.lerp_(g, 1-b1); v.mul_(b2).addcmul_(g, g, 1-b2);
 //   p.addcdiv_(m, sqrt(v)/sqrt(1-b2^t) + eps, -lr/(1-b1^t))
+// b^n in double by repeated squaring: t is integer-valued, and the bias corrections need ~1e-15
+// relative, not libm's pow (whose double-precision log / exp chain sat at the head of every block)
+__device__ __forceinline__ void powi2_d(double b1, double b2, unsigned n, double& p1, double& p2) {
+  p1 = 1.0;
+  p2 = 1.0;
+  while (n) {
+    if (n & 1u) {
+      p1 *= b1;
+      p2 *= b2;
+    }
+    b1 *= b1;
+    b2 *= b2;
+    n >>= 1;
+  }
+}
+
 __global__ void adam_multi_kernel(AdamList L, float* __restrict__ st, float b1, float b2, float eps,
                                   int step_offset) {
   __shared__ float sc[2];
   if (threadIdx.x == 0) {
     const double t = (double)st[INSR_OPT_STEP] + (double)step_offset;
-    sc[0] = (float)((double)st[INSR_OPT_LR] / (1.0 - pow((double)b1, t)));
-    sc[1] = (float)sqrt(1.0 - pow((double)b2, t));
+    double p1, p2;
+    powi2_d((double)b1, (double)b2, (unsigned)t, p1, p2);
+    sc[0] = (float)((double)st[INSR_OPT_LR] / (1.0 - p1));
+    sc[1] = (float)sqrt(1.0 - p2);
   }
   __syncthreads();
   const float step_size = sc[0], bc2s = sc[1];
@@ -562,12 +580,19 @@ __global__ void adam_multi_kernel(AdamList L, float* __restrict__ st, float b1, 
     // (relaxed ticket, no release/acquire: the last block only reads the loss -- written by an
     // earlier launch -- and st, which no other block writes; the plain loads of lr / t above
     // completed before each block's barrier)
+    // Two levels: block b adds to shard b % 8; the last adder of a shard (it knows the shard's block
+    // count) adds to the top word; the last of those runs the plateau step and zeroes all nine
+    // words -- every block has added by then.  One word would serialise all the blocks' atomics.
     __syncthreads();
     if (threadIdx.x == 0) {
-      unsigned* ticket = reinterpret_cast<unsigned*>(st + INSR_OPT_TICKET);
-      if (atomicAdd(ticket, 1u) == gridDim.x - 1) {
+      unsigned* top = reinterpret_cast<unsigned*>(st + INSR_OPT_TICKET);
+      unsigned* shard = reinterpret_cast<unsigned*>(st + INSR_OPT_TICKET_SHARDS);
+      const unsigned nb = gridDim.x, s = blockIdx.x & 7u;
+      const unsigned in_shard = (nb - s + 7u) / 8u, shards = nb < 8u ? nb : 8u;
+      if (atomicAdd(shard + s, 1u) == in_shard - 1u && atomicAdd(top, 1u) == shards - 1u) {
         plateau_update(st, L.loss, L.patience, 1);
-        atomicExch(ticket, 0u);
+        for (int q = 0; q < 8; ++q) atomicExch(shard + q, 0u);
+        atomicExch(top, 0u);
       }
     }
   }

@@ -703,8 +703,17 @@ __global__ __launch_bounds__(512) void reduce_dw_kernel(const float* __restrict_
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const long i = (long)blockIdx.x * 64 + lane;
     float acc = 0.f;
-    if (i < Ps)
-      for (int b = w; b < rs; b += 8) acc += rows[(long)b * Ps + i];
+    if (i < Ps) {  // 8 rows in flight per thread, as the W x W planes (a fixed order all the same)
+      int b = w;
+      for (; b + 56 < rs; b += 64) {
+        float v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = rows[(long)(b + 8 * u) * Ps + i];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) acc += v[u];
+      }
+      for (; b < rs; b += 8) acc += rows[(long)b * Ps + i];
+    }
     r[w * 64 + lane] = acc;
     __syncthreads();
     if (w == 0 && i < Ps) {

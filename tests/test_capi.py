@@ -27,6 +27,18 @@ def test_header_matches_binding():
     assert declared_symbols() == sorted(nat.SIGNATURES)
 
 
+def test_header_constants_match_binding():
+    """The optimiser-state layout and mode-bit constants the Python side allocates / passes are the
+    header's (#define NAME value, integers only)."""
+    import re
+    from base import _native as nat
+    text = open(HEADER).read()
+    defs = dict(re.findall(r"#define (INSR_OPT_\w+) (\d+)\b", text))
+    for name, value in defs.items():
+        assert getattr(nat, name[len("INSR_"):]) == int(value), name
+    assert "INSR_OPT_NFLOATS" in defs and "INSR_OPT_TICKET_SHARDS" in defs
+
+
 def test_exports_every_declared_symbol(lib):
     import ctypes
     for name in declared_symbols():

@@ -112,13 +112,15 @@ def test_phase_loop_early_stop(B, graph):
     assert m.optimizer.param_groups[0]["lr"] <= 1.1e-8
 
 
-def test_fused_adam_plateau_equals_two_launches(B):
+@pytest.mark.parametrize("shape", [(2, 2, 2, 64), (1, 1, 1, 32)])  # 34 blocks; 5 (< 8 ticket shards)
+def test_fused_adam_plateau_equals_two_launches(B, shape):
     """Parameters, moments and optimiser state after 12 fused Adam + plateau launches equal the
-    separate insr_adam_step_nets + insr_plateau_step launches bit for bit."""
+    separate insr_adam_step_nets + insr_plateau_step launches bit for bit; the two-level ticket's
+    nine words are back at zero."""
     out = []
     for fused in (False, True):
         torch.manual_seed(1)
-        net = B.MLP(2, 2, 2, 64, nonlinearity="sine").cuda()
+        net = B.MLP(shape[0], shape[1], shape[2], shape[3], nonlinearity="sine").cuda()
         opt = B.FusedAdam([{"params": list(net.parameters()), "lr": 1e-3, "module": net}])
         sched = B.DevicePlateau(opt, factor=0.5, patience=2, min_lr=1e-6)
         g = torch.Generator(device="cuda").manual_seed(2)
@@ -132,7 +134,8 @@ def test_fused_adam_plateau_equals_two_launches(B):
                 sched.step(loss)
         torch.cuda.synchronize()
         out.append((net.flat_params().clone(), opt._nets[0][1].clone(), opt._nets[0][2].clone(),
-                    opt.state[:B._native.OPT_TICKET].clone(), int(opt.state[B._native.OPT_TICKET].view(torch.int32))))
+                    opt.state[:B._native.OPT_TICKET].clone(),
+                    opt.state[B._native.OPT_TICKET:B._native.OPT_NFLOATS].view(torch.int32).abs().sum().item()))
     for u, v in zip(out[0][:4], out[1][:4]):
         assert torch.equal(u, v)
-    assert out[1][4] == 0  # the ticket is left at zero
+    assert out[1][4] == 0  # the ticket words are left at zero
