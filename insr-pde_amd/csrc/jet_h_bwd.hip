@@ -6,3 +6,12 @@ namespace insr {
 template int dispatch_bwd_q<4>(int, int, bool, int, const BwdJobsX6*, int, int, int, const float*, float*, long,
                                hipStream_t);
 }  // namespace insr
+
+#ifdef INSR_STAMPS
+// diagnostic build only (make diag): the f16x3 fused backward's phase stamps (this translation unit's copy)
+extern "C" int insr_diag_stamps_h(unsigned long long* host, int n) {
+  if (n > insr::kStampSlots) n = insr::kStampSlots;
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(insr::g_insr_stamps), n * sizeof(unsigned long long), 0,
+                                  hipMemcpyDeviceToHost);
+}
+#endif

@@ -28,15 +28,21 @@ def main():
     ap.add_argument("--mode", default="lap")
     ap.add_argument("--n", type=int, default=16384)
     ap.add_argument("--prec", type=int, default=0, help="1: split-bf16 (x6) kernels")
+    ap.add_argument("--fprec", type=int, default=None, help="INSR_PREC_* of the forward (with --bprec)")
+    ap.add_argument("--bprec", type=int, default=None, help="INSR_PREC_* of the backward; with the default "
+                    "f16 mask a bf16x6 backward runs the fused kernel on fp16 products (f16x3)")
     args = ap.parse_args()
     import base
     from base import _native as nat
     lib = nat.load(os.path.join(ROOT, "insr-pde_amd", "lib", "libinsr_hip_diag.so"))
     lib.insr_diag_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
     lib.insr_diag_stamps_x6.argtypes = [ctypes.c_void_p, ctypes.c_int]
-    ph = PH_X6 if args.prec else PH
+    lib.insr_diag_stamps_h.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    f16 = args.bprec is not None
+    prec = (args.fprec, args.bprec) if f16 else (args.prec, args.prec)
+    ph = PH_X6 if (args.prec or f16) else PH
     din, dout, L, W = NETS[args.net]
-    mode = {"value": 0, "grad": 1, "lap": 2}[args.mode] | nat.knob_bits(prec=(args.prec, args.prec))
+    mode = {"value": 0, "grad": 1, "lap": 2}[args.mode] | nat.knob_bits(prec=prec)
     n = args.n
     torch.manual_seed(0)
     net = base.MLP(din, dout, L, W, nonlinearity="sine").cuda()
@@ -55,9 +61,9 @@ def main():
                                          nat.ptr(gy), nat.ptr(gdy), nat.ptr(glap), nat.ptr(part), st), "bwd")
     torch.cuda.synchronize()
     buf = (ctypes.c_ulonglong * (2 * 16 * 8 * 8))()
-    (lib.insr_diag_stamps_x6 if args.prec else lib.insr_diag_stamps)(buf, len(buf))
+    (lib.insr_diag_stamps_h if f16 else lib.insr_diag_stamps_x6 if args.prec else lib.insr_diag_stamps)(buf, len(buf))
     T = lib.insr_jet_split_tiles(n, din, W, mode, 1)
-    print(f"{args.net} {args.mode} n={n} T={T} prec={args.prec}")
+    print(f"{args.net} {args.mode} n={n} T={T} prec={prec}")
     for blk in (0, 1):
         rows = []
         for wave in range(8):
