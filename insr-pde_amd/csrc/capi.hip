@@ -350,7 +350,7 @@ __global__ __launch_bounds__(64 * kRedWaves) void reduce_partials_kernel(const f
 // Partial rows padded to a multiple of 4 floats (insr_jet_partial_stride): 16-B aligned
 // rows, so the reduction streams them with 16-B loads (1 KiB per wave-instruction) and
 // 8 rows in flight per thread.  Fixed summation order as reduce_partials_kernel.
-constexpr int kRed4Waves = 8, kRed4Unroll = 8;
+constexpr int kRed4Waves = 8, kRed4Unroll = 16;  // rows in flight per thread (predicated tail)
 __global__ __launch_bounds__(64 * kRed4Waves) void reduce_partials4_kernel(const float* __restrict__ part, int nb,
                                                                             long count, long stride,
                                                                             float* __restrict__ grad, int accumulate) {
@@ -361,15 +361,17 @@ __global__ __launch_bounds__(64 * kRed4Waves) void reduce_partials4_kernel(const
   if (4 * q < count) {
     const floatx4* col = reinterpret_cast<const floatx4*>(part) + q;
     const long rs = stride / 4;
-    int b = w;
-    for (; b + (kRed4Unroll - 1) * kRed4Waves < nb; b += kRed4Unroll * kRed4Waves) {
+    // rows w, w + 8, ... in order (the fixed summation order); a batch's rows past nb add zeros
+    for (int b = w; b < nb; b += kRed4Unroll * kRed4Waves) {
       floatx4 v[kRed4Unroll];
 #pragma unroll
-      for (int u = 0; u < kRed4Unroll; ++u) v[u] = col[(long)(b + u * kRed4Waves) * rs];
+      for (int u = 0; u < kRed4Unroll; ++u) {
+        const int r = b + u * kRed4Waves;
+        v[u] = r < nb ? col[(long)r * rs] : floatx4{0.f, 0.f, 0.f, 0.f};
+      }
 #pragma unroll
       for (int u = 0; u < kRed4Unroll; ++u) acc += v[u];
     }
-    for (; b < nb; b += kRed4Waves) acc += col[(long)b * rs];
   }
   red[w][lane] = acc;
   __syncthreads();
@@ -399,15 +401,16 @@ __global__ __launch_bounds__(64 * kRed4Waves) void reduce_slices4_kernel(float* 
   floatx4* col = reinterpret_cast<floatx4*>(part) + q;
   const long rs = stride / 4;
   if (4 * q < count) {
-    int b = b0 + w;
-    for (; b + (kRed4Unroll - 1) * kRed4Waves < b1; b += kRed4Unroll * kRed4Waves) {
+    for (int b = b0 + w; b < b1; b += kRed4Unroll * kRed4Waves) {
       floatx4 v[kRed4Unroll];
 #pragma unroll
-      for (int u = 0; u < kRed4Unroll; ++u) v[u] = col[(long)(b + u * kRed4Waves) * rs];
+      for (int u = 0; u < kRed4Unroll; ++u) {
+        const int r = b + u * kRed4Waves;
+        v[u] = r < b1 ? col[(long)r * rs] : floatx4{0.f, 0.f, 0.f, 0.f};
+      }
 #pragma unroll
       for (int u = 0; u < kRed4Unroll; ++u) acc += v[u];
     }
-    for (; b < b1; b += kRed4Waves) acc += col[(long)b * rs];
   }
   red[w][lane] = acc;
   __syncthreads();

@@ -703,16 +703,14 @@ __global__ __launch_bounds__(512) void reduce_dw_kernel(const float* __restrict_
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const long i = (long)blockIdx.x * 64 + lane;
     float acc = 0.f;
-    if (i < Ps) {  // 8 rows in flight per thread, as the W x W planes (a fixed order all the same)
-      int b = w;
-      for (; b + 56 < rs; b += 64) {
-        float v[8];
+    if (i < Ps) {  // 16 rows in flight per thread, as the W x W planes (a fixed order all the same)
+      for (int b = w; b < rs; b += 128) {
+        float v[16];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) v[u] = rows[(long)(b + 8 * u) * Ps + i];
+        for (int u = 0; u < 16; ++u) v[u] = b + 8 * u < rs ? rows[(long)(b + 8 * u) * Ps + i] : 0.f;
 #pragma unroll
-        for (int u = 0; u < 8; ++u) acc += v[u];
+        for (int u = 0; u < 16; ++u) acc += v[u];
       }
-      for (; b < rs; b += 8) acc += rows[(long)b * Ps + i];
     }
     r[w * 64 + lane] = acc;
     __syncthreads();
@@ -740,15 +738,14 @@ __global__ __launch_bounds__(512) void reduce_dw_kernel(const float* __restrict_
   if (4 * q < WW) {
     const floatx4* col = reinterpret_cast<const floatx4*>(dpart + (long)(j - 1) * kslots * WW) + q;
     const long rs = WW / 4 * kstep;
-    int k = w;
-    for (; k + 56 < KS; k += 64) {
-      floatx4 v[8];
+    // slices w, w + 8, ... in order, 16 in flight per thread (a batch's slices past KS add zeros)
+    for (int k = w; k < KS; k += 128) {
+      floatx4 v[16];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = col[(long)(k + 8 * u) * rs];
+      for (int u = 0; u < 16; ++u) v[u] = k + 8 * u < KS ? col[(long)(k + 8 * u) * rs] : floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int u = 0; u < 8; ++u) acc += v[u];
+      for (int u = 0; u < 16; ++u) acc += v[u];
     }
-    for (; k < KS; k += 8) acc += col[(long)k * rs];
   }
   red[w][lane] = acc;
   __syncthreads();
