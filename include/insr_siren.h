@@ -390,6 +390,17 @@ int insr_adam_step_nets(int count, float* const* params, const float* const* gra
 int insr_adam_plateau_step_nets(int count, float* const* params, const float* const* grads, float* const* exp_avg,
                                 float* const* exp_avg_sq, const long* sizes, const int* shapes, float* opt_state,
                                 float beta1, float beta2, float eps, const float* loss, int patience, void* stream);
+/* The partial-gradient rows of a fused-path backward (insr_siren_jet_bwd's `partial`: nb rows of
+ * `stride` floats, insr_jet_partial_blocks / insr_jet_partial_stride) summed into grad (+= with
+ * accumulate) -- the same sums, bit for bit, as insr_reduce_partials_strided -- with the Adam update
+ * of those count elements (t = opt_state[STEP] + 1; shape as insr_adam_step_nets: the weight planes
+ * too) in the same launch, and with loss != NULL the plateau step after the last block
+ * (insr_adam_plateau_step_nets' ticket).  One launch instead of the sums + the Adam launch, for a
+ * flat buffer whose whole gradient is that backward's.  nb < 1024 (the one-level sums), stride a
+ * multiple of 4, partial 16-B aligned; else INSR_EINVAL. */
+int insr_adam_step_partials(const float* partial, int nb, long stride, float* grad, int accumulate, float* params,
+                            float* exp_avg, float* exp_avg_sq, long count, const int* shape, float* opt_state,
+                            float beta1, float beta2, float eps, const float* loss, int patience, void* stream);
 int insr_adam_step_multi(int count, float* const* params, const float* const* grads, float* const* exp_avg,
                          float* const* exp_avg_sq, const long* sizes, const float* opt_state, float beta1,
                          float beta2, float eps, int step_offset, void* stream);

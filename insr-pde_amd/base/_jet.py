@@ -18,6 +18,7 @@ Anything else raises UnsupportedPattern (there is no silent fallback).
 """
 import ctypes
 import os
+import threading
 
 import torch
 from torch.autograd.function import once_differentiable
@@ -143,6 +144,44 @@ class _BwdJob:
         self.cur = torch.cuda.current_stream(x2.device)
 
 
+DEFER_REDUCE = True  # BaseModel._update_network opens defer_reductions (False: A/B studies, tests)
+_Defer = threading.local()  # .depth > 0 inside defer_reductions on this thread, .nets its networks
+
+
+class defer_reductions:
+    """`with defer_reductions(): backward; optimizer.step()` -- a fused-path reverse jet (one
+    partial-gradient row per block) launched inside the scope does not launch its row sums: they are
+    held on the network (MLP.set_pending_reduce) for base.FusedAdam.step, which sums them into .grad
+    and runs the Adam (+ plateau) update in the same launch (insr_adam_step_partials).  Any other
+    access to the flat gradient lands them first (MLP.flush_pending_reduce), and the scope's exit
+    lands whatever no step consumed.  BaseModel._update_network opens it around backward + step when
+    the optimiser is FusedAdam."""
+
+    def __enter__(self):
+        _Defer.depth = getattr(_Defer, "depth", 0) + 1
+        if _Defer.depth == 1:
+            _Defer.nets = []
+        return self
+
+    def __exit__(self, *exc):
+        _Defer.depth -= 1
+        if _Defer.depth == 0:
+            nets, _Defer.nets = _Defer.nets, None
+            for mlp in nets:
+                mlp.flush_pending_reduce()
+        return False
+
+
+def launch_reduce(pr):
+    """The held-back row sums of one reverse jet (the args MLP.set_pending_reduce kept)."""
+    part, nb, count, stride, gflat, accumulate, cur, key = pr
+    lib = nat.lib()
+    with _timed("reduce", *key):
+        rc = lib.insr_reduce_partials_strided(nat.ptr(part), nb, count, stride, nat.ptr(gflat), accumulate,
+                                              ctypes.c_void_p(cur.cuda_stream))
+    nat.check(rc, "insr_reduce_partials_strided")
+
+
 def _launch_bwd(job):
     """One reverse jet into its network's flat .grad (first write of an iteration overwrites)."""
     mlp, mode, x2, act, gy, gdy, glap = job.mlp, job.mode, job.x2, job.act, job.gy, job.gdy, job.glap
@@ -176,10 +215,15 @@ def _launch_bwd(job):
         rc = lib.insr_siren_jet_bwd(nat.ptr(x2), n, din, dout, L, W, cmode, nat.ptr(mlp.flat_params()),
                                     nat.ptr(act), nat.ptr(gy), nat.ptr(gdy), nat.ptr(glap), nat.ptr(part), st)
     nat.check(rc, "insr_siren_jet_bwd")
+    nb, stride = lib.insr_jet_partial_blocks(n, din, W, cmode), lib.insr_jet_partial_stride(din, dout, L, W)
+    if getattr(_Defer, "depth", 0) > 0 and 0 < nb < 1024:  # the sums go into the Adam launch (defer_reductions)
+        mlp.set_pending_reduce((part, nb, gflat.numel(), stride, gflat, accumulate, cur, (mode, n, W, (din, dout, L))))
+        _Defer.nets.append(mlp)
+        mlp.grad_write_end(cur)
+        return
     with _timed("reduce", mode, n, W, (din, dout, L)):
-        rc = lib.insr_reduce_partials_strided(nat.ptr(part), lib.insr_jet_partial_blocks(n, din, W, cmode),
-                                              gflat.numel(), lib.insr_jet_partial_stride(din, dout, L, W),
-                                              nat.ptr(gflat), accumulate, st)
+        rc = lib.insr_reduce_partials_strided(nat.ptr(part), nb, gflat.numel(), stride, nat.ptr(gflat), accumulate,
+                                              st)
     nat.check(rc, "insr_reduce_partials_strided")
     mlp.grad_write_end(cur)
 

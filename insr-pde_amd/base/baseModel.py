@@ -20,6 +20,7 @@ the reference's semantics except where noted):
     all-reduces the flat gradients (RCCL) before the Adam step and the losses
     before the plateau step (mean or sum per `_dp_loss_reduction`).
 """
+import contextlib
 import os
 import shutil
 from abc import ABC, abstractmethod
@@ -200,14 +201,18 @@ class BaseModel(ABC):
         sum(loss_dict.values()) is run as backward of every term with a persistent unit
         seed: the same gradients without the add and ones-fill launches."""
         self.optimizer.zero_grad()
-        self._backward(loss_dict)
-        synced = self._dp_sync(loss_dict)
-        if self.scheduler is not None and getattr(self.scheduler, "fusable", False):
-            self.optimizer.step(plateau=(self.scheduler, synced['main']))  # Adam + plateau: one launch
-        else:
-            self.optimizer.step()
-            if self.scheduler is not None:
-                self.scheduler.step(synced['main'])
+        # one process with the fused optimiser: a fused-path backward's row sums run inside the Adam
+        # launch (base/_jet.py defer_reductions; under data parallelism the all-reduce needs them first)
+        defer = _jet.DEFER_REDUCE and isinstance(self.optimizer, FusedAdam) and self._dp_world() == 1
+        with (_jet.defer_reductions() if defer else contextlib.nullcontext()):
+            self._backward(loss_dict)
+            synced = self._dp_sync(loss_dict)
+            if self.scheduler is not None and getattr(self.scheduler, "fusable", False):
+                self.optimizer.step(plateau=(self.scheduler, synced['main']))  # Adam + plateau: one launch
+            else:
+                self.optimizer.step()
+                if self.scheduler is not None:
+                    self.scheduler.step(synced['main'])
         return synced
 
     def _backward(self, loss_dict):

@@ -381,7 +381,23 @@ class MLP(nn.Module):
                 p.grad = view
         return g, folded
 
+    # A fused-path backward's partial-gradient rows whose sums are held back for the Adam launch that
+    # follows (base/_jet.py defer_reductions: insr_adam_step_partials sums them into .grad and steps in
+    # one launch).  Anything else that touches the flat gradient first lands the sums
+    # (flush_pending_reduce) -- or drops them when the gradient is being discarded (mark_grad_stale).
+    def set_pending_reduce(self, args):
+        self.__dict__['_insr_pending_reduce'] = args
+
+    def take_pending_reduce(self):
+        return self.__dict__.pop('_insr_pending_reduce', None)
+
+    def flush_pending_reduce(self):
+        pr = self.take_pending_reduce()
+        if pr is not None:
+            _jet.launch_reduce(pr)
+
     def mark_grad_stale(self, set_to_none=True):
+        self.take_pending_reduce()  # zero_grad: the held-back sums would write a discarded gradient
         self.ensure_packed()
         if set_to_none:
             for p in self.plist():
@@ -394,6 +410,7 @@ class MLP(nn.Module):
 
     def grad_for_backward(self):
         """(flat grad buffer, accumulate flag) for the next HIP backward."""
+        self.flush_pending_reduce()  # an earlier write of this iteration lands first
         self.ensure_packed()
         if getattr(self, '_grad_state', 'stale') == 'stale' and all(p.grad is None for p in self.plist()):
             g, _ = self._attach_grad_views(fold_foreign=False)
@@ -411,6 +428,7 @@ class MLP(nn.Module):
         """Make `buf` (a 1-D fp32 tensor of param_count elements, e.g. a slice of a model's
         data-parallel gradient arena) this network's flat .grad storage; the current
         gradient values move into it."""
+        self.flush_pending_reduce()
         self.ensure_packed()
         if buf.numel() != self._flat.numel() or buf.dtype != self._flat.dtype or buf.device != self._flat.device:
             raise ValueError("bind_flat_grad: buffer does not match the flat parameters")
@@ -452,6 +470,12 @@ class MLP(nn.Module):
         return getattr(self, '_grad_state', 'stale') == 'live' or any(p.grad is not None for p in self.plist())
 
     def flat_grad_buffer(self):
+        """Flat gradient with every parameter's .grad attached to it (None grads -> 0); held-back
+        sums land first."""
+        self.flush_pending_reduce()
+        return self._flat_grad_buffer()
+
+    def _flat_grad_buffer(self):
         """Flat gradient with every parameter's .grad attached to it (None grads -> 0)."""
         self.ensure_packed()
         if self._flat_grad is None or any(p.grad is None for p in self.plist()):

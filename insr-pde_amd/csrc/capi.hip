@@ -461,6 +461,26 @@ __global__ void plateau_kernel(float* st, const float* loss, int patience, int a
   if (threadIdx.x == 0 && blockIdx.x == 0) plateau_update(st, loss, patience, advance_step);
 }
 
+// The plateau step after every block's Adam update, run by the last block to finish: a two-level
+// ticket -- block b adds to shard b % 8, the last adder of a shard (it knows the shard's block count)
+// adds to the top word, the last of those runs the step and zeroes all nine words (every block has
+// added by then); one word would serialise all the blocks' atomics.  Call with all of the block's
+// threads after their last read of st's lr / t.
+__device__ __forceinline__ void plateau_after_blocks(float* st, const float* loss, int patience) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned* top = reinterpret_cast<unsigned*>(st + INSR_OPT_TICKET);
+    unsigned* shard = reinterpret_cast<unsigned*>(st + INSR_OPT_TICKET_SHARDS);
+    const unsigned nb = gridDim.x, s = blockIdx.x & 7u;
+    const unsigned in_shard = (nb - s + 7u) / 8u, shards = nb < 8u ? nb : 8u;
+    if (atomicAdd(shard + s, 1u) == in_shard - 1u && atomicAdd(top, 1u) == shards - 1u) {
+      plateau_update(st, loss, patience, 1);
+      for (int q = 0; q < 8; ++q) atomicExch(shard + q, 0u);
+      atomicExch(top, 0u);
+    }
+  }
+}
+
 struct AdamList {
   float* p[INSR_ADAM_MAX_TENSORS];
   const float* g[INSR_ADAM_MAX_TENSORS];
@@ -579,26 +599,82 @@ __global__ void adam_multi_kernel(AdamList L, float* __restrict__ st, float b1, 
     L.p[k][i] = pn;
     if (L.shape[k][2] > 0) adam_wsplit(L.p[k], L.shape[k], i, pn);
   }
-  if (L.loss) {  // fused scheduler step: every block read lr / t above before it takes a ticket
-    // (relaxed ticket, no release/acquire: the last block only reads the loss -- written by an
-    // earlier launch -- and st, which no other block writes; the plain loads of lr / t above
-    // completed before each block's barrier)
-    // Two levels: block b adds to shard b % 8; the last adder of a shard (it knows the shard's block
-    // count) adds to the top word; the last of those runs the plateau step and zeroes all nine
-    // words -- every block has added by then.  One word would serialise all the blocks' atomics.
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      unsigned* top = reinterpret_cast<unsigned*>(st + INSR_OPT_TICKET);
-      unsigned* shard = reinterpret_cast<unsigned*>(st + INSR_OPT_TICKET_SHARDS);
-      const unsigned nb = gridDim.x, s = blockIdx.x & 7u;
-      const unsigned in_shard = (nb - s + 7u) / 8u, shards = nb < 8u ? nb : 8u;
-      if (atomicAdd(shard + s, 1u) == in_shard - 1u && atomicAdd(top, 1u) == shards - 1u) {
-        plateau_update(st, L.loss, L.patience, 1);
-        for (int q = 0; q < 8; ++q) atomicExch(shard + q, 0u);
-        atomicExch(top, 0u);
+  // fused scheduler step: every block read lr / t above before it takes a ticket (relaxed ticket,
+  // no release/acquire: the last block only reads the loss -- written by an earlier launch -- and
+  // st, which no other block writes; the plain loads of lr / t above completed before each block's
+  // barrier)
+  if (L.loss) plateau_after_blocks(st, L.loss, L.patience);
+}
+
+// The partial-row sums of a backward (reduce_partials4_kernel: the same rows per wave in the same
+// order, the same cross-wave combine -- bit-identical gradients) with the Adam update of those
+// elements as its epilogue, and the plateau step after the last block: one launch where the fused
+// backward path took two (sums, then adam_multi_kernel).  grad receives the gradient as well (the
+// flat .grad stays what torch would hold after backward()).  t = st[STEP] + 1, as the fused
+// Adam + plateau launch; loss == NULL: Adam only (the caller advances t).
+__global__ __launch_bounds__(64 * kRed4Waves) void reduce_adam_kernel(const float* __restrict__ part, int nb,
+                                                                      long count, long stride,
+                                                                      float* __restrict__ grad, int accumulate,
+                                                                      float* __restrict__ p, float* __restrict__ m,
+                                                                      float* __restrict__ v, int4 shp,
+                                                                      float* __restrict__ st, float b1, float b2,
+                                                                      float eps, const float* loss, int patience) {
+  __shared__ floatx4 red[kRed4Waves][64];
+  __shared__ float sc[2];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (threadIdx.x == 0) {
+    const double t = (double)st[INSR_OPT_STEP] + 1.0;
+    double p1, p2;
+    powi2_d((double)b1, (double)b2, (unsigned)t, p1, p2);
+    sc[0] = (float)((double)st[INSR_OPT_LR] / (1.0 - p1));
+    sc[1] = (float)sqrt(1.0 - p2);
+  }
+  const long q = (long)blockIdx.x * 64 + lane;  // column quad
+  floatx4 acc = floatx4{0.f, 0.f, 0.f, 0.f};
+  if (4 * q < count) {
+    const floatx4* col = reinterpret_cast<const floatx4*>(part) + q;
+    const long rs = stride / 4;
+    for (int b = w; b < nb; b += kRed4Unroll * kRed4Waves) {
+      floatx4 vv[kRed4Unroll];
+#pragma unroll
+      for (int u = 0; u < kRed4Unroll; ++u) {
+        const int r = b + u * kRed4Waves;
+        vv[u] = r < nb ? col[(long)r * rs] : floatx4{0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+      for (int u = 0; u < kRed4Unroll; ++u) acc += vv[u];
+    }
+  }
+  red[w][lane] = acc;
+  __syncthreads();
+  if (w == 0 && 4 * q < count) {
+    floatx4 tt = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < kRed4Waves; ++k) tt += red[k][lane];
+    const float step_size = sc[0], bc2s = sc[1];
+    const float w1 = (float)(1.0 - (double)b1);
+    const float w2 = (float)(1.0 - (double)b2);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const long i = 4 * q + r;
+      if (i >= count) break;
+      const float g = accumulate ? grad[i] + tt[r] : tt[r];
+      grad[i] = g;
+      const float m0 = m[i];
+      const float mi = m0 + w1 * (g - m0);
+      const float vi = v[i] * b2 + w2 * g * g;
+      m[i] = mi;
+      v[i] = vi;
+      const float denom = sqrtf(vi) / bc2s + eps;
+      const float pn = p[i] - step_size * (mi / denom);
+      p[i] = pn;
+      if (shp.z > 0) {
+        const int sh4[4] = {shp.x, shp.y, shp.z, shp.w};
+        adam_wsplit(p, sh4, i, pn);
       }
     }
   }
+  if (loss) plateau_after_blocks(st, loss, patience);
 }
 
 bool shape_ok(int din, int dout, int L, int width, int mode) {
@@ -1259,6 +1335,26 @@ int insr_adam_prepare(float* st, float b1, float b2, void* stream) {
 int insr_plateau_step(float* st, const float* loss, int patience, int advance_step, void* stream) {
   if (!st || (!loss && !advance_step)) return INSR_EINVAL;
   hipLaunchKernelGGL(plateau_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, st, loss, patience, advance_step);
+  return (int)hipGetLastError();
+}
+
+int insr_adam_step_partials(const float* partial, int nb, long stride, float* grad, int accumulate, float* params,
+                            float* exp_avg, float* exp_avg_sq, long count, const int* shape, float* st, float b1,
+                            float b2, float eps, const float* loss, int patience, void* stream) {
+  if (!partial || !grad || !params || !exp_avg || !exp_avg_sq || !st || nb < 1 || nb >= 1024 || count < 1 ||
+      stride < count || stride % 4 || ((uintptr_t)partial & 15))
+    return INSR_EINVAL;
+  int4 shp = make_int4(0, 0, 0, 0);
+  if (shape && shape[2] > 0) {  // a SIREN flat buffer with weight planes: its shape must match its size
+    if (!shape_ok(shape[0], shape[1], shape[2], shape[3], 0) ||
+        count != insr_siren_param_count(shape[0], shape[1], shape[2], shape[3]))
+      return INSR_EINVAL;
+    shp = make_int4(shape[0], shape[1], shape[2], shape[3]);
+  }
+  const long blocks = (count + 255) / 256;
+  hipLaunchKernelGGL(reduce_adam_kernel, dim3((unsigned)blocks), dim3(64 * kRed4Waves), 0, (hipStream_t)stream,
+                     partial, nb, count, stride, grad, accumulate, params, exp_avg, exp_avg_sq, shp, st, b1, b2, eps,
+                     loss, patience);
   return (int)hipGetLastError();
 }
 
