@@ -629,6 +629,17 @@ __global__ __launch_bounds__(64 * kRed4Waves) void reduce_adam_kernel(const floa
     sc[0] = (float)((double)st[INSR_OPT_LR] / (1.0 - p1));
     sc[1] = (float)sqrt(1.0 - p2);
   }
+  // the Adam epilogue's element (threads 0..255: element blockIdx.x * 256 + threadIdx.x): its state
+  // is loaded before the sums, under their latency
+  const long ie = (long)blockIdx.x * 256 + threadIdx.x;
+  const bool mine = threadIdx.x < 256 && ie < count;
+  float g0 = 0.f, m0 = 0.f, v0 = 0.f, p0 = 0.f;
+  if (mine) {
+    m0 = m[ie];
+    v0 = v[ie];
+    p0 = p[ie];
+    if (accumulate) g0 = grad[ie];
+  }
   const long q = (long)blockIdx.x * 64 + lane;  // column quad
   floatx4 acc = floatx4{0.f, 0.f, 0.f, 0.f};
   if (4 * q < count) {
@@ -647,31 +658,30 @@ __global__ __launch_bounds__(64 * kRed4Waves) void reduce_adam_kernel(const floa
   }
   red[w][lane] = acc;
   __syncthreads();
-  if (w == 0 && 4 * q < count) {
+  if (w == 0) {  // the cross-wave sums in reduce_partials4_kernel's order, back into red[0]
     floatx4 tt = floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int k = 0; k < kRed4Waves; ++k) tt += red[k][lane];
+    red[0][lane] = tt;
+  }
+  __syncthreads();
+  if (mine) {  // torch's op order, as adam_multi_kernel
+    const float tsum = reinterpret_cast<const float*>(&red[0][0])[threadIdx.x];
+    const float g = accumulate ? g0 + tsum : tsum;
+    grad[ie] = g;
     const float step_size = sc[0], bc2s = sc[1];
     const float w1 = (float)(1.0 - (double)b1);
     const float w2 = (float)(1.0 - (double)b2);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const long i = 4 * q + r;
-      if (i >= count) break;
-      const float g = accumulate ? grad[i] + tt[r] : tt[r];
-      grad[i] = g;
-      const float m0 = m[i];
-      const float mi = m0 + w1 * (g - m0);
-      const float vi = v[i] * b2 + w2 * g * g;
-      m[i] = mi;
-      v[i] = vi;
-      const float denom = sqrtf(vi) / bc2s + eps;
-      const float pn = p[i] - step_size * (mi / denom);
-      p[i] = pn;
-      if (shp.z > 0) {
-        const int sh4[4] = {shp.x, shp.y, shp.z, shp.w};
-        adam_wsplit(p, sh4, i, pn);
-      }
+    const float mi = m0 + w1 * (g - m0);
+    const float vi = v0 * b2 + w2 * g * g;
+    m[ie] = mi;
+    v[ie] = vi;
+    const float denom = sqrtf(vi) / bc2s + eps;
+    const float pn = p0 - step_size * (mi / denom);
+    p[ie] = pn;
+    if (shp.z > 0) {
+      const int sh4[4] = {shp.x, shp.y, shp.z, shp.w};
+      adam_wsplit(p, sh4, ie, pn);
     }
   }
   if (loss) plateau_after_blocks(st, loss, patience);
