@@ -481,6 +481,18 @@ __device__ __forceinline__ void plateau_after_blocks(float* st, const float* los
   }
 }
 
+// One Adam element in torch's op order (m.lerp_(g, 1-b1); v.mul_(b2).addcmul_(g, g, 1-b2);
+// p.addcdiv_(m, sqrt(v)/sqrt(1-b2^t) + eps, -step_size)) with every multiply-add spelled out, so
+// the launches that run it (adam_multi_kernel, reduce_adam_kernel) round identically whatever the
+// compiler's contraction choices around them
+__device__ __forceinline__ float adam_elem(float g, float m0, float v0, float p0, float step_size, float bc2s,
+                                           float w1, float w2, float b2, float eps, float& mi, float& vi) {
+  mi = fmaf(w1, g - m0, m0);
+  vi = fmaf(w2 * g, g, v0 * b2);
+  const float denom = __fadd_rn(__fdiv_rn(sqrtf(vi), bc2s), eps);
+  return fmaf(-step_size, __fdiv_rn(mi, denom), p0);
+}
+
 struct AdamList {
   float* p[INSR_ADAM_MAX_TENSORS];
   const float* g[INSR_ADAM_MAX_TENSORS];
@@ -588,14 +600,10 @@ __global__ void adam_multi_kernel(AdamList L, float* __restrict__ st, float b1, 
     int k = 0;
     while (k + 1 < L.count && gi >= L.start[k + 1]) ++k;
     const long i = gi - L.start[k];
-    const float g = L.g[k][i];
-    const float m0 = L.m[k][i];
-    const float mi = m0 + w1 * (g - m0);
-    const float vi = L.v[k][i] * b2 + w2 * g * g;
+    float mi, vi;
+    const float pn = adam_elem(L.g[k][i], L.m[k][i], L.v[k][i], L.p[k][i], step_size, bc2s, w1, w2, b2, eps, mi, vi);
     L.m[k][i] = mi;
     L.v[k][i] = vi;
-    const float denom = sqrtf(vi) / bc2s + eps;
-    const float pn = L.p[k][i] - step_size * (mi / denom);
     L.p[k][i] = pn;
     if (L.shape[k][2] > 0) adam_wsplit(L.p[k], L.shape[k], i, pn);
   }
@@ -672,12 +680,10 @@ __global__ __launch_bounds__(64 * kRed4Waves) void reduce_adam_kernel(const floa
     const float step_size = sc[0], bc2s = sc[1];
     const float w1 = (float)(1.0 - (double)b1);
     const float w2 = (float)(1.0 - (double)b2);
-    const float mi = m0 + w1 * (g - m0);
-    const float vi = v0 * b2 + w2 * g * g;
+    float mi, vi;
+    const float pn = adam_elem(g, m0, v0, p0, step_size, bc2s, w1, w2, b2, eps, mi, vi);
     m[ie] = mi;
     v[ie] = vi;
-    const float denom = sqrtf(vi) / bc2s + eps;
-    const float pn = p0 - step_size * (mi / denom);
     p[ie] = pn;
     if (shp.z > 0) {
       const int sh4[4] = {shp.x, shp.y, shp.z, shp.w};
