@@ -163,12 +163,15 @@ class defer_reductions:
             _Defer.nets = []
         return self
 
-    def __exit__(self, *exc):
+    def __exit__(self, exc_type, *exc):
         _Defer.depth -= 1
         if _Defer.depth == 0:
             nets, _Defer.nets = _Defer.nets, None
             for mlp in nets:
-                mlp.flush_pending_reduce()
+                if exc_type is None:
+                    mlp.flush_pending_reduce()
+                else:  # an aborted iteration (e.g. a failed capture): nothing more is launched for it
+                    mlp.take_pending_reduce()
         return False
 
 
