@@ -390,6 +390,18 @@ int insr_adam_step_nets(int count, float* const* params, const float* const* gra
 int insr_adam_plateau_step_nets(int count, float* const* params, const float* const* grads, float* const* exp_avg,
                                 float* const* exp_avg_sq, const long* sizes, const int* shapes, float* opt_state,
                                 float beta1, float beta2, float eps, const float* loss, int patience, void* stream);
+/* insr_siren_jet_bwd_grad in two halves for the backwards the jet_fb.hpp kernel serves (the recompute
+ * path and the resident sweep on the saved streams, insr_jet_bwd_kernel == 1; else INSR_EINVAL):
+ * phases 1 = the reverse sweep into `work`, 2 = the sums of `work` into grad, 3 = both.  With
+ * exp_avg != NULL the sums run the Adam update of every element they write (t = opt_state[STEP] + 1,
+ * the weight planes too under INSR_MODE_WSPLIT) and, loss != NULL, the plateau step after the last
+ * block -- insr_siren_jet_bwd_grad + insr_adam_plateau_step_nets in one launch fewer; the same sums
+ * and update, bit for bit.  params is read by phase 1 and updated by phase 2. */
+int insr_siren_jet_bwd_grad_adam(const float* x, long n_points, int d_in, int d_out, int num_hidden, int width,
+                                 int mode, float* params, const float* act, const float* gy, const float* gdy,
+                                 const float* glap, float* work, float* grad, int accumulate, int phases,
+                                 float* exp_avg, float* exp_avg_sq, float* opt_state, float beta1, float beta2,
+                                 float eps, const float* loss, int patience, void* stream);
 /* The partial-gradient rows of a fused-path backward (insr_siren_jet_bwd's `partial`: nb rows of
  * `stride` floats, insr_jet_partial_blocks / insr_jet_partial_stride) summed into grad (+= with
  * accumulate) -- the same sums, bit for bit, as insr_reduce_partials_strided -- with the Adam update

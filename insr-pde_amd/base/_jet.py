@@ -175,14 +175,49 @@ class defer_reductions:
         return False
 
 
+class PendingSums:
+    """The held-back sums of one reverse jet: kind "rows" -- a fused-path backward's partial-gradient
+    rows (insr_reduce_partials_strided / insr_adam_step_partials); kind "fb" -- the second half of a
+    jet_fb.hpp backward (insr_siren_jet_bwd_grad_adam phases 2)."""
+    __slots__ = ("kind", "buf", "nb", "stride", "job", "gflat", "accumulate", "cur", "key")
+
+    def __init__(self, kind, buf, nb, stride, job, gflat, accumulate, cur, key):
+        self.kind, self.buf, self.nb, self.stride, self.job = kind, buf, nb, stride, job
+        self.gflat, self.accumulate, self.cur, self.key = gflat, accumulate, cur, key
+
+    def launch(self, adam=None):
+        """The sums into .grad; adam = (params, m, v, state, b1, b2, eps, loss or None, patience): with
+        the Adam (+ plateau) update of every element in the same launch."""
+        lib = nat.lib()
+        st = ctypes.c_void_p(self.cur.cuda_stream)
+        p, m, v, state, b1, b2, eps, loss, patience = adam if adam is not None else (None,) * 7 + (None, 0)
+        if self.kind == "rows":
+            if adam is None:
+                with _timed("reduce", *self.key):
+                    rc = lib.insr_reduce_partials_strided(nat.ptr(self.buf), self.nb, self.gflat.numel(), self.stride,
+                                                          nat.ptr(self.gflat), self.accumulate, st)
+                nat.check(rc, "insr_reduce_partials_strided")
+                return
+            mlp = self.job
+            shape = (ctypes.c_int * 4)(mlp.in_features, mlp.out_features, mlp.num_hidden_layers, mlp.kernel_width)
+            nat.check(lib.insr_adam_step_partials(
+                nat.ptr(self.buf), self.nb, self.stride, nat.ptr(self.gflat), self.accumulate, nat.ptr(p), nat.ptr(m),
+                nat.ptr(v), self.gflat.numel(), shape, nat.ptr(state), b1, b2, eps, nat.ptr(loss), patience, st),
+                "insr_adam_step_partials")
+            return
+        mlp, x2, n, cmode = self.job
+        din, dout, L, W = mlp.in_features, mlp.out_features, mlp.num_hidden_layers, mlp.kernel_width
+        with _timed("reduce", *self.key):
+            rc = lib.insr_siren_jet_bwd_grad_adam(
+                nat.ptr(x2), n, din, dout, L, W, cmode, nat.ptr(mlp.flat_params()), None, None, None, None,
+                nat.ptr(self.buf), nat.ptr(self.gflat), self.accumulate, 2, nat.ptr(m), nat.ptr(v), nat.ptr(state),
+                b1 or 0.0, b2 or 0.0, eps or 0.0, nat.ptr(loss), patience, st)
+        nat.check(rc, "insr_siren_jet_bwd_grad_adam")
+
+
 def launch_reduce(pr):
-    """The held-back row sums of one reverse jet (the args MLP.set_pending_reduce kept)."""
-    part, nb, count, stride, gflat, accumulate, cur, key = pr
-    lib = nat.lib()
-    with _timed("reduce", *key):
-        rc = lib.insr_reduce_partials_strided(nat.ptr(part), nb, count, stride, nat.ptr(gflat), accumulate,
-                                              ctypes.c_void_p(cur.cuda_stream))
-    nat.check(rc, "insr_reduce_partials_strided")
+    """The held-back sums of one reverse jet (MLP.flush_pending_reduce)."""
+    pr.launch()
 
 
 def _launch_bwd(job):
@@ -204,6 +239,19 @@ def _launch_bwd(job):
         with torch.cuda.stream(cur):
             work = torch.empty(max(lib.insr_jet_bwd_work_bytes(n, din, dout, L, W, cmode) // 4, 1),
                                device=x2.device, dtype=torch.float32)
+        if getattr(_Defer, "depth", 0) > 0 and lib.insr_jet_bwd_kernel(n, din, dout, L, W, cmode) == 1:
+            # the jet_fb.hpp backward: its reverse sweep now, its sums with the Adam launch (defer_reductions)
+            with _timed("bwd", mode, n, W, (din, dout, L)):
+                rc = lib.insr_siren_jet_bwd_grad_adam(nat.ptr(x2), n, din, dout, L, W, cmode, nat.ptr(mlp.flat_params()),
+                                                      nat.ptr(act), nat.ptr(gy), nat.ptr(gdy), nat.ptr(glap),
+                                                      nat.ptr(work), nat.ptr(gflat), accumulate, 1, None, None, None,
+                                                      0.0, 0.0, 0.0, None, 0, st)
+            nat.check(rc, "insr_siren_jet_bwd_grad_adam")
+            mlp.set_pending_reduce(PendingSums("fb", work, 0, 0, (mlp, x2, n, cmode), gflat, accumulate, cur,
+                                               (mode, n, W, (din, dout, L))))
+            _Defer.nets.append(mlp)
+            mlp.grad_write_end(cur)
+            return
         with _timed("bwd", mode, n, W, (din, dout, L)):
             rc = lib.insr_siren_jet_bwd_grad(nat.ptr(x2), n, din, dout, L, W, cmode, nat.ptr(mlp.flat_params()),
                                              nat.ptr(act), nat.ptr(gy), nat.ptr(gdy), nat.ptr(glap), nat.ptr(work),
@@ -220,7 +268,7 @@ def _launch_bwd(job):
     nat.check(rc, "insr_siren_jet_bwd")
     nb, stride = lib.insr_jet_partial_blocks(n, din, W, cmode), lib.insr_jet_partial_stride(din, dout, L, W)
     if getattr(_Defer, "depth", 0) > 0 and 0 < nb < 1024:  # the sums go into the Adam launch (defer_reductions)
-        mlp.set_pending_reduce((part, nb, gflat.numel(), stride, gflat, accumulate, cur, (mode, n, W, (din, dout, L))))
+        mlp.set_pending_reduce(PendingSums("rows", part, nb, stride, mlp, gflat, accumulate, cur, (mode, n, W, (din, dout, L))))
         _Defer.nets.append(mlp)
         mlp.grad_write_end(cur)
         return

@@ -142,28 +142,24 @@ class FusedAdam:
 
 
     def _step_partials(self, plateau):
-        """The step of a single network whose whole gradient is one fused-path backward whose row
-        sums base._jet.defer_reductions held back: sums + Adam (+ plateau) in ONE launch
-        (insr_adam_step_partials, the same sums and update bit for bit).  False: not that case (the
-        regular launch runs, landing any held-back sums first)."""
-        import ctypes
+        """The step of a single network whose whole gradient is one reverse jet whose sums
+        base._jet.defer_reductions held back: sums + Adam (+ plateau) in ONE launch
+        (insr_adam_step_partials / insr_siren_jet_bwd_grad_adam phase 2: the same sums and update
+        bit for bit).  False: not that case (the regular launch runs, landing held-back sums first)."""
         pend = [(mlp, m, v) for mlp, m, v in self._nets if "_insr_pending_reduce" in mlp.__dict__]
         if len(pend) != 1 or any(p.grad is not None for p, _, _ in self._loose):
             return False
         mlp, m, v = pend[0]
         if any(o is not mlp and o.grad_touched() for o, _, _ in self._nets):
             return False
-        part, nb, count, stride, gflat, accumulate, cur, _ = mlp.__dict__["_insr_pending_reduce"]
-        if cur.cuda_stream != torch.cuda.current_stream(self.device).cuda_stream:
+        pr = mlp.__dict__["_insr_pending_reduce"]
+        if pr.cur.cuda_stream != torch.cuda.current_stream(self.device).cuda_stream:
             return False
         mlp.take_pending_reduce()
         b1, b2 = self.betas
         metric = plateau[0]._metric(plateau[1]) if plateau is not None else None
-        shape = (ctypes.c_int * 4)(mlp.in_features, mlp.out_features, mlp.num_hidden_layers, mlp.kernel_width)
-        nat.check(nat.lib().insr_adam_step_partials(
-            nat.ptr(part), nb, stride, nat.ptr(gflat), accumulate, nat.ptr(mlp.flat_params()), nat.ptr(m), nat.ptr(v),
-            count, shape, nat.ptr(self.state), b1, b2, self.eps, nat.ptr(metric),
-            plateau[0].patience if plateau is not None else 0, nat.stream_of(self.device)), "insr_adam_step_partials")
+        pr.launch(adam=(mlp.flat_params(), m, v, self.state, b1, b2, self.eps, metric,
+                        plateau[0].patience if plateau is not None else 0))
         mlp.mark_wsplit_current()
         self._pending_advance = plateau is None
         self.partials_steps = getattr(self, "partials_steps", 0) + 1  # (tests: the fused path ran)

@@ -6,6 +6,7 @@
 #include <tuple>
 
 #include "jet_common.hpp"
+#include "optim.hpp"
 
 namespace insr {
 
@@ -432,65 +433,8 @@ __global__ void adam_prepare_kernel(float* st, float b1, float b2) {
   }
 }
 
-// plateau scheduler step of one device state (torch ReduceLROnPlateau.step after Adam.step)
-__device__ void plateau_update(float* st, const float* loss, int patience, int advance_step) {
-  if (advance_step) st[INSR_OPT_STEP] = st[INSR_OPT_STEP] + 1.f;
-  if (!loss) return;  // advance-only (optimiser without a scheduler)
-  const float cur = *loss;
-  float best = st[INSR_OPT_BEST];
-  float bad = st[INSR_OPT_BAD];
-  // torch: a < best * (1 - threshold), threshold = 1e-4 (python double math)
-  if ((double)cur < (double)best * (1.0 - 1e-4)) {
-    best = cur;
-    bad = 0.f;
-  } else {
-    bad += 1.f;
-  }
-  if (bad > (float)patience) {
-    const double old = st[INSR_OPT_LR];
-    double nw = old * (double)st[INSR_OPT_FACTOR];
-    if (nw < (double)st[INSR_OPT_MINLR]) nw = st[INSR_OPT_MINLR];
-    if (old - nw > 1e-8) st[INSR_OPT_LR] = (float)nw;
-    bad = 0.f;
-  }
-  st[INSR_OPT_BEST] = best;
-  st[INSR_OPT_BAD] = bad;
-}
-
 __global__ void plateau_kernel(float* st, const float* loss, int patience, int advance_step) {
   if (threadIdx.x == 0 && blockIdx.x == 0) plateau_update(st, loss, patience, advance_step);
-}
-
-// The plateau step after every block's Adam update, run by the last block to finish: a two-level
-// ticket -- block b adds to shard b % 8, the last adder of a shard (it knows the shard's block count)
-// adds to the top word, the last of those runs the step and zeroes all nine words (every block has
-// added by then); one word would serialise all the blocks' atomics.  Call with all of the block's
-// threads after their last read of st's lr / t.
-__device__ __forceinline__ void plateau_after_blocks(float* st, const float* loss, int patience) {
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    unsigned* top = reinterpret_cast<unsigned*>(st + INSR_OPT_TICKET);
-    unsigned* shard = reinterpret_cast<unsigned*>(st + INSR_OPT_TICKET_SHARDS);
-    const unsigned nb = gridDim.x, s = blockIdx.x & 7u;
-    const unsigned in_shard = (nb - s + 7u) / 8u, shards = nb < 8u ? nb : 8u;
-    if (atomicAdd(shard + s, 1u) == in_shard - 1u && atomicAdd(top, 1u) == shards - 1u) {
-      plateau_update(st, loss, patience, 1);
-      for (int q = 0; q < 8; ++q) atomicExch(shard + q, 0u);
-      atomicExch(top, 0u);
-    }
-  }
-}
-
-// One Adam element in torch's op order (m.lerp_(g, 1-b1); v.mul_(b2).addcmul_(g, g, 1-b2);
-// p.addcdiv_(m, sqrt(v)/sqrt(1-b2^t) + eps, -step_size)) with every multiply-add spelled out, so
-// the launches that run it (adam_multi_kernel, reduce_adam_kernel) round identically whatever the
-// compiler's contraction choices around them
-__device__ __forceinline__ float adam_elem(float g, float m0, float v0, float p0, float step_size, float bc2s,
-                                           float w1, float w2, float b2, float eps, float& mi, float& vi) {
-  mi = fmaf(w1, g - m0, m0);
-  vi = fmaf(w2 * g, g, v0 * b2);
-  const float denom = __fadd_rn(__fdiv_rn(sqrtf(vi), bc2s), eps);
-  return fmaf(-step_size, __fdiv_rn(mi, denom), p0);
 }
 
 struct AdamList {
@@ -505,81 +449,6 @@ struct AdamList {
   int patience;
   int count;
 };
-
-// the updated hidden weight (layer j, row n, column m) of a buffer with pre-split planes:
-// its three bf16 terms (jet_x6.hpp split, element-wise identical to wsplit_kernel) stored
-// into both fragment orientations (jet_common.hpp wsplit_offset) -- the planes stay current
-// without a launch of their own
-__device__ __forceinline__ void adam_wsplit(float* base, const int (&sh)[4], long i, float w) {
-  const int din = sh[0], dout = sh[1], L = sh[2], W = sh[3];
-  const long off = i - ((long)W * din + W);
-  const long per = (long)W * W + W;
-  if (off < 0 || off >= (long)L * per) return;
-  const long r = off % per;
-  if (r >= (long)W * W) return;  // a bias
-  const int j = 1 + (int)(off / per), n = (int)(r / W), m = (int)(r % W);
-  const int NT = W / 16, KC = W / 32;
-  unsigned short t[3];
-  {
-    const __bf16 h = (__bf16)w;
-    float rs = w - (float)h;
-    const __bf16 md = (__bf16)rs;
-    rs -= (float)md;
-    const __bf16 lo = (__bf16)rs;
-    t[0] = __builtin_bit_cast(unsigned short, h);
-    t[1] = __builtin_bit_cast(unsigned short, md);
-    t[2] = __builtin_bit_cast(unsigned short, lo);
-  }
-  unsigned short* pl = reinterpret_cast<unsigned short*>(base + wsplit_offset(din, dout, L, W));
-  const long ov = wsplit_orient_vecs(L, W) * 8;  // u16 per orientation
-  // orientation 0: A row n, k = m; orientation 1: A row m (W^T), k = n
-  const int rr[2] = {n, m}, kk[2] = {m, n};
-#pragma unroll
-  for (int o = 0; o < 2; ++o) {
-    const int rt = rr[o] >> 4, c = rr[o] & 15, kc = kk[o] >> 5, g = (kk[o] & 31) >> 3, jj = kk[o] & 7;
-    const long fr = (((long)(j - 1) * NT + rt) * KC + kc) * 3;
-#pragma unroll
-    for (int q = 0; q < 3; ++q) pl[o * ov + ((fr + q) * 64 + 16 * g + c) * 8 + jj] = t[q];
-  }
-  // the fp16 planes (INSR_PREC_F16X3): 2^8 w in two fp16 terms, orientation 0 then 1; a weight outside
-  // their range is flagged in the status word (insr_siren_wsplit_status) and clamped there
-  unsigned short* ph = reinterpret_cast<unsigned short*>(base + wsplit_f16_offset(din, dout, L, W));
-  if (!(fabsf(w) < kF16WMax)) {
-    atomicOr(reinterpret_cast<unsigned*>(base + wsplit_status_offset(din, dout, L, W)), 1u);
-    w = fminf(fmaxf(w, -kF16WMax), kF16WMax);
-  }
-  const float ws = w * kF16WScale;
-  const _Float16 hh = (_Float16)ws, hl = (_Float16)(ws - (float)hh);
-  const long oh = 2L * L * W * W;  // u16 per fp16 orientation
-#pragma unroll
-  for (int o = 0; o < 2; ++o) {
-    const int rt = rr[o] >> 4, c = rr[o] & 15, kc = kk[o] >> 5, g = (kk[o] & 31) >> 3, jj = kk[o] & 7;
-    const long fr = (((long)(j - 1) * NT + rt) * KC + kc) * 2;
-    ph[o * oh + (fr * 64 + 16 * g + c) * 8 + jj] = __builtin_bit_cast(unsigned short, hh);
-    ph[o * oh + ((fr + 1) * 64 + 16 * g + c) * 8 + jj] = __builtin_bit_cast(unsigned short, hl);
-  }
-}
-
-// One launch over up to INSR_ADAM_MAX_TENSORS flat buffers.  The step t used is
-// st[STEP] + step_offset (the plateau kernel advances st[STEP] after the update,
-// so the bias corrections need no separate prepare launch); torch's op order:
-//   m.lerp_(g, 1-b1); v.mul_(b2).addcmul_(g, g, 1-b2);
-//   p.addcdiv_(m, sqrt(v)/sqrt(1-b2^t) + eps, -lr/(1-b1^t))
-// b^n in double by repeated squaring: t is integer-valued, and the bias corrections need ~1e-15
-// relative, not libm's pow (whose double-precision log / exp chain sat at the head of every block)
-__device__ __forceinline__ void powi2_d(double b1, double b2, unsigned n, double& p1, double& p2) {
-  p1 = 1.0;
-  p2 = 1.0;
-  while (n) {
-    if (n & 1u) {
-      p1 *= b1;
-      p2 *= b2;
-    }
-    b1 *= b1;
-    b2 *= b2;
-    n >>= 1;
-  }
-}
 
 __global__ void adam_multi_kernel(AdamList L, float* __restrict__ st, float b1, float b2, float eps,
                                   int step_offset) {
@@ -611,7 +480,7 @@ __global__ void adam_multi_kernel(AdamList L, float* __restrict__ st, float b1, 
   // no release/acquire: the last block only reads the loss -- written by an earlier launch -- and
   // st, which no other block writes; the plain loads of lr / t above completed before each block's
   // barrier)
-  if (L.loss) plateau_after_blocks(st, L.loss, L.patience);
+  if (L.loss) plateau_after_blocks(st, L.loss, L.patience, blockIdx.x, gridDim.x);
 }
 
 // The partial-row sums of a backward (reduce_partials4_kernel: the same rows per wave in the same
@@ -690,7 +559,7 @@ __global__ __launch_bounds__(64 * kRed4Waves) void reduce_adam_kernel(const floa
       adam_wsplit(p, sh4, ie, pn);
     }
   }
-  if (loss) plateau_after_blocks(st, loss, patience);
+  if (loss) plateau_after_blocks(st, loss, patience, blockIdx.x, gridDim.x);
 }
 
 bool shape_ok(int din, int dout, int L, int width, int mode) {
@@ -1142,7 +1011,7 @@ int insr_siren_jet_bwd_grad_multi(const InsrBwdJob* jobs, int njobs, int din, in
       J.njobs = m;
       const float* prm = params;
       if (!(prm = with_planes(params, din, dout, L, W, mode, st, 0, &rc))) return rc;
-      return dispatch_fb_bwd(c.S, c.lap, L, J, din, dout, prm, work, grad, acc, 0, st);
+      return dispatch_fb_bwd(c.S, c.lap, L, J, din, dout, prm, work, grad, acc, 0, 3, AdamArgs{}, st);
     }
   }
   if (p.nf > 0) {
@@ -1224,6 +1093,60 @@ int insr_jet_bwd_kernel(long n, int din, int dout, int L, int W, int mode) {
   return (p == 3 || (p == 2 && c.resident_f16(n, L))) ? 1 : 0;
 }
 
+// The single-job call of the jet_fb.hpp backward (the recompute kernel, or the resident sweep on the
+// saved streams): phases / Adam epilogue as fb_bwd_t
+static int fb_bwd_call(const JetCall& c, const float* x, long n, int din, int dout, int L, int W, int mode,
+                       const float* params, const float* act, const float* gy, const float* gdy, const float* glap,
+                       float* work, float* grad, int accumulate, int phases, const AdamArgs& A, hipStream_t st) {
+  int rc = 0;
+  if (!(params = with_planes(params, din, dout, L, W, mode, st, 0, &rc))) return rc;
+  FbJobs J{};
+  J.x[0] = x;
+  J.act[0] = c.recompute(L) ? nullptr : act;
+  J.gy[0] = gy;
+  J.gdy[0] = gdy;
+  J.glap[0] = glap;
+  J.n[0] = (int)n;
+  J.tstart[0] = 0;
+  J.tstart[1] = (int)((n + 15) / 16);
+  J.njobs = 1;
+  return dispatch_fb_bwd(c.S, c.lap, L, J, din, dout, params, work, grad, accumulate, c.recompute(L) ? 0 : 1, phases,
+                         A, st);
+}
+
+int insr_siren_jet_bwd_grad_adam(const float* x, long n, int din, int dout, int L, int W, int mode, float* params,
+                                 const float* act, const float* gy, const float* gdy, const float* glap, float* work,
+                                 float* grad, int accumulate, int phases, float* exp_avg, float* exp_avg_sq,
+                                 float* opt_state, float beta1, float beta2, float eps, const float* loss, int patience,
+                                 void* stream) {
+  if (!shape_ok(din, dout, L, W, mode) || n < 1 || n > 0x7fffffffL || phases < 1 || phases > 3) return INSR_EINVAL;
+  const JetCall c(din, W, mode);
+  if (!(c.recompute(L) || (c.resident(n, L) && c.resident_f16(n, L)))) return INSR_EINVAL;  // not jet_fb.hpp's
+  if (!params || !work || !grad) return INSR_EINVAL;
+  if ((phases & 1) && (!x || (!act && !c.recompute(L)))) return INSR_EINVAL;  // the sweep's inputs
+  AdamArgs A;
+  if ((phases & 2) && exp_avg) {
+    if (!exp_avg_sq || !opt_state) return INSR_EINVAL;
+    A.p = params;
+    A.m = exp_avg;
+    A.v = exp_avg_sq;
+    A.st = opt_state;
+    A.loss = loss;
+    A.patience = patience;
+    A.b1 = beta1;
+    A.b2 = beta2;
+    A.eps = eps;
+    if (mode & INSR_MODE_WSPLIT) {  // the buffer carries the weight planes: the update rewrites them
+      A.shape[0] = din;
+      A.shape[1] = dout;
+      A.shape[2] = L;
+      A.shape[3] = W;
+    }
+  }
+  return fb_bwd_call(c, x, n, din, dout, L, W, mode, params, act, gy, gdy, glap, work, grad, accumulate, phases, A,
+                     (hipStream_t)stream);
+}
+
 int insr_siren_jet_bwd_grad(const float* x, long n, int din, int dout, int L, int W, int mode, const float* params,
                             const float* act, const float* gy, const float* gdy, const float* glap, float* work,
                             float* grad, int accumulate, void* stream) {
@@ -1231,38 +1154,13 @@ int insr_siren_jet_bwd_grad(const float* x, long n, int din, int dout, int L, in
   if (n == 0) return 0;
   const JetCall c(din, W, mode);
   if (!x || !params || (!act && !c.recompute(L)) || !work || !grad) return INSR_EINVAL;
-  if (c.recompute(L)) {  // act is not read: the kernel recomputes the forward per tile
-    hipStream_t st = (hipStream_t)stream;
-    int rc = 0;
-    if (!(params = with_planes(params, din, dout, L, W, mode, st, 0, &rc))) return rc;
-    FbJobs J{};
-    J.x[0] = x;
-    J.gy[0] = gy;
-    J.gdy[0] = gdy;
-    J.glap[0] = glap;
-    J.n[0] = (int)n;
-    J.tstart[0] = 0;
-    J.tstart[1] = (int)((n + 15) / 16);
-    J.njobs = 1;
-    return dispatch_fb_bwd(c.S, c.lap, L, J, din, dout, params, work, grad, accumulate, 0, st);
-  }
+  if (c.recompute(L) || (c.resident(n, L) && c.resident_f16(n, L)))  // jet_fb.hpp: one job
+    return fb_bwd_call(c, x, n, din, dout, L, W, mode, params, act, gy, gdy, glap, work, grad, accumulate, 3,
+                       AdamArgs{}, (hipStream_t)stream);
   if (c.resident(n, L)) {
     hipStream_t st = (hipStream_t)stream;
     int rc = 0;
     if (!(params = with_planes(params, din, dout, L, W, mode, st, 0, &rc))) return rc;
-    if (c.resident_f16(n, L)) {  // the reverse sweep of jet_fb.hpp on the saved streams
-      FbJobs J{};
-      J.x[0] = x;
-      J.act[0] = act;
-      J.gy[0] = gy;
-      J.gdy[0] = gdy;
-      J.glap[0] = glap;
-      J.n[0] = (int)n;
-      J.tstart[0] = 0;
-      J.tstart[1] = (int)((n + 15) / 16);
-      J.njobs = 1;
-      return dispatch_fb_bwd(c.S, c.lap, L, J, din, dout, params, work, grad, accumulate, 1, st);
-    }
     return dispatch_resident_bwd(c.S, c.lap, L, x, (int)n, din, dout, params, act, gy, gdy, glap, work, grad,
                                  accumulate, st);
   }

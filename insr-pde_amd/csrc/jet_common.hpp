@@ -444,6 +444,20 @@ int resident_blocks(long n);
 
 // The jobs of one launch: batches of ONE network (its params), e.g. a phase's interior points and
 // its wall bands from separate network calls; job k covers global tiles [tstart[k], tstart[k + 1]).
+// The Adam (+ plateau) update a sums launch runs as its epilogue (reduce_dw_kernel with m != NULL,
+// optim.hpp): the flat parameter buffer and its moments, the optimiser state, the buffer's SIREN shape
+// (its weight planes), the plateau loss (NULL: Adam only); t = st[STEP] + 1 either way
+struct AdamArgs {
+  float* p = nullptr;
+  float* m = nullptr;
+  float* v = nullptr;
+  float* st = nullptr;
+  const float* loss = nullptr;
+  int patience = 0;
+  float b1 = 0.f, b2 = 0.f, eps = 0.f;
+  int shape[4] = {0, 0, 0, 0};
+};
+
 struct FbJobs {
   const float* x[kBwdJobs];
   const float* act[kBwdJobs];  // the forward's saved streams (the saved-stream variant; unread by recompute)
@@ -457,7 +471,7 @@ struct FbJobs {
 // recompute backward (jet_fb.hpp: W = 128, L = 4, f16x3 with per-tile scales): ONE persistent launch
 // (forward + reverse jet per tile, dW resident per CU) + the fixed-order sums; act is not read
 int dispatch_fb_bwd(int S, bool LAP, int L, const FbJobs& J, int din, int dout, const float* prm, float* work,
-                    float* grad, int accumulate, int saved, hipStream_t st);
+                    float* grad, int accumulate, int saved, int phases, const AdamArgs& A, hipStream_t st);
 bool fb_supported(int S, bool LAP, int L);
 long fb_work_floats(long tiles, int din, int dout, int L);
 int fb_launch_blocks(long tiles);

@@ -14,15 +14,15 @@ bool fb_supported(int S, bool LAP, int L) {
 // saved = 0: the recompute backward (reruns the forward per tile); 1: the same reverse sweep on the
 // forward's saved streams (J.act) -- dW resident per CU, f16x3 products, no z̄ round trip
 int dispatch_fb_bwd(int S, bool LAP, int L, const FbJobs& J, int din, int dout, const float* prm, float* work,
-                    float* grad, int accumulate, int saved, hipStream_t st) {
+                    float* grad, int accumulate, int saved, int phases, const AdamArgs& A, hipStream_t st) {
   if (!fb_supported(S, LAP, L)) return INSR_EINVAL;
   switch ((S * 2 + (LAP ? 1 : 0)) * 2 + (saved ? 1 : 0)) {
-    case 18: return fb_bwd_t<4, true, 4, 2, false>(J, din, dout, prm, work, grad, accumulate, st);
-    case 12: return fb_bwd_t<3, false, 4, 2, false>(J, din, dout, prm, work, grad, accumulate, st);
-    case 4: return fb_bwd_t<1, false, 4, 4, false>(J, din, dout, prm, work, grad, accumulate, st);
-    case 19: return fb_bwd_t<4, true, 4, 1, true>(J, din, dout, prm, work, grad, accumulate, st);
-    case 13: return fb_bwd_t<3, false, 4, 1, true>(J, din, dout, prm, work, grad, accumulate, st);
-    case 5: return fb_bwd_t<1, false, 4, 1, true>(J, din, dout, prm, work, grad, accumulate, st);
+    case 18: return fb_bwd_t<4, true, 4, 2, false>(J, din, dout, prm, work, grad, accumulate, phases, A, st);
+    case 12: return fb_bwd_t<3, false, 4, 2, false>(J, din, dout, prm, work, grad, accumulate, phases, A, st);
+    case 4: return fb_bwd_t<1, false, 4, 4, false>(J, din, dout, prm, work, grad, accumulate, phases, A, st);
+    case 19: return fb_bwd_t<4, true, 4, 1, true>(J, din, dout, prm, work, grad, accumulate, phases, A, st);
+    case 13: return fb_bwd_t<3, false, 4, 1, true>(J, din, dout, prm, work, grad, accumulate, phases, A, st);
+    case 5: return fb_bwd_t<1, false, 4, 1, true>(J, din, dout, prm, work, grad, accumulate, phases, A, st);
     default: return INSR_EINVAL;
   }
 }

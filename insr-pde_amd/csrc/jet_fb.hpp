@@ -658,9 +658,11 @@ inline long fb_work_floats_impl(long tiles, int din, int dout, int L) {
   return (long)L * nb * 128 * 128 + nb * small_count(din, dout, L, 128);
 }
 
+// phases: 1 the reverse sweep, 2 the sums (with A.m: + the Adam update, insr_siren_jet_bwd_grad_adam),
+// 3 both (the same work buffer between a 1 and a 2)
 template <int S, bool LAP, int L, int ZR, bool SAVED>
 int fb_bwd_t(const FbJobs& J, int din, int dout, const float* prm, float* work, float* grad, int accumulate,
-             hipStream_t st) {
+             int phases, const AdamArgs& A, hipStream_t st) {
   constexpr int W = 128;
   const int tiles = J.tstart[J.njobs];
   if (tiles <= 0) return 0;
@@ -674,13 +676,15 @@ int fb_bwd_t(const FbJobs& J, int din, int dout, const float* prm, float* work, 
   static const bool attr = ((void)hipFuncSetAttribute((const void*)jet_fb_x6<S, LAP, L, ZR, SAVED>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)lds), true);  // once per instantiation (thread-safe static init)
   (void)attr;
-  hipLaunchKernelGGL((jet_fb_x6<S, LAP, L, ZR, SAVED>), dim3(nb), dim3(512), lds, st, J, din, dout, prm, dpart, small, Ps, nb,
-                     tiles);
+  if (phases & 1)
+    hipLaunchKernelGGL((jet_fb_x6<S, LAP, L, ZR, SAVED>), dim3(nb), dim3(512), lds, st, J, din, dout, prm, dpart, small,
+                       Ps, nb, tiles);
+  if (!(phases & 2)) return (int)hipGetLastError();
   const int grad16 = (((uintptr_t)(grad + hidden_off(din, W, 1))) & 15) == 0 ? 1 : 0;
   const int wq = (W * W / 4 + 63) / 64;
   const int rows_x = (int)((Ps + 63) / 64);
   hipLaunchKernelGGL(reduce_dw_kernel, dim3((unsigned)(wq > rows_x ? wq : rows_x), L + 1), dim3(512), 0, st, dpart, nb,
-                     din, W, grad, accumulate, grad16, 1, L, small, nb, Ps, dout, 1, nb);
+                     din, W, grad, accumulate, grad16, 1, L, small, nb, Ps, dout, 1, nb, A);
   return (int)hipGetLastError();
 }
 

@@ -403,7 +403,7 @@ int resident_bwd_t(const float* x, int N, int din, int dout, const float* prm, c
   const int wq = (W * W / 4 + 63) / 64;
   const int rows_x = (int)((Ps + 63) / 64);
   hipLaunchKernelGGL(reduce_dw_kernel, dim3((unsigned)(wq > rows_x ? wq : rows_x), L + 1), dim3(512), 0, st, dpart, nb,
-                     din, W, grad, accumulate, grad16, 1, L, small, nb, Ps, dout, 1, nb);
+                     din, W, grad, accumulate, grad16, 1, L, small, nb, Ps, dout, 1, nb, AdamArgs{});
   return (int)hipGetLastError();
 }
 

@@ -20,6 +20,7 @@
 // Reference semantics: loss.backward() of base/baseModel.py:73-78 through the jets of
 // base/diff_ops.py:44-82 (the same math as jet_split.hpp / jet_x6.hpp).
 #include "jet_x6.hpp"
+#include "optim.hpp"
 
 // the wide path is compiled once per precision TU: jet_x6w.hip (NQ = 3) and jet_bfw.hip
 // (NQ = 1, 2) include this file with INSR_WIDE_NQ set
@@ -696,8 +697,29 @@ __global__ __launch_bounds__(256) void reduce_rows_kernel(const float* __restric
 __global__ __launch_bounds__(512) void reduce_dw_kernel(const float* __restrict__ dpart, int KS, int din, int W,
                                                         float* __restrict__ grad, int accumulate, int grad16, int frag, int L,
                                                         const float* __restrict__ rows, int rs, long Ps, int dout,
-                                                        int kstep, int kslots) {
+                                                        int kstep, int kslots, AdamArgs A) {
   __shared__ floatx4 red[8][64];
+  __shared__ float sc[2];  // A.m != NULL: Adam's step size and sqrt(1 - b2^t)
+  if (A.m && threadIdx.x == 0) {
+    const double t = (double)A.st[INSR_OPT_STEP] + 1.0;
+    double p1, p2;
+    powi2_d((double)A.b1, (double)A.b2, (unsigned)t, p1, p2);
+    sc[0] = (float)((double)A.st[INSR_OPT_LR] / (1.0 - p1));
+    sc[1] = (float)sqrt(1.0 - p2);
+  }
+  // the gradient element grad[i] = g, then (A.m) its Adam update -- torch's op order (optim.hpp)
+  auto put = [&](long i, float g) {
+    grad[i] = g;
+    if (A.m) {
+      float mi, vi;
+      const float pn = adam_elem(g, A.m[i], A.v[i], A.p[i], sc[0], sc[1], (float)(1.0 - (double)A.b1),
+                                 (float)(1.0 - (double)A.b2), A.b2, A.eps, mi, vi);
+      A.m[i] = mi;
+      A.v[i] = vi;
+      A.p[i] = pn;
+      if (A.shape[2] > 0) adam_wsplit(A.p, A.shape, i, pn);
+    }
+  };
   if ((int)blockIdx.y == L) {
     float* r = reinterpret_cast<float*>(&red[0][0]);
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -726,50 +748,52 @@ __global__ __launch_bounds__(512) void reduce_dw_kernel(const float* __restrict_
         dst = hidden_off(din, W, 1 + (int)((i - head) / W)) + (long)W * W + (i - head) % W;
       else
         dst = out_off(din, W, L) + (i - head - hid);
-      grad[dst] = accumulate ? grad[dst] + t : t;
+      put(dst, accumulate ? grad[dst] + t : t);
     }
-    return;
+  } else {
+    const int j = blockIdx.y + 1;
+    const long WW = (long)W * W;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const long q = (long)blockIdx.x * 64 + lane;  // column quad
+    floatx4 acc = floatx4{0.f, 0.f, 0.f, 0.f};
+    if (4 * q < WW) {
+      const floatx4* col = reinterpret_cast<const floatx4*>(dpart + (long)(j - 1) * kslots * WW) + q;
+      const long rs4 = WW / 4 * kstep;
+      // slices w, w + 8, ... in order, 16 in flight per thread (a batch's slices past KS add zeros)
+      for (int k = w; k < KS; k += 128) {
+        floatx4 v[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) v[u] = k + 8 * u < KS ? col[(long)(k + 8 * u) * rs4] : floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int u = 0; u < 16; ++u) acc += v[u];
+      }
+    }
+    red[w][lane] = acc;
+    __syncthreads();
+    if (w == 0 && 4 * q < WW) {
+      floatx4 t = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int k = 0; k < 8; ++k) t += red[k][lane];
+      if (frag) {
+        const int ln = (int)(q & 63), f = (int)(q >> 6), nt = W / 16;
+        const long d0 = hidden_off(din, W, j) + (long)(16 * (f / nt) + 4 * (ln >> 4)) * W + 16 * (f % nt) + (ln & 15);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) put(d0 + (long)r * W, accumulate ? grad[d0 + (long)r * W] + t[r] : t[r]);
+      } else {  // (never with an Adam epilogue: the host passes A.m only with frag = 1)
+        float* dst = grad + hidden_off(din, W, j) + 4 * q;
+        if (grad16) {  // the gradient buffer's hidden blocks are 16-B aligned (a net's own flat .grad)
+          floatx4* d4 = reinterpret_cast<floatx4*>(dst);
+          if (accumulate) t += *d4;
+          *d4 = t;
+        } else {  // e.g. a slice of a data-parallel gradient arena
+#pragma unroll
+          for (int r = 0; r < 4; ++r) dst[r] = accumulate ? dst[r] + t[r] : t[r];
+        }
+      }
+    }
   }
-  const int j = blockIdx.y + 1;
-  const long WW = (long)W * W;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const long q = (long)blockIdx.x * 64 + lane;  // column quad
-  floatx4 acc = floatx4{0.f, 0.f, 0.f, 0.f};
-  if (4 * q < WW) {
-    const floatx4* col = reinterpret_cast<const floatx4*>(dpart + (long)(j - 1) * kslots * WW) + q;
-    const long rs = WW / 4 * kstep;
-    // slices w, w + 8, ... in order, 16 in flight per thread (a batch's slices past KS add zeros)
-    for (int k = w; k < KS; k += 128) {
-      floatx4 v[16];
-#pragma unroll
-      for (int u = 0; u < 16; ++u) v[u] = k + 8 * u < KS ? col[(long)(k + 8 * u) * rs] : floatx4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int u = 0; u < 16; ++u) acc += v[u];
-    }
-  }
-  red[w][lane] = acc;
-  __syncthreads();
-  if (w == 0 && 4 * q < WW) {
-    floatx4 t = floatx4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int k = 0; k < 8; ++k) t += red[k][lane];
-    if (frag) {
-      const int ln = (int)(q & 63), f = (int)(q >> 6), nt = W / 16;
-      float* dst = grad + hidden_off(din, W, j) + (long)(16 * (f / nt) + 4 * (ln >> 4)) * W + 16 * (f % nt) + (ln & 15);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) dst[(long)r * W] = accumulate ? dst[(long)r * W] + t[r] : t[r];
-      return;
-    }
-    float* dst = grad + hidden_off(din, W, j) + 4 * q;
-    if (grad16) {  // the gradient buffer's hidden blocks are 16-B aligned (a net's own flat .grad)
-      floatx4* d4 = reinterpret_cast<floatx4*>(dst);
-      if (accumulate) t += *d4;
-      *d4 = t;
-    } else {  // e.g. a slice of a data-parallel gradient arena
-#pragma unroll
-      for (int r = 0; r < 4; ++r) dst[r] = accumulate ? dst[r] + t[r] : t[r];
-    }
-  }
+  if (A.m && A.loss) plateau_after_blocks(A.st, A.loss, A.patience, blockIdx.y * gridDim.x + blockIdx.x,
+                                          gridDim.x * gridDim.y);
 }
 
 }  // namespace
@@ -868,7 +892,7 @@ int wide_bwd_t(const float* x, int N, int din, int dout, int L, const float* prm
     const int grad16 = (((uintptr_t)(grad + hidden_off(din, W, 1))) & 15) == 0 ? 1 : 0;  // W % 4 == 0: all layers alike
     const int wq = (W * W / 4 + 63) / 64;
     hipLaunchKernelGGL(reduce_dw_kernel, dim3((unsigned)(wq > rows_x ? wq : rows_x), L + 1), dim3(512), 0, st, dpart,
-                       KS, din, W, grad, accumulate, grad16, 0, L, rows, rs, Ps, dout, 1, KS);
+                       KS, din, W, grad, accumulate, grad16, 0, L, rows, rs, Ps, dout, 1, KS, AdamArgs{});
     return (int)hipGetLastError();
   }
   hipLaunchKernelGGL(reduce_rows_kernel, dim3((unsigned)rows_x, rs), dim3(256), 0, st, small, tiles, Ps, rows);

@@ -372,35 +372,48 @@ def test_training_loop_unrolled_graph_matches(ph):
         assert res[U][2] == res[1][2], U  # the same iterations read, the same losses
 
 
+@pytest.mark.parametrize("policy", [None, 5])
 @pytest.mark.parametrize("graph", [False, True])
-def test_fused_sums_adam_bit_identical(ph, graph):
-    """base._jet.defer_reductions: a fused-path value backward's partial-row sums run inside the Adam
-    launch (insr_adam_step_partials) -- the same sums in the same order and the same update, so the
-    advect / projection loops (value jets) end with parameters, optimiser moments and state, and the
-    flat .grad bit for bit equal to the separate sums + Adam launches (DEFER_REDUCE off), eager and
+def test_fused_sums_adam_bit_identical(ph, graph, policy):
+    """base._jet.defer_reductions: a reverse jet's sums run inside the Adam launch -- a fused-path
+    value backward's partial rows (insr_adam_step_partials; default policy) and, under policy 5, the
+    resident sweep's dW sums of every jet (insr_siren_jet_bwd_grad_adam phase 2, the pressure
+    Laplacian jet included) -- the same sums in the same order and the same update, so the advect /
+    pressure / projection loops end with parameters, optimiser moments and state, and the flat .grad
+    bit for bit equal to the separate sums + Adam launches (DEFER_REDUCE off), eager and
     graph-replayed."""
+    import contextlib
     from pde.fluid import Fluid2DModel
+    import base
     res = {}
     for defer in (False, True):
         _jet.DEFER_REDUCE = defer
+        scope = base._native.knobs(policy=policy) if policy is not None else contextlib.nullcontext()
         try:
-            torch.manual_seed(0)
-            cfg = _cfg("fluid", num_hidden_layers=4, hidden_features=128, sample_resolution=32, max_n_iters=6,
-                       insr_graph=graph, insr_sync_every=3)
-            model = Fluid2DModel(cfg)
-            set_flat(model.velocity_field, ph["fluid/vel/params0"])
-            set_flat(model.velocity_field_prev, ph["fluid/vel_prev/params0"])
-            set_flat(model.pressure_field, ph["fluid/pres/params0"])
-            model.timestep = 1
-            model._advect_velocity()
-            model._projection()
-            assert getattr(model, "_insr_capture_error", None) is None
-            torch.cuda.synchronize()
-            opt = model.optimizer
-            assert (getattr(opt, "partials_steps", 0) > 0) == defer
-            res[defer] = (flat(model.velocity_field), opt._nets[0][1].cpu().numpy(), opt._nets[0][2].cpu().numpy(),
-                          opt.state.cpu().numpy(), flat_grad(model.velocity_field))
-            assert "_insr_pending_reduce" not in model.velocity_field.__dict__
+            with scope:
+                torch.manual_seed(0)
+                cfg = _cfg("fluid", num_hidden_layers=4, hidden_features=128, sample_resolution=32, max_n_iters=6,
+                           insr_graph=graph, insr_sync_every=3)
+                model = Fluid2DModel(cfg)
+                set_flat(model.velocity_field, ph["fluid/vel/params0"])
+                set_flat(model.velocity_field_prev, ph["fluid/vel_prev/params0"])
+                set_flat(model.pressure_field, ph["fluid/pres/params0"])
+                model.timestep = 1
+                out = []
+                for phase in ("_advect_velocity", "_solve_pressure", "_projection"):
+                    getattr(model, phase)()
+                    assert getattr(model, "_insr_capture_error", None) is None
+                    torch.cuda.synchronize()
+                    opt = model.optimizer
+                    fused = getattr(opt, "partials_steps", 0) > 0
+                    assert fused == defer or (phase == "_solve_pressure" and policy is None and not fused)
+                    out += [opt._nets[0][1].cpu().numpy(), opt._nets[0][2].cpu().numpy(), opt._nets[1][1].cpu().numpy(),
+                            opt._nets[1][2].cpu().numpy(), opt.state.cpu().numpy()]
+                out += [flat(model.velocity_field), flat(model.pressure_field), flat_grad(model.velocity_field),
+                        flat_grad(model.pressure_field)]
+                res[defer] = out
+                for net in (model.velocity_field, model.pressure_field):
+                    assert "_insr_pending_reduce" not in net.__dict__
         finally:
             _jet.DEFER_REDUCE = True
     for a, b in zip(res[False], res[True]):
