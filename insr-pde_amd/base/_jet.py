@@ -242,10 +242,10 @@ def _launch_bwd(job):
         if getattr(_Defer, "depth", 0) > 0 and lib.insr_jet_bwd_kernel(n, din, dout, L, W, cmode) == 1:
             # the jet_fb.hpp backward: its reverse sweep now, its sums with the Adam launch (defer_reductions)
             with _timed("bwd", mode, n, W, (din, dout, L)):
-                rc = lib.insr_siren_jet_bwd_grad_adam(nat.ptr(x2), n, din, dout, L, W, cmode, nat.ptr(mlp.flat_params()),
-                                                      nat.ptr(act), nat.ptr(gy), nat.ptr(gdy), nat.ptr(glap),
-                                                      nat.ptr(work), nat.ptr(gflat), accumulate, 1, None, None, None,
-                                                      0.0, 0.0, 0.0, None, 0, st)
+                rc = lib.insr_siren_jet_bwd_grad_adam(
+                    nat.ptr(x2), n, din, dout, L, W, cmode, nat.ptr(mlp.flat_params()), nat.ptr(act), nat.ptr(gy),
+                    nat.ptr(gdy), nat.ptr(glap), nat.ptr(work), nat.ptr(gflat), accumulate, 1, None, None, None,
+                    0.0, 0.0, 0.0, None, 0, st)
             nat.check(rc, "insr_siren_jet_bwd_grad_adam")
             mlp.set_pending_reduce(PendingSums("fb", work, 0, 0, (mlp, x2, n, cmode), gflat, accumulate, cur,
                                                (mode, n, W, (din, dout, L))))
@@ -268,7 +268,8 @@ def _launch_bwd(job):
     nat.check(rc, "insr_siren_jet_bwd")
     nb, stride = lib.insr_jet_partial_blocks(n, din, W, cmode), lib.insr_jet_partial_stride(din, dout, L, W)
     if getattr(_Defer, "depth", 0) > 0 and 0 < nb < 1024:  # the sums go into the Adam launch (defer_reductions)
-        mlp.set_pending_reduce(PendingSums("rows", part, nb, stride, mlp, gflat, accumulate, cur, (mode, n, W, (din, dout, L))))
+        mlp.set_pending_reduce(PendingSums("rows", part, nb, stride, mlp, gflat, accumulate, cur,
+                                           (mode, n, W, (din, dout, L))))
         _Defer.nets.append(mlp)
         mlp.grad_write_end(cur)
         return
