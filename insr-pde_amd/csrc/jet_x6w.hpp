@@ -707,12 +707,13 @@ __global__ __launch_bounds__(512) void reduce_dw_kernel(const float* __restrict_
     sc[0] = (float)((double)A.st[INSR_OPT_LR] / (1.0 - p1));
     sc[1] = (float)sqrt(1.0 - p2);
   }
-  // the gradient element grad[i] = g, then (A.m) its Adam update -- torch's op order (optim.hpp)
-  auto put = [&](long i, float g) {
+  // the gradient element grad[i] = g, then (A.m) its Adam update from the state (m0, v0, p0) the thread
+  // loaded before the sums -- torch's op order (optim.hpp)
+  auto put = [&](long i, float g, float m0, float v0, float p0) {
     grad[i] = g;
     if (A.m) {
       float mi, vi;
-      const float pn = adam_elem(g, A.m[i], A.v[i], A.p[i], sc[0], sc[1], (float)(1.0 - (double)A.b1),
+      const float pn = adam_elem(g, m0, v0, p0, sc[0], sc[1], (float)(1.0 - (double)A.b1),
                                  (float)(1.0 - (double)A.b2), A.b2, A.eps, mi, vi);
       A.m[i] = mi;
       A.v[i] = vi;
@@ -720,10 +721,30 @@ __global__ __launch_bounds__(512) void reduce_dw_kernel(const float* __restrict_
       if (A.shape[2] > 0) adam_wsplit(A.p, A.shape, i, pn);
     }
   };
+  float g0 = 0.f, m0 = 0.f, v0 = 0.f, p0 = 0.f;  // this thread's element's state (its epilogue)
+  auto preload = [&](long i) {
+    if (accumulate) g0 = grad[i];
+    if (A.m) {
+      m0 = A.m[i];
+      v0 = A.v[i];
+      p0 = A.p[i];
+    }
+  };
   if ((int)blockIdx.y == L) {
     float* r = reinterpret_cast<float*>(&red[0][0]);
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const long i = (long)blockIdx.x * 64 + lane;
+    const long head = (long)W * din + W, hid = (long)L * W;
+    long dst = 0;
+    if (i < Ps) {
+      if (i < head)
+        dst = i;
+      else if (i < head + hid)
+        dst = hidden_off(din, W, 1 + (int)((i - head) / W)) + (long)W * W + (i - head) % W;
+      else
+        dst = out_off(din, W, L) + (i - head - hid);
+      if (w == 0) preload(dst);
+    }
     float acc = 0.f;
     if (i < Ps) {  // 16 rows in flight per thread, as the W x W planes (a fixed order all the same)
       for (int b = w; b < rs; b += 128) {
@@ -740,21 +761,18 @@ __global__ __launch_bounds__(512) void reduce_dw_kernel(const float* __restrict_
       float t = 0.f;
 #pragma unroll
       for (int k = 0; k < 8; ++k) t += r[k * 64 + lane];
-      const long head = (long)W * din + W, hid = (long)L * W;
-      long dst;
-      if (i < head)
-        dst = i;
-      else if (i < head + hid)
-        dst = hidden_off(din, W, 1 + (int)((i - head) / W)) + (long)W * W + (i - head) % W;
-      else
-        dst = out_off(din, W, L) + (i - head - hid);
-      put(dst, accumulate ? grad[dst] + t : t);
+      put(dst, accumulate ? g0 + t : t, m0, v0, p0);
     }
   } else {
     const int j = blockIdx.y + 1;
     const long WW = (long)W * W;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const long q = (long)blockIdx.x * 64 + lane;  // column quad
+    // frag = 1: the quad's 4 elements are rows 16 (f / nt) + 4 (ln >> 4) + r of one column; wave r < 4
+    // runs element r's epilogue (its state loaded here, under the sums)
+    const int ln = (int)(q & 63), f = (int)(q >> 6), nt = W / 16;
+    const long d0 = hidden_off(din, W, j) + (long)(16 * (f / nt) + 4 * (ln >> 4)) * W + 16 * (f % nt) + (ln & 15);
+    if (frag && w < 4 && 4 * q < WW) preload(d0 + (long)w * W);
     floatx4 acc = floatx4{0.f, 0.f, 0.f, 0.f};
     if (4 * q < WW) {
       const floatx4* col = reinterpret_cast<const floatx4*>(dpart + (long)(j - 1) * kslots * WW) + q;
@@ -770,16 +788,23 @@ __global__ __launch_bounds__(512) void reduce_dw_kernel(const float* __restrict_
     }
     red[w][lane] = acc;
     __syncthreads();
-    if (w == 0 && 4 * q < WW) {
+    if (frag) {
+      if (w == 0 && 4 * q < WW) {  // the cross-wave sums in the fixed order, back into red[0]
+        floatx4 t = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int k = 0; k < 8; ++k) t += red[k][lane];
+        red[0][lane] = t;
+      }
+      __syncthreads();
+      if (w < 4 && 4 * q < WW) {
+        const float t = red[0][lane][w];
+        put(d0 + (long)w * W, accumulate ? g0 + t : t, m0, v0, p0);
+      }
+    } else if (w == 0 && 4 * q < WW) {  // (never with an Adam epilogue: the host passes A.m only with frag = 1)
       floatx4 t = floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int k = 0; k < 8; ++k) t += red[k][lane];
-      if (frag) {
-        const int ln = (int)(q & 63), f = (int)(q >> 6), nt = W / 16;
-        const long d0 = hidden_off(din, W, j) + (long)(16 * (f / nt) + 4 * (ln >> 4)) * W + 16 * (f % nt) + (ln & 15);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) put(d0 + (long)r * W, accumulate ? grad[d0 + (long)r * W] + t[r] : t[r]);
-      } else {  // (never with an Adam epilogue: the host passes A.m only with frag = 1)
+      {
         float* dst = grad + hidden_off(din, W, j) + 4 * q;
         if (grad16) {  // the gradient buffer's hidden blocks are 16-B aligned (a net's own flat .grad)
           floatx4* d4 = reinterpret_cast<floatx4*>(dst);
