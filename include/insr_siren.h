@@ -391,7 +391,8 @@ int insr_adam_plateau_step_nets(int count, float* const* params, const float* co
                                 float* const* exp_avg_sq, const long* sizes, const int* shapes, float* opt_state,
                                 float beta1, float beta2, float eps, const float* loss, int patience, void* stream);
 /* insr_siren_jet_bwd_grad in two halves for the backwards the jet_fb.hpp kernel serves (the recompute
- * path and the resident sweep on the saved streams, insr_jet_bwd_kernel == 1; else INSR_EINVAL):
+ * path and the resident sweep on the saved streams, insr_jet_bwd_kernel == 1) and for the two-kernel
+ * path (insr_jet_bwd_path == 1, num_hidden > 0); else INSR_EINVAL:
  * phases 1 = the reverse sweep into `work`, 2 = the sums of `work` into grad, 3 = both.  With
  * exp_avg != NULL the sums run the Adam update of every element they write (t = opt_state[STEP] + 1,
  * the weight planes too under INSR_MODE_WSPLIT) and, loss != NULL, the plateau step after the last

@@ -177,8 +177,8 @@ class defer_reductions:
 
 class PendingSums:
     """The held-back sums of one reverse jet: kind "rows" -- a fused-path backward's partial-gradient
-    rows (insr_reduce_partials_strided / insr_adam_step_partials); kind "fb" -- the second half of a
-    jet_fb.hpp backward (insr_siren_jet_bwd_grad_adam phases 2)."""
+    rows (insr_reduce_partials_strided / insr_adam_step_partials); kind "split" -- the second half of a
+    jet_fb.hpp or two-kernel backward (insr_siren_jet_bwd_grad_adam phase 2)."""
     __slots__ = ("kind", "buf", "nb", "stride", "job", "gflat", "accumulate", "cur", "key")
 
     def __init__(self, kind, buf, nb, stride, job, gflat, accumulate, cur, key):
@@ -232,22 +232,25 @@ def _launch_bwd(job):
     cur = job.cur
     st = ctypes.c_void_p(cur.cuda_stream)
     mlp.grad_write_begin(cur)  # order after a write of .grad made on another stream
-    if lib.insr_jet_bwd_path(n, din, dout, L, W, cmode) > 0:
+    path = lib.insr_jet_bwd_path(n, din, dout, L, W, cmode)
+    if path > 0:
         # two-kernel path (propagation + split-K dW GEMM), the resident-dW or the recompute persistent
         # kernel, with their fixed-order sums straight into .grad.  Scratch comes from the pool of the
         # stream the kernels run on (a deferred job's autograd stream may differ from the current one)
         with torch.cuda.stream(cur):
             work = torch.empty(max(lib.insr_jet_bwd_work_bytes(n, din, dout, L, W, cmode) // 4, 1),
                                device=x2.device, dtype=torch.float32)
-        if getattr(_Defer, "depth", 0) > 0 and lib.insr_jet_bwd_kernel(n, din, dout, L, W, cmode) == 1:
-            # the jet_fb.hpp backward: its reverse sweep now, its sums with the Adam launch (defer_reductions)
+        if getattr(_Defer, "depth", 0) > 0 and (lib.insr_jet_bwd_kernel(n, din, dout, L, W, cmode) == 1 or
+                                                 (path == 1 and L > 0)):
+            # the jet_fb.hpp or the two-kernel backward: its sweep now, its sums with the Adam launch
+            # (defer_reductions)
             with _timed("bwd", mode, n, W, (din, dout, L)):
                 rc = lib.insr_siren_jet_bwd_grad_adam(
                     nat.ptr(x2), n, din, dout, L, W, cmode, nat.ptr(mlp.flat_params()), nat.ptr(act), nat.ptr(gy),
                     nat.ptr(gdy), nat.ptr(glap), nat.ptr(work), nat.ptr(gflat), accumulate, 1, None, None, None,
                     0.0, 0.0, 0.0, None, 0, st)
             nat.check(rc, "insr_siren_jet_bwd_grad_adam")
-            mlp.set_pending_reduce(PendingSums("fb", work, 0, 0, (mlp, x2, n, cmode), gflat, accumulate, cur,
+            mlp.set_pending_reduce(PendingSums("split", work, 0, 0, (mlp, x2, n, cmode), gflat, accumulate, cur,
                                                (mode, n, W, (din, dout, L))))
             _Defer.nets.append(mlp)
             mlp.grad_write_end(cur)

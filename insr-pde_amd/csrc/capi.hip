@@ -1093,6 +1093,25 @@ int insr_jet_bwd_kernel(long n, int din, int dout, int L, int W, int mode) {
   return (p == 3 || (p == 2 && c.resident_f16(n, L))) ? 1 : 0;
 }
 
+// The two-kernel (wide) backward: phases / Adam epilogue as wide_bwd_t
+static int wide_bwd_call(const JetCall& c, const float* x, long n, int din, int dout, int L, int W, int mode,
+                         const float* params, const float* act, const float* gy, const float* gdy, const float* glap,
+                         float* work, float* grad, int accumulate, int phases, const AdamArgs& A, hipStream_t st) {
+  int rc = 0;
+  if (!(params = with_planes(params, din, dout, L, W, mode, st, 0, &rc))) return rc;
+  switch (c.nqb) {
+    case 3:
+      return dispatch_wide_bwd_q<3>(c.NT, c.S, c.lap, x, (int)n, din, dout, L, params, act, gy, gdy, glap, work, grad,
+                                    accumulate, c.k.f16, phases, A, st);
+    case 2:
+      return dispatch_wide_bwd_q<2>(c.NT, c.S, c.lap, x, (int)n, din, dout, L, params, act, gy, gdy, glap, work, grad,
+                                    accumulate, c.k.f16, phases, A, st);
+    default:
+      return dispatch_wide_bwd_q<1>(c.NT, c.S, c.lap, x, (int)n, din, dout, L, params, act, gy, gdy, glap, work, grad,
+                                    accumulate, c.k.f16, phases, A, st);
+  }
+}
+
 // The single-job call of the jet_fb.hpp backward (the recompute kernel, or the resident sweep on the
 // saved streams): phases / Adam epilogue as fb_bwd_t
 static int fb_bwd_call(const JetCall& c, const float* x, long n, int din, int dout, int L, int W, int mode,
@@ -1121,7 +1140,9 @@ int insr_siren_jet_bwd_grad_adam(const float* x, long n, int din, int dout, int 
                                  void* stream) {
   if (!shape_ok(din, dout, L, W, mode) || n < 1 || n > 0x7fffffffL || phases < 1 || phases > 3) return INSR_EINVAL;
   const JetCall c(din, W, mode);
-  if (!(c.recompute(L) || (c.resident(n, L) && c.resident_f16(n, L)))) return INSR_EINVAL;  // not jet_fb.hpp's
+  const bool fb = c.recompute(L) || (c.resident(n, L) && c.resident_f16(n, L));  // jet_fb.hpp's backward
+  const bool wide = !fb && !c.resident(n, L) && c.wide(n) && L > 0;               // the two-kernel backward
+  if (!fb && !wide) return INSR_EINVAL;
   if (!params || !work || !grad) return INSR_EINVAL;
   if ((phases & 1) && (!x || (!act && !c.recompute(L)))) return INSR_EINVAL;  // the sweep's inputs
   AdamArgs A;
@@ -1143,6 +1164,9 @@ int insr_siren_jet_bwd_grad_adam(const float* x, long n, int din, int dout, int 
       A.shape[3] = W;
     }
   }
+  if (wide)
+    return wide_bwd_call(c, x, n, din, dout, L, W, mode, params, act, gy, gdy, glap, work, grad, accumulate, phases,
+                         A, (hipStream_t)stream);
   return fb_bwd_call(c, x, n, din, dout, L, W, mode, params, act, gy, gdy, glap, work, grad, accumulate, phases, A,
                      (hipStream_t)stream);
 }
@@ -1164,22 +1188,9 @@ int insr_siren_jet_bwd_grad(const float* x, long n, int din, int dout, int L, in
     return dispatch_resident_bwd(c.S, c.lap, L, x, (int)n, din, dout, params, act, gy, gdy, glap, work, grad,
                                  accumulate, st);
   }
-  if (c.wide(n)) {
-    hipStream_t st = (hipStream_t)stream;
-    int rc = 0;
-    if (!(params = with_planes(params, din, dout, L, W, mode, st, 0, &rc))) return rc;
-    switch (c.nqb) {
-      case 3:
-        return dispatch_wide_bwd_q<3>(c.NT, c.S, c.lap, x, (int)n, din, dout, L, params, act, gy, gdy, glap, work, grad,
-                                      accumulate, c.k.f16, st);
-      case 2:
-        return dispatch_wide_bwd_q<2>(c.NT, c.S, c.lap, x, (int)n, din, dout, L, params, act, gy, gdy, glap, work, grad,
-                                      accumulate, c.k.f16, st);
-      default:
-        return dispatch_wide_bwd_q<1>(c.NT, c.S, c.lap, x, (int)n, din, dout, L, params, act, gy, gdy, glap, work, grad,
-                                      accumulate, c.k.f16, st);
-    }
-  }
+  if (c.wide(n))
+    return wide_bwd_call(c, x, n, din, dout, L, W, mode, params, act, gy, gdy, glap, work, grad, accumulate, 3,
+                         AdamArgs{}, (hipStream_t)stream);
   int rc = insr_siren_jet_bwd(x, n, din, dout, L, W, mode, params, act, gy, gdy, glap, work, stream);
   if (rc) return rc;
   return insr_reduce_partials_strided(work, insr_jet_partial_blocks(n, din, W, mode),

@@ -3,7 +3,9 @@
 
 namespace insr {
 template int dispatch_wide_bwd_q<1>(int, int, bool, const float*, int, int, int, int, const float*, const float*,
-                                    const float*, const float*, const float*, float*, float*, int, int, hipStream_t);
+                                    const float*, const float*, const float*, float*, float*, int, int, int,
+                                    const AdamArgs&, hipStream_t);
 template int dispatch_wide_bwd_q<2>(int, int, bool, const float*, int, int, int, int, const float*, const float*,
-                                    const float*, const float*, const float*, float*, float*, int, int, hipStream_t);
+                                    const float*, const float*, const float*, float*, float*, int, int, int,
+                                    const AdamArgs&, hipStream_t);
 }  // namespace insr

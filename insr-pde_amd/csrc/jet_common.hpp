@@ -422,10 +422,24 @@ template <int NQ>
 int dispatch_bwd_q(int NT, int S, bool LAP, int T, const BwdJobsX6* jobs, int din, int dout, int L,
                    const float* prm, float* part, long P, hipStream_t st);
 // two-kernel backward (W = 128 / 256): propagation kernel + dW GEMM + reductions (jet_x6w.hpp)
+// The Adam (+ plateau) update a sums launch runs as its epilogue (reduce_dw_kernel with m != NULL,
+// optim.hpp): the flat parameter buffer and its moments, the optimiser state, the buffer's SIREN shape
+// (its weight planes), the plateau loss (NULL: Adam only); t = st[STEP] + 1 either way
+struct AdamArgs {
+  float* p = nullptr;
+  float* m = nullptr;
+  float* v = nullptr;
+  float* st = nullptr;
+  const float* loss = nullptr;
+  int patience = 0;
+  float b1 = 0.f, b2 = 0.f, eps = 0.f;
+  int shape[4] = {0, 0, 0, 0};
+};
+
 template <int NQ>
 int dispatch_wide_bwd_q(int NT, int S, bool LAP, const float* x, int N, int din, int dout, int L, const float* prm,
                         const float* act, const float* gy, const float* gdy, const float* glap, float* work,
-                        float* grad, int accumulate, int f16, hipStream_t st);
+                        float* grad, int accumulate, int f16, int phases, const AdamArgs& A, hipStream_t st);
 long wide_work_floats(long n, int din, int dout, int L, int W, int S);
 template <int NQ>
 int dispatch_fwd_mixed_q(int NT, int din, const InsrJetJob* jobs, const int* modes, const float* scalars, int njobs,
@@ -444,20 +458,6 @@ int resident_blocks(long n);
 
 // The jobs of one launch: batches of ONE network (its params), e.g. a phase's interior points and
 // its wall bands from separate network calls; job k covers global tiles [tstart[k], tstart[k + 1]).
-// The Adam (+ plateau) update a sums launch runs as its epilogue (reduce_dw_kernel with m != NULL,
-// optim.hpp): the flat parameter buffer and its moments, the optimiser state, the buffer's SIREN shape
-// (its weight planes), the plateau loss (NULL: Adam only); t = st[STEP] + 1 either way
-struct AdamArgs {
-  float* p = nullptr;
-  float* m = nullptr;
-  float* v = nullptr;
-  float* st = nullptr;
-  const float* loss = nullptr;
-  int patience = 0;
-  float b1 = 0.f, b2 = 0.f, eps = 0.f;
-  int shape[4] = {0, 0, 0, 0};
-};
-
 struct FbJobs {
   const float* x[kBwdJobs];
   const float* act[kBwdJobs];  // the forward's saved streams (the saved-stream variant; unread by recompute)

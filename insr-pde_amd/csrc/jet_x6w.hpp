@@ -772,7 +772,10 @@ __global__ __launch_bounds__(512) void reduce_dw_kernel(const float* __restrict_
     // runs element r's epilogue (its state loaded here, under the sums)
     const int ln = (int)(q & 63), f = (int)(q >> 6), nt = W / 16;
     const long d0 = hidden_off(din, W, j) + (long)(16 * (f / nt) + 4 * (ln >> 4)) * W + 16 * (f % nt) + (ln & 15);
-    if (frag && w < 4 && 4 * q < WW) preload(d0 + (long)w * W);
+    // frag = 0 (row-major partials) with an Adam epilogue: the quad's 4 consecutive elements alike
+    const bool per_elem = frag || A.m;
+    auto elem = [&](int r) -> long { return frag ? d0 + (long)r * W : hidden_off(din, W, j) + 4 * q + r; };
+    if (per_elem && w < 4 && 4 * q < WW) preload(elem(w));
     floatx4 acc = floatx4{0.f, 0.f, 0.f, 0.f};
     if (4 * q < WW) {
       const floatx4* col = reinterpret_cast<const floatx4*>(dpart + (long)(j - 1) * kslots * WW) + q;
@@ -788,7 +791,7 @@ __global__ __launch_bounds__(512) void reduce_dw_kernel(const float* __restrict_
     }
     red[w][lane] = acc;
     __syncthreads();
-    if (frag) {
+    if (per_elem) {
       if (w == 0 && 4 * q < WW) {  // the cross-wave sums in the fixed order, back into red[0]
         floatx4 t = floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -798,9 +801,9 @@ __global__ __launch_bounds__(512) void reduce_dw_kernel(const float* __restrict_
       __syncthreads();
       if (w < 4 && 4 * q < WW) {
         const float t = red[0][lane][w];
-        put(d0 + (long)w * W, accumulate ? g0 + t : t, m0, v0, p0);
+        put(elem(w), accumulate ? g0 + t : t, m0, v0, p0);
       }
-    } else if (w == 0 && 4 * q < WW) {  // (never with an Adam epilogue: the host passes A.m only with frag = 1)
+    } else if (w == 0 && 4 * q < WW) {  // row-major partials, no epilogue: one 16-B store per quad
       floatx4 t = floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int k = 0; k < 8; ++k) t += red[k][lane];
@@ -855,10 +858,11 @@ inline void wide_launch_threads_impl(long n, int din, int dout, int L, int W, in
   out[2] = (wq > rows_x ? wq : rows_x) * (L + 1) * 512;
 }
 
+// phases (L > 0): 1 the propagation + dW partials, 2 the sums (with A.m: + the Adam update), 3 both
 template <int NQ, int NT, int S, bool LAP>
 int wide_bwd_t(const float* x, int N, int din, int dout, int L, const float* prm, const float* act, const float* gy,
                const float* gdy, const float* glap, float* work, float* grad, int accumulate, int f16,
-               hipStream_t st) {
+               int phases, const AdamArgs& A, hipStream_t st) {
   constexpr int W = 16 * NT;
   const long ntiles = ((N + 63) / 64) * 4;
   const int tiles = (N + 15) / 16;
@@ -887,6 +891,17 @@ int wide_bwd_t(const float* x, int N, int din, int dout, int L, const float* prm
     return true;
   }();
   (void)attr;
+  if (L == 0 && phases != 3) return INSR_EINVAL;  // (the phase split is for the hidden-layer sums)
+  const int rs = tiles < kSmallRS ? tiles : kSmallRS;
+  const int rows_x = (int)((Ps + 63) / 64);
+  if (!(phases & 1)) {  // the sums alone
+    const int KS = wide_ks(N, S, L);
+    const int grad16 = (((uintptr_t)(grad + hidden_off(din, W, 1))) & 15) == 0 ? 1 : 0;
+    const int wq = (W * W / 4 + 63) / 64;
+    hipLaunchKernelGGL(reduce_dw_kernel, dim3((unsigned)(wq > rows_x ? wq : rows_x), L + 1), dim3(512), 0, st, dpart,
+                       KS, din, W, grad, accumulate, grad16, 0, L, rows, rs, Ps, dout, 1, KS, A);
+    return (int)hipGetLastError();
+  }
   bool launched = false;
   if constexpr (NQ == 3) {
     if (f16p) {
@@ -898,8 +913,6 @@ int wide_bwd_t(const float* x, int N, int din, int dout, int L, const float* prm
   if (!launched)
     hipLaunchKernelGGL((jet_bwd_x6p<NQ, NT, S, LAP>), dim3(tiles), dim3(512), lds_p, st, x, N, din, dout, L, prm, act,
                        gy, gdy, glap, adj, small, Ps, f16dw ? zmax : nullptr);
-  const int rs = tiles < kSmallRS ? tiles : kSmallRS;
-  const int rows_x = (int)((Ps + 63) / 64);
   if (L > 0) {  // 3 launches: propagation | dW partials + compact rows level 1 | dW sums + rows level 2
     const int KS = wide_ks(N, S, L);
     const int planes = (rows_x * rs + KS - 1) / KS;
@@ -914,10 +927,11 @@ int wide_bwd_t(const float* x, int N, int din, int dout, int L, const float* prm
     if (!done)
       hipLaunchKernelGGL((dw_x6<NQ, NT, S, LAP>), dim3(KS, L + planes), dim3(512), (dw_lds<NQ, NT>()), st, N, act, adj,
                          dpart, KS, L, small, tiles, Ps, rows, rs, rows_x, zmax, prm, din);
+    if (!(phases & 2)) return (int)hipGetLastError();
     const int grad16 = (((uintptr_t)(grad + hidden_off(din, W, 1))) & 15) == 0 ? 1 : 0;  // W % 4 == 0: all layers alike
     const int wq = (W * W / 4 + 63) / 64;
     hipLaunchKernelGGL(reduce_dw_kernel, dim3((unsigned)(wq > rows_x ? wq : rows_x), L + 1), dim3(512), 0, st, dpart,
-                       KS, din, W, grad, accumulate, grad16, 0, L, rows, rs, Ps, dout, 1, KS, AdamArgs{});
+                       KS, din, W, grad, accumulate, grad16, 0, L, rows, rs, Ps, dout, 1, KS, A);
     return (int)hipGetLastError();
   }
   hipLaunchKernelGGL(reduce_rows_kernel, dim3((unsigned)rows_x, rs), dim3(256), 0, st, small, tiles, Ps, rows);
@@ -929,15 +943,15 @@ int wide_bwd_t(const float* x, int N, int din, int dout, int L, const float* prm
 template <int NQ, int NT>
 int wide_bwd_nt(int S, bool LAP, const float* x, int N, int din, int dout, int L, const float* prm, const float* act,
                 const float* gy, const float* gdy, const float* glap, float* work, float* grad, int accumulate,
-                int f16, hipStream_t st) {
+                int f16, int phases, const AdamArgs& A, hipStream_t st) {
   switch (S * 2 + (LAP ? 1 : 0)) {
-    case 2: return wide_bwd_t<NQ, NT, 1, false>(x, N, din, dout, L, prm, act, gy, gdy, glap, work, grad, accumulate, f16, st);
-    case 4: return wide_bwd_t<NQ, NT, 2, false>(x, N, din, dout, L, prm, act, gy, gdy, glap, work, grad, accumulate, f16, st);
-    case 6: return wide_bwd_t<NQ, NT, 3, false>(x, N, din, dout, L, prm, act, gy, gdy, glap, work, grad, accumulate, f16, st);
-    case 8: return wide_bwd_t<NQ, NT, 4, false>(x, N, din, dout, L, prm, act, gy, gdy, glap, work, grad, accumulate, f16, st);
-    case 7: return wide_bwd_t<NQ, NT, 3, true>(x, N, din, dout, L, prm, act, gy, gdy, glap, work, grad, accumulate, f16, st);
-    case 9: return wide_bwd_t<NQ, NT, 4, true>(x, N, din, dout, L, prm, act, gy, gdy, glap, work, grad, accumulate, f16, st);
-    case 11: return wide_bwd_t<NQ, NT, 5, true>(x, N, din, dout, L, prm, act, gy, gdy, glap, work, grad, accumulate, f16, st);
+    case 2: return wide_bwd_t<NQ, NT, 1, false>(x, N, din, dout, L, prm, act, gy, gdy, glap, work, grad, accumulate, f16, phases, A, st);
+    case 4: return wide_bwd_t<NQ, NT, 2, false>(x, N, din, dout, L, prm, act, gy, gdy, glap, work, grad, accumulate, f16, phases, A, st);
+    case 6: return wide_bwd_t<NQ, NT, 3, false>(x, N, din, dout, L, prm, act, gy, gdy, glap, work, grad, accumulate, f16, phases, A, st);
+    case 8: return wide_bwd_t<NQ, NT, 4, false>(x, N, din, dout, L, prm, act, gy, gdy, glap, work, grad, accumulate, f16, phases, A, st);
+    case 7: return wide_bwd_t<NQ, NT, 3, true>(x, N, din, dout, L, prm, act, gy, gdy, glap, work, grad, accumulate, f16, phases, A, st);
+    case 9: return wide_bwd_t<NQ, NT, 4, true>(x, N, din, dout, L, prm, act, gy, gdy, glap, work, grad, accumulate, f16, phases, A, st);
+    case 11: return wide_bwd_t<NQ, NT, 5, true>(x, N, din, dout, L, prm, act, gy, gdy, glap, work, grad, accumulate, f16, phases, A, st);
     default: return INSR_EINVAL;
   }
 }
@@ -945,11 +959,13 @@ int wide_bwd_nt(int S, bool LAP, const float* x, int N, int din, int dout, int L
 template <int NQ>
 int dispatch_wide_bwd_q(int NT, int S, bool LAP, const float* x, int N, int din, int dout, int L, const float* prm,
                         const float* act, const float* gy, const float* gdy, const float* glap, float* work,
-                        float* grad, int accumulate, int f16, hipStream_t st) {
+                        float* grad, int accumulate, int f16, int phases, const AdamArgs& A, hipStream_t st) {
   if (NT == 16)
-    return wide_bwd_nt<NQ, 16>(S, LAP, x, N, din, dout, L, prm, act, gy, gdy, glap, work, grad, accumulate, f16, st);
+    return wide_bwd_nt<NQ, 16>(S, LAP, x, N, din, dout, L, prm, act, gy, gdy, glap, work, grad, accumulate, f16, phases,
+                               A, st);
   if (NT == 8)
-    return wide_bwd_nt<NQ, 8>(S, LAP, x, N, din, dout, L, prm, act, gy, gdy, glap, work, grad, accumulate, f16, st);
+    return wide_bwd_nt<NQ, 8>(S, LAP, x, N, din, dout, L, prm, act, gy, gdy, glap, work, grad, accumulate, f16, phases,
+                              A, st);
   return INSR_EWIDTH;
 }
 
