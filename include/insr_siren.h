@@ -69,7 +69,7 @@ extern "C" {
  *   INSR_JET_POLICY(p)     backward path: 0 auto, 1 fused tile-split where it exists, 2 two-kernel,
  *                          3 resident dW (bf16x6 kernel), 4 recompute where it applies, 5 resident dW
  *                          with f16x3 products (the saved-stream variant of the recompute kernel;
- *                          auto for 2-d Laplacian jets from 12,288 points) (insr_jet_bwd_path)
+ *                          auto for 2-d Laplacian jets from 4,096 points) (insr_jet_bwd_path)
  *   INSR_JET_BWD_F16(m)    mask of INSR_BWD_F16_* products of the x6 backward on the fp16 matrix
  *                          cores (0..7; without the field: all three)
  *   INSR_JET_TILES(f,b,m)  tile-split blocks: forced forward / backward tiles per block (0 auto,
@@ -262,7 +262,7 @@ int insr_jet_bwd_is_wide(long n_points, int d_in, int width, int mode);
  * resident-dW persistent kernel (W = 128, <= 4 hidden layers: every hidden layer's weight
  * gradient held in registers across the batch, the saved streams read once, no adjoint round
  * trip through memory; f16x3 products with per-tile scales for 4-hidden-layer nets while the
- * INSR_BWD_F16_FUSED bit is on -- the 2-d Laplacian jets from 12,288 points by default -- else
+ * INSR_BWD_F16_FUSED bit is on -- the 2-d Laplacian jets from 4,096 points by default -- else
  * bf16x6), 3 = the RECOMPUTE backward (W = 128, 4 hidden
  * layers, fp32-level backward precision: one persistent launch that reruns the forward jet of
  * each 16-point tile next to its reverse jet, dW resident per CU -- it reads no saved streams,

@@ -99,15 +99,17 @@ bool use_resident(long n, int S, int NT, bool lap, int nq, int L, const Knobs& k
 // Which kernel serves the resident path: the saved-stream variant of the recompute kernel (jet_fb.hpp
 // SAVED: the reverse sweep on the forward's saved streams, f16x3 products with per-tile scales; the
 // INSR_BWD_F16_FUSED bit of the call's mask) or jet_x6r.hpp (bf16x6 products).  Policy 5 forces the
-// former.  Auto: 2-d Laplacian jets from 12,288 points -- backward into .grad incl. sums (kbench r4j,
+// former.  Auto: 2-d Laplacian jets from 4,096 points -- backward into .grad incl. sums (kbench r4j,
 // profiles/r04/kbench_resident_f16.jsonl): 16,708 points 142 vs 166 us two-kernel, 33,092 239 vs
-// 296-301, 66,844 428 vs 577-582; 8,192 79 vs 73 (two-kernel); value jets lose at every size (S = 1:
-// 16-point tiles, 90 vs 57 fused at 16,708), so they keep their paths.
+// 296-301, 66,844 428 vs 577-582; value jets lose at every size (S = 1: 16-point tiles, 90 vs 57 fused
+// at 16,708), so they keep their paths.  Round 4, with both backwards' sums in the Adam launch: from
+// 4,096 points (the fluid2DtlgnM 8-way shard step, 8,192 + 163 points: 0.331-0.332 vs 0.345-0.347 ms
+// with the two-kernel path, profiles/r04/ab_fb_shard/).
 bool use_resident_f16(long n, int S, int NT, bool lap, int nq, int L, const Knobs& k) {
   if (NT != 8 || nq != 3 || !fb_supported(S, lap, L)) return false;
   if (k.policy == 5) return true;
   if (k.policy != 0 || !(k.f16 & INSR_BWD_F16_FUSED)) return false;
-  return lap && S == 4 && n >= 12288;
+  return lap && S == 4 && n >= 4096;
 }
 
 // Matrix-core precision of the tile-split kernels (a call's INSR_JET_PREC(p) / INSR_JET_BPREC(p);

@@ -182,7 +182,7 @@ def test_value_backward_launch_shape(lib):
 
 def test_backward_path_policy(lib):
     """insr_jet_bwd_path answers on the host: the resident-dW path for the fluid nets' Laplacian
-    backward from 12,288 points (its f16x3 saved-stream kernel while the INSR_BWD_F16_FUSED bit is on,
+    backward from 4,096 points (its f16x3 saved-stream kernel while the INSR_BWD_F16_FUSED bit is on,
     else -- with bf16x6 products -- the two-kernel path below 32,768 points), two-kernel at W = 256, the fused kernel for value jets below 24,576 points
     (two-kernel from there), the resident-dW kernel for the fluid2DtlgnM value batch (from 49,152
     points) or when forced (policy 3); policy 4 forces the recompute backward (path 3: no saved
@@ -192,8 +192,9 @@ def test_backward_path_policy(lib):
     V, G, LAP = nat.MODE_VALUE, nat.MODE_GRAD, nat.MODE_LAP
     P = nat.jet_policy
     assert lib.insr_jet_bwd_path(16708, 2, 1, 4, 128, LAP) == 2
-    assert lib.insr_jet_bwd_path(12288, 2, 1, 4, 128, LAP) == 2
-    assert lib.insr_jet_bwd_path(12287, 2, 1, 4, 128, LAP) == 1
+    assert lib.insr_jet_bwd_path(8192 + 163, 2, 1, 4, 128, LAP) == 2   # the fluid2DtlgnM 8-way shard
+    assert lib.insr_jet_bwd_path(4096, 2, 1, 4, 128, LAP) == 2
+    assert lib.insr_jet_bwd_path(4095, 2, 1, 4, 128, LAP) in (0, 1)
     assert lib.insr_jet_bwd_path(16708, 2, 1, 4, 128, LAP | nat.jet_bwd_f16(3)) == 1  # bf16x6 resident: >= 32,768
     assert lib.insr_jet_bwd_path(16708, 2, 2, 4, 128, V) == 0
     assert lib.insr_jet_bwd_path(1024, 2, 2, 4, 128, V) == 0
