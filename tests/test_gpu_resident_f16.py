@@ -95,6 +95,29 @@ def test_value_and_gradient_jets_vs_oracle(B, kind, n):
         assert nerr(b, a) < TOL, (kind, n, k, nerr(b, a))
 
 
+@pytest.mark.parametrize("n", [4096, 8192 + 163])
+def test_auto_policy_shard_sizes_vs_oracle(B, n):
+    """The default policy takes this kernel from 4,096 points (the fluid2DtlgnM 8-way shard's
+    pressure batch, 8,192 interior + 163 band points; fluid/model.py:103-125): the pressure loss's
+    Laplacian adjoint, each parameter gradient vs the oracle."""
+    lib = B._native.lib()
+    with B._native.knobs(policy=0):
+        assert lib.insr_jet_bwd_path(n, 2, 1, 4, 128, LAP | B._native.scope_bits()) == 2
+        ref, net = pair(B, 2, 1, 4, 128, seed=74)
+        x = torch.rand(n, 2, generator=torch.Generator().manual_seed(n)) * 2 - 1
+        xr = x.clone().requires_grad_(True)
+        lr_ = O.op_laplace(ref(xr), xr)
+        R = torch.randn(lr_.shape, generator=torch.Generator().manual_seed(n + 2))
+        (lr_ * R).sum().backward()
+        xg = x.cuda().requires_grad_(True)
+        lp = B.laplace(net(xg), xg)
+        (lp * R.cuda()).sum().backward()
+        torch.cuda.synchronize()
+        assert nerr(lp, lr_) < TOL
+        for (k, _), a, b in zip(ref.named_parameters(), ref_grads(ref), grads(net)):
+            assert nerr(b, a) < TOL, (n, k, nerr(b, a))
+
+
 @pytest.mark.parametrize("n", [300, 16708])
 def test_matches_two_kernel_path(B, n):
     """Same network and adjoints: this kernel vs the saved-stream two-kernel backward (policy 2)."""
