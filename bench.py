@@ -196,12 +196,10 @@ def build_model(args, world, rank):
         if wl["pde"] in ("fluid", "advection"):
             cfg.insr_points_per_rank = n_global // args.shard_of
             return finish_model(args, cfg, wl, world, rank, n_global // args.shard_of)
-        r = round(res / args.shard_of ** (1.0 / cfg.dim))
-        if r ** cfg.dim * args.shard_of != res ** cfg.dim:
-            raise SystemExit(f"--shard-of {args.shard_of}: {res}^{cfg.dim} points do not split into cubes")
-        cfg.sample_resolution = r
-        cfg.insr_dp_weak = True
-        return finish_model(args, cfg, wl, world, rank, interior_points(cfg, wl))
+        # elasticity: rank 0's share of the global draw through the strong-scaling code itself
+        # (ElasticityModel._shard / _rows: each part's N / K rows drawn, nothing world-sized)
+        cfg.insr_shard = (0, args.shard_of)
+        return finish_model(args, cfg, wl, world, rank, n_global // args.shard_of)
     if wl["pde"] in ("fluid", "advection"):
         # strong: the global batch is split over ranks; weak: every rank keeps the full batch
         cfg.insr_points_per_rank = n_global // world if args.scaling == "strong" else n_global

@@ -592,6 +592,14 @@ typedef struct InsrBox {
 long insr_sampler_state_bytes(void);
 int insr_sample_boxes(const InsrBox* boxes, int n_boxes, int dim, unsigned long long seed, void* state,
                       void* stream);
+/*
+ * The draws of `reps` consecutive iterations in ONE launch (a hipGraph that replays U iterations
+ * draws all of their points up front): repetition r of box k writes boxes[k].n fresh points at
+ * boxes[k].out + r * rep_strides[k] floats.  reps = 1 (rep_strides may be NULL) is
+ * insr_sample_boxes.  Same stream, same distributions (base/sampling.py draw_ahead).
+ */
+int insr_sample_boxes_rep(const InsrBox* boxes, int n_boxes, int dim, int reps, const long* rep_strides,
+                          unsigned long long seed, void* state, void* stream);
 
 #ifdef __cplusplus
 }

@@ -14,14 +14,17 @@ Recognised shapes of `y` (everything the reference models use):
   * y = mlp(x)                          (advection, fluid)
   * y = mlp(x) + x   /  x + mlp(x)      (elasticity/model.py:137, q = f(x) + x)
   * y = gradient(mlp(x), x)  inside divergence  (-> Laplacian stream)
-Anything else raises UnsupportedPattern (there is no silent fallback).
+Anything else is not fused: match() returns None and base/diff_ops.py takes the reference's
+own route -- torch.autograd.grad(..., create_graph=True) -- through the graph.  A jet node
+reached by such a create_graph pass differentiates itself with torch ops on the device
+(torch_jet / _reference_backward: the reference semantics to any order, slower); the
+library stays mandatory (the forwards are HIP; no CPU path exists).
 """
 import ctypes
 import os
 import threading
 
 import torch
-from torch.autograd.function import once_differentiable
 
 from . import _native as nat
 
@@ -111,10 +114,13 @@ class _SirenJet(torch.autograd.Function):
         return tuple(outs)
 
     @staticmethod
-    @once_differentiable
     def backward(ctx, *grads):
         mlp, mode = ctx.mlp, ctx.mode
         none = (None,) * (4 + len(mlp.plist()))
+        if torch.is_grad_enabled():
+            # create_graph=True: the caller differentiates THROUGH this jet (a diff op on a graph the
+            # jet matcher does not recognise, base/diff_ops.py fallback): reference semantics
+            return _reference_backward(ctx, grads)
         if not ctx.save or not any(p.requires_grad for p in mlp.plist()):
             return none
         gy = grads[0]
@@ -124,11 +130,82 @@ class _SirenJet(torch.autograd.Function):
             return none
         c = lambda t: None if t is None else (t if t.is_contiguous() else t.contiguous())  # noqa: E731
         job = _BwdJob(mlp, mode, ctx.cmode, ctx.x2, ctx.act, c(gy), c(gdy), c(glap))
-        if _BwdBatch.pending is not None:  # launched with the network's other jobs at the scope's exit
-            _BwdBatch.pending.append(job)
+        queue = _BwdBatch.queue_for(job)
+        if queue is not None:  # launched with the network's other jobs at the scope's exit
+            queue.append(job)
         else:
             _launch_bwd(job)
         return none
+
+
+def torch_jet(mlp, x2, mode):
+    """The jet of `mlp` at x2 (n, d_in) as plain, differentiable torch ops on x2's device: (y, dy, lap)
+    with dy (n, d_out, d_in) for GRAD / LAP and lap (n, d_out) for LAP, the streams the HIP kernels
+    carry (z = W h + b on every stream, bias on the value only; h = sin(w z),
+    dh_i = w cos(w z) t_i, ddh = w cos(w z) q - w^2 sin(w z) sum_i t_i^2).  Reference semantics for
+    graphs the jet matcher does not recognise: autograd differentiates this to any order, w.r.t. x2
+    and the parameters (what base/diff_ops.py:6-82 get from torch.autograd.grad(create_graph=True)
+    through the reference's nn.Sequential, base/networks.py:67-71)."""
+    omega = 30.0
+    ps = mlp.plist()
+    L = mlp.num_hidden_layers
+    ntan = x2.shape[1] if mode != nat.MODE_VALUE else 0
+    lapm = mode == nat.MODE_LAP
+    w0, b0 = ps[0], ps[1]
+    z = torch.addmm(b0, x2, w0.t())
+    t = [w0[:, i].unsqueeze(0) for i in range(ntan)]  # first layer: the tangents are W_0's columns
+    q = None  # first layer: zero Laplacian stream
+    for layer in range(1, L + 2):
+        s = torch.sin(omega * z)
+        if ntan:
+            c = omega * torch.cos(omega * z)
+            dh = [c * ti for ti in t]
+            if lapm:
+                t2 = sum(ti * ti for ti in t)
+                ddh = -(omega * omega) * s * t2 if q is None else c * q - (omega * omega) * s * t2
+        wl, bl = ps[2 * layer], ps[2 * layer + 1]
+        z = torch.addmm(bl, s, wl.t())
+        if ntan:
+            t = [dhi @ wl.t() for dhi in dh]
+            if lapm:
+                q = ddh @ wl.t()
+    dy = torch.stack(t, dim=-1) if ntan else None
+    return z, dy, (q if lapm else None)
+
+
+def _reference_backward(ctx, grads):
+    """_SirenJet.backward under create_graph=True: the input / parameter gradients of
+    sum(g_y y + g_dy dy + g_lap lap), as a differentiable graph of torch ops (torch_jet on the
+    forward's own x2, so derivatives of the result reach x through x2's graph)."""
+    mlp, mode, x2 = ctx.mlp, ctx.mode, ctx.x2
+    params = mlp.plist()
+    none = (None,) * (4 + len(params))
+    want_x = ctx.needs_input_grad[0]
+    pidx = [i for i in range(len(params)) if ctx.needs_input_grad[4 + i]]
+    if not want_x and not pidx:
+        return none
+    outs = torch_jet(mlp, x2, mode)
+    total = None
+    for o, g in zip(outs, grads):
+        if o is not None and g is not None:
+            term = (o * g).sum()
+            total = term if total is None else total + term
+    if total is None:
+        return none
+    ins = ([x2] if want_x else []) + [params[i] for i in pidx]
+    gs = torch.autograd.grad(total, ins, create_graph=True, allow_unused=True)
+    res = [None] * len(none)
+    k = 0
+    if want_x:
+        res[0], k = gs[0], 1
+    for i in pidx:
+        res[4 + i] = gs[k]
+        k += 1
+    REF_STATS["backward"] += 1
+    return tuple(res)
+
+
+REF_STATS = {"backward": 0}  # reference-semantics (create_graph) backwards run through _SirenJet
 
 
 class _BwdJob:
@@ -317,7 +394,22 @@ def _launch_bwd_multi(jobs):
 
 
 class _BwdBatch:
-    pending = None  # list of _BwdJob while a batched_backward scope is open
+    """Open batched_backward scopes, keyed by the CUDA stream they were opened on: autograd runs a
+    CUDA backward on its device worker thread (not the thread that called backward), so a
+    thread-local list would miss the jobs; keyed by stream, a scope collects exactly the reverse
+    jets of its own stream (the re-entrancy model is one training thread per stream) and never
+    launches another thread's jobs."""
+    pending = {}  # stream handle -> list of _BwdJob while a scope is open on that stream
+    lock = threading.Lock()
+
+    @staticmethod
+    def key(dev=None):
+        return torch.cuda.current_stream(dev).cuda_stream if torch.cuda.is_available() else 0
+
+    @classmethod
+    def queue_for(cls, job):
+        with cls.lock:
+            return cls.pending.get(job.cur.cuda_stream)
 
 
 class batched_backward:
@@ -328,33 +420,41 @@ class batched_backward:
     Valid because the reverse jets return no gradient to autograd (they write the networks'
     flat .grad directly, and x gets none), so nothing inside the backward pass reads their
     results; .grad holds them when the scope exits.  BaseModel._backward opens it around the
-    loss backward of every iteration."""
+    loss backward of every iteration.  The scope collects the jobs of the stream it was opened on."""
 
     def __enter__(self):
-        self.outer = _BwdBatch.pending is None
-        if self.outer:
-            _BwdBatch.pending = []
+        self.k = _BwdBatch.key()
+        with _BwdBatch.lock:
+            self.outer = self.k not in _BwdBatch.pending
+            if self.outer:
+                _BwdBatch.pending[self.k] = []
         return self
 
     def __exit__(self, exc_type, *exc):
         if not self.outer:
             return False
-        jobs, _BwdBatch.pending = _BwdBatch.pending, None
+        with _BwdBatch.lock:
+            jobs = _BwdBatch.pending.pop(self.k)
         if exc_type is None:
             _flush_backward(jobs)
         return False
 
 
 class immediate_backward:
-    """Suspends an open batched_backward scope: a backward run inside (a custom autograd node that
-    reads .grad right after its own nested backward, diff_ops._AugLaplacian) launches at once."""
+    """Suspends the batched_backward scope of the current stream: a backward run inside (a custom
+    autograd node that reads .grad right after its own nested backward, diff_ops._AugLaplacian)
+    launches at once."""
 
     def __enter__(self):
-        self.saved, _BwdBatch.pending = _BwdBatch.pending, None
+        self.k = _BwdBatch.key()
+        with _BwdBatch.lock:
+            self.saved = _BwdBatch.pending.pop(self.k, None)
         return self
 
     def __exit__(self, *exc):
-        _BwdBatch.pending = self.saved
+        if self.saved is not None:
+            with _BwdBatch.lock:
+                _BwdBatch.pending[self.k] = self.saved
         return False
 
 
@@ -369,8 +469,11 @@ def _flush_backward(jobs):
             _launch_bwd_multi(js)
 
 
-class _Fused:
-    pending = None  # list of (arch key, job) while a fused_forwards scope is open
+class _FusedState(threading.local):
+    pending = None  # per thread: list of (arch key, job) while a fused_forwards scope is open
+
+
+_Fused = _FusedState()  # (forward jets run on the calling thread: thread-local)
 
 
 class fused_forwards:

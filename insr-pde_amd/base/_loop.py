@@ -19,8 +19,9 @@ Differences, all controlled by cfg attributes:
   insr_graph_unroll (int, default 1) -- single process only: U > 1 also captures U
       consecutive iterations into ONE graph and replays that for every group of U
       iterations that holds no host read (sync / vis point) before its last one.  Each
-      iteration inside is a full one (its own sampler draw, backward, Adam + plateau
-      step); what it saves is the host's replay call per iteration (under a kernel
+      iteration inside is a full one (its own collocation points, backward, Adam + plateau
+      step; the U iterations' points come from ONE sampler launch at the group's start,
+      base.sampling.draw_ahead); it also saves the host's replay call per iteration (under a kernel
       trace, whose per-launch host work makes the host the bottleneck, ~8.7 us of idle
       device between two replays; without a profiler the host stays ahead and U = 1 and
       U = 4 measure the same, profiles/r04/final_v1/unroll_ab_*).
@@ -28,7 +29,7 @@ Differences, all controlled by cfg attributes:
 import torch
 
 from . import _jet
-from .sampling import draw_plan
+from .sampling import draw_ahead, draw_plan
 
 try:
     from tqdm import tqdm
@@ -133,8 +134,9 @@ class PhaseLoop:
 
     def _bodies(self):
         out = None
-        for _ in range(self.unroll):
-            out = self._body()
+        with draw_ahead(self.unroll):  # the group's collocation draws: one sampler launch up front
+            for _ in range(self.unroll):
+                out = self._body()
         return out
 
     def can_group(self):
@@ -237,5 +239,10 @@ class PhaseLoop:
                     break
             if (i == 0 or (i + 1) % self.vis_every == 0) and hasattr(m, f"_vis{self.tag}"):
                 getattr(m, f"_vis{self.tag}")()
+        # the fp16 weight planes' range guard at the phase's end too, whatever insr_sync_every is (a
+        # loop that never syncs -- bench.py's 1e9 -- is still checked once per phase)
+        for net in m._trainable_networks.values():
+            if hasattr(net, "check_weight_planes"):
+                net.check_weight_planes()
         self.graph = self.graph2 = None
         self.static = None

@@ -189,6 +189,7 @@ SIGNATURES = {
     "insr_adam_step_multi": (_I, [_I, _P, _P, _P, _P, _P, _P, _F, _F, _F, _I, _P]),
     "insr_sampler_state_bytes": (_L, []),
     "insr_sample_boxes": (_I, [_P, _I, _I, ctypes.c_ulonglong, _P, _P]),
+    "insr_sample_boxes_rep": (_I, [_P, _I, _I, _I, _P, ctypes.c_ulonglong, _P, _P]),
     "insr_adam_step": (_I, [_P, _P, _P, _P, _L, _P, _F, _F, _F, _P]),
 }
 

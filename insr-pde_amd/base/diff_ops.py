@@ -16,7 +16,19 @@ base/_jet.py) and assembles the requested quantity from its streams:
 
 All results stay differentiable w.r.t. the network parameters (loss.backward()
 runs the HIP reverse jet).  `status` is returned, never raised (-1 on NaN).
+
+Reference-semantics fallback.  A graph the jet path does not serve -- y post-processed
+before differentiation (2 * net(x), net(x)[..., :1] ** 2, a sum of two networks), the
+divergence of a weighted or normalised gradient, Hessians of d_in = 3 inputs, widths or
+shapes without a compiled kernel -- takes the reference's own route: torch.autograd.grad(...,
+create_graph=True) through y's graph (_ref_* below, restating base/diff_ops.py:6-82).  The jet
+nodes in that graph differentiate themselves with torch ops on the device (base/_jet.py
+torch_jet), so the result is exact to any order and differentiable for loss.backward(); it
+is slower, and counted in FALLBACKS.  CPU tensors still raise NativeUnavailable (the
+networks' forwards are HIP-only).
 """
+import warnings
+
 import torch
 
 from . import _jet
@@ -25,23 +37,88 @@ from .networks import MLP
 
 __all__ = ["hessian", "laplace", "divergence", "gradient", "jacobian"]
 
+FALLBACKS = {}  # op name -> calls served by the reference-semantics route
+
+
+def _fallback(opname, why):
+    """Book-keeping of one reference-semantics call (a warning on the first one per op)."""
+    if _jet._Fused.pending is not None:
+        raise _jet.UnsupportedPattern(f"{opname} of an unfused graph inside a fused_forwards scope: its jets have "
+                                      "no values until the scope exits")
+    FALLBACKS[opname] = FALLBACKS.get(opname, 0) + 1
+    if FALLBACKS[opname] == 1:
+        warnings.warn(f"{opname}: {why}; using the reference-semantics autograd route (torch ops, slower)",
+                      stacklevel=3)
+
+
+# ---- the reference's definitions (base/diff_ops.py:6-82), used when the jet path does not apply ----
+def _ref_grad(y, x, grad_outputs):
+    """autograd.grad(y, [x], grad_outputs, create_graph=True)[0] (base/diff_ops.py:53-58)."""
+    return torch.autograd.grad(y, [x], grad_outputs=grad_outputs, create_graph=True)[0]
+
+
+def _ref_gradient(y, x, grad_outputs=None):
+    return _ref_grad(y, x, torch.ones_like(y) if grad_outputs is None else grad_outputs)
+
+
+def _ref_divergence(y, x):
+    """sum_i d y_i / d x_i, one reverse pass per component (base/diff_ops.py:44-50)."""
+    div = 0.
+    for i in range(y.shape[-1]):
+        yi = y[..., i]
+        div = div + _ref_grad(yi, x, torch.ones_like(yi))[..., i:i + 1]
+    return div
+
+
+def _ref_jacobian_rows(y, x):
+    """(..., dim_y, dim_x) from dim_y reverse passes (base/diff_ops.py:61-82, without the status)."""
+    rows = []
+    for i in range(y.shape[-1]):
+        yi = y[..., i]
+        rows.append(_ref_grad(yi, x, torch.ones_like(yi)))
+    return torch.stack(rows, dim=-2)
+
+
+def _ref_hessian(y, x):
+    """(..., channels, dim, dim): row j of channel i = d(d y_i / d x_j)/dx (base/diff_ops.py:6-30)."""
+    out = []
+    for i in range(y.shape[-1]):
+        yi = y[..., i]
+        g = _ref_grad(yi, x, torch.ones_like(yi))
+        out.append(torch.stack([_ref_grad(g[..., j], x, torch.ones_like(g[..., j])) for j in range(x.shape[-1])],
+                               dim=-2))
+    return torch.stack(out, dim=-3)
+
 
 def _resolve(y, x, opname):
+    """(mlp, holder, affine) of a recognised SIREN graph, ("gradient-of", ...) for the divergence of a
+    jet gradient, or None (the reference-semantics route)."""
     m = _jet.match(y, x)
     if m is None:
         gsrc = getattr(y, "_insr_gradient_of", None)
         if gsrc is not None and gsrc[1] is x and opname == "divergence":
             return ("gradient-of",) + gsrc
-        raise _jet.UnsupportedPattern(
-            f"{opname}(y, x): y is not a SIREN output of x (or f(x) + x) produced by base.MLP; "
-            "the HIP path only differentiates recognised SIREN graphs")
+        return None
     return m
+
+
+def _jet_or_none(mlp, holder, x, mode):
+    """The fused jet, or None when no kernel serves this network in `mode` (fallback)."""
+    try:
+        return _jet.jet_of(mlp, holder, x, mode)
+    except _jet.UnsupportedPattern:
+        return None
 
 
 def gradient(y, x, grad_outputs=None):
     """d(sum_c grad_outputs_c * y_c)/dx, shape x.shape (base/diff_ops.py:53-58)."""
-    mlp, value, affine = _resolve(y, x, "gradient")
-    _, J, _ = _jet.jet_of(mlp, value, x, nat.MODE_GRAD)  # (..., dout, din)
+    r = _resolve(y, x, "gradient")
+    res = _jet_or_none(r[0], r[1], x, nat.MODE_GRAD) if r is not None else None
+    if res is None:
+        _fallback("gradient", "y is not a fused SIREN output of x" if r is None else "no kernel for this network")
+        return _ref_gradient(y, x, grad_outputs)
+    mlp, value, affine = r
+    _, J, _ = res  # (..., dout, din)
     if grad_outputs is None:
         # scalar net: a view (no launch, and its backward is a view too)
         g = J.squeeze(-2) if J.shape[-2] == 1 else J.sum(dim=-2)
@@ -59,15 +136,21 @@ def gradient(y, x, grad_outputs=None):
 def divergence(y, x):
     """sum_i dy_i/dx_i, shape (..., 1) (base/diff_ops.py:44-50)."""
     r = _resolve(y, x, "divergence")
-    if r[0] == "gradient-of":
+    if r is not None and r[0] == "gradient-of":
         # divergence(gradient(f, x), x) with unit grad_outputs == laplace(f, x)
         _, mlp, _, value, affine, unit = r
-        if not unit:
-            raise _jet.UnsupportedPattern("divergence of a weighted gradient is not fused")
-        _, _, lap = _jet.jet_of(mlp, value, x, nat.MODE_LAP)
+        res = _jet_or_none(mlp, value, x, nat.MODE_LAP) if unit else None
+        if res is None:
+            _fallback("divergence", "the divergence of a weighted gradient" if not unit else "no Laplacian kernel")
+            return _ref_divergence(y, x)
+        lap = res[2]
         return lap if lap.shape[-1] == 1 else lap.sum(dim=-1, keepdim=True)
+    res = _jet_or_none(r[0], r[1], x, nat.MODE_GRAD) if r is not None else None
+    if res is None:
+        _fallback("divergence", "y is not a fused SIREN output of x" if r is None else "no kernel for this network")
+        return _ref_divergence(y, x)
     mlp, value, affine = r
-    _, J, _ = _jet.jet_of(mlp, value, x, nat.MODE_GRAD)
+    _, J, _ = res
     k = min(J.shape[-2], J.shape[-1])
     if k == 1:
         div = J[..., 0, :1]
@@ -83,11 +166,18 @@ def divergence(y, x):
 def laplace(y, x, normalize=False, eps=0., return_grad=False):
     """div(grad y) (base/diff_ops.py:33-41).  normalize=True: div(g / (|g| + eps)), g = grad y,
     = tr(H) / (|g| + eps) - g.H g / (|g| (|g| + eps)^2) with H the Hessian of sum_c y_c
-    (hessian(): d_in <= 2)."""
+    (hessian(): d_in <= 2; otherwise the reference's route)."""
     if normalize:
         return _laplace_normalized(y, x, eps, return_grad)
-    mlp, value, affine = _resolve(y, x, "laplace")
-    _, J, lap = _jet.jet_of(mlp, value, x, nat.MODE_LAP)
+    r = _resolve(y, x, "laplace")
+    res = _jet_or_none(r[0], r[1], x, nat.MODE_LAP) if r is not None else None
+    if res is None:
+        _fallback("laplace", "y is not a fused SIREN output of x" if r is None else "no Laplacian kernel")
+        g = gradient(y, x)
+        div = _ref_divergence(g, x)
+        return (div, g) if return_grad else div
+    mlp, value, affine = r
+    _, J, lap = res
     # the identity part of f(x)+x has zero Laplacian; a scalar net needs no reduction launch
     div = lap if lap.shape[-1] == 1 else lap.sum(dim=-1, keepdim=True)
     if return_grad:
@@ -100,10 +190,7 @@ def laplace(y, x, normalize=False, eps=0., return_grad=False):
 
 def jacobian(y: torch.FloatTensor, x: torch.FloatTensor):
     """(N, dim_y, dim_x) Jacobian and status (-1 if NaN) (base/diff_ops.py:61-82)."""
-    mlp, value, affine = _resolve(y, x, "jacobian")
-    _, J, _ = _jet.jet_of(mlp, value, x, nat.MODE_GRAD)
-    if affine:
-        J = J + torch.eye(J.shape[-1], device=J.device, dtype=J.dtype)
+    J = jacobian_only(y, x)
     status = -1 if bool(torch.isnan(J).any()) else 0
     return J, status
 
@@ -116,8 +203,13 @@ def jacobian_nosync(y, x):
 
 def jacobian_only(y, x):
     """The (N, dim_y, dim_x) Jacobian of jacobian() alone: no status (no NaN scan launches)."""
-    mlp, value, affine = _resolve(y, x, "jacobian")
-    _, J, _ = _jet.jet_of(mlp, value, x, nat.MODE_GRAD)
+    r = _resolve(y, x, "jacobian")
+    res = _jet_or_none(r[0], r[1], x, nat.MODE_GRAD) if r is not None else None
+    if res is None:
+        _fallback("jacobian", "y is not a fused SIREN output of x" if r is None else "no kernel for this network")
+        return _ref_jacobian_rows(y, x)
+    mlp, value, affine = r
+    _, J, _ = res
     if affine:
         J = J + torch.eye(J.shape[-1], device=J.device, dtype=J.dtype)
     return J
@@ -125,7 +217,16 @@ def jacobian_only(y, x):
 
 def _laplace_normalized(y, x, eps, return_grad):
     g = gradient(y, x)
-    H = _hessian_core(y, x, "laplace(normalize=True)").sum(dim=-3)  # Hessian of sum_c y_c
+    try:
+        H = _hessian_core(y, x, "laplace(normalize=True)").sum(dim=-3)  # Hessian of sum_c y_c
+    except _jet.UnsupportedPattern:
+        if _jet._Fused.pending is not None:
+            raise
+        # base/diff_ops.py:33-41 as written: div(g / (|g| + eps))
+        _fallback("laplace", "normalize=True beyond the polarised Hessian jets")
+        gn = g / (g.norm(dim=-1, keepdim=True) + eps)
+        div = _ref_divergence(gn, x)
+        return (div, gn) if return_grad else div
     gn = g.norm(dim=-1, keepdim=True)
     gHg = torch.einsum("...i,...ij,...j->...", g, H, g).unsqueeze(-1)
     tr = laplace(y, x)  # tr(H) straight from the Laplacian stream (no polarisation error)
@@ -184,17 +285,21 @@ class _AugLaplacian(torch.autograd.Function):
 
 
 def _hessian_core(y, x, opname):
-    """(..., d_out, d_in, d_in) Hessian of each output channel (no status)."""
-    mlp, value, affine = _resolve(y, x, opname)
+    """(..., d_out, d_in, d_in) Hessian of each output channel (no status); UnsupportedPattern where the
+    polarised jets do not apply (the callers fall back)."""
+    r = _resolve(y, x, opname)
+    if r is None or r[0] == "gradient-of":
+        raise _jet.UnsupportedPattern(f"{opname}: y is not a fused SIREN output of x")
+    mlp, value, affine = r
     if _jet._Fused.pending is not None:
         raise _jet.UnsupportedPattern(f"{opname} inside a fused_forwards scope (its jets' values are read at once)")
     d = mlp.in_features
+    if d > 2:
+        raise _jet.UnsupportedPattern(f"{opname}: Hessians of d_in = {d} inputs (d_in <= 2: the augmented "
+                                      "Laplacian jet of f(x + s v) has d_in + 1 <= 3 inputs)")
     _, _, L0 = _jet.jet_of(mlp, value, x, nat.MODE_LAP)  # (..., c): tr(H)
     if d == 1:
         return L0[..., None, None]
-    if d != 2:
-        raise _jet.UnsupportedPattern(f"{opname}: Hessians of d_in = {d} inputs (d_in <= 2: the augmented "
-                                      "Laplacian jet of f(x + s v) has d_in + 1 <= 3 inputs)")
     x2, lead = _jet._flatten_x(x, d)
     params = tuple(mlp.parameters())
     L0f = L0.reshape(-1, L0.shape[-1])
@@ -212,8 +317,14 @@ def _hessian_core(y, x, opname):
 def hessian(y, x):
     """base/diff_ops.py:6-30: y (meta, obs, channels), x (meta, obs, dim) -> the Hessian
     (meta, obs, channels, dim, dim) and status (-1 if NaN); 2-D y, x give (N, channels, dim, dim).
-    d_in <= 2 (the reference never calls it on the INSR-PDE path).  The identity part of
-    f(x) + x has zero Hessian."""
-    H = _hessian_core(y, x, "hessian")
+    The polarised jets serve d_in <= 2; other inputs (and unfused graphs) take the reference's
+    route.  The identity part of f(x) + x has zero Hessian."""
+    try:
+        H = _hessian_core(y, x, "hessian")
+    except _jet.UnsupportedPattern:
+        if _jet._Fused.pending is not None:
+            raise
+        _fallback("hessian", "beyond the polarised Hessian jets (d_in <= 2 SIREN outputs)")
+        H = _ref_hessian(y, x)
     status = -1 if bool(torch.isnan(H).any()) else 0
     return H, status

@@ -392,9 +392,14 @@ class MLP(nn.Module):
         return self.__dict__.pop('_insr_pending_reduce', None)
 
     def flush_pending_reduce(self):
+        """Land held-back sums now, on the stream their reverse jet ran on -- ordered after any
+        earlier .grad write made on another stream, and recorded as the last write, so a reader
+        on another stream (grad_read_sync) waits for the sums, not only for the sweep."""
         pr = self.take_pending_reduce()
         if pr is not None:
+            self.grad_write_begin(pr.cur)
             _jet.launch_reduce(pr)
+            self.grad_write_end(pr.cur)
 
     def mark_grad_stale(self, set_to_none=True):
         self.take_pending_reduce()  # zero_grad: the held-back sums would write a discarded gradient

@@ -109,8 +109,9 @@ class FusedAdam:
         cur = torch.cuda.current_stream(self.device)
         for mlp, m, v in self._nets:
             if mlp.grad_touched():  # torch skips params whose .grad is None
-                mlp.grad_read_sync(cur)  # a backward may have written .grad on a side stream
-                bufs.append((mlp.flat_params(), mlp.flat_grad_buffer(), m, v,
+                g = mlp.flat_grad_buffer()  # held-back sums land first (their write is recorded) ...
+                mlp.grad_read_sync(cur)  # ... then wait for the last .grad write if it ran on a side stream
+                bufs.append((mlp.flat_params(), g, m, v,
                              (mlp.in_features, mlp.out_features, mlp.num_hidden_layers, mlp.kernel_width)))
                 stepped.append(mlp)
         for p, m, v in self._loose:

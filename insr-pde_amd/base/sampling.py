@@ -9,6 +9,8 @@ with no host-side generator update), instead of up to 13 launches for a pair of
 boundary bands: same distributions, another stream -- parity tests pass explicit
 sample tensors.
 """
+import ctypes
+
 import torch
 
 _AFFINE = {}  # (N, side-key, epsilon, device) -> (scale, shift) constant tensors
@@ -120,7 +122,7 @@ def merge_samples(*parts):
     return torch.cat([p.detach() for p in parts]).requires_grad_(True)
 
 
-_SAMPLER = {}  # device index -> (Philox stream position on the device, key, torch seed, reseed mark)
+_SAMPLER = {}  # device index -> (Philox stream position on the device, key, torch seed, reseed epoch)
 
 
 def sampler_seed(torch_seed, rank):
@@ -135,27 +137,54 @@ def _dp_rank():
     return d.get_rank() if (d.is_available() and d.is_initialized()) else 0
 
 
-def _torch_rng_offset(dev):
-    """(seed, Philox offset) of the device's default torch generator (torch.cuda.get_rng_state: 8 bytes
-    seed, 8 bytes offset); manual_seed resets the offset to 0."""
-    st = torch.cuda.get_rng_state(dev)
-    seed = int.from_bytes(bytes(st[:8].tolist()), "little")
-    off = int.from_bytes(bytes(st[8:16].tolist()), "little")
-    return st, seed, off
+# Re-seed detection.  Every torch re-seed (torch.manual_seed / torch.cuda.manual_seed[_all], the same
+# seed again included) restarts the fused sampler's stream, so seeded runs repeat their draws as the
+# reference's torch samplers do.  The seeding functions are wrapped once (at import) to count
+# re-seeds; nothing reads or writes torch's generator state (its offset and every other torch
+# random stream stay untouched).  A seed CHANGE made any other way (a generator object's own
+# manual_seed) is still seen through torch.cuda.initial_seed(); a same-seed re-seed through an
+# unwrapped reference taken before `base` was imported is not.
+_RESEED = [0]
 
 
-_MARK = 4  # the generator offset step a sampler call leaves behind (torch's Philox offsets step by 4)
+def reseed_epoch():
+    """Number of torch re-seeds seen so far (the fused and mesh samplers restart when it moves)."""
+    return _RESEED[0]
+
+
+def _wrap_seeder(mod, name):
+    fn = getattr(mod, name, None)
+    if fn is None or getattr(fn, "_insr_reseed_hook", False):
+        return
+
+    def seeded(*a, **k):
+        out = fn(*a, **k)
+        _RESEED[0] += 1
+        return out
+    seeded._insr_reseed_hook = True
+    seeded.__doc__, seeded.__name__, seeded.__wrapped__ = fn.__doc__, fn.__name__, fn
+    setattr(mod, name, seeded)
+
+
+def _install_reseed_hooks():
+    import torch.cuda.random as cr
+    import torch.random as tr
+    for mod, names in ((torch, ("manual_seed", "seed")), (tr, ("manual_seed", "seed")),
+                       (torch.cuda, ("manual_seed", "manual_seed_all", "seed", "seed_all")),
+                       (cr, ("manual_seed", "manual_seed_all", "seed", "seed_all"))):
+        for name in names:
+            _wrap_seeder(mod, name)
+
+
+_install_reseed_hooks()
 
 
 def _sampler(dev):
     """Per-device Philox state of the fused sampler (insr_sample_boxes): (stream position on
     the device, key).  The key is the device's torch seed with the distributed rank folded in.
-    EVERY re-seed of torch (torch.manual_seed / torch.cuda.manual_seed, the same seed again
-    included) restarts the stream, so seeded runs repeat their draws as the reference's torch
-    samplers do: each eager call leaves torch's generator offset _MARK past where it found it, and a
-    re-seed -- which resets that offset to 0 -- shows as an offset below the last mark.  Created /
-    restarted on an eager call -- phase loops always run iteration 0 eagerly before capturing (a
-    capture keeps the current stream)."""
+    A torch re-seed (reseed_epoch) or a changed seed restarts the stream.  Created / restarted on
+    an eager call -- phase loops always run iteration 0 eagerly before capturing (a capture keeps
+    the current stream)."""
     from . import _native as nat
     key = dev.index
     ent = _SAMPLER.get(key)
@@ -163,15 +192,13 @@ def _sampler(dev):
         if ent is None:
             raise RuntimeError("sampler state must be created before graph capture (run one eager call)")
         return ent[:2]
-    st, seed, off = _torch_rng_offset(dev)
-    if ent is None or ent[2] != seed or off < ent[3]:
+    torch.cuda.init()
+    seed = torch.cuda.default_generators[dev.index].initial_seed()  # host-side state, no device sync
+    epoch = _RESEED[0]
+    if ent is None or ent[2] != seed or ent[3] != epoch:
         state = ent[0].zero_() if ent is not None else torch.zeros(nat.lib().insr_sampler_state_bytes() // 8,
                                                                     device=dev, dtype=torch.int64)
-        ent = (state, sampler_seed(seed, _dp_rank()), seed, 0)
-    mark = off + _MARK
-    st[8:16] = torch.tensor(list(mark.to_bytes(8, "little")), dtype=torch.uint8)
-    torch.cuda.set_rng_state(st, dev)
-    ent = _SAMPLER[key] = ent[:3] + (mark,)
+        ent = _SAMPLER[key] = (state, sampler_seed(seed, _dp_rank()), seed, epoch)
     return ent[:2]
 
 
@@ -186,22 +213,72 @@ def sample_random_and_bands2D(N, n_band, epsilon=1e-4, device="cuda", merged=Fal
     dev = torch.device(device)
     if dev.type != "cuda":
         raise nat.NativeUnavailable("sample_random_and_bands2D draws on the GPU only")
-    state, seed = _sampler(dev)
     h = n_band // 2
-    buf = torch.empty(N + 4 * h, 2, device=dev)  # [interior; bands]: one jet can take both (merged=True)
-    x, bxy = buf[:N], buf[N:]
+    rows = N + 4 * h
+    ahead = draw_ahead.active
+    if merged and ahead is not None:
+        buf = ahead.take((N, h, float(epsilon), dev.index), rows, dev, lambda out, reps: _draw_fluid(
+            out, N, h, epsilon, dev, reps))
+        if buf is not None:
+            return buf
+    buf = torch.empty(rows, 2, device=dev)  # [interior; bands]: one jet can take both (merged=True)
+    _draw_fluid(buf, N, h, epsilon, dev, 1)
+    if merged:
+        return buf
+    return buf[:N], buf[N:]
+
+
+def _draw_fluid(out, N, h, epsilon, dev, reps):
+    """The interior box and the four wall bands of sample_random_and_bands2D into `out` -- (reps, N + 4 h,
+    2) for reps consecutive iterations, one launch either way (insr_sample_boxes_rep)."""
+    from . import _native as nat
+    state, seed = _sampler(dev)
     full, lo, hi = (-1.0, 1.0), (-1 - epsilon, -1 + epsilon), (1 - epsilon, 1 + epsilon)
     faces = [(lo, full), (hi, full), (full, lo), (full, hi)]  # sample_boundary2D_pair's order
     f3 = nat._F * 3
+    base = out.data_ptr()
     boxes = (nat.Box * 5)()
-    boxes[0] = nat.Box(x.data_ptr(), N, f3(-1.0, -1.0, 0.0), f3(1.0, 1.0, 0.0))
-    for k, (rx, ry) in enumerate(faces):  # face k: rows [k h, (k + 1) h) of bxy, 8 bytes a row
-        boxes[1 + k] = nat.Box(bxy.data_ptr() + 8 * h * k, h, f3(rx[0], ry[0], 0.0), f3(rx[1], ry[1], 0.0))
-    nat.check(nat.lib().insr_sample_boxes(boxes, 5, 2, seed, nat.ptr(state), nat.stream_of(dev)),
-              "insr_sample_boxes")
-    if merged:
+    boxes[0] = nat.Box(base, N, f3(-1.0, -1.0, 0.0), f3(1.0, 1.0, 0.0))
+    for k, (rx, ry) in enumerate(faces):  # face k: rows [N + k h, N + (k + 1) h), 8 bytes a row
+        boxes[1 + k] = nat.Box(base + 8 * (N + h * k), h, f3(rx[0], ry[0], 0.0), f3(rx[1], ry[1], 0.0))
+    strides = (ctypes.c_long * 5)(*([2 * (N + 4 * h)] * 5))
+    nat.check(nat.lib().insr_sample_boxes_rep(boxes, 5, 2, reps, strides, seed, nat.ptr(state), nat.stream_of(dev)),
+              "insr_sample_boxes_rep")
+
+
+class draw_ahead:
+    """`with draw_ahead(U):` around U consecutive iterations that hold no host read between them (the
+    U-iteration hipGraph of base/_loop.py PhaseLoop.run_group): the first merged fluid draw
+    (sample_random_and_bands2D(merged=True)) draws the buffers of all U iterations in ONE launch
+    (insr_sample_boxes_rep) and the next U - 1 calls of the same shape take theirs -- 4 sampler launches
+    per phase and replay -> 1.  Independent uniform draws made earlier: which Philox numbers an
+    iteration gets changes, not their distribution (the points never depend on the network).  A call
+    of another shape, or a (U + 1)-th call, draws on its own."""
+
+    active = None
+
+    def __init__(self, reps):
+        self.reps = max(1, int(reps))
+
+    def __enter__(self):
+        self.saved, self.store, self.key, self.pos = draw_ahead.active, None, None, 0
+        draw_ahead.active = self if self.reps > 1 else None
+        return self
+
+    def __exit__(self, *exc):
+        draw_ahead.active = self.saved
+        return False
+
+    def take(self, key, rows, dev, draw):
+        if self.store is None:
+            self.store = torch.empty(self.reps, rows, 2, device=dev)
+            self.key = key
+            draw(self.store, self.reps)
+        if key != self.key or self.pos >= self.reps:
+            return None
+        buf = self.store[self.pos]
+        self.pos += 1
         return buf
-    return x, bxy
 
 
 class draw_plan:

@@ -20,6 +20,11 @@ constexpr int kSampThreads = 256;
 struct BoxesPk {
   InsrBox box[INSR_MAX_BOXES];
   long first[INSR_MAX_BOXES + 1];  // first value (point * dim + coordinate) of each box
+  long rep_stride[INSR_MAX_BOXES];  // floats between repetitions of a box's output
+  long per_rep;                     // values of one repetition (first[nbox])
+  long per_rep_pad;                 // ... rounded up to whole Philox groups of 4: repetition r starts at
+                                    // counter base + r ceil(per_rep / 4), exactly where the r-th of
+                                    // reps single launches would start (bit-identical draws)
   int nbox;
   int dim;
   unsigned long long seed;
@@ -56,14 +61,16 @@ __global__ __launch_bounds__(kSampThreads) void sample_boxes_kernel(const BoxesP
     for (int q = 0; q < 4; ++q) {
       const long v = v0 + q;
       if (v >= total) break;
+      const long rep = v / pk.per_rep_pad, vr = v - rep * pk.per_rep_pad;  // repetition, value within it
+      if (vr >= pk.per_rep) continue;  // the padding of a repetition's last Philox group
       int k = 0;
 #pragma unroll
-      for (int b = 1; b < INSR_MAX_BOXES; ++b) k += (b < pk.nbox && v >= pk.first[b]) ? 1 : 0;
-      const long local = v - pk.first[k];
+      for (int b = 1; b < INSR_MAX_BOXES; ++b) k += (b < pk.nbox && vr >= pk.first[b]) ? 1 : 0;
+      const long local = vr - pk.first[k];
       const int j = (int)(local % pk.dim);
       const float u = (float)(bits[q] >> 8) * 5.9604644775390625e-8f;  // 2^-24
       const float lo = pk.box[k].lo[j], hi = pk.box[k].hi[j];
-      pk.box[k].out[local] = lo + (hi - lo) * u;
+      pk.box[k].out[rep * pk.rep_stride[k] + local] = lo + (hi - lo) * u;
     }
   }
   __syncthreads();  // every thread of this block has read `base`
@@ -84,28 +91,40 @@ extern "C" {
 
 long insr_sampler_state_bytes(void) { return 2 * (long)sizeof(unsigned long long); }
 
-int insr_sample_boxes(const InsrBox* boxes, int n_boxes, int dim, unsigned long long seed, void* state,
-                      void* stream) {
-  if (!boxes || !state || n_boxes < 1 || n_boxes > INSR_MAX_BOXES || dim < 1 || dim > 3) return INSR_EINVAL;
+int insr_sample_boxes_rep(const InsrBox* boxes, int n_boxes, int dim, int reps, const long* rep_strides,
+                          unsigned long long seed, void* state, void* stream) {
+  if (!boxes || !state || n_boxes < 1 || n_boxes > INSR_MAX_BOXES || dim < 1 || dim > 3 || reps < 1) return INSR_EINVAL;
+  if (reps > 1 && !rep_strides) return INSR_EINVAL;
   BoxesPk pk{};
   long total = 0;
   for (int k = 0; k < n_boxes; ++k) {
     if (boxes[k].n < 0 || (boxes[k].n > 0 && !boxes[k].out)) return INSR_EINVAL;
+    // repetitions must not overlap the box's own rows (a stride below n * dim would)
+    if (reps > 1 && boxes[k].n > 0 && rep_strides[k] < boxes[k].n * dim) return INSR_EINVAL;
     pk.box[k] = boxes[k];
     pk.first[k] = total;
+    pk.rep_stride[k] = reps > 1 ? rep_strides[k] : 0;
     total += boxes[k].n * dim;
   }
   pk.first[n_boxes] = total;
+  pk.per_rep = total;
+  pk.per_rep_pad = (total + 3) / 4 * 4;
   pk.nbox = n_boxes;
   pk.dim = dim;
   pk.seed = seed;
   if (total == 0) return 0;
-  const long threads = (total + 3) / 4;
+  const long all = pk.per_rep_pad * reps;
+  const long threads = (all + 3) / 4;
   const long nb = (threads + kSampThreads - 1) / kSampThreads;
   if (nb > 0x7fffffffL) return INSR_EINVAL;
-  hipLaunchKernelGGL(sample_boxes_kernel, dim3((unsigned)nb), dim3(kSampThreads), 0, (hipStream_t)stream, pk, total,
+  hipLaunchKernelGGL(sample_boxes_kernel, dim3((unsigned)nb), dim3(kSampThreads), 0, (hipStream_t)stream, pk, all,
                      (unsigned long long*)state);
   return (int)hipGetLastError();
+}
+
+int insr_sample_boxes(const InsrBox* boxes, int n_boxes, int dim, unsigned long long seed, void* state,
+                      void* stream) {
+  return insr_sample_boxes_rep(boxes, n_boxes, dim, 1, nullptr, seed, state, stream);
 }
 
 }  // extern "C"

@@ -76,29 +76,69 @@ class ElasticityModel(BaseModel):
         return {'deformation': self.deformation_field}
 
     # ---- sampling ------------------------------------------------------------
+    # Data parallelism.  Strong scaling (the default under torch.distributed): rank r of K draws ONLY its
+    # share of every part of the global batch -- rows [r n / K, (r + 1) n / K) of each 'uniform' part
+    # (grid / mesh vertices: the same rows the global draw would hold) and as many fresh rows of each
+    # 'random' part (independent uniform draws: the union over ranks has the global batch's size and
+    # distribution; no rank draws the world-sized batch).  cfg.insr_dp_weak: every rank draws the whole
+    # batch (weak scaling).  cfg.insr_shard = (r, K): one process runs rank r's share of a K-rank strong
+    # run (bench.py --shard-of K measures exactly this code).  Ranks draw independent points: the device
+    # samplers fold the rank into their key (base.sampling.sampler_seed), the mesh sampler uses a
+    # generator seeded the same way (_mesh_generator).
+    def _shard(self):
+        """(r, K): this process's share of the global batch (K = 1: the whole batch)."""
+        emu = getattr(self.cfg, "insr_shard", None)
+        if emu:
+            return int(emu[0]), int(emu[1])
+        world = self._dp_world()
+        if world == 1 or getattr(self.cfg, "insr_dp_weak", False):
+            return 0, 1
+        return torch.distributed.get_rank(), world
+
+    def _rows(self, n):
+        """(first, count) of this process's rows of a part of n global rows."""
+        r, k = self._shard()
+        a, b = r * n // k, (r + 1) * n // k
+        return a, b - a
+
+    def _mesh_generator(self):
+        """None (the default CUDA generator, as the reference) on one unsharded rank; else a device
+        generator keyed by the torch seed with the rank folded in (base.sampling.sampler_seed), re-made
+        when torch is re-seeded -- ranks seeded alike still draw independent mesh points."""
+        r, k = self._shard()
+        world = self._dp_world()
+        if k == 1 and world == 1:
+            return None
+        from base.sampling import reseed_epoch, sampler_seed
+        rank = r if k > 1 else torch.distributed.get_rank()
+        dev = torch.device(self.device)
+        seed = torch.cuda.default_generators[dev.index or 0].initial_seed() if dev.type == "cuda" else torch.initial_seed()
+        key = (seed, reseed_epoch(), rank)
+        cached = self.__dict__.get("_insr_mesh_gen")
+        if cached is None or cached[0] != key:
+            g = torch.Generator(device=dev)
+            g.manual_seed(sampler_seed(seed, rank) & 0x7FFFFFFFFFFFFFFF)
+            cached = self.__dict__["_insr_mesh_gen"] = (key, g)
+        return cached[1]
+
     def _sample_in_training(self, resolution):
+        """elasticity/model.py:198-220, this process's share of it (see above)."""
         d, parts = self.dim, []
-        if self.use_mesh:  # elasticity/model.py:200-207
-            # weak scaling: each rank draws its own n points -- ranks seed their CUDA generators
-            # differently (bench.py: 1234 + 7919 rank; BaseModel._dp_shard), so the draws are
-            # independent without drawing a world-sized batch and discarding most of it
-            for s in self.sample_pattern:
-                if s == 'random':
-                    parts.append(self.mesh_sampler.sample(resolution ** d)[:, :d])
-                elif s == 'uniform':
-                    parts.append(self.mesh_V[:, :d])
-                else:
-                    raise NotImplementedError(s)
-            return self._dp_shard(torch.cat(parts, dim=0).requires_grad_(True))
         for s in self.sample_pattern:
             if s == 'random':
-                parts.append(sample_random(resolution ** d, d, device=self.device).requires_grad_(True))
+                n = self._rows(resolution ** d)[1]
+                if self.use_mesh:  # elasticity/model.py:200-207: volume-weighted points of the mesh
+                    parts.append(self.mesh_sampler.sample(n, generator=self._mesh_generator())[:, :d])
+                else:
+                    parts.append(sample_random(n, d, device=self.device).requires_grad_(True))
             elif s == 'uniform':
-                parts.append(self._uniform_grid(resolution, d))
+                full = self.mesh_V[:, :d] if self.use_mesh else self._uniform_grid(resolution, d)
+                a, n = self._rows(full.shape[0])
+                parts.append(full if n == full.shape[0] else full[a:a + n])
             else:
                 raise NotImplementedError(s)
         x = torch.cat(parts, dim=0)
-        return self._dp_shard(x)
+        return x.requires_grad_(True) if x.is_leaf else x
 
     def _uniform_grid(self, resolution, d):
         """sample_uniform(resolution, d) -- the same cell-centred grid every iteration (no RNG):
@@ -111,35 +151,26 @@ class ElasticityModel(BaseModel):
         return cache[key]
 
     def _sample_fixed_in_training(self, resolution):
-        """Points on the x = -1 face (left) and x = +1 face (right); none on a mesh (the
-        reference's mesh scenes use no positional constraint, elasticity/model.py:228)."""
+        """Points on the x = -1 face (left) and x = +1 face (right), this process's share of each part;
+        none on a mesh (the reference's mesh scenes use no positional constraint, elasticity/model.py:228)."""
         d, left, right = self.dim, [], []
         if self.use_mesh:
             empty = torch.zeros(0, d, device=self.device).requires_grad_(True)
             return empty, empty
         for s in self.sample_pattern:
             if s == 'random':
-                faces = [sample_random(resolution, d - 1, device=self.device) for _ in range(2)]
+                n = self._rows(resolution)[1]
+                faces = [sample_random(n, d - 1, device=self.device) for _ in range(2)]
             elif s == 'uniform':
                 g = self._uniform_grid(resolution, d - 1).detach()
-                faces = [g, g]
+                a, n = self._rows(g.shape[0])
+                faces = [g[a:a + n], g[a:a + n]]
             else:
                 raise NotImplementedError(s)
             one = torch.ones(faces[0].shape[0], 1, device=self.device)
-            left.append(torch.cat([-one, faces[0]], 1).requires_grad_(True))
-            right.append(torch.cat([one, faces[1]], 1).requires_grad_(True))
-        return self._dp_shard(torch.cat(left, 0)), self._dp_shard(torch.cat(right, 0))
-
-    def _dp_shard(self, x):
-        """Rank r keeps rows [r n / world, (r + 1) n / world) of the global draw (strong
-        scaling).  cfg.insr_dp_weak: every rank keeps its whole draw (weak scaling; ranks
-        seed their device RNG differently, so the draws are independent)."""
-        world = self._dp_world()
-        if world == 1 or getattr(self.cfg, "insr_dp_weak", False):
-            return x
-        r = torch.distributed.get_rank()
-        n = x.shape[0]
-        return x[r * n // world:(r + 1) * n // world]
+            left.append(torch.cat([-one, faces[0]], 1))
+            right.append(torch.cat([one, faces[1]], 1))
+        return torch.cat(left, 0).requires_grad_(True), torch.cat(right, 0).requires_grad_(True)
 
     # ---- timestepping ----------------------------------------------------------
     @BaseModel._timestepping
@@ -196,25 +227,26 @@ class ElasticityModel(BaseModel):
             return None
         if "_sample_in_training" in self.__dict__ or "_sample_fixed_in_training" in self.__dict__:
             return None  # an instance-level sampler (tests pass recorded samples) takes precedence
-        if self._dp_world() > 1 and not getattr(self.cfg, "insr_dp_weak", False):
-            return None
         d = self.dim
         use_l = 'constraint' in self.energy
         use_r = any(t in self.energy for t in ('constraint_right', 'constraint_right_compress'))
-        key = (resolution, use_l, use_r)
+        shard = self._shard()
+        key = (resolution, use_l, use_r, shard)
         cache = self.__dict__.setdefault("_insr_box_batch", {})
         if key not in cache:
             rows, boxes, fill = 0, [], []
 
             def put(kind, n, lo, hi, const):
+                """One part of the batch: this process's share of its n global rows."""
                 nonlocal rows
+                a, m = self._rows(n)
                 if kind == 'random':
-                    boxes.append((rows, n, lo, hi))
+                    boxes.append((rows, m, lo, hi))
                 elif kind == 'uniform':
-                    fill.append((rows, const))
+                    fill.append((rows, const[a:a + m]))
                 else:
                     raise NotImplementedError(kind)
-                rows += n
+                rows += m
             for s in self.sample_pattern:
                 put(s, resolution ** d, [-1.0] * d, [1.0] * d,
                     sample_uniform(resolution, d, device=self.device) if s == 'uniform' else None)
@@ -241,7 +273,7 @@ class ElasticityModel(BaseModel):
             empty = torch.zeros(0, d, device=self.device)
             fixed_l = buf[n:n + nl] if use_l else empty
             fixed_r = buf[n + nl:n + nl + nr] if use_r else empty
-            cache[key] = (buf, boxes, buf[:n], fixed_l, fixed_r)
+            cache[key] = (buf, [b for b in boxes if b[1] > 0], buf[:n], fixed_l, fixed_r)
         buf, boxes, x, fixed_l, fixed_r = cache[key]
         if boxes:
             sample_boxes_into(buf.detach(), boxes)

@@ -133,3 +133,38 @@ def test_two_streams_concurrently_match_single_stream(setup, pair):
         for a, b in zip(r.result(), want):
             assert torch.isfinite(a).all()
             assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("kind", ["value", "lap"])
+def test_deferred_backward_on_side_stream_then_step(setup, kind):
+    """A reverse jet run on a side stream inside defer_reductions holds its sums back; the optimiser
+    step on the default stream cannot fuse them (other stream), so it lands them on their own stream
+    (MLP.flush_pending_reduce records that write) and waits for it before Adam reads .grad
+    (grad_read_sync after the flush).  Parameters and .grad equal the same sequence run on one stream
+    bit for bit -- value jets (fused-path partial rows) and the Laplacian jet (split sums)."""
+    import base
+    from base import _jet
+    res = []
+    for side in (False, True):
+        torch.manual_seed(61)
+        net = base.MLP(2, 2 if kind == "value" else 1, 4, 128, nonlinearity="sine").cuda()
+        opt = base.FusedAdam([{"params": list(net.parameters()), "lr": 1e-3, "module": net}])
+        x = (torch.rand(3000, 2, generator=torch.Generator().manual_seed(62)) * 2 - 1).cuda().requires_grad_(True)
+        s = torch.cuda.Stream() if side else torch.cuda.current_stream()
+        s.wait_stream(torch.cuda.current_stream())
+        opt.zero_grad()
+        with _jet.defer_reductions():
+            with torch.cuda.stream(s):
+                y = net(x)
+                v = y if kind == "value" else base.laplace(y, x)
+                with _jet.batched_backward():
+                    (v ** 2).sum().backward()
+                # a long queue on the side stream: the sums would still be running if unordered
+                for _ in range(20):
+                    torch.matmul(torch.empty(512, 512, device="cuda"), torch.empty(512, 512, device="cuda"))
+            assert "_insr_pending_reduce" in net.__dict__  # held back for the step
+            opt.step()
+        torch.cuda.synchronize()
+        res.append((torch.cat([p.detach().reshape(-1) for p in net.parameters()]).cpu(),
+                    torch.cat([p.grad.reshape(-1) for p in net.parameters()]).cpu()))
+    assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])

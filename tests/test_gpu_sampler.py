@@ -5,6 +5,8 @@ known-answer vector, and the kernel's draws must equal it bit for bit (value v o
 launch = Philox(seed, base + v // 4)[v % 4] -> lo + (hi - lo) * (bits >> 8) * 2^-24).
 Distribution checks cover the reference samplers' boxes (base/sampling.py:14-64).
 """
+import ctypes
+
 import numpy as np
 import pytest
 import torch
@@ -265,3 +267,65 @@ def test_same_seed_reseed_repeats_draws(B):
     torch.manual_seed(1)
     c = B.sample_random(1000, 2, device="cuda")
     assert not torch.equal(a, c)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dim", [1, 2, 3])
+def test_repeated_draw_equals_consecutive_draws(B, dim):
+    """insr_sample_boxes_rep (base.sampling.draw_ahead: the U iterations of a replayed group drawn by
+    one launch): repetition r of every box is bit for bit the r-th of U single launches -- each
+    repetition starts at the Philox group where that launch would start, odd value counts included --
+    and the stream position advances exactly as far."""
+    nat = B._native
+    boxes = [(101, [-1.0] * dim, [1.0] * dim), (3, [0.5] * dim, [0.75] * dim), (40, [-2.0] * dim, [0.0] * dim)]
+    seed, U = 0xBADC0FFEE, 4
+    per = sum(n for n, _, _ in boxes)
+    st1 = torch.zeros(2, dtype=torch.int64, device="cuda")
+    singles = [torch.cat(_draw(B, boxes, dim, seed, st1)) for _ in range(U)]
+    st2 = torch.zeros(2, dtype=torch.int64, device="cuda")
+    big = torch.full((U, per, dim), float("nan"), device="cuda")
+    f3 = nat._F * 3
+    arr = (nat.Box * len(boxes))()
+    row = 0
+    for k, (n, lo, hi) in enumerate(boxes):
+        arr[k] = nat.Box(big.data_ptr() + 4 * dim * row, n, f3(*(list(lo) + [0.0] * (3 - dim))),
+                         f3(*(list(hi) + [0.0] * (3 - dim))))
+        row += n
+    strides = (ctypes.c_long * len(boxes))(*([per * dim] * len(boxes)))
+    nat.check(nat.lib().insr_sample_boxes_rep(arr, len(boxes), dim, U, strides, seed, nat.ptr(st2),
+                                              nat.stream_of(0)), "rep")
+    torch.cuda.synchronize()
+    for r in range(U):
+        assert torch.equal(big[r], singles[r]), r
+    assert int(st2[0]) == int(st1[0]) and int(st2[1]) == 0
+    # overlapping repetitions are refused
+    bad = (ctypes.c_long * len(boxes))(*([1] * len(boxes)))
+    assert nat.lib().insr_sample_boxes_rep(arr, len(boxes), dim, U, bad, seed, nat.ptr(st2), nat.stream_of(0)) != 0
+
+
+@pytest.mark.gpu
+def test_draw_ahead_one_launch_per_group(B):
+    """Inside draw_ahead(U) the merged fluid draws of U iterations come from one launch, each iteration's
+    buffer equal to what its own draw would have been (sample_random_and_bands2D(merged=True))."""
+    lib = B._native.lib()
+    from base.sampling import draw_ahead
+    torch.manual_seed(5)
+    ref = [B.sample_random_and_bands2D(1000, 10, merged=True).clone() for _ in range(4)]
+    calls = []
+    orig = lib.insr_sample_boxes_rep
+
+    def spy(*a):
+        calls.append(a[3])
+        return orig(*a)
+    lib.insr_sample_boxes_rep = spy
+    try:
+        torch.manual_seed(5)
+        with draw_ahead(4):
+            got = [B.sample_random_and_bands2D(1000, 10, merged=True) for _ in range(4)]
+            extra = B.sample_random_and_bands2D(1000, 10, merged=True)  # a 5th call draws on its own
+    finally:
+        lib.insr_sample_boxes_rep = orig
+    assert calls == [4, 1], calls
+    for a, b in zip(got, ref):
+        assert torch.equal(a, b)
+    assert extra.shape == ref[0].shape
