@@ -92,6 +92,10 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--backend", default="nccl", help="nccl (= RCCL) or gloo (functional rehearsal)")
+    ap.add_argument("--dp-path", action="store_true",
+                    help="one process runs the data-parallel iteration itself (gradient arena, a world-1 RCCL "
+                         "all-reduce between the two graphs, unfused sums + Adam): a rank's DP step measured on "
+                         "one GPU (with --shard-of K: the K-rank strong run's rank step)")
     ap.add_argument("--rehearse", action="store_true",
                     help="CPU rehearsal of the multi-rank launch (gloo, no GPU work; tests)")
     args = ap.parse_args()
@@ -137,6 +141,15 @@ def setup_dist(args):
                 dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
             else:
                 dist.init_process_group(args.backend)
+        elif args.dp_path:  # a world-1 process group: the DP iteration's own code, collective included
+            import socket
+            with socket.socket() as sk:
+                sk.bind(("127.0.0.1", 0))
+                port = sk.getsockname()[1]
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", str(port))
+            dist.init_process_group(args.backend, rank=0, world_size=1,
+                                    **({"device_id": torch.device("cuda", dev)} if args.backend == "nccl" else {}))
     if world > 1:
         assert dist.get_world_size() == args.gpus, (dist.get_world_size(), args.gpus)
         devs = [None] * world
@@ -184,7 +197,7 @@ def build_model(args, world, rank):
     base._native.set_default_knobs(policy=args.bwd_policy or None, bwd_f16=None if args.bwd_f16 < 0 else args.bwd_f16)
     wl = WORKLOADS[args.config]
     res = wl["res"]
-    cfg = baseline_config(args.config, sample_resolution=res, insr_graph=not args.no_graph,
+    cfg = baseline_config(args.config, sample_resolution=res, insr_graph=not args.no_graph, insr_dp_always=args.dp_path,
                           insr_graph_unroll=max(1, args.graph_unroll),
                           insr_sync_every=10 ** 9, insr_progress=False, early_stop=False,
                           proj_dir="/tmp/insr_bench", max_n_iters=10 ** 9,

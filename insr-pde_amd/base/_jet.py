@@ -185,15 +185,14 @@ def _reference_backward(ctx, grads):
     if not want_x and not pidx:
         return none
     outs = torch_jet(mlp, x2, mode)
-    total = None
-    for o, g in zip(outs, grads):
-        if o is not None and g is not None:
-            term = (o * g).sum()
-            total = term if total is None else total + term
-    if total is None:
+    pairs = [(o, g) for o, g in zip(outs, grads) if o is not None and g is not None]
+    if not pairs:
         return none
     ins = ([x2] if want_x else []) + [params[i] for i in pidx]
-    gs = torch.autograd.grad(total, ins, create_graph=True, allow_unused=True)
+    # the adjoints enter as grad_outputs: the vector of the VJP, not differentiated in this call
+    # (they may depend on x themselves, e.g. 2 y of d(y^2)/dx); the result stays differentiable in them
+    gs = torch.autograd.grad([o for o, _ in pairs], ins, grad_outputs=[g for _, g in pairs], create_graph=True,
+                             allow_unused=True)
     res = [None] * len(none)
     k = 0
     if want_x:

@@ -115,7 +115,7 @@ class PhaseLoop:
 
     def _capture(self):
         try:
-            if self.m._dp_world() > 1:
+            if self.m._dp_active():
                 g1, out = self._capture_graph(self._stage1)
                 g2, _ = self._capture_graph(self._stage2)
                 self.graph, self.graph2 = g1, g2
@@ -143,7 +143,7 @@ class PhaseLoop:
         """Whether run_group() may serve the next `unroll` iterations (graph mode, one process,
         the single-iteration graph already captured: iterations 0 and 1 ran)."""
         return (self.unroll > 1 and self.use_graph and self.graph is not None and self.graph2 is None
-                and self.m._dp_world() == 1)
+                and not self.m._dp_active())
 
     def run_group(self):
         """`unroll` consecutive iterations as ONE graph replay (captured on first use -- a capture
@@ -178,7 +178,7 @@ class PhaseLoop:
 
     def step(self, i):
         """Run iteration i; returns the device loss dict of that iteration."""
-        dp = self.m._dp_world() > 1
+        dp = self.m._dp_active()
         if self.use_graph and i >= 1:
             if self.graph is None and self._capture() is None:
                 return self._dp_step_eager() if dp else self._body()

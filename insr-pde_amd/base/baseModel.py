@@ -135,6 +135,16 @@ class BaseModel(ABC):
         d = torch.distributed
         return d.get_world_size() if (d.is_available() and d.is_initialized()) else 1
 
+    def _dp_active(self):
+        """Whether iterations take the data-parallel path (gradient arena + all-reduce): world > 1, or
+        cfg.insr_dp_always with a process group of any size (bench.py --dp-path: one rank's DP step,
+        world-1 all-reduce included, measured on one GPU)."""
+        if self._dp_world() > 1:
+            return True
+        d = torch.distributed
+        return bool(getattr(getattr(self, "cfg", None), "insr_dp_always", False)) and d.is_available() and \
+            d.is_initialized()
+
     def _dp_sync(self, loss_dict):
         """All-reduce gradients and losses across ranks: ONE RCCL call per iteration over the
         model's gradient arena -- every trainable network's flat .grad is a view into it (bound
@@ -146,7 +156,7 @@ class BaseModel(ABC):
         eagerly: _dp_pack (device ops: zero-fill + the losses into the arena tail; captured with
         the phase and its backward), _dp_allreduce (the RCCL call), _dp_finish (the 1/world of a
         mean reduction; captured with Adam + plateau, which read the arena in place)."""
-        if self._dp_world() == 1:
+        if not self._dp_active():
             return loss_dict
         synced = self._dp_pack(loss_dict)
         self._dp_allreduce()
@@ -164,8 +174,7 @@ class BaseModel(ABC):
     def _dp_pack(self, loss_dict):
         """The iteration's gradients and losses as one contiguous arena slice (self._insr_dp_red);
         returns the losses as views of its tail (the values after _dp_allreduce/_dp_finish)."""
-        world = self._dp_world()
-        if world == 1:
+        if not self._dp_active():
             return loss_dict
         nets = list(self._trainable_networks.values())
         keys = list(loss_dict.keys())
@@ -203,7 +212,7 @@ class BaseModel(ABC):
         self.optimizer.zero_grad()
         # one process with the fused optimiser: a fused-path backward's row sums run inside the Adam
         # launch (base/_jet.py defer_reductions; under data parallelism the all-reduce needs them first)
-        defer = _jet.DEFER_REDUCE and isinstance(self.optimizer, FusedAdam) and self._dp_world() == 1
+        defer = _jet.DEFER_REDUCE and isinstance(self.optimizer, FusedAdam) and not self._dp_active()
         with (_jet.defer_reductions() if defer else contextlib.nullcontext()):
             self._backward(loss_dict)
             synced = self._dp_sync(loss_dict)

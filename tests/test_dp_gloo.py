@@ -100,3 +100,59 @@ def test_dp_sync_two_ranks(reduction, world):
         assert abs(losses["bc"] - 10.0 * rsum * scale) < 1e-4
         assert touched
     assert torch.equal(res[0][1], res[1][1])  # replicas identical -> identical Adam steps
+
+
+def _worker_dp_always(port, q):
+    import sys
+    import types
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "insr-pde_amd")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    import base
+
+    class Toy(base.BaseModel):
+        def __init__(self, always):
+            self.device = torch.device("cpu")
+            self.cfg = types.SimpleNamespace(insr_dp_always=always)
+            torch.manual_seed(0)
+            self.a = base.MLP(2, 2, 1, 32, nonlinearity="sine")
+
+        @property
+        def _trainable_networks(self):
+            return {"a": self.a}
+
+        def _sample_in_training(self):
+            pass
+
+        def initialize(self):
+            pass
+
+        def step(self):
+            pass
+
+    out = []
+    for always in (False, True):
+        m = Toy(always)
+        g = m.a.flat_grad_buffer()
+        g.copy_(torch.arange(g.numel(), dtype=torch.float32))
+        res = m._dp_sync({"main": torch.tensor(2.0)})
+        out.append((m._dp_active(), "_insr_dp_arena" in m.__dict__, float(res["main"]),
+                    bool(torch.equal(m.a.flat_grad_buffer(), torch.arange(g.numel(), dtype=torch.float32)))))
+    q.put(out)
+    dist.destroy_process_group()
+
+
+def test_dp_path_at_world_one():
+    """cfg.insr_dp_always (bench.py --dp-path): with a world-1 process group the iteration takes the
+    data-parallel path itself -- gradient arena bound, the collective run (a no-op sum) -- so one GPU
+    can time a rank's DP step; without it a world-1 group changes nothing."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_worker_dp_always, args=(_free_port(), q))
+    p.start()
+    res = q.get(timeout=120)
+    p.join(timeout=60)
+    assert p.exitcode == 0
+    (act0, arena0, loss0, g0), (act1, arena1, loss1, g1) = res
+    assert not act0 and not arena0 and loss0 == 2.0 and g0
+    assert act1 and arena1 and loss1 == 2.0 and g1
