@@ -33,12 +33,14 @@ import torch.nn as nn
 from . import _jet
 
 OMEGA = 30.0
+KERNEL_WIDTHS = (32, 64, 128, 256)  # hidden widths the HIP jets are compiled for
 
 
 def get_network(cfg, in_features, out_features):
-    """base/networks.py:12-17: only the 'siren' network exists.  cfg.insr_precision (optional,
-    default None = the library default, fp32-accurate split-bf16) selects the matrix-core
-    precision of the net's jets: 'fp32', 'bf16x6', 'bf16x3' or 'bf16'."""
+    """base/networks.py:12-17: cfg.network 'siren' -> MLP(..., nonlinearity=cfg.nonlinearity) (a relu /
+    elu one, or a width above 256, is the reference's plain torch network: TorchMLP).
+    cfg.insr_precision (optional, default None = the library default, fp32-accurate split-bf16)
+    selects the matrix-core precision of the net's jets: 'fp32', 'bf16x6', 'bf16x3' or 'bf16'."""
     if cfg.network == 'siren':
         return MLP(in_features, out_features, cfg.num_hidden_layers, cfg.hidden_features,
                    nonlinearity=cfg.nonlinearity, precision=getattr(cfg, "insr_precision", None))
@@ -68,9 +70,6 @@ def _first_layer_sine_init(m):
         if hasattr(m, 'weight'):
             fan_in = m.weight.size(-1)
             m.weight.uniform_(-1 / fan_in, 1 / fan_in)
-
-
-KERNEL_WIDTHS = (32, 64, 128, 256)  # hidden widths the HIP jets are compiled for
 
 
 def kernel_width(width):
@@ -104,15 +103,85 @@ def _parse_precision(precision):
 _FLAT_OWNERS = weakref.WeakValueDictionary()
 
 
+def _kaiming_relu_init(m):
+    # base/networks.py:74-77 (relu networks)
+    if type(m) is nn.Linear:
+        nn.init.kaiming_normal_(m.weight, a=0.0, nonlinearity='relu', mode='fan_in')
+
+
+def _elu_init(m):
+    # base/networks.py:96-100 (elu networks)
+    if type(m) is nn.Linear:
+        nn.init.normal_(m.weight, std=math.sqrt(1.5505188080679277) / math.sqrt(m.weight.size(-1)))
+
+
+def hip_served(nonlinearity, outermost_linear, hidden_features):
+    """Whether the HIP jets serve this network: a SIREN ('sine') with a linear output layer and a hidden
+    width the kernels are compiled for (<= 256, zero-padded up to 32 / 64 / 128 / 256)."""
+    return nonlinearity == 'sine' and bool(outermost_linear) and hidden_features <= KERNEL_WIDTHS[-1]
+
+
+class TorchMLP(nn.Module):
+    """The reference's MLP (base/networks.py:30-71) as plain torch modules on the device, for the
+    configurations the HIP jets do not serve -- relu / elu networks, outermost_linear=False, SIRENs
+    wider than 256 -- none of which the INSR-PDE models build (they all use get_network's SIREN).  Same
+    module tree, init order (a seed gives the reference's weights bit for bit) and state_dict keys;
+    its derivatives take the reference's autograd route in base/diff_ops.py.  Off the hot path: a
+    warning says so once per configuration."""
+
+    _warned = set()
+
+    def __init__(self, in_features, out_features, num_hidden_layers, hidden_features,
+                 outermost_linear=True, nonlinearity='relu', weight_init=None):
+        super().__init__()
+        acts = {'sine': (Sine, _sine_init, _first_layer_sine_init), 'relu': (lambda: nn.ReLU(inplace=True),
+                                                                             _kaiming_relu_init, None),
+                'elu': (lambda: nn.ELU(inplace=True), _elu_init, None)}
+        if nonlinearity not in acts:
+            raise KeyError(nonlinearity)
+        make, init, first = acts[nonlinearity]
+        act = make()  # one module shared by every layer, as the reference's
+        self.in_features, self.out_features = in_features, out_features
+        self.num_hidden_layers, self.hidden_features = num_hidden_layers, hidden_features
+        self.first_layer_init = None
+        layers = [nn.Linear(in_features, hidden_features), act]
+        for _ in range(num_hidden_layers):
+            layers += [nn.Linear(hidden_features, hidden_features), act]
+        layers.append(nn.Linear(hidden_features, out_features))
+        if not outermost_linear:
+            layers.append(act)
+        self.net = nn.Sequential(*layers)
+        self.weight_init = weight_init if weight_init is not None else init
+        if self.weight_init is not None:
+            self.net.apply(self.weight_init)
+        if first is not None:
+            self.net[0].apply(first)
+        key = (nonlinearity, bool(outermost_linear), hidden_features > KERNEL_WIDTHS[-1])
+        if key not in TorchMLP._warned:
+            TorchMLP._warned.add(key)
+            import warnings
+            warnings.warn(f"MLP({nonlinearity}, outermost_linear={outermost_linear}, width {hidden_features}): no "
+                          "HIP jet serves it; running plain torch ops (off the INSR-PDE hot path)", stacklevel=3)
+
+    def forward(self, coords, weights=None):
+        out = self.net(coords)
+        return out * weights if weights is not None else out
+
+
 class MLP(nn.Module):
-    """SIREN MLP with flat parameter storage and a HIP forward (base/networks.py:30-71)."""
+    """SIREN MLP with flat parameter storage and a HIP forward (base/networks.py:30-71).  A
+    configuration the kernels do not serve (hip_served) is built as TorchMLP instead."""
+
+    def __new__(cls, in_features, out_features, num_hidden_layers, hidden_features,
+                outermost_linear=True, nonlinearity='relu', weight_init=None, precision=None):
+        if cls is MLP and not hip_served(nonlinearity, outermost_linear, hidden_features):
+            return TorchMLP(in_features, out_features, num_hidden_layers, hidden_features,
+                            outermost_linear=outermost_linear, nonlinearity=nonlinearity, weight_init=weight_init)
+        return super().__new__(cls)
 
     def __init__(self, in_features, out_features, num_hidden_layers, hidden_features,
                  outermost_linear=True, nonlinearity='relu', weight_init=None, precision=None):
         super().__init__()
-        if nonlinearity != 'sine' or not outermost_linear:
-            # the reference also offers relu/elu nets; INSR-PDE only ever builds SIRENs
-            raise NotImplementedError("insr-pde_amd implements the SIREN ('sine', outermost linear) network")
         self.in_features, self.out_features = in_features, out_features
         self.num_hidden_layers, self.hidden_features = num_hidden_layers, hidden_features
         self.kernel_width = kernel_width(hidden_features)

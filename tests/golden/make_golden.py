@@ -509,9 +509,45 @@ def gen_extra(base):
     return out
 
 
+def gen_other_nets(base):
+    """ref_nets.npz: the reference MLP's other configurations (base/networks.py:30-71) -- relu / elu
+    networks, outermost_linear=False, a SIREN wider than the kernels' 256 -- seeded init bit patterns,
+    the value and gradient (autograd create_graph, base/diff_ops.py:53-58) on fixed points, and the
+    parameter gradients of a fixed functional of both."""
+    cases = {"relu": (2, 1, 3, 64, True, "relu"), "elu": (2, 2, 2, 32, True, "elu"),
+             "sine_nonlinear_out": (2, 1, 2, 32, False, "sine"), "relu_nonlinear_out": (1, 2, 2, 16, False, "relu"),
+             "sine_w300": (1, 1, 1, 300, True, "sine")}
+    out = {}
+    for i, (name, (din, dout, L, W, olin, nl)) in enumerate(cases.items()):
+        seed = 700 + i
+        torch.manual_seed(seed)
+        net = base.MLP(din, dout, L, W, outermost_linear=olin, nonlinearity=nl)
+        out[f"{name}/seed"] = np.array(seed)
+        out[f"{name}/shape"] = np.array([din, dout, L, W, int(olin)])
+        out[f"{name}/nonlinearity"] = np.array(nl)
+        out[f"{name}/params"] = flat(net)
+        g = torch.Generator().manual_seed(7000 + i)
+        x = (torch.rand(128, din, generator=g) * 2 - 1).requires_grad_(True)
+        out[f"{name}/x"] = x.detach().numpy().copy()
+        y = net(x)
+        gr = base.gradient(y, x)
+        out[f"{name}/y"] = y.detach().numpy().copy()
+        out[f"{name}/gradient"] = gr.detach().numpy().copy()
+        ry, rg = torch.randn(y.shape, generator=g), torch.randn(gr.shape, generator=g)
+        out[f"{name}/y_R"], out[f"{name}/gradient_R"] = ry.numpy().copy(), rg.numpy().copy()
+        net.zero_grad(set_to_none=True)
+        ((y * ry).sum() + (gr * rg).sum()).backward()
+        out[f"{name}/pgrad"] = flat_grad(net)
+    return out
+
+
 def main():
     torch.set_num_threads(8)
     base = load_reference()
+    if "--nets" in sys.argv:  # relu / elu / outermost_linear=False / wide networks (ref_nets.npz)
+        np.savez_compressed(os.path.join(OUT, "ref_nets.npz"), **gen_other_nets(base))
+        print("ref_nets.npz", os.path.getsize(os.path.join(OUT, "ref_nets.npz")) / 1e6, "MB")
+        return
     if "--extra" in sys.argv:  # initial conditions + more samplers (ref_extra.npz)
         np.savez_compressed(os.path.join(OUT, "ref_extra.npz"), **gen_extra(base))
         print("ref_extra.npz", os.path.getsize(os.path.join(OUT, "ref_extra.npz")) / 1e6, "MB")

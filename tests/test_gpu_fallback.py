@@ -155,3 +155,15 @@ def test_fallback_keeps_the_training_step(B):
     assert abs(float(loss) - float(loss_r)) <= TOL * abs(float(loss_r))
     for a, b in zip(ref.parameters(), net.parameters()):
         assert float((a.detach() - b.detach().cpu()).abs().max()) <= 2.5e-4  # Adam's first step ~ lr sign(g)
+
+
+@pytest.mark.parametrize("name", ["relu", "elu", "sine_nonlinear_out", "relu_nonlinear_out", "sine_w300"])
+def test_other_networks_on_the_gpu(B, name):
+    """relu / elu / outermost_linear=False / width-300 networks (no HIP jet serves them: TorchMLP) on the
+    GPU against the reference's own outputs (tests/golden/ref_nets.npz)."""
+    import os
+    import numpy as np
+    from tests.test_other_nets import GOLD, check_net
+    with np.load(GOLD) as z:
+        gold = {k: z[k] for k in z.files}
+    check_net(B, gold, name, "cuda")
