@@ -68,7 +68,8 @@ CASES = {
     # eps = 1: the normalised field divides by |grad f| + eps; a small eps makes the op ill-conditioned
     # where |grad f| -> 0 (the fp32 oracle itself then drifts from fp64 by more than 1e-5)
     "laplace_normalized_d3": ((3, 1, 3, 64), lambda D, f, x: D.laplace(f(x), x, normalize=True, eps=1.0)),
-    "hessian_d3": ((3, 2, 2, 64), lambda D, f, x: D.hessian(f(x).unsqueeze(0), x.unsqueeze(0))[0]),
+    # (meta, obs, dim) input as the reference's hessian takes; the network sees the 3-d batch
+    "hessian_d3": ((3, 2, 2, 64), lambda D, f, x: (lambda xm: D.hessian(f(xm), xm)[0])(x.unsqueeze(0))),
 }
 
 
@@ -93,7 +94,8 @@ def _oracle_op(name, f, x):
         g = g / (g.norm(dim=-1, keepdim=True) + 1.0)
         return O.op_divergence(g, x)
     if name == "hessian_d3":
-        return O.op_hessian(f(x).unsqueeze(0), x.unsqueeze(0))[0]
+        xm = x.unsqueeze(0)
+        return O.op_hessian(f(xm), xm)[0]
     raise KeyError(name)
 
 
