@@ -186,14 +186,14 @@ def _sampler(dev):
     an eager call -- phase loops always run iteration 0 eagerly before capturing (a capture keeps
     the current stream)."""
     from . import _native as nat
-    key = dev.index
+    key = dev.index if dev.index is not None else torch.cuda.current_device()
     ent = _SAMPLER.get(key)
     if torch.cuda.is_current_stream_capturing():
         if ent is None:
             raise RuntimeError("sampler state must be created before graph capture (run one eager call)")
         return ent[:2]
     torch.cuda.init()
-    seed = torch.cuda.default_generators[dev.index].initial_seed()  # host-side state, no device sync
+    seed = torch.cuda.default_generators[key].initial_seed()  # host-side state, no device sync
     epoch = _RESEED[0]
     if ent is None or ent[2] != seed or ent[3] != epoch:
         state = ent[0].zero_() if ent is not None else torch.zeros(nat.lib().insr_sampler_state_bytes() // 8,
@@ -213,6 +213,8 @@ def sample_random_and_bands2D(N, n_band, epsilon=1e-4, device="cuda", merged=Fal
     dev = torch.device(device)
     if dev.type != "cuda":
         raise nat.NativeUnavailable("sample_random_and_bands2D draws on the GPU only")
+    if dev.index is None:
+        dev = torch.device("cuda", torch.cuda.current_device())
     h = n_band // 2
     rows = N + 4 * h
     ahead = draw_ahead.active
@@ -262,8 +264,17 @@ class draw_ahead:
 
     def __enter__(self):
         self.saved, self.store, self.key, self.pos = draw_ahead.active, None, None, 0
+        self.prefetch = {}  # per-group state of a model's target prefetch (pde/fluid.py _prefetched)
         draw_ahead.active = self if self.reps > 1 else None
         return self
+
+    def rep_of(self, buf):
+        """The repetition index of a buffer take() handed out in this group, or None."""
+        if self.store is None or buf.dim() != 2 or buf.untyped_storage().data_ptr() != \
+                self.store.untyped_storage().data_ptr():
+            return None
+        r, rem = divmod(buf.storage_offset() - self.store.storage_offset(), self.store.stride(0))
+        return r if rem == 0 and 0 <= r < self.reps else None
 
     def __exit__(self, *exc):
         draw_ahead.active = self.saved

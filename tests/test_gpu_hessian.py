@@ -88,14 +88,24 @@ def test_laplace_normalize_matches_oracle():
     assert e_hip <= max(1e-4, 5 * e_or), (e_hip, e_or)
 
 
-def test_hessian_3d_input_refused():
+def test_hessian_3d_input_takes_the_reference_route():
+    """d_in = 3 has no polarised Hessian jet: hessian() takes the reference's autograd route (the jet
+    nodes differentiate themselves with torch ops) and equals the oracle's Hessian
+    (tests/test_gpu_fallback.py covers it with parameter gradients)."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     import base as B
+    torch.manual_seed(3)
+    ref = O.OracleSiren(3, 1, 2, 32)
+    torch.manual_seed(3)
     net = B.MLP(3, 1, 2, 32, nonlinearity="sine").cuda()
-    x = torch.rand(10, 3, device="cuda").requires_grad_(True)
-    with pytest.raises(B.UnsupportedPattern):
-        B.hessian(net(x), x)
+    x = torch.rand(10, 3)
+    xg = x.cuda().requires_grad_(True)
+    H, st = B.hessian(net(xg), xg)
+    xr = x.clone().requires_grad_(True)
+    Hr, _ = O.op_hessian(ref(xr), xr)
+    assert st == 0 and H.shape == (10, 1, 3, 3)
+    assert float((H.detach().cpu() - Hr.detach()).abs().max() / Hr.abs().max()) < 1e-5
 
 
 @pytest.mark.parametrize("scale_x,scale_w0", [(4.0, 1.0), (1.0, 3.0), (8.0, 3.0)])

@@ -71,9 +71,13 @@ def test_grad_views_follow_the_padded_layout(B):
         assert torch.equal(p.grad, net._view(g, e))
 
 
-def test_width_above_256_refused(B):
+def test_width_above_256_is_the_torch_network(B):
+    """No kernel is compiled above width 256: such a SIREN is the reference's plain torch network
+    (TorchMLP; tests/test_other_nets.py pins it to the reference's outputs)."""
+    net = B.MLP(2, 2, 1, 300, nonlinearity="sine")
+    assert type(net).__name__ == "TorchMLP" and not isinstance(net, B.MLP)
     with pytest.raises(NotImplementedError):
-        B.MLP(2, 2, 1, 300, nonlinearity="sine")
+        B.networks.kernel_width(300)
 
 
 @pytest.mark.parametrize("shape", [(2, 1, 3, 128), (3, 3, 4, 256), (1, 1, 2, 32), (2, 3, 1, 64)])
