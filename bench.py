@@ -92,9 +92,6 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--backend", default="nccl", help="nccl (= RCCL) or gloo (functional rehearsal)")
-    ap.add_argument("--prefetch-targets", type=int, default=0, choices=[0, 1],
-                    help="fluid: the frozen networks' target jets of a replayed iteration group on a side stream "
-                         "(pde/fluid.py insr_prefetch_targets; A/B)")
     ap.add_argument("--dp-path", action="store_true",
                     help="one process runs the data-parallel iteration itself (gradient arena, a world-1 RCCL "
                          "all-reduce between the two graphs, unfused sums + Adam): a rank's DP step measured on "
@@ -201,7 +198,6 @@ def build_model(args, world, rank):
     wl = WORKLOADS[args.config]
     res = wl["res"]
     cfg = baseline_config(args.config, sample_resolution=res, insr_graph=not args.no_graph, insr_dp_always=args.dp_path,
-                          insr_prefetch_targets=bool(args.prefetch_targets),
                           insr_graph_unroll=max(1, args.graph_unroll),
                           insr_sync_every=10 ** 9, insr_progress=False, early_stop=False,
                           proj_dir="/tmp/insr_bench", max_n_iters=10 ** 9,
@@ -688,7 +684,6 @@ def main():
                    "graph_unroll": 1 if args.no_graph else max(1, args.graph_unroll),
                    "jet_precision": jet_precision_names(args.precision),
                    "bwd_policy": args.bwd_policy, "shard_of": args.shard_of, "dp_path": args.dp_path,
-                   "prefetch_targets": bool(args.prefetch_targets),
                    "bwd_f16": bwd_f16,
                    "timestep_order": f"{nts} timesteps x ({'/'.join(str(k) for k in ks)}) iterations per phase, "
                                      "phases in step() order with the prev-net snapshots; per-timestep times from HIP events"},

@@ -29,6 +29,7 @@ Differences, all controlled by cfg attributes:
 import torch
 
 from . import _jet
+from .networks import MLP
 from .sampling import draw_ahead, draw_plan
 
 try:
@@ -223,8 +224,8 @@ class PhaseLoop:
             last = (i == m.max_n_iters - 1)
             if (i + 1) % self.sync_every == 0 or last or i == 0:
                 vals = {k: float(v) for k, v in loss_dict.items()}
-                for net in m._trainable_networks.values():  # the fp16 weight planes' range guard
-                    net.check_weight_planes()
+                # the fp16 weight planes' range guard: one device-to-host read for every network
+                MLP.check_weight_planes_all(m._trainable_networks.values())
                 if m.tb is not None:
                     m.tb.add_scalars(self.tag, vals, global_step=i)
                 if tqdm is not None and hasattr(pbar, "set_postfix"):
@@ -241,8 +242,6 @@ class PhaseLoop:
                 getattr(m, f"_vis{self.tag}")()
         # the fp16 weight planes' range guard at the phase's end too, whatever insr_sync_every is (a
         # loop that never syncs -- bench.py's 1e9 -- is still checked once per phase)
-        for net in m._trainable_networks.values():
-            if hasattr(net, "check_weight_planes"):
-                net.check_weight_planes()
+        MLP.check_weight_planes_all(m._trainable_networks.values())
         self.graph = self.graph2 = None
         self.static = None

@@ -295,6 +295,28 @@ class MLP(nn.Module):
                                   "(f16x3 products); run this network at precision='bf16x6' with bwd_f16=0")
         nat.check(rc, "insr_siren_wsplit_status")
 
+    def _status_word(self):
+        """The fp16 planes' range status quad's first word (a view into the flat storage, as int32), or
+        None when this network's jets do not read the fp16 planes (insr_siren_wsplit_status's word)."""
+        if self._flat is None or not self._flat.is_cuda or self.num_hidden_layers == 0 or not self.uses_f16_planes():
+            return None
+        off = self.wsplit_offset() + 5 * self.num_hidden_layers * self.kernel_width ** 2
+        return self._store[off:off + 1].view(torch.int32)
+
+    @staticmethod
+    def check_weight_planes_all(nets):
+        """check_weight_planes of several networks with ONE device-to-host read of their status words
+        (the training loop's sync points: one small copy instead of a stream sync + copy per network)."""
+        words = [(n, w) for n in nets if isinstance(n, MLP) for w in (n._status_word(),) if w is not None]
+        if not words:
+            return
+        vals = torch.cat([w for _, w in words]).cpu()
+        for (net, _), v in zip(words, vals.tolist()):
+            if v:
+                from . import _native as nat
+                raise nat.NativeError("a hidden weight reached |w| >= 255: outside the fp16 weight planes' range "
+                                      "(f16x3 products); run this network at precision='bf16x6' with bwd_f16=0")
+
     def mark_wsplit_current(self):
         """The planes were rewritten with the parameters (insr_adam_step_nets)."""
         self._wsplit_stamp = self._param_versions()

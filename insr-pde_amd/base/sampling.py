@@ -264,17 +264,8 @@ class draw_ahead:
 
     def __enter__(self):
         self.saved, self.store, self.key, self.pos = draw_ahead.active, None, None, 0
-        self.prefetch = {}  # per-group state of a model's target prefetch (pde/fluid.py _prefetched)
         draw_ahead.active = self if self.reps > 1 else None
         return self
-
-    def rep_of(self, buf):
-        """The repetition index of a buffer take() handed out in this group, or None."""
-        if self.store is None or buf.dim() != 2 or buf.untyped_storage().data_ptr() != \
-                self.store.untyped_storage().data_ptr():
-            return None
-        r, rem = divmod(buf.storage_offset() - self.store.storage_offset(), self.store.stride(0))
-        return r if rem == 0 and 0 <= r < self.reps else None
 
     def __exit__(self, *exc):
         draw_ahead.active = self.saved

@@ -19,9 +19,7 @@ from base import (BaseModel, advect_target, axpy_clamp, divergence, fused_forwar
                   laplace,
                   merge_samples, mse_term, sample_boundary2D_pair, sample_boundary2D_separate, sample_random,
                   sample_random_and_bands2D, sample_uniform, sq_losses, wall_mse, wall_term)
-from base import _jet, _native
 from base.diff_ops import jacobian_only
-from base.sampling import draw_ahead
 
 from .examples import get_examples
 
@@ -145,61 +143,6 @@ class Fluid2DModel(BaseModel):
         with torch.no_grad():  # both detached in the reference as well
             return self.velocity_field_prev(x).detach(), gradient(self.pressure_field(x), x)
 
-    # Target prefetch (cfg.insr_prefetch_targets): the targets of a phase -- no-grad jets of the networks
-    # the phase does not train (the previous velocity, the velocity in the pressure solve, the pressure in
-    # the projection: frozen for the whole phase loop) -- depend on an iteration's points only.  In a
-    # replayed group of U iterations (base/_loop.py run_group) every iteration's points are drawn up front
-    # (base.sampling.draw_ahead), so the first iteration launches the targets of all U on a side stream
-    # (an event after each); iteration r's trainable jet runs on the main stream meanwhile and its loss
-    # waits for event r.  The same jets on the same points (bit-identical targets); what moves is when
-    # they run: into the resources the previous iterations' backward and Adam launches leave idle.
-    def _prefetch_begin(self, kind, buf, n, make):
-        """Handle (outputs, events, rep) of this iteration's prefetched targets, or None (not in a
-        prefetching group).  The group's first call launches make(points of rep q) for every rep q."""
-        ahead = draw_ahead.active
-        if ahead is None or not getattr(self.cfg, "insr_prefetch_targets", False):
-            return None
-        r = ahead.rep_of(buf)
-        if r is None:
-            return None
-        st = ahead.prefetch.get(kind)
-        if st is None:
-            cur = torch.cuda.current_stream(self.device)
-            side = self.__dict__.get("_insr_prefetch_stream")
-            if side is None:
-                side = self._insr_prefetch_stream = torch.cuda.Stream(device=self.device)
-            side.wait_stream(cur)  # the group's sampler launch (nothing of this iteration is queued yet)
-            outs, evs = [], []
-            with torch.cuda.stream(side), torch.no_grad():
-                for q in range(ahead.reps):
-                    outs.append(make(ahead.store[q][:n]))
-                    ev = torch.cuda.Event()
-                    ev.record(side)
-                    evs.append(ev)
-            st = ahead.prefetch[kind] = (outs, evs)
-        return st[0], st[1], r
-
-    def _prefetch_end(self, h):
-        """The targets of handle h, the main stream ordered after them."""
-        outs, evs, r = h
-        cur = torch.cuda.current_stream(self.device)
-        cur.wait_event(evs[r])
-        for t in (outs[r] if isinstance(outs[r], tuple) else (outs[r],)):
-            t.record_stream(cur)
-        return outs[r]
-
-    def _adv_target_of(self, xq):
-        return advect_target(self.velocity_field_prev, xq, self.cfg.dt, -1.0, 1.0)[0]
-
-    def _vel_jacobian_of(self, xq):
-        return _jet.run_jet(self.velocity_field, xq, _native.MODE_GRAD)[1]  # (n, 2, 2)
-
-    def _proj_targets_of(self, xq):
-        with fused_forwards():
-            u_prev = _jet.run_jet(self.velocity_field_prev, xq, _native.MODE_VALUE)[0]
-            J = _jet.run_jet(self.pressure_field, xq, _native.MODE_GRAD)[1]
-        return u_prev, J
-
     # Horizontal fusion (cfg.insr_fuse_forwards, default on):
     # the frozen field's value jet and the trainable field's value jet at the same points
     # are independent -- ONE insr_siren_jet_fwd_multi launch holds two blocks per CU
@@ -212,12 +155,6 @@ class Fluid2DModel(BaseModel):
         x = self._sample_in_training()
         if self._fused_pair():
             xa, n, nb = self._merged(x)
-            h = self._prefetch_begin("advect", xa, n, self._adv_target_of)
-            if h is not None:
-                ua = self.velocity_field(xa)
-                u_target = self._prefetch_end(h)
-                main, bc = sq_losses(mse_term(ua, u_target, count=u_target.numel()), wall_term(ua, nb, row0=n))
-                return {'main': main, 'bc': bc}
             # the frozen field's semi-Lagrangian target u_prev(clamp(x - dt u_prev(x), -1, 1))
             # (two value jets and the foot, point-local: one job) beside the trainable field's
             # value jet over [x; bands]: one mixed launch
@@ -241,13 +178,6 @@ class Fluid2DModel(BaseModel):
             # instead of a separate gradient jet + reverse jet for 2% of the points.  The
             # Laplacian rows of the band points get zero adjoint.
             xa, n, nb = self._merged(x)
-            h = self._prefetch_begin("pressure", xa, n, self._vel_jacobian_of)
-            if h is not None:
-                lap_p, grad_p = laplace(self.pressure_field(xa), xa, return_grad=True)
-                Ju = self._prefetch_end(h)
-                main, bc = sq_losses(mse_term(lap_p, Ju[:, 0, 0], Ju[:, 1, 1], alpha=1.0, beta=-1.0, gamma=-1.0,
-                                              count=n), wall_term(grad_p, nb, row0=n))
-                return {'main': main, 'bc': bc}
             # the velocity's Jacobian jet and the pressure's Laplacian jet are independent: one
             # mixed-mode launch (base.fused_forwards); outputs are read after the scope
             with fused_forwards():
@@ -269,13 +199,6 @@ class Fluid2DModel(BaseModel):
         x = self._sample_in_training()
         if self._fused_pair():
             xa, n, nb = self._merged(x)
-            h = self._prefetch_begin("projection", xa, n, self._proj_targets_of)
-            if h is not None:
-                ua = self.velocity_field(xa)
-                u_prev, Jp = self._prefetch_end(h)
-                main, bc = sq_losses(mse_term(ua, None, u_prev, Jp.squeeze(-2), gamma=-1.0, delta=-1.0,
-                                              count=u_prev.numel()), wall_term(ua, nb, row0=n))
-                return {'main': main, 'bc': bc}
             # frozen velocity (value), pressure gradient (detached) and the trainable velocity
             # over [x; bands]: independent jets, one mixed-mode launch
             with fused_forwards():

@@ -372,33 +372,6 @@ def test_training_loop_unrolled_graph_matches(ph):
         assert res[U][2] == res[1][2], U  # the same iterations read, the same losses
 
 
-@pytest.mark.parametrize("phase", ["_advect_velocity", "_solve_pressure", "_projection"])
-def test_prefetched_targets_bit_identical(ph, phase):
-    """cfg.insr_prefetch_targets: inside a replayed group of U iterations the phase's targets (the frozen
-    networks' no-grad jets) of all U iterations run on a side stream, each iteration's loss waiting for
-    its own -- the same jets on the same points, so parameters, optimiser state and the losses the loop
-    reads equal the mixed-launch path bit for bit."""
-    from pde.fluid import Fluid2DModel
-    res = {}
-    for pre in (False, True):
-        torch.manual_seed(0)
-        cfg = _cfg("fluid", num_hidden_layers=4, hidden_features=128, sample_resolution=32, max_n_iters=10,
-                   insr_graph=True, insr_sync_every=4, insr_graph_unroll=4, insr_prefetch_targets=pre)
-        model = Fluid2DModel(cfg)
-        set_flat(model.velocity_field, ph["fluid/vel/params0"])
-        set_flat(model.velocity_field_prev, ph["fluid/vel_prev/params0"])
-        set_flat(model.pressure_field, ph["fluid/pres/params0"])
-        model.timestep = 1
-        seen = []
-        model.tb = type("TB", (), {"add_scalars": lambda self, tag, vals, global_step: seen.append(
-            (global_step, vals["main"], vals["bc"]))})()
-        getattr(model, phase)()
-        assert getattr(model, "_insr_capture_error", None) is None
-        res[pre] = (flat(model.velocity_field), flat(model.pressure_field), model.optimizer.state.cpu().numpy(), seen)
-    assert np.array_equal(res[True][0], res[False][0]) and np.array_equal(res[True][1], res[False][1])
-    assert np.array_equal(res[True][2], res[False][2]) and res[True][3] == res[False][3]
-
-
 @pytest.mark.parametrize("policy", [None, 5])
 @pytest.mark.parametrize("graph", [False, True])
 def test_fused_sums_adam_bit_identical(ph, graph, policy):

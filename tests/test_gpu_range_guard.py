@@ -86,3 +86,24 @@ def test_bf16x6_network_ignores_the_fp16_planes(B):
     assert torch.isfinite(lp).all()
     for q in net.parameters():
         assert q.grad is None or torch.isfinite(q.grad).all()
+
+
+def test_batched_check_of_several_networks(B):
+    """MLP.check_weight_planes_all (the training loop's sync points and phase end): one read of every
+    network's status word; raises when any network's planes are flagged, passes otherwise, skips networks
+    that do not read the fp16 planes and non-kernel networks."""
+    nat = B._native
+    torch.manual_seed(63)
+    a = B.MLP(2, 1, 4, 128, nonlinearity="sine").cuda()
+    b = B.MLP(2, 2, 4, 128, nonlinearity="sine").cuda()
+    t = B.MLP(2, 1, 2, 16, nonlinearity="relu").cuda()  # TorchMLP: no planes
+    for n in (a, b):
+        n.refresh_wsplit()
+    B.MLP.check_weight_planes_all([a, b, t])
+    with torch.no_grad():
+        b.net[2].weight[0, 0] = -400.0
+    b.refresh_wsplit()
+    assert status(B, b) == nat.ERANGE
+    with pytest.raises(nat.NativeError):
+        B.MLP.check_weight_planes_all([a, b, t])
+    B.MLP.check_weight_planes_all([a, t])

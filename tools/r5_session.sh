@@ -24,9 +24,6 @@ for s in ${STEPS:-tests bench prof}; do
     pol4) run pol4_shard 300 python bench.py --config fluid2DtlgnM --shard-of 8 --bwd-policy 4 --steps 20 --warmup 3 --no-cpu-baseline --no-roofline
           run pol4_head 300 python bench.py --bwd-policy 4 --steps 20 --warmup 3 --no-cpu-baseline --no-roofline ;;
     profdp) run profdp 300 rocprofv3 --kernel-trace --stats -d "$PWD/$O/profdp" -o run --output-format csv -- python bench.py --config fluid2DtlgnM --shard-of 8 --dp-path --steps 10 --warmup 3 --no-cpu-baseline --no-roofline ;;
-    overlap) run overlap 300 python tools/overlap_probe.py ;;
-    pref) for v in 0 1 0 1; do run pref_head_$v 300 python bench.py --prefetch-targets $v --steps 40 --warmup 3 --no-cpu-baseline --no-roofline
-                               run pref_shard_$v 300 python bench.py --config fluid2DtlgnM --shard-of 8 --prefetch-targets $v --steps 40 --warmup 3 --no-cpu-baseline --no-roofline; done ;;
     prof) run prof 300 rocprofv3 --kernel-trace --stats -d "$PWD/$O/prof" -o run --output-format csv -- python bench.py --steps 10 --warmup 3 --no-cpu-baseline ;;
     profshard) run profshard 300 rocprofv3 --kernel-trace --stats -d "$PWD/$O/profshard" -o run --output-format csv -- python bench.py --config fluid2DtlgnM --shard-of 8 --steps 10 --warmup 3 --no-cpu-baseline --no-roofline ;;
     kbench) run kbench 400 python tools/kbench.py ${KARGS:---sizes 8192,16708,66844 --nets fluid_pres --modes lap --variants h3 --policies 0,2} ;;
