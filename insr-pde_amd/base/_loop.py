@@ -11,12 +11,13 @@ Differences, all controlled by cfg attributes:
       allocator settle); iteration 1 is captured into a hipGraph and every
       later iteration is one graph replay.  If capture fails (e.g. a phase
       with data-dependent shapes or host syncs) the loop stays eager.
-      Under data parallelism the iteration is two graphs -- [phase + backward +
-      the gradients' and losses' arena pack] and [1/world + Adam + plateau, which
-      read the arena in place] -- with the single RCCL all-reduce of that arena
-      issued eagerly between them (no collective inside a capture; nothing else
-      eager).
-  insr_graph_unroll (int, default 1) -- single process only: U > 1 also captures U
+      Under data parallelism with RCCL the all-reduce is captured too: one graph per
+      iteration.  A backend whose collective cannot be captured (gloo) or
+      cfg.insr_dp_capture = False gives two graphs -- [phase + backward + the
+      gradients' and losses' arena pack] and [1/world + Adam + plateau, which read
+      the arena in place] -- with the single all-reduce of that arena issued
+      eagerly between them.
+  insr_graph_unroll (int, default 1) -- single process or captured collectives: U > 1 also captures U
       consecutive iterations into ONE graph and replays that for every group of U
       iterations that holds no host read (sync / vis point) before its last one.  Each
       iteration inside is a full one (its own collocation points, backward, Adam + plateau
@@ -114,9 +115,23 @@ class PhaseLoop:
         torch.cuda.current_stream(m.device).wait_stream(side)
         return g, out
 
+    def _dp_split(self):
+        """Whether a data-parallel iteration is replayed as two graphs around an EAGER all-reduce: the
+        collective cannot be captured (gloo: host-side) or cfg.insr_dp_capture is off.  With RCCL
+        (backend 'nccl') the all-reduce is captured with the rest of the iteration: ONE graph per
+        iteration (or per group of insr_graph_unroll iterations), no host round trip between the
+        backward and the optimiser step (profiles/r05: two host gaps of ~18 + ~9 us per iteration in
+        the split form)."""
+        if not self.m._dp_active():
+            return False
+        if not getattr(self.m.cfg, "insr_dp_capture", True):
+            return True
+        d = torch.distributed
+        return d.get_backend() != "nccl" or torch.device(self.m.device).type != "cuda"
+
     def _capture(self):
         try:
-            if self.m._dp_active():
+            if self._dp_split():
                 g1, out = self._capture_graph(self._stage1)
                 g2, _ = self._capture_graph(self._stage2)
                 self.graph, self.graph2 = g1, g2
@@ -144,7 +159,7 @@ class PhaseLoop:
         """Whether run_group() may serve the next `unroll` iterations (graph mode, one process,
         the single-iteration graph already captured: iterations 0 and 1 ran)."""
         return (self.unroll > 1 and self.use_graph and self.graph is not None and self.graph2 is None
-                and not self.m._dp_active())
+                and not self._dp_split())
 
     def run_group(self):
         """`unroll` consecutive iterations as ONE graph replay (captured on first use -- a capture
@@ -179,7 +194,7 @@ class PhaseLoop:
 
     def step(self, i):
         """Run iteration i; returns the device loss dict of that iteration."""
-        dp = self.m._dp_active()
+        dp = self._dp_split()
         if self.use_graph and i >= 1:
             if self.graph is None and self._capture() is None:
                 return self._dp_step_eager() if dp else self._body()

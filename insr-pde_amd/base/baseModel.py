@@ -173,7 +173,13 @@ class BaseModel(ABC):
 
     def _dp_pack(self, loss_dict):
         """The iteration's gradients and losses as one contiguous arena slice (self._insr_dp_red);
-        returns the losses as views of its tail (the values after _dp_allreduce/_dp_finish)."""
+        returns the losses as views of their arena slots (the values after _dp_allreduce/_dp_finish).
+
+        Arena layout [net 0 | loss slots | net 1 | net 2 ...] (each network's flat .grad bound to its
+        slice on the first call): the slice reduced is the smallest contiguous span covering the loss
+        slots and every network this iteration's backward reached -- a phase that trains one of two
+        networks (every fluid phase) all-reduces [its gradient | losses] only, with no zero-fill of the
+        other network (untouched networks inside the span are zero-filled: they add nothing)."""
         if not self._dp_active():
             return loss_dict
         nets = list(self._trainable_networks.values())
@@ -185,24 +191,29 @@ class BaseModel(ABC):
                 if hasattr(net, "grad_read_sync"):
                     net.grad_read_sync(cur)
         sizes = [net.param_count for net in nets]
-        total = sum(sizes)
+        nslots = max(len(keys), 8)
         arena = self.__dict__.get("_insr_dp_arena")
-        if arena is None or arena.numel() < total + len(keys) or arena.device != dev:
-            arena = torch.zeros(total + max(len(keys), 8), device=dev, dtype=torch.float32)
+        if arena is None or arena.numel() < sum(sizes) + nslots or arena.device != dev:
+            arena = torch.zeros(sum(sizes) + nslots, device=dev, dtype=torch.float32)
             self._insr_dp_arena = arena
-            off = 0
-            for net, n in zip(nets, sizes):
+            offs, off = [], 0
+            for i, (net, n) in enumerate(zip(nets, sizes)):
+                if i == 1:
+                    off += nslots  # the loss slots sit between the first and the second network
+                offs.append(off)
                 net.bind_flat_grad(arena[off:off + n])
                 off += n
+            self._insr_dp_offs, self._insr_dp_loss_off = offs, sizes[0]
+        offs, loss_off = self._insr_dp_offs, self._insr_dp_loss_off
         touched = [net.grad_touched() for net in nets]
-        off = 0
-        for net, n, t in zip(nets, sizes, touched):
-            if not t:
-                arena[off:off + n].zero_()
-            off += n
-        tail = arena[total:total + len(keys)]
+        lo = min([loss_off] + [o for o, t in zip(offs, touched) if t])
+        hi = max([loss_off + len(keys)] + [o + n for o, n, t in zip(offs, sizes, touched) if t])
+        for o, n, t in zip(offs, sizes, touched):
+            if not t and lo <= o < hi:
+                arena[o:o + n].zero_()
+        tail = arena[loss_off:loss_off + len(keys)]
         torch.stack([torch.as_tensor(loss_dict[k], device=dev).detach().float().reshape(()) for k in keys], out=tail)
-        self._insr_dp_red = arena[:total + len(keys)]
+        self._insr_dp_red = arena[lo:hi]
         return {k: tail[i] for i, k in enumerate(keys)}
 
     def _update_network(self, loss_dict):

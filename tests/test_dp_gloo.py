@@ -59,14 +59,16 @@ def _worker(rank, world, port, reduction, q):
     out = m._dp_sync(losses)
     res = (rank, m.a.flat_grad_buffer().clone(), m.b.flat_grad_buffer().clone(),
            {k: float(v) for k, v in out.items()}, m.a.grad_touched())
-    # second iteration: b receives no gradient (zero_grad, no backward reaches it) -> it is
-    # summed as zeros and stays untouched (Adam skips it, as torch skips .grad None)
+    # second iteration: b receives no gradient (zero_grad, no backward reaches it) -> it stays out of
+    # the reduced span (arena [a | losses | b]: only [a | losses] is all-reduced) and untouched (Adam
+    # skips it, as torch skips .grad None)
     m.b.mark_grad_stale(set_to_none=True)
     ga = m.a.flat_grad_buffer()
     ga.fill_(float(rank + 1))
     m._dp_sync({"main": torch.tensor(0.0)})
-    res2 = (m.a.flat_grad_buffer().clone(), m.b.grad_touched(),
-            float(m._insr_dp_arena[m.a.param_count:m.a.param_count + m.b.param_count].abs().max()))
+    red = m._insr_dp_red
+    b_in_span = red.data_ptr() <= m.b._flat_grad.data_ptr() < red.data_ptr() + 4 * red.numel()
+    res2 = (m.a.flat_grad_buffer().clone(), m.b.grad_touched(), float(b_in_span))
     # plain numpy by value: a queued tensor travels as a shared-memory fd that the parent may
     # try to fetch after this process has exited (ConnectionResetError)
     q.put(tuple(v.numpy().copy() if isinstance(v, torch.Tensor) else v for v in res + res2))
@@ -91,7 +93,7 @@ def test_dp_sync_two_ranks(reduction, world):
     rsum = sum(r + 1 for r in range(world))  # sum over ranks of (rank + 1)
     for rank, ga, gb, losses, touched, ga2, b_touched2, b_arena_max in res:
         assert torch.allclose(ga2, torch.full_like(ga2, rsum * scale))
-        assert not b_touched2 and b_arena_max == 0.0
+        assert not b_touched2 and b_arena_max == 0.0  # (here: b's slice is outside the reduced span)
         n_a = ga.numel()
         expect_a = torch.arange(n_a, dtype=torch.float32) * rsum * scale
         expect_b = (torch.arange(gb.numel(), dtype=torch.float32) * rsum + world) * scale
