@@ -135,6 +135,12 @@ class BaseModel(ABC):
         d = torch.distributed
         return d.get_world_size() if (d.is_available() and d.is_initialized()) else 1
 
+    def _dp_total(self, count):
+        """The denominator of a mean over `count` local terms: under data parallelism the global count
+        (every rank holds an equal share), so the ranks' means -- values and gradients -- SUM to the global
+        mean (models whose losses use it declare _dp_loss_reduction = 'sum': no 1/world pass)."""
+        return count * self._dp_world() if self._dp_active() else count
+
     def _dp_active(self):
         """Whether iterations take the data-parallel path (gradient arena + all-reduce): world > 1, or
         cfg.insr_dp_always with a process group of any size (bench.py --dp-path: one rank's DP step,

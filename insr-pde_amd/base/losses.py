@@ -117,7 +117,7 @@ class LossSpec:
 
 
 def _mse_spec(a, b=None, c=None, d=None, alpha=1.0, beta=-1.0, gamma=1.0, delta=1.0, count=None, a_row0=0,
-              reduction="mean"):
+              reduction="mean", total=None):
     if count is None:
         for t in (b, c, d):
             if t is not None and t.shape != a.shape:
@@ -132,17 +132,19 @@ def _mse_spec(a, b=None, c=None, d=None, alpha=1.0, beta=-1.0, gamma=1.0, delta=
         raise ValueError("fused_mse: d needs c")
     if reduction not in ("mean", "sum"):
         raise ValueError(reduction)
-    scale = 1.0 / max(count, 1) if reduction == "mean" else 1.0
+    # total: the denominator of the mean (default: the terms summed here) -- under data parallelism the
+    # GLOBAL term count, so the ranks' losses and gradients sum to the global mean (no 1/world pass)
+    scale = 1.0 / max(count if total is None else total, 1) if reduction == "mean" else 1.0
     (b, sb), (c, sc), (d, sd) = _prep_strided(b), _prep_strided(c), _prep_strided(d)
     return LossSpec(nat.LOSS_COMBO, count, 1, (alpha, beta, gamma, delta), scale, _prep(a), b, c, d, a_off,
                     (sb, sc, sd))
 
 
-def _wall_spec(y, n, row0=0):
+def _wall_spec(y, n, row0=0, total=None):
     if y.dim() != 2 or y.shape[0] < row0 + 2 * n or y.shape[1] < 2 or (row0 == 0 and y.shape[0] != 2 * n):
         raise ValueError(f"wall_mse: expected ({row0} + 2*{n} rows, m>=2), got {tuple(y.shape)}")
-    return LossSpec(nat.LOSS_BANDS, n, y.shape[1], (0.0, 0.0, 0.0, 0.0), 1.0 / max(n, 1), _prep(y), None, None, None,
-                    int(row0) * y.shape[1])
+    return LossSpec(nat.LOSS_BANDS, n, y.shape[1], (0.0, 0.0, 0.0, 0.0), 1.0 / max(n if total is None else total, 1),
+                    _prep(y), None, None, None, int(row0) * y.shape[1])
 
 
 def mse_term(*args, **kwargs):
@@ -150,9 +152,9 @@ def mse_term(*args, **kwargs):
     return _mse_spec(*args, **kwargs)
 
 
-def wall_term(y, n, row0=0):
-    """The loss of wall_mse(y, n, row0), unlaunched: an argument of sq_losses()."""
-    return _wall_spec(y, n, row0)
+def wall_term(y, n, row0=0, total=None):
+    """The loss of wall_mse(y, n, row0, total), unlaunched: an argument of sq_losses()."""
+    return _wall_spec(y, n, row0, total)
 
 
 def _shared_a(specs):
@@ -273,22 +275,24 @@ def sq_losses(*specs):
 
 
 def fused_mse(a, b=None, c=None, d=None, alpha=1.0, beta=-1.0, gamma=1.0, delta=1.0, count=None, a_row0=0,
-              reduction="mean"):
+              reduction="mean", total=None):
     """mean((alpha*(a + beta*b) + gamma*(c + delta*d))**2) over all elements; b, c, d are
     None or the shape of a (d needs c).  fused_mse(u, target) == F.mse_loss(u, target).
 
     Merged jet launches (interior + boundary points of one network in one launch):
     count = number of terms; every tensor is read from its first element except `a`,
     which starts at row a_row0; elements outside the range get zero gradient.
-    reduction="sum" returns the sum instead of the mean."""
-    return sq_losses(_mse_spec(a, b, c, d, alpha, beta, gamma, delta, count, a_row0, reduction))[0]
+    reduction="sum" returns the sum instead of the mean; total = the mean's denominator when it is not
+    the number of terms summed here (a data-parallel rank's share of a global mean)."""
+    return sq_losses(_mse_spec(a, b, c, d, alpha, beta, gamma, delta, count, a_row0, reduction, total))[0]
 
 
-def wall_mse(y, n, row0=0):
+def wall_mse(y, n, row0=0, total=None):
     """mean(y[r:r+n, 0]**2) + mean(y[r+n:r+2n, 1]**2), r = row0, for y of shape (R, m),
     m >= 2, R >= r + 2n (the normal-component wall terms of both boundary bands in one
-    launch; the other rows -- a merged launch's interior points -- get zero gradient)."""
-    return sq_losses(_wall_spec(y, n, row0))[0]
+    launch; the other rows -- a merged launch's interior points -- get zero gradient);
+    total = the means' denominator (default n)."""
+    return sq_losses(_wall_spec(y, n, row0, total))[0]
 
 
 def axpy_clamp(x, y, alpha, lo, hi):

@@ -13,6 +13,7 @@ from .examples import get_examples
 
 class Advection1DModel(BaseModel):
     """advection equation with constant velocity"""
+    _dp_loss_reduction = 'sum'  # means over the GLOBAL point count (BaseModel._dp_total): no 1/world pass
 
     def __init__(self, cfg):
         super().__init__(cfg)
@@ -48,7 +49,8 @@ class Advection1DModel(BaseModel):
     @BaseModel._training_loop
     def _initialize(self):
         x = self._sample_in_training()
-        return {'main': fused_mse(self.field(x), self.init_cond_func(x))}
+        target = self.init_cond_func(x)
+        return {'main': fused_mse(self.field(x), target, total=self._dp_total(target.numel()))}
 
     @BaseModel._timestepping
     def step(self):
@@ -71,8 +73,9 @@ class Advection1DModel(BaseModel):
         uxa = gradient(ua, xa)
         xb = xa[n:]
         # mean(((u - u0)/dt + vel (ux + u0x)/2)^2) over the interior rows, one fused launch each way
-        main = fused_mse(ua, u0, uxa, u0x, alpha=1.0 / self.dt, beta=-1.0, gamma=self.vel / 2., delta=1.0, count=n)
-        return {'main': main, 'bc': fused_mse(ua, count=xb.shape[0], a_row0=n)}
+        main = fused_mse(ua, u0, uxa, u0x, alpha=1.0 / self.dt, beta=-1.0, gamma=self.vel / 2., delta=1.0, count=n,
+                         total=self._dp_total(n))
+        return {'main': main, 'bc': fused_mse(ua, count=xb.shape[0], a_row0=n, total=self._dp_total(xb.shape[0]))}
 
     def _advect_points(self, n_bc):
         """(x, xa = [x; boundary band]) of one iteration.  On the GPU one sampler launch

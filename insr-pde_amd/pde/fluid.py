@@ -26,6 +26,9 @@ from .examples import get_examples
 
 class Fluid2DModel(BaseModel):
     """inviscid Navier-Stokes equation. 2D fluid. [-1, 1]^2."""
+    # every loss below is a mean over the GLOBAL point count (BaseModel._dp_total): the ranks' losses
+    # and gradients sum to the global means, so the all-reduce needs no 1/world pass
+    _dp_loss_reduction = 'sum'
 
     def __init__(self, cfg):
         super().__init__(cfg)
@@ -102,7 +105,8 @@ class Fluid2DModel(BaseModel):
     @BaseModel._training_loop
     def _initialize(self):
         x = self._sample_in_training()
-        return {'main': fused_mse(self.velocity_field(x), self.init_cond_func(x))}
+        target = self.init_cond_func(x)
+        return {'main': fused_mse(self.velocity_field(x), target, total=self._dp_total(target.numel()))}
 
     @BaseModel._timestepping
     def step(self):
@@ -121,13 +125,13 @@ class Fluid2DModel(BaseModel):
         """u_x = 0 on the x-faces, u_y = 0 on the y-faces: mean(u_x^2) + mean(u_y^2)
         (fluid/model.py:90-94) as one jet launch and one fused loss launch."""
         bxy, nb = self._boundary_bands(n_interior)
-        return wall_mse(self.velocity_field(bxy), nb)
+        return wall_mse(self.velocity_field(bxy), nb, total=self._dp_total(nb))
 
     def _pressure_wall_loss(self, n_interior):
         """mean(dp/dx^2) + mean(dp/dy^2) on the bands (fluid/model.py:116-120)."""
         bxy, nb = self._boundary_bands(n_interior)  # one jet launch for both bands
         gp = gradient(self.pressure_field(bxy), bxy)
-        return wall_mse(gp, nb)
+        return wall_mse(gp, nb, total=self._dp_total(nb))
 
     def _advect_target(self, x):
         with torch.no_grad():
@@ -163,11 +167,12 @@ class Fluid2DModel(BaseModel):
                 ua = self.velocity_field(xa)
             # mean((u - u_target)^2) over the interior rows and the wall terms on the band rows,
             # one launch
-            main, bc = sq_losses(mse_term(ua, u_target, count=u_target.numel()), wall_term(ua, nb, row0=n))
+            main, bc = sq_losses(mse_term(ua, u_target, count=u_target.numel(), total=self._dp_total(u_target.numel())),
+                                 wall_term(ua, nb, row0=n, total=self._dp_total(nb)))
             return {'main': main, 'bc': bc}
         bc = self._wall_loss(x.shape[0])
         u_target = self._advect_target(x)
-        return {'main': fused_mse(self.velocity_field(x), u_target), 'bc': bc}
+        return {'main': fused_mse(self.velocity_field(x), u_target, total=self._dp_total(u_target.numel())), 'bc': bc}
 
     @BaseModel._training_loop
     def _solve_pressure(self):
@@ -186,12 +191,13 @@ class Fluid2DModel(BaseModel):
                 lap_p, grad_p = laplace(self.pressure_field(xa), xa, return_grad=True)
             # mean((lap p - du/dx - dv/dy)^2) over the interior rows (= mean((div u - lap p)^2))
             # and the wall terms, one launch; the diagonal of J is read in place (stride 4)
-            main, bc = sq_losses(mse_term(lap_p, Ju[:, 0, 0], Ju[:, 1, 1], alpha=1.0, beta=-1.0, gamma=-1.0, count=n),
-                                 wall_term(grad_p, nb, row0=n))
+            main, bc = sq_losses(mse_term(lap_p, Ju[:, 0, 0], Ju[:, 1, 1], alpha=1.0, beta=-1.0, gamma=-1.0, count=n,
+                                          total=self._dp_total(n)),
+                                 wall_term(grad_p, nb, row0=n, total=self._dp_total(nb)))
             return {'main': main, 'bc': bc}
         bc = self._pressure_wall_loss(x.shape[0])
         div_u = self._velocity_divergence(x)
-        main = fused_mse(div_u, laplace(self.pressure_field(x), x))  # mean((div u - lap p)^2), rho = 1
+        main = fused_mse(div_u, laplace(self.pressure_field(x), x), total=self._dp_total(div_u.numel()))  # rho = 1
         return {'main': main, 'bc': bc}
 
     @BaseModel._training_loop
@@ -207,13 +213,15 @@ class Fluid2DModel(BaseModel):
                     grad_p = gradient(self.pressure_field(x), x)
                 ua = self.velocity_field(xa)
             u_prev = u_prev.detach()
-            main, bc = sq_losses(mse_term(ua, None, u_prev, grad_p, gamma=-1.0, delta=-1.0, count=u_prev.numel()),
-                                 wall_term(ua, nb, row0=n))
+            main, bc = sq_losses(mse_term(ua, None, u_prev, grad_p, gamma=-1.0, delta=-1.0, count=u_prev.numel(),
+                                          total=self._dp_total(u_prev.numel())),
+                                 wall_term(ua, nb, row0=n, total=self._dp_total(nb)))
             return {'main': main, 'bc': bc}
         bc = self._wall_loss(x.shape[0])
         u_prev, grad_p = self._projection_target(x)
         # mean((u - (u_prev - grad_p))^2): r = 1*(u + 0) + (-1)*(u_prev + (-1)*grad_p)
-        main = fused_mse(self.velocity_field(x), None, u_prev, grad_p, gamma=-1.0, delta=-1.0)
+        main = fused_mse(self.velocity_field(x), None, u_prev, grad_p, gamma=-1.0, delta=-1.0,
+                         total=self._dp_total(u_prev.numel()))
         return {'main': main, 'bc': bc}
 
     # ---- output (host side; PNG figures are out of scope) ---------------------
