@@ -602,6 +602,12 @@ struct FwdMixX6 {
 // instance that covers its jobs (value + advect: 62 VGPRs, four blocks per CU; with a
 // Laplacian body: 90)
 constexpr int kMixV = 1, kMixG = 2, kMixL = 4, kMixA = 8;
+// tiles per block of the advection target job (its two value jets run back to back in one block: the
+// longest chain of the advection phase's launch)
+#ifndef INSR_MIX_ADV_T
+#define INSR_MIX_ADV_T 2
+#endif
+constexpr int kMixAdvT = INSR_MIX_ADV_T;
 
 template <int NQ, int NT, int DIN, int BODIES>
 constexpr size_t fwd_mix_lds_bytes() {
@@ -647,10 +653,11 @@ __global__ __launch_bounds__(X6Geo<NT>::THREADS, (BODIES & kMixL) ? 6 : 4) void 
       // (fluid/model.py:96-97; every quantity of a point stays in its block: one launch for
       // the frozen field's two value jets and the foot between them)
       const int n = (int)jb.n;
-      block_tiles(lb, n, 2, 0, tile0, cnt);
+      block_tiles(lb, n, kMixAdvT, 0, tile0, cnt);
       float* up = jb.dy;
       float* foot = jb.lap;
-      fwd_x6_block<NQ, NT, 1, false, 2>(jb.x, n, DIN, dk, L, jb.params, up, nullptr, nullptr, nullptr, tile0, cnt);
+      fwd_x6_block<NQ, NT, 1, false, kMixAdvT>(jb.x, n, DIN, dk, L, jb.params, up, nullptr, nullptr, nullptr, tile0,
+                                               cnt);
       // the block's own global writes, read back by its other waves: workgroup scope (the
       // stores drain before the barrier; the lines were never cached in this CU's L1)
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
@@ -663,7 +670,8 @@ __global__ __launch_bounds__(X6Geo<NT>::THREADS, (BODIES & kMixL) ? 6 : 4) void 
       }
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
       __syncthreads();
-      fwd_x6_block<NQ, NT, 1, false, 2>(foot, n, DIN, dk, L, jb.params, jb.y, nullptr, nullptr, nullptr, tile0, cnt);
+      fwd_x6_block<NQ, NT, 1, false, kMixAdvT>(foot, n, DIN, dk, L, jb.params, jb.y, nullptr, nullptr, nullptr, tile0,
+                                               cnt);
       break;
     }
     default:  // never reached: the host validates every job's mode (mixed_jobs_ok, capi.hip)
@@ -691,7 +699,8 @@ int launch_fwd_x6_mixed_t(const InsrJetJob* jobs, const int* modes, const float*
       for (int q = 0; q < 3; ++q) pk.sc[k][q] = scalars ? scalars[3 * k + q] : 0.f;
       pk.first[k] = nb;
       const long tiles = (jobs[k].n + 15) / 16;
-      nb += (int)(modes[k] == INSR_MODE_VALUE || modes[k] == INSR_MIX_ADVECT ? (tiles + 1) / 2 : tiles);
+      nb += (int)(modes[k] == INSR_MODE_VALUE ? (tiles + 1) / 2
+                                              : (modes[k] == INSR_MIX_ADVECT ? (tiles + kMixAdvT - 1) / kMixAdvT : tiles));
     }
     pk.first[njobs] = nb;
     pk.njobs = njobs;
