@@ -1,6 +1,6 @@
 """The data-parallel iteration with the RCCL all-reduce CAPTURED in the iteration's hipGraph
 (base/_loop.py PhaseLoop._dp_split: backend 'nccl'), on one GPU: a world-1 RCCL process group with
-cfg.insr_dp_always runs the DP code itself -- gradient arena, all-reduce, 1/world, unfused sums +
+cfg.insr_dp_always runs the DP code itself -- gradient arena, all-reduce, global-count loss means, unfused sums +
 Adam + plateau -- so the captured collective (one graph per iteration, groups of insr_graph_unroll
 iterations) can be checked against the two-graph split with the eager all-reduce
 (cfg.insr_dp_capture = False) and against the single-process path (no process group): every

@@ -90,17 +90,17 @@ def check_update(net, ref, p0, lr):
 
 
 # ---------------------------------------------------------------------------------------------
-def _fluid(B, config, hooks):
+def _fluid(B, config, hooks, **over):
     from pde.config import baseline_config
     from pde.fluid import Fluid2DModel
     import pde.fluid as fl
     cfg = baseline_config(config, proj_dir="/tmp/insr_fullsize_phases", insr_progress=False, early_stop=False,
-                          max_n_iters=1, insr_graph=False, insr_sync_every=1)
+                          max_n_iters=1, insr_graph=False, insr_sync_every=1, **over)
     m = Fluid2DModel(cfg)
     m.timestep = 1
     refs = {"vel": seeded(2, 2, 4, 128, 201), "vel_prev": seeded(2, 2, 4, 128, 202), "pres": seeded(2, 1, 4, 128, 203)}
     nets = {"vel": m.velocity_field, "vel_prev": m.velocity_field_prev, "pres": m.pressure_field}
-    N = cfg.sample_resolution ** 2
+    N = getattr(cfg, "insr_points_per_rank", None) or cfg.sample_resolution ** 2
     nb = N // 100
     gen = torch.Generator().manual_seed(301)
     drawn = {}
@@ -166,6 +166,13 @@ def test_fluid2dtlgn_phases_full_size_recorded_samples(B):
 
 def test_fluid2dtlgnM_phases_full_size(B):
     _fluid(B, "fluid2DtlgnM", hooks=False)
+
+
+def test_fluid2dtlgnM_rank_shard_size(B):
+    """One rank's batch of the 8-rank strong-scaling fluid2DtlgnM run (bench.py --shard-of 8):
+    65,536 / 8 = 8,192 interior + 2 x 82 band points (the tile count -- 523 tiles of 16 on 256 CUs --
+    is the shard's quantisation case)."""
+    _fluid(B, "fluid2DtlgnM", hooks=False, insr_points_per_rank=8192)
 
 
 def test_elasticity2dstretch_full_size(B):
