@@ -484,6 +484,67 @@ int insr_sq_loss_bwd(int kind, const float* a, const float* b, const float* c, c
                      float* gb, float* gc, float* gd, void* stream);
 
 /*
+ * Adjoint seeds formed inside the reverse jet (round 5).  The unit-seeded gradient of a loss group
+ * (insr_sq_loss_group) with respect to a jet's own output is point-local -- 2 scale alpha r at a
+ * COMBO term, 2 scale y at a selected BANDS element -- so the backward that consumes it can evaluate
+ * it where it reads its adjoint, and emit the squares of the terms its blocks seed: the group's
+ * launch disappears from the iteration (base/baseModel.py:73-78 seeds every loss with 1;
+ * fluid/model.py:96-101,121-125,147-151 and the wall terms are such groups).  A term seeds the
+ * elements [a_off, a_off + n) (COMBO) / the selected elements of rows a_off / m .. + 2n (BANDS) of
+ * ONE adjoint stream of the jet -- `a` is that stream's output buffer (y, dy or lap), read at the
+ * same elements as insr_sq_loss_group reads them; b, c, d, the coefficients and scale as InsrLoss.
+ * The seeds are bit for bit the gradient insr_sq_loss_group writes; each block of the launch writes
+ * its terms' square sums to loss_part[block][INSR_SEED_MAX] (term `loss` into column `loss`, other
+ * columns 0), and the sums launch that follows the backward finishes the loss values (InsrLossFin:
+ * out[k] = scale[k] * sum over the rows of column k, a fixed order; with an Adam + plateau epilogue,
+ * before the plateau step reads out[0]).
+ */
+#define INSR_SEED_MAX 4
+#define INSR_SEED_VALUE 0 /* the adjoint of y (gy) */
+#define INSR_SEED_GRAD 1  /* of dy (gdy) */
+#define INSR_SEED_LAP 2   /* of lap (glap) */
+typedef struct InsrSeed {
+  int kind;   /* INSR_LOSS_COMBO / INSR_LOSS_BANDS */
+  int m;      /* BANDS: columns of a */
+  int stream; /* INSR_SEED_VALUE / _GRAD / _LAP */
+  int loss;   /* column 0 .. INSR_SEED_MAX - 1 of loss_part */
+  long n, a_off;
+  const float *a, *b, *c, *d;
+  long sb, sc, sd;
+  float alpha, beta, gamma, delta, scale;
+} InsrSeed;
+typedef struct InsrLossFin {
+  const float* part; /* loss_part of the seeded backward */
+  int rows;          /* its rows (insr_jet_bwd_seed_rows) */
+  int nloss;         /* columns 0 .. nloss - 1 -> out[0 .. nloss - 1] */
+  float scale[INSR_SEED_MAX];
+  float* out[INSR_SEED_MAX];
+} InsrLossFin;
+/* Rows of loss_part the seeded backward of this call writes (one per block of its launch); 0 when
+ * the backward the call routes to takes no in-kernel seeds (the fused tile-split path of value jets and
+ * the saved-stream jet_fb sweep do; the two-kernel, split-bf16 resident and recompute paths, the fused
+ * path of gradient / Laplacian jets and jet_fb blocks of more than 24 tiles do not). */
+int insr_jet_bwd_seed_rows(long n_points, int d_in, int d_out, int num_hidden, int width, int mode);
+/* The backward's first launch with seeds: the fused tile-split path (insr_siren_jet_bwd: partial rows
+ * into `work`, summed by insr_reduce_partials_fin / insr_adam_step_partials_fin) or the jet_fb sweep
+ * (insr_siren_jet_bwd_grad_adam phase 1 into `work`, phase 2 by insr_siren_jet_bwd_grad_adam_fin).
+ * A stream with seeds has its adjoint pointer NULL; 1 <= n_seeds <= INSR_SEED_MAX. */
+int insr_siren_jet_bwd_seeded(const float* x, long n_points, int d_in, int d_out, int num_hidden, int width, int mode,
+                              const float* params, const float* act, const float* gy, const float* gdy,
+                              const float* glap, const InsrSeed* seeds, int n_seeds, float* loss_part, float* work,
+                              void* stream);
+int insr_reduce_partials_fin(const float* partial, int n_blocks, long count, long stride, float* grad, int accumulate,
+                             const InsrLossFin* fin, void* stream);
+int insr_adam_step_partials_fin(const float* partial, int nb, long stride, float* grad, int accumulate, float* params,
+                                float* exp_avg, float* exp_avg_sq, long count, const int* shape, float* opt_state,
+                                float beta1, float beta2, float eps, const float* loss, int patience,
+                                const InsrLossFin* fin, void* stream);
+int insr_siren_jet_bwd_grad_adam_fin(const float* x, long n_points, int d_in, int d_out, int num_hidden, int width,
+                                     int mode, float* params, float* work, float* grad, int accumulate, float* exp_avg,
+                                     float* exp_avg_sq, float* opt_state, float beta1, float beta2, float eps,
+                                     const float* loss, int patience, const InsrLossFin* fin, void* stream);
+
+/*
  * Singular-value energies of the elasticity model (elasticity/model.py:143-163):
  *   out = sum_points [ ratio_arap sum_i (s_i - 1)^2 + ratio_volume (prod_i s_i - 1)^2 ],
  * s = singular values of each d x d block of J (n blocks, row-major, d = 2 or 3).

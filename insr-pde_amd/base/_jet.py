@@ -106,6 +106,8 @@ class _SirenJet(torch.autograd.Function):
         ctx.set_materialize_grads(False)  # unused outputs -> None -> NULL adjoint (no zero-fill launch)
         ctx.mode, ctx.cmode, ctx.mlp, ctx.save = mode, cmode, mlp, save  # the backward reuses the forward's mode
         ctx.x2, ctx.act = x2, act
+        # the outputs' buffers (address, elements): a lazy loss group's terms read them (losses.LazyGroup)
+        ctx.out_bufs = tuple((0, 0) if t is None else (t.data_ptr(), t.numel()) for t in (y, dy, lap))
         outs = [y]
         if dy is not None:
             outs.append(dy)
@@ -130,6 +132,7 @@ class _SirenJet(torch.autograd.Function):
             return none
         c = lambda t: None if t is None else (t if t.is_contiguous() else t.contiguous())  # noqa: E731
         job = _BwdJob(mlp, mode, ctx.cmode, ctx.x2, ctx.act, c(gy), c(gdy), c(glap))
+        job.outs = ctx.out_bufs
         queue = _BwdBatch.queue_for(job)
         if queue is not None:  # launched with the network's other jobs at the scope's exit
             queue.append(job)
@@ -178,6 +181,8 @@ def _reference_backward(ctx, grads):
     sum(g_y y + g_dy dy + g_lap lap), as a differentiable graph of torch ops (torch_jet on the
     forward's own x2, so derivatives of the result reach x through x2's graph)."""
     mlp, mode, x2 = ctx.mlp, ctx.mode, ctx.x2
+    from . import losses
+    losses.materialize_for(*grads)  # lazy loss groups: their gradients are read as data here
     params = mlp.plist()
     none = (None,) * (4 + len(params))
     want_x = ctx.needs_input_grad[0]
@@ -212,12 +217,13 @@ class _BwdJob:
     knob bits: the backward runs with the knobs its forward ran with, whatever scope is open
     when autograd reaches it), the forward's points / saved streams, the adjoints, and the
     stream autograd ran its backward on."""
-    __slots__ = ("mlp", "mode", "cmode", "x2", "act", "gy", "gdy", "glap", "cur")
+    __slots__ = ("mlp", "mode", "cmode", "x2", "act", "gy", "gdy", "glap", "cur", "outs")
 
     def __init__(self, mlp, mode, cmode, x2, act, gy, gdy, glap):
         self.mlp, self.mode, self.cmode, self.x2, self.act = mlp, mode, cmode, x2, act
         self.gy, self.gdy, self.glap = gy, gdy, glap
         self.cur = torch.cuda.current_stream(x2.device)
+        self.outs = ((0, 0), (0, 0), (0, 0))  # the forward's (y, dy, lap) buffers (_SirenJet.backward sets them)
 
 
 DEFER_REDUCE = True  # BaseModel._update_network opens defer_reductions (False: A/B studies, tests)
@@ -255,45 +261,117 @@ class PendingSums:
     """The held-back sums of one reverse jet: kind "rows" -- a fused-path backward's partial-gradient
     rows (insr_reduce_partials_strided / insr_adam_step_partials); kind "split" -- the second half of a
     jet_fb.hpp or two-kernel backward (insr_siren_jet_bwd_grad_adam phase 2)."""
-    __slots__ = ("kind", "buf", "nb", "stride", "job", "gflat", "accumulate", "cur", "key")
+    __slots__ = ("kind", "buf", "nb", "stride", "job", "gflat", "accumulate", "cur", "key", "fin")
 
-    def __init__(self, kind, buf, nb, stride, job, gflat, accumulate, cur, key):
+    def __init__(self, kind, buf, nb, stride, job, gflat, accumulate, cur, key, fin=None):
         self.kind, self.buf, self.nb, self.stride, self.job = kind, buf, nb, stride, job
         self.gflat, self.accumulate, self.cur, self.key = gflat, accumulate, cur, key
+        self.fin = fin  # (InsrLossFin, its loss_part tensor): a seeded backward's loss values, finished here
 
     def launch(self, adam=None):
         """The sums into .grad; adam = (params, m, v, state, b1, b2, eps, loss or None, patience): with
-        the Adam (+ plateau) update of every element in the same launch."""
+        the Adam (+ plateau) update of every element in the same launch.  A seeded backward's loss values
+        are finished by the same launch (before its plateau step reads them)."""
         lib = nat.lib()
         st = ctypes.c_void_p(self.cur.cuda_stream)
         p, m, v, state, b1, b2, eps, loss, patience = adam if adam is not None else (None,) * 7 + (None, 0)
+        fin = None if self.fin is None else ctypes.addressof(self.fin[0])
         if self.kind == "rows":
             if adam is None:
                 with _timed("reduce", *self.key):
-                    rc = lib.insr_reduce_partials_strided(nat.ptr(self.buf), self.nb, self.gflat.numel(), self.stride,
-                                                          nat.ptr(self.gflat), self.accumulate, st)
+                    if fin is None:
+                        rc = lib.insr_reduce_partials_strided(nat.ptr(self.buf), self.nb, self.gflat.numel(),
+                                                              self.stride, nat.ptr(self.gflat), self.accumulate, st)
+                    else:
+                        rc = lib.insr_reduce_partials_fin(nat.ptr(self.buf), self.nb, self.gflat.numel(), self.stride,
+                                                          nat.ptr(self.gflat), self.accumulate, fin, st)
                 nat.check(rc, "insr_reduce_partials_strided")
                 return
             mlp = self.job
             shape = (ctypes.c_int * 4)(mlp.in_features, mlp.out_features, mlp.num_hidden_layers, mlp.kernel_width)
-            nat.check(lib.insr_adam_step_partials(
-                nat.ptr(self.buf), self.nb, self.stride, nat.ptr(self.gflat), self.accumulate, nat.ptr(p), nat.ptr(m),
-                nat.ptr(v), self.gflat.numel(), shape, nat.ptr(state), b1, b2, eps, nat.ptr(loss), patience, st),
-                "insr_adam_step_partials")
+            args = (nat.ptr(self.buf), self.nb, self.stride, nat.ptr(self.gflat), self.accumulate, nat.ptr(p),
+                    nat.ptr(m), nat.ptr(v), self.gflat.numel(), shape, nat.ptr(state), b1, b2, eps, nat.ptr(loss),
+                    patience)
+            if fin is None:
+                nat.check(lib.insr_adam_step_partials(*args, st), "insr_adam_step_partials")
+            else:
+                nat.check(lib.insr_adam_step_partials_fin(*args, fin, st), "insr_adam_step_partials_fin")
             return
         mlp, x2, n, cmode = self.job
         din, dout, L, W = mlp.in_features, mlp.out_features, mlp.num_hidden_layers, mlp.kernel_width
         with _timed("reduce", *self.key):
-            rc = lib.insr_siren_jet_bwd_grad_adam(
-                nat.ptr(x2), n, din, dout, L, W, cmode, nat.ptr(mlp.flat_params()), None, None, None, None,
-                nat.ptr(self.buf), nat.ptr(self.gflat), self.accumulate, 2, nat.ptr(m), nat.ptr(v), nat.ptr(state),
-                b1 or 0.0, b2 or 0.0, eps or 0.0, nat.ptr(loss), patience, st)
+            if fin is None:
+                rc = lib.insr_siren_jet_bwd_grad_adam(
+                    nat.ptr(x2), n, din, dout, L, W, cmode, nat.ptr(mlp.flat_params()), None, None, None, None,
+                    nat.ptr(self.buf), nat.ptr(self.gflat), self.accumulate, 2, nat.ptr(m), nat.ptr(v),
+                    nat.ptr(state), b1 or 0.0, b2 or 0.0, eps or 0.0, nat.ptr(loss), patience, st)
+            else:
+                rc = lib.insr_siren_jet_bwd_grad_adam_fin(
+                    nat.ptr(x2), n, din, dout, L, W, cmode, nat.ptr(mlp.flat_params()), nat.ptr(self.buf),
+                    nat.ptr(self.gflat), self.accumulate, nat.ptr(m), nat.ptr(v), nat.ptr(state), b1 or 0.0,
+                    b2 or 0.0, eps or 0.0, nat.ptr(loss), patience, fin, st)
         nat.check(rc, "insr_siren_jet_bwd_grad_adam")
 
 
 def launch_reduce(pr):
     """The held-back sums of one reverse jet (MLP.flush_pending_reduce)."""
     pr.launch()
+
+
+def _seed_plan(job, lib):
+    """(LazyGroup, InsrSeed terms, loss_part rows) when this reverse jet evaluates a lazy loss group's
+    terms itself (losses.LazyGroup: one group, all of its losses seeding this job's streams, a backward
+    path that takes seeds); otherwise the lazy groups among its adjoints are launched now (before the
+    reverse jet reads them) and None."""
+    from . import losses
+    streams = {nat.SEED_VALUE: job.gy, nat.SEED_GRAD: job.gdy, nat.SEED_LAP: job.glap}
+    groups = {}
+    for t in streams.values():
+        g = losses.lazy_group_of(t)
+        if g is not None:
+            groups[id(g)] = g
+    if not groups:
+        return None
+    if len(groups) == 1:
+        g = next(iter(groups.values()))
+        n, din = job.x2.shape
+        mlp = job.mlp
+        rows = lib.insr_jet_bwd_seed_rows(n, din, mlp.out_features, mlp.num_hidden_layers, mlp.kernel_width,
+                                          job.cmode)
+        if rows > 0:
+            terms = g.seeds_for({sid: (t, *job.outs[sid]) for sid, t in streams.items()})
+            if terms:
+                return g, terms, rows
+    for g in groups.values():
+        g.materialize(job.cur)
+    return None
+
+
+def _seeded_launch(job, plan, work, st):
+    """The seeded first launch of a reverse jet (insr_siren_jet_bwd_seeded): its seeded adjoint streams
+    pass NULL; returns the (InsrLossFin, loss_part, terms) its sums launch finishes the losses with."""
+    g, terms, rows = plan
+    mlp, x2 = job.mlp, job.x2
+    n, din = x2.shape
+    seeded = {t.stream for t in terms}
+    ptr = lambda sid, t: None if sid in seeded else nat.ptr(t)  # noqa: E731
+    with torch.cuda.stream(job.cur):
+        lpart = torch.empty(rows * nat.SEED_MAX, device=x2.device, dtype=torch.float32)
+    arr = (nat.Seed * len(terms))(*terms)
+    with _timed("bwd", job.mode, n, mlp.kernel_width, (din, mlp.out_features, mlp.num_hidden_layers)):
+        rc = nat.lib().insr_siren_jet_bwd_seeded(
+            nat.ptr(x2), n, din, mlp.out_features, mlp.num_hidden_layers, mlp.kernel_width, job.cmode,
+            nat.ptr(mlp.flat_params()), nat.ptr(job.act), ptr(nat.SEED_VALUE, job.gy), ptr(nat.SEED_GRAD, job.gdy),
+            ptr(nat.SEED_LAP, job.glap), arr, len(terms), nat.ptr(lpart), nat.ptr(work), st)
+    nat.check(rc, "insr_siren_jet_bwd_seeded")
+    g.state = "seeded"
+    g._forget()
+    SEED_STATS["seeded"] += 1
+    SEED_STATS[job.mode] = SEED_STATS.get(job.mode, 0) + 1
+    return (g.fin(lpart, rows), lpart, arr)
+
+
+SEED_STATS = {"seeded": 0}  # reverse jets that evaluated a lazy loss group's terms, in all and per jet mode
 
 
 def _launch_bwd(job):
@@ -304,6 +382,7 @@ def _launch_bwd(job):
     cmode = job.cmode
     mlp.ensure_wsplit()
     lib = nat.lib()
+    plan = _seed_plan(job, lib)  # a lazy loss group's terms evaluated in this jet (None: pointers)
     gflat, accumulate = mlp.grad_for_backward()
     cur = job.cur
     st = ctypes.c_void_p(cur.cuda_stream)
@@ -316,19 +395,27 @@ def _launch_bwd(job):
         with torch.cuda.stream(cur):
             work = torch.empty(max(lib.insr_jet_bwd_work_bytes(n, din, dout, L, W, cmode) // 4, 1),
                                device=x2.device, dtype=torch.float32)
-        if getattr(_Defer, "depth", 0) > 0 and (lib.insr_jet_bwd_kernel(n, din, dout, L, W, cmode) == 1 or
-                                                 (path == 1 and L > 0)):
+        fb_split = lib.insr_jet_bwd_kernel(n, din, dout, L, W, cmode) == 1 or (path == 1 and L > 0)
+        if plan is not None or (getattr(_Defer, "depth", 0) > 0 and fb_split):
             # the jet_fb.hpp or the two-kernel backward: its sweep now, its sums with the Adam launch
-            # (defer_reductions)
-            with _timed("bwd", mode, n, W, (din, dout, L)):
-                rc = lib.insr_siren_jet_bwd_grad_adam(
-                    nat.ptr(x2), n, din, dout, L, W, cmode, nat.ptr(mlp.flat_params()), nat.ptr(act), nat.ptr(gy),
-                    nat.ptr(gdy), nat.ptr(glap), nat.ptr(work), nat.ptr(gflat), accumulate, 1, None, None, None,
-                    0.0, 0.0, 0.0, None, 0, st)
-            nat.check(rc, "insr_siren_jet_bwd_grad_adam")
-            mlp.set_pending_reduce(PendingSums("split", work, 0, 0, (mlp, x2, n, cmode), gflat, accumulate, cur,
-                                               (mode, n, W, (din, dout, L))))
-            _Defer.nets.append(mlp)
+            # (defer_reductions) -- or, seeded outside that scope, right after it
+            if plan is not None:
+                fin = _seeded_launch(job, plan, work, st)
+            else:
+                fin = None
+                with _timed("bwd", mode, n, W, (din, dout, L)):
+                    rc = lib.insr_siren_jet_bwd_grad_adam(
+                        nat.ptr(x2), n, din, dout, L, W, cmode, nat.ptr(mlp.flat_params()), nat.ptr(act), nat.ptr(gy),
+                        nat.ptr(gdy), nat.ptr(glap), nat.ptr(work), nat.ptr(gflat), accumulate, 1, None, None, None,
+                        0.0, 0.0, 0.0, None, 0, st)
+                nat.check(rc, "insr_siren_jet_bwd_grad_adam")
+            pr = PendingSums("split", work, 0, 0, (mlp, x2, n, cmode), gflat, accumulate, cur,
+                             (mode, n, W, (din, dout, L)), fin)
+            if getattr(_Defer, "depth", 0) > 0:
+                mlp.set_pending_reduce(pr)
+                _Defer.nets.append(mlp)
+            else:
+                pr.launch()
             mlp.grad_write_end(cur)
             return
         with _timed("bwd", mode, n, W, (din, dout, L)):
@@ -341,21 +428,22 @@ def _launch_bwd(job):
     with torch.cuda.stream(cur):
         part = torch.empty(max(lib.insr_jet_partial_bytes(n, din, dout, L, W, cmode) // 4, 1), device=x2.device,
                            dtype=torch.float32)
-    with _timed("bwd", mode, n, W, (din, dout, L)):
-        rc = lib.insr_siren_jet_bwd(nat.ptr(x2), n, din, dout, L, W, cmode, nat.ptr(mlp.flat_params()),
-                                    nat.ptr(act), nat.ptr(gy), nat.ptr(gdy), nat.ptr(glap), nat.ptr(part), st)
-    nat.check(rc, "insr_siren_jet_bwd")
+    if plan is not None:
+        fin = _seeded_launch(job, plan, part, st)
+    else:
+        fin = None
+        with _timed("bwd", mode, n, W, (din, dout, L)):
+            rc = lib.insr_siren_jet_bwd(nat.ptr(x2), n, din, dout, L, W, cmode, nat.ptr(mlp.flat_params()),
+                                        nat.ptr(act), nat.ptr(gy), nat.ptr(gdy), nat.ptr(glap), nat.ptr(part), st)
+        nat.check(rc, "insr_siren_jet_bwd")
     nb, stride = lib.insr_jet_partial_blocks(n, din, W, cmode), lib.insr_jet_partial_stride(din, dout, L, W)
+    pr = PendingSums("rows", part, nb, stride, mlp, gflat, accumulate, cur, (mode, n, W, (din, dout, L)), fin)
     if getattr(_Defer, "depth", 0) > 0 and 0 < nb < 1024:  # the sums go into the Adam launch (defer_reductions)
-        mlp.set_pending_reduce(PendingSums("rows", part, nb, stride, mlp, gflat, accumulate, cur,
-                                           (mode, n, W, (din, dout, L))))
+        mlp.set_pending_reduce(pr)
         _Defer.nets.append(mlp)
         mlp.grad_write_end(cur)
         return
-    with _timed("reduce", mode, n, W, (din, dout, L)):
-        rc = lib.insr_reduce_partials_strided(nat.ptr(part), nb, gflat.numel(), stride, nat.ptr(gflat), accumulate,
-                                              st)
-    nat.check(rc, "insr_reduce_partials_strided")
+    pr.launch()
     mlp.grad_write_end(cur)
 
 
@@ -365,6 +453,12 @@ def _launch_bwd_multi(jobs):
     insr_siren_jet_bwd_grad_multi: the jobs the fused tile-split kernel serves share one launch
     and one fixed-order partial-row reduction."""
     mlp, mode, cur = jobs[0].mlp, jobs[0].mode, jobs[0].cur
+    from . import losses
+    for j in jobs:  # lazy loss groups among the adjoints: launched first (this path reads them as data)
+        for t in (j.gy, j.gdy, j.glap):
+            g = losses.lazy_group_of(t)
+            if g is not None:
+                g.materialize(cur)
     din = jobs[0].x2.shape[1]
     L, W, dout = mlp.num_hidden_layers, mlp.kernel_width, mlp.out_features
     cmode = jobs[0].cmode

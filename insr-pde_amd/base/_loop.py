@@ -31,6 +31,7 @@ import torch
 
 from . import _jet
 from .networks import MLP
+from .losses import lazy_losses
 from .sampling import draw_ahead, draw_plan
 
 try:
@@ -65,7 +66,8 @@ class PhaseLoop:
 
     def _body(self):
         self.m.optimizer, self.m.scheduler = self.opt, self.sched
-        with _jet.call_scope(self), draw_plan(self):
+        # lazy_losses: the body's loss groups ride in the reverse jets (BaseModel._lazy_losses_on)
+        with _jet.call_scope(self), draw_plan(self), lazy_losses(self.m._lazy_losses_on()):
             loss_dict = self.func(self.m, *self.args, **self.kwargs)
         synced = self.m._update_network(loss_dict)
         return synced if isinstance(synced, dict) else loss_dict

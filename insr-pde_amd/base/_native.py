@@ -191,6 +191,12 @@ SIGNATURES = {
     "insr_sample_boxes": (_I, [_P, _I, _I, ctypes.c_ulonglong, _P, _P]),
     "insr_sample_boxes_rep": (_I, [_P, _I, _I, _I, _P, ctypes.c_ulonglong, _P, _P]),
     "insr_adam_step": (_I, [_P, _P, _P, _P, _L, _P, _F, _F, _F, _P]),
+    "insr_jet_bwd_seed_rows": (_I, [_L, _I, _I, _I, _I, _I]),
+    "insr_siren_jet_bwd_seeded": (_I, [_P, _L, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _I, _P, _P, _P]),
+    "insr_reduce_partials_fin": (_I, [_P, _I, _L, _L, _P, _I, _P, _P]),
+    "insr_adam_step_partials_fin": (_I, [_P, _I, _L, _P, _I, _P, _P, _P, _L, _P, _P, _F, _F, _F, _P, _I, _P, _P]),
+    "insr_siren_jet_bwd_grad_adam_fin": (_I, [_P, _L, _I, _I, _I, _I, _I, _P, _P, _P, _I, _P, _P, _P, _F, _F, _F, _P,
+                                              _I, _P, _P]),
 }
 
 
@@ -220,6 +226,22 @@ class Loss(ctypes.Structure):
                 ("alpha", _F), ("beta", _F), ("gamma", _F), ("delta", _F), ("scale", _F), ("out", _P),
                 ("ga", _P), ("ga_lo", _L), ("ga_hi", _L), ("a_off", _L), ("gb", _P), ("gc", _P), ("gd", _P),
                 ("gb_len", _L), ("gc_len", _L), ("gd_len", _L)]
+
+
+SEED_MAX = 4  # INSR_SEED_MAX
+SEED_VALUE, SEED_GRAD, SEED_LAP = 0, 1, 2  # INSR_SEED_VALUE / _GRAD / _LAP
+
+
+class Seed(ctypes.Structure):
+    """struct InsrSeed (include/insr_siren.h): one loss term a reverse jet evaluates as its adjoint."""
+    _fields_ = [("kind", _I), ("m", _I), ("stream", _I), ("loss", _I), ("n", _L), ("a_off", _L),
+                ("a", _P), ("b", _P), ("c", _P), ("d", _P), ("sb", _L), ("sc", _L), ("sd", _L),
+                ("alpha", _F), ("beta", _F), ("gamma", _F), ("delta", _F), ("scale", _F)]
+
+
+class LossFin(ctypes.Structure):
+    """struct InsrLossFin (include/insr_siren.h): the loss values a sums launch finishes."""
+    _fields_ = [("part", _P), ("rows", _I), ("nloss", _I), ("scale", _F * SEED_MAX), ("out", _P * SEED_MAX)]
 
 
 MAX_BOXES = 8  # INSR_MAX_BOXES

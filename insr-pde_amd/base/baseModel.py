@@ -28,6 +28,7 @@ from abc import ABC, abstractmethod
 import torch
 
 from . import _jet
+from .losses import settle_lazy
 from .networks import get_network
 from .optim import DevicePlateau, FusedAdam
 
@@ -222,6 +223,17 @@ class BaseModel(ABC):
         self._insr_dp_red = arena[lo:hi]
         return {k: tail[i] for i, k in enumerate(keys)}
 
+    # A phase body that returns its sq_losses outputs and reads no jet output they read elsewhere may let
+    # its loss groups ride in the reverse jets (base/losses.py lazy_losses): the model classes that are
+    # written that way set this (pde/fluid.py, pde/advection.py); cfg.insr_seed_in_bwd = False turns it off
+    _insr_lazy_losses = False
+
+    def _lazy_losses_on(self):
+        """Whether the loop may open lazy_losses() around this model's phase body: opted in, one process,
+        the fused optimiser with deferred sums (the loss values are finished by the sums launch)."""
+        return (self._insr_lazy_losses and getattr(self.cfg, "insr_seed_in_bwd", True) and not self._dp_active()
+                and _jet.DEFER_REDUCE and isinstance(self.optimizer, FusedAdam))
+
     def _update_network(self, loss_dict):
         """update network by back propagation (base/baseModel.py:73-81).  backward of
         sum(loss_dict.values()) is run as backward of every term with a persistent unit
@@ -232,6 +244,7 @@ class BaseModel(ABC):
         defer = _jet.DEFER_REDUCE and isinstance(self.optimizer, FusedAdam) and not self._dp_active()
         with (_jet.defer_reductions() if defer else contextlib.nullcontext()):
             self._backward(loss_dict)
+            settle_lazy()  # lazy loss groups no reverse jet evaluated: launched now (base/losses.py)
             synced = self._dp_sync(loss_dict)
             if self.scheduler is not None and getattr(self.scheduler, "fusable", False):
                 self.optimizer.step(plateau=(self.scheduler, synced['main']))  # Adam + plateau: one launch

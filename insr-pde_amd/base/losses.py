@@ -13,6 +13,7 @@ reference spells as 3-5 aten launches forward and as many backward.  Gradients f
 to every input that requires them.  GPU only (the product path has no CPU fallback).
 """
 import ctypes
+import threading
 
 import torch
 
@@ -177,6 +178,149 @@ def _shared_a(specs):
     return owner
 
 
+# ---- adjoint seeds inside the reverse jet (round 5) ------------------------------------------------
+# A loss group formed inside lazy_losses() -- opened by the training loop around a phase body that opts
+# in (BaseModel._insr_lazy_losses: the body returns its sq_losses outputs and nothing else consumes the
+# jet outputs they read) -- holds its launch back.  Its unit-seeded backward hands out the gradient
+# buffers unfilled; the reverse jet that receives them (base/_jet.py _launch_bwd) evaluates the loss
+# terms itself (insr_siren_jet_bwd_seeded: bit for bit the gradient the group launch writes) and the
+# sums launch after it finishes the loss values (InsrLossFin) -- one launch fewer per iteration.  Any
+# other consumer launches the group first (LazyGroup.materialize), and settle_lazy() (after the
+# backward, BaseModel._update_network) launches every group no reverse jet took.
+class _LazyState(threading.local):
+    depth = 0
+    groups = None  # the lazy groups formed on this thread since the last settle_lazy()
+
+
+_Lazy = _LazyState()
+_LAZY = {}  # data_ptr of a handed-out gradient buffer -> (LazyGroup, index of the loss that owns it)
+_LAZY_LOCK = threading.Lock()  # (reverse jets may run on autograd's device thread)
+
+
+class lazy_losses:
+    """`with lazy_losses(on): body()` -- loss groups formed inside defer their launch (see above)."""
+
+    def __init__(self, on=True):
+        self.on = bool(on)
+
+    def __enter__(self):
+        if self.on:
+            _Lazy.depth += 1
+        return self
+
+    def __exit__(self, *exc):
+        if self.on:
+            _Lazy.depth -= 1
+        return False
+
+
+class LazyGroup:
+    """A loss group whose launch is held back: state 'pending' (formed), 'handed' (its unit-seeded
+    backward gave out the unfilled gradient buffers), 'seeded' (a reverse jet took them), 'launched'."""
+    __slots__ = ("arr", "k", "work", "dev", "outs", "metas", "owner", "real_a", "tensors", "grads", "state",
+                 "bufs", "__weakref__")
+
+    def materialize(self, stream=None):
+        """Launch the group now (its losses and gradients, as the eager path) -- before anything reads them."""
+        if self.state in ("pending", "handed"):
+            st = nat.stream_of(self.dev) if stream is None else ctypes.c_void_p(stream.cuda_stream)
+            nat.check(nat.lib().insr_sq_loss_group(self.arr, self.k, nat.ptr(self.work), st), "insr_sq_loss_group")
+            self.state = "launched"
+        self._forget()
+
+    def _forget(self):
+        with _LAZY_LOCK:
+            for p in self.bufs:
+                _LAZY.pop(p, None)
+        self.bufs = []
+
+    def seeds_for(self, streams):
+        """The InsrSeed terms of this group for a reverse jet whose adjoint streams are
+        streams = {stream id: (gradient tensor or None, the jet's output data_ptr, its numel)}: every loss of
+        the group must seed one of them from its own output buffer; None when that does not hold."""
+        if self.state != "handed":
+            return None
+        terms = []
+        covered = set()
+        for sid, (g, out_ptr, out_numel) in streams.items():
+            if g is None or g.data_ptr() not in self.bufs:
+                continue
+            o = self.bufs.index(g.data_ptr())
+            owner_idx = [i for i in range(self.k) if (self.owner[i] if self.owner[i] is not None else i) == o]
+            for i in owner_idx:
+                kind, n, m, coef, scale, a_off, (sb, sc, sd) = self.metas[i]
+                a = self.real_a[i]
+                if a.data_ptr() != out_ptr or a.numel() != out_numel:
+                    return None
+                b, c, d = self.tensors[4 * i + 1:4 * i + 4]
+                terms.append(nat.Seed(kind, m, sid, i, n, a_off, a.data_ptr(), nat.ptr(b), nat.ptr(c), nat.ptr(d),
+                                      sb, sc, sd, *coef, scale))
+                covered.add(i)
+        if covered != set(range(self.k)) or len(terms) > nat.SEED_MAX:
+            return None
+        return terms
+
+    def fin(self, part, rows):
+        """The InsrLossFin that finishes this group's loss values from a seeded backward's rows."""
+        f = nat.LossFin()
+        f.part, f.rows, f.nloss = part.data_ptr(), rows, self.k
+        for i in range(self.k):
+            f.scale[i] = self.metas[i][4]
+            f.out[i] = self.outs[i].data_ptr()
+        return f
+
+
+def lazy_group_of(t):
+    """The LazyGroup whose handed-out gradient buffer t is (None: an ordinary tensor)."""
+    if t is None or not _LAZY:
+        return None
+    with _LAZY_LOCK:
+        ent = _LAZY.get(t.data_ptr())
+    return None if ent is None else ent[0]
+
+
+def materialize_for(*ts):
+    """Launch the lazy groups any of ts came from (a consumer that reads them as data)."""
+    for t in ts:
+        g = lazy_group_of(t)
+        if g is not None:
+            g.materialize()
+
+
+def settle_lazy():
+    """After the backward: launch every lazy group of this thread that no reverse jet took (its losses
+    are read later); a group whose buffers were handed out but reached no reverse jet was read as data
+    by something else -- that is an error of the phase body's opt-in, raised."""
+    gs, _Lazy.groups = (_Lazy.groups or []), None
+    bad = False
+    for g in gs:
+        if g.state == "handed":
+            bad = True
+        if g.state in ("pending", "handed"):
+            g.materialize()
+        g._forget()
+    if bad:
+        raise RuntimeError("a lazy loss group's gradients were consumed outside the reverse jets (the phase "
+                           "body reads a jet output its sq_losses reads): do not open lazy_losses around it")
+
+
+def _lazy_ok(metas, owner, real_a, need):
+    """Whether a group may hold its launch back: every loss's trained operand is its `a` (b, c, d carry no
+    gradient), every `a` requires grad, and is a jet output (or a view of one) -- the reverse jet that
+    receives its gradient evaluates the terms."""
+    for i in range(len(metas)):
+        o = owner[i] if owner[i] is not None else i
+        if not need[4 * o] or any(need[4 * i + q] for q in (1, 2, 3)):
+            return False
+        a = real_a[i]
+        fn = a.grad_fn
+        if fn is not None and type(fn).__name__ in ("ViewBackward0", "UnsafeViewBackward0", "ReshapeAliasBackward0"):
+            fn = fn.next_functions[0][0] if fn.next_functions else None
+        if fn is None or "_SirenJet" not in type(fn).__name__:
+            return False
+    return True
+
+
 class _SqLossGroup(torch.autograd.Function):
     """Up to LOSS_GROUP_MAX losses in ONE launch forward (insr_sq_loss_group), each with the
     gradient for a unit seed written by the same launch; inputs: 4 tensor slots per loss (a
@@ -213,7 +357,17 @@ class _SqLossGroup(torch.autograd.Function):
             arr[i] = nat.Loss(kind, m, n, p(a), p(b), p(c), p(d), sb, sc, sd, *coef, scale, outs[i].data_ptr(),
                               p(g[0]), lo, hi, a_off, p(g[1]), p(g[2]), p(g[3]), *lens)
         work = _workspace(dev) if multi else None
-        nat.check(lib.insr_sq_loss_group(arr, k, nat.ptr(work), nat.stream_of(dev)), "insr_sq_loss_group")
+        ctx.lazy = None
+        if _Lazy.depth > 0 and _lazy_ok(metas, owner, real_a, need):
+            lz = LazyGroup()
+            lz.arr, lz.k, lz.work, lz.dev, lz.outs, lz.metas, lz.owner = arr, k, work, dev, outs, metas, owner
+            lz.real_a, lz.tensors, lz.grads, lz.state, lz.bufs = list(real_a), list(tensors), grads, "pending", []
+            ctx.lazy = lz
+            if _Lazy.groups is None:
+                _Lazy.groups = []
+            _Lazy.groups.append(lz)
+        else:
+            nat.check(lib.insr_sq_loss_group(arr, k, nat.ptr(work), nat.stream_of(dev)), "insr_sq_loss_group")
         ctx.save_for_backward(*[real_a[i] if owner[i] is not None and j == 0 else t
                                 for i in range(k) for j, t in enumerate(tensors[4 * i:4 * i + 4])])
         ctx.metas, ctx.owner = metas, owner
@@ -228,6 +382,22 @@ class _SqLossGroup(torch.autograd.Function):
         k = len(ctx.metas)
         res = [None] * len(tensors)
         unit = [g is not None and g.numel() == 1 and g.data_ptr() in _UNIT_SEEDS for g in gouts]
+        lz = ctx.lazy
+        if lz is not None:
+            if all(unit) and lz.state == "pending" and not getattr(ctx, "pre_used", False):
+                # the first unit-seeded backward: hand out the unfilled a-gradient buffers (a reverse jet
+                # evaluates them, or materialize() fills them before anything else reads them)
+                lz.state = "handed"
+                with _LAZY_LOCK:
+                    for o in range(k):
+                        if owner[o] is None and ctx.pre[4 * o] is not None:
+                            lz.bufs.append(ctx.pre[4 * o].data_ptr())
+                            _LAZY[ctx.pre[4 * o].data_ptr()] = (lz, o)
+                # (bufs in owner order: seeds_for maps a buffer back to the losses that share it)
+                lz.bufs = [ctx.pre[4 * o].data_ptr() if (owner[o] is None and ctx.pre[4 * o] is not None) else -1
+                           for o in range(k)]
+            else:
+                lz.materialize()
         # the forward's precomputed gradients are handed out once; a repeated backward
         # (retain_graph=True) gets copies, so nothing downstream can alias the kept buffers
         pre = ctx.pre if not getattr(ctx, "pre_used", False) else [None if g is None else g.clone() for g in ctx.pre]

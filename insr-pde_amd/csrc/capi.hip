@@ -356,9 +356,12 @@ __global__ __launch_bounds__(64 * kRedWaves) void reduce_partials_kernel(const f
 constexpr int kRed4Waves = 8, kRed4Unroll = 16;  // rows in flight per thread (predicated tail)
 __global__ __launch_bounds__(64 * kRed4Waves) void reduce_partials4_kernel(const float* __restrict__ part, int nb,
                                                                             long count, long stride,
-                                                                            float* __restrict__ grad, int accumulate) {
+                                                                            float* __restrict__ grad, int accumulate,
+                                                                            LossFin fin = LossFin{}) {
   __shared__ floatx4 red[kRed4Waves][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  // fin.nloss > 0: the grid's extra last block (no columns of its own) finishes the loss values
+  if (fin.nloss && blockIdx.x == gridDim.x - 1 && w == 0) loss_finalize(fin);
   const long q = (long)blockIdx.x * 64 + lane;  // column quad
   floatx4 acc = floatx4{0.f, 0.f, 0.f, 0.f};
   if (4 * q < count) {
@@ -497,10 +500,14 @@ __global__ __launch_bounds__(64 * kRed4Waves) void reduce_adam_kernel(const floa
                                                                       float* __restrict__ p, float* __restrict__ m,
                                                                       float* __restrict__ v, int4 shp,
                                                                       float* __restrict__ st, float b1, float b2,
-                                                                      float eps, const float* loss, int patience) {
+                                                                      float eps, const float* loss, int patience,
+                                                                      LossFin fin = LossFin{}) {
   __shared__ floatx4 red[kRed4Waves][64];
   __shared__ float sc[2];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  // fin.nloss > 0: the grid's extra last block (no elements of its own) finishes the loss values
+  // before its plateau ticket -- the plateau's last block then reads them (loss_finalize hand-off)
+  if (fin.nloss && blockIdx.x == gridDim.x - 1 && w == 0) loss_finalize(fin);
   if (threadIdx.x == 0) {
     const double t = (double)st[INSR_OPT_STEP] + 1.0;
     double p1, p2;
@@ -886,9 +893,9 @@ int insr_siren_jet_fwd_mixed(const InsrJetJob* jobs, const int* modes, const flo
   return 0;
 }
 
-int insr_siren_jet_bwd(const float* x, long n, int din, int dout, int L, int W, int mode, const float* params,
-                       const float* act, const float* gy, const float* gdy, const float* glap, float* partial,
-                       void* stream) {
+static int bwd_fused_impl(const float* x, long n, int din, int dout, int L, int W, int mode, const float* params,
+                          const float* act, const float* gy, const float* gdy, const float* glap, float* partial,
+                          const SeedTab* seeds, void* stream) {
   if (!shape_ok(din, dout, L, W, mode) || n < 0 || n > 0x7fffffffL) return INSR_EINVAL;
   if (n == 0) return 0;
   if (!x || !params || !act || !partial) return INSR_EINVAL;
@@ -910,7 +917,17 @@ int insr_siren_jet_bwd(const float* x, long n, int din, int dout, int L, int W, 
   J.first[0] = 0;
   J.first[1] = sh.nbal > 0 ? sh.nbal : (int)(((n + 15) / 16 + sh.T - 1) / sh.T);
   J.njobs = 1;
+  if (seeds) {
+    if (nq == 0) return INSR_EINVAL;  // the exact-fp32 kernel takes no seeds
+    J.seeds = *seeds;
+  }
   return bwd_q(fused_bwd_nq(nq, c.k), c.NT, c.S, c.lap, sh.T, &J, din, dout, L, params, partial, P, (hipStream_t)stream);
+}
+
+int insr_siren_jet_bwd(const float* x, long n, int din, int dout, int L, int W, int mode, const float* params,
+                       const float* act, const float* gy, const float* gdy, const float* glap, float* partial,
+                       void* stream) {
+  return bwd_fused_impl(x, n, din, dout, L, W, mode, params, act, gy, gdy, glap, partial, nullptr, stream);
 }
 
 // Plan of a multi-job backward (insr_siren_jet_bwd_grad_multi): the jobs whose own size takes the
@@ -1118,10 +1135,12 @@ static int wide_bwd_call(const JetCall& c, const float* x, long n, int din, int 
 // saved streams): phases / Adam epilogue as fb_bwd_t
 static int fb_bwd_call(const JetCall& c, const float* x, long n, int din, int dout, int L, int W, int mode,
                        const float* params, const float* act, const float* gy, const float* gdy, const float* glap,
-                       float* work, float* grad, int accumulate, int phases, const AdamArgs& A, hipStream_t st) {
+                       float* work, float* grad, int accumulate, int phases, const AdamArgs& A, hipStream_t st,
+                       const SeedTab* seeds = nullptr) {
   int rc = 0;
   if (!(params = with_planes(params, din, dout, L, W, mode, st, 0, &rc))) return rc;
   FbJobs J{};
+  if (seeds) J.seeds = *seeds;
   J.x[0] = x;
   J.act[0] = c.recompute(L) ? nullptr : act;
   J.gy[0] = gy;
@@ -1135,11 +1154,27 @@ static int fb_bwd_call(const JetCall& c, const float* x, long n, int din, int do
                          A, st);
 }
 
-int insr_siren_jet_bwd_grad_adam(const float* x, long n, int din, int dout, int L, int W, int mode, float* params,
-                                 const float* act, const float* gy, const float* gdy, const float* glap, float* work,
-                                 float* grad, int accumulate, int phases, float* exp_avg, float* exp_avg_sq,
-                                 float* opt_state, float beta1, float beta2, float eps, const float* loss, int patience,
-                                 void* stream) {
+// InsrLossFin -> the device descriptor (NULL: none)
+static int fin_of(const InsrLossFin* f, LossFin& F) {
+  F = LossFin{};
+  if (!f) return 0;
+  if (!f->part || f->rows < 1 || f->nloss < 1 || f->nloss > INSR_SEED_MAX) return INSR_EINVAL;
+  F.part = f->part;
+  F.rows = f->rows;
+  F.nloss = f->nloss;
+  for (int k = 0; k < f->nloss; ++k) {
+    if (!f->out[k]) return INSR_EINVAL;
+    F.scale[k] = f->scale[k];
+    F.out[k] = f->out[k];
+  }
+  return 0;
+}
+
+static int grad_adam_impl(const float* x, long n, int din, int dout, int L, int W, int mode, float* params,
+                          const float* act, const float* gy, const float* gdy, const float* glap, float* work,
+                          float* grad, int accumulate, int phases, float* exp_avg, float* exp_avg_sq, float* opt_state,
+                          float beta1, float beta2, float eps, const float* loss, int patience, const LossFin& fin,
+                          const SeedTab* seeds, void* stream) {
   if (!shape_ok(din, dout, L, W, mode) || n < 1 || n > 0x7fffffffL || phases < 1 || phases > 3) return INSR_EINVAL;
   const JetCall c(din, W, mode);
   const bool fb = c.recompute(L) || (c.resident(n, L) && c.resident_f16(n, L));  // jet_fb.hpp's backward
@@ -1166,11 +1201,112 @@ int insr_siren_jet_bwd_grad_adam(const float* x, long n, int din, int dout, int 
       A.shape[3] = W;
     }
   }
+  A.fin = fin;
+  if ((fin.nloss && !(phases & 2)) || ((seeds || fin.nloss) && (wide || c.recompute(L)))) return INSR_EINVAL;
   if (wide)
     return wide_bwd_call(c, x, n, din, dout, L, W, mode, params, act, gy, gdy, glap, work, grad, accumulate, phases,
                          A, (hipStream_t)stream);
   return fb_bwd_call(c, x, n, din, dout, L, W, mode, params, act, gy, gdy, glap, work, grad, accumulate, phases, A,
-                     (hipStream_t)stream);
+                     (hipStream_t)stream, seeds);
+}
+
+int insr_siren_jet_bwd_grad_adam(const float* x, long n, int din, int dout, int L, int W, int mode, float* params,
+                                 const float* act, const float* gy, const float* gdy, const float* glap, float* work,
+                                 float* grad, int accumulate, int phases, float* exp_avg, float* exp_avg_sq,
+                                 float* opt_state, float beta1, float beta2, float eps, const float* loss, int patience,
+                                 void* stream) {
+  return grad_adam_impl(x, n, din, dout, L, W, mode, params, act, gy, gdy, glap, work, grad, accumulate, phases,
+                        exp_avg, exp_avg_sq, opt_state, beta1, beta2, eps, loss, patience, LossFin{}, nullptr, stream);
+}
+
+int insr_siren_jet_bwd_grad_adam_fin(const float* x, long n, int din, int dout, int L, int W, int mode, float* params,
+                                     float* work, float* grad, int accumulate, float* exp_avg, float* exp_avg_sq,
+                                     float* opt_state, float beta1, float beta2, float eps, const float* loss,
+                                     int patience, const InsrLossFin* fin, void* stream) {
+  LossFin F;
+  if (fin_of(fin, F)) return INSR_EINVAL;
+  return grad_adam_impl(x, n, din, dout, L, W, mode, params, nullptr, nullptr, nullptr, nullptr, work, grad,
+                        accumulate, 2, exp_avg, exp_avg_sq, opt_state, beta1, beta2, eps, loss, patience, F, nullptr,
+                        stream);
+}
+
+// InsrSeed[] -> the device table of a one-job launch (job 0); rejects a seeded stream whose adjoint
+// pointer is set, overlapping terms of one stream, and malformed terms
+static int seeds_of(const InsrSeed* seeds, int ns, float* lpart, const float* gy, const float* gdy, const float* glap,
+                    SeedTab& T) {
+  T = SeedTab{};
+  if (!seeds || ns < 1 || ns > INSR_SEED_MAX || !lpart) return INSR_EINVAL;
+  for (int k = 0; k < ns; ++k) {
+    const InsrSeed& q = seeds[k];
+    if (!q.a || q.n < 0 || q.a_off < 0 || q.loss < 0 || q.loss >= INSR_SEED_MAX) return INSR_EINVAL;
+    if (q.stream < INSR_SEED_VALUE || q.stream > INSR_SEED_LAP) return INSR_EINVAL;
+    if ((q.stream == INSR_SEED_VALUE && gy) || (q.stream == INSR_SEED_GRAD && gdy) || (q.stream == INSR_SEED_LAP && glap))
+      return INSR_EINVAL;
+    if (q.kind == INSR_LOSS_COMBO) {
+      if ((q.d && !q.c) || q.sb < 1 || q.sc < 1 || q.sd < 1) return INSR_EINVAL;
+    } else if (q.kind == INSR_LOSS_BANDS) {
+      if (q.m < 2 || q.b || q.c || q.d || q.a_off % q.m) return INSR_EINVAL;
+    } else {
+      return INSR_EINVAL;
+    }
+    const long hi = q.a_off + (q.kind == INSR_LOSS_COMBO ? q.n : 2 * q.n * q.m);
+    for (int j = 0; j < k; ++j) {
+      const InsrSeed& o = seeds[j];
+      const long ohi = o.a_off + (o.kind == INSR_LOSS_COMBO ? o.n : 2 * o.n * o.m);
+      if (o.stream == q.stream && q.a_off < ohi && o.a_off < hi) return INSR_EINVAL;
+    }
+    SeedTerm& t = T.t[k];
+    t.a = q.a + q.a_off;
+    t.b = q.b;
+    t.c = q.c;
+    t.d = q.d;
+    t.alpha = q.alpha;
+    t.beta = q.beta;
+    t.gamma = q.gamma;
+    t.delta = q.delta;
+    t.sb = q.sb;
+    t.sc = q.sc;
+    t.sd = q.sd;
+    t.n = q.n;
+    t.a_off = q.a_off;
+    t.g2 = 2.f * q.scale;
+    t.kind = q.kind;
+    t.m = q.m;
+    t.job = 0;
+    t.stream = q.stream;
+    t.loss = q.loss;
+  }
+  T.nt = ns;
+  T.lpart = lpart;
+  return 0;
+}
+
+int insr_jet_bwd_seed_rows(long n, int din, int dout, int L, int W, int mode) {
+  if (!shape_ok(din, dout, L, W, mode) || n < 0 || n > 0x7fffffffL) return INSR_EINVAL;
+  if (n == 0) return 0;
+  const JetCall c(din, W, mode);
+  const int p = c.path(n, L);
+  // the fused tile-split kernel stages seeds for value jets (jet_x6.hpp jet_bwd_x6, S = 1)
+  if (p == 0) return (c.S == 1 && (c.NT > 8 ? 0 : c.nqb) > 0) ? insr_jet_partial_blocks(n, din, W, mode) : 0;
+  if (p == 2 && c.resident_f16(n, L)) {  // jet_fb.hpp on the saved streams: its tiles per block staged in LDS
+    const long tiles = (n + 15) / 16, nb = fb_launch_blocks(tiles);
+    return (tiles + nb - 1) / nb <= kFbSeedTiles ? (int)nb : 0;
+  }
+  return 0;
+}
+
+int insr_siren_jet_bwd_seeded(const float* x, long n, int din, int dout, int L, int W, int mode, const float* params,
+                              const float* act, const float* gy, const float* gdy, const float* glap,
+                              const InsrSeed* seeds, int n_seeds, float* loss_part, float* work, void* stream) {
+  if (insr_jet_bwd_seed_rows(n, din, dout, L, W, mode) <= 0) return INSR_EINVAL;
+  SeedTab T;
+  if (seeds_of(seeds, n_seeds, loss_part, gy, gdy, glap, T)) return INSR_EINVAL;
+  if (!x || !params || !act || !work) return INSR_EINVAL;
+  const JetCall c(din, W, mode);
+  if (c.path(n, L) == 2)  // the jet_fb sweep (phase 1); phase 2: insr_siren_jet_bwd_grad_adam_fin
+    return grad_adam_impl(x, n, din, dout, L, W, mode, const_cast<float*>(params), act, gy, gdy, glap, work, work, 0, 1,
+                          nullptr, nullptr, nullptr, 0.f, 0.f, 0.f, nullptr, 0, LossFin{}, &T, stream);
+  return bwd_fused_impl(x, n, din, dout, L, W, mode, params, act, gy, gdy, glap, work, &T, stream);
 }
 
 int insr_siren_jet_bwd_grad(const float* x, long n, int din, int dout, int L, int W, int mode, const float* params,
@@ -1216,12 +1352,13 @@ int insr_jet_split_tiles(long n, int din, int W, int mode, int backward) {
   return launch_shape(backward ? 1 : 0, nq, c.NT, c.S, c.lap, n, c.k).T;
 }
 
-int insr_reduce_partials_strided(const float* partial, int nb, long count, long stride, float* grad, int accumulate,
-                                 void* stream) {
+static int reduce_partials_impl(const float* partial, int nb, long count, long stride, float* grad, int accumulate,
+                                const LossFin& fin, void* stream) {
   if (!partial || !grad || nb < 0 || count < 0 || stride < count) return INSR_EINVAL;
   if (count == 0) return 0;
   if (stride % 4 == 0 && ((uintptr_t)partial & 15) == 0) {
-    const long blocks = (count + 255) / 256;
+    // fin.nloss > 0: one more block (no columns of its own) finishes the seeded loss values
+    const long blocks = (count + 255) / 256, fb = fin.nloss ? 1 : 0;
     // many rows: two levels, so ~4 blocks per CU stream rows instead of ~1 (and no grid
     // that overshoots 256 CUs by a few blocks)
     // (measured: pays from ~1024 rows -- 58 -> 50 us; at 256 / 512 rows the extra launch
@@ -1232,16 +1369,28 @@ int insr_reduce_partials_strided(const float* partial, int nb, long count, long 
       const int R = (nb + slices - 1) / slices;
       hipLaunchKernelGGL(reduce_slices4_kernel, dim3((unsigned)blocks, slices), dim3(64 * kRed4Waves), 0,
                          (hipStream_t)stream, const_cast<float*>(partial), nb, R, count, stride);
-      hipLaunchKernelGGL(reduce_partials4_kernel, dim3((unsigned)blocks), dim3(64 * kRed4Waves), 0,
-                         (hipStream_t)stream, partial, (nb + R - 1) / R, count, stride * R, grad, accumulate);
+      hipLaunchKernelGGL(reduce_partials4_kernel, dim3((unsigned)(blocks + fb)), dim3(64 * kRed4Waves), 0,
+                         (hipStream_t)stream, partial, (nb + R - 1) / R, count, stride * R, grad, accumulate, fin);
       return (int)hipGetLastError();
     }
-    hipLaunchKernelGGL(reduce_partials4_kernel, dim3((unsigned)blocks), dim3(64 * kRed4Waves), 0, (hipStream_t)stream,
-                       partial, nb, count, stride, grad, accumulate);
+    hipLaunchKernelGGL(reduce_partials4_kernel, dim3((unsigned)(blocks + fb)), dim3(64 * kRed4Waves), 0,
+                       (hipStream_t)stream, partial, nb, count, stride, grad, accumulate, fin);
     return (int)hipGetLastError();
   }
-  if (stride != count) return INSR_EINVAL;
+  if (stride != count || fin.nloss) return INSR_EINVAL;
   return insr_reduce_partials(partial, nb, count, grad, accumulate, stream);
+}
+
+int insr_reduce_partials_strided(const float* partial, int nb, long count, long stride, float* grad, int accumulate,
+                                 void* stream) {
+  return reduce_partials_impl(partial, nb, count, stride, grad, accumulate, LossFin{}, stream);
+}
+
+int insr_reduce_partials_fin(const float* partial, int nb, long count, long stride, float* grad, int accumulate,
+                             const InsrLossFin* fin, void* stream) {
+  LossFin F;
+  if (fin_of(fin, F)) return INSR_EINVAL;
+  return reduce_partials_impl(partial, nb, count, stride, grad, accumulate, F, stream);
 }
 
 int insr_reduce_partials(const float* partial, int nb, long count, float* grad, int accumulate, void* stream) {
@@ -1265,9 +1414,10 @@ int insr_plateau_step(float* st, const float* loss, int patience, int advance_st
   return (int)hipGetLastError();
 }
 
-int insr_adam_step_partials(const float* partial, int nb, long stride, float* grad, int accumulate, float* params,
-                            float* exp_avg, float* exp_avg_sq, long count, const int* shape, float* st, float b1,
-                            float b2, float eps, const float* loss, int patience, void* stream) {
+static int adam_partials_impl(const float* partial, int nb, long stride, float* grad, int accumulate, float* params,
+                              float* exp_avg, float* exp_avg_sq, long count, const int* shape, float* st, float b1,
+                              float b2, float eps, const float* loss, int patience, const LossFin& fin,
+                              void* stream) {
   if (!partial || !grad || !params || !exp_avg || !exp_avg_sq || !st || nb < 1 || nb >= 1024 || count < 1 ||
       stride < count || stride % 4 || ((uintptr_t)partial & 15))
     return INSR_EINVAL;
@@ -1278,11 +1428,28 @@ int insr_adam_step_partials(const float* partial, int nb, long stride, float* gr
       return INSR_EINVAL;
     shp = make_int4(shape[0], shape[1], shape[2], shape[3]);
   }
-  const long blocks = (count + 255) / 256;
+  const long blocks = (count + 255) / 256 + (fin.nloss ? 1 : 0);  // + the loss-finishing block
   hipLaunchKernelGGL(reduce_adam_kernel, dim3((unsigned)blocks), dim3(64 * kRed4Waves), 0, (hipStream_t)stream,
                      partial, nb, count, stride, grad, accumulate, params, exp_avg, exp_avg_sq, shp, st, b1, b2, eps,
-                     loss, patience);
+                     loss, patience, fin);
   return (int)hipGetLastError();
+}
+
+int insr_adam_step_partials(const float* partial, int nb, long stride, float* grad, int accumulate, float* params,
+                            float* exp_avg, float* exp_avg_sq, long count, const int* shape, float* st, float b1,
+                            float b2, float eps, const float* loss, int patience, void* stream) {
+  return adam_partials_impl(partial, nb, stride, grad, accumulate, params, exp_avg, exp_avg_sq, count, shape, st, b1,
+                            b2, eps, loss, patience, LossFin{}, stream);
+}
+
+int insr_adam_step_partials_fin(const float* partial, int nb, long stride, float* grad, int accumulate, float* params,
+                                float* exp_avg, float* exp_avg_sq, long count, const int* shape, float* st, float b1,
+                                float b2, float eps, const float* loss, int patience, const InsrLossFin* fin,
+                                void* stream) {
+  LossFin F;
+  if (fin_of(fin, F)) return INSR_EINVAL;
+  return adam_partials_impl(partial, nb, stride, grad, accumulate, params, exp_avg, exp_avg_sq, count, shape, st, b1,
+                            b2, eps, loss, patience, F, stream);
 }
 
 int insr_adam_step_multi(int count, float* const* params, const float* const* grads, float* const* exp_avg,

@@ -402,6 +402,124 @@ constexpr int kFwdJobs = INSR_MAX_FWD_JOBS;
 template <int NQ>
 int dispatch_fwd_multi_q(int NT, int S, bool LAP, int T, const InsrJetJob* jobs, const int* small, const int* nbal,
                          int njobs, int din, int dout, int L, hipStream_t st);
+// A squared-residual loss term's operands (residual.hip, insr_sq_loss_group): a from its first term
+struct LossIn {
+  const float* a;
+  const float* b;
+  const float* c;
+  const float* d;
+  float alpha, beta, gamma, delta;
+  long sb = 1, sc = 1, sd = 1;  // element strides of b, c, d
+};
+
+// r = alpha (a + beta b) + gamma (c + delta d), evaluated in exactly that order
+// (the reference's rounding for (u - u0)/dt + v (ux + u0x)/2 and u - (u_prev - grad_p))
+__device__ __forceinline__ float combo_r(const float* a, const float* b, const float* c, const float* d, float alpha,
+                                         float beta, float gamma, float delta, long sb, long sc, long sd, long i) {
+  float p = a[i];
+  if (b) p = p + beta * b[i * sb];
+  p = alpha * p;
+  if (c) {
+    float q = c[i * sc];
+    if (d) q = q + delta * d[i * sd];
+    p = p + gamma * q;
+  }
+  return p;
+}
+__device__ __forceinline__ float combo_residual(const LossIn& in, long i) {
+  return combo_r(in.a, in.b, in.c, in.d, in.alpha, in.beta, in.gamma, in.delta, in.sb, in.sc, in.sd, i);
+}
+
+// In-kernel adjoint seeds of a reverse jet (include/insr_siren.h InsrSeed): the loss terms that seed
+// one adjoint stream of one job, evaluated where the kernel reads that adjoint -- the same
+// expressions as sq_loss_group_kernel's gradient, so the seeds are its values bit for bit
+struct SeedTerm {
+  const float *a, *b, *c, *d;  // a = the stream's output buffer + a_off (the term's first element)
+  float alpha, beta, gamma, delta;
+  long sb, sc, sd;
+  long n, a_off;     // COMBO terms / BANDS rows per band; first element of the term range
+  float g2;          // 2 * scale
+  int kind, m, job, stream, loss;
+};
+struct SeedTab {
+  SeedTerm t[INSR_SEED_MAX];
+  int nt;            // 0: no seeded stream (every adjoint from its pointer)
+  float* lpart;      // [block][INSR_SEED_MAX] square sums of the terms each block seeds
+};
+
+__device__ __forceinline__ void seed_sq_add(float (&sq)[INSR_SEED_MAX], int k, float v) {
+#pragma unroll
+  for (int q = 0; q < INSR_SEED_MAX; ++q)
+    if (q == k) sq[q] += v;
+}
+
+// The adjoint of element e of `stream` of job `job` (0 where no term covers it); count: the lane
+// owning the element adds the covering term's square to sq[loss] (one lane per element)
+__device__ __forceinline__ float seed_adjoint(const SeedTab& S, int job, int stream, long e, bool count,
+                                              float (&sq)[INSR_SEED_MAX]) {
+  float g = 0.f;
+#pragma unroll
+  for (int k = 0; k < INSR_SEED_MAX; ++k) {
+    if (k >= S.nt) break;
+    const SeedTerm& T = S.t[k];
+    if (T.job != job || T.stream != stream) continue;
+    const long rel = e - T.a_off;
+    if (T.kind == INSR_LOSS_COMBO) {
+      if (rel < 0 || rel >= T.n) continue;
+      const float r = combo_r(T.a, T.b, T.c, T.d, T.alpha, T.beta, T.gamma, T.delta, T.sb, T.sc, T.sd, rel);
+      g = T.alpha * (T.g2 * r);  // sq_loss_group_kernel: cf[0] * (g2 * r)
+      if (count) seed_sq_add(sq, T.loss, r * r);
+    } else {
+      if (rel < 0 || rel >= 2 * T.n * T.m) continue;
+      const long row = rel / T.m;
+      const int col = (int)(rel - row * T.m);
+      if (col != (row < T.n ? 0 : 1)) continue;
+      const float v = T.a[rel];
+      g = T.g2 * v;
+      if (count) seed_sq_add(sq, T.loss, v * v);
+    }
+  }
+  return g;
+}
+
+// The block's square sums (sq of every lane of the calling wave, zeros where a lane counted nothing)
+// into its loss_part row: a fixed butterfly, lane 0 stores.  Call from one whole wave.
+__device__ __forceinline__ void seed_sq_store(const SeedTab& S, float (&sq)[INSR_SEED_MAX], unsigned block) {
+#pragma unroll
+  for (int q = 0; q < INSR_SEED_MAX; ++q) {
+    float v = sq[q];
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+    sq[q] = v;
+  }
+  if ((threadIdx.x & 63) == 0) {
+    floatx4 r = floatx4{sq[0], sq[1], sq[2], sq[3]};
+    *reinterpret_cast<floatx4*>(S.lpart + (long)block * INSR_SEED_MAX) = r;
+  }
+}
+
+// The loss values of a seeded backward (InsrLossFin) in the sums launch that follows it: one wave,
+// lane l sums rows l, l + 64, ... of each column in order, then a fixed butterfly; out[k] leaves as
+// an sc1 store acknowledged before the caller's plateau ticket (residual.hip header: the hand-off the
+// last block's sc1 load of the loss reads)
+struct LossFin {
+  const float* part = nullptr;
+  int rows = 0, nloss = 0;
+  float scale[INSR_SEED_MAX] = {0.f, 0.f, 0.f, 0.f};
+  float* out[INSR_SEED_MAX] = {nullptr, nullptr, nullptr, nullptr};
+};
+__device__ __forceinline__ void loss_finalize(const LossFin& F) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int k = 0; k < INSR_SEED_MAX; ++k) {
+    if (k >= F.nloss) break;
+    float v = 0.f;
+    for (int r = lane; r < F.rows; r += 64) v += F.part[(long)r * INSR_SEED_MAX + k];
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+    if (lane == 0) __hip_atomic_store(F.out[k], F.scale[k] * v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (lane == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
 // The jobs of one tile-split backward launch: batches of ONE network and jet mode (its weights
 // are the launch's), blocks [first[k], first[k + 1]) run job k -- nbal[k] > 0: its tiles balanced
 // over that many blocks (T = 3 / 5 shapes), else T-tile blocks.  One job = insr_siren_jet_bwd.
@@ -416,6 +534,7 @@ struct BwdJobsX6 {
   int nbal[kBwdJobs];
   int first[kBwdJobs + 1];
   int njobs;
+  SeedTab seeds;  // seeds.nt == 0: every adjoint from gy / gdy / glap
 };
 // jobs == NULL: occupancy query (resident blocks per CU of the instantiation)
 template <int NQ>
@@ -434,6 +553,7 @@ struct AdamArgs {
   int patience = 0;
   float b1 = 0.f, b2 = 0.f, eps = 0.f;
   int shape[4] = {0, 0, 0, 0};
+  LossFin fin;  // fin.nloss > 0: the sums launch also finishes a seeded backward's loss values
 };
 
 template <int NQ>
@@ -467,7 +587,9 @@ struct FbJobs {
   int n[kBwdJobs];
   int tstart[kBwdJobs + 1];
   int njobs;
+  SeedTab seeds;  // the saved-stream variant only (the recompute variant takes pointers)
 };
+constexpr int kFbSeedTiles = 24;  // at most this many tiles per block take in-kernel seeds (staged in LDS)
 // recompute backward (jet_fb.hpp: W = 128, L = 4, f16x3 with per-tile scales): ONE persistent launch
 // (forward + reverse jet per tile, dW resident per CU) + the fixed-order sums; act is not read
 int dispatch_fb_bwd(int S, bool LAP, int L, const FbJobs& J, int din, int dout, const float* prm, float* work,

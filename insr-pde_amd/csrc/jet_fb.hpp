@@ -61,7 +61,7 @@ static __device__ unsigned long long g_fb_stamps[8 * 8 * kFbStampPts];
 // operand, read by transpose reads as the A operand); ZS = fp32 z-streams of hidden layers 1..NZL
 // [layer][s][wave][lane]; SW = the small weights;
 // then the compact accumulators, the tile's seeds [S][3][16] and the block-maximum slots [2][4][8]
-template <int S, int L, int ZR, bool SAVED = false>
+template <int S, int L, int ZR, bool SAVED = false, bool SEED = false>
 struct FbGeo {
   using BG = X6BwdGeo<4, 8>;
   static constexpr int NZL = (!SAVED && (L - ZR) > 0) ? (L - ZR) : 0;
@@ -75,7 +75,10 @@ struct FbGeo {
   static constexpr size_t SACC_OFF = SW_OFF + (size_t)SW_FLOATS * 4;
   static constexpr size_t SEED_OFF = SACC_OFF + (size_t)kFbSmallMax * 4;
   static constexpr size_t MX_OFF = SEED_OFF + (size_t)S * 3 * 16 * 4;
-  static constexpr size_t BYTES = MX_OFF + 2 * 5 * 8 * 4;
+  // in-kernel seeds (saved-stream variant): the adjoints of the block's tiles [tile][S][3][16] (at most
+  // kFbSeedTiles tiles per block), then the waves' square sums [8][INSR_SEED_MAX]
+  static constexpr size_t SSEED_OFF = MX_OFF + 2 * 5 * 8 * 4;
+  static constexpr size_t BYTES = SSEED_OFF + (SEED ? ((size_t)kFbSeedTiles * S * 48 + 8 * INSR_SEED_MAX) * 4 : 0);
 };
 
 // sin / cos of w z (4 values).  A wave holding any |w z| > 8192 takes the libm path, out of line:
@@ -154,13 +157,16 @@ __device__ __forceinline__ void fb_h_bounds(const floatx4 (&z)[S], float& mt, fl
   mt *= OMEGA;
 }
 
-template <int S, bool LAP, int L, int ZR, bool SAVED>
+// SEED (saved streams only): the in-kernel adjoint seeds of FbJobs::seeds, a separate instantiation so the
+// pointer-seeded kernel is unchanged
+template <int S, bool LAP, int L, int ZR, bool SAVED, bool SEED = false>
 __global__ __launch_bounds__(512, 1) void jet_fb_x6(const FbJobs J, int din, int dout, const float* __restrict__ prm,
                                                     float* __restrict__ dpart, float* __restrict__ small, long Ps,
                                                     int nb, int tiles) {
   constexpr int NT = 8, W = 128, KC = 4;
   using BG = X6BwdGeo<4, NT>;
-  using GG = FbGeo<S, L, ZR, SAVED>;
+  using GG = FbGeo<S, L, ZR, SAVED, SEED>;
+  static_assert(!SEED || SAVED, "seeds: the saved-stream variant");
   constexpr int LDB = BG::ZROW, ZPLANE = BG::ZPLANE, ZSET = BG::ZSET;
   constexpr int NTAN = LAP ? S - 2 : S - 1;
   constexpr int NZL = GG::NZL;
@@ -192,7 +198,48 @@ __global__ __launch_bounds__(512, 1) void jet_fb_x6(const FbJobs J, int din, int
   for (int j = 0; j < L; ++j) E[j] = kNoE;
   int slot = 0;  // block-maximum slot of the next exchange (two alternate: each exchange has a barrier)
 
-  __syncthreads();  // sacc zeroed
+  // In-kernel seeds (saved streams, J.seeds): the adjoints of all the block's tiles, formed before the
+  // tile loop -- from their pointers or the loss terms (jet_common.hpp seed_adjoint, each element by one
+  // thread, which counts the term's square) -- into LDS; the block's square sums into J.seeds.lpart
+  if constexpr (SEED) {
+    float* ss = reinterpret_cast<float*>(lb + GG::SSEED_OFF);
+    float* swq = ss + kFbSeedTiles * S * 48;
+    float sq[INSR_SEED_MAX] = {0.f, 0.f, 0.f, 0.f};
+    for (int tile = t0; tile < t1; ++tile) {  // tile-uniform: the job index stays scalar
+      int k = 0;
+#pragma unroll
+      for (int q = 1; q < kBwdJobs; ++q) k += (q < J.njobs && tile >= J.tstart[q]) ? 1 : 0;
+      const int i = threadIdx.x;
+      if (i < S * 48) {
+        const int s = i / 48, o = (i / 16) % 3, pp = (tile - J.tstart[k]) * 16 + (i & 15);
+        float v = 0.f;
+        if (o < dout && pp < J.n[k]) {
+          const int sk = s == 0 ? INSR_SEED_VALUE : ((LAP && s == S - 1) ? INSR_SEED_LAP : INSR_SEED_GRAD);
+          const float* g0 = sk == INSR_SEED_VALUE ? J.gy[k] : (sk == INSR_SEED_LAP ? J.glap[k] : J.gdy[k]);
+          const long at = sk != INSR_SEED_GRAD ? (long)pp * dout + o : ((long)pp * dout + o) * din + (s - 1);
+          v = g0 ? g0[at] : seed_adjoint(J.seeds, k, sk, at, true, sq);
+        }
+        ss[(tile - t0) * S * 48 + i] = v;
+      }
+    }
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int q = 0; q < INSR_SEED_MAX; ++q) {
+      float v = sq[q];
+      for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+      if (lane == 0) swq[wave * INSR_SEED_MAX + q] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      floatx4 r = floatx4{0.f, 0.f, 0.f, 0.f};
+      for (int w = 0; w < 8; ++w)
+#pragma unroll
+        for (int q = 0; q < INSR_SEED_MAX; ++q) r[q] += swq[w * INSR_SEED_MAX + q];
+      *reinterpret_cast<floatx4*>(J.seeds.lpart + (long)blockIdx.x * INSR_SEED_MAX) = r;
+    }
+  }
+
+  __syncthreads();  // sacc zeroed (and the staged seeds written)
 
   for (int tile = t0; tile < t1; ++tile) {
     // the LDS images through an opaque per-tile offset: otherwise the compiler hoists every
@@ -259,8 +306,8 @@ __global__ __launch_bounds__(512, 1) void jet_fb_x6(const FbJobs J, int din, int
     // flight under the forward, staged into LDS before its last barrier.  Saved streams (no forward):
     // every lane loads its own point's seeds
     float sdv = 0.f;
-    float gsd[SAVED ? S : 1][3];
-    if constexpr (SAVED) {
+    float gsd[(SAVED && !SEED) ? S : 1][3];
+    if constexpr (SAVED && !SEED) {
 #pragma unroll
       for (int s = 0; s < S; ++s)
 #pragma unroll
@@ -407,10 +454,12 @@ __global__ __launch_bounds__(512, 1) void jet_fb_x6(const FbJobs J, int din, int
       float ga[S];
 #pragma unroll
       for (int s = 0; s < S; ++s) {
-        if constexpr (SAVED)
-          ga[s] = o == 0 ? gsd[s][0] : (o == 1 ? gsd[s][1] : gsd[s][2]);
-        else
+        if constexpr (!SAVED)
           ga[s] = seed[(s * 3 + o) * 16 + c];
+        else if constexpr (SEED)  // the block's staged seeds of this tile
+          ga[s] = reinterpret_cast<const float*>(lbt + GG::SSEED_OFF)[(((tile - t0) * S + s) * 3 + o) * 16 + c];
+        else
+          ga[s] = o == 0 ? gsd[s][0] : (o == 1 ? gsd[s][1] : gsd[s][2]);
       }
       const floatx4 w4 = *reinterpret_cast<const floatx4*>(Wos + (o * W + n0));
       floatx4 acc4 = floatx4{0.f, 0.f, 0.f, 0.f};
@@ -676,9 +725,28 @@ int fb_bwd_t(const FbJobs& J, int din, int dout, const float* prm, float* work, 
   static const bool attr = ((void)hipFuncSetAttribute((const void*)jet_fb_x6<S, LAP, L, ZR, SAVED>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)lds), true);  // once per instantiation (thread-safe static init)
   (void)attr;
-  if (phases & 1)
-    hipLaunchKernelGGL((jet_fb_x6<S, LAP, L, ZR, SAVED>), dim3(nb), dim3(512), lds, st, J, din, dout, prm, dpart, small,
-                       Ps, nb, tiles);
+  if (phases & 1) {
+    if constexpr (SAVED) {
+      if (J.seeds.nt) {  // the seeded instantiation: its block's tiles must fit the LDS stage
+        constexpr size_t lds_s = FbGeo<S, L, ZR, true, true>::BYTES;
+        static_assert(lds_s <= 163840, "LDS");
+        static const bool attr_s = ((void)hipFuncSetAttribute((const void*)jet_fb_x6<S, LAP, L, ZR, true, true>,
+                                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_s),
+                                    true);
+        (void)attr_s;
+        if ((tiles + nb - 1) / nb > kFbSeedTiles) return INSR_EINVAL;
+        hipLaunchKernelGGL((jet_fb_x6<S, LAP, L, ZR, true, true>), dim3(nb), dim3(512), lds_s, st, J, din, dout, prm,
+                           dpart, small, Ps, nb, tiles);
+      } else {
+        hipLaunchKernelGGL((jet_fb_x6<S, LAP, L, ZR, SAVED>), dim3(nb), dim3(512), lds, st, J, din, dout, prm, dpart,
+                           small, Ps, nb, tiles);
+      }
+    } else {
+      if (J.seeds.nt) return INSR_EINVAL;
+      hipLaunchKernelGGL((jet_fb_x6<S, LAP, L, ZR, SAVED>), dim3(nb), dim3(512), lds, st, J, din, dout, prm, dpart,
+                         small, Ps, nb, tiles);
+    }
+  }
   if (!(phases & 2)) return (int)hipGetLastError();
   const int grad16 = (((uintptr_t)(grad + hidden_off(din, W, 1))) & 15) == 0 ? 1 : 0;
   const int wq = (W * W / 4 + 63) / 64;

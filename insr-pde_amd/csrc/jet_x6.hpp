@@ -877,9 +877,16 @@ constexpr int x6_bwd_sg() {
   return 1;
 }
 
+// value jets (S = 1) take in-kernel adjoint seeds (BwdJobsX6::seeds): the block's seeds [T][3][16] and
+// the waves' square sums [8][INSR_SEED_MAX] after the maxima
+template <int S, int T>
+constexpr size_t bwd_x6_seed_floats() {
+  return S == 1 ? (size_t)T * 48 + 8 * INSR_SEED_MAX : 0;
+}
 template <int NQ, int NT, int S, int T>
 constexpr size_t bwd_x6_lds_bytes() {  // + 2 x 5 x 8 floats: the waves' per-layer maxima (NQ = 4)
-  return (size_t)T * x6_bwd_sg<NQ, NT, S, T>() * X6BwdGeo<NQ, NT>::SET_BYTES + 2 * 5 * 8 * sizeof(float);
+  return (size_t)T * x6_bwd_sg<NQ, NT, S, T>() * X6BwdGeo<NQ, NT>::SET_BYTES + 2 * 5 * 8 * sizeof(float) +
+         bwd_x6_seed_floats<S, T>() * sizeof(float);
 }
 
 template <int NQ, int NT, int S, bool LAP, int T>
@@ -933,8 +940,44 @@ __global__ __launch_bounds__(X6Geo<NT>::THREADS) void jet_bwd_x6(const BwdJobsX6
 
   // adjoint of output o, stream s, at this lane's point of tile t (0 outside / for NULL);
   // read where used: the backward's register budget is tight
+  // In-kernel seeds (value jets): the threads form the (tile, output, point) adjoints of the
+  // block -- from gy, or from the loss terms of J.seeds (jet_common.hpp seed_adjoint; that thread also
+  // counts the term's square) -- into LDS; the waves' square sums meet after one barrier and thread 0
+  // writes the block's row of J.seeds.lpart.  Before anything else of the kernel: short live ranges
+  float* sseed = zred + 2 * 5 * 8;  // [t][o][c]
+  if constexpr (S == 1) {
+    if (J.seeds.nt) {
+      float* swq = sseed + T * 48;  // [wave][INSR_SEED_MAX]
+      float sq[INSR_SEED_MAX] = {0.f, 0.f, 0.f, 0.f};
+      for (int i = threadIdx.x; i < T * 48; i += G::THREADS) {
+        const int t = i / 48, o = (i / 16) % 3, p = (tile0 + t) * 16 + (i & 15);
+        float v = 0.f;
+        if (t < cnt && p < N && o < dout) {
+          const long e = (long)p * dout + o;
+          v = gy ? gy[e] : seed_adjoint(J.seeds, jk, INSR_SEED_VALUE, e, true, sq);
+        }
+        sseed[i] = v;
+      }
+#pragma unroll
+      for (int q = 0; q < INSR_SEED_MAX; ++q) {
+        float v = sq[q];
+        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+        if (lane == 0) swq[wave * INSR_SEED_MAX + q] = v;
+      }
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        floatx4 r = floatx4{0.f, 0.f, 0.f, 0.f};
+        for (int w = 0; w < G::THREADS / 64; ++w)
+#pragma unroll
+          for (int q = 0; q < INSR_SEED_MAX; ++q) r[q] += swq[w * INSR_SEED_MAX + q];
+        *reinterpret_cast<floatx4*>(J.seeds.lpart + (long)blockIdx.x * INSR_SEED_MAX) = r;
+      }
+    }
+  }
   auto adjoint = [&](int t, int s, int o) -> float {
     const int p = (tile0 + t) * 16 + c;
+    if constexpr (S == 1)
+      if (J.seeds.nt) return sseed[(t * 3 + o) * 16 + c];
     if (t >= cnt || p >= N) return 0.f;
     if (s == 0) return gy ? gy[(long)p * dout + o] : 0.f;
     if (LAP && s == S - 1) return glap ? glap[(long)p * dout + o] : 0.f;

@@ -700,6 +700,9 @@ __global__ __launch_bounds__(512) void reduce_dw_kernel(const float* __restrict_
                                                         int kstep, int kslots, AdamArgs A) {
   __shared__ floatx4 red[8][64];
   __shared__ float sc[2];  // A.m != NULL: Adam's step size and sqrt(1 - b2^t)
+  // A.fin.nloss > 0: block (last column, plane L) -- the grid's extra column, no work of its own --
+  // finishes the seeded backward's loss values before its plateau ticket
+  if (A.fin.nloss && (int)blockIdx.y == L && blockIdx.x == gridDim.x - 1 && threadIdx.x < 64) loss_finalize(A.fin);
   if (A.m && threadIdx.x == 0) {
     const double t = (double)A.st[INSR_OPT_STEP] + 1.0;
     double p1, p2;

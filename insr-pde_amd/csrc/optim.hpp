@@ -11,7 +11,8 @@ namespace insr {
 __device__ void plateau_update(float* st, const float* loss, int patience, int advance_step) {
   if (advance_step) st[INSR_OPT_STEP] = st[INSR_OPT_STEP] + 1.f;
   if (!loss) return;  // advance-only (optimiser without a scheduler)
-  const float cur = *loss;
+  // an sc1 load: the loss may come from this launch's own finishing block (jet_common.hpp loss_finalize)
+  const float cur = __hip_atomic_load(loss, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   float best = st[INSR_OPT_BEST];
   float bad = st[INSR_OPT_BAD];
   // torch: a < best * (1 - threshold), threshold = 1e-4 (python double math)

@@ -29,28 +29,7 @@ constexpr int kLossThreads = 512;
 constexpr int kLossMaxBlocks = 256;
 constexpr long kLossPerBlock = 4096;  // elements per block (8 per thread) before the grid grows
 
-struct LossIn {
-  const float* a;
-  const float* b;
-  const float* c;
-  const float* d;
-  float alpha, beta, gamma, delta;
-  long sb = 1, sc = 1, sd = 1;  // element strides of b, c, d
-};
-
-// r = alpha (a + beta b) + gamma (c + delta d), evaluated in exactly that order
-// (the reference's rounding for (u - u0)/dt + v (ux + u0x)/2 and u - (u_prev - grad_p))
-__device__ __forceinline__ float combo_residual(const LossIn& in, long i) {
-  float p = in.a[i];
-  if (in.b) p = p + in.beta * in.b[i * in.sb];
-  p = in.alpha * p;
-  if (in.c) {
-    float q = in.c[i * in.sc];
-    if (in.d) q = q + in.delta * in.d[i * in.sd];
-    p = p + in.gamma * q;
-  }
-  return p;
-}
+// LossIn / combo_residual: jet_common.hpp (the in-kernel seeds of the reverse jets share them)
 
 __device__ __forceinline__ float loss_term(int kind, const LossIn& in, long n, int m, long i) {
   if (kind == INSR_LOSS_COMBO) {

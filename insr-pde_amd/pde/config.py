@@ -26,6 +26,7 @@ BUNNY_FIXTURE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "
 
 # insr-pde_amd execution knobs (see base/_loop.py)
 EXEC = dict(insr_precision=None, insr_sync_every=1, insr_graph=False, insr_graph_unroll=1, insr_progress=True,
+            insr_seed_in_bwd=True,  # opted-in phase bodies' loss groups ride in the reverse jets (base/losses.py)
             insr_fuse_forwards=os.environ.get("INSR_FUSE_FORWARDS", "1") != "0")
 
 

@@ -29,6 +29,9 @@ class Fluid2DModel(BaseModel):
     # every loss below is a mean over the GLOBAL point count (BaseModel._dp_total): the ranks' losses
     # and gradients sum to the global means, so the all-reduce needs no 1/world pass
     _dp_loss_reduction = 'sum'
+    # the phase bodies return their sq_losses outputs and read the jet outputs those losses read nowhere
+    # else: the loss groups ride in the reverse jets (base/losses.py lazy_losses)
+    _insr_lazy_losses = True
 
     def __init__(self, cfg):
         super().__init__(cfg)

@@ -31,7 +31,10 @@ def _worker(port, q):
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
     ph = dict(np.load(GOLD))
     out = {}
-    for name, kw in (("single", dict(insr_dp_always=False)), ("split", dict(insr_dp_always=True, insr_dp_capture=False)),
+    # (single: without in-kernel loss seeds -- base/losses.py lazy_losses, which the data-parallel path does not
+    # take -- so the three runs compute the loss values in the same launches; tests/test_gpu_seeds.py covers them)
+    for name, kw in (("single", dict(insr_dp_always=False, insr_seed_in_bwd=False)),
+                     ("split", dict(insr_dp_always=True, insr_dp_capture=False)),
                      ("captured", dict(insr_dp_always=True, insr_dp_capture=True))):
         torch.manual_seed(0)
         cfg = make_config("fluid", num_hidden_layers=4, hidden_features=128, sample_resolution=32, dt=0.05,

@@ -30,6 +30,12 @@ for s in ${STEPS:-tests bench prof}; do
              run ab_As_$r 300 python bench.py --config fluid2DtlgnM --shard-of 8 --steps 40 --warmup 3 --no-cpu-baseline --no-roofline
              run ab_Bs_$r 300 python bench.py --config fluid2DtlgnM --shard-of 8 --lib insr-pde_amd/lib_exp/libinsr_hip.so --steps 40 --warmup 3 --no-cpu-baseline --no-roofline
            done ;;
+    abseed) for r in 1 2; do
+             run sd_A_$r 300 python bench.py --steps 40 --warmup 3 --no-cpu-baseline --no-roofline
+             run sd_B_$r 300 python bench.py --no-seed-in-bwd --steps 40 --warmup 3 --no-cpu-baseline --no-roofline
+             run sd_As_$r 300 python bench.py --config fluid2DtlgnM --shard-of 8 --steps 40 --warmup 3 --no-cpu-baseline --no-roofline
+             run sd_Bs_$r 300 python bench.py --config fluid2DtlgnM --shard-of 8 --no-seed-in-bwd --steps 40 --warmup 3 --no-cpu-baseline --no-roofline
+           done ;;
     prof) run prof 300 rocprofv3 --kernel-trace --stats -d "$PWD/$O/prof" -o run --output-format csv -- python bench.py --steps 10 --warmup 3 --no-cpu-baseline ;;
     profshard) run profshard 300 rocprofv3 --kernel-trace --stats -d "$PWD/$O/profshard" -o run --output-format csv -- python bench.py --config fluid2DtlgnM --shard-of 8 --steps 10 --warmup 3 --no-cpu-baseline --no-roofline ;;
     kbench) run kbench 400 python tools/kbench.py ${KARGS:---sizes 8192,16708,66844 --nets fluid_pres --modes lap --variants h3 --policies 0,2} ;;
