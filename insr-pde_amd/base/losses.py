@@ -304,6 +304,11 @@ def settle_lazy():
                            "body reads a jet output its sq_losses reads): do not open lazy_losses around it")
 
 
+_VIEW_NODES = frozenset(("ViewBackward0", "UnsafeViewBackward0", "ReshapeAliasBackward0", "AliasBackward0",
+                         "SqueezeBackward0", "SqueezeBackward1", "SqueezeBackward2", "SqueezeBackward3",
+                         "UnsqueezeBackward0"))
+
+
 def _lazy_ok(metas, owner, real_a, need):
     """Whether a group may hold its launch back: every loss's trained operand is its `a` (b, c, d carry no
     gradient), every `a` requires grad, and is a jet output (or a view of one) -- the reverse jet that
@@ -314,7 +319,9 @@ def _lazy_ok(metas, owner, real_a, need):
             return False
         a = real_a[i]
         fn = a.grad_fn
-        if fn is not None and type(fn).__name__ in ("ViewBackward0", "UnsafeViewBackward0", "ReshapeAliasBackward0"):
+        # a view of a jet output (e.g. the scalar net's gradient J.squeeze(-2), diff_ops.gradient): its
+        # backward is a view of the incoming gradient -- the reverse jet receives the handed-out buffer itself
+        while fn is not None and type(fn).__name__ in _VIEW_NODES:
             fn = fn.next_functions[0][0] if fn.next_functions else None
         if fn is None or "_SirenJet" not in type(fn).__name__:
             return False

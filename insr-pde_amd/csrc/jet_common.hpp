@@ -482,6 +482,65 @@ __device__ __forceinline__ float seed_adjoint(const SeedTab& S, int job, int str
   return g;
 }
 
+// seed_adjoint in two halves, so a kernel can issue the operand loads early and finish after other work
+// (their latency under it): the covering term of element e and its raw operands, then the adjoint (the
+// same expressions as combo_r / sq_loss_group_kernel) and its square into sq[loss]
+struct SeedOps {
+  float a, b, c, d;
+  int k;  // the covering term, -1: none (adjoint 0)
+};
+__device__ __forceinline__ SeedOps seed_gather(const SeedTab& S, int job, int stream, long e) {
+  SeedOps v{0.f, 0.f, 0.f, 0.f, -1};
+#pragma unroll
+  for (int k = 0; k < INSR_SEED_MAX; ++k) {
+    if (k >= S.nt) break;
+    const SeedTerm& T = S.t[k];
+    if (T.job != job || T.stream != stream) continue;
+    const long rel = e - T.a_off;
+    if (T.kind == INSR_LOSS_COMBO) {
+      if (rel < 0 || rel >= T.n) continue;
+      v.k = k;
+      v.a = T.a[rel];
+      if (T.b) v.b = T.b[rel * T.sb];
+      if (T.c) v.c = T.c[rel * T.sc];
+      if (T.d) v.d = T.d[rel * T.sd];
+    } else {
+      if (rel < 0 || rel >= 2 * T.n * T.m) continue;
+      const long row = rel / T.m;
+      const int col = (int)(rel - row * T.m);
+      if (col != (row < T.n ? 0 : 1)) continue;
+      v.k = k;
+      v.a = T.a[rel];
+    }
+  }
+  return v;
+}
+__device__ __forceinline__ float seed_finish(const SeedTab& S, const SeedOps& v, float (&sq)[INSR_SEED_MAX]) {
+  float g = 0.f;
+#pragma unroll
+  for (int k = 0; k < INSR_SEED_MAX; ++k) {
+    if (k >= S.nt) break;
+    if (v.k != k) continue;
+    const SeedTerm& T = S.t[k];
+    if (T.kind == INSR_LOSS_COMBO) {
+      float p = v.a;
+      if (T.b) p = p + T.beta * v.b;
+      p = T.alpha * p;
+      if (T.c) {
+        float q = v.c;
+        if (T.d) q = q + T.delta * v.d;
+        p = p + T.gamma * q;
+      }
+      g = T.alpha * (T.g2 * p);  // sq_loss_group_kernel: cf[0] * (g2 * r)
+      seed_sq_add(sq, T.loss, p * p);
+    } else {
+      g = T.g2 * v.a;
+      seed_sq_add(sq, T.loss, v.a * v.a);
+    }
+  }
+  return g;
+}
+
 // The block's square sums (sq of every lane of the calling wave, zeros where a lane counted nothing)
 // into its loss_part row: a fixed butterfly, lane 0 stores.  Call from one whole wave.
 __device__ __forceinline__ void seed_sq_store(const SeedTab& S, float (&sq)[INSR_SEED_MAX], unsigned block) {

@@ -205,21 +205,58 @@ __global__ __launch_bounds__(512, 1) void jet_fb_x6(const FbJobs J, int din, int
     float* ss = reinterpret_cast<float*>(lb + GG::SSEED_OFF);
     float* swq = ss + kFbSeedTiles * S * 48;
     float sq[INSR_SEED_MAX] = {0.f, 0.f, 0.f, 0.f};
-    for (int tile = t0; tile < t1; ++tile) {  // tile-uniform: the job index stays scalar
-      int k = 0;
+    if (J.njobs == 1) {
+      // one job (the merged [interior; bands] batch): every element of the block's tiles in flat order,
+      // up to 3 per thread per round with all their operand loads issued before any adjoint is formed
+      const int total = (t1 - t0) * S * 48;
+      for (int b0 = threadIdx.x; b0 < total; b0 += 3 * 512) {
+        SeedOps ops[3];
+        float pv[3];
+        bool live[3];
 #pragma unroll
-      for (int q = 1; q < kBwdJobs; ++q) k += (q < J.njobs && tile >= J.tstart[q]) ? 1 : 0;
-      const int i = threadIdx.x;
-      if (i < S * 48) {
-        const int s = i / 48, o = (i / 16) % 3, pp = (tile - J.tstart[k]) * 16 + (i & 15);
-        float v = 0.f;
-        if (o < dout && pp < J.n[k]) {
+        for (int u = 0; u < 3; ++u) {
+          const int idx = b0 + u * 512, i = idx % (S * 48), tile = t0 + idx / (S * 48);
+          const int s = i / 48, o = (i / 16) % 3, pp = tile * 16 + (i & 15);
           const int sk = s == 0 ? INSR_SEED_VALUE : ((LAP && s == S - 1) ? INSR_SEED_LAP : INSR_SEED_GRAD);
-          const float* g0 = sk == INSR_SEED_VALUE ? J.gy[k] : (sk == INSR_SEED_LAP ? J.glap[k] : J.gdy[k]);
+          const float* g0 = sk == INSR_SEED_VALUE ? J.gy[0] : (sk == INSR_SEED_LAP ? J.glap[0] : J.gdy[0]);
           const long at = sk != INSR_SEED_GRAD ? (long)pp * dout + o : ((long)pp * dout + o) * din + (s - 1);
-          v = g0 ? g0[at] : seed_adjoint(J.seeds, k, sk, at, true, sq);
+          live[u] = idx < total && o < dout && pp < J.n[0];
+          ops[u] = SeedOps{0.f, 0.f, 0.f, 0.f, -1};
+          pv[u] = 0.f;
+          if (live[u]) {
+            if (g0)
+              pv[u] = g0[at];
+            else
+              ops[u] = seed_gather(J.seeds, 0, sk, at);
+          }
         }
-        ss[(tile - t0) * S * 48 + i] = v;
+#pragma unroll
+        for (int u = 0; u < 3; ++u) {
+          const int idx = b0 + u * 512;
+          if (idx >= total) continue;
+          const int s = (idx % (S * 48)) / 48;
+          const int sk = s == 0 ? INSR_SEED_VALUE : ((LAP && s == S - 1) ? INSR_SEED_LAP : INSR_SEED_GRAD);
+          const float* g0 = sk == INSR_SEED_VALUE ? J.gy[0] : (sk == INSR_SEED_LAP ? J.glap[0] : J.gdy[0]);
+          ss[idx] = (live[u] && !g0) ? seed_finish(J.seeds, ops[u], sq) : pv[u];
+        }
+      }
+    } else {
+      for (int tile = t0; tile < t1; ++tile) {  // tile-uniform: the job index stays scalar
+        int k = 0;
+#pragma unroll
+        for (int q = 1; q < kBwdJobs; ++q) k += (q < J.njobs && tile >= J.tstart[q]) ? 1 : 0;
+        const int i = threadIdx.x;
+        if (i < S * 48) {
+          const int s = i / 48, o = (i / 16) % 3, pp = (tile - J.tstart[k]) * 16 + (i & 15);
+          float v = 0.f;
+          if (o < dout && pp < J.n[k]) {
+            const int sk = s == 0 ? INSR_SEED_VALUE : ((LAP && s == S - 1) ? INSR_SEED_LAP : INSR_SEED_GRAD);
+            const float* g0 = sk == INSR_SEED_VALUE ? J.gy[k] : (sk == INSR_SEED_LAP ? J.glap[k] : J.gdy[k]);
+            const long at = sk != INSR_SEED_GRAD ? (long)pp * dout + o : ((long)pp * dout + o) * din + (s - 1);
+            v = g0 ? g0[at] : seed_adjoint(J.seeds, k, sk, at, true, sq);
+          }
+          ss[(tile - t0) * S * 48 + i] = v;
+        }
       }
     }
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;

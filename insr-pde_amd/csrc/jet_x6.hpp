@@ -940,40 +940,62 @@ __global__ __launch_bounds__(X6Geo<NT>::THREADS) void jet_bwd_x6(const BwdJobsX6
 
   // adjoint of output o, stream s, at this lane's point of tile t (0 outside / for NULL);
   // read where used: the backward's register budget is tight
-  // In-kernel seeds (value jets): the threads form the (tile, output, point) adjoints of the
-  // block -- from gy, or from the loss terms of J.seeds (jet_common.hpp seed_adjoint; that thread also
-  // counts the term's square) -- into LDS; the waves' square sums meet after one barrier and thread 0
-  // writes the block's row of J.seeds.lpart.  Before anything else of the kernel: short live ranges
+  // In-kernel seeds (value jets, J.seeds): the threads form the block's (tile, output, point) adjoints --
+  // from gy, or from the loss terms (jet_common.hpp seed_gather / seed_finish: the operands are loaded
+  // before the output layer's z-streams, the adjoint formed after them, so both loads share one latency;
+  // that thread also counts the term's square) -- into LDS; the waves' square sums meet after one
+  // barrier and thread 0 writes the block's row of J.seeds.lpart
   float* sseed = zred + 2 * 5 * 8;  // [t][o][c]
-  if constexpr (S == 1) {
+  constexpr bool kSeed1 = S == 1 && T * 48 <= G::THREADS;  // one element per thread (the value shapes)
+  SeedOps sop{0.f, 0.f, 0.f, 0.f, -1};
+  float sgy = 0.f;
+  if constexpr (kSeed1) {
     if (J.seeds.nt) {
-      float* swq = sseed + T * 48;  // [wave][INSR_SEED_MAX]
-      float sq[INSR_SEED_MAX] = {0.f, 0.f, 0.f, 0.f};
-      for (int i = threadIdx.x; i < T * 48; i += G::THREADS) {
-        const int t = i / 48, o = (i / 16) % 3, p = (tile0 + t) * 16 + (i & 15);
-        float v = 0.f;
-        if (t < cnt && p < N && o < dout) {
-          const long e = (long)p * dout + o;
-          v = gy ? gy[e] : seed_adjoint(J.seeds, jk, INSR_SEED_VALUE, e, true, sq);
-        }
-        sseed[i] = v;
-      }
-#pragma unroll
-      for (int q = 0; q < INSR_SEED_MAX; ++q) {
-        float v = sq[q];
-        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
-        if (lane == 0) swq[wave * INSR_SEED_MAX + q] = v;
-      }
-      __syncthreads();
-      if (threadIdx.x == 0) {
-        floatx4 r = floatx4{0.f, 0.f, 0.f, 0.f};
-        for (int w = 0; w < G::THREADS / 64; ++w)
-#pragma unroll
-          for (int q = 0; q < INSR_SEED_MAX; ++q) r[q] += swq[w * INSR_SEED_MAX + q];
-        *reinterpret_cast<floatx4*>(J.seeds.lpart + (long)blockIdx.x * INSR_SEED_MAX) = r;
+      const int i = threadIdx.x, t = i / 48, o = (i / 16) % 3, p = (tile0 + t) * 16 + (i & 15);
+      if (i < T * 48 && t < cnt && p < N && o < dout) {
+        const long e = (long)p * dout + o;
+        if (gy)
+          sgy = gy[e];
+        else
+          sop = seed_gather(J.seeds, jk, INSR_SEED_VALUE, e);
       }
     }
   }
+  auto seed_stage = [&]() {
+    if constexpr (S == 1) {
+      if (J.seeds.nt) {
+        float* swq = sseed + T * 48;  // [wave][INSR_SEED_MAX]
+        float sq[INSR_SEED_MAX] = {0.f, 0.f, 0.f, 0.f};
+        if constexpr (kSeed1) {
+          if (threadIdx.x < T * 48) sseed[threadIdx.x] = gy ? sgy : seed_finish(J.seeds, sop, sq);
+        } else {
+          for (int i = threadIdx.x; i < T * 48; i += G::THREADS) {
+            const int t = i / 48, o = (i / 16) % 3, p = (tile0 + t) * 16 + (i & 15);
+            float v = 0.f;
+            if (t < cnt && p < N && o < dout) {
+              const long e = (long)p * dout + o;
+              v = gy ? gy[e] : seed_adjoint(J.seeds, jk, INSR_SEED_VALUE, e, true, sq);
+            }
+            sseed[i] = v;
+          }
+        }
+#pragma unroll
+        for (int q = 0; q < INSR_SEED_MAX; ++q) {
+          float v = sq[q];
+          for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+          if (lane == 0) swq[wave * INSR_SEED_MAX + q] = v;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+          floatx4 r = floatx4{0.f, 0.f, 0.f, 0.f};
+          for (int w = 0; w < G::THREADS / 64; ++w)
+#pragma unroll
+            for (int q = 0; q < INSR_SEED_MAX; ++q) r[q] += swq[w * INSR_SEED_MAX + q];
+          *reinterpret_cast<floatx4*>(J.seeds.lpart + (long)blockIdx.x * INSR_SEED_MAX) = r;
+        }
+      }
+    }
+  };
   auto adjoint = [&](int t, int s, int o) -> float {
     const int p = (tile0 + t) * 16 + c;
     if constexpr (S == 1)
@@ -1017,6 +1039,7 @@ __global__ __launch_bounds__(X6Geo<NT>::THREADS) void jet_bwd_x6(const BwdJobsX6
   // ---- output layer (exact fp32 VALU) ----
   floatx4 sn[T][RPW], cs[T][RPW];
   load_sc(L, sn, cs);
+  seed_stage();  // (the seeds' operands were loaded before load_sc's z-streams)
   const float* Wo = prm + out_off(din, W, L);
   const long wo_off = out_off(din, W, L);
   floatx4 hb[T][RPW][S];

@@ -37,6 +37,8 @@ for s in ${STEPS:-tests bench prof}; do
              run sd_Bs_$r 300 python bench.py --config fluid2DtlgnM --shard-of 8 --no-seed-in-bwd --steps 40 --warmup 3 --no-cpu-baseline --no-roofline
            done ;;
     prof) run prof 300 rocprofv3 --kernel-trace --stats -d "$PWD/$O/prof" -o run --output-format csv -- python bench.py --steps 10 --warmup 3 --no-cpu-baseline ;;
+    profB) run profB 300 rocprofv3 --kernel-trace --stats -d "$PWD/$O/profB" -o run --output-format csv -- python bench.py --no-seed-in-bwd --steps 10 --warmup 3 --no-cpu-baseline ;;
+    profshardB) run profshardB 300 rocprofv3 --kernel-trace --stats -d "$PWD/$O/profshardB" -o run --output-format csv -- python bench.py --config fluid2DtlgnM --shard-of 8 --no-seed-in-bwd --steps 10 --warmup 3 --no-cpu-baseline --no-roofline ;;
     profshard) run profshard 300 rocprofv3 --kernel-trace --stats -d "$PWD/$O/profshard" -o run --output-format csv -- python bench.py --config fluid2DtlgnM --shard-of 8 --steps 10 --warmup 3 --no-cpu-baseline --no-roofline ;;
     kbench) run kbench 400 python tools/kbench.py ${KARGS:---sizes 8192,16708,66844 --nets fluid_pres --modes lap --variants h3 --policies 0,2} ;;
     prec) run prec 400 python tools/prec_errors.py ${PARGS:-} ;;
