@@ -31,7 +31,7 @@ import torch
 
 from . import _jet
 from .networks import MLP
-from .losses import lazy_losses
+from .losses import lazy_losses, settle_lazy
 from .sampling import draw_ahead, draw_plan
 
 try:
@@ -77,10 +77,11 @@ class PhaseLoop:
     def _stage1(self):
         m = self.m
         m.optimizer, m.scheduler = self.opt, self.sched
-        with _jet.call_scope(self), draw_plan(self):
+        with _jet.call_scope(self), draw_plan(self), lazy_losses(m._lazy_losses_on()):
             loss_dict = self.func(m, *self.args, **self.kwargs)
         m.optimizer.zero_grad()
         m._backward(loss_dict)
+        settle_lazy()  # (the seeded jets' sums launches finished the loss values the pack reads)
         packed = m._dp_pack(loss_dict)  # gradients + losses in the arena (views of its tail)
         self.static_main = packed['main'].detach().reshape(1)
         return packed

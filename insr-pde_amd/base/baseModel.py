@@ -229,10 +229,10 @@ class BaseModel(ABC):
     _insr_lazy_losses = False
 
     def _lazy_losses_on(self):
-        """Whether the loop may open lazy_losses() around this model's phase body: opted in, one process,
-        the fused optimiser with deferred sums (the loss values are finished by the sums launch)."""
-        return (self._insr_lazy_losses and getattr(self.cfg, "insr_seed_in_bwd", True) and not self._dp_active()
-                and _jet.DEFER_REDUCE and isinstance(self.optimizer, FusedAdam))
+        """Whether the loop may open lazy_losses() around this model's phase body (opted in): the loss
+        values are finished by the sums launch of the reverse jet that took the group -- inside the Adam
+        launch (deferred sums), or right after the jet (data parallelism: before the arena pack)."""
+        return self._insr_lazy_losses and getattr(self.cfg, "insr_seed_in_bwd", True)
 
     def _update_network(self, loss_dict):
         """update network by back propagation (base/baseModel.py:73-81).  backward of

@@ -31,11 +31,12 @@ def _worker(port, q):
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
     ph = dict(np.load(GOLD))
     out = {}
-    # (single: without in-kernel loss seeds -- base/losses.py lazy_losses, which the data-parallel path does not
-    # take -- so the three runs compute the loss values in the same launches; tests/test_gpu_seeds.py covers them)
+    # single / split / captured without in-kernel loss seeds (base/losses.py lazy_losses): the three compute the
+    # loss values in the same launches; "seeded" = captured with them (the default), against "captured"
     for name, kw in (("single", dict(insr_dp_always=False, insr_seed_in_bwd=False)),
-                     ("split", dict(insr_dp_always=True, insr_dp_capture=False)),
-                     ("captured", dict(insr_dp_always=True, insr_dp_capture=True))):
+                     ("split", dict(insr_dp_always=True, insr_dp_capture=False, insr_seed_in_bwd=False)),
+                     ("captured", dict(insr_dp_always=True, insr_dp_capture=True, insr_seed_in_bwd=False)),
+                     ("seeded", dict(insr_dp_always=True, insr_dp_capture=True))):
         torch.manual_seed(0)
         cfg = make_config("fluid", num_hidden_layers=4, hidden_features=128, sample_resolution=32, dt=0.05,
                           proj_dir="/tmp/insr_dp_capture_test", insr_progress=False, early_stop=False,
@@ -72,8 +73,14 @@ def test_captured_allreduce_equals_split_and_single_process():
     res = q.get(timeout=240)
     p.join(timeout=60)
     assert p.exitcode == 0
-    assert not res["single"][3] and res["split"][3] and res["captured"][3]
+    assert not res["single"][3] and res["split"][3] and res["captured"][3] and res["seeded"][3]
     for name in ("split", "captured"):
         assert np.array_equal(res[name][0], res["single"][0]), name
         assert np.array_equal(res[name][1], res["single"][1]), name
         assert res[name][2] == res["single"][2], name
+    # the seeded DP iteration: the same parameters (the seeds are the group launch's gradients bit for bit),
+    # the loss values from another summation order
+    assert np.array_equal(res["seeded"][0], res["captured"][0]) and np.array_equal(res["seeded"][1], res["captured"][1])
+    assert len(res["seeded"][2]) == len(res["captured"][2])
+    for (t1, s1, m1, b1), (t2, s2, m2, b2) in zip(res["seeded"][2], res["captured"][2]):
+        assert (t1, s1) == (t2, s2) and abs(m1 - m2) <= 1e-6 * abs(m2) and abs(b1 - b2) <= 1e-6 * abs(b2)

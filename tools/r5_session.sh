@@ -23,6 +23,10 @@ for s in ${STEPS:-tests bench prof}; do
              run dpshard_el3d8 300 python bench.py --config elasticity3Dbunny --shard-of 8 --dp-path --steps 10 --warmup 3 --no-cpu-baseline --no-roofline ;;
     pol4) run pol4_shard 300 python bench.py --config fluid2DtlgnM --shard-of 8 --bwd-policy 4 --steps 20 --warmup 3 --no-cpu-baseline --no-roofline
           run pol4_head 300 python bench.py --bwd-policy 4 --steps 20 --warmup 3 --no-cpu-baseline --no-roofline ;;
+    abseeddp) for r in 1 2; do
+             run sdp_A_$r 300 python bench.py --config fluid2DtlgnM --shard-of 8 --dp-path --steps 40 --warmup 3 --no-cpu-baseline --no-roofline
+             run sdp_B_$r 300 python bench.py --config fluid2DtlgnM --shard-of 8 --dp-path --no-seed-in-bwd --steps 40 --warmup 3 --no-cpu-baseline --no-roofline
+           done ;;
     profdp) run profdp 300 rocprofv3 --kernel-trace --stats -d "$PWD/$O/profdp" -o run --output-format csv -- python bench.py --config fluid2DtlgnM --shard-of 8 --dp-path --steps 10 --warmup 3 --no-cpu-baseline --no-roofline ;;
     ablib) for r in 1 2; do
              run ab_A_$r 300 python bench.py --steps 40 --warmup 3 --no-cpu-baseline --no-roofline
