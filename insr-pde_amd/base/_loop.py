@@ -80,6 +80,7 @@ class PhaseLoop:
         with _jet.call_scope(self), draw_plan(self), lazy_losses(m._lazy_losses_on()):
             loss_dict = self.func(m, *self.args, **self.kwargs)
         m.optimizer.zero_grad()
+        m._dp_redirect(loss_dict)  # lazy groups' losses finished straight into the arena's loss slots
         m._backward(loss_dict)
         settle_lazy()  # (the seeded jets' sums launches finished the loss values the pack reads)
         packed = m._dp_pack(loss_dict)  # gradients + losses in the arena (views of its tail)

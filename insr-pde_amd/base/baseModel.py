@@ -219,9 +219,34 @@ class BaseModel(ABC):
             if not t and lo <= o < hi:
                 arena[o:o + n].zero_()
         tail = arena[loss_off:loss_off + len(keys)]
-        torch.stack([torch.as_tensor(loss_dict[k], device=dev).detach().float().reshape(()) for k in keys], out=tail)
+        # losses a seeded reverse jet's sums launch already finished in their slots (_dp_redirect) need no copy
+        direct = self.__dict__.pop("_insr_dp_direct", {})
+        rest = [i for i, k in enumerate(keys) if not (k in direct and direct[k].state == "seeded")]
+        if len(rest) == len(keys):
+            torch.stack([torch.as_tensor(loss_dict[k], device=dev).detach().float().reshape(()) for k in keys], out=tail)
+        else:
+            for i in rest:
+                tail[i].copy_(torch.as_tensor(loss_dict[keys[i]], device=dev).detach().float().reshape(()))
         self._insr_dp_red = arena[lo:hi]
         return {k: tail[i] for i, k in enumerate(keys)}
+
+    def _dp_redirect(self, loss_dict):
+        """Before the backward of a data-parallel iteration: the losses of lazy loss groups are finished by
+        their seeded reverse jet's sums launch straight into their arena slots (the arena exists from the
+        first iteration on), so _dp_pack copies only the others."""
+        from .losses import lazy_output
+        loss_off = self.__dict__.get("_insr_dp_loss_off")
+        arena = self.__dict__.get("_insr_dp_arena")
+        if not self._dp_active() or arena is None or loss_off is None:
+            return
+        direct = {}
+        for i, (k, v) in enumerate(loss_dict.items()):
+            hit = lazy_output(v)
+            if hit is not None:
+                g, j = hit
+                g.redirect(j, arena.data_ptr() + 4 * (loss_off + i))
+                direct[k] = g
+        self._insr_dp_direct = direct
 
     # A phase body that returns its sq_losses outputs and reads no jet output they read elsewhere may let
     # its loss groups ride in the reverse jets (base/losses.py lazy_losses): the model classes that are
@@ -239,6 +264,7 @@ class BaseModel(ABC):
         sum(loss_dict.values()) is run as backward of every term with a persistent unit
         seed: the same gradients without the add and ones-fill launches."""
         self.optimizer.zero_grad()
+        self._dp_redirect(loss_dict)  # data parallel: lazy groups' losses straight into the arena slots
         # one process with the fused optimiser: a fused-path backward's row sums run inside the Adam
         # launch (base/_jet.py defer_reductions; under data parallelism the all-reduce needs them first)
         defer = _jet.DEFER_REDUCE and isinstance(self.optimizer, FusedAdam) and not self._dp_active()

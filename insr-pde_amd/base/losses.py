@@ -218,7 +218,7 @@ class LazyGroup:
     """A loss group whose launch is held back: state 'pending' (formed), 'handed' (its unit-seeded
     backward gave out the unfilled gradient buffers), 'seeded' (a reverse jet took them), 'launched'."""
     __slots__ = ("arr", "k", "work", "dev", "outs", "metas", "owner", "real_a", "tensors", "grads", "state",
-                 "bufs", "__weakref__")
+                 "bufs", "over", "__weakref__")
 
     def materialize(self, stream=None):
         """Launch the group now (its losses and gradients, as the eager path) -- before anything reads them."""
@@ -266,8 +266,22 @@ class LazyGroup:
         f.part, f.rows, f.nloss = part.data_ptr(), rows, self.k
         for i in range(self.k):
             f.scale[i] = self.metas[i][4]
-            f.out[i] = self.outs[i].data_ptr()
+            f.out[i] = self.over[i] if self.over[i] is not None else self.outs[i].data_ptr()
         return f
+
+    def redirect(self, i, address):
+        """Finish loss i's value at `address` (a device float) instead of its own output tensor -- e.g. the
+        data-parallel arena's loss slot (BaseModel._dp_pack); the output tensor is then not written."""
+        self.over[i] = address
+
+
+def lazy_output(t):
+    """(LazyGroup, index) when t is a loss output of a lazy group formed on this thread, else None."""
+    for g in _Lazy.groups or ():
+        for i, o in enumerate(g.outs):
+            if o is t:
+                return g, i
+    return None
 
 
 def lazy_group_of(t):
@@ -369,6 +383,7 @@ class _SqLossGroup(torch.autograd.Function):
             lz = LazyGroup()
             lz.arr, lz.k, lz.work, lz.dev, lz.outs, lz.metas, lz.owner = arr, k, work, dev, outs, metas, owner
             lz.real_a, lz.tensors, lz.grads, lz.state, lz.bufs = list(real_a), list(tensors), grads, "pending", []
+            lz.over = [None] * k
             ctx.lazy = lz
             if _Lazy.groups is None:
                 _Lazy.groups = []
