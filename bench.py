@@ -73,8 +73,9 @@ def parse():
                          "config), bf16x3 (3 bf16 products), bf16 (1 product) or mixed (bf16x3 forwards, bf16 "
                          "backwards: BASELINE configs[4] 'mixed fp32/bf16 MFMA', within 1e-2)")
     ap.add_argument("--api", choices=["fused", "plain"], default="fused",
-                    help="fluid: 'plain' runs pde/fluid_plain.py, phase bodies written only against the "
-                         "reference's base API (separate band samplers, torch residuals) -- the drop-in case")
+                    help="fluid / advect1D: 'plain' runs pde/fluid_plain.py / pde/advection_plain.py, phase bodies "
+                         "written only against the reference's base API (separate band samplers, torch residuals, "
+                         "lowered by the loop: base/lower.py) -- the drop-in case")
     ap.add_argument("--shard-of", type=int, default=1,
                     help="one process runs the per-rank shard of a K-rank strong-scaling run (global batch / K "
                          "points per phase iteration; elasticity: the draw at resolution / K^(1/3)); 1 GPU")
@@ -231,6 +232,8 @@ def finish_model(args, cfg, wl, world, rank, per_rank):
         from pde.fluid_plain import Fluid2DPlainModel as M
     elif wl["pde"] == "fluid":
         from pde.fluid import Fluid2DModel as M
+    elif wl["pde"] == "advection" and args.api == "plain":
+        from pde.advection_plain import Advection1DPlainModel as M
     elif wl["pde"] == "advection":
         from pde.advection import Advection1DModel as M
     else:

@@ -431,7 +431,10 @@ int insr_adam_step(float* params, const float* grads, float* exp_avg, float* exp
  *                    r = alpha (a + beta b) + gamma (c + delta d), evaluated in that
  *                    order; b, c, d may be NULL (= 0; d needs c); all contiguous, n elements
  *   INSR_LOSS_BANDS  out = scale * (sum_{r<n} y[r][0]^2 + sum_{r<n} y[n+r][1]^2)
- *                    (a = y, (2n, m) row-major, m >= 2; b = c = d = NULL)
+ *                    (a = y, (2n, m) row-major, m >= 2; c = d = NULL), or, with b != NULL,
+ *                    scale * (sum_{r<n} a[r][0]^2 + sum_{r<n} b[r][1]^2): the two bands in
+ *                    tensors of their own ((n, m) each, the reference's separate band calls
+ *                    fluid/model.py:96-98,119-122)
  * The forward reduction is deterministic (fixed order).  Up to 4096 terms it is one
  * launch; beyond, per-block partials go to `work` (insr_sq_loss_work_floats()
  * floats, ZERO-initialised once by the caller, not shared by concurrent launches)
@@ -439,7 +442,8 @@ int insr_adam_step(float* params, const float* grads, float* exp_avg, float* exp
  * leaves the work's ticket word zero again).
  * Backward: g = 2 scale gout r;  ga = alpha g, gb = alpha beta g, gc = gamma g,
  * gd = gamma delta g (bands: ga = the full (2n, m) gradient, zeros outside the
- * selected columns); any output may be NULL (bands: ga required).
+ * selected columns; with b: ga and gb the full (n, m) gradients of a and b); any output may be
+ * NULL (bands: at least one).
  */
 #define INSR_LOSS_COMBO 0
 #define INSR_LOSS_BANDS 1
@@ -456,7 +460,7 @@ int insr_sq_loss_fwd(int kind, const float* a, const float* b, const float* c, c
  * sb, sc, sd (e.g. the diagonal of a Jacobian).  ga is written on elements [ga_lo, ga_hi):
  * the loss's terms, zeros elsewhere in that range -- two losses over disjoint rows of ONE
  * tensor (a merged jet's interior and band rows) share one gradient buffer; gb / gc / gd are
- * n contiguous elements (gb_len ... = n, or 0 when NULL).  work: insr_sq_loss_work_floats()
+ * n contiguous elements (gb_len ... = n, or 0 when NULL; BANDS with b: gb = b's n x m gradient).  work: insr_sq_loss_work_floats()
  * floats, zero-initialised once (left zero).  A unit-seeded loss's backward then needs no
  * launch. */
 /* out[i] = clamp(x[i] + alpha y[i], lo, hi), i < n: the semi-Lagrangian foot of the fluid

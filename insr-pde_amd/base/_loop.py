@@ -32,6 +32,7 @@ import torch
 from . import _jet
 from .networks import MLP
 from .losses import lazy_losses, settle_lazy
+from .lower import lower_losses, lowering
 from .sampling import draw_ahead, draw_plan
 
 try:
@@ -68,7 +69,10 @@ class PhaseLoop:
         self.m.optimizer, self.m.scheduler = self.opt, self.sched
         # lazy_losses: the body's loss groups ride in the reverse jets (BaseModel._lazy_losses_on)
         with _jet.call_scope(self), draw_plan(self), lazy_losses(self.m._lazy_losses_on()):
-            loss_dict = self.func(self.m, *self.args, **self.kwargs)
+            # lowering: an unchanged reference body's residual expressions -> one loss-group launch (base/lower.py)
+            with lowering(self.m._lower_on()):
+                loss_dict = self.func(self.m, *self.args, **self.kwargs)
+            loss_dict = lower_losses(loss_dict)
         synced = self.m._update_network(loss_dict)
         return synced if isinstance(synced, dict) else loss_dict
 
@@ -78,7 +82,9 @@ class PhaseLoop:
         m = self.m
         m.optimizer, m.scheduler = self.opt, self.sched
         with _jet.call_scope(self), draw_plan(self), lazy_losses(m._lazy_losses_on()):
-            loss_dict = self.func(m, *self.args, **self.kwargs)
+            with lowering(m._lower_on()):
+                loss_dict = self.func(m, *self.args, **self.kwargs)
+            loss_dict = lower_losses(loss_dict)
         m.optimizer.zero_grad()
         m._dp_redirect(loss_dict)  # lazy groups' losses finished straight into the arena's loss slots
         m._backward(loss_dict)

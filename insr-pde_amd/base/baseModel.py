@@ -259,6 +259,16 @@ class BaseModel(ABC):
         launch (deferred sums), or right after the jet (data parallelism: before the arena pack)."""
         return self._insr_lazy_losses and getattr(self.cfg, "insr_seed_in_bwd", True)
 
+    # Loss lowering (base/lower.py): the loop runs the phase body with network / diff-op outputs as Lazy
+    # tensors and computes the losses it recognises -- the reference's torch.mean((a - b) ** 2) residuals
+    # and wall terms as written -- in ONE fused loss-group launch.  On for every model (an unchanged
+    # reference model file); the model classes written against the fused helpers (pde/fluid.py, ...) turn
+    # it off; cfg.insr_lower = False turns it off for a run
+    _insr_lower = True
+
+    def _lower_on(self):
+        return self._insr_lower and getattr(self.cfg, "insr_lower", True)
+
     def _update_network(self, loss_dict):
         """update network by back propagation (base/baseModel.py:73-81).  backward of
         sum(loss_dict.values()) is run as backward of every term with a persistent unit

@@ -33,6 +33,7 @@ import torch
 
 from . import _jet
 from . import _native as nat
+from .lower import api as _api
 from .networks import MLP
 
 __all__ = ["hessian", "laplace", "divergence", "gradient", "jacobian"]
@@ -110,6 +111,7 @@ def _jet_or_none(mlp, holder, x, mode):
         return None
 
 
+@_api
 def gradient(y, x, grad_outputs=None):
     """d(sum_c grad_outputs_c * y_c)/dx, shape x.shape (base/diff_ops.py:53-58)."""
     r = _resolve(y, x, "gradient")
@@ -133,6 +135,7 @@ def gradient(y, x, grad_outputs=None):
     return g
 
 
+@_api
 def divergence(y, x):
     """sum_i dy_i/dx_i, shape (..., 1) (base/diff_ops.py:44-50)."""
     r = _resolve(y, x, "divergence")
@@ -163,6 +166,7 @@ def divergence(y, x):
     return div
 
 
+@_api
 def laplace(y, x, normalize=False, eps=0., return_grad=False):
     """div(grad y) (base/diff_ops.py:33-41).  normalize=True: div(g / (|g| + eps)), g = grad y,
     = tr(H) / (|g| + eps) - g.H g / (|g| (|g| + eps)^2) with H the Hessian of sum_c y_c
@@ -188,6 +192,7 @@ def laplace(y, x, normalize=False, eps=0., return_grad=False):
     return div
 
 
+@_api
 def jacobian(y: torch.FloatTensor, x: torch.FloatTensor):
     """(N, dim_y, dim_x) Jacobian and status (-1 if NaN) (base/diff_ops.py:61-82)."""
     J = jacobian_only(y, x)
@@ -195,12 +200,14 @@ def jacobian(y: torch.FloatTensor, x: torch.FloatTensor):
     return J, status
 
 
+@_api
 def jacobian_nosync(y, x):
     """jacobian() without the NaN status host sync (returns the device flag instead)."""
     J = jacobian_only(y, x)
     return J, torch.isnan(J).any()
 
 
+@_api
 def jacobian_only(y, x):
     """The (N, dim_y, dim_x) Jacobian of jacobian() alone: no status (no NaN scan launches)."""
     r = _resolve(y, x, "jacobian")
@@ -314,6 +321,7 @@ def _hessian_core(y, x, opname):
     return H.reshape(*L0.shape, 2, 2)
 
 
+@_api
 def hessian(y, x):
     """base/diff_ops.py:6-30: y (meta, obs, channels), x (meta, obs, dim) -> the Hessian
     (meta, obs, channels, dim, dim) and status (-1 if NaN); 2-D y, x give (N, channels, dim, dim).

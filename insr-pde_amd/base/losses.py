@@ -112,13 +112,16 @@ class LossSpec:
         self.tensors = (a, b, c, d)
 
     def a_range(self):
-        """Elements of `a` the loss reads: [a_off, a_off + terms) (BANDS: 2n rows of m)."""
+        """Elements of `a` the loss reads: [a_off, a_off + terms) (BANDS: 2n rows of m; n rows when the
+        second band is a tensor of its own, b)."""
         kind, n, m, _, _, a_off, _ = self.meta
-        return a_off, a_off + (n if kind == nat.LOSS_COMBO else 2 * n * m)
+        if kind == nat.LOSS_COMBO:
+            return a_off, a_off + n
+        return a_off, a_off + (1 if self.tensors[1] is not None else 2) * n * m
 
 
 def _mse_spec(a, b=None, c=None, d=None, alpha=1.0, beta=-1.0, gamma=1.0, delta=1.0, count=None, a_row0=0,
-              reduction="mean", total=None):
+              reduction="mean", total=None, weight=1.0):
     if count is None:
         for t in (b, c, d):
             if t is not None and t.shape != a.shape:
@@ -136,6 +139,8 @@ def _mse_spec(a, b=None, c=None, d=None, alpha=1.0, beta=-1.0, gamma=1.0, delta=
     # total: the denominator of the mean (default: the terms summed here) -- under data parallelism the
     # GLOBAL term count, so the ranks' losses and gradients sum to the global mean (no 1/world pass)
     scale = 1.0 / max(count if total is None else total, 1) if reduction == "mean" else 1.0
+    if weight != 1.0:  # weight * the loss (base/lower.py: a reference loss scaled by a constant)
+        scale = float(weight) * scale
     (b, sb), (c, sc), (d, sd) = _prep_strided(b), _prep_strided(c), _prep_strided(d)
     return LossSpec(nat.LOSS_COMBO, count, 1, (alpha, beta, gamma, delta), scale, _prep(a), b, c, d, a_off,
                     (sb, sc, sd))
@@ -146,6 +151,18 @@ def _wall_spec(y, n, row0=0, total=None):
         raise ValueError(f"wall_mse: expected ({row0} + 2*{n} rows, m>=2), got {tuple(y.shape)}")
     return LossSpec(nat.LOSS_BANDS, n, y.shape[1], (0.0, 0.0, 0.0, 0.0), 1.0 / max(n if total is None else total, 1),
                     _prep(y), None, None, None, int(row0) * y.shape[1])
+
+
+def wall_term2(ya, yb, weight=1.0):
+    """weight * (mean(ya[:, 0] ** 2) + mean(yb[:, 1] ** 2)) for two (n, m) tensors of their own (the
+    reference's separate band calls, fluid/model.py:96-98,119-122), unlaunched: an argument of sq_losses()."""
+    if ya.dim() != 2 or ya.shape != yb.shape or ya.shape[1] < 2:
+        raise ValueError(f"wall_term2: expected two (n, m >= 2) tensors, got {tuple(ya.shape)}, {tuple(yb.shape)}")
+    if not yb.is_contiguous():
+        raise ValueError("wall_term2: the second band must be contiguous")
+    n = ya.shape[0]
+    return LossSpec(nat.LOSS_BANDS, n, ya.shape[1], (0.0, 0.0, 0.0, 0.0), float(weight) / max(n, 1), _prep(ya),
+                    _prep(yb), None, None, 0)
 
 
 def mse_term(*args, **kwargs):
@@ -368,7 +385,8 @@ class _SqLossGroup(torch.autograd.Function):
                 g[0] = grads[4 * owner[i]]
             grads.extend(g)
             terms = n if kind == nat.LOSS_COMBO else 2 * n
-            a_lo, a_hi = (a_off, a_off + terms * (1 if kind == nat.LOSS_COMBO else m))
+            a_rows = terms if (kind == nat.LOSS_COMBO or slot[1] is None) else n  # BANDS with b: a holds n rows
+            a_lo, a_hi = (a_off, a_off + a_rows * (1 if kind == nat.LOSS_COMBO else m))
             shared = owner[i] is not None or any(o == i for o in owner)
             lo, hi = (a_lo, a_hi) if shared else (0, 0 if g[0] is None else g[0].numel())
             lens = [0 if t is None else t.numel() for t in g[1:]]
@@ -379,7 +397,9 @@ class _SqLossGroup(torch.autograd.Function):
                               p(g[0]), lo, hi, a_off, p(g[1]), p(g[2]), p(g[3]), *lens)
         work = _workspace(dev) if multi else None
         ctx.lazy = None
-        if _Lazy.depth > 0 and _lazy_ok(metas, owner, real_a, need):
+        # (a BANDS term with its second band in a tensor of its own is never seeded in-kernel)
+        bands2 = any(mt[0] == nat.LOSS_BANDS and tensors[4 * i + 1] is not None for i, mt in enumerate(metas))
+        if _Lazy.depth > 0 and not bands2 and _lazy_ok(metas, owner, real_a, need):
             lz = LazyGroup()
             lz.arr, lz.k, lz.work, lz.dev, lz.outs, lz.metas, lz.owner = arr, k, work, dev, outs, metas, owner
             lz.real_a, lz.tensors, lz.grads, lz.state, lz.bufs = list(real_a), list(tensors), grads, "pending", []

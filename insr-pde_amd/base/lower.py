@@ -1,0 +1,474 @@
+"""Loss lowering for unchanged model files: the reference phase bodies' torch residual expressions
+(fluid/model.py:72-151, advection/model.py:68-91) become ONE loss-group launch per iteration.
+
+A reference phase body spells each loss as a chain of aten ops on the network outputs --
+torch.mean((u - target) ** 2), (torch.mean(ux[..., 0] ** 2) + torch.mean(uy[..., 1] ** 2)) * 1.0,
+F.mse_loss(u, ref) -- about 25 small launches forward and backward per phase iteration, which
+cost more than they compute (profiles/r03/plain_glue_attribution.txt).  While the training loop
+runs a phase body inside `lowering()` (base/_loop.py, models that do not opt out), every network
+and diff-op output is handed to the body as a `Lazy` tensor: a storage-less wrapper whose
+arithmetic is RECORDED instead of launched.  When the body returns, `lower_losses` reads each
+loss of its dict as a sum of mean squares of linear combinations of network / diff-op outputs
+and ordinary tensors and maps it onto the fused loss group (base/losses.py):
+
+    mean((c1 T1 + c2 T2 + c3 T3 + c4 T4) ** 2)              -> one COMBO term (r = alpha (a + beta b)
+                                                               + gamma (c + delta d))
+    w (mean(A[..., 0] ** 2) + mean(B[..., 1] ** 2))          -> one BANDS term over two tensors
+
+so that every loss of the iteration is ONE insr_sq_loss_group launch whose unit-seeded backward
+costs nothing.  The semi-Lagrangian foot clamp(x - dt u, lo, hi) a no-grad jet consumes is one
+insr_axpy_clamp launch.
+
+Anything else is EAGER, exactly as written: an op the recorder does not know, or any use of a
+Lazy tensor's value (float(), .cpu(), an unsupported torch function, a network input, ...),
+materialises it -- the recorded torch calls replayed on the real tensors, in the grad mode they
+were recorded in, with their autograd history (cached: one replay per node).  A loss the lowering
+does not recognise is materialised the same way.  So the lowering changes launch counts and fp32
+rounding order (a mean as scale * sum, c x / dt as (c / dt) x), never semantics; the unchanged
+reference bodies are pinned to the reference golden vectors through it
+(tests/test_gpu_plain_api.py).
+"""
+import threading
+
+import torch
+
+__all__ = ["Lazy", "lowering", "suspended", "api", "active", "leaf", "materialize", "plan", "lower_losses", "LOWERED"]
+
+LOWERED = {"groups": 0, "terms": 0, "eager_losses": 0, "materialized": 0}  # counters (tests, docs)
+
+
+class _State(threading.local):
+    depth = 0
+
+
+_S = _State()
+
+
+class lowering:
+    """`with lowering(on): body()` -- network / diff-op outputs created inside are Lazy."""
+
+    def __init__(self, on=True):
+        self.on = bool(on)
+
+    def __enter__(self):
+        if self.on:
+            _S.depth += 1
+        return self
+
+    def __exit__(self, *exc):
+        if self.on:
+            _S.depth -= 1
+        return False
+
+
+def active():
+    return _S.depth > 0
+
+
+# ---- the recorded graph ------------------------------------------------------------------------
+# node kinds: 'leaf' (a real tensor), 'lin' (sum of coefficient x node), 'sq' (x ** 2), 'mean' (all
+# elements), 'sel' (x[..., k] of a 2-D x), 'detach', 'clamp' (scalar bounds).  Every node keeps the
+# torch call that made it (func, args, kwargs, grad mode): materialisation replays exactly that.
+class _Node:
+    __slots__ = ("kind", "kids", "coef", "k", "lo", "hi", "real", "real_ng", "call", "shape", "grad_mode")
+
+    def __init__(self, kind, kids=(), coef=None, k=None, lo=None, hi=None, real=None, call=None, shape=None):
+        self.kind, self.kids, self.coef, self.k, self.lo, self.hi = kind, tuple(kids), coef, k, lo, hi
+        self.real, self.real_ng, self.call, self.shape = real, None, call, shape
+        self.grad_mode = torch.is_grad_enabled()
+
+
+_META = {"__get__", "numel", "dim", "size", "__len__", "is_floating_point", "is_contiguous", "nelement",
+         "element_size", "ndimension", "get_device", "type"}
+
+
+class Lazy(torch.Tensor):
+    """A recorded (not yet computed) tensor: shape, dtype, device and requires_grad are real; any
+    use of its value materialises it (see the module docstring)."""
+
+    @staticmethod
+    def __new__(cls, node, dtype, device, requires_grad):
+        t = torch.Tensor._make_wrapper_subclass(cls, node.shape, dtype=dtype, device=device,
+                                                requires_grad=bool(requires_grad))
+        t._insr_node = node
+        return t
+
+    def __repr__(self):
+        return f"Lazy({self._insr_node.kind}, shape={tuple(self.shape)})"
+
+    @classmethod
+    def __torch_function__(cls, func, types, args=(), kwargs=None):
+        kwargs = kwargs or {}
+        name = getattr(func, "__name__", "")
+        if name in _META:
+            with torch._C.DisableTorchFunctionSubclass():
+                return func(*args, **kwargs)
+        r = _record(name, func, args, kwargs)
+        if r is not None:
+            return r
+        return func(*_real_tree(args), **_real_tree(kwargs))
+
+    @classmethod
+    def __torch_dispatch__(cls, func, types, args=(), kwargs=None):
+        # below autograd (a path that bypassed __torch_function__): compute on the real tensors
+        return func(*_real_tree(args), **_real_tree(kwargs or {}))
+
+
+def _node(t):
+    return t._insr_node if isinstance(t, Lazy) else None
+
+
+def _wrap(node, like_dtype, like_device, requires_grad):
+    return Lazy(node, like_dtype, like_device, requires_grad)
+
+
+def leaf(t):
+    """A network / diff-op output as a Lazy leaf (inside lowering(); otherwise t itself)."""
+    if not active() or not isinstance(t, torch.Tensor) or isinstance(t, Lazy) or t.dtype != torch.float32:
+        return t
+    return _wrap(_Node("leaf", real=t, shape=tuple(t.shape)), t.dtype, t.device, t.requires_grad)
+
+
+class suspended:
+    """`with suspended():` -- no Lazy outputs inside (a base-API call's own nested calls)."""
+
+    def __enter__(self):
+        self.depth, _S.depth = _S.depth, 0
+        return self
+
+    def __exit__(self, *exc):
+        _S.depth = self.depth
+        return False
+
+
+def api(fn):
+    """Decorator of the base API entry points (the networks' forward, the diff ops): Lazy arguments are
+    materialised, the call runs unlowered, and its tensor results come back as Lazy leaves while
+    lowering() is active."""
+    import functools
+
+    @functools.wraps(fn)
+    def w(*args, **kwargs):
+        args, kwargs = _real_tree(args), _real_tree(kwargs)
+        if not active():
+            return fn(*args, **kwargs)
+        with suspended():
+            r = fn(*args, **kwargs)
+        if isinstance(r, tuple):
+            return tuple(leaf(v) for v in r)
+        return leaf(r)
+    return w
+
+
+def _scalar(v):
+    """A Python float of a number or a 0-dim CPU tensor, else None (never a device read)."""
+    if isinstance(v, bool):
+        return None
+    if isinstance(v, (int, float)):
+        return float(v)
+    if isinstance(v, torch.Tensor) and not isinstance(v, Lazy) and v.dim() == 0 and v.device.type == "cpu":
+        return float(v)
+    return None
+
+
+def _operand(v):
+    """The node of a tensor operand of a recorded op (a real tensor becomes a leaf), None otherwise."""
+    if isinstance(v, Lazy):
+        return v._insr_node
+    if isinstance(v, torch.Tensor) and v.dtype == torch.float32:
+        return _Node("leaf", real=v, shape=tuple(v.shape))
+    return None
+
+
+def _req(*vals):
+    return torch.is_grad_enabled() and any(isinstance(v, torch.Tensor) and v.requires_grad for v in vals)
+
+
+def _lazy_of(kind, kids, call, shape, like, req, **kw):
+    n = _Node(kind, kids, call=call, shape=tuple(shape), **kw)
+    return _wrap(n, like.dtype, like.device, req)
+
+
+def _record(name, func, args, kwargs):
+    """A Lazy result of func(*args, **kwargs) when it is an op the lowering knows, else None."""
+    call = (func, args, kwargs)
+    tens = [a for a in args if isinstance(a, torch.Tensor)]
+    like = next((a for a in tens if isinstance(a, Lazy)), None)
+    if like is None or like.dtype != torch.float32:
+        return None
+    if name in ("add", "sub") and len(args) == 2 and set(kwargs) <= {"alpha"}:
+        x, y = args
+        nx, ny = _operand(x), _operand(y)
+        alpha = _scalar(kwargs.get("alpha", 1.0))
+        if nx is None or ny is None or alpha is None or nx.shape != ny.shape:
+            return None  # scalar offsets (no constant term in a residual) and broadcasting stay eager
+        sgn = alpha if name == "add" else -alpha
+        return _lazy_of("lin", (nx, ny), call, nx.shape, like, _req(x, y), coef=(1.0, sgn))
+    if name in ("mul", "div") and len(args) == 2 and not kwargs:
+        x, y = args
+        if name == "mul" and isinstance(x, Lazy) and x is y:
+            return _lazy_of("sq", (x._insr_node,), call, x._insr_node.shape, like, _req(x))
+        if not isinstance(x, Lazy) and name == "mul":
+            x, y = y, x
+        c = _scalar(y)
+        if not isinstance(x, Lazy) or c is None:
+            return None
+        if name == "div":
+            if c == 0.0:
+                return None
+            c = 1.0 / c
+        return _lazy_of("lin", (x._insr_node,), call, x._insr_node.shape, like, _req(x), coef=(c,))
+    if name == "neg" and len(args) == 1 and not kwargs:
+        x = args[0]
+        return _lazy_of("lin", (x._insr_node,), call, x._insr_node.shape, like, _req(x), coef=(-1.0,))
+    if name in ("pow", "square") and not kwargs and isinstance(args[0], Lazy):
+        e = 2.0 if name == "square" else (_scalar(args[1]) if len(args) == 2 else None)
+        if e != 2.0:
+            return None
+        x = args[0]
+        return _lazy_of("sq", (x._insr_node,), call, x._insr_node.shape, like, _req(x))
+    if name == "mean" and len(args) == 1 and not kwargs and isinstance(args[0], Lazy):
+        x = args[0]
+        return _lazy_of("mean", (x._insr_node,), call, (), like, _req(x))
+    if name == "mse_loss" and len(args) == 2 and set(kwargs) <= {"reduction", "size_average", "reduce", "weight"} \
+            and kwargs.get("reduction", "mean") == "mean" and all(kwargs.get(k) is None for k in
+                                                                   ("size_average", "reduce", "weight")):
+        x, y = args
+        nx, ny = _operand(x), _operand(y)
+        if nx is None or ny is None or nx.shape != ny.shape:
+            return None
+        r = _req(x, y)
+        d = _Node("lin", (nx, ny), coef=(1.0, -1.0), call=None, shape=nx.shape)
+        s = _Node("sq", (d,), call=None, shape=nx.shape)
+        return _lazy_of("mean", (s,), call, (), like, r)
+    if name == "__getitem__" and len(args) == 2 and isinstance(args[0], Lazy):
+        x, idx = args
+        n = x._insr_node
+        if len(n.shape) == 2 and isinstance(idx, tuple) and len(idx) == 2 and isinstance(idx[1], int) and \
+                (idx[0] is Ellipsis or idx[0] == slice(None)) and -n.shape[1] <= idx[1] < n.shape[1]:
+            k = idx[1] % n.shape[1]
+            return _lazy_of("sel", (n,), call, (n.shape[0],), like, x.requires_grad, k=k)
+        return None
+    if name == "detach" and len(args) == 1 and not kwargs:
+        x = args[0]
+        return _lazy_of("detach", (x._insr_node,), call, x._insr_node.shape, like, False)
+    if name == "clamp" and isinstance(args[0], Lazy):
+        lo = kwargs.get("min", args[1] if len(args) > 1 else None)
+        hi = kwargs.get("max", args[2] if len(args) > 2 else None)
+        if _scalar(lo) is None or _scalar(hi) is None or len(args) > 3 or set(kwargs) - {"min", "max"}:
+            return None
+        x = args[0]
+        return _lazy_of("clamp", (x._insr_node,), call, x._insr_node.shape, like, _req(x), lo=_scalar(lo),
+                        hi=_scalar(hi))
+    return None
+
+
+# ---- materialisation --------------------------------------------------------------------------
+def _real_tree(v):
+    if isinstance(v, Lazy):
+        return materialize(v)
+    if isinstance(v, (list, tuple)):
+        r = [_real_tree(a) for a in v]
+        return type(v)(r) if isinstance(v, list) else tuple(r)
+    if isinstance(v, dict):
+        return {k: _real_tree(a) for k, a in v.items()}
+    return v
+
+
+def _eval(n):
+    """The real tensor of node n: its recorded torch call replayed (in its recorded grad mode)."""
+    if n.real is not None:
+        return n.real
+    if n.call is None:  # an internal node (F.mse_loss's parts): evaluated by the enclosing call
+        raise RuntimeError("internal lazy node has no call of its own")
+    func, args, kwargs = n.call
+    a, k = _real_tree(args), _real_tree(kwargs)
+    with torch.set_grad_enabled(n.grad_mode):
+        n.real = func(*a, **k)
+    LOWERED["materialized"] += 1
+    return n.real
+
+
+def _axpy_clamp_fast(n):
+    """clamp(x + alpha y, lo, hi) of two real same-shape fp32 GPU tensors as one launch (no autograd:
+    the consumer runs without gradients), or None."""
+    if n.kind != "clamp":
+        return None
+    at = _atoms(n.kids[0])
+    if at is None or len(at) != 2 or any(a.kind == "sel" for _, a in at.values()):
+        return None
+    (cx, ax), (cy, ay) = at.values()
+    if cx != 1.0:
+        (cx, ax), (cy, ay) = (cy, ay), (cx, ax)
+    if cx != 1.0:
+        return None
+    x, y = _atom_tensor(ax), _atom_tensor(ay)
+    if not (x.is_cuda and y.is_cuda and x.shape == y.shape and x.is_contiguous() and y.is_contiguous()):
+        return None
+    from .losses import axpy_clamp
+    return axpy_clamp(x.detach(), y.detach(), cy, n.lo, n.hi)
+
+
+def materialize(t):
+    """The real tensor of t (t itself when it is not Lazy).  Under no_grad a clamp(x + a y) node takes
+    the one-launch axpy_clamp (cached apart from the autograd-carrying replay)."""
+    if not isinstance(t, Lazy):
+        return t
+    n = t._insr_node
+    if not torch.is_grad_enabled() and n.real is None:
+        if n.real_ng is None:
+            n.real_ng = _axpy_clamp_fast(n)
+        if n.real_ng is not None:
+            return n.real_ng
+    return _eval(n)
+
+
+# ---- lowering of the loss dict ----------------------------------------------------------------
+def _ms_terms(n, w=1.0):
+    """n as [(w_i, E_i)] with n = sum_i w_i mean(E_i ** 2), or None."""
+    if n.kind == "mean" and n.kids[0].kind == "sq":
+        return [(w, n.kids[0].kids[0])]
+    if n.kind == "lin":
+        out = []
+        for c, kid in zip(n.coef, n.kids):
+            t = _ms_terms(kid, w * c)
+            if t is None:
+                return None
+            out.extend(t)
+        return out
+    return None
+
+
+def _atoms(n, c=1.0, acc=None):
+    """E as {atom: coefficient} over leaf / detach / sel atoms (first-appearance order), or None."""
+    acc = {} if acc is None else acc
+    if n.kind == "lin":
+        for ci, kid in zip(n.coef, n.kids):
+            if _atoms(kid, c * ci, acc) is None:
+                return None
+        return acc
+    if n.kind in ("leaf", "detach", "sel"):
+        key = _atom_key(n)
+        if key is None:
+            return None
+        if key in acc:
+            acc[key] = (acc[key][0] + c, acc[key][1])
+        else:
+            acc[key] = (c, n)
+        return acc
+    return None
+
+
+def _atom_key(n):
+    if n.kind == "leaf":
+        return ("leaf", id(n.real))
+    if n.kind == "detach":
+        k = _atom_key(n.kids[0])
+        return None if k is None else ("detach",) + k
+    if n.kind == "sel":
+        k = _atom_key(n.kids[0])
+        return None if k is None else ("sel", n.k) + k
+    return None
+
+
+def _atom_tensor(n):
+    """The real tensor (or view) an atom reads: no launch (views, detach)."""
+    if n.kind == "leaf":
+        return n.real
+    if n.kind == "detach":
+        return _atom_tensor(n.kids[0]).detach()
+    return _atom_tensor(n.kids[0])[..., n.k]
+
+
+def plan(n):
+    """The fused form of loss node n, or None (eager):
+      ("combo", (a, b, c, d), (alpha, beta, gamma, delta), w): w mean((alpha (a + beta b) + gamma (c + delta d))^2)
+      ("bands2", (A, B), w):                                   w (mean(A[:, 0]^2) + mean(B[:, 1]^2))
+    (a contiguous; b, c, d None or same-shape tensors / 1-D strided views; no launch is made here)."""
+    terms = _ms_terms(n)
+    if not terms or any(w == 0.0 for w, _ in terms):
+        return None
+    if len(terms) == 2:  # w (mean(A[..., 0]^2) + mean(B[..., 1]^2)): one BANDS term over two tensors
+        (w0, e0), (w1, e1) = terms
+        at = [_atoms(e) for e in (e0, e1)]
+        if w0 != w1 or any(a is None or len(a) != 1 for a in at):
+            return None
+        (c0, a0), = at[0].values()
+        (c1, a1), = at[1].values()
+        if abs(c0) != 1.0 or abs(c1) != 1.0 or a0.kind != "sel" or a1.kind != "sel":
+            return None
+        if (a0.k, a1.k) == (1, 0):
+            a0, a1 = a1, a0
+        A, B = _atom_tensor(a0.kids[0]), _atom_tensor(a1.kids[0])
+        if (a0.k, a1.k) != (0, 1) or A.dim() != 2 or A.shape != B.shape or A.shape[1] < 2 or \
+                not (A.is_contiguous() and B.is_contiguous()) or A.device != B.device:
+            return None
+        return ("bands2", (A, B), w0)
+    if len(terms) != 1:
+        return None
+    (w, e), = terms
+    at = _atoms(e)
+    if at is None or not 1 <= len(at) <= 4:
+        return None
+    ops = [(c, _atom_tensor(a)) for c, a in at.values() if c != 0.0]
+    if not ops:
+        return None
+    shape, dev = ops[0][1].shape, ops[0][1].device
+    if any(t.shape != shape or t.device != dev for _, t in ops):
+        return None
+    # `a` must be contiguous (b, c, d may be 1-D strided views): a contiguous operand first
+    first = next((i for i, (_, t) in enumerate(ops) if t.is_contiguous()), None)
+    if first is None:
+        return None
+    ops = [ops[first]] + ops[:first] + ops[first + 1:]
+    while len(ops) < 4:
+        ops.append((0.0, None))
+    (c1, a), (c2, b), (c3, c), (c4, d) = ops
+    alpha, beta = c1, (c2 / c1 if b is not None else -1.0)
+    gamma, delta = (1.0, 1.0) if c is None else (c3, (c4 / c3 if d is not None else 1.0))
+    return ("combo", (a, b, c, d), (alpha, beta, gamma, delta), w)
+
+
+def _spec(n):
+    """The LossSpec (base/losses.py) of loss node n, or None (eager)."""
+    from . import losses as L
+    p = plan(n)
+    if p is None or not all(t is None or t.is_cuda for t in p[1]):
+        return None
+    if p[0] == "bands2":
+        (A, B), w = p[1], p[2]
+        return L.wall_term2(A, B, weight=w)
+    (a, b, c, d), (alpha, beta, gamma, delta), w = p[1], p[2], p[3]
+    # w mean(r^2): the loss's scale is w / count (w = 1 for the reference's losses; * 1.0 is exact)
+    return L.mse_term(a, b, c, d, alpha=alpha, beta=beta, gamma=gamma, delta=delta, weight=w)
+
+
+def lower_losses(loss_dict):
+    """The loss dict a phase body returned inside lowering(), with every recognised Lazy loss computed by
+    ONE fused loss-group launch (per LOSS_GROUP_MAX losses) and every other Lazy loss materialised."""
+    if not isinstance(loss_dict, dict) or not any(isinstance(v, Lazy) for v in loss_dict.values()):
+        return loss_dict
+    from . import _native as nat
+    from .losses import sq_losses
+    specs, slot = [], {}
+    for k, v in loss_dict.items():
+        if isinstance(v, Lazy):
+            sp = _spec(v._insr_node)
+            if sp is not None:
+                slot[k] = len(specs)
+                specs.append(sp)
+    outs = []
+    for i in range(0, len(specs), nat.LOSS_GROUP_MAX):
+        outs.extend(sq_losses(*specs[i:i + nat.LOSS_GROUP_MAX]))
+        LOWERED["groups"] += 1
+    LOWERED["terms"] += len(specs)
+    res = {}
+    for k, v in loss_dict.items():
+        if k in slot:
+            res[k] = outs[slot[k]]
+        elif isinstance(v, Lazy):
+            LOWERED["eager_losses"] += 1
+            res[k] = materialize(v)
+        else:
+            res[k] = v
+    return res

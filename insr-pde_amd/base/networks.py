@@ -31,6 +31,7 @@ import torch
 import torch.nn as nn
 
 from . import _jet
+from . import lower
 
 OMEGA = 30.0
 KERNEL_WIDTHS = (32, 64, 128, 256)  # hidden widths the HIP jets are compiled for
@@ -163,6 +164,7 @@ class TorchMLP(nn.Module):
             warnings.warn(f"MLP({nonlinearity}, outermost_linear={outermost_linear}, width {hidden_features}): no "
                           "HIP jet serves it; running plain torch ops (off the INSR-PDE hot path)", stacklevel=3)
 
+    @lower.api
     def forward(self, coords, weights=None):
         out = self.net(coords)
         return out * weights if weights is not None else out
@@ -582,6 +584,7 @@ class MLP(nn.Module):
         return g
 
     # ---- forward -------------------------------------------------------------
+    @lower.api
     def forward(self, coords, weights=None):
         out = _jet.siren_value(self, coords)
         if weights is not None:

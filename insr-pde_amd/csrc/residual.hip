@@ -110,11 +110,17 @@ __global__ __launch_bounds__(256) void sq_loss_bwd_kernel(int kind, LossIn in, l
     }
     return;
   }
-  // bands: the full (2n, m) gradient, zero outside the selected columns
-  const long total = 2 * n * m;
+  // bands: the full (2n, m) gradient, zero outside the selected columns; with in.b (the second band in a
+  // tensor of its own) a's (n, m) gradient (column 0) and b's (n, m) gradient (column 1)
+  const long total = (in.b ? 1 : 2) * n * m;
   for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < total; e += (long)gridDim.x * 256) {
     const long row = e / m;
     const int col = (int)(e - row * m);
+    if (in.b) {
+      if (ga) ga[e] = col == 0 ? g2 * in.a[e] : 0.f;
+      if (gb) gb[e] = col == 1 ? g2 * in.b[e] : 0.f;
+      continue;
+    }
     const int sel = row < n ? 0 : 1;
     ga[e] = col == sel ? g2 * in.a[e] : 0.f;
   }
@@ -176,17 +182,23 @@ __global__ __launch_bounds__(kLossThreads) void sq_loss_group_kernel(const LossG
 #pragma unroll
       for (int q = 1; q < 4; ++q)
         if (gp[q] && e < gl[q]) gp[q][e] = e < n ? cf[q] * g : 0.f;
-    } else {  // BANDS: element e of a's gradient; term (row) e of the loss
+    } else {  // BANDS: element e of a's gradient; term (row) e of the loss.  With L.b the second band is
+              // rows [0, n) of b's own (n, m) tensor (column 1), and b's full gradient is written too
+      const float* bb = L.b;
       if (e < count) {
-        const float v = in.a[e * m + (e < n ? 0 : 1)];
+        const float v = (bb && e >= n) ? bb[(e - n) * m + 1] : in.a[e * m + (e < n ? 0 : 1)];
         acc += v * v;
       }
       if (gp[0] && e < gl[0]) {
         const long ea = L.ga_lo + e;
         const long row = ea / m - L.a_off / m;
         const int col = (int)(ea % m);
-        const bool hit = row >= 0 && row < 2 * n && col == (row < n ? 0 : 1);
+        const bool hit = row >= 0 && row < (bb ? n : 2 * n) && col == (row < n ? 0 : 1);
         gp[0][ea] = hit ? g2 * in.a[row * m + col] : 0.f;
+      }
+      if (gp[1] && e < gl[1]) {
+        const long row = e / m;
+        gp[1][e] = (row < n && e - row * m == 1) ? g2 * bb[e] : 0.f;
       }
     }
   }
@@ -252,7 +264,9 @@ int insr_sq_loss_group(const InsrLoss* losses, int count, float* work, void* str
     if (!L.a || !L.out || L.n < 0 || L.a_off < 0 || L.ga_lo < 0 || (L.ga && L.ga_hi < L.ga_lo)) return INSR_EINVAL;
     if (L.sb < 1 || L.sc < 1 || L.sd < 1) return INSR_EINVAL;
     if (L.kind != INSR_LOSS_COMBO && L.kind != INSR_LOSS_BANDS) return INSR_EINVAL;
-    if (L.kind == INSR_LOSS_BANDS && (L.m < 2 || L.b || L.c || L.d || L.gb || L.gc || L.gd || L.a_off % L.m))
+    // BANDS: b (optional) = the second band's own tensor, n x m like a's band (no stride), gb its gradient
+    if (L.kind == INSR_LOSS_BANDS && (L.m < 2 || L.c || L.d || L.gc || L.gd || L.a_off % L.m || (L.gb && !L.b) ||
+                                      (L.b && L.sb != 1) || (L.gb && L.gb_len > L.n * L.m)))
       return INSR_EINVAL;
     if (L.d && !L.c) return INSR_EINVAL;
     G.l[k] = L;
@@ -276,10 +290,11 @@ int insr_sq_loss_bwd(int kind, const float* a, const float* b, const float* c, c
                      float alpha, float beta, float gamma, float delta, float scale, const float* gout, float* ga,
                      float* gb, float* gc, float* gd, void* stream) {
   if (!a || !gout || n < 0) return INSR_EINVAL;
-  if (kind == INSR_LOSS_BANDS && (m < 2 || !ga || b || c || d || gb || gc || gd)) return INSR_EINVAL;
+  if (kind == INSR_LOSS_BANDS && (m < 2 || (!ga && !gb) || (gb && !b) || (!b && !ga) || c || d || gc || gd))
+    return INSR_EINVAL;
   if (kind != INSR_LOSS_COMBO && kind != INSR_LOSS_BANDS) return INSR_EINVAL;
   if (d && !c) return INSR_EINVAL;
-  const long total = kind == INSR_LOSS_COMBO ? n : 2 * n * m;
+  const long total = kind == INSR_LOSS_COMBO ? n : (b ? 1 : 2) * n * m;
   if (total == 0) return 0;
   long nb = (total + 255) / 256;
   if (nb > 2048) nb = 2048;

@@ -14,6 +14,7 @@ from .examples import get_examples
 class Advection1DModel(BaseModel):
     """advection equation with constant velocity"""
     _dp_loss_reduction = 'sum'  # means over the GLOBAL point count (BaseModel._dp_total): no 1/world pass
+    _insr_lower = False  # written against the fused helpers (no expression lowering, base/lower.py)
 
     def __init__(self, cfg):
         super().__init__(cfg)

@@ -28,6 +28,7 @@ from base.diff_ops import jacobian_only
 
 class ElasticityModel(BaseModel):
     _dp_loss_reduction = 'sum'
+    _insr_lower = False  # written against the fused helpers (no expression lowering, base/lower.py)
 
     def __init__(self, cfg):
         super().__init__(cfg)

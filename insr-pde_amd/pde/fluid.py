@@ -32,6 +32,8 @@ class Fluid2DModel(BaseModel):
     # the phase bodies return their sq_losses outputs and read the jet outputs those losses read nowhere
     # else: the loss groups ride in the reverse jets (base/losses.py lazy_losses)
     _insr_lazy_losses = True
+    # written against the fused helpers already (merged batches, loss groups): no expression lowering
+    _insr_lower = False
 
     def __init__(self, cfg):
         super().__init__(cfg)

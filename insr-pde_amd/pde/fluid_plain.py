@@ -27,6 +27,8 @@ class Fluid2DPlainModel(Fluid2DModel):
     """Fluid2DModel with phase bodies that use the reference API only (same losses)."""
     _dp_loss_reduction = 'mean'  # torch.mean over this rank's points: the all-reduce averages
     _insr_lazy_losses = False  # the reference bodies: torch expressions, no loss groups
+    # ... which the loop lowers (base/lower.py) -- as for any model file that does not opt out
+    _insr_lower = True
 
     def _sample_in_training(self):
         return sample_random(self._n_interior(), 2, device=self.device).requires_grad_(True)

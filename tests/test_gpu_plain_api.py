@@ -87,3 +87,95 @@ def test_plain_step_graph_replay():
         results.append(np.array(losses))
     assert np.all(np.isfinite(results[0])) and np.all(np.isfinite(results[1]))
     assert np.allclose(results[0], results[1], rtol=0.5, atol=1e-6), results
+
+
+def test_plain_phases_lowered_match_reference(ph, monkeypatch):
+    """The same reference bodies as the loop runs them: inside base.lower.lowering() the network and
+    diff-op outputs are Lazy, every loss is lowered to ONE fused loss-group launch per phase (no eager
+    residual expression left), and losses and gradients still match the reference's golden vectors."""
+    import pde.fluid_plain as fp
+    from base import lower as LW
+    model = _model(sample_resolution=32)
+    T = lambda k: torch.from_numpy(ph[k]).cuda()  # noqa: E731
+    nets = {"vel": model.velocity_field, "vel_prev": model.velocity_field_prev, "pres": model.pressure_field}
+    monkeypatch.setattr(fp, "sample_boundary2D_separate",
+                        lambda n, side, device=None: T("fluid/bcx0" if side == "horizontal" else "fluid/bcy0").clone())
+    model._sample_in_training = lambda: T("fluid/x0").clone().requires_grad_(True)
+    for phase in ("_advect_velocity", "_solve_pressure", "_projection"):
+        body = getattr(type(model), phase)._insr_phase
+        for k, n in nets.items():
+            with torch.no_grad():
+                n.flat_params().copy_(T(f"fluid/{k}/params0"))
+        model._reset_optimizer()
+        c0 = dict(LW.LOWERED)
+        with LW.lowering(model._lower_on()):
+            ld = body(model)
+        assert all(isinstance(v, LW.Lazy) for v in ld.values()), phase
+        ld = LW.lower_losses(ld)
+        assert LW.LOWERED["groups"] == c0["groups"] + 1 and LW.LOWERED["terms"] == c0["terms"] + 2, phase
+        assert LW.LOWERED["eager_losses"] == c0["eager_losses"], phase
+        for k, v in ld.items():
+            ref = float(ph[f"fluid/{phase}/loss_{k}"])
+            assert abs(float(v) - ref) <= 1e-5 * abs(ref) + 1e-12, (phase, k, float(v), ref)
+        model.optimizer.zero_grad()
+        model._backward(ld)
+        for key, net in (("vel", model.velocity_field), ("pres", model.pressure_field)):
+            g_ref = ph[f"fluid/{phase}/grad_{key}"]
+            if np.abs(g_ref).max() > 0:
+                g = net.flat_grad_buffer().detach().cpu().numpy()
+                assert nerr(g, g_ref) < 1e-5, (phase, key)
+
+
+def test_lowered_foot_is_one_launch_and_equal():
+    """clamp(x - dt u, -1, 1) recorded under lowering and consumed by a no-grad network call is one
+    insr_axpy_clamp launch; the value equals the eager expression (fmaf rounding: <= 1 ulp)."""
+    from base import lower as LW
+    g = torch.Generator(device="cuda").manual_seed(3)
+    x = (torch.rand(4096, 2, device="cuda", generator=g) * 2 - 1).requires_grad_(True)
+    u = torch.randn(4096, 2, device="cuda", generator=g)
+    with LW.lowering():
+        ul = LW.leaf(u)
+        foot = torch.clamp(x - ul.detach() * 0.05, min=-1.0, max=1.0)
+    assert isinstance(foot, LW.Lazy)
+    with torch.no_grad():
+        fast = LW.materialize(foot)
+    eager = torch.clamp(x - u * 0.05, min=-1.0, max=1.0)
+    assert fast.grad_fn is None
+    assert torch.allclose(fast, eager.detach(), rtol=0, atol=2e-7)
+    slow = LW.materialize(foot)  # with gradients: the recorded ops, autograd history kept
+    assert slow.grad_fn is not None and torch.equal(slow, eager)
+
+
+def test_plain_advection_lowered_matches_reference(ph, monkeypatch):
+    """advection/model.py:68-91 as written (pde/advection_plain.py), run as the loop runs it: both losses
+    lowered to one fused group (mean(((u - u0)/dt + v (ux + u0x)/2)^2) -> a 4-operand COMBO term), two
+    reference iterations (phase + Adam + plateau) against the golden loss trace and update."""
+    import pde.advection_plain as ap
+    from base import lower as LW
+    from pde.config import make_config
+    cfg = make_config("advection", proj_dir="/tmp/insr_test", insr_progress=False, early_stop=False, max_n_iters=2,
+                      lr=1e-4, num_hidden_layers=3, hidden_features=64, sample_resolution=512, dt=0.05, vel=0.25,
+                      length=4.0)
+    model = ap.Advection1DPlainModel(cfg)
+    T = lambda k: torch.from_numpy(ph[k]).cuda()  # noqa: E731
+    with torch.no_grad():
+        model.field.flat_params().copy_(T("advect/field/params0"))
+        model.field_prev.flat_params().copy_(T("advect/field_prev/params0"))
+    body = ap.Advection1DPlainModel._advect._insr_phase
+    model._reset_optimizer()
+    trace = []
+    for it in range(2):
+        model._sample_in_training = lambda it=it: T(f"advect/x{it}").clone().requires_grad_(True)
+        monkeypatch.setattr(ap, "sample_boundary", lambda n, sdim, device=None, it=it, **k: T(f"advect/bc{it}") / 2.0)
+        c0 = dict(LW.LOWERED)
+        with LW.lowering(model._lower_on()):
+            ld = body(model)
+        ld = LW.lower_losses(ld)
+        assert LW.LOWERED["terms"] == c0["terms"] + 2 and LW.LOWERED["eager_losses"] == c0["eager_losses"]
+        if it == 0:
+            for k, v in ld.items():
+                ref = float(ph[f"advect/_advect/loss_{k}"])
+                assert abs(float(v) - ref) <= 1e-5 * abs(ref) + 1e-12, (k, float(v), ref)
+        model._update_network(ld)
+        trace.append([float(ld[k]) for k in sorted(ld)])
+    assert nerr(np.array(trace), ph["advect/_advect/loss_trace"]) < 1e-5

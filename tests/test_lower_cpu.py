@@ -1,0 +1,170 @@
+"""base/lower.py on the CPU: the recorder and the loss plans, with CPU tensors standing in for the jets'
+outputs (the networks are HIP-only; the fused launch itself is covered by tests/test_gpu_plain_api.py).
+
+* every reference phase body's loss (fluid/model.py:72-151, advection/model.py:68-91) is recognised,
+  and its plan -- evaluated here with torch ops -- equals the eager expression, value and gradients;
+* anything the recorder does not know runs eagerly with the same values and autograd history;
+* Lazy tensors answer shape / dtype / requires_grad without materialising.
+"""
+import os
+import sys
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "insr-pde_amd"))
+from base import lower as LW  # noqa: E402
+
+
+def _eval_plan(p):
+    if p[0] == "bands2":
+        (A, B), w = p[1], p[2]
+        return w * ((A[:, 0] ** 2).mean() + (B[:, 1] ** 2).mean())
+    (a, b, c, d), (al, be, ga, de), w = p[1], p[2], p[3]
+    r = a if b is None else a + be * b
+    r = al * r
+    if c is not None:
+        q = c if d is None else c + de * d
+        r = r + ga * q
+    return w * (r ** 2).mean()
+
+
+def _leaves(*ts):
+    return [LW.leaf(t) for t in ts]
+
+
+def _grads(loss, ts):
+    return torch.autograd.grad(loss, ts, allow_unused=True)
+
+
+def _check(build, ts, kind):
+    """build(*inputs) -> a loss: its Lazy plan == the eager loss (value and gradients)."""
+    ref = build(*ts)
+    g_ref = _grads(ref, [t for t in ts if t.requires_grad])
+    with LW.lowering():
+        lz = build(*_leaves(*ts))
+    assert isinstance(lz, LW.Lazy) and lz.shape == ()
+    p = LW.plan(lz._insr_node)
+    assert p is not None and p[0] == kind
+    v = _eval_plan(p)
+    assert torch.allclose(v, ref, rtol=1e-6, atol=0), (float(v), float(ref))
+    g = _grads(v, [t for t in ts if t.requires_grad])
+    for a, b in zip(g, g_ref):
+        assert (a is None) == (b is None)
+        if a is not None:
+            assert torch.allclose(a, b, rtol=1e-5, atol=1e-9)
+    # the materialised Lazy loss (the eager route) is the expression itself
+    m = LW.materialize(lz)
+    assert torch.equal(m, ref)
+    gm = _grads(m, [t for t in ts if t.requires_grad])
+    for a, b in zip(gm, g_ref):
+        if a is not None:
+            assert torch.equal(a, b)
+
+
+def _t(*shape, grad=True, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    return torch.randn(*shape, generator=g).requires_grad_(grad)
+
+
+def test_fluid_advect_main():
+    u, target = _t(64, 2), _t(64, 2, grad=False, seed=1)
+    _check(lambda u, t: torch.mean((u - t) ** 2), [u, target], "combo")
+
+
+def test_fluid_walls_two_tensors():
+    ux, uy = _t(9, 2, seed=2), _t(9, 2, seed=3)
+    _check(lambda a, b: (torch.mean(a[..., 0] ** 2) + torch.mean(b[..., 1] ** 2)) * 1.0, [ux, uy], "bands2")
+    # the pressure walls (no * 1.0) and the bands written in the other order
+    _check(lambda a, b: torch.mean(a[:, 0] ** 2) + torch.mean(b[:, 1] ** 2), [ux, uy], "bands2")
+    _check(lambda a, b: torch.mean(b[..., 1] ** 2) + torch.mean(a[..., 0] ** 2), [ux, uy], "bands2")
+
+
+def test_fluid_pressure_main():
+    div_u, lap_p = _t(64, 1, grad=False, seed=4), _t(64, 1, seed=5)
+    _check(lambda d, l: torch.mean((d.detach() - l) ** 2), [div_u, lap_p], "combo")
+
+
+def test_fluid_projection_main():
+    u, u_old, gp = _t(64, 2), _t(64, 2, grad=False, seed=6), _t(64, 2, seed=7)
+    _check(lambda u, uo, g: torch.mean((u - (uo - g.detach())) ** 2), [u, u_old, gp], "combo")
+
+
+def test_advection_main_and_bc():
+    dt, vel = 0.05, 0.8
+    u, u0, gu, gu0 = _t(50, 1), _t(50, 1, grad=False, seed=8), _t(50, 1, seed=9), _t(50, 1, seed=10)
+    _check(lambda u, u0, gu, gu0: torch.mean(((u - u0) / dt + vel * (gu + gu0.detach()) / 2.) ** 2),
+           [u, u0, gu, gu0], "combo")
+    ub = _t(10, 1, seed=11)
+    _check(lambda b: torch.mean(b ** 2) * 1., [ub], "combo")
+
+
+def test_initialize_mse_loss():
+    u, ref = _t(64, 2), _t(64, 2, grad=False, seed=12)
+    _check(lambda u, r: F.mse_loss(u, r), [u, ref], "combo")
+
+
+def test_unknown_ops_stay_eager():
+    u, v = _t(16, 2), _t(16, 2, seed=13)
+    with LW.lowering():
+        a, b = _leaves(u, v)
+        y = torch.sin(a) * b + 1.0           # sin: not recorded -> real; * b, + 1.0 on reals: eager
+        z = (a * b).sum()                     # a * b of two tensors: not linear -> eager
+        w = torch.mean(a ** 3)                # ** 3 -> eager
+    assert not isinstance(y, LW.Lazy) and not isinstance(z, LW.Lazy) and not isinstance(w, LW.Lazy)
+    assert torch.equal(y, torch.sin(u) * v + 1.0)
+    assert torch.equal(z, (u * v).sum())
+    assert torch.equal(w, torch.mean(u ** 3))
+    gz = torch.autograd.grad(z, [u])[0]
+    assert torch.equal(gz, v)
+
+
+def test_metadata_without_materialising():
+    u = _t(8, 2)
+    with LW.lowering():
+        (a,) = _leaves(u)
+        d = (a - a.detach() * 2.0)
+        before = LW.LOWERED["materialized"]
+        assert d.shape == (8, 2) and d.dtype == torch.float32 and d.requires_grad and d.dim() == 2
+        assert d.numel() == 16 and d.size(0) == 8 and len(d) == 8
+        assert not a.detach().requires_grad
+        with torch.no_grad():
+            assert not (a * 2.0).requires_grad
+        assert LW.LOWERED["materialized"] == before
+        assert float(torch.mean(d ** 2)) == pytest.approx(float(torch.mean((u - u.detach() * 2.0) ** 2)))
+
+
+def test_unrecognised_loss_materialised_by_lower_losses():
+    u, v = _t(16, 2), _t(16, 2, seed=14)
+    with LW.lowering():
+        a, b = _leaves(u, v)
+        ld = {"main": torch.mean((a - b) ** 2) + torch.mean(a ** 2),  # two unpaired terms: eager
+              "bc": torch.mean(a[..., 0] ** 2) + torch.mean(b[..., 0] ** 2)}  # both column 0: eager
+    assert LW.plan(ld["main"]._insr_node) is None and LW.plan(ld["bc"]._insr_node) is None
+    out = LW.lower_losses(ld)
+    assert not any(isinstance(v_, LW.Lazy) for v_ in out.values())
+    assert torch.allclose(out["main"], torch.mean((u - v) ** 2) + torch.mean(u ** 2))
+    out["main"].backward()
+    assert u.grad is not None
+
+
+def test_broadcasting_and_offsets_stay_eager():
+    u, w = _t(16, 1), _t(16, seed=15)
+    with LW.lowering():
+        (a,) = _leaves(u)
+        r = a - w  # (16, 1) - (16,) broadcasts: eager
+        s = a + 1.0  # a constant offset: eager
+    assert not isinstance(r, LW.Lazy) and r.shape == (16, 16)
+    assert not isinstance(s, LW.Lazy)
+
+
+def test_lowering_inactive_outside_scope():
+    u = _t(4, 2)
+    assert LW.leaf(u) is u
+    with LW.lowering(False):
+        assert LW.leaf(u) is u
+    with LW.lowering():
+        with LW.suspended():
+            assert LW.leaf(u) is u
+        assert isinstance(LW.leaf(u), LW.Lazy)
