@@ -100,6 +100,9 @@ def parse():
     ap.add_argument("--no-seed-in-bwd", action="store_true",
                     help="launch every loss group (A/B studies; default: the fluid / advection bodies' groups are "
                          "evaluated inside the reverse jets, base/losses.py lazy_losses)")
+    ap.add_argument("--no-defer-jets", action="store_true",
+                    help="api plain: launch each network / diff-op call at once (A/B; default: the lowered body's "
+                         "jets are queued and launched together at the first read, base/lower.py deferred_jets)")
     ap.add_argument("--rehearse", action="store_true",
                     help="CPU rehearsal of the multi-rank launch (gloo, no GPU work; tests)")
     args = ap.parse_args()
@@ -203,6 +206,7 @@ def build_model(args, world, rank):
     res = wl["res"]
     cfg = baseline_config(args.config, sample_resolution=res, insr_graph=not args.no_graph, insr_dp_always=args.dp_path,
                           insr_graph_unroll=max(1, args.graph_unroll), insr_seed_in_bwd=not args.no_seed_in_bwd,
+                          insr_defer_jets=not args.no_defer_jets,
                           insr_sync_every=10 ** 9, insr_progress=False, early_stop=False,
                           proj_dir="/tmp/insr_bench", max_n_iters=10 ** 9,
                           insr_precision=None if args.precision == "fp32" else args.precision)
@@ -691,6 +695,7 @@ def main():
                    "jet_precision": jet_precision_names(args.precision),
                    "bwd_policy": args.bwd_policy, "shard_of": args.shard_of, "dp_path": args.dp_path,
                    "seeds_in_bwd": bool(getattr(cfg, "insr_seed_in_bwd", True)),
+                   "lowered": bool(model._lower_on()), "deferred_jets": bool(model._defer_on()),
                    "bwd_f16": bwd_f16,
                    "timestep_order": f"{nts} timesteps x ({'/'.join(str(k) for k in ks)}) iterations per phase, "
                                      "phases in step() order with the prev-net snapshots; per-timestep times from HIP events"},

@@ -622,10 +622,11 @@ def _launch_mixed(din, L, W, pbits, dev, alljobs):
     nat.check(rc, "insr_siren_jet_fwd_mixed")
 
 
-def advect_target(mlp, x, dt, lo=-1.0, hi=1.0):
+def advect_target(mlp, x, dt, lo=-1.0, hi=1.0, up=None):
     """(f(clamp(x - dt f(x), lo, hi)), f(x)) of a frozen field f (fluid/model.py:96-97, the
     semi-Lagrangian target of the advection) as ONE job of a mixed launch -- inside a
-    fused_forwards scope together with the phase's other jets.  No autograd (a target)."""
+    fused_forwards scope together with the phase's other jets.  No autograd (a target).
+    up: the (n, d) buffer f(x) is written to (default: a new one)."""
     mlp.ensure_packed()
     mlp.ensure_wsplit()
     n, din = x.shape
@@ -634,7 +635,10 @@ def advect_target(mlp, x, dt, lo=-1.0, hi=1.0):
     x2 = x.detach() if x.is_contiguous() else x.detach().contiguous()
     dev = x2.device
     y = torch.empty(n, din, device=dev, dtype=torch.float32)
-    up = torch.empty(n, din, device=dev, dtype=torch.float32)
+    if up is None:
+        up = torch.empty(n, din, device=dev, dtype=torch.float32)
+    elif up.shape != (n, din) or not up.is_contiguous():
+        raise UnsupportedPattern("advect_target: up must be a contiguous (n, d) buffer")
     foot = torch.empty(n, din, device=dev, dtype=torch.float32)
     cmode = (mlp.call_mode(nat.MODE_VALUE) & ~nat.MODE_MASK) | MIX_ADVECT
     job = (x2, mlp.flat_params(), y, up, foot, None, n, din, (float(dt), float(lo), float(hi)))

@@ -32,7 +32,7 @@ import torch
 from . import _jet
 from .networks import MLP
 from .losses import lazy_losses, settle_lazy
-from .lower import lower_losses, lowering
+from .lower import deferred_jets, lower_losses, lowering
 from .sampling import draw_ahead, draw_plan
 
 try:
@@ -70,7 +70,7 @@ class PhaseLoop:
         # lazy_losses: the body's loss groups ride in the reverse jets (BaseModel._lazy_losses_on)
         with _jet.call_scope(self), draw_plan(self), lazy_losses(self.m._lazy_losses_on()):
             # lowering: an unchanged reference body's residual expressions -> one loss-group launch (base/lower.py)
-            with lowering(self.m._lower_on()):
+            with lowering(self.m._lower_on()), deferred_jets(self.m._defer_on()):
                 loss_dict = self.func(self.m, *self.args, **self.kwargs)
             loss_dict = lower_losses(loss_dict)
         synced = self.m._update_network(loss_dict)
@@ -82,7 +82,7 @@ class PhaseLoop:
         m = self.m
         m.optimizer, m.scheduler = self.opt, self.sched
         with _jet.call_scope(self), draw_plan(self), lazy_losses(m._lazy_losses_on()):
-            with lowering(m._lower_on()):
+            with lowering(m._lower_on()), deferred_jets(m._defer_on()):
                 loss_dict = self.func(m, *self.args, **self.kwargs)
             loss_dict = lower_losses(loss_dict)
         m.optimizer.zero_grad()

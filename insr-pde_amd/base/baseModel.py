@@ -269,6 +269,11 @@ class BaseModel(ABC):
     def _lower_on(self):
         return self._insr_lower and getattr(self.cfg, "insr_lower", True)
 
+    def _defer_on(self):
+        """With lowering: the body's forward jets are queued and launched together at the first read of a
+        value (base/lower.py deferred_jets); cfg.insr_defer_jets = False launches each call at once."""
+        return self._lower_on() and getattr(self.cfg, "insr_defer_jets", True)
+
     def _update_network(self, loss_dict):
         """update network by back propagation (base/baseModel.py:73-81).  backward of
         sum(loss_dict.values()) is run as backward of every term with a persistent unit

@@ -33,6 +33,7 @@ import torch
 
 from . import _jet
 from . import _native as nat
+from . import lower as _lower
 from .lower import api as _api
 from .networks import MLP
 
@@ -43,7 +44,9 @@ FALLBACKS = {}  # op name -> calls served by the reference-semantics route
 
 def _fallback(opname, why):
     """Book-keeping of one reference-semantics call (a warning on the first one per op)."""
-    if _jet._Fused.pending is not None:
+    if _lower.deferring():  # the loop's deferred jets (base/lower.py): the route reads values -- launch them
+        _lower.flush()
+    elif _jet._Fused.pending is not None:
         raise _jet.UnsupportedPattern(f"{opname} of an unfused graph inside a fused_forwards scope: its jets have "
                                       "no values until the scope exits")
     FALLBACKS[opname] = FALLBACKS.get(opname, 0) + 1
@@ -121,6 +124,8 @@ def gradient(y, x, grad_outputs=None):
         return _ref_gradient(y, x, grad_outputs)
     mlp, value, affine = r
     _, J, _ = res  # (..., dout, din)
+    if J.shape[-2] != 1 or affine or grad_outputs is not None:
+        _lower.flush()  # a reduction / add over the jet's outputs: their values first (deferred jets)
     if grad_outputs is None:
         # scalar net: a view (no launch, and its backward is a view too)
         g = J.squeeze(-2) if J.shape[-2] == 1 else J.sum(dim=-2)
@@ -147,6 +152,8 @@ def divergence(y, x):
             _fallback("divergence", "the divergence of a weighted gradient" if not unit else "no Laplacian kernel")
             return _ref_divergence(y, x)
         lap = res[2]
+        if lap.shape[-1] != 1:
+            _lower.flush()
         return lap if lap.shape[-1] == 1 else lap.sum(dim=-1, keepdim=True)
     res = _jet_or_none(r[0], r[1], x, nat.MODE_GRAD) if r is not None else None
     if res is None:
@@ -157,9 +164,10 @@ def divergence(y, x):
     k = min(J.shape[-2], J.shape[-1])
     if k == 1:
         div = J[..., 0, :1]
-    elif k == 2:  # one fused add instead of diagonal + reduction
-        div = J[..., 0, 0:1] + J[..., 1, 1:2]
+    elif k == 2:  # one fused add instead of diagonal + reduction (recorded while jets are deferred)
+        div = _lower.add_views(J[..., 0, 0:1], J[..., 1, 1:2])
     else:
+        _lower.flush()
         div = torch.diagonal(J[..., :k, :k], dim1=-2, dim2=-1).sum(dim=-1, keepdim=True)
     if affine:
         div = div + float(k)
@@ -182,6 +190,8 @@ def laplace(y, x, normalize=False, eps=0., return_grad=False):
         return (div, g) if return_grad else div
     mlp, value, affine = r
     _, J, lap = res
+    if lap.shape[-1] != 1 or (return_grad and (J.shape[-2] != 1 or affine)):
+        _lower.flush()  # reductions over the jet's outputs: their values first (deferred jets)
     # the identity part of f(x)+x has zero Laplacian; a scalar net needs no reduction launch
     div = lap if lap.shape[-1] == 1 else lap.sum(dim=-1, keepdim=True)
     if return_grad:
@@ -196,6 +206,7 @@ def laplace(y, x, normalize=False, eps=0., return_grad=False):
 def jacobian(y: torch.FloatTensor, x: torch.FloatTensor):
     """(N, dim_y, dim_x) Jacobian and status (-1 if NaN) (base/diff_ops.py:61-82)."""
     J = jacobian_only(y, x)
+    _lower.flush()  # the status reads the values
     status = -1 if bool(torch.isnan(J).any()) else 0
     return J, status
 
@@ -204,6 +215,7 @@ def jacobian(y: torch.FloatTensor, x: torch.FloatTensor):
 def jacobian_nosync(y, x):
     """jacobian() without the NaN status host sync (returns the device flag instead)."""
     J = jacobian_only(y, x)
+    _lower.flush()
     return J, torch.isnan(J).any()
 
 
@@ -218,11 +230,17 @@ def jacobian_only(y, x):
     mlp, value, affine = r
     _, J, _ = res
     if affine:
+        _lower.flush()
         J = J + torch.eye(J.shape[-1], device=J.device, dtype=J.dtype)
     return J
 
 
 def _laplace_normalized(y, x, eps, return_grad):
+    with _lower.immediate():  # reads its jets' values in this call
+        return _laplace_normalized_now(y, x, eps, return_grad)
+
+
+def _laplace_normalized_now(y, x, eps, return_grad):
     g = gradient(y, x)
     try:
         H = _hessian_core(y, x, "laplace(normalize=True)").sum(dim=-3)  # Hessian of sum_c y_c
@@ -328,7 +346,8 @@ def hessian(y, x):
     The polarised jets serve d_in <= 2; other inputs (and unfused graphs) take the reference's
     route.  The identity part of f(x) + x has zero Hessian."""
     try:
-        H = _hessian_core(y, x, "hessian")
+        with _lower.immediate():  # the polarised jets' values are read in this call
+            H = _hessian_core(y, x, "hessian")
     except _jet.UnsupportedPattern:
         if _jet._Fused.pending is not None:
             raise

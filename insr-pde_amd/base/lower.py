@@ -32,13 +32,15 @@ import threading
 
 import torch
 
-__all__ = ["Lazy", "lowering", "suspended", "api", "active", "leaf", "materialize", "plan", "lower_losses", "LOWERED"]
+__all__ = ["Lazy", "lowering", "deferred_jets", "deferring", "flush", "immediate", "add_views", "suspended", "api",
+           "active", "leaf", "materialize", "plan", "lower_losses", "LOWERED"]
 
 LOWERED = {"groups": 0, "terms": 0, "eager_losses": 0, "materialized": 0}  # counters (tests, docs)
 
 
 class _State(threading.local):
     depth = 0
+    defer = 0  # > 0: network / diff-op jets are queued (a fused_forwards scope) and launched at the first read
 
 
 _S = _State()
@@ -63,6 +65,83 @@ class lowering:
 
 def active():
     return _S.depth > 0
+
+
+# ---- deferred jets ------------------------------------------------------------------------------
+# Inside `deferred_jets()` (opened by the loop with lowering()) the forward jets the body asks for are
+# QUEUED, as in a base.fused_forwards scope (base/_jet.py): the phase body gets Lazy leaves of their
+# (not yet written) outputs, and the queue is launched -- jets of one architecture as ONE multi / mixed
+# launch -- at the first read of any value (materialize), before a diff op that needs values, and at the
+# scope's exit.  So the reference's separate calls (the interior batch and each wall band, the frozen and
+# the trainable field) share launches as the hand-fused model files arrange them.
+class deferred_jets:
+    """`with deferred_jets(on): body()` -- see above."""
+
+    def __init__(self, on=True):
+        self.on = bool(on)
+
+    def __enter__(self):
+        if self.on:
+            from . import _jet
+            self.ff = _jet.fused_forwards()
+            self.ff.__enter__()
+            _S.defer += 1
+        return self
+
+    def __exit__(self, *exc):
+        if self.on:
+            _S.defer -= 1
+            self.ff.__exit__(*exc)
+        return False
+
+
+def deferring():
+    """Whether jets are being queued right now (a deferred_jets scope with its fused scope open)."""
+    if _S.defer <= 0:
+        return False
+    from . import _jet
+    return _jet._Fused.pending is not None
+
+
+def flush():
+    """Launch the queued jets now (the scope stays open for the next ones)."""
+    if _S.defer <= 0:
+        return
+    from . import _jet
+    jobs = _jet._Fused.pending
+    if jobs:
+        _jet._Fused.pending = []
+        _jet._launch_fused(jobs)
+
+
+class immediate:
+    """`with immediate():` -- jets launched at once inside (the queue flushed first): a diff-op route that
+    reads its jets' values in the same call (Hessian polarisation, the reference-semantics fallback)."""
+
+    def __enter__(self):
+        from . import _jet
+        self.saved = None
+        if _S.defer > 0 and _jet._Fused.pending is not None:
+            flush()
+            self.saved, _jet._Fused.pending = _jet._Fused.pending, None
+        return self
+
+    def __exit__(self, *exc):
+        if self.saved is not None:
+            from . import _jet
+            _jet._Fused.pending = self.saved
+        return False
+
+
+def add_views(a, b):
+    """a + b of two views of queued jet outputs (the divergence's J[..., 0, 0:1] + J[..., 1, 1:2]): recorded
+    as a Lazy sum while jets are deferred (its operands have no values yet), else added now."""
+    if not deferring():
+        return a + b
+    n = _Node("lin", (_Node("leaf", real=a, shape=tuple(a.shape)), _Node("leaf", real=b, shape=tuple(b.shape))),
+              coef=(1.0, 1.0), call=(torch.add, (a, b), {}), shape=tuple(a.shape))
+    n.grad_mode = torch.is_grad_enabled()
+    return _wrap(n, a.dtype, a.device, torch.is_grad_enabled() and (a.requires_grad or b.requires_grad))
 
 
 # ---- the recorded graph ------------------------------------------------------------------------
@@ -149,6 +228,11 @@ def api(fn):
 
     @functools.wraps(fn)
     def w(*args, **kwargs):
+        if len(args) == 2 and not kwargs and isinstance(args[1], Lazy) and deferring() and \
+                not torch.is_grad_enabled():
+            r = _advect_target(args[0], args[1])
+            if r is not None:
+                return leaf(r)
         args, kwargs = _real_tree(args), _real_tree(kwargs)
         if not active():
             return fn(*args, **kwargs)
@@ -158,6 +242,40 @@ def api(fn):
             return tuple(leaf(v) for v in r)
         return leaf(r)
     return w
+
+
+def _advect_target(mlp, foot):
+    """f(clamp(x - dt f(x), lo, hi)) of a frozen field f asked for (no_grad) while f(x) is still a queued
+    value jet of the same network at the same x (fluid/model.py:79-87 as written): ONE advection-target job
+    of the mixed launch (base._jet.advect_target) that also writes f(x) into the queued jet's output, whose
+    own job is dropped -- the hand-fused model's launch (pde/fluid.py).  None when the pattern does not hold."""
+    from . import _jet
+    n = foot._insr_node
+    if n.kind != "clamp" or not hasattr(mlp, "flat_params") or _jet._Fused.pending is None:
+        return None
+    at = _atoms(n.kids[0])
+    if at is None or len(at) != 2:
+        return None
+    (cx, ax), (cy, ay) = at.values()
+    if cx != 1.0:
+        (cx, ax), (cy, ay) = (cy, ay), (cx, ax)
+    if cx != 1.0 or ax.kind != "leaf" or ay.kind != "leaf":
+        return None
+    x, u = ax.base, ay.base
+    if x.dim() != 2 or u.shape != x.shape or not x.is_contiguous():
+        return None
+    flat = mlp.flat_params()
+    for i, (key, job) in enumerate(_jet._Fused.pending):
+        if len(job) == 8 and job[2] is u and job[1] is flat and job[3] is None and job[5] is None and \
+                job[0].data_ptr() == x.data_ptr() and job[0].shape == x.shape and \
+                (key[3] & 0xF) == 0:  # a VALUE jet (INSR_MODE_VALUE)
+            try:
+                y, _ = _jet.advect_target(mlp, x, -cy, n.lo, n.hi, up=u)
+            except _jet.UnsupportedPattern:
+                return None
+            del _jet._Fused.pending[i]  # f(x) now comes from the target job
+            return y
+    return None
 
 
 def _scalar(v):
@@ -302,7 +420,7 @@ def _axpy_clamp_fast(n):
         (cx, ax), (cy, ay) = (cy, ay), (cx, ax)
     if cx != 1.0:
         return None
-    x, y = _atom_tensor(ax), _atom_tensor(ay)
+    x, y = ax.base, ay.base
     if not (x.is_cuda and y.is_cuda and x.shape == y.shape and x.is_contiguous() and y.is_contiguous()):
         return None
     from .losses import axpy_clamp
@@ -311,9 +429,11 @@ def _axpy_clamp_fast(n):
 
 def materialize(t):
     """The real tensor of t (t itself when it is not Lazy).  Under no_grad a clamp(x + a y) node takes
-    the one-launch axpy_clamp (cached apart from the autograd-carrying replay)."""
+    the one-launch axpy_clamp (cached apart from the autograd-carrying replay).  Queued jets are
+    launched first (their outputs are what the value reads)."""
     if not isinstance(t, Lazy):
         return t
+    flush()
     n = t._insr_node
     if not torch.is_grad_enabled() and n.real is None:
         if n.real_ng is None:
@@ -339,45 +459,45 @@ def _ms_terms(n, w=1.0):
     return None
 
 
-def _atoms(n, c=1.0, acc=None):
-    """E as {atom: coefficient} over leaf / detach / sel atoms (first-appearance order), or None."""
+class _Atom:
+    """An operand of a linear residual: a leaf tensor or a column of one (sel), possibly detached."""
+    __slots__ = ("kind", "k", "base", "det")
+
+    def __init__(self, kind, k, base, det):
+        self.kind, self.k, self.base, self.det = kind, k, base, det
+
+
+def _atoms(n, c=1.0, acc=None, det=False):
+    """E as {key: (coefficient, _Atom)} over leaf / sel operands (first-appearance order; a detach anywhere
+    above an operand detaches it: detach(sum c_i T_i) = sum c_i detach(T_i)), or None."""
     acc = {} if acc is None else acc
     if n.kind == "lin":
         for ci, kid in zip(n.coef, n.kids):
-            if _atoms(kid, c * ci, acc) is None:
+            if _atoms(kid, c * ci, acc, det) is None:
                 return None
         return acc
-    if n.kind in ("leaf", "detach", "sel"):
-        key = _atom_key(n)
-        if key is None:
-            return None
-        if key in acc:
-            acc[key] = (acc[key][0] + c, acc[key][1])
-        else:
-            acc[key] = (c, n)
-        return acc
-    return None
-
-
-def _atom_key(n):
-    if n.kind == "leaf":
-        return ("leaf", id(n.real))
     if n.kind == "detach":
-        k = _atom_key(n.kids[0])
-        return None if k is None else ("detach",) + k
+        return _atoms(n.kids[0], c, acc, True)
     if n.kind == "sel":
-        k = _atom_key(n.kids[0])
-        return None if k is None else ("sel", n.k) + k
-    return None
+        base = n.kids[0]
+        while base.kind == "detach":
+            det, base = True, base.kids[0]
+        if base.kind != "leaf":
+            return None
+        a = _Atom("sel", n.k, base.real, det)
+    elif n.kind == "leaf":
+        a = _Atom("leaf", None, n.real, det)
+    else:
+        return None
+    key = (a.kind, a.k, id(a.base), a.det)
+    acc[key] = (acc[key][0] + c, a) if key in acc else (c, a)
+    return acc
 
 
-def _atom_tensor(n):
+def _atom_tensor(a):
     """The real tensor (or view) an atom reads: no launch (views, detach)."""
-    if n.kind == "leaf":
-        return n.real
-    if n.kind == "detach":
-        return _atom_tensor(n.kids[0]).detach()
-    return _atom_tensor(n.kids[0])[..., n.k]
+    t = a.base if a.kind == "leaf" else a.base[..., a.k]
+    return t.detach() if a.det else t
 
 
 def plan(n):
@@ -399,7 +519,8 @@ def plan(n):
             return None
         if (a0.k, a1.k) == (1, 0):
             a0, a1 = a1, a0
-        A, B = _atom_tensor(a0.kids[0]), _atom_tensor(a1.kids[0])
+        A = a0.base.detach() if a0.det else a0.base
+        B = a1.base.detach() if a1.det else a1.base
         if (a0.k, a1.k) != (0, 1) or A.dim() != 2 or A.shape != B.shape or A.shape[1] < 2 or \
                 not (A.is_contiguous() and B.is_contiguous()) or A.device != B.device:
             return None
@@ -448,6 +569,7 @@ def lower_losses(loss_dict):
     ONE fused loss-group launch (per LOSS_GROUP_MAX losses) and every other Lazy loss materialised."""
     if not isinstance(loss_dict, dict) or not any(isinstance(v, Lazy) for v in loss_dict.values()):
         return loss_dict
+    flush()  # (the loop calls this after its deferred scope closed: nothing is queued any more)
     from . import _native as nat
     from .losses import sq_losses
     specs, slot = [], {}

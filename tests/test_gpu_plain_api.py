@@ -89,10 +89,12 @@ def test_plain_step_graph_replay():
     assert np.allclose(results[0], results[1], rtol=0.5, atol=1e-6), results
 
 
-def test_plain_phases_lowered_match_reference(ph, monkeypatch):
+@pytest.mark.parametrize("defer", [False, True])
+def test_plain_phases_lowered_match_reference(ph, monkeypatch, defer):
     """The same reference bodies as the loop runs them: inside base.lower.lowering() the network and
     diff-op outputs are Lazy, every loss is lowered to ONE fused loss-group launch per phase (no eager
-    residual expression left), and losses and gradients still match the reference's golden vectors."""
+    residual expression left), and losses and gradients still match the reference's golden vectors.
+    defer: the body's jets queued and launched together at the first read (base.lower.deferred_jets)."""
     import pde.fluid_plain as fp
     from base import lower as LW
     model = _model(sample_resolution=32)
@@ -108,7 +110,7 @@ def test_plain_phases_lowered_match_reference(ph, monkeypatch):
                 n.flat_params().copy_(T(f"fluid/{k}/params0"))
         model._reset_optimizer()
         c0 = dict(LW.LOWERED)
-        with LW.lowering(model._lower_on()):
+        with LW.lowering(model._lower_on()), LW.deferred_jets(defer):
             ld = body(model)
         assert all(isinstance(v, LW.Lazy) for v in ld.values()), phase
         ld = LW.lower_losses(ld)
@@ -179,3 +181,38 @@ def test_plain_advection_lowered_matches_reference(ph, monkeypatch):
         model._update_network(ld)
         trace.append([float(ld[k]) for k in sorted(ld)])
     assert nerr(np.array(trace), ph["advect/_advect/loss_trace"]) < 1e-5
+
+
+def test_deferred_jets_share_launches(ph, monkeypatch):
+    """Under deferred_jets the reference advection body's five network calls take two launches: the frozen
+    field's target chain f(clamp(x - dt f(x))) as ONE advection-target job beside the trainable field's
+    interior and band jets (plus nothing else); values equal the immediate calls'."""
+    import pde.fluid_plain as fp
+    from base import _jet
+    from base import lower as LW
+    model = _model(sample_resolution=32)
+    T = lambda k: torch.from_numpy(ph[k]).cuda()  # noqa: E731
+    for k, n in {"vel": model.velocity_field, "vel_prev": model.velocity_field_prev, "pres": model.pressure_field}.items():
+        with torch.no_grad():
+            n.flat_params().copy_(T(f"fluid/{k}/params0"))
+    monkeypatch.setattr(fp, "sample_boundary2D_separate",
+                        lambda n, side, device=None: T("fluid/bcx0" if side == "horizontal" else "fluid/bcy0").clone())
+    model._sample_in_training = lambda: T("fluid/x0").clone().requires_grad_(True)
+    body = type(model)._advect_velocity._insr_phase
+    launched = []
+    real_launch = _jet._launch_fused
+    monkeypatch.setattr(_jet, "_launch_fused", lambda jobs: (launched.append(len(jobs)), real_launch(jobs))[1])
+    out = {}
+    for defer in (False, True):
+        launched.clear()
+        model._reset_optimizer()
+        with LW.lowering(), LW.deferred_jets(defer):
+            ld = body(model)
+        ld = LW.lower_losses(ld)
+        out[defer] = {k: float(v) for k, v in ld.items()}
+        if defer:
+            assert launched == [4], launched  # [advect target, u(x), u(bx), u(by)] in one launch
+        else:
+            assert launched == [], launched
+    for k in out[False]:
+        assert abs(out[True][k] - out[False][k]) <= 1e-6 * abs(out[False][k]) + 1e-12, (k, out)

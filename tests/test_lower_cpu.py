@@ -168,3 +168,18 @@ def test_lowering_inactive_outside_scope():
         with LW.suspended():
             assert LW.leaf(u) is u
         assert isinstance(LW.leaf(u), LW.Lazy)
+
+
+def test_detached_sum_of_views():
+    """mean((div_u - lap_p) ** 2) with div_u = (J[..., 0, 0:1] + J[..., 1, 1:2]).detach() recorded as a sum of
+    two strided views (the deferred divergence, base/lower.py add_views): a 3-operand COMBO term."""
+    J, lap = _t(64, 2, 2, grad=False, seed=16), _t(64, 1, seed=17)
+    ref = torch.mean(((J[..., 0, 0:1] + J[..., 1, 1:2]).detach() - lap) ** 2)
+    with LW.lowering():
+        a, b, l_ = LW.leaf(J[..., 0, 0:1]), LW.leaf(J[..., 1, 1:2]), LW.leaf(lap)
+        lz = torch.mean(((a + b).detach() - l_) ** 2)
+    p = LW.plan(lz._insr_node)
+    assert p is not None and p[0] == "combo" and p[1][0] is lap and sum(t is not None for t in p[1]) == 3
+    assert torch.allclose(_eval_plan(p), ref, rtol=1e-6)
+    g = torch.autograd.grad(_eval_plan(p), [lap])[0]
+    assert torch.allclose(g, torch.autograd.grad(ref, [lap])[0], rtol=1e-5, atol=1e-9)
