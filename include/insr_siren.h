@@ -254,6 +254,14 @@ int insr_siren_jet_bwd_grad_multi(const InsrBwdJob* jobs, int n_jobs, int d_in, 
 /* Scratch bytes of insr_siren_jet_bwd_grad_multi for jobs of n[0..n_jobs) points. */
 long insr_jet_bwd_multi_work_bytes(const long* n, int n_jobs, int d_in, int d_out, int num_hidden, int width,
                                    int mode);
+/* The reverse jets of insr_siren_jet_bwd_grad_multi WITHOUT their sums, when every job takes the fused
+ * tile-split path: one launch writes the jobs' partial-gradient rows into `work` (row stride
+ * insr_jet_partial_stride) and the call returns the number of rows (>= 0); the caller sums them later --
+ * insr_reduce_partials_strided, or insr_adam_step_partials (the sums with the Adam update, one launch: the
+ * reference's separate interior / band calls of one network, fluid/model.py:80,96-97, then cost what one
+ * merged call costs).  INSR_EINVAL when a job takes another path (use insr_siren_jet_bwd_grad_multi). */
+int insr_siren_jet_bwd_multi_rows(const InsrBwdJob* jobs, int n_jobs, int d_in, int d_out, int num_hidden,
+                                  int width, int mode, const float* params, float* work, void* stream);
 /* 1 if insr_siren_jet_bwd_grad takes the wide path for this batch / width / mode. */
 int insr_jet_bwd_is_wide(long n_points, int d_in, int width, int mode);
 

@@ -467,6 +467,32 @@ def _launch_bwd_multi(jobs):
     gflat, accumulate = mlp.grad_for_backward()
     st = ctypes.c_void_p(cur.cuda_stream)
     mlp.grad_write_begin(cur)
+    if getattr(_Defer, "depth", 0) > 0 and len(jobs) <= nat.MAX_BWD_JOBS and all(j.act is not None for j in jobs):
+        # every job on the fused tile-split path: their partial rows now, the sums with the Adam launch
+        # (defer_reductions), as a single job's -- insr_siren_jet_bwd_multi_rows
+        arr = (nat.BwdJob * len(jobs))(*[
+            nat.BwdJob(j.x2.data_ptr(), nat.ptr(j.act), nat.ptr(j.gy), nat.ptr(j.gdy), nat.ptr(j.glap), j.x2.shape[0])
+            for j in jobs])
+        ns = (ctypes.c_long * len(jobs))(*[j.x2.shape[0] for j in jobs])
+        wb = lib.insr_jet_bwd_multi_work_bytes(ns, len(jobs), din, dout, L, W, cmode)
+        if wb >= 0:
+            with torch.cuda.stream(cur):
+                work = torch.empty(max(wb // 4, 1), device=jobs[0].x2.device, dtype=torch.float32)
+            with _timed("bwd%d" % len(jobs), mode, sum(ns), W, (din, dout, L)):
+                nb = lib.insr_siren_jet_bwd_multi_rows(arr, len(jobs), din, dout, L, W, cmode,
+                                                       nat.ptr(mlp.flat_params()), nat.ptr(work), st)
+            if nb >= 0:
+                stride = lib.insr_jet_partial_stride(din, dout, L, W)
+                pr = PendingSums("rows", work, nb, stride, mlp, gflat, accumulate, cur,
+                                 (mode, int(sum(ns)), W, (din, dout, L)))
+                if 0 < nb < 1024:
+                    mlp.set_pending_reduce(pr)
+                    _Defer.nets.append(mlp)
+                elif nb > 0:
+                    pr.launch()
+                mlp.grad_write_end(cur)
+                return
+            # (INSR_EINVAL: a job takes another path -- the full call below)
     for k in range(0, len(jobs), nat.MAX_BWD_JOBS):
         chunk = jobs[k:k + nat.MAX_BWD_JOBS]
         arr = (nat.BwdJob * len(chunk))(*[

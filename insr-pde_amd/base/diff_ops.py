@@ -34,7 +34,11 @@ import torch
 from . import _jet
 from . import _native as nat
 from . import lower as _lower
-from .lower import api as _api
+from .lower import api as _lower_api
+
+
+def _api(fn):
+    return _lower_api(fn, operand_first=True)
 from .networks import MLP
 
 __all__ = ["hessian", "laplace", "divergence", "gradient", "jacobian"]

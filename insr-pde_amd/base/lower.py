@@ -220,10 +220,12 @@ class suspended:
         return False
 
 
-def api(fn):
+def api(fn, operand_first=False):
     """Decorator of the base API entry points (the networks' forward, the diff ops): Lazy arguments are
     materialised, the call runs unlowered, and its tensor results come back as Lazy leaves while
-    lowering() is active."""
+    lowering() is active.  operand_first (the diff ops): the first argument -- the differentiated output,
+    read for its provenance, not its values -- is handed over without launching the queued jets when it
+    is a Lazy leaf."""
     import functools
 
     @functools.wraps(fn)
@@ -233,7 +235,11 @@ def api(fn):
             r = _advect_target(args[0], args[1])
             if r is not None:
                 return leaf(r)
-        args, kwargs = _real_tree(args), _real_tree(kwargs)
+        if operand_first and args:
+            args = (_api_tree(args[0]),) + tuple(_real_tree(a) for a in args[1:])
+        else:
+            args = _real_tree(args)
+        kwargs = _real_tree(kwargs)
         if not active():
             return fn(*args, **kwargs)
         with suspended():
@@ -382,6 +388,15 @@ def _record(name, func, args, kwargs):
 
 
 # ---- materialisation --------------------------------------------------------------------------
+def _api_tree(v):
+    """A diff op's operand: a Lazy LEAF is handed over as its real tensor without launching the queued jets
+    (the diff ops read its provenance, not its values -- they flush where they do); any other Lazy tensor
+    is materialised."""
+    if isinstance(v, Lazy) and v._insr_node.kind == "leaf":
+        return v._insr_node.real
+    return materialize(v)
+
+
 def _real_tree(v):
     if isinstance(v, Lazy):
         return materialize(v)

@@ -994,6 +994,9 @@ long insr_jet_bwd_multi_work_bytes(const long* n, int njobs, int din, int dout, 
   return bytes;
 }
 
+static int multi_fused_rows(const InsrBwdJob* jobs, const MultiPlan& p, int din, int dout, int L, int W, int mode,
+                            const float* params, float* work, hipStream_t st);
+
 int insr_siren_jet_bwd_grad_multi(const InsrBwdJob* jobs, int njobs, int din, int dout, int L, int W, int mode,
                                   const float* params, float* work, float* grad, int accumulate, void* stream) {
   if (!jobs || njobs < 1 || njobs > kBwdJobs) return INSR_EINVAL;
@@ -1034,6 +1037,45 @@ int insr_siren_jet_bwd_grad_multi(const InsrBwdJob* jobs, int njobs, int din, in
     }
   }
   if (p.nf > 0) {
+    if ((rc = multi_fused_rows(jobs, p, din, dout, L, W, mode, params, work, st))) return rc;
+    if ((rc = insr_reduce_partials_strided(work, p.nb, insr_siren_param_count(din, dout, L, W),
+                                           insr_jet_partial_stride(din, dout, L, W), grad, acc, stream)))
+      return rc;
+    acc = 1;
+  }
+  for (int q = 0; q < p.ns; ++q) {  // stream order: the previous job's reduction has read `work`
+    const InsrBwdJob& jb = jobs[p.solo[q]];
+    if ((rc = insr_siren_jet_bwd_grad(jb.x, jb.n, din, dout, L, W, mode, params, jb.act, jb.gy, jb.gdy, jb.glap, work,
+                                      grad, acc, stream)))
+      return rc;
+    acc = 1;
+  }
+  return 0;
+}
+
+int insr_siren_jet_bwd_multi_rows(const InsrBwdJob* jobs, int njobs, int din, int dout, int L, int W, int mode,
+                                  const float* params, float* work, void* stream) {
+  if (!jobs || njobs < 1 || njobs > kBwdJobs) return INSR_EINVAL;
+  long ns[kBwdJobs];
+  for (int k = 0; k < njobs; ++k) {
+    ns[k] = jobs[k].n;
+    if (jobs[k].n > 0 && (!jobs[k].x || !jobs[k].act)) return INSR_EINVAL;
+  }
+  MultiPlan p;
+  int rc = plan_multi(ns, njobs, din, dout, L, W, mode, p);
+  if (rc) return rc;
+  if (p.ns > 0 || JetCall(din, W, mode).recompute(L)) return INSR_EINVAL;  // a job another path serves
+  if (p.nf == 0) return 0;
+  if (!params || !work) return INSR_EINVAL;
+  if ((rc = multi_fused_rows(jobs, p, din, dout, L, W, mode, params, work, (hipStream_t)stream))) return rc;
+  return p.nb;
+}
+
+// the multi plan's fused tile-split jobs in ONE jet_bwd_x6 launch: p.nb partial-gradient rows into work
+static int multi_fused_rows(const InsrBwdJob* jobs, const MultiPlan& p, int din, int dout, int L, int W, int mode,
+                            const float* params, float* work, hipStream_t st) {
+  int rc = 0;
+  {
     const JetCall c(din, W, mode);
     const float* prm = params;
     if (!(prm = with_planes(params, din, dout, L, W, mode, st, 0, &rc))) return rc;
@@ -1054,19 +1096,8 @@ int insr_siren_jet_bwd_grad_multi(const InsrBwdJob* jobs, int njobs, int din, in
     J.first[p.nf] = b;
     J.njobs = p.nf;
     const long P = insr_jet_partial_stride(din, dout, L, W);
-    if ((rc = bwd_q(fused_bwd_nq(p.nq, c.k), c.NT, c.S, c.lap, p.T, &J, din, dout, L, prm, work, P, st))) return rc;
-    if ((rc = insr_reduce_partials_strided(work, p.nb, insr_siren_param_count(din, dout, L, W), P, grad, acc, stream)))
-      return rc;
-    acc = 1;
+    return bwd_q(fused_bwd_nq(p.nq, c.k), c.NT, c.S, c.lap, p.T, &J, din, dout, L, prm, work, P, st);
   }
-  for (int q = 0; q < p.ns; ++q) {  // stream order: the previous job's reduction has read `work`
-    const InsrBwdJob& jb = jobs[p.solo[q]];
-    if ((rc = insr_siren_jet_bwd_grad(jb.x, jb.n, din, dout, L, W, mode, params, jb.act, jb.gy, jb.gdy, jb.glap, work,
-                                      grad, acc, stream)))
-      return rc;
-    acc = 1;
-  }
-  return 0;
 }
 
 long insr_jet_bwd_work_bytes(long n, int din, int dout, int L, int W, int mode) {
