@@ -166,7 +166,7 @@ int insr_siren_jet_fwd(const float* x, long n_points, int d_in, int d_out, int n
  * may differ per job (InsrJetJob.d_out: e.g. the velocity and pressure fields).
  * Replaces: consecutive MLP.forward calls (base/networks.py:67-71).
  */
-#define INSR_MAX_FWD_JOBS 4
+#define INSR_MAX_FWD_JOBS 6
 typedef struct InsrJetJob {
   const float* x;       /* (n, d_in) */
   const float* params;  /* flat parameters of this job's network */

@@ -780,6 +780,21 @@ def _supported(mlp, mode):
                                                mlp.kernel_width, mlp.call_mode(mode)))
 
 
+def _promote_to_grad(mlp):
+    """A value call of a network whose GRADIENT jet is already queued in the loop's deferred scope
+    (base/lower.py deferred_jets; the advection body's band call after its interior gradient jets,
+    advection/model.py:86-87) runs as a gradient jet too: its value is the jet's value stream (the same
+    bits), and both calls share one forward launch and one reverse launch (one job mode)."""
+    jobs = _Fused.pending
+    if not jobs or not _supported(mlp, nat.MODE_GRAD):
+        return False
+    from . import lower
+    if not lower.deferring():
+        return False
+    flat = mlp.flat_params()
+    return any(len(j) == 8 and j[1] is flat and (k[3] & nat.MODE_MASK) == nat.MODE_GRAD for k, j in jobs)
+
+
 def siren_value(mlp, x):
     """MLP.forward.  Provenance lives on the tensor AND on its autograd node, because
     in `q = mlp(x) + x` the value tensor itself is a dropped temporary; only the node
@@ -792,6 +807,8 @@ def siren_value(mlp, x):
         mode = _HintScope.hints.get(key, nat.MODE_VALUE)
         if mode != nat.MODE_VALUE and not (x.requires_grad and _supported(mlp, mode)):
             mode = nat.MODE_VALUE
+    if mode == nat.MODE_VALUE and _promote_to_grad(mlp):
+        mode = nat.MODE_GRAD
     res = run_jet(mlp, x, mode)
     y = res[0]
     jets = {} if mode == nat.MODE_VALUE else {mode: res}

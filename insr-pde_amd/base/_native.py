@@ -201,7 +201,7 @@ SIGNATURES = {
 }
 
 
-MAX_FWD_JOBS = 4  # INSR_MAX_FWD_JOBS
+MAX_FWD_JOBS = 6  # INSR_MAX_FWD_JOBS
 
 
 class JetJob(ctypes.Structure):

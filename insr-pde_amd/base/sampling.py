@@ -76,6 +76,9 @@ def _band(n, ranges, device):
 def sample_boundary(N, sdim, epsilon=1e-4, device='cpu'):
     """Random points in thin bands around the box faces (base/sampling.py:21-42)."""
     if sdim == 1:
+        if torch.device(device).type == "cuda":  # both bands in one device Philox launch
+            return _fused_bands(N // 2, [((-1 - epsilon, -1 + epsilon),), ((1 - epsilon, 1 + epsilon),)],
+                                ("box1", epsilon), device)
         left = (torch.rand(N // 2, 1, device=device) * 2 - 1) * epsilon - 1.
         right = (torch.rand(N // 2, 1, device=device) * 2 - 1) * epsilon + 1.
         return torch.cat([left, right], dim=0)

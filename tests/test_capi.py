@@ -157,7 +157,7 @@ def test_mixed_launch_rejects_malformed_jobs(lib):
         ([job(d_out=1)], [ADV]),                          # advect needs f: R^d -> R^d
         ([job(), job(x=P[4], y=P[6], dy=P[7], lap=P[8])], [ADV, V]),  # the foot is another job's input
         ([job()], [ADV], None),                           # advect without its (dt, lo, hi)
-        ([job()] * 5, [V] * 5),                           # more jobs than INSR_MAX_FWD_JOBS
+        ([job()] * 7, [V] * 7),                           # more jobs than INSR_MAX_FWD_JOBS (6)
         ([job(n=0x40000000), job(n=0x40000000, x=P[5])], [V, V]),  # total beyond int range
     ]
     for case in bad:

@@ -125,8 +125,8 @@ def test_multi_mixed_output_widths(B, mode):
 def test_multi_rejects_bad_arguments(B):
     lib, nat = B._native.lib(), B._native
     assert lib.insr_siren_jet_fwd_multi(None, 2, 2, 2, 4, 128, 0, None) == -1
-    arr = (nat.JetJob * 5)()
-    assert lib.insr_siren_jet_fwd_multi(arr, 5, 2, 2, 4, 128, 0, None) == -1  # > INSR_MAX_FWD_JOBS
+    arr = (nat.JetJob * (nat.MAX_FWD_JOBS + 1))()
+    assert lib.insr_siren_jet_fwd_multi(arr, nat.MAX_FWD_JOBS + 1, 2, 2, 4, 128, 0, None) == -1  # > INSR_MAX_FWD_JOBS
     assert lib.insr_siren_jet_fwd_multi(arr, 2, 2, 2, 4, 100, 0, None) == -1  # width
     assert lib.insr_siren_jet_fwd_multi(arr, 2, 2, 2, 4, 128, 0, None) == 0   # all jobs empty
     arr[0].n = 10  # a live job with NULL buffers

@@ -172,11 +172,12 @@ def test_reference_band_samplers_on_the_device(B):
         (lambda: B.sample_boundary2D_separate(4000, side="vertical", device="cuda"), [(full, lo), (full, hi)]),
         (lambda: B.sample_boundary(8000, 2, device="cuda"), [(full, lo), (full, hi), (lo, full), (hi, full)]),
         (lambda: B.sample_boundary2D_pair(4000, device="cuda"), [(lo, full), (hi, full), (full, lo), (full, hi)]),
+        (lambda: B.sample_boundary(4000, 1, device="cuda"), [(lo,), (hi,)]),  # advection/model.py:86
     ]
     for draw, faces in cases:
         a, b = draw(), draw()
         n = 2000
-        assert a.shape == (n * len(faces), 2) and a.is_cuda and a.dtype == torch.float32
+        assert a.shape == (n * len(faces), len(faces[0])) and a.is_cuda and a.dtype == torch.float32
         assert not torch.equal(a, b)
         for k, face in enumerate(faces):
             rows = a[k * n:(k + 1) * n].cpu().double()
