@@ -21,11 +21,14 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 GOLD = os.path.join(ROOT, "tests", "golden", "ref_phases.npz")
 
 
-def _worker(port, q):
+def _worker(port, q, plain=False):
     sys.path[:0] = [ROOT, os.path.join(ROOT, "insr-pde_amd")]
     import torch.distributed as dist
     from pde.config import make_config
-    from pde.fluid import Fluid2DModel
+    if plain:  # the reference bodies as written, lowered by the loop (base/lower.py)
+        from pde.fluid_plain import Fluid2DPlainModel as Fluid2DModel
+    else:
+        from pde.fluid import Fluid2DModel
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), LOCAL_RANK="0")
     torch.cuda.set_device(0)
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
@@ -33,10 +36,11 @@ def _worker(port, q):
     out = {}
     # single / split / captured without in-kernel loss seeds (base/losses.py lazy_losses): the three compute the
     # loss values in the same launches; "seeded" = captured with them (the default), against "captured"
-    for name, kw in (("single", dict(insr_dp_always=False, insr_seed_in_bwd=False)),
-                     ("split", dict(insr_dp_always=True, insr_dp_capture=False, insr_seed_in_bwd=False)),
-                     ("captured", dict(insr_dp_always=True, insr_dp_capture=True, insr_seed_in_bwd=False)),
-                     ("seeded", dict(insr_dp_always=True, insr_dp_capture=True))):
+    runs = (("single", dict(insr_dp_always=False, insr_seed_in_bwd=False)),
+            ("split", dict(insr_dp_always=True, insr_dp_capture=False, insr_seed_in_bwd=False)),
+            ("captured", dict(insr_dp_always=True, insr_dp_capture=True, insr_seed_in_bwd=False)),
+            ("seeded", dict(insr_dp_always=True, insr_dp_capture=True)))
+    for name, kw in (runs[:3] if plain else runs):
         torch.manual_seed(0)
         cfg = make_config("fluid", num_hidden_layers=4, hidden_features=128, sample_resolution=32, dt=0.05,
                           proj_dir="/tmp/insr_dp_capture_test", insr_progress=False, early_stop=False,
@@ -84,3 +88,27 @@ def test_captured_allreduce_equals_split_and_single_process():
     assert len(res["seeded"][2]) == len(res["captured"][2])
     for (t1, s1, m1, b1), (t2, s2, m2, b2) in zip(res["seeded"][2], res["captured"][2]):
         assert (t1, s1) == (t2, s2) and abs(m1 - m2) <= 1e-6 * abs(m2) and abs(b1 - b2) <= 1e-6 * abs(b2)
+
+
+def test_captured_allreduce_plain_bodies():
+    """The same three DP paths for the reference's fluid bodies as written (pde/fluid_plain.py: lowered losses,
+    deferred jets, multi-job reverse jets): DP code path == single process, parameters bit for bit."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_worker, args=(port, q, True))
+    p.start()
+    res = q.get(timeout=240)
+    p.join(timeout=60)
+    assert p.exitcode == 0
+    assert not res["single"][3] and res["split"][3] and res["captured"][3]
+    for name in ("split", "captured"):
+        assert np.array_equal(res[name][0], res["single"][0]), name
+        assert np.array_equal(res[name][1], res["single"][1]), name
+        assert len(res[name][2]) == len(res["single"][2]), name
+        for (t1, s1, m1, b1), (t2, s2, m2, b2) in zip(res[name][2], res["single"][2]):
+            assert (t1, s1) == (t2, s2) and abs(m1 - m2) <= 1e-6 * abs(m2) and abs(b1 - b2) <= 1e-6 * abs(b2)
