@@ -356,7 +356,9 @@ def roofline(loops, n_local, precision="fp32"):
         name = f"{k[0]}:{k[1]}:n{k[2]}:{k[4][0]}-{k[3]}x{k[4][2]}-{k[4][1]}"
         table[name] = round(table.get(name, 0.0) + v, 4)
     nq = PRECISION[precision][2]
-    kname, grid, x6, np_run = kernel_identity(kind, mode, n, din, dout, L, W, nq)
+    # the loss groups ride in the reverse jets (in-kernel seeds): the saved-stream backward's seeded instantiation
+    seeded = bool(loops and loops[0].m._lazy_losses_on())
+    kname, grid, x6, np_run = kernel_identity(kind, mode, n, din, dout, L, W, nq, seeded)
     traffic, tsrc = pmc_traffic(kname, grid)
     # peak = the dense matrix ceiling of the products the launch actually runs: its split kernels run NP
     # v_mfma_f32_16x16x32_{bf16,f16} (16 cyc, the ~2.5 PF dense rate) per fp32-level 16x16x32 MAC block
@@ -380,7 +382,7 @@ def roofline(loops, n_local, precision="fp32"):
     return out
 
 
-def kernel_identity(kind, mode, n, din, dout, L, W, nq=3):
+def kernel_identity(kind, mode, n, din, dout, L, W, nq=3, seeded=False):
     """The rocprof name and grid (threads) of the jet kernel the library picks for this launch, and
     the split products per fp32-equivalent MAC it runs (6 bf16x6, 3 f16x3 / bf16x3, 1 bf16).
     nq = 3 (the fp32-level precision): the forward runs f16x3 (template NQ = 4), the backward's
@@ -411,7 +413,8 @@ def kernel_identity(kind, mode, n, din, dout, L, W, nq=3):
         import ctypes
         thr = (ctypes.c_long * 3)()
         nat.check(lib.insr_jet_wide_launch_threads(n, din, dout, L, W, m_b, thr), "insr_jet_wide_launch_threads")
-        parts = [(f"insr::jet_fb_x6<{S}, {lap}, {L}, 1, true>", thr[0]), ("insr::reduce_dw_kernel", thr[1])]
+        parts = [(f"insr::jet_fb_x6<{S}, {lap}, {L}, 1, true{', true' if seeded else ''}>", thr[0]),
+                 ("insr::reduce_dw_kernel", thr[1])]
         return " + ".join(f"{k}|grid={g}" for k, g in parts) + " (resident-dW backward, f16x3: the reverse " \
             "sweep on the saved streams, dW in registers per CU, no adjoint round trip; then the dW / " \
             "compact-row sums; time = both launches)", parts, True, 3

@@ -49,6 +49,10 @@ for s in ${STEPS:-tests bench prof}; do
     profB) run profB 300 rocprofv3 --kernel-trace --stats -d "$PWD/$O/profB" -o run --output-format csv -- python bench.py --no-seed-in-bwd --steps 10 --warmup 3 --no-cpu-baseline ;;
     profshardB) run profshardB 300 rocprofv3 --kernel-trace --stats -d "$PWD/$O/profshardB" -o run --output-format csv -- python bench.py --config fluid2DtlgnM --shard-of 8 --no-seed-in-bwd --steps 10 --warmup 3 --no-cpu-baseline --no-roofline ;;
     profadvplain) run profadvplain 300 rocprofv3 --kernel-trace --stats -d "$PWD/$O/profadvplain" -o run --output-format csv -- python bench.py --api plain --config advect1D --steps 20 --warmup 3 --no-cpu-baseline --no-roofline ;;
+    pmc) PRX='jet_|dw_x6|reduce_'  # HBM bytes per dispatch (eager run): FETCH_SIZE, WRITE_SIZE and SQ in passes of their own
+         run pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$PRX" -d "$PWD/$O/pmc_fetch" -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-graph --no-cpu-baseline --no-roofline
+         run pmc_write 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$PRX" -d "$PWD/$O/pmc_write" -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-graph --no-cpu-baseline --no-roofline
+         run pmc_sq 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT --kernel-include-regex "$PRX" -d "$PWD/$O/pmc_sq" -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-graph --no-cpu-baseline --no-roofline ;;
     profplain) run profplain 300 rocprofv3 --kernel-trace --stats -d "$PWD/$O/profplain" -o run --output-format csv -- python bench.py --api plain --steps 10 --warmup 3 --no-cpu-baseline --no-roofline ;;
     profshard) run profshard 300 rocprofv3 --kernel-trace --stats -d "$PWD/$O/profshard" -o run --output-format csv -- python bench.py --config fluid2DtlgnM --shard-of 8 --steps 10 --warmup 3 --no-cpu-baseline --no-roofline ;;
     kbench) run kbench 400 python tools/kbench.py ${KARGS:---sizes 8192,16708,66844 --nets fluid_pres --modes lap --variants h3 --policies 0,2} ;;
