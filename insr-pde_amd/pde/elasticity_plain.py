@@ -1,0 +1,87 @@
+"""The elastodynamics phase written ONLY against the reference's public `base` API -- what an unchanged
+user model file (elasticity/model.py:127-189 and the energy helpers of elasticity/losses.py:6-39) runs on
+this package: q = f(x) + x, the Jacobian through `jacobian`, `torch.svd` of it, and every energy term as
+plain torch sums, the positional constraints through separate network calls.  None of the fused helpers of
+pde/elasticity.py (merged batches, the one-launch energy kernel).
+
+The training loop runs it under its loss lowering (base/lower.py) like any unchanged model file: none of
+these energies is a mean square, so every expression runs eagerly, exactly as written -- the point of this
+model is that the lowering and the deferred jets never change a result they do not recognise
+(tests/test_gpu_plain_api.py pins it to the reference's golden vectors), not speed.
+"""
+import torch
+
+from base import BaseModel, jacobian
+
+from .elasticity import ElasticityModel
+
+
+def _positional(q_fixed, target, ratio):
+    """ratio * sum |q_fixed - target|^2 (elasticity/losses.py:6-8)."""
+    return ratio * torch.sum((q_fixed - target) ** 2)
+
+
+def _collision_plane(q, qdot, dt, ratio, height):
+    """-dt sum qdot . f over the points below the plane y = height, f = ratio (0, .., height - q_y)
+    (elasticity/losses.py:10-20)."""
+    hit = q[:, -1] < height
+    if not bool(hit.any()):
+        return 0
+    depth = height - q[hit][:, -1]
+    force = ratio * torch.column_stack((torch.zeros(depth.shape[0], q.shape[1] - 1, device=q.device), depth))
+    return -dt * torch.sum(torch.mul(qdot[hit], force))
+
+
+def _collision_sphere(q, qdot, dt, ratio, center, radius):
+    """-dt sum qdot . f over the points inside the sphere, f = ratio * distance * direction from the centre
+    (elasticity/losses.py:22-39; the 3-d case keeps the reference's (n, 1, 1) broadcast)."""
+    vec = q - center
+    dist = torch.sqrt(torch.sum(vec ** 2, dim=1))
+    direction = vec / dist[:, None]
+    hit = dist < radius
+    if not bool(hit.any()):
+        return 0
+    d_in, dir_in = dist[hit], direction[hit]
+    force = ratio * (d_in[:, None] * dir_in if q.shape[1] == 2 else d_in[:, None, None] * dir_in)
+    return -dt * torch.sum(torch.mul(qdot[hit], force))
+
+
+class ElasticityPlainModel(ElasticityModel):
+    """ElasticityModel with the reference's phase body (same energies)."""
+    _insr_lower = True  # an unchanged model file: the loop's lowering scopes are open around its body
+
+    @BaseModel._training_loop
+    def _solve_deformation(self):
+        x = self._sample_in_training(self.sample_resolution)
+        fixed_l, fixed_r = self._sample_fixed_in_training(self.sample_resolution)
+        with torch.no_grad():
+            q_prev = self.deformation_field_prev(x) + x
+            q_pp = self.deformation_field_prev_prev(x) + x
+        q = self.deformation_field(x) + x
+        qdot = (q - q_prev) / self.dt
+        qdot_prev = (q_prev - q_pp) / self.dt
+        J, _ = jacobian(q, x)
+        _, S, _ = torch.svd(J)
+        terms = {
+            'arap': lambda: self.ratio_arap * torch.sum((S - 1.0) ** 2),
+            'volume': lambda: self.ratio_volume * torch.sum((torch.prod(S, dim=1) - 1) ** 2),
+            'kinematics': lambda: self.ratio_kinematics * torch.sum((qdot - qdot_prev) ** 2),
+            'external': lambda: (-self.dt * torch.sum(torch.mul(qdot, self.external_force.repeat(x.shape[0], 1)))
+                                 if self.timestep <= self.external_force_timesteps else 0),
+            'constraint': lambda: _positional(self.deformation_field(fixed_l), 0, self.ratio_constraint),
+            'constraint_right': lambda: _positional(self.deformation_field(fixed_r),
+                                                    self.constraint_offset_right.repeat(fixed_r.shape[0], 1),
+                                                    self.ratio_constraint),
+            'constraint_right_compress': lambda: _positional(self.deformation_field(fixed_r),
+                                                             -self.constraint_offset_right.repeat(fixed_r.shape[0], 1),
+                                                             self.ratio_constraint),
+            'collision': lambda: _collision_plane(q, qdot, self.dt, self.ratio_collide, self.plane_height),
+            'collision_sphere': lambda: _collision_sphere(q, qdot, self.dt, self.ratio_collide, self.circle_center,
+                                                          self.circle_radius),
+        }
+        loss = 0
+        for name in self.energy:  # added in cfg.energy order, as elasticity/model.py:150-183
+            if name not in terms:
+                raise NotImplementedError(name)
+            loss = loss + terms[name]()
+        return {'main': loss}

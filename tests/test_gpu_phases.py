@@ -420,3 +420,73 @@ def test_fused_sums_adam_bit_identical(ph, graph, policy):
             _jet.DEFER_REDUCE = True
     for a, b in zip(res[False], res[True]):
         assert np.array_equal(a, b)
+
+
+@pytest.mark.parametrize("dim", [2, 3])
+def test_plain_elasticity_body_through_lowering(ph, dim):
+    """The reference's elasticity body as written (pde/elasticity_plain.py: q = f(x) + x, jacobian, torch.svd,
+    torch energy sums, separate constraint calls) run the way the loop runs an unchanged model file -- inside
+    base.lower's lowering() + deferred_jets() scopes.  None of its energies is lowered (no mean squares): every
+    expression runs eagerly through the Lazy tensors' fallback, and the deferred jets are launched at the first
+    read.  Losses, gradients and two Adam + plateau iterations against the reference's golden vectors."""
+    from base import lower as LW
+    from pde.elasticity_plain import ElasticityPlainModel
+    if dim == 2:
+        g = ph
+        energy = [str(e) for e in g["el2d/cfg_energy"]]
+        cfg = _cfg("elasticity", num_hidden_layers=5, hidden_features=128, sample_resolution=16, dt=0.1, dim=2,
+                   energy=energy, ratio_constraint=1e4, ratio_volume=1e3, ratio_arap=1.0, ratio_collide=1e2,
+                   ratio_kinematics=1.0, external_force_timesteps=5, external_force_y=-1.0,
+                   constraint_right_offset_x=2.0, plane_height=-0.9)
+        pre = "el2d"
+    else:
+        g = dict(np.load(GOLD.replace("ref_phases.npz", "ref_phases_el3d.npz")))
+        energy = [str(e) for e in g["el3d/cfg_energy"]]
+        cfg = _cfg("elasticity", num_hidden_layers=2, hidden_features=64, sample_resolution=6, dt=0.1, dim=3,
+                   energy=energy, ratio_constraint=1e4, ratio_volume=1e3, ratio_arap=1e2, ratio_collide=1e3,
+                   ratio_kinematics=1.0, external_force_timesteps=5, external_force_x=0.0, external_force_y=0.0,
+                   external_force_z=-1e2, constraint_right_offset_x=0.0, plane_height=-0.5, collide_circle_x=0.0,
+                   collide_circle_y=-1.6, collide_circle_z=0.0, collide_circle_radius=1.0)
+        pre = "el3d"
+    model = ElasticityPlainModel(cfg)
+    model.timestep = 1
+    for k, n in (("f", model.deformation_field), ("f_prev", model.deformation_field_prev),
+                 ("f_pp", model.deformation_field_prev_prev)):
+        set_flat(n, g[f"{pre}/{k}/params0"])
+    T = lambda k: torch.from_numpy(g[k]).cuda()  # noqa: E731
+
+    def patch(it):
+        model._sample_in_training = lambda res: T(f"{pre}/x{it}").clone().requires_grad_(True)
+        if dim == 2:
+            model._sample_fixed_in_training = lambda res: (T(f"el2d/fixed_l{it}").clone().requires_grad_(True),
+                                                           T(f"el2d/fixed_r{it}").clone().requires_grad_(True))
+
+    body = ElasticityPlainModel._solve_deformation._insr_phase
+    assert model._lower_on() and model._defer_on()
+
+    def run():
+        with LW.lowering(model._lower_on()), LW.deferred_jets(model._defer_on()):
+            ld = body(model)
+        return LW.lower_losses(ld)
+
+    patch(0)
+    model._reset_optimizer()
+    ld = run()
+    ref = float(g[f"{pre}/_solve_deformation/loss_main"])
+    assert abs(float(ld["main"]) - ref) <= TOL * abs(ref), (float(ld["main"]), ref)
+    model.optimizer.zero_grad()
+    model._backward(ld)
+    assert nerr(flat_grad(model.deformation_field), g[f"{pre}/_solve_deformation/grad_f"]) < TOL
+    set_flat(model.deformation_field, g[f"{pre}/f/params0"])
+    model._reset_optimizer()
+    trace = []
+    owner = types.SimpleNamespace()
+    for it in range(2):
+        patch(it)
+        with _jet.call_scope(owner):
+            ld = run()
+        model._update_network(ld)
+        trace.append([float(ld[k]) for k in sorted(ld)])
+    assert nerr(np.array(trace), g[f"{pre}/_solve_deformation/loss_trace"]) < TOL
+    check_update(flat(model.deformation_field), g[f"{pre}/f/params0"], g[f"{pre}/_solve_deformation/f_after"],
+                 g[f"{pre}/_solve_deformation/grad_f"])
