@@ -157,8 +157,12 @@ class _Node:
         self.grad_mode = torch.is_grad_enabled()
 
 
-_META = {"__get__", "numel", "dim", "size", "__len__", "is_floating_point", "is_contiguous", "nelement",
-         "element_size", "ndimension", "get_device", "type"}
+_META = {"numel", "dim", "size", "__len__", "is_floating_point", "nelement", "element_size", "ndimension",
+         "get_device"}
+# properties a Lazy tensor answers from its own metadata; every other attribute (data, grad_fn, is_leaf,
+# grad, T, ...) is read off the materialised tensor
+_META_ATTRS = {"shape", "dtype", "device", "requires_grad", "is_cuda", "ndim", "layout", "is_sparse", "is_quantized",
+               "is_meta", "is_nested", "is_mkldnn", "is_complex"}
 
 
 class Lazy(torch.Tensor):
@@ -172,14 +176,15 @@ class Lazy(torch.Tensor):
         t._insr_node = node
         return t
 
-    def __repr__(self):
-        return f"Lazy({self._insr_node.kind}, shape={tuple(self.shape)})"
+    def __repr__(self):  # what eager code would print: the value
+        return repr(materialize(self))
 
     @classmethod
     def __torch_function__(cls, func, types, args=(), kwargs=None):
         kwargs = kwargs or {}
         name = getattr(func, "__name__", "")
-        if name in _META:
+        if name in _META or (name == "__get__" and getattr(getattr(func, "__self__", None), "__name__", "")
+                             in _META_ATTRS):
             with torch._C.DisableTorchFunctionSubclass():
                 return func(*args, **kwargs)
         r = _record(name, func, args, kwargs)
@@ -448,8 +453,11 @@ def materialize(t):
     launched first (their outputs are what the value reads)."""
     if not isinstance(t, Lazy):
         return t
+    n = getattr(t, "_insr_node", None)
+    if n is None:
+        raise RuntimeError("a storage-less Lazy tensor without its record (made by torch from a Lazy tensor "
+                           "below __torch_function__): base/lower.py cannot compute it")
     flush()
-    n = t._insr_node
     if not torch.is_grad_enabled() and n.real is None:
         if n.real_ng is None:
             n.real_ng = _axpy_clamp_fast(n)

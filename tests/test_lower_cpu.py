@@ -183,3 +183,17 @@ def test_detached_sum_of_views():
     assert torch.allclose(_eval_plan(p), ref, rtol=1e-6)
     g = torch.autograd.grad(_eval_plan(p), [lap])[0]
     assert torch.allclose(g, torch.autograd.grad(ref, [lap])[0], rtol=1e-5, atol=1e-9)
+
+
+def test_attributes_of_lazy_tensors():
+    """Only shape-like metadata is answered by the wrapper; data / grad_fn / is_leaf / T come from the real
+    tensor (materialised), so code that inspects autograd state or reads .data sees what eager code sees."""
+    u = _t(4, 2)
+    with LW.lowering():
+        (a,) = _leaves(u)
+        b = a * 2.0
+        assert isinstance(b, LW.Lazy)
+        assert b.shape == (4, 2) and b.requires_grad and b.layout == torch.strided
+        assert type(b.grad_fn).__name__ == "MulBackward0" and not b.is_leaf
+        assert torch.equal(b.data, (u * 2.0).data) and torch.equal(b.T, (u * 2.0).T)
+        assert a.is_leaf == u.is_leaf and a.grad_fn is u.grad_fn
