@@ -262,6 +262,14 @@ long insr_jet_bwd_multi_work_bytes(const long* n, int n_jobs, int d_in, int d_ou
  * merged call costs).  INSR_EINVAL when a job takes another path (use insr_siren_jet_bwd_grad_multi). */
 int insr_siren_jet_bwd_multi_rows(const InsrBwdJob* jobs, int n_jobs, int d_in, int d_out, int num_hidden,
                                   int width, int mode, const float* params, float* work, void* stream);
+/* The reverse jets of several calls of ONE network (the reference's interior + band calls of a Laplacian
+ * loss, fluid/model.py:111,119-120) as ONE launch of the saved-stream resident sweep (jet_fb.hpp) when that
+ * sweep serves the jobs' total point count: phase 1 of insr_siren_jet_bwd_grad_adam for all jobs at once.
+ * The per-CU partials land in `work` (insr_jet_bwd_work_bytes(16 * total tiles, ...)); phase 2 --
+ * insr_siren_jet_bwd_grad_adam(..., n_points = 16 * (total 16-point tiles), phases = 2, ...), with or
+ * without the Adam update -- sums them.  INSR_EINVAL when another path serves that total. */
+int insr_siren_jet_bwd_multi_sweep(const InsrBwdJob* jobs, int n_jobs, int d_in, int d_out, int num_hidden,
+                                   int width, int mode, const float* params, float* work, void* stream);
 /* 1 if insr_siren_jet_bwd_grad takes the wide path for this batch / width / mode. */
 int insr_jet_bwd_is_wide(long n_points, int d_in, int width, int mode);
 

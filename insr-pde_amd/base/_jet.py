@@ -467,12 +467,37 @@ def _launch_bwd_multi(jobs):
     gflat, accumulate = mlp.grad_for_backward()
     st = ctypes.c_void_p(cur.cuda_stream)
     mlp.grad_write_begin(cur)
-    if getattr(_Defer, "depth", 0) > 0 and len(jobs) <= nat.MAX_BWD_JOBS and all(j.act is not None for j in jobs):
-        # every job on the fused tile-split path: their partial rows now, the sums with the Adam launch
-        # (defer_reductions), as a single job's -- insr_siren_jet_bwd_multi_rows
+    defer = getattr(_Defer, "depth", 0) > 0
+    if len(jobs) <= nat.MAX_BWD_JOBS and all(j.act is not None for j in jobs):
         arr = (nat.BwdJob * len(jobs))(*[
             nat.BwdJob(j.x2.data_ptr(), nat.ptr(j.act), nat.ptr(j.gy), nat.ptr(j.gdy), nat.ptr(j.glap), j.x2.shape[0])
             for j in jobs])
+        # the saved-stream resident sweep serves the jobs' total (a Laplacian interior + its bands): ONE launch
+        # for all of them, the sums (phase 2) with the Adam launch -- insr_siren_jet_bwd_multi_sweep
+        tiles = sum((j.x2.shape[0] + 15) // 16 for j in jobs)
+        n_pass = 16 * tiles
+        if lib.insr_jet_bwd_kernel(n_pass, din, dout, L, W, cmode) == 1 and \
+                lib.insr_jet_bwd_path(n_pass, din, dout, L, W, cmode) == 2:
+            with torch.cuda.stream(cur):
+                work = torch.empty(max(lib.insr_jet_bwd_work_bytes(n_pass, din, dout, L, W, cmode) // 4, 1),
+                                   device=jobs[0].x2.device, dtype=torch.float32)
+            with _timed("bwd%d" % len(jobs), mode, n_pass, W, (din, dout, L)):
+                rc = lib.insr_siren_jet_bwd_multi_sweep(arr, len(jobs), din, dout, L, W, cmode,
+                                                        nat.ptr(mlp.flat_params()), nat.ptr(work), st)
+            if rc == 0:
+                pr = PendingSums("split", work, 0, 0, (mlp, jobs[0].x2, n_pass, cmode), gflat, accumulate, cur,
+                                 (mode, n_pass, W, (din, dout, L)))
+                if defer:
+                    mlp.set_pending_reduce(pr)
+                    _Defer.nets.append(mlp)
+                else:  # (the same sums now: deferred or not, the gradient is the same bits)
+                    pr.launch()
+                mlp.grad_write_end(cur)
+                return
+            if rc != -1:  # (INSR_EINVAL: not this path after all -- the calls below)
+                nat.check(rc, "insr_siren_jet_bwd_multi_sweep")
+        # every job on the fused tile-split path: their partial rows now, the sums with the Adam launch
+        # (defer_reductions), as a single job's -- insr_siren_jet_bwd_multi_rows
         ns = (ctypes.c_long * len(jobs))(*[j.x2.shape[0] for j in jobs])
         wb = lib.insr_jet_bwd_multi_work_bytes(ns, len(jobs), din, dout, L, W, cmode)
         if wb >= 0:
@@ -485,7 +510,7 @@ def _launch_bwd_multi(jobs):
                 stride = lib.insr_jet_partial_stride(din, dout, L, W)
                 pr = PendingSums("rows", work, nb, stride, mlp, gflat, accumulate, cur,
                                  (mode, int(sum(ns)), W, (din, dout, L)))
-                if 0 < nb < 1024:
+                if defer and 0 < nb < 1024:
                     mlp.set_pending_reduce(pr)
                     _Defer.nets.append(mlp)
                 elif nb > 0:
@@ -780,19 +805,25 @@ def _supported(mlp, mode):
                                                mlp.kernel_width, mlp.call_mode(mode)))
 
 
-def _promote_to_grad(mlp):
-    """A value call of a network whose GRADIENT jet is already queued in the loop's deferred scope
-    (base/lower.py deferred_jets; the advection body's band call after its interior gradient jets,
-    advection/model.py:86-87) runs as a gradient jet too: its value is the jet's value stream (the same
-    bits), and both calls share one forward launch and one reverse launch (one job mode)."""
+def _promoted(mlp, mode):
+    """The jet mode of a network call inside the loop's deferred scope (base/lower.py deferred_jets): a
+    call whose network already has a jet of a HIGHER mode queued (gradient over value, Laplacian over
+    gradient) runs in that mode too -- the advection body's band call after its interior gradient jets
+    (advection/model.py:86-87), the pressure bands' gradient calls after the interior Laplacian jet
+    (fluid/model.py:111,119-120).  Its outputs are the same bits (lower streams of a higher jet), and
+    the calls share one forward launch and one reverse launch."""
     jobs = _Fused.pending
-    if not jobs or not _supported(mlp, nat.MODE_GRAD):
-        return False
+    if not jobs or mode == nat.MODE_LAP:
+        return mode
     from . import lower
     if not lower.deferring():
-        return False
+        return mode
     flat = mlp.flat_params()
-    return any(len(j) == 8 and j[1] is flat and (k[3] & nat.MODE_MASK) == nat.MODE_GRAD for k, j in jobs)
+    top = max(((k[3] & nat.MODE_MASK) for k, j in jobs if len(j) == 8 and j[1] is flat
+               and (k[3] & nat.MODE_MASK) in (nat.MODE_GRAD, nat.MODE_LAP)), default=mode)
+    if top > mode and _supported(mlp, top) and not (top == nat.MODE_LAP and mlp.in_features > 2):
+        return top
+    return mode
 
 
 def siren_value(mlp, x):
@@ -807,8 +838,7 @@ def siren_value(mlp, x):
         mode = _HintScope.hints.get(key, nat.MODE_VALUE)
         if mode != nat.MODE_VALUE and not (x.requires_grad and _supported(mlp, mode)):
             mode = nat.MODE_VALUE
-    if mode == nat.MODE_VALUE and _promote_to_grad(mlp):
-        mode = nat.MODE_GRAD
+    mode = _promoted(mlp, mode)
     res = run_jet(mlp, x, mode)
     y = res[0]
     jets = {} if mode == nat.MODE_VALUE else {mode: res}

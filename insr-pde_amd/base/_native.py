@@ -151,6 +151,7 @@ SIGNATURES = {
     "insr_siren_jet_bwd_grad_multi": (_I, [_P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _I, _P]),
     "insr_jet_bwd_multi_work_bytes": (_L, [_P, _I, _I, _I, _I, _I, _I]),
     "insr_siren_jet_bwd_multi_rows": (_I, [_P, _I, _I, _I, _I, _I, _I, _P, _P, _P]),
+    "insr_siren_jet_bwd_multi_sweep": (_I, [_P, _I, _I, _I, _I, _I, _I, _P, _P, _P]),
     "insr_jet_bwd_is_wide": (_I, [_L, _I, _I, _I]),
     "insr_jet_bwd_path": (_I, [_L, _I, _I, _I, _I, _I]),
     "insr_jet_bwd_kernel": (_I, [_L, _I, _I, _I, _I, _I]),

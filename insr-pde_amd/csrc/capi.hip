@@ -1071,6 +1071,44 @@ int insr_siren_jet_bwd_multi_rows(const InsrBwdJob* jobs, int njobs, int din, in
   return p.nb;
 }
 
+int insr_siren_jet_bwd_multi_sweep(const InsrBwdJob* jobs, int njobs, int din, int dout, int L, int W, int mode,
+                                   const float* params, float* work, void* stream) {
+  if (!jobs || njobs < 1 || njobs > kBwdJobs || !shape_ok(din, dout, L, W, mode)) return INSR_EINVAL;
+  const JetCall c(din, W, mode);
+  long total = 0, tiles = 0;
+  for (int k = 0; k < njobs; ++k) {
+    if (jobs[k].n < 0 || jobs[k].n > 0x7fffffffL) return INSR_EINVAL;
+    if (jobs[k].n > 0 && (!jobs[k].x || !jobs[k].act)) return INSR_EINVAL;
+    total += jobs[k].n;
+    tiles += (jobs[k].n + 15) / 16;
+  }
+  // the saved-stream resident sweep must be the path of the jobs' total (jet_fb.hpp, f16x3)
+  if (total > 0x7fffffffL || c.recompute(L) || !(c.resident(total, L) && c.resident_f16(total, L))) return INSR_EINVAL;
+  if (tiles == 0) return 0;
+  if (!params || !work) return INSR_EINVAL;
+  hipStream_t st = (hipStream_t)stream;
+  int rc = 0;
+  const float* prm = params;
+  if (!(prm = with_planes(params, din, dout, L, W, mode, st, 0, &rc))) return rc;
+  FbJobs J{};
+  int m = 0, t = 0;
+  for (int k = 0; k < njobs; ++k) {
+    if (jobs[k].n <= 0) continue;
+    J.x[m] = jobs[k].x;
+    J.act[m] = jobs[k].act;
+    J.gy[m] = jobs[k].gy;
+    J.gdy[m] = jobs[k].gdy;
+    J.glap[m] = jobs[k].glap;
+    J.n[m] = (int)jobs[k].n;
+    J.tstart[m] = t;
+    t += (int)((jobs[k].n + 15) / 16);
+    ++m;
+  }
+  J.tstart[m] = t;
+  J.njobs = m;
+  return dispatch_fb_bwd(c.S, c.lap, L, J, din, dout, prm, work, nullptr, 0, 1, 1, AdamArgs{}, st);
+}
+
 // the multi plan's fused tile-split jobs in ONE jet_bwd_x6 launch: p.nb partial-gradient rows into work
 static int multi_fused_rows(const InsrBwdJob* jobs, const MultiPlan& p, int din, int dout, int L, int W, int mode,
                             const float* params, float* work, hipStream_t st) {
