@@ -114,6 +114,47 @@ def test_lap_interior_two_kernel_beside_fused_band_gradients(B):
         assert nerr(g, ga) < TOL, k
 
 
+def test_lap_jobs_in_one_saved_stream_sweep(B):
+    """Laplacian jets of one network on three point sets (an interior + two bands whose gradient streams
+    the loss reads -- the plain pressure body once its band calls share the interior jet's mode) whose
+    total takes the saved-stream resident sweep: ONE insr_siren_jet_bwd_multi_sweep launch + its sums,
+    with and without the sums held back for the Adam launch; = job by job and = the oracle."""
+    ref, net = pair(B, 2, 1, 4, 128, seed=12)
+    x, bx, by = pts(16384, 2, 21), pts(162, 2, 22), pts(162, 2, 23)
+    div = torch.randn(16384, 1, generator=torch.Generator().manual_seed(24))
+    lib, nat = B._native.lib(), B._native
+    mode = net.call_mode(nat.MODE_LAP)
+    assert lib.insr_jet_bwd_kernel(16384 + 2 * 176, 2, 1, 4, 128, mode) == 1  # the sweep serves the total
+
+    def loss_hip(x, bx, by, dv):
+        lap = B.laplace(net(x), x)
+        _, gbx = B.laplace(net(bx), bx, return_grad=True)
+        _, gby = B.laplace(net(by), by, return_grad=True)
+        return torch.mean((dv - lap) ** 2) + torch.mean(gbx[..., 0] ** 2) + torch.mean(gby[..., 1] ** 2)
+
+    xg = [t.cuda().requires_grad_(True) for t in (x, bx, by)]
+    g1 = run(B, net, lambda: loss_hip(*xg, div.cuda()), batched=False)
+    g2 = run(B, net, lambda: loss_hip(*xg, div.cuda()), batched=True)
+    for a, b in zip(g2, g1):
+        assert nerr(a, b) < TOL
+    net.zero_grad(set_to_none=True)
+    with B._jet.defer_reductions():  # (its exit lands the held-back sums)
+        with B._jet.batched_backward():
+            loss_hip(*xg, div.cuda()).backward()
+    torch.cuda.synchronize()
+    g3 = grads(net)
+    for a, b in zip(g3, g2):
+        assert torch.equal(a, b)  # held back or not: the same sums
+    lo = (lambda f, z: O.op_laplace(f(z), z))
+    xs = [t.requires_grad_(True) for t in (x, bx, by)]
+    l0 = torch.mean((div - lo(ref, xs[0])) ** 2) + torch.mean(O.op_gradient(ref(xs[1]), xs[1])[..., 0] ** 2) + \
+        torch.mean(O.op_gradient(ref(xs[2]), xs[2])[..., 1] ** 2)
+    l0.backward()
+    for (k, p), g in zip(ref.named_parameters(), g2):
+        ga = p.grad if p.grad is not None else torch.zeros_like(p)
+        assert nerr(g, ga) < TOL, k
+
+
 def test_more_jobs_than_one_launch(B):
     """11 band calls of one network: chunks of INSR_MAX_BWD_JOBS, gradients accumulated."""
     ref, net = pair(B, 2, 2, 4, 128, seed=5)
