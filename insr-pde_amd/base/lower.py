@@ -356,12 +356,12 @@ def _record(name, func, args, kwargs):
             return None
         x = args[0]
         return _lazy_of("sq", (x._insr_node,), call, x._insr_node.shape, like, _req(x))
-    if name == "mean" and len(args) == 1 and not kwargs and isinstance(args[0], Lazy):
+    if name in ("mean", "sum") and len(args) == 1 and not kwargs and isinstance(args[0], Lazy):
         x = args[0]
-        return _lazy_of("mean", (x._insr_node,), call, (), like, _req(x))
+        return _lazy_of(name, (x._insr_node,), call, (), like, _req(x))
     if name == "mse_loss" and len(args) == 2 and set(kwargs) <= {"reduction", "size_average", "reduce", "weight"} \
-            and kwargs.get("reduction", "mean") == "mean" and all(kwargs.get(k) is None for k in
-                                                                   ("size_average", "reduce", "weight")):
+            and kwargs.get("reduction", "mean") in ("mean", "sum") and all(kwargs.get(k) is None for k in
+                                                                             ("size_average", "reduce", "weight")):
         x, y = args
         nx, ny = _operand(x), _operand(y)
         if nx is None or ny is None or nx.shape != ny.shape:
@@ -369,7 +369,7 @@ def _record(name, func, args, kwargs):
         r = _req(x, y)
         d = _Node("lin", (nx, ny), coef=(1.0, -1.0), call=None, shape=nx.shape)
         s = _Node("sq", (d,), call=None, shape=nx.shape)
-        return _lazy_of("mean", (s,), call, (), like, r)
+        return _lazy_of(kwargs.get("reduction", "mean"), (s,), call, (), like, r)
     if name == "__getitem__" and len(args) == 2 and isinstance(args[0], Lazy):
         x, idx = args
         n = x._insr_node
@@ -468,9 +468,9 @@ def materialize(t):
 
 # ---- lowering of the loss dict ----------------------------------------------------------------
 def _ms_terms(n, w=1.0):
-    """n as [(w_i, E_i)] with n = sum_i w_i mean(E_i ** 2), or None."""
-    if n.kind == "mean" and n.kids[0].kind == "sq":
-        return [(w, n.kids[0].kids[0])]
+    """n as [(w_i, E_i, red_i)] with n = sum_i w_i red_i(E_i ** 2), red = 'mean' or 'sum', or None."""
+    if n.kind in ("mean", "sum") and n.kids[0].kind == "sq":
+        return [(w, n.kids[0].kids[0], n.kind)]
     if n.kind == "lin":
         out = []
         for c, kid in zip(n.coef, n.kids):
@@ -525,14 +525,17 @@ def _atom_tensor(a):
 
 def plan(n):
     """The fused form of loss node n, or None (eager):
-      ("combo", (a, b, c, d), (alpha, beta, gamma, delta), w): w mean((alpha (a + beta b) + gamma (c + delta d))^2)
+      ("combo", (a, b, c, d), (alpha, beta, gamma, delta), w, red): w red((alpha (a + beta b) + gamma (c + delta d))^2),
+                                                                   red = 'mean' or 'sum'
       ("bands2", (A, B), w):                                   w (mean(A[:, 0]^2) + mean(B[:, 1]^2))
     (a contiguous; b, c, d None or same-shape tensors / 1-D strided views; no launch is made here)."""
     terms = _ms_terms(n)
-    if not terms or any(w == 0.0 for w, _ in terms):
+    if not terms or any(w == 0.0 for w, _, _ in terms):
         return None
     if len(terms) == 2:  # w (mean(A[..., 0]^2) + mean(B[..., 1]^2)): one BANDS term over two tensors
-        (w0, e0), (w1, e1) = terms
+        (w0, e0, r0), (w1, e1, r1) = terms
+        if r0 != "mean" or r1 != "mean":
+            return None
         at = [_atoms(e) for e in (e0, e1)]
         if w0 != w1 or any(a is None or len(a) != 1 for a in at):
             return None
@@ -550,7 +553,7 @@ def plan(n):
         return ("bands2", (A, B), w0)
     if len(terms) != 1:
         return None
-    (w, e), = terms
+    (w, e, red), = terms
     at = _atoms(e)
     if at is None or not 1 <= len(at) <= 4:
         return None
@@ -570,7 +573,7 @@ def plan(n):
     (c1, a), (c2, b), (c3, c), (c4, d) = ops
     alpha, beta = c1, (c2 / c1 if b is not None else -1.0)
     gamma, delta = (1.0, 1.0) if c is None else (c3, (c4 / c3 if d is not None else 1.0))
-    return ("combo", (a, b, c, d), (alpha, beta, gamma, delta), w)
+    return ("combo", (a, b, c, d), (alpha, beta, gamma, delta), w, red)
 
 
 def _spec(n):
@@ -582,9 +585,9 @@ def _spec(n):
     if p[0] == "bands2":
         (A, B), w = p[1], p[2]
         return L.wall_term2(A, B, weight=w)
-    (a, b, c, d), (alpha, beta, gamma, delta), w = p[1], p[2], p[3]
-    # w mean(r^2): the loss's scale is w / count (w = 1 for the reference's losses; * 1.0 is exact)
-    return L.mse_term(a, b, c, d, alpha=alpha, beta=beta, gamma=gamma, delta=delta, weight=w)
+    (a, b, c, d), (alpha, beta, gamma, delta), w, red = p[1], p[2], p[3], p[4]
+    # w mean(r^2): the loss's scale is w / count (w = 1 for the reference's losses; * 1.0 is exact); w sum(r^2): w
+    return L.mse_term(a, b, c, d, alpha=alpha, beta=beta, gamma=gamma, delta=delta, reduction=red, weight=w)
 
 
 def lower_losses(loss_dict):

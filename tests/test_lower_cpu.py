@@ -21,13 +21,13 @@ def _eval_plan(p):
     if p[0] == "bands2":
         (A, B), w = p[1], p[2]
         return w * ((A[:, 0] ** 2).mean() + (B[:, 1] ** 2).mean())
-    (a, b, c, d), (al, be, ga, de), w = p[1], p[2], p[3]
+    (a, b, c, d), (al, be, ga, de), w, red = p[1], p[2], p[3], p[4]
     r = a if b is None else a + be * b
     r = al * r
     if c is not None:
         q = c if d is None else c + de * d
         r = r + ga * q
-    return w * (r ** 2).mean()
+    return w * ((r ** 2).mean() if red == "mean" else (r ** 2).sum())
 
 
 def _leaves(*ts):
@@ -197,3 +197,16 @@ def test_attributes_of_lazy_tensors():
         assert type(b.grad_fn).__name__ == "MulBackward0" and not b.is_leaf
         assert torch.equal(b.data, (u * 2.0).data) and torch.equal(b.T, (u * 2.0).T)
         assert a.is_leaf == u.is_leaf and a.grad_fn is u.grad_fn
+
+
+def test_sum_of_squares_losses():
+    """ratio * torch.sum((q - target) ** 2) (elasticity/losses.py:6-8 style) and F.mse_loss(..., reduction='sum'):
+    one COMBO term with reduction 'sum'."""
+    q, tgt = _t(32, 2, seed=18), _t(32, 2, grad=False, seed=19)
+    _check(lambda q, t: 1e4 * torch.sum((q - t) ** 2), [q, tgt], "combo")
+    _check(lambda q, t: (q - t).pow(2).sum() * 0.5, [q, tgt], "combo")
+    _check(lambda q, t: F.mse_loss(q, t, reduction="sum"), [q, tgt], "combo")
+    with LW.lowering():
+        a, b = _leaves(q, tgt)
+        mixed = torch.sum((a - b) ** 2) + torch.mean(a[..., 0] ** 2)  # two reductions: eager
+    assert LW.plan(mixed._insr_node) is None
