@@ -216,3 +216,48 @@ def test_deferred_jets_share_launches(ph, monkeypatch):
             assert launched == [], launched
     for k in out[False]:
         assert abs(out[True][k] - out[False][k]) <= 1e-6 * abs(out[False][k]) + 1e-12, (k, out)
+
+
+@pytest.mark.parametrize("kind", ["mean", "sum", "mse_sum", "weighted_mean", "walls"])
+def test_lowered_loss_equals_eager(kind):
+    """Each loss form the lowering recognises, on real jet outputs: the fused group's value and the network's
+    parameter gradients equal the same expression run eagerly (the materialised Lazy loss) -- values 1e-6,
+    gradients 1e-5 normwise (another fp32 summation order)."""
+    import torch.nn.functional as F
+    import base
+    from base import lower as LW
+    torch.manual_seed(7)
+    net = base.MLP(2, 2, 4, 128, nonlinearity="sine").cuda()
+    g = torch.Generator(device="cuda").manual_seed(8)
+    x = (torch.rand(3000, 2, device="cuda", generator=g) * 2 - 1).requires_grad_(True)
+    bx = (torch.rand(81, 2, device="cuda", generator=g) * 2 - 1).requires_grad_(True)
+    tgt = torch.randn(3000, 2, device="cuda", generator=g)
+    forms = {
+        "mean": lambda u, ub: torch.mean((u - tgt) ** 2),
+        "sum": lambda u, ub: 1e2 * torch.sum((u - tgt) ** 2),
+        "mse_sum": lambda u, ub: F.mse_loss(u, tgt, reduction="sum"),
+        "weighted_mean": lambda u, ub: 0.25 * torch.mean((2.0 * u - tgt) ** 2),
+        "walls": lambda u, ub: (torch.mean(ub[..., 0] ** 2) + torch.mean(u[:81][..., 1] ** 2)) * 1.0,
+    }
+    out = {}
+    for lowered in (False, True):
+        net.zero_grad(set_to_none=True)
+        with LW.lowering():
+            u, ub = net(x), net(bx)
+            if kind == "walls":  # two band tensors of the same shape
+                ub, u = net(bx), net(bx[:81] * 0.5)
+                loss = (torch.mean(ub[..., 0] ** 2) + torch.mean(u[..., 1] ** 2)) * 1.0
+            else:
+                loss = forms[kind](u, ub)
+        assert isinstance(loss, LW.Lazy)
+        if lowered:
+            c0 = LW.LOWERED["terms"]
+            loss = LW.lower_losses({"main": loss})["main"]
+            assert LW.LOWERED["terms"] == c0 + 1
+        else:
+            loss = LW.materialize(loss)
+        loss.backward()
+        torch.cuda.synchronize()
+        out[lowered] = (float(loss), net.flat_grad_buffer().detach().clone())
+    assert abs(out[True][0] - out[False][0]) <= 1e-6 * abs(out[False][0]), out
+    assert nerr(out[True][1].cpu().numpy(), out[False][1].cpu().numpy()) < 1e-5
