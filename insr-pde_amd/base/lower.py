@@ -17,7 +17,8 @@ and ordinary tensors and maps it onto the fused loss group (base/losses.py):
 
 so that every loss of the iteration is ONE insr_sq_loss_group launch whose unit-seeded backward
 costs nothing.  The semi-Lagrangian foot clamp(x - dt u, lo, hi) a no-grad jet consumes is one
-insr_axpy_clamp launch.
+insr_axpy_clamp launch.  Inside `deferred_jets()` (opened with it) the body's network / diff-op calls
+are queued and launched together at the first read of a value (below).
 
 Anything else is EAGER, exactly as written: an op the recorder does not know, or any use of a
 Lazy tensor's value (float(), .cpu(), an unsupported torch function, a network input, ...),
@@ -198,10 +199,6 @@ class Lazy(torch.Tensor):
         return func(*_real_tree(args), **_real_tree(kwargs or {}))
 
 
-def _node(t):
-    return t._insr_node if isinstance(t, Lazy) else None
-
-
 def _wrap(node, like_dtype, like_device, requires_grad):
     return Lazy(node, like_dtype, like_device, requires_grad)
 
@@ -235,8 +232,8 @@ def api(fn, operand_first=False):
 
     @functools.wraps(fn)
     def w(*args, **kwargs):
-        if len(args) == 2 and not kwargs and isinstance(args[1], Lazy) and deferring() and \
-                not torch.is_grad_enabled():
+        if not operand_first and len(args) == 2 and not kwargs and isinstance(args[1], Lazy) and deferring() \
+                and not torch.is_grad_enabled():  # a network call at the advection foot
             r = _advect_target(args[0], args[1])
             if r is not None:
                 return leaf(r)
