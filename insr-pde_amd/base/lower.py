@@ -42,6 +42,7 @@ LOWERED = {"groups": 0, "terms": 0, "eager_losses": 0, "materialized": 0}  # cou
 class _State(threading.local):
     depth = 0
     defer = 0  # > 0: network / diff-op jets are queued (a fused_forwards scope) and launched at the first read
+    nodes = None  # the recorded nodes of the open scope (evaluated before an in-place op, see _pin_all)
 
 
 _S = _State()
@@ -61,6 +62,8 @@ class lowering:
     def __exit__(self, *exc):
         if self.on:
             _S.depth -= 1
+            if _S.depth == 0:
+                _S.nodes = None
         return False
 
 
@@ -142,6 +145,7 @@ def add_views(a, b):
     n = _Node("lin", (_Node("leaf", real=a, shape=tuple(a.shape)), _Node("leaf", real=b, shape=tuple(b.shape))),
               coef=(1.0, 1.0), call=(torch.add, (a, b), {}), shape=tuple(a.shape))
     n.grad_mode = torch.is_grad_enabled()
+    _register(n)
     return _wrap(n, a.dtype, a.device, torch.is_grad_enabled() and (a.requires_grad or b.requires_grad))
 
 
@@ -149,13 +153,64 @@ def add_views(a, b):
 # node kinds: 'leaf' (a real tensor), 'lin' (sum of coefficient x node), 'sq' (x ** 2), 'mean' (all
 # elements), 'sel' (x[..., k] of a 2-D x), 'detach', 'clamp' (scalar bounds).  Every node keeps the
 # torch call that made it (func, args, kwargs, grad mode): materialisation replays exactly that.
+#
+# In-place writes.  A recorded expression is evaluated later than eager code would evaluate it, so a
+# tensor it reads must not change in between.  An in-place op on a Lazy tensor (add_, __setitem__,
+# out=, ...) first evaluates every node recorded so far in the scope (_pin_all: their values are the
+# ones eager code computed before the write), then writes the real tensor, and the Lazy tensor stands
+# for the written tensor from then on.  Every leaf keeps its tensor's version counter: a loss whose
+# leaves were written since they were recorded is not lowered (its cached / replayed values are used),
+# and a replay that would read a tensor written behind the recorder's back (an in-place op on a plain
+# tensor a recorded expression reads) raises instead of computing with the new values.
 class _Node:
-    __slots__ = ("kind", "kids", "coef", "k", "lo", "hi", "real", "real_ng", "call", "shape", "grad_mode")
+    __slots__ = ("kind", "kids", "coef", "k", "lo", "hi", "real", "real_ng", "call", "shape", "grad_mode", "ver")
 
     def __init__(self, kind, kids=(), coef=None, k=None, lo=None, hi=None, real=None, call=None, shape=None):
         self.kind, self.kids, self.coef, self.k, self.lo, self.hi = kind, tuple(kids), coef, k, lo, hi
         self.real, self.real_ng, self.call, self.shape = real, None, call, shape
         self.grad_mode = torch.is_grad_enabled()
+        self.ver = real._version if real is not None else None
+
+
+def _register(n):
+    if _S.depth > 0:
+        if _S.nodes is None:
+            _S.nodes = []
+        _S.nodes.append(n)
+
+
+def _stale(n, through=True, seen=None):
+    """Whether a leaf under n was written since it was recorded.  through=False stops at evaluated nodes
+    (a replay reads their cached values); through=True looks through them (a plan reads the leaves)."""
+    seen = set() if seen is None else seen
+    if id(n) in seen:
+        return False
+    seen.add(id(n))
+    if n.kind == "leaf":
+        return n.real._version != n.ver
+    if not through and n.real is not None:
+        return False
+    return any(_stale(k, through, seen) for k in n.kids)
+
+
+def _mutated(name, args, kwargs):
+    """The tensors an op writes in place (empty for a functional op)."""
+    out = []
+    if "out" in kwargs:
+        o = kwargs["out"]
+        out.extend(o if isinstance(o, (list, tuple)) else [o])
+    if args and (name == "__setitem__" or (name.startswith("__i") and name.endswith("__")) or
+                 (name.endswith("_") and not name.startswith("_") and name != "requires_grad_")):
+        out.append(args[0])
+    return [t for t in out if isinstance(t, torch.Tensor)]
+
+
+def _pin_all():
+    """Evaluate every node recorded in the open scope that is not evaluated yet (before an in-place op)."""
+    flush()  # (a node may read a queued jet's output directly, e.g. add_views)
+    for n in list(_S.nodes or ()):
+        if n.real is None and n.call is not None:
+            _eval(n)
 
 
 _META = {"numel", "dim", "size", "__len__", "is_floating_point", "nelement", "element_size", "ndimension",
@@ -188,6 +243,14 @@ class Lazy(torch.Tensor):
                              in _META_ATTRS):
             with torch._C.DisableTorchFunctionSubclass():
                 return func(*args, **kwargs)
+        written = [t for t in _mutated(name, args, kwargs) if isinstance(t, Lazy)]
+        if written:
+            _pin_all()
+            r = func(*_real_tree(args), **_real_tree(kwargs))
+            for t in written:  # the Lazy tensor now stands for its written real tensor
+                real = materialize(t)
+                t._insr_node = _Node("leaf", real=real, shape=tuple(real.shape))
+            return r
         r = _record(name, func, args, kwargs)
         if r is not None:
             return r
@@ -312,6 +375,7 @@ def _req(*vals):
 
 def _lazy_of(kind, kids, call, shape, like, req, **kw):
     n = _Node(kind, kids, call=call, shape=tuple(shape), **kw)
+    _register(n)
     return _wrap(n, like.dtype, like.device, req)
 
 
@@ -416,6 +480,10 @@ def _eval(n):
         return n.real
     if n.call is None:  # an internal node (F.mse_loss's parts): evaluated by the enclosing call
         raise RuntimeError("internal lazy node has no call of its own")
+    if _stale(n, through=False):
+        raise RuntimeError("base/lower.py: a tensor read by a recorded expression was written in place after "
+                           "the expression was recorded (an in-place op on a plain tensor); evaluating it now "
+                           "would read the new values. Run this model unlowered (cfg.insr_lower = False).")
     func, args, kwargs = n.call
     a, k = _real_tree(args), _real_tree(kwargs)
     with torch.set_grad_enabled(n.grad_mode):
@@ -526,6 +594,8 @@ def plan(n):
                                                                    red = 'mean' or 'sum'
       ("bands2", (A, B), w):                                   w (mean(A[:, 0]^2) + mean(B[:, 1]^2))
     (a contiguous; b, c, d None or same-shape tensors / 1-D strided views; no launch is made here)."""
+    if _stale(n):  # a leaf written since it was recorded: the recorded values are the cached ones (eager)
+        return None
     terms = _ms_terms(n)
     if not terms or any(w == 0.0 for w, _, _ in terms):
         return None

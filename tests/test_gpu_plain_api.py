@@ -261,3 +261,39 @@ def test_lowered_loss_equals_eager(kind):
         out[lowered] = (float(loss), net.flat_grad_buffer().detach().clone())
     assert abs(out[True][0] - out[False][0]) <= 1e-6 * abs(out[False][0]), out
     assert nerr(out[True][1].cpu().numpy(), out[False][1].cpu().numpy()) < 1e-5
+
+
+def test_in_place_write_under_deferred_jets():
+    """An in-place write inside the deferred scope, on a tensor made from a queued jet's output: the queue is
+    launched and every expression recorded before the write evaluated first (eager order); the losses and the
+    network's parameter gradients equal the same body run without the lowering."""
+    import base
+    from base import lower as LW
+    torch.manual_seed(9)
+    net = base.MLP(2, 2, 4, 128, nonlinearity="sine").cuda()
+    g = torch.Generator(device="cuda").manual_seed(10)
+    x = (torch.rand(2000, 2, device="cuda", generator=g) * 2 - 1).requires_grad_(True)
+    tgt = torch.randn(2000, 2, device="cuda", generator=g)
+
+    def body():
+        u = net(x)
+        d = u - tgt
+        v = u * 1.0
+        v.add_(0.25)  # d was recorded before the write, v ** 2 after it
+        return {"a": torch.mean(d ** 2), "b": torch.mean(v ** 2)}
+
+    out = {}
+    for lowered in (False, True):
+        net.zero_grad(set_to_none=True)
+        if lowered:
+            with LW.lowering(), LW.deferred_jets():
+                ld = body()
+            ld = LW.lower_losses(ld)
+        else:
+            ld = body()
+        sum(ld.values()).backward()
+        torch.cuda.synchronize()
+        out[lowered] = ({k: float(v) for k, v in ld.items()}, net.flat_grad_buffer().detach().clone())
+    for k in ("a", "b"):
+        assert abs(out[True][0][k] - out[False][0][k]) <= 1e-6 * abs(out[False][0][k]), (k, out)
+    assert nerr(out[True][1].cpu().numpy(), out[False][1].cpu().numpy()) < 1e-5

@@ -210,3 +210,54 @@ def test_sum_of_squares_losses():
         a, b = _leaves(q, tgt)
         mixed = torch.sum((a - b) ** 2) + torch.mean(a[..., 0] ** 2)  # two reductions: eager
     assert LW.plan(mixed._insr_node) is None
+
+
+def test_in_place_write_on_a_lazy_tensor():
+    """An in-place op on a Lazy tensor evaluates what was recorded before it (eager order): d = u - t read
+    before u.add_(1) keeps the old u, u ** 2 after it reads the new one; value and gradients = eager."""
+    base, t = _t(16, 2, seed=20), _t(16, 2, grad=False, seed=21)
+
+    def body(u, t):
+        d = u - t
+        u.add_(1.0)
+        u[:, 1] = 0.5 * u[:, 1].detach()
+        return torch.mean(d ** 2), torch.mean(u ** 2)
+
+    ref1, ref2 = body(base * 1.0, t)
+    g_ref = torch.autograd.grad(ref1 + ref2, [base])[0]
+    with LW.lowering():
+        (a,) = _leaves(base * 1.0)
+        l1, l2 = body(a, t)
+    assert LW.plan(l1._insr_node) is None  # reads the old u: eager (its value was computed before the write)
+    p2 = LW.plan(l2._insr_node)
+    assert p2 is not None and p2[0] == "combo"
+    m1, m2 = LW.materialize(l1), _eval_plan(p2)
+    assert torch.equal(m1, ref1) and torch.allclose(m2, ref2, rtol=1e-6)
+    g = torch.autograd.grad(m1 + m2, [base])[0]
+    assert torch.allclose(g, g_ref, rtol=1e-5, atol=1e-9)
+
+
+def test_plain_tensor_written_behind_the_recorder():
+    """A plain tensor a recorded expression reads, written in place before the expression is evaluated: the
+    replay raises instead of reading the new values, and the loss is not lowered."""
+    u, t = _t(8, 2, seed=22), _t(8, 2, grad=False, seed=23)
+    with LW.lowering():
+        (a,) = _leaves(u)
+        d = a - t
+        loss = torch.mean(d ** 2)
+        t.zero_()
+    assert LW.plan(loss._insr_node) is None
+    with pytest.raises(RuntimeError, match="written in place"):
+        LW.materialize(loss)
+
+
+def test_requires_grad_is_not_a_write():
+    """requires_grad_ changes no values: nothing else recorded is evaluated and the tensor keeps its record."""
+    u = _t(8, 2, seed=24)
+    with LW.lowering():
+        (a,) = _leaves(u)
+        e = a * 3.0
+        d = a * 2.0
+        node = d._insr_node
+        d.requires_grad_(True)
+        assert e._insr_node.real is None and d._insr_node is node
