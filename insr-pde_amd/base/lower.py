@@ -193,13 +193,17 @@ def _stale(n, through=True, seen=None):
     return any(_stale(k, through, seen) for k in n.kids)
 
 
+_INPLACE_DUNDER = frozenset("__%s__" % n for n in ("setitem", "iadd", "isub", "imul", "itruediv", "ifloordiv", "imod",
+                                                  "ipow", "iand", "ior", "ixor", "ilshift", "irshift", "imatmul"))
+
+
 def _mutated(name, args, kwargs):
     """The tensors an op writes in place (empty for a functional op)."""
     out = []
     if "out" in kwargs:
         o = kwargs["out"]
         out.extend(o if isinstance(o, (list, tuple)) else [o])
-    if args and (name == "__setitem__" or (name.startswith("__i") and name.endswith("__")) or
+    if args and (name in _INPLACE_DUNDER or
                  (name.endswith("_") and not name.startswith("_") and name != "requires_grad_")):
         out.append(args[0])
     return [t for t in out if isinstance(t, torch.Tensor)]
@@ -250,6 +254,8 @@ class Lazy(torch.Tensor):
             for t in written:  # the Lazy tensor now stands for its written real tensor
                 real = materialize(t)
                 t._insr_node = _Node("leaf", real=real, shape=tuple(real.shape))
+                if r is real:  # u.add_(1) / u += 1 return u itself, as in eager code
+                    r = t
             return r
         r = _record(name, func, args, kwargs)
         if r is not None:

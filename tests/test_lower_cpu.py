@@ -261,3 +261,25 @@ def test_requires_grad_is_not_a_write():
         node = d._insr_node
         d.requires_grad_(True)
         assert e._insr_node.real is None and d._insr_node is node
+
+
+def test_augmented_assignment_is_a_write():
+    """u += 1 / u *= 2 on a Lazy tensor (Tensor.__iadd__ / __imul__): writes, in eager order; int() / iter()
+    are reads (nothing else recorded is evaluated)."""
+    base, t = _t(8, 2, seed=25), _t(8, 2, grad=False, seed=26)
+
+    def body(u, t):
+        d = u - t
+        u += 1.0
+        u *= 2.0
+        return torch.mean(d ** 2) + torch.mean(u ** 2)
+
+    ref = body(base * 1.0, t)
+    with LW.lowering():
+        (a,) = _leaves(base * 1.0)
+        lz = body(a, t)
+        e = a * 3.0
+        rows = [r for r in lz.reshape(1)]
+        assert e._insr_node.real is None and len(rows) == 1
+        assert a.mul_(1.0) is a and isinstance(a, LW.Lazy)
+    assert torch.allclose(LW.materialize(lz), ref, rtol=1e-6)
