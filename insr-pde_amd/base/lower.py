@@ -247,11 +247,13 @@ class Lazy(torch.Tensor):
                              in _META_ATTRS):
             with torch._C.DisableTorchFunctionSubclass():
                 return func(*args, **kwargs)
-        written = [t for t in _mutated(name, args, kwargs) if isinstance(t, Lazy)]
-        if written:
+        written = _mutated(name, args, kwargs)
+        if written:  # (a plain tensor written with a Lazy operand, x[:, 0] = u, may be read by a record too)
             _pin_all()
             r = func(*_real_tree(args), **_real_tree(kwargs))
-            for t in written:  # the Lazy tensor now stands for its written real tensor
+            for t in written:  # a written Lazy tensor now stands for its written real tensor
+                if not isinstance(t, Lazy):
+                    continue
                 real = materialize(t)
                 t._insr_node = _Node("leaf", real=real, shape=tuple(real.shape))
                 if r is real:  # u.add_(1) / u += 1 return u itself, as in eager code

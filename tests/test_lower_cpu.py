@@ -283,3 +283,20 @@ def test_augmented_assignment_is_a_write():
         assert e._insr_node.real is None and len(rows) == 1
         assert a.mul_(1.0) is a and isinstance(a, LW.Lazy)
     assert torch.allclose(LW.materialize(lz), ref, rtol=1e-6)
+
+
+def test_plain_tensor_written_with_a_lazy_value():
+    """x[:, 0] = u[:, 1] (a plain tensor written from a Lazy one) after d = x - u was recorded: d keeps the
+    old x, as in eager code."""
+    base, x0 = _t(8, 2, seed=27), _t(8, 2, grad=False, seed=28)
+
+    def body(u, x):
+        d = x - u
+        x[:, 0] = u[:, 1].detach()
+        return torch.mean(d ** 2) + torch.mean((x - u) ** 2)
+
+    ref = body(base * 1.0, x0.clone())
+    with LW.lowering():
+        (a,) = _leaves(base * 1.0)
+        lz = body(a, x0.clone())
+    assert torch.allclose(LW.materialize(lz), ref, rtol=1e-6)
