@@ -6,6 +6,8 @@ tests/test_oracle_golden.py) on the SAME points:
   * fluid2DtlgnM  the same at 256^2 = 65,536 + 2 x 654
   * elasticity2Dstretch  _solve_deformation at 20,000 points (SIREN 5x128) + 2 x 200 fixed
   * advect1D     _advect at 4,096 interior + 2 x 20 band points (SIREN 3x64)
+  * the reference's own bodies (pde/fluid_plain.py, pde/advection_plain.py) at the fluid2Dtlgn and advect1D
+    sizes, through the training loop's loss lowering and deferred jets (the drop-in path)
 
 The GPU runs the product path exactly as bench.py does -- device sampler into the merged
 [interior; bands] buffer (fluid) / the persistent box batch (elasticity), mixed launches,
@@ -90,13 +92,17 @@ def check_update(net, ref, p0, lr):
 
 
 # ---------------------------------------------------------------------------------------------
-def _fluid(B, config, hooks, **over):
+def _fluid(B, config, hooks, plain=False, **over):
     from pde.config import baseline_config
     from pde.fluid import Fluid2DModel
+    from pde.fluid_plain import Fluid2DPlainModel
     import pde.fluid as fl
+    import pde.fluid_plain as fp
+    from base import lower as LW
     cfg = baseline_config(config, proj_dir="/tmp/insr_fullsize_phases", insr_progress=False, early_stop=False,
                           max_n_iters=1, insr_graph=False, insr_sync_every=1, **over)
-    m = Fluid2DModel(cfg)
+    cls = Fluid2DPlainModel if plain else Fluid2DModel
+    m = cls(cfg)
     m.timestep = 1
     refs = {"vel": seeded(2, 2, 4, 128, 201), "vel_prev": seeded(2, 2, 4, 128, 202), "pres": seeded(2, 1, 4, 128, 203)}
     nets = {"vel": m.velocity_field, "vel_prev": m.velocity_field_prev, "pres": m.pressure_field}
@@ -111,6 +117,10 @@ def _fluid(B, config, hooks, **over):
         m._sample_in_training = lambda: x.cuda().requires_grad_(True)
         m._boundary_pair = lambda n: (bx.cuda().requires_grad_(True), by.cuda().requires_grad_(True))
         drawn["pts"] = (x, bx, by)
+        if plain:  # the reference bodies' separate band samplers (x-faces, then y-faces)
+            orig_sep = fp.sample_boundary2D_separate
+            fp.sample_boundary2D_separate = lambda n, side, device=None: (bx if side == "horizontal" else by).cuda()
+            drawn["restore"] = lambda: setattr(fp, "sample_boundary2D_separate", orig_sep)
     else:  # the product sampler: record the merged buffer it draws
         orig = fl.sample_random_and_bands2D
 
@@ -133,7 +143,13 @@ def _fluid(B, config, hooks, **over):
                 load(nets[k], refs[k])
             p0 = {k: O.flat_params(refs[k]).numpy().copy() for k in ("vel", "pres")}
             m._reset_optimizer()
-            ld = getattr(Fluid2DModel, phase)._insr_phase(m)
+            body = getattr(cls, phase)._insr_phase
+            if plain:  # as the training loop runs an unchanged model file: lowered, jets deferred
+                with LW.lowering(m._lower_on()), LW.deferred_jets(m._defer_on()):
+                    ld = body(m)
+                ld = LW.lower_losses(ld)
+            else:
+                ld = body(m)
             m._update_network(ld)
             torch.cuda.synchronize()
             assert len(ld) == 2
@@ -162,6 +178,13 @@ def test_fluid2dtlgn_phases_full_size(B):
 
 def test_fluid2dtlgn_phases_full_size_recorded_samples(B):
     _fluid(B, "fluid2Dtlgn", hooks=True)
+
+
+def test_fluid2dtlgn_plain_phases_full_size(B):
+    """The reference's fluid bodies as written (pde/fluid_plain.py) at the headline size, through the
+    training loop's loss lowering and deferred jets -- the drop-in path of bench.py --api plain -- against
+    the oracle on the same 16,384 + 2 x 162 points."""
+    _fluid(B, "fluid2Dtlgn", hooks=True, plain=True)
 
 
 def test_fluid2dtlgnM_phases_full_size(B):
@@ -269,4 +292,51 @@ def test_advect1d_full_size(B):
     for k, v in ldo.items():
         assert abs(float(ld[k]) - float(v)) <= TOL * abs(float(v)) + 1e-12, (k, float(ld[k]), float(v))
     check_grads(m.field, r["f"], "advect1D")
+    check_update(m.field, r["f"], p0, cfg.lr)
+
+
+def test_advect1d_plain_full_size(B):
+    """The reference's advection body as written (pde/advection_plain.py) at the advect1D size (4,096 +
+    2 x 20 points), through the training loop's loss lowering and deferred jets, vs the oracle on the same
+    points: both losses, every parameter gradient, the Adam update."""
+    import pde.advection_plain as ap
+    from base import lower as LW
+    from pde.config import baseline_config
+    cfg = baseline_config("advect1D", proj_dir="/tmp/insr_fullsize_adv_plain", insr_progress=False, early_stop=False,
+                          max_n_iters=1, insr_graph=False, insr_sync_every=1)
+    m = ap.Advection1DPlainModel(cfg)
+    m.timestep = 1
+    refs = {"f": seeded(1, 1, 3, 64, 231), "f_prev": seeded(1, 1, 3, 64, 232)}
+    load(m.field, refs["f"])
+    load(m.field_prev, refs["f_prev"])
+    p0 = O.flat_params(refs["f"]).numpy().copy()
+    gen = torch.Generator().manual_seed(233)
+    half = cfg.length / 2
+    x = (torch.rand(4096, 1, generator=gen) * 2 - 1) * half
+    eps = 1e-4
+    bu = torch.cat([-1 + eps * (torch.rand(20, 1, generator=gen) * 2 - 1), 1 + eps * (torch.rand(20, 1, generator=gen) * 2 - 1)])
+    m._sample_in_training = lambda: x.cuda().requires_grad_(True)
+    orig = ap.sample_boundary
+    ap.sample_boundary = lambda n, d, device=None: bu.cuda()
+    try:
+        m._reset_optimizer()
+        with LW.lowering(m._lower_on()), LW.deferred_jets(m._defer_on()):
+            ld = ap.Advection1DPlainModel._advect._insr_phase(m)
+        ld = LW.lower_losses(ld)
+        m._update_network(ld)
+        torch.cuda.synchronize()
+    finally:
+        ap.sample_boundary = orig
+    bc = (bu.cuda() * cfg.length / 2).cpu()  # the body's own scaling, in its op order
+    r = {k: seeded(1, 1, 3, 64, s) for k, s in (("f", 231), ("f_prev", 232))}
+    for p in r["f_prev"].parameters():
+        p.requires_grad_(False)
+    opt = O.OracleAdam(list(r["f"].parameters()), lr=cfg.lr)
+    ldo = O.advect1d_loss(r["f"], r["f_prev"], x.clone().requires_grad_(True), bc.clone().requires_grad_(True),
+                          cfg.dt, cfg.vel)
+    O.update_step([r["f"]], ldo, opt)
+    assert set(ld) == set(ldo) == {"main", "bc"}
+    for k, v in ldo.items():
+        assert abs(float(ld[k]) - float(v)) <= TOL * abs(float(v)) + 1e-12, (k, float(ld[k]), float(v))
+    check_grads(m.field, r["f"], "advect1D plain")
     check_update(m.field, r["f"], p0, cfg.lr)
