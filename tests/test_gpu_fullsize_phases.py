@@ -6,8 +6,9 @@ tests/test_oracle_golden.py) on the SAME points:
   * fluid2DtlgnM  the same at 256^2 = 65,536 + 2 x 654
   * elasticity2Dstretch  _solve_deformation at 20,000 points (SIREN 5x128) + 2 x 200 fixed
   * advect1D     _advect at 4,096 interior + 2 x 20 band points (SIREN 3x64)
-  * the reference's own bodies (pde/fluid_plain.py, pde/advection_plain.py) at the fluid2Dtlgn and advect1D
-    sizes, through the training loop's loss lowering and deferred jets (the drop-in path)
+  * the reference's own bodies (pde/fluid_plain.py, pde/advection_plain.py, pde/elasticity_plain.py) at the
+    fluid2Dtlgn, advect1D and elasticity2Dstretch sizes, through the training loop's loss lowering and
+    deferred jets (the drop-in path)
 
 The GPU runs the product path exactly as bench.py does -- device sampler into the merged
 [interior; bands] buffer (fluid) / the persistent box batch (elasticity), mixed launches,
@@ -340,3 +341,51 @@ def test_advect1d_plain_full_size(B):
         assert abs(float(ld[k]) - float(v)) <= TOL * abs(float(v)) + 1e-12, (k, float(ld[k]), float(v))
     check_grads(m.field, r["f"], "advect1D plain")
     check_update(m.field, r["f"], p0, cfg.lr)
+
+
+def test_elasticity2dstretch_plain_full_size(B):
+    """The reference's elastodynamics body as written (pde/elasticity_plain.py: q = f(x) + x, jacobian,
+    torch.svd, the energies as torch sums, separate constraint calls) at the elasticity2Dstretch size
+    (20,000 + 2 x 200 points), through the training loop's lowering scopes, vs the oracle on the same points."""
+    from base import lower as LW
+    from pde.config import baseline_config
+    from pde.elasticity_plain import ElasticityPlainModel
+    cfg = baseline_config("elasticity2Dstretch", proj_dir="/tmp/insr_fullsize_el2d_plain", insr_progress=False,
+                          early_stop=False, max_n_iters=1, insr_graph=False, insr_sync_every=1)
+    m = ElasticityPlainModel(cfg)
+    m.timestep = 1
+    for k, s, net in (("f", 241, m.deformation_field), ("f_prev", 242, m.deformation_field_prev),
+                      ("f_pp", 243, m.deformation_field_prev_prev)):
+        load(net, seeded(2, 2, 5, 128, s))
+    p0 = O.flat_params(seeded(2, 2, 5, 128, 241)).numpy().copy()
+    gen = torch.Generator().manual_seed(244)
+    x = torch.rand(20000, 2, generator=gen) * 2 - 1
+    fl_ = torch.rand(200, 2, generator=gen) * 0.02 - 1.0
+    fr_ = torch.rand(200, 2, generator=gen) * 0.02 + 0.98
+    m._sample_in_training = lambda resolution: x.cuda().requires_grad_(True)
+    m._sample_fixed_in_training = lambda resolution: (fl_.cuda().requires_grad_(True), fr_.cuda().requires_grad_(True))
+    m._reset_optimizer()
+    with LW.lowering(m._lower_on()), LW.deferred_jets(m._defer_on()):
+        ld = ElasticityPlainModel._solve_deformation._insr_phase(m)
+    ld = LW.lower_losses(ld)
+    m._update_network(ld)
+    torch.cuda.synchronize()
+    ecfg = dict(dt=cfg.dt, energy=list(cfg.energy), ratio_arap=cfg.ratio_arap, ratio_volume=cfg.ratio_volume,
+                ratio_kinematics=cfg.ratio_kinematics, ratio_constraint=cfg.ratio_constraint,
+                ratio_collide=cfg.ratio_collide, plane_height=cfg.plane_height,
+                external_force=[cfg.external_force_x, cfg.external_force_y],
+                constraint_offset_right=[cfg.constraint_right_offset_x, cfg.constraint_right_offset_y],
+                circle_center=[cfg.collide_circle_x, cfg.collide_circle_y], circle_radius=cfg.collide_circle_radius,
+                external_force_timesteps=cfg.external_force_timesteps)
+    r = {k: seeded(2, 2, 5, 128, s) for k, s in (("f", 241), ("f_prev", 242), ("f_pp", 243))}
+    for k in ("f_prev", "f_pp"):
+        for p in r[k].parameters():
+            p.requires_grad_(False)
+    opt = O.OracleAdam(list(r["f"].parameters()), lr=cfg.lr)
+    ldo = O.elasticity_loss(r["f"], r["f_prev"], r["f_pp"], x.clone().requires_grad_(True),
+                            fl_.clone().requires_grad_(True), fr_.clone().requires_grad_(True), ecfg, timestep=1)
+    O.update_step([r["f"]], ldo, opt)
+    assert abs(float(ld["main"]) - float(ldo["main"])) <= TOL * abs(float(ldo["main"])), (float(ld["main"]),
+                                                                                             float(ldo["main"]))
+    check_grads(m.deformation_field, r["f"], "el2d plain")
+    check_update(m.deformation_field, r["f"], p0, cfg.lr)
