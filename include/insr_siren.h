@@ -594,11 +594,15 @@ int insr_svd_energy_bwd(const float* J, long n, int d, float ratio_arap, float r
  *   CONSTRAINT      ratio * sum |f(x_l)|^2
  *   CONSTRAINT_RIGHT ratio * sum |f(x_r) - target|^2  (target = +-offset)
  *   COLLISION       -dt * sum_{q_z < h} qdot_z ratio (h - q_z)   (plane, z = last coordinate)
- *   SPHERE          -dt * sum_{|q - c| < R} qdot . ratio |q - c| dir   (d = 2 only)
+ *   SPHERE          d = 2: -dt * sum_{|q - c| < R} qdot . ratio |q - c| dir
+ *                   d = 3: -dt * ratio * (sum_{|q - c| < R} |q - c|) * (sum_{|q - c| < R} qdot . dir)
+ *                   (elasticity/losses.py:22-39: in 3-D the reference's dist[:, None, None] * dir
+ *                   broadcasts to (K, K, 3), a product of two sums; its gradient needs both sums,
+ *                   so the launch adds a second pass over the interior rows when d = 3)
  * *out = the terms of order[0 .. n_order) added in that order (cfg.energy); terms[t] = term t
  * (terms may be NULL).  gf (rows, d) / gJ (rows, d, d) (either may be NULL): d out[0] / d f, d out[0] / dJ,
  * zeros on rows no term reads.  Each term's sum is reduced in a fixed order; work:
- * insr_elastic_work_floats() floats, zero-initialised once (the launch leaves it zero).
+ * insr_elastic_work_floats() floats, zero-initialised once (the launch leaves its ticket zero).
  */
 #define INSR_EL_ARAP 0
 #define INSR_EL_VOLUME 1

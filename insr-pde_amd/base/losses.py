@@ -654,9 +654,6 @@ def elastic_energy(f, J, x, f_prev, f_pp, *, n, dt, energy, ratios, ext=(0.0, 0.
             continue
         order.append(t)
         ratio[t] = 1.0 if term == "external" else float(ratios[term])
-    d = f.shape[1]
-    if ids["collision_sphere"] in ratio and d != 2:
-        raise _unsupported("3-D collision_sphere (a product of two sums) is not fused")
     spec = {"n": int(n), "dt": float(dt), "ratio": ratio, "order": order, "ext": [float(v) for v in ext],
             "target": [float(v) for v in target], "center": [float(v) for v in center],
             "plane_height": float(plane_height), "radius": float(radius),

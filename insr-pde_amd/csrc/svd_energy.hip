@@ -236,15 +236,22 @@ __global__ __launch_bounds__(kSvdThreads) void svd_energy_bwd_kernel(const float
 // ---------------------------------------------------------------------------------------
 constexpr int kElThreads = 256;
 constexpr int kElMaxBlocks = 1024;
+// reduced sums: the INSR_EL_TERMS terms' raw sums, then the 3-D sphere's second factor
+// (sum qdot . dir over the colliding rows; the term's own slot holds sum |q - c|)
+constexpr int kElSphereB = INSR_EL_TERMS;
+constexpr int kElAcc = INSR_EL_TERMS + 1;
+// work: [kElAcc][kElMaxBlocks] block partials, the ticket, then the 3-D sphere's two sums for
+// the gradient pass (elastic_sphere3_grad_kernel)
+constexpr long kElTicket = (long)kElAcc * kElMaxBlocks;
 
 __global__ __launch_bounds__(kElThreads) void elastic_energy_kernel(const InsrElastic E, float* __restrict__ work) {
-  __shared__ float red[INSR_EL_TERMS][kElThreads / 64];
+  __shared__ float red[kElAcc][kElThreads / 64];
   const int d = E.d;
   const float dt = E.dt;
   const bool svd = E.ratio[INSR_EL_ARAP] != 0.f || E.ratio[INSR_EL_VOLUME] != 0.f;
-  float acc[INSR_EL_TERMS];
+  float acc[kElAcc];
 #pragma unroll
-  for (int t = 0; t < INSR_EL_TERMS; ++t) acc[t] = 0.f;
+  for (int t = 0; t < kElAcc; ++t) acc[t] = 0.f;
   for (long r = (long)blockIdx.x * kElThreads + threadIdx.x; r < E.rows; r += (long)gridDim.x * kElThreads) {
     float gf[3] = {0.f, 0.f, 0.f};
     if (r < E.n) {
@@ -275,7 +282,7 @@ __global__ __launch_bounds__(kElThreads) void elastic_energy_kernel(const InsrEl
           gf[d - 1] += (-dt * force) / dt + dt * qd[d - 1] * E.ratio[INSR_EL_COLLISION];
         }
       }
-      if (E.ratio[INSR_EL_SPHERE] != 0.f) {  // 2-D sphere: -dt sum qdot . rc dist dir over dist < R
+      if (E.ratio[INSR_EL_SPHERE] != 0.f) {  // sphere: penalty force rc dist dir on rows with dist < R
         float vec[3], ss = 0.f;
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
@@ -284,7 +291,12 @@ __global__ __launch_bounds__(kElThreads) void elastic_energy_kernel(const InsrEl
           ss += vec[k] * vec[k];
         }
         const float dist = sqrtf(ss);
-        if (dist < E.radius) {
+        if (d == 3) {  // the two factors of the 3-D product; the gradient pass follows the totals
+          if (dist < E.radius) {
+            acc[INSR_EL_SPHERE] += dist;
+            acc[kElSphereB] += qd[0] * (vec[0] / dist) + qd[1] * (vec[1] / dist) + qd[2] * (vec[2] / dist);
+          }
+        } else if (dist < E.radius) {  // 2-D: -dt sum qdot . rc dist dir
           const float rd = E.ratio[INSR_EL_SPHERE] * dist;
 #pragma unroll
           for (int k = 0; k < 3; ++k) {
@@ -350,15 +362,15 @@ __global__ __launch_bounds__(kElThreads) void elastic_energy_kernel(const InsrEl
   }
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
 #pragma unroll
-  for (int t = 0; t < INSR_EL_TERMS; ++t) {
+  for (int t = 0; t < kElAcc; ++t) {
     float v = acc[t];
     for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
     if (lane == 0) red[t][w] = v;
   }
-  __shared__ float tot[INSR_EL_TERMS];
+  __shared__ float tot[kElAcc];
   __shared__ int last;
   __syncthreads();
-  if (threadIdx.x < INSR_EL_TERMS) {  // the block's partial of term t (waves in order)
+  if (threadIdx.x < kElAcc) {  // the block's partial of sum t (waves in order)
     const int t = threadIdx.x;
     float part = 0.f;
 #pragma unroll
@@ -372,24 +384,25 @@ __global__ __launch_bounds__(kElThreads) void elastic_energy_kernel(const InsrEl
     if (gridDim.x > 1) {  // relaxed ticket after the sc1 stores complete: the hardware hand-off
                           // of block_partial_combine (residual.hip header; no release/acquire)
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      unsigned* ticket = reinterpret_cast<unsigned*>(work + INSR_EL_TERMS * kElMaxBlocks);
+      unsigned* ticket = reinterpret_cast<unsigned*>(work + kElTicket);
       last = atomicAdd(ticket, 1u) == gridDim.x - 1 ? 1 : 0;
     }
   }
   __syncthreads();
   if (!last) return;
   if (gridDim.x > 1) {
-    // the last block: wave w sums terms w and w + 4 over every block's partial, lanes load in
+    // the last block: wave w sums w, w + 4, w + 8 over every block's partial, lanes load in
     // parallel (lane l: blocks l, l + 64, ...), fixed butterfly -- deterministic
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
+    for (int h = 0; h < (kElAcc + 3) / 4; ++h) {
       const int t = w + 4 * h;
       float v = 0.f;
-      for (int q = lane; q < (int)gridDim.x; q += 64)
-        v += __hip_atomic_load(work + t * kElMaxBlocks + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (t < kElAcc)
+        for (int q = lane; q < (int)gridDim.x; q += 64)
+          v += __hip_atomic_load(work + t * kElMaxBlocks + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
       __syncthreads();
-      if (lane == 0) tot[t] = v;
+      if (lane == 0 && t < kElAcc) tot[t] = v;
     }
     __syncthreads();
   }
@@ -401,6 +414,7 @@ __global__ __launch_bounds__(kElThreads) void elastic_energy_kernel(const InsrEl
   for (int t = 0; t < INSR_EL_TERMS; ++t) {
     const float scale = (t == INSR_EL_EXTERNAL || t == INSR_EL_COLLISION || t == INSR_EL_SPHERE) ? -dt : E.ratio[t];
     et[t] = scale * tot[t];
+    if (t == INSR_EL_SPHERE && d == 3) et[t] = -dt * (E.ratio[t] * tot[t]) * tot[kElSphereB];
     if (E.terms) E.terms[t] = et[t];
   }
   float loss = 0.f;
@@ -411,7 +425,43 @@ __global__ __launch_bounds__(kElThreads) void elastic_energy_kernel(const InsrEl
       if (q == t) loss += et[q];
   }
   E.out[0] = loss;
-  if (gridDim.x > 1) atomicExch(reinterpret_cast<unsigned*>(work + INSR_EL_TERMS * kElMaxBlocks), 0u);
+  if (d == 3 && E.ratio[INSR_EL_SPHERE] != 0.f) {  // the two sums, for the gradient pass
+    work[kElTicket + 1] = tot[INSR_EL_SPHERE];
+    work[kElTicket + 2] = tot[kElSphereB];
+  }
+  if (gridDim.x > 1) atomicExch(reinterpret_cast<unsigned*>(work + kElTicket), 0u);
+}
+
+// The 3-D sphere term's gradient, after elastic_energy_kernel has both sums A = sum |q - c| and
+// B = sum qdot . dir (colliding rows): E = -dt rc A B, so on a colliding row
+//   dE/dq = -dt rc (B dir + A (dir / dt + (qdot - (qdot . dir) dir) / |q - c|))
+// (d|q - c|/dq = dir, d(qdot . dir)/dq = dir / dt + (I - dir dir^T) qdot / |q - c|), added to gf.
+__global__ __launch_bounds__(kElThreads) void elastic_sphere3_grad_kernel(const InsrElastic E,
+                                                                          const float* __restrict__ work) {
+  const float A = work[kElTicket + 1], Bs = work[kElTicket + 2];
+  const float dt = E.dt, c = -dt * E.ratio[INSR_EL_SPHERE];
+  for (long r = (long)blockIdx.x * kElThreads + threadIdx.x; r < E.n; r += (long)gridDim.x * kElThreads) {
+    float vec[3], qd[3], ss = 0.f;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const float xk = E.x[r * 3 + k];
+      const float q = E.f[r * 3 + k] + xk;
+      qd[k] = (q - (E.f_prev[r * 3 + k] + xk)) / dt;
+      vec[k] = q - E.center[k];
+      ss += vec[k] * vec[k];
+    }
+    const float dist = sqrtf(ss);
+    if (!(dist < E.radius)) continue;
+    float dir[3], qdir = 0.f;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      dir[k] = vec[k] / dist;
+      qdir += qd[k] * dir[k];
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+      E.gf[r * 3 + k] += c * (Bs * dir[k] + A * (dir[k] / dt + (qd[k] - qdir * dir[k]) / dist));
+  }
 }
 
 }  // namespace insr
@@ -448,7 +498,7 @@ int insr_svd_energy_bwd(const float* J, long n, int d, float ratio_arap, float r
 }
 
 
-long insr_elastic_work_floats(void) { return (long)INSR_EL_TERMS * kElMaxBlocks + 4; }
+long insr_elastic_work_floats(void) { return kElTicket + 4; }
 
 int insr_elastic_energy(const InsrElastic* e, float* work, void* stream) {
   if (!e || (e->d != 2 && e->d != 3) || e->n < 0 || e->rows < e->n || !e->out) return INSR_EINVAL;
@@ -457,7 +507,7 @@ int insr_elastic_energy(const InsrElastic* e, float* work, void* stream) {
   const bool svd = e->ratio[INSR_EL_ARAP] != 0.f || e->ratio[INSR_EL_VOLUME] != 0.f;
   if (svd && e->n > 0 && !e->J) return INSR_EINVAL;
   if (!(e->dt > 0.f) || e->n_order < 0 || e->n_order > INSR_EL_TERMS) return INSR_EINVAL;
-  if (e->ratio[INSR_EL_SPHERE] != 0.f && e->d != 2) return INSR_EINVAL;  // 3-D: a product of two sums
+  const bool sphere3 = e->ratio[INSR_EL_SPHERE] != 0.f && e->d == 3;  // 3-D: a product of two sums
   for (int k = 0; k < e->n_order; ++k)
     if (e->order[k] < 0 || e->order[k] >= INSR_EL_TERMS) return INSR_EINVAL;
   if (e->n_l < 0 || e->n_r < 0 || (e->n_l > 0 && (e->row_l < e->n || e->row_l + e->n_l > e->rows)) ||
@@ -468,8 +518,14 @@ int insr_elastic_energy(const InsrElastic* e, float* work, void* stream) {
   long nb = (e->rows + kElThreads - 1) / kElThreads;
   if (nb < 1) nb = 1;
   if (nb > kElMaxBlocks) nb = kElMaxBlocks;
-  if (nb > 1 && !work) return INSR_EINVAL;
+  if ((nb > 1 || sphere3) && !work) return INSR_EINVAL;
   hipLaunchKernelGGL(elastic_energy_kernel, dim3((unsigned)nb), dim3(kElThreads), 0, (hipStream_t)stream, *e, work);
+  if (sphere3 && e->gf && e->n > 0) {
+    long ng = (e->n + kElThreads - 1) / kElThreads;
+    if (ng > kElMaxBlocks) ng = kElMaxBlocks;
+    hipLaunchKernelGGL(elastic_sphere3_grad_kernel, dim3((unsigned)ng), dim3(kElThreads), 0, (hipStream_t)stream, *e,
+                       work);
+  }
   return (int)hipGetLastError();
 }
 

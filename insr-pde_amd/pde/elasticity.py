@@ -8,7 +8,8 @@ Energy terms (all SUMS over collocation points, as in the reference):
   kinematics  r_k  sum |qdot - qdot_prev|^2     qdot = (q - q_prev)/dt
   external    -dt  sum qdot . f_ext             (first T_ext timesteps)
   constraint(_right[_compress]) r_c sum |f(x_fixed) - target|^2
-  collision(_sphere)  -dt sum qdot . penalty force on penetrating points
+  collision(_sphere)  -dt sum qdot . penalty force on penetrating points (3-D sphere: the
+              reference's broadcast makes it -dt r_c (sum dist) (sum qdot . dir), reproduced as is)
 
 Geometry: the synthetic box [-1, 1]^d (use_mesh=False), or a tet / triangle mesh
 (use_mesh=True, cfg.mesh_path: MEDIT .mesh or .obj; pde/mesh.py): volume-weighted
@@ -19,8 +20,7 @@ import os
 import numpy as np
 import torch
 
-from base import (BaseModel, elastic_energy, fused_forwards, fused_mse, merge_samples, sample_random, sample_uniform,
-                  svd_energy)
+from base import BaseModel, elastic_energy, fused_forwards, merge_samples, sample_random, sample_uniform
 from base.sampling import sample_boxes_into
 from base.diff_ops import jacobian_only
 
@@ -300,59 +300,21 @@ class ElasticityModel(BaseModel):
                 f_prev = self.deformation_field_prev(x)
                 f_pp = self.deformation_field_prev_prev(x)
             fa = self.deformation_field(xa)
-        if not (self.dim == 3 and 'collision_sphere' in self.energy):
-            # every term in ONE launch with its unit-seed gradient (base.elastic_energy): the
-            # singular values of dq/dx = J + I, kinematics, external force, collisions and the
-            # positional constraints; J is the Jacobian jet of the same field launch
-            J = jacobian_only(fa, xa) if ('arap' in self.energy or 'volume' in self.energy) else None
-            sign = -1.0 if 'constraint_right_compress' in self.energy else 1.0
-            ratios = {'arap': self.ratio_arap, 'volume': self.ratio_volume, 'kinematics': self.ratio_kinematics,
-                      'constraint': self.ratio_constraint, 'constraint_right': self.ratio_constraint,
-                      'constraint_right_compress': self.ratio_constraint, 'collision': self.ratio_collide,
-                      'collision_sphere': self.ratio_collide}
-            total, _ = elastic_energy(
-                fa, J, x, f_prev, f_pp, n=n, dt=dt, energy=self.energy, ratios=ratios,
-                ext=self._host_vec('external_force'), external_on=self.timestep <= self.external_force_timesteps,
-                rows_l=(row_l, fixed_l.shape[0] if use_l else 0), rows_r=(row_r, fixed_r.shape[0] if use_r else 0),
-                target=[sign * v for v in self._host_vec('constraint_offset_right')], plane_height=self.plane_height,
-                center=self._host_vec('circle_center'), radius=self.circle_radius)
-            return total
-        # 3-D collision_sphere (the reference's broadcast makes it a product of two sums): torch terms
-        with torch.no_grad():
-            q_prev = f_prev + x
-            q_pp = f_pp + x
-        qa = fa + xa
-        q = qa if xa is x else qa[:n]
-        qdot = (q - q_prev) / dt
-        total = 0
-        if 'arap' in self.energy or 'volume' in self.energy:
-            # both singular-value terms in one fused HIP launch each way (torch.svd + ~12 ops in the reference)
-            J = jacobian_only(qa, xa)  # the status is unused (as in the reference): no NaN scan
-            total = svd_energy(J, self.ratio_arap if 'arap' in self.energy else 0.0,
-                               self.ratio_volume if 'volume' in self.energy else 0.0, count=n)
-        for term in self.energy:
-            if term in ('arap', 'volume'):
-                continue
-            elif term == 'kinematics':
-                qdot_prev = (q_prev - q_pp) / dt
-                total = total + self.ratio_kinematics * torch.sum((qdot - qdot_prev) ** 2)
-            elif term == 'external':
-                if self.timestep <= self.external_force_timesteps:
-                    total = total - dt * torch.sum(qdot * self.external_force)
-            elif term == 'constraint':  # r_c sum |f(x_fixed)|^2
-                total = total + self.ratio_constraint * fused_mse(fa, count=fixed_l.numel(), a_row0=row_l,
-                                                                  reduction="sum")
-            elif term in ('constraint_right', 'constraint_right_compress'):  # r_c sum |f(x_r) -/+ offset|^2
-                sign = 1.0 if term == 'constraint_right' else -1.0
-                tgt = self._target_rows(sign, fixed_r.shape[0])
-                total = total + self.ratio_constraint * fused_mse(fa, tgt, count=fixed_r.numel(), a_row0=row_r,
-                                                                  reduction="sum")
-            elif term == 'collision':
-                total = total + self._plane_penalty(q, qdot)
-            elif term == 'collision_sphere':
-                total = total + self._sphere_penalty(q, qdot)
-            else:
-                raise NotImplementedError(term)
+        # every term in ONE launch with its unit-seed gradient (base.elastic_energy): the
+        # singular values of dq/dx = J + I, kinematics, external force, collisions and the
+        # positional constraints; J is the Jacobian jet of the same field launch
+        J = jacobian_only(fa, xa) if ('arap' in self.energy or 'volume' in self.energy) else None
+        sign = -1.0 if 'constraint_right_compress' in self.energy else 1.0
+        ratios = {'arap': self.ratio_arap, 'volume': self.ratio_volume, 'kinematics': self.ratio_kinematics,
+                  'constraint': self.ratio_constraint, 'constraint_right': self.ratio_constraint,
+                  'constraint_right_compress': self.ratio_constraint, 'collision': self.ratio_collide,
+                  'collision_sphere': self.ratio_collide}
+        total, _ = elastic_energy(
+            fa, J, x, f_prev, f_pp, n=n, dt=dt, energy=self.energy, ratios=ratios,
+            ext=self._host_vec('external_force'), external_on=self.timestep <= self.external_force_timesteps,
+            rows_l=(row_l, fixed_l.shape[0] if use_l else 0), rows_r=(row_r, fixed_r.shape[0] if use_r else 0),
+            target=[sign * v for v in self._host_vec('constraint_offset_right')], plane_height=self.plane_height,
+            center=self._host_vec('circle_center'), radius=self.circle_radius)
         return total
 
     def _host_vec(self, name):
@@ -361,33 +323,6 @@ class ElasticityModel(BaseModel):
         if name not in cache:
             cache[name] = [float(v) for v in getattr(self, name).cpu()]
         return cache[name]
-
-    def _target_rows(self, sign, rows):
-        """sign * constraint_offset_right repeated over the fixed points (cached constant)."""
-        cache = self.__dict__.setdefault("_insr_targets", {})
-        key = (sign, rows)
-        if key not in cache:
-            cache[key] = (sign * self.constraint_offset_right).expand(rows, self.dim).contiguous()
-        return cache[key]
-
-    def _plane_penalty(self, q, qdot):
-        """elasticity/losses.py:10-20, written mask-free (no host sync): force only
-        on points below the plane; the reference's empty-set case gives 0 too."""
-        depth = torch.clamp(self.plane_height - q[:, -1], min=0.0)
-        hit = (q[:, -1] < self.plane_height).to(q.dtype)
-        return -self.dt * torch.sum(qdot[:, -1] * self.ratio_collide * depth * hit)
-
-    def _sphere_penalty(self, q, qdot):
-        """elasticity/losses.py:22-39, mask-free.  In 3-D the reference broadcasts
-        dist[:, None, None] * dir (K,1,1)x(K,3) -> (K,K,3), i.e. the energy becomes
-        (sum_i dist_i) * (sum_j qdot_j . dir_j); that is reproduced as is."""
-        vec = q - self.circle_center
-        dist = torch.sqrt(torch.sum(vec ** 2, dim=1))
-        hit = (dist < self.circle_radius).to(q.dtype)
-        direc = vec / dist[:, None]
-        if q.shape[1] == 2:
-            return -self.dt * torch.sum(qdot * (self.ratio_collide * dist[:, None] * direc) * hit[:, None])
-        return -self.dt * self.ratio_collide * torch.sum(dist * hit) * torch.sum(qdot * direc * hit[:, None])
 
     # ---- output (host side; PNG figures are out of scope) ---------------------------
     def sample_visualization(self, resolution):

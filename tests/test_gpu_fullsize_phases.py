@@ -242,6 +242,55 @@ def test_elasticity2dstretch_full_size(B):
     check_update(m.deformation_field, r["f"], p0, cfg.lr)
 
 
+def test_elasticity3d_sphere_collision(B):
+    """A 3-D box scene whose energy holds collision_sphere (elasticity/losses.py:22-39: the reference's
+    dist[:, None, None] * dir broadcast makes the 3-D term -dt r_c (sum dist) (sum qdot . dir)), one
+    iteration through the fused energy launch and its gradient pass, vs the oracle's literal broadcast on
+    the same points.  The sphere is placed inside the box so that a large share of the points collide."""
+    from pde.config import make_config
+    from pde.elasticity import ElasticityModel
+    energy = ["arap", "kinematics", "collision_sphere", "external", "volume"]
+    cfg = make_config("elasticity", proj_dir="/tmp/insr_el3d_sphere", insr_progress=False, early_stop=False,
+                      max_n_iters=1, insr_graph=False, insr_sync_every=1, dim=3, num_hidden_layers=3,
+                      hidden_features=64, sample_resolution=12, dt=0.1, energy=energy, ratio_collide=1e3,
+                      collide_circle_x=0.1, collide_circle_y=-0.4, collide_circle_z=0.2, collide_circle_radius=0.8)
+    m = ElasticityModel(cfg)
+    m.timestep = 1
+    refs = {"f": seeded(3, 3, 3, 64, 221), "f_prev": seeded(3, 3, 3, 64, 222), "f_pp": seeded(3, 3, 3, 64, 223)}
+    for k, net in (("f", m.deformation_field), ("f_prev", m.deformation_field_prev),
+                   ("f_pp", m.deformation_field_prev_prev)):
+        load(net, refs[k])
+    p0 = O.flat_params(refs["f"]).numpy().copy()
+    m._reset_optimizer()
+    ld = ElasticityModel._solve_deformation._insr_phase(m)
+    m._update_network(ld)
+    torch.cuda.synchronize()
+    (buf, _, x, _, _), = m.__dict__["_insr_box_batch"].values()
+    x = x.detach().cpu().clone()
+    dist = (x - torch.tensor([0.1, -0.4, 0.2])).norm(dim=1)
+    assert x.shape[1] == 3 and int((dist < 0.8).sum()) > 0.1 * x.shape[0]
+    ecfg = dict(dt=cfg.dt, energy=energy, ratio_arap=cfg.ratio_arap, ratio_volume=cfg.ratio_volume,
+                ratio_kinematics=cfg.ratio_kinematics, ratio_constraint=cfg.ratio_constraint,
+                ratio_collide=cfg.ratio_collide, plane_height=cfg.plane_height,
+                external_force=[cfg.external_force_x, cfg.external_force_y, cfg.external_force_z],
+                constraint_offset_right=[cfg.constraint_right_offset_x, cfg.constraint_right_offset_y,
+                                         cfg.constraint_right_offset_z],
+                circle_center=[0.1, -0.4, 0.2], circle_radius=0.8,
+                external_force_timesteps=cfg.external_force_timesteps)
+    r = {k: seeded(3, 3, 3, 64, s) for k, s in (("f", 221), ("f_prev", 222), ("f_pp", 223))}
+    for k in ("f_prev", "f_pp"):
+        for p in r[k].parameters():
+            p.requires_grad_(False)
+    opt = O.OracleAdam(list(r["f"].parameters()), lr=cfg.lr)
+    empty = torch.zeros(0, 3)
+    ldo = O.elasticity_loss(r["f"], r["f_prev"], r["f_pp"], x.requires_grad_(True), empty, empty, ecfg, timestep=1)
+    O.update_step([r["f"]], ldo, opt)
+    assert abs(float(ld["main"]) - float(ldo["main"])) <= TOL * abs(float(ldo["main"])), (float(ld["main"]),
+                                                                                             float(ldo["main"]))
+    check_grads(m.deformation_field, r["f"], "el3d sphere")
+    check_update(m.deformation_field, r["f"], p0, cfg.lr)
+
+
 def test_advect1d_full_size(B):
     """advect1D (BASELINE.json configs[0]: SIREN 3x64, sample_resolution 4,096): one _advect iteration
     on the product sampler path -- ONE insr_sample_boxes launch writes the 4,096 interior points and the
