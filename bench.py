@@ -79,6 +79,8 @@ def parse():
     ap.add_argument("--shard-of", type=int, default=1,
                     help="one process runs the per-rank shard of a K-rank strong-scaling run (global batch / K "
                          "points per phase iteration; elasticity: the draw at resolution / K^(1/3)); 1 GPU")
+    ap.add_argument("--warm-ms", type=float, default=200.0,
+                    help="untimed timesteps (graph replays as in the timed region) for this long before timing")
     ap.add_argument("--graph-unroll", type=int, default=4,
                     help="iterations per hipGraph replay inside a timestep's phase loop (PhaseLoop "
                          "insr_graph_unroll; 1 = one replay per iteration)")
@@ -651,6 +653,15 @@ def main():
         run_timestep(model, wl, loops, w_eff, U)
         torch.cuda.synchronize()
         w_eff += U
+    # sustained untimed timesteps (the graphs replayed as in the timed region) until --warm-ms of wall
+    # time has passed: the timed region then starts with the replays warm and the device clocks at their
+    # sustained level (without it the first timed timesteps run slower, profiles/r05/warm/)
+    k_warm = U if (U > 1 and not args.no_graph) else 1
+    t_warm = time.perf_counter()
+    while (time.perf_counter() - t_warm) * 1e3 < args.warm_ms:
+        run_timestep(model, wl, loops, w_eff, k_warm)
+        w_eff += k_warm
+        torch.cuda.synchronize()
     # timed region: --steps iterations of every phase, as `nts` timesteps in step() order
     # (K iterations per phase, phases in order, median of 5 timesteps); no loss
     # reads inside (sync_every = 1e9) and no host sync at the timestep boundaries either: the
@@ -694,7 +705,7 @@ def main():
                    "points_per_phase_iter": n_all, "phases": nph, "global_batch": n_all,
                    "seq_len": None, "parallelism": f"dp{world}", "graph": not args.no_graph,
                    "precision": args.precision, "api": args.api, "sync_every": cfg.insr_sync_every,
-                   "graph_unroll": 1 if args.no_graph else max(1, args.graph_unroll),
+                   "graph_unroll": 1 if args.no_graph else max(1, args.graph_unroll), "warm_ms": args.warm_ms,
                    "jet_precision": jet_precision_names(args.precision),
                    "bwd_policy": args.bwd_policy, "shard_of": args.shard_of, "dp_path": args.dp_path,
                    "seeds_in_bwd": bool(getattr(cfg, "insr_seed_in_bwd", True)),

@@ -5,8 +5,8 @@ import os
 import numpy as np
 import torch
 
-from base import (BaseModel, fused_forwards, fused_mse, gradient, merge_samples, sample_boundary, sample_boxes,
-                  sample_random, sample_uniform)
+from base import (BaseModel, fused_forwards, fused_mse, gradient, merge_samples, mse_term, sample_boundary,
+                  sample_boxes, sample_random, sample_uniform, sq_losses)
 
 from .examples import get_examples
 
@@ -73,10 +73,13 @@ class Advection1DModel(BaseModel):
             u0x = gradient(u0, x)
         uxa = gradient(ua, xa)
         xb = xa[n:]
-        # mean(((u - u0)/dt + vel (ux + u0x)/2)^2) over the interior rows, one fused launch each way
-        main = fused_mse(ua, u0, uxa, u0x, alpha=1.0 / self.dt, beta=-1.0, gamma=self.vel / 2., delta=1.0, count=n,
-                         total=self._dp_total(n))
-        return {'main': main, 'bc': fused_mse(ua, count=xb.shape[0], a_row0=n, total=self._dp_total(xb.shape[0]))}
+        # mean(((u - u0)/dt + vel (ux + u0x)/2)^2) over the interior rows and mean(u^2) over the band rows:
+        # ONE loss-group launch; the two terms' gradients w.r.t. ua cover its rows [0, n) and [n, n + n_bc)
+        # and share one buffer (no separate launch per loss, no gradient add)
+        main, bc = sq_losses(mse_term(ua, u0, uxa, u0x, alpha=1.0 / self.dt, beta=-1.0, gamma=self.vel / 2., delta=1.0,
+                                      count=n, total=self._dp_total(n)),
+                             mse_term(ua, count=xb.shape[0], a_row0=n, total=self._dp_total(xb.shape[0])))
+        return {'main': main, 'bc': bc}
 
     def _advect_points(self, n_bc):
         """(x, xa = [x; boundary band]) of one iteration.  On the GPU one sampler launch
