@@ -614,6 +614,7 @@ class _ElasticEnergy(torch.autograd.Function):
                   "insr_elastic_energy")
         ctx.pre = (gf, gJ)
         ctx.mark_non_differentiable(terms)
+        ctx.set_materialize_grads(False)  # the unused terms output: no zero-filled gradient launch
         return out, terms
 
     @staticmethod
