@@ -45,8 +45,8 @@ for s in ${STEPS:-tests bench prof}; do
              run sd_As_$r 300 python bench.py --config fluid2DtlgnM --shard-of 8 --steps 40 --warmup 3 --no-cpu-baseline --no-roofline
              run sd_Bs_$r 300 python bench.py --config fluid2DtlgnM --shard-of 8 --no-seed-in-bwd --steps 40 --warmup 3 --no-cpu-baseline --no-roofline
            done ;;
-    prof) run prof 300 rocprofv3 --kernel-trace --stats -d "$PWD/$O/prof" -o run --output-format csv -- python bench.py --steps 10 --warmup 3 --no-cpu-baseline ;;
-    profB) run profB 300 rocprofv3 --kernel-trace --stats -d "$PWD/$O/profB" -o run --output-format csv -- python bench.py --no-seed-in-bwd --steps 10 --warmup 3 --no-cpu-baseline ;;
+    prof) run prof 300 rocprofv3 --kernel-trace --stats -d "$PWD/$O/prof" -o run --output-format csv -- python bench.py --steps 20 --warmup 3 --no-cpu-baseline ;;
+    profB) run profB 300 rocprofv3 --kernel-trace --stats -d "$PWD/$O/profB" -o run --output-format csv -- python bench.py --no-seed-in-bwd --steps 20 --warmup 3 --no-cpu-baseline ;;
     profshardB) run profshardB 300 rocprofv3 --kernel-trace --stats -d "$PWD/$O/profshardB" -o run --output-format csv -- python bench.py --config fluid2DtlgnM --shard-of 8 --no-seed-in-bwd --steps 10 --warmup 3 --no-cpu-baseline --no-roofline ;;
     profadvplain) run profadvplain 300 rocprofv3 --kernel-trace --stats -d "$PWD/$O/profadvplain" -o run --output-format csv -- python bench.py --api plain --config advect1D --steps 20 --warmup 3 --no-cpu-baseline --no-roofline ;;
     pmc) PRX='jet_|dw_x6|reduce_'  # HBM bytes per dispatch (eager run): FETCH_SIZE, WRITE_SIZE and SQ in passes of their own
