@@ -14,3 +14,12 @@ from .optim import DevicePlateau, FusedAdam  # noqa: F401
 from .losses import axpy_clamp, elastic_energy, fused_mse, mse_term, sq_losses, svd_energy, wall_mse, wall_term  # noqa: F401
 from ._jet import UnsupportedPattern, advect_target, fused_forwards  # noqa: F401
 from ._native import NativeUnavailable, NativeError  # noqa: F401
+from . import sampling as _sampling
+from .lower import sampler_api as _sampler_api
+
+# the samplers a model file imports from `base` hand their draws to the loss lowering as ready leaves
+# (base/lower.py sampler_api; outside lowering() they are the plain functions)
+sample_random = _sampler_api(_sampling.sample_random)
+sample_uniform = _sampler_api(_sampling.sample_uniform)
+sample_boundary = _sampler_api(_sampling.sample_boundary)
+sample_boundary2D_separate = _sampler_api(_sampling.sample_boundary2D_separate)

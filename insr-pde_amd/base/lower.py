@@ -34,7 +34,7 @@ import threading
 import torch
 
 __all__ = ["Lazy", "lowering", "deferred_jets", "deferring", "flush", "immediate", "add_views", "suspended", "api",
-           "active", "leaf", "materialize", "plan", "lower_losses", "LOWERED"]
+           "sampler_api", "active", "leaf", "materialize", "plan", "lower_losses", "LOWERED"]
 
 LOWERED = {"groups": 0, "terms": 0, "eager_losses": 0, "materialized": 0}  # counters (tests, docs)
 
@@ -163,11 +163,13 @@ def add_views(a, b):
 # and a replay that would read a tensor written behind the recorder's back (an in-place op on a plain
 # tensor a recorded expression reads) raises instead of computing with the new values.
 class _Node:
-    __slots__ = ("kind", "kids", "coef", "k", "lo", "hi", "real", "real_ng", "call", "shape", "grad_mode", "ver")
+    __slots__ = ("kind", "kids", "coef", "k", "lo", "hi", "real", "real_ng", "call", "shape", "grad_mode", "ver",
+                 "ready")
 
     def __init__(self, kind, kids=(), coef=None, k=None, lo=None, hi=None, real=None, call=None, shape=None):
         self.kind, self.kids, self.coef, self.k, self.lo, self.hi = kind, tuple(kids), coef, k, lo, hi
         self.real, self.real_ng, self.call, self.shape = real, None, call, shape
+        self.ready = False  # real holds final values no queued jet writes (a sampler's draw, or c times one)
         self.grad_mode = torch.is_grad_enabled()
         self.ver = real._version if real is not None else None
 
@@ -279,6 +281,26 @@ def leaf(t):
     if not active() or not isinstance(t, torch.Tensor) or isinstance(t, Lazy) or t.dtype != torch.float32:
         return t
     return _wrap(_Node("leaf", real=t, shape=tuple(t.shape)), t.dtype, t.device, t.requires_grad)
+
+
+def sampler_api(fn):
+    """A sampler of the base API (sample_random, sample_boundary, ...).  Inside lowering() its GPU result is
+    a READY Lazy leaf -- a drawn tensor, which no queued jet writes: handing it to a network or diff op
+    launches nothing, and a body's scalar rescale of its samples (advection/model.py:27,86:
+    sample_random(...).requires_grad_(True) * self.length / 2) is recorded and evaluated as ONE launch
+    instead of one per operator."""
+    import functools
+
+    @functools.wraps(fn)
+    def w(*args, **kwargs):
+        r = fn(*_real_tree(args), **_real_tree(kwargs))
+        if not active() or not isinstance(r, torch.Tensor) or isinstance(r, Lazy) or r.dtype != torch.float32 \
+                or not r.is_cuda:
+            return r
+        n = _Node("leaf", real=r, shape=tuple(r.shape))
+        n.ready = True
+        return _wrap(n, r.dtype, r.device, r.requires_grad)
+    return w
 
 
 class suspended:
@@ -447,6 +469,14 @@ def _record(name, func, args, kwargs):
             k = idx[1] % n.shape[1]
             return _lazy_of("sel", (n,), call, (n.shape[0],), like, x.requires_grad, k=k)
         return None
+    if name == "requires_grad_" and isinstance(args[0], Lazy) and args[0]._insr_node.kind == "leaf" and \
+            args[0]._insr_node.ready and len(args) <= 2 and set(kwargs) <= {"requires_grad"}:
+        x = args[0]  # a sampler's leaf: flag its tensor and the wrapper, as eager code flags the tensor
+        flag = bool(args[1]) if len(args) == 2 else bool(kwargs.get("requires_grad", True))
+        x._insr_node.real.requires_grad_(flag)
+        with torch._C.DisableTorchFunctionSubclass():
+            torch.Tensor.requires_grad_(x, flag)
+        return x
     if name == "detach" and len(args) == 1 and not kwargs:
         x = args[0]
         return _lazy_of("detach", (x._insr_node,), call, x._insr_node.shape, like, False)
@@ -492,12 +522,32 @@ def _eval(n):
         raise RuntimeError("base/lower.py: a tensor read by a recorded expression was written in place after "
                            "the expression was recorded (an in-place op on a plain tensor); evaluating it now "
                            "would read the new values. Run this model unlowered (cfg.insr_lower = False).")
+    sc = _ready_scale(n)
+    if sc is not None:  # c x of a ready leaf (a chain of scalar multiplies / divides): one launch
+        c, base = sc
+        with torch.set_grad_enabled(n.grad_mode):
+            n.real = base * c
+        n.ready = True
+        LOWERED["materialized"] += 1
+        return n.real
     func, args, kwargs = n.call
     a, k = _real_tree(args), _real_tree(kwargs)
     with torch.set_grad_enabled(n.grad_mode):
         n.real = func(*a, **k)
     LOWERED["materialized"] += 1
     return n.real
+
+
+def _ready_scale(n):
+    """(c, tensor) when n is c times a ready value (a sampler's draw, or an evaluated rescale of one) through
+    single-operand scalar 'lin' nodes, else None."""
+    c, m = 1.0, n
+    while m.kind == "lin" and len(m.kids) == 1 and m.real is None:
+        c *= m.coef[0]
+        m = m.kids[0]
+    if m is n or m.real is None or not m.ready:
+        return None
+    return c, m.real
 
 
 def _axpy_clamp_fast(n):
@@ -530,6 +580,10 @@ def materialize(t):
     if n is None:
         raise RuntimeError("a storage-less Lazy tensor without its record (made by torch from a Lazy tensor "
                            "below __torch_function__): base/lower.py cannot compute it")
+    if n.ready and n.real is not None:  # a sampler's draw, or c times one: no queued jet's output in it
+        return n.real
+    if n.real is None and _ready_scale(n) is not None:
+        return _eval(n)
     flush()
     if not torch.is_grad_enabled() and n.real is None:
         if n.real_ng is None:
