@@ -300,3 +300,26 @@ def test_plain_tensor_written_with_a_lazy_value():
         (a,) = _leaves(base * 1.0)
         lz = body(a, x0.clone())
     assert torch.allclose(LW.materialize(lz), ref, rtol=1e-6)
+
+
+def test_ready_sampler_leaf_rescale_is_one_op_and_cached():
+    """A sampler's draw (base/lower.py sampler_api: a READY leaf) rescaled as the reference advection body
+    does (advection/model.py:27: sample_random(...).requires_grad_(True) * length / 2) evaluates as one
+    multiply by the folded scalar, with autograd, is cached, and reading the draw itself returns its tensor."""
+    torch.manual_seed(3)
+    draw = torch.rand(16, 1) * 2 - 1
+    with LW.lowering():
+        n = LW._Node("leaf", real=draw, shape=tuple(draw.shape))
+        n.ready = True
+        x = LW._wrap(n, draw.dtype, draw.device, False)
+        xg = x.requires_grad_(True)
+        assert xg is x and x.requires_grad and draw.requires_grad
+        y = x * 4.0 / 2
+        assert isinstance(y, LW.Lazy) and y.requires_grad
+        before = LW.LOWERED["materialized"]
+        r = LW.materialize(y)
+        assert LW.LOWERED["materialized"] == before + 1  # one evaluation for the whole chain
+        assert torch.equal(r, draw * 2.0) and r.requires_grad and r.grad_fn is not None
+        assert LW.materialize(y) is r and LW.materialize(x) is draw
+        r.sum().backward()
+        assert torch.equal(draw.grad, torch.full_like(draw, 2.0))
