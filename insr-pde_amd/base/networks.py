@@ -445,7 +445,8 @@ class MLP(nn.Module):
         params = self.plist()
         if self._flat is None or not params or self._flat.numel() != self.param_count:
             return False
-        return all(self._sig_of(p.data) == sg for p, sg in zip(params, self._view_sigs(self._flat)))
+        # (the parameters' own metadata: the same as p.data's, without building a tensor per parameter)
+        return all(self._sig_of(p) == sg for p, sg in zip(params, self._view_sigs(self._flat)))
 
     def ensure_packed(self):
         if not self._is_packed():
