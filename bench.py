@@ -73,9 +73,12 @@ def parse():
                          "config), bf16x3 (3 bf16 products), bf16 (1 product) or mixed (bf16x3 forwards, bf16 "
                          "backwards: BASELINE configs[4] 'mixed fp32/bf16 MFMA', within 1e-2)")
     ap.add_argument("--api", choices=["fused", "plain"], default="fused",
-                    help="fluid / advect1D: 'plain' runs pde/fluid_plain.py / pde/advection_plain.py, phase bodies "
-                         "written only against the reference's base API (separate band samplers, torch residuals, "
-                         "lowered by the loop: base/lower.py) -- the drop-in case")
+                    help="'plain' runs pde/fluid_plain.py / pde/advection_plain.py / pde/elasticity_plain.py, phase "
+                         "bodies written only against the reference's base API (separate band samplers, torch "
+                         "residuals and energies, lowered by the loop: base/lower.py) -- the drop-in case")
+    ap.add_argument("--plain-line", choices=["auto", "on", "off"], default="auto",
+                    help="also time the unchanged reference phase bodies (--api plain) after the fused run and add "
+                         "them to the line as `plain` (auto: on for the default fluid2Dtlgn line on one GPU)")
     ap.add_argument("--shard-of", type=int, default=1,
                     help="one process runs the per-rank shard of a K-rank strong-scaling run (global batch / K "
                          "points per phase iteration; elasticity: the draw at resolution / K^(1/3)); 1 GPU")
@@ -242,6 +245,8 @@ def finish_model(args, cfg, wl, world, rank, per_rank):
         from pde.advection_plain import Advection1DPlainModel as M
     elif wl["pde"] == "advection":
         from pde.advection import Advection1DModel as M
+    elif args.api == "plain":
+        from pde.elasticity_plain import ElasticityPlainModel as M
     else:
         from pde.elasticity import ElasticityModel as M
     model = M(cfg)
@@ -467,7 +472,7 @@ def pmc_traffic(kname, grid):
     return tot, tab.get("_source")
 
 
-def cpu_baseline(config, seconds):
+def cpu_baseline(config, seconds, n_rounds=3, iters=10):
     """The oracle (torch-CPU restatement of the reference graph) on this host's cores, over a
     bounded sample of the same workload (same nets, same phases; elasticity3Dbunny on a
     16384-point slice of its 262144-point batch: the per-point cost is size-independent)."""
@@ -556,10 +561,10 @@ def cpu_baseline(config, seconds):
     # rounds within the time budget); the round with the smallest spread is reported
     rounds = []
     t_start = time.perf_counter()
-    for _ in range(3):
+    for _ in range(n_rounds):
         times = []
         t_all = time.perf_counter()
-        for _ in range(10):
+        for _ in range(iters):
             t0 = time.perf_counter()
             one_step()
             times.append(time.perf_counter() - t0)
@@ -571,7 +576,8 @@ def cpu_baseline(config, seconds):
             break
     times = min(rounds, key=lambda t: t[-1] / t[0])
     dt = times[len(times) // 2]
-    return {"value": round(pts / dt, 1), "unit": "collocation-points/s", "cores": cores, "kind": "port",
+    return {"value": round(pts / dt, 1), "value_min_time": round(pts / times[0], 1),
+            "unit": "collocation-points/s", "cores": cores, "kind": "port",
             "cpu_model": cpu_model(), "statistic": f"median of {len(times)} iterations after 2 warm-up",
             "spread_max_over_min": round(times[-1] / times[0], 3),
             # the explicit uncertainty of `value`: the sample's iteration rates span median x (1 +- u)
@@ -619,20 +625,12 @@ def rehearse(args, world, rank):
         dist.destroy_process_group()
 
 
-def main():
-    args = parse()
-    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
-        sys.exit(launch_ranks(args))
-    world, rank, local = setup_dist(args)
-    log(f"world={world} rank={rank}")
-    if args.rehearse:
-        return rehearse(args, world, rank)
-    model, cfg, wl, n_local = build_model(args, world, rank)
-    from base import _native
-    bwd_f16 = _native.bwd_f16_mask()  # the backward products on fp16 matrix cores in effect
-    nph = len(wl["phases"])
+def measure(args, model, wl, world):
+    """Warm-up (eager iteration, graph captures, one timestep in step() order, the U-iteration group
+    graphs, --warm-ms of sustained replays), then the timed region: --steps iterations of every phase as
+    up to 5 timesteps.  Returns (phase loops, elapsed s (max over ranks), per-timestep ms, iterations per
+    timestep, effective warm-up iterations)."""
     loops = phase_loops(model, wl)
-    log(f"model built, {n_local} points per rank per phase")
     # iteration 0 runs eagerly, iteration 1 captures the hipGraphs: both must be warm-up,
     # so at least 2 untimed iterations run even when --warmup < 2 (reported as warmup_effective)
     w_eff = max(args.warmup, 0 if args.no_graph else 2, 1)
@@ -689,6 +687,23 @@ def main():
     for pl in loops:  # which replay form each phase loop ended up with
         log(f"  {pl.tag}: graph {pl.graph is not None}, unroll {pl.unroll}, group graph {pl.graphU is not None}"
             + (f", capture error {pl.capture_error}" if getattr(pl, "capture_error", None) else ""))
+    return loops, elapsed, ts_ms, ks, w_eff
+
+
+def main():
+    args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args))
+    world, rank, local = setup_dist(args)
+    log(f"world={world} rank={rank}")
+    if args.rehearse:
+        return rehearse(args, world, rank)
+    model, cfg, wl, n_local = build_model(args, world, rank)
+    from base import _native
+    bwd_f16 = _native.bwd_f16_mask()  # the backward products on fp16 matrix cores in effect
+    nph = len(wl["phases"])
+    log(f"model built, {n_local} points per rank per phase")
+    loops, elapsed, ts_ms, ks, w_eff = measure(args, model, wl, world)
     # points all ranks processed: strong = the global batch, weak = world x the per-rank batch
     n_all = interior_points(cfg, wl) if (args.scaling == "strong" and args.shard_of == 1) else n_local * world
     total_points = n_all * nph * args.steps
@@ -724,6 +739,23 @@ def main():
         if rank == 0:
             result["roofline"] = roof
         log("roofline done")
+    plain_on = args.plain_line == "on" or (args.plain_line == "auto" and args.config == "fluid2Dtlgn")
+    if plain_on and world == 1 and args.api == "fused" and args.shard_of == 1:
+        # the drop-in number, driver-timed: the reference's phase bodies as written (pde/*_plain.py) on the
+        # same kernels, through the loop's lowering and deferred jets, same steps / warm-up / timing
+        pargs = argparse.Namespace(**vars(args))
+        pargs.api = "plain"
+        pmodel, _, _, _ = build_model(pargs, world, rank)
+        log("plain model built")
+        _, p_el, p_ts, p_ks, _ = measure(pargs, pmodel, wl, world)
+        p_val = n_all * nph * args.steps / p_el
+        p_per_ts = sorted((n_all * nph * k) / (ms * 1e-3) for k, ms in zip(p_ks, p_ts))
+        result["plain"] = {"value": round(p_val, 1), "ms_per_step": round(p_el / args.steps * 1e3, 4),
+                           "value_median_timestep": round(p_per_ts[len(p_per_ts) // 2], 1),
+                           "vs_fused": round(p_val / value, 3), "lowered": bool(pmodel._lower_on()),
+                           "model": f"pde/{wl['pde']}_plain.py: the reference's phase bodies as written "
+                                    "(reference base API only; base/lower.py lowers them)"}
+        log(f"plain line {p_val / 1e6:.1f} M pts/s")
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args.config, args.cpu_seconds)
         log("cpu baseline done")

@@ -125,6 +125,21 @@ class PhaseLoop:
         torch.cuda.current_stream(m.device).wait_stream(side)
         return g, out
 
+    _warned = set()
+
+    def _capture_failed(self, e, fallback):
+        """Record a failed hipGraph capture on the model (`_insr_capture_error`: tests assert it is None)
+        and warn once per (model class, phase, error type) -- a phase that silently ran eagerly had hidden
+        the round-5 el3D strong-path failure."""
+        self.capture_error = repr(e)
+        self.m._insr_capture_error = self.capture_error  # visible after run() (tests, logs)
+        key = (type(self.m).__name__, self.tag, type(e).__name__)
+        if key not in PhaseLoop._warned:
+            PhaseLoop._warned.add(key)
+            import warnings
+            warnings.warn(f"{type(self.m).__name__}.{self.tag}: hipGraph capture failed ({self.capture_error}); "
+                          f"{fallback}", RuntimeWarning, stacklevel=3)
+
     def _dp_split(self):
         """Whether a data-parallel iteration is replayed as two graphs around an EAGER all-reduce: the
         collective cannot be captured (gloo: host-side) or cfg.insr_dp_capture is off.  With RCCL
@@ -151,8 +166,7 @@ class PhaseLoop:
         except Exception as e:  # not capturable: stay eager
             torch.cuda.synchronize(self.m.device)
             self.use_graph = False
-            self.capture_error = repr(e)
-            self.m._insr_capture_error = self.capture_error  # visible after run() (tests, logs)
+            self._capture_failed(e, "the phase runs eagerly")
             self.graph = self.graph2 = None
             return None
         self.static = {k: v.detach() for k, v in out.items()}
@@ -181,7 +195,7 @@ class PhaseLoop:
             except Exception as e:  # not capturable as a group: iterate singly from now on
                 torch.cuda.synchronize(self.m.device)
                 self.unroll = 1
-                self.capture_error = repr(e)
+                self._capture_failed(e, "iterations replay one graph each")
                 self.graphU = None
                 return None
             self.staticU = {k: v.detach() for k, v in out.items()}

@@ -210,7 +210,7 @@ class BaseModel(ABC):
                 offs.append(off)
                 net.bind_flat_grad(arena[off:off + n])
                 off += n
-            self._insr_dp_offs, self._insr_dp_loss_off = offs, sizes[0]
+            self._insr_dp_offs, self._insr_dp_loss_off, self._insr_dp_nslots = offs, sizes[0], nslots
         offs, loss_off = self._insr_dp_offs, self._insr_dp_loss_off
         touched = [net.grad_touched() for net in nets]
         lo = min([loss_off] + [o for o, t in zip(offs, touched) if t])
@@ -239,6 +239,8 @@ class BaseModel(ABC):
         arena = self.__dict__.get("_insr_dp_arena")
         if not self._dp_active() or arena is None or loss_off is None:
             return
+        if len(loss_dict) > self.__dict__.get("_insr_dp_nslots", 0):
+            return  # more losses than the arena has slots: _dp_pack grows the arena and copies every loss
         direct = {}
         for i, (k, v) in enumerate(loss_dict.items()):
             hit = lazy_output(v)

@@ -23,6 +23,7 @@ What differs is storage and execution:
     aten addmm/sin chain, and tags its output with its provenance so the
     diff ops (base/diff_ops.py) can dispatch derivative jets.
 """
+import copy
 import math
 import weakref
 
@@ -170,15 +171,28 @@ class TorchMLP(nn.Module):
         return out * weights if weights is not None else out
 
 
+class _MLPArgs:
+    """MLP's constructor arguments by name (the signature of MLP.__init__), for __new__'s dispatch."""
+
+    def __init__(self, in_features, out_features, num_hidden_layers, hidden_features,
+                 outermost_linear=True, nonlinearity='relu', weight_init=None, precision=None):
+        self.in_features, self.out_features = in_features, out_features
+        self.num_hidden_layers, self.hidden_features = num_hidden_layers, hidden_features
+        self.outermost_linear, self.nonlinearity, self.weight_init = outermost_linear, nonlinearity, weight_init
+
+
 class MLP(nn.Module):
     """SIREN MLP with flat parameter storage and a HIP forward (base/networks.py:30-71).  A
     configuration the kernels do not serve (hip_served) is built as TorchMLP instead."""
 
-    def __new__(cls, in_features, out_features, num_hidden_layers, hidden_features,
-                outermost_linear=True, nonlinearity='relu', weight_init=None, precision=None):
-        if cls is MLP and not hip_served(nonlinearity, outermost_linear, hidden_features):
-            return TorchMLP(in_features, out_features, num_hidden_layers, hidden_features,
-                            outermost_linear=outermost_linear, nonlinearity=nonlinearity, weight_init=weight_init)
+    def __new__(cls, *args, **kwargs):
+        # copy.deepcopy / pickle rebuild through cls.__new__(cls) with no arguments: plain allocation then
+        if cls is MLP and (args or kwargs):
+            a = _MLPArgs(*args, **kwargs)
+            if not hip_served(a.nonlinearity, a.outermost_linear, a.hidden_features):
+                return TorchMLP(a.in_features, a.out_features, a.num_hidden_layers, a.hidden_features,
+                                outermost_linear=a.outermost_linear, nonlinearity=a.nonlinearity,
+                                weight_init=a.weight_init)
         return super().__new__(cls)
 
     def __init__(self, in_features, out_features, num_hidden_layers, hidden_features,
@@ -384,6 +398,23 @@ class MLP(nn.Module):
         self._flat_grad = gflat
         self._wsplit_stamp = None
         _FLAT_OWNERS[flat.data_ptr()] = self
+
+    def __deepcopy__(self, memo):
+        """nn.Module's deep copy (Parameters cloned one by one), then the copy's parameters moved into
+        a flat buffer of its own, so the copy is a packed MLP like the original (a model file keeping a
+        previous-step copy of its network with copy.deepcopy)."""
+        cls = type(self)
+        new = cls.__new__(cls)
+        memo[id(self)] = new
+        for k, v in self.__dict__.items():
+            if k in ("_flat", "_store", "_flat_grad"):  # rebuilt by _repack below
+                continue
+            new.__dict__[k] = copy.deepcopy(v, memo)
+        new._flat = new._store = new._flat_grad = None
+        new._repack()
+        if new._flat.is_cuda:
+            new.refresh_wsplit()
+        return new
 
     # ---- snapshots: prev = net.state_dict() ----------------------------------------
     def _snapshot_source(self, state_dict):

@@ -84,8 +84,8 @@ class ElasticityModel(BaseModel):
     # distribution; no rank draws the world-sized batch).  cfg.insr_dp_weak: every rank draws the whole
     # batch (weak scaling).  cfg.insr_shard = (r, K): one process runs rank r's share of a K-rank strong
     # run (bench.py --shard-of K measures exactly this code).  Ranks draw independent points: the device
-    # samplers fold the rank into their key (base.sampling.sampler_seed), the mesh sampler uses a
-    # generator seeded the same way (_mesh_generator).
+    # samplers fold the rank into their key (base.sampling.sampler_seed); a sharded rank's mesh draw takes
+    # its uniforms from the same device stream (_mesh_draw; on the CPU a generator keyed alike).
     def _shard(self):
         """(r, K): this process's share of the global batch (K = 1: the whole batch)."""
         emu = getattr(self.cfg, "insr_shard", None)
@@ -102,10 +102,27 @@ class ElasticityModel(BaseModel):
         a, b = r * n // k, (r + 1) * n // k
         return a, b - a
 
+    def _mesh_draw(self, sampler, n):
+        """n volume-weighted mesh points (elasticity/model.py:200-207).  One unsharded rank: torch's default
+        generator, as the reference (a hipGraph capture registers it).  A rank of a sharded run on the GPU:
+        the uniforms come from the rank-keyed device Philox sampler (base.sampling.sample_boxes, the box
+        scenes' stream) -- capturable, each replay draws fresh points, and ranks seeded alike draw
+        independent points.  (A private torch.Generator is not registered with the capture: the strong
+        path's graph came out empty and the phase ran eagerly, round 5.)  On the CPU: _mesh_generator."""
+        r, k = self._shard()
+        if (k == 1 and self._dp_world() == 1) or torch.device(self.device).type != "cuda":
+            return sampler.sample(n, generator=self._mesh_generator())
+        from base.sampling import sample_boxes
+        m = sampler.uniforms_per_point()  # 6 (tets) or 4 (triangles): n * m / 2 rows of 2 or 3 coordinates
+        dim = 3 if m % 3 == 0 else 2
+        u = sample_boxes([(n * m // dim, (0.0,) * dim, (1.0,) * dim)], dim, device=self.device) if n > 0 else \
+            torch.zeros(0, dim, device=self.device)
+        return sampler.sample(n, uniforms=u.view(n, m))
+
     def _mesh_generator(self):
-        """None (the default CUDA generator, as the reference) on one unsharded rank; else a device
-        generator keyed by the torch seed with the rank folded in (base.sampling.sampler_seed), re-made
-        when torch is re-seeded -- ranks seeded alike still draw independent mesh points."""
+        """None (the default generator, as the reference) on one unsharded rank; else (a CPU rank of a
+        sharded run) a generator keyed by the torch seed with the rank folded in (base.sampling.sampler_seed),
+        re-made when torch is re-seeded -- ranks seeded alike still draw independent mesh points."""
         r, k = self._shard()
         world = self._dp_world()
         if k == 1 and world == 1:
@@ -113,7 +130,11 @@ class ElasticityModel(BaseModel):
         from base.sampling import reseed_epoch, sampler_seed
         rank = r if k > 1 else torch.distributed.get_rank()
         dev = torch.device(self.device)
-        seed = torch.cuda.default_generators[dev.index or 0].initial_seed() if dev.type == "cuda" else torch.initial_seed()
+        if dev.type == "cuda":
+            idx = dev.index if dev.index is not None else torch.cuda.current_device()
+            seed = torch.cuda.default_generators[idx].initial_seed()
+        else:
+            seed = torch.initial_seed()
         key = (seed, reseed_epoch(), rank)
         cached = self.__dict__.get("_insr_mesh_gen")
         if cached is None or cached[0] != key:
@@ -129,7 +150,7 @@ class ElasticityModel(BaseModel):
             if s == 'random':
                 n = self._rows(resolution ** d)[1]
                 if self.use_mesh:  # elasticity/model.py:200-207: volume-weighted points of the mesh
-                    parts.append(self.mesh_sampler.sample(n, generator=self._mesh_generator())[:, :d])
+                    parts.append(self._mesh_draw(self.mesh_sampler, n)[:, :d])
                 else:
                     parts.append(sample_random(n, d, device=self.device).requires_grad_(True))
             elif s == 'uniform':
@@ -285,6 +306,14 @@ class ElasticityModel(BaseModel):
         constraint terms need go through ONE jet launch of the deformation field
         (base.merge_samples, or the caller's merged buffer xa); every term reads its rows."""
         dt, n = self.dt, x.shape[0]
+        if self.dim == 3 and 'collision_sphere' in self.energy and self._shard()[1] > 1 and \
+                not self.__dict__.get("_insr_sphere_warned"):
+            self._insr_sphere_warned = True
+            import warnings
+            warnings.warn("elasticity: the 3-D collision_sphere term is a product of two sums over the batch "
+                          "(elasticity/losses.py:35); a rank of a strong-scaling run forms it from its own shard's "
+                          "sums, so the all-reduced energy is not the single-process one (DESIGN.md §7)",
+                          RuntimeWarning, stacklevel=2)
         use_l = 'constraint' in self.energy
         use_r = any(t in self.energy for t in ('constraint_right', 'constraint_right_compress'))
         parts = [x] + ([fixed_l] if use_l else []) + ([fixed_r] if use_r else [])

@@ -131,16 +131,33 @@ class MeshSampler:
         self.corners = V[E].to(self.device, torch.float32)  # (k, 3|4, dim) vertex coordinates per element
         self.k = E.shape[0]
 
-    def sample(self, n, generator=None):
-        u = torch.rand(n, device=self.device, dtype=torch.float64, generator=generator)
+    def uniforms_per_point(self):
+        """Uniform [0, 1) draws one sample() point consumes when they are handed in (`uniforms`): two for
+        the element (one float64 of 48 bits) and 4 (tet barycentrics) or 2 (triangle)."""
+        return 2 + self.corners.shape[1] if self.corners.shape[1] == 4 else 4
+
+    def sample(self, n, generator=None, uniforms=None):
+        """n points; torch.rand draws from `generator` (None: torch's default), or the caller's
+        (n, uniforms_per_point()) fp32 uniforms in [0, 1) with 24-bit resolution (the rank-keyed device
+        Philox stream under data parallelism, which a hipGraph capture replays with fresh draws)."""
+        if uniforms is not None:
+            if tuple(uniforms.shape) != (n, self.uniforms_per_point()):
+                raise ValueError(f"uniforms: ({n}, {self.uniforms_per_point()}) expected, got {tuple(uniforms.shape)}")
+            ud = uniforms.to(torch.float64)
+            u = ud[:, 0] + ud[:, 1] * 2.0 ** -24  # two 24-bit draws: one uniform of 48 bits
+            rest = uniforms[:, 2:]
+        else:
+            u = torch.rand(n, device=self.device, dtype=torch.float64, generator=generator)
+            rest = None
         idx = torch.searchsorted(self.cdf, u, right=True).clamp_(max=self.k - 1)
         cor = self.corners[idx]  # (n, 3|4, dim)
         if cor.shape[1] == 4:
             # Dirichlet(1, 1, 1, 1) barycentrics = normalised Exp(1) draws
-            e = -torch.log(torch.rand(n, 4, device=self.device, generator=generator).clamp_min(1e-30))
+            r4 = rest if rest is not None else torch.rand(n, 4, device=self.device, generator=generator)
+            e = -torch.log(r4.clamp_min(1e-30))
             bary = e / e.sum(dim=1, keepdim=True)
         else:  # (1 - sqrt(r1), sqrt(r1)(1 - r2), sqrt(r1) r2)  (torchgp/sample_surface.py)
-            r = torch.rand(n, 2, device=self.device, generator=generator)
+            r = rest if rest is not None else torch.rand(n, 2, device=self.device, generator=generator)
             su = torch.sqrt(r[:, :1])
             bary = torch.cat([1 - su, su * (1 - r[:, 1:]), su * r[:, 1:]], dim=1)
         return torch.sum(bary.unsqueeze(-1) * cor, dim=1)

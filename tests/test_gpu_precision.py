@@ -1,12 +1,14 @@
-"""Reduced-precision jets (MLP(precision=...), per-call precision bits of the jet mode) vs
-the CPU oracle.  The fp32 parity configs run at the default 'bf16x6' (test_gpu_parity.py,
-1e-5); these are the OPT-IN variants a user selects per network, each with the normwise
-tolerance (max |hip - oracle| / max |oracle|, per tensor) it is documented with in DESIGN.md:
+"""Jet precisions (MLP(precision=...), per-call precision bits of the jet mode) vs the CPU
+oracle.  The fp32 parity configs run at the library default -- f16x3 products in every forward and
+(through the backward's fp16 product mask, INSR_JET_BWD_F16 = 7, and the resident f16x3 Laplacian
+sweep) in the backwards, the bf16x6 contract where a kernel has no fp16 products (test_gpu_parity.py,
+1e-5).  Each precision below is held to the normwise tolerance (max |hip - oracle| / max |oracle|, per
+tensor) it is documented with in DESIGN.md:
 
-    bf16x6  6 bf16 products per fp32 product (default)   1e-5   (measured <= 5e-6)
-    f16x3   forward: 2^k-scaled operands in two fp16 terms, 3 products; backward bf16x6
-            1e-5   (the default forward since round 3; measured fields <= 4.2e-6, gradients
-            <= 5.1e-6, profiles/r03/prec_f16x3.jsonl -- x6: 3.5e-6 / 5.1e-6)
+    f16x3   2^k-scaled operands in two fp16 terms, 3 products (the default)   1e-5
+            (measured fields <= 4.2e-6, gradients <= 5.1e-6, profiles/r03/prec_f16x3.jsonl; the
+            round-5 defaults as the bench runs them: profiles/r05/prec_defaults.jsonl, <= 3.5e-6)
+    bf16x6  6 bf16 products per fp32 product (opt-in)     1e-5   (measured <= 5e-6)
     bf16x3  3 products (hi*hi + hi*lo + lo*hi)             5e-5   (measured <= 3.3e-5)
     bf16    1 product, fp32 accumulation                   2.5e-2 (measured <= 1.6e-2)
     mixed   bf16x3 forwards / bf16 backwards              1e-2   (measured: fields <= 2.1e-5,

@@ -108,3 +108,23 @@ def test_reference_import_surface(B):
              "sample_uniform", "sample_boundary", "sample_boundary2D_separate", "MLP", "Sine", "get_network"]
     for n in names:
         assert hasattr(B, n), n
+
+
+def test_deepcopy_round_trip(B):
+    """copy.deepcopy rebuilds through MLP.__new__(cls) with no arguments (a model file keeping a
+    previous-step copy of its network): the copy is an MLP with equal parameters on storage of its
+    own, still one flat buffer; a TorchMLP deep-copies as well."""
+    import copy
+    torch.manual_seed(0)
+    a = B.MLP(2, 1, 2, 64, nonlinearity="sine")
+    b = copy.deepcopy(a)
+    assert type(b) is type(a)
+    assert torch.equal(a.flat_params(), b.flat_params())
+    assert b.flat_params().data_ptr() != a.flat_params().data_ptr()
+    for p in b.parameters():  # the copy's parameters are views of the copy's flat buffer
+        assert b.flat_params().data_ptr() <= p.data_ptr() < b.flat_params().data_ptr() + 4 * b.param_count
+    with torch.no_grad():
+        next(b.parameters()).add_(1.0)
+    assert not torch.equal(a.flat_params(), b.flat_params())
+    t = copy.deepcopy(B.MLP(2, 1, 2, 64, nonlinearity="relu"))
+    assert type(t).__name__ == "TorchMLP"
