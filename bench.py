@@ -102,6 +102,13 @@ def parse():
                     help="one process runs the data-parallel iteration itself (gradient arena, a world-1 RCCL "
                          "all-reduce between the two graphs, unfused sums + Adam): a rank's DP step measured on "
                          "one GPU (with --shard-of K: the K-rank strong run's rank step)")
+    ap.add_argument("--no-frozen-ahead", action="store_true",
+                    help="fluid: evaluate the frozen networks inside each iteration's mixed forward launch (A/B; "
+                         "default: once per replayed group of U iterations, base.sampling.frozen_ahead)")
+    ap.add_argument("--frozen-stream", action="store_true",
+                    help="fluid: run the group's frozen-network evaluation on a side stream (A/B)")
+    ap.add_argument("--frozen-pipe", action="store_true",
+                    help="fluid: frozen-network work per iteration on a side stream, one iteration ahead (A/B)")
     ap.add_argument("--no-seed-in-bwd", action="store_true",
                     help="launch every loss group (A/B studies; default: the fluid / advection bodies' groups are "
                          "evaluated inside the reverse jets, base/losses.py lazy_losses)")
@@ -211,7 +218,8 @@ def build_model(args, world, rank):
     res = wl["res"]
     cfg = baseline_config(args.config, sample_resolution=res, insr_graph=not args.no_graph, insr_dp_always=args.dp_path,
                           insr_graph_unroll=max(1, args.graph_unroll), insr_seed_in_bwd=not args.no_seed_in_bwd,
-                          insr_defer_jets=not args.no_defer_jets,
+                          insr_defer_jets=not args.no_defer_jets, insr_frozen_ahead=False if args.no_frozen_ahead else ("pipe" if args.frozen_pipe else True),
+                          insr_frozen_stream=args.frozen_stream,
                           insr_sync_every=10 ** 9, insr_progress=False, early_stop=False,
                           proj_dir="/tmp/insr_bench", max_n_iters=10 ** 9,
                           insr_precision=None if args.precision == "fp32" else args.precision)
@@ -724,6 +732,8 @@ def main():
                    "jet_precision": jet_precision_names(args.precision),
                    "bwd_policy": args.bwd_policy, "shard_of": args.shard_of, "dp_path": args.dp_path,
                    "seeds_in_bwd": bool(getattr(cfg, "insr_seed_in_bwd", True)),
+                   "frozen_ahead": bool(getattr(cfg, "insr_frozen_ahead", True)) and wl["pde"] == "fluid"
+                   and args.api == "fused", "frozen_stream": bool(args.frozen_stream), "frozen_pipe": bool(args.frozen_pipe),
                    "lowered": bool(model._lower_on()), "deferred_jets": bool(model._defer_on()),
                    "bwd_f16": bwd_f16,
                    "timestep_order": f"{nts} timesteps x ({'/'.join(str(k) for k in ks)}) iterations per phase, "

@@ -102,6 +102,8 @@ def _resolve(y, x, opname):
     """(mlp, holder, affine) of a recognised SIREN graph, ("gradient-of", ...) for the divergence of a
     jet gradient, or None (the reference-semantics route)."""
     m = _jet.match(y, x)
+    if m is not None and _lower.affine_operand():  # f of a recorded q = f(x) + x (base/lower.py api)
+        m = (m[0], m[1], True)
     if m is None:
         gsrc = getattr(y, "_insr_gradient_of", None)
         if gsrc is not None and gsrc[1] is x and opname == "divergence":
@@ -210,9 +212,17 @@ def laplace(y, x, normalize=False, eps=0., return_grad=False):
 def jacobian(y: torch.FloatTensor, x: torch.FloatTensor):
     """(N, dim_y, dim_x) Jacobian and status (-1 if NaN) (base/diff_ops.py:61-82)."""
     J = jacobian_only(y, x)
+    if _lower.deferring():
+        # the reference's NaN status (a host read) as a Lazy 0-dim tensor computed only when a body reads it:
+        # no launch, no sync, and the iteration stays capturable (elasticity/model.py:143 discards it)
+        return J, _lower.lazy_call(_nan_status, (J,), (), torch.int64, J.device)
     _lower.flush()  # the status reads the values
     status = -1 if bool(torch.isnan(J).any()) else 0
     return J, status
+
+
+def _nan_status(J):
+    return torch.where(torch.isnan(J).any(), -1, 0)
 
 
 @_api
@@ -233,9 +243,8 @@ def jacobian_only(y, x):
         return _ref_jacobian_rows(y, x)
     mlp, value, affine = r
     _, J, _ = res
-    if affine:
-        _lower.flush()
-        J = J + torch.eye(J.shape[-1], device=J.device, dtype=J.dtype)
+    if affine:  # J + I: recorded while jets are deferred (an energy lowering reads J itself, base/lower.py)
+        return _lower.eye_add(J, (mlp, res[0], x))
     return J
 
 

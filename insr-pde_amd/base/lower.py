@@ -33,13 +33,15 @@ import threading
 
 import torch
 
-__all__ = ["Lazy", "lowering", "deferred_jets", "deferring", "flush", "immediate", "add_views", "suspended", "api",
-           "sampler_api", "active", "leaf", "materialize", "plan", "lower_losses", "LOWERED"]
+__all__ = ["Lazy", "lowering", "deferred_jets", "deferring", "flush", "immediate", "add_views", "eye_add", "lazy_call",
+           "suspended", "api", "sampler_api", "active", "leaf", "materialize", "plan", "energy_plan", "lower_losses",
+           "LOWERED"]
 
-LOWERED = {"groups": 0, "terms": 0, "eager_losses": 0, "materialized": 0}  # counters (tests, docs)
+LOWERED = {"groups": 0, "terms": 0, "eager_losses": 0, "materialized": 0, "energies": 0}  # counters (tests, docs)
 
 
 class _State(threading.local):
+    affine = False  # the running diff op's operand is f of a recorded f(x) + x (api, _affine_operand)
     depth = 0
     defer = 0  # > 0: network / diff-op jets are queued (a fused_forwards scope) and launched at the first read
     nodes = None  # the recorded nodes of the open scope (evaluated before an in-place op, see _pin_all)
@@ -164,12 +166,13 @@ def add_views(a, b):
 # tensor a recorded expression reads) raises instead of computing with the new values.
 class _Node:
     __slots__ = ("kind", "kids", "coef", "k", "lo", "hi", "real", "real_ng", "call", "shape", "grad_mode", "ver",
-                 "ready")
+                 "ready", "meta")
 
     def __init__(self, kind, kids=(), coef=None, k=None, lo=None, hi=None, real=None, call=None, shape=None):
         self.kind, self.kids, self.coef, self.k, self.lo, self.hi = kind, tuple(kids), coef, k, lo, hi
         self.real, self.real_ng, self.call, self.shape = real, None, call, shape
         self.ready = False  # real holds final values no queued jet writes (a sampler's draw, or c times one)
+        self.meta = None  # (eyeadd) the Jacobian jet's provenance: (mlp, value f, x)
         self.grad_mode = torch.is_grad_enabled()
         self.ver = real._version if real is not None else None
 
@@ -330,19 +333,49 @@ def api(fn, operand_first=False):
             r = _advect_target(args[0], args[1])
             if r is not None:
                 return leaf(r)
+        affine = False
         if operand_first and args:
-            args = (_api_tree(args[0]),) + tuple(_real_tree(a) for a in args[1:])
+            rest = tuple(_real_tree(a) for a in args[1:])
+            f = _affine_operand(args[0], rest[0] if rest else None)
+            if f is not None:  # q = f(x) + x still recorded: the diff op takes f with the identity added
+                args, affine = (f,) + rest, True
+            else:
+                args = (_api_tree(args[0]),) + rest
         else:
             args = _real_tree(args)
         kwargs = _real_tree(kwargs)
         if not active():
             return fn(*args, **kwargs)
-        with suspended():
-            r = fn(*args, **kwargs)
+        _S.affine = affine
+        try:
+            with suspended():
+                r = fn(*args, **kwargs)
+        finally:
+            _S.affine = False
         if isinstance(r, tuple):
             return tuple(leaf(v) for v in r)
         return leaf(r)
     return w
+
+
+def _affine_operand(v, x):
+    """f when v is the recorded q = f + x (x + f) of a network output f at x (elasticity/model.py:137), else None."""
+    if not isinstance(v, Lazy) or x is None:
+        return None
+    n = v._insr_node
+    if n.kind != "lin" or len(n.kids) != 2 or tuple(n.coef) != (1.0, 1.0) or any(k.kind != "leaf" for k in n.kids):
+        return None
+    a, b = n.kids
+    for f, y in ((a, b), (b, a)):
+        src = getattr(f.real, "_insr_src", None)
+        if y.real is x and src is not None and src[1] is x and f.real.shape == x.shape and not _stale(n):
+            return f.real
+    return None
+
+
+def affine_operand():
+    """Whether the diff op running now was handed f of a recorded f(x) + x (its result adds the identity)."""
+    return getattr(_S, "affine", False)
 
 
 def _advect_target(mlp, foot):
@@ -416,6 +449,43 @@ def _record(name, func, args, kwargs):
     like = next((a for a in tens if isinstance(a, Lazy)), None)
     if like is None or like.dtype != torch.float32:
         return None
+    if name in ("add", "sub", "__radd__", "__rsub__") and len(args) == 2 and set(kwargs) <= {"alpha"} and \
+            isinstance(args[0], Lazy) and _scalar(args[1]) is not None and _scalar(kwargs.get("alpha", 1.0)) is not None:
+        # x + c, x - c (S - 1.0, q_fixed - 0: elasticity/model.py:146-147, losses.py:7), c + x, c - x
+        x, c = args[0], _scalar(args[1]) * _scalar(kwargs.get("alpha", 1.0))
+        nx = x._insr_node
+        if name == "__rsub__":
+            nx = _Node("lin", (nx,), coef=(-1.0,), call=None, shape=nx.shape)
+        return _lazy_of("off", (nx,), call, nx.shape, like, _req(x), lo=(-c if name == "sub" else c))
+    if name == "prod" and isinstance(args[0], Lazy) and len(args[0]._insr_node.shape) == 2 and \
+            ((len(args) == 2 and not kwargs) or (len(args) == 1 and set(kwargs) == {"dim"})):
+        x = args[0]
+        dim = args[1] if len(args) == 2 else kwargs["dim"]
+        if not isinstance(dim, int) or dim % 2 != 1:
+            return None
+        return _lazy_of("prod", (x._insr_node,), call, x._insr_node.shape[:1], like, _req(x), k=1)
+    if name == "mul" and len(args) == 2 and not kwargs and _scalar(args[0]) is None and _scalar(args[1]) is None:
+        # x * T with a constant tensor T of x's shape (elasticity/model.py:149's external-force product)
+        x, y = args
+        if not isinstance(x, Lazy):
+            x, y = y, x
+        if isinstance(x, Lazy) and isinstance(y, torch.Tensor) and not isinstance(y, Lazy) and not y.requires_grad:
+            ny = _operand(y)
+            if ny is not None and ny.shape == x._insr_node.shape:
+                return _lazy_of("mulT", (x._insr_node, ny), call, x._insr_node.shape, like, _req(x, y))
+        return None
+    if name == "svd" and len(args) == 1 and not kwargs and isinstance(args[0], Lazy) and \
+            len(args[0]._insr_node.shape) == 3 and args[0]._insr_node.shape[1] == args[0]._insr_node.shape[2]:
+        # torch.svd(J) of a batch of square Jacobians (elasticity/model.py:144): three Lazy parts of ONE svd
+        # node, evaluated (torch.svd) only when a part's value is read
+        x = args[0]
+        nd = x._insr_node
+        parent = _Node("svd", (nd,), call=call, shape=nd.shape)
+        _register(parent)
+        req = _req(x)
+        shapes = (nd.shape, nd.shape[:2], nd.shape)
+        return tuple(_lazy_of("svdpart", (parent,), (_svd_part, (parent, i), {}), shapes[i], like, req, k=i)
+                     for i in range(3))
     if name in ("add", "sub") and len(args) == 2 and set(kwargs) <= {"alpha"}:
         x, y = args
         nx, ny = _operand(x), _operand(y)
@@ -489,6 +559,33 @@ def _record(name, func, args, kwargs):
         return _lazy_of("clamp", (x._insr_node,), call, x._insr_node.shape, like, _req(x), lo=_scalar(lo),
                         hi=_scalar(hi))
     return None
+
+
+def _svd_part(parent, i):
+    """Part i (U, S, V) of a recorded torch.svd, the decomposition computed once."""
+    return _eval(parent)[i]
+
+
+def eye_add(J, meta):
+    """J + I of a Jacobian jet J (the affine f(x) + x of elasticity/model.py:137,143): recorded while jets are
+    deferred (J has no values yet; an energy lowering reads J itself), else added now.  meta = (mlp, value,
+    x) of the jet."""
+    eye = torch.eye(J.shape[-1], device=J.device, dtype=J.dtype)
+    if not deferring():
+        return J + eye
+    leafJ = _Node("leaf", real=J, shape=tuple(J.shape))
+    n = _Node("eyeadd", (leafJ,), call=(torch.add, (J, eye), {}), shape=tuple(J.shape))
+    n.meta = meta
+    _register(n)
+    return _wrap(n, J.dtype, J.device, torch.is_grad_enabled() and J.requires_grad)
+
+
+def lazy_call(fn, args, shape, dtype, device):
+    """A Lazy result of fn(*args) with no autograd, computed only when its value is read (the NaN status of
+    jacobian(): the reference's host read, elasticity/model.py:143, which no body uses)."""
+    n = _Node("call", (), call=(fn, args, {}), shape=tuple(shape))
+    _register(n)
+    return _wrap(n, dtype, device, False)
 
 
 # ---- materialisation --------------------------------------------------------------------------
@@ -628,6 +725,8 @@ def _atoms(n, c=1.0, acc=None, det=False):
         return acc
     if n.kind == "detach":
         return _atoms(n.kids[0], c, acc, True)
+    if n.kind == "off" and n.lo == 0.0:  # x - 0 (a positional constraint's zero target)
+        return _atoms(n.kids[0], c, acc, det)
     if n.kind == "sel":
         base = n.kids[0]
         while base.kind == "detach":
@@ -719,6 +818,118 @@ def _spec(n):
     return L.mse_term(a, b, c, d, alpha=alpha, beta=beta, gamma=gamma, delta=delta, reduction=red, weight=w)
 
 
+# ---- elastodynamics energies (elasticity/model.py:127-189, losses.py:6-8) ----------------------------
+def _lin_terms(n, w=1.0, out=None):
+    """n as [(w_i, T_i)] with n = sum_i w_i T_i through 'lin' nodes and zero offsets (loss = 0; loss = loss + E)."""
+    out = [] if out is None else out
+    if n.kind == "lin":
+        for c, kid in zip(n.coef, n.kids):
+            _lin_terms(kid, w * c, out)
+    elif n.kind == "off" and n.lo == 0.0:
+        _lin_terms(n.kids[0], w, out)
+    else:
+        out.append((w, n))
+    return out
+
+
+def _svd_of(n):
+    """The svd node whose singular values n is (an 'svdpart' k = 1), or None."""
+    return n.kids[0] if n.kind == "svdpart" and n.k == 1 else None
+
+
+def _energy_term(T):
+    """('arap' | 'volume', svd node) when T = sum((S - 1)^2) / sum((prod(S, 1) - 1)^2) over the singular values S
+    of a recorded torch.svd, else None."""
+    if T.kind != "sum" or T.kids[0].kind != "sq":
+        return None
+    X = T.kids[0].kids[0]
+    if X.kind != "off" or X.lo != -1.0:
+        return None
+    Y = X.kids[0]
+    sv = _svd_of(Y)
+    if sv is not None:
+        return "arap", sv
+    if Y.kind == "prod" and Y.k == 1:
+        sv = _svd_of(Y.kids[0])
+        if sv is not None:
+            return "volume", sv
+    return None
+
+
+def energy_plan(n):
+    """The loss node of an unchanged elasticity body as [(kind, weight, payload)], or None:
+      ('energy', w, (term, svd node))   w * E_term from the singular values of J + I (one insr_elastic_energy
+                                         launch for every such term: arap, volume)
+      ('sq', w, plan)                    w * a sum / mean of squares of a linear residual (the positional
+                                         constraints, kinematics): one term of the loss group
+      ('eager', w, node)                 anything else, materialised as written
+    The singular values must be those of the Jacobian jet of f(x) + x (jacobian(q, x), an eyeadd node)."""
+    if _stale(n):
+        return None
+    terms = _lin_terms(n)
+    out, svds = [], set()
+    for w, T in terms:
+        e = _energy_term(T)
+        if e is not None:
+            J = e[1].kids[0]
+            if J.kind != "eyeadd" or J.meta is None:
+                return None
+            svds.add(id(e[1]))
+            out.append(("energy", w, e))
+            continue
+        p = plan(T) if T.kind in ("sum", "mean") else None
+        if p is not None and p[0] == "combo":
+            out.append(("sq", w, p))
+        else:
+            out.append(("eager", w, T))
+    if not any(k == "energy" for k, _, _ in out) or len(svds) != 1:
+        return None
+    return out
+
+
+def _energy_loss(ep):
+    """Evaluate an energy_plan: ONE insr_elastic_energy launch for the singular-value terms, ONE loss-group
+    launch for the squared residuals, the rest eager; their sum."""
+    from .losses import elastic_energy, mse_term, sq_losses
+    parts = []
+    order, ratios, svd = [], {}, None
+    for kind, w, pay in ep:
+        if kind == "energy":
+            term, svd = pay
+            if term in ratios:  # the same term twice: weights add (the kernel has one slot per term)
+                ratios[term] += w
+            else:
+                order.append(term)
+                ratios[term] = w
+    Jn = svd.kids[0]
+    mlp, f, x = Jn.meta
+    Jraw = Jn.kids[0].real
+    flush()
+    n = f.shape[0]
+    total, _ = elastic_energy(f, Jraw, x, f.detach(), f.detach(), n=n, dt=1.0, energy=order, ratios=ratios)
+    parts.append(total)
+    specs = []
+    for kind, w, pay in ep:
+        if kind == "sq":
+            (a, b, c, d), (alpha, beta, gamma, delta), w2, red = pay[1], pay[2], pay[3], pay[4]
+            specs.append(mse_term(a, b, c, d, alpha=alpha, beta=beta, gamma=gamma, delta=delta, reduction=red,
+                                  weight=w * w2))
+        elif kind == "eager":
+            LOWERED["eager_losses"] += 1
+            v = _eval(pay) if pay.real is None else pay.real
+            parts.append(v * w if w != 1.0 else v)
+    from . import _native as nat
+    for i in range(0, len(specs), nat.LOSS_GROUP_MAX):
+        parts.extend(sq_losses(*specs[i:i + nat.LOSS_GROUP_MAX]))
+        LOWERED["groups"] += 1
+    LOWERED["energies"] = LOWERED.get("energies", 0) + 1
+    LOWERED["terms"] += len(order) + len(specs)
+    res = parts[0]
+    for v in parts[1:]:
+        res = res + v
+    return res
+
+
 def lower_losses(loss_dict):
     """The loss dict a phase body returned inside lowering(), with every recognised Lazy loss computed by
     ONE fused loss-group launch (per LOSS_GROUP_MAX losses) and every other Lazy loss materialised."""
@@ -727,13 +938,19 @@ def lower_losses(loss_dict):
     flush()  # (the loop calls this after its deferred scope closed: nothing is queued any more)
     from . import _native as nat
     from .losses import sq_losses
-    specs, slot = [], {}
+    specs, slot, energies = [], {}, {}
     for k, v in loss_dict.items():
         if isinstance(v, Lazy):
             sp = _spec(v._insr_node)
             if sp is not None:
                 slot[k] = len(specs)
                 specs.append(sp)
+            else:
+                ep = energy_plan(v._insr_node)
+                if ep is not None and all(
+                        all(t is None or t.is_cuda for t in p[1]) for kind, _, p in ep if kind == "sq") and \
+                        all(p[1].kids[0].kids[0].real.is_cuda for kind, _, p in ep if kind == "energy"):
+                    energies[k] = ep
     outs = []
     for i in range(0, len(specs), nat.LOSS_GROUP_MAX):
         outs.extend(sq_losses(*specs[i:i + nat.LOSS_GROUP_MAX]))
@@ -743,6 +960,8 @@ def lower_losses(loss_dict):
     for k, v in loss_dict.items():
         if k in slot:
             res[k] = outs[slot[k]]
+        elif k in energies:
+            res[k] = _energy_loss(energies[k])
         elif isinstance(v, Lazy):
             LOWERED["eager_losses"] += 1
             res[k] = materialize(v)

@@ -267,12 +267,24 @@ class draw_ahead:
 
     def __enter__(self):
         self.saved, self.store, self.key, self.pos = draw_ahead.active, None, None, 0
+        self.frozen = {}  # frozen_ahead results of this group, by name
         draw_ahead.active = self if self.reps > 1 else None
         return self
 
     def __exit__(self, *exc):
         draw_ahead.active = self.saved
         return False
+
+    def group_of(self, buf):
+        """(store, k) when `buf` is (a leading-row view of) iteration k's buffer of this group's draw, else None."""
+        st = self.store
+        if st is None or buf.dim() != 2 or buf.shape[1] != st.shape[2] or buf.dtype != st.dtype:
+            return None
+        off = buf.data_ptr() - st.data_ptr()
+        rb = st.shape[1] * st.shape[2] * st.element_size()
+        if off < 0 or off % rb or off // rb >= st.shape[0] or not buf.is_contiguous():
+            return None
+        return st, off // rb
 
     def take(self, key, rows, dev, draw):
         if self.store is None:
@@ -284,6 +296,94 @@ class draw_ahead:
         buf = self.store[self.pos]
         self.pos += 1
         return buf
+
+
+def frozen_ahead(name, x, fn, stream=None, pipe=False):
+    """Work on FROZEN networks for the iterations of a draw_ahead group, ahead of the iterations themselves.
+    `x` is an iteration's merged draw (or its leading rows) from the group's store; `fn(X)` evaluates the
+    frozen networks at points X (no autograd) and returns a tuple of tensors whose rows follow X's.  Exact for
+    networks no iteration of the group trains (the previous-step field, the other field of a phase): their
+    outputs at the group's points do not depend on any iteration's update.  Returns iteration k's outputs
+    (rows [:x.shape[0]]), or None outside a group (U = 1, eager iterations): the caller computes its own.
+
+      batched (pipe=False): on the group's first call of `name` fn runs ONCE on all U buffers (U x rows points:
+          one launch per jet instead of U latency-bound shares of a mixed launch; the band rows and the other
+          iterations' rows are computed too).  stream: run it on this side stream (forked after the group's
+          draw), overlapping the first iteration's trained-network forward.
+      pipelined (pipe=True, stream required): fn runs per iteration on its own points, on the side stream, one
+          iteration AHEAD: frozen_join(name) (called by the body after its trained-network forward) waits for
+          iteration k's outputs and issues iteration k + 1's, which then run under iteration k's reverse jets,
+          gradient all-reduce and Adam step -- the latency-bound tail of a backward launch and the collective
+          leave most CUs idle.
+    The caller calls frozen_join(name) before the first read of the outputs whenever a stream is given (a group
+    runs under hipGraph capture: the forks and joins become graph edges)."""
+    da = draw_ahead.active
+    if da is None:
+        return None
+    hit = da.group_of(x)
+    if hit is None:
+        return None
+    st, k = hit
+    U, rows, n = st.shape[0], st.shape[1], x.shape[0]
+    if pipe and stream is not None:
+        ent = da.frozen.get(name)
+        if ent is None:  # iteration 0: its own outputs, on the side stream, forked here
+            ent = da.frozen[name] = {"fn": fn, "stream": stream, "n": n, "outs": {}, "ev": {}}
+            _frozen_issue(da, name, 0)
+        if k not in ent["outs"]:
+            raise RuntimeError(f"frozen_ahead({name!r}): iteration {k}'s outputs were not issued (frozen_join "
+                               "must follow every iteration's call)")
+        ent["cur"] = k
+        return ent["outs"][k]
+    outs = da.frozen.get(name)
+    if outs is None:
+        X = st.view(-1, st.shape[2]).detach().requires_grad_(True)
+        if stream is not None:
+            stream.wait_stream(torch.cuda.current_stream(st.device))
+            with torch.cuda.stream(stream), torch.no_grad():
+                outs = tuple(fn(X))
+            ev = torch.cuda.Event()
+            ev.record(stream)
+            da.frozen[name + "/join"] = ev
+        else:
+            with torch.no_grad():
+                outs = tuple(fn(X))
+        da.frozen[name] = outs
+    return tuple(o.view(U, rows, *o.shape[1:])[k, :n] for o in outs)
+
+
+def _frozen_issue(da, name, k):
+    """Pipelined frozen_ahead: iteration k's frozen outputs on the side stream, forked from the current stream
+    now (so they run after everything issued so far, beside everything issued later)."""
+    ent = da.frozen[name]
+    st, side = da.store, ent["stream"]
+    X = st[k, :ent["n"]].detach().requires_grad_(True)
+    side.wait_stream(torch.cuda.current_stream(st.device))
+    with torch.cuda.stream(side), torch.no_grad():
+        ent["outs"][k] = tuple(ent["fn"](X))
+    ev = torch.cuda.Event()
+    ev.record(side)
+    ent["ev"][k] = ev
+
+
+def frozen_join(name):
+    """Before the first read of frozen_ahead(name, ...)'s outputs when they run on a side stream: the current
+    stream waits for them (batched: once per group); pipelined: waits for iteration k's and issues k + 1's."""
+    da = draw_ahead.active
+    if da is None:
+        return
+    ent = da.frozen.get(name)
+    if isinstance(ent, dict):  # pipelined
+        k = ent.get("cur")
+        ev = ent["ev"].pop(k, None)
+        if ev is not None:
+            torch.cuda.current_stream().wait_event(ev)
+        if k is not None and k + 1 < da.store.shape[0] and k + 1 not in ent["outs"]:
+            _frozen_issue(da, name, k + 1)
+        return
+    ev = da.frozen.pop(name + "/join", None)
+    if ev is not None:
+        torch.cuda.current_stream().wait_event(ev)
 
 
 class draw_plan:

@@ -20,6 +20,7 @@ from base import (BaseModel, advect_target, axpy_clamp, divergence, fused_forwar
                   merge_samples, mse_term, sample_boundary2D_pair, sample_boundary2D_separate, sample_random,
                   sample_random_and_bands2D, sample_uniform, sq_losses, wall_mse, wall_term)
 from base.diff_ops import jacobian_only
+from base.sampling import frozen_ahead, frozen_join
 
 from .examples import get_examples
 
@@ -159,17 +160,61 @@ class Fluid2DModel(BaseModel):
     def _fused_pair(self):
         return getattr(self.cfg, "insr_fuse_forwards", True)
 
+    # Frozen work ahead (cfg.insr_frozen_ahead, default on).  Inside a group of U iterations replayed as one
+    # hipGraph (base/_loop.py run_group; their points drawn by ONE sampler launch, base.sampling.draw_ahead),
+    # what a phase evaluates on networks it does not train -- the advection's semi-Lagrangian target on
+    # u_prev, the pressure phase's div u, the projection's u_prev and grad p -- does not depend on any
+    # iteration's update: it runs ONCE for all U iterations' points (base.sampling.frozen_ahead), and each
+    # iteration's forward launch holds only the trained network's jet.
+    # cfg.insr_frozen_stream (default off): that evaluation runs on a side stream, overlapping the group's first
+    # trained-network forward; _join makes the main stream wait before the first loss reads it.
+    # cfg.insr_frozen_ahead = "pipe": per iteration on the side stream, one iteration ahead (under the previous
+    # iteration's reverse jets, all-reduce and Adam step; base.sampling.frozen_ahead).
+    def _ahead(self, name, x, fn):
+        mode = getattr(self.cfg, "insr_frozen_ahead", True)
+        if not mode:
+            return None
+        pipe = mode == "pipe"
+        side = None
+        if pipe or getattr(self.cfg, "insr_frozen_stream", False):
+            side = self.__dict__.get("_insr_frozen_side")
+            if side is None:
+                side = self._insr_frozen_side = torch.cuda.Stream(device=self.device)
+        return frozen_ahead(name, x, fn, stream=side, pipe=pipe)
+
+    @staticmethod
+    def _join(name):
+        frozen_join(name)
+
+    def _target_all(self, X):
+        return (advect_target(self.velocity_field_prev, X, self.cfg.dt, -1.0, 1.0)[0],)
+
+    def _div_all(self, X):
+        return (jacobian_only(self.velocity_field(X), X),)
+
+    def _projection_all(self, X):
+        with fused_forwards():
+            u_prev = self.velocity_field_prev(X)
+            grad_p = gradient(self.pressure_field(X), X)
+        return u_prev, grad_p
+
     @BaseModel._training_loop
     def _advect_velocity(self):
         x = self._sample_in_training()
         if self._fused_pair():
             xa, n, nb = self._merged(x)
-            # the frozen field's semi-Lagrangian target u_prev(clamp(x - dt u_prev(x), -1, 1))
-            # (two value jets and the foot, point-local: one job) beside the trainable field's
-            # value jet over [x; bands]: one mixed launch
-            with fused_forwards():
-                u_target, _ = advect_target(self.velocity_field_prev, x, self.cfg.dt, -1.0, 1.0)
+            pre = self._ahead("advect", x, self._target_all)
+            if pre is not None:  # the group's targets, computed once (_ahead)
+                u_target, = pre
                 ua = self.velocity_field(xa)
+                self._join("advect")
+            else:
+                # the frozen field's semi-Lagrangian target u_prev(clamp(x - dt u_prev(x), -1, 1))
+                # (two value jets and the foot, point-local: one job) beside the trainable field's
+                # value jet over [x; bands]: one mixed launch
+                with fused_forwards():
+                    u_target, _ = advect_target(self.velocity_field_prev, x, self.cfg.dt, -1.0, 1.0)
+                    ua = self.velocity_field(xa)
             # mean((u - u_target)^2) over the interior rows and the wall terms on the band rows,
             # one launch
             main, bc = sq_losses(mse_term(ua, u_target, count=u_target.numel(), total=self._dp_total(u_target.numel())),
@@ -188,12 +233,18 @@ class Fluid2DModel(BaseModel):
             # instead of a separate gradient jet + reverse jet for 2% of the points.  The
             # Laplacian rows of the band points get zero adjoint.
             xa, n, nb = self._merged(x)
-            # the velocity's Jacobian jet and the pressure's Laplacian jet are independent: one
-            # mixed-mode launch (base.fused_forwards); outputs are read after the scope
-            with fused_forwards():
-                with torch.no_grad():  # div u = du/dx + dv/dy, read off the velocity's Jacobian
-                    Ju = jacobian_only(self.velocity_field(x), x)
+            pre = self._ahead("pressure", x, self._div_all)
+            if pre is not None:  # the group's velocity Jacobians, computed once (_ahead)
+                Ju, = pre
                 lap_p, grad_p = laplace(self.pressure_field(xa), xa, return_grad=True)
+                self._join("pressure")
+            else:
+                # the velocity's Jacobian jet and the pressure's Laplacian jet are independent: one
+                # mixed-mode launch (base.fused_forwards); outputs are read after the scope
+                with fused_forwards():
+                    with torch.no_grad():  # div u = du/dx + dv/dy, read off the velocity's Jacobian
+                        Ju = jacobian_only(self.velocity_field(x), x)
+                    lap_p, grad_p = laplace(self.pressure_field(xa), xa, return_grad=True)
             # mean((lap p - du/dx - dv/dy)^2) over the interior rows (= mean((div u - lap p)^2))
             # and the wall terms, one launch; the diagonal of J is read in place (stride 4)
             main, bc = sq_losses(mse_term(lap_p, Ju[:, 0, 0], Ju[:, 1, 1], alpha=1.0, beta=-1.0, gamma=-1.0, count=n,
@@ -210,13 +261,19 @@ class Fluid2DModel(BaseModel):
         x = self._sample_in_training()
         if self._fused_pair():
             xa, n, nb = self._merged(x)
-            # frozen velocity (value), pressure gradient (detached) and the trainable velocity
-            # over [x; bands]: independent jets, one mixed-mode launch
-            with fused_forwards():
-                with torch.no_grad():
-                    u_prev = self.velocity_field_prev(x)
-                    grad_p = gradient(self.pressure_field(x), x)
+            pre = self._ahead("projection", x, self._projection_all)
+            if pre is not None:  # the group's u_prev and grad p, computed once (_ahead)
+                u_prev, grad_p = pre
                 ua = self.velocity_field(xa)
+                self._join("projection")
+            else:
+                # frozen velocity (value), pressure gradient (detached) and the trainable velocity
+                # over [x; bands]: independent jets, one mixed-mode launch
+                with fused_forwards():
+                    with torch.no_grad():
+                        u_prev = self.velocity_field_prev(x)
+                        grad_p = gradient(self.pressure_field(x), x)
+                    ua = self.velocity_field(xa)
             u_prev = u_prev.detach()
             main, bc = sq_losses(mse_term(ua, None, u_prev, grad_p, gamma=-1.0, delta=-1.0, count=u_prev.numel(),
                                           total=self._dp_total(u_prev.numel())),

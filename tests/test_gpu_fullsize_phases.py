@@ -414,9 +414,12 @@ def test_elasticity2dstretch_plain_full_size(B):
     m._sample_in_training = lambda resolution: x.cuda().requires_grad_(True)
     m._sample_fixed_in_training = lambda resolution: (fl_.cuda().requires_grad_(True), fr_.cuda().requires_grad_(True))
     m._reset_optimizer()
+    e0 = LW.LOWERED["energies"]
     with LW.lowering(m._lower_on()), LW.deferred_jets(m._defer_on()):
         ld = ElasticityPlainModel._solve_deformation._insr_phase(m)
     ld = LW.lower_losses(ld)
+    # the svd energies went through ONE insr_elastic_energy launch, the constraints through a loss group
+    assert LW.LOWERED["energies"] == e0 + 1
     m._update_network(ld)
     torch.cuda.synchronize()
     ecfg = dict(dt=cfg.dt, energy=list(cfg.energy), ratio_arap=cfg.ratio_arap, ratio_volume=cfg.ratio_volume,
@@ -438,3 +441,28 @@ def test_elasticity2dstretch_plain_full_size(B):
                                                                                              float(ldo["main"]))
     check_grads(m.deformation_field, r["f"], "el2d plain")
     check_update(m.deformation_field, r["f"], p0, cfg.lr)
+
+
+def test_elasticity2dstretch_plain_loop_is_captured(B):
+    """The unchanged elasticity body through the real training loop with hipGraph replay (U = 4 groups): no
+    host read inside an iteration any more (jacobian()'s NaN status is a Lazy value nobody reads, the svd
+    energies lowered), so every iteration after the first is captured and replayed; the energy decreases."""
+    import warnings
+    from base import lower as LW
+    from pde.config import baseline_config
+    from pde.elasticity_plain import ElasticityPlainModel
+    cfg = baseline_config("elasticity2Dstretch", proj_dir="/tmp/insr_el2d_plain_loop", insr_progress=False,
+                          early_stop=False, max_n_iters=7, insr_graph=True, insr_graph_unroll=4, insr_sync_every=1000)
+    torch.manual_seed(0)
+    m = ElasticityPlainModel(cfg)
+    m.timestep = 1
+    seen = []
+    m.tb = type("TB", (), {"add_scalars": lambda self, tag, vals, global_step: seen.append(vals["main"])})()
+    e0 = LW.LOWERED["energies"]
+    with warnings.catch_warnings():
+        warnings.simplefilter("error", RuntimeWarning)  # a capture fallback warns
+        m._solve_deformation()
+    torch.cuda.synchronize()
+    assert getattr(m, "_insr_capture_error", None) is None, m._insr_capture_error
+    assert LW.LOWERED["energies"] >= e0 + 3  # iteration 0, the captured iteration 1, the group graph's bodies
+    assert len(seen) == 2 and np.isfinite(seen).all() and seen[1] < seen[0]

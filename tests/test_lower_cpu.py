@@ -154,9 +154,13 @@ def test_broadcasting_and_offsets_stay_eager():
     with LW.lowering():
         (a,) = _leaves(u)
         r = a - w  # (16, 1) - (16,) broadcasts: eager
-        s = a + 1.0  # a constant offset: eager
+        s = a + 1.0  # a constant offset: recorded (the elasticity energies' S - 1), but no residual plan takes it
+        loss = torch.mean(s ** 2)
     assert not isinstance(r, LW.Lazy) and r.shape == (16, 16)
-    assert not isinstance(s, LW.Lazy)
+    assert isinstance(s, LW.Lazy) and s._insr_node.kind == "off" and LW.plan(loss._insr_node) is None
+    assert torch.equal(LW.materialize(s), u + 1.0)
+    out = LW.lower_losses({"main": loss})  # eager, as written
+    assert torch.equal(out["main"], torch.mean((u + 1.0) ** 2))
 
 
 def test_lowering_inactive_outside_scope():
@@ -323,3 +327,67 @@ def test_ready_sampler_leaf_rescale_is_one_op_and_cached():
         assert LW.materialize(y) is r and LW.materialize(x) is draw
         r.sum().backward()
         assert torch.equal(draw.grad, torch.full_like(draw, 2.0))
+
+
+def _el2d_loss(Jz, Fl, Fr, T, torch_mod=torch):
+    """elasticity/model.py:143-183 with energy = [arap, constraint, constraint_right, volume] (el2D)."""
+    U, S, V = torch.svd(Jz)
+    E_arap = 1.0 * torch.sum((S - 1.0) ** 2)
+    E_volume = 1e3 * torch.sum((torch.prod(S, dim=1) - 1) ** 2)
+    loss = 0
+    loss = loss + E_arap
+    loss = loss + 1e4 * torch.sum((Fl - 0) ** 2)
+    loss = loss + 1e4 * torch.sum((Fr - T) ** 2)
+    loss = loss + E_volume
+    return loss
+
+
+def test_elasticity_energy_plan():
+    """The unchanged elasticity body's energy (svd of J + I, the arap / volume sums over its singular values,
+    the positional constraints): energy_plan finds one singular-value energy per term and the constraints as
+    sum-of-squares terms, records nothing eagerly, and the materialised Lazy loss is the eager expression."""
+    from base import _jet  # noqa: F401  (deferred_jets opens a fused_forwards scope)
+    n = 40
+    Jraw, f, x = _t(n, 2, 2, seed=4), _t(n, 2, seed=5), _t(n, 2, grad=False, seed=6)
+    Fl, Fr, T = _t(7, 2, seed=7), _t(7, 2, seed=8), _t(7, 2, grad=False, seed=9)
+    with torch.no_grad():
+        Jraw.mul_(0.2)
+    ref = _el2d_loss(Jraw + torch.eye(2), Fl, Fr, T)
+    mat0 = LW.LOWERED["materialized"]
+    with LW.lowering(), LW.deferred_jets():
+        Jz = LW.eye_add(Jraw, (None, f, x))
+        lz = _el2d_loss(Jz, *_leaves(Fl, Fr), T)
+        assert isinstance(lz, LW.Lazy) and LW.LOWERED["materialized"] == mat0  # nothing evaluated while recording
+        ep = LW.energy_plan(lz._insr_node)
+        assert ep is not None
+        kinds = [(k, w) for k, w, _ in ep]
+        assert kinds == [("energy", 1.0), ("sq", 1e4), ("sq", 1e4), ("energy", 1e3)]
+        assert [p[0] for k, _, p in ep if k == "energy"] == ["arap", "volume"]
+        sq = [w * _eval_plan(p) for k, w, p in ep if k == "sq"]
+        assert all(p[0] == "combo" and p[4] == "sum" for k, _, p in ep if k == "sq")
+        assert torch.allclose(sq[0], 1e4 * torch.sum(Fl ** 2)) and torch.allclose(sq[1], 1e4 * torch.sum((Fr - T) ** 2))
+        m = LW.materialize(lz)
+    assert torch.allclose(m, ref, rtol=1e-6)
+    g, g_ref = _grads(m, [Jraw, Fl, Fr]), _grads(ref, [Jraw, Fl, Fr])
+    for a, b in zip(g, g_ref):
+        assert torch.allclose(a, b, rtol=1e-5, atol=1e-6)
+
+
+def test_kinematics_is_a_sum_of_squares_term():
+    """E_kinematics = r sum((qdot - qdot_prev)^2), qdot = (q - q_prev) / dt, q = f + x (elasticity/model.py:
+    137-148): the x terms cancel exactly and the residual is one 3-operand combo (f, f_prev, f_pp)."""
+    n, dt = 30, 0.1
+    f, fp, fpp, x = _t(n, 3, seed=1), _t(n, 3, grad=False, seed=2), _t(n, 3, grad=False, seed=3), _t(n, 3, grad=False, seed=4)
+
+    def body(f, fp, fpp, x):
+        q, q_prev, q_pp = f + x, fp + x, fpp + x
+        qdot = (q - q_prev) / dt
+        qdot_prev = (q_prev - q_pp) / dt
+        return 1.0 * torch.sum((qdot - qdot_prev) ** 2)
+    ref = body(f, fp, fpp, x)
+    with LW.lowering():
+        lz = body(*_leaves(f, fp, fpp, x))
+    p = LW.plan(lz._insr_node)
+    assert p is not None and p[0] == "combo" and p[4] == "sum"
+    assert sum(t is not None for t in p[1]) == 3
+    assert torch.allclose(_eval_plan(p), ref, rtol=1e-5)
