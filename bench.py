@@ -712,6 +712,7 @@ def main():
     nph = len(wl["phases"])
     log(f"model built, {n_local} points per rank per phase")
     loops, elapsed, ts_ms, ks, w_eff = measure(args, model, wl, world)
+    nts = len(ks)
     # points all ranks processed: strong = the global batch, weak = world x the per-rank batch
     n_all = interior_points(cfg, wl) if (args.scaling == "strong" and args.shard_of == 1) else n_local * world
     total_points = n_all * nph * args.steps
