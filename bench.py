@@ -102,11 +102,11 @@ def parse():
                     help="one process runs the data-parallel iteration itself (gradient arena, a world-1 RCCL "
                          "all-reduce between the two graphs, unfused sums + Adam): a rank's DP step measured on "
                          "one GPU (with --shard-of K: the K-rank strong run's rank step)")
-    ap.add_argument("--no-frozen-ahead", action="store_true",
-                    help="fluid: evaluate the frozen networks inside each iteration's mixed forward launch (A/B; "
-                         "default: once per replayed group of U iterations, base.sampling.frozen_ahead)")
+    ap.add_argument("--frozen-ahead", action="store_true",
+                    help="fluid: evaluate the frozen networks once per replayed group of U iterations "
+                         "(base.sampling.frozen_ahead; A/B -- default: inside each iteration's mixed forward launch)")
     ap.add_argument("--frozen-stream", action="store_true",
-                    help="fluid: run the group's frozen-network evaluation on a side stream (A/B)")
+                    help="fluid, with --frozen-ahead: that evaluation on a side stream (A/B)")
     ap.add_argument("--frozen-pipe", action="store_true",
                     help="fluid: frozen-network work per iteration on a side stream, one iteration ahead (A/B)")
     ap.add_argument("--no-seed-in-bwd", action="store_true",
@@ -218,7 +218,7 @@ def build_model(args, world, rank):
     res = wl["res"]
     cfg = baseline_config(args.config, sample_resolution=res, insr_graph=not args.no_graph, insr_dp_always=args.dp_path,
                           insr_graph_unroll=max(1, args.graph_unroll), insr_seed_in_bwd=not args.no_seed_in_bwd,
-                          insr_defer_jets=not args.no_defer_jets, insr_frozen_ahead=False if args.no_frozen_ahead else ("pipe" if args.frozen_pipe else True),
+                          insr_defer_jets=not args.no_defer_jets, insr_frozen_ahead="pipe" if args.frozen_pipe else bool(args.frozen_ahead),
                           insr_frozen_stream=args.frozen_stream,
                           insr_sync_every=10 ** 9, insr_progress=False, early_stop=False,
                           proj_dir="/tmp/insr_bench", max_n_iters=10 ** 9,
@@ -486,8 +486,7 @@ def cpu_baseline(config, seconds, n_rounds=3, iters=10):
     16384-point slice of its 262144-point batch: the per-point cost is size-independent)."""
     from oracle import siren_oracle as O
     from pde.config import baseline_config
-    # the box exports OMP_NUM_THREADS = its CPU share; affinity may list the whole host
-    cores = min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "1024")))
+    cores, share = cpu_threads()
     torch.set_num_threads(cores)
     torch.manual_seed(0)
     wl = WORKLOADS[config]
@@ -563,37 +562,52 @@ def cpu_baseline(config, seconds, n_rounds=3, iters=10):
         what = f"1 phase x {N} pts" + (f" (slice of the {full}-point batch; points/s scaled as per-point "
                                         f"cost independent of the batch size)" if N < full else "")
 
-    for _ in range(2):  # 2 warm-up iterations, then the median of 10
+    for _ in range(2):  # 2 warm-up iterations, then the median of 10 or more
         one_step()
-    # the box's CPU share is noisy: a round whose max/min exceeds 1.5 is re-sampled (up to 3
-    # rounds within the time budget); the round with the smallest spread is reported
-    rounds = []
-    t_start = time.perf_counter()
-    for _ in range(n_rounds):
-        times = []
-        t_all = time.perf_counter()
-        for _ in range(iters):
-            t0 = time.perf_counter()
-            one_step()
-            times.append(time.perf_counter() - t0)
-            if time.perf_counter() - t_all > seconds and len(times) >= 3:  # bounded sample
-                break
-        times.sort()
-        rounds.append(times)
-        if times[-1] / times[0] <= 1.5 or time.perf_counter() - t_start > 2.5 * seconds:
+    # the box's CPU share is a CFS quota on a shared host (tools/cpu_leg_study.py, profiles/r06/r6b/
+    # cpustudy.jsonl): iteration times spread 1.5-2.3x whatever the thread count or pinning, so the sample is
+    # as many iterations as the budget allows (>= 10) and the line carries the median, the fastest iteration
+    # and both spreads (max / min, and p90 / p10 of the middle 80 %)
+    times = []
+    t_all = time.perf_counter()
+    while len(times) < max(10, n_rounds * iters) and (len(times) < 10 or time.perf_counter() - t_all < seconds):
+        t0 = time.perf_counter()
+        one_step()
+        times.append(time.perf_counter() - t0)
+        if time.perf_counter() - t_all > seconds and len(times) >= 3:  # bounded sample
             break
-    times = min(rounds, key=lambda t: t[-1] / t[0])
+    times.sort()
     dt = times[len(times) // 2]
+    p10, p90 = times[len(times) // 10], times[min(len(times) - 1, (9 * len(times)) // 10)]
     return {"value": round(pts / dt, 1), "value_min_time": round(pts / times[0], 1),
-            "unit": "collocation-points/s", "cores": cores, "kind": "port",
+            "unit": "collocation-points/s", "cores": cores, "kind": "port", "cpu_share": share,
             "cpu_model": cpu_model(), "statistic": f"median of {len(times)} iterations after 2 warm-up",
-            "spread_max_over_min": round(times[-1] / times[0], 3),
+            "spread_max_over_min": round(times[-1] / times[0], 3), "spread_p90_over_p10": round(p90 / p10, 3),
             # the explicit uncertainty of `value`: the sample's iteration rates span median x (1 +- u)
             "uncertainty_pct": round(50.0 * (times[-1] - times[0]) / dt, 1),
-            "rounds": [{"n": len(t), "min_ms": round(t[0] * 1e3, 1), "max_ms": round(t[-1] * 1e3, 1)} for t in rounds],
             "sample": f"oracle/siren_oracle.py {config}: {what}, torch CPU autograd + Adam, "
                       f"{torch.get_num_threads()} threads, median {dt * 1e3:.1f} ms/iter "
-                      f"(min {times[0] * 1e3:.1f}, max {times[-1] * 1e3:.1f})"}
+                      f"(min {times[0] * 1e3:.1f}, p10 {p10 * 1e3:.1f}, p90 {p90 * 1e3:.1f}, max {times[-1] * 1e3:.1f})"}
+
+
+def cpu_threads():
+    """(threads, share description) of the CPU leg.  The box exports OMP_NUM_THREADS = its CPU share and
+    limits the container by a CFS quota (cgroup cpu.max, 16 CPUs of a 256-CPU host) while the affinity lists
+    every CPU: with as many busy threads as the quota the process is throttled (16 threads: fastest
+    iteration 425-436 ms; 12 threads: 308 ms, profiles/r06/r6b/cpustudy.jsonl), so the leg uses 3/4 of the
+    quota."""
+    omp = int(os.environ.get("OMP_NUM_THREADS", "1024"))
+    cores = min(len(os.sched_getaffinity(0)), omp)
+    share = f"affinity {len(os.sched_getaffinity(0))} CPUs, OMP_NUM_THREADS {os.environ.get('OMP_NUM_THREADS')}"
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max":
+            q = int(quota) / int(period)
+            share += f", cgroup quota {q:g} CPUs"
+            cores = max(1, min(cores, int(q * 3 // 4)))
+    except (OSError, ValueError):
+        pass
+    return cores, share
 
 
 def cpu_model():
@@ -733,7 +747,7 @@ def main():
                    "jet_precision": jet_precision_names(args.precision),
                    "bwd_policy": args.bwd_policy, "shard_of": args.shard_of, "dp_path": args.dp_path,
                    "seeds_in_bwd": bool(getattr(cfg, "insr_seed_in_bwd", True)),
-                   "frozen_ahead": bool(getattr(cfg, "insr_frozen_ahead", True)) and wl["pde"] == "fluid"
+                   "frozen_ahead": bool(getattr(cfg, "insr_frozen_ahead", False)) and wl["pde"] == "fluid"
                    and args.api == "fused", "frozen_stream": bool(args.frozen_stream), "frozen_pipe": bool(args.frozen_pipe),
                    "lowered": bool(model._lower_on()), "deferred_jets": bool(model._defer_on()),
                    "bwd_f16": bwd_f16,

@@ -160,18 +160,22 @@ class Fluid2DModel(BaseModel):
     def _fused_pair(self):
         return getattr(self.cfg, "insr_fuse_forwards", True)
 
-    # Frozen work ahead (cfg.insr_frozen_ahead, default on).  Inside a group of U iterations replayed as one
-    # hipGraph (base/_loop.py run_group; their points drawn by ONE sampler launch, base.sampling.draw_ahead),
-    # what a phase evaluates on networks it does not train -- the advection's semi-Lagrangian target on
-    # u_prev, the pressure phase's div u, the projection's u_prev and grad p -- does not depend on any
-    # iteration's update: it runs ONCE for all U iterations' points (base.sampling.frozen_ahead), and each
-    # iteration's forward launch holds only the trained network's jet.
+    # Frozen work ahead (cfg.insr_frozen_ahead, default OFF: measured slower, below).  Inside a group of U
+    # iterations replayed as one hipGraph (base/_loop.py run_group; their points drawn by ONE sampler launch,
+    # base.sampling.draw_ahead), what a phase evaluates on networks it does not train -- the advection's
+    # semi-Lagrangian target on u_prev, the pressure phase's div u, the projection's u_prev and grad p -- does
+    # not depend on any iteration's update: with it on, that runs ONCE for all U iterations' points
+    # (base.sampling.frozen_ahead), and each iteration's forward launch holds only the trained network's jet.
+    # Same-box A/B (profiles/r06/frozen_ahead/, 40-step lines, two rounds): headline 100.9 / 101.3 M pts/s on
+    # vs 108.0 / 108.2 M off, fluid2DtlgnM 8-way DP-path shard 0.344 / 0.345 vs 0.322 / 0.322 ms -- the mixed
+    # launch already runs the frozen job beside the trained one for free (both latency-bound); a batch of
+    # its own is one more launch.  Side stream: 102.2 / 102.5 M, 0.344 ms; pipelined: 91.4 / 92.1 M, 0.378 ms.
     # cfg.insr_frozen_stream (default off): that evaluation runs on a side stream, overlapping the group's first
     # trained-network forward; _join makes the main stream wait before the first loss reads it.
     # cfg.insr_frozen_ahead = "pipe": per iteration on the side stream, one iteration ahead (under the previous
     # iteration's reverse jets, all-reduce and Adam step; base.sampling.frozen_ahead).
     def _ahead(self, name, x, fn):
-        mode = getattr(self.cfg, "insr_frozen_ahead", True)
+        mode = getattr(self.cfg, "insr_frozen_ahead", False)
         if not mode:
             return None
         pipe = mode == "pipe"

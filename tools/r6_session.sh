@@ -17,13 +17,13 @@ for s in ${STEPS:-tests bench prof}; do
     smoke) run smoke 300 python __graft_entry__.py smoke ;;
     bench) run bench 300 python bench.py --steps ${BSTEPS:-20} --warmup 3 --no-cpu-baseline ;;
     abfrozen) for r in 1 2; do
-             run fa_on_$r 300 python bench.py --steps 40 --warmup 3 --no-cpu-baseline --no-roofline --plain-line off
-             run fa_off_$r 300 python bench.py --steps 40 --warmup 3 --no-cpu-baseline --no-roofline --plain-line off --no-frozen-ahead
-             run fa_str_$r 300 python bench.py --steps 40 --warmup 3 --no-cpu-baseline --no-roofline --plain-line off --frozen-stream
+             run fa_on_$r 300 python bench.py --steps 40 --warmup 3 --no-cpu-baseline --no-roofline --plain-line off --frozen-ahead
+             run fa_off_$r 300 python bench.py --steps 40 --warmup 3 --no-cpu-baseline --no-roofline --plain-line off
+             run fa_str_$r 300 python bench.py --steps 40 --warmup 3 --no-cpu-baseline --no-roofline --plain-line off --frozen-ahead --frozen-stream
              run fa_pipe_$r 300 python bench.py --steps 40 --warmup 3 --no-cpu-baseline --no-roofline --plain-line off --frozen-pipe
-             run fs_on_$r 300 python bench.py --config fluid2DtlgnM --shard-of 8 --dp-path --steps 40 --warmup 3 --no-cpu-baseline --no-roofline
-             run fs_off_$r 300 python bench.py --config fluid2DtlgnM --shard-of 8 --dp-path --steps 40 --warmup 3 --no-cpu-baseline --no-roofline --no-frozen-ahead
-             run fs_str_$r 300 python bench.py --config fluid2DtlgnM --shard-of 8 --dp-path --steps 40 --warmup 3 --no-cpu-baseline --no-roofline --frozen-stream
+             run fs_on_$r 300 python bench.py --config fluid2DtlgnM --shard-of 8 --dp-path --steps 40 --warmup 3 --no-cpu-baseline --no-roofline --frozen-ahead
+             run fs_off_$r 300 python bench.py --config fluid2DtlgnM --shard-of 8 --dp-path --steps 40 --warmup 3 --no-cpu-baseline --no-roofline
+             run fs_str_$r 300 python bench.py --config fluid2DtlgnM --shard-of 8 --dp-path --steps 40 --warmup 3 --no-cpu-baseline --no-roofline --frozen-ahead --frozen-stream
              run fs_pipe_$r 300 python bench.py --config fluid2DtlgnM --shard-of 8 --dp-path --steps 40 --warmup 3 --no-cpu-baseline --no-roofline --frozen-pipe
            done ;;
     benchcpu) run benchcpu 400 python bench.py --steps ${BSTEPS:-20} --warmup 3 ;;
@@ -69,6 +69,8 @@ for s in ${STEPS:-tests bench prof}; do
     profplain) run profplain 300 rocprofv3 --kernel-trace --stats -d "$PWD/$O/profplain" -o run --output-format csv -- python bench.py --api plain --steps 10 --warmup 3 --no-cpu-baseline --no-roofline ;;
     profshard) run profshard 300 rocprofv3 --kernel-trace --stats -d "$PWD/$O/profshard" -o run --output-format csv -- python bench.py --config fluid2DtlgnM --shard-of 8 --steps 10 --warmup 3 --no-cpu-baseline --no-roofline ;;
     kbench) run kbench 400 python tools/kbench.py ${KARGS:---sizes 8192,16708,66844 --nets fluid_pres --modes lap --variants h3 --policies 0,2} ;;
+    profel) run profel_plain 300 rocprofv3 --kernel-trace --stats -d "$PWD/$O/profel_plain" -o run --output-format csv -- python bench.py --api plain --config elasticity2Dstretch --steps 10 --warmup 3 --no-cpu-baseline --no-roofline
+            run profel_fused 300 rocprofv3 --kernel-trace --stats -d "$PWD/$O/profel_fused" -o run --output-format csv -- python bench.py --config elasticity2Dstretch --steps 10 --warmup 3 --no-cpu-baseline --no-roofline ;;
     cpustudy) run cpustudy 400 python -u tools/cpu_leg_study.py ${CPUSEC:-8} ;;
     plainel) run plain_el2d 300 python bench.py --api plain --config elasticity2Dstretch --steps 10 --warmup 3 --no-cpu-baseline --no-roofline
              run fused_el2d 300 python bench.py --config elasticity2Dstretch --steps 10 --warmup 3 --no-cpu-baseline --no-roofline ;;
