@@ -4,10 +4,13 @@ this package: q = f(x) + x, the Jacobian through `jacobian`, `torch.svd` of it, 
 plain torch sums, the positional constraints through separate network calls.  None of the fused helpers of
 pde/elasticity.py (merged batches, the one-launch energy kernel).
 
-The training loop runs it under its loss lowering (base/lower.py) like any unchanged model file: none of
-these energies is a mean square, so every expression runs eagerly, exactly as written -- the point of this
-model is that the lowering and the deferred jets never change a result they do not recognise
-(tests/test_gpu_plain_api.py pins it to the reference's golden vectors), not speed.
+The training loop runs it under its loss lowering (base/lower.py) like any unchanged model file (round 6):
+the network calls are queued and launched together, the arap / volume sums over the singular values of
+torch.svd(J + I) become ONE insr_elastic_energy launch (no torch.svd), the positional constraints and the
+kinematic term one loss-group launch, and jacobian()'s NaN status is never computed unless read, so the
+iteration is capturable.  The collision terms (boolean indexing + a host-side test) run as written.
+Pinned to the oracle at the elasticity2Dstretch size (tests/test_gpu_fullsize_phases.py) and to the
+reference's golden vectors (tests/test_gpu_plain_api.py).
 """
 import torch
 
@@ -49,6 +52,26 @@ def _collision_sphere(q, qdot, dt, ratio, center, radius):
 class ElasticityPlainModel(ElasticityModel):
     """ElasticityModel with the reference's phase body (same energies)."""
     _insr_lower = True  # an unchanged model file: the loop's lowering scopes are open around its body
+
+    # The body calls the model's own samplers (elasticity/model.py:198-230): on a box scene on the GPU they
+    # hand out row ranges of ElasticityModel's persistent [x; fixed_l; fixed_r] batch, redrawn by ONE sampler
+    # launch per iteration -- the same distributions as the reference's torch.rand / grid / torch.cat chain,
+    # which cost ~10 small launches per iteration (profiles/r06/r6c: 7 cat copies, 3 fills, 2 negations and 3
+    # sampler draws).  The phase body below is unchanged either way; elsewhere (mesh, CPU, recorded samples)
+    # the inherited samplers run.
+    def _sample_in_training(self, resolution):
+        fast = self._box_batch(resolution)
+        if fast is None:
+            return super()._sample_in_training(resolution)
+        _, x, fixed_l, fixed_r = fast
+        self._insr_fixed = (resolution, fixed_l, fixed_r)
+        return x
+
+    def _sample_fixed_in_training(self, resolution):
+        got = self.__dict__.pop("_insr_fixed", None)
+        if got is not None and got[0] == resolution:
+            return got[1], got[2]
+        return super()._sample_fixed_in_training(resolution)
 
     @BaseModel._training_loop
     def _solve_deformation(self):
