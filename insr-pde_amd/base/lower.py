@@ -566,11 +566,25 @@ def _svd_part(parent, i):
     return _eval(parent)[i]
 
 
+_EYES = {}
+
+
+def _eye(d, device, dtype):
+    """torch.eye(d) on `device`, made once (two fill launches each time otherwise); read-only."""
+    key = (d, str(device), dtype)
+    e = _EYES.get(key)
+    if e is None:
+        if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
+            return torch.eye(d, device=device, dtype=dtype)  # (no allocation kept from a capture pool)
+        e = _EYES[key] = torch.eye(d, device=device, dtype=dtype)
+    return e
+
+
 def eye_add(J, meta):
     """J + I of a Jacobian jet J (the affine f(x) + x of elasticity/model.py:137,143): recorded while jets are
     deferred (J has no values yet; an energy lowering reads J itself), else added now.  meta = (mlp, value,
     x) of the jet."""
-    eye = torch.eye(J.shape[-1], device=J.device, dtype=J.dtype)
+    eye = _eye(J.shape[-1], J.device, J.dtype)
     if not deferring():
         return J + eye
     leafJ = _Node("leaf", real=J, shape=tuple(J.shape))
