@@ -264,10 +264,13 @@ int insr_siren_jet_bwd_multi_rows(const InsrBwdJob* jobs, int n_jobs, int d_in, 
                                   int width, int mode, const float* params, float* work, void* stream);
 /* The reverse jets of several calls of ONE network (the reference's interior + band calls of a Laplacian
  * loss, fluid/model.py:111,119-120) as ONE launch of the saved-stream resident sweep (jet_fb.hpp) when that
- * sweep serves the jobs' total point count: phase 1 of insr_siren_jet_bwd_grad_adam for all jobs at once.
- * The per-CU partials land in `work` (insr_jet_bwd_work_bytes(16 * total tiles, ...)); phase 2 --
- * insr_siren_jet_bwd_grad_adam(..., n_points = 16 * (total 16-point tiles), phases = 2, ...), with or
- * without the Adam update -- sums them.  INSR_EINVAL when another path serves that total. */
+ * sweep serves the jobs' total point count, or (round 6) as ONE propagation + ONE split-K dW launch of the
+ * two-kernel backward (jet_x6w.hpp) when that path serves 16 * (total 16-point tiles) points (the reference's
+ * elasticity interior + constraint calls, elasticity/model.py:137,161-174): phase 1 of
+ * insr_siren_jet_bwd_grad_adam for all jobs at once.  The partials land in `work`
+ * (insr_jet_bwd_work_bytes(16 * total tiles, ...)); phase 2 -- insr_siren_jet_bwd_grad_adam(..., n_points =
+ * 16 * (total 16-point tiles), phases = 2, ...), with or without the Adam update -- sums them.  INSR_EINVAL
+ * when another path serves that total. */
 int insr_siren_jet_bwd_multi_sweep(const InsrBwdJob* jobs, int n_jobs, int d_in, int d_out, int num_hidden,
                                    int width, int mode, const float* params, float* work, void* stream);
 /* 1 if insr_siren_jet_bwd_grad takes the wide path for this batch / width / mode. */

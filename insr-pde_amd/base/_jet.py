@@ -472,12 +472,15 @@ def _launch_bwd_multi(jobs):
         arr = (nat.BwdJob * len(jobs))(*[
             nat.BwdJob(j.x2.data_ptr(), nat.ptr(j.act), nat.ptr(j.gy), nat.ptr(j.gdy), nat.ptr(j.glap), j.x2.shape[0])
             for j in jobs])
-        # the saved-stream resident sweep serves the jobs' total (a Laplacian interior + its bands): ONE launch
-        # for all of them, the sums (phase 2) with the Adam launch -- insr_siren_jet_bwd_multi_sweep
+        # the saved-stream resident sweep serves the jobs' total (a Laplacian interior + its bands), or the
+        # two-kernel backward does (round 6: the elasticity interior + its constraint calls): ONE launch (one
+        # propagation + one dW launch) for all of them, the sums (phase 2) with the Adam launch --
+        # insr_siren_jet_bwd_multi_sweep
         tiles = sum((j.x2.shape[0] + 15) // 16 for j in jobs)
         n_pass = 16 * tiles
-        if lib.insr_jet_bwd_kernel(n_pass, din, dout, L, W, cmode) == 1 and \
-                lib.insr_jet_bwd_path(n_pass, din, dout, L, W, cmode) == 2:
+        path_pass = lib.insr_jet_bwd_path(n_pass, din, dout, L, W, cmode)
+        if (lib.insr_jet_bwd_kernel(n_pass, din, dout, L, W, cmode) == 1 and path_pass == 2) or \
+                (path_pass == 1 and L > 0):
             with torch.cuda.stream(cur):
                 work = torch.empty(max(lib.insr_jet_bwd_work_bytes(n_pass, din, dout, L, W, cmode) // 4, 1),
                                    device=jobs[0].x2.device, dtype=torch.float32)

@@ -10,6 +10,7 @@ boundary bands: same distributions, another stream -- parity tests pass explicit
 sample tensors.
 """
 import ctypes
+import os
 
 import torch
 
@@ -169,17 +170,36 @@ def _wrap_seeder(mod, name):
     setattr(mod, name, seeded)
 
 
-def _install_reseed_hooks():
+def _seeder_sites():
     import torch.cuda.random as cr
     import torch.random as tr
-    for mod, names in ((torch, ("manual_seed", "seed")), (tr, ("manual_seed", "seed")),
-                       (torch.cuda, ("manual_seed", "manual_seed_all", "seed", "seed_all")),
-                       (cr, ("manual_seed", "manual_seed_all", "seed", "seed_all"))):
+    return ((torch, ("manual_seed", "seed")), (tr, ("manual_seed", "seed")),
+            (torch.cuda, ("manual_seed", "manual_seed_all", "seed", "seed_all")),
+            (cr, ("manual_seed", "manual_seed_all", "seed", "seed_all")))
+
+
+def install_reseed_hooks():
+    """Wrap torch's seeding functions to count re-seeds (done once at import unless the environment sets
+    INSR_NO_RESEED_HOOKS=1).  The wrappers call the original and add one to reseed_epoch(); each keeps the
+    original as `__wrapped__`.  Idempotent."""
+    for mod, names in _seeder_sites():
         for name in names:
             _wrap_seeder(mod, name)
 
 
-_install_reseed_hooks()
+def uninstall_reseed_hooks():
+    """Put torch's own seeding functions back (undoes install_reseed_hooks; idempotent).  Without the hooks
+    a same-seed re-seed no longer restarts the fused sampler's stream -- a seed CHANGE still does (the
+    sampler compares torch.cuda.initial_seed())."""
+    for mod, names in _seeder_sites():
+        for name in names:
+            fn = getattr(mod, name, None)
+            if fn is not None and getattr(fn, "_insr_reseed_hook", False):
+                setattr(mod, name, fn.__wrapped__)
+
+
+if os.environ.get("INSR_NO_RESEED_HOOKS", "0") in ("", "0"):
+    install_reseed_hooks()
 
 
 def _sampler(dev):

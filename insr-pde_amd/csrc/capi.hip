@@ -994,6 +994,9 @@ long insr_jet_bwd_multi_work_bytes(const long* n, int njobs, int din, int dout, 
   return bytes;
 }
 
+static int wide_bwd_jobs(const JetCall& c, const FbJobs& J, long N, int din, int dout, int L, int W, int mode,
+                         const float* params, float* work, float* grad, int accumulate, int phases, const AdamArgs& A,
+                         hipStream_t st);
 static int multi_fused_rows(const InsrBwdJob* jobs, const MultiPlan& p, int din, int dout, int L, int W, int mode,
                             const float* params, float* work, hipStream_t st);
 
@@ -1082,8 +1085,14 @@ int insr_siren_jet_bwd_multi_sweep(const InsrBwdJob* jobs, int njobs, int din, i
     total += jobs[k].n;
     tiles += (jobs[k].n + 15) / 16;
   }
-  // the saved-stream resident sweep must be the path of the jobs' total (jet_fb.hpp, f16x3)
-  if (total > 0x7fffffffL || c.recompute(L) || !(c.resident(total, L) && c.resident_f16(total, L))) return INSR_EINVAL;
+  // the saved-stream resident sweep (jet_fb.hpp, f16x3) or -- round 6 -- the two-kernel backward (jet_x6w.hpp,
+  // e.g. elasticity's interior batch + constraint bands, elasticity/model.py:137,161-174) must be the path of the
+  // jobs' total; the two-kernel jobs are laid out over npass = 16 x their tiles, and phase 2 (the sums, with the
+  // Adam launch: insr_siren_jet_bwd_grad_adam phases 2 at n = npass) finds them there
+  const long npass = 16 * tiles;
+  const bool fbp = !c.recompute(L) && c.resident(total, L) && c.resident_f16(total, L);
+  const bool widep = !fbp && !c.recompute(L) && L > 0 && !c.resident(npass, L) && c.wide(npass);
+  if (total > 0x7fffffffL || npass > 0x7fffffffL || !(fbp || widep)) return INSR_EINVAL;
   if (tiles == 0) return 0;
   if (!params || !work) return INSR_EINVAL;
   hipStream_t st = (hipStream_t)stream;
@@ -1106,6 +1115,7 @@ int insr_siren_jet_bwd_multi_sweep(const InsrBwdJob* jobs, int njobs, int din, i
   }
   J.tstart[m] = t;
   J.njobs = m;
+  if (widep) return wide_bwd_jobs(c, J, npass, din, dout, L, W, mode, params, work, nullptr, 0, 1, AdamArgs{}, st);
   return dispatch_fb_bwd(c.S, c.lap, L, J, din, dout, prm, work, nullptr, 0, 1, 1, AdamArgs{}, st);
 }
 
@@ -1181,23 +1191,34 @@ int insr_jet_bwd_kernel(long n, int din, int dout, int L, int W, int mode) {
   return (p == 3 || (p == 2 && c.resident_f16(n, L))) ? 1 : 0;
 }
 
-// The two-kernel (wide) backward: phases / Adam epilogue as wide_bwd_t
-static int wide_bwd_call(const JetCall& c, const float* x, long n, int din, int dout, int L, int W, int mode,
-                         const float* params, const float* act, const float* gy, const float* gdy, const float* glap,
-                         float* work, float* grad, int accumulate, int phases, const AdamArgs& A, hipStream_t st) {
+// The two-kernel (wide) backward of a job table laid out over N points (jet_x6w.hpp wide_bwd_t)
+static int wide_bwd_jobs(const JetCall& c, const FbJobs& J, long N, int din, int dout, int L, int W, int mode,
+                         const float* params, float* work, float* grad, int accumulate, int phases, const AdamArgs& A,
+                         hipStream_t st) {
   int rc = 0;
   if (!(params = with_planes(params, din, dout, L, W, mode, st, 0, &rc))) return rc;
   switch (c.nqb) {
-    case 3:
-      return dispatch_wide_bwd_q<3>(c.NT, c.S, c.lap, x, (int)n, din, dout, L, params, act, gy, gdy, glap, work, grad,
-                                    accumulate, c.k.f16, phases, A, st);
-    case 2:
-      return dispatch_wide_bwd_q<2>(c.NT, c.S, c.lap, x, (int)n, din, dout, L, params, act, gy, gdy, glap, work, grad,
-                                    accumulate, c.k.f16, phases, A, st);
-    default:
-      return dispatch_wide_bwd_q<1>(c.NT, c.S, c.lap, x, (int)n, din, dout, L, params, act, gy, gdy, glap, work, grad,
-                                    accumulate, c.k.f16, phases, A, st);
+    case 3: return dispatch_wide_bwd_q<3>(c.NT, c.S, c.lap, J, (int)N, din, dout, L, params, work, grad, accumulate, c.k.f16, phases, A, st);
+    case 2: return dispatch_wide_bwd_q<2>(c.NT, c.S, c.lap, J, (int)N, din, dout, L, params, work, grad, accumulate, c.k.f16, phases, A, st);
+    default: return dispatch_wide_bwd_q<1>(c.NT, c.S, c.lap, J, (int)N, din, dout, L, params, work, grad, accumulate, c.k.f16, phases, A, st);
   }
+}
+
+// The two-kernel (wide) backward of one call: phases / Adam epilogue as wide_bwd_t
+static int wide_bwd_call(const JetCall& c, const float* x, long n, int din, int dout, int L, int W, int mode,
+                         const float* params, const float* act, const float* gy, const float* gdy, const float* glap,
+                         float* work, float* grad, int accumulate, int phases, const AdamArgs& A, hipStream_t st) {
+  FbJobs J{};
+  J.x[0] = x;
+  J.act[0] = act;
+  J.gy[0] = gy;
+  J.gdy[0] = gdy;
+  J.glap[0] = glap;
+  J.n[0] = (int)n;
+  J.tstart[0] = 0;
+  J.tstart[1] = (int)((n + 15) / 16);
+  J.njobs = 1;
+  return wide_bwd_jobs(c, J, n, din, dout, L, W, mode, params, work, grad, accumulate, phases, A, st);
 }
 
 // The single-job call of the jet_fb.hpp backward (the recompute kernel, or the resident sweep on the

@@ -2,10 +2,8 @@
 #include "jet_x6w.hpp"
 
 namespace insr {
-template int dispatch_wide_bwd_q<1>(int, int, bool, const float*, int, int, int, int, const float*, const float*,
-                                    const float*, const float*, const float*, float*, float*, int, int, int,
+template int dispatch_wide_bwd_q<1>(int, int, bool, const FbJobs&, int, int, int, int, const float*, float*, float*, int, int, int,
                                     const AdamArgs&, hipStream_t);
-template int dispatch_wide_bwd_q<2>(int, int, bool, const float*, int, int, int, int, const float*, const float*,
-                                    const float*, const float*, const float*, float*, float*, int, int, int,
+template int dispatch_wide_bwd_q<2>(int, int, bool, const FbJobs&, int, int, int, int, const float*, float*, float*, int, int, int,
                                     const AdamArgs&, hipStream_t);
 }  // namespace insr

@@ -615,10 +615,11 @@ struct AdamArgs {
   LossFin fin;  // fin.nloss > 0: the sums launch also finishes a seeded backward's loss values
 };
 
+struct FbJobs;  // (below) the job table of the two-kernel and jet_fb.hpp backwards
 template <int NQ>
-int dispatch_wide_bwd_q(int NT, int S, bool LAP, const float* x, int N, int din, int dout, int L, const float* prm,
-                        const float* act, const float* gy, const float* gdy, const float* glap, float* work,
-                        float* grad, int accumulate, int f16, int phases, const AdamArgs& A, hipStream_t st);
+int dispatch_wide_bwd_q(int NT, int S, bool LAP, const FbJobs& J, int N, int din, int dout, int L, const float* prm,
+                        float* work, float* grad, int accumulate, int f16, int phases, const AdamArgs& A,
+                        hipStream_t st);
 long wide_work_floats(long n, int din, int dout, int L, int W, int S);
 template <int NQ>
 int dispatch_fwd_mixed_q(int NT, int din, const InsrJetJob* jobs, const int* modes, const float* scalars, int njobs,

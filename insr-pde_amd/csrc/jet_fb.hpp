@@ -659,6 +659,14 @@ __global__ __launch_bounds__(512, 1) void jet_fb_x6(const FbJobs J, int din, int
         }
       }
       FB_STAMP(sp + 3);
+      if (tile == t1 - 1) {
+        // the block's last tile: dW_j is final -- its partial (fragment order, power of two undone) leaves
+        // now and drains under the remaining layers' sweep instead of as one burst after the loop (round 6)
+        floatx4* out = reinterpret_cast<floatx4*>(dpart + ((long)(j - 1) * nb + blockIdx.x) * W * W);
+        const float f = ldexpf(1.f, -E[j - 1]);
+#pragma unroll
+        for (int q = 0; q < NT; ++q) out[((2 * ra + q / 4) * NT + 4 * cb + q % 4) * 64 + lane] = dacc[j - 1][q] * f;
+      }
       // propagation: h̄_{j-1}[m] = sum_n W_j[n][m] z̄_j[n] (A = 2^8 W^T fragments, B = P rows)
       floatx4 nh[S];
 #pragma unroll
@@ -717,14 +725,16 @@ __global__ __launch_bounds__(512, 1) void jet_fb_x6(const FbJobs J, int din, int
 
   // ---- the block's partials: dW of every hidden layer in fragment order (one 1 KiB wave store per
   // accumulator, the accumulator's power of two undone; reduce_dw_kernel frag = 1 scatters the
-  // sums), then the compact row ----
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, ra = wave >> 1, cb = wave & 1;
+  // sums) -- stored inside the last tile's sweep, layer by layer; a block without tiles stores its
+  // zeros here -- then the compact row ----
+  if (t1 == t0) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, ra = wave >> 1, cb = wave & 1;
 #pragma unroll
-  for (int jl = 0; jl < L; ++jl) {
-    floatx4* out = reinterpret_cast<floatx4*>(dpart + ((long)jl * nb + blockIdx.x) * W * W);
-    const float f = E[jl] == kNoE ? 1.f : ldexpf(1.f, -E[jl]);
+    for (int jl = 0; jl < L; ++jl) {
+      floatx4* out = reinterpret_cast<floatx4*>(dpart + ((long)jl * nb + blockIdx.x) * W * W);
 #pragma unroll
-    for (int q = 0; q < NT; ++q) out[((2 * ra + q / 4) * NT + 4 * cb + q % 4) * 64 + lane] = dacc[jl][q] * f;
+      for (int q = 0; q < NT; ++q) out[((2 * ra + q / 4) * NT + 4 * cb + q % 4) * 64 + lane] = dacc[jl][q];
+    }
   }
   __syncthreads();  // every owner lane's last compact update
   for (int i = threadIdx.x; i < Ps; i += 512) small[(long)blockIdx.x * Ps + i] = sacc0[i];
@@ -733,9 +743,15 @@ __global__ __launch_bounds__(512, 1) void jet_fb_x6(const FbJobs J, int din, int
 // ---------------------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------------------
+// Balanced persistent grid (round 6): the launch lasts ceil(tiles / CUs) tile-times whatever the block
+// count, so take the FEWEST blocks that still need no more tiles each -- 16,708 points = 1,045 tiles:
+// 209 blocks x 5 instead of 256 blocks of 4 or 5; the shard's 523 tiles: 175 x 3 instead of 256 x 2-3 --
+// the same critical path with 18-32 % fewer per-CU dW partials written here and re-read by the sums
 inline int fb_blocks(long tiles) {
-  const int cus = device_cus();
-  return (int)(tiles < cus ? tiles : cus);
+  const long cus = device_cus();
+  if (tiles <= cus) return (int)(tiles > 0 ? tiles : 1);
+  const long per = (tiles + cus - 1) / cus;
+  return (int)((tiles + per - 1) / per);
 }
 
 // workspace floats: dW partials [layer][block][W^2] | compact rows [block][Ps]

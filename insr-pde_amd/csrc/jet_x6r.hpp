@@ -373,7 +373,9 @@ __global__ __launch_bounds__(512 / RPW, 1) void jet_bwd_x6r(const float* __restr
 inline int x6r_blocks(long n) {
   const int cus = device_cus();
   const long tiles = (n + 15) / 16;
-  return (int)(tiles < cus ? tiles : cus);
+  if (tiles <= cus) return (int)(tiles > 0 ? tiles : 1);
+  const long per = (tiles + cus - 1) / cus;  // balanced: fewest blocks at the same tiles per block (jet_fb.hpp)
+  return (int)((tiles + per - 1) / per);
 }
 
 // workspace floats: dW partials [layer][block][W^2] | compact rows [block][Ps]

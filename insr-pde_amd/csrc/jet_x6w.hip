@@ -3,8 +3,7 @@
 #include "jet_x6w.hpp"
 
 namespace insr {
-template int dispatch_wide_bwd_q<3>(int, int, bool, const float*, int, int, int, int, const float*, const float*,
-                                    const float*, const float*, const float*, float*, float*, int, int, int,
+template int dispatch_wide_bwd_q<3>(int, int, bool, const FbJobs&, int, int, int, int, const float*, float*, float*, int, int, int,
                                     const AdamArgs&, hipStream_t);
 long wide_work_floats(long n, int din, int dout, int L, int W, int S) {
   return wide_work_floats_impl(n, din, dout, L, W, S);

@@ -104,10 +104,8 @@ template <int NQ, int NT>
 constexpr int x6p_min_waves() { return NT == 8 ? (NQ == 4 ? INSR_F16_BWD_WAVES : 4) : 1; }
 
 template <int NQ, int NT, int S, bool LAP>
-__global__ __launch_bounds__(512, (x6p_min_waves<NQ, NT>())) void jet_bwd_x6p(const float* __restrict__ x, int N, int din, int dout, int L,
-                                                   const float* __restrict__ prm, const float* __restrict__ act,
-                                                   const float* __restrict__ gy, const float* __restrict__ gdy,
-                                                   const float* __restrict__ glap, float* __restrict__ adj,
+__global__ __launch_bounds__(512, (x6p_min_waves<NQ, NT>())) void jet_bwd_x6p(const FbJobs J, int N, int din, int dout, int L,
+                                                   const float* __restrict__ prm, float* __restrict__ adj,
                                                    float* __restrict__ part, long Ps, float* __restrict__ zmax) {
   constexpr int W = 16 * NT, RPW = NT / 8, KC = NT / 2;
   constexpr int LDB = W + 8, ZPLANE = 16 * LDB, ZSET = np_of<NQ>() * ZPLANE;
@@ -127,11 +125,24 @@ __global__ __launch_bounds__(512, (x6p_min_waves<NQ, NT>())) void jet_bwd_x6p(co
   float* hq = zmax ? zmax + 3L * L * tiles_n : nullptr;
   float* ht = zmax ? hq + 8L * L * tiles_n : nullptr;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
+  // several jobs (round 6: e.g. an interior batch and its constraint bands from separate network calls):
+  // block = tile of the launch (z̄, the compact rows and the maxima are laid out by it, over N = 16 x the
+  // jobs' tiles); the job's points, adjoints and saved streams by its own tile lt
   const int ntiles = ((N + 63) / 64) * 4;
   const int tile = blockIdx.x;
+  int jk = 0;
+#pragma unroll
+  for (int q = 1; q < kBwdJobs; ++q) jk += (q < J.njobs && tile >= J.tstart[q]) ? 1 : 0;
+  const int lt = tile - J.tstart[jk], Nk = J.n[jk];
+  const int ntk = ((Nk + 63) / 64) * 4;
+  const float* __restrict__ x = J.x[jk];
+  const float* __restrict__ act = J.act[jk];
+  const float* __restrict__ gy = J.gy[jk];
+  const float* __restrict__ gdy = J.gdy[jk];
+  const float* __restrict__ glap = J.glap[jk];
   const int rt0 = wave * RPW;
-  const int p = tile * 16 + c;
-  const bool valid = p < N;
+  const int p = lt * 16 + c;
+  const bool valid = p < Nk;
   float* mypart = part + (long)blockIdx.x * Ps;
   const long sb = (long)W * din + W;       // compact offset of b_1
   const long so = sb + (long)L * W;        // compact offset of Wout
@@ -143,7 +154,7 @@ __global__ __launch_bounds__(512, (x6p_min_waves<NQ, NT>())) void jet_bwd_x6p(co
     return gdy ? gdy[((long)p * dout + o) * din + (s - 1)] : 0.f;
   };
   auto load_sc = [&](int layer, floatx4(&s_)[RPW], floatx4(&c_)[RPW]) {
-    const float* base = act_base(act, layer, ntiles, tile, S, NT);
+    const float* base = act_base(act, layer, ntk, lt, S, NT);
     floatx4 z[RPW];
     float amax = 0.f;
 #pragma unroll
@@ -176,7 +187,7 @@ __global__ __launch_bounds__(512, (x6p_min_waves<NQ, NT>())) void jet_bwd_x6p(co
   for (int i = 0; i < RPW; ++i)
 #pragma unroll
     for (int s = 0; s < S; ++s) hb[i][s] = floatx4{0.f, 0.f, 0.f, 0.f};
-  const float* baseL = act_base(act, L, ntiles, tile, S, NT);
+  const float* baseL = act_base(act, L, ntk, lt, S, NT);
   for (int o = 0; o < dout; ++o) {
     float ga[S];
 #pragma unroll
@@ -209,7 +220,7 @@ __global__ __launch_bounds__(512, (x6p_min_waves<NQ, NT>())) void jet_bwd_x6p(co
 
   // ---- sine layers j = L .. 0 ----
   for (int j = L; j >= 0; --j) {
-    const float* basej = act_base(act, j, ntiles, tile, S, NT);
+    const float* basej = act_base(act, j, ntk, lt, S, NT);
     float hl = 0.f, htb = 0.f;  // this wave's bounds of |h_j|'s Laplacian and tangent streams
     constexpr int NTAN = LAP ? S - 2 : S - 1;
 #pragma unroll
@@ -451,7 +462,7 @@ __device__ __forceinline__ void rows_level1(const float* __restrict__ part, int 
 // z̄ x 2^e on the value / tangent streams and x 2^(e - eh) on the Laplacian one, e mapping the larger
 // of the two maxima into [2^14, 2^15) -- every product carries 2^e, undone on the partial (exact).
 template <int NQ, int NT, int S, bool LAP>
-__global__ __launch_bounds__(512, (NQ == 4 && NT == 8) ? INSR_F16_BWD_WAVES : 1) void dw_x6(int N, const float* __restrict__ act, const float* __restrict__ adj,
+__global__ __launch_bounds__(512, (NQ == 4 && NT == 8) ? INSR_F16_BWD_WAVES : 1) void dw_x6(int N, const FbJobs J, const float* __restrict__ adj,
                                              float* __restrict__ dpart, int KS, int L, const float* __restrict__ small,
                                              int tiles, long Ps, float* __restrict__ rows, int rs, int rows_x,
                                              const float* __restrict__ zmax, const float* __restrict__ w0, int din) {
@@ -469,8 +480,15 @@ __global__ __launch_bounds__(512, (NQ == 4 && NT == 8) ? INSR_F16_BWD_WAVES : 1)
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
   const int j = blockIdx.y + 1;
   const bool l0 = l0_rebuilt(j - 1, L);  // h_0's derivative streams: rebuilt from W_0 (not saved)
-  const int ntiles = ((N + 63) / 64) * 4;
+  const int ntiles = ((N + 63) / 64) * 4;  // z̄: launch tiles (all jobs)
   const int units = ((N + 15) / 16) * S;
+  // saved streams of launch tile t: its job's buffer at the job's own tile (t wave-uniform)
+  auto abase = [&](int t) -> const float* {
+    int k = 0;
+#pragma unroll
+    for (int q = 1; q < kBwdJobs; ++q) k += (q < J.njobs && t >= J.tstart[q]) ? 1 : 0;
+    return act_base(J.act[k], j - 1, ((J.n[k] + 63) / 64) * 4, t - J.tstart[k], S, NT);
+  };
   const int chunks = (units + 1) / 2;
   const int c0 = (int)((long)chunks * blockIdx.x / KS), c1 = (int)((long)chunks * (blockIdx.x + 1) / KS);
   // fp16 operand scales (NQ = 4): z̄ x asc (x ascl more on the Laplacian stream), h's Laplacian
@@ -531,7 +549,7 @@ __global__ __launch_bounds__(512, (NQ == 4 && NT == 8) ? INSR_F16_BWD_WAVES : 1)
       const int u = 2 * ch + ul;
       const int uu = (ch < c1 && u < units) ? u : 0;
       const int t = uu / S, s = uu - t * S;
-      const float* ba = act_base(act, j - 1, ntiles, t, S, NT);
+      const float* ba = abase(t);
       rzb[it] = *reinterpret_cast<const floatx4*>(act_base(adj, j - 1, ntiles, t, S, NT) +
                                                   ((s * NT + rt) * 64 + lane) * 4);
       if (S % 2 != 0 || it < RT) rz0[it] = *reinterpret_cast<const floatx4*>(ba + (rt * 64 + lane) * 4);
@@ -574,7 +592,7 @@ __global__ __launch_bounds__(512, (NQ == 4 && NT == 8) ? INSR_F16_BWD_WAVES : 1)
           // (summed in stream order 1 .. S - 2, as h_stream and the forward do)
           const floatx4 zsib = rzs[it >= RT ? it - RT : 0];
           floatx4 t2 = floatx4{0.f, 0.f, 0.f, 0.f};
-          const float* ba = act_base(act, j - 1, ntiles, t, S, NT);
+          const float* ba = abase(t);
 #pragma unroll
           for (int ti = 1; ti < S - 2; ++ti) {
             const floatx4 z = load_zs<NT, S, LAP>(ba, ti, rt, lane, l0, w0, din);
@@ -586,7 +604,7 @@ __global__ __launch_bounds__(512, (NQ == 4 && NT == 8) ? INSR_F16_BWD_WAVES : 1)
 #pragma unroll
           for (int r = 0; r < 4; ++r) hv[r] = OMEGA * cv[r] * rzs[it][r] - OMEGA2 * sv[r] * t2[r];
         } else {
-          hv = h_stream<NT, S, LAP>(act_base(act, j - 1, ntiles, t, S, NT), s, rt, lane, sv, cv, l0, w0, din);
+          hv = h_stream<NT, S, LAP>(abase(t), s, rt, lane, sv, cv, l0, w0, din);
         }
       } else {
 #pragma unroll
@@ -863,9 +881,11 @@ inline void wide_launch_threads_impl(long n, int din, int dout, int L, int W, in
 
 // phases (L > 0): 1 the propagation + dW partials, 2 the sums (with A.m: + the Adam update), 3 both
 template <int NQ, int NT, int S, bool LAP>
-int wide_bwd_t(const float* x, int N, int din, int dout, int L, const float* prm, const float* act, const float* gy,
-               const float* gdy, const float* glap, float* work, float* grad, int accumulate, int f16,
-               int phases, const AdamArgs& A, hipStream_t st) {
+// J: the jobs (one for a single call); N: the layout count, 16 x the jobs' tiles for several (a single
+// call passes its own n) -- the workspace, KS and the sums launch all follow N, so a phase-2 call with the
+// same N finds what phase 1 wrote
+int wide_bwd_t(const FbJobs& J, int N, int din, int dout, int L, const float* prm, float* work, float* grad,
+               int accumulate, int f16, int phases, const AdamArgs& A, hipStream_t st) {
   constexpr int W = 16 * NT;
   const long ntiles = ((N + 63) / 64) * 4;
   const int tiles = (N + 15) / 16;
@@ -908,27 +928,27 @@ int wide_bwd_t(const float* x, int N, int din, int dout, int L, const float* prm
   bool launched = false;
   if constexpr (NQ == 3) {
     if (f16p) {
-      hipLaunchKernelGGL((jet_bwd_x6p<4, NT, S, LAP>), dim3(tiles), dim3(512), lds_p4, st, x, N, din, dout, L, prm, act,
-                         gy, gdy, glap, adj, small, Ps, f16dw ? zmax : nullptr);
+      hipLaunchKernelGGL((jet_bwd_x6p<4, NT, S, LAP>), dim3(tiles), dim3(512), lds_p4, st, J, N, din, dout, L, prm, adj,
+                         small, Ps, f16dw ? zmax : nullptr);
       launched = true;
     }
   }
   if (!launched)
-    hipLaunchKernelGGL((jet_bwd_x6p<NQ, NT, S, LAP>), dim3(tiles), dim3(512), lds_p, st, x, N, din, dout, L, prm, act,
-                       gy, gdy, glap, adj, small, Ps, f16dw ? zmax : nullptr);
+    hipLaunchKernelGGL((jet_bwd_x6p<NQ, NT, S, LAP>), dim3(tiles), dim3(512), lds_p, st, J, N, din, dout, L, prm, adj,
+                       small, Ps, f16dw ? zmax : nullptr);
   if (L > 0) {  // 3 launches: propagation | dW partials + compact rows level 1 | dW sums + rows level 2
     const int KS = wide_ks(N, S, L);
     const int planes = (rows_x * rs + KS - 1) / KS;
     bool done = false;
     if constexpr (NQ == 3) {
       if (f16dw) {
-        hipLaunchKernelGGL((dw_x6<4, NT, S, LAP>), dim3(KS, L + planes), dim3(512), (dw_lds<4, NT>()), st, N, act, adj,
+        hipLaunchKernelGGL((dw_x6<4, NT, S, LAP>), dim3(KS, L + planes), dim3(512), (dw_lds<4, NT>()), st, N, J, adj,
                            dpart, KS, L, small, tiles, Ps, rows, rs, rows_x, zmax, prm, din);
         done = true;
       }
     }
     if (!done)
-      hipLaunchKernelGGL((dw_x6<NQ, NT, S, LAP>), dim3(KS, L + planes), dim3(512), (dw_lds<NQ, NT>()), st, N, act, adj,
+      hipLaunchKernelGGL((dw_x6<NQ, NT, S, LAP>), dim3(KS, L + planes), dim3(512), (dw_lds<NQ, NT>()), st, N, J, adj,
                          dpart, KS, L, small, tiles, Ps, rows, rs, rows_x, zmax, prm, din);
     if (!(phases & 2)) return (int)hipGetLastError();
     const int grad16 = (((uintptr_t)(grad + hidden_off(din, W, 1))) & 15) == 0 ? 1 : 0;  // W % 4 == 0: all layers alike
@@ -944,31 +964,28 @@ int wide_bwd_t(const float* x, int N, int din, int dout, int L, const float* prm
 }
 
 template <int NQ, int NT>
-int wide_bwd_nt(int S, bool LAP, const float* x, int N, int din, int dout, int L, const float* prm, const float* act,
-                const float* gy, const float* gdy, const float* glap, float* work, float* grad, int accumulate,
-                int f16, int phases, const AdamArgs& A, hipStream_t st) {
+int wide_bwd_nt(int S, bool LAP, const FbJobs& J, int N, int din, int dout, int L, const float* prm, float* work,
+                float* grad, int accumulate, int f16, int phases, const AdamArgs& A, hipStream_t st) {
   switch (S * 2 + (LAP ? 1 : 0)) {
-    case 2: return wide_bwd_t<NQ, NT, 1, false>(x, N, din, dout, L, prm, act, gy, gdy, glap, work, grad, accumulate, f16, phases, A, st);
-    case 4: return wide_bwd_t<NQ, NT, 2, false>(x, N, din, dout, L, prm, act, gy, gdy, glap, work, grad, accumulate, f16, phases, A, st);
-    case 6: return wide_bwd_t<NQ, NT, 3, false>(x, N, din, dout, L, prm, act, gy, gdy, glap, work, grad, accumulate, f16, phases, A, st);
-    case 8: return wide_bwd_t<NQ, NT, 4, false>(x, N, din, dout, L, prm, act, gy, gdy, glap, work, grad, accumulate, f16, phases, A, st);
-    case 7: return wide_bwd_t<NQ, NT, 3, true>(x, N, din, dout, L, prm, act, gy, gdy, glap, work, grad, accumulate, f16, phases, A, st);
-    case 9: return wide_bwd_t<NQ, NT, 4, true>(x, N, din, dout, L, prm, act, gy, gdy, glap, work, grad, accumulate, f16, phases, A, st);
-    case 11: return wide_bwd_t<NQ, NT, 5, true>(x, N, din, dout, L, prm, act, gy, gdy, glap, work, grad, accumulate, f16, phases, A, st);
+    case 2: return wide_bwd_t<NQ, NT, 1, false>(J, N, din, dout, L, prm, work, grad, accumulate, f16, phases, A, st);
+    case 4: return wide_bwd_t<NQ, NT, 2, false>(J, N, din, dout, L, prm, work, grad, accumulate, f16, phases, A, st);
+    case 6: return wide_bwd_t<NQ, NT, 3, false>(J, N, din, dout, L, prm, work, grad, accumulate, f16, phases, A, st);
+    case 8: return wide_bwd_t<NQ, NT, 4, false>(J, N, din, dout, L, prm, work, grad, accumulate, f16, phases, A, st);
+    case 7: return wide_bwd_t<NQ, NT, 3, true>(J, N, din, dout, L, prm, work, grad, accumulate, f16, phases, A, st);
+    case 9: return wide_bwd_t<NQ, NT, 4, true>(J, N, din, dout, L, prm, work, grad, accumulate, f16, phases, A, st);
+    case 11: return wide_bwd_t<NQ, NT, 5, true>(J, N, din, dout, L, prm, work, grad, accumulate, f16, phases, A, st);
     default: return INSR_EINVAL;
   }
 }
 
 template <int NQ>
-int dispatch_wide_bwd_q(int NT, int S, bool LAP, const float* x, int N, int din, int dout, int L, const float* prm,
-                        const float* act, const float* gy, const float* gdy, const float* glap, float* work,
-                        float* grad, int accumulate, int f16, int phases, const AdamArgs& A, hipStream_t st) {
+int dispatch_wide_bwd_q(int NT, int S, bool LAP, const FbJobs& J, int N, int din, int dout, int L, const float* prm,
+                        float* work, float* grad, int accumulate, int f16, int phases, const AdamArgs& A,
+                        hipStream_t st) {
   if (NT == 16)
-    return wide_bwd_nt<NQ, 16>(S, LAP, x, N, din, dout, L, prm, act, gy, gdy, glap, work, grad, accumulate, f16, phases,
-                               A, st);
+    return wide_bwd_nt<NQ, 16>(S, LAP, J, N, din, dout, L, prm, work, grad, accumulate, f16, phases, A, st);
   if (NT == 8)
-    return wide_bwd_nt<NQ, 8>(S, LAP, x, N, din, dout, L, prm, act, gy, gdy, glap, work, grad, accumulate, f16, phases,
-                              A, st);
+    return wide_bwd_nt<NQ, 8>(S, LAP, J, N, din, dout, L, prm, work, grad, accumulate, f16, phases, A, st);
   return INSR_EWIDTH;
 }
 

@@ -155,6 +155,53 @@ def test_lap_jobs_in_one_saved_stream_sweep(B):
         assert nerr(g, ga) < TOL, k
 
 
+@pytest.mark.parametrize("sizes", [(20000, 200, 200), (8192, 17, 1, 0)])
+def test_grad_jobs_in_one_two_kernel_launch(B, sizes):
+    """The elasticity body as the reference writes it (elasticity/model.py:137,143,161-174): the Jacobian of
+    q = f(x) + x on the interior and the positional constraints on two fixed bands from separate calls of ONE
+    5 x 128 network, all gradient jets (the loop's deferred scope promotes the band calls), whose total takes
+    the two-kernel backward: ONE insr_siren_jet_bwd_multi_sweep (one propagation + one dW launch over a job
+    table, round 6) + its sums, held back for the Adam launch or not; = job by job and = the oracle."""
+    ref, net = pair(B, 2, 2, 5, 128, seed=13)
+    xs = [pts(n, 2, 40 + k) for k, n in enumerate(sizes)]
+    lib, nat = B._native.lib(), B._native
+    mode = net.call_mode(nat.MODE_GRAD)
+    n_pass = 16 * sum((n + 15) // 16 for n in sizes)
+    assert lib.insr_jet_bwd_path(n_pass, 2, 2, 5, 128, mode) == 1  # the two-kernel path serves the total
+
+    def loss_hip(xs):
+        y0, J0, _ = B._jet.run_jet(net, xs[0], nat.MODE_GRAD)
+        tot = 1e-3 * torch.sum(J0 ** 2) + 1e-3 * torch.sum(y0 ** 2)
+        for k, x in enumerate(xs[1:]):
+            yk, _, _ = B._jet.run_jet(net, x, nat.MODE_GRAD)  # (a promoted call: its values are read)
+            tot = tot + (k + 1) * torch.sum((yk - 0.1 * k) ** 2)
+        return tot
+
+    def loss_ref(xs):
+        y0 = ref(xs[0])
+        tot = 1e-3 * torch.sum(O.op_jacobian(y0, xs[0])[0] ** 2) + 1e-3 * torch.sum(y0 ** 2)
+        for k, x in enumerate(xs[1:]):
+            tot = tot + (k + 1) * torch.sum((ref(x) - 0.1 * k) ** 2)
+        return tot
+
+    xg = [t.cuda().requires_grad_(True) for t in xs]
+    g1 = run(B, net, lambda: loss_hip(xg), batched=False)
+    g2 = run(B, net, lambda: loss_hip(xg), batched=True)
+    for a, b in zip(g2, g1):
+        assert nerr(a, b) < TOL
+    net.zero_grad(set_to_none=True)
+    with B._jet.defer_reductions():
+        with B._jet.batched_backward():
+            loss_hip(xg).backward()
+    torch.cuda.synchronize()
+    for a, b in zip(grads(net), g2):
+        assert torch.equal(a, b)  # held back or not: the same sums
+    loss_ref([t.requires_grad_(True) for t in xs]).backward()
+    for (k, p), g in zip(ref.named_parameters(), g2):
+        ga = p.grad if p.grad is not None else torch.zeros_like(p)
+        assert nerr(g, ga) < TOL, k
+
+
 def test_more_jobs_than_one_launch(B):
     """11 band calls of one network: chunks of INSR_MAX_BWD_JOBS, gradients accumulated."""
     ref, net = pair(B, 2, 2, 4, 128, seed=5)

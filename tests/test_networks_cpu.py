@@ -128,3 +128,24 @@ def test_deepcopy_round_trip(B):
     assert not torch.equal(a.flat_params(), b.flat_params())
     t = copy.deepcopy(B.MLP(2, 1, 2, 64, nonlinearity="relu"))
     assert type(t).__name__ == "TorchMLP"
+
+
+def test_reseed_hooks_reversible():
+    """base.sampling's re-seed counters wrap torch's seeding functions reversibly: uninstall
+    puts the originals back, install wraps them again, and a re-seed is counted only while installed."""
+    import torch
+    from base import sampling as S
+    orig = torch.manual_seed.__wrapped__ if hasattr(torch.manual_seed, "_insr_reseed_hook") else torch.manual_seed
+    try:
+        S.uninstall_reseed_hooks()
+        assert torch.manual_seed is orig and not hasattr(torch.cuda.manual_seed_all, "_insr_reseed_hook")
+        e = S.reseed_epoch()
+        torch.manual_seed(3)
+        assert S.reseed_epoch() == e
+        S.install_reseed_hooks()
+        S.install_reseed_hooks()  # idempotent: no wrapper of a wrapper
+        assert torch.manual_seed.__wrapped__ is orig
+        torch.manual_seed(3)
+        assert S.reseed_epoch() > e
+    finally:
+        S.install_reseed_hooks()
