@@ -115,6 +115,9 @@ def parse():
     ap.add_argument("--no-defer-jets", action="store_true",
                     help="api plain: launch each network / diff-op call at once (A/B; default: the lowered body's "
                          "jets are queued and launched together at the first read, base/lower.py deferred_jets)")
+    ap.add_argument("--no-advect-fused", action="store_true",
+                    help="advect1D: the generic launches per iteration (A/B; default: one insr_advect1d_iteration "
+                         "launch + the sums / Adam launch, base/advect_iter.py)")
     ap.add_argument("--rehearse", action="store_true",
                     help="CPU rehearsal of the multi-rank launch (gloo, no GPU work; tests)")
     args = ap.parse_args()
@@ -219,7 +222,7 @@ def build_model(args, world, rank):
     cfg = baseline_config(args.config, sample_resolution=res, insr_graph=not args.no_graph, insr_dp_always=args.dp_path,
                           insr_graph_unroll=max(1, args.graph_unroll), insr_seed_in_bwd=not args.no_seed_in_bwd,
                           insr_defer_jets=not args.no_defer_jets, insr_frozen_ahead="pipe" if args.frozen_pipe else bool(args.frozen_ahead),
-                          insr_frozen_stream=args.frozen_stream,
+                          insr_frozen_stream=args.frozen_stream, insr_advect_fused=not args.no_advect_fused,
                           insr_sync_every=10 ** 9, insr_progress=False, early_stop=False,
                           proj_dir="/tmp/insr_bench", max_n_iters=10 ** 9,
                           insr_precision=None if args.precision == "fp32" else args.precision)
@@ -357,13 +360,16 @@ def roofline(loops, n_local, precision="fp32"):
     # dominant kernel = the longest launch over the interior batch (boundary bands are ~1% of points;
     # a merged launch carries the interior plus its boundary / fixed points: n >= n_local)
     # (fused multi-network forwards, kind "fwdK", are listed in the table but not candidates)
-    dom = max((k for k in per_step if k[2] >= n_local and k[0] in ("fwd", "bwd")), key=lambda k: sum(agg[k]) / len(agg[k]))
+    # (kind "iter": the one-launch advection iteration, base/advect_iter.py)
+    dom = max((k for k in per_step if k[2] >= n_local and k[0] in ("fwd", "bwd", "iter")),
+              key=lambda k: sum(agg[k]) / len(agg[k]))
     kind, mode, n, W, (din, dout, L) = dom
     ms = sum(agg[dom]) / len(agg[dom])
     # algorithmic flops per launch: 2P per point per stream per GEMM pass
     P = macs_per_point(din, dout, L, W)
     streams = {"value": 1, "grad": 1 + din, "lap": 2 + din}[mode]
-    passes = 1 if kind == "fwd" else 2
+    # an advection iteration launch: two fields' forward jets (1 pass each) + the trainable one's reverse (2)
+    passes = {"fwd": 1, "bwd": 2, "iter": 4}[kind]
     flops = n * streams * passes * 2 * P
     achieved = flops / (ms * 1e-3) / 1e12
     table = {}
@@ -412,6 +418,9 @@ def kernel_identity(kind, mode, n, din, dout, L, W, nq=3, seeded=False):
     lap = "true" if mode == "lap" else "false"
     f16 = nat.bwd_f16_mask() if nq == 3 else 0
     nprod = {4: 3, 3: 6, 2: 3, 1: 1}
+    if kind == "iter":  # insr_advect1d_iteration: exact-fp32 products (v_mfma_f32_16x16x4_f32)
+        nb = lib.insr_advect1d_rows(n)
+        return f"insr::advect1d_iter_kernel<{L}>", nb * 256, False, 1
     path = lib.insr_jet_bwd_path(n, din, dout, L, W, m_b) if kind == "bwd" else 0
     if path == 3:  # the recompute backward (forward + reverse jet per tile, f16x3) + the fixed-order sums
         import ctypes
@@ -747,6 +756,7 @@ def main():
                    "jet_precision": jet_precision_names(args.precision),
                    "bwd_policy": args.bwd_policy, "shard_of": args.shard_of, "dp_path": args.dp_path,
                    "seeds_in_bwd": bool(getattr(cfg, "insr_seed_in_bwd", True)),
+                   "advect_fused": bool(getattr(model, "_fused_iteration_ok", lambda: False)()),
                    "frozen_ahead": bool(getattr(cfg, "insr_frozen_ahead", False)) and wl["pde"] == "fluid"
                    and args.api == "fused", "frozen_stream": bool(args.frozen_stream), "frozen_pipe": bool(args.frozen_pipe),
                    "lowered": bool(model._lower_on()), "deferred_jets": bool(model._defer_on()),

@@ -689,6 +689,32 @@ int insr_sample_boxes(const InsrBox* boxes, int n_boxes, int dim, unsigned long 
 int insr_sample_boxes_rep(const InsrBox* boxes, int n_boxes, int dim, int reps, const long* rep_strides,
                           unsigned long long seed, void* state, void* stream);
 
+/*
+ * One advection iteration's forward, residual and reverse in ONE launch (round 6; csrc/advect_iter.hip):
+ * the reference's Advection1DModel._advect (advection/model.py:68-91) on a 1 -> 1 SIREN of width 64 and
+ * num_hidden (1..3) hidden layers -- the draw of n interior points in [box_lo[0], box_hi[0]) and
+ * n_band_half points in each of the two Dirichlet bands (boxes 1, 2: the stream, values and device
+ * state advance of insr_sample_boxes with those three boxes, dim 1), the value + x-derivative jets of
+ * the frozen field (prev_params) and the trainable one (params), the residual
+ *   r = (u - u0) / dt + vel (u_x + u0_x) / 2 on the interior, u on the bands,
+ * and the parameter gradient of  sum r_int^2 / main_total + sum u_band^2 / bc_total  as one partial row
+ * per block into `partials` ([rows][stride], stride >= the parameter count, a multiple of 4) with the
+ * blocks' loss sums into loss_part ([rows][INSR_SEED_MAX] scratch); the last block to finish writes the
+ * two losses to losses[0] (main = sum r_int^2 / main_total) and losses[1] (bc).  `points` (n + 2
+ * n_band_half floats, may be NULL) receives the drawn points.  Returns the row count (=
+ * insr_advect1d_rows(n + 2 n_band_half)) or a negative INSR_E*.  The rows are summed -- with the Adam (+
+ * plateau, reading losses[0]) update -- by insr_adam_step_partials (or insr_reduce_partials_strided): an
+ * iteration is two launches.  Replaces:
+ * sample_random / sample_boundary (base/sampling.py:14-30), MLP.forward + gradient (base/diff_ops.py:44-58)
+ * of both fields, the loss expressions and loss.backward() (base/baseModel.py:73-78).
+ */
+long insr_advect1d_rows(long n_points);
+int insr_advect1d_iteration(const float* params, const float* prev_params, int num_hidden, int width, long n,
+                            long n_band_half, const float* box_lo, const float* box_hi, float dt, float vel,
+                            float main_total, float bc_total, unsigned long long seed, void* sampler_state,
+                            float* points, float* partials, long stride, float* loss_part, float* losses,
+                            void* stream);
+
 #ifdef __cplusplus
 }
 #endif

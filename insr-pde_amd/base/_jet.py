@@ -64,6 +64,11 @@ class _timed:
 
     def __enter__(self):
         if TIMING["on"]:
+            # the device is kept busy past the host's submission of the timed launches (a spin kernel of
+            # ~100 us queued first), so the events bracket device time only -- without it a short launch
+            # (the one-launch advection iteration: ~25 us of work behind ~30 us of Python per call) is
+            # timed as the host's submission gap
+            torch.cuda._sleep(TIMING.get("spin", 250000))
             self.e0 = torch.cuda.Event(enable_timing=True)
             self.e0.record()
         return self
@@ -608,6 +613,9 @@ class immediate_backward:
 def _flush_backward(jobs):
     groups = {}
     for j in jobs:
+        if hasattr(j, "run"):  # a finished gradient's sums to register (base/advect_iter.py): on this thread
+            j.run()
+            continue
         groups.setdefault((id(j.mlp), j.cmode, j.cur.cuda_stream), []).append(j)
     for js in groups.values():
         if len(js) == 1:

@@ -192,6 +192,9 @@ SIGNATURES = {
     "insr_sampler_state_bytes": (_L, []),
     "insr_sample_boxes": (_I, [_P, _I, _I, ctypes.c_ulonglong, _P, _P]),
     "insr_sample_boxes_rep": (_I, [_P, _I, _I, _I, _P, ctypes.c_ulonglong, _P, _P]),
+    "insr_advect1d_rows": (_L, [_L]),
+    "insr_advect1d_iteration": (_I, [_P, _P, _I, _I, _L, _L, _P, _P, _F, _F, _F, _F, ctypes.c_ulonglong, _P, _P,
+                                     _P, _L, _P, _P, _P]),
     "insr_adam_step": (_I, [_P, _P, _P, _P, _L, _P, _F, _F, _F, _P]),
     "insr_jet_bwd_seed_rows": (_I, [_L, _I, _I, _I, _I, _I]),
     "insr_siren_jet_bwd_seeded": (_I, [_P, _L, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _I, _P, _P, _P]),

@@ -58,10 +58,28 @@ class Advection1DModel(BaseModel):
         self.field_prev.load_state_dict(self.field.state_dict())
         self._advect()
 
+    def _fused_iteration_ok(self):
+        """Whether an iteration runs as ONE insr_advect1d_iteration launch (base/advect_iter.py): the 1 -> 1
+        width-64 SIREN on the GPU, the device sampler (no recorded samples), cfg.insr_advect_fused (default
+        on).  Under data parallelism too: the rows are summed into the arena-bound .grad before the
+        all-reduce, and the draws are rank-keyed like the sampler's."""
+        from base import advect_iter
+        return bool(getattr(self.cfg, "insr_advect_fused", True)) and "_sample_in_training" not in self.__dict__ \
+            and torch.device(self.device).type == "cuda" and advect_iter.supported(self.field, self.field_prev)
+
     @BaseModel._training_loop
     def _advect(self):
         """advection/model.py:68-91 (midpoint rule + Dirichlet band term)."""
         n_bc = max(self._n_interior() // 100, 10)
+        if self._fused_iteration_ok():
+            # the draw, both fields' jets, the residuals and the reverse jet in ONE launch; its rows are
+            # summed by the Adam launch (two launches per iteration instead of five)
+            from base.advect_iter import advect1d_iteration
+            n, h = self._n_interior(), n_bc // 2
+            main, bc = advect1d_iteration(self.field, self.field_prev, n, h, self.length / 2, 1e-4, self.dt,
+                                          self.vel, self._dp_total(n), self._dp_total(2 * h),
+                                          points=self.__dict__.get("_insr_points_out"))
+            return {'main': main, 'bc': bc}
         x, xa = self._advect_points(n_bc)
         n = x.shape[0]
         # the frozen field at x and the trainable one at [x; band] are independent jets: one

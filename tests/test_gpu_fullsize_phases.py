@@ -291,17 +291,21 @@ def test_elasticity3d_sphere_collision(B):
     check_update(m.deformation_field, r["f"], p0, cfg.lr)
 
 
-def test_advect1d_full_size(B):
+@pytest.mark.parametrize("fused", [False, True])
+def test_advect1d_full_size(B, fused):
     """advect1D (BASELINE.json configs[0]: SIREN 3x64, sample_resolution 4,096): one _advect iteration
-    on the product sampler path -- ONE insr_sample_boxes launch writes the 4,096 interior points and the
+    on the product path -- fused=False: ONE insr_sample_boxes launch writes the 4,096 interior points and the
     2 x 20 band points at +-L/2 into the merged buffer (pde/advection.py _advect_points), the frozen and
-    the trainable field run as one fused jet launch, the loss is fused_mse, Adam + plateau one launch --
-    vs the oracle's advection/model.py:68-91 loss on the points that launch drew: both losses, every
-    parameter gradient, the Adam update."""
+    the trainable field run as one fused jet launch, the loss is fused_mse, Adam + plateau one launch;
+    fused=True (the default, round 6): the whole iteration but the sums as ONE insr_advect1d_iteration
+    launch (base/advect_iter.py), its rows summed by the Adam launch -- vs the oracle's
+    advection/model.py:68-91 loss on the points the launch drew: both losses, every parameter gradient, the
+    Adam update."""
     import pde.advection as adv
+    from base import advect_iter
     from pde.config import baseline_config
     cfg = baseline_config("advect1D", proj_dir="/tmp/insr_fullsize_adv", insr_progress=False, early_stop=False,
-                          max_n_iters=1, insr_graph=False, insr_sync_every=1)
+                          max_n_iters=1, insr_graph=False, insr_sync_every=1, insr_advect_fused=fused)
     m = adv.Advection1DModel(cfg)
     m.timestep = 1
     refs = {"f": seeded(1, 1, 3, 64, 221), "f_prev": seeded(1, 1, 3, 64, 222)}
@@ -317,6 +321,9 @@ def test_advect1d_full_size(B):
         drawn["n"] = [b[0] for b in boxes]
         return buf
     adv.sample_boxes = rec
+    if fused:
+        m._insr_points_out = torch.empty(4096 + 40, device="cuda")
+    it0 = advect_iter.STATS["iterations"]
     try:
         m._reset_optimizer()
         ld = adv.Advection1DModel._advect._insr_phase(m)
@@ -324,6 +331,10 @@ def test_advect1d_full_size(B):
         torch.cuda.synchronize()
     finally:
         adv.sample_boxes = orig
+    assert advect_iter.STATS["iterations"] - it0 == (1 if fused else 0)
+    if fused:
+        assert "buf" not in drawn  # no sampler launch: the iteration kernel drew the points
+        drawn["buf"], drawn["n"] = m._insr_points_out.detach().cpu().view(-1, 1).clone(), [4096, 20, 20]
     n, h, h2 = drawn["n"]
     assert (n, h, h2) == (4096, 20, 20)
     buf = drawn["buf"]

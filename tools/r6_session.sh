@@ -78,6 +78,12 @@ for s in ${STEPS:-tests bench prof}; do
          run pmcel_fetch 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$PRX" -d "$PWD/$O/pmcel_fetch" -o run --output-format csv -- python bench.py --config elasticity3Dbunny --steps 1 --warmup 1 --no-graph --no-cpu-baseline --no-roofline
          run pmcel_write 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$PRX" -d "$PWD/$O/pmcel_write" -o run --output-format csv -- python bench.py --config elasticity3Dbunny --steps 1 --warmup 1 --no-graph --no-cpu-baseline --no-roofline
          run pmcel_sq 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT --kernel-include-regex "$PRX" -d "$PWD/$O/pmcel_sq" -o run --output-format csv -- python bench.py --config elasticity3Dbunny --steps 1 --warmup 1 --no-graph --no-cpu-baseline --no-roofline ;;
+    advab) for r in 1 2; do
+             run adv_fused_$r 300 python bench.py --config advect1D --steps 40 --warmup 3 --no-cpu-baseline
+             run adv_generic_$r 300 python bench.py --config advect1D --steps 40 --warmup 3 --no-cpu-baseline --no-advect-fused
+           done
+           run adv_plain 300 python bench.py --api plain --config advect1D --steps 40 --warmup 3 --no-cpu-baseline --no-roofline ;;
+    profadv) run profadv 300 rocprofv3 --kernel-trace --stats -d "$PWD/$O/profadv" -o run --output-format csv -- python bench.py --config advect1D --steps 20 --warmup 3 --no-cpu-baseline ;;
     prec) run prec 400 python tools/prec_errors.py ${PARGS:-} ;;
     precd) run precd 900 python -u tools/prec_defaults.py ${PDARGS:-} ;;
   esac
