@@ -29,6 +29,9 @@ def share():
 CHILD = r'''
 import json, os, sys, time
 threads, pin, seconds = int(sys.argv[1]), sys.argv[2], float(sys.argv[3])
+if len(sys.argv) > 6 and sys.argv[6] == "passive":  # (must precede the OpenMP runtime's start)
+    os.environ["OMP_WAIT_POLICY"] = "PASSIVE"
+    os.environ["GOMP_SPINCOUNT"] = "0"
 cpus = sorted(os.sched_getaffinity(0))
 if pin == "first":
     os.sched_setaffinity(0, cpus[:threads])
@@ -47,14 +50,16 @@ def main():
     seconds = float(sys.argv[1]) if len(sys.argv) > 1 else 10.0
     print(json.dumps({"share": share()}), flush=True)
     omp = int(os.environ.get("OMP_NUM_THREADS", "16"))
-    configs = [(omp, "none"), (omp, "first"), (max(1, omp * 3 // 4), "none"), (max(1, omp // 2), "none"),
-               (max(1, omp // 2), "first"), (omp, "none")]
-    for threads, pin in configs:
+    h = max(1, omp // 2)
+    configs = [(max(1, omp * 3 // 4), "none", "active"), (max(1, omp * 3 // 4), "none", "passive"),
+               (h, "none", "passive"), (h, "first", "passive"), (h, "spread", "passive"),
+               (max(1, omp // 4), "none", "passive"), (max(1, omp * 3 // 4), "none", "passive")]
+    for threads, pin, wait in configs:
         t0 = time.time()
-        out = subprocess.run([sys.executable, "-c", CHILD, str(threads), pin, str(seconds), ROOT, "20"],
+        out = subprocess.run([sys.executable, "-c", CHILD, str(threads), pin, str(seconds), ROOT, "20", wait],
                              capture_output=True, text=True, timeout=300)
         line = out.stdout.strip().splitlines()[-1] if out.stdout.strip() else None
-        rec = {"threads": threads, "pin": pin, "wall_s": round(time.time() - t0, 1)}
+        rec = {"threads": threads, "pin": pin, "omp_wait": wait, "wall_s": round(time.time() - t0, 1)}
         if line:
             r = json.loads(line)
             rec.update({k: r.get(k) for k in ("value", "value_min_time", "spread_max_over_min", "statistic",

@@ -84,6 +84,15 @@ for s in ${STEPS:-tests bench prof}; do
            done
            run adv_plain 300 python bench.py --api plain --config advect1D --steps 40 --warmup 3 --no-cpu-baseline --no-roofline ;;
     profadv) run profadv 300 rocprofv3 --kernel-trace --stats -d "$PWD/$O/profadv" -o run --output-format csv -- python bench.py --config advect1D --steps 20 --warmup 3 --no-cpu-baseline ;;
+    pmcall) PRX='jet_|dw_x6|reduce_|advect1d'  # per config: FETCH_SIZE, WRITE_SIZE, SQ in passes of their own
+         for spec in "head:" "adv:--config advect1D" "shard:--config fluid2DtlgnM --shard-of 8" "el2d:--config elasticity2Dstretch"; do
+           nm=${spec%%:*}; ca=${spec#*:}
+           for pass in fetch write sq; do
+             case $pass in fetch) cnt="FETCH_SIZE";; write) cnt="WRITE_SIZE";;
+               sq) cnt="SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT";; esac
+             run pmc_${nm}_$pass 300 rocprofv3 --pmc $cnt --kernel-include-regex "$PRX" -d "$PWD/$O/$nm/pmc_$pass" -o run --output-format csv -- python bench.py $ca --steps 2 --warmup 1 --no-graph --no-cpu-baseline --no-roofline
+           done
+         done ;;
     prec) run prec 400 python tools/prec_errors.py ${PARGS:-} ;;
     precd) run precd 900 python -u tools/prec_defaults.py ${PDARGS:-} ;;
   esac
