@@ -153,14 +153,31 @@ __global__ __launch_bounds__(kAdvThreads) void advect1d_iter_kernel(const Advect
   constexpr int kB = 128, kWo = 128 + 64 * L;  // SM offsets of b_1 and W_out (b_out at kWo + 64)
   const float* SMq = SM + grp * SMN;           // this wave's field's small parameters (forward)
 
-  // ---- stage both fields' parameters (every later weight read is LDS) ----
+  // ---- stage both fields' parameters (every later weight read is LDS): all of a thread's 16-B loads are
+  // issued before its first LDS store (one L2 / HBM latency per block, not one per load) ----
+  {
+    constexpr int NV = L * W * W / 4 / kAdvThreads;  // float4 per thread and field (L = 3: 6)
+    static_assert(NV * kAdvThreads == L * W * W / 4, "staging split");
+    floatx4 v[2][NV];
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+#pragma unroll
+      for (int u = 0; u < NV; ++u) {
+        const int i = tid + u * kAdvThreads;
+        const int j = i / (W * W / 4), rem = i - j * (W * W / 4);
+        v[q][u] = *reinterpret_cast<const floatx4*>(P[q] + hidden_off(1, W, j + 1) + 4 * rem);
+      }
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+#pragma unroll
+      for (int u = 0; u < NV; ++u) {
+        const int i = tid + u * kAdvThreads;
+        const int j = i / (W * W / 4), rem = i - j * (W * W / 4), row = rem >> 4, c4 = rem & 15;
+        *reinterpret_cast<floatx4*>(WS + ((q * L + j) * W + row) * WL + 4 * c4) = v[q][u];
+      }
+  }
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
-    for (int i = tid; i < L * W * W / 4; i += kAdvThreads) {
-      const int j = i / (W * W / 4), rem = i - j * (W * W / 4), row = rem >> 4, c4 = rem & 15;
-      const floatx4 v = *reinterpret_cast<const floatx4*>(P[q] + hidden_off(1, W, j + 1) + row * W + 4 * c4);
-      *reinterpret_cast<floatx4*>(WS + ((q * L + j) * W + row) * WL + 4 * c4) = v;
-    }
     for (int k = tid; k < 193 + 64 * L; k += kAdvThreads) {
       long src;
       if (k < kB)
