@@ -79,7 +79,9 @@ bool use_fb(int S, int NT, bool lap, int nq, int L, const Knobs& k) {
 // 65,536: 544 vs 632), value jets from 49,152 (65,536: 171-177 vs 224-234; 33,092 equal;
 // 16,708: 80 vs 64-69 fused -- below ~8 tiles per CU the 64 MB of per-CU dW partials dominate).
 bool resident_ok(int S, int NT, bool lap, int nq, int L) {
-  if (NT != 8 || nq != 3 || L != 4) return false;
+  if (NT != 8 || nq != 3) return false;
+  if (L == 5) return S == 3 && !lap;  // (the jet_fb.hpp saved-stream sweep only: jet_x6r is compiled for L = 4)
+  if (L != 4) return false;
   return (S == 1 && !lap) || (S == 3 && !lap) || (S == 4 && lap);
 }
 // Round 3: with the two-kernel path's products on the fp16 matrix cores (INSR_BWD_F16_DW | PROP;
@@ -89,6 +91,7 @@ bool resident_ok(int S, int NT, bool lap, int nq, int L) {
 bool use_resident_f16(long n, int S, int NT, bool lap, int nq, int L, const Knobs& k);
 bool use_resident(long n, int S, int NT, bool lap, int nq, int L, const Knobs& k) {
   if (!resident_ok(S, NT, lap, nq, L)) return false;
+  if (L == 5) return use_resident_f16(n, S, NT, lap, nq, L, k);  // no jet_x6r instantiation at this depth
   if (k.policy == 3 || k.policy == 5) return true;
   if (k.policy != 0) return false;
   if (use_resident_f16(n, S, NT, lap, nq, L, k)) return true;
@@ -106,10 +109,11 @@ bool use_resident(long n, int S, int NT, bool lap, int nq, int L, const Knobs& k
 // 4,096 points (the fluid2DtlgnM 8-way shard step, 8,192 + 163 points: 0.331-0.332 vs 0.345-0.347 ms
 // with the two-kernel path, profiles/r04/ab_fb_shard/).
 bool use_resident_f16(long n, int S, int NT, bool lap, int nq, int L, const Knobs& k) {
-  if (NT != 8 || nq != 3 || !fb_supported(S, lap, L)) return false;
+  if (NT != 8 || nq != 3 || !fb_saved_supported(S, lap, L)) return false;
   if (k.policy == 5) return true;
   if (k.policy != 0 || !(k.f16 & INSR_BWD_F16_FUSED)) return false;
-  return lap && S == 4 && n >= 4096;
+  // round 6: also the 5-layer 2-d gradient jet (the el2D deformation net's Jacobian) from 4,096 points
+  return (lap && S == 4 && n >= 4096) || (!lap && S == 3 && L == 5 && n >= 4096);
 }
 
 // Matrix-core precision of the tile-split kernels (a call's INSR_JET_PREC(p) / INSR_JET_BPREC(p);

@@ -655,6 +655,7 @@ constexpr int kFbSeedTiles = 24;  // at most this many tiles per block take in-k
 int dispatch_fb_bwd(int S, bool LAP, int L, const FbJobs& J, int din, int dout, const float* prm, float* work,
                     float* grad, int accumulate, int saved, int phases, const AdamArgs& A, hipStream_t st);
 bool fb_supported(int S, bool LAP, int L);
+bool fb_saved_supported(int S, bool LAP, int L);
 long fb_work_floats(long tiles, int din, int dout, int L);
 int fb_launch_blocks(long tiles);
 

@@ -10,11 +10,18 @@ bool fb_supported(int S, bool LAP, int L) {
   if (L != 4) return false;
   return (S == 4 && LAP) || (S == 3 && !LAP) || (S == 1 && !LAP);
 }
+// the saved-stream sweep also serves the 2-d gradient jet of 5 hidden layers (round 6: the
+// elasticity2Dstretch deformation net's Jacobian, elasticity/model.py:143; 255 VGPRs, no spills)
+bool fb_saved_supported(int S, bool LAP, int L) { return fb_supported(S, LAP, L) || (L == 5 && S == 3 && !LAP); }
 
 // saved = 0: the recompute backward (reruns the forward per tile); 1: the same reverse sweep on the
 // forward's saved streams (J.act) -- dW resident per CU, f16x3 products, no z̄ round trip
 int dispatch_fb_bwd(int S, bool LAP, int L, const FbJobs& J, int din, int dout, const float* prm, float* work,
                     float* grad, int accumulate, int saved, int phases, const AdamArgs& A, hipStream_t st) {
+  if (L == 5) {
+    if (S == 3 && !LAP && saved) return fb_bwd_t<3, false, 5, 1, true>(J, din, dout, prm, work, grad, accumulate, phases, A, st);
+    return INSR_EINVAL;
+  }
   if (!fb_supported(S, LAP, L)) return INSR_EINVAL;
   switch ((S * 2 + (LAP ? 1 : 0)) * 2 + (saved ? 1 : 0)) {
     case 18: return fb_bwd_t<4, true, 4, 2, false>(J, din, dout, prm, work, grad, accumulate, phases, A, st);

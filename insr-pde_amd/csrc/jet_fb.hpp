@@ -695,6 +695,7 @@ __global__ __launch_bounds__(512, 1) void jet_fb_x6(const FbJobs J, int din, int
       fb_sincos(zc[0], sn, cs);
       FB_STAMP(sp + 4);
     };
+    if constexpr (L >= 5) bwd_layer(std::integral_constant<int, 5>{});
     if constexpr (L >= 4) bwd_layer(std::integral_constant<int, 4>{});
     if constexpr (L >= 3) bwd_layer(std::integral_constant<int, 3>{});
     if constexpr (L >= 2) bwd_layer(std::integral_constant<int, 2>{});

@@ -205,7 +205,13 @@ def test_backward_path_policy(lib):
     assert lib.insr_jet_bwd_path(33092, 2, 2, 4, 128, V) == 1   # value jets two-kernel from 24,576
     assert lib.insr_jet_bwd_path(24000, 2, 2, 4, 128, V) == 0
     assert lib.insr_jet_bwd_path(32768, 3, 3, 5, 256, G) == 1
-    assert lib.insr_jet_bwd_path(20400, 2, 2, 5, 128, G) not in (2, 3)  # 5 hidden layers
+    # 5 hidden layers: the 2-d gradient jet (el2D's Jacobian) takes the saved-stream resident sweep from 4,096
+    # points (round 6); value / Laplacian jets of that depth and the recompute kernel are not served by it
+    assert lib.insr_jet_bwd_path(20400, 2, 2, 5, 128, G) == 2
+    assert lib.insr_jet_bwd_kernel(20400, 2, 2, 5, 128, G) == 1
+    assert lib.insr_jet_bwd_path(4095, 2, 2, 5, 128, G) not in (2, 3)
+    assert lib.insr_jet_bwd_path(20400, 2, 2, 5, 128, V) not in (2, 3)
+    assert lib.insr_jet_bwd_path(20400, 2, 1, 5, 128, LAP) not in (2, 3)
     assert lib.insr_jet_bwd_path(16708, 2, 1, 4, 128, LAP | nat.jet_prec(nat.PREC_BF16)) not in (2, 3)
     assert lib.insr_jet_bwd_path(16708, 2, 1, 4, 128, LAP | P(2)) == 1
     assert lib.insr_jet_bwd_path(16708, 2, 1, 4, 128, LAP | P(1)) == 0

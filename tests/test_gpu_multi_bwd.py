@@ -155,19 +155,26 @@ def test_lap_jobs_in_one_saved_stream_sweep(B):
         assert nerr(g, ga) < TOL, k
 
 
+@pytest.mark.parametrize("policy", [2, 0])
 @pytest.mark.parametrize("sizes", [(20000, 200, 200), (8192, 17, 1, 0)])
-def test_grad_jobs_in_one_two_kernel_launch(B, sizes):
+def test_grad_jobs_in_one_two_kernel_launch(B, sizes, policy):
     """The elasticity body as the reference writes it (elasticity/model.py:137,143,161-174): the Jacobian of
     q = f(x) + x on the interior and the positional constraints on two fixed bands from separate calls of ONE
     5 x 128 network, all gradient jets (the loop's deferred scope promotes the band calls), whose total takes
     the two-kernel backward: ONE insr_siren_jet_bwd_multi_sweep (one propagation + one dW launch over a job
-    table, round 6) + its sums, held back for the Adam launch or not; = job by job and = the oracle."""
+    table, round 6) + its sums, held back for the Adam launch or not; = job by job and = the oracle.  policy 0
+    (the default since round 6): the same jobs through ONE saved-stream resident sweep (jet_fb.hpp, 5 layers)."""
+    with B._native.knobs(policy=policy):
+        _grad_jobs(B, sizes, policy)
+
+
+def _grad_jobs(B, sizes, policy):
     ref, net = pair(B, 2, 2, 5, 128, seed=13)
     xs = [pts(n, 2, 40 + k) for k, n in enumerate(sizes)]
     lib, nat = B._native.lib(), B._native
     mode = net.call_mode(nat.MODE_GRAD)
     n_pass = 16 * sum((n + 15) // 16 for n in sizes)
-    assert lib.insr_jet_bwd_path(n_pass, 2, 2, 5, 128, mode) == 1  # the two-kernel path serves the total
+    assert lib.insr_jet_bwd_path(n_pass, 2, 2, 5, 128, mode) == (1 if policy == 2 else 2)  # the path of the total
 
     def loss_hip(xs):
         y0, J0, _ = B._jet.run_jet(net, xs[0], nat.MODE_GRAD)

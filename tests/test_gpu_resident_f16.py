@@ -118,6 +118,33 @@ def test_auto_policy_shard_sizes_vs_oracle(B, n):
             assert nerr(b, a) < TOL, (n, k, nerr(b, a))
 
 
+@pytest.mark.parametrize("n", [4113, 20400])
+def test_five_layer_gradient_jet_auto_policy(B, n):
+    """Round 6: the default policy takes this kernel for the 2-d gradient jet of a 5 x 128 net from 4,096
+    points -- elasticity2Dstretch's Jacobian of q = f(x) + x (elasticity/model.py:137,143; 20,000 interior +
+    2 x 200 constraint points) -- vs the oracle (every parameter gradient) and vs the two-kernel backward."""
+    lib = B._native.lib()
+    out = []
+    for pol in (0, 2):
+        with B._native.knobs(policy=pol):
+            assert lib.insr_jet_bwd_path(n, 2, 2, 5, 128, G | B._native.scope_bits()) == (2 if pol == 0 else 1)
+            ref, net = pair(B, 2, 2, 5, 128, seed=75)
+            x = torch.rand(n, 2, generator=torch.Generator().manual_seed(n)) * 2 - 1
+            xg = x.cuda().requires_grad_(True)
+            J = B.jacobian(net(xg) + xg, xg)[0]
+            R = torch.randn(J.shape, generator=torch.Generator().manual_seed(n + 3))
+            (J * R.cuda()).sum().backward()
+            torch.cuda.synchronize()
+            out.append(grads(net))
+    xr = x.clone().requires_grad_(True)
+    Jr = O.op_jacobian(ref(xr) + xr, xr)[0]
+    (Jr * R).sum().backward()
+    for (k, _), a, b in zip(ref.named_parameters(), ref_grads(ref), out[0]):
+        assert nerr(b, a) < TOL, (n, k, nerr(b, a))
+    for a, b in zip(*out):
+        assert nerr(a, b) < TOL
+
+
 @pytest.mark.parametrize("n", [300, 16708])
 def test_matches_two_kernel_path(B, n):
     """Same network and adjoints: this kernel vs the saved-stream two-kernel backward (policy 2)."""

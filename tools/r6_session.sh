@@ -93,6 +93,11 @@ for s in ${STEPS:-tests bench prof}; do
              run pmc_${nm}_$pass 300 rocprofv3 --pmc $cnt --kernel-include-regex "$PRX" -d "$PWD/$O/$nm/pmc_$pass" -o run --output-format csv -- python bench.py $ca --steps 2 --warmup 1 --no-graph --no-cpu-baseline --no-roofline
            done
          done ;;
+    abel) for r in 1 2; do
+             run el_res_$r 300 python bench.py --config elasticity2Dstretch --steps 20 --warmup 3 --no-cpu-baseline
+             run el_2k_$r 300 python bench.py --config elasticity2Dstretch --steps 20 --warmup 3 --no-cpu-baseline --bwd-policy 2
+           done
+           run el_plain 300 python bench.py --api plain --config elasticity2Dstretch --steps 20 --warmup 3 --no-cpu-baseline --no-roofline ;;
     prec) run prec 400 python tools/prec_errors.py ${PARGS:-} ;;
     precd) run precd 900 python -u tools/prec_defaults.py ${PDARGS:-} ;;
   esac
