@@ -147,4 +147,7 @@ def test_default_routing(B):
     assert lib.insr_jet_bwd_path(66844, 2, 1, 4, 128, nat.MODE_LAP) == 2    # fluid2DtlgnM batch
     assert lib.insr_jet_bwd_path(66844, 2, 1, 4, 128, nat.MODE_LAP | nat.jet_bwd_f16(0)) == 2
     assert lib.insr_jet_bwd_path(66844, 2, 2, 4, 128, nat.MODE_VALUE) == 2
-    assert lib.insr_jet_bwd_path(20400, 2, 2, 5, 128, nat.MODE_GRAD) not in (2, 3)  # 5 hidden layers
+    # 5 hidden layers (el2D's Jacobian): the saved-stream resident sweep since round 6 (jet_fb.hpp, kernel 1)
+    assert lib.insr_jet_bwd_path(20400, 2, 2, 5, 128, nat.MODE_GRAD) == 2
+    assert lib.insr_jet_bwd_kernel(20400, 2, 2, 5, 128, nat.MODE_GRAD) == 1
+    assert lib.insr_jet_bwd_path(20400, 2, 2, 5, 128, nat.MODE_VALUE) not in (2, 3)
