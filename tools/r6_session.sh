@@ -98,6 +98,25 @@ for s in ${STEPS:-tests bench prof}; do
              run el_2k_$r 300 python bench.py --config elasticity2Dstretch --steps 20 --warmup 3 --no-cpu-baseline --bwd-policy 2
            done
            run el_plain 300 python bench.py --api plain --config elasticity2Dstretch --steps 20 --warmup 3 --no-cpu-baseline --no-roofline ;;
+    abpol5) for r in 1 2; do
+             run p0_head_$r 300 python bench.py --steps 40 --warmup 3 --no-cpu-baseline --plain-line off
+             run p5_head_$r 300 python bench.py --steps 40 --warmup 3 --no-cpu-baseline --plain-line off --bwd-policy 5
+             run p0_shard_$r 300 python bench.py --config fluid2DtlgnM --shard-of 8 --steps 40 --warmup 3 --no-cpu-baseline --no-roofline
+             run p5_shard_$r 300 python bench.py --config fluid2DtlgnM --shard-of 8 --steps 40 --warmup 3 --no-cpu-baseline --no-roofline --bwd-policy 5
+           done
+           run p0_M 300 python bench.py --config fluid2DtlgnM --steps 20 --warmup 3 --no-cpu-baseline
+           run p5_M 300 python bench.py --config fluid2DtlgnM --steps 20 --warmup 3 --no-cpu-baseline --bwd-policy 5 ;;
+    default) run default 600 python bench.py ;;
+    closing) run bench_advect1D 300 python bench.py --config advect1D --steps 40 --warmup 3 --no-cpu-baseline
+             for c in elasticity2Dstretch elasticity3Dbunny fluid2DtlgnM; do
+               run bench_$c 400 python bench.py --config $c --steps 20 --warmup 3 --no-cpu-baseline; done
+             run shard_M8 300 python bench.py --config fluid2DtlgnM --shard-of 8 --steps 40 --warmup 3 --no-cpu-baseline --no-roofline
+             run dpshard_M8 300 python bench.py --config fluid2DtlgnM --shard-of 8 --dp-path --steps 40 --warmup 3 --no-cpu-baseline --no-roofline
+             run shard_el3d8 300 python bench.py --config elasticity3Dbunny --shard-of 8 --steps 10 --warmup 3 --no-cpu-baseline --no-roofline
+             run dpshard_el3d8 300 python bench.py --config elasticity3Dbunny --shard-of 8 --dp-path --steps 10 --warmup 3 --no-cpu-baseline --no-roofline
+             run plain_el2d 300 python bench.py --api plain --config elasticity2Dstretch --steps 20 --warmup 3 --no-cpu-baseline --no-roofline
+             run plain_adv 300 python bench.py --api plain --config advect1D --steps 40 --warmup 3 --no-cpu-baseline --no-roofline
+             run plain_M 300 python bench.py --api plain --config fluid2DtlgnM --steps 20 --warmup 3 --no-cpu-baseline --no-roofline ;;
     prec) run prec 400 python tools/prec_errors.py ${PARGS:-} ;;
     precd) run precd 900 python -u tools/prec_defaults.py ${PDARGS:-} ;;
   esac
