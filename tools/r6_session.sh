@@ -107,6 +107,13 @@ for s in ${STEPS:-tests bench prof}; do
            run p0_M 300 python bench.py --config fluid2DtlgnM --steps 20 --warmup 3 --no-cpu-baseline
            run p5_M 300 python bench.py --config fluid2DtlgnM --steps 20 --warmup 3 --no-cpu-baseline --bwd-policy 5 ;;
     default) run default 600 python bench.py ;;
+    abx) for r in 1 2; do  # this tree's library (A) vs insr-pde_amd/lib_exp (B: the previous build)
+           run x_A_$r 300 python bench.py --steps 40 --warmup 3 --no-cpu-baseline --plain-line off
+           run x_B_$r 300 python bench.py --lib insr-pde_amd/lib_exp/libinsr_hip.so --steps 40 --warmup 3 --no-cpu-baseline --plain-line off
+           run x_As_$r 300 python bench.py --config fluid2DtlgnM --shard-of 8 --steps 40 --warmup 3 --no-cpu-baseline --no-roofline
+           run x_Bs_$r 300 python bench.py --config fluid2DtlgnM --shard-of 8 --lib insr-pde_amd/lib_exp/libinsr_hip.so --steps 40 --warmup 3 --no-cpu-baseline --no-roofline
+         done
+         run x_prof 300 rocprofv3 --kernel-trace --stats -d "$PWD/$O/xprof" -o run --output-format csv -- python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-roofline --plain-line off ;;
     closing) run bench_advect1D 300 python bench.py --config advect1D --steps 40 --warmup 3 --no-cpu-baseline
              for c in elasticity2Dstretch elasticity3Dbunny fluid2DtlgnM; do
                run bench_$c 400 python bench.py --config $c --steps 20 --warmup 3 --no-cpu-baseline; done
