@@ -420,7 +420,7 @@ def kernel_identity(kind, mode, n, din, dout, L, W, nq=3, seeded=False):
     nprod = {4: 3, 3: 6, 2: 3, 1: 1}
     if kind == "iter":  # insr_advect1d_iteration: exact-fp32 products (v_mfma_f32_16x16x4_f32)
         nb = lib.insr_advect1d_rows(n)
-        return f"insr::advect1d_iter_kernel<{L}>", nb * 256, False, 1
+        return f"insr::advect1d_iter_kernel<{L}>", nb * 512, False, 1  # (512 threads per block)
     path = lib.insr_jet_bwd_path(n, din, dout, L, W, m_b) if kind == "bwd" else 0
     if path == 3:  # the recompute backward (forward + reverse jet per tile, f16x3) + the fixed-order sums
         import ctypes

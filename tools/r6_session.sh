@@ -107,6 +107,12 @@ for s in ${STEPS:-tests bench prof}; do
            run p0_M 300 python bench.py --config fluid2DtlgnM --steps 20 --warmup 3 --no-cpu-baseline
            run p5_M 300 python bench.py --config fluid2DtlgnM --steps 20 --warmup 3 --no-cpu-baseline --bwd-policy 5 ;;
     default) run default 600 python bench.py ;;
+    advf16) run tadv 600 python -u -m pytest tests/test_gpu_advect_iter.py tests/test_gpu_fullsize_phases.py -m gpu -x -v --timeout 120 --timeout-method thread -k "advect"
+            for r in 1 2; do
+              run adv16_$r 300 python bench.py --config advect1D --steps 40 --warmup 3 --no-cpu-baseline
+              run adv32_$r 300 python bench.py --config advect1D --steps 40 --warmup 3 --no-cpu-baseline --advect-fp32
+            done
+            run advprof 300 rocprofv3 --kernel-trace --stats -d "$PWD/$O/advprof" -o run --output-format csv -- python bench.py --config advect1D --steps 20 --warmup 3 --no-cpu-baseline --no-roofline ;;
     abx) for r in 1 2; do  # this tree's library (A) vs insr-pde_amd/lib_exp (B: the previous build)
            run x_A_$r 300 python bench.py --steps 40 --warmup 3 --no-cpu-baseline --plain-line off
            run x_B_$r 300 python bench.py --lib insr-pde_amd/lib_exp/libinsr_hip.so --steps 40 --warmup 3 --no-cpu-baseline --plain-line off
