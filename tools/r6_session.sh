@@ -107,6 +107,8 @@ for s in ${STEPS:-tests bench prof}; do
            run p0_M 300 python bench.py --config fluid2DtlgnM --steps 20 --warmup 3 --no-cpu-baseline
            run p5_M 300 python bench.py --config fluid2DtlgnM --steps 20 --warmup 3 --no-cpu-baseline --bwd-policy 5 ;;
     default) run default 600 python bench.py ;;
+    topt) run topt 600 python -u -m pytest tests/test_gpu_optim.py tests/test_gpu_phases.py tests/test_gpu_fullsize_phases.py tests/test_gpu_dp_capture.py -m gpu -x -q --timeout 120 --timeout-method thread ;;
+    adamcost) run adamcost 300 python tools/study/adam_sums_cost.py ;;
     profshard) run profshard 300 rocprofv3 --kernel-trace --stats -d "$PWD/$O/profshard" -o run --output-format csv -- python bench.py --config fluid2DtlgnM --shard-of 8 --steps 20 --warmup 3 --no-cpu-baseline --no-roofline
                run profshardB 300 rocprofv3 --kernel-trace --stats -d "$PWD/$O/profshardB" -o run --output-format csv -- python bench.py --config fluid2DtlgnM --shard-of 8 --steps 20 --warmup 3 --no-cpu-baseline --no-roofline --lib insr-pde_amd/lib_exp/libinsr_hip.so ;;
     t3) run tt3 600 python -u -m pytest tests/test_gpu_fullsize.py tests/test_gpu_multi_bwd.py tests/test_gpu_fullsize_phases.py tests/test_gpu_phases.py -m gpu -x -q --timeout 120 --timeout-method thread ;;
