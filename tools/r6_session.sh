@@ -107,6 +107,13 @@ for s in ${STEPS:-tests bench prof}; do
            run p0_M 300 python bench.py --config fluid2DtlgnM --steps 20 --warmup 3 --no-cpu-baseline
            run p5_M 300 python bench.py --config fluid2DtlgnM --steps 20 --warmup 3 --no-cpu-baseline --bwd-policy 5 ;;
     default) run default 600 python bench.py ;;
+    abpol4) for r in 1 2; do
+              run p0h_$r 300 python bench.py --steps 40 --warmup 3 --no-cpu-baseline --plain-line off
+              run p4h_$r 300 python bench.py --steps 40 --warmup 3 --no-cpu-baseline --plain-line off --bwd-policy 4
+              run p0s_$r 300 python bench.py --config fluid2DtlgnM --shard-of 8 --steps 40 --warmup 3 --no-cpu-baseline --no-roofline
+              run p4s_$r 300 python bench.py --config fluid2DtlgnM --shard-of 8 --steps 40 --warmup 3 --no-cpu-baseline --no-roofline --bwd-policy 4
+            done
+            run p4prof 300 rocprofv3 --kernel-trace --stats -d "$PWD/$O/p4prof" -o run --output-format csv -- python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-roofline --plain-line off --bwd-policy 4 ;;
     topt) run topt 600 python -u -m pytest tests/test_gpu_optim.py tests/test_gpu_phases.py tests/test_gpu_fullsize_phases.py tests/test_gpu_dp_capture.py -m gpu -x -q --timeout 120 --timeout-method thread ;;
     adamcost) run adamcost 300 python tools/study/adam_sums_cost.py ;;
     profshard) run profshard 300 rocprofv3 --kernel-trace --stats -d "$PWD/$O/profshard" -o run --output-format csv -- python bench.py --config fluid2DtlgnM --shard-of 8 --steps 20 --warmup 3 --no-cpu-baseline --no-roofline
