@@ -107,6 +107,7 @@ for s in ${STEPS:-tests bench prof}; do
            run p0_M 300 python bench.py --config fluid2DtlgnM --steps 20 --warmup 3 --no-cpu-baseline
            run p5_M 300 python bench.py --config fluid2DtlgnM --steps 20 --warmup 3 --no-cpu-baseline --bwd-policy 5 ;;
     default) run default 600 python bench.py ;;
+    tfb) run tfb 900 python -u -m pytest tests/test_gpu_resident_f16.py tests/test_gpu_multi_bwd.py tests/test_gpu_recompute.py tests/test_gpu_seeds.py tests/test_gpu_phases.py tests/test_gpu_fullsize_phases.py -m gpu -x -q --timeout 120 --timeout-method thread ;;
     abpol4) for r in 1 2; do
               run p0h_$r 300 python bench.py --steps 40 --warmup 3 --no-cpu-baseline --plain-line off
               run p4h_$r 300 python bench.py --steps 40 --warmup 3 --no-cpu-baseline --plain-line off --bwd-policy 4
