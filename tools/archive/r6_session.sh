@@ -1,7 +1,7 @@
 #!/bin/bash
 # round-6 GPU session: STEPS (default "tests bench prof") with per-step time limits; stops at the first failure
 set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 O=gpurun_out/${SESSION:-r6}; mkdir -p $O
 # a failing step ends the session, except pytest's "some tests failed" (exit 1): assertion failures are no GPU
 # fault, so the benches after it still run; timeouts, aborts and crashes (124, 137, 134, 139, ...) end it
