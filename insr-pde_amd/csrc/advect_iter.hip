@@ -36,7 +36,7 @@ constexpr int kAdvStamps = 32;
 static __device__ unsigned long long g_adv_stamps[8 * kAdvStamps];
 #define ADV_STAMP(k)                                                                                       \
   do {                                                                                                     \
-    if (blockIdx.x == 0 && lane == 0 && tile == t0) g_adv_stamps[wave * kAdvStamps + (k)] = __builtin_amdgcn_s_memtime(); \
+    if (blockIdx.x == 0 && lane == 0 && tile == (int)blockIdx.x) g_adv_stamps[wave * kAdvStamps + (k)] = __builtin_amdgcn_s_memtime(); \
   } while (0)
 #else
 #define ADV_STAMP(k) \
@@ -146,7 +146,6 @@ __global__ __launch_bounds__(kAdvThreads) void advect1d_iter_kernel(const Advect
   const int g = lane >> 4, c = lane & 15;
   const int n0 = 16 * wg + 4 * g;  // this lane's first neuron of every hidden layer
   const unsigned long long base = pk.state[0];
-  const int t0 = (int)((long)blockIdx.x * pk.tiles / pk.nb), t1 = (int)((long)(blockIdx.x + 1) * pk.tiles / pk.nb);
   const int total = pk.n + 2 * pk.h;
   const float* P[2] = {pk.prm, pk.prev};  // 0: trainable, 1: frozen
   const long wout = out_off(1, W, L);
@@ -202,7 +201,14 @@ __global__ __launch_bounds__(kAdvThreads) void advect1d_iter_kernel(const Advect
   for (int j = 0; j < L; ++j) gb[j] = floatx4{0.f, 0.f, 0.f, 0.f};
   float gbo = 0.f, lmain = 0.f, lbc = 0.f;
 
-  for (int tile = t0; tile < t1; ++tile) {
+  // tiles b, b + nb, b + 2 nb, ... (nb = min(tiles, CUs)): the advect1D batch's 256 interior tiles one per
+  // block, its 3 band tiles the second tile of blocks 0-2.  A band tile (every point a band point) needs
+  // neither the frozen field (no residual) nor the tangent streams (u_x enters no band term: their
+  // adjoints are zero), so its frozen waves skip the forward and every tangent product is skipped --
+  // the critical path is one interior tile plus that lighter one instead of two interior tiles.
+  for (int tile = blockIdx.x; tile < pk.tiles; tile += pk.nb) {
+    const bool band = tile * 16 >= pk.n;  // (uniform)
+    const bool work = !(band && grp == 1);  // this wave's forward runs
     __syncthreads();  // the staged parameters / the previous tile's last readers of HT, ZB, RED, SD
     ADV_STAMP(0);
     // ---- the tile's points: value v of the draw = lo + (hi - lo) u(v), u from Philox(seed, base + v / 4)
@@ -221,7 +227,7 @@ __global__ __launch_bounds__(kAdvThreads) void advect1d_iter_kernel(const Advect
 
     // ---- forward: this wave's field, value (stream 0) and tangent (stream 1) ----
     floatx4 zs[L + 1], ts[L + 1];  // z / t of sine layers 0 .. L (the trainable field's: the reverse's)
-    {
+    if (work) {
       floatx4 z, t, s, cs;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
@@ -241,27 +247,37 @@ __global__ __launch_bounds__(kAdvThreads) void advect1d_iter_kernel(const Advect
 #pragma unroll
     for (int j = 1; j <= L; ++j) {
       // B = h_{j-1}[16 g + kc][point c] (point-major: 16 consecutive floats), A = W_j[16 wg + c][16 g + kc]
-      const float* Bq = grp == 0 ? HT + (j - 1) * 2 * PL : (((j - 1) & 1) ? ZB : HP);
-      float a[16], bv[16], bt[16];
-      lds_get16(WS + ((grp * L + j - 1) * W + 16 * wg + c) * WL + 16 * g, a);
-      lds_get16(Bq + c * LD + 16 * g, bv);
-      lds_get16(Bq + PL + c * LD + 16 * g, bt);
-      floatx4 av, at = {0.f, 0.f, 0.f, 0.f};
+      floatx4 av = {0.f, 0.f, 0.f, 0.f}, at = {0.f, 0.f, 0.f, 0.f};
+      if (work) {
+        const float* Bq = grp == 0 ? HT + (j - 1) * 2 * PL : (((j - 1) & 1) ? ZB : HP);
+        float a[16], bv[16];
+        lds_get16(WS + ((grp * L + j - 1) * W + 16 * wg + c) * WL + 16 * g, a);
+        lds_get16(Bq + c * LD + 16 * g, bv);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) av[r] = SMq[kB + 64 * (j - 1) + n0 + r];
+        for (int r = 0; r < 4; ++r) av[r] = SMq[kB + 64 * (j - 1) + n0 + r];
+        if (band) {  // value stream only
 #pragma unroll
-      for (int kc = 0; kc < 16; ++kc) {
-        av = mfma4(a[kc], bv[kc], av);
-        at = mfma4(a[kc], bt[kc], at);
+          for (int kc = 0; kc < 16; ++kc) av = mfma4(a[kc], bv[kc], av);
+        } else {
+          float bt[16];
+          lds_get16(Bq + PL + c * LD + 16 * g, bt);
+#pragma unroll
+          for (int kc = 0; kc < 16; ++kc) {
+            av = mfma4(a[kc], bv[kc], av);
+            at = mfma4(a[kc], bt[kc], at);
+          }
+        }
       }
       zs[j] = av;
       ts[j] = at;
       if (j < L) {  // h_j -> LDS (the next layer's B operand; the trainable one also dW's)
-        floatx4 s, cs;
-        adv_sincos(av, s, cs);
-        float* Hn = grp == 0 ? HT + j * 2 * PL : ((j & 1) ? ZB : HP);
-        *reinterpret_cast<floatx4*>(Hn + c * LD + n0) = s;
-        *reinterpret_cast<floatx4*>(Hn + PL + c * LD + n0) = OMEGA * cs * at;
+        if (work) {
+          floatx4 s, cs;
+          adv_sincos(av, s, cs);
+          float* Hn = grp == 0 ? HT + j * 2 * PL : ((j & 1) ? ZB : HP);
+          *reinterpret_cast<floatx4*>(Hn + c * LD + n0) = s;
+          *reinterpret_cast<floatx4*>(Hn + PL + c * LD + n0) = OMEGA * cs * at;  // (band: zeros)
+        }
         __syncthreads();
       }
     }
@@ -274,7 +290,7 @@ __global__ __launch_bounds__(kAdvThreads) void advect1d_iter_kernel(const Advect
       float acc0 = 0.f, acc1 = 0.f;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float wt = SMq[kWo + n0 + r];
+        const float wt = work ? SMq[kWo + n0 + r] : 0.f;  // (a band tile's frozen waves: zeros)
         acc0 = fmaf(wt, sL[r], acc0);
         acc1 = fmaf(wt, OMEGA * cL[r] * ts[L][r], acc1);
       }
@@ -350,11 +366,16 @@ __global__ __launch_bounds__(kAdvThreads) void advect1d_iter_kernel(const Advect
         lds_get16(Z + c * LD + 16 * g, bv);
         lds_get16(Z + PL + c * LD + 16 * g, bt);
         floatx4 nv = {0.f, 0.f, 0.f, 0.f}, nt = {0.f, 0.f, 0.f, 0.f};
+        if (band) {  // zero tangent adjoints: the value stream only
 #pragma unroll
-        for (int kc = 0; kc < 16; ++kc) {
-          const float a = AT[kc * WL];
-          nv = mfma4(a, bv[kc], nv);
-          nt = mfma4(a, bt[kc], nt);
+          for (int kc = 0; kc < 16; ++kc) nv = mfma4(AT[kc * WL], bv[kc], nv);
+        } else {
+#pragma unroll
+          for (int kc = 0; kc < 16; ++kc) {
+            const float a = AT[kc * WL];
+            nv = mfma4(a, bv[kc], nv);
+            nt = mfma4(a, bt[kc], nt);
+          }
         }
         hv = nv;
         ht = nt;
@@ -453,13 +474,12 @@ __global__ __launch_bounds__(kAdvThreads) void advect1d_iter_kernel(const Advect
   }
 }
 
-// blocks: the fewest that keep ceil(tiles / CUs) tiles each (jet_fb.hpp fb_blocks; one block per CU: its
-// staged weights fill the LDS) -- the 4,136-point advect1D batch is 259 tiles: 130 blocks of 2
+// blocks: one per tile up to one per CU (one block per CU: its staged weights fill the LDS); the tiles past
+// that are dealt round-robin (advect1d_iter_kernel) -- the 4,136-point advect1D batch is 259 tiles: 256
+// blocks, blocks 0-2 also take the three band tiles
 inline int adv_blocks(long tiles) {
   const long cus = device_cus();
-  if (tiles <= cus) return (int)(tiles > 0 ? tiles : 1);
-  const long per = (tiles + cus - 1) / cus;
-  return (int)((tiles + per - 1) / per);
+  return (int)(tiles < 1 ? 1 : (tiles < cus ? tiles : cus));
 }
 
 template <int L>
